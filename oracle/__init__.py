@@ -1,0 +1,129 @@
+"""ctypes access to the CPU checkers -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker / CPU baseline.  The product
+(srsran_project_amd) never imports it.
+
+  ORACLE : oracle/libsrs_oracle.so, our C restatement (srs_oracle.c, srs_oracle_rm.c)
+  REF    : oracle/_ref/libsrsran_ref.so, the reference's own sources compiled here
+           (oracle/Makefile); may be absent, then REF is None.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_PATH = os.path.join(_HERE, "libsrs_oracle.so")
+REF_PATH = os.path.join(_HERE, "_ref", "libsrsran_ref.so")
+
+P = ctypes.c_void_p
+c_int, c_uint = ctypes.c_int, ctypes.c_uint
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(P)
+
+
+def _load_oracle():
+    if not os.path.exists(ORACLE_PATH):
+        raise ImportError("oracle not built: %s (run make -C oracle)" % ORACLE_PATH)
+    lib = ctypes.CDLL(ORACLE_PATH)
+    lib.srs_oracle_ldpc_decode.restype = c_int
+    lib.srs_oracle_ldpc_decode.argtypes = [c_int] * 8 + [P, c_uint, P, P]
+    lib.srs_oracle_ldpc_encode.restype = c_int
+    lib.srs_oracle_ldpc_encode.argtypes = [c_int, c_int, P, P]
+    lib.srs_oracle_ldpc_syndrome.restype = c_int
+    lib.srs_oracle_ldpc_syndrome.argtypes = [c_int, c_int, P]
+    lib.srs_oracle_crc_bits.restype = ctypes.c_uint32
+    lib.srs_oracle_crc_bits.argtypes = [c_int, P, c_uint]
+    lib.srs_oracle_lifting_index.restype = c_int
+    lib.srs_oracle_lifting_index.argtypes = [c_int]
+    return lib
+
+
+def _load_ref():
+    if not os.path.exists(REF_PATH):
+        return None
+    lib = ctypes.CDLL(REF_PATH)
+    lib.srs_ref_has_impl.restype = c_int
+    lib.srs_ref_has_impl.argtypes = [ctypes.c_char_p]
+    lib.srs_ref_ldpc_decode.restype = c_int
+    lib.srs_ref_ldpc_decode.argtypes = [ctypes.c_char_p] + [c_int] * 7 + [P, c_uint, P]
+    lib.srs_ref_ldpc_encode.restype = c_int
+    lib.srs_ref_ldpc_encode.argtypes = [ctypes.c_char_p, c_int, c_int, P, P, c_uint]
+    lib.srs_ref_crc_bits.restype = c_uint
+    lib.srs_ref_crc_bits.argtypes = [c_int, P, c_uint]
+    lib.srs_ref_ldpc_decode_many.restype = ctypes.c_double
+    lib.srs_ref_ldpc_decode_many.argtypes = [ctypes.c_char_p, c_int, c_int, c_int, c_int, P, c_uint, c_uint, c_int,
+                                             P, P]
+    return lib
+
+
+ORACLE = _load_oracle()
+REF = _load_ref()
+
+BG_K = {1: 22, 2: 10}
+BG_N_SHORT = {1: 66, 2: 50}
+BG_N_FULL = {1: 68, 2: 52}
+ARITH = {"simd": 0, "avx512": 0, "avx2": 0, "auto": 0, "generic": 1}
+
+
+def ldpc_decode(llrs, bg, Z, max_iterations=6, arith="simd", crc_poly=None, nof_filler_bits=0, nof_crc_bits=16,
+                force_decoding=False, want_soft=False):
+    """Oracle decode of one codeblock. Returns (iterations or None, packed bits, soft or None)."""
+    llrs = np.ascontiguousarray(llrs, dtype=np.int8)
+    K = BG_K[bg] * Z
+    out = np.zeros((K + 7) // 8, np.uint8)
+    soft = np.zeros(BG_N_FULL[bg] * Z, np.int8) if want_soft else None
+    r = ORACLE.srs_oracle_ldpc_decode(bg, Z, nof_filler_bits, nof_crc_bits, max_iterations, ARITH[arith],
+                                      int(force_decoding), -1 if crc_poly is None else int(crc_poly), _ptr(llrs),
+                                      llrs.size, _ptr(out), _ptr(soft))
+    if r == -2:
+        raise ValueError("invalid decoder arguments")
+    return (None if r < 0 else r), out, soft
+
+
+def ldpc_encode(msg_bits, bg, Z):
+    """Oracle systematic encode: K message bits -> N_short*Z codeblock bits (one per byte)."""
+    msg_bits = np.ascontiguousarray(msg_bits, dtype=np.uint8)
+    cw = np.zeros(BG_N_SHORT[bg] * Z, np.uint8)
+    if ORACLE.srs_oracle_ldpc_encode(bg, Z, _ptr(msg_bits), _ptr(cw)) != 0:
+        raise ValueError("invalid encoder arguments")
+    return cw
+
+
+def crc_bits(poly, bits):
+    bits = np.ascontiguousarray(bits, dtype=np.uint8)
+    return int(ORACLE.srs_oracle_crc_bits(int(poly), _ptr(bits), bits.size))
+
+
+def ref_ldpc_decode(impl, llrs, bg, Z, max_iterations=6, crc_poly=None, nof_filler_bits=0, nof_crc_bits=16,
+                    force_decoding=False, out_init=None):
+    """Reference decoder (compiled from /root/reference). Returns (iterations or None, packed bits)."""
+    llrs = np.ascontiguousarray(llrs, dtype=np.int8)
+    K = BG_K[bg] * Z
+    out = np.zeros((K + 7) // 8, np.uint8) if out_init is None else out_init.copy()
+    r = REF.srs_ref_ldpc_decode(impl.encode(), bg, Z, nof_filler_bits, nof_crc_bits, max_iterations,
+                                int(force_decoding), -1 if crc_poly is None else int(crc_poly), _ptr(llrs),
+                                llrs.size, _ptr(out))
+    if r == -2:
+        raise ValueError("reference implementation %r unavailable" % impl)
+    return (None if r < 0 else r), out
+
+
+def ref_ldpc_encode(msg_bits, bg, Z, n_out=None, impl="generic"):
+    msg_bits = np.ascontiguousarray(msg_bits, dtype=np.uint8)
+    n = BG_N_SHORT[bg] * Z if n_out is None else n_out
+    cw = np.zeros(n, np.uint8)
+    if REF.srs_ref_ldpc_encode(impl.encode(), bg, Z, _ptr(msg_bits), _ptr(cw), n) != 0:
+        raise ValueError("reference encoder %r unavailable" % impl)
+    return cw
+
+
+def pack_bits(bits):
+    return np.packbits(np.asarray(bits, dtype=np.uint8))
+
+
+def unpack_bits(packed, n):
+    return np.unpackbits(np.asarray(packed, dtype=np.uint8))[:n]

@@ -1,0 +1,19 @@
+"""srsran_project_amd -- MI355X-native (gfx950 HIP) implementation of srsRAN's
+PUSCH/PDSCH channel-coding hot path behind the reference's own interfaces.
+
+See DESIGN.md for the path, the boundary and the kernels.
+"""
+from . import _lib  # noqa: F401
+from .ldpc import (  # noqa: F401
+    CrcGeneratorPoly,
+    LdpcBaseGraph,
+    LdpcDecoder,
+    LdpcDecoderConfiguration,
+    LdpcDecoderFactory,
+    LIFTING_SIZES,
+    codeblock_length,
+    create_ldpc_decoder_factory_hip,
+    message_length,
+)
+
+__version__ = "0.1.0"

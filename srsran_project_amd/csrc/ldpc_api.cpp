@@ -1,0 +1,416 @@
+// ldpc_api.cpp -- C-ABI entry points of the MI355X LDPC path (include/srsran_amd/ldpc.h).
+//
+// Error behaviour mirrors the reference's srsran_assert checks in
+// lib/phy/upper/channel_coding/ldpc/ldpc_decoder_impl.cpp:30-75 (invalid
+// lifting size, iterations == 0, CRC length, input length bounds); instead of
+// aborting, the call returns SRS_AMD_EINVAL with the reference's message.
+#include "srsran_amd/ldpc.h"
+
+#include <hip/hip_runtime.h>
+
+#include "ldpc_common.h"
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace srs_amd {
+
+
+hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, int arith, int grid, hipStream_t stream);
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...)
+{
+  char    buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what)
+{
+  return fail(SRS_AMD_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+constexpr int      MAX_CRC_BITS_LEN = 22 * MAX_LIFTING_SIZE;
+constexpr uint32_t DEFAULT_SLOTS    = 2048;
+
+// x^(k+L) mod g for k = 0..MAX_CRC_BITS_LEN-1: the CRC of a single 1 bit
+// followed by k zeros (crc_calculator_generic_impl.cpp:98 long division).
+std::vector<uint32_t> crc_linear_table(int poly)
+{
+  uint32_t polynom = 0;
+  int      order   = 0;
+  crc_params(poly, polynom, order);
+  std::vector<uint32_t> t(MAX_CRC_BITS_LEN);
+  uint64_t              highbit = 1ull << order;
+  uint64_t              r       = 1;
+  for (int i = 0; i < order; ++i) {
+    r <<= 1;
+    if (r & highbit) {
+      r ^= polynom;
+    }
+  }
+  for (int k = 0; k < MAX_CRC_BITS_LEN; ++k) {
+    t[k] = static_cast<uint32_t>(r & (highbit - 1));
+    r <<= 1;
+    if (r & highbit) {
+      r ^= polynom;
+    }
+  }
+  return t;
+}
+
+} // namespace
+
+const char* last_error()
+{
+  return g_last_error.c_str();
+}
+
+} // namespace srs_amd
+
+using namespace srs_amd;
+
+struct srs_amd_ldpc_decoder {
+  int                     arith          = ARITH_SIMD;
+  int                     force_decoding = 0;
+  int                     device         = 0;
+  uint32_t                max_slots      = DEFAULT_SLOTS;
+  int8_t*                 c2v_ws         = nullptr;
+  size_t                  ws_bytes       = 0;
+  uint32_t*               crc_tables     = nullptr; // 6 x MAX_CRC_BITS_LEN
+  int8_t*                 h_in           = nullptr; // staging for the single-CB host call
+  uint8_t*                h_out          = nullptr;
+  int32_t*                h_it           = nullptr;
+  hipStream_t             stream         = nullptr;
+  lifted_graph            graph{};
+  int                     graph_bg = 0, graph_Z = 0;
+  std::mutex              mtx;
+};
+
+namespace {
+
+int validate(const srs_amd_ldpc_decoder_config* cfg, int crc_poly)
+{
+  if (cfg == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null configuration");
+  }
+  if (cfg->base_graph != 1 && cfg->base_graph != 2) {
+    return fail(SRS_AMD_EINVAL, "Invalid base graph %u", cfg->base_graph);
+  }
+  if (lifting_index(static_cast<int>(cfg->lifting_size)) < 0) {
+    return fail(SRS_AMD_EINVAL, "Invalid lifting size %u", cfg->lifting_size);
+  }
+  if (cfg->max_iterations == 0) {
+    return fail(SRS_AMD_EINVAL, "Max iterations must be different to 0");
+  }
+  if (cfg->nof_crc_bits != 16 && cfg->nof_crc_bits != 24) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of CRC bits.");
+  }
+  uint32_t K = (cfg->base_graph == 1 ? 22 : 10) * cfg->lifting_size;
+  if (cfg->nof_filler_bits >= K) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of filler bits %u", cfg->nof_filler_bits);
+  }
+  if (crc_poly != SRS_AMD_NO_CRC && (crc_poly < 0 || crc_poly > 5)) {
+    return fail(SRS_AMD_EINVAL, "Invalid CRC polynomial %d", crc_poly);
+  }
+  return SRS_AMD_OK;
+}
+
+int ensure_workspace(srs_amd_ldpc_decoder* d)
+{
+  size_t need = static_cast<size_t>(d->max_slots) * MAX_EDGES * MAX_LIFTING_SIZE;
+  if (d->ws_bytes >= need) {
+    return SRS_AMD_OK;
+  }
+  if (d->c2v_ws) {
+    (void)hipFree(d->c2v_ws);
+    d->c2v_ws   = nullptr;
+    d->ws_bytes = 0;
+  }
+  hipError_t e = hipMalloc(&d->c2v_ws, need);
+  if (e != hipSuccess) {
+    return hip_fail(e, "hipMalloc(check-to-variable workspace)");
+  }
+  d->ws_bytes = need;
+  return SRS_AMD_OK;
+}
+
+const lifted_graph& get_graph(srs_amd_ldpc_decoder* d, int bg, int Z)
+{
+  if (d->graph_bg != bg || d->graph_Z != Z) {
+    build_lifted_graph(d->graph, bg, Z);
+    d->graph_bg = bg;
+    d->graph_Z  = Z;
+  }
+  return d->graph;
+}
+
+} // namespace
+
+extern "C" {
+
+const char* srs_amd_last_error(void)
+{
+  return srs_amd::last_error();
+}
+
+const char* srs_amd_version(void)
+{
+  return "srsran_amd 0.1.0 (gfx950)";
+}
+
+uint32_t srs_amd_ldpc_message_length(uint32_t base_graph, uint32_t lifting_size)
+{
+  if ((base_graph != 1 && base_graph != 2) || lifting_index(static_cast<int>(lifting_size)) < 0) {
+    return 0;
+  }
+  return (base_graph == 1 ? 22u : 10u) * lifting_size;
+}
+
+uint32_t srs_amd_ldpc_codeblock_length(uint32_t base_graph, uint32_t lifting_size)
+{
+  if ((base_graph != 1 && base_graph != 2) || lifting_index(static_cast<int>(lifting_size)) < 0) {
+    return 0;
+  }
+  return (base_graph == 1 ? 66u : 50u) * lifting_size;
+}
+
+int srs_amd_ldpc_decoder_create(srs_amd_ldpc_decoder** decoder, int arith, int force_decoding, int device)
+{
+  if (decoder == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null decoder pointer");
+  }
+  if (arith != ARITH_SIMD && arith != ARITH_GENERIC) {
+    return fail(SRS_AMD_EINVAL, "Invalid arithmetic flavour %d", arith);
+  }
+  *decoder = nullptr;
+  int        ndev = 0;
+  hipError_t e    = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) {
+    return fail(SRS_AMD_EHIP, "no HIP device available (%s)", hipGetErrorString(e));
+  }
+  if (device < 0) {
+    e = hipGetDevice(&device);
+    if (e != hipSuccess) {
+      return hip_fail(e, "hipGetDevice");
+    }
+  }
+  e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    return hip_fail(e, "hipSetDevice");
+  }
+  auto* d           = new srs_amd_ldpc_decoder();
+  d->arith          = arith;
+  d->force_decoding = force_decoding ? 1 : 0;
+  d->device         = device;
+  std::vector<uint32_t> tables;
+  tables.reserve(6 * MAX_CRC_BITS_LEN);
+  for (int p = 0; p < 6; ++p) {
+    auto t = crc_linear_table(p);
+    tables.insert(tables.end(), t.begin(), t.end());
+  }
+  e = hipMalloc(&d->crc_tables, tables.size() * sizeof(uint32_t));
+  if (e == hipSuccess) {
+    e = hipMemcpy(d->crc_tables, tables.data(), tables.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess) {
+    e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+  }
+  if (e != hipSuccess) {
+    srs_amd_ldpc_decoder_destroy(d);
+    return hip_fail(e, "decoder setup");
+  }
+  *decoder = d;
+  return SRS_AMD_OK;
+}
+
+void srs_amd_ldpc_decoder_destroy(srs_amd_ldpc_decoder* d)
+{
+  if (d == nullptr) {
+    return;
+  }
+  (void)hipSetDevice(d->device);
+  if (d->stream) {
+    (void)hipStreamSynchronize(d->stream);
+    (void)hipStreamDestroy(d->stream);
+  }
+  (void)hipFree(d->c2v_ws);
+  (void)hipFree(d->crc_tables);
+  (void)hipFree(d->h_in);
+  (void)hipFree(d->h_out);
+  (void)hipFree(d->h_it);
+  delete d;
+}
+
+int srs_amd_ldpc_decoder_set_max_slots(srs_amd_ldpc_decoder* d, uint32_t max_slots)
+{
+  if (d == nullptr || max_slots == 0) {
+    return fail(SRS_AMD_EINVAL, "invalid decoder or slot count");
+  }
+  std::lock_guard<std::mutex> lock(d->mtx);
+  if (max_slots != d->max_slots) {
+    d->max_slots = max_slots;
+    if (d->c2v_ws) {
+      (void)hipStreamSynchronize(d->stream);
+      (void)hipFree(d->c2v_ws);
+      d->c2v_ws   = nullptr;
+      d->ws_bytes = 0;
+    }
+  }
+  return SRS_AMD_OK;
+}
+
+int srs_amd_ldpc_decode_batch(srs_amd_ldpc_decoder*              d,
+                              const srs_amd_ldpc_decoder_config* cfg,
+                              int                                crc_poly,
+                              const int8_t*                      d_llrs,
+                              uint32_t                           llr_stride,
+                              const uint32_t*                    d_llr_lens,
+                              uint32_t                           llr_len,
+                              uint8_t*                           d_output,
+                              uint32_t                           out_stride,
+                              int32_t*                           d_nof_iters,
+                              int8_t*                            d_soft_out,
+                              uint32_t                           nof_cbs,
+                              void*                              stream)
+{
+  if (d == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null decoder");
+  }
+  int rc = validate(cfg, crc_poly);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  const uint32_t Z       = cfg->lifting_size;
+  const uint32_t K       = (cfg->base_graph == 1 ? 22 : 10) * Z;
+  const uint32_t N_short = (cfg->base_graph == 1 ? 66 : 50) * Z;
+  if (nof_cbs == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_llrs == nullptr || d_output == nullptr || d_nof_iters == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  if (out_stride < (K + 7) / 8) {
+    return fail(SRS_AMD_EINVAL, "The output size %u is not equal to the message length %u.", out_stride * 8, K);
+  }
+  if (d_llr_lens == nullptr) {
+    // ldpc_decoder_impl.cpp:62-75 input length bounds (per-row lengths are the caller's contract).
+    if (llr_len > N_short) {
+      return fail(SRS_AMD_EINVAL, "The input size %u exceeds the maximum message length %u.", llr_len, N_short);
+    }
+    if (llr_len < K + 2 * Z) {
+      return fail(SRS_AMD_EINVAL, "The input length %u does not reach minimum %u", llr_len, K + 2 * Z);
+    }
+    if (llr_stride < llr_len) {
+      return fail(SRS_AMD_EINVAL, "llr_stride %u smaller than llr_len %u", llr_stride, llr_len);
+    }
+  }
+  std::lock_guard<std::mutex> lock(d->mtx);
+  hipError_t                  e = hipSetDevice(d->device);
+  if (e != hipSuccess) {
+    return hip_fail(e, "hipSetDevice");
+  }
+  rc = ensure_workspace(d);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  const lifted_graph& g = get_graph(d, static_cast<int>(cfg->base_graph), static_cast<int>(Z));
+
+  decode_args a{};
+  a.llrs            = d_llrs;
+  a.llr_lens        = d_llr_lens;
+  a.out             = d_output;
+  a.nof_iters       = d_nof_iters;
+  a.soft_out        = d_soft_out;
+  a.c2v_ws          = d->c2v_ws;
+  a.crc_table       = crc_poly == SRS_AMD_NO_CRC ? nullptr : d->crc_tables + static_cast<size_t>(crc_poly) * MAX_CRC_BITS_LEN;
+  a.llr_stride      = llr_stride;
+  a.llr_len         = llr_len;
+  a.out_stride      = out_stride;
+  a.nof_cbs         = nof_cbs;
+  a.nof_filler_bits = static_cast<int32_t>(cfg->nof_filler_bits);
+  a.max_iterations  = static_cast<int32_t>(cfg->max_iterations);
+  a.force_decoding  = d->force_decoding;
+  a.zpad            = static_cast<int32_t>(MAX_LIFTING_SIZE);
+  const int grid    = static_cast<int>(nof_cbs < d->max_slots ? nof_cbs : d->max_slots);
+  e = launch_ldpc_decode(a, g, d->arith, grid, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) {
+    return hip_fail(e, "ldpc_decode_kernel launch");
+  }
+  return SRS_AMD_OK;
+}
+
+int srs_amd_ldpc_decode(srs_amd_ldpc_decoder*              d,
+                        uint8_t*                           output_packed,
+                        const int8_t*                      input,
+                        uint32_t                           input_len,
+                        int                                crc_poly,
+                        const srs_amd_ldpc_decoder_config* cfg,
+                        int32_t*                           nof_iterations)
+{
+  if (d == nullptr || output_packed == nullptr || input == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  int rc = validate(cfg, crc_poly);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  const uint32_t K      = (cfg->base_graph == 1 ? 22 : 10) * cfg->lifting_size;
+  const uint32_t obytes = (K + 7) / 8;
+  {
+    std::lock_guard<std::mutex> lock(d->mtx);
+    hipError_t                  e = hipSetDevice(d->device);
+    if (e == hipSuccess && d->h_in == nullptr) {
+      e = hipMalloc(&d->h_in, 66 * MAX_LIFTING_SIZE);
+      if (e == hipSuccess) {
+        e = hipMalloc(&d->h_out, (22 * MAX_LIFTING_SIZE + 7) / 8);
+      }
+      if (e == hipSuccess) {
+        e = hipMalloc(&d->h_it, sizeof(int32_t));
+      }
+    }
+    if (e == hipSuccess && input_len <= 66 * MAX_LIFTING_SIZE) {
+      e = hipMemcpyAsync(d->h_in, input, input_len, hipMemcpyHostToDevice, d->stream);
+    }
+    if (e == hipSuccess) {
+      // the reference leaves the output untouched on the forced / CRC path: preload it.
+      e = hipMemcpyAsync(d->h_out, output_packed, obytes, hipMemcpyHostToDevice, d->stream);
+    }
+    if (e != hipSuccess) {
+      return hip_fail(e, "staging input");
+    }
+  }
+  rc = srs_amd_ldpc_decode_batch(
+      d, cfg, crc_poly, d->h_in, input_len, nullptr, input_len, d->h_out, obytes, d->h_it, nullptr, 1, d->stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  int32_t    it = -1;
+  hipError_t e  = hipMemcpyAsync(output_packed, d->h_out, obytes, hipMemcpyDeviceToHost, d->stream);
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(&it, d->h_it, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream);
+  }
+  if (e == hipSuccess) {
+    e = hipStreamSynchronize(d->stream);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "ldpc decode");
+  }
+  if (nof_iterations) {
+    *nof_iterations = it;
+  }
+  return SRS_AMD_OK;
+}
+
+} // extern "C"

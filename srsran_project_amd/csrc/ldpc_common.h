@@ -1,0 +1,75 @@
+// ldpc_common.h -- host/device shared definitions for the MI355X LDPC path.
+//
+// Mirrors the constants of the reference:
+//   include/srsran/phy/upper/channel_coding/ldpc/ldpc.h        (lifting sizes, lengths)
+//   lib/phy/upper/channel_coding/ldpc/ldpc_graph_impl.h:36-60   (BG dimensions)
+//   include/srsran/phy/upper/log_likelihood_ratio.h:300-311      (LLR_MAX=120, LLR_INFTY=127)
+#pragma once
+
+#include <cstdint>
+
+namespace srs_amd {
+
+constexpr int LLR_MAX      = 120;
+constexpr int LLR_INFINITY = 127;
+// ldpc_decoder_impl.h:233 soft_bits_clamp_low/high.
+constexpr int SOFT_CLAMP = 64;
+
+constexpr int MAX_LIFTING_SIZE = 384;
+constexpr int MAX_BG_M         = 46;
+constexpr int MAX_BG_N_FULL    = 68;
+constexpr int MAX_EDGES        = 316;
+constexpr int BG1_MAX_DEGREE   = 19;
+constexpr int BG2_MAX_DEGREE   = 10;
+
+enum arith_flavour : int {
+  // avx2_support.h:65 scale_epi8: floor(x * 52428 / 65536) -- AVX2/AVX512 decoders.
+  ARITH_SIMD = 0,
+  // ldpc_decoder_generic.cpp:66 scale_llr: round(x * 0.8f).
+  ARITH_GENERIC = 1,
+};
+
+// Lifted Tanner graph of one (base graph, lifting size) pair, passed to the
+// kernels by value (kernarg segment -> scalar loads).
+struct lifted_graph {
+  int32_t  bg;
+  int32_t  Z;
+  int32_t  K;       // information nodes (22 / 10)
+  int32_t  N_full;  // 68 / 52
+  int32_t  N_short; // 66 / 50
+  int32_t  M;       // check nodes (46 / 42)
+  int32_t  nedges;
+  int32_t  row_start[MAX_BG_M + 1];
+  uint8_t  var[MAX_EDGES];
+  uint16_t shift[MAX_EDGES];
+};
+
+// Arguments of the batched decoder kernel (ldpc_decoder.hip).
+struct decode_args {
+  const int8_t*   llrs;         // [nof_cbs][llr_stride]
+  const uint32_t* llr_lens;     // optional per-codeblock input length
+  uint8_t*        out;          // [nof_cbs][out_stride] packed MSB-first hard bits
+  int32_t*        nof_iters;    // [nof_cbs]: iterations on CRC pass, -1 = no value
+  int8_t*         soft_out;     // optional [nof_cbs][N_full*Z] final soft bits
+  int8_t*         c2v_ws;       // [gridDim.x][nedges][Zpad] check-to-variable scratch
+  const uint32_t* crc_table;    // x^(k+L) mod g, k = 0..K*Z-1 (null = no CRC)
+  uint32_t        llr_stride;
+  uint32_t        llr_len;
+  uint32_t        out_stride;
+  uint32_t        nof_cbs;
+  int32_t         nof_filler_bits;
+  int32_t         max_iterations;
+  int32_t         force_decoding;
+  int32_t         zpad;
+};
+
+// Fills g for (bg, Z); returns false for an invalid pair.
+bool build_lifted_graph(lifted_graph& g, int bg, int Z);
+
+// TS 38.212 Table 5.3.2-1 lifting-size set index, -1 if Z is not a valid lifting size.
+int lifting_index(int Z);
+
+// CRC polynomials of crc_calculator_generic_impl.cpp:27-52, by crc_generator_poly value.
+bool crc_params(int poly, uint32_t& polynom, int& order);
+
+} // namespace srs_amd

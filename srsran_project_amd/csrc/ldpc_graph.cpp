@@ -1,0 +1,78 @@
+// ldpc_graph.cpp -- host-side construction of lifted LDPC graphs and CRC tables.
+//
+// Base graph data: TS 38.212 Tables 5.3.2-2 / 5.3.2-3 (bg_tables.inc).
+// Reference counterpart: lib/phy/upper/channel_coding/ldpc/ldpc_luts_impl.cpp:4530
+// (get_graph: shift = V mod Z) and ldpc_graph_impl.cpp.
+#include "ldpc_common.h"
+
+namespace srs_amd {
+
+#include "bg_tables.inc"
+
+int lifting_index(int Z)
+{
+  static const int odd_to_ils[16] = {-1, 0, -1, 1, -1, 2, -1, 3, -1, 4, -1, 5, -1, 6, -1, 7};
+  if (Z < 2 || Z > MAX_LIFTING_SIZE) {
+    return -1;
+  }
+  int a = Z;
+  while ((a & 1) == 0) {
+    a >>= 1;
+  }
+  return (a > 15) ? -1 : odd_to_ils[a];
+}
+
+bool build_lifted_graph(lifted_graph& g, int bg, int Z)
+{
+  const unsigned short(*tab)[10] = nullptr;
+  int count                      = 0;
+  if (bg == 1) {
+    g.K = 22; g.N_full = 68; g.N_short = 66; g.M = 46;
+    tab   = SRS_BG1_EDGES;
+    count = SRS_BG1_EDGES_COUNT;
+  } else if (bg == 2) {
+    g.K = 10; g.N_full = 52; g.N_short = 50; g.M = 42;
+    tab   = SRS_BG2_EDGES;
+    count = SRS_BG2_EDGES_COUNT;
+  } else {
+    return false;
+  }
+  int ils = lifting_index(Z);
+  if (ils < 0) {
+    return false;
+  }
+  g.bg     = bg;
+  g.Z      = Z;
+  g.nedges = count;
+  int m    = 0;
+  g.row_start[0] = 0;
+  for (int e = 0; e < count; ++e) {
+    while (tab[e][0] != m) {
+      g.row_start[++m] = e;
+    }
+    g.var[e]   = static_cast<uint8_t>(tab[e][1]);
+    g.shift[e] = static_cast<uint16_t>(tab[e][2 + ils] % Z);
+  }
+  while (m < g.M) {
+    g.row_start[++m] = count;
+  }
+  for (int r = g.M + 1; r <= MAX_BG_M; ++r) {
+    g.row_start[r] = count;
+  }
+  return true;
+}
+
+bool crc_params(int poly, uint32_t& polynom, int& order)
+{
+  switch (poly) {
+    case 0: order = 24; polynom = 0x1864cfb; return true; // CRC24A
+    case 1: order = 24; polynom = 0x1800063; return true; // CRC24B
+    case 2: order = 24; polynom = 0x1b2b117; return true; // CRC24C
+    case 3: order = 16; polynom = 0x11021; return true;   // CRC16
+    case 4: order = 11; polynom = 0xe21; return true;     // CRC11
+    case 5: order = 6; polynom = 0x61; return true;       // CRC6
+    default: return false;
+  }
+}
+
+} // namespace srs_amd

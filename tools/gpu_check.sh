@@ -1,0 +1,26 @@
+#!/bin/bash
+# Runs GPU tests, a short bench and a rocprofv3 kernel-trace summary on the GPU box.
+# Stops at the first fault / abort / timeout (exit codes other than 0 and 1).
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
+    benchq) step bench 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
