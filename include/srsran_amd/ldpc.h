@@ -72,8 +72,8 @@ const char* srs_amd_version(void);
 int srs_amd_ldpc_decoder_create(srs_amd_ldpc_decoder** decoder, int arith, int force_decoding, int device);
 void srs_amd_ldpc_decoder_destroy(srs_amd_ldpc_decoder* decoder);
 
-/* Maximum number of workgroups (codeblocks decoded concurrently) per launch;
- * sizes the check-to-variable scratch.  Default 2048. */
+/* Caps the launch grid (workgroups); larger batches are walked grid-stride.
+ * Default 2^20 (one workgroup per codeblock). */
 int srs_amd_ldpc_decoder_set_max_slots(srs_amd_ldpc_decoder* decoder, uint32_t max_slots);
 
 /* Single codeblock, HOST buffers, synchronous: ldpc_decoder::decode. */

@@ -20,6 +20,7 @@ namespace srs_amd {
 
 
 hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, int arith, int grid, hipStream_t stream);
+size_t     ldpc_decode_lds_bytes(const lifted_graph& g);
 
 namespace {
 
@@ -42,7 +43,7 @@ int hip_fail(hipError_t e, const char* what)
 }
 
 constexpr int      MAX_CRC_BITS_LEN = 22 * MAX_LIFTING_SIZE;
-constexpr uint32_t DEFAULT_SLOTS    = 2048;
+constexpr uint32_t DEFAULT_SLOTS    = 1u << 20;
 
 // x^(k+L) mod g for k = 0..MAX_CRC_BITS_LEN-1: the CRC of a single 1 bit
 // followed by k zeros (crc_calculator_generic_impl.cpp:98 long division).
@@ -86,8 +87,6 @@ struct srs_amd_ldpc_decoder {
   int                     force_decoding = 0;
   int                     device         = 0;
   uint32_t                max_slots      = DEFAULT_SLOTS;
-  int8_t*                 c2v_ws         = nullptr;
-  size_t                  ws_bytes       = 0;
   uint32_t*               crc_tables     = nullptr; // 6 x MAX_CRC_BITS_LEN
   int8_t*                 h_in           = nullptr; // staging for the single-CB host call
   uint8_t*                h_out          = nullptr;
@@ -124,25 +123,6 @@ int validate(const srs_amd_ldpc_decoder_config* cfg, int crc_poly)
   if (crc_poly != SRS_AMD_NO_CRC && (crc_poly < 0 || crc_poly > 5)) {
     return fail(SRS_AMD_EINVAL, "Invalid CRC polynomial %d", crc_poly);
   }
-  return SRS_AMD_OK;
-}
-
-int ensure_workspace(srs_amd_ldpc_decoder* d)
-{
-  size_t need = static_cast<size_t>(d->max_slots) * MAX_EDGES * MAX_LIFTING_SIZE;
-  if (d->ws_bytes >= need) {
-    return SRS_AMD_OK;
-  }
-  if (d->c2v_ws) {
-    (void)hipFree(d->c2v_ws);
-    d->c2v_ws   = nullptr;
-    d->ws_bytes = 0;
-  }
-  hipError_t e = hipMalloc(&d->c2v_ws, need);
-  if (e != hipSuccess) {
-    return hip_fail(e, "hipMalloc(check-to-variable workspace)");
-  }
-  d->ws_bytes = need;
   return SRS_AMD_OK;
 }
 
@@ -245,7 +225,6 @@ void srs_amd_ldpc_decoder_destroy(srs_amd_ldpc_decoder* d)
     (void)hipStreamSynchronize(d->stream);
     (void)hipStreamDestroy(d->stream);
   }
-  (void)hipFree(d->c2v_ws);
   (void)hipFree(d->crc_tables);
   (void)hipFree(d->h_in);
   (void)hipFree(d->h_out);
@@ -259,15 +238,7 @@ int srs_amd_ldpc_decoder_set_max_slots(srs_amd_ldpc_decoder* d, uint32_t max_slo
     return fail(SRS_AMD_EINVAL, "invalid decoder or slot count");
   }
   std::lock_guard<std::mutex> lock(d->mtx);
-  if (max_slots != d->max_slots) {
-    d->max_slots = max_slots;
-    if (d->c2v_ws) {
-      (void)hipStreamSynchronize(d->stream);
-      (void)hipFree(d->c2v_ws);
-      d->c2v_ws   = nullptr;
-      d->ws_bytes = 0;
-    }
-  }
+  d->max_slots = max_slots;
   return SRS_AMD_OK;
 }
 
@@ -321,10 +292,6 @@ int srs_amd_ldpc_decode_batch(srs_amd_ldpc_decoder*              d,
   if (e != hipSuccess) {
     return hip_fail(e, "hipSetDevice");
   }
-  rc = ensure_workspace(d);
-  if (rc != SRS_AMD_OK) {
-    return rc;
-  }
   const lifted_graph& g = get_graph(d, static_cast<int>(cfg->base_graph), static_cast<int>(Z));
 
   decode_args a{};
@@ -333,7 +300,6 @@ int srs_amd_ldpc_decode_batch(srs_amd_ldpc_decoder*              d,
   a.out             = d_output;
   a.nof_iters       = d_nof_iters;
   a.soft_out        = d_soft_out;
-  a.c2v_ws          = d->c2v_ws;
   a.crc_table       = crc_poly == SRS_AMD_NO_CRC ? nullptr : d->crc_tables + static_cast<size_t>(crc_poly) * MAX_CRC_BITS_LEN;
   a.llr_stride      = llr_stride;
   a.llr_len         = llr_len;
@@ -342,7 +308,6 @@ int srs_amd_ldpc_decode_batch(srs_amd_ldpc_decoder*              d,
   a.nof_filler_bits = static_cast<int32_t>(cfg->nof_filler_bits);
   a.max_iterations  = static_cast<int32_t>(cfg->max_iterations);
   a.force_decoding  = d->force_decoding;
-  a.zpad            = static_cast<int32_t>(MAX_LIFTING_SIZE);
   const int grid    = static_cast<int>(nof_cbs < d->max_slots ? nof_cbs : d->max_slots);
   e = launch_ldpc_decode(a, g, d->arith, grid, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) {

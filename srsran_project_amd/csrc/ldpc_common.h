@@ -40,8 +40,8 @@ struct lifted_graph {
   int32_t  M;       // check nodes (46 / 42)
   int32_t  nedges;
   int32_t  row_start[MAX_BG_M + 1];
-  uint8_t  var[MAX_EDGES];
-  uint16_t shift[MAX_EDGES];
+  // edge e: (var * Z) | (shift << 16), edges of check row m in [row_start[m], row_start[m+1]).
+  uint32_t edge[MAX_EDGES];
 };
 
 // Arguments of the batched decoder kernel (ldpc_decoder.hip).
@@ -51,7 +51,6 @@ struct decode_args {
   uint8_t*        out;          // [nof_cbs][out_stride] packed MSB-first hard bits
   int32_t*        nof_iters;    // [nof_cbs]: iterations on CRC pass, -1 = no value
   int8_t*         soft_out;     // optional [nof_cbs][N_full*Z] final soft bits
-  int8_t*         c2v_ws;       // [gridDim.x][nedges][Zpad] check-to-variable scratch
   const uint32_t* crc_table;    // x^(k+L) mod g, k = 0..K*Z-1 (null = no CRC)
   uint32_t        llr_stride;
   uint32_t        llr_len;
@@ -60,7 +59,6 @@ struct decode_args {
   int32_t         nof_filler_bits;
   int32_t         max_iterations;
   int32_t         force_decoding;
-  int32_t         zpad;
 };
 
 // Fills g for (bg, Z); returns false for an invalid pair.

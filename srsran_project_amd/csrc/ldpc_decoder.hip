@@ -18,9 +18,10 @@
 //     whole decode: every edge update is an LDS gather/scatter at a per-edge
 //     cyclic shift, HBM is touched only to read the LLRs once and write the
 //     packed hard bits once;
-//   * check-to-variable messages: int8 per (edge, check row), kept in a per-slot
-//     scratch region read/written with coalesced byte accesses (L2/MALL resident);
-//   * the graph (per-layer edge list: variable node + shift) is a kernel
+//   * check-to-variable messages: int8 per (edge, check row), also in LDS
+//     (BG1 Z=384: 26 KiB soft bits + 121 KiB messages = 147 KiB of the 160 KiB),
+//     so the whole decoder state of a codeblock stays on chip;
+//   * the graph (per-layer edge list, packed (var*Z) | shift<<16) is a kernel
 //     argument, read through the scalar cache;
 //   * CRC early stop: the CRC is linear over GF(2), so each lane XORs the
 //     precomputed remainders x^(n-1-i+L) mod g of its set hard bits and the
@@ -73,24 +74,87 @@ __device__ __forceinline__ int wave_max(int v)
   return v;
 }
 
+// One layer (base-graph check row) for check row j of the lifted graph:
+// ldpc_decoder_impl.cpp:235 (v2c), :290 (min / second min / sign, scaling),
+// :270 (soft-bit promotion sum).  DEG is the row degree, so the body is
+// straight-line code: all LDS gathers are issued before the first use.
+template <int DEG, int ARITH>
+__device__ __forceinline__ void
+process_layer(int8_t* soft, int8_t* c2v, const uint32_t* edge, int e0, int Z, int j, bool active)
+{
+  int ad[DEG];
+  int sb[DEG];
+  int cv[DEG];
+#pragma unroll
+  for (int e = 0; e < DEG; ++e) {
+    const uint32_t d = edge[e0 + e];
+    int            p = j + static_cast<int>(d >> 16);
+    p                = p >= Z ? p - Z : p;
+    ad[e]            = static_cast<int>(d & 0xffffu) + p;
+  }
+#pragma unroll
+  for (int e = 0; e < DEG; ++e) {
+    sb[e] = soft[ad[e]];
+    cv[e] = c2v[(e0 + e) * Z + j];
+  }
+  int min1 = LLR_MAX, min2 = LLR_MAX, idx = 0, sgn = 0;
+#pragma unroll
+  for (int e = 0; e < DEG; ++e) {
+    // v2c = soft - c2v saturated to +-LLR_MAX; infinite soft bits stay infinite.
+    const int  x   = sb[e];
+    const bool inf = (x > LLR_MAX) || (x < -LLR_MAX);
+    const int  v   = inf ? x : clamp_i(x - cv[e], -LLR_MAX, LLR_MAX);
+    sb[e]          = v; // reuse as v2c
+    const int  av  = v < 0 ? -v : v;
+    const bool lt1 = av < min1;
+    min2           = lt1 ? min1 : (av < min2 ? av : min2);
+    idx            = lt1 ? e : idx;
+    min1           = lt1 ? av : min1;
+    sgn ^= (v < 0);
+  }
+  const int s1 = scale_mag<ARITH>(min1);
+  const int s2 = scale_mag<ARITH>(min2);
+#pragma unroll
+  for (int e = 0; e < DEG; ++e) {
+    const int  v   = sb[e];
+    const int  mag = (e == idx) ? s2 : s1;
+    const int  c   = (sgn ^ (v < 0)) ? -mag : mag;
+    // promotion sum (log_likelihood_ratio.cpp:75); c is always finite, and
+    // c == -v gives 0 through the plain sum.
+    const bool inf = (v > LLR_MAX) || (v < -LLR_MAX);
+    int        t   = c + v;
+    t              = t > LLR_MAX ? LLR_INFINITY : (t < -LLR_MAX ? -LLR_INFINITY : t);
+    cv[e]          = c;
+    sb[e]          = inf ? v : t;
+  }
+  if (active) {
+#pragma unroll
+    for (int e = 0; e < DEG; ++e) {
+      c2v[(e0 + e) * Z + j] = static_cast<int8_t>(cv[e]);
+      soft[ad[e]]           = static_cast<int8_t>(sb[e]);
+    }
+  }
+}
+
 template <int MAXDEG, int ARITH>
 __global__ void __launch_bounds__(MAX_LIFTING_SIZE) ldpc_decode_kernel(decode_args a, lifted_graph g)
 {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   // smem layout: [0, 64) reduction slots (int32 x 16), then soft bits N_full*Z.
-  int32_t* red  = reinterpret_cast<int32_t*>(smem);
-  int8_t*  soft = smem + 64;
+  const int Z    = g.Z;
+  int32_t*  red  = reinterpret_cast<int32_t*>(smem);
+  int8_t*   soft = smem + 64;
+  int8_t*   c2v  = soft + ((g.N_full * Z + 15) & ~15); // [edge][check row]
 
-  const int  Z       = g.Z;
   const int  j       = threadIdx.x;
   const int  nthr    = blockDim.x;
   const bool active  = j < Z;
+  const int  jj      = active ? j : 0; // idle lanes gather valid addresses, store nothing
   const int  wave    = j >> 6;
   const int  nwaves  = nthr >> 6;
   const int  lane    = j & 63;
   const int  msg_len = g.K * Z;
   const int  NZ      = g.N_full * Z;
-  int8_t*    c2v     = a.c2v_ws + static_cast<size_t>(blockIdx.x) * g.nedges * a.zpad;
 
   for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
     const int8_t* in      = a.llrs + static_cast<size_t>(cb) * a.llr_stride;
@@ -158,56 +222,27 @@ __global__ void __launch_bounds__(MAX_LIFTING_SIZE) ldpc_decode_kernel(decode_ar
     int       result         = -1;
     __syncthreads();
 
+    // check-to-variable messages start at zero (ldpc_decoder_impl.cpp:244: an
+    // uninitialised layer uses v2c = soft, identical to v2c = soft - 0).
+    for (int i = j * 16; i < g.nedges * Z; i += nthr * 16) {
+      *reinterpret_cast<int4*>(c2v + i) = make_int4(0, 0, 0, 0);
+    }
+    __syncthreads();
+
     for (int it = 0; it < a.max_iterations; ++it) {
       for (int l = 0; l < nof_layers; ++l) {
         const int e0  = g.row_start[l];
         const int deg = g.row_start[l + 1] - e0;
-        int       v2c[MAXDEG];
-        int       addr[MAXDEG];
-        int       min1 = LLR_MAX, min2 = LLR_MAX, idx = 0, sgn = 0;
-#pragma unroll
-        for (int e = 0; e < MAXDEG; ++e) {
-          if (e < deg) {
-            const int var = g.var[e0 + e];
-            int       p   = j + g.shift[e0 + e];
-            p             = p >= Z ? p - Z : p;
-            addr[e]       = var * Z + p;
-            int sb        = active ? soft[addr[e]] : 0;
-            int c         = (it > 0 && active) ? c2v[(e0 + e) * a.zpad + j] : 0;
-            // v2c = soft - c2v saturated to +-LLR_MAX; infinite soft bits stay infinite.
-            int v    = (sb == LLR_INFINITY || sb == -LLR_INFINITY) ? sb : clamp_i(sb - c, -LLR_MAX, LLR_MAX);
-            v2c[e]   = v;
-            int  av  = v < 0 ? -v : v;
-            bool lt1 = av < min1;
-            min2     = lt1 ? min1 : (av < min2 ? av : min2);
-            idx      = lt1 ? e : idx;
-            min1     = lt1 ? av : min1;
-            sgn ^= (v < 0);
-          }
-        }
-        const int s1 = scale_mag<ARITH>(min1);
-        const int s2 = scale_mag<ARITH>(min2);
-#pragma unroll
-        for (int e = 0; e < MAXDEG; ++e) {
-          if (e < deg) {
-            const int v   = v2c[e];
-            const int mag = (e == idx) ? s2 : s1;
-            const int c   = (sgn ^ (v < 0)) ? -mag : mag;
-            // promotion sum (log_likelihood_ratio.cpp:75); c is always finite.
-            int s;
-            if (c == -v) {
-              s = 0;
-            } else if (v == LLR_INFINITY || v == -LLR_INFINITY) {
-              s = v;
-            } else {
-              s = c + v;
-              s = s > LLR_MAX ? LLR_INFINITY : (s < -LLR_MAX ? -LLR_INFINITY : s);
-            }
-            if (active) {
-              c2v[(e0 + e) * a.zpad + j] = static_cast<int8_t>(c);
-              soft[addr[e]]              = static_cast<int8_t>(s);
-            }
-          }
+        switch (deg) {
+          case 3: process_layer<3, ARITH>(soft, c2v, g.edge, e0, Z, jj, active); break;
+          case 4: process_layer<4, ARITH>(soft, c2v, g.edge, e0, Z, jj, active); break;
+          case 5: process_layer<5, ARITH>(soft, c2v, g.edge, e0, Z, jj, active); break;
+          case 6: process_layer<6, ARITH>(soft, c2v, g.edge, e0, Z, jj, active); break;
+          case 7: process_layer<7, ARITH>(soft, c2v, g.edge, e0, Z, jj, active); break;
+          case 8: process_layer<8, ARITH>(soft, c2v, g.edge, e0, Z, jj, active); break;
+          case 9: process_layer<9, ARITH>(soft, c2v, g.edge, e0, Z, jj, active); break;
+          case 10: process_layer<10, ARITH>(soft, c2v, g.edge, e0, Z, jj, active); break;
+          default: process_layer<19, ARITH>(soft, c2v, g.edge, e0, Z, jj, active); break;
         }
         __syncthreads();
       }
@@ -268,10 +303,15 @@ __global__ void __launch_bounds__(MAX_LIFTING_SIZE) ldpc_decode_kernel(decode_ar
 }
 
 // Host launcher (declared in ldpc_api.cpp).
+size_t ldpc_decode_lds_bytes(const lifted_graph& g)
+{
+  return 64 + ((static_cast<size_t>(g.N_full) * g.Z + 15) / 16) * 16 + static_cast<size_t>(g.nedges) * g.Z;
+}
+
 hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, int arith, int grid, hipStream_t stream)
 {
-  const int threads = ((g.Z + 63) / 64) * 64;
-  const size_t lds  = 64 + ((static_cast<size_t>(g.N_full) * g.Z + 15) / 16) * 16;
+  const int    threads = ((g.Z + 63) / 64) * 64;
+  const size_t lds     = ldpc_decode_lds_bytes(g);
   if (g.bg == 1) {
     if (arith == ARITH_GENERIC) {
       hipLaunchKernelGGL((ldpc_decode_kernel<BG1_MAX_DEGREE, ARITH_GENERIC>), dim3(grid), dim3(threads), lds, stream, args, g);

@@ -50,8 +50,9 @@ bool build_lifted_graph(lifted_graph& g, int bg, int Z)
     while (tab[e][0] != m) {
       g.row_start[++m] = e;
     }
-    g.var[e]   = static_cast<uint8_t>(tab[e][1]);
-    g.shift[e] = static_cast<uint16_t>(tab[e][2 + ils] % Z);
+    const uint32_t var   = tab[e][1];
+    const uint32_t shift = tab[e][2 + ils] % Z;
+    g.edge[e]            = (var * static_cast<uint32_t>(Z)) | (shift << 16);
   }
   while (m < g.M) {
     g.row_start[++m] = count;
