@@ -9,7 +9,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsrsran_amd.so")
+LIB_PATH = os.environ.get("SRSRAN_AMD_LIB") or os.path.join(_HERE, "lib", "libsrsran_amd.so")
 
 SRS_AMD_OK = 0
 SRS_AMD_EINVAL = -1

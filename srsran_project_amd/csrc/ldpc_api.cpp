@@ -14,6 +14,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 namespace srs_amd {
@@ -88,6 +89,7 @@ struct srs_amd_ldpc_decoder {
   int                     device         = 0;
   uint32_t                max_slots      = DEFAULT_SLOTS;
   uint32_t*               crc_tables     = nullptr; // 6 x MAX_CRC_BITS_LEN
+  uint32_t*               edges          = nullptr; // [2][51][MAX_EDGES] lifted edge descriptors
   int8_t*                 h_in           = nullptr; // staging for the single-CB host call
   uint8_t*                h_out          = nullptr;
   int32_t*                h_it           = nullptr;
@@ -204,6 +206,26 @@ int srs_amd_ldpc_decoder_create(srs_amd_ldpc_decoder** decoder, int arith, int f
   if (e == hipSuccess) {
     e = hipMemcpy(d->crc_tables, tables.data(), tables.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   }
+  // Every lifted graph (2 base graphs x 51 lifting sizes, 129 KiB), uploaded once.
+  std::vector<uint32_t> edges(2 * NOF_LIFTING_SIZES * MAX_EDGES, 0);
+  for (int bg = 1; bg <= 2; ++bg) {
+    for (int pos = 0; pos < NOF_LIFTING_SIZES; ++pos) {
+      lifted_graph lg{};
+      for (int z = 2; z <= MAX_LIFTING_SIZE; ++z) {
+        if (lifting_size_position(z) == pos) {
+          build_lifted_graph(lg, bg, z);
+          break;
+        }
+      }
+      std::copy(lg.edge, lg.edge + MAX_EDGES, edges.begin() + ((bg - 1) * NOF_LIFTING_SIZES + pos) * MAX_EDGES);
+    }
+  }
+  if (e == hipSuccess) {
+    e = hipMalloc(&d->edges, edges.size() * sizeof(uint32_t));
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpy(d->edges, edges.data(), edges.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) {
     e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
   }
@@ -226,6 +248,7 @@ void srs_amd_ldpc_decoder_destroy(srs_amd_ldpc_decoder* d)
     (void)hipStreamDestroy(d->stream);
   }
   (void)hipFree(d->crc_tables);
+  (void)hipFree(d->edges);
   (void)hipFree(d->h_in);
   (void)hipFree(d->h_out);
   (void)hipFree(d->h_it);
@@ -301,6 +324,8 @@ int srs_amd_ldpc_decode_batch(srs_amd_ldpc_decoder*              d,
   a.nof_iters       = d_nof_iters;
   a.soft_out        = d_soft_out;
   a.crc_table       = crc_poly == SRS_AMD_NO_CRC ? nullptr : d->crc_tables + static_cast<size_t>(crc_poly) * MAX_CRC_BITS_LEN;
+  a.edges = d->edges + ((cfg->base_graph - 1) * NOF_LIFTING_SIZES + lifting_size_position(static_cast<int>(Z))) *
+                             static_cast<size_t>(MAX_EDGES);
   a.llr_stride      = llr_stride;
   a.llr_len         = llr_len;
   a.out_stride      = out_stride;

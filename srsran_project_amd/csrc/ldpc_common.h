@@ -52,6 +52,7 @@ struct decode_args {
   int32_t*        nof_iters;    // [nof_cbs]: iterations on CRC pass, -1 = no value
   int8_t*         soft_out;     // optional [nof_cbs][N_full*Z] final soft bits
   const uint32_t* crc_table;    // x^(k+L) mod g, k = 0..K*Z-1 (null = no CRC)
+  const uint32_t* edges;        // device copy of lifted_graph::edge for this (BG, Z)
   uint32_t        llr_stride;
   uint32_t        llr_len;
   uint32_t        out_stride;
@@ -60,6 +61,10 @@ struct decode_args {
   int32_t         max_iterations;
   int32_t         force_decoding;
 };
+
+// Position of a lifting size in the 51-entry list (ldpc.h all_lifting_sizes), -1 if invalid.
+int lifting_size_position(int Z);
+constexpr int NOF_LIFTING_SIZES = 51;
 
 // Fills g for (bg, Z); returns false for an invalid pair.
 bool build_lifted_graph(lifted_graph& g, int bg, int Z);

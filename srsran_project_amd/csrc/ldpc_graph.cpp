@@ -22,6 +22,20 @@ int lifting_index(int Z)
   return (a > 15) ? -1 : odd_to_ils[a];
 }
 
+int lifting_size_position(int Z)
+{
+  static const int sizes[NOF_LIFTING_SIZES] = {2,   3,   4,   5,   6,   7,   8,   9,   10,  11,  12,  13,  14,
+                                               15,  16,  18,  20,  22,  24,  26,  28,  30,  32,  36,  40,  44,
+                                               48,  52,  56,  60,  64,  72,  80,  88,  96,  104, 112, 120, 128,
+                                               144, 160, 176, 192, 208, 224, 240, 256, 288, 320, 352, 384};
+  for (int i = 0; i < NOF_LIFTING_SIZES; ++i) {
+    if (sizes[i] == Z) {
+      return i;
+    }
+  }
+  return -1;
+}
+
 bool build_lifted_graph(lifted_graph& g, int bg, int Z)
 {
   const unsigned short(*tab)[10] = nullptr;

@@ -1,0 +1,12 @@
+#!/bin/bash
+# ab.sh <variant>... : bench each exp/<variant>/libsrsran_amd.so (short runs, no CPU baseline).
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+mkdir -p gpurun_out
+for r in 1 2; do
+for v in "$@"; do
+  SRSRAN_AMD_LIB=$PWD/exp/$v/libsrsran_amd.so timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err
+  rc=$?
+  if [ $rc -ne 0 ]; then echo "$v rc=$rc"; tail -3 gpurun_out/ab_$v.err; exit $rc; fi
+  python -c "import json,sys; d=json.load(open('gpurun_out/ab_$v.json')); print('$v', round(d['value']), 'CB/s', round(d['roofline']['kernel_ms'],3), 'ms')"
+done
+done
