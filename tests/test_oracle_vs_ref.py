@@ -1,0 +1,84 @@
+"""Pins the CPU oracle (oracle/srs_oracle.c) to the reference itself.
+
+oracle/_ref/libsrsran_ref.so is compiled from /root/reference's own LDPC/CRC
+sources (oracle/Makefile); the reference's .dat test vectors are not shipped,
+so this is the pin: the oracle must reproduce the reference decoders
+(generic, AVX2, AVX512) bit-for-bit, the reference encoder and CRCs.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from tests.ldpc_cases import noisy_codeblocks
+
+pytestmark = pytest.mark.skipif(oracle.REF is None, reason="oracle/_ref/libsrsran_ref.so not built")
+
+IMPLS = [("generic", "generic"), ("avx2", "simd"), ("avx512", "simd")]
+
+
+def _impls():
+    return [(i, a) for i, a in IMPLS if oracle.REF.srs_ref_has_impl(i.encode())]
+
+
+@pytest.mark.parametrize("bg", [1, 2])
+def test_encoder_matches_reference(bg):
+    rng = np.random.default_rng(bg)
+    for Z in (2, 3, 5, 6, 7, 9, 11, 13, 15, 22, 36, 60, 104, 176, 208, 240, 352, 384):
+        K = oracle.BG_K[bg] * Z
+        m = rng.integers(0, 2, K).astype(np.uint8)
+        np.testing.assert_array_equal(oracle.ldpc_encode(m, bg, Z), oracle.ref_ldpc_encode(m, bg, Z),
+                                      err_msg="bg%d Z%d" % (bg, Z))
+
+
+@pytest.mark.parametrize("bg", [1, 2])
+def test_decoder_matches_reference(bg):
+    for impl, arith in _impls():
+        for Z in (2, 5, 14, 40, 112, 384):
+            for noise in (4.0, 10.0):
+                msgs, llrs = noisy_codeblocks(bg, Z, 2, noise=noise, seed=Z + int(noise))
+                for i in range(2):
+                    for iters in (1, 5):
+                        r1, o1 = oracle.ref_ldpc_decode(impl, llrs[i], bg, Z, iters)
+                        r2, o2, _ = oracle.ldpc_decode(llrs[i], bg, Z, iters, arith)
+                        assert r1 == r2
+                        np.testing.assert_array_equal(o1, o2, err_msg="%s bg%d Z%d" % (impl, bg, Z))
+
+
+def test_decoder_crc_early_stop_matches_reference():
+    for impl, arith in _impls():
+        for bg, Z, poly in ((1, 384, 1), (1, 52, 0), (2, 16, 3)):
+            msgs, llrs = noisy_codeblocks(bg, Z, 3, noise=10.0, seed=Z, crc_poly=poly)
+            nb = 24 if poly in (0, 1) else 16
+            for i in range(3):
+                r1, o1 = oracle.ref_ldpc_decode(impl, llrs[i], bg, Z, 10, crc_poly=poly, nof_crc_bits=nb)
+                r2, o2, _ = oracle.ldpc_decode(llrs[i], bg, Z, 10, arith, crc_poly=poly, nof_crc_bits=nb)
+                assert r1 == r2, (impl, bg, Z, i)
+                np.testing.assert_array_equal(o1, o2)
+
+
+def test_decoder_shortened_filler_and_force():
+    for impl, arith in _impls():
+        bg, Z = 1, 64
+        msgs, llrs = noisy_codeblocks(bg, Z, 1, noise=6.0, seed=3)
+        for L in (24 * Z, 38 * Z, 52 * Z, 66 * Z, 30 * Z + 7):
+            r1, o1 = oracle.ref_ldpc_decode(impl, llrs[0, :L], bg, Z, 4, crc_poly=0, nof_filler_bits=40,
+                                            nof_crc_bits=24)
+            r2, o2, _ = oracle.ldpc_decode(llrs[0, :L], bg, Z, 4, arith, crc_poly=0, nof_filler_bits=40,
+                                           nof_crc_bits=24)
+            assert r1 == r2
+            np.testing.assert_array_equal(o1, o2)
+        short = np.zeros(66 * Z, np.int8)
+        short[:100] = 9
+        r1, o1 = oracle.ref_ldpc_decode(impl, short, bg, Z, 2, force_decoding=True)
+        r2, o2, _ = oracle.ldpc_decode(short, bg, Z, 2, arith, force_decoding=True)
+        assert r1 == r2 is None
+        np.testing.assert_array_equal(o1, o2)
+
+
+def test_crc_matches_reference():
+    rng = np.random.default_rng(0)
+    for poly in range(6):
+        for n in (0, 1, 7, 8, 100, 3823, 8424):
+            bits = rng.integers(0, 2, n).astype(np.uint8)
+            ref = oracle.REF.srs_ref_crc_bits(poly, bits.ctypes.data_as(oracle.P), n)
+            assert oracle.crc_bits(poly, bits) == ref, (poly, n)
