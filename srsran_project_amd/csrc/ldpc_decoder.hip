@@ -17,13 +17,18 @@
 //     workgroup barrier);
 //   * soft bits (N_full x Z int8, <= 26 KiB) live in LDS for the whole decode:
 //     every edge update is an LDS gather/scatter at the edge's cyclic shift;
-//   * check-to-variable messages live in VGPRs: lane j holds the int8 message of
-//     every edge of check row j (BG1: 316 edges = 79 packed registers).  The
-//     layer schedule is unrolled at compile time over the base graph's row
-//     degrees, so every message has a fixed register and byte; extraction is
-//     one v_bfe_i32, insertion one v_perm_b32.  With 26 KiB of LDS and <= 128
-//     VGPRs per lane, two Z=384 codeblocks (12 waves) share a CU and hide each
-//     other's barrier / LDS latency;
+//   * check-to-variable messages: lane j holds the int8 message of every edge of
+//     check row j.  The layer schedule is unrolled at compile time over the base
+//     graph's row degrees, so every message has a fixed home: the light layers
+//     (degree <= 10, 240 of BG1's 316 edges) in VGPRs packed 4 per register
+//     (read as a sign-extended SDWA byte operand, written with one v_perm_b32),
+//     the four degree-19 rows of BG1 in LDS ([edge][row], 29 KiB at Z=384).
+//     That keeps a Z=384 codeblock at <= 128 VGPRs and 55 KiB of LDS, so two
+//     codeblocks (12 waves) share a CU and hide each other's barrier and LDS
+//     latency;
+//   * for Z=384 (the 100 MHz workloads) the lifted graph is compile-time: shifts
+//     and node offsets are literals (gather address = add, add, min); other Z
+//     read packed edge descriptors through the scalar unit;
 //   * HBM is touched only to read the LLRs once and write the packed hard bits;
 //   * CRC early stop: the CRC is linear over GF(2), so each lane XORs the
 //     precomputed remainders x^(n-1-i+L) mod g of its set hard bits and the
@@ -35,12 +40,29 @@
 
 namespace srs_amd {
 
+#define SRS_BG_TABLE_QUAL constexpr
+namespace tables {
+#include "bg_tables.inc"
+}
+#undef SRS_BG_TABLE_QUAL
+
 // Edge descriptors are read through the scalar unit (s_load from the constant
 // address space), never as per-lane vector loads.
 using const_u32_ptr = const __attribute__((address_space(4))) uint32_t*;
 
-// Row degrees of the base graphs (TS 38.212 Tables 5.3.2-2/3); the host checks
-// them against bg_tables.inc (ldpc_graph.cpp, check_row_degrees).
+// LDS addressing.  The kernels declare no static LDS, so the dynamic segment
+// starts at LDS address 0 and the carve-up offsets are plain integers: with a
+// compile-time Z every gather/scatter offset folds into the ds instruction's
+// immediate, and the compiler's occupancy model does not see a fixed 55 KiB
+// block (which would let it trade the 4-waves/SIMD target for registers).
+// Layout (bytes): [16,80) reductions | soft bits | LDS-resident messages | pad.
+constexpr int LDS_RED_OFFSET  = 16;
+constexpr int LDS_SOFT_OFFSET = 80;
+using lds_i8                  = __attribute__((address_space(3))) int8_t;
+using lds_i32                 = __attribute__((address_space(3))) int32_t;
+
+
+// Row degrees of the base graphs (TS 38.212 Tables 5.3.2-2/3).
 constexpr int BG1_DEG[46] = {19, 19, 19, 19, 3, 8, 9, 7, 10, 9, 7, 8, 7, 6, 7, 7, 6, 6, 6, 6, 6, 6, 5,
                              5,  6,  5,  5,  4, 5, 5, 5, 5,  5, 5, 5, 5, 5, 4, 5, 5, 4, 5, 4, 5, 5, 4};
 constexpr int BG2_DEG[42] = {8, 10, 8, 10, 4, 6, 6, 6, 4, 5, 5, 5, 4, 5, 5, 4, 5, 5, 4, 4, 4,
@@ -50,12 +72,15 @@ template <int BG>
 struct bg_traits;
 template <>
 struct bg_traits<1> {
-  static constexpr int M = 46, NEDGES = 316;
+  static constexpr int M = 46, NEDGES = 316, N_FULL = 68, K = 22;
+  // leading rows whose messages live in LDS (the degree-19 rows)
+  static constexpr int LDS_ROWS = 4, LDS_EDGES = 76;
   static constexpr int deg(int l) { return BG1_DEG[l]; }
 };
 template <>
 struct bg_traits<2> {
-  static constexpr int M = 42, NEDGES = 197;
+  static constexpr int M = 42, NEDGES = 197, N_FULL = 52, K = 10;
+  static constexpr int LDS_ROWS = 0, LDS_EDGES = 0;
   static constexpr int deg(int l) { return BG2_DEG[l]; }
 };
 template <int BG>
@@ -67,8 +92,45 @@ constexpr int row_start(int l)
   }
   return s;
 }
-static_assert(row_start<1>(46) == 316, "BG1 degree table");
+static_assert(row_start<1>(46) == 316 && row_start<1>(4) == bg_traits<1>::LDS_EDGES, "BG1 degree table");
 static_assert(row_start<2>(42) == 197, "BG2 degree table");
+template <int BG>
+constexpr int reg_words()
+{
+  return (bg_traits<BG>::NEDGES - bg_traits<BG>::LDS_EDGES + 3) / 4;
+}
+
+// TS 38.212 Table 5.3.2-1 set index of a lifting size (compile-time).
+constexpr int lifting_index_c(int Z)
+{
+  int a = Z;
+  while ((a & 1) == 0) {
+    a >>= 1;
+  }
+  return a == 1 ? 0 : a == 3 ? 1 : a == 5 ? 2 : a == 7 ? 3 : a == 9 ? 4 : a == 11 ? 5 : a == 13 ? 6 : 7;
+}
+
+// Edge E of base graph BG lifted to a compile-time Z: variable node and shift.
+template <int BG, int ZC, int E>
+struct const_edge {
+  static constexpr int var   = BG == 1 ? tables::SRS_BG1_EDGES[E][1] : tables::SRS_BG2_EDGES[E][1];
+  static constexpr int shift = (BG == 1 ? tables::SRS_BG1_EDGES[E][2 + lifting_index_c(ZC)]
+                                        : tables::SRS_BG2_EDGES[E][2 + lifting_index_c(ZC)]) %
+                               ZC;
+};
+
+// LDS carve-up (bytes): [0,64) reductions | soft bits N_full*Z | LDS-resident
+// messages LDS_EDGES*Z | 64-byte idle-lane pad.
+template <int BG>
+__host__ __device__ constexpr int lds_soft_bytes(int Z)
+{
+  return (bg_traits<BG>::N_FULL * Z + 15) & ~15;
+}
+template <int BG>
+__host__ __device__ constexpr int lds_total_bytes(int Z)
+{
+  return 80 + lds_soft_bytes<BG>(Z) + ((bg_traits<BG>::LDS_EDGES * Z + 15) & ~15) + 64;
+}
 
 __device__ __forceinline__ int med3_i(int x, int lo, int hi)
 {
@@ -111,31 +173,48 @@ __device__ __forceinline__ int wave_max(int v)
   return v;
 }
 
-// int8 message K of the packed register file.
+// int8 value K of a packed register array.
 template <int K, int NW>
-__device__ __forceinline__ int c2v_get(const uint32_t (&r)[NW])
+__device__ __forceinline__ int byte_get(const uint32_t (&r)[NW])
 {
   return static_cast<int>(static_cast<int8_t>(r[K >> 2] >> (8 * (K & 3))));
 }
 template <int K, int NW>
-__device__ __forceinline__ void c2v_set(uint32_t (&r)[NW], int c)
+__device__ __forceinline__ void byte_set(uint32_t (&r)[NW], int c)
 {
   // v_perm_b32: byte (K&3) from c, the other bytes from the old word.
   constexpr uint32_t sel = (K & 3) == 0 ? 0x07060500u : (K & 3) == 1 ? 0x07060004u : (K & 3) == 2 ? 0x07000504u : 0x00060504u;
   r[K >> 2]              = __builtin_amdgcn_perm(r[K >> 2], static_cast<uint32_t>(c), sel);
 }
 
-// Pass 1 for edge E: form v2c from the gathered soft bit and the old message
-// and update the check-node statistics (ldpc_decoder_impl.cpp:235 / :290).
-// v2c is kept packed (4 per register; pass 2 reads it back as a sign-extended
-// SDWA byte operand, free on gfx950).
-template <int E0, int E, int NW, int NX>
-__device__ __forceinline__ void
-edge_pass1(int s, uint32_t (&xp)[NX], const uint32_t (&c2v)[NW], int& min1, int& min2, int& idx, int& sgn)
+// Message of edge K (global edge index): a register byte, or (LDS-resident
+// rows) the value gathered into cl[] at the start of the layer.
+template <int BG, int K, int NW, int DEG>
+__device__ __forceinline__ int c2v_old(const uint32_t (&c2v)[NW], const int (&cl)[DEG], int e)
+{
+  if constexpr (K < bg_traits<BG>::LDS_EDGES) {
+    return cl[e];
+  } else {
+    return byte_get<K - bg_traits<BG>::LDS_EDGES>(c2v);
+  }
+}
+
+// Pass 1 for edge E: v2c from the gathered soft bit and the old message, plus
+// the check-node statistics (ldpc_decoder_impl.cpp:235 / :290).  v2c is kept
+// packed 4 per register (pass 2 reads it back as an SDWA byte operand).
+template <int BG, int E0, int E, int NW, int NX, int DEG>
+__device__ __forceinline__ void edge_pass1(int            s,
+                                           uint32_t (&xp)[NX],
+                                           const uint32_t (&c2v)[NW],
+                                           const int (&cl)[DEG],
+                                           int&           min1,
+                                           int&           min2,
+                                           int&           idx,
+                                           int&           sgn)
 {
   // v2c = soft - c2v saturated to +-LLR_MAX; infinite soft bits stay infinite.
   const bool inf = static_cast<unsigned>(s + LLR_MAX) > static_cast<unsigned>(2 * LLR_MAX);
-  const int  v   = inf ? s : med3_i(s - c2v_get<E0 + E>(c2v), -LLR_MAX, LLR_MAX);
+  const int  v   = inf ? s : med3_i(s - c2v_old<BG, E0 + E>(c2v, cl, E), -LLR_MAX, LLR_MAX);
   const int  av  = v < 0 ? -v : v;
   const bool lt1 = av < min1;
   idx            = lt1 ? E : idx;
@@ -143,15 +222,18 @@ edge_pass1(int s, uint32_t (&xp)[NX], const uint32_t (&c2v)[NW], int& min1, int&
   min2 = av < min1 ? min1 : (av < min2 ? av : min2);
   min1 = lt1 ? av : min1;
   sgn ^= v;
-  c2v_set<E>(xp, v);
+  byte_set<E>(xp, v);
 }
 
-// Pass 2 for edge E: new c2v (scaled min / second min with the extrinsic sign)
-// and the new soft bit, promotion sum c2v + v2c (ldpc_decoder_impl.cpp:310, :270).
-template <int E0, int E, int NW, int NX>
-__device__ __forceinline__ int edge_pass2(const uint32_t (&xp)[NX], uint32_t (&c2v)[NW], int s1, int s2, int idx, int sgn)
+// Pass 2 for edge E: the new message (scaled min / second min with the
+// extrinsic sign) and the new soft bit, the promotion sum message + v2c
+// (ldpc_decoder_impl.cpp:310, :270).  Returns the soft bit; the message goes to
+// its register byte or to cl[E].
+template <int BG, int E0, int E, int NW, int NX, int DEG>
+__device__ __forceinline__ int
+edge_pass2(const uint32_t (&xp)[NX], uint32_t (&c2v)[NW], int (&cl)[DEG], int s1, int s2, int idx, int sgn)
 {
-  const int v   = c2v_get<E>(xp);
+  const int v   = byte_get<E>(xp);
   const int mag = (E == idx) ? s2 : s1;
   const int c   = ((sgn ^ v) < 0) ? -mag : mag;
   // promotion sum (log_likelihood_ratio.cpp:75); c is always finite, and
@@ -159,65 +241,112 @@ __device__ __forceinline__ int edge_pass2(const uint32_t (&xp)[NX], uint32_t (&c
   const bool inf = static_cast<unsigned>(v + LLR_MAX) > static_cast<unsigned>(2 * LLR_MAX);
   int        t   = c + v;
   t              = t > LLR_MAX ? LLR_INFINITY : (t < -LLR_MAX ? -LLR_INFINITY : t);
-  c2v_set<E0 + E>(c2v, c);
+  if constexpr (E0 + E < bg_traits<BG>::LDS_EDGES) {
+    cl[E] = c;
+  } else {
+    byte_set<E0 + E - bg_traits<BG>::LDS_EDGES>(c2v, c);
+  }
   return inf ? v : t;
 }
 
-// One layer (base-graph check row) for check row j of the lifted graph.
-// E0/DEG are compile-time, so the body is straight-line code: all DEG gathers
-// are issued before the first use and all DEG scatters after the last, so no
-// LDS read ever waits behind a (possibly aliasing) LDS write of the same layer.
-// Idle lanes (j >= Z, only when Z is not a multiple of 64) are redirected to a
-// private dummy slot, so no exec-mask branches are needed.
-template <int E0, int ARITH, int NW, int... E>
-__device__ __forceinline__ void process_layer(int8_t*                  soft,
-                                              uint32_t (&c2v)[NW],
-                                              const_u32_ptr            edge,
-                                              int                      Z,
-                                              int                      j,
-                                              int                      idle_slot,
-                                              std::integer_sequence<int, E...>)
+// Gather address of edge E0+E for lane j: var*Z + (j + shift) mod Z, where
+// (j + shift - Z) wraps as an unsigned value exactly when j + shift < Z, so the
+// mod is one v_min_u32.  Compile-time Z: shift and node offset are literals.
+template <int BG, int ZC, int EI>
+__device__ __forceinline__ int gather_addr(const_u32_ptr edge, int Z, int j)
 {
-  constexpr int DEG = sizeof...(E);
-  constexpr int NX  = (DEG + 3) / 4;
-  int           ad[DEG];
-  int           x[DEG];
-  uint32_t      xp[NX];
-#pragma unroll
-  for (int e = 0; e < DEG; ++e) {
-    // gather address = var*Z + (j + shift) mod Z; (j + shift - Z) wraps as an
-    // unsigned value exactly when j + shift < Z, so the mod is one v_min_u32.
-    const uint32_t d     = edge[E0 + e];
+  if constexpr (ZC > 0) {
+    constexpr uint32_t s = const_edge<BG, ZC, EI>::shift;
+    return static_cast<int>(__builtin_elementwise_min(static_cast<uint32_t>(j) + s,
+                                                      static_cast<uint32_t>(j) + (s - static_cast<uint32_t>(ZC))) +
+                            static_cast<uint32_t>(const_edge<BG, ZC, EI>::var * ZC));
+  } else {
+    const uint32_t d     = edge[EI];
     const uint32_t shift = d >> 16;
     const uint32_t t1    = static_cast<uint32_t>(j) + shift;
     const uint32_t t2    = static_cast<uint32_t>(j) + (shift - static_cast<uint32_t>(Z));
-    ad[e]                = static_cast<int>((t1 < t2 ? t1 : t2) + (d & 0xffffu));
-    if (idle_slot >= 0) {
-      ad[e] = idle_slot;
-    }
+    return static_cast<int>((t1 < t2 ? t1 : t2) + (d & 0xffffu));
   }
-#pragma unroll
-  for (int e = 0; e < DEG; ++e) {
-    x[e] = soft[ad[e]];
-  }
+}
+
+// Edges of a layer are gathered and reduced in chunks of EDGE_CHUNK with a
+// scheduling barrier in between, which bounds the registers a degree-19 row
+// keeps in flight next to the message file.
+constexpr int EDGE_CHUNK = 5;
+
+// One layer (base-graph check row L) for check row j of the lifted graph.
+// Straight-line code: every gather of the layer precedes every scatter, so no
+// LDS read waits behind a (possibly aliasing) LDS write of the same layer.
+// Idle lanes (j >= Z, only possible when Z is not a multiple of 64) are
+// redirected to a private pad.  Rows of degree > 10 recompute their gather
+// addresses for the scatter instead of holding 19 of them live.
+template <int BG, int ZC, int L, int ARITH, int NW, int... E>
+__device__ __forceinline__ void process_layer(lds_i8*       soft,
+                                              lds_i8*       c2v_lds,
+                                              uint32_t (&c2v)[NW],
+                                              const_u32_ptr edge,
+                                              int           Z,
+                                              int           j,
+                                              int           idle_slot,
+                                              std::integer_sequence<int, E...>)
+{
+  constexpr int  E0     = row_start<BG>(L);
+  constexpr int  DEG    = sizeof...(E);
+  constexpr int  NX     = (DEG + 3) / 4;
+  constexpr bool IN_LDS = L < bg_traits<BG>::LDS_ROWS;
+  constexpr bool ALL_ON = ZC > 0 && (ZC % 64) == 0;
+  constexpr bool KEEP   = DEG <= 10;
+  int            ad[DEG];
+  int            cl[DEG];
+  uint32_t       xp[NX];
 #pragma unroll
   for (int w = 0; w < NX; ++w) {
     xp[w] = 0;
   }
+  const int jl = ALL_ON ? j : (idle_slot >= 0 ? 0 : j);
+  auto addr = [&](auto ec) {
+    constexpr int e = decltype(ec)::value;
+    const int     a = gather_addr<BG, ZC, E0 + e>(edge, Z, j);
+    return ALL_ON ? a : (idle_slot >= 0 ? idle_slot : a);
+  };
   int min1 = LLR_MAX, min2 = LLR_MAX, idx = 0, sgn = 0;
-  (edge_pass1<E0, E>(x[E], xp, c2v, min1, min2, idx, sgn), ...);
+  (
+      [&] {
+        if constexpr (E % EDGE_CHUNK == 0 && E > 0) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        ad[E]       = addr(std::integral_constant<int, E>{});
+        const int x = soft[ad[E]];
+        if constexpr (IN_LDS) {
+          cl[E] = c2v_lds[(E0 + E) * Z + jl];
+        }
+        edge_pass1<BG, E0, E>(x, xp, c2v, cl, min1, min2, idx, sgn);
+      }(),
+      ...);
+  __builtin_amdgcn_sched_barrier(0);
   const int s1 = scale_mag<ARITH>(min1);
   const int s2 = scale_mag<ARITH>(min2);
-  ((x[E] = edge_pass2<E0, E>(xp, c2v, s1, s2, idx, sgn)), ...);
-#pragma unroll
-  for (int e = 0; e < DEG; ++e) {
-    soft[ad[e]] = static_cast<int8_t>(x[e]);
-  }
+  (
+      [&] {
+        if constexpr (E % EDGE_CHUNK == 0 && E > 0 && !KEEP) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const int snew = edge_pass2<BG, E0, E>(xp, c2v, cl, s1, s2, idx, sgn);
+        const int a    = KEEP ? ad[E] : addr(std::integral_constant<int, E>{});
+        soft[a]        = static_cast<int8_t>(snew);
+        if constexpr (IN_LDS) {
+          if (ALL_ON || idle_slot < 0) {
+            c2v_lds[(E0 + E) * Z + j] = static_cast<int8_t>(cl[E]);
+          }
+        }
+      }(),
+      ...);
 }
 
-// Layers L .. M-1 of one iteration, stopping (uniformly) at nof_layers.
-template <int BG, int L, int ARITH, int NW>
-__device__ __forceinline__ void run_layers(int8_t*       soft,
+// Layers L .. M-1 of one iteration, skipping (uniformly) layers >= nof_layers.
+template <int BG, int ZC, int L, int ARITH, int NW>
+__device__ __forceinline__ void run_layers(lds_i8*       soft,
+                                           lds_i8*       c2v_lds,
                                            uint32_t (&c2v)[NW],
                                            const_u32_ptr edge,
                                            int           Z,
@@ -230,38 +359,47 @@ __device__ __forceinline__ void run_layers(int8_t*       soft,
     // it merges only the few message registers this layer writes, whereas 46
     // early exits would each merge the whole message file.
     if (L < nof_layers) {
-      // Launder the graph pointer and Z per layer: the gather addresses are
-      // iteration-invariant, and letting the compiler hoist (and keep live) the
-      // addresses and descriptors of later layers would spill the register file.
-      asm volatile("" : "+s"(edge), "+s"(Z));
-      process_layer<row_start<BG>(L), ARITH>(
-          soft, c2v, edge, Z, j, idle_slot, std::make_integer_sequence<int, bg_traits<BG>::deg(L)>{});
+      // Launder the lane index, graph pointer and Z per layer: the gather
+      // addresses are iteration-invariant, and letting the compiler hoist (and
+      // keep live) the addresses of later layers would spill the register file.
+      asm volatile("" : "+v"(j), "+s"(edge), "+s"(Z));
+      process_layer<BG, ZC, L, ARITH>(
+          soft, c2v_lds, c2v, edge, Z, j, idle_slot, std::make_integer_sequence<int, bg_traits<BG>::deg(L)>{});
       __syncthreads();
     }
-    run_layers<BG, L + 1, ARITH>(soft, c2v, edge, Z, j, idle_slot, nof_layers);
+    run_layers<BG, ZC, L + 1, ARITH>(soft, c2v_lds, c2v, edge, Z, j, idle_slot, nof_layers);
   }
 }
 
-template <int BG, int ARITH>
-__global__ void __launch_bounds__(MAX_LIFTING_SIZE, 4) ldpc_decode_kernel(decode_args a, lifted_graph g)
+// Occupancy target: 4 waves per SIMD (<= 128 VGPRs).  A Z=384 workgroup is 6
+// waves; two of them fit a CU whatever SIMD the dispatcher starts them on only
+// if every SIMD can hold 4 (at 3 per SIMD the second workgroup is mostly refused).
+template <int BG, int ZC>
+constexpr int waves_per_simd()
 {
-  constexpr int NW = (bg_traits<BG>::NEDGES + 3) / 4;
-  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  // smem layout: [0, 64) reduction slots (int32 x 16), then soft bits N_full*Z.
-  const int Z    = g.Z;
-  int32_t*  red  = reinterpret_cast<int32_t*>(smem);
-  int8_t*   soft = smem + 64;
+  return 4;
+}
+
+template <int BG, int ARITH, int ZC>
+__global__ void __launch_bounds__(MAX_LIFTING_SIZE, (waves_per_simd<BG, ZC>())) ldpc_decode_kernel(decode_args a, lifted_graph g)
+{
+  constexpr int NW      = reg_words<BG>();
+  constexpr int N_FULL  = bg_traits<BG>::N_FULL;
+  const int     Z       = ZC > 0 ? ZC : g.Z;
+  lds_i32*      red     = (lds_i32*)(uintptr_t)LDS_RED_OFFSET;
+  lds_i8*       soft    = (lds_i8*)(uintptr_t)LDS_SOFT_OFFSET;
+  lds_i8*       c2v_lds = soft + lds_soft_bytes<BG>(Z);
 
   const int  j       = threadIdx.x;
   const int  nthr    = blockDim.x;
   const bool active  = j < Z;
-  // idle lanes (Z not a multiple of 64) work on a private dummy byte past the soft bits
-  const int idle_slot = active ? -1 : ((g.N_full * Z + 15) & ~15) + (j & 63);
-  const int  wave    = j >> 6;
-  const int  nwaves  = nthr >> 6;
-  const int  lane    = j & 63;
-  const int  msg_len = g.K * Z;
-  const int  NZ      = g.N_full * Z;
+  // idle lanes (Z not a multiple of 64) work on a private pad byte after the messages
+  const int idle_slot = active ? -1 : lds_total_bytes<BG>(Z) - LDS_SOFT_OFFSET - 64 + (j & 63);
+  const int wave      = j >> 6;
+  const int nwaves    = nthr >> 6;
+  const int lane      = j & 63;
+  const int msg_len   = bg_traits<BG>::K * Z;
+  const int NZ        = N_FULL * Z;
 
   for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
     const int8_t* in     = a.llrs + static_cast<size_t>(cb) * a.llr_stride;
@@ -308,7 +446,7 @@ __global__ void __launch_bounds__(MAX_LIFTING_SIZE, 4) ldpc_decode_kernel(decode
     {
       const int nof_full_nodes = n_llrs / Z + 2;
       const int tail           = n_llrs - (nof_full_nodes - 2) * Z;
-      for (int node = 0; node < g.N_full; ++node) {
+      for (int node = 0; node < N_FULL; ++node) {
         for (int p = j; p < Z; p += nthr) {
           int v = 0;
           if (node >= 2 && node < nof_full_nodes) {
@@ -320,11 +458,15 @@ __global__ void __launch_bounds__(MAX_LIFTING_SIZE, 4) ldpc_decode_kernel(decode
         }
       }
     }
+    // LDS-resident messages start at zero, like the register ones below.
+    for (int i = j; i < bg_traits<BG>::LDS_EDGES * Z / 4; i += nthr) {
+      reinterpret_cast<lds_i32*>(c2v_lds)[i] = 0;
+    }
     int cb_len = input_size + 2 * Z;
     if (cb_len < msg_len + 4 * Z) {
       cb_len = msg_len + 4 * Z;
     }
-    const int nof_layers = (cb_len + Z - 1) / Z - g.K;
+    const int nof_layers = (cb_len + Z - 1) / Z - bg_traits<BG>::K;
     const int nof_sig    = msg_len - a.nof_filler_bits;
     int       result     = -1;
 
@@ -338,7 +480,7 @@ __global__ void __launch_bounds__(MAX_LIFTING_SIZE, 4) ldpc_decode_kernel(decode
     __syncthreads();
 
     for (int it = 0; it < a.max_iterations; ++it) {
-      run_layers<BG, 0, ARITH>(soft, c2v, (const_u32_ptr)(a.edges), Z, j, idle_slot, nof_layers);
+      run_layers<BG, ZC, 0, ARITH>(soft, c2v_lds, c2v, (const_u32_ptr)(a.edges), Z, j, idle_slot, nof_layers);
 
       if (a.crc_table) {
         // get_hard_bits + CRC early stop (ldpc_decoder_impl.cpp:125).
@@ -397,24 +539,36 @@ __global__ void __launch_bounds__(MAX_LIFTING_SIZE, 4) ldpc_decode_kernel(decode
 
 size_t ldpc_decode_lds_bytes(const lifted_graph& g)
 {
-  return 64 + ((static_cast<size_t>(g.N_full) * g.Z + 15) / 16) * 16 + 64;
+  return g.bg == 1 ? lds_total_bytes<1>(g.Z) : lds_total_bytes<2>(g.Z);
+}
+
+template <int BG, int ARITH>
+static void launch_bg(const decode_args& args, const lifted_graph& g, int grid, int threads, hipStream_t stream)
+{
+  // Specialised kernels for the largest lifting size (the 100 MHz workloads);
+  // every other Z runs the runtime-Z instantiation.
+  const size_t lds = lds_total_bytes<BG>(g.Z);
+  if (g.Z == 384) {
+    hipLaunchKernelGGL((ldpc_decode_kernel<BG, ARITH, 384>), dim3(grid), dim3(threads), lds, stream, args, g);
+  } else {
+    hipLaunchKernelGGL((ldpc_decode_kernel<BG, ARITH, 0>), dim3(grid), dim3(threads), lds, stream, args, g);
+  }
 }
 
 hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, int arith, int grid, hipStream_t stream)
 {
-  const int    threads = ((g.Z + 63) / 64) * 64;
-  const size_t lds     = ldpc_decode_lds_bytes(g);
+  const int threads = ((g.Z + 63) / 64) * 64;
   if (g.bg == 1) {
     if (arith == ARITH_GENERIC) {
-      hipLaunchKernelGGL((ldpc_decode_kernel<1, ARITH_GENERIC>), dim3(grid), dim3(threads), lds, stream, args, g);
+      launch_bg<1, ARITH_GENERIC>(args, g, grid, threads, stream);
     } else {
-      hipLaunchKernelGGL((ldpc_decode_kernel<1, ARITH_SIMD>), dim3(grid), dim3(threads), lds, stream, args, g);
+      launch_bg<1, ARITH_SIMD>(args, g, grid, threads, stream);
     }
   } else {
     if (arith == ARITH_GENERIC) {
-      hipLaunchKernelGGL((ldpc_decode_kernel<2, ARITH_GENERIC>), dim3(grid), dim3(threads), lds, stream, args, g);
+      launch_bg<2, ARITH_GENERIC>(args, g, grid, threads, stream);
     } else {
-      hipLaunchKernelGGL((ldpc_decode_kernel<2, ARITH_SIMD>), dim3(grid), dim3(threads), lds, stream, args, g);
+      launch_bg<2, ARITH_SIMD>(args, g, grid, threads, stream);
     }
   }
   return hipGetLastError();

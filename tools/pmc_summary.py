@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Summarises rocprofv3 outputs for the LDPC decoder kernel.
+
+  pmc_summary.py traffic <fetch_dir> <write_dir> <out.json>
+      HBM traffic per launch from separate FETCH_SIZE / WRITE_SIZE passes
+      (MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of a wide coalesced
+      stream on gfx950 -> doubled; both are in KiB).
+  pmc_summary.py stats <kernel_stats.csv> <out.md>
+"""
+import csv
+import glob
+import json
+import sys
+
+KERNEL = "ldpc_decode_kernel"
+
+
+def counter(dirname, name):
+    files = glob.glob(dirname + "/**/*counter_collection.csv", recursive=True)
+    vals = []
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == name:
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def traffic(fetch_dir, write_dir, out):
+    fetch = counter(fetch_dir, "FETCH_SIZE")
+    write = counter(write_dir, "WRITE_SIZE")
+    f = sum(fetch) / len(fetch)
+    w = sum(write) / len(write)
+    res = {
+        "kernel": KERNEL,
+        "launches": [len(fetch), len(write)],
+        "fetch_size_kib_raw": f,
+        "write_size_kib": w,
+        "hbm_read_bytes_corrected": 2 * f * 1024,
+        "hbm_write_bytes": w * 1024,
+        "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
+        "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half of a wide coalesced read); "
+                "separate --pmc passes for FETCH_SIZE and WRITE_SIZE",
+    }
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+def stats(path, out):
+    rows = list(csv.DictReader(open(path)))
+    with open(out, "w") as fo:
+        fo.write("| kernel | calls | total ns | avg ns | min ns | max ns | % |\n|---|---|---|---|---|---|---|\n")
+        for r in rows:
+            fo.write("| %s | %s | %s | %s | %s | %s | %s |\n" % (
+                r["Name"][:90], r["Calls"], r["TotalDurationNs"], r["AverageNs"], r["MinNs"], r["MaxNs"],
+                r["Percentage"]))
+    print(open(out).read())
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "traffic":
+        traffic(*sys.argv[2:5])
+    else:
+        stats(*sys.argv[2:4])
