@@ -200,21 +200,22 @@ __device__ __forceinline__ int c2v_old(const uint32_t (&c2v)[NW], const int (&cl
 }
 
 // Pass 1 for edge E: v2c from the gathered soft bit and the old message, plus
-// the check-node statistics (ldpc_decoder_impl.cpp:235 / :290).  v2c is kept
-// packed 4 per register (pass 2 reads it back as an SDWA byte operand).
-template <int BG, int E0, int E, int NW, int NX, int DEG>
-__device__ __forceinline__ void edge_pass1(int            s,
-                                           uint32_t (&xp)[NX],
-                                           const uint32_t (&c2v)[NW],
-                                           const int (&cl)[DEG],
-                                           int&           min1,
-                                           int&           min2,
-                                           int&           idx,
-                                           int&           sgn)
+// the check-node statistics (ldpc_decoder_impl.cpp:235 / :290).  An infinite
+// soft bit (+-127) yields v2c = +-254 here: it can never be a minimum (> 120),
+// its sign is right, and in pass 2 c2v + v2c always lands beyond +-120, so the
+// promotion sum returns +-127 with no separate infinity test.
+template <int BG, int E0, int E, int NW, int DEG>
+__device__ __forceinline__ int edge_pass1(int            s,
+                                          const uint32_t (&c2v)[NW],
+                                          const int (&cl)[DEG],
+                                          int&           min1,
+                                          int&           min2,
+                                          int&           idx,
+                                          int&           sgn)
 {
   // v2c = soft - c2v saturated to +-LLR_MAX; infinite soft bits stay infinite.
   const bool inf = static_cast<unsigned>(s + LLR_MAX) > static_cast<unsigned>(2 * LLR_MAX);
-  const int  v   = inf ? s : med3_i(s - c2v_old<BG, E0 + E>(c2v, cl, E), -LLR_MAX, LLR_MAX);
+  const int  v   = inf ? s + s : med3_i(s - c2v_old<BG, E0 + E>(c2v, cl, E), -LLR_MAX, LLR_MAX);
   const int  av  = v < 0 ? -v : v;
   const bool lt1 = av < min1;
   idx            = lt1 ? E : idx;
@@ -222,32 +223,58 @@ __device__ __forceinline__ void edge_pass1(int            s,
   min2 = av < min1 ? min1 : (av < min2 ? av : min2);
   min1 = lt1 ? av : min1;
   sgn ^= v;
-  byte_set<E>(xp, v);
+  return v;
 }
 
 // Pass 2 for edge E: the new message (scaled min / second min with the
 // extrinsic sign) and the new soft bit, the promotion sum message + v2c
 // (ldpc_decoder_impl.cpp:310, :270).  Returns the soft bit; the message goes to
 // its register byte or to cl[E].
-template <int BG, int E0, int E, int NW, int NX, int DEG>
-__device__ __forceinline__ int
-edge_pass2(const uint32_t (&xp)[NX], uint32_t (&c2v)[NW], int (&cl)[DEG], int s1, int s2, int idx, int sgn)
+template <int BG, int E0, int E, int NW, int DEG>
+__device__ __forceinline__ int edge_pass2(int v, uint32_t (&c2v)[NW], int (&cl)[DEG], int s1, int s2, int idx, int sgn)
 {
-  const int v   = byte_get<E>(xp);
   const int mag = (E == idx) ? s2 : s1;
   const int c   = ((sgn ^ v) < 0) ? -mag : mag;
-  // promotion sum (log_likelihood_ratio.cpp:75); c is always finite, and
-  // c == -v gives 0 through the plain sum.
-  const bool inf = static_cast<unsigned>(v + LLR_MAX) > static_cast<unsigned>(2 * LLR_MAX);
-  int        t   = c + v;
-  t              = t > LLR_MAX ? LLR_INFINITY : (t < -LLR_MAX ? -LLR_INFINITY : t);
+  // promotion sum (log_likelihood_ratio.cpp:75); c is always finite, c == -v
+  // gives 0 through the plain sum, |v| = 254 (infinite) always promotes.
+  int t = c + v;
+  t     = t > LLR_MAX ? LLR_INFINITY : (t < -LLR_MAX ? -LLR_INFINITY : t);
   if constexpr (E0 + E < bg_traits<BG>::LDS_EDGES) {
     cl[E] = c;
   } else {
     byte_set<E0 + E - bg_traits<BG>::LDS_EDGES>(c2v, c);
   }
-  return inf ? v : t;
+  return t;
 }
+
+// v2c store of one layer between pass 1 and pass 2: plain registers for light
+// rows, 16-bit pairs (read back as SDWA word operands) for degree > 10.
+template <int DEG, bool PACKED = (DEG > 10)>
+struct v2c_store {
+  int v[DEG];
+  template <int E>
+  __device__ __forceinline__ void put(int x) { v[E] = x; }
+  template <int E>
+  __device__ __forceinline__ int get() const { return v[E]; }
+};
+template <int DEG>
+struct v2c_store<DEG, true> {
+  uint32_t w[(DEG + 1) / 2];
+  template <int E>
+  __device__ __forceinline__ void put(int x)
+  {
+    if constexpr ((E & 1) == 0) {
+      w[E >> 1] = static_cast<uint32_t>(x) & 0xffffu;
+    } else {
+      w[E >> 1] = __builtin_amdgcn_perm(static_cast<uint32_t>(x), w[E >> 1], 0x05040100u);
+    }
+  }
+  template <int E>
+  __device__ __forceinline__ int get() const
+  {
+    return static_cast<int>(static_cast<int16_t>(w[E >> 1] >> (16 * (E & 1))));
+  }
+};
 
 // Gather address of edge E0+E for lane j: var*Z + (j + shift) mod Z, where
 // (j + shift - Z) wraps as an unsigned value exactly when j + shift < Z, so the
@@ -292,17 +319,12 @@ __device__ __forceinline__ void process_layer(lds_i8*       soft,
 {
   constexpr int  E0     = row_start<BG>(L);
   constexpr int  DEG    = sizeof...(E);
-  constexpr int  NX     = (DEG + 3) / 4;
   constexpr bool IN_LDS = L < bg_traits<BG>::LDS_ROWS;
   constexpr bool ALL_ON = ZC > 0 && (ZC % 64) == 0;
   constexpr bool KEEP   = DEG <= 10;
   int            ad[DEG];
   int            cl[DEG];
-  uint32_t       xp[NX];
-#pragma unroll
-  for (int w = 0; w < NX; ++w) {
-    xp[w] = 0;
-  }
+  v2c_store<DEG> vs;
   const int jl = ALL_ON ? j : (idle_slot >= 0 ? 0 : j);
   auto addr = [&](auto ec) {
     constexpr int e = decltype(ec)::value;
@@ -320,7 +342,7 @@ __device__ __forceinline__ void process_layer(lds_i8*       soft,
         if constexpr (IN_LDS) {
           cl[E] = c2v_lds[(E0 + E) * Z + jl];
         }
-        edge_pass1<BG, E0, E>(x, xp, c2v, cl, min1, min2, idx, sgn);
+        vs.template put<E>(edge_pass1<BG, E0, E>(x, c2v, cl, min1, min2, idx, sgn));
       }(),
       ...);
   __builtin_amdgcn_sched_barrier(0);
@@ -331,7 +353,7 @@ __device__ __forceinline__ void process_layer(lds_i8*       soft,
         if constexpr (E % EDGE_CHUNK == 0 && E > 0 && !KEEP) {
           __builtin_amdgcn_sched_barrier(0);
         }
-        const int snew = edge_pass2<BG, E0, E>(xp, c2v, cl, s1, s2, idx, sgn);
+        const int snew = edge_pass2<BG, E0, E>(vs.template get<E>(), c2v, cl, s1, s2, idx, sgn);
         const int a    = KEEP ? ad[E] : addr(std::integral_constant<int, E>{});
         soft[a]        = static_cast<int8_t>(snew);
         if constexpr (IN_LDS) {
