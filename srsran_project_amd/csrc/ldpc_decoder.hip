@@ -137,6 +137,30 @@ __device__ __forceinline__ int med3_i(int x, int lo, int hi)
   return x < lo ? lo : (x > hi ? hi : x);
 }
 
+// v_med3_i32 as an opaque instruction: left to itself the compiler rewrites
+// some medians into compare + v_cndmask pairs (two instructions plus hazard
+// s_nops each), which is what the branch-free formulations below avoid.
+__device__ __forceinline__ int med3_op(int x, int y, int z)
+{
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+  return r;
+}
+// median(x, -120, 120): the +-LLR_MAX saturation.
+__device__ __forceinline__ int sat120(int x)
+{
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(-LLR_MAX), "v"(LLR_MAX));
+  return r;
+}
+// median(x, -1, 1)
+__device__ __forceinline__ int sign3(int x)
+{
+  int r;
+  asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 template <int ARITH>
 __device__ __forceinline__ int scale_mag(int mag)
 {
@@ -201,7 +225,7 @@ __device__ __forceinline__ int c2v_old(const uint32_t (&c2v)[NW], const int (&cl
 
 // Pass 1 for edge E: v2c from the gathered soft bit and the old message, plus
 // the check-node statistics (ldpc_decoder_impl.cpp:235 / :290).  An infinite
-// soft bit (+-127) yields v2c = +-254 here: it can never be a minimum (> 120),
+// soft bit (+-127) yields |v2c| >= 220 here: it can never be a minimum (> 120),
 // its sign is right, and in pass 2 c2v + v2c always lands beyond +-120, so the
 // promotion sum returns +-127 with no separate infinity test.
 template <int BG, int E0, int E, int NW, int DEG>
@@ -214,13 +238,15 @@ __device__ __forceinline__ int edge_pass1(int            s,
                                           int&           sgn)
 {
   // v2c = soft - c2v saturated to +-LLR_MAX; infinite soft bits stay infinite.
-  const bool inf = static_cast<unsigned>(s + LLR_MAX) > static_cast<unsigned>(2 * LLR_MAX);
-  const int  v   = inf ? s + s : med3_i(s - c2v_old<BG, E0 + E>(c2v, cl, E), -LLR_MAX, LLR_MAX);
+  // Branch-free: s - med3(s, +-120) is 0 for a finite soft bit and +-7 for an
+  // infinite one, which pushes v2c to +-[220, 309] (|v2c| > 120: never a
+  // minimum; |c2v + v2c| >= 124: always promoted to +-127 in pass 2).
+  const int  v   = sat120(s - c2v_old<BG, E0 + E>(c2v, cl, E)) + __mul24(27, s - sat120(s));
   const int  av  = v < 0 ? -v : v;
   const bool lt1 = av < min1;
   idx            = lt1 ? E : idx;
   // new second minimum = median(min1, |v|, min2)
-  min2 = av < min1 ? min1 : (av < min2 ? av : min2);
+  min2 = med3_op(min1, av, min2);
   min1 = lt1 ? av : min1;
   sgn ^= v;
   return v;
@@ -234,17 +260,22 @@ template <int BG, int E0, int E, int NW, int DEG>
 __device__ __forceinline__ int edge_pass2(int v, uint32_t (&c2v)[NW], int (&cl)[DEG], int s1, int s2, int idx, int sgn)
 {
   const int mag = (E == idx) ? s2 : s1;
-  const int c   = ((sgn ^ v) < 0) ? -mag : mag;
-  // promotion sum (log_likelihood_ratio.cpp:75); c is always finite, c == -v
-  // gives 0 through the plain sum, |v| = 254 (infinite) always promotes.
-  int t = c + v;
-  t     = t > LLR_MAX ? LLR_INFINITY : (t < -LLR_MAX ? -LLR_INFINITY : t);
+  // extrinsic sign: negate when the sign product without this edge is negative
+  const int neg = (sgn ^ v) >> 31;
+  const int c   = (mag ^ neg) - neg;
+  // promotion sum (log_likelihood_ratio.cpp:75) without compares: m is the
+  // +-120 saturation, (t - m) clamped to [-1, 1] flags an overflow, which moves
+  // m on to +-127.  c is always finite, c == -v gives 0 through the plain sum,
+  // an infinite v2c (|v| >= 220) always overflows.
+  const int t   = c + v;
+  const int m   = sat120(t);
+  const int out = m + __mul24(LLR_INFINITY - LLR_MAX, sign3(t - m));
   if constexpr (E0 + E < bg_traits<BG>::LDS_EDGES) {
     cl[E] = c;
   } else {
     byte_set<E0 + E - bg_traits<BG>::LDS_EDGES>(c2v, c);
   }
-  return t;
+  return out;
 }
 
 // v2c store of one layer between pass 1 and pass 2: plain registers for light
