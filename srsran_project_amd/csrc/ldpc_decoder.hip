@@ -153,6 +153,14 @@ __device__ __forceinline__ int sat120(int x)
   asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(-LLR_MAX), "v"(LLR_MAX));
   return r;
 }
+// a * K + b with a 24-bit signed multiply (K an inline constant)
+template <int K>
+__device__ __forceinline__ int mad24(int a, int b)
+{
+  int r;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(K), "v"(b));
+  return r;
+}
 // median(x, -1, 1)
 __device__ __forceinline__ int sign3(int x)
 {
@@ -241,7 +249,7 @@ __device__ __forceinline__ int edge_pass1(int            s,
   // Branch-free: s - med3(s, +-120) is 0 for a finite soft bit and +-7 for an
   // infinite one, which pushes v2c to +-[220, 309] (|v2c| > 120: never a
   // minimum; |c2v + v2c| >= 124: always promoted to +-127 in pass 2).
-  const int  v   = sat120(s - c2v_old<BG, E0 + E>(c2v, cl, E)) + __mul24(27, s - sat120(s));
+  const int  v   = mad24<27>(s - sat120(s), sat120(s - c2v_old<BG, E0 + E>(c2v, cl, E)));
   const int  av  = v < 0 ? -v : v;
   const bool lt1 = av < min1;
   idx            = lt1 ? E : idx;
@@ -269,7 +277,7 @@ __device__ __forceinline__ int edge_pass2(int v, uint32_t (&c2v)[NW], int (&cl)[
   // an infinite v2c (|v| >= 220) always overflows.
   const int t   = c + v;
   const int m   = sat120(t);
-  const int out = m + __mul24(LLR_INFINITY - LLR_MAX, sign3(t - m));
+  const int out = mad24<LLR_INFINITY - LLR_MAX>(sign3(t - m), m);
   if constexpr (E0 + E < bg_traits<BG>::LDS_EDGES) {
     cl[E] = c;
   } else {
@@ -433,8 +441,24 @@ constexpr int waves_per_simd()
   return 4;
 }
 
+// Check rows per wavefront.  64 for every Z except the compile-time Z=384
+// kernel, which may spread its 384 rows over 8 waves of 48 (lanes 48-63 then
+// duplicate rows 32-47: identical values to identical addresses), so that two
+// workgroups put exactly 2 + 2 waves on every SIMD instead of 2/2/1/1 + 1/1/2/2.
+constexpr int Z384_CHECKS_PER_WAVE = 48;
+template <int ZC>
+constexpr int checks_per_wave()
+{
+  return ZC == 384 ? Z384_CHECKS_PER_WAVE : 64;
+}
+template <int ZC>
+constexpr int max_threads()
+{
+  return ZC == 384 ? 64 * (384 / Z384_CHECKS_PER_WAVE) : MAX_LIFTING_SIZE;
+}
+
 template <int BG, int ARITH, int ZC>
-__global__ void __launch_bounds__(MAX_LIFTING_SIZE, (waves_per_simd<BG, ZC>())) ldpc_decode_kernel(decode_args a, lifted_graph g)
+__global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>())) ldpc_decode_kernel(decode_args a, lifted_graph g)
 {
   constexpr int NW      = reg_words<BG>();
   constexpr int N_FULL  = bg_traits<BG>::N_FULL;
@@ -445,7 +469,10 @@ __global__ void __launch_bounds__(MAX_LIFTING_SIZE, (waves_per_simd<BG, ZC>())) 
 
   const int  j       = threadIdx.x;
   const int  nthr    = blockDim.x;
-  const bool active  = j < Z;
+  // check row of this lane (== j unless rows are spread 48 per wave)
+  constexpr int CPW  = checks_per_wave<ZC>();
+  const int  jc      = CPW == 64 ? j : (j >> 6) * CPW + ((j & 63) < CPW ? (j & 63) : (j & 63) - (64 - CPW));
+  const bool active  = CPW == 64 ? j < Z : true;
   // idle lanes (Z not a multiple of 64) work on a private pad byte after the messages
   const int idle_slot = active ? -1 : lds_total_bytes<BG>(Z) - LDS_SOFT_OFFSET - 64 + (j & 63);
   const int wave      = j >> 6;
@@ -533,7 +560,7 @@ __global__ void __launch_bounds__(MAX_LIFTING_SIZE, (waves_per_simd<BG, ZC>())) 
     __syncthreads();
 
     for (int it = 0; it < a.max_iterations; ++it) {
-      run_layers<BG, ZC, 0, ARITH>(soft, c2v_lds, c2v, (const_u32_ptr)(a.edges), Z, j, idle_slot, nof_layers);
+      run_layers<BG, ZC, 0, ARITH>(soft, c2v_lds, c2v, (const_u32_ptr)(a.edges), Z, jc, idle_slot, nof_layers);
 
       if (a.crc_table) {
         // get_hard_bits + CRC early stop (ldpc_decoder_impl.cpp:125).
@@ -602,7 +629,7 @@ static void launch_bg(const decode_args& args, const lifted_graph& g, int grid, 
   // every other Z runs the runtime-Z instantiation.
   const size_t lds = lds_total_bytes<BG>(g.Z);
   if (g.Z == 384) {
-    hipLaunchKernelGGL((ldpc_decode_kernel<BG, ARITH, 384>), dim3(grid), dim3(threads), lds, stream, args, g);
+    hipLaunchKernelGGL((ldpc_decode_kernel<BG, ARITH, 384>), dim3(grid), dim3(max_threads<384>()), lds, stream, args, g);
   } else {
     hipLaunchKernelGGL((ldpc_decode_kernel<BG, ARITH, 0>), dim3(grid), dim3(threads), lds, stream, args, g);
   }
