@@ -58,25 +58,28 @@ def cpu_baseline(args, llrs_host):
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     P = oracle.P
     sample = np.ascontiguousarray(llrs_host[:512])
-    n0 = min(64, sample.shape[0])
-    # calibrate on a small sample
-    t = oracle.REF.srs_ref_ldpc_decode_many(impl, BG, Z, args.iters, -1, sample.ctypes.data_as(P), N_LLRS, n0,
+    ns = sample.shape[0]
+    # calibrate on a small sample, then decode ~cpu_seconds worth, cycling over the sample
+    n0 = min(4 * threads, 256)
+    t = oracle.REF.srs_ref_ldpc_decode_many(impl, BG, Z, args.iters, -1, sample.ctypes.data_as(P), N_LLRS, ns, n0,
                                             threads, None, None)
-    rate = n0 / max(t, 1e-9)
-    n = int(min(max(rate * args.cpu_seconds, n0), 1 << 16))
-    # decode n codeblocks cycling over the 512-codeblock sample
-    reps = (n + sample.shape[0] - 1) // sample.shape[0]
-    big = np.ascontiguousarray(np.tile(sample, (reps, 1))[:n])
-    t = oracle.REF.srs_ref_ldpc_decode_many(impl, BG, Z, args.iters, -1, big.ctypes.data_as(P), N_LLRS, n, threads,
-                                            None, None)
+    n = int(max(n0, min(n0 / max(t, 1e-9) * args.cpu_seconds, 1 << 22)))
+    t = oracle.REF.srs_ref_ldpc_decode_many(impl, BG, Z, args.iters, -1, sample.ctypes.data_as(P), N_LLRS, ns, n,
+                                            threads, None, None)
+    # single-thread rate on a shorter sample, for the per-core figure
+    n1 = max(8, int(n / threads / 4))
+    t1 = oracle.REF.srs_ref_ldpc_decode_many(impl, BG, Z, args.iters, -1, sample.ctypes.data_as(P), N_LLRS, ns, n1,
+                                             1, None, None)
     return {
         "value": n / t,
         "unit": "codeblocks/s",
         "cores": threads,
         "kind": "reference",
         "impl": impl.decode(),
-        "sample": "%d BG1 Z=384 full-length codeblocks, %d iterations, reference ldpc_decoder_%s, "
-                  "%d worker threads (one decoder each), %.1f s" % (n, args.iters, impl.decode(), threads, t),
+        "single_thread_value": n1 / t1,
+        "sample": "%d BG1 Z=384 full-length codeblocks (cycling over 512 distinct ones), %d iterations, reference "
+                  "ldpc_decoder_%s compiled from /root/reference, %d worker threads with one decoder each, %.1f s; "
+                  "single thread: %d codeblocks in %.1f s" % (n, args.iters, impl.decode(), threads, t, n1, t1),
     }
 
 
@@ -136,6 +139,13 @@ def main():
     bytes_per_cb = N_LLRS + OUT_BYTES + 4  # LLRs in, packed message out, iteration count
     achieved_gbs = bytes_per_cb * args.batch / (kernel_ms * 1e-3) / 1e9
 
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r01_ldpc_decode_traffic.json")
+    if os.path.exists(tpath):
+        # HBM bytes per launch of this kernel on this workload, from rocprofv3
+        # FETCH_SIZE / WRITE_SIZE in separate --pmc passes (tools/gpu_check.sh traffic)
+        traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -171,7 +181,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
                 "kernel": "ldpc_decode_kernel",
                 "kernel_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": bytes_per_cb * args.batch,

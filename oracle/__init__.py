@@ -55,8 +55,8 @@ def _load_ref():
     lib.srs_ref_crc_bits.restype = c_uint
     lib.srs_ref_crc_bits.argtypes = [c_int, P, c_uint]
     lib.srs_ref_ldpc_decode_many.restype = ctypes.c_double
-    lib.srs_ref_ldpc_decode_many.argtypes = [ctypes.c_char_p, c_int, c_int, c_int, c_int, P, c_uint, c_uint, c_int,
-                                             P, P]
+    lib.srs_ref_ldpc_decode_many.argtypes = [ctypes.c_char_p, c_int, c_int, c_int, c_int, P, c_uint, c_uint, c_uint,
+                                             c_int, P, P]
     return lib
 
 

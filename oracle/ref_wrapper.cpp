@@ -144,7 +144,8 @@ unsigned srs_ref_crc_bits(int poly, const uint8_t* bits, unsigned nbits)
   return c->calculate_bit(span<const uint8_t>(bits, nbits));
 }
 
-// CPU baseline: decodes n_cbs codeblocks (each n_llrs LLRs, stride n_llrs) with
+// CPU baseline: decodes n_cbs codeblocks (codeblock i = sample row i % n_sample,
+// each n_llrs LLRs) with
 // `threads` worker threads, each owning one decoder (as the PUSCH decoder pool
 // does).  Returns wall seconds; iteration results written to iters (may be null).
 double srs_ref_ldpc_decode_many(const char*   impl,
@@ -154,6 +155,7 @@ double srs_ref_ldpc_decode_many(const char*   impl,
                                 int           crc_poly,
                                 const int8_t* llrs,
                                 unsigned      n_llrs,
+                                unsigned      n_sample,
                                 unsigned      n_cbs,
                                 int           threads,
                                 uint8_t*      out_packed,
@@ -182,14 +184,15 @@ double srs_ref_ldpc_decode_many(const char*   impl,
       cfg.max_iterations = max_iterations;
       dynamic_bit_buffer out(K);
       for (unsigned i = next++; i < n_cbs; i = next++) {
-        span<const log_likelihood_ratio> in(reinterpret_cast<const log_likelihood_ratio*>(llrs) + size_t(i) * n_llrs,
-                                            n_llrs);
+        // codeblock i reads sample row i % n_sample (bounded memory for long CPU runs)
+        span<const log_likelihood_ratio> in(
+            reinterpret_cast<const log_likelihood_ratio*>(llrs) + size_t(i % n_sample) * n_llrs, n_llrs);
         std::optional<unsigned>          r = dec->decode(out, in, crc_poly >= 0 ? get_crc(crc_poly) : nullptr, cfg);
         if (out_packed) {
-          std::memcpy(out_packed + size_t(i) * obyte, out.get_buffer().data(), obyte);
+          std::memcpy(out_packed + size_t(i % n_sample) * obyte, out.get_buffer().data(), obyte);
         }
         if (iters) {
-          iters[i] = r.has_value() ? static_cast<int>(*r) : -1;
+          iters[i % n_sample] = r.has_value() ? static_cast<int>(*r) : -1;
         }
       }
     });

@@ -26,6 +26,11 @@ for s in "$@"; do
              python3 tools/pmc_summary.py traffic gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/traffic.json ;;
     pmc) step pmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline && \
          step pmc2 600 rocprofv3 --kernel-trace --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE SQ_ACTIVE_INST_SCA -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    save) mkdir -p gpurun_out/profiles && \
+          python3 tools/pmc_summary.py stats gpurun_out/prof/run_kernel_stats.csv gpurun_out/profiles/kernel_stats.md > /dev/null && \
+          cp gpurun_out/prof/run_kernel_stats.csv gpurun_out/profiles/kernel_stats.csv && \
+          cp gpurun_out/traffic.json gpurun_out/profiles/traffic.json && \
+          tail -1 gpurun_out/bench.log > gpurun_out/profiles/bench.json ;;
     *) echo "unknown step $s" ;;
   esac
 done
