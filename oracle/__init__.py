@@ -39,6 +39,10 @@ def _load_oracle():
     lib.srs_oracle_crc_bits.argtypes = [c_int, P, c_uint]
     lib.srs_oracle_lifting_index.restype = c_int
     lib.srs_oracle_lifting_index.argtypes = [c_int]
+    lib.srs_oracle_ldpc_rate_match.restype = c_int
+    lib.srs_oracle_ldpc_rate_match.argtypes = [c_uint] * 6 + [P, c_uint, P]
+    lib.srs_oracle_ldpc_rate_dematch.restype = c_int
+    lib.srs_oracle_ldpc_rate_dematch.argtypes = [c_uint] * 6 + [c_int, P, c_uint, P]
     return lib
 
 
@@ -54,6 +58,10 @@ def _load_ref():
     lib.srs_ref_ldpc_encode.argtypes = [ctypes.c_char_p, c_int, c_int, P, P, c_uint]
     lib.srs_ref_crc_bits.restype = c_uint
     lib.srs_ref_crc_bits.argtypes = [c_int, P, c_uint]
+    lib.srs_ref_ldpc_encode_rate_match.restype = c_int
+    lib.srs_ref_ldpc_encode_rate_match.argtypes = [c_int, c_int] + [c_uint] * 4 + [P, c_uint, P]
+    lib.srs_ref_ldpc_rate_dematch.restype = c_int
+    lib.srs_ref_ldpc_rate_dematch.argtypes = [ctypes.c_char_p, c_int, c_int] + [c_uint] * 4 + [c_int, P, c_uint, P]
     lib.srs_ref_ldpc_decode_many.restype = ctypes.c_double
     lib.srs_ref_ldpc_decode_many.argtypes = [ctypes.c_char_p, c_int, c_int, c_int, c_int, P, c_uint, c_uint, c_uint,
                                              c_int, P, P]
@@ -127,3 +135,37 @@ def pack_bits(bits):
 
 def unpack_bits(packed, n):
     return np.unpackbits(np.asarray(packed, dtype=np.uint8))[:n]
+
+
+def rate_match(cw_bits, bg, Z, rv, Qm, E, Nref=0, filler=0):
+    """Oracle rate matching of a full codeblock (one bit per byte) -> E packed bits."""
+    cw_bits = np.ascontiguousarray(cw_bits, dtype=np.uint8)
+    out = np.zeros((E + 7) // 8, np.uint8)
+    if ORACLE.srs_oracle_ldpc_rate_match(bg, Z, rv, Qm, Nref, filler, _ptr(cw_bits), E, _ptr(out)) != 0:
+        raise ValueError("invalid rate matching arguments")
+    return out
+
+
+def rate_dematch(llrs, bg, Z, rv, Qm, buf, new_data=True, Nref=0, filler=0):
+    """Oracle rate dematching of E LLRs into the soft buffer `buf` (modified in place)."""
+    llrs = np.ascontiguousarray(llrs, dtype=np.int8)
+    assert buf.dtype == np.int8 and buf.flags["C_CONTIGUOUS"]
+    if ORACLE.srs_oracle_ldpc_rate_dematch(bg, Z, rv, Qm, Nref, filler, int(new_data), _ptr(llrs), llrs.size,
+                                           _ptr(buf)) != 0:
+        raise ValueError("invalid rate dematching arguments")
+    return buf
+
+
+def ref_encode_rate_match(msg_bits, bg, Z, rv, Qm, E, Nref=0, filler=0):
+    msg_bits = np.ascontiguousarray(msg_bits, dtype=np.uint8)
+    out = np.zeros((E + 7) // 8, np.uint8)
+    REF.srs_ref_ldpc_encode_rate_match(bg, Z, rv, Qm, Nref, filler, _ptr(msg_bits), E, _ptr(out))
+    return out
+
+
+def ref_rate_dematch(llrs, bg, Z, rv, Qm, buf, new_data=True, Nref=0, filler=0, impl="generic"):
+    llrs = np.ascontiguousarray(llrs, dtype=np.int8)
+    if REF.srs_ref_ldpc_rate_dematch(impl.encode(), bg, Z, rv, Qm, Nref, filler, int(new_data), _ptr(llrs), llrs.size,
+                                     _ptr(buf)) != 0:
+        raise ValueError("reference dematcher %r unavailable" % impl)
+    return buf

@@ -15,6 +15,8 @@
 #include "phy/upper/channel_coding/ldpc/ldpc_decoder_generic.h"
 #include "phy/upper/channel_coding/ldpc/ldpc_encoder_avx2.h"
 #include "phy/upper/channel_coding/ldpc/ldpc_encoder_generic.h"
+#include "phy/upper/channel_coding/ldpc/ldpc_rate_dematcher_avx2_impl.h"
+#include "phy/upper/channel_coding/ldpc/ldpc_rate_dematcher_avx512_impl.h"
 #include "phy/upper/channel_coding/ldpc/ldpc_rate_dematcher_impl.h"
 #include "phy/upper/channel_coding/ldpc/ldpc_rate_matcher_impl.h"
 #include "srsran/phy/upper/channel_coding/ldpc/ldpc_encoder_buffer.h"
@@ -142,6 +144,96 @@ unsigned srs_ref_crc_bits(int poly, const uint8_t* bits, unsigned nbits)
     return 0xffffffffu;
   }
   return c->calculate_bit(span<const uint8_t>(bits, nbits));
+}
+
+static modulation_scheme mod_of(unsigned Qm)
+{
+  switch (Qm) {
+    case 1:
+      return modulation_scheme::BPSK;
+    case 2:
+      return modulation_scheme::QPSK;
+    case 4:
+      return modulation_scheme::QAM16;
+    case 6:
+      return modulation_scheme::QAM64;
+    default:
+      return modulation_scheme::QAM256;
+  }
+}
+
+static codeblock_metadata make_meta(int bg, int Z, unsigned rv, unsigned Qm, unsigned Nref, unsigned F, unsigned E)
+{
+  codeblock_metadata m;
+  m.tb_common.base_graph        = static_cast<ldpc_base_graph_type>(bg);
+  m.tb_common.lifting_size      = static_cast<ldpc::lifting_size_t>(Z);
+  m.tb_common.rv                = rv;
+  m.tb_common.mod               = mod_of(Qm);
+  m.tb_common.Nref              = Nref;
+  m.tb_common.cw_length         = E;
+  m.cb_specific.full_length     = (bg == 1 ? 66 : 50) * Z;
+  m.cb_specific.rm_length       = E;
+  m.cb_specific.nof_filler_bits = F;
+  return m;
+}
+
+// Encodes msg (K bits, one per byte, filler positions 0) with the reference
+// encoder and rate-matches it: E bits packed MSB-first.
+int srs_ref_ldpc_encode_rate_match(int            bg,
+                                   int            Z,
+                                   unsigned       rv,
+                                   unsigned       Qm,
+                                   unsigned       Nref,
+                                   unsigned       F,
+                                   const uint8_t* msg_bits,
+                                   unsigned       E,
+                                   uint8_t*       out_packed)
+{
+  ldpc_encoder_generic enc;
+  unsigned             K = (bg == 1 ? 22 : 10) * Z;
+  dynamic_bit_buffer   msg(K);
+  srsvec::bit_pack(msg, span<const uint8_t>(msg_bits, K));
+  ldpc_encoder::configuration cfg;
+  cfg.base_graph                = static_cast<ldpc_base_graph_type>(bg);
+  cfg.lifting_size              = static_cast<ldpc::lifting_size_t>(Z);
+  cfg.Nref                      = Nref;
+  const ldpc_encoder_buffer& rb = enc.encode(msg, cfg);
+  auto                       rm = std::make_unique<ldpc_rate_matcher_impl>();
+  dynamic_bit_buffer         out(E);
+  rm->rate_match(out, rb, make_meta(bg, Z, rv, Qm, Nref, F, E));
+  std::memcpy(out_packed, out.get_buffer().data(), (E + 7) / 8);
+  return 0;
+}
+
+// Rate-dematches E LLRs into the soft buffer buf (N = N_short*Z LLRs, in/out).
+int srs_ref_ldpc_rate_dematch(const char*   impl,
+                              int           bg,
+                              int           Z,
+                              unsigned      rv,
+                              unsigned      Qm,
+                              unsigned      Nref,
+                              unsigned      F,
+                              int           new_data,
+                              const int8_t* in,
+                              unsigned      E,
+                              int8_t*       buf)
+{
+  std::unique_ptr<ldpc_rate_dematcher> dm;
+  if (std::string(impl) == "generic") {
+    dm = std::make_unique<ldpc_rate_dematcher_impl>();
+  } else if (std::string(impl) == "avx2" && __builtin_cpu_supports("avx2")) {
+    dm = std::make_unique<ldpc_rate_dematcher_avx2_impl>();
+  } else if (std::string(impl) == "avx512" && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw")) {
+    dm = std::make_unique<ldpc_rate_dematcher_avx512_impl>();
+  } else {
+    return -2;
+  }
+  unsigned N = (bg == 1 ? 66 : 50) * Z;
+  dm->rate_dematch(span<log_likelihood_ratio>(reinterpret_cast<log_likelihood_ratio*>(buf), N),
+                   span<const log_likelihood_ratio>(reinterpret_cast<const log_likelihood_ratio*>(in), E),
+                   new_data != 0,
+                   make_meta(bg, Z, rv, Qm, Nref, F, E));
+  return 0;
 }
 
 // CPU baseline: decodes n_cbs codeblocks (codeblock i = sample row i % n_sample,

@@ -82,3 +82,57 @@ def test_crc_matches_reference():
             bits = rng.integers(0, 2, n).astype(np.uint8)
             ref = oracle.REF.srs_ref_crc_bits(poly, bits.ctypes.data_as(oracle.P), n)
             assert oracle.crc_bits(poly, bits) == ref, (poly, n)
+
+
+def _rm_cases(rng):
+    """(bg, Z, F, rv, Qm, Nref, E) covering filler, LBRM, every rv/Qm, E < / > Ncb."""
+    for bg in (1, 2):
+        for Z in (2, 7, 52, 384):
+            N = oracle.BG_N_SHORT[bg] * Z
+            for F in (0, 5, Z):
+                for rv in range(4):
+                    for Qm in (1, 2, 4, 6, 8):
+                        for Nref in (0, (N * 2) // 3):
+                            for E in (Qm * 3, Qm * ((N // Qm) // 2), Qm * ((5 * N // 2) // Qm)):
+                                yield bg, Z, F, rv, Qm, Nref, E
+
+
+def test_rate_matcher_matches_reference():
+    rng = np.random.default_rng(11)
+    for bg, Z, F, rv, Qm, Nref, E in _rm_cases(rng):
+        K = oracle.BG_K[bg] * Z
+        m = rng.integers(0, 2, K).astype(np.uint8)
+        m[K - F:K] = 0
+        cw = oracle.ldpc_encode(m, bg, Z)
+        np.testing.assert_array_equal(oracle.rate_match(cw, bg, Z, rv, Qm, E, Nref, F),
+                                      oracle.ref_encode_rate_match(m, bg, Z, rv, Qm, E, Nref, F),
+                                      err_msg=str((bg, Z, F, rv, Qm, Nref, E)))
+
+
+@pytest.mark.parametrize("impl", ["generic", "avx2", "avx512"])
+def test_rate_dematcher_matches_reference(impl):
+    rng = np.random.default_rng(12)
+    probe = np.zeros(66 * 2, np.int8)
+    try:
+        oracle.ref_rate_dematch(np.zeros(2, np.int8), 1, 2, 0, 2, probe, impl=impl)
+    except ValueError:
+        pytest.skip("%s dematcher not supported on this host" % impl)
+    # The SIMD dematchers combine with a clamped saturating byte add
+    # (ldpc_rate_dematcher_avx2_impl.cpp:49), the generic one with the LLR sum's
+    # infinity rules (log_likelihood_ratio.cpp:38); they agree on finite LLRs,
+    # which is all a PUSCH soft buffer ever combines (demodulator output is
+    # within +-LLR_MAX and the +inf filler positions are never combined).
+    # The oracle follows generic, so infinities are exercised against it only.
+    lim = 127 if impl == "generic" else 120
+    corners = np.array([-127, -121, -120, -119, -1, 0, 1, 60, 119, 120, 121, 127], np.int8)
+    corners = corners[np.abs(corners.astype(int)) <= lim]
+    for bg, Z, F, rv, Qm, Nref, E in _rm_cases(rng):
+        N = oracle.BG_N_SHORT[bg] * Z
+        llr = rng.choice(corners, E)
+        llr[::3] = rng.integers(-120, 121, len(llr[::3]))
+        for new_data in (True, False):
+            init = rng.integers(-lim, lim + 1, N).astype(np.int8)
+            a, b = init.copy(), init.copy()
+            oracle.rate_dematch(llr, bg, Z, rv, Qm, a, new_data, Nref, F)
+            oracle.ref_rate_dematch(llr, bg, Z, rv, Qm, b, new_data, Nref, F, impl=impl)
+            np.testing.assert_array_equal(a, b, err_msg=str((impl, bg, Z, F, rv, Qm, Nref, E, new_data)))
