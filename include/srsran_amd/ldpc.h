@@ -7,13 +7,13 @@
  *   srs_amd_ldpc_decoder_create
  *       create_ldpc_decoder_factory_sw(dec_type, {force_decoding})->create()
  *       include/srsran/phy/upper/channel_coding/channel_coding_factories.h
- *       (implementation selection: lib/phy/upper/channel_coding/channel_coding_factories.cpp:95-118;
+ *       (implementation selection: lib/phy/upper/channel_coding/channel_coding_factories.cpp:102-139,285;
  *        `arith` selects which reference implementation's rounding is reproduced
  *        bit-exactly: SRS_AMD_ARITH_SIMD = "avx2"/"avx512"/"auto" on x86,
  *        SRS_AMD_ARITH_GENERIC = "generic")
  *   srs_amd_ldpc_decode
  *       ldpc_decoder::decode(bit_buffer&, span<const log_likelihood_ratio>, crc_calculator*, const configuration&)
- *       include/srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h:68
+ *       include/srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h:72
  *   srs_amd_ldpc_decode_batch
  *       the same operation for many codeblocks of one transport block / slot,
  *       device-resident: the enqueue/dequeue pair of
@@ -51,7 +51,7 @@ extern "C" {
 #define SRS_AMD_ARITH_SIMD 0
 #define SRS_AMD_ARITH_GENERIC 1
 
-/* ldpc_decoder::configuration (ldpc_decoder.h:40). */
+/* ldpc_decoder::configuration (ldpc_decoder.h:44). */
 typedef struct srs_amd_ldpc_decoder_config {
   uint32_t base_graph;      /* 1 = BG1, 2 = BG2 (ldpc_base_graph_type) */
   uint32_t lifting_size;    /* ldpc::lifting_size_t */
@@ -61,6 +61,17 @@ typedef struct srs_amd_ldpc_decoder_config {
 } srs_amd_ldpc_decoder_config;
 
 typedef struct srs_amd_ldpc_decoder srs_amd_ldpc_decoder;
+
+/* The codeblock_metadata fields the rate matcher / dematcher use
+ * (include/srsran/phy/upper/codeblock_metadata.h:44 tb_common, :63 cb_specific). */
+typedef struct srs_amd_codeblock_metadata {
+  uint32_t base_graph;       /* tb_common.base_graph: 1 = BG1, 2 = BG2 */
+  uint32_t lifting_size;     /* tb_common.lifting_size */
+  uint32_t rv;               /* tb_common.rv, 0..3 */
+  uint32_t modulation_order; /* get_bits_per_symbol(tb_common.mod): 1, 2, 4, 6 or 8 */
+  uint32_t Nref;             /* tb_common.Nref: limited-buffer length, 0 = unlimited */
+  uint32_t nof_filler_bits;  /* cb_specific.nof_filler_bits */
+} srs_amd_codeblock_metadata;
 
 /* Last error message of the calling thread ("" if none). */
 const char* srs_amd_last_error(void);

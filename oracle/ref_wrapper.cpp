@@ -6,7 +6,7 @@
 // bench.py's cpu_baseline leg ("kind": "reference").  The product never loads it.
 //
 // Wrapped reference interfaces:
-//   include/srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h:68  ldpc_decoder::decode
+//   include/srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h:72  ldpc_decoder::decode
 //   include/srsran/phy/upper/channel_coding/ldpc/ldpc_encoder.h     ldpc_encoder::encode
 //   include/srsran/phy/upper/channel_coding/crc_calculator.h        crc_calculator::calculate_bit
 //   include/srsran/phy/upper/channel_coding/ldpc/ldpc_rate_matcher.h / ldpc_rate_dematcher.h

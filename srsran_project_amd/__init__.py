@@ -16,4 +16,16 @@ from .ldpc import (  # noqa: F401
     message_length,
 )
 
+from .ldpc_codec import (  # noqa: F401
+    CodeblockMetadata,
+    LdpcEncoder,
+    LdpcEncoderConfiguration,
+    LdpcRateDematcher,
+    LdpcRateMatcher,
+    MODULATION_ORDER,
+    create_ldpc_encoder_factory_hip,
+    create_ldpc_rate_dematcher_factory_hip,
+    create_ldpc_rate_matcher_factory_hip,
+)
+
 __version__ = "0.1.0"

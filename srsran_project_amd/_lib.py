@@ -32,6 +32,29 @@ class LDPCDecoderConfig(ctypes.Structure):
     ]
 
 
+class CodeblockMetadata(ctypes.Structure):
+    """``srs_amd_codeblock_metadata`` (include/srsran_amd/ldpc.h)."""
+
+    _fields_ = [
+        ("base_graph", ctypes.c_uint32),
+        ("lifting_size", ctypes.c_uint32),
+        ("rv", ctypes.c_uint32),
+        ("modulation_order", ctypes.c_uint32),
+        ("Nref", ctypes.c_uint32),
+        ("nof_filler_bits", ctypes.c_uint32),
+    ]
+
+
+class LDPCEncoderConfig(ctypes.Structure):
+    """``srs_amd_ldpc_encoder_config`` (include/srsran_amd/ldpc_encoder.h)."""
+
+    _fields_ = [
+        ("base_graph", ctypes.c_uint32),
+        ("lifting_size", ctypes.c_uint32),
+        ("Nref", ctypes.c_uint32),
+    ]
+
+
 class SrsAmdError(RuntimeError):
     pass
 
@@ -54,6 +77,22 @@ def _declare(lib):
             [P, c.POINTER(LDPCDecoderConfig), c.c_int, P, c.c_uint32, P, c.c_uint32, P, c.c_uint32, P, P,
              c.c_uint32, P],
         ),
+        "srs_amd_ldpc_encoder_create": (c.c_int, [c.POINTER(P), c.c_int]),
+        "srs_amd_ldpc_encoder_destroy": (None, [P]),
+        "srs_amd_ldpc_encode": (c.c_int, [P, P, c.c_uint32, P, c.c_uint32, c.POINTER(LDPCEncoderConfig)]),
+        "srs_amd_ldpc_encode_batch": (
+            c.c_int, [P, c.POINTER(LDPCEncoderConfig), P, c.c_uint32, P, c.c_uint32, c.c_uint32, P]),
+        "srs_amd_ldpc_rate_matcher_create": (c.c_int, [c.POINTER(P), c.c_int]),
+        "srs_amd_ldpc_rate_matcher_destroy": (None, [P]),
+        "srs_amd_ldpc_rate_match": (c.c_int, [P, P, c.c_uint32, P, c.c_uint32, c.POINTER(CodeblockMetadata)]),
+        "srs_amd_ldpc_rate_match_batch": (
+            c.c_int, [P, c.POINTER(CodeblockMetadata), P, c.c_uint32, P, P, c.c_uint32, P, c.c_uint32, P]),
+        "srs_amd_ldpc_rate_dematcher_create": (c.c_int, [c.POINTER(P), c.c_int]),
+        "srs_amd_ldpc_rate_dematcher_destroy": (None, [P]),
+        "srs_amd_ldpc_rate_dematch": (
+            c.c_int, [P, P, c.c_uint32, P, c.c_uint32, c.c_int, c.POINTER(CodeblockMetadata)]),
+        "srs_amd_ldpc_rate_dematch_batch": (
+            c.c_int, [P, c.POINTER(CodeblockMetadata), c.c_int, P, P, P, P, c.c_uint32, c.c_uint32, P]),
         "srs_amd_ldpc_message_length": (c.c_uint32, [c.c_uint32, c.c_uint32]),
         "srs_amd_ldpc_codeblock_length": (c.c_uint32, [c.c_uint32, c.c_uint32]),
     }

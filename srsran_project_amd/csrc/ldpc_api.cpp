@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "api_common.h"
 #include "ldpc_common.h"
 #include <cstdarg>
 #include <cstdio>
@@ -24,24 +25,6 @@ hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, in
 size_t     ldpc_decode_lds_bytes(const lifted_graph& g);
 
 namespace {
-
-thread_local std::string g_last_error;
-
-int fail(int code, const char* fmt, ...)
-{
-  char    buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  g_last_error = buf;
-  return code;
-}
-
-int hip_fail(hipError_t e, const char* what)
-{
-  return fail(SRS_AMD_EHIP, "%s: %s", what, hipGetErrorString(e));
-}
 
 constexpr int      MAX_CRC_BITS_LEN = 22 * MAX_LIFTING_SIZE;
 constexpr uint32_t DEFAULT_SLOTS    = 1u << 20;
@@ -74,10 +57,6 @@ std::vector<uint32_t> crc_linear_table(int poly)
 
 } // namespace
 
-const char* last_error()
-{
-  return g_last_error.c_str();
-}
 
 } // namespace srs_amd
 
@@ -177,21 +156,11 @@ int srs_amd_ldpc_decoder_create(srs_amd_ldpc_decoder** decoder, int arith, int f
     return fail(SRS_AMD_EINVAL, "Invalid arithmetic flavour %d", arith);
   }
   *decoder = nullptr;
-  int        ndev = 0;
-  hipError_t e    = hipGetDeviceCount(&ndev);
-  if (e != hipSuccess || ndev == 0) {
-    return fail(SRS_AMD_EHIP, "no HIP device available (%s)", hipGetErrorString(e));
+  int rc    = select_device(device);
+  if (rc != SRS_AMD_OK) {
+    return rc;
   }
-  if (device < 0) {
-    e = hipGetDevice(&device);
-    if (e != hipSuccess) {
-      return hip_fail(e, "hipGetDevice");
-    }
-  }
-  e = hipSetDevice(device);
-  if (e != hipSuccess) {
-    return hip_fail(e, "hipSetDevice");
-  }
+  hipError_t e = hipSuccess;
   auto* d           = new srs_amd_ldpc_decoder();
   d->arith          = arith;
   d->force_decoding = force_decoding ? 1 : 0;
@@ -207,19 +176,7 @@ int srs_amd_ldpc_decoder_create(srs_amd_ldpc_decoder** decoder, int arith, int f
     e = hipMemcpy(d->crc_tables, tables.data(), tables.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   }
   // Every lifted graph (2 base graphs x 51 lifting sizes, 129 KiB), uploaded once.
-  std::vector<uint32_t> edges(2 * NOF_LIFTING_SIZES * MAX_EDGES, 0);
-  for (int bg = 1; bg <= 2; ++bg) {
-    for (int pos = 0; pos < NOF_LIFTING_SIZES; ++pos) {
-      lifted_graph lg{};
-      for (int z = 2; z <= MAX_LIFTING_SIZE; ++z) {
-        if (lifting_size_position(z) == pos) {
-          build_lifted_graph(lg, bg, z);
-          break;
-        }
-      }
-      std::copy(lg.edge, lg.edge + MAX_EDGES, edges.begin() + ((bg - 1) * NOF_LIFTING_SIZES + pos) * MAX_EDGES);
-    }
-  }
+  std::vector<uint32_t> edges = all_lifted_edges();
   if (e == hipSuccess) {
     e = hipMalloc(&d->edges, edges.size() * sizeof(uint32_t));
   }

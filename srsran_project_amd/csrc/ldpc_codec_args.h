@@ -1,0 +1,56 @@
+// ldpc_codec_args.h -- kernel argument blocks and launchers of the LDPC
+// encoder (ldpc_encoder.hip) and rate (de)matcher (ldpc_rate_matching.hip),
+// shared with their C-ABI (ldpc_codec_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ldpc_common.h"
+#include "rate_matching_common.h"
+
+namespace srs_amd {
+
+struct encode_args {
+  const uint8_t*  msgs;      // [nof_cbs][msg_stride] packed messages
+  uint8_t*        cws;       // [nof_cbs][cw_stride] packed shortened codewords
+  const uint32_t* edges;     // lifted edge descriptors (var*Z | shift << 16), row-major
+  uint32_t        msg_stride;
+  uint32_t        cw_stride;
+  uint32_t        nof_cbs;
+  int32_t         bg;
+  int32_t         Z;
+  int32_t         K;         // K_bg
+  int32_t         M;         // check rows
+  int32_t         N_short;
+  int32_t         p0_shift;  // s: p0 = P^-s (sum of lambdas)
+  int32_t         core_a[4]; // shift of column K_bg in rows 0..3 (0 where absent)
+  int32_t         row_start[MAX_BG_M + 1];
+};
+
+struct dematch_args {
+  const int8_t*   in;
+  const uint32_t* in_offsets;
+  const uint32_t* rm_lengths;
+  int8_t*         soft;
+  uint32_t        soft_stride;
+  uint32_t        nof_cbs;
+  int32_t         new_data;
+  rm_geometry     g;
+};
+
+struct rate_match_args {
+  const uint8_t*  cw;
+  uint32_t        cw_stride;
+  const uint32_t* rm_lengths;
+  const uint32_t* out_offsets;
+  uint8_t*        out;
+  uint32_t        nof_cbs;
+  rm_geometry     g;
+};
+
+hipError_t launch_ldpc_encode(const encode_args& a, int grid, hipStream_t stream);
+size_t     ldpc_encode_lds_bytes(int K, int M, int Z);
+hipError_t launch_rate_dematch(const dematch_args& a, hipStream_t stream);
+hipError_t launch_rate_match(const rate_match_args& a, uint32_t max_rm_length, hipStream_t stream);
+
+} // namespace srs_amd

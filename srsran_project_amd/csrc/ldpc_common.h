@@ -6,7 +6,9 @@
 //   include/srsran/phy/upper/log_likelihood_ratio.h:300-311      (LLR_MAX=120, LLR_INFTY=127)
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
+#include <vector>
 
 namespace srs_amd {
 
@@ -68,6 +70,16 @@ constexpr int NOF_LIFTING_SIZES = 51;
 
 // Fills g for (bg, Z); returns false for an invalid pair.
 bool build_lifted_graph(lifted_graph& g, int bg, int Z);
+
+// Edge descriptors of every lifted graph, [2 base graphs][51 lifting sizes][MAX_EDGES],
+// in the order of build_lifted_graph (device tables of the decoder and encoder).
+std::vector<uint32_t> all_lifted_edges();
+
+// Offset of the (bg, Z) graph in all_lifted_edges().
+inline size_t lifted_edges_offset(int bg, int Z)
+{
+  return (static_cast<size_t>(bg - 1) * NOF_LIFTING_SIZES + lifting_size_position(Z)) * MAX_EDGES;
+}
 
 // TS 38.212 Table 5.3.2-1 lifting-size set index, -1 if Z is not a valid lifting size.
 int lifting_index(int Z);

@@ -5,6 +5,8 @@
 // (get_graph: shift = V mod Z) and ldpc_graph_impl.cpp.
 #include "ldpc_common.h"
 
+#include <algorithm>
+
 namespace srs_amd {
 
 #include "bg_tables.inc"
@@ -75,6 +77,22 @@ bool build_lifted_graph(lifted_graph& g, int bg, int Z)
     g.row_start[r] = count;
   }
   return true;
+}
+
+std::vector<uint32_t> all_lifted_edges()
+{
+  std::vector<uint32_t> edges(2 * NOF_LIFTING_SIZES * MAX_EDGES, 0);
+  for (int bg = 1; bg <= 2; ++bg) {
+    for (int z = 2; z <= MAX_LIFTING_SIZE; ++z) {
+      if (lifting_size_position(z) < 0) {
+        continue;
+      }
+      lifted_graph lg{};
+      build_lifted_graph(lg, bg, z);
+      std::copy(lg.edge, lg.edge + MAX_EDGES, edges.begin() + lifted_edges_offset(bg, z));
+    }
+  }
+  return edges;
 }
 
 bool crc_params(int poly, uint32_t& polynom, int& order)

@@ -1,0 +1,230 @@
+// ldpc_rate_matching.hip -- MI355X kernels for LDPC rate matching (PDSCH) and
+// rate dematching (PUSCH), TS 38.212 Section 5.4.2.
+//
+// Both kernels are gathers over the circular buffer (rate_matching_common.h):
+// HBM traffic is one read of the source and one write of the destination, so
+// they are HBM/latency bound and trivial next to the decoder; what matters is
+// being exact and never needing a host round trip.
+//
+// Dematching (ldpc_rate_dematcher_impl.cpp:36-217) is recast from the
+// reference's sequential walk over the input into a per-OUTPUT-position rule,
+// so every soft-buffer byte is produced by one thread with no write conflicts:
+//   * deinterleaving (…:200 deinterleave_bits_Qm): input index t reads
+//     in[(t mod K) * Qm + t div K], K = E / Qm;
+//   * position p (non-filler, p < Ncb) receives inputs t0(p) + c*L, c = 0, 1, …
+//     with t0(p) = (walk(p) - rank0) mod L;
+//   * new data (…:123 allot_llrs copy mode): the reference's first loop pass
+//     (the walk from k0 to the end of the buffer, t < L1 = L - rank0) copies,
+//     everything after combines; before copying it zeroes [0, k0) when k0 lies
+//     in the information part, else [0, nof_info), and sets the filler bits to
+//     +inf (127); when the input ends inside the first pass it zeroes the LAST
+//     Ncb - tmp positions of the N-long buffer (…:214, out.last()), tmp being
+//     where the walk stopped (skips to nof_sys if it stopped in the systematic
+//     part); positions it does not cover keep their old value.
+//   * combining is the LLR saturated sum new += old (log_likelihood_ratio.cpp:58):
+//     two infinities of opposite sign give 0, otherwise an infinite operand
+//     (|x| > 120) wins -- the new one first -- otherwise clamp to +-120.
+//
+// Rate matching (ldpc_rate_matcher_impl.cpp:93-170): output bit o of a
+// codeblock is e[(o mod Qm) * K + o div Qm] (bit interleaver), e[t] the
+// codeblock bit at walk index (rank0 + t) mod L.  One thread per output BYTE
+// of the concatenated codeword; a byte that straddles two codeblocks' segments
+// is owned by the codeblock holding its first bit, which also computes the
+// following codeblocks' bits, so no two threads write one byte.
+#include <hip/hip_runtime.h>
+
+#include "ldpc_common.h"
+#include "ldpc_codec_args.h"
+
+namespace srs_amd {
+
+namespace {
+
+// q = n / d, r = n % d for n < 2^24 via a float reciprocal and one correction
+// (the float estimate is off by at most one).
+struct fast_div {
+  uint32_t d;
+  float    rcp;
+  __device__ explicit fast_div(uint32_t d_) : d(d_), rcp(1.0f / static_cast<float>(d_ ? d_ : 1)) {}
+  __device__ __forceinline__ uint32_t div(uint32_t n, uint32_t& r) const
+  {
+    uint32_t q = static_cast<uint32_t>(static_cast<float>(n) * rcp);
+    int32_t  x = static_cast<int32_t>(n - q * d);
+    if (x < 0) {
+      q -= 1;
+      x += static_cast<int32_t>(d);
+    } else if (x >= static_cast<int32_t>(d)) {
+      q += 1;
+      x -= static_cast<int32_t>(d);
+    }
+    r = static_cast<uint32_t>(x);
+    return q;
+  }
+};
+
+// LLR saturated sum a += b, a = new input, b = old soft bit (log_likelihood_ratio.cpp:38-74).
+__device__ __forceinline__ int llr_sum(int a, int b)
+{
+  if (a == -b) {
+    return 0;
+  }
+  if (a > LLR_MAX || a < -LLR_MAX) {
+    return a;
+  }
+  if (b > LLR_MAX || b < -LLR_MAX) {
+    return b;
+  }
+  return min(max(a + b, -LLR_MAX), LLR_MAX);
+}
+
+} // namespace
+
+
+constexpr int DEMATCH_THREADS   = 256;
+constexpr int DEMATCH_PER_THREAD = 4;
+
+__global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dematch_args a)
+{
+  const rm_geometry& g = a.g;
+  for (uint32_t cb = blockIdx.y; cb < a.nof_cbs; cb += gridDim.y) {
+    const uint32_t E   = a.rm_lengths[cb];
+    const int8_t*  in  = a.in + a.in_offsets[cb];
+    int8_t*        buf = a.soft + static_cast<size_t>(cb) * a.soft_stride;
+    const uint32_t Kq  = E / g.Qm;
+    const fast_div divK(Kq);
+
+    // First loop pass of the reference (copy mode), see the file header.
+    const bool     first_pass = a.new_data && E > 0;
+    const uint32_t L1         = g.L - g.rank0;
+    const uint32_t ncopy      = first_pass ? min(E, L1) : 0u;
+    const bool     k0_in_info = g.k0 < g.nof_info;
+    const uint32_t zero_end   = first_pass ? (k0_in_info ? g.k0 : g.nof_info) : 0u;
+    uint32_t       zero_from  = g.N; // final tail zeroing
+    if (a.new_data) {
+      uint32_t tmp;
+      if (E == 0) {
+        tmp = g.k0;
+      } else if (g.rank0 < g.nof_info) {
+        const uint32_t n1 = min(g.nof_info - g.rank0, E);
+        tmp               = (g.nof_sys + (E - n1)) % g.Ncb;
+      } else {
+        tmp = (g.rank0 + g.F + E) % g.Ncb;
+      }
+      if (E <= L1 && tmp != 0) {
+        zero_from = g.N - (g.Ncb - tmp);
+      }
+    }
+
+    const uint32_t step = gridDim.x * DEMATCH_THREADS * DEMATCH_PER_THREAD;
+    for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < g.N; p0 += step) {
+#pragma unroll
+      for (int k = 0; k < DEMATCH_PER_THREAD; ++k) {
+        const uint32_t p = p0 + k;
+        if (p >= g.N) {
+          break;
+        }
+        int v = buf[p];
+        if (p < zero_end) {
+          v = 0;
+        }
+        const bool filler = p >= g.nof_info && p < g.nof_sys;
+        if (first_pass && filler) {
+          v = LLR_INFINITY;
+        }
+        if (!filler && p < g.Ncb) {
+          const uint32_t w = p < g.nof_info ? p : p - g.F;
+          uint32_t       t = w >= g.rank0 ? w - g.rank0 : w + L1;
+          if (t < ncopy) {
+            uint32_t i, j;
+            j = divK.div(t, i);
+            v = in[i * g.Qm + j];
+            t += g.L;
+          }
+          for (; t < E; t += g.L) {
+            uint32_t i, j;
+            j = divK.div(t, i);
+            v = llr_sum(in[i * g.Qm + j], v);
+          }
+        }
+        if (p >= zero_from) {
+          v = 0;
+        }
+        buf[p] = static_cast<int8_t>(v);
+      }
+    }
+  }
+}
+
+
+constexpr int RATE_MATCH_THREADS = 256;
+
+__global__ __launch_bounds__(RATE_MATCH_THREADS) void ldpc_rate_match_kernel(rate_match_args a)
+{
+  const rm_geometry& g = a.g;
+  const fast_div     divL(g.L);
+  for (uint32_t cb = blockIdx.y; cb < a.nof_cbs; cb += gridDim.y) {
+    const uint32_t off   = a.out_offsets[cb];
+    const uint32_t E     = a.rm_lengths[cb];
+    const uint32_t first = (off + 7) / 8;
+    const uint32_t last  = (off + E + 7) / 8;
+    for (uint32_t b = first + blockIdx.x * RATE_MATCH_THREADS + threadIdx.x; b < last;
+         b += gridDim.x * RATE_MATCH_THREADS) {
+      uint32_t c = cb, off_c = off, E_c = E;
+      uint32_t byte = 0;
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t gbit = 8 * b + k;
+        bool           have = true;
+        while (gbit >= off_c + E_c) {
+          if (++c >= a.nof_cbs) {
+            have = false;
+            break;
+          }
+          off_c = a.out_offsets[c];
+          E_c   = a.rm_lengths[c];
+        }
+        if (!have) {
+          break;
+        }
+        if (gbit < off_c) {
+          continue; // gap between segments
+        }
+        const uint32_t o = gbit - off_c;
+        uint32_t       i, j;
+        if (g.Qm == 6) {
+          i = __umulhi(o >> 1, 0xAAAAAAABu) >> 1;
+          j = o - 6 * i;
+        } else {
+          const uint32_t sh = g.Qm == 8 ? 3 : g.Qm == 4 ? 2 : g.Qm == 2 ? 1 : 0;
+          i                 = o >> sh;
+          j                 = o & (g.Qm - 1);
+        }
+        const uint32_t t = j * (E_c / g.Qm) + i;
+        uint32_t       w;
+        divL.div(g.rank0 + t, w);
+        const uint32_t p   = w < g.nof_info ? w : w + g.F;
+        const uint8_t* src = a.cw + static_cast<size_t>(c) * a.cw_stride;
+        byte |= ((src[p >> 3] >> (7 - (p & 7))) & 1u) << (7 - k);
+      }
+      a.out[b] = static_cast<uint8_t>(byte);
+    }
+  }
+}
+
+hipError_t launch_rate_dematch(const dematch_args& a, hipStream_t stream)
+{
+  const uint32_t per_block = DEMATCH_THREADS * DEMATCH_PER_THREAD;
+  dim3           grid((a.g.N + per_block - 1) / per_block, a.nof_cbs < 65535u ? a.nof_cbs : 65535u);
+  hipLaunchKernelGGL(ldpc_rate_dematch_kernel, grid, dim3(DEMATCH_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rate_match(const rate_match_args& a, uint32_t max_rm_length, hipStream_t stream)
+{
+  const uint32_t bytes = (max_rm_length + 7) / 8 + 1;
+  uint32_t       gx    = (bytes + RATE_MATCH_THREADS - 1) / RATE_MATCH_THREADS;
+  dim3           grid(gx ? gx : 1, a.nof_cbs < 65535u ? a.nof_cbs : 65535u);
+  hipLaunchKernelGGL(ldpc_rate_match_kernel, grid, dim3(RATE_MATCH_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+} // namespace srs_amd
