@@ -62,6 +62,18 @@ def _load_ref():
     lib.srs_ref_ldpc_encode_rate_match.argtypes = [c_int, c_int] + [c_uint] * 4 + [P, c_uint, P]
     lib.srs_ref_ldpc_rate_dematch.restype = c_int
     lib.srs_ref_ldpc_rate_dematch.argtypes = [ctypes.c_char_p, c_int, c_int] + [c_uint] * 4 + [c_int, P, c_uint, P]
+    lib.srs_ref_dft.restype = c_int
+    lib.srs_ref_dft.argtypes = [c_uint, c_int, P, P]
+    lib.srs_ref_ofdm_slot_size.restype = c_uint
+    lib.srs_ref_ofdm_slot_size.argtypes = [c_uint, c_uint, c_uint, c_int, c_uint]
+    lib.srs_ref_ofdm_modulate_slot.restype = c_int
+    lib.srs_ref_ofdm_modulate_slot.argtypes = [c_uint, c_uint, c_uint, c_int, ctypes.c_float, ctypes.c_double, c_uint,
+                                               P, P]
+    lib.srs_ref_ofdm_demodulate_slot.restype = c_int
+    lib.srs_ref_ofdm_demodulate_slot.argtypes = [c_uint, c_uint, c_uint, c_int, c_uint, ctypes.c_float,
+                                                 ctypes.c_double, c_uint, P, P]
+    lib.srs_ref_ofdm_roundtrip_many.restype = ctypes.c_double
+    lib.srs_ref_ofdm_roundtrip_many.argtypes = [c_uint, c_uint, c_uint, P, c_uint, c_uint, c_uint]
     lib.srs_ref_ldpc_decode_many.restype = ctypes.c_double
     lib.srs_ref_ldpc_decode_many.argtypes = [ctypes.c_char_p, c_int, c_int, c_int, c_int, P, c_uint, c_uint, c_uint,
                                              c_int, P, P]
@@ -169,3 +181,30 @@ def ref_rate_dematch(llrs, bg, Z, rv, Qm, buf, new_data=True, Nref=0, filler=0, 
                                      _ptr(buf)) != 0:
         raise ValueError("reference dematcher %r unavailable" % impl)
     return buf
+
+
+def ref_dft(x, inverse=False):
+    x = np.ascontiguousarray(x, dtype=np.complex64)
+    out = np.zeros_like(x)
+    if REF.srs_ref_dft(x.size, int(inverse), _ptr(x), _ptr(out)) != 0:
+        raise ValueError("reference DFT size %d not supported" % x.size)
+    return out
+
+
+def ref_ofdm_modulate_slot(grid_u16, slot, numerology, bw_rb, dft_size, scale, fc, extended_cp=False):
+    grid_u16 = np.ascontiguousarray(grid_u16, dtype=np.uint16)
+    n = REF.srs_ref_ofdm_slot_size(numerology, bw_rb, dft_size, int(extended_cp), slot)
+    out = np.zeros(n, np.complex64)
+    REF.srs_ref_ofdm_modulate_slot(numerology, bw_rb, dft_size, int(extended_cp), scale, fc, slot, _ptr(grid_u16),
+                                   _ptr(out))
+    return out
+
+
+def ref_ofdm_demodulate_slot(samples, slot, numerology, bw_rb, dft_size, scale, fc, window_offset=0,
+                             extended_cp=False):
+    samples = np.ascontiguousarray(samples, dtype=np.complex64)
+    ns = 12 if extended_cp else 14
+    grid = np.zeros((ns, 2 * bw_rb * 12), np.uint16)
+    REF.srs_ref_ofdm_demodulate_slot(numerology, bw_rb, dft_size, int(extended_cp), window_offset, scale, fc, slot,
+                                     _ptr(samples), _ptr(grid))
+    return grid

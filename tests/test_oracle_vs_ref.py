@@ -136,3 +136,54 @@ def test_rate_dematcher_matches_reference(impl):
             oracle.rate_dematch(llr, bg, Z, rv, Qm, a, new_data, Nref, F)
             oracle.ref_rate_dematch(llr, bg, Z, rv, Qm, b, new_data, Nref, F, impl=impl)
             np.testing.assert_array_equal(a, b, err_msg=str((impl, bg, Z, F, rv, Qm, Nref, E, new_data)))
+
+
+# --- OFDM (oracle/ofdm.py vs the reference modulator / demodulator / generic DFT) ---
+
+# ofdm_modulator_test_data.h / ofdm_demodulator_test_data.h configurations
+# {numerology, bw_rb, dft_size, cp, scale, center_freq_Hz}, port, slot (the .dat
+# vectors themselves are not shipped; grids are synthetic).
+OFDM_CASES = [
+    (0, 12, 256, False, 0.81158, 2740100000, 0), (0, 96, 2048, False, 0.93184, 97900000, 0),
+    (0, 192, 4096, False, 0.87523, 1424700000, 0), (1, 24, 512, False, -0.47474, 293200000, 0),
+    (1, 48, 1024, False, 0.27046, 1607000000, 1), (1, 192, 4096, False, -0.54681, 619800000, 1),
+    (2, 12, 256, True, 0.73538, 837900000, 2), (2, 48, 1024, False, -0.14768, 2527000000, 3),
+    (2, 96, 2048, True, -0.93258, 2059300000, 3), (3, 192, 4096, False, 0.73052, 2633100000, 6),
+    (1, 273, 4096, False, 1.0, 3500000000, 0), (1, 106, 1536, False, 0.5, 1800000000, 1),
+]
+
+
+def test_dft_matches_reference():
+    """Float tolerance: max |ref - exact| <= 1e-5 * rms (the reference's float32 DFT)."""
+    rng = np.random.default_rng(21)
+    for N in (12, 128, 256, 512, 1024, 1536, 2048, 3072, 4096):
+        x = (rng.normal(size=N) + 1j * rng.normal(size=N)).astype(np.complex64)
+        for inv in (False, True):
+            r = oracle.ref_dft(x, inv)
+            e = np.fft.ifft(x.astype(complex)) * N if inv else np.fft.fft(x.astype(complex))
+            assert np.max(np.abs(r - e)) <= 1e-5 * np.sqrt(np.mean(np.abs(e) ** 2)), (N, inv)
+
+
+@pytest.mark.parametrize("case", OFDM_CASES)
+def test_ofdm_matches_reference(case):
+    from oracle import ofdm
+
+    mu, bw, N, ext, scale, fc, slot = case
+    rng = np.random.default_rng(N + bw)
+    g = ofdm.random_grid(rng, 12 if ext else 14, bw * 12)
+    r = oracle.ref_ofdm_modulate_slot(g, slot, mu, bw, N, scale, fc, ext)
+    o = ofdm.modulate_slot(g, slot, mu, bw, N, scale, fc, ext)
+    assert r.size == o.size == ofdm.slot_size(slot, mu, N, ext)
+    # modulator: float tolerance 1e-5 x RMS of the symbol stream
+    assert np.max(np.abs(r - o)) <= 1e-5 * np.sqrt(np.mean(np.abs(o) ** 2))
+    # received signal: the modulated slot plus noise (a pure round trip of a bf16
+    # grid can land exactly on bf16 rounding ties)
+    rx = (r + (rng.normal(0, 0.05, r.size) + 1j * rng.normal(0, 0.05, r.size)) * np.sqrt(np.mean(np.abs(r) ** 2)))
+    rx = rx.astype(np.complex64)
+    for off in (0, 5):
+        rg = oracle.ref_ofdm_demodulate_slot(rx, slot, mu, bw, N, scale, fc, off, ext)
+        og = ofdm.demodulate_slot(rx, slot, mu, bw, N, scale, fc, off, ext)
+        # demodulator: bf16 grid; equal except values straddling a bf16 rounding
+        # boundary, which may differ by one bf16 ulp
+        diff = np.abs(rg.astype(np.int32) - og.astype(np.int32))
+        assert diff.max() <= 1 and np.mean(diff != 0) < 1e-3, (off, diff.max(), np.mean(diff != 0))
