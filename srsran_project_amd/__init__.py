@@ -28,4 +28,17 @@ from .ldpc_codec import (  # noqa: F401
     create_ldpc_rate_matcher_factory_hip,
 )
 
+from .ofdm import (  # noqa: F401
+    CyclicPrefix,
+    DftDirection,
+    DftProcessor,
+    OfdmDemodulatorConfiguration,
+    OfdmModulatorConfiguration,
+    OfdmSlotDemodulator,
+    OfdmSlotModulator,
+    create_dft_processor_factory_hip,
+    create_ofdm_demodulator_factory_hip,
+    create_ofdm_modulator_factory_hip,
+)
+
 __version__ = "0.1.0"
