@@ -1,18 +1,27 @@
 #!/usr/bin/env python3
-"""bench.py -- MI355X LDPC decoder throughput (BASELINE.json configs[1]).
+"""bench.py -- MI355X PHY hot-path throughput (BASELINE.json configs).
 
-Workload (one "step"): decode one batch of BG1, Z=384 full-length codeblocks
-(66*384 = 25344 LLRs each, rate 1/3, 46 layers) with exactly 8 layered min-sum
-iterations (no early stop), as the reference benchmark
+Default workload (`--workload ldpc`, the headline, configs[1]): one "step"
+decodes one batch of BG1, Z=384 full-length codeblocks (66*384 = 25344 LLRs
+each, rate 1/3, 46 layers) with exactly 8 layered min-sum iterations (no early
+stop), as the reference benchmark
 tests/benchmarks/phy/upper/channel_coding/ldpc/ldpc_decoder_benchmark.cpp does
-(random +-10 LLR codeblocks, -I 8 -L 384, cb_len = max).  Inputs are resident in
-HBM before the timed region.  Multi-GPU: codeblocks are independent, so every
-rank decodes its own batch (weak scaling, no data-path collective); the timed
-region is bracketed by barriers and the max time over ranks is reported.
+(random +-10 LLR codeblocks, -I 8 -L 384, cb_len = max).
 
-cpu_baseline: the REFERENCE decoder itself (oracle/_ref, compiled from
-/root/reference sources: AVX512 if the host has it, else AVX2) on a bounded
-sample of the same workload, on the host cores of the same box, rank 0 only.
+`--workload ofdm` (configs[2]): one step OFDM-modulates and then demodulates a
+batch of slots of the 100 MHz numerology-1 carrier (273 PRB, 4096-point DFT,
+normal CP): 4 antenna ports x `--slots` slots, cbf16 resource grids to complex
+float baseband and back (ofdm_slot_modulator / ofdm_slot_demodulator).
+
+Inputs are resident in HBM before the timed region.  Multi-GPU: codeblocks /
+slots are independent, so every rank processes its own batch (weak scaling, no
+data-path collective); the timed region is bracketed by barriers and the max
+time over ranks is reported.
+
+cpu_baseline: the REFERENCE implementation itself (oracle/_ref, compiled from
+/root/reference sources: the AVX512 decoder if the host has it, else AVX2; the
+generic DFT for OFDM since FFTW is not in the image) on a bounded sample of the
+same workload, on the host cores of the same box, rank 0 only.
 """
 import argparse
 import json
@@ -25,11 +34,16 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md chip-level parameters (spec)
+
+# LDPC headline workload
 BG, Z, ITERS = 1, 384, 8
 K_BITS = 22 * Z                 # information bits per codeblock (message incl. CRC)
 N_LLRS = 66 * Z                 # LLRs per codeblock (full length)
 OUT_BYTES = (K_BITS + 7) // 8
-HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md chip-level parameters (spec)
+
+# OFDM workload: 100 MHz, 30 kHz SCS
+OFDM_MU, OFDM_BW, OFDM_N, OFDM_PORTS = 1, 273, 4096, 4
 
 
 def parse():
@@ -37,7 +51,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--batch", type=int, default=4096, help="codeblocks per rank per step")
+    p.add_argument("--workload", default="ldpc", choices=["ldpc", "ofdm"])
+    p.add_argument("--batch", type=int, default=4096, help="ldpc: codeblocks per rank per step")
+    p.add_argument("--slots", type=int, default=160, help="ofdm: slots per rank per step (x 4 ports)")
     p.add_argument("--iters", type=int, default=ITERS)
     p.add_argument("--arith", default="simd", choices=["simd", "generic"])
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -46,7 +62,47 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(args, llrs_host):
+def load_traffic(name):
+    """HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    (tools/gpu_check.sh traffic), committed under profiles/."""
+    tpath = os.path.join(ROOT, "profiles", name)
+    if os.path.exists(tpath):
+        return json.load(open(tpath)).get("hbm_bytes_per_launch")
+    return None
+
+
+def timed(args, dist, world, dev, stream, step):
+    """Warmup, then K steps bracketed by barrier + synchronize; per-step HIP
+    events on the launch stream.  Returns (elapsed_s max over ranks, mean event ms)."""
+    import torch
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        starts[s].record(stream)
+        step()
+        ends[s].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    event_ms = float(np.mean([starts[s].elapsed_time(ends[s]) for s in range(args.steps)]))
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), event_ms
+
+
+# ------------------------------------------------------------------ LDPC ----
+
+def ldpc_cpu_baseline(args, llrs_host):
     """Times the reference CPU decoder on a bounded sample of the same workload."""
     try:
         import oracle  # test infrastructure: only used here as the CPU baseline
@@ -83,6 +139,195 @@ def cpu_baseline(args, llrs_host):
     }
 
 
+def run_ldpc(args, dist, world, rank, dev):
+    import torch
+
+    import srsran_project_amd as amd
+
+    dec = amd.LdpcDecoder(args.arith, device=dev.index)
+    cfg = amd.LdpcDecoderConfiguration(base_graph=BG, lifting_size=Z, nof_crc_bits=24, max_iterations=args.iters)
+    # Synthetic input, as ldpc_decoder_benchmark.cpp:172: random (+-10) LLRs.
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    llrs = (torch.randint(0, 2, (args.batch, N_LLRS), device=dev, generator=g, dtype=torch.int8) * 20 - 10)
+    out = torch.empty((args.batch, OUT_BYTES), dtype=torch.uint8, device=dev)
+    its = torch.empty((args.batch,), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        dec.decode_batch(llrs, cfg, None, out=out, nof_iters=its, stream=stream)
+
+    elapsed, kernel_ms = timed(args, dist, world, dev, stream, step)
+    total_cbs = args.batch * args.steps * world
+    value = total_cbs / elapsed
+    bytes_per_cb = N_LLRS + OUT_BYTES + 4  # LLRs in, packed message out, iteration count
+    achieved_gbs = bytes_per_cb * args.batch / (kernel_ms * 1e-3) / 1e9
+    if rank != 0:
+        return None
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = ldpc_cpu_baseline(args, llrs[:512].cpu().numpy())
+    return {
+        "metric": "LDPC decode codeblocks/s (BG1 Z=384, 8 min-sum iterations, full-length rate-1/3 codeblocks)",
+        "value": value,
+        "unit": "codeblocks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic (random +-10 LLRs, as ldpc_decoder_benchmark.cpp)",
+        "config": {
+            "workload": "configs[1]: LDPC decode BG1 Z=384 8 iterations",
+            "base_graph": BG,
+            "lifting_size": Z,
+            "max_iterations": args.iters,
+            "codeblock_llrs": N_LLRS,
+            "codeblocks_per_step_per_gpu": args.batch,
+            "early_stop": False,
+            "arith": args.arith,
+            "parallelism": "codeblocks sharded over ranks" if world > 1 else "single GPU",
+        },
+        "info_throughput_gbps": value * K_BITS / 1e9,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": load_traffic("r01_ldpc_decode_traffic.json"),
+            "kernel": "ldpc_decode_kernel",
+            "kernel_ms": kernel_ms,
+            "algorithmic_bytes_per_launch": bytes_per_cb * args.batch,
+        },
+        "cpu_baseline": cpu,
+    }
+
+
+# ------------------------------------------------------------------ OFDM ----
+
+def ofdm_cpu_baseline(args, grids_host):
+    try:
+        import oracle
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "unit": "symbols/s", "error": "oracle unavailable: %s" % e}
+    if oracle.REF is None:
+        return {"value": None, "unit": "symbols/s", "error": "oracle/_ref/libsrsran_ref.so not built"}
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    sample = np.ascontiguousarray(grids_host)
+    ns = sample.shape[0]
+    n0 = 2 * threads
+    t = oracle.REF.srs_ref_ofdm_roundtrip_many(OFDM_MU, OFDM_BW, OFDM_N, sample.ctypes.data_as(oracle.P), ns, n0,
+                                               threads)
+    n = int(max(n0, min(n0 / max(t, 1e-9) * args.cpu_seconds, 1 << 20)))
+    t = oracle.REF.srs_ref_ofdm_roundtrip_many(OFDM_MU, OFDM_BW, OFDM_N, sample.ctypes.data_as(oracle.P), ns, n,
+                                               threads)
+    return {
+        "value": n * 14 / t,
+        "unit": "symbols/s",
+        "cores": threads,
+        "kind": "reference",
+        "impl": "ofdm_slot_modulator_impl + ofdm_slot_demodulator_impl, dft_processor_generic_impl",
+        "sample": "%d slot-ports (14 symbols each) modulated then demodulated, 100 MHz mu=1 273 PRB 4096-point, "
+                  "cycling over %d grids, %d worker threads with one modulator + demodulator each, %.1f s "
+                  "(reference generic DFT: FFTW is not in the image)" % (n, ns, threads, t),
+    }
+
+
+def run_ofdm(args, dist, world, rank, dev):
+    import torch
+
+    import srsran_project_amd as amd
+
+    rg = OFDM_BW * 12
+    mod = amd.OfdmSlotModulator(amd.OfdmModulatorConfiguration(OFDM_MU, OFDM_BW, OFDM_N, 0, 1.0, 3.5e9),
+                                device=dev.index)
+    dem = amd.OfdmSlotDemodulator(amd.OfdmDemodulatorConfiguration(OFDM_MU, OFDM_BW, OFDM_N, 0, 1.0, 3.5e9, 0),
+                                  device=dev.index)
+    g = torch.Generator(device=dev)
+    g.manual_seed(99 + rank)
+    # QPSK-like cbf16 grid: +-0.707 in bf16 (0x3F35 / 0xBF35)
+    bits = torch.randint(0, 2, (args.slots, OFDM_PORTS, 14, 2 * rg), device=dev, generator=g, dtype=torch.int16)
+    grid = torch.where(bits == 0, torch.tensor(0x3F35, dtype=torch.int16, device=dev),
+                       torch.tensor(0xBF35 - 0x10000, dtype=torch.int16, device=dev)).contiguous()
+    stride = mod.max_slot_size()
+    samples = torch.empty((args.slots, OFDM_PORTS, stride), dtype=torch.complex64, device=dev)
+    back = torch.empty_like(grid)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        mod.modulate_batch(grid, 0, out=samples, stream=stream)
+        dem.demodulate_batch(samples, 0, grid=back, stream=stream)
+
+    # per-kernel timing on the launch stream: modulator alone, demodulator alone
+    elapsed, step_ms = timed(args, dist, world, dev, stream, step)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record(stream)
+    for _ in range(args.steps):
+        mod.modulate_batch(grid, 0, out=samples, stream=stream)
+    ev[1].record(stream)
+    for _ in range(args.steps):
+        dem.demodulate_batch(samples, 0, grid=back, stream=stream)
+    ev[2].record(stream)
+    torch.cuda.synchronize(dev)
+    mod_ms = ev[0].elapsed_time(ev[1]) / args.steps
+    dem_ms = ev[1].elapsed_time(ev[2]) / args.steps
+
+    nsym = args.slots * OFDM_PORTS * 14
+    # algorithmic HBM bytes: grid (cbf16, 4 B/RE) + samples (cf32, 8 B) once each way
+    samp = sum(mod.get_slot_size(s % (1 << OFDM_MU)) for s in range(args.slots))
+    mod_bytes = OFDM_PORTS * (args.slots * 14 * rg * 4 + samp * 8)
+    dem_bytes = nsym * (OFDM_N * 8 + rg * 4)
+    mod_gbs = mod_bytes / (mod_ms * 1e-3) / 1e9
+    dem_gbs = dem_bytes / (dem_ms * 1e-3) / 1e9
+    value = nsym * args.steps * world / elapsed
+    if rank != 0:
+        return None
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = ofdm_cpu_baseline(args, grid[:8, 0].cpu().numpy().view(np.uint16))
+    return {
+        "metric": "OFDM modulate+demodulate symbols/s (100 MHz numerology-1, 273 PRB, 4096-point DFT)",
+        "value": value,
+        "unit": "symbols/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (random QPSK cbf16 resource grids)",
+        "config": {
+            "workload": "configs[2]: OFDM modulate+demodulate, 100 MHz numerology-1 (4096-pt FFT), batched slots",
+            "numerology": OFDM_MU,
+            "bw_rb": OFDM_BW,
+            "dft_size": OFDM_N,
+            "ports": OFDM_PORTS,
+            "slots_per_step_per_gpu": args.slots,
+            "symbols_per_step_per_gpu": nsym,
+            "parallelism": "slots sharded over ranks" if world > 1 else "single GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": (mod_bytes + dem_bytes) / ((mod_ms + dem_ms) * 1e-3) / 1e9,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (mod_bytes + dem_bytes) / ((mod_ms + dem_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "traffic": load_traffic("r01_ofdm_traffic.json"),
+            "kernel": "ofdm_modulate_kernel<4096> + ofdm_demodulate_kernel<4096>",
+            "modulate": {"ms": mod_ms, "bytes": mod_bytes, "GB/s": mod_gbs},
+            "demodulate": {"ms": dem_ms, "bytes": dem_bytes, "GB/s": dem_gbs},
+            "step_event_ms": step_ms,
+        },
+        "cpu_baseline": cpu,
+    }
+
+
 def main():
     args = parse()
     import torch
@@ -95,99 +340,9 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
-
-    import srsran_project_amd as amd
-
-    dec = amd.LdpcDecoder(args.arith, device=local_rank)
-    cfg = amd.LdpcDecoderConfiguration(base_graph=BG, lifting_size=Z, nof_crc_bits=24, max_iterations=args.iters)
-
-    # Synthetic input, as ldpc_decoder_benchmark.cpp:172: random (+-10) LLRs.
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    llrs = (torch.randint(0, 2, (args.batch, N_LLRS), device=dev, generator=g, dtype=torch.int8) * 20 - 10)
-    out = torch.empty((args.batch, OUT_BYTES), dtype=torch.uint8, device=dev)
-    its = torch.empty((args.batch,), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-
-    for _ in range(args.warmup):
-        dec.decode_batch(llrs, cfg, None, out=out, nof_iters=its, stream=stream)
-    torch.cuda.synchronize(dev)
-
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        starts[s].record(stream)
-        dec.decode_batch(llrs, cfg, None, out=out, nof_iters=its, stream=stream)
-        ends[s].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([starts[s].elapsed_time(ends[s]) for s in range(args.steps)]))
-
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-
-    total_cbs = args.batch * args.steps * world
-    value = total_cbs / elapsed
-    bytes_per_cb = N_LLRS + OUT_BYTES + 4  # LLRs in, packed message out, iteration count
-    achieved_gbs = bytes_per_cb * args.batch / (kernel_ms * 1e-3) / 1e9
-
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r01_ldpc_decode_traffic.json")
-    if os.path.exists(tpath):
-        # HBM bytes per launch of this kernel on this workload, from rocprofv3
-        # FETCH_SIZE / WRITE_SIZE in separate --pmc passes (tools/gpu_check.sh traffic)
-        traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
-
+    run = run_ldpc if args.workload == "ldpc" else run_ofdm
+    line = run(args, dist, world, rank, dev)
     if rank == 0:
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args, llrs[:512].cpu().numpy())
-        line = {
-            "metric": "LDPC decode codeblocks/s (BG1 Z=384, 8 min-sum iterations, full-length rate-1/3 codeblocks)",
-            "value": value,
-            "unit": "codeblocks/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int8",
-            "data": "synthetic (random +-10 LLRs, as ldpc_decoder_benchmark.cpp)",
-            "config": {
-                "workload": "configs[1]: LDPC decode BG1 Z=384 8 iterations",
-                "base_graph": BG,
-                "lifting_size": Z,
-                "max_iterations": args.iters,
-                "codeblock_llrs": N_LLRS,
-                "codeblocks_per_step_per_gpu": args.batch,
-                "early_stop": False,
-                "arith": args.arith,
-                "parallelism": "codeblocks sharded over ranks" if world > 1 else "single GPU",
-            },
-            "info_throughput_gbps": value * K_BITS / 1e9,
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved_gbs,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "kernel": "ldpc_decode_kernel",
-                "kernel_ms": kernel_ms,
-                "algorithmic_bytes_per_launch": bytes_per_cb * args.batch,
-            },
-            "cpu_baseline": cpu,
-        }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

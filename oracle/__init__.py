@@ -74,6 +74,12 @@ def _load_ref():
                                                  ctypes.c_double, c_uint, P, P]
     lib.srs_ref_ofdm_roundtrip_many.restype = ctypes.c_double
     lib.srs_ref_ofdm_roundtrip_many.argtypes = [c_uint, c_uint, c_uint, P, c_uint, c_uint, c_uint]
+    lib.srs_ref_equalizer_is_supported.restype = c_int
+    lib.srs_ref_equalizer_is_supported.argtypes = [c_int, c_uint, c_uint]
+    lib.srs_ref_equalize.restype = c_int
+    lib.srs_ref_equalize.argtypes = [c_int, c_uint, c_uint, c_uint, P, P, P, ctypes.c_float, P, P]
+    lib.srs_ref_equalize_many.restype = ctypes.c_double
+    lib.srs_ref_equalize_many.argtypes = [c_uint, c_uint, c_uint, P, P, P, c_uint, c_uint]
     lib.srs_ref_ldpc_decode_many.restype = ctypes.c_double
     lib.srs_ref_ldpc_decode_many.argtypes = [ctypes.c_char_p, c_int, c_int, c_int, c_int, P, c_uint, c_uint, c_uint,
                                              c_int, P, P]
@@ -208,3 +214,17 @@ def ref_ofdm_demodulate_slot(samples, slot, numerology, bw_rb, dft_size, scale, 
     REF.srs_ref_ofdm_demodulate_slot(numerology, bw_rb, dft_size, int(extended_cp), window_offset, scale, fc, slot,
                                      _ptr(samples), _ptr(grid))
     return grid
+
+
+def ref_equalize(symbols_u16, est_u16, noise_vars, tx_scaling, nof_layers, mmse=False):
+    symbols_u16 = np.ascontiguousarray(symbols_u16, dtype=np.uint16)
+    est_u16 = np.ascontiguousarray(est_u16, dtype=np.uint16)
+    nv = np.ascontiguousarray(noise_vars, dtype=np.float32)
+    P = symbols_u16.shape[0]
+    R = symbols_u16.shape[1] // 2
+    eq = np.zeros((R, nof_layers), np.complex64)
+    nvo = np.zeros((R, nof_layers), np.float32)
+    if REF.srs_ref_equalize(int(mmse), R, P, nof_layers, _ptr(symbols_u16), _ptr(est_u16), _ptr(nv),
+                            float(tx_scaling), _ptr(eq), _ptr(nvo)) != 0:
+        raise ValueError("reference equalizer does not support %d ports x %d layers" % (P, nof_layers))
+    return eq, nvo

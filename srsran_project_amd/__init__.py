@@ -41,4 +41,10 @@ from .ofdm import (  # noqa: F401
     create_ofdm_modulator_factory_hip,
 )
 
+from .equalizer import (  # noqa: F401
+    ChannelEqualizer,
+    ChannelEqualizerAlgorithmType,
+    create_channel_equalizer_generic_factory_hip,
+)
+
 __version__ = "0.1.0"

@@ -18,9 +18,10 @@
 //
 // LDS holds the vector padded by one complex every 16 (index i -> i + i/16):
 // the first pass's stride-R writes then spread over all 64 banks.
-// Pass twiddles W_N^m come from a per-size table (double-precision values
-// rounded to float, HBM/L2-resident); the DFT_R kernels' internal twiddles are
-// compile-time constants.
+// Pass twiddles: the base W_N^m of each butterfly comes from a per-size table
+// (double-precision values rounded to float, L2-resident), its powers are
+// formed in registers; the DFT_R kernels' internal twiddles are compile-time
+// constants.
 //
 // Accuracy: float32 arithmetic with exactly rounded twiddles; the error is that
 // of any radix-R float FFT, O(eps * log N) of the RMS (tests state the bound).
@@ -207,14 +208,41 @@ constexpr int lds_complex()
   return N + N / 16;
 }
 
+template <int R, int... Rest>
+struct first_of {
+  static constexpr int value = R;
+};
+
+// w[r] = w1^r, r = 1..R-1, by squarings and one multiply each (error grows
+// with the depth, <= 6 products for R = 16).
+template <int R>
+__device__ __forceinline__ void twiddle_powers(cf w1, cf* w)
+{
+  w[1] = w1;
+#pragma unroll
+  for (int r = 2; r < R; ++r) {
+    w[r] = (r & 1) ? cmul(w[r - 1], w1) : cmul(w[r / 2], w[r / 2]);
+  }
+}
+
 // Runs the passes Rs... over one N-point vector with T threads.
 //   load(i)       -> cf  : input sample i (first pass only)
 //   store(i, v)          : output sample i (last pass only)
 //   tw                   : table W_N^m = exp(-2*pi*i*m/N), m in [0, N) (conjugated for S = +1)
+// Each butterfly of a later pass needs W_{Ns*R}^{r*k}, r = 1..R-1: only the
+// base W_{Ns*R}^k is read from the table -- one HBM/L2 load per butterfly,
+// issued a whole pass ahead so its latency hides behind the previous pass --
+// and the powers are formed in registers.
 template <int N, int T, int S, int... Rs>
 struct stockham {
+  template <int Ns, int R>
+  static constexpr int per()
+  {
+    return N / R / T;
+  }
+
   template <int Ns, int R, int... Rest, class Load, class Store>
-  __device__ __forceinline__ static void pass(cf* lds, const cf* tw, Load& load, Store& store)
+  __device__ __forceinline__ static void pass(cf* lds, const cf* tw, Load& load, Store& store, const cf* wbase)
   {
     constexpr int  NB    = N / R;           // butterflies in this pass
     constexpr int  PER   = NB / T;          // butterflies per thread
@@ -222,7 +250,21 @@ struct stockham {
     constexpr bool LAST  = sizeof...(Rest) == 0;
     static_assert(NB % T == 0, "butterflies must divide evenly over the threads");
     const int tid = threadIdx.x;
-    cf        v[PER][R];
+
+    // prefetch the next pass's twiddle bases
+    constexpr int R2   = LAST ? 1 : first_of<Rest..., 1>::value;
+    constexpr int Ns2  = Ns * R;
+    constexpr int PER2 = LAST ? 1 : N / R2 / T;
+    cf            wnext[PER2];
+    if constexpr (!LAST) {
+#pragma unroll
+      for (int b = 0; b < PER2; ++b) {
+        const int j2 = tid + b * T;
+        wnext[b]     = tw[(j2 % Ns2) * (N / (Ns2 * R2))];
+      }
+    }
+
+    cf v[PER][R];
 #pragma unroll
     for (int b = 0; b < PER; ++b) {
       const int j = tid + b * T;
@@ -230,15 +272,19 @@ struct stockham {
       for (int r = 0; r < R; ++r) {
         v[b][r] = FIRST ? load(j + r * NB) : lds[pad(j + r * NB)];
       }
+    }
+#pragma unroll
+    for (int b = 0; b < PER; ++b) {
       if constexpr (!FIRST) {
-        const int k = j % Ns;
+        cf w1 = wbase[b];
+        if (S > 0) {
+          w1.y = -w1.y;
+        }
+        cf w[R];
+        twiddle_powers<R>(w1, w);
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          cf w = tw[(r * k) * (N / (Ns * R))];
-          if (S > 0) {
-            w.y = -w.y;
-          }
-          v[b][r] = cmul(v[b][r], w);
+          v[b][r] = cmul(v[b][r], w[r]);
         }
       }
       small_dft<R, S>::run(v[b]);
@@ -267,14 +313,14 @@ struct stockham {
         }
       }
       __syncthreads();
-      pass<Ns * R, Rest...>(lds, tw, load, store);
+      pass<Ns * R, Rest...>(lds, tw, load, store, wnext);
     }
   }
 
   template <class Load, class Store>
   __device__ __forceinline__ static void run(cf* lds, const cf* tw, Load& load, Store& store)
   {
-    pass<1, Rs...>(lds, tw, load, store);
+    pass<1, Rs...>(lds, tw, load, store, nullptr);
   }
 };
 
@@ -296,9 +342,9 @@ SRS_DFT_PLAN(768, 64, 4, 4, 4, 4, 3)
 SRS_DFT_PLAN(1024, 64, 16, 16, 4)
 SRS_DFT_PLAN(1536, 64, 8, 8, 8, 3)
 SRS_DFT_PLAN(2048, 128, 16, 16, 8)
-SRS_DFT_PLAN(3072, 64, 16, 16, 4, 3)
+SRS_DFT_PLAN(3072, 256, 4, 4, 4, 4, 4, 3)
 SRS_DFT_PLAN(4096, 256, 16, 16, 16)
-SRS_DFT_PLAN(6144, 128, 16, 16, 8, 3)
+SRS_DFT_PLAN(6144, 256, 8, 8, 8, 4, 3)
 SRS_DFT_PLAN(8192, 256, 16, 16, 16, 2)
 #undef SRS_DFT_PLAN
 

@@ -60,6 +60,7 @@ constexpr int LDS_RED_OFFSET  = 16;
 constexpr int LDS_SOFT_OFFSET = 80;
 using lds_i8                  = __attribute__((address_space(3))) int8_t;
 using lds_i32                 = __attribute__((address_space(3))) int32_t;
+using lds_u32                 = __attribute__((address_space(3))) uint32_t;
 
 
 // Row degrees of the base graphs (TS 38.212 Tables 5.3.2-2/3).
@@ -467,43 +468,40 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
   lds_i8*       soft    = (lds_i8*)(uintptr_t)LDS_SOFT_OFFSET;
   lds_i8*       c2v_lds = soft + lds_soft_bytes<BG>(Z);
 
-  const int  j       = threadIdx.x;
   const int  nthr    = blockDim.x;
-  // check row of this lane (== j unless rows are spread 48 per wave)
   constexpr int CPW  = checks_per_wave<ZC>();
-  const int  jc      = CPW == 64 ? j : (j >> 6) * CPW + ((j & 63) < CPW ? (j & 63) : (j & 63) - (64 - CPW));
-  const bool active  = CPW == 64 ? j < Z : true;
-  // idle lanes (Z not a multiple of 64) work on a private pad byte after the messages
-  const int idle_slot = active ? -1 : lds_total_bytes<BG>(Z) - LDS_SOFT_OFFSET - 64 + (j & 63);
-  const int wave      = j >> 6;
-  const int nwaves    = nthr >> 6;
-  const int lane      = j & 63;
-  const int msg_len   = bg_traits<BG>::K * Z;
-  const int NZ        = N_FULL * Z;
+  const int  msg_len = bg_traits<BG>::K * Z;
+  const int  NZ      = N_FULL * Z;
 
   for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
+    // Per-lane values are rebuilt from a laundered thread id in each phase, so
+    // the compiler cannot hoist them out of the codeblock loop and keep them
+    // live (spilled to scratch) across the iterations.
+    int j = threadIdx.x;
+    asm volatile("" : "+v"(j));
     const int8_t* in     = a.llrs + static_cast<size_t>(cb) * a.llr_stride;
     const int     n_llrs = a.llr_lens ? static_cast<int>(a.llr_lens[cb]) : static_cast<int>(a.llr_len);
     uint8_t*      out    = a.out + static_cast<size_t>(cb) * a.out_stride;
     const int     obytes = (msg_len + 7) >> 3;
 
     // ---- input trimming: position of the last non-zero LLR (ldpc_decoder_impl.cpp:86).
-    int last = -1;
-    for (int i = j; i < n_llrs; i += nthr) {
-      if (in[i] != 0) {
-        last = i;
+    if (j == 0) {
+      red[0] = -1;
+    }
+    __syncthreads();
+    {
+      int last = -1;
+      for (int i = j; i < n_llrs; i += nthr) {
+        if (in[i] != 0) {
+          last = i;
+        }
+      }
+      if (last >= 0) {
+        __hip_atomic_fetch_max(&red[0], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
-    last = wave_max(last);
     __syncthreads();
-    if (lane == 0) {
-      red[wave] = last;
-    }
-    __syncthreads();
-    int input_size = 0;
-    for (int w = 0; w < nwaves; ++w) {
-      input_size = red[w] + 1 > input_size ? red[w] + 1 : input_size;
-    }
+    const int input_size = __builtin_amdgcn_readfirstlane(red[0] + 1);
 
     if (input_size < msg_len && a.force_decoding) {
       // ldpc_decoder_impl.cpp:92: not enough soft bits -- all ones when no CRC,
@@ -550,6 +548,12 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
     const int nof_sig    = msg_len - a.nof_filler_bits;
     int       result     = -1;
 
+    // check row of this lane (== j unless rows are spread 48 per wave)
+    const int jc        = CPW == 64 ? j : (j >> 6) * CPW + ((j & 63) < CPW ? (j & 63) : (j & 63) - (64 - CPW));
+    const bool active   = CPW == 64 ? j < Z : true;
+    // idle lanes (Z not a multiple of 64) work on a private pad byte after the messages
+    const int idle_slot = active ? -1 : lds_total_bytes<BG>(Z) - LDS_SOFT_OFFSET - 64 + (j & 63);
+
     // check-to-variable messages start at zero (ldpc_decoder_impl.cpp:244: an
     // uninitialised layer uses v2c = soft, identical to v2c = soft - 0).
     uint32_t c2v[NW];
@@ -563,27 +567,34 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
       run_layers<BG, ZC, 0, ARITH>(soft, c2v_lds, c2v, (const_u32_ptr)(a.edges), Z, jc, idle_slot, nof_layers);
 
       if (a.crc_table) {
-        // get_hard_bits + CRC early stop (ldpc_decoder_impl.cpp:125).
+        // get_hard_bits + CRC early stop (ldpc_decoder_impl.cpp:125): linear
+        // CRC, every lane XORs the remainders of its set bits into LDS.
+        int jj = threadIdx.x;
+        asm volatile("" : "+v"(jj));
+        if (jj == 0) {
+          red[1] = 0;
+          red[2] = 0;
+        }
+        __syncthreads();
         uint32_t crc = 0, zero = 0;
-        for (int i = j; i < msg_len; i += nthr) {
+        for (int i = jj; i < msg_len; i += nthr) {
           int sb = soft[i];
           zero |= (sb == 0);
           if (i < nof_sig && sb <= 0) {
             crc ^= a.crc_table[nof_sig - 1 - i];
           }
         }
-        crc  = wave_xor(crc);
-        zero = wave_or(zero);
-        if (lane == 0) {
-          red[wave]     = static_cast<int32_t>(crc);
-          red[8 + wave] = static_cast<int32_t>(zero);
+        if (crc != 0) {
+          __hip_atomic_fetch_xor(reinterpret_cast<lds_u32*>(&red[1]), crc, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (zero != 0) {
+          __hip_atomic_fetch_or(reinterpret_cast<lds_u32*>(&red[2]), zero, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         __syncthreads();
-        uint32_t c_all = 0, z_all = 0;
-        for (int w = 0; w < nwaves; ++w) {
-          c_all ^= static_cast<uint32_t>(red[w]);
-          z_all |= static_cast<uint32_t>(red[8 + w]);
-        }
+        const uint32_t c_all = __builtin_amdgcn_readfirstlane(red[1]);
+        const uint32_t z_all = __builtin_amdgcn_readfirstlane(red[2]);
         __syncthreads();
         if (z_all == 0 && c_all == 0) {
           result = it + 1;
@@ -593,7 +604,9 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
     }
 
     // ---- hard decision, packed MSB-first (log_likelihood_ratio.cpp hard_decision).
-    for (int b = j; b < obytes; b += nthr) {
+    int je = threadIdx.x;
+    asm volatile("" : "+v"(je));
+    for (int b = je; b < obytes; b += nthr) {
       uint32_t byte = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -606,11 +619,11 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
     }
     if (a.soft_out) {
       int8_t* so = a.soft_out + static_cast<size_t>(cb) * NZ;
-      for (int i = j; i < NZ; i += nthr) {
+      for (int i = je; i < NZ; i += nthr) {
         so[i] = soft[i];
       }
     }
-    if (j == 0) {
+    if (je == 0) {
       a.nof_iters[cb] = result;
     }
     __syncthreads();

@@ -1,0 +1,95 @@
+"""GPU parity: MI355X channel equalizer (through the C-ABI) vs the CPU oracle
+oracle/equalizer.py (exact arithmetic on the bf16 inputs), itself pinned to the
+reference's channel_equalizer_generic_impl in tests/test_oracle_vs_ref.py.
+
+Tolerance (the contract): |gpu - exact| <= 1e-3 * |exact| + 1e-6 on equalized
+symbols and <= 2e-3 * exact on noise variances (the reference's own AVX2 path
+sits at ~3e-4 / 6e-4 because of its approximate reciprocal); the abnormal
+cases (zero / infinite / NaN channel, invalid noise variances) give exactly
+zero symbols and infinite variances where the reference's scalar path does.
+"""
+import numpy as np
+import pytest
+
+from oracle import equalizer as E
+from oracle.ofdm import float_to_bf16
+
+pytestmark = pytest.mark.gpu
+
+TOPOLOGIES = [(1, 1), (2, 1), (4, 1), (2, 2), (4, 2)]
+
+
+@pytest.fixture(scope="module")
+def amd():
+    import srsran_project_amd as amd
+
+    return amd
+
+
+def _close(got, gotn, want, wantn):
+    assert np.all(np.abs(got - want) <= 1e-3 * np.abs(want) + 1e-6)
+    fin = np.isfinite(wantn)
+    assert np.array_equal(np.isfinite(gotn), fin)
+    assert np.all(np.abs(gotn[fin] - wantn[fin]) <= 2e-3 * wantn[fin])
+
+
+@pytest.mark.parametrize("ports,layers", TOPOLOGIES)
+def test_equalizer_random_channels(amd, ports, layers):
+    rng = np.random.default_rng(ports * 7 + layers)
+    for algo in (amd.ChannelEqualizerAlgorithmType.zf, amd.ChannelEqualizerAlgorithmType.mmse):
+        eq = amd.ChannelEqualizer(algo)
+        if not eq.is_supported(ports, layers):
+            assert not E.is_supported(algo.name, ports, layers)
+            continue
+        for nre, tx, snr in ((1, 1.0, 20.0), (257, 0.5, 5.0), (3276 * 14, 1.0, 30.0)):
+            s, h, nv, _ = E.random_channel(rng, nre, ports, layers, snr)
+            got, gotn = eq.equalize(s, h, nv, tx)
+            want, wantn = E.equalize(s, h, nv, tx, layers)
+            _close(got, gotn, want, wantn)
+
+
+@pytest.mark.parametrize("ports,layers", TOPOLOGIES)
+def test_equalizer_abnormal_inputs(amd, ports, layers):
+    rng = np.random.default_rng(99)
+    eq = amd.ChannelEqualizer()
+    s, h, nv, _ = E.random_channel(rng, 64, ports, layers)
+    h = h.copy()
+    # RE 0: zero channel on every path; RE 1: NaN on the first path; RE 2: infinity
+    h[:, :, 0:2] = 0
+    h[0, 0, 2:4] = float_to_bf16(np.array([np.nan, 0.0], np.float32))
+    h[0, 0, 4:6] = float_to_bf16(np.array([np.inf, 1.0], np.float32))
+    got, gotn = eq.equalize(s, h, nv, 1.0)
+    want, wantn = E.equalize(s, h, nv, 1.0, layers)
+    assert got[0].tolist() == [0] * layers and np.all(np.isinf(gotn[0]))
+    ok = ~np.isnan(want).any(axis=1)
+    _close(got[ok], gotn[ok], want[ok], wantn[ok])
+    for bad in ([0.0] * ports, [-1.0] + [0.01] * (ports - 1), [np.inf] + [0.02] * (ports - 1)):
+        got, gotn = eq.equalize(s, h, np.array(bad, np.float32), 1.0)
+        want, wantn = E.equalize(s, h, np.array(bad, np.float32), 1.0, layers)
+        ok = ~np.isnan(want).any(axis=1)
+        _close(got[ok], gotn[ok], want[ok], wantn[ok])
+
+
+def test_equalizer_batch_device(amd):
+    import torch
+
+    rng = np.random.default_rng(1)
+    eq = amd.ChannelEqualizer()
+    s, h, nv, _ = E.random_channel(rng, 3276 * 12, 4, 2)
+    ds = torch.from_numpy(s.view(np.int16)).cuda()
+    dh = torch.from_numpy(h.view(np.int16)).cuda()
+    got, gotn = eq.equalize_batch(ds, dh, nv, 0.8)
+    torch.cuda.synchronize()
+    want, wantn = E.equalize(s, h, nv, 0.8, 2)
+    _close(got.cpu().numpy(), gotn.cpu().numpy(), want, wantn)
+
+
+def test_equalizer_unsupported(amd):
+    eq = amd.ChannelEqualizer(amd.ChannelEqualizerAlgorithmType.mmse)
+    assert not eq.is_supported(2, 2)
+    assert not eq.is_supported(3, 1)
+    s, h, nv, _ = E.random_channel(np.random.default_rng(0), 8, 2, 2)
+    with pytest.raises(ValueError):
+        eq.equalize(s, h, nv, 1.0)
+    with pytest.raises(ValueError):
+        amd.ChannelEqualizer().equalize(s, h, nv, 0.0)

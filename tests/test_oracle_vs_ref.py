@@ -187,3 +187,37 @@ def test_ofdm_matches_reference(case):
         # boundary, which may differ by one bf16 ulp
         diff = np.abs(rg.astype(np.int32) - og.astype(np.int32))
         assert diff.max() <= 1 and np.mean(diff != 0) < 1e-3, (off, diff.max(), np.mean(diff != 0))
+
+
+# --- channel equalizer (oracle/equalizer.py vs channel_equalizer_generic_impl) ---
+
+@pytest.mark.parametrize("ports,layers", [(1, 1), (2, 1), (4, 1), (2, 2), (4, 2)])
+def test_equalizer_matches_reference(ports, layers):
+    """The reference's AVX2 path uses an approximate reciprocal (_mm256_rcp_ps,
+    relative error <= 1.5 * 2^-12): tolerance 1e-3 relative on symbols, 2e-3 on
+    variances (squared reciprocal)."""
+    from oracle import equalizer as E
+
+    rng = np.random.default_rng(ports * 10 + layers)
+    for nre, tx in ((1, 1.0), (37, 0.5), (3276, 1.0)):
+        s, h, nv, _ = E.random_channel(rng, nre, ports, layers)
+        for mmse in (False, True):
+            if not E.is_supported("mmse" if mmse else "zf", ports, layers):
+                continue
+            a, an = oracle.ref_equalize(s, h, nv, tx, layers, mmse)
+            b, bn = E.equalize(s, h, nv, tx, layers)
+            assert np.all(np.abs(a - b) <= 1e-3 * np.abs(b) + 1e-6), (ports, layers, nre)
+            assert np.all(np.abs(an - bn) <= 2e-3 * bn), (ports, layers, nre)
+
+
+def test_equalizer_invalid_noise_matches_reference():
+    from oracle import equalizer as E
+
+    rng = np.random.default_rng(5)
+    s, h, nv, _ = E.random_channel(rng, 100, 4, 1)
+    for bad in ([0.0, 0.01, 0.01, 0.01], [np.inf, 0.01, -1.0, 0.02], [0.0, 0.0, 0.0, 0.0]):
+        nvb = np.array(bad, np.float32)
+        a, an = oracle.ref_equalize(s, h, nvb, 1.0, 1)
+        b, bn = E.equalize(s, h, nvb, 1.0, 1)
+        assert np.all(np.abs(a - b) <= 1e-3 * np.abs(b) + 1e-6)
+        assert np.all((np.isinf(an) & np.isinf(bn)) | (np.abs(an - bn) <= 2e-3 * bn))

@@ -1,12 +1,12 @@
 #!/bin/bash
 # build_variant.sh <name> <sed-expr>... : builds srsran_project_amd with a patched
-# ldpc_decoder.hip into exp/<name>/libsrsran_amd.so (for A/B timing only).
+# csrc/$VFILE (default ldpc_decoder.hip) into exp/<name>/libsrsran_amd.so (for A/B timing only).
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; shift
 W=$(mktemp -d)
 cp -r "$ROOT/srsran_project_amd/csrc" "$W/csrc"
-for e in "$@"; do sed -i "$e" "$W/csrc/ldpc_decoder.hip"; done
+for e in "$@"; do sed -i "$e" "$W/csrc/${VFILE:-ldpc_decoder.hip}"; done
 mkdir -p "$ROOT/exp/$name"
 objs=""
 pids=""

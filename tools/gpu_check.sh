@@ -19,6 +19,7 @@ for s in "$@"; do
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
     codec) step pytest_codec 600 python -m pytest tests/test_ldpc_codec_gpu.py -x -q ;;
     ofdm) step pytest_ofdm 600 python -m pytest tests/test_ofdm_gpu.py -x -q ;;
+    eq) step pytest_eq 600 python -m pytest tests/test_equalizer_gpu.py -x -q ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
     benchq) step bench 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
@@ -28,6 +29,12 @@ for s in "$@"; do
              python3 tools/pmc_summary.py traffic gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/traffic.json ;;
     pmc) step pmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline && \
          step pmc2 600 rocprofv3 --kernel-trace --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE SQ_ACTIVE_INST_SCA -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    obench) step bench_ofdm 600 python bench.py --workload ofdm --steps 10 --warmup 2 ;;
+    oprof) step rocprof_ofdm 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ofdm -o run --output-format csv -- python3 bench.py --workload ofdm --steps 10 --warmup 2 --no-cpu-baseline ;;
+    otraffic) step pmc_fetch_ofdm 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_ofdm -o run --output-format csv -- python3 bench.py --workload ofdm --steps 3 --warmup 1 --no-cpu-baseline && \
+              step pmc_write_ofdm 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write_ofdm -o run --output-format csv -- python3 bench.py --workload ofdm --steps 3 --warmup 1 --no-cpu-baseline && \
+              python3 tools/pmc_summary.py traffic gpurun_out/pmc_fetch_ofdm gpurun_out/pmc_write_ofdm gpurun_out/traffic_ofdm.json ofdm_modulate_kernel ofdm_demodulate_kernel ;;
+    opmc) step pmc_ofdm 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_ofdm -o run --output-format csv -- python3 bench.py --workload ofdm --steps 2 --warmup 1 --no-cpu-baseline ;;
     save) mkdir -p gpurun_out/profiles && \
           python3 tools/pmc_summary.py stats gpurun_out/prof/run_kernel_stats.csv gpurun_out/profiles/kernel_stats.md > /dev/null && \
           cp gpurun_out/prof/run_kernel_stats.csv gpurun_out/profiles/kernel_stats.csv && \
