@@ -39,6 +39,14 @@ def _load_oracle():
     lib.srs_oracle_crc_bits.argtypes = [c_int, P, c_uint]
     lib.srs_oracle_lifting_index.restype = c_int
     lib.srs_oracle_lifting_index.argtypes = [c_int]
+    lib.srs_oracle_polar_code.restype = c_uint
+    lib.srs_oracle_polar_code.argtypes = [c_uint, c_uint, c_uint, P, P, P]
+    lib.srs_oracle_polar_encode_chain.restype = c_int
+    lib.srs_oracle_polar_encode_chain.argtypes = [c_uint, c_uint, c_uint, c_int, P, P]
+    lib.srs_oracle_polar_decode_chain.restype = c_int
+    lib.srs_oracle_polar_decode_chain.argtypes = [c_uint, c_uint, c_uint, c_int, P, P]
+    lib.srs_oracle_polar_interleave.restype = c_int
+    lib.srs_oracle_polar_interleave.argtypes = [P, P, c_uint, c_int]
     lib.srs_oracle_ldpc_rate_match.restype = c_int
     lib.srs_oracle_ldpc_rate_match.argtypes = [c_uint] * 6 + [P, c_uint, P]
     lib.srs_oracle_ldpc_rate_dematch.restype = c_int
@@ -80,6 +88,16 @@ def _load_ref():
     lib.srs_ref_equalize.argtypes = [c_int, c_uint, c_uint, c_uint, P, P, P, ctypes.c_float, P, P]
     lib.srs_ref_equalize_many.restype = ctypes.c_double
     lib.srs_ref_equalize_many.argtypes = [c_uint, c_uint, c_uint, P, P, P, c_uint, c_uint]
+    lib.srs_ref_polar_code.restype = c_uint
+    lib.srs_ref_polar_code.argtypes = [c_uint, c_uint, c_uint, P, P, P]
+    lib.srs_ref_polar_encode_chain.restype = c_int
+    lib.srs_ref_polar_encode_chain.argtypes = [c_uint, c_uint, c_uint, c_int, P, P]
+    lib.srs_ref_polar_decode_chain.restype = c_int
+    lib.srs_ref_polar_decode_chain.argtypes = [c_uint, c_uint, c_uint, c_int, P, P]
+    lib.srs_ref_polar_interleave.restype = c_int
+    lib.srs_ref_polar_interleave.argtypes = [P, P, c_uint, c_int]
+    lib.srs_ref_polar_decode_many.restype = ctypes.c_double
+    lib.srs_ref_polar_decode_many.argtypes = [c_uint, c_uint, c_uint, P, c_uint, c_uint, c_uint]
     lib.srs_ref_ldpc_decode_many.restype = ctypes.c_double
     lib.srs_ref_ldpc_decode_many.argtypes = [ctypes.c_char_p, c_int, c_int, c_int, c_int, P, c_uint, c_uint, c_uint,
                                              c_int, P, P]
@@ -228,3 +246,57 @@ def ref_equalize(symbols_u16, est_u16, noise_vars, tx_scaling, nof_layers, mmse=
                             float(tx_scaling), _ptr(eq), _ptr(nvo)) != 0:
         raise ValueError("reference equalizer does not support %d ports x %d layers" % (P, nof_layers))
     return eq, nvo
+
+
+def _polar_code(lib, K, E, nMax):
+    kmask = np.zeros(1024, np.uint8)
+    pc = np.zeros(8, np.uint16)
+    npc = ctypes.c_uint(0)
+    N = lib(K, E, nMax, _ptr(kmask), _ptr(pc), ctypes.byref(npc))
+    if N == 0:
+        raise ValueError("invalid polar code K=%d E=%d nMax=%d" % (K, E, nMax))
+    return N, kmask[:N].copy(), pc[:npc.value].copy()
+
+
+def polar_code(K, E, nMax):
+    """(N, K_set mask [N], PC set) as polar_code::set builds them."""
+    return _polar_code(ORACLE.srs_oracle_polar_code, K, E, nMax)
+
+
+def ref_polar_code(K, E, nMax):
+    return _polar_code(REF.srs_ref_polar_code, K, E, nMax)
+
+
+def polar_encode_chain(msg_bits, E, nMax, ibil=False, lib=None):
+    msg = np.ascontiguousarray(msg_bits, dtype=np.uint8)
+    out = np.zeros(E, np.uint8)
+    f = ORACLE.srs_oracle_polar_encode_chain if lib is None else lib.srs_ref_polar_encode_chain
+    if f(msg.size, E, nMax, int(ibil), _ptr(msg), _ptr(out)) != 0:
+        raise ValueError("invalid polar code")
+    return out
+
+
+def ref_polar_encode_chain(msg_bits, E, nMax, ibil=False):
+    return polar_encode_chain(msg_bits, E, nMax, ibil, lib=REF)
+
+
+def polar_decode_chain(llrs, K, nMax, ibil=False, lib=None):
+    llrs = np.ascontiguousarray(llrs, dtype=np.int8)
+    msg = np.zeros(K, np.uint8)
+    f = ORACLE.srs_oracle_polar_decode_chain if lib is None else lib.srs_ref_polar_decode_chain
+    if f(K, llrs.size, nMax, int(ibil), _ptr(llrs), _ptr(msg)) != 0:
+        raise ValueError("invalid polar code")
+    return msg
+
+
+def ref_polar_decode_chain(llrs, K, nMax, ibil=False):
+    return polar_decode_chain(llrs, K, nMax, ibil, lib=REF)
+
+
+def polar_interleave(bits, direction=0, lib=None):
+    bits = np.ascontiguousarray(bits, dtype=np.uint8)
+    out = np.zeros_like(bits)
+    f = ORACLE.srs_oracle_polar_interleave if lib is None else lib.srs_ref_polar_interleave
+    if f(_ptr(bits), _ptr(out), bits.size, int(direction)) != 0:
+        raise ValueError("K > 164")
+    return out

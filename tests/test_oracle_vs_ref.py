@@ -221,3 +221,53 @@ def test_equalizer_invalid_noise_matches_reference():
         b, bn = E.equalize(s, h, nvb, 1.0, 1)
         assert np.all(np.abs(a - b) <= 1e-3 * np.abs(b) + 1e-6)
         assert np.all((np.isinf(an) & np.isinf(bn)) | (np.abs(an - bn) <= 2e-3 * bn))
+
+
+# --- polar codes (oracle/srs_oracle_polar.c vs the reference's polar classes) ---
+
+def polar_cases():
+    """(K, E, nMax): DCI sizes (nMax 9, PDCCH aggregation levels 1-16 -> E = 108 * L)
+    and UCI sizes (nMax 10, with and without parity-check bits), covering
+    repetition (E >= N), puncturing and shortening."""
+    cases = []
+    for K in (36, 41, 57, 80, 100, 140, 164):
+        for L in (1, 2, 4, 8, 16):
+            if 108 * L > K:
+                cases.append((K, 108 * L, 9))
+    for K in (18, 19, 22, 25, 31, 40, 64, 130, 300, 500, 1000):
+        for E in (K + 7, int(K * 1.7), 2 * K + 60, K + 220, 1200, 3000, 8192):
+            if K + (3 if K <= 25 else 0) < E <= 8192:
+                cases.append((K, E, 10))
+    return sorted(set(cases))
+
+
+def test_polar_code_construction_matches_reference():
+    for K, E, nMax in polar_cases():
+        try:
+            want = oracle.ref_polar_code(K, E, nMax)
+        except Exception:
+            continue
+        got = oracle.polar_code(K, E, nMax)
+        assert got[0] == want[0] and np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2]), (K, E)
+
+
+def test_polar_chains_match_reference():
+    rng = np.random.default_rng(33)
+    for K, E, nMax in polar_cases():
+        for ibil in (False, True):
+            m = rng.integers(0, 2, K).astype(np.uint8)
+            cw = oracle.polar_encode_chain(m, E, nMax, ibil)
+            np.testing.assert_array_equal(cw, oracle.ref_polar_encode_chain(m, E, nMax, ibil), err_msg=str((K, E)))
+            llr = np.clip(np.round((1 - 2.0 * cw) * 5 + rng.normal(0, 7, E)), -120, 120).astype(np.int8)
+            llr[rng.random(E) < 0.03] = 127
+            llr[rng.random(E) < 0.03] = -127
+            np.testing.assert_array_equal(oracle.polar_decode_chain(llr, K, nMax, ibil),
+                                          oracle.ref_polar_decode_chain(llr, K, nMax, ibil), err_msg=str((K, E)))
+
+
+def test_polar_interleaver_matches_reference():
+    rng = np.random.default_rng(2)
+    for K in (1, 12, 40, 100, 164):
+        b = rng.integers(0, 2, K).astype(np.uint8)
+        for d in (0, 1):
+            np.testing.assert_array_equal(oracle.polar_interleave(b, d), oracle.polar_interleave(b, d, lib=oracle.REF))
