@@ -47,4 +47,12 @@ from .equalizer import (  # noqa: F401
     create_channel_equalizer_generic_factory_hip,
 )
 
+from .polar import (  # noqa: F401
+    PolarCode,
+    PolarCodeIbil,
+    PolarInterleaverDirection,
+    polar_code_construct,
+    polar_interleave,
+)
+
 __version__ = "0.1.0"

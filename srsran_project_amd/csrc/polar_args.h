@@ -1,0 +1,34 @@
+// polar_args.h -- argument block of the polar kernels (polar.hip), shared with
+// their C-ABI (polar_api.cpp).  Tables are device copies of polar_code_desc.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "polar_code.h"
+
+namespace srs_amd {
+
+struct polar_args {
+  // codewords
+  const uint8_t*  msgs;   // encode input / decode output: [nof][msg_stride], one bit per byte
+  uint8_t*        cws;    // encode output: [nof][cw_stride], one bit per byte
+  const int8_t*   llrs;   // decode input: [nof][llr_stride]
+  uint8_t*        msgs_out;
+  uint32_t        msg_stride, cw_stride, llr_stride, nof;
+  // code
+  uint32_t        K, E, N, nPC, mode, prog_len;
+  uint32_t        pc_set[4];
+  const uint8_t*  kset;    // [N]
+  const uint16_t* msg_pos; // [K]
+  const uint16_t* tx_map;  // [E]
+  const uint16_t* rx_e2f;  // [E]
+  const uint16_t* blk;     // [N]
+  const uint32_t* program; // [prog_len]
+};
+
+hipError_t launch_polar_encode(const polar_args& a, hipStream_t stream);
+hipError_t launch_polar_decode(const polar_args& a, hipStream_t stream);
+
+} // namespace srs_amd

@@ -6,6 +6,7 @@ import glob
 import os
 import re
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -67,3 +68,36 @@ def test_invalid_decoder_type():
 
     with pytest.raises(ValueError):
         amd.create_ldpc_decoder_factory_hip("neon")
+
+
+def test_polar_construction_host_only():
+    """The product's polar_code::set restatement equals the oracle (which is
+    pinned to the reference) -- host-only entry point, no device needed."""
+    import oracle
+    import srsran_project_amd as amd
+    from tests.test_oracle_vs_ref import polar_cases
+
+    for K, E, nMax in polar_cases():
+        try:
+            want = oracle.polar_code(K, E, nMax)
+        except ValueError:
+            with pytest.raises(ValueError):
+                amd.polar_code_construct(K, E, nMax)
+            continue
+        got = amd.polar_code_construct(K, E, nMax)
+        assert got[0] == want[0]
+        np.testing.assert_array_equal(got[1], want[1])
+        np.testing.assert_array_equal(got[2], want[2])
+
+
+def test_polar_interleaver_host_only():
+    import oracle
+    import srsran_project_amd as amd
+
+    rng = np.random.default_rng(4)
+    for K in (1, 20, 164):
+        b = rng.integers(0, 2, K).astype(np.uint8)
+        for d in (0, 1):
+            np.testing.assert_array_equal(amd.polar_interleave(b, d), oracle.polar_interleave(b, d))
+    with pytest.raises(ValueError):
+        amd.polar_interleave(np.zeros(165, np.uint8))
