@@ -41,6 +41,11 @@ for s in "$@"; do
           cp gpurun_out/prof/run_kernel_stats.csv gpurun_out/profiles/kernel_stats.csv && \
           cp gpurun_out/traffic.json gpurun_out/profiles/traffic.json && \
           tail -1 gpurun_out/bench.log > gpurun_out/profiles/bench.json ;;
+    osave) mkdir -p gpurun_out/profiles && \
+          python3 tools/pmc_summary.py stats gpurun_out/prof_ofdm/run_kernel_stats.csv gpurun_out/profiles/ofdm_kernel_stats.md > /dev/null && \
+          cp gpurun_out/prof_ofdm/run_kernel_stats.csv gpurun_out/profiles/ofdm_kernel_stats.csv && \
+          cp gpurun_out/traffic_ofdm.json gpurun_out/profiles/ofdm_traffic.json && \
+          tail -1 gpurun_out/bench_ofdm.log > gpurun_out/profiles/ofdm_bench.json ;;
     *) echo "unknown step $s" ;;
   esac
 done
