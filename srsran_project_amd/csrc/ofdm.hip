@@ -24,6 +24,11 @@ namespace srs_amd {
 
 using dft::cf;
 
+#ifndef OFDM_NONTEMPORAL_DEFAULT
+#define OFDM_NONTEMPORAL_DEFAULT 1
+#endif
+constexpr bool OFDM_NONTEMPORAL = OFDM_NONTEMPORAL_DEFAULT;
+
 namespace {
 
 __device__ __forceinline__ cf from_cbf16(uint32_t u)
@@ -37,6 +42,44 @@ __device__ __forceinline__ uint32_t bf16_bits(float f)
   uint32_t u = __float_as_uint(f);
   u += 0x7fffu + ((u >> 16) & 1u);
   return u >> 16;
+}
+
+// Streaming (non-temporal) stores for the outputs and loads for the
+// demodulator's baseband input: every sample is touched exactly once, so
+// keeping it out of the caches measured +40 % (modulator) / +5 % (demodulator);
+// non-temporal grid loads in the modulator measured slower and are not used.
+template <class T>
+__device__ __forceinline__ void stream_store(T* p, T v)
+{
+  if constexpr (OFDM_NONTEMPORAL) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
+}
+
+__device__ __forceinline__ void stream_store(cf* p, cf v)
+{
+  stream_store(reinterpret_cast<float*>(p), v.x);
+  stream_store(reinterpret_cast<float*>(p) + 1, v.y);
+}
+
+#ifndef OFDM_NT_LOADS
+#define OFDM_NT_LOADS 1
+#endif
+template <class T>
+__device__ __forceinline__ T stream_load(const T* p)
+{
+  if constexpr (OFDM_NT_LOADS) {
+    return __builtin_nontemporal_load(p);
+  } else {
+    return *p;
+  }
+}
+
+__device__ __forceinline__ cf stream_load(const cf* p)
+{
+  return {stream_load(reinterpret_cast<const float*>(p)), stream_load(reinterpret_cast<const float*>(p) + 1)};
 }
 
 __device__ __forceinline__ uint32_t to_cbf16(cf v)
@@ -69,9 +112,9 @@ __global__ __launch_bounds__(dft::plan<N>::T) void ofdm_modulate_kernel(ofdm_arg
   };
   auto store = [&](int n, cf v) {
     v          = dft::cmul(v, coef);
-    out[cp + n] = v;
+    stream_store(out + cp + n, v);
     if (n >= N - cp) {
-      out[n - (N - cp)] = v;
+      stream_store(out + n - (N - cp), v);
     }
   };
   dft::plan<N>::template engine<+1>::run(lds, reinterpret_cast<const cf*>(a.twiddles), load, store);
@@ -92,7 +135,7 @@ __global__ __launch_bounds__(dft::plan<N>::T) void ofdm_demodulate_kernel(ofdm_a
   const cf        coef = {si.coef_re, si.coef_im};
   const cf*       win  = reinterpret_cast<const cf*>(a.window);
 
-  auto load  = [&](int i) -> cf { return in[i]; };
+  auto load  = [&](int i) -> cf { return stream_load(in + i); };
   auto store = [&](int k, cf v) {
     if (k >= half && k < N - half) {
       return; // guard band
@@ -101,7 +144,7 @@ __global__ __launch_bounds__(dft::plan<N>::T) void ofdm_demodulate_kernel(ofdm_a
     if (win != nullptr) {
       v = dft::cmul(v, win[k]);
     }
-    grid[k < half ? k + half : k - (N - half)] = to_cbf16(v);
+    stream_store(grid + (k < half ? k + half : k - (N - half)), to_cbf16(v));
   };
   dft::plan<N>::template engine<-1>::run(lds, reinterpret_cast<const cf*>(a.twiddles), load, store);
 }
