@@ -47,6 +47,12 @@ def _load_oracle():
     lib.srs_oracle_polar_decode_chain.argtypes = [c_uint, c_uint, c_uint, c_int, P, P]
     lib.srs_oracle_polar_interleave.restype = c_int
     lib.srs_oracle_polar_interleave.argtypes = [P, P, c_uint, c_int]
+    lib.srs_oracle_demodulate.restype = c_int
+    lib.srs_oracle_demodulate.argtypes = [c_int, P, P, c_uint, P]
+    lib.srs_oracle_modulate.restype = c_int
+    lib.srs_oracle_modulate.argtypes = [c_int, P, c_uint, P]
+    lib.srs_oracle_prbs.restype = c_int
+    lib.srs_oracle_prbs.argtypes = [ctypes.c_uint32, c_uint, P]
     lib.srs_oracle_ldpc_rate_match.restype = c_int
     lib.srs_oracle_ldpc_rate_match.argtypes = [c_uint] * 6 + [P, c_uint, P]
     lib.srs_oracle_ldpc_rate_dematch.restype = c_int
@@ -98,6 +104,16 @@ def _load_ref():
     lib.srs_ref_polar_interleave.argtypes = [P, P, c_uint, c_int]
     lib.srs_ref_polar_decode_many.restype = ctypes.c_double
     lib.srs_ref_polar_decode_many.argtypes = [c_uint, c_uint, c_uint, P, c_uint, c_uint, c_uint]
+    lib.srs_ref_modulate.restype = c_int
+    lib.srs_ref_modulate.argtypes = [c_int, P, c_uint, P]
+    lib.srs_ref_demodulate.restype = c_int
+    lib.srs_ref_demodulate.argtypes = [c_int, P, P, c_uint, P]
+    lib.srs_ref_prbs.restype = c_int
+    lib.srs_ref_prbs.argtypes = [ctypes.c_uint32, c_uint, P]
+    lib.srs_ref_descramble_llrs.restype = c_int
+    lib.srs_ref_descramble_llrs.argtypes = [ctypes.c_uint32, c_uint, P, P]
+    lib.srs_ref_scramble_bits.restype = c_int
+    lib.srs_ref_scramble_bits.argtypes = [ctypes.c_uint32, c_uint, P, P]
     lib.srs_ref_ldpc_decode_many.restype = ctypes.c_double
     lib.srs_ref_ldpc_decode_many.argtypes = [ctypes.c_char_p, c_int, c_int, c_int, c_int, P, c_uint, c_uint, c_uint,
                                              c_int, P, P]
@@ -300,3 +316,51 @@ def polar_interleave(bits, direction=0, lib=None):
     if f(_ptr(bits), _ptr(out), bits.size, int(direction)) != 0:
         raise ValueError("K > 164")
     return out
+
+
+QM_CODE = {"pi/2-BPSK": 0, "BPSK": 1, "QPSK": 2, "QAM16": 4, "QAM64": 6, "QAM256": 8}
+
+
+def _bits_per_symbol(qm):
+    return 1 if qm in (0, 1) else qm
+
+
+def demodulate(symbols, noise_vars, qm, lib=None):
+    """Soft demapping: complex64 symbols, float32 noise variances -> int8 LLRs."""
+    sym = np.ascontiguousarray(symbols, dtype=np.complex64)
+    nv = np.ascontiguousarray(noise_vars, dtype=np.float32)
+    out = np.zeros(sym.size * _bits_per_symbol(qm), np.int8)
+    f = ORACLE.srs_oracle_demodulate if lib is None else lib.srs_ref_demodulate
+    if f(qm, _ptr(sym), _ptr(nv), sym.size, _ptr(out)) != 0:
+        raise ValueError("invalid modulation")
+    return out
+
+
+def ref_demodulate(symbols, noise_vars, qm):
+    return demodulate(symbols, noise_vars, qm, lib=REF)
+
+
+def modulate(bits_packed, nsym, qm, lib=None):
+    b = np.ascontiguousarray(bits_packed, dtype=np.uint8)
+    out = np.zeros(nsym, np.complex64)
+    f = ORACLE.srs_oracle_modulate if lib is None else lib.srs_ref_modulate
+    if f(qm, _ptr(b), nsym, _ptr(out)) != 0:
+        raise ValueError("invalid modulation")
+    return out
+
+
+def ref_modulate(bits_packed, nsym, qm):
+    return modulate(bits_packed, nsym, qm, lib=REF)
+
+
+def prbs(c_init, length, lib=None):
+    """Gold sequence c(0..length-1), one bit per byte."""
+    out = np.zeros(length, np.uint8)
+    f = ORACLE.srs_oracle_prbs if lib is None else lib.srs_ref_prbs
+    if f(c_init, length, _ptr(out)) != 0:
+        raise ValueError("sequence too long")
+    return out
+
+
+def ref_prbs(c_init, length):
+    return prbs(c_init, length, lib=REF)
