@@ -55,4 +55,6 @@ from .polar import (  # noqa: F401
     polar_interleave,
 )
 
+from .modulation import MODULATION, Modulator  # noqa: F401
+
 __version__ = "0.1.0"
