@@ -20,6 +20,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 /* ---------------------------------------------------------------- tables */
@@ -265,10 +266,14 @@ int srs_oracle_modulate(int Qm, const uint8_t* bits, unsigned nsym, float* out)
 int srs_oracle_prbs(uint32_t c_init, unsigned len, uint8_t* c)
 {
   enum { NC = 1600 };
-  static uint8_t x1[NC + 200000 + 31], x2[NC + 200000 + 31];
-  if (len > 200000) return -1;
-  memset(x1, 0, sizeof(x1));
-  memset(x2, 0, sizeof(x2));
+  if (len > (1u << 24)) return -1;
+  uint8_t* x1 = (uint8_t*)calloc(NC + len + 31, 1);
+  uint8_t* x2 = (uint8_t*)calloc(NC + len + 31, 1);
+  if (!x1 || !x2) {
+    free(x1);
+    free(x2);
+    return -1;
+  }
   x1[0] = 1;
   for (int i = 0; i < 31; ++i) x2[i] = (c_init >> i) & 1;
   for (unsigned n = 0; n + 31 < NC + len; ++n) {
@@ -276,5 +281,7 @@ int srs_oracle_prbs(uint32_t c_init, unsigned len, uint8_t* c)
     x2[n + 31] = x2[n + 3] ^ x2[n + 2] ^ x2[n + 1] ^ x2[n];
   }
   for (unsigned n = 0; n < len; ++n) c[n] = x1[n + NC] ^ x2[n + NC];
+  free(x1);
+  free(x2);
   return 0;
 }
