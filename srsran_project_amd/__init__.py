@@ -57,4 +57,6 @@ from .polar import (  # noqa: F401
 
 from .modulation import MODULATION, Modulator  # noqa: F401
 
+from .crc import CrcCalculator, create_crc_calculator_factory_hip  # noqa: F401
+
 __version__ = "0.1.0"

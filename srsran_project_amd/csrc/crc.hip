@@ -1,0 +1,105 @@
+// crc.hip -- CRC calculation / attachment over rows of packed bits (MI355X).
+//
+// The reference computes crc_calculator::calculate (crc_calculator.h:81) by
+// bitwise or byte-table long division of the whole message, one bit after the
+// other (crc_calculator_generic_impl.cpp:98-127).  The CRC is linear, so the
+// GPU splits each row into one contiguous chunk per thread:
+//   1. thread t divides its own chunk:   R_t = chunk_t(x) mod g  (shift register)
+//   2. and moves it to the row's end:     R_t(x) * x^(n - e_t + L) mod g
+//      = XOR over set bits j of R_t of table[j + n - e_t]   (table[k] = x^(k+L) mod g)
+//   3. the block XOR-reduces the contributions (wave shuffles + LDS).
+// One workgroup per row; the chunk loop reads whole bytes, so a row costs one
+// pass over its ceil(n/8) bytes plus <= L table reads per thread.
+#include <hip/hip_runtime.h>
+
+#include "crc_args.h"
+
+namespace srs_amd {
+
+namespace {
+
+constexpr int CRC_THREADS = 256;
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v)
+{
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    v ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), o, 64));
+  }
+  return v;
+}
+
+__device__ uint32_t row_crc(const crc_args& a, const uint8_t* row)
+{
+  __shared__ uint32_t partial[CRC_THREADS / 64];
+  const uint32_t      n       = a.nof_bits;
+  const uint32_t      L       = a.order;
+  const uint32_t      highbit = 1u << L;
+  // Chunk of whole bytes per thread.
+  const uint32_t nbytes = (n + 7) / 8;
+  const uint32_t per    = (nbytes + CRC_THREADS - 1) / CRC_THREADS;
+  const uint32_t b0     = threadIdx.x * per;
+  const uint32_t b1     = min(nbytes, b0 + per);
+  uint32_t       contrib = 0;
+  if (b0 < b1) {
+    uint32_t r = 0;
+    for (uint32_t b = b0; b < b1; ++b) {
+      const uint32_t byte  = row[b];
+      const int      nb    = (b * 8 + 8 <= n) ? 8 : static_cast<int>(n - b * 8);
+      for (int i = 0; i < nb; ++i) {
+        r = (r << 1) | ((byte >> (7 - i)) & 1u);
+        if (r & highbit) {
+          r ^= a.polynom;
+        }
+      }
+    }
+    const uint32_t e = min(n, b1 * 8); // chunk end (exclusive, bits)
+    for (uint32_t j = 0; j < L; ++j) {
+      if ((r >> j) & 1u) {
+        contrib ^= a.table[j + n - e];
+      }
+    }
+  }
+  contrib = wave_xor(contrib);
+  if ((threadIdx.x & 63) == 0) {
+    partial[threadIdx.x >> 6] = contrib;
+  }
+  __syncthreads();
+  uint32_t crc = 0;
+#pragma unroll
+  for (int w = 0; w < CRC_THREADS / 64; ++w) {
+    crc ^= partial[w];
+  }
+  return crc;
+}
+
+__global__ void __launch_bounds__(CRC_THREADS) crc_kernel(crc_args a)
+{
+  uint8_t*       row = a.bits + static_cast<size_t>(blockIdx.x) * a.stride;
+  const uint32_t crc = row_crc(a, row);
+  if (threadIdx.x != 0) {
+    return;
+  }
+  if (a.checksums != nullptr) {
+    a.checksums[blockIdx.x] = crc;
+  }
+  if (a.attach) {
+    // CRC bits MSB-first into bits [n, n + L); other bits of the touched bytes kept.
+    for (uint32_t k = 0; k < a.order; ++k) {
+      const uint32_t pos  = a.nof_bits + k;
+      const uint32_t bit  = (crc >> (a.order - 1 - k)) & 1u;
+      const uint8_t  mask = static_cast<uint8_t>(0x80u >> (pos & 7));
+      row[pos >> 3]       = static_cast<uint8_t>((row[pos >> 3] & ~mask) | (bit ? mask : 0));
+    }
+  }
+}
+
+} // namespace
+
+hipError_t launch_crc(const crc_args& a, uint32_t nof_rows, hipStream_t stream)
+{
+  hipLaunchKernelGGL(crc_kernel, dim3(nof_rows), dim3(CRC_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+} // namespace srs_amd

@@ -1,0 +1,24 @@
+// crc_args.h -- argument block of the CRC kernel (crc.hip), shared with its
+// C-ABI (crc_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace srs_amd {
+
+struct crc_args {
+  uint8_t*        bits;      // rows of stride bytes, packed MSB-first
+  uint32_t*       checksums; // per row (may be null when attaching)
+  const uint32_t* table;     // x^(k+L) mod g, k < nof_bits + L
+  uint32_t        stride;
+  uint32_t        nof_bits;
+  uint32_t        polynom;   // including the x^L term
+  uint32_t        order;     // L
+  int32_t         attach;
+};
+
+hipError_t launch_crc(const crc_args& a, uint32_t nof_rows, hipStream_t stream);
+
+} // namespace srs_amd

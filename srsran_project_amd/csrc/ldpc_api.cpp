@@ -29,32 +29,6 @@ namespace {
 constexpr int      MAX_CRC_BITS_LEN = 22 * MAX_LIFTING_SIZE;
 constexpr uint32_t DEFAULT_SLOTS    = 1u << 20;
 
-// x^(k+L) mod g for k = 0..MAX_CRC_BITS_LEN-1: the CRC of a single 1 bit
-// followed by k zeros (crc_calculator_generic_impl.cpp:98 long division).
-std::vector<uint32_t> crc_linear_table(int poly)
-{
-  uint32_t polynom = 0;
-  int      order   = 0;
-  crc_params(poly, polynom, order);
-  std::vector<uint32_t> t(MAX_CRC_BITS_LEN);
-  uint64_t              highbit = 1ull << order;
-  uint64_t              r       = 1;
-  for (int i = 0; i < order; ++i) {
-    r <<= 1;
-    if (r & highbit) {
-      r ^= polynom;
-    }
-  }
-  for (int k = 0; k < MAX_CRC_BITS_LEN; ++k) {
-    t[k] = static_cast<uint32_t>(r & (highbit - 1));
-    r <<= 1;
-    if (r & highbit) {
-      r ^= polynom;
-    }
-  }
-  return t;
-}
-
 } // namespace
 
 
@@ -168,7 +142,7 @@ int srs_amd_ldpc_decoder_create(srs_amd_ldpc_decoder** decoder, int arith, int f
   std::vector<uint32_t> tables;
   tables.reserve(6 * MAX_CRC_BITS_LEN);
   for (int p = 0; p < 6; ++p) {
-    auto t = crc_linear_table(p);
+    auto t = crc_linear_table(p, MAX_CRC_BITS_LEN);
     tables.insert(tables.end(), t.begin(), t.end());
   }
   e = hipMalloc(&d->crc_tables, tables.size() * sizeof(uint32_t));

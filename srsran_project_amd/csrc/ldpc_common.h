@@ -87,4 +87,9 @@ int lifting_index(int Z);
 // CRC polynomials of crc_calculator_generic_impl.cpp:27-52, by crc_generator_poly value.
 bool crc_params(int poly, uint32_t& polynom, int& order);
 
+// x^(k+L) mod g for k = 0..nbits-1: the CRC of a single 1 bit followed by k
+// zeros (crc_calculator_generic_impl.cpp:116 long division), so the CRC of an
+// n-bit message is the XOR of table[n-1-i] over its set bits i.
+std::vector<uint32_t> crc_linear_table(int poly, int nbits);
+
 } // namespace srs_amd

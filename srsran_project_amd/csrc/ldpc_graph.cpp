@@ -95,6 +95,30 @@ std::vector<uint32_t> all_lifted_edges()
   return edges;
 }
 
+std::vector<uint32_t> crc_linear_table(int poly, int nbits)
+{
+  uint32_t polynom = 0;
+  int      order   = 0;
+  crc_params(poly, polynom, order);
+  std::vector<uint32_t> t(nbits);
+  const uint64_t        highbit = 1ull << order;
+  uint64_t              r       = 1;
+  for (int i = 0; i < order; ++i) {
+    r <<= 1;
+    if (r & highbit) {
+      r ^= polynom;
+    }
+  }
+  for (int k = 0; k < nbits; ++k) {
+    t[k] = static_cast<uint32_t>(r & (highbit - 1));
+    r <<= 1;
+    if (r & highbit) {
+      r ^= polynom;
+    }
+  }
+  return t;
+}
+
 bool crc_params(int poly, uint32_t& polynom, int& order)
 {
   switch (poly) {
