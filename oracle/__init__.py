@@ -114,6 +114,14 @@ def _load_ref():
     lib.srs_ref_descramble_llrs.argtypes = [ctypes.c_uint32, c_uint, P, P]
     lib.srs_ref_scramble_bits.restype = c_int
     lib.srs_ref_scramble_bits.argtypes = [ctypes.c_uint32, c_uint, P, P]
+    lib.srs_ref_pdsch_encode.restype = c_int
+    lib.srs_ref_pdsch_encode.argtypes = [P, c_uint] + [c_uint] * 6 + [P]
+    lib.srs_ref_rx_buffer_create.restype = ctypes.c_void_p
+    lib.srs_ref_rx_buffer_create.argtypes = [c_uint]
+    lib.srs_ref_rx_buffer_destroy.restype = None
+    lib.srs_ref_rx_buffer_destroy.argtypes = [ctypes.c_void_p]
+    lib.srs_ref_pusch_decode.restype = c_int
+    lib.srs_ref_pusch_decode.argtypes = [ctypes.c_void_p, P, c_uint, P, c_uint] + [c_uint] * 6 + [c_int] * 4 + [P]
     lib.srs_ref_ldpc_decode_many.restype = ctypes.c_double
     lib.srs_ref_ldpc_decode_many.argtypes = [ctypes.c_char_p, c_int, c_int, c_int, c_int, P, c_uint, c_uint, c_uint,
                                              c_int, P, P]
@@ -364,3 +372,37 @@ def prbs(c_init, length, lib=None):
 
 def ref_prbs(c_init, length):
     return prbs(c_init, length, lib=REF)
+
+
+def ref_pdsch_encode(tb_bytes, p):
+    """Reference pdsch_encoder_impl::encode; p: an oracle.sch.plan() dict. Codeword bits, one per byte."""
+    tb = np.ascontiguousarray(tb_bytes, dtype=np.uint8)
+    cw = np.zeros(p["cw_length"], np.uint8)
+    REF.srs_ref_pdsch_encode(_ptr(tb), tb.size, p["base_graph"], p["rv"], p["modulation_order"], p["Nref"],
+                             p["nof_layers"], p["nof_ch_symbols"], _ptr(cw))
+    return cw
+
+
+class RefRxBuffer:
+    """HARQ soft buffer of the reference PUSCH decoder."""
+
+    def __init__(self, nof_cbs):
+        self.h = REF.srs_ref_rx_buffer_create(nof_cbs)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            REF.srs_ref_rx_buffer_destroy(self.h)
+            self.h = None
+
+
+def ref_pusch_decode(llrs, p, rxbuf, tb_out, max_iterations=6, generic=False, use_early_stop=True,
+                     force_decoding=False, new_data=True):
+    """Reference pusch_decoder_impl. Returns (tb_crc_ok, nof_cbs, nof_obs, iteration sum, min, max)."""
+    llrs = np.ascontiguousarray(llrs, dtype=np.int8)
+    res = np.zeros(6, np.float64)
+    r = REF.srs_ref_pusch_decode(rxbuf.h, _ptr(llrs), llrs.size, _ptr(tb_out), tb_out.size, p["base_graph"], p["rv"],
+                                 p["modulation_order"], p["Nref"], p["nof_layers"], max_iterations,
+                                 int(force_decoding), int(use_early_stop), int(new_data), int(generic), _ptr(res))
+    if r != 0:
+        raise RuntimeError("reference PUSCH decoder did not notify")
+    return bool(res[0]), int(res[1]), int(res[2]), int(round(res[3])), int(res[4]), int(res[5])

@@ -59,4 +59,17 @@ from .modulation import MODULATION, Modulator  # noqa: F401
 
 from .crc import CrcCalculator, create_crc_calculator_factory_hip  # noqa: F401
 
+
+
+from .sch import (  # noqa: F401
+    PdschEncoder,
+    PuschDecoder,
+    PuschDecoderConfig,
+    PuschDecoderResult,
+    SchPlan,
+    sch_plan,
+    sch_segments,
+    soft_buffer_size,
+    tbs_calculator_calculate,
+)
 __version__ = "0.1.0"

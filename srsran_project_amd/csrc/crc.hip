@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "crc_args.h"
+#include "crc_device.h"
 
 namespace srs_amd {
 
@@ -20,63 +21,11 @@ namespace {
 
 constexpr int CRC_THREADS = 256;
 
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v)
-{
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    v ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), o, 64));
-  }
-  return v;
-}
-
-__device__ uint32_t row_crc(const crc_args& a, const uint8_t* row)
-{
-  __shared__ uint32_t partial[CRC_THREADS / 64];
-  const uint32_t      n       = a.nof_bits;
-  const uint32_t      L       = a.order;
-  const uint32_t      highbit = 1u << L;
-  // Chunk of whole bytes per thread.
-  const uint32_t nbytes = (n + 7) / 8;
-  const uint32_t per    = (nbytes + CRC_THREADS - 1) / CRC_THREADS;
-  const uint32_t b0     = threadIdx.x * per;
-  const uint32_t b1     = min(nbytes, b0 + per);
-  uint32_t       contrib = 0;
-  if (b0 < b1) {
-    uint32_t r = 0;
-    for (uint32_t b = b0; b < b1; ++b) {
-      const uint32_t byte  = row[b];
-      const int      nb    = (b * 8 + 8 <= n) ? 8 : static_cast<int>(n - b * 8);
-      for (int i = 0; i < nb; ++i) {
-        r = (r << 1) | ((byte >> (7 - i)) & 1u);
-        if (r & highbit) {
-          r ^= a.polynom;
-        }
-      }
-    }
-    const uint32_t e = min(n, b1 * 8); // chunk end (exclusive, bits)
-    for (uint32_t j = 0; j < L; ++j) {
-      if ((r >> j) & 1u) {
-        contrib ^= a.table[j + n - e];
-      }
-    }
-  }
-  contrib = wave_xor(contrib);
-  if ((threadIdx.x & 63) == 0) {
-    partial[threadIdx.x >> 6] = contrib;
-  }
-  __syncthreads();
-  uint32_t crc = 0;
-#pragma unroll
-  for (int w = 0; w < CRC_THREADS / 64; ++w) {
-    crc ^= partial[w];
-  }
-  return crc;
-}
-
 __global__ void __launch_bounds__(CRC_THREADS) crc_kernel(crc_args a)
 {
-  uint8_t*       row = a.bits + static_cast<size_t>(blockIdx.x) * a.stride;
-  const uint32_t crc = row_crc(a, row);
+  __shared__ uint32_t partial[CRC_THREADS / 64];
+  uint8_t*            row = a.bits + static_cast<size_t>(blockIdx.x) * a.stride;
+  const uint32_t      crc = block_row_crc<CRC_THREADS>(row, a.nof_bits, a.order, a.polynom, a.table, partial);
   if (threadIdx.x != 0) {
     return;
   }

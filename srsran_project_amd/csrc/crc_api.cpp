@@ -8,6 +8,7 @@
 
 #include "api_common.h"
 #include "crc_args.h"
+#include "crc_internal.h"
 #include "ldpc_common.h"
 #include <mutex>
 #include <vector>
@@ -215,3 +216,8 @@ int srs_amd_crc_calculate(srs_amd_crc_calculator* crc, uint32_t* checksum, const
 }
 
 } // extern "C"
+
+const uint32_t* srs_amd::crc_device_table(const srs_amd_crc_calculator* crc)
+{
+  return crc ? crc->d_table : nullptr;
+}

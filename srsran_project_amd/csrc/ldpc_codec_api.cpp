@@ -13,6 +13,7 @@
 #include "api_common.h"
 #include "ldpc_common.h"
 #include "ldpc_codec_args.h"
+#include "ldpc_codec_internal.h"
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -478,6 +479,24 @@ int srs_amd_ldpc_rate_dematch_batch(srs_amd_ldpc_rate_dematcher*      dm,
                                     uint32_t                          nof_cbs,
                                     void*                             stream)
 {
+  return srs_amd::rate_dematch_batch_ex(
+      dm, cfg, new_data, d_input, d_in_offsets, d_rm_lengths, d_soft, soft_stride, nof_cbs, stream, false);
+}
+
+} // extern "C"
+
+int srs_amd::rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
+                                   const srs_amd_codeblock_metadata* cfg,
+                                   int                               new_data,
+                                   const int8_t*                     d_input,
+                                   const uint32_t*                   d_in_offsets,
+                                   const uint32_t*                   d_rm_lengths,
+                                   int8_t*                           d_soft,
+                                   uint32_t                          soft_stride,
+                                   uint32_t                          nof_cbs,
+                                   void*                             stream,
+                                   bool                              fresh)
+{
   if (dm == nullptr) {
     return fail(SRS_AMD_EINVAL, "null rate dematcher");
   }
@@ -502,6 +521,7 @@ int srs_amd_ldpc_rate_dematch_batch(srs_amd_ldpc_rate_dematcher*      dm,
   a.soft_stride = soft_stride;
   a.nof_cbs     = nof_cbs;
   a.new_data    = new_data ? 1 : 0;
+  a.fresh       = (fresh && new_data) ? 1 : 0;
   std::lock_guard<std::mutex> lock(dm->mtx);
   hipError_t                  e = hipSetDevice(dm->device);
   if (e == hipSuccess) {
@@ -509,6 +529,8 @@ int srs_amd_ldpc_rate_dematch_batch(srs_amd_ldpc_rate_dematcher*      dm,
   }
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_rate_dematch_kernel launch");
 }
+
+extern "C" {
 
 int srs_amd_ldpc_rate_dematch(srs_amd_ldpc_rate_dematcher*      dm,
                               int8_t*                           output,

@@ -35,6 +35,7 @@ struct dematch_args {
   uint32_t        soft_stride;
   uint32_t        nof_cbs;
   int32_t         new_data;
+  int32_t         fresh;    // previous soft-buffer contents are known to be zero (not read)
   rm_geometry     g;
 };
 

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
         if (p >= g.N) {
           break;
         }
-        int v = buf[p];
+        int v = a.fresh ? 0 : buf[p];
         if (p < zero_end) {
           v = 0;
         }

@@ -1,0 +1,365 @@
+// pusch_api.cpp -- C-ABI of the MI355X PUSCH decoder (include/srsran_amd/sch.h),
+// pusch_decoder_impl (lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.cpp)
+// for a batch of transport blocks:
+//   1. rate dematching + HARQ combining    srs_amd_ldpc_rate_dematch_batch into the soft buffers
+//   2. LDPC decoding, CB CRC early stop    srs_amd_ldpc_decode_batch
+//      (without early stop: decode, then a CRC of the K - F message bits,
+//       pusch_codeblock_decoder.cpp:75-86)
+//   3. CB status, statistics, concatenation and TB CRC24A   assemble_kernel (sch.hip)
+// Soft buffer of one TB: C rows of soft_row_layout::row_bytes:
+//   [N_short*Z soft LLRs | ceil(K/8) message bytes | int32 CB CRC flag]
+// (the codeblock soft bits, data bits and CRC flags of the reference's rx_buffer).
+#include "srsran_amd/crc.h"
+#include "srsran_amd/ldpc.h"
+#include "srsran_amd/ldpc_rate_matching.h"
+#include "srsran_amd/sch.h"
+
+#include <hip/hip_runtime.h>
+
+#include "api_common.h"
+#include "crc_internal.h"
+#include "device_buffer.h"
+#include "ldpc_codec_internal.h"
+#include "sch_args.h"
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+using namespace srs_amd;
+
+struct srs_amd_pusch_decoder {
+  int                          device = 0;
+  int                          arith  = 0;
+  hipStream_t                  stream = nullptr;
+  srs_amd_crc_calculator*      crc[3] = {nullptr, nullptr, nullptr}; // CRC16, CRC24A, CRC24B
+  srs_amd_ldpc_rate_dematcher* dm     = nullptr;
+  srs_amd_ldpc_decoder*        dec[2] = {nullptr, nullptr}; // force_decoding 0 / 1
+  device_buffer                soft, msgs, iters, checks, arrays, results, host_io;
+  std::vector<uint32_t>        h_arrays;
+  srs_amd_sch_plan             key_plan{};
+  uint32_t                     key_tbs = 0, key_stride = 0;
+  std::mutex                   mtx;
+  ~srs_amd_pusch_decoder()
+  {
+    (void)hipSetDevice(device);
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+    for (auto* c : crc) {
+      srs_amd_crc_calculator_destroy(c);
+    }
+    srs_amd_ldpc_rate_dematcher_destroy(dm);
+    srs_amd_ldpc_decoder_destroy(dec[0]);
+    srs_amd_ldpc_decoder_destroy(dec[1]);
+  }
+};
+
+namespace {
+
+soft_row_layout layout_of(const srs_amd_sch_plan* p)
+{
+  soft_row_layout l{};
+  l.soft_bytes  = srs_amd_ldpc_codeblock_length(p->base_graph, p->lifting_size);
+  l.msg_offset  = static_cast<uint32_t>(align_up(l.soft_bytes, 64));
+  l.flag_offset = static_cast<uint32_t>(l.msg_offset + align_up((p->segment_length + 7) / 8, 16));
+  l.row_bytes   = static_cast<uint32_t>(align_up(l.flag_offset + 4, 64));
+  return l;
+}
+
+int check_plan(const srs_amd_sch_plan* p)
+{
+  if (p == nullptr || p->nof_segments == 0 || p->lifting_size == 0) {
+    return fail(SRS_AMD_EINVAL, "plan not computed (srs_amd_sch_plan_compute)");
+  }
+  return SRS_AMD_OK;
+}
+
+int decode_locked(srs_amd_pusch_decoder*              d,
+                  const srs_amd_sch_plan*             p,
+                  const srs_amd_pusch_decoder_config* cfg,
+                  uint8_t*                            d_tbs,
+                  uint32_t                            tb_stride,
+                  srs_amd_pusch_decoder_result*       d_results,
+                  const int8_t*                       d_llrs,
+                  uint32_t                            llr_stride,
+                  int8_t*                             d_soft,
+                  int32_t*                            d_cb_iterations,
+                  uint32_t                            nof_tbs,
+                  hipStream_t                         stream)
+{
+  const uint32_t        C          = p->nof_segments;
+  const uint32_t        rows       = nof_tbs * C;
+  const soft_row_layout lay        = layout_of(p);
+  const uint32_t        msg_stride = static_cast<uint32_t>(align_up((p->segment_length + 7) / 8, 64));
+  const bool            internal   = d_soft == nullptr;
+  hipError_t            he         = hipSetDevice(d->device);
+  if (internal && he == hipSuccess) {
+    he     = d->soft.ensure(static_cast<size_t>(rows) * lay.row_bytes);
+    d_soft = d->soft.as<int8_t>();
+  }
+  if (he == hipSuccess) {
+    he = d->msgs.ensure(static_cast<size_t>(rows) * msg_stride);
+  }
+  if (he == hipSuccess) {
+    he = d->iters.ensure(sizeof(int32_t) * rows);
+  }
+  if (he == hipSuccess) {
+    he = d->checks.ensure(sizeof(uint32_t) * rows);
+  }
+  if (he == hipSuccess) {
+    he = d->arrays.ensure(sizeof(uint32_t) * 2 * rows);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PUSCH decoder scratch");
+  }
+  if (std::memcmp(&d->key_plan, p, sizeof(*p)) != 0 || d->key_tbs != nof_tbs || d->key_stride != llr_stride) {
+    std::vector<uint32_t> E(C), off(C);
+    srs_amd_sch_plan_segments(p, E.data(), off.data());
+    d->h_arrays.resize(2 * rows);
+    for (uint32_t t = 0; t < nof_tbs; ++t) {
+      for (uint32_t r = 0; r < C; ++r) {
+        d->h_arrays[t * C + r]        = E[r];
+        d->h_arrays[rows + t * C + r] = t * llr_stride + off[r];
+      }
+    }
+    he = hipMemcpyAsync(d->arrays.ptr, d->h_arrays.data(), sizeof(uint32_t) * 2 * rows, hipMemcpyHostToDevice,
+                        stream);
+    if (he == hipSuccess) {
+      he = hipStreamSynchronize(stream);
+    }
+    if (he != hipSuccess) {
+      return hip_fail(he, "PUSCH decoder rate-matching arrays");
+    }
+    d->key_plan   = *p;
+    d->key_tbs    = nof_tbs;
+    d->key_stride = llr_stride;
+  }
+  // 1. Rate dematching + combining.
+  srs_amd_codeblock_metadata md{p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                                p->nof_filler_bits};
+  // Internal buffers stand for a fresh (zeroed) rx_buffer: nothing of theirs is read.
+  int rc = rate_dematch_batch_ex(d->dm, &md, cfg->new_data ? 1 : 0, d_llrs, d->arrays.as<uint32_t>() + rows,
+                                 d->arrays.as<uint32_t>(), d_soft, lay.row_bytes, rows, stream, internal);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  // 2. LDPC decoding (select_crc, pusch_decoder_impl.cpp:35-46).
+  const int crc_index = C > 1 ? 2 : (p->tbs > 3824 ? 1 : 0);
+  const int crc_poly  = C > 1 ? 1 : (p->tbs > 3824 ? 0 : 3);
+  srs_amd_ldpc_decoder_config dc{};
+  dc.base_graph      = p->base_graph;
+  dc.lifting_size    = p->lifting_size;
+  dc.nof_filler_bits = p->nof_filler_bits;
+  dc.nof_crc_bits    = C > 1 ? p->nof_crc_bits : p->nof_tb_crc_bits;
+  dc.max_iterations  = cfg->nof_ldpc_iterations;
+  srs_amd_ldpc_decoder* dec = d->dec[cfg->force_decoding ? 1 : 0];
+  rc = srs_amd_ldpc_decode_batch(dec, &dc, cfg->use_early_stop ? crc_poly : SRS_AMD_NO_CRC, d_soft, lay.row_bytes,
+                                 nullptr, lay.soft_bytes, d->msgs.as<uint8_t>(), msg_stride, d->iters.as<int32_t>(),
+                                 nullptr, rows, stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  if (!cfg->use_early_stop) {
+    rc = srs_amd_crc_calculate_batch(d->crc[crc_index], d->checks.as<uint32_t>(), d->msgs.as<uint8_t>(), msg_stride,
+                                     p->segment_length - p->nof_filler_bits, rows, stream);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+  }
+  // 3. Concatenation and TB CRC.
+  assemble_args a{};
+  a.msgs           = d->msgs.as<uint8_t>();
+  a.iters          = d->iters.as<int32_t>();
+  a.crc_checks     = cfg->use_early_stop ? nullptr : d->checks.as<uint32_t>();
+  a.soft           = internal ? nullptr : reinterpret_cast<uint8_t*>(d_soft); // no HARQ state to keep
+  a.tbs            = d_tbs;
+  a.results        = d_results;
+  a.cb_iterations  = d_cb_iterations;
+  a.crc24a_table   = crc_device_table(d->crc[1]);
+  a.lay            = lay;
+  a.msg_stride     = msg_stride;
+  a.tb_stride      = tb_stride;
+  a.nof_segments   = C;
+  a.cb_info_bits   = p->cb_info_bits;
+  a.tbs_bits       = p->tbs;
+  a.max_iterations = cfg->nof_ldpc_iterations;
+  a.new_data       = cfg->new_data ? 1 : 0;
+  he               = launch_assemble(a, nof_tbs, stream);
+  return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "assemble_kernel launch");
+}
+
+int check_args(srs_amd_pusch_decoder* dec, const srs_amd_sch_plan* plan, const srs_amd_pusch_decoder_config* cfg)
+{
+  if (dec == nullptr || cfg == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  int rc = check_plan(plan);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  if (cfg->nof_ldpc_iterations == 0) {
+    return fail(SRS_AMD_EINVAL, "The number of LDPC iterations must be positive.");
+  }
+  return SRS_AMD_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int srs_amd_pusch_decoder_create(srs_amd_pusch_decoder** out, int arith, int device)
+{
+  if (out == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null handle pointer");
+  }
+  *out = nullptr;
+  if (arith != SRS_AMD_ARITH_SIMD && arith != SRS_AMD_ARITH_GENERIC) {
+    return fail(SRS_AMD_EINVAL, "invalid LDPC arithmetic %d", arith);
+  }
+  int rc = select_device(device);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  auto* d   = new srs_amd_pusch_decoder();
+  d->device = device;
+  d->arith  = arith;
+  rc        = srs_amd_crc_calculator_create(&d->crc[0], 3, 8448, device);
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_crc_calculator_create(&d->crc[1], 0, 1277992, device);
+  }
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_crc_calculator_create(&d->crc[2], 1, 8448, device);
+  }
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_ldpc_rate_dematcher_create(&d->dm, device);
+  }
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_ldpc_decoder_create(&d->dec[0], arith, 0, device);
+  }
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_ldpc_decoder_create(&d->dec[1], arith, 1, device);
+  }
+  if (rc == SRS_AMD_OK) {
+    hipError_t he = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+    if (he != hipSuccess) {
+      rc = hip_fail(he, "PUSCH decoder stream");
+    }
+  }
+  if (rc != SRS_AMD_OK) {
+    delete d;
+    return rc;
+  }
+  *out = d;
+  return SRS_AMD_OK;
+}
+
+void srs_amd_pusch_decoder_destroy(srs_amd_pusch_decoder* dec)
+{
+  delete dec;
+}
+
+uint64_t srs_amd_pusch_soft_buffer_size(const srs_amd_sch_plan* plan)
+{
+  if (plan == nullptr || plan->nof_segments == 0 || plan->lifting_size == 0) {
+    return 0;
+  }
+  return static_cast<uint64_t>(plan->nof_segments) * layout_of(plan).row_bytes;
+}
+
+int srs_amd_pusch_decode_batch(srs_amd_pusch_decoder*              dec,
+                               const srs_amd_sch_plan*             plan,
+                               const srs_amd_pusch_decoder_config* cfg,
+                               uint8_t*                            d_tbs,
+                               uint32_t                            tb_stride,
+                               srs_amd_pusch_decoder_result*       d_results,
+                               const int8_t*                       d_llrs,
+                               uint32_t                            llr_stride,
+                               int8_t*                             d_soft,
+                               int32_t*                            d_cb_iterations,
+                               uint32_t                            nof_tbs,
+                               void*                               stream)
+{
+  int rc = check_args(dec, plan, cfg);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  if (nof_tbs == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_tbs == nullptr || d_results == nullptr || d_llrs == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  if (d_soft == nullptr && !cfg->new_data) {
+    return fail(SRS_AMD_EINVAL, "HARQ combining (new_data = 0) needs the caller's soft buffers");
+  }
+  if (static_cast<uint64_t>(tb_stride) * 8 < plan->tbs || llr_stride < plan->cw_length) {
+    return fail(SRS_AMD_EINVAL, "row strides too small (TB %u bits, codeword %u LLRs)", plan->tbs, plan->cw_length);
+  }
+  if (static_cast<uint64_t>(nof_tbs) * llr_stride >= (1ull << 32)) {
+    return fail(SRS_AMD_EINVAL, "batch of %u codewords exceeds 2^32 LLRs", nof_tbs);
+  }
+  std::lock_guard<std::mutex> lock(dec->mtx);
+  return decode_locked(dec, plan, cfg, d_tbs, tb_stride, d_results, d_llrs, llr_stride, d_soft, d_cb_iterations,
+                       nof_tbs, static_cast<hipStream_t>(stream));
+}
+
+int srs_amd_pusch_decode(srs_amd_pusch_decoder*              dec,
+                         uint8_t*                            transport_block,
+                         srs_amd_pusch_decoder_result*       result,
+                         const int8_t*                       llrs,
+                         int8_t*                             soft_buffer,
+                         const srs_amd_sch_plan*             plan,
+                         const srs_amd_pusch_decoder_config* cfg)
+{
+  int rc = check_args(dec, plan, cfg);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  if (transport_block == nullptr || result == nullptr || llrs == nullptr || soft_buffer == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  const uint32_t tb_bytes   = plan->tbs / 8;
+  const uint64_t soft_bytes = srs_amd_pusch_soft_buffer_size(plan);
+  const size_t   o_soft     = 0;
+  const size_t   o_llr      = align_up(soft_bytes, 256);
+  const size_t   o_tb       = o_llr + align_up(plan->cw_length, 256);
+  const size_t   o_res      = o_tb + align_up(tb_bytes, 256);
+  std::lock_guard<std::mutex> lock(dec->mtx);
+  hipError_t                  he = hipSetDevice(dec->device);
+  if (he == hipSuccess) {
+    he = dec->host_io.ensure(o_res + sizeof(srs_amd_pusch_decoder_result));
+  }
+  auto* base = dec->host_io.as<uint8_t>();
+  if (he == hipSuccess) {
+    he = hipMemcpyAsync(base + o_soft, soft_buffer, soft_bytes, hipMemcpyHostToDevice, dec->stream);
+  }
+  if (he == hipSuccess) {
+    he = hipMemcpyAsync(base + o_llr, llrs, plan->cw_length, hipMemcpyHostToDevice, dec->stream);
+  }
+  if (he == hipSuccess) {
+    he = hipMemcpyAsync(base + o_tb, transport_block, tb_bytes, hipMemcpyHostToDevice, dec->stream);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PUSCH decoder upload");
+  }
+  auto* d_res = reinterpret_cast<srs_amd_pusch_decoder_result*>(base + o_res);
+  rc = decode_locked(dec, plan, cfg, base + o_tb, tb_bytes, d_res, reinterpret_cast<int8_t*>(base + o_llr),
+                     plan->cw_length, reinterpret_cast<int8_t*>(base + o_soft), nullptr, 1, dec->stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  he = hipMemcpyAsync(soft_buffer, base + o_soft, soft_bytes, hipMemcpyDeviceToHost, dec->stream);
+  if (he == hipSuccess) {
+    he = hipMemcpyAsync(transport_block, base + o_tb, tb_bytes, hipMemcpyDeviceToHost, dec->stream);
+  }
+  if (he == hipSuccess) {
+    he = hipMemcpyAsync(result, d_res, sizeof(*result), hipMemcpyDeviceToHost, dec->stream);
+  }
+  if (he == hipSuccess) {
+    he = hipStreamSynchronize(dec->stream);
+  }
+  return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "PUSCH decoder download");
+}
+
+} // extern "C"

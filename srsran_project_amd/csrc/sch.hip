@@ -1,0 +1,211 @@
+// sch.hip -- transport-block kernels of the PDSCH encoder and PUSCH decoder.
+//
+//   segment_kernel   TX segmentation (ldpc_segmenter_tx_impl.cpp:137-207): one
+//                    thread per output byte of a (TB, segment) message row.
+//   assemble_kernel  RX tail of pusch_decoder_impl.cpp:309-500: one workgroup per
+//                    TB; CB CRC status + HARQ flags, LDPC statistics, codeblock
+//                    concatenation (concatenate_codeblocks, :460-503) and the
+//                    TB CRC24A check, computed from the concatenated bytes as
+//                    they are produced (block-wide linear CRC, crc_device.h).
+// Both are byte-gather kernels far below any roofline next to the LDPC
+// kernels they sit between (a few hundred KB per slot).
+#include <hip/hip_runtime.h>
+
+#include "crc_device.h"
+#include "sch_args.h"
+
+namespace srs_amd {
+namespace {
+
+constexpr int SEG_THREADS = 256;
+constexpr int ASM_THREADS = 256;
+constexpr uint32_t CRC24A_POLY = 0x1864cfb;
+constexpr uint32_t SCH_MAX_SEGMENTS = 512;
+
+__device__ __forceinline__ uint32_t bit_at(const uint8_t* b, uint32_t p)
+{
+  return (b[p >> 3] >> (7 - (p & 7))) & 1u;
+}
+
+__global__ __launch_bounds__(SEG_THREADS) void segment_kernel(segment_args a)
+{
+  const uint32_t row = blockIdx.y;
+  const uint32_t j   = blockIdx.x * SEG_THREADS + threadIdx.x;
+  if (row >= a.nof_rows || j >= a.msg_bytes) {
+    return;
+  }
+  const uint32_t t       = row / a.nof_segments;
+  const uint32_t r       = row - t * a.nof_segments;
+  const bool     last    = r == a.nof_segments - 1;
+  const uint32_t n_data  = last ? a.last_data_bits : a.cb_info_bits;
+  const uint32_t tb_off  = r * a.cb_info_bits;
+  const uint8_t* tb      = a.tbs + static_cast<size_t>(t) * a.tb_stride;
+  const uint32_t crc     = a.tb_crcs[t];
+  uint32_t       byte    = 0;
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t p = 8 * j + k;
+    uint32_t       v = 0;
+    if (p < n_data) {
+      v = bit_at(tb, tb_off + p);
+    } else if (last && p < n_data + a.tb_crc_bits) {
+      v = (crc >> (a.tb_crc_bits - 1 - (p - n_data))) & 1u;
+    }
+    byte |= v << (7 - k);
+  }
+  a.msgs[static_cast<size_t>(row) * a.msg_stride + j] = static_cast<uint8_t>(byte);
+}
+
+// TB byte j (bits 8j..8j+7) gathered from the concatenated codeblock data bits.
+struct tb_gather {
+  const uint8_t* base;
+  uint32_t       stride;
+  uint32_t       cbi;
+  __device__ uint32_t operator()(uint32_t j) const
+  {
+    uint32_t byte = 0;
+    uint32_t b    = 8 * j;
+    uint32_t r    = b / cbi;
+    uint32_t o    = b - r * cbi;
+    for (int k = 0; k < 8; ++k) {
+      byte |= bit_at(base + static_cast<size_t>(r) * stride, o) << (7 - k);
+      if (++o == cbi) {
+        o = 0;
+        ++r;
+      }
+    }
+    return byte;
+  }
+};
+
+__global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
+{
+  __shared__ uint32_t s_ok, s_sum, s_min, s_max, s_tb_ok;
+  __shared__ uint8_t  s_fresh[SCH_MAX_SEGMENTS]; // decoded in this call (not OK from a previous transmission)
+  __shared__ uint8_t  s_cb_ok[SCH_MAX_SEGMENTS];
+  __shared__ uint32_t partial[ASM_THREADS / 64];
+  const uint32_t      t = blockIdx.x;
+  const uint32_t      C = a.nof_segments;
+  if (threadIdx.x == 0) {
+    s_ok    = 0;
+    s_sum   = 0;
+    s_min   = 0xffffffffu;
+    s_max   = 0;
+    s_tb_ok = 0;
+  }
+  __syncthreads();
+  // 1. CB CRC status (pusch_decoder_impl.cpp:334-375) and LDPC statistics.
+  for (uint32_t r = threadIdx.x; r < C; r += ASM_THREADS) {
+    const uint32_t cb   = t * C + r;
+    const uint8_t* srow = a.soft ? a.soft + static_cast<size_t>(cb) * a.lay.row_bytes : nullptr;
+    const bool     prev = srow && !a.new_data && *reinterpret_cast<const int32_t*>(srow + a.lay.flag_offset) != 0;
+    const int32_t  it   = a.iters[cb];
+    const bool     dec  = a.crc_checks ? (a.crc_checks[cb] == 0) : (it >= 0);
+    const uint32_t stat = dec ? (a.crc_checks ? a.max_iterations : static_cast<uint32_t>(it)) : a.max_iterations;
+    const bool     ok   = prev || dec;
+    s_fresh[r]          = prev ? 0 : 1;
+    s_cb_ok[r]          = ok ? 1 : 0;
+    if (a.cb_iterations) {
+      a.cb_iterations[cb] = dec ? static_cast<int32_t>(stat) : -1;
+    }
+    atomicAdd(&s_ok, ok ? 1u : 0u);
+    atomicAdd(&s_sum, stat);
+    atomicMin(&s_min, stat);
+    atomicMax(&s_max, stat);
+  }
+  __syncthreads();
+  // 2. HARQ: freshly decoded messages and CRC flags into the soft buffer.
+  const uint8_t* src        = a.msgs + static_cast<size_t>(t) * C * a.msg_stride;
+  uint32_t       src_stride = a.msg_stride;
+  if (a.soft) {
+    const uint32_t msg_bytes = a.lay.flag_offset - a.lay.msg_offset;
+    for (uint32_t r = 0; r < C; ++r) {
+      if (!s_fresh[r]) {
+        continue;
+      }
+      const uint32_t cb   = t * C + r;
+      uint8_t*       srow = a.soft + static_cast<size_t>(cb) * a.lay.row_bytes;
+      const uint8_t* m    = a.msgs + static_cast<size_t>(cb) * a.msg_stride;
+      for (uint32_t j = threadIdx.x; j < msg_bytes; j += ASM_THREADS) {
+        srow[a.lay.msg_offset + j] = m[j];
+      }
+      if (threadIdx.x == 0) {
+        *reinterpret_cast<int32_t*>(srow + a.lay.flag_offset) = s_cb_ok[r];
+      }
+    }
+    __syncthreads();
+    src        = a.soft + static_cast<size_t>(t) * C * a.lay.row_bytes + a.lay.msg_offset;
+    src_stride = a.lay.row_bytes;
+  }
+  // 3. Transport block (pusch_decoder_impl.cpp:416-437).
+  uint8_t*       tb     = a.tbs + static_cast<size_t>(t) * a.tb_stride;
+  const uint32_t nbytes = a.tbs_bits / 8;
+  const bool     all_ok = s_ok == C;
+  if (C == 1) {
+    if (all_ok) {
+      for (uint32_t j = threadIdx.x; j < nbytes; j += ASM_THREADS) {
+        tb[j] = src[j];
+      }
+    }
+    if (threadIdx.x == 0) {
+      s_tb_ok = all_ok ? 1 : 0;
+    }
+  } else if (all_ok) {
+    const tb_gather g{src, src_stride, a.cb_info_bits};
+    for (uint32_t j = threadIdx.x; j < nbytes; j += ASM_THREADS) {
+      tb[j] = static_cast<uint8_t>(g(j));
+    }
+    const uint32_t crc = block_crc_bytes<ASM_THREADS>(g, a.tbs_bits, 24, CRC24A_POLY, a.crc24a_table, partial);
+    if (threadIdx.x == 0) {
+      // Checksum: the 24 bits after the TB data in the last codeblock.
+      const uint32_t off = a.tbs_bits - (C - 1) * a.cb_info_bits;
+      const uint8_t* m   = src + static_cast<size_t>(C - 1) * src_stride;
+      uint32_t       chk = 0;
+      for (uint32_t k = 0; k < 24; ++k) {
+        chk = (chk << 1) | bit_at(m, off + k);
+      }
+      s_tb_ok = crc == chk ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_tb_ok && a.soft) {
+      // A wrong TB checksum flags a false CB CRC positive: reset every CB (reset_codeblocks_crc).
+      for (uint32_t r = threadIdx.x; r < C; r += ASM_THREADS) {
+        uint8_t* srow = a.soft + static_cast<size_t>(t * C + r) * a.lay.row_bytes;
+        *reinterpret_cast<int32_t*>(srow + a.lay.flag_offset) = 0;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    srs_amd_pusch_decoder_result res{};
+    res.tb_crc_ok             = static_cast<int32_t>(s_tb_ok);
+    res.nof_codeblocks_total  = C;
+    res.ldpc_iterations_sum   = s_sum;
+    res.ldpc_iterations_min   = s_min;
+    res.ldpc_iterations_max   = s_max;
+    res.nof_codeblocks_crc_ok = s_ok;
+    a.results[t]              = res;
+  }
+}
+
+} // namespace
+
+hipError_t launch_segment(const segment_args& a, hipStream_t stream)
+{
+  if (a.nof_rows == 0) {
+    return hipSuccess;
+  }
+  dim3 grid((a.msg_bytes + SEG_THREADS - 1) / SEG_THREADS, a.nof_rows);
+  hipLaunchKernelGGL(segment_kernel, grid, dim3(SEG_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_assemble(const assemble_args& a, uint32_t nof_tbs, hipStream_t stream)
+{
+  if (nof_tbs == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(assemble_kernel, dim3(nof_tbs), dim3(ASM_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+} // namespace srs_amd

@@ -1,0 +1,63 @@
+// sch_args.h -- argument blocks of the transport-block kernels (sch.hip),
+// shared with their C-ABI (pdsch_api.cpp, pusch_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "srsran_amd/sch.h"
+
+namespace srs_amd {
+
+// ldpc_segmenter_tx_impl::read_codeblock (ldpc_segmenter_tx_impl.cpp:137-207) for
+// every (TB, segment) pair: data bits, TB CRC + zero pad in the last segment,
+// zeros where the CB CRC (attached afterwards) and the filler bits go.
+struct segment_args {
+  const uint8_t*  tbs;        // nof_tbs rows of tb_stride bytes
+  const uint32_t* tb_crcs;    // TB checksum per TB
+  uint8_t*        msgs;       // nof_tbs * C rows of msg_stride bytes
+  uint32_t        tb_stride;
+  uint32_t        msg_stride;
+  uint32_t        msg_bytes;  // ceil(K / 8)
+  uint32_t        nof_segments;
+  uint32_t        cb_info_bits;
+  uint32_t        last_data_bits; // TB bits in the last segment
+  uint32_t        tb_crc_bits;
+  uint32_t        nof_rows;   // nof_tbs * C
+};
+
+// Per-CB soft-buffer row (HARQ rx_buffer): [soft LLRs | saved message | CRC flag].
+struct soft_row_layout {
+  uint32_t soft_bytes; // N_short * Z
+  uint32_t msg_offset;
+  uint32_t flag_offset;
+  uint32_t row_bytes;
+};
+
+// pusch_decoder_impl.cpp:309-500 after the decoder: per-CB CRC status (kept in the
+// soft buffer across HARQ transmissions), statistics, codeblock concatenation
+// and the TB CRC check.
+struct assemble_args {
+  const uint8_t*                msgs;         // decoder output rows (msg_stride)
+  const int32_t*                iters;        // decoder iterations per CB (-1: CRC failed)
+  const uint32_t*               crc_checks;   // non-null when decoding without early stop: CRC of each message
+  uint8_t*                      soft;         // soft-buffer rows, or null
+  uint8_t*                      tbs;          // output TB rows
+  srs_amd_pusch_decoder_result* results;
+  int32_t*                      cb_iterations; // optional per-CB report
+  const uint32_t*               crc24a_table; // x^(k+24) mod g(CRC24A)
+  soft_row_layout               lay;
+  uint32_t                      msg_stride;
+  uint32_t                      tb_stride;
+  uint32_t                      nof_segments;
+  uint32_t                      cb_info_bits;
+  uint32_t                      tbs_bits;
+  uint32_t                      max_iterations;
+  int32_t                       new_data;
+};
+
+hipError_t launch_segment(const segment_args& a, hipStream_t stream);
+hipError_t launch_assemble(const assemble_args& a, uint32_t nof_tbs, hipStream_t stream);
+
+} // namespace srs_amd

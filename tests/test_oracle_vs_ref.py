@@ -299,3 +299,56 @@ def test_gold_sequence_matches_reference():
     for ci in (0, 1, 0x1234567, 2 ** 31 - 1):
         for n in (1, 31, 32, 1000, 100003):
             np.testing.assert_array_equal(oracle.prbs(ci, n), oracle.ref_prbs(ci, n))
+
+
+# --- PDSCH encoder / PUSCH decoder (transport-block chain) ---
+
+def test_sch_pdsch_encode_matches_reference():
+    """oracle.sch.pdsch_encode == pdsch_encoder_impl (segmenter + AVX2 LDPC encoder + rate matcher), bit-exact."""
+    import oracle.sch as sch
+    from tests.sch_cases import SCH_CASES, tb_bytes
+
+    for i, (tbs, bg, qm, lay, nre, rv, nref) in enumerate(SCH_CASES):
+        p = sch.plan(tbs, bg, rv, qm, nref, lay, nre)
+        tb = tb_bytes(tbs, i)
+        np.testing.assert_array_equal(sch.pdsch_encode(tb, p), oracle.ref_pdsch_encode(tb, p), err_msg=str(p))
+
+
+@pytest.mark.parametrize("arith", ["simd", "generic"])
+def test_sch_pusch_decode_matches_reference(arith):
+    """oracle.sch.pusch_decode == pusch_decoder_impl: TB bytes, TB CRC status and LDPC
+    statistics, with and without early stop, and a two-transmission HARQ sequence
+    (rv 0 too noisy to decode, rv 2 combined in the soft buffer)."""
+    import oracle.sch as sch
+    from tests.sch_cases import SCH_CASES, noisy_llrs, tb_bytes
+
+    for i, (tbs, bg, qm, lay, nre, rv, nref) in enumerate(SCH_CASES[:6]):
+        p = sch.plan(tbs, bg, rv, qm, nref, lay, nre)
+        tb = tb_bytes(tbs, i)
+        cw = sch.pdsch_encode(tb, p)
+        for early in (True, False):
+            llr = noisy_llrs(cw, 10, 9, seed=i)
+            h = sch.HarqBuffer(p)
+            out = np.zeros(tbs // 8, np.uint8)
+            ok, _, stats = sch.pusch_decode(llr, p, h, out, 6, arith, use_early_stop=early)
+            rb = oracle.RefRxBuffer(p["nof_segments"])
+            out2 = np.zeros(tbs // 8, np.uint8)
+            r = oracle.ref_pusch_decode(llr, p, rb, out2, 6, arith == "generic", use_early_stop=early)
+            assert r[0] == ok and r[1] == p["nof_segments"], (p, r, ok)
+            assert (r[3], r[4], r[5]) == (sum(stats), min(stats), max(stats)), (r, stats)
+            np.testing.assert_array_equal(out, out2)
+    # HARQ: first transmission undecodable, the second (rv 2) combined.
+    tbs, bg, qm, lay, nre = 8 * 1056, 1, 2, 1, 6000
+    p0 = sch.plan(tbs, bg, 0, qm, 0, lay, nre)
+    p2 = sch.plan(tbs, bg, 2, qm, 0, lay, nre)
+    tb = tb_bytes(tbs, 99)
+    h = sch.HarqBuffer(p0)
+    rb = oracle.RefRxBuffer(p0["nof_segments"])
+    out, out2 = np.zeros(tbs // 8, np.uint8), np.zeros(tbs // 8, np.uint8)
+    for p, new, sigma in ((p0, True, 9), (p2, False, 5)):
+        llr = noisy_llrs(sch.pdsch_encode(tb, p), 8, sigma, seed=p["rv"])
+        ok, _, _ = sch.pusch_decode(llr, p, h, out, 6, arith, new_data=new)
+        r = oracle.ref_pusch_decode(llr, p, rb, out2, 6, arith == "generic", new_data=new)
+        assert r[0] == ok
+        np.testing.assert_array_equal(out, out2)
+    assert ok, "HARQ combining should recover the TB"

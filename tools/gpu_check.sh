@@ -23,6 +23,7 @@ for s in "$@"; do
     polar) step pytest_polar 600 python -m pytest tests/test_polar_gpu.py -x -q ;;
     mod) step pytest_mod 600 python -m pytest tests/test_modulation_gpu.py -x -q ;;
     crc) step pytest_crc 600 python -m pytest tests/test_crc_gpu.py -x -q ;;
+    sch) step pytest_sch 900 python -m pytest tests/test_sch_gpu.py -x -q ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
     benchq) step bench 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
