@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for s in "$@"; do
   case $s in
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     codec) step pytest_codec 600 python -m pytest tests/test_ldpc_codec_gpu.py -x -q ;;
     ofdm) step pytest_ofdm 600 python -m pytest tests/test_ofdm_gpu.py -x -q ;;
     eq) step pytest_eq 600 python -m pytest tests/test_equalizer_gpu.py -x -q ;;
