@@ -1,0 +1,145 @@
+/*
+ * srsran_amd/pdsch_modulator.h -- C-ABI of the MI355X PDSCH modulator and
+ * PDSCH DM-RS processor: one launch turns a batch of encoded codewords into
+ * precoded resource-grid REs (scrambling, modulation, layer mapping,
+ * precoding, RE mapping fused), one launch writes the DM-RS of a batch of grids.
+ *
+ * Replaces (reference interfaces):
+ *   pdsch_modulator::modulate(resource_grid_writer&, span<const bit_buffer>, const config_t&)
+ *       include/srsran/phy/upper/channel_processors/pdsch/pdsch_modulator.h:97
+ *       (impl lib/phy/upper/channel_processors/pdsch/pdsch_modulator_impl.cpp:94-115)
+ *   dmrs_pdsch_processor::map(resource_grid_writer&, const config_t&)
+ *       include/srsran/phy/upper/signal_processors/pdsch/dmrs_pdsch_processor.h:65
+ *       (impl lib/phy/upper/signal_processors/pdsch/dmrs_pdsch_processor_impl.cpp:126-234)
+ *
+ * Resource grids are complex bf16 (real in the low 16 bits of each 32-bit RE)
+ * [port][symbol (14)][subcarrier], the reference's resource_grid_impl storage.
+ * Only the REs the reference writes are written. Precoded values are bit-exact
+ * with the reference's channel_precoder (generic / AVX2 / AVX512 agree).
+ */
+#ifndef SRSRAN_AMD_PDSCH_MODULATOR_H
+#define SRSRAN_AMD_PDSCH_MODULATOR_H
+
+#include <stdint.h>
+
+#include "srsran_amd/ldpc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRS_AMD_MAX_RB 275
+#define SRS_AMD_CRB_MASK_BYTES 35 /* ceil(275 / 8) */
+#define SRS_AMD_MAX_RE_PATTERNS 8
+#define SRS_AMD_MAX_LAYERS 4
+#define SRS_AMD_MAX_TX_PORTS 4
+
+/* re_pattern (include/srsran/phy/support/re_pattern.h:35): REs of the CRBs in
+ * crb_mask (bit i % 8 of byte i / 8 = CRB i) at the subcarriers of re_mask
+ * (bit k = subcarrier k of the RB) in the OFDM symbols of symbols (bit l). */
+typedef struct srs_amd_re_pattern {
+  uint8_t  crb_mask[SRS_AMD_CRB_MASK_BYTES];
+  uint8_t  reserved0;
+  uint16_t re_mask;
+  uint16_t symbols;
+} srs_amd_re_pattern;
+
+/* pdsch_modulator::config_t (pdsch_modulator.h:50-85), the frequency allocation
+ * resolved to CRBs (rb_allocation::get_crb_indices). */
+typedef struct srs_amd_pdsch_mod_config {
+  uint32_t           rnti;
+  uint32_t           n_id;
+  int32_t            modulation;   /* Qm code: 0 pi/2-BPSK, 1 BPSK, 2 QPSK, 4, 6, 8 */
+  uint32_t           bwp_start;    /* CRB */
+  uint32_t           bwp_size;     /* RBs */
+  uint8_t            crb_mask[SRS_AMD_CRB_MASK_BYTES]; /* allocated CRBs */
+  uint8_t            reserved0;
+  uint32_t           start_symbol; /* time_alloc */
+  uint32_t           nof_symbols;
+  uint32_t           dmrs_symbol_mask;
+  uint32_t           dmrs_type;    /* 1 or 2 */
+  uint32_t           nof_cdm_groups_without_data;
+  float              scaling;      /* applied when normal, as the reference */
+  uint32_t           nof_layers;   /* 1..4 */
+  uint32_t           nof_ports;    /* 1..4, >= nof_layers */
+  float              weights[SRS_AMD_MAX_LAYERS][SRS_AMD_MAX_TX_PORTS][2]; /* [layer][port] (re, im), PRG 0 */
+  uint32_t           nof_reserved;
+  srs_amd_re_pattern reserved[SRS_AMD_MAX_RE_PATTERNS];
+} srs_amd_pdsch_mod_config;
+
+/* dmrs_pdsch_processor::config_t (dmrs_pdsch_processor.h:38-57). The reference
+ * maps with one precoding PRG (dmrs_pdsch_processor_impl.cpp:149). */
+typedef struct srs_amd_dmrs_pdsch_config {
+  uint32_t slot_index;            /* slot_point::slot_index() */
+  uint32_t reference_point_k_rb;
+  uint32_t type;                  /* 1 or 2 */
+  uint32_t scrambling_id;
+  uint32_t n_scid;
+  float    amplitude;
+  uint32_t symbols_mask;
+  uint8_t  crb_mask[SRS_AMD_CRB_MASK_BYTES];
+  uint8_t  reserved0;
+  uint32_t nof_layers;            /* DM-RS ports 0..nof_layers-1 */
+  uint32_t nof_ports;
+  float    weights[SRS_AMD_MAX_LAYERS][SRS_AMD_MAX_TX_PORTS][2];
+} srs_amd_dmrs_pdsch_config;
+
+typedef struct srs_amd_pdsch_modulator srs_amd_pdsch_modulator;
+typedef struct srs_amd_pdsch_mod_plan  srs_amd_pdsch_mod_plan;
+
+int  srs_amd_pdsch_modulator_create(srs_amd_pdsch_modulator** mod, int device);
+void srs_amd_pdsch_modulator_destroy(srs_amd_pdsch_modulator* mod);
+
+/* Resolves the RE allocation of a configuration for grids of nof_subc
+ * subcarriers once (the reserved list + DM-RS pattern exclusion of
+ * pdsch_modulator_impl.cpp:53-86) and uploads it. *nof_re = data REs per
+ * layer; a codeword must carry nof_re * nof_layers * Qm bits. */
+int  srs_amd_pdsch_mod_plan_create(srs_amd_pdsch_modulator*        mod,
+                                   const srs_amd_pdsch_mod_config* cfg,
+                                   uint32_t                        nof_subc,
+                                   srs_amd_pdsch_mod_plan**        plan,
+                                   uint32_t*                       nof_re);
+void srs_amd_pdsch_mod_plan_destroy(srs_amd_pdsch_mod_plan* plan);
+
+/* HOST, synchronous: grid [grid_ports][14][nof_subc] cbf16 (as uint32) updated in
+ * place; codeword packed MSB first (bit_buffer), nof_bits bits. */
+int srs_amd_pdsch_modulate(srs_amd_pdsch_modulator*      mod,
+                           const srs_amd_pdsch_mod_plan* plan,
+                           uint32_t*                     grid,
+                           uint32_t                      grid_ports,
+                           const uint8_t*                codeword,
+                           uint32_t                      nof_bits);
+
+/* DEVICE, asynchronous: nof_cws codewords (rows of cw_stride bytes) into nof_cws
+ * grids (grid_stride REs apart, ports nof_subc * 14 REs apart). */
+int srs_amd_pdsch_modulate_batch(srs_amd_pdsch_modulator*      mod,
+                                 const srs_amd_pdsch_mod_plan* plan,
+                                 uint32_t*                     d_grids,
+                                 uint64_t                      grid_stride,
+                                 const uint8_t*                d_codewords,
+                                 uint32_t                      cw_stride,
+                                 uint32_t                      nof_bits,
+                                 uint32_t                      nof_cws,
+                                 void*                         stream);
+
+/* HOST, synchronous DM-RS mapping into grid [grid_ports][14][nof_subc]. */
+int srs_amd_dmrs_pdsch_map(srs_amd_pdsch_modulator*         mod,
+                           const srs_amd_dmrs_pdsch_config* cfg,
+                           uint32_t*                        grid,
+                           uint32_t                         grid_ports,
+                           uint32_t                         nof_subc);
+
+/* DEVICE, asynchronous DM-RS mapping into nof_grids grids. */
+int srs_amd_dmrs_pdsch_map_batch(srs_amd_pdsch_modulator*         mod,
+                                 const srs_amd_dmrs_pdsch_config* cfg,
+                                 uint32_t*                        d_grids,
+                                 uint64_t                         grid_stride,
+                                 uint32_t                         nof_subc,
+                                 uint32_t                         nof_grids,
+                                 void*                            stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRSRAN_AMD_PDSCH_MODULATOR_H */

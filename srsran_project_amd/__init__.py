@@ -59,7 +59,13 @@ from .modulation import MODULATION, Modulator  # noqa: F401
 
 from .crc import CrcCalculator, create_crc_calculator_factory_hip  # noqa: F401
 
-
+from .pdsch_modulator import (  # noqa: F401
+    DmrsPdschConfig,
+    PdschModPlan,
+    PdschModulator,
+    PdschModulatorConfig,
+    ReservedPattern,
+)
 
 from .sch import (  # noqa: F401
     PdschEncoder,

@@ -16,6 +16,7 @@
 // one launch without any sequential pass.
 #include <hip/hip_runtime.h>
 
+#include "gold_sequence.h"
 #include "modulation_args.h"
 
 #pragma clang fp contract(off)
@@ -182,43 +183,6 @@ __global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
   }
 }
 
-namespace {
-
-// state' = M * state over GF(2), M given by its 31 columns.
-__device__ __forceinline__ uint32_t gf2_apply(const uint32_t* cols, uint32_t state)
-{
-  uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < 31; ++j) {
-    r ^= cols[j] & (0u - ((state >> j) & 1u));
-  }
-  return r;
-}
-
-// 32 sequence bits c(n0 .. n0+31), c(n0 + b) at bit b.
-__device__ uint32_t gold_word(const uint32_t* jump, uint32_t c_init, uint32_t n0)
-{
-  uint32_t x1 = 1u, x2 = c_init & 0x7fffffffu;
-  const uint32_t n = n0 + 1600u;
-  for (int k = 0; k < PRBS_NJUMP; ++k) {
-    if ((n >> k) & 1u) {
-      x1 = gf2_apply(jump + (0 * PRBS_NJUMP + k) * 31, x1);
-      x2 = gf2_apply(jump + (1 * PRBS_NJUMP + k) * 31, x2);
-    }
-  }
-  uint32_t c = 0;
-#pragma unroll
-  for (int b = 0; b < 32; ++b) {
-    c |= ((x1 ^ x2) & 1u) << b;
-    const uint32_t n1 = ((x1 >> 3) ^ x1) & 1u;
-    const uint32_t n2 = ((x2 >> 3) ^ (x2 >> 2) ^ (x2 >> 1) ^ x2) & 1u;
-    x1                = (x1 >> 1) | (n1 << 30);
-    x2                = (x2 >> 1) | (n2 << 30);
-  }
-  return c;
-}
-
-} // namespace
 
 __global__ __launch_bounds__(256) void scramble_bits_kernel(prbs_args a)
 {

@@ -105,7 +105,7 @@ uint32_t lfsr_step(uint32_t s, bool x2)
   return (s >> 1) | (nb << 30);
 }
 
-uint32_t gf2_apply(const uint32_t* cols, uint32_t s)
+uint32_t gf2_apply_host(const uint32_t* cols, uint32_t s)
 {
   uint32_t r = 0;
   for (int j = 0; j < 31; ++j) {
@@ -116,7 +116,9 @@ uint32_t gf2_apply(const uint32_t* cols, uint32_t s)
   return r;
 }
 
-std::vector<uint32_t> jump_tables()
+} // namespace
+
+std::vector<uint32_t> srs_amd::gold_jump_tables()
 {
   std::vector<uint32_t> t(2 * PRBS_NJUMP * 31);
   for (int which = 0; which < 2; ++which) {
@@ -128,14 +130,13 @@ std::vector<uint32_t> jump_tables()
       const uint32_t* prev = t.data() + (which * PRBS_NJUMP + k - 1) * 31;
       uint32_t*       cur  = t.data() + (which * PRBS_NJUMP + k) * 31;
       for (int j = 0; j < 31; ++j) {
-        cur[j] = gf2_apply(prev, prev[j]);
+        cur[j] = gf2_apply_host(prev, prev[j]);
       }
     }
   }
   return t;
 }
 
-} // namespace
 
 struct srs_amd_modulator {
   int                  device = 0;
@@ -242,7 +243,7 @@ int srs_amd_modulator_create(srs_amd_modulator** mod, int device)
     m->tab256[k] = make_table(4, k, a256, 170.0F);
   }
   m->qam16_scale         = 1.0F / std::sqrt(10.0F);
-  std::vector<uint32_t> j = jump_tables();
+  std::vector<uint32_t> j = gold_jump_tables();
   hipError_t            e = hipMalloc(&m->d_tables, tables.size() * sizeof(float));
   if (e == hipSuccess) {
     e = hipMemcpy(m->d_tables, tables.data(), tables.size() * sizeof(float), hipMemcpyHostToDevice);

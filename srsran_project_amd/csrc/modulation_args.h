@@ -6,6 +6,8 @@
 
 #include <cstdint>
 
+#include "gold_sequence.h"
+
 namespace srs_amd {
 
 // Soft-demapper piecewise-linear LLR table of one PAM axis bit.
@@ -45,7 +47,6 @@ struct prbs_args {
   uint32_t       length;   // bits / LLRs
 };
 
-constexpr int PRBS_NJUMP = 24; // jumps by 2^k, k < 24 (sequences up to 2^24 - 1600 bits)
 
 hipError_t launch_modulate(const modulate_args& a, hipStream_t stream);
 hipError_t launch_demodulate(const demodulate_args& a, hipStream_t stream);

@@ -1,0 +1,235 @@
+// pdsch_modulator.hip -- MI355X PDSCH modulator and PDSCH DM-RS kernels.
+//
+// pdsch_map_kernel fuses what the reference does in four passes over a
+// codeword (pdsch_modulator_impl.cpp:94-115): Gold-sequence scrambling,
+// modulation to integer constellation points (ci8_t, modulation_mapper_lut_impl.cpp:37-67),
+// layer mapping + precoding (channel_precoder_avx2.cpp:214-330) and RE mapping
+// around the reserved / DM-RS REs (resource_grid_mapper_impl.cpp:341-460).
+// One workgroup per (codeword, OFDM symbol, 256 subcarriers): thread t owns
+// subcarrier k; its data-RE index j comes from the per-PRB table (prefix <<
+// 12 | 12-bit mask, built once per plan on the host). The workgroup's data
+// REs are contiguous in the codeword, so it scrambles exactly its bit range
+// into LDS (one Gold word per thread, jump-ahead, no sequential pass), then
+// every thread gathers its L x Qm bits, builds the integer points and writes
+// the precoded cbf16 RE of every port (coalesced 4-byte stores).
+//
+// dmrs_pdsch_kernel: one thread per (grid, DM-RS symbol, allocated CRB); the
+// 2 x 6 (type 1) / 2 x 4 (type 2) sequence bits of its RB from at most two
+// Gold words, CDM codes w_f / w_t (dmrs_helper.cpp:34-56), precoding with the
+// same SIMD complex product, DM-RS REs of every CDM group and port.
+//
+// Both are HBM-store bound: 4 bytes per RE and port written, Qm * L / 8 bytes
+// per RE read.
+#include <hip/hip_runtime.h>
+
+#include "gold_sequence.h"
+#include "pdsch_modulator_args.h"
+
+#pragma clang fp contract(off)
+
+namespace srs_amd {
+namespace {
+
+// x * w as _mm256_fmaddsub_ps(x, w.re, swap(x) * w.im).
+__device__ __forceinline__ float2 cmul_simd(float2 x, float wr, float wi)
+{
+  return make_float2(__builtin_fmaf(x.x, wr, -(x.y * wi)), __builtin_fmaf(x.y, wr, x.x * wi));
+}
+
+// ps_to_cbf16: round half to even on the bit pattern.
+__device__ __forceinline__ uint32_t to_bf16(float f)
+{
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+__device__ __forceinline__ uint32_t pack_cbf16(float2 v)
+{
+  return to_bf16(v.x) | (to_bf16(v.y) << 16);
+}
+
+// Integer constellation point of a Qm-bit index (modulation_mapper_lut_impl.cpp:44-56).
+__device__ __forceinline__ float2 qam_point(uint32_t idx, int qm)
+{
+  float off = -1.0f, re = 0.0f, im = 0.0f;
+  for (int j = 0; j < qm / 2; ++j) {
+    re += off;
+    im += off;
+    off *= 2.0f;
+    re = ((idx >> (2 * j + 1)) & 1u) ? re : -re;
+    im = ((idx >> (2 * j)) & 1u) ? im : -im;
+  }
+  return make_float2(re, im);
+}
+
+// Data REs of symbol row `row` before subcarrier k (k may be nof_subc).
+__device__ __forceinline__ uint32_t data_re_before(const uint32_t* row, uint32_t nof_prb, uint32_t k)
+{
+  const uint32_t prb = k / PDSCH_NRE;
+  if (prb >= nof_prb) {
+    const uint32_t e = row[nof_prb - 1];
+    return (e >> 12) + __builtin_popcount(e & 0xfffu);
+  }
+  const uint32_t e = row[prb];
+  return (e >> 12) + __builtin_popcount(e & ((1u << (k % PDSCH_NRE)) - 1u));
+}
+
+// Stream bits 32w .. 32w+31 of a packed MSB-first codeword, bit b at bit b (0 past the end).
+__device__ __forceinline__ uint32_t codeword_word(const uint8_t* cw, uint32_t nof_bytes, uint32_t w)
+{
+  uint32_t v = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t p = 4 * w + q;
+    const uint32_t b = p < nof_bytes ? cw[p] : 0u;
+    v |= (__builtin_bitreverse32(b) >> 24) << (8 * q);
+  }
+  return v;
+}
+
+constexpr int MAX_WORDS = PDSCH_THREADS + 2; // 256 REs x 4 layers x 8 bits / 32 + 2
+
+__global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args a)
+{
+  __shared__ uint32_t scrambled[MAX_WORDS];
+
+  const uint32_t  l   = a.first_symbol + blockIdx.y;
+  const uint32_t  k0  = a.first_subc + blockIdx.x * PDSCH_THREADS;
+  const uint32_t  k   = k0 + threadIdx.x;
+  const uint32_t* row = a.re_table + l * a.nof_prb;
+  const uint32_t  kend = min(k0 + PDSCH_THREADS, a.nof_subc);
+
+  const uint32_t bits_per_re = static_cast<uint32_t>(a.nof_layers) * (a.qm < 2 ? 1u : static_cast<uint32_t>(a.qm));
+  const uint32_t j_lo        = data_re_before(row, a.nof_prb, k0);
+  const uint32_t j_hi        = data_re_before(row, a.nof_prb, kend);
+  if (j_hi == j_lo) {
+    return; // no data RE in this block (uniform over the workgroup)
+  }
+  const uint32_t w_lo = j_lo * bits_per_re / 32;
+  const uint32_t w_hi = (j_hi * bits_per_re + 31) / 32;
+
+  const uint8_t* cw        = a.codewords + static_cast<uint64_t>(blockIdx.z) * a.cw_stride;
+  const uint32_t nof_bytes = (a.nof_bits + 7) / 8;
+  for (uint32_t w = w_lo + threadIdx.x; w < w_hi; w += PDSCH_THREADS) {
+    scrambled[w - w_lo] = codeword_word(cw, nof_bytes, w) ^ gold_word(a.jump, a.c_init, 32 * w);
+  }
+  __syncthreads();
+
+  if (k >= kend) {
+    return;
+  }
+  const uint32_t e   = row[k / PDSCH_NRE];
+  const uint32_t bit = k % PDSCH_NRE;
+  if (((e >> bit) & 1u) == 0) {
+    return;
+  }
+  const uint32_t j = (e >> 12) + __builtin_popcount(e & ((1u << bit) - 1u));
+
+  const int bps = a.qm < 2 ? 1 : a.qm;
+  float2    x[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    if (v < a.nof_layers) {
+      const uint32_t s   = j * a.nof_layers + v; // symbol index in the codeword
+      const uint32_t o   = s * bps - w_lo * 32;  // bit offset in LDS
+      const uint64_t win = static_cast<uint64_t>(scrambled[o / 32]) |
+                           (static_cast<uint64_t>(scrambled[min(o / 32 + 1, static_cast<uint32_t>(MAX_WORDS - 1))])
+                            << 32);
+      const uint32_t seq = static_cast<uint32_t>(win >> (o % 32)) & ((1u << bps) - 1u); // bit i = i-th bit
+      const uint32_t idx = __builtin_bitreverse32(seq) >> (32 - bps);                    // MSB-first index
+      if (a.qm >= 2) {
+        x[v] = qam_point(idx, a.qm);
+      } else {
+        const float b = idx ? -1.0f : 1.0f;
+        x[v]          = make_float2((a.qm == 0 && (s & 1u)) ? -b : b, b);
+      }
+    }
+  }
+
+  uint32_t* grid = a.grids + static_cast<uint64_t>(blockIdx.z) * a.grid_stride + l * a.nof_subc + k;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (p < a.nof_ports) {
+      float2 y = cmul_simd(x[0], a.w[0][p][0], a.w[0][p][1]);
+#pragma unroll
+      for (int v = 1; v < 4; ++v) {
+        if (v < a.nof_layers) {
+          const float2 t = cmul_simd(x[v], a.w[v][p][0], a.w[v][p][1]);
+          y.x            = y.x + t.x;
+          y.y            = y.y + t.y;
+        }
+      }
+      grid[static_cast<uint64_t>(p) * a.port_stride] = pack_cbf16(y);
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void dmrs_pdsch_kernel(dmrs_pdsch_args a)
+{
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x; // allocated CRB
+  if (i >= a.nof_crb) {
+    return;
+  }
+  const uint32_t l   = a.symbol[blockIdx.y];
+  const int      nd  = a.type2 ? 4 : 6;
+  const uint32_t crb = a.crbs[i];
+
+  // Sequence bits 2 * nd * (crb - reference) .. + 2 * nd - 1 (dmrs_helper.cpp:70-90).
+  const uint32_t b0 = 2u * nd * (crb - a.reference_point_k_rb);
+  const uint32_t w0 = b0 / 32;
+  uint64_t       c  = gold_word(a.jump, a.c_init[blockIdx.y], 32 * w0);
+  if ((b0 % 32) + 2 * nd > 32) {
+    c |= static_cast<uint64_t>(gold_word(a.jump, a.c_init[blockIdx.y], 32 * (w0 + 1))) << 32;
+  }
+  const uint32_t bits = static_cast<uint32_t>(c >> (b0 % 32));
+
+  uint32_t* grid = a.grids + static_cast<uint64_t>(blockIdx.z) * a.grid_stride + l * (a.port_stride / 14);
+  for (int g = 0; 2 * g < a.nof_layers; ++g) {
+    for (int t = 0; t < nd; ++t) {
+      const float  amp = a.amplitude;
+      const float2 base =
+          make_float2(((bits >> (2 * t)) & 1u) ? -amp : amp, ((bits >> (2 * t + 1)) & 1u) ? -amp : amp);
+      // Ports 2g and 2g+1 of the CDM group: w_f = -1 on odd sequence indices for the odd port,
+      // w_t = +1 for every port < 4 (type 1) / < 6 (type 2) and every DM-RS symbol.
+      float2 seq[2];
+      seq[0] = base;
+      seq[1] = (t & 1) ? make_float2(-base.x, -base.y) : base;
+      const uint32_t sc = crb * PDSCH_NRE + (a.type2 ? (2 * g + (t & 1) + 6 * (t >> 1)) : (2 * t + g));
+      for (int p = 0; p < a.nof_ports; ++p) {
+        float2 y = cmul_simd(seq[0], a.w[2 * g][p][0], a.w[2 * g][p][1]);
+        if (2 * g + 1 < a.nof_layers) {
+          const float2 u = cmul_simd(seq[1], a.w[2 * g + 1][p][0], a.w[2 * g + 1][p][1]);
+          y.x            = y.x + u.x;
+          y.y            = y.y + u.y;
+        }
+        grid[static_cast<uint64_t>(p) * a.port_stride + sc] = pack_cbf16(y);
+      }
+    }
+  }
+}
+
+} // namespace
+
+hipError_t launch_pdsch_map(const pdsch_map_args& a, uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_cws,
+                            hipStream_t stream)
+{
+  if (nof_symbols == 0 || span_subc == 0 || nof_cws == 0) {
+    return hipSuccess;
+  }
+  const dim3 grid((span_subc + PDSCH_THREADS - 1) / PDSCH_THREADS, nof_symbols, nof_cws);
+  hipLaunchKernelGGL(pdsch_map_kernel, grid, dim3(PDSCH_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dmrs_pdsch(const dmrs_pdsch_args& a, uint32_t nof_grids, hipStream_t stream)
+{
+  if (a.nof_crb == 0 || a.nof_dmrs_symbols == 0 || nof_grids == 0) {
+    return hipSuccess;
+  }
+  const dim3 grid((a.nof_crb + 63) / 64, a.nof_dmrs_symbols, nof_grids);
+  hipLaunchKernelGGL(dmrs_pdsch_kernel, grid, dim3(64), 0, stream, a);
+  return hipGetLastError();
+}
+
+} // namespace srs_amd

@@ -1,0 +1,482 @@
+// pdsch_modulator_api.cpp -- C-ABI of the MI355X PDSCH modulator and PDSCH
+// DM-RS processor (include/srsran_amd/pdsch_modulator.h).
+//
+// Host-side logic:
+//   plan: the RE allocation of pdsch_modulator_impl::map (pdsch_modulator_impl.cpp:53-86):
+//     allocated CRBs minus the reserved patterns and the DM-RS pattern
+//     (dmrs_type::get_dmrs_pattern, dmrs_mapping.h:76-123) in every symbol of the
+//     time allocation, flattened to a per-(symbol, PRB) table;
+//   scaling: modulation scaling (sqrt(1 / average power), modulation_mapper_lut_impl.cpp:60-66)
+//     times config.scaling when normal, folded into the precoding weights (:74-79);
+//   scrambling: c_init = rnti << 15 + q << 14 + n_id, q = 0 (pdsch_modulator_impl.cpp:33);
+//   DM-RS: c_init per symbol (dmrs_pdsch_processor_impl.cpp:66), amplitude
+//     M_SQRT1_2 * amplitude (:60), CRB list of the rb_mask.
+#include "srsran_amd/pdsch_modulator.h"
+
+#include <hip/hip_runtime.h>
+
+#include "api_common.h"
+#include "device_buffer.h"
+#include "gold_sequence.h"
+#include "pdsch_modulator_args.h"
+#include <cmath>
+#include <mutex>
+#include <vector>
+
+using namespace srs_amd;
+
+struct srs_amd_pdsch_modulator {
+  int           device = 0;
+  hipStream_t   stream = nullptr;
+  uint32_t*     d_jump = nullptr;
+  device_buffer scratch;
+  std::mutex    mtx;
+  ~srs_amd_pdsch_modulator()
+  {
+    (void)hipSetDevice(device);
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+    (void)hipFree(d_jump);
+  }
+};
+
+struct srs_amd_pdsch_mod_plan {
+  int            device = 0;
+  pdsch_map_args args{};
+  uint32_t       nof_symbols = 0;
+  uint32_t       span_subc   = 0;
+  uint32_t       nof_re      = 0;
+  uint32_t*      d_table     = nullptr;
+  ~srs_amd_pdsch_mod_plan()
+  {
+    (void)hipSetDevice(device);
+    (void)hipFree(d_table);
+  }
+};
+
+namespace {
+
+bool crb_bit(const uint8_t* mask, uint32_t i)
+{
+  return i < SRS_AMD_MAX_RB && ((mask[i / 8] >> (i % 8)) & 1u);
+}
+
+bool valid_qm(int qm)
+{
+  return qm == 0 || qm == 1 || qm == 2 || qm == 4 || qm == 6 || qm == 8;
+}
+
+// modulation_mapper_lut_impl.cpp:40-67 (QAM) and :176 / :205 (BPSK, pi/2-BPSK).
+float modulation_scaling(int qm)
+{
+  if (qm < 2) {
+    return static_cast<float>(M_SQRT1_2);
+  }
+  const int L   = 1 << qm;
+  float     sum = 0;
+  for (int i = 0; i < L; ++i) {
+    float off = -1, re = 0, im = 0;
+    for (int j = 0; j < qm / 2; ++j) {
+      re += off;
+      im += off;
+      off *= 2;
+      re *= ((i & (1 << (2 * j + 1))) != 0) ? +1 : -1;
+      im *= ((i & (1 << (2 * j + 0))) != 0) ? +1 : -1;
+    }
+    sum += re * re + im * im; // integers: exact
+  }
+  return std::sqrt(1 / (sum / static_cast<float>(L)));
+}
+
+// get_dmrs_prb_mask (dmrs_mapping.h:76-91).
+uint32_t dmrs_prb_mask(uint32_t type, uint32_t nof_cdm_groups_without_data)
+{
+  uint32_t m = 0;
+  for (uint32_t k = 0; k < 12; ++k) {
+    const bool in = type == 1 ? (k % 2) < nof_cdm_groups_without_data : (k % 6) < 2 * nof_cdm_groups_without_data;
+    m |= in ? (1u << k) : 0u;
+  }
+  return m;
+}
+
+int check_weights(uint32_t nof_layers, uint32_t nof_ports)
+{
+  if (nof_layers < 1 || nof_layers > SRS_AMD_MAX_LAYERS) {
+    return fail(SRS_AMD_EINVAL, "The number of layers (i.e., %u) must be in range [1, %d].", nof_layers,
+                SRS_AMD_MAX_LAYERS);
+  }
+  if (nof_ports < nof_layers || nof_ports > SRS_AMD_MAX_TX_PORTS) {
+    return fail(SRS_AMD_EINVAL, "The number of antennas (i.e., %u) must be in range [%u, %d].", nof_ports,
+                nof_layers, SRS_AMD_MAX_TX_PORTS);
+  }
+  return SRS_AMD_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int srs_amd_pdsch_modulator_create(srs_amd_pdsch_modulator** mod, int device)
+{
+  if (mod == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null handle pointer");
+  }
+  *mod   = nullptr;
+  int rc = select_device(device);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  auto* m                 = new srs_amd_pdsch_modulator();
+  m->device               = device;
+  std::vector<uint32_t> j = gold_jump_tables();
+  hipError_t            e = hipMalloc(&m->d_jump, j.size() * sizeof(uint32_t));
+  if (e == hipSuccess) {
+    e = hipMemcpy(m->d_jump, j.data(), j.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess) {
+    e = hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking);
+  }
+  if (e != hipSuccess) {
+    delete m;
+    return hip_fail(e, "PDSCH modulator tables");
+  }
+  *mod = m;
+  return SRS_AMD_OK;
+}
+
+void srs_amd_pdsch_modulator_destroy(srs_amd_pdsch_modulator* mod)
+{
+  delete mod;
+}
+
+int srs_amd_pdsch_mod_plan_create(srs_amd_pdsch_modulator*        mod,
+                                  const srs_amd_pdsch_mod_config* cfg,
+                                  uint32_t                        nof_subc,
+                                  srs_amd_pdsch_mod_plan**        plan,
+                                  uint32_t*                       nof_re)
+{
+  if (mod == nullptr || cfg == nullptr || plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  *plan = nullptr;
+  if (nof_subc == 0 || nof_subc % 12 != 0 || nof_subc > 12 * SRS_AMD_MAX_RB) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of grid subcarriers (i.e., %u).", nof_subc);
+  }
+  if (!valid_qm(cfg->modulation)) {
+    return fail(SRS_AMD_EINVAL, "Invalid modulation scheme %d.", cfg->modulation);
+  }
+  int rc = check_weights(cfg->nof_layers, cfg->nof_ports);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  if (cfg->nof_symbols == 0 || cfg->start_symbol + cfg->nof_symbols > PDSCH_NSYMB) {
+    return fail(SRS_AMD_EINVAL, "The time allocation of the transmission [%u, %u) exceeds the slot boundary.",
+                cfg->start_symbol, cfg->start_symbol + cfg->nof_symbols);
+  }
+  if (cfg->dmrs_type != 1 && cfg->dmrs_type != 2) {
+    return fail(SRS_AMD_EINVAL, "Invalid DM-RS type %u.", cfg->dmrs_type);
+  }
+  if (cfg->nof_cdm_groups_without_data < 1 || cfg->nof_cdm_groups_without_data > (cfg->dmrs_type == 1 ? 2u : 3u)) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of CDM groups without data (i.e., %u).",
+                cfg->nof_cdm_groups_without_data);
+  }
+  if (cfg->nof_reserved > SRS_AMD_MAX_RE_PATTERNS) {
+    return fail(SRS_AMD_EINVAL, "Too many reserved RE patterns (i.e., %u).", cfg->nof_reserved);
+  }
+  const uint32_t nof_prb = nof_subc / 12;
+  uint32_t       lo = nof_prb, hi = 0;
+  for (uint32_t c = 0; c < nof_prb; ++c) {
+    if (crb_bit(cfg->crb_mask, c)) {
+      lo = std::min(lo, c);
+      hi = c + 1;
+    }
+  }
+  for (uint32_t c = nof_prb; c < SRS_AMD_MAX_RB; ++c) {
+    if (crb_bit(cfg->crb_mask, c)) {
+      return fail(SRS_AMD_EINVAL, "Allocated CRB %u exceeds the grid bandwidth (%u RB).", c, nof_prb);
+    }
+  }
+  if (hi == 0) {
+    return fail(SRS_AMD_EINVAL, "Empty frequency allocation.");
+  }
+
+  // re_pattern_list::get_exclusion_mask per symbol (re_pattern.cpp:62-100), DM-RS pattern merged.
+  const uint32_t        dmrs_re = dmrs_prb_mask(cfg->dmrs_type, cfg->nof_cdm_groups_without_data);
+  std::vector<uint32_t> table(PDSCH_NSYMB * nof_prb, 0);
+  uint32_t              count = 0;
+  for (uint32_t l = 0; l < PDSCH_NSYMB; ++l) {
+    const bool in_time = l >= cfg->start_symbol && l < cfg->start_symbol + cfg->nof_symbols;
+    for (uint32_t c = 0; c < nof_prb; ++c) {
+      uint32_t m = (in_time && crb_bit(cfg->crb_mask, c)) ? 0xfffu : 0u;
+      if (m != 0) {
+        for (uint32_t r = 0; r < cfg->nof_reserved; ++r) {
+          const srs_amd_re_pattern& p = cfg->reserved[r];
+          if (((p.symbols >> l) & 1u) && crb_bit(p.crb_mask, c)) {
+            m &= ~static_cast<uint32_t>(p.re_mask);
+          }
+        }
+        if (((cfg->dmrs_symbol_mask >> l) & 1u) && c >= cfg->bwp_start && c < cfg->bwp_start + cfg->bwp_size) {
+          m &= ~dmrs_re;
+        }
+      }
+      table[l * nof_prb + c] = (count << 12) | m;
+      count += static_cast<uint32_t>(__builtin_popcount(m));
+    }
+  }
+
+  auto* p                 = new srs_amd_pdsch_mod_plan();
+  p->device               = mod->device;
+  p->nof_re               = count;
+  p->nof_symbols          = cfg->nof_symbols;
+  p->span_subc            = (hi - lo) * 12;
+  pdsch_map_args& a       = p->args;
+  a.jump                  = mod->d_jump;
+  a.port_stride           = PDSCH_NSYMB * nof_subc;
+  a.nof_subc              = nof_subc;
+  a.nof_prb               = nof_prb;
+  a.c_init                = (cfg->rnti << 15) + cfg->n_id;
+  a.first_symbol          = cfg->start_symbol;
+  a.qm                    = cfg->modulation;
+  a.nof_layers            = static_cast<int32_t>(cfg->nof_layers);
+  a.nof_ports             = static_cast<int32_t>(cfg->nof_ports);
+  a.first_subc            = lo * 12;
+  float scaling           = modulation_scaling(cfg->modulation);
+  if (std::isnormal(cfg->scaling)) {
+    scaling *= cfg->scaling;
+  }
+  for (uint32_t v = 0; v < cfg->nof_layers; ++v) {
+    for (uint32_t q = 0; q < cfg->nof_ports; ++q) {
+      a.w[v][q][0] = cfg->weights[v][q][0] * scaling;
+      a.w[v][q][1] = cfg->weights[v][q][1] * scaling;
+    }
+  }
+  hipError_t e = hipSetDevice(mod->device);
+  if (e == hipSuccess) {
+    e = hipMalloc(&p->d_table, table.size() * sizeof(uint32_t));
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpy(p->d_table, table.data(), table.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "PDSCH modulator plan");
+  }
+  a.re_table = p->d_table;
+  *plan      = p;
+  if (nof_re != nullptr) {
+    *nof_re = count;
+  }
+  return SRS_AMD_OK;
+}
+
+void srs_amd_pdsch_mod_plan_destroy(srs_amd_pdsch_mod_plan* plan)
+{
+  delete plan;
+}
+
+int srs_amd_pdsch_modulate_batch(srs_amd_pdsch_modulator*      mod,
+                                 const srs_amd_pdsch_mod_plan* plan,
+                                 uint32_t*                     d_grids,
+                                 uint64_t                      grid_stride,
+                                 const uint8_t*                d_codewords,
+                                 uint32_t                      cw_stride,
+                                 uint32_t                      nof_bits,
+                                 uint32_t                      nof_cws,
+                                 void*                         stream)
+{
+  if (mod == nullptr || plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  const pdsch_map_args& pa  = plan->args;
+  const uint32_t        bps = pa.qm < 2 ? 1u : static_cast<uint32_t>(pa.qm);
+  if (static_cast<uint64_t>(nof_bits) != static_cast<uint64_t>(plan->nof_re) * pa.nof_layers * bps) {
+    return fail(SRS_AMD_EINVAL,
+                "The codeword length (i.e., %u bits) does not match the allocation (i.e., %u RE x %d layers x %u "
+                "bits).",
+                nof_bits, plan->nof_re, pa.nof_layers, bps);
+  }
+  if (nof_cws == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_grids == nullptr || d_codewords == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  if (nof_cws > 1 && (cw_stride < (nof_bits + 7) / 8 || grid_stride < static_cast<uint64_t>(pa.nof_ports) *
+                                                                           pa.port_stride)) {
+    return fail(SRS_AMD_EINVAL, "codeword or grid stride too small");
+  }
+  pdsch_map_args a = pa;
+  a.codewords      = d_codewords;
+  a.grids          = d_grids;
+  a.grid_stride    = grid_stride;
+  a.cw_stride      = cw_stride;
+  a.nof_bits       = nof_bits;
+  hipError_t e     = hipSetDevice(mod->device);
+  if (e == hipSuccess) {
+    e = launch_pdsch_map(a, plan->nof_symbols, plan->span_subc, nof_cws, static_cast<hipStream_t>(stream));
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pdsch_map_kernel launch");
+}
+
+int srs_amd_pdsch_modulate(srs_amd_pdsch_modulator*      mod,
+                           const srs_amd_pdsch_mod_plan* plan,
+                           uint32_t*                     grid,
+                           uint32_t                      grid_ports,
+                           const uint8_t*                codeword,
+                           uint32_t                      nof_bits)
+{
+  if (mod == nullptr || plan == nullptr || grid == nullptr || codeword == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (grid_ports < static_cast<uint32_t>(plan->args.nof_ports)) {
+    return fail(SRS_AMD_EINVAL, "The precoding number of ports (i.e., %d) exceeds the grid number of ports (i.e., %u).",
+                plan->args.nof_ports, grid_ports);
+  }
+  std::lock_guard<std::mutex> lock(mod->mtx);
+  const size_t                grid_bytes = static_cast<size_t>(grid_ports) * plan->args.port_stride * 4;
+  const size_t                cw_bytes   = (nof_bits + 7) / 8;
+  hipError_t                  e          = hipSetDevice(mod->device);
+  if (e == hipSuccess) {
+    e = mod->scratch.ensure(grid_bytes + align_up(cw_bytes, 256) + 256);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PDSCH modulator scratch");
+  }
+  auto* d_grid = mod->scratch.as<uint32_t>();
+  auto* d_cw   = mod->scratch.as<uint8_t>() + align_up(grid_bytes, 256);
+  e            = hipMemcpyAsync(d_grid, grid, grid_bytes, hipMemcpyHostToDevice, mod->stream);
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(d_cw, codeword, cw_bytes, hipMemcpyHostToDevice, mod->stream);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PDSCH modulator upload");
+  }
+  int rc = srs_amd_pdsch_modulate_batch(mod, plan, d_grid, 0, d_cw, static_cast<uint32_t>(cw_bytes), nof_bits, 1,
+                                        mod->stream);
+  if (rc != SRS_AMD_OK) {
+    (void)hipStreamSynchronize(mod->stream);
+    return rc;
+  }
+  e = hipMemcpyAsync(grid, d_grid, grid_bytes, hipMemcpyDeviceToHost, mod->stream);
+  if (e == hipSuccess) {
+    e = hipStreamSynchronize(mod->stream);
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PDSCH modulator download");
+}
+
+int srs_amd_dmrs_pdsch_map_batch(srs_amd_pdsch_modulator*         mod,
+                                 const srs_amd_dmrs_pdsch_config* cfg,
+                                 uint32_t*                        d_grids,
+                                 uint64_t                         grid_stride,
+                                 uint32_t                         nof_subc,
+                                 uint32_t                         nof_grids,
+                                 void*                            stream)
+{
+  if (mod == nullptr || cfg == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  int rc = check_weights(cfg->nof_layers, cfg->nof_ports);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  if (cfg->type != 1 && cfg->type != 2) {
+    return fail(SRS_AMD_EINVAL, "Invalid DM-RS type %u.", cfg->type);
+  }
+  if (nof_subc == 0 || nof_subc % 12 != 0 || nof_subc > 12 * SRS_AMD_MAX_RB) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of grid subcarriers (i.e., %u).", nof_subc);
+  }
+  dmrs_pdsch_args a{};
+  a.jump                 = mod->d_jump;
+  a.grids                = d_grids;
+  a.grid_stride          = grid_stride;
+  a.port_stride          = PDSCH_NSYMB * nof_subc;
+  a.reference_point_k_rb = cfg->reference_point_k_rb;
+  a.type2                = cfg->type == 2 ? 1 : 0;
+  a.nof_layers           = static_cast<int32_t>(cfg->nof_layers);
+  a.nof_ports            = static_cast<int32_t>(cfg->nof_ports);
+  a.amplitude            = static_cast<float>(M_SQRT1_2 * cfg->amplitude);
+  for (uint32_t c = 0; c < SRS_AMD_MAX_RB; ++c) {
+    if (crb_bit(cfg->crb_mask, c)) {
+      if (c >= nof_subc / 12) {
+        return fail(SRS_AMD_EINVAL, "DM-RS CRB %u exceeds the grid bandwidth.", c);
+      }
+      if (c < cfg->reference_point_k_rb) {
+        return fail(SRS_AMD_EINVAL, "DM-RS CRB %u below the reference point %u.", c, cfg->reference_point_k_rb);
+      }
+      a.crbs[a.nof_crb++] = static_cast<uint16_t>(c);
+    }
+  }
+  const unsigned nslot = cfg->slot_index;
+  const unsigned nid   = cfg->scrambling_id;
+  const unsigned nscid = cfg->n_scid ? 1 : 0;
+  for (uint32_t l = 0; l < PDSCH_NSYMB; ++l) {
+    if ((cfg->symbols_mask >> l) & 1u) {
+      const uint32_t i = a.nof_dmrs_symbols++;
+      a.symbol[i]      = static_cast<uint8_t>(l);
+      a.lprime[i]      = (l > 0 && ((cfg->symbols_mask >> (l - 1)) & 1u)) ? 1 : 0;
+      // dmrs_pdsch_processor_impl.cpp:66, unsigned arithmetic modulo 2^32 then % 2^31.
+      a.c_init[i] = ((PDSCH_NSYMB * nslot + l + 1) * (2 * nid + 1) * (1u << 17) + (2 * nid + nscid)) % (1u << 31);
+    }
+  }
+  for (uint32_t v = 0; v < cfg->nof_layers; ++v) {
+    for (uint32_t q = 0; q < cfg->nof_ports; ++q) {
+      a.w[v][q][0] = cfg->weights[v][q][0];
+      a.w[v][q][1] = cfg->weights[v][q][1];
+    }
+  }
+  if (nof_grids == 0 || a.nof_crb == 0 || a.nof_dmrs_symbols == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_grids == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  if (nof_grids > 1 && grid_stride < static_cast<uint64_t>(cfg->nof_ports) * a.port_stride) {
+    return fail(SRS_AMD_EINVAL, "grid stride too small");
+  }
+  hipError_t e = hipSetDevice(mod->device);
+  if (e == hipSuccess) {
+    e = launch_dmrs_pdsch(a, nof_grids, static_cast<hipStream_t>(stream));
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "dmrs_pdsch_kernel launch");
+}
+
+int srs_amd_dmrs_pdsch_map(srs_amd_pdsch_modulator*         mod,
+                           const srs_amd_dmrs_pdsch_config* cfg,
+                           uint32_t*                        grid,
+                           uint32_t                         grid_ports,
+                           uint32_t                         nof_subc)
+{
+  if (mod == nullptr || cfg == nullptr || grid == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (grid_ports < cfg->nof_ports) {
+    return fail(SRS_AMD_EINVAL, "The precoding number of ports (i.e., %u) exceeds the grid number of ports (i.e., %u).",
+                cfg->nof_ports, grid_ports);
+  }
+  std::lock_guard<std::mutex> lock(mod->mtx);
+  const size_t                grid_bytes = static_cast<size_t>(grid_ports) * PDSCH_NSYMB * nof_subc * 4;
+  hipError_t                  e          = hipSetDevice(mod->device);
+  if (e == hipSuccess) {
+    e = mod->scratch.ensure(grid_bytes);
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(mod->scratch.ptr, grid, grid_bytes, hipMemcpyHostToDevice, mod->stream);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "DM-RS upload");
+  }
+  int rc = srs_amd_dmrs_pdsch_map_batch(mod, cfg, mod->scratch.as<uint32_t>(), 0, nof_subc, 1, mod->stream);
+  if (rc != SRS_AMD_OK) {
+    (void)hipStreamSynchronize(mod->stream);
+    return rc;
+  }
+  e = hipMemcpyAsync(grid, mod->scratch.ptr, grid_bytes, hipMemcpyDeviceToHost, mod->stream);
+  if (e == hipSuccess) {
+    e = hipStreamSynchronize(mod->stream);
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "DM-RS download");
+}
+
+} // extern "C"

@@ -1,0 +1,59 @@
+// pdsch_modulator_args.h -- argument blocks of the PDSCH modulator and PDSCH
+// DM-RS kernels (pdsch_modulator.hip), shared with their C-ABI (pdsch_modulator_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace srs_amd {
+
+constexpr int PDSCH_NSYMB   = 14;
+constexpr int PDSCH_NRE     = 12;
+constexpr int PDSCH_MAX_RB  = 275;
+constexpr int PDSCH_THREADS = 256;
+
+struct pdsch_map_args {
+  const uint8_t*  codewords;  // packed MSB first, rows of cw_stride bytes
+  uint32_t*       grids;      // cbf16 REs
+  const uint32_t* re_table;   // [14][nof_prb]: (data RE index of the PRB's first RE) << 12 | 12-bit data RE mask
+  const uint32_t* jump;       // Gold-sequence jump matrices
+  uint64_t        grid_stride;
+  uint32_t        port_stride; // 14 * nof_subc
+  uint32_t        nof_subc;
+  uint32_t        nof_prb;     // ceil(nof_subc / 12)
+  uint32_t        cw_stride;
+  uint32_t        nof_bits;
+  uint32_t        c_init;
+  uint32_t        first_symbol;
+  int32_t         qm;
+  int32_t         nof_layers;
+  int32_t         nof_ports;
+  uint32_t        first_subc;  // first allocated subcarrier (grid.x offset)
+  float           w[4][4][2];  // [layer][port] weights x modulation scaling x config scaling
+};
+
+struct dmrs_pdsch_args {
+  uint32_t*       grids;
+  const uint32_t* jump;
+  uint64_t        grid_stride;
+  uint32_t        port_stride;
+  uint32_t        nof_crb;
+  uint32_t        reference_point_k_rb;
+  int32_t         type2;
+  int32_t         nof_layers;
+  int32_t         nof_ports;
+  float           amplitude;    // M_SQRT1_2 * config amplitude (double product rounded to float)
+  uint32_t        nof_dmrs_symbols;
+  uint8_t         symbol[PDSCH_NSYMB];
+  uint8_t         lprime[PDSCH_NSYMB];
+  uint32_t        c_init[PDSCH_NSYMB];
+  float           w[4][4][2];   // [layer][port]
+  uint16_t        crbs[PDSCH_MAX_RB];
+};
+
+hipError_t launch_pdsch_map(const pdsch_map_args& a, uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_cws,
+                            hipStream_t stream);
+hipError_t launch_dmrs_pdsch(const dmrs_pdsch_args& a, uint32_t nof_grids, hipStream_t stream);
+
+} // namespace srs_amd

@@ -352,3 +352,30 @@ def test_sch_pusch_decode_matches_reference(arith):
         assert r[0] == ok
         np.testing.assert_array_equal(out, out2)
     assert ok, "HARQ combining should recover the TB"
+
+
+# ---- PDSCH modulator / DM-RS (oracle/pdsch_mod.py vs the reference's classes) ----
+from tests.pdsch_cases import DMRS_CASES, MOD_CASES, dmrs_case, mod_case  # noqa: E402
+
+
+@pytest.mark.parametrize("case", MOD_CASES, ids=[c[0] for c in MOD_CASES])
+@pytest.mark.parametrize("precoder", ["generic", "avx2", "avx512"])
+def test_pdsch_modulator_matches_reference(case, precoder):
+    from oracle import pdsch_mod as pm
+
+    grid0, bits, kw = mod_case(case)
+    want = pm.ref_pdsch_modulate(grid0.copy(), bits, precoder=precoder, **kw)
+    got = pm.pdsch_modulate(grid0.copy(), bits, **kw)
+    np.testing.assert_array_equal(got, want)
+    assert (want != grid0).any()
+
+
+@pytest.mark.parametrize("case", DMRS_CASES, ids=[c[0] for c in DMRS_CASES])
+@pytest.mark.parametrize("precoder", ["generic", "avx2", "avx512"])
+def test_dmrs_pdsch_matches_reference(case, precoder):
+    from oracle import pdsch_mod as pm
+
+    grid0, kw = dmrs_case(case)
+    want = pm.ref_dmrs_pdsch_map(grid0.copy(), precoder=precoder, **kw)
+    got = pm.dmrs_pdsch_map(grid0.copy(), **kw)
+    np.testing.assert_array_equal(got, want)
