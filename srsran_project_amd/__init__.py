@@ -67,6 +67,14 @@ from .pdsch_modulator import (  # noqa: F401
     ReservedPattern,
 )
 
+from .pusch_chest import (  # noqa: F401
+    ChestPortStats,
+    DmrsPuschEstimator,
+    DmrsPuschEstimatorConfig,
+    FdSmoothingStrategy,
+    TdInterpolationStrategy,
+)
+
 from .sch import (  # noqa: F401
     PdschEncoder,
     PuschDecoder,

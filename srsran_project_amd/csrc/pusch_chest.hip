@@ -1,0 +1,667 @@
+// pusch_chest.hip -- MI355X PUSCH DM-RS channel estimator (dmrs_pusch_estimator_impl
+// + port_channel_estimator_average_impl, DM-RS type 1, one hop).
+//
+// Three launches per batch of grids:
+//   chest_pilot_kernel   one 1024-thread workgroup per (grid, rx port). The DM-RS
+//                        Gold words of every DM-RS symbol are generated into LDS
+//                        (jump-ahead, one word per thread); thread t owns pilots
+//                        t and t + 1024 and keeps their received values in
+//                        registers. Per layer: LSE (rx * conj(pilot)), CFO from
+//                        the first two DM-RS symbols (block reduction), CFO
+//                        compensation and time accumulation, CDM pair averaging
+//                        (lane shuffle), scaling, FD smoothing in LDS (mean, or
+//                        virtual pilots + raised-cosine FIR), RSRP, linear
+//                        interpolation to every RE of the allocation; then the
+//                        noise energy per CDM group
+//                        (port_channel_estimator_average_impl.cpp:130-506).
+//   chest_ta_kernel<N>   one workgroup per (grid, port): the N-point IDFT of every
+//                        (layer, LSE symbol) slice of smoothed pilots with the
+//                        fused Stockham engine, |.|^2 accumulated in LDS, peak
+//                        search and quadratic refinement
+//                        (time_alignment_estimator_dft_impl.cpp:122-310), and the
+//                        per-port measurements (noise variance, EPRE, RSRP, SNR, CFO).
+//   chest_expand_kernel  one thread per output RE: the time-domain strategy
+//                        (average or interpolation between DM-RS symbols), bf16
+//                        rounding and the CFO phase of the symbol -- the only
+//                        HBM-heavy step (4 bytes per RE x layer x port written).
+// Complex products follow the reference's AVX2+FMA srsran_simd_cf_prod
+// (re = fma(a.re, b.re, -a.im b.im), im = fma(a.re, b.im, a.im b.re)); sums
+// are reassociated by the reductions (float tolerance).
+#include <hip/hip_runtime.h>
+
+#include "dft_engine.h"
+#include "gold_sequence.h"
+#include "pusch_chest_args.h"
+
+#pragma clang fp contract(off)
+
+namespace srs_amd {
+namespace {
+
+constexpr float TWOPI_F = 6.28318530717958647692f;
+constexpr float AMP     = 0.70710678118654752440f; // M_SQRT1_2 as float
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b)
+{
+  return make_float2(__builtin_fmaf(a.x, b.x, -(a.y * b.y)), __builtin_fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) // a * conj(b)
+{
+  return cmul(a, make_float2(b.x, -b.y));
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b)
+{
+  return make_float2(a.x + b.x, a.y + b.y);
+}
+__device__ __forceinline__ float2 csub(float2 a, float2 b)
+{
+  return make_float2(a.x - b.x, a.y - b.y);
+}
+__device__ __forceinline__ float2 cscale(float2 a, float s)
+{
+  return make_float2(a.x * s, a.y * s);
+}
+__device__ __forceinline__ float2 from_cbf16(uint32_t u)
+{
+  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+}
+__device__ __forceinline__ uint32_t bf16_bits(float f)
+{
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+__device__ __forceinline__ uint32_t to_cbf16(float2 v)
+{
+  return bf16_bits(v.x) | (bf16_bits(v.y) << 16);
+}
+__device__ __forceinline__ float2 polar1(float theta)
+{
+  float s, c;
+  sincosf(theta, &s, &c);
+  return make_float2(c, s);
+}
+
+// rx[g][d][k] with runtime indices through selects (no dynamic register indexing).
+__device__ __forceinline__ float2 rx_sel(const float2 (&rx)[2][CH_MAXDMRS][CH_PPT], int g, int d, int k)
+{
+  float2 r = rx[0][0][0];
+#pragma unroll
+  for (int gg = 0; gg < 2; ++gg) {
+#pragma unroll
+    for (int dd = 0; dd < CH_MAXDMRS; ++dd) {
+#pragma unroll
+      for (int kk = 0; kk < CH_PPT; ++kk) {
+        r = (gg == g && dd == d && kk == k) ? rx[gg][dd][kk] : r;
+      }
+    }
+  }
+  return r;
+}
+
+// Sum of 4 floats over the workgroup (result broadcast). red: >= 4 * 16 floats.
+__device__ float4 block_sum4(float4 v, float* red)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v.x += __shfl_xor(v.x, o);
+    v.y += __shfl_xor(v.y, o);
+    v.z += __shfl_xor(v.z, o);
+    v.w += __shfl_xor(v.w, o);
+  }
+  const int wave = threadIdx.x / 64, nw = blockDim.x / 64;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[4 * wave + 0] = v.x;
+    red[4 * wave + 1] = v.y;
+    red[4 * wave + 2] = v.z;
+    red[4 * wave + 3] = v.w;
+  }
+  __syncthreads();
+  float4 r = make_float4(0, 0, 0, 0);
+  for (int w = 0; w < nw; ++w) {
+    r.x += red[4 * w + 0];
+    r.y += red[4 * w + 1];
+    r.z += red[4 * w + 2];
+    r.w += red[4 * w + 3];
+  }
+  return r;
+}
+
+// Pilot of layer v at DM-RS symbol d, index m (dmrs_pusch_estimator_impl.cpp:72-184): amplitude
+// M_SQRT1_2, w_f = -1 on odd indices of odd layers (w_t = +1 for layers < 4).
+__device__ __forceinline__ float2 pilot(const uint32_t (*seq)[CH_SEQWORDS], uint32_t bit0, int d, int v, uint32_t m)
+{
+  const uint32_t b  = bit0 + 2 * m;
+  const uint32_t c0 = (seq[d][b >> 5] >> (b & 31)) & 1u;
+  const uint32_t c1 = (seq[d][(b + 1) >> 5] >> ((b + 1) & 31)) & 1u;
+  float2         p  = make_float2(c0 ? -AMP : AMP, c1 ? -AMP : AMP);
+  if ((v & 1) && (m & 1)) {
+    p = make_float2(-p.x, -p.y);
+  }
+  return p;
+}
+
+// compute_v_pilots (port_channel_estimator_helpers.cpp:334-378), sequential over n <= 12 values.
+__device__ void virtual_pilots(float2* out, const float2* in, int n, bool is_start)
+{
+  float absv[CH_MAXV], argv[CH_MAXV];
+  for (int i = 0; i < n; ++i) {
+    absv[i] = sqrtf(in[i].x * in[i].x + in[i].y * in[i].y);
+    argv[i] = atan2f(in[i].y, in[i].x);
+  }
+  // unwrap_list (unwrap.cpp:42-62)
+  const float width = 3.14159265358979323846f;
+  float       k     = 0;
+  for (int i = 0; i < n - 1; ++i) {
+    const float old_a = argv[i], next_a = argv[i + 1];
+    argv[i] += 2.0f * k * width;
+    const float jump = next_a - old_a;
+    if (fabsf(jump) > width) {
+      k = k - copysignf(1.0f, jump);
+    }
+  }
+  argv[n - 1] += 2.0f * k * width;
+
+  const float mean_x    = static_cast<float>(n * (n - 1)) / 2.0f / n;
+  const float norm_x_sq = static_cast<float>((n - 1) * n * (2 * n - 1)) / 6.0f;
+  float       sa = 0, sg = 0, ma = 0, mg = 0;
+  for (int i = 0; i < n; ++i) {
+    ma += absv[i];
+    mg += argv[i];
+    sa += absv[i] * static_cast<float>(i);
+    sg += argv[i] * static_cast<float>(i);
+  }
+  ma /= n;
+  mg /= n;
+  sa -= mean_x * ma * n;
+  sa /= (norm_x_sq - n * mean_x * mean_x);
+  sg -= mean_x * mg * n;
+  sg /= (norm_x_sq - n * mean_x * mean_x);
+  const float ia  = ma - sa * mean_x;
+  const float ig  = mg - sg * mean_x;
+  const int   off = is_start ? -n : n;
+  for (int i = 0; i < n; ++i) {
+    const int   iv  = i + off;
+    const float rho = sa * iv + ia;
+    const float ph  = sg * iv + ig + ((rho > 0) ? 0.0f : 3.14159265358979323846f);
+    const float r   = fabsf(rho);
+    out[i]          = make_float2(r * cosf(ph), r * sinf(ph));
+  }
+}
+
+__global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
+{
+  __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
+  __shared__ float2   enl_in[CH_MAXPIL + 2 * CH_MAXV];
+  __shared__ float2   enl_out[CH_MAXPIL + 2 * CH_MAXV];
+  __shared__ float    red[4 * 16];
+  __shared__ float    s_cfo;
+  __shared__ int      s_has_cfo;
+  __shared__ float2   s_rot[CH_MAXDMRS];
+
+  const uint32_t gp   = blockIdx.x; // grid * nof_ports + port
+  const uint32_t grid = gp / a.nof_ports;
+  const uint32_t port = gp % a.nof_ports;
+  const uint32_t tid  = threadIdx.x;
+  const uint32_t npil = a.npil;
+  const int      nds  = static_cast<int>(a.nds);
+  const int      L    = static_cast<int>(a.L);
+
+  // DM-RS Gold words: sequence bits 2 * 6 * prb_lo .. of every DM-RS symbol.
+  const uint32_t bit_first = 12u * a.prb_lo;
+  const uint32_t w_first   = bit_first / 32;
+  const uint32_t nwords    = (bit_first + 2 * npil + 31) / 32 - w_first;
+  for (uint32_t i = tid; i < nwords * static_cast<uint32_t>(nds); i += CH_THREADS) {
+    const uint32_t d = i / nwords, w = i % nwords;
+    seq[d][w]        = gold_word(a.jump, a.c_init[d], 32 * (w_first + w));
+  }
+  const uint32_t bit0 = bit_first - 32 * w_first;
+
+  // Received pilots of the owned indices: rx[g][d][k] at subcarrier 12 prb_lo + 2m + g.
+  const uint32_t* gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc;
+  float2          rx[2][CH_MAXDMRS][CH_PPT];
+  float           epre = 0;
+#pragma unroll
+  for (int k = 0; k < CH_PPT; ++k) {
+    const uint32_t m = tid + k * CH_THREADS;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+#pragma unroll
+      for (int d = 0; d < CH_MAXDMRS; ++d) {
+        float2 v = make_float2(0, 0);
+        if (m < npil && d < nds && g < static_cast<int>(a.ncdm)) {
+          v    = from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 12 * a.prb_lo + 2 * m + g]);
+          epre = __builtin_fmaf(v.x, v.x, __builtin_fmaf(v.y, v.y, epre));
+        }
+        rx[g][d][k] = v;
+      }
+    }
+  }
+  __syncthreads(); // seq ready
+
+  // CFO from the first two DM-RS symbols (preprocess_pilots_and_estimate_cfo, :390-445).
+  if (nds >= 2) {
+    float4 acc = make_float4(0, 0, 0, 0); // (re, im) of CDM group 0, then 1
+#pragma unroll
+    for (int k = 0; k < CH_PPT; ++k) {
+      const uint32_t m = tid + k * CH_THREADS;
+      if (m < npil) {
+        for (int v = 0; v < L; ++v) {
+          const int    g  = v / 2;
+          const float2 p0 = cmulc(rx_sel(rx, g, 0, k), pilot(seq, bit0, 0, v, m));
+          const float2 p1 = cmulc(rx_sel(rx, g, 1, k), pilot(seq, bit0, 1, v, m));
+          const float2 t  = cmulc(p1, p0);
+          if (g == 0) {
+            acc.x += t.x;
+            acc.y += t.y;
+          } else {
+            acc.z += t.x;
+            acc.w += t.y;
+          }
+        }
+      }
+    }
+    acc = block_sum4(acc, red);
+    if (tid == 0) {
+      const float de  = a.epoch[a.dmrs_sym[1]] - a.epoch[a.dmrs_sym[0]];
+      float       cfo = atan2f(acc.y, acc.x) / TWOPI_F / de;
+      if (a.ncdm > 1) {
+        cfo += atan2f(acc.w, acc.z) / TWOPI_F / de;
+      }
+      cfo /= static_cast<float>(a.ncdm);
+      s_cfo     = cfo;
+      s_has_cfo = 1;
+      for (int d = 0; d < nds; ++d) {
+        s_rot[d] = a.compensate_cfo ? polar1(-TWOPI_F * a.epoch[a.dmrs_sym[d]] * cfo) : make_float2(1, 0);
+      }
+    }
+  } else if (tid == 0) {
+    s_cfo     = 0;
+    s_has_cfo = 0;
+    s_rot[0]  = make_float2(1, 0);
+  }
+  __syncthreads();
+  const bool  has_cfo  = s_has_cfo != 0;
+  const bool  rotate   = has_cfo && a.compensate_cfo;
+  const float total    = a.td == SRS_AMD_CHEST_TD_AVERAGE ? (1.0f / a.beta) / static_cast<float>(nds) : 1.0f / a.beta;
+  const float rsrp_nrm = a.beta * a.beta * static_cast<float>(nds) / static_cast<float>(a.nof_lse);
+  // Pair averaging (average_pairs): one DM-RS symbol -> layers of two-layer CDM groups; more -> every layer if L > 1.
+  float2* filt = a.filt + static_cast<uint64_t>(gp) * a.L * a.nof_lse * npil;
+  float2* freq = a.freq + static_cast<uint64_t>(gp) * a.L * a.nof_lse * a.nof_re;
+  float   rsrp = 0;
+
+  for (int v = 0; v < L; ++v) {
+    const int  g        = v / 2;
+    const bool pair_avg = nds == 1 ? (2 * g + 2 <= L) : (L > 1);
+    for (int s = 0; s < static_cast<int>(a.nof_lse); ++s) {
+      float2 x[CH_PPT];
+#pragma unroll
+      for (int k = 0; k < CH_PPT; ++k) {
+        const uint32_t m = tid + k * CH_THREADS;
+        float2         y = make_float2(0, 0);
+        if (m < npil) {
+          if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
+            y = cmulc(rx_sel(rx, g, 0, k), pilot(seq, bit0, 0, v, m));
+            if (rotate) {
+              y = cmul(y, s_rot[0]);
+            }
+            for (int d = 1; d < nds; ++d) {
+              float2 t = cmulc(rx_sel(rx, g, d, k), pilot(seq, bit0, d, v, m));
+              if (rotate) {
+                t = cmul(t, s_rot[d]);
+              }
+              y = cadd(y, t);
+            }
+          } else {
+            y = cmulc(rx_sel(rx, g, s, k), pilot(seq, bit0, s, v, m));
+            if (rotate) {
+              y = cmul(y, s_rot[s]);
+            }
+          }
+        }
+        const float2 o = make_float2(__shfl_xor(y.x, 1), __shfl_xor(y.y, 1));
+        if (pair_avg && m < npil) {
+          const float2 sum = (m & 1) ? cadd(o, y) : cadd(y, o);
+          y                = make_float2(sum.x / 2.0f, sum.y / 2.0f);
+        }
+        x[k] = cscale(y, total);
+      }
+
+      // FD smoothing (apply_fd_smoothing, port_channel_estimator_helpers.cpp:213-260).
+      if (a.fd == SRS_AMD_CHEST_FD_MEAN) {
+        float4 sm = make_float4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < CH_PPT; ++k) {
+          if (tid + k * CH_THREADS < npil) {
+            sm.x += x[k].x;
+            sm.y += x[k].y;
+          }
+        }
+        sm              = block_sum4(sm, red);
+        const float2 mu = make_float2(sm.x / npil, sm.y / npil);
+#pragma unroll
+        for (int k = 0; k < CH_PPT; ++k) {
+          x[k] = mu;
+        }
+      } else if (a.fd == SRS_AMD_CHEST_FD_FILTER) {
+        const int nv = a.nof_v;
+        for (uint32_t i = tid; i < npil + 2 * CH_MAXV; i += CH_THREADS) {
+          enl_in[i] = make_float2(0, 0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < CH_PPT; ++k) {
+          const uint32_t m = tid + k * CH_THREADS;
+          if (m < npil) {
+            enl_in[CH_MAXV + m] = x[k];
+          }
+        }
+        __syncthreads();
+        if (tid == 0) {
+          virtual_pilots(enl_in + CH_MAXV - nv, enl_in + CH_MAXV, nv, true);
+        } else if (tid == 64) {
+          virtual_pilots(enl_in + CH_MAXV + npil, enl_in + CH_MAXV + npil - nv, nv, false);
+        }
+        __syncthreads();
+        const int half = a.nof_taps / 2;
+#pragma unroll
+        for (int k = 0; k < CH_PPT; ++k) {
+          const int m = static_cast<int>(tid + k * CH_THREADS);
+          if (m < static_cast<int>(npil)) {
+            float2 acc = make_float2(0, 0);
+            for (int j = 0; j < a.nof_taps; ++j) {
+              const int i = m + j - half; // convolution input index (pilot domain)
+              if (i >= -nv && i < static_cast<int>(npil) + nv) {
+                const float2 in = enl_in[CH_MAXV + i];
+                const float  c  = a.rc[a.nof_taps - 1 - j];
+                acc.x           = acc.x + in.x * c; // srsran_simd_f_mul then _add
+                acc.y           = acc.y + in.y * c;
+              }
+            }
+            x[k] = acc;
+          }
+        }
+      }
+
+      // RSRP, store the smoothed pilots, stage them for the interpolation.
+#pragma unroll
+      for (int k = 0; k < CH_PPT; ++k) {
+        const uint32_t m = tid + k * CH_THREADS;
+        if (m < npil) {
+          rsrp = __builtin_fmaf(x[k].x * x[k].x + x[k].y * x[k].y, rsrp_nrm, rsrp);
+          filt[(static_cast<uint64_t>(v) * a.nof_lse + s) * npil + m] = x[k];
+          enl_out[m]                                                  = x[k];
+        }
+      }
+      __syncthreads();
+      // Linear interpolation (interpolator_linear_impl.cpp): pilots at offset g + 2i.
+      float2* fr = freq + (static_cast<uint64_t>(v) * a.nof_lse + s) * a.nof_re;
+      for (uint32_t kk = tid; kk < a.nof_re; kk += CH_THREADS) {
+        float2 out;
+        if (kk <= static_cast<uint32_t>(g)) {
+          out = enl_out[0];
+        } else {
+          const uint32_t j = (kk - g) / 2, r = (kk - g) % 2;
+          if (j + 1 < npil) {
+            const float2 p0 = enl_out[j], p1 = enl_out[j + 1];
+            out = r ? make_float2((p1.x - p0.x) * 0.5f + p0.x, (p1.y - p0.y) * 0.5f + p0.y) : p0;
+          } else {
+            out = enl_out[npil - 1];
+          }
+        }
+        fr[kk] = out;
+      }
+      __syncthreads(); // enl_in / enl_out reused
+    }
+  }
+
+  // Noise energy per CDM group (estimate_noise, :594-690).
+  float       noise0 = 0, noise1 = 0;
+  const float sf     = a.beta / static_cast<float>(a.nof_lse);
+#pragma unroll
+  for (int k = 0; k < CH_PPT; ++k) {
+    const uint32_t m = tid + k * CH_THREADS;
+    if (m >= npil) {
+      continue;
+    }
+    for (int g = 0; g < static_cast<int>(a.ncdm); ++g) {
+      const int v0 = 2 * g, v1 = min(2 * g + 2, L);
+      float2    sc0 = make_float2(0, 0), sc1 = make_float2(0, 0);
+      for (int v = v0; v < v1; ++v) {
+        const float2* fv = filt + static_cast<uint64_t>(v) * a.nof_lse * npil + m;
+        float2        t  = cscale(fv[0], sf);
+        for (int s = 1; s < static_cast<int>(a.nof_lse); ++s) {
+          t = cadd(cscale(fv[static_cast<uint64_t>(s) * npil], sf), t);
+        }
+        if (v == v0) {
+          sc0 = t;
+        } else {
+          sc1 = t;
+        }
+      }
+      for (int d = 0; d < nds; ++d) {
+        float2 rot = make_float2(1, 0);
+        if (rotate) {
+          rot = polar1(TWOPI_F * a.epoch[a.dmrs_sym[d]] * s_cfo);
+        }
+        float2 pred = cmul(sc0, pilot(seq, bit0, d, v0, m));
+        if (rotate) {
+          pred = cmul(pred, rot);
+        }
+        if (v1 - v0 == 2) {
+          float2 po = cmul(sc1, pilot(seq, bit0, d, v0 + 1, m));
+          if (rotate) {
+            po = cmul(po, rot);
+          }
+          pred = cadd(pred, po);
+        }
+        const float2 n = csub(rx_sel(rx, g, d, k), pred);
+        const float  e = __builtin_fmaf(n.x, n.x, n.y * n.y);
+        if (g == 0) {
+          noise0 += e;
+        } else {
+          noise1 += e;
+        }
+      }
+    }
+  }
+  const float4 tot = block_sum4(make_float4(epre, rsrp, noise0, noise1), red);
+  if (tid == 0) {
+    float* acc  = a.acc + static_cast<uint64_t>(gp) * 8;
+    float  nsum = 0;
+    nsum += (isnormal(tot.z) ? tot.z : 0.0f);
+    if (a.ncdm > 1) {
+      nsum += (isnormal(tot.w) ? tot.w : 0.0f);
+    }
+    acc[0] = tot.x;
+    acc[1] = tot.y;
+    acc[2] = nsum;
+    acc[3] = has_cfo ? 1.0f : 0.0f;
+    acc[4] = s_cfo;
+  }
+}
+
+// Time alignment + per-port measurements, one workgroup per (grid, port).
+template <int N>
+__global__ __launch_bounds__(dft::plan<N>::T) void chest_ta_kernel(chest_args a)
+{
+  using dft::cf;
+  __shared__ cf    lds[dft::lds_complex<N>()];
+  __shared__ float corr[N];
+  const uint32_t   gp   = blockIdx.x;
+  const uint32_t   npil = a.npil;
+  const float2*    filt = a.filt + static_cast<uint64_t>(gp) * a.L * a.nof_lse * npil;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    corr[i] = 0;
+  }
+  __syncthreads();
+  const uint32_t nslices = a.L * a.nof_lse;
+  for (uint32_t sl = 0; sl < nslices; ++sl) {
+    // estimate_time_alignment orders the slices symbol-major; the correlation sum is order-free.
+    const float2* in    = filt + static_cast<uint64_t>(sl) * npil;
+    auto          load  = [&](int i) -> cf {
+      if (i < static_cast<int>(npil)) {
+        const float2 v = in[i];
+        return cf{v.x, v.y};
+      }
+      return cf{0, 0};
+    };
+    auto store = [&](int k, cf v) { corr[k] += v.x * v.x + v.y * v.y; };
+    dft::plan<N>::template engine<+1>::run(lds, reinterpret_cast<const cf*>(a.ta_tw), load, store);
+    __syncthreads();
+  }
+
+  if (threadIdx.x == 0) {
+    // estimate_ta_correlation (time_alignment_estimator_dft_impl.cpp:248-310).
+    const int max_taps = a.ta_max_taps;
+    int       i_d = 0, i_a = 0;
+    float     v_d = corr[0], v_a = corr[N - max_taps];
+    for (int i = 1; i < max_taps; ++i) {
+      if (corr[i] > v_d) {
+        v_d = corr[i];
+        i_d = i;
+      }
+      if (corr[N - max_taps + i] > v_a) {
+        v_a = corr[N - max_taps + i];
+        i_a = i;
+      }
+    }
+    int idx = -(max_taps - i_a);
+    if (v_d >= v_a) {
+      idx = i_d;
+    }
+    double frac = 0.0;
+    if (a.ta_frac) {
+      const int nt = max_taps > 2 ? 5 : 3;
+      float     pk[5];
+      for (int i = 0; i < nt; ++i) {
+        pk[i] = corr[(idx + i + N - nt / 2) % N];
+      }
+      float num, den, corr_f;
+      if (nt == 5) {
+        num    = -0.4f * pk[0] + -0.2f * pk[1] + 0.0f * pk[2] + 0.2f * pk[3] + 0.4f * pk[4];
+        den    = 0.571429f * pk[0] + -0.285714f * pk[1] + -0.571429f * pk[2] + -0.285714f * pk[3] + 0.571429f * pk[4];
+        corr_f = 1.0f;
+      } else {
+        num    = -0.5f * pk[0] + 0.5f * pk[2];
+        den    = 0.5f * pk[0] - pk[1] + 0.5f * pk[2];
+        corr_f = 0.5f;
+      }
+      const float r = -corr_f * num / den;
+      frac          = (isnan(r) || isinf(r) || fabsf(r) > 1.0f) ? 0.0 : static_cast<double>(r);
+    }
+    const double ta_s = (static_cast<double>(idx) + frac) / a.ta_fs;
+    // phy_time_unit::from_seconds (phy_time_unit.h:275-283) -> to_seconds.
+    constexpr double T_C = 1.0 / (480000.0 * 4096.0);
+    const long       tcx = static_cast<long>(ta_s / T_C * 10.0);
+    const long       tc  = tcx / 10 + (tcx % 10) / 5;
+
+    // do_compute tail (port_channel_estimator_average_impl.cpp:160-199).
+    const float* acc   = a.acc + static_cast<uint64_t>(gp) * 8;
+    const float  npilt = static_cast<float>(npil * a.nds);
+    const float  rsrp  = acc[1] / (npilt * static_cast<float>(a.L));
+    const float  epre  = acc[0] / npilt;
+    float        nvar  = acc[2] / (npilt * static_cast<float>(a.ncdm) - 1.0f);
+    nvar               = fmaxf(rsrp / 1e10f, nvar);
+    const float datarp = rsrp * static_cast<float>(a.L) / a.beta / a.beta;
+    const float snr    = isnormal(nvar) ? datarp / nvar : 0.0f;
+
+    srs_amd_chest_port_stats st;
+    st.noise_var        = nvar;
+    st.epre             = epre;
+    st.rsrp             = rsrp;
+    st.snr              = snr;
+    st.time_alignment_s = static_cast<float>(static_cast<double>(tc) * T_C);
+    st.cfo_hz           = acc[3] != 0.0f ? acc[4] * a.scs_hz : __builtin_nanf("");
+    a.stats[gp]         = st;
+  }
+}
+
+// Channel estimates: one thread per (grid, port, layer, symbol, subcarrier). Inside the
+// allocation the time-domain strategy and bf16 rounding; the CFO phase then multiplies the
+// whole OFDM symbol (do_compute, port_channel_estimator_average_impl.cpp:184-193), so REs
+// outside the allocation are rotated in place, as the reference does.
+__global__ __launch_bounds__(256) void chest_expand_kernel(chest_args a)
+{
+  const uint32_t sc = blockIdx.x * 256 + threadIdx.x;
+  if (sc >= a.nsubc) {
+    return;
+  }
+  const uint32_t l    = a.first_symbol + blockIdx.y;
+  const uint32_t gpv  = blockIdx.z; // (grid * nof_ports + port) * L + layer
+  const uint32_t gp   = gpv / a.L;
+  const uint32_t v    = gpv % a.L;
+  const uint32_t grid = gp / a.nof_ports, port = gp % a.nof_ports;
+  const float*   acc  = a.acc + static_cast<uint64_t>(gp) * 8;
+  const bool     rot  = a.compensate_cfo && acc[3] != 0.0f;
+  uint32_t*      est  = a.estimates + grid * a.est_stride +
+                  ((static_cast<uint64_t>(port) * a.L + v) * CH_NSYMB + l) * a.nsubc + sc;
+  const uint32_t kk   = sc - 12 * a.prb_lo; // wraps for sc below the allocation
+  uint32_t       out;
+  if (kk < a.nof_re) {
+    const float2* fr = a.freq + (static_cast<uint64_t>(gp) * a.L + v) * a.nof_lse * a.nof_re + kk;
+    float2        e;
+    if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
+      e = fr[0];
+    } else {
+      const int    i0 = a.td_i0[l];
+      const float2 x0 = fr[static_cast<uint64_t>(i0) * a.nof_re];
+      if (a.td_interp[l]) {
+        const float2 x1 = fr[static_cast<uint64_t>(i0 + 1) * a.nof_re];
+        const float  w  = a.td_w[l];
+        e               = make_float2(__builtin_fmaf(x1.x - x0.x, w, x0.x), __builtin_fmaf(x1.y - x0.y, w, x0.y));
+      } else {
+        e = x0;
+      }
+    }
+    out = to_cbf16(e);
+  } else if (rot) {
+    out = *est;
+  } else {
+    return;
+  }
+  if (rot) {
+    out = to_cbf16(cmul(from_cbf16(out), polar1(TWOPI_F * a.epoch[l] * acc[4])));
+  }
+  *est = out;
+}
+
+} // namespace
+
+hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t stream)
+{
+  const uint32_t nb = nof_grids * a.nof_ports;
+  if (nb == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(chest_pilot_kernel, dim3(nb), dim3(CH_THREADS), 0, stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    return e;
+  }
+  switch (a.ta_n) {
+#define SRS_TA_CASE(NN)                                                                                               \
+  case NN:                                                                                                            \
+    hipLaunchKernelGGL(chest_ta_kernel<NN>, dim3(nb), dim3(dft::plan<NN>::T), 0, stream, a);                         \
+    break;
+    SRS_TA_CASE(128)
+    SRS_TA_CASE(256)
+    SRS_TA_CASE(512)
+    SRS_TA_CASE(1024)
+    SRS_TA_CASE(2048)
+    SRS_TA_CASE(4096)
+#undef SRS_TA_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) {
+    return e;
+  }
+  hipLaunchKernelGGL(chest_expand_kernel, dim3((a.nsubc + 255) / 256, a.nof_symbols, nb * a.L), dim3(256), 0, stream,
+                     a);
+  return hipGetLastError();
+}
+
+} // namespace srs_amd

@@ -1,0 +1,71 @@
+// pusch_chest_args.h -- argument block of the PUSCH DM-RS channel-estimator
+// kernels (pusch_chest.hip), shared with their C-ABI (pusch_chest_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "srsran_amd/pusch_chest.h"
+
+namespace srs_amd {
+
+constexpr int CH_THREADS  = 1024;           // pilot kernel workgroup
+constexpr int CH_MAXPIL   = 2048;           // pilots per DM-RS symbol (type 1: 6 x 275 = 1650)
+constexpr int CH_PPT      = CH_MAXPIL / CH_THREADS;
+constexpr int CH_MAXV     = 12;             // MAX_V_PILOTS
+constexpr int CH_MAXDMRS  = 4;              // DM-RS symbols per slot
+constexpr int CH_MAXL     = 4;              // layers
+constexpr int CH_SEQWORDS = 2 * CH_MAXPIL / 32 + 2;
+constexpr int CH_NSYMB    = 14;
+
+struct chest_args {
+  // inputs / outputs
+  const uint32_t*           grids;
+  uint64_t                  grid_stride;
+  uint32_t*                 estimates;
+  uint64_t                  est_stride;
+  srs_amd_chest_port_stats* stats;
+  // scratch (per grid and port)
+  float2* filt; // [L][nof_lse][npil]
+  float2* freq; // [L][nof_lse][nof_re]
+  float*  acc;  // [8]: epre, rsrp, noise, cfo valid, cfo
+  // constants
+  const uint32_t* jump;    // Gold-sequence jump matrices
+  const float2*   ta_tw;   // W_N^m table of the time-alignment IDFT size
+  uint32_t nof_ports;
+  uint32_t nsubc;
+  uint32_t L;
+  uint32_t ncdm;
+  uint32_t nds;            // DM-RS symbols
+  uint32_t nof_lse;        // 1 (average) or nds
+  uint32_t npil;           // pilots per DM-RS symbol
+  uint32_t nof_re;         // 12 x rb_count
+  uint32_t prb_lo;
+  uint32_t first_symbol;
+  uint32_t nof_symbols;
+  uint32_t dmrs_sym[CH_MAXDMRS];
+  uint32_t c_init[CH_MAXDMRS];
+  float    epoch[CH_NSYMB];
+  float    beta;
+  int32_t  fd;
+  int32_t  td;
+  int32_t  compensate_cfo;
+  int32_t  nof_taps;
+  int32_t  nof_v;          // virtual pilots per side (filter)
+  float    rc[CH_MAXV + 4]; // filter coefficients (<= 15)
+  // time-domain strategy per symbol of the allocation: lse slice i0, weight, interpolate flag
+  int32_t  td_i0[CH_NSYMB];
+  float    td_w[CH_NSYMB];
+  int32_t  td_interp[CH_NSYMB];
+  // time alignment
+  uint32_t ta_n;
+  int32_t  ta_max_taps;
+  int32_t  ta_frac;
+  double   ta_fs;
+  float    scs_hz;
+};
+
+hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t stream);
+
+} // namespace srs_amd

@@ -379,3 +379,19 @@ def test_dmrs_pdsch_matches_reference(case, precoder):
     want = pm.ref_dmrs_pdsch_map(grid0.copy(), precoder=precoder, **kw)
     got = pm.dmrs_pdsch_map(grid0.copy(), **kw)
     np.testing.assert_array_equal(got, want)
+
+
+# ---- PUSCH DM-RS channel estimator (oracle/chest.py vs the reference's classes) ----
+from tests import chest_cases  # noqa: E402
+
+
+@pytest.mark.parametrize("case", chest_cases.CASES, ids=[c[0] for c in chest_cases.CASES])
+def test_pusch_chest_matches_reference(case):
+    from oracle import chest
+
+    grid, kw = chest_cases.case_args(case, seed=1)
+    est0 = chest_cases.stale_estimates(grid.shape, kw["nof_layers"])
+    want, ws = chest.ref_pusch_chest(grid, estimates=est0, **kw)
+    got, gs = chest.pusch_chest(grid, estimates=est0, **kw)
+    chest_cases.assert_estimates_close(got, want, case[0])
+    chest_cases.assert_stats_close(gs, ws, case[0])
