@@ -75,6 +75,8 @@ from .pusch_chest import (  # noqa: F401
     TdInterpolationStrategy,
 )
 
+from .pusch_demodulator import PuschDemodPlan, PuschDemodulator, PuschDemodulatorConfig  # noqa: F401
+
 from .sch import (  # noqa: F401
     PdschEncoder,
     PuschDecoder,

@@ -1,0 +1,348 @@
+// pusch_demod_api.cpp -- C-ABI of the MI355X PUSCH demodulator
+// (include/srsran_amd/pusch_demodulator.h).
+//
+// Host-side logic, once per plan: the data-RE table of pusch_demodulator_impl.cpp:218-262
+// (rb_mask x all 12 REs, or x the REs outside the DM-RS CDM groups without data
+// on DM-RS symbols, dmrs_mapping.h:76-91), the equalizer support check
+// (channel_equalizer_generic_impl.cpp:240-270). Per batch: equalize (fused
+// gather), soft demapping (the modulator object's kernel, modulation.h) and
+// descrambling, three launches on the caller's stream.
+#include "srsran_amd/pusch_demodulator.h"
+
+#include <hip/hip_runtime.h>
+
+#include "api_common.h"
+#include "device_buffer.h"
+#include "gold_sequence.h"
+#include "pusch_demod_args.h"
+#include "srsran_amd/modulation.h"
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+using namespace srs_amd;
+
+struct srs_amd_pusch_demodulator {
+  int                 device = 0;
+  hipStream_t         stream = nullptr;
+  uint32_t*           d_jump = nullptr;
+  srs_amd_modulator*  demapper = nullptr;
+  device_buffer       scratch;
+  device_buffer       host_io;
+  std::mutex          mtx;
+  ~srs_amd_pusch_demodulator()
+  {
+    (void)hipSetDevice(device);
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+    srs_amd_modulator_destroy(demapper);
+    (void)hipFree(d_jump);
+  }
+};
+
+struct srs_amd_pusch_demod_plan {
+  int           device = 0;
+  pusch_eq_args args{};
+  uint32_t      nof_ports   = 0;
+  uint32_t      nof_layers  = 0;
+  uint32_t      nof_symbols = 0;
+  uint32_t      span_subc   = 0;
+  int32_t       qm          = 0;
+  uint32_t      c_init      = 0;
+  uint32_t*     d_table     = nullptr;
+  ~srs_amd_pusch_demod_plan()
+  {
+    (void)hipSetDevice(device);
+    (void)hipFree(d_table);
+  }
+  uint32_t nof_llrs() const { return args.nof_re * nof_layers * (qm < 2 ? 1u : static_cast<uint32_t>(qm)); }
+};
+
+namespace {
+
+bool crb_bit(const uint8_t* mask, uint32_t i)
+{
+  return i < SRS_AMD_MAX_RB && ((mask[i / 8] >> (i % 8)) & 1u);
+}
+
+uint32_t dmrs_prb_mask(uint32_t type, uint32_t nof_cdm_groups_without_data)
+{
+  uint32_t m = 0;
+  for (uint32_t k = 0; k < 12; ++k) {
+    const bool in = type == 1 ? (k % 2) < nof_cdm_groups_without_data : (k % 6) < 2 * nof_cdm_groups_without_data;
+    m |= in ? (1u << k) : 0u;
+  }
+  return m;
+}
+
+bool equalizer_supported(int algorithm, uint32_t ports, uint32_t layers)
+{
+  if ((ports != 1 && ports != 2 && ports != 4) || ports < layers) {
+    return false;
+  }
+  return algorithm == SRS_AMD_EQ_ZF ? (layers >= 1 && layers <= 2) : layers == 1;
+}
+
+} // namespace
+
+extern "C" {
+
+int srs_amd_pusch_demodulator_create(srs_amd_pusch_demodulator** dem, int device)
+{
+  if (dem == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null handle pointer");
+  }
+  *dem   = nullptr;
+  int rc = select_device(device);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  auto* d   = new srs_amd_pusch_demodulator();
+  d->device = device;
+  rc        = srs_amd_modulator_create(&d->demapper, device);
+  if (rc != SRS_AMD_OK) {
+    delete d;
+    return rc;
+  }
+  std::vector<uint32_t> j = gold_jump_tables();
+  hipError_t            e = hipMalloc(&d->d_jump, j.size() * sizeof(uint32_t));
+  if (e == hipSuccess) {
+    e = hipMemcpy(d->d_jump, j.data(), j.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess) {
+    e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+  }
+  if (e != hipSuccess) {
+    delete d;
+    return hip_fail(e, "PUSCH demodulator tables");
+  }
+  *dem = d;
+  return SRS_AMD_OK;
+}
+
+void srs_amd_pusch_demodulator_destroy(srs_amd_pusch_demodulator* dem)
+{
+  delete dem;
+}
+
+int srs_amd_pusch_demod_plan_create(srs_amd_pusch_demodulator*        dem,
+                                    const srs_amd_pusch_demod_config* cfg,
+                                    uint32_t                          nof_subc,
+                                    srs_amd_pusch_demod_plan**        plan,
+                                    uint32_t*                         nof_re)
+{
+  if (dem == nullptr || cfg == nullptr || plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  *plan = nullptr;
+  if (nof_subc == 0 || nof_subc % 12 != 0 || nof_subc > 12 * SRS_AMD_MAX_RB) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of grid subcarriers (i.e., %u).", nof_subc);
+  }
+  const int qm = cfg->modulation;
+  if (!(qm == 0 || qm == 1 || qm == 2 || qm == 4 || qm == 6 || qm == 8)) {
+    return fail(SRS_AMD_EINVAL, "Invalid modulation scheme %d.", qm);
+  }
+  if (!equalizer_supported(cfg->equalizer, cfg->nof_rx_ports, cfg->nof_tx_layers)) {
+    return fail(SRS_AMD_EINVAL,
+                "Invalid combination of channel spatial topology (i.e., %u Rx ports, %u Tx layers) and algorithm.",
+                cfg->nof_rx_ports, cfg->nof_tx_layers);
+  }
+  if (cfg->nof_symbols == 0 || cfg->start_symbol + cfg->nof_symbols > 14) {
+    return fail(SRS_AMD_EINVAL, "Invalid time allocation.");
+  }
+  if ((cfg->dmrs_type != 1 && cfg->dmrs_type != 2) || cfg->nof_cdm_groups_without_data < 1 ||
+      cfg->nof_cdm_groups_without_data > (cfg->dmrs_type == 1 ? 2u : 3u)) {
+    return fail(SRS_AMD_EINVAL, "Invalid DM-RS configuration.");
+  }
+  const uint32_t nof_prb = nof_subc / 12;
+  uint32_t       lo = nof_prb, hi = 0;
+  for (uint32_t c = 0; c < SRS_AMD_MAX_RB; ++c) {
+    if (crb_bit(cfg->crb_mask, c)) {
+      if (c >= nof_prb) {
+        return fail(SRS_AMD_EINVAL, "Allocated RB %u exceeds the grid bandwidth.", c);
+      }
+      lo = std::min(lo, c);
+      hi = c + 1;
+    }
+  }
+  if (hi == 0) {
+    return fail(SRS_AMD_EINVAL, "Empty frequency allocation.");
+  }
+  const uint32_t        dmrs_excl = dmrs_prb_mask(cfg->dmrs_type, cfg->nof_cdm_groups_without_data);
+  std::vector<uint32_t> table(14 * nof_prb, 0);
+  uint32_t              count = 0;
+  for (uint32_t l = 0; l < 14; ++l) {
+    const bool in_time = l >= cfg->start_symbol && l < cfg->start_symbol + cfg->nof_symbols;
+    const bool dmrs    = (cfg->dmrs_symbol_mask >> l) & 1u;
+    for (uint32_t c = 0; c < nof_prb; ++c) {
+      uint32_t m = (in_time && crb_bit(cfg->crb_mask, c)) ? 0xfffu : 0u;
+      if (dmrs) {
+        m &= ~dmrs_excl;
+      }
+      table[l * nof_prb + c] = (count << 12) | m;
+      count += static_cast<uint32_t>(__builtin_popcount(m));
+    }
+  }
+  auto* p         = new srs_amd_pusch_demod_plan();
+  p->device       = dem->device;
+  p->nof_ports    = cfg->nof_rx_ports;
+  p->nof_layers   = cfg->nof_tx_layers;
+  p->nof_symbols  = cfg->nof_symbols;
+  p->span_subc    = (hi - lo) * 12;
+  p->qm           = qm;
+  p->c_init       = cfg->rnti * (1u << 15) + cfg->n_id; // pusch_demodulator_impl.cpp:209
+  pusch_eq_args& a = p->args;
+  a.nof_subc       = nof_subc;
+  a.nof_prb        = nof_prb;
+  a.nof_re         = count;
+  a.first_symbol   = cfg->start_symbol;
+  a.first_subc     = lo * 12;
+  hipError_t e     = hipSetDevice(dem->device);
+  if (e == hipSuccess) {
+    e = hipMalloc(&p->d_table, table.size() * sizeof(uint32_t));
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpy(p->d_table, table.data(), table.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "PUSCH demodulator plan");
+  }
+  a.re_table = p->d_table;
+  *plan      = p;
+  if (nof_re != nullptr) {
+    *nof_re = count;
+  }
+  return SRS_AMD_OK;
+}
+
+void srs_amd_pusch_demod_plan_destroy(srs_amd_pusch_demod_plan* plan)
+{
+  delete plan;
+}
+
+int srs_amd_pusch_demodulate_batch(srs_amd_pusch_demodulator*      dem,
+                                   const srs_amd_pusch_demod_plan* plan,
+                                   const uint32_t*                 d_grids,
+                                   uint64_t                        grid_stride,
+                                   const uint32_t*                 d_estimates,
+                                   uint64_t                        est_stride,
+                                   const srs_amd_chest_port_stats* d_stats,
+                                   int8_t*                         d_llrs,
+                                   uint64_t                        llr_stride,
+                                   uint32_t                        nof_grids,
+                                   void*                           stream)
+{
+  if (dem == nullptr || plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_grids == 0 || plan->args.nof_re == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_grids == nullptr || d_estimates == nullptr || d_stats == nullptr || d_llrs == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  const uint32_t nllr = plan->nof_llrs();
+  const uint64_t plane = 14ull * plan->args.nof_subc;
+  if (nof_grids > 1 && (grid_stride < plan->nof_ports * plane || est_stride < plan->nof_ports * plan->nof_layers * plane ||
+                        llr_stride < nllr)) {
+    return fail(SRS_AMD_EINVAL, "grid, estimate or LLR stride too small");
+  }
+  const size_t nsym  = static_cast<size_t>(nof_grids) * plan->args.nof_re * plan->nof_layers;
+  const size_t bytes = align_up(nsym * 8, 256) + align_up(nsym * 4, 256) + static_cast<size_t>(nof_grids) * nllr;
+  std::lock_guard<std::mutex> lock(dem->mtx);
+  hipError_t                  e = hipSetDevice(dem->device);
+  if (e == hipSuccess) {
+    e = dem->scratch.ensure(bytes);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH demodulator scratch");
+  }
+  auto*         base = dem->scratch.as<uint8_t>();
+  pusch_eq_args a    = plan->args;
+  a.grids            = d_grids;
+  a.grid_stride      = grid_stride;
+  a.estimates        = d_estimates;
+  a.est_stride       = est_stride;
+  a.stats            = d_stats;
+  a.eq_symbols       = reinterpret_cast<float2*>(base);
+  a.eq_noise_vars    = reinterpret_cast<float*>(base + align_up(nsym * 8, 256));
+  int8_t* raw        = reinterpret_cast<int8_t*>(base + align_up(nsym * 8, 256) + align_up(nsym * 4, 256));
+  auto    s          = static_cast<hipStream_t>(stream);
+  e = launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->nof_symbols, plan->span_subc, nof_grids, s);
+  if (e != hipSuccess) {
+    return hip_fail(e, "pusch_equalize_kernel launch");
+  }
+  int rc = srs_amd_demodulate_soft_batch(dem->demapper, raw, reinterpret_cast<const float*>(a.eq_symbols),
+                                         a.eq_noise_vars, static_cast<uint32_t>(nsym), plan->qm, stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  pusch_descramble_args d{};
+  d.in         = raw;
+  d.out        = d_llrs;
+  d.jump       = dem->d_jump;
+  d.out_stride = llr_stride;
+  d.length     = nllr;
+  d.c_init     = plan->c_init;
+  e            = launch_pusch_descramble(d, nof_grids, s);
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_descramble_kernel launch");
+}
+
+int srs_amd_pusch_demodulate(srs_amd_pusch_demodulator*      dem,
+                             const srs_amd_pusch_demod_plan* plan,
+                             const uint32_t*                 grid,
+                             const uint32_t*                 estimates,
+                             const srs_amd_chest_port_stats* stats,
+                             int8_t*                         llrs)
+{
+  if (dem == nullptr || plan == nullptr || grid == nullptr || estimates == nullptr || stats == nullptr ||
+      llrs == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  const size_t grid_bytes = plan->nof_ports * 14ull * plan->args.nof_subc * 4;
+  const size_t est_bytes  = grid_bytes * plan->nof_layers;
+  const size_t st_bytes   = plan->nof_ports * sizeof(srs_amd_chest_port_stats);
+  const size_t nllr       = plan->nof_llrs();
+  hipError_t   e;
+  {
+    std::lock_guard<std::mutex> lock(dem->mtx);
+    e = hipSetDevice(dem->device);
+    if (e == hipSuccess) {
+      e = dem->host_io.ensure(align_up(grid_bytes, 256) + align_up(est_bytes, 256) + align_up(st_bytes, 256) + nllr);
+    }
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH demodulator buffers");
+  }
+  auto* b      = dem->host_io.as<uint8_t>();
+  auto* d_grid = reinterpret_cast<uint32_t*>(b);
+  auto* d_est  = reinterpret_cast<uint32_t*>(b + align_up(grid_bytes, 256));
+  auto* d_st   = reinterpret_cast<srs_amd_chest_port_stats*>(b + align_up(grid_bytes, 256) + align_up(est_bytes, 256));
+  auto* d_llr  = reinterpret_cast<int8_t*>(b + align_up(grid_bytes, 256) + align_up(est_bytes, 256) +
+                                          align_up(st_bytes, 256));
+  e            = hipMemcpyAsync(d_grid, grid, grid_bytes, hipMemcpyHostToDevice, dem->stream);
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(d_est, estimates, est_bytes, hipMemcpyHostToDevice, dem->stream);
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(d_st, stats, st_bytes, hipMemcpyHostToDevice, dem->stream);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH demodulator upload");
+  }
+  int rc = srs_amd_pusch_demodulate_batch(dem, plan, d_grid, 0, d_est, 0, d_st, d_llr, 0, 1, dem->stream);
+  if (rc != SRS_AMD_OK) {
+    (void)hipStreamSynchronize(dem->stream);
+    return rc;
+  }
+  e = hipMemcpyAsync(llrs, d_llr, nllr, hipMemcpyDeviceToHost, dem->stream);
+  if (e == hipSuccess) {
+    e = hipStreamSynchronize(dem->stream);
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH demodulator download");
+}
+
+} // extern "C"

@@ -1,0 +1,42 @@
+// pusch_demod_args.h -- argument blocks of the PUSCH demodulator kernels
+// (pusch_demod.hip), shared with their C-ABI (pusch_demod_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "srsran_amd/pusch_chest.h"
+
+namespace srs_amd {
+
+struct pusch_eq_args {
+  const uint32_t*                 grids;     // cbf16 [grid][port][14][subc]
+  const uint32_t*                 estimates; // cbf16 [grid][port][layer][14][subc]
+  const srs_amd_chest_port_stats* stats;     // [grid][port]
+  const uint32_t*                 re_table;  // [14][nof_prb]: data RE index << 12 | 12-bit mask
+  float2*                         eq_symbols;    // [grid][nof_re][layer]
+  float*                          eq_noise_vars; // [grid][nof_re][layer]
+  uint64_t                        grid_stride;
+  uint64_t                        est_stride;
+  uint32_t                        nof_subc;
+  uint32_t                        nof_prb;
+  uint32_t                        nof_re;
+  uint32_t                        first_symbol;
+  uint32_t                        first_subc;
+};
+
+struct pusch_descramble_args {
+  const int8_t*   in;  // [grid][length]
+  int8_t*         out; // rows of out_stride
+  const uint32_t* jump;
+  uint64_t        out_stride;
+  uint32_t        length;
+  uint32_t        c_init;
+};
+
+hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers,
+                                 uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_grids, hipStream_t stream);
+hipError_t launch_pusch_descramble(const pusch_descramble_args& a, uint32_t nof_grids, hipStream_t stream);
+
+} // namespace srs_amd
