@@ -8,6 +8,9 @@ stop), as the reference benchmark
 tests/benchmarks/phy/upper/channel_coding/ldpc/ldpc_decoder_benchmark.cpp does
 (random +-10 LLR codeblocks, -I 8 -L 384, cb_len = max).
 
+`--workload pipeline` (configs[3] / the BASELINE.json headline metric): the
+full PDSCH + PUSCH slot chain of 100 MHz cells, see bench_pipeline.py.
+
 `--workload ofdm` (configs[2]): one step OFDM-modulates and then demodulates a
 batch of slots of the 100 MHz numerology-1 carrier (273 PRB, 4096-point DFT,
 normal CP): 4 antenna ports x `--slots` slots, cbf16 resource grids to complex
@@ -51,9 +54,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="ldpc", choices=["ldpc", "ofdm"])
+    p.add_argument("--workload", default="ldpc", choices=["ldpc", "ofdm", "pipeline"])
     p.add_argument("--batch", type=int, default=4096, help="ldpc: codeblocks per rank per step")
     p.add_argument("--slots", type=int, default=160, help="ofdm: slots per rank per step (x 4 ports)")
+    p.add_argument("--slots-pipeline", type=int, default=32,
+                   help="pipeline: cells (one slot each) per rank per step")
     p.add_argument("--iters", type=int, default=ITERS)
     p.add_argument("--arith", default="simd", choices=["simd", "generic"])
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -340,8 +345,13 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
-    run = run_ldpc if args.workload == "ldpc" else run_ofdm
-    line = run(args, dist, world, rank, dev)
+    if args.workload == "pipeline":
+        from bench_pipeline import run_pipeline
+
+        line = run_pipeline(args, dist, world, rank, dev, timed, HBM_PEAK_GBS)
+    else:
+        run = run_ldpc if args.workload == "ldpc" else run_ofdm
+        line = run(args, dist, world, rank, dev)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

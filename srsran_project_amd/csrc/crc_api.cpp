@@ -25,6 +25,8 @@ struct srs_amd_crc_calculator {
   hipStream_t stream   = nullptr;
   void*       scratch  = nullptr;
   size_t      scratch_size = 0;
+  uint32_t*   d_acc        = nullptr; // per-row accumulators of the long-row path
+  uint32_t    acc_rows     = 0;
   std::mutex  mtx;
   ~srs_amd_crc_calculator()
   {
@@ -35,6 +37,7 @@ struct srs_amd_crc_calculator {
     }
     (void)hipFree(d_table);
     (void)hipFree(scratch);
+    (void)hipFree(d_acc);
   }
 };
 
@@ -67,6 +70,20 @@ int launch(srs_amd_crc_calculator* crc, uint32_t* d_out, uint8_t* d_bits, uint32
   a.order     = static_cast<uint32_t>(crc->order);
   a.attach    = attach ? 1 : 0;
   hipError_t e = hipSetDevice(crc->device);
+  if (e == hipSuccess && crc_needs_accumulator(nof_bits)) {
+    // One accumulator per row (the caller holds crc->mtx); grown only (hipFree waits for
+    // the device), calls on one calculator are serialised by the caller's stream order.
+    if (crc->acc_rows < nof_rows) {
+      (void)hipFree(crc->d_acc);
+      crc->d_acc    = nullptr;
+      crc->acc_rows = 0;
+      e             = hipMalloc(&crc->d_acc, sizeof(uint32_t) * nof_rows);
+      if (e == hipSuccess) {
+        crc->acc_rows = nof_rows;
+      }
+    }
+    a.acc = crc->d_acc;
+  }
   if (e == hipSuccess) {
     e = launch_crc(a, nof_rows, stream);
   }

@@ -34,7 +34,7 @@ struct srs_amd_pusch_decoder {
   srs_amd_crc_calculator*      crc[3] = {nullptr, nullptr, nullptr}; // CRC16, CRC24A, CRC24B
   srs_amd_ldpc_rate_dematcher* dm     = nullptr;
   srs_amd_ldpc_decoder*        dec[2] = {nullptr, nullptr}; // force_decoding 0 / 1
-  device_buffer                soft, msgs, iters, checks, arrays, results, host_io;
+  device_buffer                soft, msgs, iters, checks, arrays, results, host_io, tb_acc;
   std::vector<uint32_t>        h_arrays;
   srs_amd_sch_plan             key_plan{};
   uint32_t                     key_tbs = 0, key_stride = 0;
@@ -110,6 +110,9 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   if (he == hipSuccess) {
     he = d->arrays.ensure(sizeof(uint32_t) * 2 * rows);
   }
+  if (he == hipSuccess) {
+    he = d->tb_acc.ensure(sizeof(uint32_t) * nof_tbs);
+  }
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH decoder scratch");
   }
@@ -177,6 +180,7 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   a.results        = d_results;
   a.cb_iterations  = d_cb_iterations;
   a.crc24a_table   = crc_device_table(d->crc[1]);
+  a.acc            = d->tb_acc.as<uint32_t>();
   a.lay            = lay;
   a.msg_stride     = msg_stride;
   a.tb_stride      = tb_stride;

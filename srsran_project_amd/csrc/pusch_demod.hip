@@ -84,23 +84,31 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
   }
 }
 
+// 8192 LLRs per workgroup: the 256 Gold words into LDS (one jump-ahead per thread), then each thread
+// flips 4 consecutive LLRs per pass, so consecutive lanes touch consecutive bytes.
 __global__ __launch_bounds__(256) void pusch_descramble_kernel(pusch_descramble_args a)
 {
-  const uint32_t w  = blockIdx.x * 256 + threadIdx.x;
-  const uint32_t gi = blockIdx.y;
-  if (w * 32 >= a.length) {
-    return;
+  __shared__ uint32_t words[256];
+  const uint32_t      gi    = blockIdx.y;
+  const uint32_t      base  = blockIdx.x * 256 * 32; // first LLR of the workgroup
+  const uint32_t      wfrst = blockIdx.x * 256;
+  if (base + threadIdx.x * 32 < a.length) {
+    words[threadIdx.x] = gold_word(a.jump, a.c_init, (wfrst + threadIdx.x) * 32);
   }
-  const uint32_t c   = gold_word(a.jump, a.c_init, w * 32);
-  const int8_t*  in  = a.in + static_cast<uint64_t>(gi) * a.length;
-  int8_t*        out = a.out + gi * a.out_stride;
-  for (int b = 0; b < 32; ++b) {
-    const uint32_t i = w * 32 + b;
-    if (i >= a.length) {
-      break;
+  __syncthreads();
+  const int8_t* in  = a.in + static_cast<uint64_t>(gi) * a.length;
+  int8_t*       out = a.out + gi * a.out_stride;
+  for (uint32_t q = threadIdx.x; q < 256 * 8; q += 256) {
+    const uint32_t i0 = base + 4 * q;
+    const uint32_t c  = words[q >> 3] >> (4 * (q & 7));
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t i = i0 + b;
+      if (i < a.length) {
+        const int v = in[i];
+        out[i]      = static_cast<int8_t>(((c >> b) & 1u) ? -v : v);
+      }
     }
-    const int v = in[i];
-    out[i]      = static_cast<int8_t>(((c >> b) & 1u) ? -v : v);
   }
 }
 
@@ -132,8 +140,8 @@ hipError_t launch_pusch_descramble(const pusch_descramble_args& a, uint32_t nof_
   if (a.length == 0 || nof_grids == 0) {
     return hipSuccess;
   }
-  const uint32_t words = (a.length + 31) / 32;
-  hipLaunchKernelGGL(pusch_descramble_kernel, dim3((words + 255) / 256, nof_grids), dim3(256), 0, stream, a);
+  const uint32_t blocks = (a.length + 256 * 32 - 1) / (256 * 32);
+  hipLaunchKernelGGL(pusch_descramble_kernel, dim3(blocks, nof_grids), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

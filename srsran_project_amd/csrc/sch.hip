@@ -4,9 +4,12 @@
 //                    thread per output byte of a (TB, segment) message row.
 //   assemble_kernel  RX tail of pusch_decoder_impl.cpp:309-500: one workgroup per
 //                    TB; CB CRC status + HARQ flags, LDPC statistics, codeblock
-//                    concatenation (concatenate_codeblocks, :460-503) and the
-//                    TB CRC24A check, computed from the concatenated bytes as
-//                    they are produced (block-wide linear CRC, crc_device.h).
+//                    copies of single-codeblock TBs;
+//   asm_tb_kernel    codeblock concatenation (concatenate_codeblocks, :460-503)
+//                    and the TB CRC24A computed from the concatenated bytes as
+//                    they are produced, 8 KiB of a TB per workgroup (linear
+//                    CRC, crc_device.h, partials XOR-ed with atomics);
+//   asm_final_kernel the TB CRC verdict and the HARQ flag reset.
 // Both are byte-gather kernels far below any roofline next to the LDPC
 // kernels they sit between (a few hundred KB per slot).
 #include <hip/hip_runtime.h>
@@ -21,6 +24,8 @@ constexpr int SEG_THREADS = 256;
 constexpr int ASM_THREADS = 256;
 constexpr uint32_t CRC24A_POLY = 0x1864cfb;
 constexpr uint32_t SCH_MAX_SEGMENTS = 512;
+constexpr uint32_t ASM_TB_PER       = 32;                        // TB bytes per thread
+constexpr uint32_t ASM_TB_CHUNK     = ASM_THREADS * ASM_TB_PER;  // TB bytes per workgroup
 
 __device__ __forceinline__ uint32_t bit_at(const uint8_t* b, uint32_t p)
 {
@@ -82,7 +87,6 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
   __shared__ uint32_t s_ok, s_sum, s_min, s_max, s_tb_ok;
   __shared__ uint8_t  s_fresh[SCH_MAX_SEGMENTS]; // decoded in this call (not OK from a previous transmission)
   __shared__ uint8_t  s_cb_ok[SCH_MAX_SEGMENTS];
-  __shared__ uint32_t partial[ASM_THREADS / 64];
   const uint32_t      t = blockIdx.x;
   const uint32_t      C = a.nof_segments;
   if (threadIdx.x == 0) {
@@ -114,8 +118,7 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
   }
   __syncthreads();
   // 2. HARQ: freshly decoded messages and CRC flags into the soft buffer.
-  const uint8_t* src        = a.msgs + static_cast<size_t>(t) * C * a.msg_stride;
-  uint32_t       src_stride = a.msg_stride;
+  const uint8_t* src = a.msgs + static_cast<size_t>(t) * C * a.msg_stride;
   if (a.soft) {
     const uint32_t msg_bytes = a.lay.flag_offset - a.lay.msg_offset;
     for (uint32_t r = 0; r < C; ++r) {
@@ -133,8 +136,7 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
       }
     }
     __syncthreads();
-    src        = a.soft + static_cast<size_t>(t) * C * a.lay.row_bytes + a.lay.msg_offset;
-    src_stride = a.lay.row_bytes;
+    src = a.soft + static_cast<size_t>(t) * C * a.lay.row_bytes + a.lay.msg_offset;
   }
   // 3. Transport block (pusch_decoder_impl.cpp:416-437).
   uint8_t*       tb     = a.tbs + static_cast<size_t>(t) * a.tb_stride;
@@ -149,41 +151,92 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
     if (threadIdx.x == 0) {
       s_tb_ok = all_ok ? 1 : 0;
     }
-  } else if (all_ok) {
-    const tb_gather g{src, src_stride, a.cb_info_bits};
-    for (uint32_t j = threadIdx.x; j < nbytes; j += ASM_THREADS) {
-      tb[j] = static_cast<uint8_t>(g(j));
-    }
-    const uint32_t crc = block_crc_bytes<ASM_THREADS>(g, a.tbs_bits, 24, CRC24A_POLY, a.crc24a_table, partial);
-    if (threadIdx.x == 0) {
-      // Checksum: the 24 bits after the TB data in the last codeblock.
-      const uint32_t off = a.tbs_bits - (C - 1) * a.cb_info_bits;
-      const uint8_t* m   = src + static_cast<size_t>(C - 1) * src_stride;
-      uint32_t       chk = 0;
-      for (uint32_t k = 0; k < 24; ++k) {
-        chk = (chk << 1) | bit_at(m, off + k);
-      }
-      s_tb_ok = crc == chk ? 1 : 0;
-    }
-    __syncthreads();
-    if (!s_tb_ok && a.soft) {
-      // A wrong TB checksum flags a false CB CRC positive: reset every CB (reset_codeblocks_crc).
-      for (uint32_t r = threadIdx.x; r < C; r += ASM_THREADS) {
-        uint8_t* srow = a.soft + static_cast<size_t>(t * C + r) * a.lay.row_bytes;
-        *reinterpret_cast<int32_t*>(srow + a.lay.flag_offset) = 0;
-      }
-    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     srs_amd_pusch_decoder_result res{};
-    res.tb_crc_ok             = static_cast<int32_t>(s_tb_ok);
+    res.tb_crc_ok             = static_cast<int32_t>(s_tb_ok); // C > 1: set by asm_final_kernel
     res.nof_codeblocks_total  = C;
     res.ldpc_iterations_sum   = s_sum;
     res.ldpc_iterations_min   = s_min;
     res.ldpc_iterations_max   = s_max;
     res.nof_codeblocks_crc_ok = s_ok;
     a.results[t]              = res;
+  }
+}
+
+// Source of the concatenated codeblock messages of TB t (the soft-buffer copies when HARQ state is kept).
+__device__ __forceinline__ const uint8_t* asm_source(const assemble_args& a, uint32_t t, uint32_t& stride)
+{
+  const uint32_t C = a.nof_segments;
+  if (a.soft) {
+    stride = a.lay.row_bytes;
+    return a.soft + static_cast<size_t>(t) * C * a.lay.row_bytes + a.lay.msg_offset;
+  }
+  stride = a.msg_stride;
+  return a.msgs + static_cast<size_t>(t) * C * a.msg_stride;
+}
+
+struct tb_gather_write {
+  tb_gather g;
+  uint8_t*  tb;
+  __device__ uint32_t operator()(uint32_t j) const
+  {
+    const uint32_t b = g(j);
+    tb[j]            = static_cast<uint8_t>(b);
+    return b;
+  }
+};
+
+// C > 1, every codeblock OK: concatenation (concatenate_codeblocks, pusch_decoder_impl.cpp:460-503) and
+// TB CRC24A contributions, one workgroup per TB_CHUNK bytes of a TB.
+__global__ __launch_bounds__(ASM_THREADS) void asm_tb_kernel(assemble_args a)
+{
+  __shared__ uint32_t partial[ASM_THREADS / 64];
+  __shared__ uint32_t T[256];
+  const uint32_t      t = blockIdx.y;
+  if (a.results[t].nof_codeblocks_crc_ok != a.nof_segments) {
+    return; // uniform over the workgroup
+  }
+  crc_table8_init<ASM_THREADS>(T, 24, CRC24A_POLY);
+  __syncthreads();
+  uint32_t            stride;
+  const uint8_t*      src = asm_source(a, t, stride);
+  const tb_gather_write f{tb_gather{src, stride, a.cb_info_bits}, a.tbs + static_cast<size_t>(t) * a.tb_stride};
+  const uint32_t      nbytes = a.tbs_bits / 8;
+  const uint32_t      b0     = blockIdx.x * ASM_TB_CHUNK + threadIdx.x * ASM_TB_PER;
+  const uint32_t      b1     = min(nbytes, b0 + ASM_TB_PER);
+  const uint32_t      v      = crc_block_xor<ASM_THREADS>(
+      crc_chunk_contrib(f, b0, b1, a.tbs_bits, 24, CRC24A_POLY, a.crc24a_table, T), partial);
+  if (threadIdx.x == 0 && v != 0) {
+    atomicXor(a.acc + t, v);
+  }
+}
+
+// TB CRC verdict (pusch_decoder_impl.cpp:416-437): the checksum is the 24 bits after the TB data in the
+// last codeblock; a mismatch flags a false CB CRC positive and resets the kept CB flags.
+__global__ __launch_bounds__(64) void asm_final_kernel(assemble_args a, uint32_t nof_tbs)
+{
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t C = a.nof_segments;
+  if (t >= nof_tbs || C == 1 || a.results[t].nof_codeblocks_crc_ok != C) {
+    return;
+  }
+  uint32_t       stride;
+  const uint8_t* src = asm_source(a, t, stride);
+  const uint32_t off = a.tbs_bits - (C - 1) * a.cb_info_bits;
+  const uint8_t* m   = src + static_cast<size_t>(C - 1) * stride;
+  uint32_t       chk = 0;
+  for (uint32_t k = 0; k < 24; ++k) {
+    chk = (chk << 1) | bit_at(m, off + k);
+  }
+  const bool ok           = a.acc[t] == chk;
+  a.results[t].tb_crc_ok  = ok ? 1 : 0;
+  if (!ok && a.soft) {
+    for (uint32_t r = 0; r < C; ++r) {
+      uint8_t* srow = a.soft + static_cast<size_t>(t * C + r) * a.lay.row_bytes;
+      *reinterpret_cast<int32_t*>(srow + a.lay.flag_offset) = 0;
+    }
   }
 }
 
@@ -205,6 +258,22 @@ hipError_t launch_assemble(const assemble_args& a, uint32_t nof_tbs, hipStream_t
     return hipSuccess;
   }
   hipLaunchKernelGGL(assemble_kernel, dim3(nof_tbs), dim3(ASM_THREADS), 0, stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || a.nof_segments == 1) {
+    return e;
+  }
+  e = hipMemsetAsync(a.acc, 0, sizeof(uint32_t) * nof_tbs, stream);
+  if (e != hipSuccess) {
+    return e;
+  }
+  const uint32_t nbytes = a.tbs_bits / 8;
+  hipLaunchKernelGGL(asm_tb_kernel, dim3((nbytes + ASM_TB_CHUNK - 1) / ASM_TB_CHUNK, nof_tbs), dim3(ASM_THREADS), 0,
+                     stream, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) {
+    return e;
+  }
+  hipLaunchKernelGGL(asm_final_kernel, dim3((nof_tbs + 63) / 64), dim3(64), 0, stream, a, nof_tbs);
   return hipGetLastError();
 }
 

@@ -47,6 +47,7 @@ struct assemble_args {
   srs_amd_pusch_decoder_result* results;
   int32_t*                      cb_iterations; // optional per-CB report
   const uint32_t*               crc24a_table; // x^(k+24) mod g(CRC24A)
+  uint32_t*                     acc;          // per-TB CRC accumulators (nof_tbs words of scratch)
   soft_row_layout               lay;
   uint32_t                      msg_stride;
   uint32_t                      tb_stride;

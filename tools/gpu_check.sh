@@ -37,6 +37,9 @@ for s in "$@"; do
     pmc) step pmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline && \
          step pmc2 600 rocprofv3 --kernel-trace --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE SQ_ACTIVE_INST_SCA -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     obench) step bench_ofdm 600 python bench.py --workload ofdm --steps 10 --warmup 2 ;;
+    pbench) step bench_pipe 600 python bench.py --workload pipeline --steps 10 --warmup 2 ;;
+    pbenchq) step bench_pipe 600 python bench.py --workload pipeline --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pprof) step rocprof_pipe 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pipe -o run --output-format csv -- python3 bench.py --workload pipeline --steps 5 --warmup 1 --no-cpu-baseline ;;
     oprof) step rocprof_ofdm 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ofdm -o run --output-format csv -- python3 bench.py --workload ofdm --steps 10 --warmup 2 --no-cpu-baseline ;;
     otraffic) step pmc_fetch_ofdm 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_ofdm -o run --output-format csv -- python3 bench.py --workload ofdm --steps 3 --warmup 1 --no-cpu-baseline && \
               step pmc_write_ofdm 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write_ofdm -o run --output-format csv -- python3 bench.py --workload ofdm --steps 3 --warmup 1 --no-cpu-baseline && \
