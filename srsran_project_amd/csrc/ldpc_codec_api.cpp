@@ -234,14 +234,17 @@ void srs_amd_ldpc_encoder_destroy(srs_amd_ldpc_encoder* encoder)
   destroy_with_stream(encoder);
 }
 
-int srs_amd_ldpc_encode_batch(srs_amd_ldpc_encoder*              enc,
+} // extern "C"
+
+int srs_amd::ldpc_encode_batch_ex(srs_amd_ldpc_encoder*              enc,
                               const srs_amd_ldpc_encoder_config* cfg,
                               const uint8_t*                     d_messages,
                               uint32_t                           msg_stride,
                               uint8_t*                           d_codeblocks,
                               uint32_t                           cb_stride,
                               uint32_t                           nof_cbs,
-                              void*                              stream)
+                              void*                              stream,
+                              uint32_t                           max_bits)
 {
   if (enc == nullptr) {
     return fail(SRS_AMD_EINVAL, "null encoder");
@@ -276,12 +279,34 @@ int srs_amd_ldpc_encode_batch(srs_amd_ldpc_encoder*              enc,
   a.msg_stride = msg_stride;
   a.cw_stride  = cb_stride;
   a.nof_cbs    = nof_cbs;
+  // Rows whose parity columns hold shortened-codeword positions < max_bits (column c at (c - 2) Z).
+  const uint32_t full_bits = static_cast<uint32_t>(g.N_short * Z);
+  max_bits                 = std::min(max_bits, full_bits);
+  const int cols           = static_cast<int>((max_bits + Z - 1) / Z) + 2;
+  a.M_eff                  = std::max(4, std::min(a.M, cols - a.K));
+  a.pack_bits              = max_bits == full_bits ? static_cast<int32_t>(full_bits)
+                                                   : static_cast<int32_t>(std::min(full_bits, (max_bits + 7) / 8 * 8));
   std::lock_guard<std::mutex> lock(enc->mtx);
   hipError_t                  e = hipSetDevice(enc->device);
   if (e == hipSuccess) {
     e = launch_ldpc_encode(a, static_cast<int>(std::min(nof_cbs, ENCODE_GRID_CAP)), static_cast<hipStream_t>(stream));
   }
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_encode_kernel launch");
+}
+
+extern "C" {
+
+int srs_amd_ldpc_encode_batch(srs_amd_ldpc_encoder*              enc,
+                              const srs_amd_ldpc_encoder_config* cfg,
+                              const uint8_t*                     d_messages,
+                              uint32_t                           msg_stride,
+                              uint8_t*                           d_codeblocks,
+                              uint32_t                           cb_stride,
+                              uint32_t                           nof_cbs,
+                              void*                              stream)
+{
+  return ldpc_encode_batch_ex(enc, cfg, d_messages, msg_stride, d_codeblocks, cb_stride, nof_cbs, stream,
+                              0xffffffffu);
 }
 
 int srs_amd_ldpc_encode(srs_amd_ldpc_encoder*              enc,

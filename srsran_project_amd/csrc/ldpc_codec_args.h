@@ -21,6 +21,8 @@ struct encode_args {
   int32_t         Z;
   int32_t         K;         // K_bg
   int32_t         M;         // check rows
+  int32_t         M_eff;     // rows computed: 4 + the extension rows whose parity columns are read
+  int32_t         pack_bits; // leading bits of the shortened codeword written (multiple of 8 or N_short * Z)
   int32_t         N_short;
   int32_t         p0_shift;  // s: p0 = P^-s (sum of lambdas)
   int32_t         core_a[4]; // shift of column K_bg in rows 0..3 (0 where absent)
@@ -50,7 +52,7 @@ struct rate_match_args {
 };
 
 hipError_t launch_ldpc_encode(const encode_args& a, int grid, hipStream_t stream);
-size_t     ldpc_encode_lds_bytes(int K, int M, int Z);
+size_t     ldpc_encode_lds_bytes(int K, int M_eff, int Z);
 hipError_t launch_rate_dematch(const dematch_args& a, hipStream_t stream);
 hipError_t launch_rate_match(const rate_match_args& a, uint32_t max_rm_length, hipStream_t stream);
 

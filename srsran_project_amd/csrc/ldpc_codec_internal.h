@@ -1,6 +1,7 @@
 // ldpc_codec_internal.h -- library-internal entry points of the LDPC rate matching objects.
 #pragma once
 
+#include "srsran_amd/ldpc_encoder.h"
 #include "srsran_amd/ldpc_rate_matching.h"
 
 namespace srs_amd {
@@ -21,5 +22,19 @@ int rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
                           uint32_t                          nof_cbs,
                           void*                             stream,
                           bool                              fresh);
+
+// srs_amd_ldpc_encode_batch producing only the first max_bits of each shortened
+// codeword (the rows of the extension region beyond them are not computed and
+// the codeblock rows are written up to ceil(max_bits / 8) bytes): what a rate
+// matcher reading the circular buffer window [0, max_bits) needs.
+int ldpc_encode_batch_ex(srs_amd_ldpc_encoder*              enc,
+                         const srs_amd_ldpc_encoder_config* cfg,
+                         const uint8_t*                     d_messages,
+                         uint32_t                           msg_stride,
+                         uint8_t*                           d_codeblocks,
+                         uint32_t                           cb_stride,
+                         uint32_t                           nof_cbs,
+                         void*                              stream,
+                         uint32_t                           max_bits);
 
 } // namespace srs_amd

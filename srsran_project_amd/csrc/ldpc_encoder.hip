@@ -19,7 +19,11 @@
 //     lambda_r the systematic part of row r; p1..p3 then follow row by row.
 //   * extension region (rows 4..M-1): row r is an identity on column K_bg + r
 //     and otherwise touches only columns < K_bg + 4: p_(K_bg+r) is the XOR of
-//     that row's other gathers -- all rows independent.
+//     that row's other gathers -- all rows independent.  Only the rows whose
+//     parity columns the rate matcher will read are computed (M_eff), and
+//     only the leading pack_bits of the codeword are written: a high-rate
+//     PDSCH codeblock (R = 0.93) needs 2 of BG1's 42 extension rows, and the
+//     LDS footprint shrinks with them.
 #include <hip/hip_runtime.h>
 
 #include "ldpc_codec_args.h"
@@ -39,7 +43,7 @@ __global__ __launch_bounds__(MAX_LIFTING_SIZE) void ldpc_encode_kernel(encode_ar
   const int Z    = a.Z;
   const int j    = threadIdx.x;
   uint8_t*  cw   = lds;                                    // [N_full][Z] bits, one per byte
-  uint8_t*  lsum = lds + ((a.K + a.M) * Z + 15) / 16 * 16; // [Z]
+  uint8_t*  lsum = lds + ((a.K + a.M_eff) * Z + 15) / 16 * 16; // [Z]
   const int kz   = a.K * Z;
 
   for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
@@ -110,7 +114,7 @@ __global__ __launch_bounds__(MAX_LIFTING_SIZE) void ldpc_encode_kernel(encode_ar
     // 5. Extension region: independent single-parity rows.
     if (j < Z) {
       const int hz = kz + 4 * Z;
-      for (int r = 4; r < a.M; ++r) {
+      for (int r = 4; r < a.M_eff; ++r) {
         uint32_t acc = 0;
         for (int e = a.row_start[r]; e < a.row_start[r + 1]; ++e) {
           const uint32_t ed   = a.edges[e];
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(MAX_LIFTING_SIZE) void ldpc_encode_kernel(encode_ar
 
     // 6. Pack the shortened codeword (drop the first 2Z systematic bits), MSB-first.
     uint8_t*  out   = a.cws + static_cast<size_t>(cb) * a.cw_stride;
-    const int nbits = a.N_short * Z;
+    const int nbits = a.pack_bits;
     const int nb    = (nbits + 7) / 8;
     for (int q = j; q < nb; q += blockDim.x) {
       uint32_t byte = 0;
@@ -145,15 +149,15 @@ __global__ __launch_bounds__(MAX_LIFTING_SIZE) void ldpc_encode_kernel(encode_ar
   }
 }
 
-size_t ldpc_encode_lds_bytes(int K, int M, int Z)
+size_t ldpc_encode_lds_bytes(int K, int M_eff, int Z)
 {
-  return static_cast<size_t>(((K + M) * Z + 15) / 16 * 16 + Z);
+  return static_cast<size_t>(((K + M_eff) * Z + 15) / 16 * 16 + Z);
 }
 
 hipError_t launch_ldpc_encode(const encode_args& a, int grid, hipStream_t stream)
 {
   const int threads = (a.Z + 63) / 64 * 64;
-  hipLaunchKernelGGL(ldpc_encode_kernel, dim3(grid), dim3(threads), ldpc_encode_lds_bytes(a.K, a.M, a.Z), stream, a);
+  hipLaunchKernelGGL(ldpc_encode_kernel, dim3(grid), dim3(threads), ldpc_encode_lds_bytes(a.K, a.M_eff, a.Z), stream, a);
   return hipGetLastError();
 }
 

@@ -16,7 +16,10 @@
 #include "api_common.h"
 #include "crc_internal.h"
 #include "device_buffer.h"
+#include "ldpc_codec_internal.h"
+#include "rate_matching_common.h"
 #include "sch_args.h"
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -147,9 +150,18 @@ int encode_locked(srs_amd_pdsch_encoder* e,
     }
   }
   // 4. LDPC encoding.
+  // Only the circular-buffer window the rate matcher reads, [0, k0 + E + F) capped at Ncb
+  // (ldpc_rate_matcher_impl.cpp:95-130), is encoded.
   srs_amd_ldpc_encoder_config ec{p->base_graph, p->lifting_size, p->Nref};
-  rc = srs_amd_ldpc_encode_batch(e->enc, &ec, e->msgs.as<uint8_t>(), msg_stride, e->coded.as<uint8_t>(), cb_stride,
-                                 rows, stream);
+  rm_geometry                 rg{};
+  uint32_t                    max_bits = 0xffffffffu;
+  if (make_rm_geometry(rg, p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                       p->nof_filler_bits) == nullptr) {
+    const uint64_t window = static_cast<uint64_t>(rg.k0) + std::max(p->rm_length_long, p->rm_length_short) + rg.F;
+    max_bits              = window >= rg.Ncb ? rg.Ncb : static_cast<uint32_t>(window);
+  }
+  rc = ldpc_encode_batch_ex(e->enc, &ec, e->msgs.as<uint8_t>(), msg_stride, e->coded.as<uint8_t>(), cb_stride, rows,
+                            stream, max_bits);
   if (rc != SRS_AMD_OK) {
     return rc;
   }

@@ -12,7 +12,7 @@
 // The per-port noise variances come from the DM-RS estimator's measurements
 // on the device, so the chain needs no host round trip.
 // pusch_descramble_kernel: revert_scrambling (pusch_demodulator_impl.cpp:36-190)
-// 32 LLRs per thread from one jump-ahead Gold word, batched over grids.
+// 8192 LLRs per workgroup from 256 jump-ahead Gold words in LDS, batched over grids.
 #include <hip/hip_runtime.h>
 
 #include "equalizer_device.h"
