@@ -1,15 +1,17 @@
 #!/usr/bin/env python3
 """bench.py -- MI355X PHY hot-path throughput (BASELINE.json configs).
 
-Default workload (`--workload ldpc`, the headline, configs[1]): one "step"
+Default workload (`--workload pipeline`, the BASELINE.json headline metric
+"PDSCH+PUSCH codeblocks/s @ 100 MHz 273-PRB 4x4 MIMO", configs[3]): one step
+runs every cell-slot of a batch through the full PDSCH transmit and PUSCH
+receive chains -- see bench_pipeline.py.
+
+`--workload ldpc` (configs[1], the headline of the decoder alone): one "step"
 decodes one batch of BG1, Z=384 full-length codeblocks (66*384 = 25344 LLRs
 each, rate 1/3, 46 layers) with exactly 8 layered min-sum iterations (no early
 stop), as the reference benchmark
 tests/benchmarks/phy/upper/channel_coding/ldpc/ldpc_decoder_benchmark.cpp does
 (random +-10 LLR codeblocks, -I 8 -L 384, cb_len = max).
-
-`--workload pipeline` (configs[3] / the BASELINE.json headline metric): the
-full PDSCH + PUSCH slot chain of 100 MHz cells, see bench_pipeline.py.
 
 `--workload ofdm` (configs[2]): one step OFDM-modulates and then demodulates a
 batch of slots of the 100 MHz numerology-1 carrier (273 PRB, 4096-point DFT,
@@ -54,7 +56,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="ldpc", choices=["ldpc", "ofdm", "pipeline"])
+    p.add_argument("--workload", default="pipeline", choices=["pipeline", "ldpc", "ofdm"])
     p.add_argument("--batch", type=int, default=4096, help="ldpc: codeblocks per rank per step")
     p.add_argument("--slots", type=int, default=160, help="ofdm: slots per rank per step (x 4 ports)")
     p.add_argument("--slots-pipeline", type=int, default=32,
@@ -348,7 +350,8 @@ def main():
     if args.workload == "pipeline":
         from bench_pipeline import run_pipeline
 
-        line = run_pipeline(args, dist, world, rank, dev, timed, HBM_PEAK_GBS)
+        line = run_pipeline(args, dist, world, rank, dev, timed, HBM_PEAK_GBS,
+                            load_traffic("r01_pipeline_ldpc_traffic.json"))
     else:
         run = run_ldpc if args.workload == "ldpc" else run_ofdm
         line = run(args, dist, world, rank, dev)
