@@ -258,6 +258,7 @@ int srs_amd_ldpc_decode_batch(srs_amd_ldpc_decoder*              d,
   a.edges = d->edges + ((cfg->base_graph - 1) * NOF_LIFTING_SIZES + lifting_size_position(static_cast<int>(Z))) *
                              static_cast<size_t>(MAX_EDGES);
   a.llr_stride      = llr_stride;
+  a.aligned4        = ((reinterpret_cast<uintptr_t>(d_llrs) | llr_stride) & 3u) == 0 ? 1 : 0;
   a.llr_len         = llr_len;
   a.out_stride      = out_stride;
   a.nof_cbs         = nof_cbs;

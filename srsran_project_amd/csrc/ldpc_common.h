@@ -62,6 +62,7 @@ struct decode_args {
   int32_t         nof_filler_bits;
   int32_t         max_iterations;
   int32_t         force_decoding;
+  int32_t         aligned4;     // llrs and llr_stride are multiples of 4 bytes (vector loads)
 };
 
 // Position of a lifting size in the 51-entry list (ldpc.h all_lifting_sizes), -1 if invalid.

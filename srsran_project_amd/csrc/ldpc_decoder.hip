@@ -484,12 +484,61 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
     uint8_t*      out    = a.out + static_cast<size_t>(cb) * a.out_stride;
     const int     obytes = (msg_len + 7) >> 3;
 
-    // ---- input trimming: position of the last non-zero LLR (ldpc_decoder_impl.cpp:86).
+    // ---- input trimming: position of the last non-zero LLR (ldpc_decoder_impl.cpp:86),
+    // fused with the soft-bit load (ldpc_decoder_impl.cpp:160 load_soft_bits) when the rows
+    // allow 4-byte accesses: soft[2Z + i] = clamp(in[i]) for i < B = (n_llrs / Z) Z, in[i]
+    // unclamped for the partial tail node, zero elsewhere.
     if (j == 0) {
       red[0] = -1;
     }
     __syncthreads();
-    {
+    const bool vec4 = a.aligned4 != 0 && (Z & 3) == 0;
+    if (vec4) {
+      const int       nw   = n_llrs >> 2;
+      const int       B4   = (n_llrs / Z) * Z >> 2; // words of full (clamped) nodes
+      const int32_t*  in4  = reinterpret_cast<const int32_t*>(in);
+      lds_i32*        s4   = reinterpret_cast<lds_i32*>(soft);
+      const int       off4 = (2 * Z) >> 2;
+      int             last = -1;
+      for (int w = j; w < off4; w += nthr) {
+        s4[w] = 0;
+      }
+      for (int w = j; w < nw; w += nthr) {
+        const uint32_t v = static_cast<uint32_t>(in4[w]);
+        if (v != 0) {
+          last = 4 * w + (31 - __builtin_clz(v)) / 8;
+        }
+        uint32_t o = v;
+        if (w < B4) {
+          o = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int x = static_cast<int8_t>(v >> (8 * b));
+            o |= (static_cast<uint32_t>(med3_i(x, -SOFT_CLAMP, SOFT_CLAMP)) & 0xffu) << (8 * b);
+          }
+        }
+        s4[off4 + w] = static_cast<int32_t>(o);
+      }
+      // trailing bytes (n_llrs not a multiple of 4), then zeros up to N_FULL Z
+      const int tb0 = nw << 2;
+      if (j < n_llrs - tb0) {
+        const int v = in[tb0 + j];
+        if (v != 0) {
+          last = max(last, tb0 + j);
+        }
+        soft[2 * Z + tb0 + j] = static_cast<int8_t>(v); // inside the partial tail node: unclamped
+      }
+      const int z0 = 2 * Z + n_llrs; // first byte after the data
+      for (int i = z0 + j; i < ((z0 + 3) & ~3) && i < NZ; i += nthr) {
+        soft[i] = 0;
+      }
+      for (int w = ((z0 + 3) >> 2) + j; w < (NZ >> 2); w += nthr) {
+        s4[w] = 0;
+      }
+      if (last >= 0) {
+        __hip_atomic_fetch_max(&red[0], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else {
       int last = -1;
       for (int i = j; i < n_llrs; i += nthr) {
         if (in[i] != 0) {
@@ -520,8 +569,8 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
       continue;
     }
 
-    // ---- load soft bits (ldpc_decoder_impl.cpp:160 load_soft_bits).
-    {
+    if (!vec4) {
+      // ---- load soft bits (ldpc_decoder_impl.cpp:160 load_soft_bits).
       const int nof_full_nodes = n_llrs / Z + 2;
       const int tail           = n_llrs - (nof_full_nodes - 2) * Z;
       for (int node = 0; node < N_FULL; ++node) {
@@ -577,8 +626,22 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
         }
         __syncthreads();
         uint32_t crc = 0, zero = 0;
-        for (int i = jj; i < msg_len; i += nthr) {
-          int sb = soft[i];
+        // four soft bits per LDS read (msg_len = K_bg Z is even; a 2-bit remainder for odd Z)
+        const int nq = msg_len >> 2;
+        for (int q = jj; q < nq; q += nthr) {
+          const uint32_t w4 = static_cast<uint32_t>(reinterpret_cast<lds_i32*>(soft)[q]);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int sb = static_cast<int8_t>(w4 >> (8 * b));
+            const int i  = 4 * q + b;
+            zero |= (sb == 0);
+            if (i < nof_sig && sb <= 0) {
+              crc ^= a.crc_table[nof_sig - 1 - i];
+            }
+          }
+        }
+        for (int i = 4 * nq + jj; i < msg_len; i += nthr) {
+          const int sb = soft[i];
           zero |= (sb == 0);
           if (i < nof_sig && sb <= 0) {
             crc ^= a.crc_table[nof_sig - 1 - i];
@@ -608,11 +671,22 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
     asm volatile("" : "+v"(je));
     for (int b = je; b < obytes; b += nthr) {
       uint32_t byte = 0;
+      if (b * 8 + 8 <= msg_len) {
+        // 8 soft bits from two aligned LDS words; bit k set when soft <= 0
+        const uint32_t w0 = static_cast<uint32_t>(reinterpret_cast<lds_i32*>(soft)[2 * b]);
+        const uint32_t w1 = static_cast<uint32_t>(reinterpret_cast<lds_i32*>(soft)[2 * b + 1]);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        int i = b * 8 + k;
-        if (i < msg_len && soft[i] <= 0) {
-          byte |= 0x80u >> k;
+        for (int k = 0; k < 8; ++k) {
+          const int sb = static_cast<int8_t>((k < 4 ? w0 : w1) >> (8 * (k & 3)));
+          byte |= sb <= 0 ? (0x80u >> k) : 0u;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          int i = b * 8 + k;
+          if (i < msg_len && soft[i] <= 0) {
+            byte |= 0x80u >> k;
+          }
         }
       }
       out[b] = static_cast<uint8_t>(byte);
