@@ -59,7 +59,7 @@ def parse():
     p.add_argument("--workload", default="pipeline", choices=["pipeline", "ldpc", "ofdm"])
     p.add_argument("--batch", type=int, default=4096, help="ldpc: codeblocks per rank per step")
     p.add_argument("--slots", type=int, default=160, help="ofdm: slots per rank per step (x 4 ports)")
-    p.add_argument("--slots-pipeline", type=int, default=32,
+    p.add_argument("--slots-pipeline", type=int, default=64,
                    help="pipeline: cells (one slot each) per rank per step")
     p.add_argument("--iters", type=int, default=ITERS)
     p.add_argument("--arith", default="simd", choices=["simd", "generic"])

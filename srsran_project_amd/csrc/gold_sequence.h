@@ -30,17 +30,30 @@ __device__ __forceinline__ uint32_t gf2_apply(const uint32_t* cols, uint32_t sta
   return r;
 }
 
-// 32 sequence bits c(n0 .. n0+31), c(n0 + b) at bit b.
-__device__ inline uint32_t gold_word(const uint32_t* jump, uint32_t c_init, uint32_t n0)
+// LFSR states advanced by `steps` positions (steps < 2^PRBS_NJUMP): one matrix-vector product per
+// set bit of steps.
+__device__ __forceinline__ void gold_advance(const uint32_t* jump, uint32_t steps, uint32_t& x1, uint32_t& x2)
 {
-  uint32_t       x1 = 1u, x2 = c_init & 0x7fffffffu;
-  const uint32_t n  = n0 + 1600u;
   for (int k = 0; k < PRBS_NJUMP; ++k) {
-    if ((n >> k) & 1u) {
+    if ((steps >> k) & 1u) {
       x1 = gf2_apply(jump + (0 * PRBS_NJUMP + k) * 31, x1);
       x2 = gf2_apply(jump + (1 * PRBS_NJUMP + k) * 31, x2);
     }
   }
+}
+
+// States whose next output is c(n0).
+__device__ __forceinline__ void gold_state(const uint32_t* jump, uint32_t c_init, uint32_t n0, uint32_t& x1,
+                                           uint32_t& x2)
+{
+  x1 = 1u;
+  x2 = c_init & 0x7fffffffu;
+  gold_advance(jump, n0 + 1600u, x1, x2);
+}
+
+// The next 32 outputs from the states (the b-th output at bit b).
+__device__ __forceinline__ uint32_t gold_emit32(uint32_t x1, uint32_t x2)
+{
   uint32_t c = 0;
 #pragma unroll
   for (int b = 0; b < 32; ++b) {
@@ -51,6 +64,34 @@ __device__ inline uint32_t gold_word(const uint32_t* jump, uint32_t c_init, uint
     x2                = (x2 >> 1) | (n2 << 30);
   }
   return c;
+}
+
+// 32 sequence bits c(n0 .. n0+31), c(n0 + b) at bit b.
+__device__ inline uint32_t gold_word(const uint32_t* jump, uint32_t c_init, uint32_t n0)
+{
+  uint32_t x1, x2;
+  gold_state(jump, c_init, n0, x1, x2);
+  return gold_emit32(x1, x2);
+}
+
+// Word t of a block of consecutive sequence words starting at bit n0 (t < 2^(PRBS_NJUMP - 5)):
+// thread 0 jumps to n0 (up to PRBS_NJUMP products) and shares the states through LDS (`base`, 2
+// words); every thread then advances by 32 t bits (log2(t) products instead of PRBS_NJUMP).
+// All threads of the block must call it.
+__device__ inline uint32_t gold_block_word(const uint32_t* jump, uint32_t c_init, uint32_t n0, uint32_t t,
+                                           uint32_t* base)
+{
+  __syncthreads(); // `base` may still be read by a previous call
+  if (threadIdx.x == 0) {
+    uint32_t x1, x2;
+    gold_state(jump, c_init, n0, x1, x2);
+    base[0] = x1;
+    base[1] = x2;
+  }
+  __syncthreads();
+  uint32_t x1 = base[0], x2 = base[1];
+  gold_advance(jump, 32u * t, x1, x2);
+  return gold_emit32(x1, x2);
 }
 
 } // namespace srs_amd

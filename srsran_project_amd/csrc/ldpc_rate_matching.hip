@@ -115,15 +115,20 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
       }
     }
 
+    // With new data, k0 = 0, no limited-buffer rate matching and an input covering the whole first
+    // pass, every position is copied from the input or set to +inf: the old contents are never needed.
+    const bool read_old = !a.fresh && !(a.new_data && E >= L1 && g.k0 == 0 && g.Ncb == g.N);
+    const bool vec_out  = ((reinterpret_cast<uintptr_t>(buf) | g.N) & 3u) == 0;
     const uint32_t step = gridDim.x * DEMATCH_THREADS * DEMATCH_PER_THREAD;
     for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < g.N; p0 += step) {
+      uint32_t packed = 0;
 #pragma unroll
       for (int k = 0; k < DEMATCH_PER_THREAD; ++k) {
         const uint32_t p = p0 + k;
         if (p >= g.N) {
           break;
         }
-        int v = a.fresh ? 0 : buf[p];
+        int v = read_old ? buf[p] : 0;
         if (p < zero_end) {
           v = 0;
         }
@@ -149,7 +154,14 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
         if (p >= zero_from) {
           v = 0;
         }
-        buf[p] = static_cast<int8_t>(v);
+        if (vec_out) {
+          packed |= (static_cast<uint32_t>(v) & 0xffu) << (8 * k);
+        } else {
+          buf[p] = static_cast<int8_t>(v);
+        }
+      }
+      if (vec_out) {
+        *reinterpret_cast<uint32_t*>(buf + p0) = packed; // N is a multiple of 4: the word is in range
       }
     }
   }
