@@ -59,6 +59,7 @@ class Pipeline:
         import srsran_project_amd as amd
 
         self.torch, self.dev, self.S = torch, dev, slots
+        self.ul_stream = None
         d = dev.index
         all_crbs = list(range(NPRB))
         # ---- plans -------------------------------------------------------------------------
@@ -164,8 +165,21 @@ class Pipeline:
                                                soft=self.soft, stream=stream)
 
     def step(self, stream):
-        self.pdsch(stream)
-        self.pusch(stream)
+        """One slot of every cell through both chains. The PDSCH (TX) and PUSCH (RX) chains share no data,
+        so they run concurrently on two HIP streams (fork / join with events on `stream`): their small
+        per-TB kernels fill each other's idle CUs."""
+        t = self.torch
+        if self.ul_stream is None:
+            self.ul_stream = t.cuda.Stream(self.dev)
+            self.ev_fork, self.ev_join = t.cuda.Event(), t.cuda.Event()
+        self.ev_fork.record(stream)
+        self.ul_stream.wait_event(self.ev_fork)
+        with t.cuda.stream(stream):
+            self.pdsch(stream)
+        with t.cuda.stream(self.ul_stream):
+            self.pusch(self.ul_stream)
+        self.ev_join.record(self.ul_stream)
+        stream.wait_event(self.ev_join)
 
     def check(self):
         """Fraction of PUSCH transport blocks with TB CRC ok and bit-equal to what the UE sent."""

@@ -3,7 +3,7 @@
 //
 // c(n) = x1(n + 1600) ^ x2(n + 1600); the two 31-bit LFSR states are jumped to
 // n + 1600 with the GF(2) matrices A^(2^k) (columns, built once on the host by
-// gold_jump_tables()), then stepped 32 times.  Same sequence as
+// gold_jump_tables()), then advanced 32 bits at a time with word-parallel shifts (gold_next32).  Same sequence as
 // lib/phy/upper/sequence_generators/pseudo_random_generator_impl.cpp.
 #pragma once
 
@@ -51,19 +51,25 @@ __device__ __forceinline__ void gold_state(const uint32_t* jump, uint32_t c_init
   gold_advance(jump, n0 + 1600u, x1, x2);
 }
 
-// The next 32 outputs from the states (the b-th output at bit b).
+// The next 32 outputs from the states (the b-th output at bit b), word-parallel: with the state
+// s = x(n .. n+30) in bits 0..30, x1(n+31+i) = x1(n+3+i) ^ x1(n+i) gives 28 new bits in one shift/xor
+// (x2: taps 3, 2, 1, 0), a second round the next 4; the states advance by 32.
+__device__ __forceinline__ uint32_t gold_next32(uint32_t& x1, uint32_t& x2)
+{
+  uint64_t a = x1;
+  a |= static_cast<uint64_t>(((a >> 3) ^ a) & 0x0fffffffu) << 31;
+  a |= static_cast<uint64_t>(((a >> 31) ^ (a >> 28)) & 0xfu) << 59;
+  uint64_t b = x2;
+  b |= static_cast<uint64_t>(((b >> 3) ^ (b >> 2) ^ (b >> 1) ^ b) & 0x0fffffffu) << 31;
+  b |= static_cast<uint64_t>(((b >> 31) ^ (b >> 30) ^ (b >> 29) ^ (b >> 28)) & 0xfu) << 59;
+  x1 = static_cast<uint32_t>(a >> 32) & 0x7fffffffu;
+  x2 = static_cast<uint32_t>(b >> 32) & 0x7fffffffu;
+  return static_cast<uint32_t>(a ^ b);
+}
+
 __device__ __forceinline__ uint32_t gold_emit32(uint32_t x1, uint32_t x2)
 {
-  uint32_t c = 0;
-#pragma unroll
-  for (int b = 0; b < 32; ++b) {
-    c |= ((x1 ^ x2) & 1u) << b;
-    const uint32_t n1 = ((x1 >> 3) ^ x1) & 1u;
-    const uint32_t n2 = ((x2 >> 3) ^ (x2 >> 2) ^ (x2 >> 1) ^ x2) & 1u;
-    x1                = (x1 >> 1) | (n1 << 30);
-    x2                = (x2 >> 1) | (n2 << 30);
-  }
-  return c;
+  return gold_next32(x1, x2);
 }
 
 // 32 sequence bits c(n0 .. n0+31), c(n0 + b) at bit b.
@@ -71,26 +77,6 @@ __device__ inline uint32_t gold_word(const uint32_t* jump, uint32_t c_init, uint
 {
   uint32_t x1, x2;
   gold_state(jump, c_init, n0, x1, x2);
-  return gold_emit32(x1, x2);
-}
-
-// Word t of a block of consecutive sequence words starting at bit n0 (t < 2^(PRBS_NJUMP - 5)):
-// thread 0 jumps to n0 (up to PRBS_NJUMP products) and shares the states through LDS (`base`, 2
-// words); every thread then advances by 32 t bits (log2(t) products instead of PRBS_NJUMP).
-// All threads of the block must call it.
-__device__ inline uint32_t gold_block_word(const uint32_t* jump, uint32_t c_init, uint32_t n0, uint32_t t,
-                                           uint32_t* base)
-{
-  __syncthreads(); // `base` may still be read by a previous call
-  if (threadIdx.x == 0) {
-    uint32_t x1, x2;
-    gold_state(jump, c_init, n0, x1, x2);
-    base[0] = x1;
-    base[1] = x2;
-  }
-  __syncthreads();
-  uint32_t x1 = base[0], x2 = base[1];
-  gold_advance(jump, 32u * t, x1, x2);
   return gold_emit32(x1, x2);
 }
 

@@ -81,7 +81,7 @@ __device__ __forceinline__ int llr_sum(int a, int b)
 
 
 constexpr int DEMATCH_THREADS   = 256;
-constexpr int DEMATCH_PER_THREAD = 4;
+constexpr int DEMATCH_PER_THREAD = 16;
 
 __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dematch_args a)
 {
@@ -115,20 +115,29 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
       }
     }
 
-    // With new data, k0 = 0, no limited-buffer rate matching and an input covering the whole first
-    // pass, every position is copied from the input or set to +inf: the old contents are never needed.
-    const bool read_old = !a.fresh && !(a.new_data && E >= L1 && g.k0 == 0 && g.Ncb == g.N);
-    const bool vec_out  = ((reinterpret_cast<uintptr_t>(buf) | g.N) & 3u) == 0;
+    // With new data, k0 = 0 and no limited-buffer rate matching, the first pass covers [0, E + F) (the
+    // walk skips to nof_sys when the input ends in the information part) and the tail zeroing starts
+    // where it stopped: once E >= nof_info nothing of the old contents survives.
+    const bool read_old = !a.fresh && !(a.new_data && E >= g.nof_info && g.k0 == 0 && g.Ncb == g.N);
+    const bool vec      = ((reinterpret_cast<uintptr_t>(buf) | g.N) & 15u) == 0;
     const uint32_t step = gridDim.x * DEMATCH_THREADS * DEMATCH_PER_THREAD;
     for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < g.N; p0 += step) {
-      uint32_t packed = 0;
+      union {
+        uint4  v;
+        int8_t b[16];
+      } old, out;
+      if (read_old && vec) {
+        old.v = *reinterpret_cast<const uint4*>(buf + p0);
+      }
+      // deinterleaver index (i, j) of the previous input, advanced incrementally along the run
+      uint32_t t_prev = 0xfffffffeu, i = 0, j = 0; // t_prev + 1 matches no t
 #pragma unroll
       for (int k = 0; k < DEMATCH_PER_THREAD; ++k) {
         const uint32_t p = p0 + k;
-        if (p >= g.N) {
-          break;
+        if (!vec && p >= g.N) {
+          continue; // vec: N is a multiple of 16, every run is whole
         }
-        int v = read_old ? buf[p] : 0;
+        int v = read_old ? (vec ? old.b[k] : buf[p]) : 0;
         if (p < zero_end) {
           v = 0;
         }
@@ -140,67 +149,120 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
           const uint32_t w = p < g.nof_info ? p : p - g.F;
           uint32_t       t = w >= g.rank0 ? w - g.rank0 : w + L1;
           if (t < ncopy) {
-            uint32_t i, j;
-            j = divK.div(t, i);
-            v = in[i * g.Qm + j];
+            if (t == t_prev + 1) {
+              if (++i == Kq) {
+                i = 0;
+                ++j;
+              }
+            } else {
+              j = divK.div(t, i);
+            }
+            t_prev = t;
+            v      = in[i * g.Qm + j];
             t += g.L;
           }
           for (; t < E; t += g.L) {
-            uint32_t i, j;
-            j = divK.div(t, i);
-            v = llr_sum(in[i * g.Qm + j], v);
+            uint32_t ii, jj;
+            jj = divK.div(t, ii);
+            v  = llr_sum(in[ii * g.Qm + jj], v);
           }
         }
         if (p >= zero_from) {
           v = 0;
         }
-        if (vec_out) {
-          packed |= (static_cast<uint32_t>(v) & 0xffu) << (8 * k);
+        if (vec) {
+          out.b[k] = static_cast<int8_t>(v);
         } else {
           buf[p] = static_cast<int8_t>(v);
         }
       }
-      if (vec_out) {
-        *reinterpret_cast<uint32_t*>(buf + p0) = packed; // N is a multiple of 4: the word is in range
+      if (vec) {
+        *reinterpret_cast<uint4*>(buf + p0) = out.v; // N is a multiple of 16: the run is in range
       }
     }
   }
 }
 
 
-constexpr int RATE_MATCH_THREADS = 256;
+constexpr int      RATE_MATCH_THREADS = 256;
+constexpr uint32_t RM_MAX_CW_BYTES    = 66 * 384 / 8; // circular buffer of BG1, Z = 384
 
-__global__ __launch_bounds__(RATE_MATCH_THREADS) void ldpc_rate_match_kernel(rate_match_args a)
+// Output byte b of the concatenated codeword, bits of segment cb and (when it straddles) the following
+// segments.
+__device__ uint32_t rm_byte(const rate_match_args& a, const fast_div& divL, uint32_t cb, uint32_t b)
 {
   const rm_geometry& g = a.g;
+  uint32_t c = cb, off_c = a.out_offsets[cb], E_c = a.rm_lengths[cb];
+  uint32_t byte = 0;
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t gbit = 8 * b + k;
+    bool           have = true;
+    while (gbit >= off_c + E_c) {
+      if (++c >= a.nof_cbs) {
+        have = false;
+        break;
+      }
+      off_c = a.out_offsets[c];
+      E_c   = a.rm_lengths[c];
+    }
+    if (!have) {
+      break;
+    }
+    if (gbit < off_c) {
+      continue; // gap between segments
+    }
+    const uint32_t o = gbit - off_c;
+    uint32_t       i, j;
+    if (g.Qm == 6) {
+      i = __umulhi(o >> 1, 0xAAAAAAABu) >> 1;
+      j = o - 6 * i;
+    } else {
+      const uint32_t sh = g.Qm == 8 ? 3 : g.Qm == 4 ? 2 : g.Qm == 2 ? 1 : 0;
+      i                 = o >> sh;
+      j                 = o & (g.Qm - 1);
+    }
+    const uint32_t t = j * (E_c / g.Qm) + i;
+    uint32_t       w;
+    divL.div(g.rank0 + t, w);
+    const uint32_t p   = w < g.nof_info ? w : w + g.F;
+    const uint8_t* src = a.cw + static_cast<size_t>(c) * a.cw_stride;
+    byte |= ((src[p >> 3] >> (7 - (p & 7))) & 1u) << (7 - k);
+  }
+  return byte;
+}
+
+// One workgroup per codeblock: the circular buffer (Ncb bits of the packed codeword) is staged in LDS
+// with coalesced loads, then one thread per output byte gathers its 8 bits from LDS (bit selection +
+// interleaver as index arithmetic). A byte straddling the next segment is built from global memory.
+__global__ __launch_bounds__(RATE_MATCH_THREADS) void ldpc_rate_match_kernel(rate_match_args a)
+{
+  __shared__ uint8_t s_cw[RM_MAX_CW_BYTES];
+  const rm_geometry& g = a.g;
   const fast_div     divL(g.L);
+  const uint32_t     cw_bytes = (g.Ncb + 7) / 8;
   for (uint32_t cb = blockIdx.y; cb < a.nof_cbs; cb += gridDim.y) {
     const uint32_t off   = a.out_offsets[cb];
     const uint32_t E     = a.rm_lengths[cb];
     const uint32_t first = (off + 7) / 8;
     const uint32_t last  = (off + E + 7) / 8;
+    const uint32_t whole = (off + E) / 8; // bytes [first, whole) hold only bits of this segment
+    const uint32_t Kq    = E / g.Qm;
+    const uint8_t* src   = a.cw + static_cast<size_t>(cb) * a.cw_stride;
+    __syncthreads(); // s_cw of the previous codeblock is no longer read
+    for (uint32_t x = threadIdx.x; x < cw_bytes; x += RATE_MATCH_THREADS) {
+      s_cw[x] = src[x];
+    }
+    __syncthreads();
     for (uint32_t b = first + blockIdx.x * RATE_MATCH_THREADS + threadIdx.x; b < last;
          b += gridDim.x * RATE_MATCH_THREADS) {
-      uint32_t c = cb, off_c = off, E_c = E;
+      if (b >= whole) {
+        a.out[b] = static_cast<uint8_t>(rm_byte(a, divL, cb, b));
+        continue;
+      }
       uint32_t byte = 0;
+#pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const uint32_t gbit = 8 * b + k;
-        bool           have = true;
-        while (gbit >= off_c + E_c) {
-          if (++c >= a.nof_cbs) {
-            have = false;
-            break;
-          }
-          off_c = a.out_offsets[c];
-          E_c   = a.rm_lengths[c];
-        }
-        if (!have) {
-          break;
-        }
-        if (gbit < off_c) {
-          continue; // gap between segments
-        }
-        const uint32_t o = gbit - off_c;
+        const uint32_t o = 8 * b + k - off;
         uint32_t       i, j;
         if (g.Qm == 6) {
           i = __umulhi(o >> 1, 0xAAAAAAABu) >> 1;
@@ -210,12 +272,15 @@ __global__ __launch_bounds__(RATE_MATCH_THREADS) void ldpc_rate_match_kernel(rat
           i                 = o >> sh;
           j                 = o & (g.Qm - 1);
         }
-        const uint32_t t = j * (E_c / g.Qm) + i;
-        uint32_t       w;
-        divL.div(g.rank0 + t, w);
-        const uint32_t p   = w < g.nof_info ? w : w + g.F;
-        const uint8_t* src = a.cw + static_cast<size_t>(c) * a.cw_stride;
-        byte |= ((src[p >> 3] >> (7 - (p & 7))) & 1u) << (7 - k);
+        uint32_t w = g.rank0 + j * Kq + i;
+        if (w >= g.L) {
+          w -= g.L;
+          if (w >= g.L) {
+            divL.div(w, w); // repetition beyond one more turn
+          }
+        }
+        const uint32_t p = w < g.nof_info ? w : w + g.F;
+        byte |= ((s_cw[p >> 3] >> (7 - (p & 7))) & 1u) << (7 - k);
       }
       a.out[b] = static_cast<uint8_t>(byte);
     }

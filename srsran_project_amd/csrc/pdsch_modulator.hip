@@ -9,7 +9,7 @@
 // subcarrier k; its data-RE index j comes from the per-PRB table (prefix <<
 // 12 | 12-bit mask, built once per plan on the host). The workgroup's data
 // REs are contiguous in the codeword, so it scrambles exactly its bit range
-// into LDS (one Gold word per thread, jump-ahead, no sequential pass), then
+// into LDS (four Gold words per thread: one jump-ahead, then word-parallel steps), then
 // every thread gathers its L x Qm bits, builds the integer points and writes
 // the precoded cbf16 RE of every port (coalesced 4-byte stores).
 //
@@ -89,6 +89,7 @@ __device__ __forceinline__ uint32_t codeword_word(const uint8_t* cw, uint32_t no
 }
 
 constexpr int MAX_WORDS = PDSCH_THREADS + 2; // 256 REs x 4 layers x 8 bits / 32 + 2
+constexpr uint32_t GOLD_RUN = 4;             // Gold words per scrambling thread
 
 __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args a)
 {
@@ -111,8 +112,18 @@ __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args
 
   const uint8_t* cw        = a.codewords + static_cast<uint64_t>(blockIdx.z) * a.cw_stride;
   const uint32_t nof_bytes = (a.nof_bits + 7) / 8;
-  for (uint32_t w = w_lo + threadIdx.x; w < w_hi; w += PDSCH_THREADS) {
-    scrambled[w - w_lo] = codeword_word(cw, nof_bytes, w) ^ gold_word(a.jump, a.c_init, 32 * w);
+  // GOLD_RUN consecutive words per thread: one jump-ahead, then word-parallel LFSR steps
+  const uint32_t nw = w_hi - w_lo;
+  for (uint32_t q = threadIdx.x * GOLD_RUN; q < nw; q += PDSCH_THREADS * GOLD_RUN) {
+    uint32_t x1, x2;
+    gold_state(a.jump, a.c_init, 32 * (w_lo + q), x1, x2);
+#pragma unroll
+    for (uint32_t r = 0; r < GOLD_RUN; ++r) {
+      const uint32_t c = gold_next32(x1, x2);
+      if (q + r < nw) {
+        scrambled[q + r] = codeword_word(cw, nof_bytes, w_lo + q + r) ^ c;
+      }
+    }
   }
   __syncthreads();
 
@@ -178,10 +189,10 @@ __global__ __launch_bounds__(64) void dmrs_pdsch_kernel(dmrs_pdsch_args a)
   // Sequence bits 2 * nd * (crb - reference) .. + 2 * nd - 1 (dmrs_helper.cpp:70-90).
   const uint32_t b0 = 2u * nd * (crb - a.reference_point_k_rb);
   const uint32_t w0 = b0 / 32;
-  uint64_t       c  = gold_word(a.jump, a.c_init[blockIdx.y], 32 * w0);
-  if ((b0 % 32) + 2 * nd > 32) {
-    c |= static_cast<uint64_t>(gold_word(a.jump, a.c_init[blockIdx.y], 32 * (w0 + 1))) << 32;
-  }
+  uint32_t       x1, x2;
+  gold_state(a.jump, a.c_init[blockIdx.y], 32 * w0, x1, x2);
+  uint64_t c = gold_next32(x1, x2);
+  c |= static_cast<uint64_t>(gold_next32(x1, x2)) << 32;
   const uint32_t bits = static_cast<uint32_t>(c >> (b0 % 32));
 
   uint32_t* grid = a.grids + static_cast<uint64_t>(blockIdx.z) * a.grid_stride + l * (a.port_stride / 14);

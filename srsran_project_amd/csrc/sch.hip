@@ -2,12 +2,14 @@
 //
 //   segment_kernel   TX segmentation (ldpc_segmenter_tx_impl.cpp:137-207): one
 //                    thread per output byte of a (TB, segment) message row.
+//   asm_copy_kernel  HARQ message copies into the soft buffer, one thread per
+//                    4 message bytes of the batch;
 //   assemble_kernel  RX tail of pusch_decoder_impl.cpp:309-500: one workgroup per
 //                    TB; CB CRC status + HARQ flags, LDPC statistics, codeblock
 //                    copies of single-codeblock TBs;
 //   asm_tb_kernel    codeblock concatenation (concatenate_codeblocks, :460-503)
 //                    and the TB CRC24A computed from the concatenated bytes as
-//                    they are produced, 8 KiB of a TB per workgroup (linear
+//                    they are produced, 2 KiB of a TB per workgroup (linear
 //                    CRC, crc_device.h, partials XOR-ed with atomics);
 //   asm_final_kernel the TB CRC verdict and the HARQ flag reset.
 // Both are byte-gather kernels far below any roofline next to the LDPC
@@ -24,7 +26,7 @@ constexpr int SEG_THREADS = 256;
 constexpr int ASM_THREADS = 256;
 constexpr uint32_t CRC24A_POLY = 0x1864cfb;
 constexpr uint32_t SCH_MAX_SEGMENTS = 512;
-constexpr uint32_t ASM_TB_PER       = 32;                        // TB bytes per thread
+constexpr uint32_t ASM_TB_PER       = 8;                         // TB bytes per thread
 constexpr uint32_t ASM_TB_CHUNK     = ASM_THREADS * ASM_TB_PER;  // TB bytes per workgroup
 
 __device__ __forceinline__ uint32_t bit_at(const uint8_t* b, uint32_t p)
@@ -71,6 +73,16 @@ struct tb_gather {
     uint32_t b    = 8 * j;
     uint32_t r    = b / cbi;
     uint32_t o    = b - r * cbi;
+    if (o + 8 <= cbi) {
+      // the 8 bits lie in one codeblock: one or two byte loads
+      const uint8_t* m  = base + static_cast<size_t>(r) * stride + (o >> 3);
+      const uint32_t sh = o & 7u;
+      uint32_t       w  = static_cast<uint32_t>(m[0]) << 8;
+      if (sh != 0) {
+        w |= m[1];
+      }
+      return (w >> (8 - sh)) & 0xffu;
+    }
     for (int k = 0; k < 8; ++k) {
       byte |= bit_at(base + static_cast<size_t>(r) * stride, o) << (7 - k);
       if (++o == cbi) {
@@ -81,6 +93,33 @@ struct tb_gather {
     return byte;
   }
 };
+
+// HARQ message copies (pusch_decoder_impl.cpp:334-375): every decoded codeblock not already OK from an
+// earlier transmission stores its message in its soft-buffer row. One thread per 4 message bytes over
+// all codeblocks of the batch; runs before assemble_kernel rewrites the CRC flags it reads.
+__global__ __launch_bounds__(ASM_THREADS) void asm_copy_kernel(assemble_args a, uint32_t nof_cbs, uint32_t nw)
+{
+  const uint32_t x = blockIdx.x * ASM_THREADS + threadIdx.x;
+  if (x >= nof_cbs * nw) {
+    return;
+  }
+  const uint32_t cb   = x / nw;
+  const uint32_t w    = x - cb * nw;
+  uint8_t*       srow = a.soft + static_cast<size_t>(cb) * a.lay.row_bytes;
+  if (!a.new_data && *reinterpret_cast<const int32_t*>(srow + a.lay.flag_offset) != 0) {
+    return; // kept from a previous transmission
+  }
+  const uint32_t msg_bytes = a.lay.flag_offset - a.lay.msg_offset;
+  const uint8_t* m         = a.msgs + static_cast<size_t>(cb) * a.msg_stride;
+  if ((((reinterpret_cast<uintptr_t>(a.soft) | reinterpret_cast<uintptr_t>(a.msgs)) | a.lay.row_bytes |
+        a.lay.msg_offset | a.msg_stride | msg_bytes) & 3u) == 0) {
+    reinterpret_cast<uint32_t*>(srow + a.lay.msg_offset)[w] = reinterpret_cast<const uint32_t*>(m)[w];
+    return;
+  }
+  for (uint32_t j = 4 * w; j < min(msg_bytes, 4 * w + 4); ++j) {
+    srow[a.lay.msg_offset + j] = m[j];
+  }
+}
 
 __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
 {
@@ -117,22 +156,15 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
     atomicMax(&s_max, stat);
   }
   __syncthreads();
-  // 2. HARQ: freshly decoded messages and CRC flags into the soft buffer.
+  // 2. HARQ: CRC flags of the freshly decoded codeblocks into the soft buffer.
   const uint8_t* src = a.msgs + static_cast<size_t>(t) * C * a.msg_stride;
   if (a.soft) {
-    const uint32_t msg_bytes = a.lay.flag_offset - a.lay.msg_offset;
-    for (uint32_t r = 0; r < C; ++r) {
-      if (!s_fresh[r]) {
-        continue;
-      }
-      const uint32_t cb   = t * C + r;
-      uint8_t*       srow = a.soft + static_cast<size_t>(cb) * a.lay.row_bytes;
-      const uint8_t* m    = a.msgs + static_cast<size_t>(cb) * a.msg_stride;
-      for (uint32_t j = threadIdx.x; j < msg_bytes; j += ASM_THREADS) {
-        srow[a.lay.msg_offset + j] = m[j];
-      }
-      if (threadIdx.x == 0) {
-        *reinterpret_cast<int32_t*>(srow + a.lay.flag_offset) = s_cb_ok[r];
+    // the fresh messages were copied by asm_copy_kernel (launched before this kernel, which then
+    // overwrites the flags it read)
+    for (uint32_t r = threadIdx.x; r < C; r += ASM_THREADS) {
+      if (s_fresh[r]) {
+        *reinterpret_cast<int32_t*>(a.soft + static_cast<size_t>(t * C + r) * a.lay.row_bytes + a.lay.flag_offset) =
+            s_cb_ok[r];
       }
     }
     __syncthreads();
@@ -256,6 +288,12 @@ hipError_t launch_assemble(const assemble_args& a, uint32_t nof_tbs, hipStream_t
 {
   if (nof_tbs == 0) {
     return hipSuccess;
+  }
+  if (a.soft) {
+    const uint32_t nw  = (a.lay.flag_offset - a.lay.msg_offset + 3) / 4;
+    const uint32_t ncb = nof_tbs * a.nof_segments;
+    hipLaunchKernelGGL(asm_copy_kernel, dim3((ncb * nw + ASM_THREADS - 1) / ASM_THREADS), dim3(ASM_THREADS), 0,
+                       stream, a, ncb, nw);
   }
   hipLaunchKernelGGL(assemble_kernel, dim3(nof_tbs), dim3(ASM_THREADS), 0, stream, a);
   hipError_t e = hipGetLastError();
