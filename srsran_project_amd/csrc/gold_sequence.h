@@ -16,7 +16,11 @@ namespace srs_amd {
 
 constexpr int PRBS_NJUMP = 24; // jumps by 2^k, k < 24 (sequences up to 2^24 - 1600 bits)
 
-// [2][PRBS_NJUMP][31] jump matrices (columns), x1 then x2.
+constexpr int PRBS_RADIX_DIGITS = 6;                        // 4-bit digits of a jump (24 bits)
+constexpr int PRBS_RADIX_OFF    = 2 * PRBS_NJUMP * 31;      // start of the radix-16 matrices
+
+// [2][PRBS_NJUMP][31] jump matrices A^(2^k) (columns), x1 then x2, followed by the radix-16 matrices
+// [2][PRBS_RADIX_DIGITS][16][31] A^(d 16^k) (d = 0 unused).
 std::vector<uint32_t> gold_jump_tables();
 
 // state' = M * state over GF(2), M given by its 31 columns.
@@ -42,13 +46,37 @@ __device__ __forceinline__ void gold_advance(const uint32_t* jump, uint32_t step
   }
 }
 
+// LFSR states advanced by `steps` (< 2^24) positions: one product per non-zero 4-bit digit (half the
+// products of the binary decomposition).
+__device__ __forceinline__ void gold_advance16(const uint32_t* jump, uint32_t steps, uint32_t& x1, uint32_t& x2)
+{
+  const uint32_t* r = jump + PRBS_RADIX_OFF;
+  for (int k = 0; k < PRBS_RADIX_DIGITS; ++k) {
+    const uint32_t d = (steps >> (4 * k)) & 15u;
+    if (d != 0) {
+      x1 = gf2_apply(r + ((0 * PRBS_RADIX_DIGITS + k) * 16 + d) * 31, x1);
+      x2 = gf2_apply(r + ((1 * PRBS_RADIX_DIGITS + k) * 16 + d) * 31, x2);
+    }
+  }
+}
+
 // States whose next output is c(n0).
 __device__ __forceinline__ void gold_state(const uint32_t* jump, uint32_t c_init, uint32_t n0, uint32_t& x1,
                                            uint32_t& x2)
 {
   x1 = 1u;
   x2 = c_init & 0x7fffffffu;
-  gold_advance(jump, n0 + 1600u, x1, x2);
+  gold_advance16(jump, n0 + 1600u, x1, x2);
+}
+
+// States whose next output is c(n_wave + off), n_wave the same for every lane of the wave: the jump
+// to n_wave runs once per wave on the scalar unit (readfirstlane makes its inputs uniform), each lane
+// then applies one product per set bit of its own offset (a few, against ~12 for a jump from 0).
+__device__ __forceinline__ void gold_state_wave(const uint32_t* jump, uint32_t c_init, uint32_t n_wave, uint32_t off,
+                                                uint32_t& x1, uint32_t& x2)
+{
+  gold_state(jump, __builtin_amdgcn_readfirstlane(c_init), __builtin_amdgcn_readfirstlane(n_wave), x1, x2);
+  gold_advance(jump, off, x1, x2);
 }
 
 // The next 32 outputs from the states (the b-th output at bit b), word-parallel: with the state

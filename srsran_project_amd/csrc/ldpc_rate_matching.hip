@@ -82,9 +82,13 @@ __device__ __forceinline__ int llr_sum(int a, int b)
 
 constexpr int DEMATCH_THREADS   = 256;
 constexpr int DEMATCH_PER_THREAD = 16;
+constexpr uint32_t DEMATCH_LDS   = 24576; // received LLRs of a codeblock staged in LDS up to this length
 
+// One workgroup per codeblock: the codeblock's received LLRs (deinterleaver input) are staged in LDS
+// with coalesced loads when they fit, then each thread produces 16 consecutive soft-buffer bytes.
 __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dematch_args a)
 {
+  __shared__ int8_t  s_in[DEMATCH_LDS];
   const rm_geometry& g = a.g;
   for (uint32_t cb = blockIdx.y; cb < a.nof_cbs; cb += gridDim.y) {
     const uint32_t E   = a.rm_lengths[cb];
@@ -92,6 +96,21 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
     int8_t*        buf = a.soft + static_cast<size_t>(cb) * a.soft_stride;
     const uint32_t Kq  = E / g.Qm;
     const fast_div divK(Kq);
+    const bool     staged = E <= DEMATCH_LDS;
+    if (staged) {
+      __syncthreads(); // s_in of the previous codeblock is no longer read
+      if (((reinterpret_cast<uintptr_t>(in) | E) & 15u) == 0) {
+        for (uint32_t x = threadIdx.x; x < E / 16; x += DEMATCH_THREADS) {
+          reinterpret_cast<uint4*>(s_in)[x] = reinterpret_cast<const uint4*>(in)[x];
+        }
+      } else {
+        for (uint32_t x = threadIdx.x; x < E; x += DEMATCH_THREADS) {
+          s_in[x] = in[x];
+        }
+      }
+      __syncthreads();
+    }
+    auto llr_in = [&](uint32_t idx) -> int { return staged ? s_in[idx] : in[idx]; };
 
     // First loop pass of the reference (copy mode), see the file header.
     const bool     first_pass = a.new_data && E > 0;
@@ -119,15 +138,92 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
     // walk skips to nof_sys when the input ends in the information part) and the tail zeroing starts
     // where it stopped: once E >= nof_info nothing of the old contents survives.
     const bool read_old = !a.fresh && !(a.new_data && E >= g.nof_info && g.k0 == 0 && g.Ncb == g.N);
-    const bool vec      = ((reinterpret_cast<uintptr_t>(buf) | g.N) & 15u) == 0;
+    // soft-buffer rows are 4-byte aligned (HARQ rows carry a message and a flag after the LLRs)
+    const bool vec      = (reinterpret_cast<uintptr_t>(buf) & 3u) == 0 && (g.N & 15u) == 0;
     const uint32_t step = gridDim.x * DEMATCH_THREADS * DEMATCH_PER_THREAD;
+    if (staged && vec && first_pass && E <= L1) {
+      // Single first pass (no combining), branch-free: every position selects between its old value,
+      // zero, +inf (filler) and its input, whose LDS read is always issued at a clamped index.
+      for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < g.N; p0 += step) {
+        union {
+          uint4  v;
+          int8_t b[16];
+        } old, out;
+        // deinterleaver index of the run's first position; along the run t advances by one (i + 1,
+        // wrapping to the next j at Kq) unless the run crosses the filler block or the k0 wrap, where
+        // each position divides on its own
+        auto t_of = [&](uint32_t p) {
+          const uint32_t w = p < g.nof_info ? p : p - g.F;
+          return w >= g.rank0 ? w - g.rank0 : w + L1;
+        };
+        const uint32_t t0     = t_of(p0);
+        const bool     linear = Kq >= DEMATCH_PER_THREAD && t_of(p0 + DEMATCH_PER_THREAD - 1) == t0 + DEMATCH_PER_THREAD - 1 &&
+                            (p0 + DEMATCH_PER_THREAD <= g.nof_info || p0 >= g.nof_sys);
+        uint32_t i0;
+        const uint32_t j0 = divK.div(min(t0, E - 1), i0);
+        uint32_t*      o4 = reinterpret_cast<uint32_t*>(buf + p0);
+        constexpr uint32_t R = DEMATCH_PER_THREAD;
+        if (p0 >= zero_from) {
+          // the whole run lies in the tail zeroing (most of a high-rate codeblock)
+          o4[0] = o4[1] = o4[2] = o4[3] = 0;
+          continue;
+        }
+        if (linear && t0 + R <= E && p0 >= zero_end && p0 + R <= zero_from && p0 + R <= g.Ncb) {
+          // pure copy run: input index advances by Qm, once wrapping to the next interleaver row
+          const uint32_t idx0 = __umul24(i0, g.Qm) + j0;
+          const uint32_t kw   = Kq - i0; // first k in the next row
+#pragma unroll
+          for (uint32_t k = 0; k < R; ++k) {
+            const uint32_t idx = idx0 + __umul24(k, g.Qm) - (k >= kw ? __umul24(Kq, g.Qm) - 1 : 0u);
+            out.b[k]           = s_in[idx];
+          }
+          o4[0] = out.v.x;
+          o4[1] = out.v.y;
+          o4[2] = out.v.z;
+          o4[3] = out.v.w;
+          continue;
+        }
+        old.v = read_old ? make_uint4(o4[0], o4[1], o4[2], o4[3]) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < DEMATCH_PER_THREAD; ++k) {
+          const uint32_t p      = p0 + k;
+          const bool     filler = p >= g.nof_info && p < g.nof_sys;
+          const uint32_t t      = t_of(p);
+          uint32_t       i, j;
+          if (linear) {
+            i = i0 + k;
+            j = j0;
+            if (i >= Kq) {
+              i -= Kq;
+              ++j;
+            }
+            i = t < E ? i : 0u; // past the input: any in-range index (the value is not used)
+            j = t < E ? j : 0u;
+          } else {
+            j = divK.div(min(t, E - 1), i);
+          }
+          const int x = s_in[__umul24(i, g.Qm) + j];
+          int            v = p < zero_end ? 0 : old.b[k];
+          v                = filler ? LLR_INFINITY : v;
+          v                = (!filler && p < g.Ncb && t < E) ? x : v;
+          v                = p >= zero_from ? 0 : v;
+          out.b[k]         = static_cast<int8_t>(v);
+        }
+        o4[0] = out.v.x;
+        o4[1] = out.v.y;
+        o4[2] = out.v.z;
+        o4[3] = out.v.w;
+      }
+      continue;
+    }
     for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < g.N; p0 += step) {
       union {
         uint4  v;
         int8_t b[16];
       } old, out;
       if (read_old && vec) {
-        old.v = *reinterpret_cast<const uint4*>(buf + p0);
+        const uint32_t* o4 = reinterpret_cast<const uint32_t*>(buf + p0);
+        old.v              = make_uint4(o4[0], o4[1], o4[2], o4[3]);
       }
       // deinterleaver index (i, j) of the previous input, advanced incrementally along the run
       uint32_t t_prev = 0xfffffffeu, i = 0, j = 0; // t_prev + 1 matches no t
@@ -158,13 +254,13 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
               j = divK.div(t, i);
             }
             t_prev = t;
-            v      = in[i * g.Qm + j];
+            v      = llr_in(i * g.Qm + j);
             t += g.L;
           }
           for (; t < E; t += g.L) {
             uint32_t ii, jj;
             jj = divK.div(t, ii);
-            v  = llr_sum(in[ii * g.Qm + jj], v);
+            v  = llr_sum(llr_in(ii * g.Qm + jj), v);
           }
         }
         if (p >= zero_from) {
@@ -177,7 +273,11 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
         }
       }
       if (vec) {
-        *reinterpret_cast<uint4*>(buf + p0) = out.v; // N is a multiple of 16: the run is in range
+        uint32_t* o4 = reinterpret_cast<uint32_t*>(buf + p0);
+        o4[0]        = out.v.x;
+        o4[1]        = out.v.y;
+        o4[2]        = out.v.z;
+        o4[3]        = out.v.w;
       }
     }
   }
@@ -289,17 +389,16 @@ __global__ __launch_bounds__(RATE_MATCH_THREADS) void ldpc_rate_match_kernel(rat
 
 hipError_t launch_rate_dematch(const dematch_args& a, hipStream_t stream)
 {
-  const uint32_t per_block = DEMATCH_THREADS * DEMATCH_PER_THREAD;
-  dim3           grid((a.g.N + per_block - 1) / per_block, a.nof_cbs < 65535u ? a.nof_cbs : 65535u);
+  dim3 grid(1, a.nof_cbs < 65535u ? a.nof_cbs : 65535u);
   hipLaunchKernelGGL(ldpc_rate_dematch_kernel, grid, dim3(DEMATCH_THREADS), 0, stream, a);
   return hipGetLastError();
 }
 
 hipError_t launch_rate_match(const rate_match_args& a, uint32_t max_rm_length, hipStream_t stream)
 {
-  const uint32_t bytes = (max_rm_length + 7) / 8 + 1;
-  uint32_t       gx    = (bytes + RATE_MATCH_THREADS - 1) / RATE_MATCH_THREADS;
-  dim3           grid(gx ? gx : 1, a.nof_cbs < 65535u ? a.nof_cbs : 65535u);
+  // one workgroup per codeblock: the staged circular buffer is loaded once
+  (void)max_rm_length;
+  dim3 grid(1, a.nof_cbs < 65535u ? a.nof_cbs : 65535u);
   hipLaunchKernelGGL(ldpc_rate_match_kernel, grid, dim3(RATE_MATCH_THREADS), 0, stream, a);
   return hipGetLastError();
 }

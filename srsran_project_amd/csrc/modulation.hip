@@ -190,7 +190,9 @@ __global__ __launch_bounds__(256) void scramble_bits_kernel(prbs_args a)
   if (w * 32 >= a.length) {
     return;
   }
-  const uint32_t c = gold_word(a.jump, a.c_init, w * 32);
+  uint32_t x1, x2; // the wave's first word is the scalar jump, lanes advance by 32 x lane bits
+  gold_state_wave(a.jump, a.c_init, (w - (threadIdx.x & 63u)) * 32, (threadIdx.x & 63u) * 32, x1, x2);
+  const uint32_t c = gold_next32(x1, x2);
 #pragma unroll
   for (int byte = 0; byte < 4; ++byte) {
     const uint32_t p = w * 4 + byte;
@@ -215,7 +217,9 @@ __global__ __launch_bounds__(256) void descramble_llrs_kernel(prbs_args a)
   if (w * 32 >= a.length) {
     return;
   }
-  const uint32_t c = gold_word(a.jump, a.c_init, w * 32);
+  uint32_t x1, x2; // the wave's first word is the scalar jump, lanes advance by 32 x lane bits
+  gold_state_wave(a.jump, a.c_init, (w - (threadIdx.x & 63u)) * 32, (threadIdx.x & 63u) * 32, x1, x2);
+  const uint32_t c = gold_next32(x1, x2);
   for (int b = 0; b < 32; ++b) {
     const uint32_t i = w * 32 + b;
     if (i >= a.length) {

@@ -120,7 +120,7 @@ uint32_t gf2_apply_host(const uint32_t* cols, uint32_t s)
 
 std::vector<uint32_t> srs_amd::gold_jump_tables()
 {
-  std::vector<uint32_t> t(2 * PRBS_NJUMP * 31);
+  std::vector<uint32_t> t(PRBS_RADIX_OFF + 2 * PRBS_RADIX_DIGITS * 16 * 31, 0u);
   for (int which = 0; which < 2; ++which) {
     uint32_t* m0 = t.data() + (which * PRBS_NJUMP) * 31;
     for (int j = 0; j < 31; ++j) {
@@ -131,6 +131,19 @@ std::vector<uint32_t> srs_amd::gold_jump_tables()
       uint32_t*       cur  = t.data() + (which * PRBS_NJUMP + k) * 31;
       for (int j = 0; j < 31; ++j) {
         cur[j] = gf2_apply_host(prev, prev[j]);
+      }
+    }
+    // radix 16: A^(d 16^k) = A^((d-1) 16^k) A^(16^k), A^(16^k) = the binary matrix 4k
+    for (int k = 0; k < PRBS_RADIX_DIGITS; ++k) {
+      const uint32_t* base = t.data() + (which * PRBS_NJUMP + 4 * k) * 31;
+      uint32_t*       row  = t.data() + PRBS_RADIX_OFF + ((which * PRBS_RADIX_DIGITS + k) * 16) * 31;
+      for (int j = 0; j < 31; ++j) {
+        row[31 + j] = base[j];
+      }
+      for (int d = 2; d < 16; ++d) {
+        for (int j = 0; j < 31; ++j) {
+          row[d * 31 + j] = gf2_apply_host(row + (d - 1) * 31, base[j]);
+        }
       }
     }
   }

@@ -94,6 +94,7 @@ constexpr uint32_t GOLD_RUN = 4;             // Gold words per scrambling thread
 __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args a)
 {
   __shared__ uint32_t scrambled[MAX_WORDS];
+  __shared__ float2   s_qam[256]; // constellation point of every Qm-bit index (qm >= 2)
 
   const uint32_t  l   = a.first_symbol + blockIdx.y;
   const uint32_t  k0  = a.first_subc + blockIdx.x * PDSCH_THREADS;
@@ -112,6 +113,9 @@ __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args
 
   const uint8_t* cw        = a.codewords + static_cast<uint64_t>(blockIdx.z) * a.cw_stride;
   const uint32_t nof_bytes = (a.nof_bits + 7) / 8;
+  if (a.qm >= 2 && threadIdx.x < (1u << a.qm)) {
+    s_qam[threadIdx.x] = qam_point(threadIdx.x, a.qm);
+  }
   // GOLD_RUN consecutive words per thread: one jump-ahead, then word-parallel LFSR steps
   const uint32_t nw = w_hi - w_lo;
   for (uint32_t q = threadIdx.x * GOLD_RUN; q < nw; q += PDSCH_THREADS * GOLD_RUN) {
@@ -150,7 +154,7 @@ __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args
       const uint32_t seq = static_cast<uint32_t>(win >> (o % 32)) & ((1u << bps) - 1u); // bit i = i-th bit
       const uint32_t idx = __builtin_bitreverse32(seq) >> (32 - bps);                    // MSB-first index
       if (a.qm >= 2) {
-        x[v] = qam_point(idx, a.qm);
+        x[v] = s_qam[idx];
       } else {
         const float b = idx ? -1.0f : 1.0f;
         x[v]          = make_float2((a.qm == 0 && (s & 1u)) ? -b : b, b);

@@ -199,6 +199,8 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
   __shared__ float    s_cfo;
   __shared__ int      s_has_cfo;
   __shared__ float2   s_rot[CH_MAXDMRS];
+  __shared__ float2   s_rot_fwd[CH_MAXDMRS];
+  __shared__ uint32_t s_rx[2][CH_MAXDMRS][CH_MAXPIL]; // received pilots (cbf16) of every CDM group / DM-RS symbol
 
   const uint32_t gp   = blockIdx.x; // grid * nof_ports + port
   const uint32_t grid = gp / a.nof_ports;
@@ -220,7 +222,9 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
 
   // Received pilots of the owned indices: rx[g][d][k] at subcarrier 12 prb_lo + 2m + g.
   const uint32_t* gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc;
-  float2          rx[2][CH_MAXDMRS][CH_PPT];
+  // kept in LDS as the raw cbf16 words (lossless) rather than registers: the 1024-thread workgroup
+  // has 128 VGPRs per lane, and 32 of them for the pilots made the kernel spill to scratch
+  auto rxv = [&](int g, int d, int k) { return from_cbf16(s_rx[g][d][tid + k * CH_THREADS]); };
   float           epre = 0;
 #pragma unroll
   for (int k = 0; k < CH_PPT; ++k) {
@@ -229,12 +233,15 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
     for (int g = 0; g < 2; ++g) {
 #pragma unroll
       for (int d = 0; d < CH_MAXDMRS; ++d) {
-        float2 v = make_float2(0, 0);
+        uint32_t u = 0;
         if (m < npil && d < nds && g < static_cast<int>(a.ncdm)) {
-          v    = from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 12 * a.prb_lo + 2 * m + g]);
-          epre = __builtin_fmaf(v.x, v.x, __builtin_fmaf(v.y, v.y, epre));
+          u              = gridp[a.dmrs_sym[d] * a.nsubc + 12 * a.prb_lo + 2 * m + g];
+          const float2 v = from_cbf16(u);
+          epre           = __builtin_fmaf(v.x, v.x, __builtin_fmaf(v.y, v.y, epre));
         }
-        rx[g][d][k] = v;
+        if (m < CH_MAXPIL) {
+          s_rx[g][d][m] = u;
+        }
       }
     }
   }
@@ -249,8 +256,8 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
       if (m < npil) {
         for (int v = 0; v < L; ++v) {
           const int    g  = v / 2;
-          const float2 p0 = cmulc(rx_sel(rx, g, 0, k), pilot(seq, bit0, 0, v, m));
-          const float2 p1 = cmulc(rx_sel(rx, g, 1, k), pilot(seq, bit0, 1, v, m));
+          const float2 p0 = cmulc(rxv(g, 0, k), pilot(seq, bit0, 0, v, m));
+          const float2 p1 = cmulc(rxv(g, 1, k), pilot(seq, bit0, 1, v, m));
           const float2 t  = cmulc(p1, p0);
           if (g == 0) {
             acc.x += t.x;
@@ -273,7 +280,8 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
       s_cfo     = cfo;
       s_has_cfo = 1;
       for (int d = 0; d < nds; ++d) {
-        s_rot[d] = a.compensate_cfo ? polar1(-TWOPI_F * a.epoch[a.dmrs_sym[d]] * cfo) : make_float2(1, 0);
+        s_rot[d]     = a.compensate_cfo ? polar1(-TWOPI_F * a.epoch[a.dmrs_sym[d]] * cfo) : make_float2(1, 0);
+        s_rot_fwd[d] = polar1(TWOPI_F * a.epoch[a.dmrs_sym[d]] * cfo); // the noise predictor's phase
       }
     }
   } else if (tid == 0) {
@@ -302,19 +310,19 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
         float2         y = make_float2(0, 0);
         if (m < npil) {
           if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
-            y = cmulc(rx_sel(rx, g, 0, k), pilot(seq, bit0, 0, v, m));
+            y = cmulc(rxv(g, 0, k), pilot(seq, bit0, 0, v, m));
             if (rotate) {
               y = cmul(y, s_rot[0]);
             }
             for (int d = 1; d < nds; ++d) {
-              float2 t = cmulc(rx_sel(rx, g, d, k), pilot(seq, bit0, d, v, m));
+              float2 t = cmulc(rxv(g, d, k), pilot(seq, bit0, d, v, m));
               if (rotate) {
                 t = cmul(t, s_rot[d]);
               }
               y = cadd(y, t);
             }
           } else {
-            y = cmulc(rx_sel(rx, g, s, k), pilot(seq, bit0, s, v, m));
+            y = cmulc(rxv(g, s, k), pilot(seq, bit0, s, v, m));
             if (rotate) {
               y = cmul(y, s_rot[s]);
             }
@@ -441,10 +449,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
         }
       }
       for (int d = 0; d < nds; ++d) {
-        float2 rot = make_float2(1, 0);
-        if (rotate) {
-          rot = polar1(TWOPI_F * a.epoch[a.dmrs_sym[d]] * s_cfo);
-        }
+        const float2 rot = s_rot_fwd[d];
         float2 pred = cmul(sc0, pilot(seq, bit0, d, v0, m));
         if (rotate) {
           pred = cmul(pred, rot);
@@ -456,7 +461,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
           }
           pred = cadd(pred, po);
         }
-        const float2 n = csub(rx_sel(rx, g, d, k), pred);
+        const float2 n = csub(rxv(g, d, k), pred);
         const float  e = __builtin_fmaf(n.x, n.x, n.y * n.y);
         if (g == 0) {
           noise0 += e;

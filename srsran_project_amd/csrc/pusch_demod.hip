@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
 }
 
 // 8192 LLRs per workgroup: the 256 Gold words into LDS (4 per lane of one wave), then each thread
-// flips 4 consecutive LLRs per pass, so consecutive lanes touch consecutive bytes.
+// flips the 32 LLRs of one word (16-byte vector accesses).
 __global__ __launch_bounds__(256) void pusch_descramble_kernel(pusch_descramble_args a)
 {
   __shared__ uint32_t words[256];
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void pusch_descramble_kernel(pusch_descramble_
   if (threadIdx.x < 64 && base + threadIdx.x * 128 < a.length) {
     // four consecutive words per lane of the first wave: one jump-ahead, then word-parallel steps
     uint32_t x1, x2;
-    gold_state(a.jump, a.c_init, (wfrst + 4 * threadIdx.x) * 32, x1, x2);
+    gold_state_wave(a.jump, a.c_init, wfrst * 32, 4 * threadIdx.x * 32, x1, x2);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       words[4 * threadIdx.x + r] = gold_next32(x1, x2);
@@ -104,16 +104,30 @@ __global__ __launch_bounds__(256) void pusch_descramble_kernel(pusch_descramble_
   __syncthreads();
   const int8_t* in  = a.in + static_cast<uint64_t>(gi) * a.length;
   int8_t*       out = a.out + gi * a.out_stride;
-  for (uint32_t q = threadIdx.x; q < 256 * 8; q += 256) {
-    const uint32_t i0 = base + 4 * q;
-    const uint32_t c  = words[q >> 3] >> (4 * (q & 7));
+  // thread t: the 32 LLRs of Gold word t, two 16-byte loads and stores when aligned and whole
+  const uint32_t i0 = base + 32 * threadIdx.x;
+  const uint32_t c  = words[threadIdx.x];
+  if (i0 + 32 <= a.length && (((reinterpret_cast<uintptr_t>(in + i0)) | reinterpret_cast<uintptr_t>(out + i0)) & 15u) == 0) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const uint32_t i = i0 + b;
-      if (i < a.length) {
-        const int v = in[i];
-        out[i]      = static_cast<int8_t>(((c >> b) & 1u) ? -v : v);
+    for (int h = 0; h < 2; ++h) {
+      union {
+        uint4  v;
+        int8_t b[16];
+      } x;
+      x.v = *reinterpret_cast<const uint4*>(in + i0 + 16 * h);
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        x.b[b] = static_cast<int8_t>(((c >> (16 * h + b)) & 1u) ? -x.b[b] : x.b[b]);
       }
+      *reinterpret_cast<uint4*>(out + i0 + 16 * h) = x.v;
+    }
+    return;
+  }
+  for (uint32_t b = 0; b < 32; ++b) {
+    const uint32_t i = i0 + b;
+    if (i < a.length) {
+      const int v = in[i];
+      out[i]      = static_cast<int8_t>(((c >> b) & 1u) ? -v : v);
     }
   }
 }

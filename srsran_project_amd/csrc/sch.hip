@@ -49,6 +49,17 @@ __global__ __launch_bounds__(SEG_THREADS) void segment_kernel(segment_args a)
   const uint8_t* tb      = a.tbs + static_cast<size_t>(t) * a.tb_stride;
   const uint32_t crc     = a.tb_crcs[t];
   uint32_t       byte    = 0;
+  if (8 * j + 8 <= n_data) {
+    // all 8 bits from the TB: one or two byte loads
+    const uint32_t q  = tb_off + 8 * j;
+    const uint32_t sh = q & 7u;
+    uint32_t       w  = static_cast<uint32_t>(tb[q >> 3]) << 8;
+    if (sh != 0) {
+      w |= tb[(q >> 3) + 1];
+    }
+    a.msgs[static_cast<size_t>(row) * a.msg_stride + j] = static_cast<uint8_t>(w >> (8 - sh));
+    return;
+  }
   for (int k = 0; k < 8; ++k) {
     const uint32_t p = 8 * j + k;
     uint32_t       v = 0;

@@ -36,6 +36,9 @@ for s in "$@"; do
              python3 tools/pmc_summary.py traffic gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/traffic.json ;;
     pmc) step pmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline && \
          step pmc2 600 rocprofv3 --kernel-trace --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE SQ_ACTIVE_INST_SCA -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    ppmc) step ppmc1 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY -d gpurun_out/ppmc1 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline && \
+          step ppmc_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/ppmc_fetch -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline && \
+          step ppmc_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/ppmc_write -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     obench) step bench_ofdm 600 python bench.py --workload ofdm --steps 10 --warmup 2 ;;
     pbench) step bench_pipe 600 python bench.py --workload pipeline --steps 10 --warmup 2 ;;
     pbenchq) step bench_pipe 600 python bench.py --workload pipeline --steps 10 --warmup 2 --no-cpu-baseline ;;
