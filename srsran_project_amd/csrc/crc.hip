@@ -30,25 +30,36 @@ __device__ void write_crc(const crc_args& a, uint32_t row_index, uint32_t crc)
   }
   if (a.attach) {
     // CRC bits MSB-first into bits [n, n + L); other bits of the touched bytes kept.
-    uint8_t* row = a.bits + static_cast<size_t>(row_index) * a.stride;
-    for (uint32_t k = 0; k < a.order; ++k) {
-      const uint32_t pos  = a.nof_bits + k;
-      const uint32_t bit  = (crc >> (a.order - 1 - k)) & 1u;
-      const uint8_t  mask = static_cast<uint8_t>(0x80u >> (pos & 7));
-      row[pos >> 3]       = static_cast<uint8_t>((row[pos >> 3] & ~mask) | (bit ? mask : 0));
+    // each touched byte read and written once (at most 4 bytes for a 24-bit CRC)
+    uint8_t*       row   = a.bits + static_cast<size_t>(row_index) * a.stride;
+    const uint32_t first = a.nof_bits >> 3, last = (a.nof_bits + a.order - 1) >> 3;
+    for (uint32_t q = first; q <= last; ++q) {
+      uint32_t byte = row[q];
+      for (uint32_t b = 0; b < 8; ++b) {
+        const uint32_t pos = 8 * q + b;
+        if (pos >= a.nof_bits && pos < a.nof_bits + a.order) {
+          const uint32_t bit  = (crc >> (a.order - 1 - (pos - a.nof_bits))) & 1u;
+          const uint32_t mask = 0x80u >> b;
+          byte                = (byte & ~mask) | (bit ? mask : 0u);
+        }
+      }
+      row[q] = static_cast<uint8_t>(byte);
     }
   }
 }
 
-__global__ void __launch_bounds__(CRC_THREADS) crc_kernel(crc_args a)
+// One wave per row: ~17 bytes per lane for a 1056-byte codeblock, so few remainder moves per byte.
+constexpr int CRC_ROW_THREADS = 64;
+
+__global__ void __launch_bounds__(CRC_ROW_THREADS) crc_kernel(crc_args a)
 {
-  __shared__ uint32_t partial[CRC_THREADS / 64];
+  __shared__ uint32_t partial[1];
   __shared__ uint32_t T[256];
-  crc_table8_init<CRC_THREADS>(T, a.order, a.polynom);
+  crc_table8_init<CRC_ROW_THREADS>(T, a.order, a.polynom);
   __syncthreads();
   const uint8_t* row = a.bits + static_cast<size_t>(blockIdx.x) * a.stride;
-  const uint32_t crc = block_crc_bytes<CRC_THREADS>(row_fetch{row}, a.nof_bits, a.order, a.polynom, a.table, T,
-                                                    partial);
+  const uint32_t crc = block_crc_bytes<CRC_ROW_THREADS>(row_fetch{row}, a.nof_bits, a.order, a.polynom, a.table, T,
+                                                        partial);
   if (threadIdx.x == 0) {
     write_crc(a, blockIdx.x, crc);
   }
@@ -93,7 +104,7 @@ hipError_t launch_crc(const crc_args& a, uint32_t nof_rows, hipStream_t stream)
   }
   const uint32_t nbytes = (a.nof_bits + 7) / 8;
   if (nbytes <= CRC_CHUNK || a.acc == nullptr) {
-    hipLaunchKernelGGL(crc_kernel, dim3(nof_rows), dim3(CRC_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(crc_kernel, dim3(nof_rows), dim3(CRC_ROW_THREADS), 0, stream, a);
     return hipGetLastError();
   }
   hipError_t e = hipMemsetAsync(a.acc, 0, sizeof(uint32_t) * nof_rows, stream);

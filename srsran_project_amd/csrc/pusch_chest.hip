@@ -20,7 +20,7 @@
 //                        search and quadratic refinement
 //                        (time_alignment_estimator_dft_impl.cpp:122-310), and the
 //                        per-port measurements (noise variance, EPRE, RSRP, SNR, CFO).
-//   chest_expand_kernel  one thread per output RE: the time-domain strategy
+//   chest_expand_kernel  one thread per (subcarrier, port, layer), every symbol: the time-domain strategy
 //                        (average or interpolation between DM-RS symbols), bf16
 //                        rounding and the CFO phase of the symbol -- the only
 //                        HBM-heavy step (4 bytes per RE x layer x port written).
@@ -589,47 +589,73 @@ __global__ __launch_bounds__(dft::plan<N>::T) void chest_ta_kernel(chest_args a)
 // outside the allocation are rotated in place, as the reference does.
 __global__ __launch_bounds__(256) void chest_expand_kernel(chest_args a)
 {
-  const uint32_t sc = blockIdx.x * 256 + threadIdx.x;
+  // one thread per subcarrier and (grid, port, layer): the LSE estimates of the subcarrier are read
+  // once and every OFDM symbol of the allocation written from them
+  __shared__ float2 s_ph[CH_NSYMB];
+  const uint32_t    sc   = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t    gpv  = blockIdx.y; // (grid * nof_ports + port) * L + layer
+  const uint32_t    gp   = gpv / a.L;
+  const uint32_t    v    = gpv % a.L;
+  const uint32_t    grid = gp / a.nof_ports, port = gp % a.nof_ports;
+  const float*      acc  = a.acc + static_cast<uint64_t>(gp) * 8;
+  const bool        rot  = a.compensate_cfo && acc[3] != 0.0f;
+  if (rot && threadIdx.x < a.nof_symbols) {
+    const uint32_t l  = a.first_symbol + threadIdx.x;
+    s_ph[threadIdx.x] = polar1(TWOPI_F * a.epoch[l] * acc[4]);
+  }
+  __syncthreads();
   if (sc >= a.nsubc) {
     return;
   }
-  const uint32_t l    = a.first_symbol + blockIdx.y;
-  const uint32_t gpv  = blockIdx.z; // (grid * nof_ports + port) * L + layer
-  const uint32_t gp   = gpv / a.L;
-  const uint32_t v    = gpv % a.L;
-  const uint32_t grid = gp / a.nof_ports, port = gp % a.nof_ports;
-  const float*   acc  = a.acc + static_cast<uint64_t>(gp) * 8;
-  const bool     rot  = a.compensate_cfo && acc[3] != 0.0f;
-  uint32_t*      est  = a.estimates + grid * a.est_stride +
-                  ((static_cast<uint64_t>(port) * a.L + v) * CH_NSYMB + l) * a.nsubc + sc;
-  const uint32_t kk   = sc - 12 * a.prb_lo; // wraps for sc below the allocation
-  uint32_t       out;
-  if (kk < a.nof_re) {
-    const float2* fr = a.freq + (static_cast<uint64_t>(gp) * a.L + v) * a.nof_lse * a.nof_re + kk;
-    float2        e;
-    if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
-      e = fr[0];
-    } else {
-      const int    i0 = a.td_i0[l];
-      const float2 x0 = fr[static_cast<uint64_t>(i0) * a.nof_re];
-      if (a.td_interp[l]) {
-        const float2 x1 = fr[static_cast<uint64_t>(i0 + 1) * a.nof_re];
-        const float  w  = a.td_w[l];
-        e               = make_float2(__builtin_fmaf(x1.x - x0.x, w, x0.x), __builtin_fmaf(x1.y - x0.y, w, x0.y));
-      } else {
-        e = x0;
-      }
-    }
-    out = to_cbf16(e);
-  } else if (rot) {
-    out = *est;
-  } else {
+  uint32_t*      est = a.estimates + grid * a.est_stride + (static_cast<uint64_t>(port) * a.L + v) * CH_NSYMB * a.nsubc + sc;
+  const uint32_t kk  = sc - 12 * a.prb_lo; // wraps for sc below the allocation
+  const bool     in  = kk < a.nof_re;
+  if (!in && !rot) {
     return;
   }
-  if (rot) {
-    out = to_cbf16(cmul(from_cbf16(out), polar1(TWOPI_F * a.epoch[l] * acc[4])));
+  float2 x[CH_MAXDMRS];
+  if (in) {
+    const float2* fr = a.freq + (static_cast<uint64_t>(gp) * a.L + v) * a.nof_lse * a.nof_re + kk;
+#pragma unroll
+    for (int s = 0; s < CH_MAXDMRS; ++s) {
+      x[s] = s < static_cast<int>(a.nof_lse) ? fr[static_cast<uint64_t>(s) * a.nof_re] : make_float2(0, 0);
+    }
   }
-  *est = out;
+  auto lse = [&](int i) { // x[i] without dynamic register indexing
+    float2 r = x[0];
+#pragma unroll
+    for (int s = 1; s < CH_MAXDMRS; ++s) {
+      r = i == s ? x[s] : r;
+    }
+    return r;
+  };
+  for (uint32_t n = 0; n < a.nof_symbols; ++n) {
+    const uint32_t l = a.first_symbol + n;
+    uint32_t       out;
+    if (in) {
+      float2 e;
+      if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
+        e = x[0];
+      } else {
+        const int    i0 = a.td_i0[l];
+        const float2 x0 = lse(i0);
+        if (a.td_interp[l]) {
+          const float2 x1 = lse(i0 + 1);
+          const float  w  = a.td_w[l];
+          e               = make_float2(__builtin_fmaf(x1.x - x0.x, w, x0.x), __builtin_fmaf(x1.y - x0.y, w, x0.y));
+        } else {
+          e = x0;
+        }
+      }
+      out = to_cbf16(e);
+    } else {
+      out = est[static_cast<uint64_t>(l) * a.nsubc];
+    }
+    if (rot) {
+      out = to_cbf16(cmul(from_cbf16(out), s_ph[n]));
+    }
+    est[static_cast<uint64_t>(l) * a.nsubc] = out;
+  }
 }
 
 } // namespace
@@ -664,8 +690,7 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   if (e != hipSuccess) {
     return e;
   }
-  hipLaunchKernelGGL(chest_expand_kernel, dim3((a.nsubc + 255) / 256, a.nof_symbols, nb * a.L), dim3(256), 0, stream,
-                     a);
+  hipLaunchKernelGGL(chest_expand_kernel, dim3((a.nsubc + 255) / 256, nb * a.L), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
