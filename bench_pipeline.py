@@ -309,6 +309,8 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         },
         "throughput_gbps": bits / elapsed / 1e9,
         "pusch_tb_ok_fraction": ok_frac,
+        # srs_amd_pusch_decoder_result: tb_crc_ok, nof_codeblocks_total, ldpc_iterations_sum / min / max, ...
+        "pusch_ldpc_iterations_mean": float(res[:, 2].sum() / max(1, res[:, 1].sum())),
         "stage_ms": stages,
         "stage_gbs": gbs,
         "roofline": {

@@ -69,16 +69,6 @@ __device__ __forceinline__ void gold_state(const uint32_t* jump, uint32_t c_init
   gold_advance16(jump, n0 + 1600u, x1, x2);
 }
 
-// States whose next output is c(n_wave + off), n_wave the same for every lane of the wave: the jump
-// to n_wave runs once per wave on the scalar unit (readfirstlane makes its inputs uniform), each lane
-// then applies one product per set bit of its own offset (a few, against ~12 for a jump from 0).
-__device__ __forceinline__ void gold_state_wave(const uint32_t* jump, uint32_t c_init, uint32_t n_wave, uint32_t off,
-                                                uint32_t& x1, uint32_t& x2)
-{
-  gold_state(jump, __builtin_amdgcn_readfirstlane(c_init), __builtin_amdgcn_readfirstlane(n_wave), x1, x2);
-  gold_advance(jump, off, x1, x2);
-}
-
 // The next 32 outputs from the states (the b-th output at bit b), word-parallel: with the state
 // s = x(n .. n+30) in bits 0..30, x1(n+31+i) = x1(n+3+i) ^ x1(n+i) gives 28 new bits in one shift/xor
 // (x2: taps 3, 2, 1, 0), a second round the next 4; the states advance by 32.
@@ -106,6 +96,16 @@ __device__ inline uint32_t gold_word(const uint32_t* jump, uint32_t c_init, uint
   uint32_t x1, x2;
   gold_state(jump, c_init, n0, x1, x2);
   return gold_emit32(x1, x2);
+}
+
+// States whose next output is c(n_wave + off), n_wave the same for every lane of the wave: the jump
+// to n_wave runs once per wave on the scalar unit (readfirstlane makes its inputs uniform), each lane
+// then applies one product per non-zero 4-bit digit of its own offset.
+__device__ __forceinline__ void gold_state_wave(const uint32_t* jump, uint32_t c_init, uint32_t n_wave, uint32_t off,
+                                                uint32_t& x1, uint32_t& x2)
+{
+  gold_state(jump, __builtin_amdgcn_readfirstlane(c_init), __builtin_amdgcn_readfirstlane(n_wave), x1, x2);
+  gold_advance16(jump, off, x1, x2);
 }
 
 } // namespace srs_amd

@@ -79,15 +79,11 @@ __global__ __launch_bounds__(256) void modulate_kernel(modulate_args a)
   reinterpret_cast<float2*>(a.symbols)[i] = v;
 }
 
-__global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
+// LLRs of one symbol into o[0 .. max(qm, 1)); i: the symbol's index in its demodulation call (the
+// pi/2-BPSK rotation parity), simd: the symbol lies in the reference's AVX2 blocks.
+__device__ __forceinline__ void demap_symbol(const demodulate_args& a, const float* lt, float2 s, float nv, uint32_t i,
+                                             bool simd, int8_t* o)
 {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.nof_symbols) {
-    return;
-  }
-  const float2 s    = reinterpret_cast<const float2*>(a.symbols)[i];
-  const float  nv   = a.noise_vars[i];
-  const bool   simd = i < a.block_end;
   const float  xs[2] = {s.x, s.y};
   constexpr float SQRT2 = 1.41421356237309504880f;
   if (a.qm <= 1) { // BPSK / pi/2-BPSK: scalar code only
@@ -97,10 +93,9 @@ __global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
       re            = im;
       im            = -t;
     }
-    a.llrs[i] = static_cast<int8_t>(nv > 0.0f ? q_scalar(2.0f * SQRT2 * (re + im) / nv, 24.0f) : 0);
+    o[0] = static_cast<int8_t>(nv > 0.0f ? q_scalar(2.0f * SQRT2 * (re + im) / nv, 24.0f) : 0);
     return;
   }
-  int8_t* o = a.llrs + static_cast<size_t>(i) * a.qm;
   if (a.qm == 2) {
     const float GAIN = 2.0f * SQRT2;
 #pragma unroll
@@ -164,9 +159,9 @@ __global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
       if (zero) {
         q = 0;
       } else if (simd) {
-        int idx = static_cast<int>(floorf(x * (1.0f / t.width))) + t.n / 2;
+        int idx = static_cast<int>(floorf(x * t.inv_width)) + t.n / 2;
         idx     = idx < 0 ? 0 : (idx > t.n - 1 ? t.n - 1 : idx);
-        float l = (t.slope[idx] * x + t.icpt[idx]) * rcp;
+        float l = (lt[(2 * k) * 16 + idx] * x + lt[(2 * k + 1) * 16 + idx]) * rcp;
         if (fabsf(x) <= NEAR_ZERO) {
           l = 0.0f;
         }
@@ -174,7 +169,7 @@ __global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
       } else {
         int idx = static_cast<int>(floorf(x / t.width)) + t.n / 2;
         idx     = idx < 0 ? 0 : (idx > t.n - 1 ? t.n - 1 : idx);
-        float l = __builtin_fmaf(t.slope[idx], x, t.icpt[idx]);
+        float l = __builtin_fmaf(lt[(2 * k) * 16 + idx], x, lt[(2 * k + 1) * 16 + idx]);
         l *= rcp;
         q = q_scalar(l, 20.0f);
       }
@@ -183,6 +178,82 @@ __global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
   }
 }
 
+// The interval tables' slopes and intercepts ([k][slope, icpt][16]) into LDS: per-lane lookups at a
+// data-dependent interval would otherwise be loads from the kernel-argument segment.
+__device__ __forceinline__ void stage_interval_tables(const demodulate_args& a, float* lt)
+{
+  for (uint32_t x = threadIdx.x; x < 4 * 2 * 16; x += blockDim.x) {
+    const uint32_t k = x / 32, w = (x / 16) % 2, j = x % 16;
+    lt[x]            = w == 0 ? a.tab[k].slope[j] : a.tab[k].icpt[j];
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
+{
+  __shared__ float lt[4 * 2 * 16];
+  stage_interval_tables(a, lt);
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.nof_symbols) {
+    return;
+  }
+  demap_symbol(a, lt, reinterpret_cast<const float2*>(a.symbols)[i], a.noise_vars[i], i, i < a.block_end,
+               a.llrs + static_cast<size_t>(i) * (a.qm < 1 ? 1 : a.qm));
+}
+
+// Soft demapping + descrambling of nof_grids codewords (PUSCH, pusch_demodulator_impl.cpp:203-330):
+// symbols [grid][grid_symbols], LLRs [grid][llr_stride]. A workgroup demaps DD_SYMS symbols of one
+// grid into LDS (4 per thread), builds the Gold words of its LLR range (one per lane, each wave's base
+// state jumped once on the scalar unit) and writes the descrambled LLRs 8 bytes at a time.
+constexpr uint32_t DD_SYMS = 1024;
+
+__global__ __launch_bounds__(256) void demap_descramble_kernel(demodulate_args a, demap_descramble_args d)
+{
+  __shared__ int8_t   s_llr[DD_SYMS * 8];
+  __shared__ uint32_t words[DD_SYMS * 8 / 32];
+  __shared__ float    lt[4 * 2 * 16];
+  stage_interval_tables(a, lt);
+  const uint32_t      g   = blockIdx.y;
+  const uint32_t      bpp = a.qm < 1 ? 1u : static_cast<uint32_t>(a.qm); // LLRs per symbol
+  const uint32_t      s0  = blockIdx.x * DD_SYMS;                        // first symbol (within the grid)
+  const uint32_t      n0  = s0 * bpp;                                    // first LLR of the workgroup
+  if (threadIdx.x < DD_SYMS * bpp / 32) {
+    uint32_t x1, x2;
+    gold_state_wave(d.jump, d.c_init, n0 + 32 * (threadIdx.x & ~63u), 32 * (threadIdx.x & 63u), x1, x2);
+    words[threadIdx.x] = gold_next32(x1, x2);
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < DD_SYMS / 256; ++r) {
+    const uint32_t t = r * 256 + threadIdx.x, i = s0 + t;
+    if (i < d.grid_symbols) {
+      const size_t gs = static_cast<size_t>(g) * d.grid_symbols + i;
+      demap_symbol(a, lt, reinterpret_cast<const float2*>(a.symbols)[gs], a.noise_vars[gs], i, i < a.block_end,
+                   s_llr + t * bpp);
+    }
+  }
+  __syncthreads();
+  const uint32_t nb  = min(DD_SYMS, d.grid_symbols - s0) * bpp;
+  int8_t*        row = d.llrs + static_cast<uint64_t>(g) * d.llr_stride + n0;
+  for (uint32_t b0 = 8 * threadIdx.x; b0 < nb; b0 += 8 * 256) {
+    const uint32_t c = words[b0 / 32] >> (b0 % 32);
+    union {
+      uint2  v;
+      int8_t b[8];
+    } x;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int v = s_llr[b0 + k];
+      x.b[k]      = static_cast<int8_t>(((c >> k) & 1u) ? -v : v);
+    }
+    if (b0 + 8 <= nb && (reinterpret_cast<uintptr_t>(row + b0) & 7u) == 0) {
+      *reinterpret_cast<uint2*>(row + b0) = x.v;
+    } else {
+      for (uint32_t k = 0; k < 8 && b0 + k < nb; ++k) {
+        row[b0 + k] = x.b[k];
+      }
+    }
+  }
+}
 
 __global__ __launch_bounds__(256) void scramble_bits_kernel(prbs_args a)
 {
@@ -245,6 +316,17 @@ hipError_t launch_demodulate(const demodulate_args& a, hipStream_t stream)
     return hipSuccess;
   }
   hipLaunchKernelGGL(demodulate_kernel, dim3((a.nof_symbols + 255) / 256), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_demap_descramble(const demodulate_args& a, const demap_descramble_args& d, uint32_t nof_grids,
+                                  hipStream_t stream)
+{
+  if (d.grid_symbols == 0 || nof_grids == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(demap_descramble_kernel, dim3((d.grid_symbols + DD_SYMS - 1) / DD_SYMS, nof_grids), dim3(256), 0,
+                     stream, a, d);
   return hipGetLastError();
 }
 

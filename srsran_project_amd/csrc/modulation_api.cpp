@@ -74,6 +74,7 @@ demod_interval_table make_table(int m, int k, float a, float norm)
   const bool           lsb = (k == m - 1);
   t.n                     = lsb ? L / 2 : L;
   t.width                 = static_cast<float>(lsb ? 4 : 2) * a;
+  t.inv_width             = 1.0f / t.width;
   const double w          = lsb ? 4.0 : 2.0;
   for (int i = 0; i < t.n; ++i) {
     const double x  = ((i - t.n / 2) + 0.5) * w;
@@ -328,24 +329,10 @@ int srs_amd_demodulate_soft_batch(srs_amd_modulator* mod,
   if (d_llrs == nullptr || d_symbols == nullptr || d_noise_vars == nullptr) {
     return fail(SRS_AMD_EINVAL, "null device buffer");
   }
-  demodulate_args a{};
-  a.symbols     = d_symbols;
-  a.noise_vars  = d_noise_vars;
-  a.llrs        = d_llrs;
-  a.nof_symbols = nof_symbols;
-  a.qm          = qm;
-  const uint32_t blk = avx2_block(qm);
-  a.block_end        = blk ? (nof_symbols / blk) * blk : 0;
-  a.qam16_scale      = mod->qam16_scale;
-  if (qm == 6) {
-    for (int k = 0; k < 3; ++k) {
-      a.tab[k] = mod->tab64[k];
-    }
-  } else if (qm == 8) {
-    for (int k = 0; k < 4; ++k) {
-      a.tab[k] = mod->tab256[k];
-    }
-  }
+  demodulate_args a = srs_amd::demodulate_args_for(mod, qm, nof_symbols);
+  a.symbols         = d_symbols;
+  a.noise_vars      = d_noise_vars;
+  a.llrs            = d_llrs;
   std::lock_guard<std::mutex> lock(mod->mtx);
   hipError_t                  e = hipSetDevice(mod->device);
   if (e == hipSuccess) {
@@ -549,3 +536,48 @@ int srs_amd_descramble_llrs(srs_amd_modulator* mod, int8_t* out, const int8_t* i
 }
 
 } // extern "C"
+
+demodulate_args srs_amd::demodulate_args_for(const srs_amd_modulator* mod, int qm, uint32_t nof_symbols)
+{
+  demodulate_args a{};
+  a.nof_symbols      = nof_symbols;
+  a.qm               = qm;
+  const uint32_t blk = avx2_block(qm);
+  a.block_end        = blk ? (nof_symbols / blk) * blk : 0;
+  a.qam16_scale      = mod->qam16_scale;
+  if (qm == 6) {
+    for (int k = 0; k < 3; ++k) {
+      a.tab[k] = mod->tab64[k];
+    }
+  } else if (qm == 8) {
+    for (int k = 0; k < 4; ++k) {
+      a.tab[k] = mod->tab256[k];
+    }
+  }
+  return a;
+}
+
+int srs_amd::demap_descramble_batch(srs_amd_modulator* mod, int qm, int8_t* d_llrs, uint64_t llr_stride,
+                                    const float* d_symbols, const float* d_noise_vars, uint32_t grid_symbols,
+                                    uint32_t nof_grids, const uint32_t* d_jump, uint32_t c_init, void* stream)
+{
+  int rc = check(mod, qm);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  demodulate_args a = demodulate_args_for(mod, qm, grid_symbols); // block_end per grid, as per call
+  a.symbols         = d_symbols;
+  a.noise_vars      = d_noise_vars;
+  demap_descramble_args d{};
+  d.llrs         = d_llrs;
+  d.jump         = d_jump;
+  d.llr_stride   = llr_stride;
+  d.grid_symbols = grid_symbols;
+  d.c_init       = c_init;
+  std::lock_guard<std::mutex> lock(mod->mtx);
+  hipError_t                  e = hipSetDevice(mod->device);
+  if (e == hipSuccess) {
+    e = launch_demap_descramble(a, d, nof_grids, static_cast<hipStream_t>(stream));
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "demap_descramble_kernel launch");
+}

@@ -12,8 +12,9 @@ namespace srs_amd {
 
 // Soft-demapper piecewise-linear LLR table of one PAM axis bit.
 struct demod_interval_table {
-  int32_t n;      // intervals
+  int32_t n;         // intervals
   float   width;
+  float   inv_width; // 1.0f / width (the reference's SIMD path multiplies by it)
   float   slope[16];
   float   icpt[16];
 };
@@ -50,6 +51,31 @@ struct prbs_args {
 
 hipError_t launch_modulate(const modulate_args& a, hipStream_t stream);
 hipError_t launch_demodulate(const demodulate_args& a, hipStream_t stream);
+
+struct demap_descramble_args {
+  int8_t*         llrs;         // [grid][llr_stride]
+  const uint32_t* jump;         // gold_jump_tables()
+  uint64_t        llr_stride;
+  uint32_t        grid_symbols; // symbols per grid (block_end of demodulate_args is per grid)
+  uint32_t        c_init;
+};
+hipError_t launch_demap_descramble(const demodulate_args& a, const demap_descramble_args& d, uint32_t nof_grids,
+                                   hipStream_t stream);
+
+} // namespace srs_amd
+
+struct srs_amd_modulator;
+
+namespace srs_amd {
+
+// Demapper arguments (tables, AVX2 block end) for calls of nof_symbols symbols (modulation_api.cpp).
+demodulate_args demodulate_args_for(const srs_amd_modulator* mod, int qm, uint32_t nof_symbols);
+
+// Soft demapping of nof_grids x grid_symbols symbols and descrambling of each grid's LLRs with the
+// Gold sequence of c_init, one launch (the PUSCH demodulator's last two steps).
+int demap_descramble_batch(srs_amd_modulator* mod, int qm, int8_t* d_llrs, uint64_t llr_stride, const float* d_symbols,
+                           const float* d_noise_vars, uint32_t grid_symbols, uint32_t nof_grids,
+                           const uint32_t* d_jump, uint32_t c_init, void* stream);
 hipError_t launch_scramble_bits(const prbs_args& a, hipStream_t stream);
 hipError_t launch_descramble_llrs(const prbs_args& a, hipStream_t stream);
 

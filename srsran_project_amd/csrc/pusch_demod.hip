@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
   }
 }
 
-// 8192 LLRs per workgroup: the 256 Gold words into LDS (4 per lane of one wave), then each thread
+// 8192 LLRs per workgroup: the 256 Gold words into LDS (one per lane), then each thread
 // flips the 32 LLRs of one word (16-byte vector accesses).
 __global__ __launch_bounds__(256) void pusch_descramble_kernel(pusch_descramble_args a)
 {
@@ -92,14 +92,11 @@ __global__ __launch_bounds__(256) void pusch_descramble_kernel(pusch_descramble_
   const uint32_t      gi    = blockIdx.y;
   const uint32_t      base  = blockIdx.x * 256 * 32; // first LLR of the workgroup
   const uint32_t      wfrst = blockIdx.x * 256;
-  if (threadIdx.x < 64 && base + threadIdx.x * 128 < a.length) {
-    // four consecutive words per lane of the first wave: one jump-ahead, then word-parallel steps
+  {
+    // one word per lane; each wave's base state is jumped once on the scalar unit
     uint32_t x1, x2;
-    gold_state_wave(a.jump, a.c_init, wfrst * 32, 4 * threadIdx.x * 32, x1, x2);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      words[4 * threadIdx.x + r] = gold_next32(x1, x2);
-    }
+    gold_state_wave(a.jump, a.c_init, (wfrst + (threadIdx.x & ~63u)) * 32, (threadIdx.x & 63u) * 32, x1, x2);
+    words[threadIdx.x] = gold_next32(x1, x2);
   }
   __syncthreads();
   const int8_t* in  = a.in + static_cast<uint64_t>(gi) * a.length;

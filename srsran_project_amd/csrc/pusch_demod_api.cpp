@@ -14,6 +14,7 @@
 #include "api_common.h"
 #include "device_buffer.h"
 #include "gold_sequence.h"
+#include "modulation_args.h"
 #include "pusch_demod_args.h"
 #include "srsran_amd/modulation.h"
 #include <algorithm>
@@ -251,7 +252,7 @@ int srs_amd_pusch_demodulate_batch(srs_amd_pusch_demodulator*      dem,
     return fail(SRS_AMD_EINVAL, "grid, estimate or LLR stride too small");
   }
   const size_t nsym  = static_cast<size_t>(nof_grids) * plan->args.nof_re * plan->nof_layers;
-  const size_t bytes = align_up(nsym * 8, 256) + align_up(nsym * 4, 256) + static_cast<size_t>(nof_grids) * nllr;
+  const size_t bytes = align_up(nsym * 8, 256) + align_up(nsym * 4, 256);
   std::lock_guard<std::mutex> lock(dem->mtx);
   hipError_t                  e = hipSetDevice(dem->device);
   if (e == hipSuccess) {
@@ -269,26 +270,15 @@ int srs_amd_pusch_demodulate_batch(srs_amd_pusch_demodulator*      dem,
   a.stats            = d_stats;
   a.eq_symbols       = reinterpret_cast<float2*>(base);
   a.eq_noise_vars    = reinterpret_cast<float*>(base + align_up(nsym * 8, 256));
-  int8_t* raw        = reinterpret_cast<int8_t*>(base + align_up(nsym * 8, 256) + align_up(nsym * 4, 256));
   auto    s          = static_cast<hipStream_t>(stream);
   e = launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->nof_symbols, plan->span_subc, nof_grids, s);
   if (e != hipSuccess) {
     return hip_fail(e, "pusch_equalize_kernel launch");
   }
-  int rc = srs_amd_demodulate_soft_batch(dem->demapper, raw, reinterpret_cast<const float*>(a.eq_symbols),
-                                         a.eq_noise_vars, static_cast<uint32_t>(nsym), plan->qm, stream);
-  if (rc != SRS_AMD_OK) {
-    return rc;
-  }
-  pusch_descramble_args d{};
-  d.in         = raw;
-  d.out        = d_llrs;
-  d.jump       = dem->d_jump;
-  d.out_stride = llr_stride;
-  d.length     = nllr;
-  d.c_init     = plan->c_init;
-  e            = launch_pusch_descramble(d, nof_grids, s);
-  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_descramble_kernel launch");
+  // soft demapper + descrambling (revert_scrambling) in one pass: LLRs straight into the caller's rows
+  return demap_descramble_batch(dem->demapper, plan->qm, d_llrs, llr_stride, reinterpret_cast<const float*>(a.eq_symbols),
+                                a.eq_noise_vars, static_cast<uint32_t>(plan->args.nof_re * plan->nof_layers), nof_grids,
+                                dem->d_jump, plan->c_init, stream);
 }
 
 int srs_amd_pusch_demodulate(srs_amd_pusch_demodulator*      dem,
