@@ -11,12 +11,11 @@
 // (equalizer_device.h), writing [j][layer] symbols and variances.
 // The per-port noise variances come from the DM-RS estimator's measurements
 // on the device, so the chain needs no host round trip.
-// pusch_descramble_kernel: revert_scrambling (pusch_demodulator_impl.cpp:36-190)
-// 8192 LLRs per workgroup from 256 jump-ahead Gold words in LDS, batched over grids.
+// The soft demapper and revert_scrambling (pusch_demodulator_impl.cpp:36-190) run fused in
+// demap_descramble_kernel (modulation.hip).
 #include <hip/hip_runtime.h>
 
 #include "equalizer_device.h"
-#include "gold_sequence.h"
 #include "pusch_demod_args.h"
 
 namespace srs_amd {
@@ -84,51 +83,6 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
   }
 }
 
-// 8192 LLRs per workgroup: the 256 Gold words into LDS (one per lane), then each thread
-// flips the 32 LLRs of one word (16-byte vector accesses).
-__global__ __launch_bounds__(256) void pusch_descramble_kernel(pusch_descramble_args a)
-{
-  __shared__ uint32_t words[256];
-  const uint32_t      gi    = blockIdx.y;
-  const uint32_t      base  = blockIdx.x * 256 * 32; // first LLR of the workgroup
-  const uint32_t      wfrst = blockIdx.x * 256;
-  {
-    // one word per lane; each wave's base state is jumped once on the scalar unit
-    uint32_t x1, x2;
-    gold_state_wave(a.jump, a.c_init, (wfrst + (threadIdx.x & ~63u)) * 32, (threadIdx.x & 63u) * 32, x1, x2);
-    words[threadIdx.x] = gold_next32(x1, x2);
-  }
-  __syncthreads();
-  const int8_t* in  = a.in + static_cast<uint64_t>(gi) * a.length;
-  int8_t*       out = a.out + gi * a.out_stride;
-  // thread t: the 32 LLRs of Gold word t, two 16-byte loads and stores when aligned and whole
-  const uint32_t i0 = base + 32 * threadIdx.x;
-  const uint32_t c  = words[threadIdx.x];
-  if (i0 + 32 <= a.length && (((reinterpret_cast<uintptr_t>(in + i0)) | reinterpret_cast<uintptr_t>(out + i0)) & 15u) == 0) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      union {
-        uint4  v;
-        int8_t b[16];
-      } x;
-      x.v = *reinterpret_cast<const uint4*>(in + i0 + 16 * h);
-#pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        x.b[b] = static_cast<int8_t>(((c >> (16 * h + b)) & 1u) ? -x.b[b] : x.b[b]);
-      }
-      *reinterpret_cast<uint4*>(out + i0 + 16 * h) = x.v;
-    }
-    return;
-  }
-  for (uint32_t b = 0; b < 32; ++b) {
-    const uint32_t i = i0 + b;
-    if (i < a.length) {
-      const int v = in[i];
-      out[i]      = static_cast<int8_t>(((c >> b) & 1u) ? -v : v);
-    }
-  }
-}
-
 } // namespace
 
 hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers,
@@ -152,14 +106,5 @@ hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uin
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_pusch_descramble(const pusch_descramble_args& a, uint32_t nof_grids, hipStream_t stream)
-{
-  if (a.length == 0 || nof_grids == 0) {
-    return hipSuccess;
-  }
-  const uint32_t blocks = (a.length + 256 * 32 - 1) / (256 * 32);
-  hipLaunchKernelGGL(pusch_descramble_kernel, dim3(blocks, nof_grids), dim3(256), 0, stream, a);
-  return hipGetLastError();
-}
 
 } // namespace srs_amd

@@ -26,17 +26,8 @@ struct pusch_eq_args {
   uint32_t                        first_subc;
 };
 
-struct pusch_descramble_args {
-  const int8_t*   in;  // [grid][length]
-  int8_t*         out; // rows of out_stride
-  const uint32_t* jump;
-  uint64_t        out_stride;
-  uint32_t        length;
-  uint32_t        c_init;
-};
 
 hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers,
                                  uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_grids, hipStream_t stream);
-hipError_t launch_pusch_descramble(const pusch_descramble_args& a, uint32_t nof_grids, hipStream_t stream);
 
 } // namespace srs_amd
