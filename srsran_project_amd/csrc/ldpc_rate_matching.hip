@@ -82,7 +82,7 @@ __device__ __forceinline__ int llr_sum(int a, int b)
 
 constexpr int DEMATCH_THREADS   = 256;
 constexpr int DEMATCH_PER_THREAD = 16;
-constexpr uint32_t DEMATCH_LDS   = 24576; // received LLRs of a codeblock staged in LDS up to this length
+constexpr uint32_t DEMATCH_LDS   = 12288; // received LLRs of a codeblock staged in LDS up to this length (8 resident workgroups per CU)
 
 // One workgroup per codeblock: the codeblock's received LLRs (deinterleaver input) are staged in LDS
 // with coalesced loads when they fit, then each thread produces 16 consecutive soft-buffer bytes.

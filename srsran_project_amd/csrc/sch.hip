@@ -26,7 +26,7 @@ constexpr int SEG_THREADS = 256;
 constexpr int ASM_THREADS = 256;
 constexpr uint32_t CRC24A_POLY = 0x1864cfb;
 constexpr uint32_t SCH_MAX_SEGMENTS = 512;
-constexpr uint32_t ASM_TB_PER       = 8;                         // TB bytes per thread
+constexpr uint32_t ASM_TB_PER       = 32;                        // TB bytes per thread
 constexpr uint32_t ASM_TB_CHUNK     = ASM_THREADS * ASM_TB_PER;  // TB bytes per workgroup
 
 __device__ __forceinline__ uint32_t bit_at(const uint8_t* b, uint32_t p)
