@@ -32,6 +32,7 @@ DL_START, DL_NSYM = 1, 13
 UL_START, UL_NSYM = 0, 14
 RNTI, N_ID, SLOT = 0x4601, 500, 0
 SNR_DB = 35.0
+UL_LANES = 1  # PUSCH streams (cell shares) next to the PDSCH stream; 2 measured 10% slower (smaller kernels contend)
 
 
 def base_graph(tbs, r):
@@ -92,13 +93,25 @@ class Pipeline:
             slot_index=SLOT, numerology=MU, nof_tx_layers=UL_LAYERS, scrambling_id=N_ID, n_scid=False, scaling=1.0,
             symbols_mask=DMRS_MASK, rb_start=0, rb_count=NPRB, first_symbol=UL_START, nof_symbols=UL_NSYM)
         self.demod = amd.PuschDemodulator(device=d)
-        self.demod_plan = self.demod.plan(amd.PuschDemodulatorConfig(
+        self.demod_cfg = amd.PuschDemodulatorConfig(
             rnti=RNTI, crbs=all_crbs, modulation=QM, start_symbol=UL_START, nof_symbols=UL_NSYM,
             dmrs_symb_pos=DMRS_MASK, n_id=N_ID, nof_tx_layers=UL_LAYERS, nof_rx_ports=UL_PORTS,
-            nof_cdm_groups_without_data=2), NSUBC)
+            nof_cdm_groups_without_data=2)
+        self.demod_plan = self.demod.plan(self.demod_cfg, NSUBC)
         assert self.demod_plan.nof_llrs == self.plan_ul.cw_length
         self.dec = amd.PuschDecoder("simd", device=d)
         self.dec_cfg = amd.PuschDecoder.config(nof_ldpc_iterations=iters, use_early_stop=True)
+        # PUSCH lanes: the cells are split into UL_LANES contiguous shares, each run by its own processor
+        # objects on its own stream (a multi-cell PHY runs independent cells concurrently)
+        self.ul_objs = [(self.ofdm_dem, self.chest, self.demod, self.demod_plan, self.dec)]
+        for _ in range(1, UL_LANES):
+            dem = amd.PuschDemodulator(device=d)
+            self.ul_objs.append((amd.OfdmSlotDemodulator(amd.OfdmDemodulatorConfiguration(MU, NPRB, NFFT, 0, 1.0,
+                                                                                          3.5e9, 0), device=d),
+                                 amd.DmrsPuschEstimator(device=d), dem, dem.plan(self.demod_cfg, NSUBC),
+                                 amd.PuschDecoder("simd", device=d)))
+        self.ul_bounds = [slots * k // UL_LANES for k in range(UL_LANES + 1)]
+        self.res_ul = [None] * UL_LANES
 
         # ---- resident inputs and buffers --------------------------------------------------------
         S = slots
@@ -153,16 +166,21 @@ class Pipeline:
         self.ofdm_mod.modulate_batch(self.grid_dl.view(t.int16).view(self.S, DL_PORTS, 14, 2 * NSUBC), SLOT,
                                      out=self.samp_dl, stream=stream)
 
-    def pusch(self, stream):
+    def pusch(self, stream, lane=0):
+        """The PUSCH chain of the cells of one lane (a contiguous share of the batch), with that lane's
+        own processor objects (each keeps its own device scratch)."""
         t = self.torch
-        self.ofdm_dem.demodulate_batch(self.samp_ul, SLOT,
-                                       grid=self.grid_ul.view(t.int16).view(self.S, UL_PORTS, 14, 2 * NSUBC),
-                                       stream=stream)
-        self.chest.estimate_batch(self.grid_ul, self.chest_cfg, self.est_ul, self.stats_ul, stream=stream)
-        self.demod.demodulate_batch(self.grid_ul, self.est_ul, self.stats_ul, self.demod_plan, llrs=self.llr_ul,
-                                    stream=stream)
-        _, self.res_ul = self.dec.decode_batch(self.llr_ul, self.plan_ul, self.dec_cfg, tbs=self.tb_rx,
-                                               soft=self.soft, stream=stream)
+        ofdm_dem, chest, demod, demod_plan, dec = self.ul_objs[lane]
+        a, b = self.ul_bounds[lane], self.ul_bounds[lane + 1]
+        n = b - a
+        grid = self.grid_ul[a:b]
+        ofdm_dem.demodulate_batch(self.samp_ul[a:b], SLOT, grid=grid.view(t.int16).view(n, UL_PORTS, 14, 2 * NSUBC),
+                                  stream=stream)
+        chest.estimate_batch(grid, self.chest_cfg, self.est_ul[a:b], self.stats_ul[a:b], stream=stream)
+        demod.demodulate_batch(grid, self.est_ul[a:b], self.stats_ul[a:b], demod_plan, llrs=self.llr_ul[a:b],
+                               stream=stream)
+        _, self.res_ul[lane] = dec.decode_batch(self.llr_ul[a:b], self.plan_ul, self.dec_cfg, tbs=self.tb_rx[a:b],
+                                                soft=self.soft[a:b], stream=stream)
 
     def step(self, stream):
         """One slot of every cell through both chains. The PDSCH (TX) and PUSCH (RX) chains share no data,
@@ -170,20 +188,24 @@ class Pipeline:
         per-TB kernels fill each other's idle CUs."""
         t = self.torch
         if self.ul_stream is None:
-            self.ul_stream = t.cuda.Stream(self.dev)
-            self.ev_fork, self.ev_join = t.cuda.Event(), t.cuda.Event()
+            self.ul_stream = [t.cuda.Stream(self.dev) for _ in range(UL_LANES)]
+            self.ev_fork = t.cuda.Event()
+            self.ev_join = [t.cuda.Event() for _ in range(UL_LANES)]
         self.ev_fork.record(stream)
-        self.ul_stream.wait_event(self.ev_fork)
+        for st in self.ul_stream:
+            st.wait_event(self.ev_fork)
         with t.cuda.stream(stream):
             self.pdsch(stream)
-        with t.cuda.stream(self.ul_stream):
-            self.pusch(self.ul_stream)
-        self.ev_join.record(self.ul_stream)
-        stream.wait_event(self.ev_join)
+        for k, st in enumerate(self.ul_stream):
+            with t.cuda.stream(st):
+                self.pusch(st, k)
+            self.ev_join[k].record(st)
+        for ev in self.ev_join:
+            stream.wait_event(ev)
 
     def check(self):
         """Fraction of PUSCH transport blocks with TB CRC ok and bit-equal to what the UE sent."""
-        res = self.res_ul.cpu().numpy()
+        res = self.torch.cat(self.res_ul).cpu().numpy()
         crc_ok = res[:, 0] != 0
         same = (self.tb_rx.cpu().numpy() == self.tb_ul.cpu().numpy()).all(axis=1)
         return float(np.mean(crc_ok & same)), res

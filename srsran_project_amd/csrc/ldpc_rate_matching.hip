@@ -138,8 +138,18 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
     // walk skips to nof_sys when the input ends in the information part) and the tail zeroing starts
     // where it stopped: once E >= nof_info nothing of the old contents survives.
     const bool read_old = !a.fresh && !(a.new_data && E >= g.nof_info && g.k0 == 0 && g.Ncb == g.N);
-    // soft-buffer rows are 4-byte aligned (HARQ rows carry a message and a flag after the LLRs)
     const bool vec      = (reinterpret_cast<uintptr_t>(buf) & 3u) == 0 && (g.N & 15u) == 0;
+    const bool vec16    = (reinterpret_cast<uintptr_t>(buf) & 15u) == 0; // PUSCH soft rows are 64-byte aligned
+    auto       store16  = [&](uint32_t* o, uint4 v) {
+      if (vec16) {
+        *reinterpret_cast<uint4*>(o) = v;
+      } else {
+        o[0] = v.x;
+        o[1] = v.y;
+        o[2] = v.z;
+        o[3] = v.w;
+      }
+    };
     const uint32_t step = gridDim.x * DEMATCH_THREADS * DEMATCH_PER_THREAD;
     if (staged && vec && first_pass && E <= L1) {
       // Single first pass (no combining), branch-free: every position selects between its old value,
@@ -165,7 +175,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
         constexpr uint32_t R = DEMATCH_PER_THREAD;
         if (p0 >= zero_from) {
           // the whole run lies in the tail zeroing (most of a high-rate codeblock)
-          o4[0] = o4[1] = o4[2] = o4[3] = 0;
+          store16(o4, make_uint4(0, 0, 0, 0));
           continue;
         }
         if (linear && t0 + R <= E && p0 >= zero_end && p0 + R <= zero_from && p0 + R <= g.Ncb) {
@@ -177,10 +187,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
             const uint32_t idx = idx0 + __umul24(k, g.Qm) - (k >= kw ? __umul24(Kq, g.Qm) - 1 : 0u);
             out.b[k]           = s_in[idx];
           }
-          o4[0] = out.v.x;
-          o4[1] = out.v.y;
-          o4[2] = out.v.z;
-          o4[3] = out.v.w;
+          store16(o4, out.v);
           continue;
         }
         old.v = read_old ? make_uint4(o4[0], o4[1], o4[2], o4[3]) : make_uint4(0, 0, 0, 0);
@@ -209,10 +216,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
           v                = p >= zero_from ? 0 : v;
           out.b[k]         = static_cast<int8_t>(v);
         }
-        o4[0] = out.v.x;
-        o4[1] = out.v.y;
-        o4[2] = out.v.z;
-        o4[3] = out.v.w;
+        store16(o4, out.v);
       }
       continue;
     }
