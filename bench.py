@@ -80,27 +80,36 @@ def load_traffic(name):
 
 def timed(args, dist, world, dev, stream, step):
     """Warmup, then K steps bracketed by barrier + synchronize; per-step HIP
-    events on the launch stream.  Returns (elapsed_s max over ranks, mean event ms)."""
+    events on the launch stream.  Returns (elapsed_s max over ranks, mean event ms).
+    On a CPU device (the gloo tests of the multi-rank path) the events are skipped."""
     import torch
 
+    gpu = dev.type == "cuda"
+    sync = (lambda: torch.cuda.synchronize(dev)) if gpu else (lambda: None)
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    sync()
+    if gpu:
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        starts[s].record(stream)
+        if gpu:
+            starts[s].record(stream)
         step()
-        ends[s].record(stream)
-    torch.cuda.synchronize(dev)
+        if gpu:
+            ends[s].record(stream)
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    event_ms = float(np.mean([starts[s].elapsed_time(ends[s]) for s in range(args.steps)]))
+    if gpu:
+        event_ms = float(np.mean([starts[s].elapsed_time(ends[s]) for s in range(args.steps)]))
+    else:
+        event_ms = elapsed * 1e3 / max(1, args.steps)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
