@@ -218,7 +218,7 @@ class PuschDecoder:
         dev = llrs.device
         if tbs is None:
             tbs = torch.zeros((n, plan.tbs // 8), dtype=torch.uint8, device=dev)
-        res = torch.zeros((n, RESULT_WORDS), dtype=torch.int32, device=dev)
+        res = torch.empty((n, RESULT_WORDS), dtype=torch.int32, device=dev)  # every field written by the decoder
         _lib.check(self._lib.srs_amd_pusch_decode_batch(
             self._h, ctypes.byref(plan), ctypes.byref(cfg), tbs.data_ptr(), tbs.shape[1], res.data_ptr(),
             llrs.data_ptr(), llrs.shape[1], None if soft is None else soft.data_ptr(),
