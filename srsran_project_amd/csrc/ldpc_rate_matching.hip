@@ -88,7 +88,7 @@ constexpr uint32_t DEMATCH_LDS   = 12288; // received LLRs of a codeblock staged
 // with coalesced loads when they fit, then each thread produces 16 consecutive soft-buffer bytes.
 __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dematch_args a)
 {
-  __shared__ int8_t  s_in[DEMATCH_LDS];
+  __shared__ __attribute__((aligned(16))) int8_t s_in[DEMATCH_LDS];
   const rm_geometry& g = a.g;
   for (uint32_t cb = blockIdx.y; cb < a.nof_cbs; cb += gridDim.y) {
     const uint32_t E   = a.rm_lengths[cb];
@@ -96,21 +96,39 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
     int8_t*        buf = a.soft + static_cast<size_t>(cb) * a.soft_stride;
     const uint32_t Kq  = E / g.Qm;
     const fast_div divK(Kq);
-    const bool     staged = E <= DEMATCH_LDS;
+    // Staged in LDS already deinterleaved (s_in[t], t = j Kq + i <- in[i Qm + j]): consecutive soft-buffer
+    // positions then read consecutive LDS bytes (the interleaved order put the lanes of a wave 16 Qm
+    // bytes apart, a 32-way bank conflict per read).
+    const bool staged = E <= DEMATCH_LDS && Kq * g.Qm == E;
     if (staged) {
       __syncthreads(); // s_in of the previous codeblock is no longer read
+      const fast_div divQ(g.Qm);
+      auto           put = [&](uint32_t x, int8_t v) {
+        uint32_t j;
+        const uint32_t i = divQ.div(x, j);
+        s_in[j * Kq + i] = v;
+      };
       if (((reinterpret_cast<uintptr_t>(in) | E) & 15u) == 0) {
         for (uint32_t x = threadIdx.x; x < E / 16; x += DEMATCH_THREADS) {
-          reinterpret_cast<uint4*>(s_in)[x] = reinterpret_cast<const uint4*>(in)[x];
+          union {
+            uint4  v;
+            int8_t b[16];
+          } w;
+          w.v = reinterpret_cast<const uint4*>(in)[x];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            put(16 * x + k, w.b[k]);
+          }
         }
       } else {
         for (uint32_t x = threadIdx.x; x < E; x += DEMATCH_THREADS) {
-          s_in[x] = in[x];
+          put(x, in[x]);
         }
       }
       __syncthreads();
     }
-    auto llr_in = [&](uint32_t idx) -> int { return staged ? s_in[idx] : in[idx]; };
+    // received LLR of deinterleaver index t = j Kq + i
+    auto llr_in = [&](uint32_t t, uint32_t i, uint32_t j) -> int { return staged ? s_in[t] : in[i * g.Qm + j]; };
 
     // First loop pass of the reference (copy mode), see the file header.
     const bool     first_pass = a.new_data && E > 0;
@@ -179,13 +197,15 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
           continue;
         }
         if (linear && t0 + R <= E && p0 >= zero_end && p0 + R <= zero_from && p0 + R <= g.Ncb) {
-          // pure copy run: input index advances by Qm, once wrapping to the next interleaver row
-          const uint32_t idx0 = __umul24(i0, g.Qm) + j0;
-          const uint32_t kw   = Kq - i0; // first k in the next row
+          // pure copy run: 16 consecutive deinterleaved LLRs
+          if ((t0 & 3u) == 0) {
+            const uint32_t* w4 = reinterpret_cast<const uint32_t*>(s_in + t0);
+            out.v              = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+          } else {
 #pragma unroll
-          for (uint32_t k = 0; k < R; ++k) {
-            const uint32_t idx = idx0 + __umul24(k, g.Qm) - (k >= kw ? __umul24(Kq, g.Qm) - 1 : 0u);
-            out.b[k]           = s_in[idx];
+            for (uint32_t k = 0; k < R; ++k) {
+              out.b[k] = s_in[t0 + k];
+            }
           }
           store16(o4, out.v);
           continue;
@@ -209,7 +229,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
           } else {
             j = divK.div(min(t, E - 1), i);
           }
-          const int x = s_in[__umul24(i, g.Qm) + j];
+          const int x = s_in[min(t, E - 1)];
           int            v = p < zero_end ? 0 : old.b[k];
           v                = filler ? LLR_INFINITY : v;
           v                = (!filler && p < g.Ncb && t < E) ? x : v;
@@ -258,13 +278,13 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
               j = divK.div(t, i);
             }
             t_prev = t;
-            v      = llr_in(i * g.Qm + j);
+            v      = llr_in(t, i, j);
             t += g.L;
           }
           for (; t < E; t += g.L) {
             uint32_t ii, jj;
             jj = divK.div(t, ii);
-            v  = llr_sum(llr_in(ii * g.Qm + jj), v);
+            v  = llr_sum(llr_in(t, ii, jj), v);
           }
         }
         if (p >= zero_from) {
