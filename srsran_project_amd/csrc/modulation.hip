@@ -150,7 +150,11 @@ __device__ __forceinline__ void demap_symbol(const demodulate_args& a, const flo
   const int  m    = a.qm / 2;
   const bool zero = !simd && (s.x * s.x + s.y * s.y) < NEAR_ZERO;
   const float rcp = safe_rcp(nv);
-  for (int k = 0; k < m; ++k) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { // compile-time k: the table fields are scalar loads
+    if (k >= m) {
+      break;
+    }
     const demod_interval_table& t = a.tab[k];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
