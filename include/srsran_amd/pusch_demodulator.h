@@ -88,6 +88,22 @@ int srs_amd_pusch_demodulate_batch(srs_amd_pusch_demodulator*      dem,
                                    uint32_t                        nof_grids,
                                    void*                           stream);
 
+/* DEVICE, asynchronous: the demodulator's last two steps alone -- soft demapping
+ * (one demapper call per OFDM symbol, pusch_demodulator_impl.cpp:363-400) and
+ * revert_scrambling (:36-190) -- of equalized symbols produced elsewhere (a custom
+ * MIMO detector, or the reference's own equalizer). d_eq_symbols complex float
+ * [grid][nof_re][layer] (interleaved re/im), d_eq_noise_vars float
+ * [grid][nof_re][layer], both with a per-grid stride of nof_re * layers entries;
+ * LLRs as srs_amd_pusch_demodulate_batch. */
+int srs_amd_pusch_demap_descramble_batch(srs_amd_pusch_demodulator*      dem,
+                                         const srs_amd_pusch_demod_plan* plan,
+                                         const float*                    d_eq_symbols,
+                                         const float*                    d_eq_noise_vars,
+                                         int8_t*                         d_llrs,
+                                         uint64_t                        llr_stride,
+                                         uint32_t                        nof_grids,
+                                         void*                           stream);
+
 #ifdef __cplusplus
 }
 #endif

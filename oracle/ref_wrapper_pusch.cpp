@@ -1,0 +1,329 @@
+// ref_wrapper_pusch.cpp -- extern "C" glue around the REFERENCE's own PUSCH
+// demodulator (pusch_demodulator_impl) and PUSCH processor
+// (pusch_processor_impl: DM-RS estimator -> demodulator -> UL-SCH
+// demultiplexer -> decoder), compiled from /root/reference by oracle/Makefile
+// into oracle/_ref/libsrsran_ref.so.
+//
+// TEST INFRASTRUCTURE ONLY: pins the GPU PUSCH demodulator and PUSCH processor
+// (tests/test_pusch_demod_gpu.py, tests/test_pusch_processor_gpu.py) and the
+// configs[0] plumbing run.  Never loaded by the product.
+//
+// Glue (interfaces implemented here, nothing of the reference replaced; see
+// ref_builders.h): an in-memory pusch_codeword_buffer that hands out views
+// exactly as pusch_decoder_impl::get_next_block_view does (the requested block,
+// pusch_decoder_impl.cpp:140-157) so the demodulator splits its demapper calls
+// per OFDM symbol as in the real chain; notifiers that record the results.
+#include "ref_builders.h"
+#include "phy/support/resource_grid_reader_impl.h"
+#include "srsran/adt/tensor.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_codeword_buffer.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_demodulator_notifier.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_processor_result_notifier.h"
+#include "srsran/ran/sch/sch_constants.h"
+#include <atomic>
+#include <cmath>
+#include <cstring>
+
+using namespace srsran;
+using namespace srs_ref;
+
+namespace {
+
+using grid_tensor =
+    dynamic_tensor<static_cast<unsigned>(resource_grid_dimensions::all), cbf16_t, resource_grid_dimensions>;
+
+modulation_scheme scheme_of(int qm)
+{
+  switch (qm) {
+    case 0:
+      return modulation_scheme::PI_2_BPSK;
+    case 1:
+      return modulation_scheme::BPSK;
+    case 2:
+      return modulation_scheme::QPSK;
+    case 4:
+      return modulation_scheme::QAM16;
+    case 6:
+      return modulation_scheme::QAM64;
+    default:
+      return modulation_scheme::QAM256;
+  }
+}
+
+symbol_slot_mask to_symbols(unsigned mask)
+{
+  symbol_slot_mask s(MAX_NSYMB_PER_SLOT);
+  for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+    if ((mask >> l) & 1u) {
+      s.set(l);
+    }
+  }
+  return s;
+}
+
+void load_grid(grid_tensor& data, const uint32_t* grid, unsigned nports, unsigned nsubc)
+{
+  for (unsigned p = 0; p != nports; ++p) {
+    for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+      span<cbf16_t> row = data.get_view<static_cast<unsigned>(resource_grid_dimensions::symbol)>({l, p});
+      std::memcpy(row.data(), grid + (p * MAX_NSYMB_PER_SLOT + l) * nsubc, nsubc * sizeof(cbf16_t));
+    }
+  }
+}
+
+class vector_codeword_buffer : public pusch_codeword_buffer
+{
+public:
+  explicit vector_codeword_buffer(span<log_likelihood_ratio> out_) : out(out_) {}
+  span<log_likelihood_ratio> get_next_block_view(unsigned block_size) override
+  {
+    if (count + block_size > out.size()) {
+      std::abort();
+    }
+    return out.subspan(count, block_size);
+  }
+  void on_new_block(span<const log_likelihood_ratio> data, const bit_buffer&) override
+  {
+    if (data.data() != out.data() + count) {
+      std::memcpy(out.data() + count, data.data(), data.size());
+    }
+    count += data.size();
+    ++nof_blocks;
+  }
+  void                       on_end_codeword() override { ended = true; }
+  span<log_likelihood_ratio> out;
+  unsigned                   count      = 0;
+  unsigned                   nof_blocks = 0;
+  bool                       ended      = false;
+};
+
+class stats_notifier : public pusch_demodulator_notifier
+{
+public:
+  void on_provisional_stats(unsigned i_symbol, const demodulation_stats& stats) override
+  {
+    if (i_symbol < MAX_NSYMB_PER_SLOT) {
+      sinr[i_symbol] = stats.sinr_dB.value_or(NAN);
+    }
+  }
+  void  on_end_stats(const demodulation_stats& stats) override { end_sinr = stats.sinr_dB.value_or(NAN); }
+  float sinr[MAX_NSYMB_PER_SLOT] = {NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN};
+  float end_sinr                 = NAN;
+};
+
+class result_notifier : public pusch_processor_result_notifier
+{
+public:
+  void on_uci(const pusch_processor_result_control&) override { ++nof_uci; }
+  void on_sch(const pusch_processor_result_data& sch) override
+  {
+    result = sch;
+    done   = true;
+  }
+  pusch_processor_result_data result;
+  bool                        done    = false;
+  unsigned                    nof_uci = 0;
+};
+
+} // namespace
+
+extern "C" {
+
+// pusch_demodulator::demodulate (pusch_demodulator_impl.cpp:203-445) of one grid [P][14][nsubc]
+// with channel estimates [P][L][14][nsubc] (cbf16 as uint32) and per-port noise variances.
+// crbs: 0/1 bytes [nsubc / 12]. eq: 0 ZF, 1 MMSE. llrs: nof_llrs (= data REs x L x Qm) int8.
+// sinr_out[15]: per-OFDM-symbol provisional SINR (dB, NaN when not notified) then the final one
+// (computed only when post_eq_sinr != 0). Returns the number of codeword blocks the demodulator
+// produced, or -1 on a size mismatch.
+int srs_ref_pusch_demodulate(const uint32_t* grid,
+                             unsigned        nof_rx_ports,
+                             unsigned        nsubc,
+                             const uint32_t* estimates,
+                             unsigned        nof_layers,
+                             const float*    noise_vars,
+                             unsigned        rnti,
+                             unsigned        n_id,
+                             int             qm,
+                             const uint8_t*  crbs,
+                             unsigned        start_symbol,
+                             unsigned        nof_symbols,
+                             unsigned        dmrs_symb_mask,
+                             int             dmrs_type2,
+                             unsigned        nof_cdm_groups_without_data,
+                             int             eq,
+                             int             transform_precoding,
+                             int             post_eq_sinr,
+                             int8_t*         llrs,
+                             unsigned        nof_llrs,
+                             float*          sinr_out)
+{
+  const unsigned nof_prb = nsubc / NRE;
+  auto           demod   = make_pusch_demodulator(eq, nof_prb, post_eq_sinr != 0, transform_precoding != 0);
+
+  grid_tensor data({nsubc, MAX_NSYMB_PER_SLOT, nof_rx_ports});
+  load_grid(data, grid, nof_rx_ports, nsubc);
+  std::atomic<unsigned>     empty{0};
+  resource_grid_reader_impl reader(data, empty);
+
+  channel_estimate::channel_estimate_dimensions dims;
+  dims.nof_prb       = nof_prb;
+  dims.nof_symbols   = MAX_NSYMB_PER_SLOT;
+  dims.nof_rx_ports  = nof_rx_ports;
+  dims.nof_tx_layers = nof_layers;
+  channel_estimate est(dims);
+  for (unsigned p = 0; p != nof_rx_ports; ++p) {
+    est.set_noise_variance(noise_vars[p], p);
+    for (unsigned v = 0; v != nof_layers; ++v) {
+      for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+        span<cbf16_t> s = est.get_symbol_ch_estimate(l, p, v);
+        std::memcpy(s.data(), estimates + ((p * nof_layers + v) * MAX_NSYMB_PER_SLOT + l) * nsubc, nsubc * 4);
+      }
+    }
+  }
+
+  pusch_demodulator::configuration cfg;
+  cfg.rnti = static_cast<uint16_t>(rnti);
+  cfg.rb_mask.resize(nof_prb);
+  for (unsigned i = 0; i != nof_prb; ++i) {
+    if (crbs[i]) {
+      cfg.rb_mask.set(i);
+    }
+  }
+  cfg.modulation                  = scheme_of(qm);
+  cfg.start_symbol_index          = start_symbol;
+  cfg.nof_symbols                 = nof_symbols;
+  cfg.dmrs_symb_pos               = to_symbols(dmrs_symb_mask);
+  cfg.dmrs_config_type            = dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
+  cfg.nof_cdm_groups_without_data = nof_cdm_groups_without_data;
+  cfg.n_id                        = n_id;
+  cfg.nof_tx_layers               = nof_layers;
+  cfg.enable_transform_precoding  = transform_precoding != 0;
+  for (unsigned p = 0; p != nof_rx_ports; ++p) {
+    cfg.rx_ports.push_back(static_cast<uint8_t>(p));
+  }
+
+  vector_codeword_buffer buf(span<log_likelihood_ratio>(reinterpret_cast<log_likelihood_ratio*>(llrs), nof_llrs));
+  stats_notifier         notifier;
+  demod->demodulate(buf, notifier, reader, est, cfg);
+  if (buf.count != nof_llrs || !buf.ended) {
+    return -1;
+  }
+  if (sinr_out != nullptr) {
+    for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+      sinr_out[l] = notifier.sinr[l];
+    }
+    sinr_out[MAX_NSYMB_PER_SLOT] = notifier.end_sinr;
+  }
+  return static_cast<int>(buf.nof_blocks);
+}
+
+// pusch_processor::process (pusch_processor_impl.cpp:134-386) of one PDU on a received grid
+// [P][14][nsubc] (cbf16 as uint32), configured as the reference PUSCH processor benchmark.
+// Type-1 contiguous allocation [rb_start, rb_start + rb_count) of a BWP [bwp_start, +bwp_size).
+// choice: 0 generic, 1 AVX2, 2 the "auto" factory choice (ref_builders.h).
+// rx_buffer: srs_ref_rx_buffer_create handle (HARQ process). tb: tb_bytes output bytes.
+// result[0..5] = tb_crc_ok, nof_codeblocks_total, LDPC observations, sum, min, max;
+// csi[0..3] = SINR (channel estimator, dB), EPRE dB, RSRP dB, time alignment (s).
+int srs_ref_pusch_process(const uint32_t* grid,
+                          unsigned        nof_rx_ports,
+                          unsigned        nsubc,
+                          unsigned        numerology,
+                          unsigned        slot_index,
+                          unsigned        rnti,
+                          unsigned        bwp_start,
+                          unsigned        bwp_size,
+                          int             qm,
+                          float           target_code_rate,
+                          unsigned        rv,
+                          unsigned        base_graph,
+                          int             new_data,
+                          unsigned        n_id,
+                          unsigned        nof_layers,
+                          unsigned        dmrs_symb_mask,
+                          int             dmrs_type2,
+                          unsigned        scrambling_id,
+                          int             n_scid,
+                          unsigned        nof_cdm_groups_without_data,
+                          unsigned        rb_start,
+                          unsigned        rb_count,
+                          unsigned        start_symbol,
+                          unsigned        nof_symbols,
+                          unsigned        tbs_lbrm_bytes,
+                          unsigned        iterations,
+                          int             choice,
+                          void*           rx_buffer,
+                          uint8_t*        tb,
+                          unsigned        tb_bytes,
+                          double*         result,
+                          double*         csi)
+{
+  const unsigned nof_prb = nsubc / NRE;
+  auto           bundle  = make_pusch_processor(
+      static_cast<impl>(choice), nof_prb, nof_rx_ports, nof_layers, iterations, 0, 2, 0, true);
+
+  grid_tensor data({nsubc, MAX_NSYMB_PER_SLOT, nof_rx_ports});
+  load_grid(data, grid, nof_rx_ports, nsubc);
+  std::atomic<unsigned>     empty{0};
+  resource_grid_reader_impl reader(data, empty);
+
+  pusch_processor::pdu_t pdu = {};
+  pdu.slot                   = slot_point(numerology, slot_index);
+  pdu.rnti                   = static_cast<uint16_t>(rnti);
+  pdu.bwp_size_rb            = bwp_size;
+  pdu.bwp_start_rb           = bwp_start;
+  pdu.cp                     = cyclic_prefix::NORMAL;
+  pdu.mcs_descr              = sch_mcs_description{scheme_of(qm), target_code_rate};
+  pdu.codeword.emplace(pusch_processor::codeword_description{
+      rv, base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2, new_data != 0});
+  pdu.uci.alpha_scaling         = 1.0;
+  pdu.uci.beta_offset_harq_ack  = 5.0;
+  pdu.uci.beta_offset_csi_part1 = 5.0;
+  pdu.uci.beta_offset_csi_part2 = 5.0;
+  pdu.uci.nof_harq_ack          = 0;
+  pdu.uci.nof_csi_part1         = 0;
+  pdu.n_id                      = n_id;
+  pdu.nof_tx_layers             = nof_layers;
+  for (unsigned p = 0; p != nof_rx_ports; ++p) {
+    pdu.rx_ports.push_back(static_cast<uint8_t>(p));
+  }
+  pdu.dmrs_symbol_mask   = to_symbols(dmrs_symb_mask);
+  pdu.dmrs               = pusch_processor::dmrs_configuration{.dmrs          = dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1,
+                                                               .scrambling_id = scrambling_id,
+                                                               .n_scid        = n_scid != 0,
+                                                               .nof_cdm_groups_without_data = nof_cdm_groups_without_data};
+  pdu.freq_alloc         = rb_allocation::make_type1(rb_start, rb_count);
+  pdu.start_symbol_index = start_symbol;
+  pdu.nof_symbols        = nof_symbols;
+  pdu.tbs_lbrm           = tbs_lbrm_bytes ? units::bytes(tbs_lbrm_bytes) : tbs_lbrm_default;
+
+  result_notifier  notifier;
+  unique_rx_buffer buf(*static_cast<ref_rx_buffer*>(rx_buffer));
+  bundle->proc->process(span<uint8_t>(tb, tb_bytes), std::move(buf), notifier, reader, pdu);
+  if (!notifier.done) {
+    return -1;
+  }
+  const pusch_decoder_result& r  = notifier.result.data;
+  const auto&                 st = r.ldpc_decoder_stats;
+  result[0]                      = r.tb_crc_ok ? 1 : 0;
+  result[1]                      = r.nof_codeblocks_total;
+  result[2]                      = st.get_nof_observations();
+  result[3]                      = st.get_mean() * st.get_nof_observations();
+  result[4]                      = st.get_min();
+  result[5]                      = st.get_max();
+  if (csi != nullptr) {
+    const channel_state_information& c = notifier.result.csi;
+    csi[0]                             = c.get_sinr_dB().value_or(NAN);
+    csi[1]                             = c.get_epre_dB().value_or(NAN);
+    csi[2]                             = c.get_rsrp_dB().value_or(NAN);
+    csi[3]                             = c.get_time_alignment().has_value() ? c.get_time_alignment()->to_seconds() : NAN;
+  }
+  return 0;
+}
+
+// Describes what choice 2 ("auto") selects on this host.
+const char* srs_ref_describe_choice(int choice)
+{
+  return describe(static_cast<impl>(choice));
+}
+
+} // extern "C"

@@ -14,6 +14,7 @@
 // The rx_buffer the PUSCH decoder needs is an in-memory implementation of the
 // reference's unique_rx_buffer::callback interface (the role of
 // lib/phy/upper/rx_buffer_impl.h), kept per HARQ process by the caller.
+#include "ref_builders.h"
 #include "phy/upper/channel_coding/crc_calculator_generic_impl.h"
 #include "phy/upper/channel_coding/ldpc/ldpc_decoder_avx2.h"
 #include "phy/upper/channel_coding/ldpc/ldpc_decoder_generic.h"
@@ -71,35 +72,7 @@ std::unique_ptr<pdsch_encoder_impl> make_pdsch_encoder()
                                               std::make_unique<ldpc_rate_matcher_impl>());
 }
 
-// In-memory rx_buffer (one HARQ process).
-class ref_rx_buffer : public unique_rx_buffer::callback
-{
-public:
-  explicit ref_rx_buffer(unsigned nof_cbs) : soft(nof_cbs), data(nof_cbs), crcs(nof_cbs, false)
-  {
-    for (unsigned i = 0; i != nof_cbs; ++i) {
-      soft[i].assign(3 * 8448 + 64, log_likelihood_ratio(0));
-      data[i].resize(8448 + 64);
-    }
-  }
-  unsigned   get_nof_codeblocks() const override { return soft.size(); }
-  void       reset_codeblocks_crc() override { std::fill(crcs.begin(), crcs.end(), false); }
-  span<bool> get_codeblocks_crc() override { return span<bool>(reinterpret_cast<bool*>(crcs.data()), crcs.size()); }
-  unsigned   get_absolute_codeblock_id(unsigned codeblock_id) const override { return codeblock_id; }
-  span<log_likelihood_ratio> get_codeblock_soft_bits(unsigned id, unsigned size) override
-  {
-    return span<log_likelihood_ratio>(soft[id]).first(size);
-  }
-  bit_buffer get_codeblock_data_bits(unsigned id, unsigned size) override { return data[id].first(size); }
-  bool       try_lock() override { return true; }
-  void       unlock() override {}
-  void       release() override {}
-
-private:
-  std::vector<std::vector<log_likelihood_ratio>> soft;
-  std::vector<dynamic_bit_buffer>                data;
-  std::vector<char>                              crcs;
-};
+using srs_ref::ref_rx_buffer; // in-memory rx_buffer (one HARQ process), ref_builders.h
 
 class result_catcher : public pusch_decoder_notifier
 {

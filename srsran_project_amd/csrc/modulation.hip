@@ -205,7 +205,8 @@ __global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
                a.llrs + static_cast<size_t>(i) * (a.qm < 1 ? 1 : a.qm));
 }
 
-// Soft demapping + descrambling of nof_grids codewords (PUSCH, pusch_demodulator_impl.cpp:203-330):
+// Soft demapping + descrambling of nof_grids codewords (PUSCH, pusch_demodulator_impl.cpp:203-400,
+// one demapper call per OFDM symbol as the reference makes them):
 // symbols [grid][grid_symbols], LLRs [grid][llr_stride]. A workgroup demaps DD_SYMS symbols of one
 // grid into LDS (4 per thread), builds the Gold words of its LLR range (one per lane, each wave's base
 // state jumped once on the scalar unit) and writes the descrambled LLRs 8 bytes at a time.
@@ -231,7 +232,12 @@ __global__ __launch_bounds__(256) void demap_descramble_kernel(demodulate_args a
     const uint32_t t = r * 256 + threadIdx.x, i = s0 + t;
     if (i < d.grid_symbols) {
       const size_t gs = static_cast<size_t>(g) * d.grid_symbols + i;
-      demap_symbol(a, lt, reinterpret_cast<const float2*>(a.symbols)[gs], a.noise_vars[gs], i, i < a.block_end,
+      bool simd = false;
+#pragma unroll
+      for (int l = 0; l < 14; ++l) { // uniform bounds (SGPRs): the OFDM symbol's SIMD block range
+        simd |= (i >= d.sym_lo[l]) & (i < d.simd_hi[l]);
+      }
+      demap_symbol(a, lt, reinterpret_cast<const float2*>(a.symbols)[gs], a.noise_vars[gs], i, simd,
                    s_llr + t * bpp);
     }
   }

@@ -559,13 +559,14 @@ demodulate_args srs_amd::demodulate_args_for(const srs_amd_modulator* mod, int q
 
 int srs_amd::demap_descramble_batch(srs_amd_modulator* mod, int qm, int8_t* d_llrs, uint64_t llr_stride,
                                     const float* d_symbols, const float* d_noise_vars, uint32_t grid_symbols,
-                                    uint32_t nof_grids, const uint32_t* d_jump, uint32_t c_init, void* stream)
+                                    const uint32_t* sym_counts, uint32_t nof_grids, const uint32_t* d_jump,
+                                    uint32_t c_init, void* stream)
 {
   int rc = check(mod, qm);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
-  demodulate_args a = demodulate_args_for(mod, qm, grid_symbols); // block_end per grid, as per call
+  demodulate_args a = demodulate_args_for(mod, qm, grid_symbols);
   a.symbols         = d_symbols;
   a.noise_vars      = d_noise_vars;
   demap_descramble_args d{};
@@ -574,6 +575,18 @@ int srs_amd::demap_descramble_batch(srs_amd_modulator* mod, int qm, int8_t* d_ll
   d.llr_stride   = llr_stride;
   d.grid_symbols = grid_symbols;
   d.c_init       = c_init;
+  // one demapper call per OFDM symbol: SIMD blocks of avx2_block(qm) symbols from each symbol's start
+  const uint32_t blk = avx2_block(qm);
+  uint32_t       s0  = 0;
+  for (int l = 0; l < 14; ++l) {
+    const uint32_t n = sym_counts[l];
+    d.sym_lo[l]      = s0;
+    d.simd_hi[l]     = s0 + (blk ? (n / blk) * blk : 0);
+    s0 += n;
+  }
+  if (s0 != grid_symbols) {
+    return fail(SRS_AMD_EINVAL, "per-symbol counts (%u) do not add up to the grid symbols (%u)", s0, grid_symbols);
+  }
   std::lock_guard<std::mutex> lock(mod->mtx);
   hipError_t                  e = hipSetDevice(mod->device);
   if (e == hipSuccess) {

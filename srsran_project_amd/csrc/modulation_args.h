@@ -56,8 +56,13 @@ struct demap_descramble_args {
   int8_t*         llrs;         // [grid][llr_stride]
   const uint32_t* jump;         // gold_jump_tables()
   uint64_t        llr_stride;
-  uint32_t        grid_symbols; // symbols per grid (block_end of demodulate_args is per grid)
+  uint32_t        grid_symbols; // symbols per grid
   uint32_t        c_init;
+  // The reference demaps each OFDM symbol in its own call (pusch_demodulator_impl.cpp:363-400), so the
+  // SIMD blocks end at every symbol's end: symbols [sym_lo[l], simd_hi[l]) of the grid take the SIMD
+  // arithmetic, the rest of [sym_lo[l], sym_lo[l + 1]) the scalar tail (sym_lo = simd_hi when empty).
+  uint32_t        sym_lo[14];
+  uint32_t        simd_hi[14];
 };
 hipError_t launch_demap_descramble(const demodulate_args& a, const demap_descramble_args& d, uint32_t nof_grids,
                                    hipStream_t stream);
@@ -73,9 +78,10 @@ demodulate_args demodulate_args_for(const srs_amd_modulator* mod, int qm, uint32
 
 // Soft demapping of nof_grids x grid_symbols symbols and descrambling of each grid's LLRs with the
 // Gold sequence of c_init, one launch (the PUSCH demodulator's last two steps).
+// sym_counts[l]: demapper symbols (REs x layers) of OFDM symbol l, in grid order (sum = grid_symbols).
 int demap_descramble_batch(srs_amd_modulator* mod, int qm, int8_t* d_llrs, uint64_t llr_stride, const float* d_symbols,
-                           const float* d_noise_vars, uint32_t grid_symbols, uint32_t nof_grids,
-                           const uint32_t* d_jump, uint32_t c_init, void* stream);
+                           const float* d_noise_vars, uint32_t grid_symbols, const uint32_t* sym_counts,
+                           uint32_t nof_grids, const uint32_t* d_jump, uint32_t c_init, void* stream);
 hipError_t launch_scramble_bits(const prbs_args& a, hipStream_t stream);
 hipError_t launch_descramble_llrs(const prbs_args& a, hipStream_t stream);
 

@@ -52,6 +52,7 @@ struct srs_amd_pusch_demod_plan {
   uint32_t      span_subc   = 0;
   int32_t       qm          = 0;
   uint32_t      c_init      = 0;
+  uint32_t      sym_counts[14] = {}; // demapper symbols (data REs x layers) per OFDM symbol
   uint32_t*     d_table     = nullptr;
   ~srs_amd_pusch_demod_plan()
   {
@@ -174,7 +175,9 @@ int srs_amd_pusch_demod_plan_create(srs_amd_pusch_demodulator*        dem,
   const uint32_t        dmrs_excl = dmrs_prb_mask(cfg->dmrs_type, cfg->nof_cdm_groups_without_data);
   std::vector<uint32_t> table(14 * nof_prb, 0);
   uint32_t              count = 0;
+  uint32_t              sym_counts[14];
   for (uint32_t l = 0; l < 14; ++l) {
+    const uint32_t sym_start = count;
     const bool in_time = l >= cfg->start_symbol && l < cfg->start_symbol + cfg->nof_symbols;
     const bool dmrs    = (cfg->dmrs_symbol_mask >> l) & 1u;
     for (uint32_t c = 0; c < nof_prb; ++c) {
@@ -185,6 +188,7 @@ int srs_amd_pusch_demod_plan_create(srs_amd_pusch_demodulator*        dem,
       table[l * nof_prb + c] = (count << 12) | m;
       count += static_cast<uint32_t>(__builtin_popcount(m));
     }
+    sym_counts[l] = count - sym_start;
   }
   auto* p         = new srs_amd_pusch_demod_plan();
   p->device       = dem->device;
@@ -194,6 +198,9 @@ int srs_amd_pusch_demod_plan_create(srs_amd_pusch_demodulator*        dem,
   p->span_subc    = (hi - lo) * 12;
   p->qm           = qm;
   p->c_init       = cfg->rnti * (1u << 15) + cfg->n_id; // pusch_demodulator_impl.cpp:209
+  for (uint32_t l = 0; l < 14; ++l) {
+    p->sym_counts[l] = sym_counts[l] * cfg->nof_tx_layers;
+  }
   pusch_eq_args& a = p->args;
   a.nof_subc       = nof_subc;
   a.nof_prb        = nof_prb;
@@ -277,8 +284,38 @@ int srs_amd_pusch_demodulate_batch(srs_amd_pusch_demodulator*      dem,
   }
   // soft demapper + descrambling (revert_scrambling) in one pass: LLRs straight into the caller's rows
   return demap_descramble_batch(dem->demapper, plan->qm, d_llrs, llr_stride, reinterpret_cast<const float*>(a.eq_symbols),
-                                a.eq_noise_vars, static_cast<uint32_t>(plan->args.nof_re * plan->nof_layers), nof_grids,
-                                dem->d_jump, plan->c_init, stream);
+                                a.eq_noise_vars, static_cast<uint32_t>(plan->args.nof_re * plan->nof_layers),
+                                plan->sym_counts, nof_grids, dem->d_jump, plan->c_init, stream);
+}
+
+int srs_amd_pusch_demap_descramble_batch(srs_amd_pusch_demodulator*      dem,
+                                         const srs_amd_pusch_demod_plan* plan,
+                                         const float*                    d_eq_symbols,
+                                         const float*                    d_eq_noise_vars,
+                                         int8_t*                         d_llrs,
+                                         uint64_t                        llr_stride,
+                                         uint32_t                        nof_grids,
+                                         void*                           stream)
+{
+  if (dem == nullptr || plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_grids == 0 || plan->args.nof_re == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_eq_symbols == nullptr || d_eq_noise_vars == nullptr || d_llrs == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  if (nof_grids > 1 && llr_stride < plan->nof_llrs()) {
+    return fail(SRS_AMD_EINVAL, "LLR stride too small");
+  }
+  hipError_t e = hipSetDevice(dem->device);
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH demodulator device");
+  }
+  return demap_descramble_batch(dem->demapper, plan->qm, d_llrs, llr_stride, d_eq_symbols, d_eq_noise_vars,
+                                static_cast<uint32_t>(plan->args.nof_re * plan->nof_layers), plan->sym_counts,
+                                nof_grids, dem->d_jump, plan->c_init, stream);
 }
 
 int srs_amd_pusch_demodulate(srs_amd_pusch_demodulator*      dem,

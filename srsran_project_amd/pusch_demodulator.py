@@ -62,6 +62,7 @@ def _declare(lib):
         "srs_amd_pusch_demod_plan_destroy": (None, [P]),
         "srs_amd_pusch_demodulate": (c.c_int, [P, P, P, P, P, P]),
         "srs_amd_pusch_demodulate_batch": (c.c_int, [P, P, P, c.c_uint64, P, c.c_uint64, P, P, c.c_uint64, u, P]),
+        "srs_amd_pusch_demap_descramble_batch": (c.c_int, [P, P, P, P, P, c.c_uint64, u, P]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -158,4 +159,23 @@ class PuschDemodulator:
             self._h, plan._h, grids.data_ptr(), grids.stride(0), estimates.data_ptr(), estimates.stride(0),
             stats.data_ptr(), llrs.data_ptr(), llrs.stride(0), n, ctypes.c_void_p(stream.cuda_stream)),
             "pusch_demodulate_batch")
+        return llrs
+
+    def demap_descramble_batch(self, eq_symbols, eq_noise_vars, plan, llrs=None, stream=None):
+        """Device: the demodulator's soft demapping (per OFDM symbol) + descrambling of equalized symbols
+        complex64 [n][nof_re * layers] and noise variances float32 [n][nof_re * layers]."""
+        import torch
+
+        n = eq_symbols.shape[0]
+        if eq_symbols.shape[1] != plan.nof_re * plan.config.nof_tx_layers or eq_noise_vars.shape != eq_symbols.shape:
+            raise ValueError("equalized symbols must be [n][nof_re * layers]")
+        if not (eq_symbols.is_contiguous() and eq_noise_vars.is_contiguous()):
+            raise ValueError("equalized symbols must be contiguous")
+        if llrs is None:
+            llrs = torch.empty((n, plan.nof_llrs), dtype=torch.int8, device=eq_symbols.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(eq_symbols.device)
+        _lib.check(self._lib.srs_amd_pusch_demap_descramble_batch(
+            self._h, plan._h, eq_symbols.data_ptr(), eq_noise_vars.data_ptr(), llrs.data_ptr(), llrs.stride(0), n,
+            ctypes.c_void_p(stream.cuda_stream)), "pusch_demap_descramble_batch")
         return llrs

@@ -395,3 +395,31 @@ def test_pusch_chest_matches_reference(case):
     got, gs = chest.pusch_chest(grid, estimates=est0, **kw)
     chest_cases.assert_estimates_close(got, want, case[0])
     chest_cases.assert_stats_close(gs, ws, case[0])
+
+
+@pytest.mark.skipif(oracle.REF is None, reason="oracle/_ref not built")
+@pytest.mark.parametrize("case_idx", range(10))
+def test_pusch_demodulator_matches_reference(case_idx):
+    """The restated PUSCH demodulator tail (one demapper call per OFDM symbol, descrambling) on the
+    reference equalizer's per-symbol output reproduces pusch_demodulator_impl bit-exactly; the
+    float64-equalizer restatement is within one LLR step."""
+    from oracle import pusch_demod as od
+    from tests.pusch_demod_cases import CASES, assert_llrs_close, demod_args, dyadic_equalized, make_case
+
+    case = CASES[case_idx]
+    name, P, L, nprb, _, qm, start, nsym, dmrs, ncdm = case
+    grid, est, nv, crbs = make_case(case, 7, "random")
+    want = od.ref_pusch_demodulate(grid, est, nv, 0x4601, 17, crbs=crbs, **demod_args(case))
+    a = dict(demod_args(case))
+    a.pop("qm")
+    eq, env = od.ref_equalize_per_symbol(grid, est, nv, crbs, **a)
+    counts = od.data_re_mask(12 * nprb, crbs, start, nsym, dmrs, False, ncdm).sum(axis=1) * L
+    got = od.demap_descramble_per_symbol(eq, env, counts, qm, 0x4601 * (1 << 15) + 17)
+    assert np.array_equal(got, want), name
+    assert_llrs_close(od.pusch_demodulate(grid, est, nv, 0x4601, 17, crbs=crbs, **demod_args(case)), want, name,
+                      0.97)
+    # demapper ties: restated per-symbol demapping == the reference demapper per symbol
+    if qm >= 4:
+        deq, dnv = dyadic_equalized(qm, int(counts.sum()), 3, oracle.ref_demodulate)
+        ref = od.demap_descramble_per_symbol(deq, dnv, counts, qm, 99, demod=oracle.ref_demodulate)
+        assert np.array_equal(od.demap_descramble_per_symbol(deq, dnv, counts, qm, 99), ref), name

@@ -1,56 +1,52 @@
 """GPU parity: MI355X PUSCH demodulator (fused RE gather + equalizer, soft
-demapper, descrambler; through the C-ABI) vs the CPU oracle
-oracle/pusch_demod.py (a composition of restatements each pinned to the
-reference).  Bar: float equalizer inside, so LLRs agree within one
-quantisation step (|dLLR| <= 1) and at least 99 % of them exactly."""
+demapper, descrambler; through the C-ABI) against the REFERENCE's own
+pusch_demodulator_impl (oracle/_ref, ref_wrapper_pusch.cpp) and the restated
+oracle (oracle/pusch_demod.py).
+
+Bars:
+  * demapper + descrambler on the reference's own equalized symbols
+    (pusch_demod_cases / ref_equalize_per_symbol, the exact values the reference
+    class demaps): bit-exact with the reference class, which pins the
+    per-OFDM-symbol demapper blocks (pusch_demodulator_impl.cpp:363-400);
+  * the same stage on dyadic symbols chosen so that the reference demapper's SIMD
+    and scalar-tail arithmetic differ: bit-exact with the reference demapper
+    called once per OFDM symbol (and provably different from one call per codeword);
+  * full demodulator (GPU float equalizer inside): |dLLR| <= 1 and >= 99 % equal
+    against the reference class (>= 97 % on the narrow 16QAM/256QAM cases and the
+    identity channels, where the reference's approximate-reciprocal equalizer
+    moves more LLRs).
+"""
 import numpy as np
 import pytest
 
+import oracle
 from oracle import pusch_demod as od
-from tests.chest_cases import bf16_grid
+from tests.pusch_demod_cases import CASES, assert_llrs_close, demod_args, SIMD_BLOCK, dyadic_equalized, make_case
 
 pytestmark = pytest.mark.gpu
 
-# (name, ports, layers, nof_prb, crbs, qm, start, nsym, dmrs mask, cdm groups without data)
-CASES = [
-    ("1x1_qpsk", 1, 1, 52, (0, 52), 2, 0, 14, (1 << 2) | (1 << 11), 2),
-    ("2x1_16qam_cdm1", 2, 1, 52, (4, 40), 4, 1, 13, (1 << 2), 1),
-    ("4x1_64qam", 4, 1, 106, (0, 106), 6, 0, 14, (1 << 2) | (1 << 7) | (1 << 11), 2),
-    ("2x2_256qam_273", 2, 2, 273, (0, 273), 8, 0, 14, (1 << 2) | (1 << 11), 2),
-    ("4x2_64qam", 4, 2, 51, (0, 51), 6, 0, 14, (1 << 2), 1),
-]
+RNTI, N_ID = 0x1234, 321
+C_INIT = RNTI * (1 << 15) + N_ID
+NARROW = {"2x1_16qam_cdm1", "1x1_16qam_5prb_tail", "2x1_256qam_7prb_tail"}
 
 
-def _make(case, seed):
-    name, P, L, nprb, (lo, hi), qm, start, nsym, dmrs, ncdm = case
-    rng = np.random.default_rng(seed)
-    nsubc = 12 * nprb
-    k = np.arange(nsubc)
-    h = np.zeros((P, L, 14, nsubc), np.complex64)
-    for p in range(P):
-        for v in range(L):
-            h[p, v] = ((0.7 + 0.2 * p - 0.3j * v) * np.exp(-2j * np.pi * k * (2 + p + 3 * v) / 4096))[None, :]
-    x = ((rng.integers(0, 2, (L, 14, nsubc)) * 2 - 1) + 1j * (rng.integers(0, 2, (L, 14, nsubc)) * 2 - 1)) * 0.7
-    y = np.einsum("pvls,vls->pls", h, x) + 0.05 * (rng.normal(size=(P, 14, nsubc)) + 1j * rng.normal(size=(P, 14, nsubc)))
-    nv = (0.005 * (1 + 0.1 * np.arange(P))).astype(np.float32)
-    crbs = list(range(lo, hi))
-    return bf16_grid(y), bf16_grid(h), nv, crbs
-
-
-def _cfg(case, crbs, rnti=0x1234, n_id=321):
+def _cfg(case, crbs):
     import srsran_project_amd as amd
 
     name, P, L, nprb, _, qm, start, nsym, dmrs, ncdm = case
-    return amd.PuschDemodulatorConfig(rnti=rnti, crbs=crbs, modulation=qm, start_symbol=start, nof_symbols=nsym,
-                                      dmrs_symb_pos=dmrs, n_id=n_id, nof_tx_layers=L, nof_rx_ports=P,
+    return amd.PuschDemodulatorConfig(rnti=RNTI, crbs=crbs, modulation=qm, start_symbol=start, nof_symbols=nsym,
+                                      dmrs_symb_pos=dmrs, n_id=N_ID, nof_tx_layers=L, nof_rx_ports=P,
                                       nof_cdm_groups_without_data=ncdm)
 
 
-def _check(got, want, what):
-    assert got.shape == want.shape, what
-    d = np.abs(got.astype(np.int16) - want.astype(np.int16))
-    assert d.max() <= 1, "%s: max |dLLR| %d" % (what, d.max())
-    assert (d == 0).mean() >= 0.99, "%s: only %.4f equal" % (what, (d == 0).mean())
+def _counts(case, crbs):
+    name, P, L, nprb, _, qm, start, nsym, dmrs, ncdm = case
+    mask = od.data_re_mask(12 * nprb, crbs, start, nsym, dmrs, False, ncdm)
+    return mask.sum(axis=1) * L
+
+
+def _stats(nv):
+    return [{"noise_var": v, "epre": 0, "rsrp": 0, "snr": 0, "time_alignment_s": 0, "cfo_hz": 0} for v in nv]
 
 
 @pytest.fixture(scope="module")
@@ -60,23 +56,69 @@ def dem():
     return amd.PuschDemodulator(device=0)
 
 
+def _gpu_demap(dem, plan, eq, nv):
+    import torch
+
+    e = torch.from_numpy(np.ascontiguousarray(eq[None], np.complex64)).to("cuda:0")
+    v = torch.from_numpy(np.ascontiguousarray(nv[None], np.float32)).to("cuda:0")
+    out = dem.demap_descramble_batch(e, v, plan)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()[0]
+
+
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_pusch_demodulate_host(dem, case):
-    grid, est, nv, crbs = _make(case, 3)
+def test_demap_descramble_on_reference_equalizer_bit_exact(dem, case):
+    grid, est, nv, crbs = make_case(case, 5, "random")
+    a = dict(demod_args(case))
+    a.pop("qm")
+    eq, env = od.ref_equalize_per_symbol(grid, est, nv, crbs, **a)
+    want = od.ref_pusch_demodulate(grid, est, nv, RNTI, N_ID, crbs=crbs, **demod_args(case))
+    got = _gpu_demap(dem, dem.plan(_cfg(case, crbs), 12 * case[3]), eq, env)
+    assert np.array_equal(got, want), "%s: %d LLRs differ from pusch_demodulator_impl" % (case[0],
+                                                                                         int((got != want).sum()))
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[5] >= 4], ids=[c[0] for c in CASES if c[5] >= 4])
+def test_demap_blocks_follow_ofdm_symbols(dem, case):
+    """Dyadic equalized symbols (many land on the rounding ties where the reference demapper's SIMD and
+    scalar paths differ): the GPU equals per-OFDM-symbol demapping exactly."""
     name, P, L, nprb, _, qm, start, nsym, dmrs, ncdm = case
-    want = od.pusch_demodulate(grid, est, nv, 0x1234, 321, qm, crbs, start, nsym, dmrs, False, ncdm, L)
-    got = dem.demodulate(grid, est, [{"noise_var": v, "epre": 0, "rsrp": 0, "snr": 0, "time_alignment_s": 0,
-                                      "cfo_hz": 0} for v in nv], _cfg(case, crbs))
-    _check(got, want, name)
+    crbs = list(range(*case[4]))
+    counts = _counts(case, crbs)
+    n = int(counts.sum())
+    eq, nv = dyadic_equalized(qm, n, 11, oracle.ref_demodulate)
+    want = od.demap_descramble_per_symbol(eq, nv, counts, qm, C_INIT, demod=oracle.ref_demodulate)
+    got = _gpu_demap(dem, dem.plan(_cfg(case, crbs), 12 * nprb), eq, nv)
+    assert np.array_equal(got, want), "%s: %d LLRs differ" % (name, int((got != want).sum()))
+    restated = od.demap_descramble_per_symbol(eq, nv, counts, qm, C_INIT)
+    assert np.array_equal(restated, want)
+    blk = SIMD_BLOCK[qm]
+    if any(c % blk for c in counts):
+        whole = od.demap_descramble_per_symbol(eq, nv, [n], qm, C_INIT, demod=oracle.ref_demodulate)
+        assert not np.array_equal(whole, want), "case does not exercise a tail"
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("kind", ["random", "identity"])
+def test_pusch_demodulate_host_vs_reference(dem, case, kind):
+    grid, est, nv, crbs = make_case(case, 3, kind)
+    want = od.ref_pusch_demodulate(grid, est, nv, RNTI, N_ID, crbs=crbs, **demod_args(case))
+    got = dem.demodulate(grid, est, _stats(nv), _cfg(case, crbs))
+    # identity channels: the reference's approximate reciprocal (1 - 2^-12 on |h|^2 = 1) biases every
+    # equalized value the same way, so more LLRs sit one step away than on a random channel
+    assert_llrs_close(got, want, case[0], 0.97 if (case[0] in NARROW or kind == "identity") else 0.99)
+    # the restated oracle (float64 equalizer) as a second opinion
+    rest = od.pusch_demodulate(grid, est, nv, RNTI, N_ID, crbs=crbs, **demod_args(case))
+    assert_llrs_close(got, rest, case[0] + " (restated)", 0.97)
 
 
 def test_pusch_demodulate_batch(dem):
     import torch
 
-    case = CASES[3]
+    case = CASES[6]  # 4x2 256QAM 273 PRB
     name, P, L, nprb, _, qm, start, nsym, dmrs, ncdm = case
     n = 2
-    data = [_make(case, s) for s in range(n)]
+    data = [make_case(case, s) for s in range(n)]
     crbs = data[0][3]
     plan = dem.plan(_cfg(case, crbs), 12 * nprb)
     g = torch.from_numpy(np.stack([d[0] for d in data]).view(np.int32)).to("cuda:0")
@@ -88,6 +130,6 @@ def test_pusch_demodulate_batch(dem):
     torch.cuda.synchronize()
     got = llrs.cpu().numpy()
     for i in range(n):
-        want = od.pusch_demodulate(data[i][0], data[i][1], data[i][2], 0x1234, 321, qm, crbs, start, nsym, dmrs,
-                                   False, ncdm, L)
-        _check(got[i], want, "grid %d" % i)
+        want = od.ref_pusch_demodulate(data[i][0], data[i][1], data[i][2], RNTI, N_ID, crbs=crbs,
+                                       **demod_args(case))
+        assert_llrs_close(got[i], want, "grid %d" % i)
