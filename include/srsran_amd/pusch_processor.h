@@ -1,0 +1,146 @@
+/*
+ * srsran_amd/pusch_processor.h -- C-ABI of the MI355X PUSCH processor: DM-RS
+ * channel estimation -> demodulation (equalizer, soft demapper, descrambler)
+ * -> UL-SCH decoding (rate dematching, LDPC, CB/TB CRC) of a batch of received
+ * slot grids, one transport block per grid.
+ *
+ * Replaces (reference interface):
+ *   pusch_processor::process(span<uint8_t> data, unique_rx_buffer rm_buffer,
+ *                            pusch_processor_result_notifier& notifier,
+ *                            const resource_grid_reader& grid, const pdu_t& pdu)
+ *       include/srsran/phy/upper/channel_processors/pusch/pusch_processor.h:181
+ *       (impl lib/phy/upper/channel_processors/pusch/pusch_processor_impl.cpp:134-386)
+ *   created as pusch_processor_factory_sw_configuration describes
+ *       (include/srsran/phy/upper/channel_processors/pusch/factories.h:107-130).
+ *
+ * Composition: srs_amd_pusch_chest (pusch_chest.h) -> srs_amd_pusch_demodulator
+ * (pusch_demodulator.h) -> srs_amd_pusch_decoder (sch.h), three asynchronous
+ * stages on the caller's stream; the processor owns the intermediate channel
+ * estimates, port measurements and codeword LLRs in HBM.
+ * Derived exactly as pusch_processor_impl does it: DM-RS scaling
+ * convert_dB_to_amplitude(-get_sch_to_dmrs_ratio_dB(cdm groups)) (:193),
+ * Nref = compute_N_ref(tbs_lbrm, C) (ldpc.h:225), nof_ch_symbols from
+ * get_ulsch_information without UCI (all data REs x layers), rb_mask of the
+ * type-1 allocation relative to the BWP (:166).
+ * Scope: data-only PUSCH (no UCI multiplexing, the pdu carries a codeword),
+ * pseudo-random DM-RS type 1 (no transform precoding), no intra-slot frequency
+ * hopping, no DC-carrier zeroing (pdu.dc_position unset), as the estimator and
+ * demodulator C-ABIs support.
+ */
+#ifndef SRSRAN_AMD_PUSCH_PROCESSOR_H
+#define SRSRAN_AMD_PUSCH_PROCESSOR_H
+
+#include <stdint.h>
+
+#include "srsran_amd/pusch_chest.h"
+#include "srsran_amd/pusch_demodulator.h"
+#include "srsran_amd/sch.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* pusch_processor_factory_sw_configuration (factories.h:107-130) / the components it
+ * builds (pusch_processor_benchmark.cpp:133-140, 560-640). */
+typedef struct srs_amd_pusch_processor_config {
+  uint32_t dec_nof_iterations;    /* LDPC iterations (factory default 10; the benchmark uses 2) */
+  int32_t  dec_enable_early_stop; /* CRC early stop */
+  int32_t  dec_force_decoding;
+  int32_t  equalizer;             /* SRS_AMD_EQ_ZF / SRS_AMD_EQ_MMSE */
+  int32_t  fd_smoothing;          /* SRS_AMD_CHEST_FD_* */
+  int32_t  td_interpolation;      /* SRS_AMD_CHEST_TD_* */
+  int32_t  compensate_cfo;
+  int32_t  ldpc_arith;            /* SRS_AMD_ARITH_SIMD ("auto" on x86) or SRS_AMD_ARITH_GENERIC */
+} srs_amd_pusch_processor_config;
+
+/* pusch_processor::pdu_t (pusch_processor.h:117-167), data-only subset. */
+typedef struct srs_amd_pusch_pdu {
+  uint32_t numerology;        /* slot */
+  uint32_t slot_index;
+  uint32_t rnti;
+  uint32_t bwp_start_rb;
+  uint32_t bwp_size_rb;
+  int32_t  modulation;        /* mcs_descr.modulation as Qm (2, 4, 6, 8) */
+  float    target_code_rate;  /* mcs_descr.target_code_rate (R x 1024) */
+  uint32_t rv;                /* codeword */
+  uint32_t base_graph;        /* 1 or 2 */
+  int32_t  new_data;
+  uint32_t n_id;
+  uint32_t nof_tx_layers;
+  uint32_t nof_rx_ports;      /* rx_ports = 0 .. nof_rx_ports - 1 */
+  uint32_t dmrs_symbol_mask;
+  uint32_t dmrs_type;         /* 1 */
+  uint32_t scrambling_id;     /* dmrs_configuration */
+  uint32_t n_scid;
+  uint32_t nof_cdm_groups_without_data;
+  uint32_t rb_start;          /* freq_alloc: type-1 VRBs [rb_start, rb_start + rb_count) of the BWP */
+  uint32_t rb_count;
+  uint32_t start_symbol_index;
+  uint32_t nof_symbols;
+  uint32_t tbs_lbrm_bytes;    /* 0: tbs_lbrm_default (159749) */
+  uint32_t tbs;               /* transport block size in bits (data.size() * 8) */
+} srs_amd_pusch_pdu;
+
+/* Per-transport-block results: pusch_decoder_result (sch.h) and the channel
+ * state information channel_estimate::get_channel_state_information derives
+ * (channel_estimation.h:244-286): SINR from the channel estimator
+ * (layer-0 RSRP summed over ports / noise variances summed over ports), EPRE
+ * and RSRP averaged linearly over ports, time alignment of the best-SNR port. */
+typedef struct srs_amd_pusch_processor_result {
+  srs_amd_pusch_decoder_result data;
+  float                        sinr_db;
+  float                        epre_db;
+  float                        rsrp_db;
+  float                        time_alignment_s;
+} srs_amd_pusch_processor_result;
+
+typedef struct srs_amd_pusch_processor      srs_amd_pusch_processor;
+typedef struct srs_amd_pusch_processor_plan srs_amd_pusch_processor_plan;
+
+int  srs_amd_pusch_processor_create(srs_amd_pusch_processor**             proc,
+                                    const srs_amd_pusch_processor_config* cfg,
+                                    int                                   device);
+void srs_amd_pusch_processor_destroy(srs_amd_pusch_processor* proc);
+
+/* Resolves a PDU for grids of nof_subc subcarriers (host, once per configuration):
+ * estimator configuration, demodulator data-RE table, segmentation plan.
+ * Outputs (optional): the UL-SCH plan and the HARQ soft-buffer bytes per TB. */
+int  srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
+                                         const srs_amd_pusch_pdu*       pdu,
+                                         uint32_t                       nof_subc,
+                                         srs_amd_pusch_processor_plan** plan,
+                                         srs_amd_sch_plan*              sch_plan,
+                                         uint64_t*                      soft_buffer_bytes);
+void srs_amd_pusch_processor_plan_destroy(srs_amd_pusch_processor_plan* plan);
+
+/* DEVICE, asynchronous: nof_grids received grids cbf16 [grid][port][14][nof_subc]
+ * (grid_stride uint32 apart) -> transport blocks (rows of tb_stride bytes) and
+ * d_results[nof_grids]. d_soft: nof_grids HARQ soft buffers (soft_buffer_bytes
+ * each, kept between transmissions by the caller) or NULL for new-data-only
+ * decoding. Optional d_port_stats [grid][port] receives the estimator measurements. */
+int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
+                                const srs_amd_pusch_processor_plan* plan,
+                                const uint32_t*                     d_grids,
+                                uint64_t                            grid_stride,
+                                uint32_t                            nof_grids,
+                                uint8_t*                            d_tbs,
+                                uint32_t                            tb_stride,
+                                srs_amd_pusch_processor_result*     d_results,
+                                int8_t*                             d_soft,
+                                srs_amd_chest_port_stats*           d_port_stats,
+                                void*                               stream);
+
+/* HOST, synchronous: one grid [port][14][nof_subc]; tb gets tbs/8 bytes;
+ * soft_buffer: HOST HARQ buffer of soft_buffer_bytes (or NULL for new data only). */
+int srs_amd_pusch_process(srs_amd_pusch_processor*            proc,
+                          const srs_amd_pusch_processor_plan* plan,
+                          const uint32_t*                     grid,
+                          uint8_t*                            tb,
+                          srs_amd_pusch_processor_result*     result,
+                          int8_t*                             soft_buffer);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRSRAN_AMD_PUSCH_PROCESSOR_H */

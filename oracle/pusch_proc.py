@@ -1,0 +1,123 @@
+"""The REFERENCE's own PUSCH processor and a UE PUSCH transmitter -- TEST
+INFRASTRUCTURE ONLY (tests/, bench.py's cpu_baseline leg).
+
+ref_pusch_process: pusch_processor_impl::process (pusch_processor_impl.cpp:134-386)
+compiled from /root/reference (oracle/ref_wrapper_pusch.cpp, ref_builders.h),
+configured as the reference PUSCH processor benchmark (ZF, filter FD smoothing,
+interpolate TD, CFO compensation, `iterations` LDPC iterations with early stop).
+
+ue_transmit: a UE PUSCH transmission without transform precoding built from the
+reference's own transmit classes (pdsch_encoder_impl for the UL-SCH coding --
+identical TS 38.212 6.2 chain --, pdsch_modulator_impl for scrambling with
+c_init = rnti * 2^15 + n_id, modulation and RE mapping, dmrs_pdsch_processor_impl
+for the type-1 pseudo-random DM-RS of TS 38.211 6.4.1.1 -- the same sequence and
+mapping as PDSCH), DM-RS amplitude = the processor's estimator scaling
+convert_dB_to_amplitude(-beta_DMRS) (pusch_processor_impl.cpp:193).
+"""
+import ctypes as _c
+
+import numpy as np
+
+from . import REF, RefRxBuffer, _ptr, ref_pdsch_encode
+from . import sch as osch
+
+CHOICE = {"generic": 0, "avx2": 1, "auto": 2}
+BETA_DMRS_DB = {1: 0.0, 2: -3.0, 3: -4.77}
+
+if REF is not None and hasattr(REF, "srs_ref_pusch_process"):
+    REF.srs_ref_pusch_process.restype = _c.c_int
+    REF.srs_ref_pusch_process.argtypes = ([_c.c_void_p] + [_c.c_uint] * 7 + [_c.c_int, _c.c_float, _c.c_uint,
+                                                                             _c.c_uint, _c.c_int, _c.c_uint,
+                                                                             _c.c_uint, _c.c_uint, _c.c_int, _c.c_uint,
+                                                                             _c.c_int, _c.c_uint]
+                                          + [_c.c_uint] * 6 + [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_uint,
+                                                               _c.c_void_p, _c.c_void_p])
+    REF.srs_ref_describe_choice.restype = _c.c_char_p
+    REF.srs_ref_describe_choice.argtypes = [_c.c_int]
+
+
+def dmrs_scaling(nof_cdm_groups_without_data):
+    return float(np.power(np.float32(10.0), np.float32(-BETA_DMRS_DB[nof_cdm_groups_without_data]) / np.float32(20.0)))
+
+
+def nof_codeblocks(tbs, bg):
+    b = tbs + (24 if tbs > 3824 else 16)
+    m = 8448 if bg == 1 else 3840
+    return 1 if b <= m else -(-b // (m - 24))
+
+
+def nref(tbs, bg, tbs_lbrm_bytes=0):
+    lbrm = tbs_lbrm_bytes or 159749
+    return min(lbrm * 8 * 3 // (2 * nof_codeblocks(tbs, bg)), 384 * 66)
+
+
+def describe(choice="auto"):
+    return REF.srs_ref_describe_choice(CHOICE[choice]).decode()
+
+
+def ref_pusch_process(grid, pdu, tb_bytes, iterations=2, choice="auto", rx_buffer=None):
+    """grid uint32 [P][14][nsubc]; pdu: dict with the PuschPdu fields. Returns (tb, result dict)."""
+    if REF is None:
+        raise RuntimeError("oracle/_ref not built")
+    g = np.ascontiguousarray(grid, np.uint32)
+    P, _, nsubc = g.shape
+    C = nof_codeblocks(tb_bytes * 8, pdu["base_graph"])
+    buf = rx_buffer or RefRxBuffer(C)
+    tb = np.zeros(tb_bytes, np.uint8)
+    res = np.zeros(6, np.float64)
+    csi = np.zeros(4, np.float64)
+    r = REF.srs_ref_pusch_process(
+        _ptr(g), P, nsubc, pdu["numerology"], pdu["slot_index"], pdu["rnti"], pdu["bwp_start_rb"], pdu["bwp_size_rb"],
+        pdu["modulation"], float(pdu["target_code_rate"]), pdu["rv"], pdu["base_graph"], int(pdu["new_data"]),
+        pdu["n_id"], pdu["nof_tx_layers"], pdu["dmrs_symbol_mask"], 0, pdu["scrambling_id"], int(pdu["n_scid"]),
+        pdu["nof_cdm_groups_without_data"], pdu["rb_start"], pdu["rb_count"], pdu["start_symbol_index"],
+        pdu["nof_symbols"], pdu.get("tbs_lbrm_bytes", 0), iterations, CHOICE[choice], buf.h, _ptr(tb), tb_bytes,
+        _ptr(res), _ptr(csi))
+    if r != 0:
+        raise RuntimeError("reference PUSCH processor did not notify")
+    return tb, dict(tb_crc_ok=bool(res[0]), nof_codeblocks_total=int(res[1]), nof_observations=int(res[2]),
+                    iterations_sum=int(round(res[3])), iterations_min=int(res[4]), iterations_max=int(res[5]),
+                    sinr_db=csi[0], epre_db=csi[1], rsrp_db=csi[2], time_alignment_s=csi[3])
+
+
+def ue_transmit(tb, pdu, nsubc, channel=None, snr_db=None, seed=0, nof_rx_ports=None):
+    """UE PUSCH transmission of transport block bytes `tb` for `pdu` (dict), through `channel`
+    (complex [layer][rx port], default identity) plus AWGN at snr_db (None: noiseless).
+    Returns the received grid uint32 [rx ports][14][nsubc] (cbf16) and the UL-SCH plan."""
+    from .pdsch_mod import ref_dmrs_pdsch_map, ref_pdsch_modulate, to_bf16
+    from .pusch_demod import data_re_mask
+
+    L = pdu["nof_tx_layers"]
+    P = nof_rx_ports or pdu["nof_rx_ports"]
+    if channel is None:
+        channel = np.eye(L, P, dtype=np.complex64)
+    channel = np.asarray(channel, np.complex64)
+    crb0 = pdu["bwp_start_rb"] + pdu["rb_start"]
+    crbs = list(range(crb0, crb0 + pdu["rb_count"]))
+    mask = data_re_mask(nsubc, crbs, pdu["start_symbol_index"], pdu["nof_symbols"], pdu["dmrs_symbol_mask"], False,
+                        pdu["nof_cdm_groups_without_data"])
+    nre = int(mask.sum())
+    tbs = len(tb) * 8
+    p = osch.plan(tbs, pdu["base_graph"], pdu["rv"], pdu["modulation"], nref(tbs, pdu["base_graph"],
+                                                                            pdu.get("tbs_lbrm_bytes", 0)),
+                  L, nre * L)
+    cw = ref_pdsch_encode(np.asarray(tb, np.uint8), p)
+    grid = np.zeros((P, 14, nsubc, 2), np.uint16)
+    ref_pdsch_modulate(grid, cw, pdu["rnti"], pdu["n_id"], pdu["modulation"], crbs, pdu["start_symbol_index"],
+                       pdu["nof_symbols"], pdu["dmrs_symbol_mask"], False, pdu["nof_cdm_groups_without_data"], [],
+                       channel, 1.0, bwp=(0, nsubc // 12))
+    ref_dmrs_pdsch_map(grid, pdu["slot_index"], 0, False, pdu["scrambling_id"], pdu["n_scid"],
+                       dmrs_scaling(pdu["nof_cdm_groups_without_data"]), pdu["dmrs_symbol_mask"], crbs,
+                       channel[None], numerology=pdu["numerology"])
+    g = grid.view(np.uint32).reshape(P, 14, nsubc)
+    if snr_db is not None:
+        f = np.stack([((g & 0xFFFF) << 16).view(np.float32), ((g >> 16) << 16).view(np.float32)], -1)
+        z = f[..., 0] + 1j * f[..., 1]
+        occ = np.abs(z) > 0
+        pw = float(np.mean(np.abs(z[occ]) ** 2))
+        rng = np.random.default_rng(seed)
+        sigma = np.sqrt(pw / 10 ** (snr_db / 10) / 2)
+        z = z + sigma * (rng.normal(size=z.shape) + 1j * rng.normal(size=z.shape))
+        g = (to_bf16(z.real.astype(np.float32)).astype(np.uint32)
+             | (to_bf16(z.imag.astype(np.float32)).astype(np.uint32) << 16))
+    return np.ascontiguousarray(g), p

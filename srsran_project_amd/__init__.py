@@ -77,6 +77,15 @@ from .pusch_chest import (  # noqa: F401
 
 from .pusch_demodulator import PuschDemodPlan, PuschDemodulator, PuschDemodulatorConfig  # noqa: F401
 
+from .pusch_processor import (  # noqa: F401
+    PuschPdu,
+    PuschProcessor,
+    PuschProcessorConfig,
+    PuschProcessorPlan,
+    PuschProcessorResult,
+    make_pdu,
+)
+
 from .sch import (  # noqa: F401
     PdschEncoder,
     PuschDecoder,

@@ -36,6 +36,37 @@ struct device_buffer {
   }
 };
 
+// Orders the reuse of an object's device scratch across the caller's streams: a batch call on stream s
+// first waits for the previous call's completion event when that call ran on another stream, so two
+// calls on different streams never overwrite each other's in-flight scratch.
+struct stream_order {
+  hipEvent_t  done = nullptr;
+  hipStream_t last = nullptr;
+  bool        used = false;
+  stream_order() = default;
+  stream_order(const stream_order&) = delete;
+  stream_order& operator=(const stream_order&) = delete;
+  ~stream_order()
+  {
+    if (done) {
+      (void)hipEventDestroy(done);
+    }
+  }
+  hipError_t begin(hipStream_t s) const { return (used && s != last) ? hipStreamWaitEvent(s, done, 0) : hipSuccess; }
+  hipError_t end(hipStream_t s)
+  {
+    if (done == nullptr) {
+      hipError_t e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        return e;
+      }
+    }
+    last = s;
+    used = true;
+    return hipEventRecord(done, s);
+  }
+};
+
 inline size_t align_up(size_t n, size_t a)
 {
   return (n + a - 1) / a * a;

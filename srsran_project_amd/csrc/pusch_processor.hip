@@ -1,0 +1,47 @@
+// pusch_processor.hip -- the PUSCH processor's result kernel: per transport block, the
+// decoder result plus the channel state information of channel_estimate::
+// get_channel_state_information (channel_estimation.h:244-286) from the estimator's port stats.
+#include <hip/hip_runtime.h>
+
+#include "pusch_processor_args.h"
+
+namespace srs_amd {
+
+__global__ __launch_bounds__(64) void pusch_result_kernel(pusch_result_args a)
+{
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= a.nof_grids) {
+    return;
+  }
+  const srs_amd_chest_port_stats* st = a.stats + static_cast<size_t>(g) * a.nof_ports;
+  float    noise = 0.0f, rsrp = 0.0f, epre = 0.0f, best_snr = 0.0f;
+  uint32_t best  = 0;
+  for (uint32_t p = 0; p < a.nof_ports; ++p) {
+    noise += st[p].noise_var;
+    rsrp += st[p].rsrp;
+    epre += st[p].epre;
+    if (st[p].snr > best_snr) {
+      best_snr = st[p].snr;
+      best     = p;
+    }
+  }
+  srs_amd_pusch_processor_result r;
+  r.data             = a.dec_results[g];
+  const bool normal  = isfinite(noise) && fabsf(noise) >= 1.17549435e-38f;
+  r.sinr_db          = 10.0f * log10f(normal ? rsrp / noise : 0.0f);
+  r.epre_db          = 10.0f * log10f(epre / static_cast<float>(a.nof_ports));
+  r.rsrp_db          = 10.0f * log10f(rsrp / static_cast<float>(a.nof_ports));
+  r.time_alignment_s = st[best].time_alignment_s;
+  a.results[g]       = r;
+}
+
+hipError_t launch_pusch_result(const pusch_result_args& a, hipStream_t stream)
+{
+  if (a.nof_grids == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(pusch_result_kernel, dim3((a.nof_grids + 63) / 64), dim3(64), 0, stream, a);
+  return hipGetLastError();
+}
+
+} // namespace srs_amd

@@ -1,0 +1,370 @@
+// pusch_processor_api.cpp -- C-ABI of the MI355X PUSCH processor
+// (include/srsran_amd/pusch_processor.h): pusch_processor_impl::process
+// (pusch_processor_impl.cpp:134-386) as three asynchronous device stages --
+// DM-RS channel estimation, demodulation, UL-SCH decoding -- over a batch of
+// grids, with the processor's own HBM scratch between them.
+#include "srsran_amd/pusch_processor.h"
+
+#include <hip/hip_runtime.h>
+
+#include "api_common.h"
+#include "device_buffer.h"
+#include "pusch_processor_args.h"
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+
+using namespace srs_amd;
+
+struct srs_amd_pusch_processor {
+  int                            device = 0;
+  srs_amd_pusch_processor_config cfg{};
+  srs_amd_pusch_chest*           chest  = nullptr;
+  srs_amd_pusch_demodulator*     demod  = nullptr;
+  srs_amd_pusch_decoder*         dec    = nullptr;
+  hipStream_t                    stream = nullptr; // host-call stream
+  device_buffer                  estimates, stats, llrs, dec_results, host_io;
+  stream_order                   order;
+  std::mutex                     mtx;
+  ~srs_amd_pusch_processor()
+  {
+    (void)hipSetDevice(device);
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+    srs_amd_pusch_chest_destroy(chest);
+    srs_amd_pusch_demodulator_destroy(demod);
+    srs_amd_pusch_decoder_destroy(dec);
+  }
+};
+
+struct srs_amd_pusch_processor_plan {
+  srs_amd_pusch_pdu            pdu{};
+  uint32_t                     nof_subc = 0;
+  srs_amd_pusch_chest_config   chest_cfg{};
+  srs_amd_pusch_demod_plan*    demod_plan = nullptr;
+  uint32_t                     nof_re     = 0;
+  srs_amd_sch_plan             sch{};
+  srs_amd_pusch_decoder_config dec_cfg{};
+  uint64_t                     soft_bytes = 0;
+  ~srs_amd_pusch_processor_plan() { srs_amd_pusch_demod_plan_destroy(demod_plan); }
+};
+
+namespace {
+
+// ldpc::compute_nof_codeblocks (ldpc.h:140-151).
+uint32_t nof_codeblocks(uint32_t tbs, uint32_t bg)
+{
+  const uint32_t tb_and_crc = tbs + (tbs > 3824 ? 24u : 16u);
+  const uint32_t max_seg    = bg == 1 ? 8448u : 3840u;
+  return tb_and_crc <= max_seg ? 1u : (tb_and_crc + (max_seg - 24) - 1) / (max_seg - 24);
+}
+
+// ldpc::compute_N_ref (ldpc.h:225-228); MAX_CODEBLOCK_SIZE = 384 x 66.
+uint32_t compute_N_ref(uint32_t tbs_lbrm_bytes, uint32_t C)
+{
+  const uint64_t n = static_cast<uint64_t>(tbs_lbrm_bytes) * 8 * 3 / (2 * C);
+  return static_cast<uint32_t>(std::min<uint64_t>(n, 384 * 66));
+}
+
+// convert_dB_to_amplitude(-get_sch_to_dmrs_ratio_dB(n)) (sch_dmrs_power.h, math_utils.h:118), in float as
+// the reference evaluates it.
+float dmrs_scaling(uint32_t nof_cdm_groups_without_data)
+{
+  static const float beta_dmrs_db[4] = {NAN, 0.0F, -3.0F, -4.77F};
+  const float        v               = -beta_dmrs_db[nof_cdm_groups_without_data];
+  return std::pow(10.0F, v / 20.0F);
+}
+
+} // namespace
+
+extern "C" {
+
+int srs_amd_pusch_processor_create(srs_amd_pusch_processor**             proc,
+                                   const srs_amd_pusch_processor_config* cfg,
+                                   int                                   device)
+{
+  if (proc == nullptr || cfg == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  *proc = nullptr;
+  if (cfg->dec_nof_iterations == 0) {
+    return fail(SRS_AMD_EINVAL, "The decoder number of iterations must be non-zero.");
+  }
+  int rc = select_device(device);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  auto* p   = new srs_amd_pusch_processor();
+  p->device = device;
+  p->cfg    = *cfg;
+  rc        = srs_amd_pusch_chest_create(&p->chest, device);
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_pusch_demodulator_create(&p->demod, device);
+  }
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_pusch_decoder_create(&p->dec, cfg->ldpc_arith, device);
+  }
+  if (rc == SRS_AMD_OK) {
+    hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      rc = hip_fail(e, "PUSCH processor stream");
+    }
+  }
+  if (rc != SRS_AMD_OK) {
+    delete p;
+    return rc;
+  }
+  *proc = p;
+  return SRS_AMD_OK;
+}
+
+void srs_amd_pusch_processor_destroy(srs_amd_pusch_processor* proc)
+{
+  delete proc;
+}
+
+int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
+                                        const srs_amd_pusch_pdu*       pdu,
+                                        uint32_t                       nof_subc,
+                                        srs_amd_pusch_processor_plan** plan,
+                                        srs_amd_sch_plan*              sch_plan,
+                                        uint64_t*                      soft_buffer_bytes)
+{
+  if (proc == nullptr || pdu == nullptr || plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  *plan = nullptr;
+  // pusch_processor_validator_impl.cpp checks, where the C-ABI subset narrows them
+  if (pdu->dmrs_type != 1) {
+    return fail(SRS_AMD_EINVAL, "Only DM-RS type 1 is supported.");
+  }
+  if (pdu->nof_cdm_groups_without_data < 1 || pdu->nof_cdm_groups_without_data > 2) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of CDM groups without data (i.e., %u).",
+                pdu->nof_cdm_groups_without_data);
+  }
+  if (pdu->rb_count == 0 || pdu->rb_start + pdu->rb_count > pdu->bwp_size_rb) {
+    return fail(SRS_AMD_EINVAL, "Invalid frequency allocation.");
+  }
+  if (pdu->bwp_start_rb + pdu->bwp_size_rb > nof_subc / 12) {
+    return fail(SRS_AMD_EINVAL, "The BWP exceeds the resource grid.");
+  }
+  if (pdu->tbs == 0 || pdu->tbs % 8 != 0) {
+    return fail(SRS_AMD_EINVAL, "Invalid transport block size (i.e., %u).", pdu->tbs);
+  }
+  if (pdu->base_graph != 1 && pdu->base_graph != 2) {
+    return fail(SRS_AMD_EINVAL, "Invalid base graph.");
+  }
+  auto* pl     = new srs_amd_pusch_processor_plan();
+  pl->pdu      = *pdu;
+  pl->nof_subc = nof_subc;
+  // DM-RS estimator configuration (pusch_processor_impl.cpp:184-200)
+  const uint32_t crb0       = pdu->bwp_start_rb + pdu->rb_start;
+  srs_amd_pusch_chest_config& c = pl->chest_cfg;
+  c.numerology              = pdu->numerology;
+  c.slot_index              = pdu->slot_index;
+  c.scrambling_id           = pdu->scrambling_id;
+  c.n_scid                  = pdu->n_scid;
+  c.nof_tx_layers           = pdu->nof_tx_layers;
+  c.scaling                 = dmrs_scaling(pdu->nof_cdm_groups_without_data);
+  c.symbols_mask            = pdu->dmrs_symbol_mask;
+  c.rb_start                = crb0;
+  c.rb_count                = pdu->rb_count;
+  c.first_symbol            = pdu->start_symbol_index;
+  c.nof_symbols             = pdu->nof_symbols;
+  c.fd_smoothing            = proc->cfg.fd_smoothing;
+  c.td_interpolation        = proc->cfg.td_interpolation;
+  c.compensate_cfo          = proc->cfg.compensate_cfo;
+  // demodulator configuration (pusch_processor_impl.cpp:368-383)
+  srs_amd_pusch_demod_config dc{};
+  dc.rnti = pdu->rnti;
+  dc.n_id = pdu->n_id;
+  dc.modulation = pdu->modulation;
+  for (uint32_t r = crb0; r < crb0 + pdu->rb_count; ++r) {
+    dc.crb_mask[r / 8] |= static_cast<uint8_t>(1u << (r % 8));
+  }
+  dc.start_symbol                = pdu->start_symbol_index;
+  dc.nof_symbols                 = pdu->nof_symbols;
+  dc.dmrs_symbol_mask            = pdu->dmrs_symbol_mask;
+  dc.dmrs_type                   = pdu->dmrs_type;
+  dc.nof_cdm_groups_without_data = pdu->nof_cdm_groups_without_data;
+  dc.nof_tx_layers               = pdu->nof_tx_layers;
+  dc.nof_rx_ports                = pdu->nof_rx_ports;
+  dc.equalizer                   = proc->cfg.equalizer;
+  int rc = srs_amd_pusch_demod_plan_create(proc->demod, &dc, nof_subc, &pl->demod_plan, &pl->nof_re);
+  if (rc != SRS_AMD_OK) {
+    delete pl;
+    return rc;
+  }
+  // decoder configuration (pusch_processor_impl.cpp:322-347): UL-SCH without UCI gets every data RE
+  const uint32_t C       = nof_codeblocks(pdu->tbs, pdu->base_graph);
+  const uint32_t tbs_lbrm = pdu->tbs_lbrm_bytes ? pdu->tbs_lbrm_bytes : 159749u; // tbs_lbrm_default
+  rc = srs_amd_sch_plan_compute(&pl->sch, pdu->tbs, pdu->base_graph, pdu->rv, static_cast<uint32_t>(pdu->modulation),
+                                compute_N_ref(tbs_lbrm, C), pdu->nof_tx_layers, pl->nof_re * pdu->nof_tx_layers);
+  if (rc != SRS_AMD_OK) {
+    delete pl;
+    return rc;
+  }
+  pl->dec_cfg.nof_ldpc_iterations = proc->cfg.dec_nof_iterations;
+  pl->dec_cfg.force_decoding      = proc->cfg.dec_force_decoding;
+  pl->dec_cfg.use_early_stop      = proc->cfg.dec_enable_early_stop;
+  pl->dec_cfg.new_data            = pdu->new_data;
+  pl->soft_bytes                  = srs_amd_pusch_soft_buffer_size(&pl->sch);
+  if (sch_plan != nullptr) {
+    *sch_plan = pl->sch;
+  }
+  if (soft_buffer_bytes != nullptr) {
+    *soft_buffer_bytes = pl->soft_bytes;
+  }
+  *plan = pl;
+  return SRS_AMD_OK;
+}
+
+void srs_amd_pusch_processor_plan_destroy(srs_amd_pusch_processor_plan* plan)
+{
+  delete plan;
+}
+
+int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
+                                const srs_amd_pusch_processor_plan* plan,
+                                const uint32_t*                     d_grids,
+                                uint64_t                            grid_stride,
+                                uint32_t                            nof_grids,
+                                uint8_t*                            d_tbs,
+                                uint32_t                            tb_stride,
+                                srs_amd_pusch_processor_result*     d_results,
+                                int8_t*                             d_soft,
+                                srs_amd_chest_port_stats*           d_port_stats,
+                                void*                               stream)
+{
+  if (proc == nullptr || plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_grids == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_grids == nullptr || d_tbs == nullptr || d_results == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  const uint32_t P     = plan->pdu.nof_rx_ports;
+  const uint32_t L     = plan->pdu.nof_tx_layers;
+  const uint64_t plane = 14ull * plan->nof_subc;
+  if (nof_grids > 1 && (grid_stride < P * plane || tb_stride < plan->pdu.tbs / 8)) {
+    return fail(SRS_AMD_EINVAL, "grid or transport block stride too small");
+  }
+  const uint64_t est_stride = P * L * plane;
+  const uint32_t G          = plan->sch.cw_length;
+  const uint32_t llr_stride = static_cast<uint32_t>(align_up(G, 64));
+  auto           s          = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(proc->mtx);
+  hipError_t                  e = hipSetDevice(proc->device);
+  if (e == hipSuccess) {
+    e = proc->estimates.ensure(nof_grids * est_stride * 4);
+  }
+  if (e == hipSuccess) {
+    e = proc->stats.ensure(static_cast<size_t>(nof_grids) * P * sizeof(srs_amd_chest_port_stats));
+  }
+  if (e == hipSuccess) {
+    e = proc->llrs.ensure(static_cast<size_t>(nof_grids) * llr_stride);
+  }
+  if (e == hipSuccess) {
+    e = proc->dec_results.ensure(static_cast<size_t>(nof_grids) * sizeof(srs_amd_pusch_decoder_result));
+  }
+  if (e == hipSuccess) {
+    e = proc->order.begin(s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH processor scratch");
+  }
+  srs_amd_chest_port_stats* st = d_port_stats ? d_port_stats : proc->stats.as<srs_amd_chest_port_stats>();
+  int rc = srs_amd_pusch_chest_estimate_batch(proc->chest, &plan->chest_cfg, d_grids, grid_stride, P, plan->nof_subc,
+                                              nof_grids, proc->estimates.as<uint32_t>(), est_stride, st, stream);
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_pusch_demodulate_batch(proc->demod, plan->demod_plan, d_grids, grid_stride,
+                                        proc->estimates.as<uint32_t>(), est_stride, st, proc->llrs.as<int8_t>(),
+                                        llr_stride, nof_grids, stream);
+  }
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_pusch_decode_batch(proc->dec, &plan->sch, &plan->dec_cfg, d_tbs, tb_stride,
+                                    proc->dec_results.as<srs_amd_pusch_decoder_result>(), proc->llrs.as<int8_t>(),
+                                    llr_stride, d_soft, nullptr, nof_grids, stream);
+  }
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  pusch_result_args a{};
+  a.dec_results = proc->dec_results.as<srs_amd_pusch_decoder_result>();
+  a.stats       = st;
+  a.results     = d_results;
+  a.nof_grids   = nof_grids;
+  a.nof_ports   = P;
+  e             = launch_pusch_result(a, s);
+  if (e == hipSuccess) {
+    e = proc->order.end(s);
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_result_kernel launch");
+}
+
+int srs_amd_pusch_process(srs_amd_pusch_processor*            proc,
+                          const srs_amd_pusch_processor_plan* plan,
+                          const uint32_t*                     grid,
+                          uint8_t*                            tb,
+                          srs_amd_pusch_processor_result*     result,
+                          int8_t*                             soft_buffer)
+{
+  if (proc == nullptr || plan == nullptr || grid == nullptr || tb == nullptr || result == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  const size_t grid_bytes = plan->pdu.nof_rx_ports * 14ull * plan->nof_subc * 4;
+  const size_t tb_bytes   = plan->pdu.tbs / 8;
+  const size_t soft_bytes = soft_buffer ? plan->soft_bytes : 0;
+  const size_t off_tb     = align_up(grid_bytes, 256);
+  const size_t off_res    = off_tb + align_up(tb_bytes, 256);
+  const size_t off_soft   = off_res + align_up(sizeof(srs_amd_pusch_processor_result), 256);
+  hipError_t   e;
+  {
+    std::lock_guard<std::mutex> lock(proc->mtx);
+    e = hipSetDevice(proc->device);
+    if (e == hipSuccess) {
+      e = proc->host_io.ensure(off_soft + soft_bytes);
+    }
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH processor buffers");
+  }
+  auto* b = proc->host_io.as<uint8_t>();
+  e       = hipMemcpyAsync(b, grid, grid_bytes, hipMemcpyHostToDevice, proc->stream);
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(b + off_tb, tb, tb_bytes, hipMemcpyHostToDevice, proc->stream); // untouched bytes keep
+  }
+  if (e == hipSuccess && soft_buffer) {
+    e = hipMemcpyAsync(b + off_soft, soft_buffer, soft_bytes, hipMemcpyHostToDevice, proc->stream);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH processor upload");
+  }
+  int rc = srs_amd_pusch_process_batch(proc, plan, reinterpret_cast<const uint32_t*>(b), grid_bytes / 4, 1, b + off_tb,
+                                       static_cast<uint32_t>(tb_bytes),
+                                       reinterpret_cast<srs_amd_pusch_processor_result*>(b + off_res),
+                                       soft_buffer ? reinterpret_cast<int8_t*>(b + off_soft) : nullptr, nullptr,
+                                       proc->stream);
+  if (rc != SRS_AMD_OK) {
+    (void)hipStreamSynchronize(proc->stream);
+    return rc;
+  }
+  e = hipMemcpyAsync(tb, b + off_tb, tb_bytes, hipMemcpyDeviceToHost, proc->stream);
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(result, b + off_res, sizeof(*result), hipMemcpyDeviceToHost, proc->stream);
+  }
+  if (e == hipSuccess && soft_buffer) {
+    e = hipMemcpyAsync(soft_buffer, b + off_soft, soft_bytes, hipMemcpyDeviceToHost, proc->stream);
+  }
+  if (e == hipSuccess) {
+    e = hipStreamSynchronize(proc->stream);
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH processor download");
+}
+
+} // extern "C"

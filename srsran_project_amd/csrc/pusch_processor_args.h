@@ -1,0 +1,23 @@
+// pusch_processor_args.h -- argument block of the PUSCH processor's result kernel
+// (pusch_processor.hip), shared with its C-ABI (pusch_processor_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "srsran_amd/pusch_processor.h"
+
+namespace srs_amd {
+
+struct pusch_result_args {
+  const srs_amd_pusch_decoder_result* dec_results; // [grid]
+  const srs_amd_chest_port_stats*     stats;       // [grid][port]
+  srs_amd_pusch_processor_result*     results;     // [grid]
+  uint32_t                            nof_grids;
+  uint32_t                            nof_ports;
+};
+
+hipError_t launch_pusch_result(const pusch_result_args& a, hipStream_t stream);
+
+} // namespace srs_amd

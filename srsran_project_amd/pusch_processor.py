@@ -1,0 +1,199 @@
+"""Host-side mirror of srsRAN's PUSCH processor over the MI355X C-ABI
+(include/srsran_amd/pusch_processor.h).
+
+Reference interface:
+  pusch_processor.h:181   process(span<uint8_t> data, unique_rx_buffer rm_buffer,
+                                  pusch_processor_result_notifier& notifier,
+                                  const resource_grid_reader& grid, const pdu_t& pdu)
+  pusch_processor.h:117   pdu_t (slot, rnti, bwp, mcs_descr, codeword {rv, base graph, new_data}, n_id,
+                                 nof_tx_layers, rx_ports, dmrs_symbol_mask, dmrs, freq_alloc, time allocation,
+                                 tbs_lbrm)
+  factories.h:107         pusch_processor_factory_sw_configuration (decoder iterations, early stop, ...)
+The notifier's pusch_processor_result_data (decoder result + CSI) comes back as a
+PuschProcessorResult per transport block.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .pusch_chest import ChestPortStats
+from .sch import PuschDecoderResult, SchPlan
+
+
+class PuschProcessorConfig(ctypes.Structure):
+    """``srs_amd_pusch_processor_config`` (pusch_processor_factory_sw_configuration + component choices). The
+    defaults are the reference PUSCH processor benchmark's (pusch_processor_benchmark.cpp:133-140, 637-638)."""
+
+    _fields_ = [("dec_nof_iterations", ctypes.c_uint32), ("dec_enable_early_stop", ctypes.c_int32),
+                ("dec_force_decoding", ctypes.c_int32), ("equalizer", ctypes.c_int32),
+                ("fd_smoothing", ctypes.c_int32), ("td_interpolation", ctypes.c_int32),
+                ("compensate_cfo", ctypes.c_int32), ("ldpc_arith", ctypes.c_int32)]
+
+    def __init__(self, dec_nof_iterations=2, dec_enable_early_stop=True, dec_force_decoding=False, equalizer=0,
+                 fd_smoothing=2, td_interpolation=0, compensate_cfo=True, ldpc_arith=0):
+        super().__init__(dec_nof_iterations, int(dec_enable_early_stop), int(dec_force_decoding), equalizer,
+                         fd_smoothing, td_interpolation, int(compensate_cfo), ldpc_arith)
+
+
+class PuschPdu(ctypes.Structure):
+    """``srs_amd_pusch_pdu`` (pusch_processor::pdu_t, data-only subset)."""
+
+    _fields_ = [(n, ctypes.c_uint32) for n in ("numerology", "slot_index", "rnti", "bwp_start_rb", "bwp_size_rb")] + \
+        [("modulation", ctypes.c_int32), ("target_code_rate", ctypes.c_float), ("rv", ctypes.c_uint32),
+         ("base_graph", ctypes.c_uint32), ("new_data", ctypes.c_int32)] + \
+        [(n, ctypes.c_uint32) for n in ("n_id", "nof_tx_layers", "nof_rx_ports", "dmrs_symbol_mask", "dmrs_type",
+                                        "scrambling_id", "n_scid", "nof_cdm_groups_without_data", "rb_start",
+                                        "rb_count", "start_symbol_index", "nof_symbols", "tbs_lbrm_bytes", "tbs")]
+
+
+class PuschProcessorResult(ctypes.Structure):
+    """``srs_amd_pusch_processor_result``: pusch_decoder_result + channel state information."""
+
+    _fields_ = [("data", PuschDecoderResult), ("sinr_db", ctypes.c_float), ("epre_db", ctypes.c_float),
+                ("rsrp_db", ctypes.c_float), ("time_alignment_s", ctypes.c_float)]
+
+
+RESULT_BYTES = ctypes.sizeof(PuschProcessorResult)
+
+
+def make_pdu(**kw):
+    """PuschPdu with the reference benchmark's defaults (pusch_processor_benchmark.cpp:396-431)."""
+    d = dict(numerology=1, slot_index=0, rnti=1, bwp_start_rb=0, bwp_size_rb=51, modulation=2,
+             target_code_rate=679.0, rv=0, base_graph=1, new_data=1, n_id=0, nof_tx_layers=1, nof_rx_ports=1,
+             dmrs_symbol_mask=(1 << 2) | (1 << 11), dmrs_type=1, scrambling_id=0, n_scid=0,
+             nof_cdm_groups_without_data=2, rb_start=0, rb_count=None, start_symbol_index=0, nof_symbols=14,
+             tbs_lbrm_bytes=0, tbs=0)
+    d.update(kw)
+    if d["rb_count"] is None:
+        d["rb_count"] = d["bwp_size_rb"] - d["rb_start"]
+    p = PuschPdu()
+    for k, v in d.items():
+        setattr(p, k, v)
+    return p
+
+
+def _declare(lib):
+    c = ctypes
+    P = c.c_void_p
+    u = c.c_uint32
+    sigs = {
+        "srs_amd_pusch_processor_create": (c.c_int, [c.POINTER(P), c.POINTER(PuschProcessorConfig), c.c_int]),
+        "srs_amd_pusch_processor_destroy": (None, [P]),
+        "srs_amd_pusch_processor_plan_create": (c.c_int, [P, c.POINTER(PuschPdu), u, c.POINTER(P),
+                                                          c.POINTER(SchPlan), c.POINTER(c.c_uint64)]),
+        "srs_amd_pusch_processor_plan_destroy": (None, [P]),
+        "srs_amd_pusch_process_batch": (c.c_int, [P, P, P, c.c_uint64, u, P, u, P, P, P, P]),
+        "srs_amd_pusch_process": (c.c_int, [P, P, P, P, c.POINTER(PuschProcessorResult), P]),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+_declared = False
+
+
+def _L():
+    global _declared
+    lib = _lib.lib()
+    if not _declared:
+        _declare(lib)
+        _declared = True
+    return lib
+
+
+class PuschProcessorPlan:
+    def __init__(self, proc, pdu, nof_subc):
+        self._lib = proc._lib
+        h = ctypes.c_void_p()
+        self.sch = SchPlan()
+        sb = ctypes.c_uint64()
+        self.pdu = pdu
+        _lib.check(self._lib.srs_amd_pusch_processor_plan_create(proc._h, ctypes.byref(pdu), nof_subc,
+                                                                ctypes.byref(h), ctypes.byref(self.sch),
+                                                                ctypes.byref(sb)), "pusch_processor plan")
+        self._h = h
+        self.nof_subc = nof_subc
+        self.soft_bytes = sb.value
+        self.tb_bytes = pdu.tbs // 8
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.srs_amd_pusch_processor_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PuschProcessor:
+    """pusch_processor over the MI355X chain (estimator -> demodulator -> decoder)."""
+
+    def __init__(self, config=None, device=-1):
+        self._lib = _L()
+        self.config = config or PuschProcessorConfig()
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.srs_amd_pusch_processor_create(ctypes.byref(h), ctypes.byref(self.config), int(device)),
+                   "pusch_processor create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.srs_amd_pusch_processor_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def plan(self, pdu, nof_subc):
+        return PuschProcessorPlan(self, pdu, nof_subc)
+
+    def process(self, grid, plan, soft_buffer=None):
+        """Host: grid uint32 [P][14][nsubc] -> (tb bytes, PuschProcessorResult). soft_buffer: int8 numpy HARQ
+        buffer of plan.soft_bytes kept between transmissions (None: new data only)."""
+        g = np.ascontiguousarray(grid, dtype=np.uint32)
+        tb = np.zeros(plan.tb_bytes, np.uint8)
+        res = PuschProcessorResult()
+        sb = None
+        if soft_buffer is not None:
+            if soft_buffer.dtype != np.int8 or soft_buffer.size != plan.soft_bytes:
+                raise ValueError("soft buffer must be int8 of %d bytes" % plan.soft_bytes)
+            sb = soft_buffer.ctypes.data
+        _lib.check(self._lib.srs_amd_pusch_process(self._h, plan._h, g.ctypes.data, tb.ctypes.data,
+                                                   ctypes.byref(res), sb), "pusch_process")
+        return tb, res
+
+    def process_batch(self, grids, plan, tbs=None, results=None, soft=None, port_stats=None, stream=None):
+        """Device: grids int32 [n][P][14][nsubc] -> tbs uint8 [n][tbs/8], results uint8 [n][RESULT_BYTES]."""
+        import torch
+
+        n = grids.shape[0]
+        dev = grids.device
+        if tbs is None:
+            tbs = torch.zeros((n, plan.tb_bytes), dtype=torch.uint8, device=dev)
+        if results is None:
+            results = torch.zeros((n, RESULT_BYTES), dtype=torch.uint8, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        _lib.check(self._lib.srs_amd_pusch_process_batch(
+            self._h, plan._h, grids.data_ptr(), grids.stride(0), n, tbs.data_ptr(), tbs.stride(0),
+            results.data_ptr(), None if soft is None else soft.data_ptr(),
+            None if port_stats is None else port_stats.data_ptr(), ctypes.c_void_p(stream.cuda_stream)),
+            "pusch_process_batch")
+        return tbs, results
+
+
+def parse_results(results):
+    """uint8 [n][RESULT_BYTES] (host numpy) -> list of PuschProcessorResult."""
+    arr = np.ascontiguousarray(results, np.uint8)
+    return [PuschProcessorResult.from_buffer_copy(arr[i].tobytes()) for i in range(arr.shape[0])]
