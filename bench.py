@@ -18,10 +18,13 @@ batch of slots of the 100 MHz numerology-1 carrier (273 PRB, 4096-point DFT,
 normal CP): 4 antenna ports x `--slots` slots, cbf16 resource grids to complex
 float baseband and back (ofdm_slot_modulator / ofdm_slot_demodulator).
 
-Inputs are resident in HBM before the timed region.  Multi-GPU: codeblocks /
-slots are independent, so every rank processes its own batch (weak scaling, no
-data-path collective); the timed region is bracketed by barriers and the max
-time over ranks is reported.
+Inputs are resident in HBM before the timed region.  Multi-GPU: `--gpus N`
+starts N ranks itself (one process per GPU, before any GPU call), or runs under
+torch.distributed.run; cells / codeblocks / slots are independent, so every
+rank processes its own batch (weak scaling, no data-path collective; the
+pipeline's optional `--ingest` adds the RCCL scatter / gather of slot inputs and
+results, timed separately); the timed region is bracketed by barriers and the
+max time over ranks is reported.
 
 cpu_baseline: the REFERENCE implementation itself (oracle/_ref, compiled from
 /root/reference sources: the AVX512 decoder if the host has it, else AVX2; the
@@ -66,6 +69,12 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample duration")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--snr-db", type=float, default=35.0, help="pipeline: PUSCH SNR of the headline line")
+    p.add_argument("--low-snr-db", type=float, default=None,
+                   help="pipeline: also report a line at this SNR (near the decoding threshold)")
+    p.add_argument("--ingest", action="store_true",
+                   help="pipeline, N > 1: rank 0 holds all cells' slot inputs; RCCL scatter / gather every step")
+    p.add_argument("--no-latency", action="store_true", help="pipeline: skip the 1 / 8 cell latency figures")
     return p.parse_args()
 
 
@@ -344,12 +353,36 @@ def run_ofdm(args, dist, world, rank, dev):
     }
 
 
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: start N ranks of this script (one process per GPU) before anything touches
+    the GPU, each with RANK / LOCAL_RANK / WORLD_SIZE and a 127.0.0.1 rendezvous, forward their output and exit
+    with the worst return code. Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(sys.argv[0])] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("warning: --gpus %d but WORLD_SIZE %d; reporting the launched world" % (args.gpus, world),
+              file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:

@@ -236,7 +236,7 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
                                 uint32_t                            tb_stride,
                                 srs_amd_pusch_processor_result*     d_results,
                                 int8_t*                             d_soft,
-                                srs_amd_chest_port_stats*           d_port_stats,
+                                const srs_amd_pusch_intermediates*  io,
                                 void*                               stream)
 {
   if (proc == nullptr || plan == nullptr) {
@@ -254,19 +254,24 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   if (nof_grids > 1 && (grid_stride < P * plane || tb_stride < plan->pdu.tbs / 8)) {
     return fail(SRS_AMD_EINVAL, "grid or transport block stride too small");
   }
-  const uint64_t est_stride = P * L * plane;
-  const uint32_t G          = plan->sch.cw_length;
-  const uint32_t llr_stride = static_cast<uint32_t>(align_up(G, 64));
+  const uint32_t G            = plan->sch.cw_length;
+  const bool     own_est      = io == nullptr || io->d_estimates == nullptr;
+  const bool     own_llrs     = io == nullptr || io->d_llrs == nullptr;
+  const uint64_t est_stride   = own_est ? P * L * plane : io->est_stride;
+  const uint32_t llr_stride   = own_llrs ? static_cast<uint32_t>(align_up(G, 64)) : io->llr_stride;
+  if ((!own_est && nof_grids > 1 && est_stride < P * L * plane) || (!own_llrs && llr_stride < G)) {
+    return fail(SRS_AMD_EINVAL, "intermediate estimate or LLR stride too small");
+  }
   auto           s          = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(proc->mtx);
   hipError_t                  e = hipSetDevice(proc->device);
-  if (e == hipSuccess) {
+  if (e == hipSuccess && own_est) {
     e = proc->estimates.ensure(nof_grids * est_stride * 4);
   }
   if (e == hipSuccess) {
     e = proc->stats.ensure(static_cast<size_t>(nof_grids) * P * sizeof(srs_amd_chest_port_stats));
   }
-  if (e == hipSuccess) {
+  if (e == hipSuccess && own_llrs) {
     e = proc->llrs.ensure(static_cast<size_t>(nof_grids) * llr_stride);
   }
   if (e == hipSuccess) {
@@ -278,18 +283,19 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   if (e != hipSuccess) {
     return hip_fail(e, "PUSCH processor scratch");
   }
-  srs_amd_chest_port_stats* st = d_port_stats ? d_port_stats : proc->stats.as<srs_amd_chest_port_stats>();
+  srs_amd_chest_port_stats* st   = (io && io->d_port_stats) ? io->d_port_stats : proc->stats.as<srs_amd_chest_port_stats>();
+  uint32_t*                 est  = own_est ? proc->estimates.as<uint32_t>() : io->d_estimates;
+  int8_t*                   llrs = own_llrs ? proc->llrs.as<int8_t>() : io->d_llrs;
   int rc = srs_amd_pusch_chest_estimate_batch(proc->chest, &plan->chest_cfg, d_grids, grid_stride, P, plan->nof_subc,
-                                              nof_grids, proc->estimates.as<uint32_t>(), est_stride, st, stream);
+                                              nof_grids, est, est_stride, st, stream);
   if (rc == SRS_AMD_OK) {
-    rc = srs_amd_pusch_demodulate_batch(proc->demod, plan->demod_plan, d_grids, grid_stride,
-                                        proc->estimates.as<uint32_t>(), est_stride, st, proc->llrs.as<int8_t>(),
+    rc = srs_amd_pusch_demodulate_batch(proc->demod, plan->demod_plan, d_grids, grid_stride, est, est_stride, st, llrs,
                                         llr_stride, nof_grids, stream);
   }
   if (rc == SRS_AMD_OK) {
     rc = srs_amd_pusch_decode_batch(proc->dec, &plan->sch, &plan->dec_cfg, d_tbs, tb_stride,
-                                    proc->dec_results.as<srs_amd_pusch_decoder_result>(), proc->llrs.as<int8_t>(),
-                                    llr_stride, d_soft, nullptr, nof_grids, stream);
+                                    proc->dec_results.as<srs_amd_pusch_decoder_result>(), llrs, llr_stride, d_soft,
+                                    nullptr, nof_grids, stream);
   }
   if (rc != SRS_AMD_OK) {
     return rc;

@@ -58,6 +58,13 @@ class PuschProcessorResult(ctypes.Structure):
 RESULT_BYTES = ctypes.sizeof(PuschProcessorResult)
 
 
+class PuschIntermediates(ctypes.Structure):
+    """``srs_amd_pusch_intermediates``: caller-owned buffers for the processor's intermediate results."""
+
+    _fields_ = [("d_estimates", ctypes.c_void_p), ("est_stride", ctypes.c_uint64), ("d_port_stats", ctypes.c_void_p),
+                ("d_llrs", ctypes.c_void_p), ("llr_stride", ctypes.c_uint32)]
+
+
 def make_pdu(**kw):
     """PuschPdu with the reference benchmark's defaults (pusch_processor_benchmark.cpp:396-431)."""
     d = dict(numerology=1, slot_index=0, rnti=1, bwp_start_rb=0, bwp_size_rb=51, modulation=2,
@@ -173,8 +180,11 @@ class PuschProcessor:
                                                    ctypes.byref(res), sb), "pusch_process")
         return tb, res
 
-    def process_batch(self, grids, plan, tbs=None, results=None, soft=None, port_stats=None, stream=None):
-        """Device: grids int32 [n][P][14][nsubc] -> tbs uint8 [n][tbs/8], results uint8 [n][RESULT_BYTES]."""
+    def process_batch(self, grids, plan, tbs=None, results=None, soft=None, port_stats=None, estimates=None,
+                      llrs=None, stream=None):
+        """Device: grids int32 [n][P][14][nsubc] -> tbs uint8 [n][tbs/8], results uint8 [n][RESULT_BYTES].
+        Optional caller buffers for the intermediates: port_stats float32 [n][P][6], estimates int32
+        [n][P][L][14][nsubc], llrs int8 [n][>= codeword length]."""
         import torch
 
         n = grids.shape[0]
@@ -185,10 +195,16 @@ class PuschProcessor:
             results = torch.zeros((n, RESULT_BYTES), dtype=torch.uint8, device=dev)
         if stream is None:
             stream = torch.cuda.current_stream(dev)
+        io = None
+        if port_stats is not None or estimates is not None or llrs is not None:
+            io = PuschIntermediates(
+                None if estimates is None else estimates.data_ptr(), 0 if estimates is None else estimates.stride(0),
+                None if port_stats is None else port_stats.data_ptr(), None if llrs is None else llrs.data_ptr(),
+                0 if llrs is None else llrs.stride(0))
         _lib.check(self._lib.srs_amd_pusch_process_batch(
             self._h, plan._h, grids.data_ptr(), grids.stride(0), n, tbs.data_ptr(), tbs.stride(0),
             results.data_ptr(), None if soft is None else soft.data_ptr(),
-            None if port_stats is None else port_stats.data_ptr(), ctypes.c_void_p(stream.cuda_stream)),
+            None if io is None else ctypes.byref(io), ctypes.c_void_p(stream.cuda_stream)),
             "pusch_process_batch")
         return tbs, results
 

@@ -26,6 +26,8 @@ for s in "$@"; do
     sch) step pytest_sch 900 python -m pytest tests/test_sch_gpu.py -x -q ;;
     chest) step pytest_chest 300 python -u -m pytest tests/test_pusch_chest_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     demod) step pytest_demod 300 python -u -m pytest tests/test_pusch_demod_gpu.py -x -v --timeout 120 --timeout-method thread ;;
+    pipe) step pytest_pipe 300 python -u -m pytest tests/test_pipeline_gpu.py -x -v --timeout 200 --timeout-method thread ;;
+    proc) step pytest_proc 300 python -u -m pytest tests/test_pusch_processor_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     pdsch) step pytest_pdsch 300 python -u -m pytest tests/test_pdsch_modulator_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
