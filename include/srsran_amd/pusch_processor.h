@@ -113,11 +113,24 @@ int  srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
                                          uint64_t*                      soft_buffer_bytes);
 void srs_amd_pusch_processor_plan_destroy(srs_amd_pusch_processor_plan* plan);
 
+/* Optional caller-owned DEVICE buffers for the processor's intermediate results
+ * (any member NULL: the processor uses its own scratch for that one):
+ * channel estimates cbf16 [grid][rx port][layer][14][nof_subc] (est_stride uint32
+ * apart), estimator measurements [grid][rx port], codeword LLRs int8 [grid][G]
+ * (llr_stride bytes apart). Lets a caller inspect or reuse every stage's output. */
+typedef struct srs_amd_pusch_intermediates {
+  uint32_t*                 d_estimates;
+  uint64_t                  est_stride;
+  srs_amd_chest_port_stats* d_port_stats;
+  int8_t*                   d_llrs;
+  uint32_t                  llr_stride;
+} srs_amd_pusch_intermediates;
+
 /* DEVICE, asynchronous: nof_grids received grids cbf16 [grid][port][14][nof_subc]
  * (grid_stride uint32 apart) -> transport blocks (rows of tb_stride bytes) and
  * d_results[nof_grids]. d_soft: nof_grids HARQ soft buffers (soft_buffer_bytes
  * each, kept between transmissions by the caller) or NULL for new-data-only
- * decoding. Optional d_port_stats [grid][port] receives the estimator measurements. */
+ * decoding. io: optional caller buffers for the intermediates (or NULL). */
 int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
                                 const srs_amd_pusch_processor_plan* plan,
                                 const uint32_t*                     d_grids,
@@ -127,7 +140,7 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
                                 uint32_t                            tb_stride,
                                 srs_amd_pusch_processor_result*     d_results,
                                 int8_t*                             d_soft,
-                                srs_amd_chest_port_stats*           d_port_stats,
+                                const srs_amd_pusch_intermediates*  io,
                                 void*                               stream);
 
 /* HOST, synchronous: one grid [port][14][nof_subc]; tb gets tbs/8 bytes;
