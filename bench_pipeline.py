@@ -226,6 +226,8 @@ class Pipeline:
         dec.decode_batch(self.llr_ul, p, amd.PuschDecoder.config(nof_ldpc_iterations=self.iters, use_early_stop=True),
                          tbs=t.zeros_like(self.tb_rx), soft=soft, stream=stream)
         row = soft_bytes // C
+        # the LLR prefix the PUSCH decoder hands to the LDPC decoder (the rest of each row is zero)
+        n_llr = amd.decoder_llr_prefix(p, new_data=True, fresh=True)
         rows = soft.view(-1).as_strided((self.S * C, n_llr), (row, 1))
         ldpc = amd.LdpcDecoder("simd", device=self.dev.index)
         cfg = amd.LdpcDecoderConfiguration(base_graph=p.base_graph, lifting_size=p.lifting_size,
@@ -240,8 +242,8 @@ class Pipeline:
         e1.record(stream)
         t.cuda.synchronize(self.dev)
         it = its.cpu().numpy()
-        # algorithmic bytes: every CB reads its soft-buffer row (the decoder trims at the last non-zero
-        # LLR) and writes its message + iteration count
+        # algorithmic bytes: every CB reads the LLR prefix of its soft-buffer row and writes its message +
+        # iteration count
         nbytes = self.S * C * (n_llr + (amd.message_length(p.base_graph, p.lifting_size) + 7) // 8 + 4)
         return e0.elapsed_time(e1) / reps, nbytes, self.S * C, float(np.mean(np.where(it < 0, self.iters, it)))
 

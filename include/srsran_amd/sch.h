@@ -128,6 +128,13 @@ void srs_amd_pusch_decoder_destroy(srs_amd_pusch_decoder* dec);
 /* Bytes of device soft buffer one transport block of this plan needs (HARQ rx_buffer). */
 uint64_t srs_amd_pusch_soft_buffer_size(const srs_amd_sch_plan* plan);
 
+/* LLRs per soft-buffer row the LDPC decoder scans after rate dematching this plan's codeblocks
+ * (the rest of the row is provably zero): the whole row unless new data with k0 = 0 and no
+ * circular wrap lands in a fresh buffer (fresh != 0) or covers the information bits of a
+ * full-length buffer; then max(E + F, (K_bg - 2) Z) rounded up to whole Z nodes.  The reference
+ * decoder trims its input at the last non-zero LLR the same way (ldpc_decoder_impl.cpp:86). */
+uint32_t srs_amd_pusch_decoder_llr_prefix(const srs_amd_sch_plan* plan, int new_data, int fresh);
+
 /* HOST, synchronous: one codeword of plan->cw_length LLRs -> transport block
  * (tbs/8 bytes, written only where the reference writes it) + result.
  * soft_buffer: HOST HARQ buffer of srs_amd_pusch_soft_buffer_size() bytes, kept

@@ -95,6 +95,7 @@ from .sch import (  # noqa: F401
     sch_plan,
     sch_segments,
     soft_buffer_size,
+    decoder_llr_prefix,
     tbs_calculator_calculate,
 )
 __version__ = "0.1.0"

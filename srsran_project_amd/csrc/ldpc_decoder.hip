@@ -36,6 +36,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ldpc_common.h"
+#include <cstdlib>
 #include <utility>
 
 namespace srs_amd {
@@ -704,6 +705,345 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
   }
 }
 
+// ============================================================================
+// High-rate BG1 / Z = 384 decoder: two check rows per lane in packed int16.
+//
+// A high-rate codeblock (the 256QAM R ~ 0.93 PUSCH of the 100 MHz workloads)
+// has input_size <= (20 + MAXL) Z, so the reference processes only its first
+// nof_layers <= MAXL layers (ldpc_decoder_impl.cpp:104-113) and touches only
+// variable nodes 0 .. 21 + MAXL.  The host selects this kernel when the row
+// length bounds nof_layers by MAXL (launch_ldpc_decode), so:
+//   * lane t in [0, 192) owns check rows t and t + 192 of every layer; both
+//     rows' values travel as the two halves of one VGPR and every check-node
+//     operation is one v_pk_* instruction for both (3 waves per codeblock,
+//     every lane busy);
+//   * the check-to-variable messages of all MAXL layers live in registers
+//     (int16 pairs), so LDS holds only the 22 + MAXL soft-bit nodes (10 KiB
+//     for MAXL = 4) and several codeblocks share a CU;
+//   * gather addresses: for each edge one of the two rows never wraps around
+//     the cyclic shift, so its address is the lane index plus an immediate
+//     offset; the other takes add, add, min;
+//   * no argmin index: an edge takes the second minimum exactly when its
+//     |v2c| equals the minimum (when two edges tie, min1 == min2 and the
+//     choice does not matter), computed as min(|v2c| - min1, 1);
+//   * CRC early stop: the remainder is only tested for zero, so it is
+//     accumulated as CRC(msg) x^(K Z - nof_sig) mod g (a unit multiple: zero
+//     iff the CRC is zero) from one fixed table order, which makes the four
+//     remainders of a soft-bit word one aligned 16-byte load.
+// Bit-exact with ldpc_decode_kernel (same per-edge arithmetic, identical
+// outputs, iteration counts and final soft bits).
+// ============================================================================
+
+typedef short pk16 __attribute__((ext_vector_type(2)));
+
+constexpr int HR_Z       = 384;
+constexpr int HR_HALF    = HR_Z / 2; // lanes per codeblock
+constexpr int HR_THREADS = HR_HALF;
+
+__device__ __forceinline__ pk16 pk_splat(int v)
+{
+  return pk16{static_cast<short>(v), static_cast<short>(v)};
+}
+__device__ __forceinline__ pk16 pk_min(pk16 a, pk16 b)
+{
+  return __builtin_elementwise_min(a, b);
+}
+__device__ __forceinline__ pk16 pk_max(pk16 a, pk16 b)
+{
+  return __builtin_elementwise_max(a, b);
+}
+__device__ __forceinline__ pk16 pk_clamp(pk16 x, int lim)
+{
+  return pk_min(pk_max(x, pk_splat(-lim)), pk_splat(lim));
+}
+
+template <int MAXL>
+__host__ __device__ constexpr int hr_lds_bytes()
+{
+  return LDS_SOFT_OFFSET + (22 + MAXL) * HR_Z;
+}
+
+// LDS byte offset of the soft bit that row (t + H) of edge EI reads, H = 0 or 192.
+// One of the two rows of an edge never wraps: its address is t + literal.
+template <int EI, int H>
+__device__ __forceinline__ uint32_t hr_addr(uint32_t t)
+{
+  constexpr uint32_t s    = (const_edge<1, HR_Z, EI>::shift + H) % HR_Z;
+  constexpr uint32_t base = LDS_SOFT_OFFSET + const_edge<1, HR_Z, EI>::var * HR_Z;
+  if constexpr (s <= HR_HALF) {
+    return t + (base + s); // t < 192: t + s < 384
+  } else {
+    return __builtin_elementwise_min(t + s, t + (s - HR_Z)) + base;
+  }
+}
+
+template <int ARITH>
+__device__ __forceinline__ pk16 pk_scale(pk16 m)
+{
+  return pk16{static_cast<short>(scale_mag<ARITH>(m.x)), static_cast<short>(scale_mag<ARITH>(m.y))};
+}
+
+// One layer (base-graph row L, global edges E0 .. E0 + DEG - 1) for rows t, t + 192.
+template <int L, int ARITH, int NE, int... E>
+__device__ __forceinline__ void hr_layer(lds_i8* lds, pk16 (&c2v)[NE], uint32_t t, std::integer_sequence<int, E...>)
+{
+  constexpr int E0  = row_start<1>(L);
+  constexpr int DEG = sizeof...(E);
+  pk16          v[DEG];
+  pk16          min1 = pk_splat(LLR_MAX), min2 = pk_splat(LLR_MAX), sgn = pk_splat(0);
+  // pass 1 (ldpc_decoder_impl.cpp:235 / :290): v2c and the check-node statistics
+  (
+      [&] {
+        if constexpr (E % EDGE_CHUNK == 0 && E > 0) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const pk16 s   = pk16{static_cast<short>(lds[hr_addr<E0 + E, 0>(t)]),
+                            static_cast<short>(lds[hr_addr<E0 + E, HR_HALF>(t)])};
+        const pk16 sat = pk_clamp(s, LLR_MAX);
+        // infinite soft bits (+-127) push |v2c| beyond 220 (see edge_pass1)
+        const pk16 x  = (s - sat) * pk_splat(27) + pk_clamp(s - c2v[E0 + E], LLR_MAX);
+        const pk16 ax = __builtin_elementwise_abs(x);
+        min2          = pk_max(min1, pk_min(ax, min2)); // median(min1, |v|, min2)
+        min1          = pk_min(min1, ax);
+        sgn ^= x;
+        v[E] = x;
+      }(),
+      ...);
+  __builtin_amdgcn_sched_barrier(0);
+  const pk16 s1  = pk_scale<ARITH>(min1);
+  const pk16 s2  = pk_scale<ARITH>(min2);
+  const pk16 d12 = s1 - s2;
+  // pass 2 (ldpc_decoder_impl.cpp:310, :270): new message and promotion sum
+  (
+      [&] {
+        if constexpr (E % EDGE_CHUNK == 0 && E > 0) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const pk16 x   = v[E];
+        const pk16 f   = pk_min(__builtin_elementwise_abs(x) - min1, pk_splat(1)); // 0: this edge holds min1
+        const pk16 mag = f * d12 + s2;
+        const pk16 neg = (sgn ^ x) >> 15;
+        const pk16 c   = (mag ^ neg) - neg;
+        const pk16 sum = c + x;
+        const pk16 m   = pk_clamp(sum, LLR_MAX);
+        const pk16 out = (pk_clamp(sum, LLR_MAX + 1) - m) * pk_splat(LLR_INFINITY - LLR_MAX) + m;
+        c2v[E0 + E]    = c;
+        lds[hr_addr<E0 + E, 0>(t)]       = static_cast<int8_t>(out.x);
+        lds[hr_addr<E0 + E, HR_HALF>(t)] = static_cast<int8_t>(out.y);
+      }(),
+      ...);
+}
+
+template <int L, int MAXL, int ARITH, int NE>
+__device__ __forceinline__ void hr_layers(lds_i8* lds, pk16 (&c2v)[NE], uint32_t t, int nof_layers)
+{
+  if constexpr (L < MAXL) {
+    if (L < 4 || L < nof_layers) {
+      asm volatile("" : "+v"(t));
+      hr_layer<L, ARITH>(lds, c2v, t, std::make_integer_sequence<int, bg_traits<1>::deg(L)>{});
+      __syncthreads();
+    }
+    hr_layers<L + 1, MAXL, ARITH>(lds, c2v, t, nof_layers);
+  }
+}
+
+template <int ARITH, int MAXL>
+__global__ void __launch_bounds__(HR_THREADS, 4) ldpc_decode_hr_kernel(decode_args a)
+{
+  constexpr int Z       = HR_Z;
+  constexpr int K       = 22 * Z;
+  constexpr int NODES   = 22 + MAXL;
+  constexpr int NE      = row_start<1>(MAXL);
+  constexpr int MAX_LLR = (NODES - 2) * Z; // host guarantees llr_len <= MAX_LLR
+  constexpr int NT      = HR_THREADS;
+  lds_i32*      red     = (lds_i32*)(uintptr_t)LDS_RED_OFFSET;
+  lds_i8*       lds     = (lds_i8*)(uintptr_t)0;
+  lds_i8*       soft    = lds + LDS_SOFT_OFFSET;
+  lds_i32*      soft4   = reinterpret_cast<lds_i32*>(soft);
+
+  for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    const int8_t* in     = a.llrs + static_cast<size_t>(cb) * a.llr_stride;
+    const int     n_llrs = static_cast<int>(a.llr_len);
+    uint8_t*      out    = a.out + static_cast<size_t>(cb) * a.out_stride;
+
+    // ---- input scan (last non-zero LLR, ldpc_decoder_impl.cpp:86) fused with the soft-bit load
+    // (:160): clamped full nodes, the partial tail node unclamped, zeros elsewhere.
+    if (t == 0) {
+      red[0] = -1;
+      red[1] = 0;
+      red[2] = 0;
+    }
+    __syncthreads();
+    {
+      const int      nw  = n_llrs >> 2;
+      const int      B4  = (n_llrs / Z) * Z >> 2;
+      const int32_t* in4 = reinterpret_cast<const int32_t*>(in);
+      const int      tail = n_llrs & 3; // trailing bytes of the partial word nw (tail node: unclamped)
+      int            last = -1;
+      uint32_t       w_in[(MAX_LLR / 4 + NT - 1) / NT];
+#pragma unroll
+      for (int k = 0; k < (MAX_LLR / 4 + NT - 1) / NT; ++k) {
+        const int w = static_cast<int>(t) + k * NT;
+        uint32_t  v = w < nw ? static_cast<uint32_t>(in4[w]) : 0u;
+        if (w == nw && tail != 0) {
+          for (int b = 0; b < tail; ++b) {
+            v |= static_cast<uint32_t>(static_cast<uint8_t>(in[4 * nw + b])) << (8 * b);
+          }
+        }
+        w_in[k] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < (MAX_LLR / 4 + NT - 1) / NT; ++k) {
+        const int      w = static_cast<int>(t) + k * NT;
+        const uint32_t v = w_in[k];
+        if (v != 0) {
+          last = 4 * w + (31 - __builtin_clz(v)) / 8;
+        }
+        uint32_t o = v;
+        if (w < B4) {
+          o = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int x = static_cast<int8_t>(v >> (8 * b));
+            o |= (static_cast<uint32_t>(med3_i(x, -SOFT_CLAMP, SOFT_CLAMP)) & 0xffu) << (8 * b);
+          }
+        }
+        if (w < (NODES - 2) * Z / 4) {
+          soft4[(2 * Z) / 4 + w] = static_cast<int32_t>(o); // words past nw hold zeros
+        }
+      }
+      // punctured nodes 0 and 1
+      soft4[t] = 0;
+      if (last >= 0) {
+        __hip_atomic_fetch_max(&red[0], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    __syncthreads();
+    const int input_size = __builtin_amdgcn_readfirstlane(red[0] + 1);
+
+    if (input_size < K && a.force_decoding) {
+      // ldpc_decoder_impl.cpp:92 (see ldpc_decode_kernel)
+      for (int b = t; b < K / 8 && !a.crc_table; b += NT) {
+        out[b] = 0xff;
+      }
+      if (t == 0) {
+        a.nof_iters[cb] = -1;
+      }
+      __syncthreads();
+      continue;
+    }
+    const int cb_len     = max(input_size + 2 * Z, K + 4 * Z);
+    const int nof_layers = (cb_len + Z - 1) / Z - 22;
+    const int nof_sig    = K - a.nof_filler_bits;
+    int       result     = -1;
+
+    pk16 c2v[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      c2v[e] = pk_splat(0);
+    }
+
+    for (int it = 0; it < a.max_iterations; ++it) {
+      hr_layers<0, MAXL, ARITH>(lds, c2v, t, nof_layers);
+
+      if (a.crc_table) {
+        // hard bits + CRC early stop (ldpc_decoder_impl.cpp:125), remainder up to a unit factor:
+        // bit i contributes crc_table[K - 1 - i]; the word of soft bits 4q .. 4q+3 reads the
+        // remainders [K - 4 - 4q, K - 1 - 4q] as one 16-byte load.
+        uint32_t tq = threadIdx.x;
+        asm volatile("" : "+v"(tq));
+        uint32_t crc = 0, zero = 0;
+#pragma unroll
+        for (int k = 0; k < K / 4 / NT; ++k) {
+          const int      q  = static_cast<int>(tq) + k * NT;
+          const uint32_t w4 = static_cast<uint32_t>(soft4[q]);
+          const uint4    r  = *reinterpret_cast<const uint4*>(a.crc_table + (K - 4 - 4 * q));
+          zero |= (w4 - 0x01010101u) & ~w4 & 0x80808080u; // some byte is zero
+          const uint32_t rr[4] = {r.w, r.z, r.y, r.x};
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int sb = static_cast<int8_t>(w4 >> (8 * b));
+            if (sb <= 0 && (4 * q + b < nof_sig)) {
+              crc ^= rr[b];
+            }
+          }
+        }
+        lds_u32* acc = reinterpret_cast<lds_u32*>(&red[1 + 2 * (it & 1)]);
+        if (crc != 0) {
+          __hip_atomic_fetch_xor(&acc[0], crc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (zero != 0) {
+          __hip_atomic_fetch_or(&acc[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        const uint32_t c_all = __builtin_amdgcn_readfirstlane(acc[0]);
+        const uint32_t z_all = __builtin_amdgcn_readfirstlane(acc[1]);
+        if (tq == 0) {
+          // the other slot was read before this iteration's barrier: reset it for the next check
+          lds_u32* nxt = reinterpret_cast<lds_u32*>(&red[1 + 2 * ((it + 1) & 1)]);
+          nxt[0]       = 0;
+          nxt[1]       = 0;
+        }
+        if (z_all == 0 && c_all == 0) {
+          result = it + 1;
+          break;
+        }
+      }
+    }
+
+    // ---- hard decision, packed MSB-first: 4 output bytes per task
+    uint32_t te = threadIdx.x;
+    asm volatile("" : "+v"(te));
+    for (int task = te; task < K / 32; task += NT) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        const uint32_t w = static_cast<uint32_t>(soft4[8 * task + h]);
+        // per-byte (x <= 0) = sign of x - 1 (SWAR subtract, no borrow between bytes)
+        const uint32_t d    = ((w | 0x80808080u) - 0x01010101u) ^ (~w & 0x80808080u);
+        const uint32_t nib  = (((d & 0x80808080u) >> 7) * 0x08040201u) >> 24; // byte0 -> bit 3
+        const int      byte = h >> 1;
+        o |= (nib & 0xfu) << (8 * byte + ((h & 1) ? 0 : 4));
+      }
+      uint8_t* ob = out + 4 * task;
+      if (((reinterpret_cast<uintptr_t>(ob)) & 3u) == 0) {
+        *reinterpret_cast<uint32_t*>(ob) = o;
+      } else {
+        ob[0] = static_cast<uint8_t>(o);
+        ob[1] = static_cast<uint8_t>(o >> 8);
+        ob[2] = static_cast<uint8_t>(o >> 16);
+        ob[3] = static_cast<uint8_t>(o >> 24);
+      }
+    }
+    if (a.soft_out) {
+      int32_t* so = reinterpret_cast<int32_t*>(a.soft_out + static_cast<size_t>(cb) * (68 * Z));
+      for (int i = te; i < 68 * Z / 4; i += NT) {
+        so[i] = i < NODES * Z / 4 ? soft4[i] : 0;
+      }
+    }
+    if (te == 0) {
+      a.nof_iters[cb] = result;
+    }
+    __syncthreads();
+  }
+}
+
+constexpr int HR_MAXL = 4;
+
+bool ldpc_decode_hr_eligible(const decode_args& args, const lifted_graph& g)
+{
+  // SRSRAN_AMD_LDPC_HR=0 keeps every launch on ldpc_decode_kernel (A/B timing, cross-checks).
+  static const bool enabled = [] {
+    const char* e = std::getenv("SRSRAN_AMD_LDPC_HR");
+    return e == nullptr || e[0] != '0';
+  }();
+  return enabled && g.bg == 1 && g.Z == HR_Z && args.llr_lens == nullptr && args.aligned4 != 0 &&
+         args.llr_len <= static_cast<uint32_t>((20 + HR_MAXL) * HR_Z) &&
+         ((reinterpret_cast<uintptr_t>(args.soft_out) | (args.soft_out ? 68u * HR_Z : 0u)) & 3u) == 0;
+}
+
 size_t ldpc_decode_lds_bytes(const lifted_graph& g)
 {
   return g.bg == 1 ? lds_total_bytes<1>(g.Z) : lds_total_bytes<2>(g.Z);
@@ -724,6 +1064,18 @@ static void launch_bg(const decode_args& args, const lifted_graph& g, int grid, 
 
 hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, int arith, int grid, hipStream_t stream)
 {
+  if (ldpc_decode_hr_eligible(args, g)) {
+    // The crc table of the high-rate kernel is indexed from K Z - 1 down, 16-byte aligned.
+    constexpr size_t lds = hr_lds_bytes<HR_MAXL>();
+    if (arith == ARITH_GENERIC) {
+      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_GENERIC, HR_MAXL>), dim3(grid), dim3(HR_THREADS), lds, stream,
+                         args);
+    } else {
+      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_SIMD, HR_MAXL>), dim3(grid), dim3(HR_THREADS), lds, stream,
+                         args);
+    }
+    return hipGetLastError();
+  }
   const int threads = ((g.Z + 63) / 64) * 64;
   if (g.bg == 1) {
     if (arith == ARITH_GENERIC) {

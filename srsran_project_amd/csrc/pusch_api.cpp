@@ -20,8 +20,10 @@
 #include "crc_internal.h"
 #include "device_buffer.h"
 #include "ldpc_codec_internal.h"
+#include "rate_matching_common.h"
 #include "sch_args.h"
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -65,6 +67,32 @@ soft_row_layout layout_of(const srs_amd_sch_plan* p)
   l.flag_offset = static_cast<uint32_t>(l.msg_offset + align_up((p->segment_length + 7) / 8, 16));
   l.row_bytes   = static_cast<uint32_t>(align_up(l.flag_offset + 4, 64));
   return l;
+}
+
+// Length of the soft-buffer prefix that can hold non-zero LLRs after this call's rate dematching,
+// rounded up to whole lifting-size nodes (so the decoder's clamped-node load is unchanged), or the
+// whole row when it cannot be bounded.  New data with k0 = 0 and no circular wrap writes LLRs to
+// [0, E), +inf fillers to [nof_info, nof_sys) and data to [nof_sys, E + F); the rest of the row is
+// zeroed when the buffer is fresh, or when E covers the information bits of a full-length buffer
+// (nothing of the old contents survives, see ldpc_rate_dematch_kernel).  The decoder then scans
+// (ldpc_decoder_impl.cpp:86) only this prefix, and a short prefix bounds its layer count.
+uint32_t llr_prefix(const srs_amd_sch_plan* p, const soft_row_layout& lay, bool new_data, bool fresh)
+{
+  rm_geometry g{};
+  if (!new_data || make_rm_geometry(g, p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                                    p->nof_filler_bits) != nullptr) {
+    return lay.soft_bytes;
+  }
+  const uint32_t C     = p->nof_segments;
+  const uint32_t e_min = p->nof_short_segments > 0 ? p->rm_length_short : p->rm_length_long;
+  const uint32_t e_max = p->nof_short_segments < C ? p->rm_length_long : p->rm_length_short;
+  if (g.k0 != 0 || e_max + g.F > g.Ncb || !(fresh || (e_min >= g.nof_info && g.Ncb == g.N))) {
+    return lay.soft_bytes;
+  }
+  const uint32_t Z   = p->lifting_size;
+  const uint32_t end = std::max(e_max + g.F, g.nof_sys);
+  const uint32_t lo  = (p->base_graph == 1 ? 24u : 12u) * Z; // ldpc_decoder_impl.cpp:78 minimum input length
+  return std::min(lay.soft_bytes, std::max(lo, (end + Z - 1) / Z * Z));
 }
 
 int check_plan(const srs_amd_sch_plan* p)
@@ -158,8 +186,8 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   dc.max_iterations  = cfg->nof_ldpc_iterations;
   srs_amd_ldpc_decoder* dec = d->dec[cfg->force_decoding ? 1 : 0];
   rc = srs_amd_ldpc_decode_batch(dec, &dc, cfg->use_early_stop ? crc_poly : SRS_AMD_NO_CRC, d_soft, lay.row_bytes,
-                                 nullptr, lay.soft_bytes, d->msgs.as<uint8_t>(), msg_stride, d->iters.as<int32_t>(),
-                                 nullptr, rows, stream);
+                                 nullptr, llr_prefix(p, lay, cfg->new_data != 0, internal), d->msgs.as<uint8_t>(),
+                                 msg_stride, d->iters.as<int32_t>(), nullptr, rows, stream);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
@@ -261,6 +289,14 @@ int srs_amd_pusch_decoder_create(srs_amd_pusch_decoder** out, int arith, int dev
 void srs_amd_pusch_decoder_destroy(srs_amd_pusch_decoder* dec)
 {
   delete dec;
+}
+
+uint32_t srs_amd_pusch_decoder_llr_prefix(const srs_amd_sch_plan* plan, int new_data, int fresh)
+{
+  if (plan == nullptr || plan->nof_segments == 0 || plan->lifting_size == 0) {
+    return 0;
+  }
+  return llr_prefix(plan, layout_of(plan), new_data != 0, fresh != 0);
 }
 
 uint64_t srs_amd_pusch_soft_buffer_size(const srs_amd_sch_plan* plan)

@@ -61,6 +61,7 @@ def _declare(lib):
         "srs_amd_pusch_decoder_create": (c.c_int, [c.POINTER(P), c.c_int, c.c_int]),
         "srs_amd_pusch_decoder_destroy": (None, [P]),
         "srs_amd_pusch_soft_buffer_size": (c.c_uint64, [PP]),
+        "srs_amd_pusch_decoder_llr_prefix": (c.c_uint32, [PP, c.c_int, c.c_int]),
         "srs_amd_pusch_decode": (c.c_int, [P, P, c.POINTER(PuschDecoderResult), P, P, PP,
                                            c.POINTER(PuschDecoderConfig)]),
         "srs_amd_pusch_decode_batch": (c.c_int, [P, PP, c.POINTER(PuschDecoderConfig), P, u, P, P, u, P, P, u, P]),
@@ -122,6 +123,11 @@ def sch_segments(plan):
 
 def soft_buffer_size(plan):
     return int(_L().srs_amd_pusch_soft_buffer_size(ctypes.byref(plan)))
+
+
+def decoder_llr_prefix(plan, new_data=True, fresh=True):
+    """LLRs of each soft-buffer row the PUSCH decoder hands to the LDPC decoder (srs_amd_pusch_decoder_llr_prefix)."""
+    return int(_L().srs_amd_pusch_decoder_llr_prefix(ctypes.byref(plan), int(new_data), int(fresh)))
 
 
 class PdschEncoder:

@@ -186,3 +186,77 @@ def test_invalid_configuration_raises(amd):
     with pytest.raises(ValueError):
         dec.decode(np.zeros((22 * 4 + 7) // 8, np.uint8), np.zeros(200, np.int8), None,
                    amd.LdpcDecoderConfiguration(lifting_size=4, max_iterations=0))
+
+
+# ---- high-rate BG1 / Z = 384 kernel (ldpc_decode_hr_kernel): rows of at most 24 Z LLRs, so at most
+# four layers; selected by the launch for those rows (ldpc_decoder.hip, ldpc_decode_hr_eligible).
+HR_LEN = 24 * 384
+
+
+def _high_rate_rows(n, seed, noise, crc=None, zero_from=None, filler=0):
+    msgs, llrs = noisy_codeblocks(1, 384, n, length=HR_LEN, noise=noise, seed=seed, crc_poly=crc)
+    if filler:
+        llrs[:, 20 * 384 - filler:20 * 384] = 127  # the rate dematcher's +inf filler LLRs
+    if zero_from is not None:
+        for i, z in enumerate(zero_from):
+            llrs[i, z:] = 0
+    return msgs, llrs
+
+
+@pytest.mark.parametrize("arith", ["simd", "generic"])
+def test_high_rate_kernel_parity(amd, arith):
+    dec = amd.LdpcDecoder(arith)
+    # near threshold (several iterations, some failures), moderate, noiseless-ish
+    for seed, noise, crc in ((1, 11.0, 1), (2, 7.0, 1), (3, 2.0, 1), (4, 9.0, None), (5, 10.0, 0)):
+        _, llrs = _high_rate_rows(12, seed, noise, crc)
+        _check(amd, dec, arith, llrs, 1, 384, iters=6, crc=crc)
+
+
+def test_high_rate_kernel_fillers_and_trimming(amd):
+    dec = amd.LdpcDecoder("simd")
+    _, llrs = _high_rate_rows(6, 21, 8.0, crc=1, filler=136)
+    _check(amd, dec, "simd", llrs, 1, 384, iters=5, crc=1, filler=136)
+    # trailing zeros: the decoder trims at the last non-zero LLR (23 Z + 5, 22 Z + 2 Z - 1, ...)
+    _, llrs = _high_rate_rows(4, 22, 6.0, crc=1, zero_from=[23 * 384 + 5, 24 * 384 - 1, 22 * 384, 21 * 384 + 7])
+    _check(amd, dec, "simd", llrs, 1, 384, iters=4, crc=1)
+    # infinite soft bits anywhere in the row (saturated LLRs)
+    _, llrs = _high_rate_rows(4, 23, 30.0)
+    llrs[:, ::97] = np.where(llrs[:, ::97] >= 0, 127, -127)
+    _check(amd, dec, "simd", llrs, 1, 384, iters=3)
+
+
+def test_high_rate_kernel_force_decoding(amd):
+    dec = amd.LdpcDecoder("simd", force_decoding=True)
+    llrs = np.zeros((3, HR_LEN), np.int8)
+    llrs[0, :100] = 5  # input_size < K: no value, all ones
+    llrs[1, : 22 * 384 + 3] = -9
+    llrs[2] = _high_rate_rows(1, 31, 6.0)[1][0]
+    out, it, _ = _gpu_decode(amd, dec, llrs, 1, 384, 3)
+    assert it[0] == -1 and (oracle.unpack_bits(out[0], 22 * 384) == 1).all()
+    for i in (1, 2):
+        r, o, _ = oracle.ldpc_decode(llrs[i], 1, 384, 3, force_decoding=True)
+        np.testing.assert_array_equal(out[i], o)
+        assert (-1 if r is None else r) == it[i]
+
+
+def test_high_rate_kernel_grid_stride_and_offsets(amd):
+    import torch
+
+    dec = amd.LdpcDecoder("simd")
+    dec.set_max_slots(48)
+    _, llrs = _high_rate_rows(16, 41, 9.0, crc=1)
+    big = np.concatenate([llrs] * 10)
+    # rows with a stride larger than the length (PUSCH soft-buffer rows) and an odd output stride
+    rows = np.zeros((big.shape[0], 26112), np.int8)
+    rows[:, :HR_LEN] = big
+    d = torch.from_numpy(rows).cuda()[:, :HR_LEN]
+    cfg = amd.LdpcDecoderConfiguration(base_graph=1, lifting_size=384, nof_crc_bits=24, max_iterations=6)
+    out = torch.zeros((big.shape[0], 1061), dtype=torch.uint8, device="cuda")
+    out, it = dec.decode_batch(d, cfg, amd.CrcGeneratorPoly.CRC24B, out=out[:, 1:1057])
+    torch.cuda.synchronize()
+    out, it = out.cpu().numpy(), it.cpu().numpy()
+    for i in range(16):
+        r, o, _ = oracle.ldpc_decode(llrs[i], 1, 384, 6, crc_poly=1, nof_crc_bits=24)
+        for k in range(10):
+            np.testing.assert_array_equal(out[16 * k + i], o)
+            assert it[16 * k + i] == (-1 if r is None else r)
