@@ -777,15 +777,79 @@ __device__ __forceinline__ uint32_t hr_addr(uint32_t t)
   }
 }
 
+// Check-to-variable messages of the first MAXL layers, register resident: one int16 pair per edge
+// (default), or (HR_PACK8) two edges per VGPR as int8 pairs, edge 2w in the high byte and edge 2w+1
+// in the low byte of each 16-bit half, unpacked with one or two packed shifts and repacked with one
+// v_perm_b32.  Measured (tools/ldpc_hr_probe.py, 4,544 codeblocks): the layers are VALU-bound, and
+// the 2.5 extra VALU per edge of the int8 form cost more (75.6 vs 70.2 us per iteration) than its
+// occupancy gain (98 vs 128 VGPRs) returns; the edge chunking (5, 10, 19) changes nothing.
+#ifndef HR_PACK8
+#define HR_PACK8 0
+#endif
+template <int NE, bool PACK8 = HR_PACK8>
+struct hr_msgs {
+  pk16 m[NE];
+  __device__ __forceinline__ void zero()
+  {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      m[e] = pk16{0, 0};
+    }
+  }
+  template <int E>
+  __device__ __forceinline__ pk16 get() const { return m[E]; }
+  template <int E>
+  __device__ __forceinline__ void set(pk16 c) { m[E] = c; }
+};
+template <int NE>
+struct hr_msgs<NE, true> {
+  uint32_t w[(NE + 1) / 2];
+  __device__ __forceinline__ void zero()
+  {
+#pragma unroll
+    for (int e = 0; e < (NE + 1) / 2; ++e) {
+      w[e] = 0;
+    }
+  }
+  template <int E>
+  __device__ __forceinline__ pk16 get() const
+  {
+    const pk16 x = __builtin_bit_cast(pk16, w[E >> 1]);
+    if constexpr ((E & 1) == 0) {
+      return x >> 8;
+    } else {
+      return (x << 8) >> 8;
+    }
+  }
+  template <int E>
+  __device__ __forceinline__ void set(pk16 c)
+  {
+    const uint32_t cv = __builtin_bit_cast(uint32_t, c);
+    // v_perm_b32(src0 = c, src1 = w): selector bytes 0-3 pick w, 4-7 pick c
+    w[E >> 1] = __builtin_amdgcn_perm(cv, w[E >> 1], (E & 1) == 0 ? 0x06020400u : 0x03060104u);
+    // pin the repacked word here: left alone the compiler sinks the v_perm_b32 to the end of the
+    // iteration and keeps every new message unpacked (and spilled) until then
+    asm volatile("" : "+v"(w[E >> 1]));
+  }
+};
+
 template <int ARITH>
 __device__ __forceinline__ pk16 pk_scale(pk16 m)
 {
   return pk16{static_cast<short>(scale_mag<ARITH>(m.x)), static_cast<short>(scale_mag<ARITH>(m.y))};
 }
 
+// Edges per scheduling group in the two passes of a layer (bounds the gathered values in flight).
+#ifndef HR_CHUNK1
+#define HR_CHUNK1 5
+#endif
+#ifndef HR_CHUNK2
+#define HR_CHUNK2 5
+#endif
+
 // One layer (base-graph row L, global edges E0 .. E0 + DEG - 1) for rows t, t + 192.
-template <int L, int ARITH, int NE, int... E>
-__device__ __forceinline__ void hr_layer(lds_i8* lds, pk16 (&c2v)[NE], uint32_t t, std::integer_sequence<int, E...>)
+template <int L, int ARITH, typename MSGS, int... E>
+__device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std::integer_sequence<int, E...>)
 {
   constexpr int E0  = row_start<1>(L);
   constexpr int DEG = sizeof...(E);
@@ -794,14 +858,14 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, pk16 (&c2v)[NE], uint32_t 
   // pass 1 (ldpc_decoder_impl.cpp:235 / :290): v2c and the check-node statistics
   (
       [&] {
-        if constexpr (E % EDGE_CHUNK == 0 && E > 0) {
+        if constexpr (E % HR_CHUNK1 == 0 && E > 0) {
           __builtin_amdgcn_sched_barrier(0);
         }
         const pk16 s   = pk16{static_cast<short>(lds[hr_addr<E0 + E, 0>(t)]),
                             static_cast<short>(lds[hr_addr<E0 + E, HR_HALF>(t)])};
         const pk16 sat = pk_clamp(s, LLR_MAX);
         // infinite soft bits (+-127) push |v2c| beyond 220 (see edge_pass1)
-        const pk16 x  = (s - sat) * pk_splat(27) + pk_clamp(s - c2v[E0 + E], LLR_MAX);
+        const pk16 x  = (s - sat) * pk_splat(27) + pk_clamp(s - c2v.template get<E0 + E>(), LLR_MAX);
         const pk16 ax = __builtin_elementwise_abs(x);
         min2          = pk_max(min1, pk_min(ax, min2)); // median(min1, |v|, min2)
         min1          = pk_min(min1, ax);
@@ -816,10 +880,12 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, pk16 (&c2v)[NE], uint32_t 
   // pass 2 (ldpc_decoder_impl.cpp:310, :270): new message and promotion sum
   (
       [&] {
-        if constexpr (E % EDGE_CHUNK == 0 && E > 0) {
+        if constexpr (E % HR_CHUNK2 == 0 && E > 0) {
           __builtin_amdgcn_sched_barrier(0);
         }
-        const pk16 x   = v[E];
+        pk16 x = v[E];
+        // opaque: otherwise |x| of pass 1 is kept live (19 more VGPRs) instead of being recomputed
+        asm volatile("" : "+v"(x));
         const pk16 f   = pk_min(__builtin_elementwise_abs(x) - min1, pk_splat(1)); // 0: this edge holds min1
         const pk16 mag = f * d12 + s2;
         const pk16 neg = (sgn ^ x) >> 15;
@@ -827,15 +893,15 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, pk16 (&c2v)[NE], uint32_t 
         const pk16 sum = c + x;
         const pk16 m   = pk_clamp(sum, LLR_MAX);
         const pk16 out = (pk_clamp(sum, LLR_MAX + 1) - m) * pk_splat(LLR_INFINITY - LLR_MAX) + m;
-        c2v[E0 + E]    = c;
+        c2v.template set<E0 + E>(c);
         lds[hr_addr<E0 + E, 0>(t)]       = static_cast<int8_t>(out.x);
         lds[hr_addr<E0 + E, HR_HALF>(t)] = static_cast<int8_t>(out.y);
       }(),
       ...);
 }
 
-template <int L, int MAXL, int ARITH, int NE>
-__device__ __forceinline__ void hr_layers(lds_i8* lds, pk16 (&c2v)[NE], uint32_t t, int nof_layers)
+template <int L, int MAXL, int ARITH, typename MSGS>
+__device__ __forceinline__ void hr_layers(lds_i8* lds, MSGS& c2v, uint32_t t, int nof_layers)
 {
   if constexpr (L < MAXL) {
     if (L < 4 || L < nof_layers) {
@@ -939,11 +1005,8 @@ __global__ void __launch_bounds__(HR_THREADS, 4) ldpc_decode_hr_kernel(decode_ar
     const int nof_sig    = K - a.nof_filler_bits;
     int       result     = -1;
 
-    pk16 c2v[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      c2v[e] = pk_splat(0);
-    }
+    hr_msgs<NE> c2v;
+    c2v.zero();
 
     for (int it = 0; it < a.max_iterations; ++it) {
       hr_layers<0, MAXL, ARITH>(lds, c2v, t, nof_layers);
@@ -955,8 +1018,14 @@ __global__ void __launch_bounds__(HR_THREADS, 4) ldpc_decode_hr_kernel(decode_ar
         uint32_t tq = threadIdx.x;
         asm volatile("" : "+v"(tq));
         uint32_t crc = 0, zero = 0;
+        // chunks of CRC_CHUNK words with a scheduling barrier in between: all eleven 16-byte remainder
+        // loads in flight at once would need 44 VGPRs next to the message file
+        constexpr int CRC_CHUNK = 4;
 #pragma unroll
         for (int k = 0; k < K / 4 / NT; ++k) {
+          if (k % CRC_CHUNK == 0 && k > 0) {
+            __builtin_amdgcn_sched_barrier(0);
+          }
           const int      q  = static_cast<int>(tq) + k * NT;
           const uint32_t w4 = static_cast<uint32_t>(soft4[q]);
           const uint4    r  = *reinterpret_cast<const uint4*>(a.crc_table + (K - 4 - 4 * q));
