@@ -372,7 +372,7 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
     if world == 1 and not args.no_latency:
         lat = {"1_cell": latency_ms(dev, 1), "8_cells": latency_ms(dev, 8)}
     low = None
-    if world == 1 and args.low_snr_db is not None:
+    if world == 1 and args.low_snr_db is not None and args.low_snr_db >= 0:
         low = low_snr_line(args, dev, timed, dist)
     cpu = None
     if not args.no_cpu_baseline and world == 1:

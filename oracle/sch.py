@@ -93,6 +93,7 @@ class HarqBuffer:
         self.soft = [np.zeros(BG_N_SHORT[bg] * Z, np.int8) for _ in range(C)]
         self.msgs = [np.zeros(_ceil(p["segment_length"], 8), np.uint8) for _ in range(C)]
         self.crc = [False] * C
+        self.its = [0] * C  # iterations of the decoding that set crc[r]
 
 
 def pusch_decode(llrs, p, harq, tb_out, max_iterations=6, arith="simd", use_early_stop=True, force_decoding=False,
@@ -110,8 +111,10 @@ def pusch_decode(llrs, p, harq, tb_out, max_iterations=6, arith="simd", use_earl
     for r, (E, off) in enumerate(segments(p)):
         rate_dematch(llrs[off:off + E], bg, Z, p["rv"], p["modulation_order"], harq.soft[r], new_data, p["Nref"], F)
         if harq.crc[r]:
+            # not decoded again; the reference's cb_stats[r] is not updated and holds the iterations of the
+            # decoding that passed (pusch_decoder_impl.cpp:333-345, for one decoder object serving the process)
             iters.append(None)
-            stats.append(None)  # the reference keeps a stale statistic here
+            stats.append(harq.its[r])
             continue
         if use_early_stop:
             it, msg, _ = ldpc_decode(harq.soft[r], bg, Z, max_iterations, arith, crc_poly, F, nof_crc, force_decoding)
@@ -121,6 +124,7 @@ def pusch_decode(llrs, p, harq, tb_out, max_iterations=6, arith="simd", use_earl
         harq.msgs[r] = msg
         if it is not None:
             harq.crc[r] = True
+            harq.its[r] = it
         iters.append(it)
         stats.append(it if it is not None else max_iterations)
     tbs = p["tbs"]

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include "api_common.h"
+#include "ldpc_codec_internal.h"
 #include "ldpc_common.h"
 #include <cstdarg>
 #include <cstdio>
@@ -210,6 +211,28 @@ int srs_amd_ldpc_decode_batch(srs_amd_ldpc_decoder*              d,
                               uint32_t                           nof_cbs,
                               void*                              stream)
 {
+  return srs_amd::ldpc_decode_batch_ex(d, cfg, crc_poly, d_llrs, llr_stride, d_llr_lens, llr_len, d_output,
+                                       out_stride, d_nof_iters, d_soft_out, nof_cbs, stream, nullptr, 0);
+}
+
+} // extern "C"
+
+int srs_amd::ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
+                                  const srs_amd_ldpc_decoder_config* cfg,
+                                  int                                crc_poly,
+                                  const int8_t*                      d_llrs,
+                                  uint32_t                           llr_stride,
+                                  const uint32_t*                    d_llr_lens,
+                                  uint32_t                           llr_len,
+                                  uint8_t*                           d_output,
+                                  uint32_t                           out_stride,
+                                  int32_t*                           d_nof_iters,
+                                  int8_t*                            d_soft_out,
+                                  uint32_t                           nof_cbs,
+                                  void*                              stream,
+                                  const uint8_t*                     d_skip_flags,
+                                  uint32_t                           skip_stride)
+{
   if (d == nullptr) {
     return fail(SRS_AMD_EINVAL, "null decoder");
   }
@@ -265,6 +288,8 @@ int srs_amd_ldpc_decode_batch(srs_amd_ldpc_decoder*              d,
   a.nof_filler_bits = static_cast<int32_t>(cfg->nof_filler_bits);
   a.max_iterations  = static_cast<int32_t>(cfg->max_iterations);
   a.force_decoding  = d->force_decoding;
+  a.skip_flags      = d_skip_flags;
+  a.skip_stride     = skip_stride;
   const int grid    = static_cast<int>(nof_cbs < d->max_slots ? nof_cbs : d->max_slots);
   e = launch_ldpc_decode(a, g, d->arith, grid, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) {
@@ -272,6 +297,8 @@ int srs_amd_ldpc_decode_batch(srs_amd_ldpc_decoder*              d,
   }
   return SRS_AMD_OK;
 }
+
+extern "C" {
 
 int srs_amd_ldpc_decode(srs_amd_ldpc_decoder*              d,
                         uint8_t*                           output_packed,

@@ -1,6 +1,7 @@
 // ldpc_codec_internal.h -- library-internal entry points of the LDPC rate matching objects.
 #pragma once
 
+#include "srsran_amd/ldpc.h"
 #include "srsran_amd/ldpc_encoder.h"
 #include "srsran_amd/ldpc_rate_matching.h"
 
@@ -36,5 +37,24 @@ int ldpc_encode_batch_ex(srs_amd_ldpc_encoder*              enc,
                          uint32_t                           nof_cbs,
                          void*                              stream,
                          uint32_t                           max_bits);
+
+// srs_amd_ldpc_decode_batch with an optional per-codeblock skip flag (int32 at d_skip_flags + cb *
+// skip_stride, non-zero: not decoded, nof_iters[cb] = -2): the PUSCH decoder's retransmissions of
+// codeblocks whose CRC passed in an earlier transmission (pusch_decoder_impl.cpp:330-345).
+int ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
+                         const srs_amd_ldpc_decoder_config* cfg,
+                         int                                crc_poly,
+                         const int8_t*                      d_llrs,
+                         uint32_t                           llr_stride,
+                         const uint32_t*                    d_llr_lens,
+                         uint32_t                           llr_len,
+                         uint8_t*                           d_output,
+                         uint32_t                           out_stride,
+                         int32_t*                           d_nof_iters,
+                         int8_t*                            d_soft_out,
+                         uint32_t                           nof_cbs,
+                         void*                              stream,
+                         const uint8_t*                     d_skip_flags,
+                         uint32_t                           skip_stride);
 
 } // namespace srs_amd

@@ -63,7 +63,13 @@ struct decode_args {
   int32_t         max_iterations;
   int32_t         force_decoding;
   int32_t         aligned4;     // llrs and llr_stride are multiples of 4 bytes (vector loads)
+  // optional: codeblock cb is not decoded (nof_iters[cb] = -2, output untouched) when the int32 at
+  // skip_flags + cb * skip_stride is non-zero -- a PUSCH HARQ retransmission of a codeblock whose CRC
+  // passed earlier is only rate dematched (pusch_decoder_impl.cpp:330-345)
+  const uint8_t*  skip_flags;
+  uint32_t        skip_stride;
 };
+constexpr int32_t LDPC_ITERS_SKIPPED = -2;
 
 // Position of a lifting size in the 51-entry list (ldpc.h all_lifting_sizes), -1 if invalid.
 int lifting_size_position(int Z);

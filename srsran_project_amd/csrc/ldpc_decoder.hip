@@ -475,6 +475,12 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
   const int  NZ      = N_FULL * Z;
 
   for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
+    if (a.skip_flags && *reinterpret_cast<const int32_t*>(a.skip_flags + static_cast<size_t>(cb) * a.skip_stride)) {
+      if (threadIdx.x == 0) {
+        a.nof_iters[cb] = LDPC_ITERS_SKIPPED; // uniform over the workgroup
+      }
+      continue;
+    }
     // Per-lane values are rebuilt from a laundered thread id in each phase, so
     // the compiler cannot hoist them out of the codeblock loop and keep them
     // live (spilled to scratch) across the iterations.
@@ -928,6 +934,12 @@ __global__ void __launch_bounds__(HR_THREADS, 4) ldpc_decode_hr_kernel(decode_ar
   lds_i32*      soft4   = reinterpret_cast<lds_i32*>(soft);
 
   for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
+    if (a.skip_flags && *reinterpret_cast<const int32_t*>(a.skip_flags + static_cast<size_t>(cb) * a.skip_stride)) {
+      if (threadIdx.x == 0) {
+        a.nof_iters[cb] = LDPC_ITERS_SKIPPED; // uniform over the workgroup
+      }
+      continue;
+    }
     uint32_t t = threadIdx.x;
     asm volatile("" : "+v"(t));
     const int8_t* in     = a.llrs + static_cast<size_t>(cb) * a.llr_stride;

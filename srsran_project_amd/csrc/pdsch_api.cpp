@@ -35,11 +35,8 @@ struct srs_amd_pdsch_encoder {
   srs_amd_ldpc_encoder*      enc    = nullptr;
   srs_amd_ldpc_rate_matcher* rm     = nullptr;
   device_buffer              tb_crcs, msgs, coded, rm_arrays, host_io;
-  std::vector<uint32_t>      h_arrays;
-  // Cached key of the uploaded rate-matching arrays.
-  srs_amd_sch_plan key_plan{};
-  uint32_t         key_tbs = 0, key_stride = 0;
-  std::mutex       mtx;
+  stream_order               order; // scratch reuse across the callers' streams
+  std::mutex                 mtx;
   ~srs_amd_pdsch_encoder()
   {
     (void)hipSetDevice(device);
@@ -97,27 +94,13 @@ int encode_locked(srs_amd_pdsch_encoder* e,
     return hip_fail(he, "PDSCH encoder scratch");
   }
   // Rate-matching lengths and codeword offsets, uploaded when the geometry changes.
-  if (std::memcmp(&e->key_plan, p, sizeof(*p)) != 0 || e->key_tbs != nof_tbs || e->key_stride != cw_stride) {
-    std::vector<uint32_t> E(C), off(C);
-    srs_amd_sch_plan_segments(p, E.data(), off.data());
-    e->h_arrays.resize(2 * rows);
-    for (uint32_t t = 0; t < nof_tbs; ++t) {
-      for (uint32_t r = 0; r < C; ++r) {
-        e->h_arrays[t * C + r]        = E[r];
-        e->h_arrays[rows + t * C + r] = t * cw_stride * 8 + off[r];
-      }
-    }
-    he = hipMemcpyAsync(e->rm_arrays.ptr, e->h_arrays.data(), sizeof(uint32_t) * 2 * rows, hipMemcpyHostToDevice,
-                        stream);
-    if (he == hipSuccess) {
-      he = hipStreamSynchronize(stream);
-    }
-    if (he != hipSuccess) {
-      return hip_fail(he, "PDSCH encoder rate-matching arrays");
-    }
-    e->key_plan   = *p;
-    e->key_tbs    = nof_tbs;
-    e->key_stride = cw_stride;
+  he = e->order.begin(stream);
+  if (he == hipSuccess) {
+    he = launch_rm_arrays(e->rm_arrays.as<uint32_t>(), nof_tbs, C, p->nof_short_segments, p->rm_length_short,
+                          p->rm_length_long, cw_stride * 8, stream);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH encoder rate-matching arrays");
   }
   // 1. TB CRC.
   srs_amd_crc_calculator* tbcrc = p->nof_tb_crc_bits == 16 ? e->crc16 : e->crc24a;
@@ -168,8 +151,13 @@ int encode_locked(srs_amd_pdsch_encoder* e,
   // 5. Rate matching into the codeword rows.
   srs_amd_codeblock_metadata md{p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
                                 p->nof_filler_bits};
-  return srs_amd_ldpc_rate_match_batch(e->rm, &md, e->coded.as<uint8_t>(), cb_stride, e->rm_arrays.as<uint32_t>(),
-                                       e->rm_arrays.as<uint32_t>() + rows, p->rm_length_long, d_cw, rows, stream);
+  rc = srs_amd_ldpc_rate_match_batch(e->rm, &md, e->coded.as<uint8_t>(), cb_stride, e->rm_arrays.as<uint32_t>(),
+                                     e->rm_arrays.as<uint32_t>() + rows, p->rm_length_long, d_cw, rows, stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  he = e->order.end(stream);
+  return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "PDSCH encoder completion event");
 }
 
 } // namespace

@@ -37,9 +37,7 @@ struct srs_amd_pusch_decoder {
   srs_amd_ldpc_rate_dematcher* dm     = nullptr;
   srs_amd_ldpc_decoder*        dec[2] = {nullptr, nullptr}; // force_decoding 0 / 1
   device_buffer                soft, msgs, iters, checks, arrays, results, host_io, tb_acc;
-  std::vector<uint32_t>        h_arrays;
-  srs_amd_sch_plan             key_plan{};
-  uint32_t                     key_tbs = 0, key_stride = 0;
+  stream_order                 order; // scratch reuse across the callers' streams
   std::mutex                   mtx;
   ~srs_amd_pusch_decoder()
   {
@@ -144,27 +142,13 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH decoder scratch");
   }
-  if (std::memcmp(&d->key_plan, p, sizeof(*p)) != 0 || d->key_tbs != nof_tbs || d->key_stride != llr_stride) {
-    std::vector<uint32_t> E(C), off(C);
-    srs_amd_sch_plan_segments(p, E.data(), off.data());
-    d->h_arrays.resize(2 * rows);
-    for (uint32_t t = 0; t < nof_tbs; ++t) {
-      for (uint32_t r = 0; r < C; ++r) {
-        d->h_arrays[t * C + r]        = E[r];
-        d->h_arrays[rows + t * C + r] = t * llr_stride + off[r];
-      }
-    }
-    he = hipMemcpyAsync(d->arrays.ptr, d->h_arrays.data(), sizeof(uint32_t) * 2 * rows, hipMemcpyHostToDevice,
-                        stream);
-    if (he == hipSuccess) {
-      he = hipStreamSynchronize(stream);
-    }
-    if (he != hipSuccess) {
-      return hip_fail(he, "PUSCH decoder rate-matching arrays");
-    }
-    d->key_plan   = *p;
-    d->key_tbs    = nof_tbs;
-    d->key_stride = llr_stride;
+  he = d->order.begin(stream);
+  if (he == hipSuccess) {
+    he = launch_rm_arrays(d->arrays.as<uint32_t>(), nof_tbs, C, p->nof_short_segments, p->rm_length_short,
+                          p->rm_length_long, llr_stride, stream);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PUSCH decoder rate-matching arrays");
   }
   // 1. Rate dematching + combining.
   srs_amd_codeblock_metadata md{p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
@@ -185,9 +169,13 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   dc.nof_crc_bits    = C > 1 ? p->nof_crc_bits : p->nof_tb_crc_bits;
   dc.max_iterations  = cfg->nof_ldpc_iterations;
   srs_amd_ldpc_decoder* dec = d->dec[cfg->force_decoding ? 1 : 0];
-  rc = srs_amd_ldpc_decode_batch(dec, &dc, cfg->use_early_stop ? crc_poly : SRS_AMD_NO_CRC, d_soft, lay.row_bytes,
-                                 nullptr, llr_prefix(p, lay, cfg->new_data != 0, internal), d->msgs.as<uint8_t>(),
-                                 msg_stride, d->iters.as<int32_t>(), nullptr, rows, stream);
+  // a retransmission does not decode again the codeblocks whose CRC passed earlier (their soft-buffer
+  // flag holds the iteration count of that decoding), pusch_decoder_impl.cpp:330-345
+  const bool skip = !cfg->new_data && !internal;
+  rc = ldpc_decode_batch_ex(dec, &dc, cfg->use_early_stop ? crc_poly : SRS_AMD_NO_CRC, d_soft, lay.row_bytes, nullptr,
+                            llr_prefix(p, lay, cfg->new_data != 0, internal), d->msgs.as<uint8_t>(), msg_stride,
+                            d->iters.as<int32_t>(), nullptr, rows, stream,
+                            skip ? reinterpret_cast<const uint8_t*>(d_soft) + lay.flag_offset : nullptr, lay.row_bytes);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
@@ -218,6 +206,9 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   a.max_iterations = cfg->nof_ldpc_iterations;
   a.new_data       = cfg->new_data ? 1 : 0;
   he               = launch_assemble(a, nof_tbs, stream);
+  if (he == hipSuccess) {
+    he = d->order.end(stream);
+  }
   return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "assemble_kernel launch");
 }
 

@@ -65,6 +65,7 @@ struct srs_amd_pusch_chest {
   float*        d_tw   = nullptr; // twiddle tables of N = 128 .. 4096, back to back
   device_buffer scratch;
   device_buffer host_io;
+  stream_order  order; // scratch reuse across the callers' streams
   std::mutex    mtx;
   ~srs_amd_pusch_chest()
   {
@@ -334,8 +335,8 @@ int srs_amd_pusch_chest_estimate_batch(srs_amd_pusch_chest*              chest,
   std::lock_guard<std::mutex> lock(chest->mtx);
   hipError_t                  e = hipSetDevice(chest->device);
   if (e == hipSuccess) {
-    // One scratch per object: batches on one stream are ordered; a growing
-    // reallocation frees the old block only after the device is idle (hipFree).
+    // One scratch per object: a batch on another stream than the previous one waits for it
+    // (stream_order); a growing reallocation frees the old block only after the device is idle (hipFree).
     e = chest->scratch.ensure(scratch_bytes(a, nof_grids));
   }
   if (e != hipSuccess) {
@@ -355,7 +356,13 @@ int srs_amd_pusch_chest_estimate_batch(srs_amd_pusch_chest*              chest,
   a.stats       = d_stats;
   a.jump        = chest->d_jump;
   a.ta_tw       = chest->tw(a.ta_n);
-  e             = launch_chest(a, nof_grids, static_cast<hipStream_t>(stream));
+  e             = chest->order.begin(static_cast<hipStream_t>(stream));
+  if (e == hipSuccess) {
+    e = launch_chest(a, nof_grids, static_cast<hipStream_t>(stream));
+  }
+  if (e == hipSuccess) {
+    e = chest->order.end(static_cast<hipStream_t>(stream));
+  }
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "channel estimator launch");
 }
 

@@ -29,6 +29,7 @@ struct srs_amd_pusch_demodulator {
   uint32_t*           d_jump = nullptr;
   srs_amd_modulator*  demapper = nullptr;
   device_buffer       scratch;
+  stream_order        order; // scratch reuse across the callers' streams
   device_buffer       host_io;
   std::mutex          mtx;
   ~srs_amd_pusch_demodulator()
@@ -278,14 +279,23 @@ int srs_amd_pusch_demodulate_batch(srs_amd_pusch_demodulator*      dem,
   a.eq_symbols       = reinterpret_cast<float2*>(base);
   a.eq_noise_vars    = reinterpret_cast<float*>(base + align_up(nsym * 8, 256));
   auto    s          = static_cast<hipStream_t>(stream);
-  e = launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->nof_symbols, plan->span_subc, nof_grids, s);
+  e                  = dem->order.begin(s);
+  if (e == hipSuccess) {
+    e = launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->nof_symbols, plan->span_subc, nof_grids, s);
+  }
   if (e != hipSuccess) {
     return hip_fail(e, "pusch_equalize_kernel launch");
   }
   // soft demapper + descrambling (revert_scrambling) in one pass: LLRs straight into the caller's rows
-  return demap_descramble_batch(dem->demapper, plan->qm, d_llrs, llr_stride, reinterpret_cast<const float*>(a.eq_symbols),
-                                a.eq_noise_vars, static_cast<uint32_t>(plan->args.nof_re * plan->nof_layers),
-                                plan->sym_counts, nof_grids, dem->d_jump, plan->c_init, stream);
+  int rc = demap_descramble_batch(dem->demapper, plan->qm, d_llrs, llr_stride,
+                                  reinterpret_cast<const float*>(a.eq_symbols), a.eq_noise_vars,
+                                  static_cast<uint32_t>(plan->args.nof_re * plan->nof_layers), plan->sym_counts,
+                                  nof_grids, dem->d_jump, plan->c_init, stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  e = dem->order.end(s);
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH demodulator completion event");
 }
 
 int srs_amd_pusch_demap_descramble_batch(srs_amd_pusch_demodulator*      dem,

@@ -137,6 +137,7 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
   __shared__ uint32_t s_ok, s_sum, s_min, s_max, s_tb_ok;
   __shared__ uint8_t  s_fresh[SCH_MAX_SEGMENTS]; // decoded in this call (not OK from a previous transmission)
   __shared__ uint8_t  s_cb_ok[SCH_MAX_SEGMENTS];
+  __shared__ uint16_t s_stat[SCH_MAX_SEGMENTS]; // iterations of the freshly decoded codeblocks
   const uint32_t      t = blockIdx.x;
   const uint32_t      C = a.nof_segments;
   if (threadIdx.x == 0) {
@@ -151,15 +152,23 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
   for (uint32_t r = threadIdx.x; r < C; r += ASM_THREADS) {
     const uint32_t cb   = t * C + r;
     const uint8_t* srow = a.soft ? a.soft + static_cast<size_t>(cb) * a.lay.row_bytes : nullptr;
-    const bool     prev = srow && !a.new_data && *reinterpret_cast<const int32_t*>(srow + a.lay.flag_offset) != 0;
+    // the soft-buffer flag of a codeblock OK from an earlier transmission holds that decoding's iteration
+    // count, which the reference's statistics keep for it (cb_stats is not updated, :333-345)
+    const int32_t  flag = srow && !a.new_data ? *reinterpret_cast<const int32_t*>(srow + a.lay.flag_offset) : 0;
+    const bool     prev = flag != 0;
     const int32_t  it   = a.iters[cb];
-    const bool     dec  = a.crc_checks ? (a.crc_checks[cb] == 0) : (it >= 0);
-    const uint32_t stat = dec ? (a.crc_checks ? a.max_iterations : static_cast<uint32_t>(it)) : a.max_iterations;
+    const bool     dec  = !prev && (a.crc_checks ? (a.crc_checks[cb] == 0) : (it >= 0));
+    const uint32_t stat = prev  ? static_cast<uint32_t>(flag)
+                          : dec ? (a.crc_checks ? a.max_iterations : static_cast<uint32_t>(it))
+                                : a.max_iterations;
     const bool     ok   = prev || dec;
     s_fresh[r]          = prev ? 0 : 1;
     s_cb_ok[r]          = ok ? 1 : 0;
     if (a.cb_iterations) {
-      a.cb_iterations[cb] = dec ? static_cast<int32_t>(stat) : -1;
+      a.cb_iterations[cb] = ok ? static_cast<int32_t>(stat) : -1;
+    }
+    if (!prev && a.soft) {
+      s_stat[r] = stat;
     }
     atomicAdd(&s_ok, ok ? 1u : 0u);
     atomicAdd(&s_sum, stat);
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
     for (uint32_t r = threadIdx.x; r < C; r += ASM_THREADS) {
       if (s_fresh[r]) {
         *reinterpret_cast<int32_t*>(a.soft + static_cast<size_t>(t * C + r) * a.lay.row_bytes + a.lay.flag_offset) =
-            s_cb_ok[r];
+            s_cb_ok[r] ? static_cast<int32_t>(s_stat[r]) : 0;
       }
     }
     __syncthreads();
@@ -284,6 +293,26 @@ __global__ __launch_bounds__(64) void asm_final_kernel(assemble_args a, uint32_t
 }
 
 } // namespace
+
+__global__ __launch_bounds__(256) void rm_arrays_kernel(uint32_t* arrays, uint32_t rows, uint32_t C, uint32_t S,
+                                                       uint32_t e_short, uint32_t e_long, uint32_t tb_units)
+{
+  const uint32_t row = blockIdx.x * 256 + threadIdx.x;
+  if (row < rows) {
+    const uint32_t tb = row / C, r = row - tb * C;
+    arrays[row]        = r < S ? e_short : e_long;
+    arrays[rows + row] = tb * tb_units + (r < S ? r * e_short : S * e_short + (r - S) * e_long);
+  }
+}
+
+hipError_t launch_rm_arrays(uint32_t* arrays, uint32_t nof_tbs, uint32_t C, uint32_t nof_short, uint32_t e_short,
+                            uint32_t e_long, uint32_t tb_units, hipStream_t stream)
+{
+  const uint32_t rows = nof_tbs * C;
+  hipLaunchKernelGGL(rm_arrays_kernel, dim3((rows + 255) / 256), dim3(256), 0, stream, arrays, rows, C, nof_short,
+                     e_short, e_long, tb_units);
+  return hipGetLastError();
+}
 
 hipError_t launch_segment(const segment_args& a, hipStream_t stream)
 {

@@ -59,6 +59,11 @@ struct assemble_args {
 };
 
 hipError_t launch_segment(const segment_args& a, hipStream_t stream);
+// Per-codeblock rate-matching lengths and codeword offsets of nof_tbs transport blocks of one plan
+// (srs_amd_sch_plan_segments per TB), written on the device: arrays[row] = E_r, arrays[rows + row] =
+// tb * tb_units + offset_r, row = tb * C + r.  No host upload, so a plan change never blocks the host.
+hipError_t launch_rm_arrays(uint32_t* arrays, uint32_t nof_tbs, uint32_t C, uint32_t nof_short, uint32_t e_short,
+                            uint32_t e_long, uint32_t tb_units, hipStream_t stream);
 hipError_t launch_assemble(const assemble_args& a, uint32_t nof_tbs, hipStream_t stream);
 
 } // namespace srs_amd

@@ -123,6 +123,50 @@ def test_pusch_harq_combining(decs):
     assert r.tb_crc_ok == 1 and np.array_equal(out2, tb)
 
 
+def test_pusch_harq_partial_retransmission(decs):
+    """A retransmission after a partially decoded first transmission: codeblocks whose CRC passed are only
+    rate dematched, not decoded again (pusch_decoder_impl.cpp:330-345); their statistic is the iteration
+    count of the decoding that passed.  TB, CRC verdict, CB CRC count and LDPC statistics vs the oracle."""
+    import torch
+
+    import srsran_project_amd as amd
+
+    tbs_bits, bg, qm, lay, nre = 8 * 4000, 1, 4, 1, 12000
+    tb = tb_bytes(tbs_bits, 7)
+    dec = decs["simd"]
+    p0, op0 = _plan((tbs_bits, bg, qm, lay, nre, 0, 0))
+    p2, op2 = _plan((tbs_bits, bg, qm, lay, nre, 2, 0))
+    C = p0.nof_segments
+    assert C >= 3
+    E, off = amd.sch_segments(p0)
+    soft = torch.zeros(amd.soft_buffer_size(p0), dtype=torch.int8, device="cuda")
+    h = osch.HarqBuffer(op0)
+    out = np.zeros(tbs_bits // 8, np.uint8)
+    d_tb = torch.zeros((1, tbs_bits // 8), dtype=torch.uint8, device="cuda")
+    cb_it = torch.zeros(C, dtype=torch.int32, device="cuda")
+    for k, (p, op, new) in enumerate(((p0, op0, True), (p0, op0, False), (p2, op2, False))):
+        llr = noisy_llrs(osch.pdsch_encode(tb, op), 8, 3, seed=10 + k)
+        if k == 0:  # codeblock 1 lost in the first transmission
+            llr[off[1]:off[1] + E[1]] = 0
+        ok, iters, stats = osch.pusch_decode(llr, op, h, out, 6, "simd", new_data=new)
+        _, res = dec.decode_batch(torch.from_numpy(llr[None]).cuda(), p, amd.PuschDecoder.config(new_data=new),
+                                  tbs=d_tb, soft=soft, cb_iterations=cb_it)
+        torch.cuda.synchronize()
+        res = res.cpu().numpy()
+        msg = "transmission %d" % k
+        assert bool(res[0, 0]) == ok, msg
+        assert res[0, 2] == sum(stats) and res[0, 3] == min(stats) and res[0, 4] == max(stats), (msg, res[0], stats)
+        assert res[0, 5] == sum(h.crc), msg
+        got = cb_it.cpu().numpy()
+        for i in range(C):
+            want = iters[i] if iters[i] is not None else (h.its[i] if h.crc[i] else -1)
+            assert got[i] == want, (msg, i, got, iters)
+        if k == 0:
+            assert not ok and iters[1] is None and all(iters[i] is not None for i in range(C) if i != 1)
+        np.testing.assert_array_equal(d_tb[0].cpu().numpy(), out, err_msg=msg)
+    assert ok and np.array_equal(out, tb)
+
+
 def test_pipeline_slot_roundtrip(enc, decs):
     """configs[3] transport block (273 PRB, 14 symbols with 2 DM-RS, 2 layers,
     256QAM MCS 27, R = 948/1024, TBS 590128): 8 TBs encoded and decoded back
