@@ -70,9 +70,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample duration")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--snr-db", type=float, default=35.0, help="pipeline: PUSCH SNR of the headline line")
-    p.add_argument("--low-snr-db", type=float, default=23.8,
+    p.add_argument("--low-snr-db", type=float, default=None,
                    help="pipeline: also report a line at this SNR, near the 256QAM R=0.93 decoding threshold where "
-                        "the decoder runs ~4-5 iterations per codeblock (tools/snr_sweep.py; < 0 disables)")
+                        "the decoder runs ~4 iterations per codeblock (default per PUSCH layers, from "
+                        "tools/snr_sweep.py: 31.0 dB for 4 layers, 23.8 dB for 2; < 0 disables)")
+    p.add_argument("--ul-layers", type=int, default=4, choices=[1, 2, 3, 4],
+                   help="pipeline: PUSCH layers (4: MMSE 4x4, parity unpinned; 2: the reference-pinned ZF 2x4)")
     p.add_argument("--ingest", action="store_true",
                    help="pipeline, N > 1: rank 0 holds all cells' slot inputs; RCCL scatter / gather every step")
     p.add_argument("--no-latency", action="store_true", help="pipeline: skip the 1 / 8 cell latency figures")

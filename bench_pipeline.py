@@ -7,7 +7,9 @@ Per slot (= one cell; `--slots-pipeline` cells per step and rank, all resident i
          transport block -> pdsch_encoder (CRC, segmentation, LDPC, rate matching)
          -> pdsch_modulator (scrambling, modulation, layer mapping, precoding, RE mapping)
          -> dmrs_pdsch_processor (DM-RS +3 dB, 2 CDM groups without data) -> OFDM modulator.
-  PUSCH  (gNB RX, UL_LAYERS layers x 4 rx ports, 256QAM R = 948/1024, 273 PRB, symbols 0-13)
+  PUSCH  (gNB RX, UL_LAYERS layers x 4 rx ports, 256QAM R = 948/1024, 273 PRB, symbols 0-13; 4 layers with the
+         MMSE 4 x 4 solve by default -- the open reference's equalizer asserts for 4 layers, so that stage is
+         parity unpinned; --ul-layers 2 runs the reference-pinned ZF 2 x 4 chain)
          baseband -> OFDM demodulator -> pusch_processor (the C-ABI PUSCH processor:
          DM-RS estimator -> demodulator -> UL-SCH decoder with CRC early stop), configured as
          the reference pusch_processor_impl (DM-RS scaling from the CDM groups, Nref from
@@ -29,13 +31,15 @@ import numpy as np
 NPRB, NSUBC, MU, NFFT = 273, 273 * 12, 1, 4096
 QM, RATE = 8, 948.0  # 256QAM, target code rate x 1024 (MCS 27 of the 256QAM table)
 DL_LAYERS, DL_PORTS = 4, 4
-UL_LAYERS, UL_PORTS = 2, 4
+UL_LAYERS, UL_PORTS, UL_EQ = 4, 4, "mmse"
 DMRS_MASK = (1 << 2) | (1 << 11)
 NCDM = 2
 DL_START, DL_NSYM = 1, 13
 UL_START, UL_NSYM = 0, 14
 RNTI, N_ID, SLOT = 0x4601, 500, 0
 SNR_DB = 35.0
+# near the decoding threshold (tools/snr_sweep.py, mean LDPC iterations ~4): per PUSCH layer count
+LOW_SNR_DB = {2: 23.8, 4: 31.0}
 LDPC_ITERS = 6
 # DM-RS amplitude relative to data: convert_dB_to_amplitude(-get_sch_to_dmrs_ratio_dB(2)) = 10^(3/20),
 # evaluated in float as the reference (sch_dmrs_power.h, math_utils.h:118)
@@ -77,13 +81,15 @@ def ul_pdu(amd, layers, tbs):
 
 
 class Pipeline:
-    def __init__(self, slots, dev, iters=LDPC_ITERS, snr_db=SNR_DB, ul_layers=UL_LAYERS, seed=0):
+    def __init__(self, slots, dev, iters=LDPC_ITERS, snr_db=SNR_DB, ul_layers=UL_LAYERS, seed=0, ul_equalizer=None):
         import torch
 
         import srsran_project_amd as amd
 
         self.torch, self.dev, self.S = torch, dev, slots
         self.ul_layers, self.snr_db, self.iters = ul_layers, snr_db, iters
+        # the reference-pinned ZF for two layers, MMSE (parity unpinned) for four unless asked otherwise
+        self.ul_equalizer = ul_equalizer or ("zf" if ul_layers <= 2 else UL_EQ)
         self.ul_stream = None
         d = dev.index
         all_crbs = list(range(NPRB))
@@ -109,9 +115,10 @@ class Pipeline:
                                               device=d)
         self.ofdm_dem = amd.OfdmSlotDemodulator(
             amd.OfdmDemodulatorConfiguration(MU, NPRB, NFFT, 0, 1.0, 3.5e9, 0), device=d)
-        self.proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=iters, dec_enable_early_stop=True,
-                                                                fd_smoothing=2, td_interpolation=0,
-                                                                compensate_cfo=True), device=d)
+        self.proc = amd.PuschProcessor(amd.PuschProcessorConfig(
+            dec_nof_iterations=iters, dec_enable_early_stop=True, fd_smoothing=2, td_interpolation=0,
+            compensate_cfo=True, equalizer=int(getattr(amd.ChannelEqualizerAlgorithmType, self.ul_equalizer))),
+            device=d)
         self.pdu_ul = ul_pdu(amd, ul_layers, self.tbs_ul)
         self.proc_plan = self.proc.plan(self.pdu_ul, NSUBC)
         self.plan_ul = self.proc_plan.sch  # the processor's UL-SCH plan (Nref from tbs_lbrm_default)
@@ -289,11 +296,11 @@ def chain_config(pl, choice="auto"):
                           ul_target_code_rate=RATE, choice={"generic": 0, "avx2": 1, "auto": 2}[choice])
 
 
-def latency_ms(dev, cells, steps=10, warmup=3):
+def latency_ms(dev, cells, steps=10, warmup=3, ul_layers=UL_LAYERS):
     """Wall time of one step (both chains of `cells` cells) measured step by step (synchronized each step)."""
     import torch
 
-    pl = Pipeline(cells, dev)
+    pl = Pipeline(cells, dev, ul_layers=ul_layers)
     stream = torch.cuda.current_stream(dev)
     for _ in range(warmup):
         pl.step(stream)
@@ -313,7 +320,7 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
     from srsran_project_amd.cell_fanout import SlotFanout
 
     stream = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
-    pl = Pipeline(args.slots_pipeline, dev, snr_db=args.snr_db)
+    pl = Pipeline(args.slots_pipeline, dev, snr_db=args.snr_db, ul_layers=args.ul_layers)
     S = pl.S
     ingest_ms = None
     if args.ingest and world > 1:
@@ -370,9 +377,11 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         return None
     lat = None
     if world == 1 and not args.no_latency:
-        lat = {"1_cell": latency_ms(dev, 1), "8_cells": latency_ms(dev, 8)}
+        lat = {"1_cell": latency_ms(dev, 1, ul_layers=L), "8_cells": latency_ms(dev, 8, ul_layers=L)}
     low = None
-    if world == 1 and args.low_snr_db is not None and args.low_snr_db >= 0:
+    if args.low_snr_db is None:
+        args.low_snr_db = LOW_SNR_DB.get(L, -1.0)
+    if world == 1 and args.low_snr_db >= 0:
         low = low_snr_line(args, dev, timed, dist)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -397,6 +406,10 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
             "cells_per_step_per_gpu": S,
             "pdsch": {"layers": DL_LAYERS, "ports": DL_PORTS, "tbs": pl.tbs_dl, "codeblocks": cbs_dl},
             "pusch": {"layers": L, "rx_ports": UL_PORTS, "tbs": pl.tbs_ul, "codeblocks": cbs_ul,
+                      "equalizer": pl.ul_equalizer,
+                      "equalizer_parity": "pinned (reference ZF)" if (L <= 2 and pl.ul_equalizer == "zf") or L == 1
+                      else "unpinned: the open reference asserts for this topology; fp64 solve within stated "
+                           "tolerance (tests/test_equalizer_mimo_gpu.py)",
                       "ldpc_max_iterations": pl.iters, "early_stop": True},
             "parallelism": ("cells sharded over ranks" + (", slot ingest scatter/gather over RCCL"
                                                            if ingest_ms is not None else "")) if world > 1
@@ -451,7 +464,7 @@ def low_snr_line(args, dev, timed, dist):
     iterations per codeblock (the headline runs at 35 dB, ~2 iterations)."""
     import torch
 
-    pl = Pipeline(args.slots_pipeline, dev, snr_db=args.low_snr_db, seed=1)
+    pl = Pipeline(args.slots_pipeline, dev, snr_db=args.low_snr_db, seed=1, ul_layers=args.ul_layers)
     stream = torch.cuda.current_stream(dev)
     elapsed, _ = timed(args, dist, 1, dev, stream, lambda: pl.step(stream))
     ok, its = pl.check()
@@ -477,14 +490,18 @@ def pipeline_cpu_baseline(args, pl):
         return {"value": None, "unit": "codeblocks/s", "error": "oracle/_ref not built"}
     import os
 
-    cfg = chain_config(pl)
-    tb = pl.tb_dl[0].cpu().numpy()
+    # The open reference's PUSCH processor runs at most two layers (its equalizer asserts for 3 / 4,
+    # channel_equalizer_generic_impl.cpp:197-247): for a 4-layer GPU line the CPU chain processes the same cell
+    # with a 2-layer PUSCH (inputs from a 1-cell 2-layer pipeline); codeblocks/s is normalised per codeblock.
+    ref_pl = pl if pl.ul_layers <= 2 else Pipeline(1, pl.dev, snr_db=pl.snr_db, ul_layers=2)
+    cfg = chain_config(ref_pl)
+    tb = ref_pl.tb_dl[0].cpu().numpy()
     n = oc.slot_size(cfg)
-    samp = np.ascontiguousarray(pl.samp_ul[0, :, :n].cpu().numpy())
+    samp = np.ascontiguousarray(ref_pl.samp_ul[0, :, :n].cpu().numpy())
     logical, physical = oc.host_cores()
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or logical
     threads = max(1, min(physical, share, args.cpu_threads))
-    cbs = pl.plan_dl.nof_segments + pl.plan_ul.nof_segments
+    cbs = ref_pl.plan_dl.nof_segments + ref_pl.plan_ul.nof_segments
     # single thread: per-stage breakdown
     w1, st1, ok1, _ = oc.many(cfg, tb, samp, 2, 1)
     n1 = max(2, int(args.cpu_seconds / 4 / max(w1 / 2, 1e-6)))
@@ -503,6 +520,11 @@ def pipeline_cpu_baseline(args, pl):
                       "dmrs_pdsch_processor_impl, ofdm_slot_modulator_impl / ofdm_slot_demodulator_impl, "
                       "pusch_processor_impl (dmrs_pusch_estimator_impl, pusch_demodulator_impl, "
                       "ulsch_demultiplex_impl, pusch_decoder_impl) with the \"auto\" factory implementations "
-                      "(%s); PUSCH TB CRC ok in %d of %d slots"
-                      % (nmt, threads, wm, n1, w1, opp.describe("auto"), okm, nmt),
+                      "(%s); PUSCH TB CRC ok in %d of %d slots; per cell PDSCH 4 layers x 4 ports and PUSCH "
+                      "%d layers x 4 rx (%d codeblocks)%s"
+                      % (nmt, threads, wm, n1, w1, opp.describe("auto"), okm, nmt, ref_pl.ul_layers, cbs,
+                         "" if ref_pl is pl else "; the open reference cannot run the GPU line's %d-layer PUSCH "
+                         "(its equalizer asserts), so its chain runs the 2-layer PUSCH of the same cell"
+                         % pl.ul_layers),
+            "pusch_layers": ref_pl.ul_layers,
             "stage_s_per_slot": {k: v / n1 for k, v in st1.items()}}

@@ -14,9 +14,13 @@
  *                                   noise_var_estimates, tx_scaling)   channel_equalizer.h:89
  *   srs_amd_channel_equalize_batch: the same on device buffers, asynchronous.
  *
- * Supported as the open-source reference (channel_equalizer_generic_impl.cpp:240-270):
- * ZF 1 layer x {1, 2, 4} ports, ZF 2 layers x {2, 4} ports, MMSE 1 layer (equal
- * to ZF there).  Layouts (the reference containers):
+ * Supported: the open-source reference's topologies (channel_equalizer_generic_impl.cpp:240-270,
+ * pinned): ZF 1 layer x {1, 2, 4} ports, ZF 2 layers x {2, 4} ports, MMSE 1 layer (equal to ZF
+ * there); and the ones the open reference declares but asserts for (:197-247, the enterprise
+ * build's equalize_zf_3x4 / 4x4, equalize_mmse_2x2 / 2x4 / 3x4 / 4x4), PARITY UNPINNED: an L x L
+ * Cholesky solve per RE of ZF or the unbiased MMSE estimate (equalizer_device.h equalize_mimo),
+ * checked against an fp64 solve (tests/test_equalizer_mimo_gpu.py, tolerance stated there).
+ * Layouts (the reference containers):
  *   ch_symbols   : cbf16 [port][nof_re]            (re_buffer_reader<cbf16_t> slices)
  *   ch_estimates : cbf16 [layer][port][nof_re]     (dynamic_ch_est_list.h dims {re, port, layer})
  *   eq_symbols   : complex float [nof_re][layer];  eq_noise_vars: float [nof_re][layer]

@@ -11,8 +11,9 @@
  *       (impl lib/phy/upper/channel_processors/pusch/pusch_demodulator_impl.cpp:203-330)
  *
  * Scope: no transform precoding, no UCI multiplexing (the codeword is all
- * UL-SCH), equalizers of the open-source reference (ZF 1 layer x {1,2,4} ports,
- * ZF 2 layers x {2,4} ports, MMSE 1 layer). The post-equalization SINR / EVM
+ * UL-SCH), the equalizers of equalizer.h: the open-source reference's (ZF 1 layer x
+ * {1,2,4} ports, ZF 2 layers x {2,4} ports, MMSE 1 layer) and the L-layer ZF 3x4 / 4x4 and
+ * MMSE 2x2 / 2x4 / 3x4 / 4x4 solves (parity unpinned). The post-equalization SINR / EVM
  * statistics are not produced.
  * Inputs per grid: the received grid cbf16 [port][14][subc], the channel
  * estimates cbf16 [port][layer][14][subc] and per-port measurements
@@ -47,7 +48,7 @@ typedef struct srs_amd_pusch_demod_config {
   uint32_t dmrs_symbol_mask;           /* dmrs_symb_pos */
   uint32_t dmrs_type;                  /* 1 or 2 */
   uint32_t nof_cdm_groups_without_data;
-  uint32_t nof_tx_layers;              /* 1 or 2 */
+  uint32_t nof_tx_layers;              /* 1 to 4 (no more than nof_rx_ports) */
   uint32_t nof_rx_ports;               /* 1, 2 or 4 */
   int32_t  equalizer;                  /* SRS_AMD_EQ_ZF or SRS_AMD_EQ_MMSE */
 } srs_amd_pusch_demod_config;

@@ -77,6 +77,83 @@ def equalize(symbols_u16, est_u16, noise_vars, tx_scaling, nof_layers):
     return eq, out_nv
 
 
+PIVOT_REL = 2.0 ** -20  # equalizer_device.h: a Cholesky pivot below 2^-20 x its diagonal entry is singular
+
+
+def is_supported_mimo(algorithm, nof_ports, nof_layers):
+    """Topologies of the MI355X equalizer: the reference's (is_supported) plus the L-layer solves the open
+    reference asserts for (ZF 3x4 / 4x4, MMSE 2xN / 3x4 / 4x4, channel_equalizer_generic_impl.cpp:197-247)."""
+    return nof_ports in (1, 2, 4) and 1 <= nof_layers <= min(4, nof_ports) and algorithm in ("zf", "mmse")
+
+
+def equalize_mimo(symbols_u16, est_u16, noise_vars, tx_scaling, nof_layers, algorithm):
+    """fp64 restatement of equalizer_device.h equalize_mimo -- PARITY UNPINNED (no open reference): y = ts H x + n,
+    sigma^2 = the largest port noise variance (channel_equalizer_generic_impl.cpp:304).
+      zf:   x = (H^H H)^-1 H^H y / ts, nv_l = sigma^2 [(H^H H)^-1]_ll / ts^2
+      mmse: A = ts^2 H^H H + sigma^2 I, u = A^-1 ts H^H y, d = diag(A^-1), mu = 1 - sigma^2 d,
+            x = u / mu, nv = sigma^2 d / mu (unbiased MMSE; equal to ZF for one layer).
+    Invalid sigma^2 (not a positive normal number for MMSE, not normal and >= 0 for ZF), a Gram / A matrix with a
+    Cholesky pivot not above 2^-20 times its diagonal entry (singular in float32 terms): zero symbols and
+    infinite variances; likewise mu_l <= 2^-20 (no signal on the layer).
+    Returns (eq complex128 [R, L], nv float64 [R, L], kappa [R]: condition number of the solve, x 1/min(mu) for
+    MMSE -- the float32 error amplification the GPU tolerance scales with)."""
+    y = cbf16_to_complex(symbols_u16)           # [P, R]
+    h = cbf16_to_complex(est_u16)               # [L, P, R]
+    P, R = y.shape
+    L = nof_layers
+    eq = np.zeros((R, L), np.complex128)
+    out_nv = np.full((R, L), np.inf)
+    kappa = np.ones(R)
+    sigma = float(np.max(np.asarray(noise_vars, np.float64)))
+    mmse = algorithm == "mmse"
+    noise_ok = _isnormal(sigma) and (sigma > 0 if mmse else sigma >= 0)
+    if not noise_ok:
+        return eq, out_nv, kappa
+    H = np.transpose(h, (2, 1, 0))              # [R, P, L]
+    G = np.einsum("rpi,rpk->rik", np.conj(H), H)
+    b = np.einsum("rpi,rp->ri", np.conj(H), y.T)
+    ts = float(tx_scaling)
+    A = ts * ts * G + sigma * np.eye(L) if mmse else G
+    rhs = ts * b if mmse else b
+    finite = np.all(np.isfinite(A.reshape(R, -1)), axis=1)
+    A_ok = np.where(finite[:, None, None], A, np.eye(L))
+    # positive definiteness as the Cholesky pivots see it
+    def _chol_ok(M):
+        # the GPU's singularity rule: every Cholesky pivot a normal number above 2^-20 times its diagonal entry
+        C = np.linalg.cholesky(M)
+        piv = np.real(np.diagonal(C, axis1=-2, axis2=-1)) ** 2
+        diag = np.real(np.diagonal(M, axis1=-2, axis2=-1))
+        return np.all(_isnormal(piv) & (piv > PIVOT_REL * diag), axis=-1)
+
+    try:
+        good = finite & _chol_ok(A_ok)
+    except np.linalg.LinAlgError:  # some RE is not positive definite: decide RE by RE
+        good = np.zeros(R, bool)
+        for r in np.nonzero(finite)[0]:
+            try:
+                good[r] = bool(_chol_ok(A_ok[r]))
+            except np.linalg.LinAlgError:
+                good[r] = False
+    A_ok = np.where(good[:, None, None], A_ok, np.eye(L))
+    Ainv = np.linalg.inv(A_ok)
+    u = np.einsum("rik,rk->ri", Ainv, rhs)
+    d = np.real(np.diagonal(Ainv, axis1=1, axis2=2))
+    kappa = np.where(good, np.linalg.cond(A_ok), 1.0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        if mmse:
+            mu = 1.0 - sigma * d
+            good = good & np.all(mu > PIVOT_REL, axis=1)  # mu_l (SINR / (1 + SINR)) above 2^-20, as the GPU
+            x = u / mu
+            nv = sigma * d / mu
+            kappa = kappa / np.clip(np.min(mu, axis=1), 1e-30, None)
+        else:
+            x = u / ts
+            nv = sigma * d / (ts * ts)
+    eq[good] = x[good]
+    out_nv[good] = nv[good]
+    return eq, out_nv, np.where(good, kappa, 1.0)
+
+
 def random_channel(rng, nof_re, nof_ports, nof_layers, snr_db=20.0):
     """Rayleigh channel, QPSK per layer, AWGN: returns (symbols uint16 [P, 2R], est uint16
     [L, P, 2R], noise_var float32 [P], tx complex [R, L])."""

@@ -19,7 +19,7 @@ import ctypes as _c
 import numpy as np
 
 from . import REF, _ptr, demodulate, prbs
-from .equalizer import equalize
+from .equalizer import equalize, equalize_mimo
 from .pdsch_mod import dmrs_prb_mask
 
 
@@ -45,7 +45,11 @@ def pusch_demodulate(grid, estimates, noise_vars, rnti, n_id, qm, crbs, start_sy
     ls, ks = np.nonzero(mask)
     sym = np.ascontiguousarray(grid[:, ls, ks]).view(np.uint16)                       # [P][2*nre]
     est = np.ascontiguousarray(np.transpose(estimates[:, :, ls, ks], (1, 0, 2))).view(np.uint16)  # [L][P][2*nre]
-    eq, nv = equalize(sym, est, noise_vars, 1.0, nof_layers)  # MMSE with one layer is ZF (channel_equalizer_generic_impl.cpp:348)
+    if nof_layers >= 3 or (mmse and nof_layers == 2):
+        # the L-layer solves the open reference does not implement (parity unpinned, fp64)
+        eq, nv, _ = equalize_mimo(sym, est, noise_vars, 1.0, nof_layers, "mmse" if mmse else "zf")
+    else:
+        eq, nv = equalize(sym, est, noise_vars, 1.0, nof_layers)  # MMSE with one layer is ZF (channel_equalizer_generic_impl.cpp:348)
     eq = eq.reshape(-1).astype(np.complex64)
     nv = nv.reshape(-1).astype(np.float32)
     # one demapper call per OFDM symbol (its SIMD blocks end at the symbol's last RE)

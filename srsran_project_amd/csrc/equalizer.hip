@@ -60,6 +60,33 @@ __global__ __launch_bounds__(256) void equalize_2xn_kernel(equalizer_args a)
   }
 }
 
+// L-layer ZF / MMSE (equalize_mimo): estimates [layer][port][re], outputs [re][layer].
+template <int P, int L, bool MMSE>
+__global__ __launch_bounds__(256) void equalize_mimo_kernel(equalizer_args a)
+{
+  const uint32_t* sym = static_cast<const uint32_t*>(a.symbols);
+  const uint32_t* est = static_cast<const uint32_t*>(a.estimates);
+  for (uint32_t re = blockIdx.x * 256 + threadIdx.x; re < a.nof_re; re += gridDim.x * 256) {
+    cplx y[P], h[P * L];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      y[p] = from_cbf16(sym[p * a.nof_re + re]);
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        h[p * L + l] = from_cbf16(est[(l * P + p) * a.nof_re + re]);
+      }
+    }
+    cplx  out[L];
+    float nv[L];
+    eq::equalize_mimo<P, L, MMSE>(y, h, a.noise_var, a.noise_ok != 0, a.tx_scaling, out, nv);
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      reinterpret_cast<float2*>(a.eq_symbols)[static_cast<uint64_t>(re) * L + l] = make_float2(out[l].x, out[l].y);
+      a.eq_noise_vars[static_cast<uint64_t>(re) * L + l]                         = nv[l];
+    }
+  }
+}
+
 } // namespace
 
 hipError_t launch_equalizer(const equalizer_args& a, uint32_t nof_ports, uint32_t nof_layers, hipStream_t stream)
@@ -83,7 +110,7 @@ hipError_t launch_equalizer(const equalizer_args& a, uint32_t nof_ports, uint32_
       default:
         return hipErrorInvalidValue;
     }
-  } else if (nof_layers == 2) {
+  } else if (nof_layers == 2 && !a.mmse) {
     switch (nof_ports) {
       case 2:
         hipLaunchKernelGGL(equalize_2xn_kernel<2>, dim3(blocks), dim3(256), 0, stream, a);
@@ -95,6 +122,18 @@ hipError_t launch_equalizer(const equalizer_args& a, uint32_t nof_ports, uint32_
         return hipErrorInvalidValue;
     }
   } else {
+#define SRS_MIMO_CASE(PP, LL, MM)                                                                                     \
+  if (nof_ports == PP && nof_layers == LL && (a.mmse != 0) == MM) {                                                   \
+    hipLaunchKernelGGL((equalize_mimo_kernel<PP, LL, MM>), dim3(blocks), dim3(256), 0, stream, a);                   \
+    return hipGetLastError();                                                                                         \
+  }
+    SRS_MIMO_CASE(2, 2, true)
+    SRS_MIMO_CASE(4, 2, true)
+    SRS_MIMO_CASE(4, 3, false)
+    SRS_MIMO_CASE(4, 3, true)
+    SRS_MIMO_CASE(4, 4, false)
+    SRS_MIMO_CASE(4, 4, true)
+#undef SRS_MIMO_CASE
     return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -44,10 +44,10 @@ bool supported(int algorithm, uint32_t nof_ports, uint32_t nof_layers)
   if (nof_ports < nof_layers) {
     return false;
   }
-  if (algorithm == SRS_AMD_EQ_ZF) {
-    return nof_layers >= 1 && nof_layers <= 2;
-  }
-  return nof_layers == 1;
+  // channel_equalizer_generic_impl.cpp:240-270 allows ZF for 1-2 layers and MMSE for 1; the L-layer
+  // solves of equalizer_device.h add ZF 3 x 4 / 4 x 4 and MMSE 2 x N / 3 x 4 / 4 x 4 (parity unpinned:
+  // the open reference asserts for them, channel_equalizer_generic_impl.cpp:197-247).
+  return nof_layers >= 1 && nof_layers <= 4 && (algorithm == SRS_AMD_EQ_ZF || algorithm == SRS_AMD_EQ_MMSE);
 }
 
 int make_args(equalizer_args& a, const srs_amd_channel_equalizer* eq, const float* nvars, uint32_t nof_re,
@@ -76,6 +76,7 @@ int make_args(equalizer_args& a, const srs_amd_channel_equalizer* eq, const floa
   }
   a.noise_var = *std::max_element(nvars, nvars + nof_ports);
   a.noise_ok  = (std::isnormal(a.noise_var) && a.noise_var >= 0.0F) ? 1 : 0;
+  a.mmse      = eq->algorithm == SRS_AMD_EQ_MMSE ? 1 : 0;
   return SRS_AMD_OK;
 }
 

@@ -22,6 +22,7 @@ struct equalizer_args {
   // 2 layers: the largest per-port variance (channel_equalizer_generic_impl.cpp:304)
   float       noise_var;
   int32_t     noise_ok;       // isnormal(noise_var) && noise_var >= 0 (equalize_zf_2xn.h:57)
+  int32_t     mmse;           // SRS_AMD_EQ_MMSE (L >= 2: the unbiased MMSE solve of equalizer_device.h)
 };
 
 hipError_t launch_equalizer(const equalizer_args& a, uint32_t nof_ports, uint32_t nof_layers, hipStream_t stream);

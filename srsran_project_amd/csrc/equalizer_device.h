@@ -124,5 +124,158 @@ __device__ __forceinline__ void equalize_2xn(const cplx* y,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// L-layer solves the open reference does not implement (channel_equalizer_generic_impl.cpp:197-247
+// asserts for ZF 3x4 / 4x4 and MMSE 2x2 / 2x4 / 3x4 / 4x4): parity unpinned, checked against an
+// fp64 solve of the same model (oracle/equalizer.py equalize_mimo).  Model and scaling follow the
+// reference's ZF equalizers: y = tx_scaling H x + n, the largest port noise variance sigma^2.
+//   ZF:   x = (H^H H)^-1 H^H y / ts,               nv_l = sigma^2 [(H^H H)^-1]_ll / ts^2
+//         (equalize_zf_2xn.h for L = 2, generalised);
+//   MMSE: A = ts^2 H^H H + sigma^2 I, u = A^-1 ts H^H y, d_l = [A^-1]_ll, mu_l = 1 - sigma^2 d_l,
+//         x_l = u_l / mu_l, nv_l = sigma^2 d_l / mu_l  -- the unbiased MMSE estimate, which for one
+//         layer is exactly the ZF one (channel_equalizer_generic_impl.cpp:343).
+// One RE per thread in registers: Gram matrix and matched filter (P L (L+3)/2 complex MACs), an
+// L x L complex Cholesky factorisation, forward / backward substitution and the diagonal of the
+// inverse from L^-1 -- a few hundred FLOPs against 4 P (L + 1) + 12 L bytes of HBM traffic per RE,
+// so the kernel stays HBM-bound and matrix cores would not shorten it.  A Cholesky pivot that is
+// not a normal number above 2^-20 times its diagonal entry (a singular channel in float32 terms),
+// an invalid sigma^2 or mu_l <= 2^-20 gives zero symbols with infinite variances for the RE, as the
+// reference does for abnormal 2 x N inputs.
+template <int P, int L, bool MMSE>
+__device__ __forceinline__ void equalize_mimo(const cplx* y,  // [P]
+                                              const cplx* h,  // [P][L]
+                                              float       noise_var,
+                                              bool        noise_ok,
+                                              float       tx_scaling,
+                                              cplx*       out, // [L]
+                                              float*      nv)  // [L]
+{
+  // A (lower triangle, row i >= column k) and the right-hand side
+  cplx a[L][L];
+  cplx b[L];
+  const float ga = MMSE ? tx_scaling * tx_scaling : 1.0f;
+  const float gb = MMSE ? tx_scaling : 1.0f;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+#pragma unroll
+    for (int k = 0; k <= i; ++k) {
+      cplx acc = {0.0f, 0.0f};
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const cplx t = mul_conj(h[p * L + k], h[p * L + i]); // (H^H H)_{i,k} = sum_p conj(H_pi) H_pk
+        acc.x += t.x;
+        acc.y += t.y;
+      }
+      a[i][k] = {acc.x * ga, acc.y * ga};
+    }
+    a[i][i].y = 0.0f;
+    if (MMSE) {
+      a[i][i].x += noise_var;
+    }
+    cplx acc = {0.0f, 0.0f};
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const cplx t = mul_conj(y[p], h[p * L + i]); // conj(h_i) y
+      acc.x += t.x;
+      acc.y += t.y;
+    }
+    b[i] = {acc.x * gb, acc.y * gb};
+  }
+  // Cholesky A = C C^H (C lower, real diagonal), kept in a[][]; r[k] = 1 / C_kk
+  float r[L];
+  bool  ok = noise_ok && (!MMSE || noise_var > 0.0f);
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    float d = a[k][k].x;
+#pragma unroll
+    for (int j = 0; j < k; ++j) {
+      d -= norm(a[k][j]);
+    }
+    // singular in float terms: a pivot below 2^-20 of its diagonal entry (or not a positive normal number)
+    ok            = ok && __builtin_isnormal(d) && d > 0x1p-20f * a[k][k].x;
+    const float c = __builtin_sqrtf(d);
+    r[k]          = 1.0f / c;
+#pragma unroll
+    for (int i = k + 1; i < L; ++i) {
+      cplx s = a[i][k];
+#pragma unroll
+      for (int j = 0; j < k; ++j) {
+        const cplx t = mul_conj(a[i][j], a[k][j]); // C_ij conj(C_kj)
+        s.x -= t.x;
+        s.y -= t.y;
+      }
+      a[i][k] = {s.x * r[k], s.y * r[k]};
+    }
+  }
+  // z = C^-1 b, then x = C^-H z
+  cplx z[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    cplx s = b[k];
+#pragma unroll
+    for (int j = 0; j < k; ++j) {
+      const cplx t = cmul(a[k][j], z[j]);
+      s.x -= t.x;
+      s.y -= t.y;
+    }
+    z[k] = {s.x * r[k], s.y * r[k]};
+  }
+  cplx x[L];
+#pragma unroll
+  for (int k = L - 1; k >= 0; --k) {
+    cplx s = z[k];
+#pragma unroll
+    for (int j = k + 1; j < L; ++j) {
+      const cplx t = mul_conj(x[j], a[j][k]); // conj(C_jk) x_j
+      s.x -= t.x;
+      s.y -= t.y;
+    }
+    x[k] = {s.x * r[k], s.y * r[k]};
+  }
+  // diag(A^-1) = column norms of W = C^-1 (lower): W_kk = r_k, W_ik = -r_i sum_{j=k}^{i-1} C_ij W_jk
+  float dinv[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    cplx w[L];
+    w[k]      = {r[k], 0.0f};
+    float acc = r[k] * r[k];
+#pragma unroll
+    for (int i = k + 1; i < L; ++i) {
+      cplx s = {0.0f, 0.0f};
+#pragma unroll
+      for (int j = k; j < i; ++j) {
+        const cplx t = cmul(a[i][j], w[j]);
+        s.x += t.x;
+        s.y += t.y;
+      }
+      w[i] = {-s.x * r[i], -s.y * r[i]};
+      acc += norm(w[i]);
+    }
+    dinv[k] = acc;
+  }
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    if (MMSE) {
+      const float mu = 1.0f - noise_var * dinv[l];
+      // mu_l = SINR / (1 + SINR) of the layer: below 2^-20 (no signal) the RE is abnormal
+      ok             = ok && __builtin_isnormal(mu) && mu > 0x1p-20f;
+      const float rm = 1.0f / mu;
+      out[l]         = {x[l].x * rm, x[l].y * rm};
+      nv[l]          = noise_var * dinv[l] * rm;
+    } else {
+      const float rt = 1.0f / tx_scaling;
+      out[l]         = {x[l].x * rt, x[l].y * rt};
+      nv[l]          = noise_var * dinv[l] * rt * rt;
+    }
+  }
+  if (!ok) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      out[l] = {0.0f, 0.0f};
+      nv[l]  = __builtin_inff();
+    }
+  }
+}
+
 } // namespace eq
 } // namespace srs_amd

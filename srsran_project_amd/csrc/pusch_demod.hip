@@ -8,7 +8,9 @@
 // coefficients straight from the grid and the estimate tensor (the reference
 // copies both into temporary buffers first, get_ch_data_re /
 // get_ch_data_estimates) and equalizes with the shared ZF math
-// (equalizer_device.h), writing [j][layer] symbols and variances.
+// (equalizer_device.h: the reference's ZF 1 x N / 2 x N, or the L-layer Cholesky solve for the
+// ZF 3 x 4 / 4 x 4 and MMSE 2 x N / 3 x 4 / 4 x 4 cases the open reference does not implement),
+// writing [j][layer] symbols and variances.
 // The per-port noise variances come from the DM-RS estimator's measurements
 // on the device, so the chain needs no host round trip.
 // The soft demapper and revert_scrambling (pusch_demodulator_impl.cpp:36-190) run fused in
@@ -21,7 +23,7 @@
 namespace srs_amd {
 namespace {
 
-template <int P, int L>
+template <int P, int L, bool MMSE>
 __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
 {
   const uint32_t  l   = a.first_symbol + blockIdx.y;
@@ -42,17 +44,22 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
   const srs_amd_chest_port_stats* st = a.stats + gi * P;
   const uint32_t  plane = 14 * a.nof_subc;
 
-  eq::cplx y[P], h0[P], h1[P];
+  eq::cplx y[P], h[P * L];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
-    y[p]  = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane]);
-    h0[p] = eq::from_cbf16(est[static_cast<uint64_t>(p * L + 0) * plane]);
-    if (L == 2) {
-      h1[p] = eq::from_cbf16(est[static_cast<uint64_t>(p * L + 1) * plane]);
+    y[p] = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane]);
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      h[p * L + l] = eq::from_cbf16(est[static_cast<uint64_t>(p * L + l) * plane]);
     }
   }
   const uint64_t out = static_cast<uint64_t>(gi) * a.nof_re * L + static_cast<uint64_t>(j) * L;
   if (L == 1) {
+    eq::cplx h0[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      h0[p] = h[p];
+    }
     float    nvp[P];
     uint32_t valid = 0;
 #pragma unroll
@@ -73,35 +80,59 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
       nmax = (nmax < st[p].noise_var) ? st[p].noise_var : nmax;
     }
     const bool ok = __builtin_isnormal(nmax) && nmax >= 0.0f;
-    float4     s;
-    float2     nv;
-    eq::equalize_2xn<P>(y, h0, h1, nmax, ok, 1.0f, s, nv);
-    a.eq_symbols[out]        = make_float2(s.x, s.y);
-    a.eq_symbols[out + 1]    = make_float2(s.z, s.w);
-    a.eq_noise_vars[out]     = nv.x;
-    a.eq_noise_vars[out + 1] = nv.y;
+    if constexpr (L == 2 && !MMSE) {
+      eq::cplx h0[P], h1[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        h0[p] = h[p * 2];
+        h1[p] = h[p * 2 + 1];
+      }
+      float4 s;
+      float2 nv;
+      eq::equalize_2xn<P>(y, h0, h1, nmax, ok, 1.0f, s, nv);
+      a.eq_symbols[out]        = make_float2(s.x, s.y);
+      a.eq_symbols[out + 1]    = make_float2(s.z, s.w);
+      a.eq_noise_vars[out]     = nv.x;
+      a.eq_noise_vars[out + 1] = nv.y;
+    } else {
+      eq::cplx s[L];
+      float    nv[L];
+      eq::equalize_mimo<P, L, MMSE>(y, h, nmax, ok, 1.0f, s, nv);
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        a.eq_symbols[out + l]    = make_float2(s[l].x, s[l].y);
+        a.eq_noise_vars[out + l] = nv[l];
+      }
+    }
   }
 }
 
 } // namespace
 
-hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers,
+hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers, bool mmse,
                                  uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_grids, hipStream_t stream)
 {
   if (nof_symbols == 0 || span_subc == 0 || nof_grids == 0) {
     return hipSuccess;
   }
   const dim3 grid((span_subc + 255) / 256, nof_symbols, nof_grids);
-#define SRS_EQ_CASE(PP, LL)                                                                                           \
-  if (nof_ports == PP && nof_layers == LL) {                                                                          \
-    hipLaunchKernelGGL((pusch_equalize_kernel<PP, LL>), grid, dim3(256), 0, stream, a);                              \
+#define SRS_EQ_CASE(PP, LL, MM)                                                                                       \
+  if (nof_ports == PP && nof_layers == LL && mmse == MM) {                                                            \
+    hipLaunchKernelGGL((pusch_equalize_kernel<PP, LL, MM>), grid, dim3(256), 0, stream, a);                          \
     return hipGetLastError();                                                                                         \
   }
-  SRS_EQ_CASE(1, 1)
-  SRS_EQ_CASE(2, 1)
-  SRS_EQ_CASE(4, 1)
-  SRS_EQ_CASE(2, 2)
-  SRS_EQ_CASE(4, 2)
+  // one layer: MMSE is the ZF equalizer (channel_equalizer_generic_impl.cpp:343)
+  SRS_EQ_CASE(1, 1, false)
+  SRS_EQ_CASE(2, 1, false)
+  SRS_EQ_CASE(4, 1, false)
+  SRS_EQ_CASE(2, 2, false)
+  SRS_EQ_CASE(4, 2, false)
+  SRS_EQ_CASE(4, 3, false)
+  SRS_EQ_CASE(4, 4, false)
+  SRS_EQ_CASE(2, 2, true)
+  SRS_EQ_CASE(4, 2, true)
+  SRS_EQ_CASE(4, 3, true)
+  SRS_EQ_CASE(4, 4, true)
 #undef SRS_EQ_CASE
   return hipErrorInvalidValue;
 }

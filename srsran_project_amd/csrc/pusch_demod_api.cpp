@@ -49,6 +49,7 @@ struct srs_amd_pusch_demod_plan {
   pusch_eq_args args{};
   uint32_t      nof_ports   = 0;
   uint32_t      nof_layers  = 0;
+  bool          mmse        = false;
   uint32_t      nof_symbols = 0;
   uint32_t      span_subc   = 0;
   int32_t       qm          = 0;
@@ -80,12 +81,14 @@ uint32_t dmrs_prb_mask(uint32_t type, uint32_t nof_cdm_groups_without_data)
   return m;
 }
 
+// channel_equalizer_generic_impl.cpp:240-270 (one, two or four ports, no more layers than ports), extended
+// by the L-layer solves of equalizer_device.h: ZF and MMSE for 1 to 4 layers (3 and 4 layers on four ports).
 bool equalizer_supported(int algorithm, uint32_t ports, uint32_t layers)
 {
-  if ((ports != 1 && ports != 2 && ports != 4) || ports < layers) {
+  if ((ports != 1 && ports != 2 && ports != 4) || ports < layers || layers < 1 || layers > 4) {
     return false;
   }
-  return algorithm == SRS_AMD_EQ_ZF ? (layers >= 1 && layers <= 2) : layers == 1;
+  return algorithm == SRS_AMD_EQ_ZF || algorithm == SRS_AMD_EQ_MMSE;
 }
 
 } // namespace
@@ -195,6 +198,7 @@ int srs_amd_pusch_demod_plan_create(srs_amd_pusch_demodulator*        dem,
   p->device       = dem->device;
   p->nof_ports    = cfg->nof_rx_ports;
   p->nof_layers   = cfg->nof_tx_layers;
+  p->mmse         = cfg->equalizer == SRS_AMD_EQ_MMSE;
   p->nof_symbols  = cfg->nof_symbols;
   p->span_subc    = (hi - lo) * 12;
   p->qm           = qm;
@@ -281,7 +285,8 @@ int srs_amd_pusch_demodulate_batch(srs_amd_pusch_demodulator*      dem,
   auto    s          = static_cast<hipStream_t>(stream);
   e                  = dem->order.begin(s);
   if (e == hipSuccess) {
-    e = launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->nof_symbols, plan->span_subc, nof_grids, s);
+    e = launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->mmse, plan->nof_symbols, plan->span_subc,
+                              nof_grids, s);
   }
   if (e != hipSuccess) {
     return hip_fail(e, "pusch_equalize_kernel launch");

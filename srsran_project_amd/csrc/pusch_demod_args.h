@@ -27,7 +27,7 @@ struct pusch_eq_args {
 };
 
 
-hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers,
+hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers, bool mmse,
                                  uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_grids, hipStream_t stream);
 
 } // namespace srs_amd

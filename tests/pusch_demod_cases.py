@@ -36,13 +36,37 @@ CASES = [
 ]
 
 
+# L-layer topologies the open reference's equalizer asserts for (parity unpinned): (name, ports, layers, nof_prb,
+# crbs, qm, start, nsym, dmrs mask, cdm groups without data, algorithm)
+MIMO_CASES = [
+    ("4x4_256qam_273_mmse", 4, 4, 273, (0, 273), 8, 0, 14, (1 << 2) | (1 << 11), 2, "mmse"),
+    ("4x4_64qam_51_zf", 4, 4, 51, (0, 51), 6, 0, 14, (1 << 2), 2, "zf"),
+    ("4x3_16qam_52_mmse", 4, 3, 52, (4, 40), 4, 1, 13, (1 << 3) | (1 << 10), 2, "mmse"),
+    ("4x3_qpsk_25_zf", 4, 3, 25, (0, 25), 2, 0, 14, (1 << 2), 2, "zf"),
+    ("4x2_256qam_106_mmse", 4, 2, 106, (0, 106), 8, 0, 14, (1 << 2) | (1 << 11), 1, "mmse"),
+    ("2x2_64qam_24_mmse", 2, 2, 24, (0, 24), 6, 0, 14, (1 << 3), 2, "mmse"),
+]
+
+
 def make_case(case, seed, kind="random"):
     """Returns (grid uint32 [P][14][nsubc], estimates uint32 [P][L][14][nsubc], noise vars [P], crbs)."""
-    name, P, L, nprb, (lo, hi), qm, start, nsym, dmrs, ncdm = case
+    name, P, L, nprb, (lo, hi), qm, start, nsym, dmrs, ncdm = case[:10]
     rng = np.random.default_rng(seed)
     nsubc = 12 * nprb
     k = np.arange(nsubc)
     h = np.zeros((P, L, 14, nsubc), np.complex64)
+    if kind == "mimo":
+        # full-rank frequency-selective channel: random complex gains, one delay per (port, layer)
+        g = (rng.normal(size=(P, L)) + 1j * rng.normal(size=(P, L))) * 0.6 + 0.8 * np.eye(P, L)
+        tau = rng.integers(0, 24, (P, L))
+        for p in range(P):
+            for v in range(L):
+                h[p, v] = (g[p, v] * np.exp(-2j * np.pi * k * tau[p, v] / 4096))[None, :]
+        x = ((rng.integers(0, 2, (L, 14, nsubc)) * 2 - 1) + 1j * (rng.integers(0, 2, (L, 14, nsubc)) * 2 - 1)) * 0.7
+        y = np.einsum("pvls,vls->pls", h, x) + 0.03 * (rng.normal(size=(P, 14, nsubc))
+                                                       + 1j * rng.normal(size=(P, 14, nsubc)))
+        nv = (0.0018 * (1 + 0.1 * np.arange(P))).astype(np.float32)
+        return bf16_grid(y), bf16_grid(h), nv, list(range(lo, hi))
     if kind == "identity":
         for p in range(P):
             h[p, p % L] = 1.0
@@ -63,9 +87,12 @@ def make_case(case, seed, kind="random"):
 
 
 def demod_args(case):
-    name, P, L, nprb, _, qm, start, nsym, dmrs, ncdm = case
-    return dict(qm=qm, start_symbol=start, nof_symbols=nsym, dmrs_symb_mask=dmrs, dmrs_type2=False,
-                nof_cdm_groups_without_data=ncdm, nof_layers=L)
+    name, P, L, nprb, _, qm, start, nsym, dmrs, ncdm = case[:10]
+    d = dict(qm=qm, start_symbol=start, nof_symbols=nsym, dmrs_symb_mask=dmrs, dmrs_type2=False,
+             nof_cdm_groups_without_data=ncdm, nof_layers=L)
+    if len(case) > 10:
+        d["mmse"] = case[10] == "mmse"
+    return d
 
 
 def assert_llrs_close(got, want, what, min_equal=0.99):

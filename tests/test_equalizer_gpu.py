@@ -58,8 +58,10 @@ def test_equalizer_random_channels(amd, ports, layers):
     rng = np.random.default_rng(ports * 7 + layers)
     for algo in (amd.ChannelEqualizerAlgorithmType.zf, amd.ChannelEqualizerAlgorithmType.mmse):
         eq = amd.ChannelEqualizer(algo)
-        if not eq.is_supported(ports, layers):
-            assert not E.is_supported(algo.name, ports, layers)
+        if not E.is_supported(algo.name, ports, layers):
+            # MMSE with two layers: the open reference asserts; the MI355X solve is tested (parity unpinned)
+            # in test_equalizer_mimo_gpu.py
+            assert eq.is_supported(ports, layers) == E.is_supported_mimo(algo.name, ports, layers)
             continue
         for nre, tx, snr in ((1, 1.0, 20.0), (257, 0.5, 5.0), (3276 * 14, 1.0, 30.0)):
             s, h, nv, _ = E.random_channel(rng, nre, ports, layers, snr)
@@ -107,9 +109,10 @@ def test_equalizer_batch_device(amd):
 
 def test_equalizer_unsupported(amd):
     eq = amd.ChannelEqualizer(amd.ChannelEqualizerAlgorithmType.mmse)
-    assert not eq.is_supported(2, 2)
+    assert not eq.is_supported(2, 4)  # more layers than ports
     assert not eq.is_supported(3, 1)
-    s, h, nv, _ = E.random_channel(np.random.default_rng(0), 8, 2, 2)
+    assert not eq.is_supported(4, 5)
+    s, h, nv, _ = E.random_channel(np.random.default_rng(0), 8, 2, 4)
     with pytest.raises(ValueError):
         eq.equalize(s, h, nv, 1.0)
     with pytest.raises(ValueError):

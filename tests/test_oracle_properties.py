@@ -43,3 +43,36 @@ def test_zero_llrs_give_all_ones():
         r, out, _ = oracle.ldpc_decode(llrs, bg, Z, 1)
         assert r is None
         assert (oracle.unpack_bits(out, oracle.BG_K[bg] * Z) == 1).all()
+
+
+def test_mimo_equalizer_oracle_reduces_to_pinned_zf():
+    """oracle.equalizer.equalize_mimo (fp64, parity unpinned for L >= 3 / MMSE L >= 2) agrees with the pinned
+    reference restatement where the topologies overlap: ZF with one and two layers, MMSE with one layer (which
+    the reference evaluates with its ZF equalizer)."""
+    from oracle import equalizer as E
+
+    rng = np.random.default_rng(4)
+    for ports, layers in ((1, 1), (2, 1), (4, 1), (2, 2), (4, 2)):
+        s, h, nv, _ = E.random_channel(rng, 500, ports, layers, 12.0)
+        want, wantn = E.equalize(s, h, nv, 0.7, layers)
+        for algo in (("zf", "mmse") if layers == 1 else ("zf",)):
+            got, gotn, _ = E.equalize_mimo(s, h, nv, 0.7, layers, algo)
+            if layers == 1:  # the 1-layer reference weights ports by their own noise variances; equal here
+                assert np.allclose(got, want, rtol=1e-9, atol=1e-12)
+                assert np.allclose(gotn, wantn, rtol=1e-9)
+            else:
+                assert np.allclose(got, want, rtol=1e-9, atol=1e-12)
+                assert np.allclose(gotn, wantn, rtol=1e-9)
+
+
+def test_mimo_equalizer_oracle_mmse_is_unbiased():
+    """Unbiased MMSE: with noise-free observations the estimate equals the transmitted symbols scaled back, and
+    the MMSE variance never exceeds the ZF one."""
+    from oracle import equalizer as E
+
+    rng = np.random.default_rng(8)
+    s, h, nv, x = E.random_channel(rng, 300, 4, 4, 60.0)
+    zf, zfn, _ = E.equalize_mimo(s, h, nv, 1.0, 4, "zf")
+    mm, mmn, _ = E.equalize_mimo(s, h, nv, 1.0, 4, "mmse")
+    assert np.all(mmn <= zfn * (1 + 1e-9))
+    assert np.median(np.abs(mm - x)) < 0.02

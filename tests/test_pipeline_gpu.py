@@ -15,6 +15,10 @@ pusch_processor_impl with the "auto" factory implementations), stage by stage:
                             |dLLR| <= 1, >= 99 % identical (float equalizer)
   UL transport blocks       the reference chain's decoded TB bytes and TB CRC flag: identical, and equal
                             to what the UE sent
+The 4-layer PUSCH of the default bench line (MMSE 4 x 4; the open reference's equalizer asserts for it) is
+checked stage by stage against the pinned reference stages where they exist (OFDM demodulator, DM-RS
+estimator with four layers) and against the restated demodulator with the fp64 4 x 4 solve (PARITY UNPINNED
+equalizer), and its transport blocks must equal what the UE sent.
 """
 import numpy as np
 import pytest
@@ -29,7 +33,7 @@ def run():
     import bench_pipeline as bp
 
     dev = torch.device("cuda", 0)
-    pl = bp.Pipeline(2, dev)
+    pl = bp.Pipeline(2, dev, ul_layers=2)  # the reference chain runs PUSCH with at most 2 layers
     stream = torch.cuda.current_stream(dev)
     pl.step(stream)
     torch.cuda.synchronize(dev)
@@ -100,3 +104,46 @@ def test_pipeline_vs_reference_chain(run):
         assert np.array_equal(tb, tb_ref), "cell %d: decoded TB differs from the reference chain" % c
         assert ok_ref and np.array_equal(tb, pl.tb_ul[c].cpu().numpy()), c
         assert res[c].data.ldpc_iterations_sum == it_ref, (c, res[c].data.ldpc_iterations_sum, it_ref)
+
+
+def test_pipeline_four_layer_pusch():
+    import torch
+
+    import bench_pipeline as bp
+    import oracle
+    from oracle import chest as och
+    from oracle import pusch_demod as od
+    from tests.chest_cases import assert_estimates_close, assert_stats_close
+    from tests.pusch_demod_cases import assert_llrs_close
+
+    dev = torch.device("cuda", 0)
+    pl = bp.Pipeline(2, dev, ul_layers=4)
+    assert pl.ul_equalizer == "mmse"
+    stream = torch.cuda.current_stream(dev)
+    pl.step(stream)
+    torch.cuda.synchronize(dev)
+    res = pl.results()
+    ok, its = pl.check()
+    assert ok == 1.0, ok
+    for c in range(pl.S):
+        gul = pl.grid_ul[c].cpu().numpy().view(np.uint32)
+        samp_ul = pl.samp_ul[c].cpu().numpy()
+        for p in range(bp.UL_PORTS):
+            ref = oracle.ref_ofdm_demodulate_slot(samp_ul[p], bp.SLOT, bp.MU, bp.NPRB, bp.NFFT, 1.0, 3.5e9)
+            same = gul[p] == ref.view(np.uint32).reshape(14, bp.NSUBC)
+            assert same.mean() >= 0.99, (c, p, same.mean())
+        est = pl.est_ul[c].cpu().numpy().view(np.uint32)
+        est_ref, st_ref = och.ref_pusch_chest(gul, bp.SLOT, False, 4, bp.N_ID, 0, bp.DMRS_AMP, bp.DMRS_MASK, 0,
+                                              bp.NPRB, bp.UL_START, bp.UL_NSYM, fd=2, td=0, compensate_cfo=True,
+                                              numerology=bp.MU)
+        assert_estimates_close(est, est_ref, "cell %d estimates" % c)
+        st = pl.stats_ul[c].cpu().numpy()
+        got_st = [dict(zip(("noise_var", "epre", "rsrp", "snr", "time_alignment_s", "cfo_hz"), row)) for row in st]
+        assert_stats_close(got_st, st_ref, "cell %d stats" % c)
+        G = pl.plan_ul.cw_length
+        llr = pl.llr_ul[c, :G].cpu().numpy()
+        want = od.pusch_demodulate(gul, est, st[:, 0], bp.RNTI, bp.N_ID, bp.QM, list(range(bp.NPRB)), bp.UL_START,
+                                   bp.UL_NSYM, bp.DMRS_MASK, False, bp.NCDM, 4, mmse=True)
+        assert_llrs_close(llr, want, "cell %d LLRs (4 x 4 MMSE)" % c)
+        assert res[c].data.tb_crc_ok == 1
+        assert np.array_equal(pl.tb_rx[c].cpu().numpy(), pl.tb_ul[c].cpu().numpy()), c
