@@ -520,7 +520,8 @@ int srs_amd::rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
                                    uint32_t                          soft_stride,
                                    uint32_t                          nof_cbs,
                                    void*                             stream,
-                                   bool                              fresh)
+                                   bool                              fresh,
+                                   uint32_t                          write_end)
 {
   if (dm == nullptr) {
     return fail(SRS_AMD_EINVAL, "null rate dematcher");
@@ -547,6 +548,7 @@ int srs_amd::rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
   a.nof_cbs     = nof_cbs;
   a.new_data    = new_data ? 1 : 0;
   a.fresh       = (fresh && new_data) ? 1 : 0;
+  a.write_end   = (write_end == 0 || write_end > a.g.N) ? a.g.N : write_end;
   std::lock_guard<std::mutex> lock(dm->mtx);
   hipError_t                  e = hipSetDevice(dm->device);
   if (e == hipSuccess) {

@@ -37,7 +37,8 @@ struct dematch_args {
   uint32_t        soft_stride;
   uint32_t        nof_cbs;
   int32_t         new_data;
-  int32_t         fresh;    // previous soft-buffer contents are known to be zero (not read)
+  int32_t         fresh;     // previous soft-buffer contents are known to be zero (not read)
+  uint32_t        write_end; // soft-buffer bytes [write_end, N) are not written (nobody reads them); N: all
   rm_geometry     g;
 };
 

@@ -11,7 +11,8 @@ namespace srs_amd {
 // buffers' previous contents are taken as zero and not read (internal,
 // freshly owned buffers; saves one N-byte read per codeblock).  The C-ABI
 // entry point keeps the reference's semantics, where positions outside the
-// rate-matched window keep what the buffer held.
+// rate-matched window keep what the buffer held.  write_end (0: the whole codeblock): soft-buffer
+// bytes from write_end on are not written -- an internal buffer whose consumer reads only a prefix.
 int rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
                           const srs_amd_codeblock_metadata* cfg,
                           int                               new_data,
@@ -22,7 +23,8 @@ int rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
                           uint32_t                          soft_stride,
                           uint32_t                          nof_cbs,
                           void*                             stream,
-                          bool                              fresh);
+                          bool                              fresh,
+                          uint32_t                          write_end = 0);
 
 // srs_amd_ldpc_encode_batch producing only the first max_bits of each shortened
 // codeword (the rows of the extension region beyond them are not computed and

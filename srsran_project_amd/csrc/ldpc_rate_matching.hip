@@ -172,7 +172,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
     if (staged && vec && first_pass && E <= L1) {
       // Single first pass (no combining), branch-free: every position selects between its old value,
       // zero, +inf (filler) and its input, whose LDS read is always issued at a clamped index.
-      for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < g.N; p0 += step) {
+      for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < a.write_end; p0 += step) {
         union {
           uint4  v;
           int8_t b[16];
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
       }
       continue;
     }
-    for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < g.N; p0 += step) {
+    for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < a.write_end; p0 += step) {
       union {
         uint4  v;
         int8_t b[16];

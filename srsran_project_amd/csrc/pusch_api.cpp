@@ -154,8 +154,12 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   srs_amd_codeblock_metadata md{p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
                                 p->nof_filler_bits};
   // Internal buffers stand for a fresh (zeroed) rx_buffer: nothing of theirs is read.
+  // An internal (fresh) buffer is read back only by the LDPC decoder, over the provably non-zero prefix:
+  // the dematcher writes just that prefix.
+  const uint32_t prefix = llr_prefix(p, lay, cfg->new_data != 0, internal);
   int rc = rate_dematch_batch_ex(d->dm, &md, cfg->new_data ? 1 : 0, d_llrs, d->arrays.as<uint32_t>() + rows,
-                                 d->arrays.as<uint32_t>(), d_soft, lay.row_bytes, rows, stream, internal);
+                                 d->arrays.as<uint32_t>(), d_soft, lay.row_bytes, rows, stream, internal,
+                                 internal ? prefix : 0);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
@@ -173,7 +177,7 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   // flag holds the iteration count of that decoding), pusch_decoder_impl.cpp:330-345
   const bool skip = !cfg->new_data && !internal;
   rc = ldpc_decode_batch_ex(dec, &dc, cfg->use_early_stop ? crc_poly : SRS_AMD_NO_CRC, d_soft, lay.row_bytes, nullptr,
-                            llr_prefix(p, lay, cfg->new_data != 0, internal), d->msgs.as<uint8_t>(), msg_stride,
+                            prefix, d->msgs.as<uint8_t>(), msg_stride,
                             d->iters.as<int32_t>(), nullptr, rows, stream,
                             skip ? reinterpret_cast<const uint8_t*>(d_soft) + lay.flag_offset : nullptr, lay.row_bytes);
   if (rc != SRS_AMD_OK) {
