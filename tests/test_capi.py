@@ -136,3 +136,18 @@ def test_sch_plan_host_only():
                 amd.sch_plan(tbs, bg, 0, qm, 0, lay, nre)
             continue
         assert amd.sch_plan(tbs, bg, 0, qm, 0, lay, nre).as_dict() == want
+
+
+def test_integration_plugins_built_against_reference_headers():
+    """integration/_build/libsrsran_amd_hal.so -- the srsRAN plug-ins over the C-ABI (hal::hw_accelerator_pusch_dec
+    and its factory, the ldpc_decoder "hip" factory), compiled against the reference's own headers -- exists, links
+    with no undefined symbols (-Wl,--no-undefined) and exports the factory entry points."""
+    import subprocess
+
+    path = os.path.join(os.path.dirname(__file__), "..", "integration", "_build", "libsrsran_amd_hal.so")
+    if not os.path.exists(path):
+        pytest.skip("integration plug-ins not built (the reference headers are needed)")
+    out = subprocess.run(["nm", "-D", "-C", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    assert "srsran::hip::create_hip_pusch_dec_acc_factory(srsran::hip::pusch_dec_accelerator_config const&)" in out
+    assert "srsran::hip::create_ldpc_decoder_factory_hip(" in out
+    ctypes.CDLL(path)  # loads with libsrsran_amd.so found through its rpath
