@@ -46,7 +46,7 @@ def test_hw_plugin_matches_pusch_decoder_impl(hw, ci):
         want = oracle.ref_pusch_decode(llr, p, oracle.RefRxBuffer(p["nof_segments"]), want_tb)
         assert got == want, (case, sigma, got, want)
         np.testing.assert_array_equal(got_tb, want_tb, err_msg="case %d sigma %g" % (ci, sigma))
-        if k == 0:
+        if k == 0 and p["rv"] == 0:  # clean first transmission (rv > 0 alone may lack systematic bits)
             assert got[0] and np.array_equal(got_tb, tb)
 
 
@@ -54,14 +54,14 @@ def test_hw_plugin_harq_combining(hw):
     """rv 0 too noisy, then rv 2 and rv 3 combined in the accelerator's HBM HARQ rows (new_data = 0), then a new
     transport block on the same HARQ process (new_data = 1 resets)."""
     ohw, dec = hw
-    case = (8 * 4000, 1, 4, 1, 6000, 0, 0)
+    case = (8 * 4000, 1, 4, 1, 12000, 0, 0)
     rx_hw = ohw.HwRxBuffer(_plan(case)["nof_segments"], 50000)
     rx_ref = oracle.RefRxBuffer(_plan(case)["nof_segments"])
     tb = tb_bytes(case[0], 5)
     got_tb = np.zeros(case[0] // 8, np.uint8)
     want_tb = np.zeros(case[0] // 8, np.uint8)
     oks = []
-    for k, (rv, new, sigma) in enumerate(((0, True, 14.0), (2, False, 11.0), (3, False, 9.0))):
+    for k, (rv, new, sigma) in enumerate(((0, True, 12.0), (2, False, 9.0), (3, False, 7.0))):
         p = _plan(case, rv)
         llr = noisy_llrs(osch.pdsch_encode(tb, p), 8, sigma, seed=77 + k)
         got = ohw.hw_pusch_decode(dec, llr, p, rx_hw, got_tb, new_data=new)
