@@ -397,7 +397,7 @@ def main():
         from bench_pipeline import run_pipeline
 
         line = run_pipeline(args, dist, world, rank, dev, timed, HBM_PEAK_GBS,
-                            load_traffic("r01_pipeline_ldpc_traffic.json"))
+                            load_traffic("r02_pipeline_ldpc_traffic.json"))
     else:
         run = run_ldpc if args.workload == "ldpc" else run_ofdm
         line = run(args, dist, world, rank, dev)

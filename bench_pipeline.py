@@ -425,8 +425,10 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         "low_snr": low,
         "roofline": {
             "bound": "valu",
-            "kernel": "ldpc_decode_kernel (PUSCH codeblocks of one step, BG%d Z=%d, CRC24B early stop, <= %d it)"
-                      % (pl.plan_ul.base_graph, pl.plan_ul.lifting_size, pl.iters),
+            "kernel": "ldpc_decode_hr_kernel (PUSCH codeblocks of one step, BG%d Z=%d, CRC24B early stop, <= %d it; "
+                      "the decoder reads the %d-LLR non-zero prefix of each soft-buffer row)"
+                      % (pl.plan_ul.base_graph, pl.plan_ul.lifting_size, pl.iters,
+                         __import__("srsran_project_amd").decoder_llr_prefix(pl.plan_ul)),
             "achieved": dec_bytes / (dec_ms * 1e-3) / 1e9,
             "peak": hbm_peak,
             "unit": "GB/s",
@@ -435,8 +437,10 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
             "kernel_ms": dec_ms,
             "algorithmic_bytes_per_launch": dec_bytes,
             "valu_issue": valu,
-            "note": "HBM fraction of the decoder (algorithmic bytes / kernel time / 8 TB/s); the kernel is bound by "
-                    "VALU issue and LDS latency, see valu_issue (2 cycles per wave64 VALU instruction)",
+            "note": "HBM fraction of the decoder (algorithmic bytes / kernel time / 8 TB/s; PMC traffic = algorithmic, "
+                    "no re-reads). The kernel is latency-bound: valu_issue is its VALU-issue fraction (measured VALU "
+                    "wave-instructions x 2 cycles per wave64 instruction over 1,024 SIMDs at 2.4 GHz, "
+                    "profiles/ldpc_valu_model.json); PMC: ~40 % of wave time waiting on barriers / LDS",
         },
         "cpu_baseline": cpu,
     }
