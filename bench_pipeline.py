@@ -81,7 +81,8 @@ def ul_pdu(amd, layers, tbs):
 
 
 class Pipeline:
-    def __init__(self, slots, dev, iters=LDPC_ITERS, snr_db=SNR_DB, ul_layers=UL_LAYERS, seed=0, ul_equalizer=None):
+    def __init__(self, slots, dev, iters=LDPC_ITERS, snr_db=SNR_DB, ul_layers=UL_LAYERS, seed=0, ul_equalizer=None,
+                 keep_estimates=False):
         import torch
 
         import srsran_project_amd as amd
@@ -134,7 +135,10 @@ class Pipeline:
         stride = self.ofdm_mod.max_slot_size()
         self.samp_dl = torch.empty((S, DL_PORTS, stride), dtype=torch.complex64, device=dev)
         self.grid_ul = torch.zeros((S, UL_PORTS, 14, NSUBC), dtype=torch.int32, device=dev)
-        self.est_ul = torch.zeros((S, UL_PORTS, ul_layers, 14, NSUBC), dtype=torch.int32, device=dev)
+        # keep_estimates: the processor also writes the expanded channel estimates (tests check them); without
+        # it the equalizer rebuilds them per RE from the estimator's per-subcarrier output (no HBM tensor)
+        self.est_ul = (torch.zeros((S, UL_PORTS, ul_layers, 14, NSUBC), dtype=torch.int32, device=dev)
+                       if keep_estimates else None)
         self.stats_ul = torch.zeros((S, UL_PORTS, 6), dtype=torch.float32, device=dev)
         self.llr_ul = torch.empty((S, (self.plan_ul.cw_length + 63) // 64 * 64), dtype=torch.int8, device=dev)
         self.tb_rx = torch.zeros((S, self.tbs_ul // 8), dtype=torch.uint8, device=dev)

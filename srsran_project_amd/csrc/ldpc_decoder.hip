@@ -769,18 +769,30 @@ __host__ __device__ constexpr int hr_lds_bytes()
   return LDS_SOFT_OFFSET + (22 + MAXL) * HR_Z;
 }
 
-// LDS byte offset of the soft bit that row (t + H) of edge EI reads, H = 0 or 192.
+// LDS byte offset of the soft bit that row (t + KOFF + H) of edge EI reads, H = 0 or 192, t + KOFF < 192.
 // One of the two rows of an edge never wraps: its address is t + literal.
-template <int EI, int H>
+template <int EI, int H, int KOFF = 0>
 __device__ __forceinline__ uint32_t hr_addr(uint32_t t)
 {
   constexpr uint32_t s    = (const_edge<1, HR_Z, EI>::shift + H) % HR_Z;
   constexpr uint32_t base = LDS_SOFT_OFFSET + const_edge<1, HR_Z, EI>::var * HR_Z;
   if constexpr (s <= HR_HALF) {
-    return t + (base + s); // t < 192: t + s < 384
+    return t + (base + KOFF + s); // t + KOFF < 192: t + KOFF + s < 384
   } else {
-    return __builtin_elementwise_min(t + s, t + (s - HR_Z)) + base;
+    return __builtin_elementwise_min(t + (KOFF + s), t + (KOFF + s - HR_Z)) + base;
   }
+}
+
+// Compile-time loop: f(std::integral_constant<int, 0>) ... f(std::integral_constant<int, N - 1>).
+template <int N, typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>)
+{
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f)
+{
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
 }
 
 // Check-to-variable messages of the first MAXL layers, register resident: one int16 pair per edge
@@ -853,81 +865,108 @@ __device__ __forceinline__ pk16 pk_scale(pk16 m)
 #define HR_CHUNK2 5
 #endif
 
-// One layer (base-graph row L, global edges E0 .. E0 + DEG - 1) for rows t, t + 192.
-template <int L, int ARITH, typename MSGS, int... E>
+// One layer (base-graph row L, global edges E0 .. E0 + DEG - 1) for the NP row pairs of lane t:
+// rows t + k T and t + k T + 192, T = 192 / NP, k < NP (message of edge e, pair k: index e NP + k).
+template <int L, int ARITH, int NP, typename MSGS, int... E>
 __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std::integer_sequence<int, E...>)
 {
   constexpr int E0  = row_start<1>(L);
   constexpr int DEG = sizeof...(E);
-  pk16          v[DEG];
-  pk16          min1 = pk_splat(LLR_MAX), min2 = pk_splat(LLR_MAX), sgn = pk_splat(0);
+  constexpr int T   = HR_HALF / NP;
+  pk16          v[DEG][NP];
+  pk16          min1[NP], min2[NP], sgn[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    min1[k] = pk_splat(LLR_MAX);
+    min2[k] = pk_splat(LLR_MAX);
+    sgn[k]  = pk_splat(0);
+  }
   // pass 1 (ldpc_decoder_impl.cpp:235 / :290): v2c and the check-node statistics
   (
       [&] {
         if constexpr (E % HR_CHUNK1 == 0 && E > 0) {
           __builtin_amdgcn_sched_barrier(0);
         }
-        const pk16 s   = pk16{static_cast<short>(lds[hr_addr<E0 + E, 0>(t)]),
-                            static_cast<short>(lds[hr_addr<E0 + E, HR_HALF>(t)])};
-        const pk16 sat = pk_clamp(s, LLR_MAX);
-        // infinite soft bits (+-127) push |v2c| beyond 220 (see edge_pass1)
-        const pk16 x  = (s - sat) * pk_splat(27) + pk_clamp(s - c2v.template get<E0 + E>(), LLR_MAX);
-        const pk16 ax = __builtin_elementwise_abs(x);
-        min2          = pk_max(min1, pk_min(ax, min2)); // median(min1, |v|, min2)
-        min1          = pk_min(min1, ax);
-        sgn ^= x;
-        v[E] = x;
+        static_for<NP>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          const pk16    s = pk16{static_cast<short>(lds[hr_addr<E0 + E, 0, k * T>(t)]),
+                              static_cast<short>(lds[hr_addr<E0 + E, HR_HALF, k * T>(t)])};
+          const pk16 sat = pk_clamp(s, LLR_MAX);
+          // infinite soft bits (+-127) push |v2c| beyond 220 (see edge_pass1)
+          const pk16 x = (s - sat) * pk_splat(27) + pk_clamp(s - c2v.template get<(E0 + E) * NP + k>(), LLR_MAX);
+          const pk16 ax = __builtin_elementwise_abs(x);
+          min2[k]       = pk_max(min1[k], pk_min(ax, min2[k])); // median(min1, |v|, min2)
+          min1[k]       = pk_min(min1[k], ax);
+          sgn[k] ^= x;
+          v[E][k] = x;
+        });
       }(),
       ...);
   __builtin_amdgcn_sched_barrier(0);
-  const pk16 s1  = pk_scale<ARITH>(min1);
-  const pk16 s2  = pk_scale<ARITH>(min2);
-  const pk16 d12 = s1 - s2;
+  pk16 s1[NP], s2[NP], d12[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    s1[k]  = pk_scale<ARITH>(min1[k]);
+    s2[k]  = pk_scale<ARITH>(min2[k]);
+    d12[k] = s1[k] - s2[k];
+  }
   // pass 2 (ldpc_decoder_impl.cpp:310, :270): new message and promotion sum
   (
       [&] {
         if constexpr (E % HR_CHUNK2 == 0 && E > 0) {
           __builtin_amdgcn_sched_barrier(0);
         }
-        pk16 x = v[E];
-        // opaque: otherwise |x| of pass 1 is kept live (19 more VGPRs) instead of being recomputed
-        asm volatile("" : "+v"(x));
-        const pk16 f   = pk_min(__builtin_elementwise_abs(x) - min1, pk_splat(1)); // 0: this edge holds min1
-        const pk16 mag = f * d12 + s2;
-        const pk16 neg = (sgn ^ x) >> 15;
-        const pk16 c   = (mag ^ neg) - neg;
-        const pk16 sum = c + x;
-        const pk16 m   = pk_clamp(sum, LLR_MAX);
-        const pk16 out = (pk_clamp(sum, LLR_MAX + 1) - m) * pk_splat(LLR_INFINITY - LLR_MAX) + m;
-        c2v.template set<E0 + E>(c);
-        lds[hr_addr<E0 + E, 0>(t)]       = static_cast<int8_t>(out.x);
-        lds[hr_addr<E0 + E, HR_HALF>(t)] = static_cast<int8_t>(out.y);
+        static_for<NP>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          pk16          x = v[E][k];
+          // opaque: otherwise |x| of pass 1 is kept live (19 more VGPRs) instead of being recomputed
+          asm volatile("" : "+v"(x));
+          const pk16 f   = pk_min(__builtin_elementwise_abs(x) - min1[k], pk_splat(1)); // 0: this edge holds min1
+          const pk16 mag = f * d12[k] + s2[k];
+          const pk16 neg = (sgn[k] ^ x) >> 15;
+          const pk16 c   = (mag ^ neg) - neg;
+          const pk16 sum = c + x;
+          const pk16 m   = pk_clamp(sum, LLR_MAX);
+          const pk16 out = (pk_clamp(sum, LLR_MAX + 1) - m) * pk_splat(LLR_INFINITY - LLR_MAX) + m;
+          c2v.template set<(E0 + E) * NP + k>(c);
+          lds[hr_addr<E0 + E, 0, k * T>(t)]       = static_cast<int8_t>(out.x);
+          lds[hr_addr<E0 + E, HR_HALF, k * T>(t)] = static_cast<int8_t>(out.y);
+        });
       }(),
       ...);
 }
 
-template <int L, int MAXL, int ARITH, typename MSGS>
+template <int L, int MAXL, int ARITH, int NP, typename MSGS>
 __device__ __forceinline__ void hr_layers(lds_i8* lds, MSGS& c2v, uint32_t t, int nof_layers)
 {
   if constexpr (L < MAXL) {
     if (L < 4 || L < nof_layers) {
       asm volatile("" : "+v"(t));
-      hr_layer<L, ARITH>(lds, c2v, t, std::make_integer_sequence<int, bg_traits<1>::deg(L)>{});
+      hr_layer<L, ARITH, NP>(lds, c2v, t, std::make_integer_sequence<int, bg_traits<1>::deg(L)>{});
+      // one wave per codeblock (NP = 3): the wave's LDS accesses are processed in order, no barrier
       __syncthreads();
     }
-    hr_layers<L + 1, MAXL, ARITH>(lds, c2v, t, nof_layers);
+    hr_layers<L + 1, MAXL, ARITH, NP>(lds, c2v, t, nof_layers);
   }
 }
 
-template <int ARITH, int MAXL>
-__global__ void __launch_bounds__(HR_THREADS, 4) ldpc_decode_hr_kernel(decode_args a)
+// NP row pairs per lane: NP = 1 -> 192 threads (3 waves) per codeblock, NP = 3 -> one wave per codeblock
+// (no workgroup barriers, three independent pair streams per lane).
+template <int NP>
+constexpr int hr_waves_per_simd()
+{
+  return NP == 1 ? 4 : 2;
+}
+
+template <int ARITH, int MAXL, int NP>
+__global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_decode_hr_kernel(decode_args a)
 {
   constexpr int Z       = HR_Z;
   constexpr int K       = 22 * Z;
   constexpr int NODES   = 22 + MAXL;
-  constexpr int NE      = row_start<1>(MAXL);
+  constexpr int NE      = row_start<1>(MAXL) * NP;
   constexpr int MAX_LLR = (NODES - 2) * Z; // host guarantees llr_len <= MAX_LLR
-  constexpr int NT      = HR_THREADS;
+  constexpr int NT      = HR_HALF / NP;
   lds_i32*      red     = (lds_i32*)(uintptr_t)LDS_RED_OFFSET;
   lds_i8*       lds     = (lds_i8*)(uintptr_t)0;
   lds_i8*       soft    = lds + LDS_SOFT_OFFSET;
@@ -993,7 +1032,9 @@ __global__ void __launch_bounds__(HR_THREADS, 4) ldpc_decode_hr_kernel(decode_ar
         }
       }
       // punctured nodes 0 and 1
-      soft4[t] = 0;
+      for (int w = t; w < 2 * Z / 4; w += NT) {
+        soft4[w] = 0;
+      }
       if (last >= 0) {
         __hip_atomic_fetch_max(&red[0], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -1021,7 +1062,7 @@ __global__ void __launch_bounds__(HR_THREADS, 4) ldpc_decode_hr_kernel(decode_ar
     c2v.zero();
 
     for (int it = 0; it < a.max_iterations; ++it) {
-      hr_layers<0, MAXL, ARITH>(lds, c2v, t, nof_layers);
+      hr_layers<0, MAXL, ARITH, NP>(lds, c2v, t, nof_layers);
 
       if (a.crc_table) {
         // hard bits + CRC early stop (ldpc_decoder_impl.cpp:125), remainder up to a unit factor:
@@ -1112,6 +1153,10 @@ __global__ void __launch_bounds__(HR_THREADS, 4) ldpc_decode_hr_kernel(decode_ar
 }
 
 constexpr int HR_MAXL = 4;
+#ifndef HR_NP_DEFAULT
+#define HR_NP_DEFAULT 1
+#endif
+constexpr int HR_NP = HR_NP_DEFAULT; // row pairs per lane (1: three waves per codeblock, 3: one wave)
 
 bool ldpc_decode_hr_eligible(const decode_args& args, const lifted_graph& g)
 {
@@ -1148,11 +1193,12 @@ hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, in
   if (ldpc_decode_hr_eligible(args, g)) {
     // The crc table of the high-rate kernel is indexed from K Z - 1 down, 16-byte aligned.
     constexpr size_t lds = hr_lds_bytes<HR_MAXL>();
+    constexpr int    NT  = HR_HALF / HR_NP;
     if (arith == ARITH_GENERIC) {
-      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_GENERIC, HR_MAXL>), dim3(grid), dim3(HR_THREADS), lds, stream,
+      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_GENERIC, HR_MAXL, HR_NP>), dim3(grid), dim3(NT), lds, stream,
                          args);
     } else {
-      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_SIMD, HR_MAXL>), dim3(grid), dim3(HR_THREADS), lds, stream,
+      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_SIMD, HR_MAXL, HR_NP>), dim3(grid), dim3(NT), lds, stream,
                          args);
     }
     return hipGetLastError();

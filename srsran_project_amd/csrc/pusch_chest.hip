@@ -31,6 +31,7 @@
 
 #include "dft_engine.h"
 #include "gold_sequence.h"
+#include "chest_device.h"
 #include "pusch_chest_args.h"
 
 #pragma clang fp contract(off)
@@ -38,13 +39,14 @@
 namespace srs_amd {
 namespace {
 
-constexpr float TWOPI_F = 6.28318530717958647692f;
-constexpr float AMP     = 0.70710678118654752440f; // M_SQRT1_2 as float
+using chdev::bf16_bits;
+using chdev::cmul;
+using chdev::from_cbf16;
+using chdev::polar1;
+using chdev::to_cbf16;
+using chdev::TWOPI_F;
+constexpr float AMP = 0.70710678118654752440f; // M_SQRT1_2 as float
 
-__device__ __forceinline__ float2 cmul(float2 a, float2 b)
-{
-  return make_float2(__builtin_fmaf(a.x, b.x, -(a.y * b.y)), __builtin_fmaf(a.x, b.y, a.y * b.x));
-}
 __device__ __forceinline__ float2 cmulc(float2 a, float2 b) // a * conj(b)
 {
   return cmul(a, make_float2(b.x, -b.y));
@@ -60,26 +62,6 @@ __device__ __forceinline__ float2 csub(float2 a, float2 b)
 __device__ __forceinline__ float2 cscale(float2 a, float s)
 {
   return make_float2(a.x * s, a.y * s);
-}
-__device__ __forceinline__ float2 from_cbf16(uint32_t u)
-{
-  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
-}
-__device__ __forceinline__ uint32_t bf16_bits(float f)
-{
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
-}
-__device__ __forceinline__ uint32_t to_cbf16(float2 v)
-{
-  return bf16_bits(v.x) | (bf16_bits(v.y) << 16);
-}
-__device__ __forceinline__ float2 polar1(float theta)
-{
-  float s, c;
-  sincosf(theta, &s, &c);
-  return make_float2(c, s);
 }
 
 // rx[g][d][k] with runtime indices through selects (no dynamic register indexing).
@@ -598,10 +580,10 @@ __global__ __launch_bounds__(256) void chest_expand_kernel(chest_args a)
   const uint32_t    v    = gpv % a.L;
   const uint32_t    grid = gp / a.nof_ports, port = gp % a.nof_ports;
   const float*      acc  = a.acc + static_cast<uint64_t>(gp) * 8;
-  const bool        rot  = a.compensate_cfo && acc[3] != 0.0f;
+  const bool        rot  = chdev::cfo_rotates(a, acc);
   if (rot && threadIdx.x < a.nof_symbols) {
     const uint32_t l  = a.first_symbol + threadIdx.x;
-    s_ph[threadIdx.x] = polar1(TWOPI_F * a.epoch[l] * acc[4]);
+    s_ph[threadIdx.x] = chdev::cfo_phase(a, acc, l);
   }
   __syncthreads();
   if (sc >= a.nsubc) {
@@ -621,38 +603,16 @@ __global__ __launch_bounds__(256) void chest_expand_kernel(chest_args a)
       x[s] = s < static_cast<int>(a.nof_lse) ? fr[static_cast<uint64_t>(s) * a.nof_re] : make_float2(0, 0);
     }
   }
-  auto lse = [&](int i) { // x[i] without dynamic register indexing
-    float2 r = x[0];
-#pragma unroll
-    for (int s = 1; s < CH_MAXDMRS; ++s) {
-      r = i == s ? x[s] : r;
-    }
-    return r;
-  };
   for (uint32_t n = 0; n < a.nof_symbols; ++n) {
     const uint32_t l = a.first_symbol + n;
     uint32_t       out;
     if (in) {
-      float2 e;
-      if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
-        e = x[0];
-      } else {
-        const int    i0 = a.td_i0[l];
-        const float2 x0 = lse(i0);
-        if (a.td_interp[l]) {
-          const float2 x1 = lse(i0 + 1);
-          const float  w  = a.td_w[l];
-          e               = make_float2(__builtin_fmaf(x1.x - x0.x, w, x0.x), __builtin_fmaf(x1.y - x0.y, w, x0.y));
-        } else {
-          e = x0;
-        }
-      }
-      out = to_cbf16(e);
+      out = chdev::expand_value(a, x, l, rot, rot ? s_ph[n] : make_float2(1, 0));
     } else {
       out = est[static_cast<uint64_t>(l) * a.nsubc];
-    }
-    if (rot) {
-      out = to_cbf16(cmul(from_cbf16(out), s_ph[n]));
+      if (rot) {
+        out = to_cbf16(cmul(from_cbf16(out), s_ph[n]));
+      }
     }
     est[static_cast<uint64_t>(l) * a.nsubc] = out;
   }
@@ -660,7 +620,7 @@ __global__ __launch_bounds__(256) void chest_expand_kernel(chest_args a)
 
 } // namespace
 
-hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t stream)
+hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t stream, bool expand)
 {
   const uint32_t nb = nof_grids * a.nof_ports;
   if (nb == 0) {
@@ -689,6 +649,9 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
+  }
+  if (!expand) {
+    return hipSuccess; // the consumer rebuilds the estimates from a.freq / a.acc (chest_device.h)
   }
   hipLaunchKernelGGL(chest_expand_kernel, dim3((a.nsubc + 255) / 256, nb * a.L), dim3(256), 0, stream, a);
   return hipGetLastError();

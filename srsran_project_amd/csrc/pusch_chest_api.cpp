@@ -302,7 +302,9 @@ void srs_amd_pusch_chest_destroy(srs_amd_pusch_chest* chest)
   delete chest;
 }
 
-int srs_amd_pusch_chest_estimate_batch(srs_amd_pusch_chest*              chest,
+} // extern "C"
+
+static int estimate_batch_impl(srs_amd_pusch_chest*              chest,
                                        const srs_amd_pusch_chest_config* cfg,
                                        const uint32_t*                   d_grids,
                                        uint64_t                          grid_stride,
@@ -312,7 +314,9 @@ int srs_amd_pusch_chest_estimate_batch(srs_amd_pusch_chest*              chest,
                                        uint32_t*                         d_estimates,
                                        uint64_t                          est_stride,
                                        srs_amd_chest_port_stats*         d_stats,
-                                       void*                             stream)
+                                       void*                             stream,
+                                       bool                              expand,
+                                       chest_args*                       view)
 {
   if (chest == nullptr) {
     return fail(SRS_AMD_EINVAL, "null estimator");
@@ -325,11 +329,11 @@ int srs_amd_pusch_chest_estimate_batch(srs_amd_pusch_chest*              chest,
   if (nof_grids == 0) {
     return SRS_AMD_OK;
   }
-  if (d_grids == nullptr || d_estimates == nullptr || d_stats == nullptr) {
+  if (d_grids == nullptr || (expand && d_estimates == nullptr) || d_stats == nullptr) {
     return fail(SRS_AMD_EINVAL, "null device buffer");
   }
   if (nof_grids > 1 && (grid_stride < static_cast<uint64_t>(nof_ports) * CH_NSYMB * nof_subc ||
-                        est_stride < static_cast<uint64_t>(nof_ports) * a.L * CH_NSYMB * nof_subc)) {
+                        (expand && est_stride < static_cast<uint64_t>(nof_ports) * a.L * CH_NSYMB * nof_subc))) {
     return fail(SRS_AMD_EINVAL, "grid or estimate stride too small");
   }
   std::lock_guard<std::mutex> lock(chest->mtx);
@@ -358,12 +362,48 @@ int srs_amd_pusch_chest_estimate_batch(srs_amd_pusch_chest*              chest,
   a.ta_tw       = chest->tw(a.ta_n);
   e             = chest->order.begin(static_cast<hipStream_t>(stream));
   if (e == hipSuccess) {
-    e = launch_chest(a, nof_grids, static_cast<hipStream_t>(stream));
+    e = launch_chest(a, nof_grids, static_cast<hipStream_t>(stream), expand);
   }
   if (e == hipSuccess) {
     e = chest->order.end(static_cast<hipStream_t>(stream));
   }
+  if (view != nullptr) {
+    *view = a;
+  }
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "channel estimator launch");
+}
+
+int srs_amd::chest_estimate_batch_unexpanded(::srs_amd_pusch_chest*            chest,
+                                             const srs_amd_pusch_chest_config* cfg,
+                                             const uint32_t*                   d_grids,
+                                             uint64_t                          grid_stride,
+                                             uint32_t                          nof_ports,
+                                             uint32_t                          nof_subc,
+                                             uint32_t                          nof_grids,
+                                             srs_amd_chest_port_stats*         d_stats,
+                                             void*                             stream,
+                                             chest_args*                       view)
+{
+  return estimate_batch_impl(chest, cfg, d_grids, grid_stride, nof_ports, nof_subc, nof_grids, nullptr, 0, d_stats,
+                             stream, false, view);
+}
+
+extern "C" {
+
+int srs_amd_pusch_chest_estimate_batch(srs_amd_pusch_chest*              chest,
+                                       const srs_amd_pusch_chest_config* cfg,
+                                       const uint32_t*                   d_grids,
+                                       uint64_t                          grid_stride,
+                                       uint32_t                          nof_ports,
+                                       uint32_t                          nof_subc,
+                                       uint32_t                          nof_grids,
+                                       uint32_t*                         d_estimates,
+                                       uint64_t                          est_stride,
+                                       srs_amd_chest_port_stats*         d_stats,
+                                       void*                             stream)
+{
+  return estimate_batch_impl(chest, cfg, d_grids, grid_stride, nof_ports, nof_subc, nof_grids, d_estimates,
+                             est_stride, d_stats, stream, true, nullptr);
 }
 
 int srs_amd_pusch_chest_estimate(srs_amd_pusch_chest*              chest,

@@ -66,6 +66,23 @@ struct chest_args {
   float    scs_hz;
 };
 
-hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t stream);
+// expand = false: pilot and time-alignment kernels only -- the per-subcarrier estimates (freq) and the
+// per-port accumulators (acc) stay in the estimator's scratch for a consumer that rebuilds each RE's
+// estimate itself (the PUSCH demodulator's fused equalizer, chest_device.h).
+hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t stream, bool expand = true);
+
+// srs_amd_pusch_chest_estimate_batch without the expansion to per-RE estimates (nothing is written to an
+// estimate tensor): *view receives the argument block whose freq / acc scratch the fused consumer reads,
+// valid until the next call on this estimator.  Same validation and errors as the C-ABI call.
+int chest_estimate_batch_unexpanded(::srs_amd_pusch_chest*            chest,
+                                    const srs_amd_pusch_chest_config* cfg,
+                                    const uint32_t*                   d_grids,
+                                    uint64_t                          grid_stride,
+                                    uint32_t                          nof_ports,
+                                    uint32_t                          nof_subc,
+                                    uint32_t                          nof_grids,
+                                    srs_amd_chest_port_stats*         d_stats,
+                                    void*                             stream,
+                                    chest_args*                       view);
 
 } // namespace srs_amd

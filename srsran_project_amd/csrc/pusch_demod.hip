@@ -17,43 +17,21 @@
 // demap_descramble_kernel (modulation.hip).
 #include <hip/hip_runtime.h>
 
+#include "chest_device.h"
 #include "equalizer_device.h"
 #include "pusch_demod_args.h"
 
 namespace srs_amd {
 namespace {
 
+// Equalizes data RE j of grid gi from its received samples y[P] and channel coefficients h[P][L] and writes
+// [j][layer] symbols and variances.
 template <int P, int L, bool MMSE>
-__global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
+__device__ __forceinline__ void equalize_write(const pusch_eq_args& a, uint32_t gi, uint32_t j, const eq::cplx* y,
+                                               const eq::cplx* h)
 {
-  const uint32_t  l   = a.first_symbol + blockIdx.y;
-  const uint32_t  sc  = a.first_subc + blockIdx.x * 256 + threadIdx.x;
-  const uint32_t  gi  = blockIdx.z;
-  if (sc >= a.nof_subc) {
-    return;
-  }
-  const uint32_t e   = a.re_table[l * a.nof_prb + sc / 12];
-  const uint32_t bit = sc % 12;
-  if (((e >> bit) & 1u) == 0) {
-    return;
-  }
-  const uint32_t j = (e >> 12) + __builtin_popcount(e & ((1u << bit) - 1u));
-
-  const uint32_t* grid = a.grids + gi * a.grid_stride + l * a.nof_subc + sc;
-  const uint32_t* est  = a.estimates + gi * a.est_stride + l * a.nof_subc + sc;
-  const srs_amd_chest_port_stats* st = a.stats + gi * P;
-  const uint32_t  plane = 14 * a.nof_subc;
-
-  eq::cplx y[P], h[P * L];
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    y[p] = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane]);
-#pragma unroll
-    for (int l = 0; l < L; ++l) {
-      h[p * L + l] = eq::from_cbf16(est[static_cast<uint64_t>(p * L + l) * plane]);
-    }
-  }
-  const uint64_t out = static_cast<uint64_t>(gi) * a.nof_re * L + static_cast<uint64_t>(j) * L;
+  const srs_amd_chest_port_stats* st  = a.stats + gi * P;
+  const uint64_t                  out = static_cast<uint64_t>(gi) * a.nof_re * L + static_cast<uint64_t>(j) * L;
   if (L == 1) {
     eq::cplx h0[P];
 #pragma unroll
@@ -107,6 +85,103 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
   }
 }
 
+template <int P, int L, bool MMSE>
+__global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
+{
+  const uint32_t  l   = a.first_symbol + blockIdx.y;
+  const uint32_t  sc  = a.first_subc + blockIdx.x * 256 + threadIdx.x;
+  const uint32_t  gi  = blockIdx.z;
+  if (sc >= a.nof_subc) {
+    return;
+  }
+  const uint32_t e   = a.re_table[l * a.nof_prb + sc / 12];
+  const uint32_t bit = sc % 12;
+  if (((e >> bit) & 1u) == 0) {
+    return;
+  }
+  const uint32_t j = (e >> 12) + __builtin_popcount(e & ((1u << bit) - 1u));
+
+  const uint32_t* grid  = a.grids + gi * a.grid_stride + l * a.nof_subc + sc;
+  const uint32_t* est   = a.estimates + gi * a.est_stride + l * a.nof_subc + sc;
+  const uint32_t  plane = 14 * a.nof_subc;
+
+  eq::cplx y[P], h[P * L];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    y[p] = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane]);
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      h[p * L + l] = eq::from_cbf16(est[static_cast<uint64_t>(p * L + l) * plane]);
+    }
+  }
+  equalize_write<P, L, MMSE>(a, gi, j, y, h);
+}
+
+// Estimator-fused form: one thread per (grid, subcarrier, half of the OFDM symbols) rebuilds the channel
+// coefficients of each data RE from the estimator's per-subcarrier values (c.freq) and per-port CFO phases
+// with the expansion kernel's own operations (chest_device.h expand_value: identical cbf16 estimates), so
+// the P x L x 14 x subcarrier estimate tensor is neither written nor read.
+constexpr int EQ_SYM_GROUPS = 2;
+
+template <int P, int L, bool MMSE, int NLSE>
+__global__ __launch_bounds__(256) void pusch_equalize_fused_kernel(pusch_eq_args a, chest_args c)
+{
+  __shared__ float2 s_ph[P][CH_NSYMB];
+  __shared__ int    s_rot[P];
+  const uint32_t    gi = blockIdx.z;
+  if (threadIdx.x < P * CH_NSYMB) {
+    const uint32_t p   = threadIdx.x / CH_NSYMB, n = threadIdx.x % CH_NSYMB;
+    const float*   acc = c.acc + (static_cast<uint64_t>(gi) * P + p) * 8;
+    s_ph[p][n]         = n < c.nof_symbols ? chdev::cfo_phase(c, acc, c.first_symbol + n) : make_float2(1, 0);
+    if (n == 0) {
+      s_rot[p] = chdev::cfo_rotates(c, acc) ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  const uint32_t sc = a.first_subc + blockIdx.x * 256 + threadIdx.x;
+  const uint32_t kk = sc - 12 * c.prb_lo; // estimator allocation index (wraps below it)
+  if (sc >= a.nof_subc || kk >= c.nof_re) {
+    return;
+  }
+  float2 x[P][L][NLSE];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+#pragma unroll
+    for (int v = 0; v < L; ++v) {
+      const float2* fr = c.freq + ((static_cast<uint64_t>(gi) * P + p) * L + v) * c.nof_lse * c.nof_re + kk;
+#pragma unroll
+      for (int s = 0; s < NLSE; ++s) {
+        x[p][v][s] = fr[static_cast<uint64_t>(s) * c.nof_re];
+      }
+    }
+  }
+  const uint32_t* grid  = a.grids + gi * a.grid_stride + sc;
+  const uint32_t  plane = 14 * a.nof_subc;
+  const uint32_t  per   = (c.nof_symbols + EQ_SYM_GROUPS - 1) / EQ_SYM_GROUPS;
+  const uint32_t  n0    = blockIdx.y * per;
+  const uint32_t  n1    = min(c.nof_symbols, n0 + per);
+  for (uint32_t n = n0; n < n1; ++n) {
+    const uint32_t l   = c.first_symbol + n;
+    const uint32_t e   = a.re_table[l * a.nof_prb + sc / 12];
+    const uint32_t bit = sc % 12;
+    if (((e >> bit) & 1u) == 0) {
+      continue;
+    }
+    const uint32_t j = (e >> 12) + __builtin_popcount(e & ((1u << bit) - 1u));
+    eq::cplx       y[P], h[P * L];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      y[p] = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane + l * a.nof_subc]);
+#pragma unroll
+      for (int v = 0; v < L; ++v) {
+        const uint32_t u = chdev::expand_value(c, x[p][v], l, s_rot[p] != 0, s_ph[p][n]);
+        h[p * L + v]     = eq::from_cbf16(u);
+      }
+    }
+    equalize_write<P, L, MMSE>(a, gi, j, y, h);
+  }
+}
+
 } // namespace
 
 hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers, bool mmse,
@@ -134,6 +209,43 @@ hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uin
   SRS_EQ_CASE(4, 3, true)
   SRS_EQ_CASE(4, 4, true)
 #undef SRS_EQ_CASE
+  return hipErrorInvalidValue;
+}
+
+bool pusch_equalize_fusable(uint32_t nof_ports, uint32_t nof_layers, bool mmse, uint32_t nof_lse)
+{
+  (void)mmse;
+  return nof_lse >= 1 && nof_lse <= 2 && nof_layers >= 1 && nof_layers <= 4 && nof_layers <= nof_ports &&
+         (nof_ports == 1 || nof_ports == 2 || nof_ports == 4) && !(nof_layers == 3 && nof_ports != 4);
+}
+
+hipError_t launch_pusch_equalize_fused(const pusch_eq_args& a, const chest_args& c, uint32_t nof_ports,
+                                       uint32_t nof_layers, bool mmse, uint32_t span_subc, uint32_t nof_grids,
+                                       hipStream_t stream)
+{
+  if (span_subc == 0 || nof_grids == 0) {
+    return hipSuccess;
+  }
+  const dim3 grid((span_subc + 255) / 256, EQ_SYM_GROUPS, nof_grids);
+#define SRS_EQF_CASE(PP, LL, MM, NN)                                                                                  \
+  if (nof_ports == PP && nof_layers == LL && mmse == MM && c.nof_lse == NN) {                                         \
+    hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM, NN>), grid, dim3(256), 0, stream, a, c);             \
+    return hipGetLastError();                                                                                         \
+  }
+#define SRS_EQF_LSE(PP, LL, MM) SRS_EQF_CASE(PP, LL, MM, 1) SRS_EQF_CASE(PP, LL, MM, 2)
+  SRS_EQF_LSE(1, 1, false)
+  SRS_EQF_LSE(2, 1, false)
+  SRS_EQF_LSE(4, 1, false)
+  SRS_EQF_LSE(2, 2, false)
+  SRS_EQF_LSE(4, 2, false)
+  SRS_EQF_LSE(4, 3, false)
+  SRS_EQF_LSE(4, 4, false)
+  SRS_EQF_LSE(2, 2, true)
+  SRS_EQF_LSE(4, 2, true)
+  SRS_EQF_LSE(4, 3, true)
+  SRS_EQF_LSE(4, 4, true)
+#undef SRS_EQF_LSE
+#undef SRS_EQF_CASE
   return hipErrorInvalidValue;
 }
 

@@ -93,6 +93,104 @@ bool equalizer_supported(int algorithm, uint32_t ports, uint32_t layers)
 
 } // namespace
 
+// The equalizer + demapper pass of a batch; the channel coefficients come from an expanded estimate tensor
+// (d_estimates) or, when fused != nullptr, are rebuilt per RE from the estimator's unexpanded output.
+static int demodulate_impl(srs_amd_pusch_demodulator*      dem,
+                           const srs_amd_pusch_demod_plan* plan,
+                           const uint32_t*                 d_grids,
+                           uint64_t                        grid_stride,
+                           const uint32_t*                 d_estimates,
+                           uint64_t                        est_stride,
+                           const chest_args*               fused,
+                           const srs_amd_chest_port_stats* d_stats,
+                           int8_t*                         d_llrs,
+                           uint64_t                        llr_stride,
+                           uint32_t                        nof_grids,
+                           void*                           stream)
+{
+  if (dem == nullptr || plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_grids == 0 || plan->args.nof_re == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_grids == nullptr || (fused == nullptr && d_estimates == nullptr) || d_stats == nullptr || d_llrs == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  const uint32_t nllr  = plan->nof_llrs();
+  const uint64_t plane = 14ull * plan->args.nof_subc;
+  if (nof_grids > 1 && (grid_stride < plan->nof_ports * plane ||
+                        (fused == nullptr && est_stride < plan->nof_ports * plan->nof_layers * plane) ||
+                        llr_stride < nllr)) {
+    return fail(SRS_AMD_EINVAL, "grid, estimate or LLR stride too small");
+  }
+  if (fused != nullptr) {
+    // the estimator's allocation must cover every data RE and describe the same ports, layers and symbols
+    const chest_args& c = *fused;
+    if (c.nof_ports != plan->nof_ports || c.L != plan->nof_layers || c.nsubc != plan->args.nof_subc ||
+        c.first_symbol != plan->args.first_symbol || c.nof_symbols != plan->nof_symbols ||
+        plan->args.first_subc < 12 * c.prb_lo || plan->args.first_subc + plan->span_subc > 12 * c.prb_lo + c.nof_re ||
+        !pusch_equalize_fusable(plan->nof_ports, plan->nof_layers, plan->mmse, c.nof_lse)) {
+      return fail(SRS_AMD_EINVAL, "channel estimator output does not match the demodulator plan");
+    }
+  }
+  const size_t nsym  = static_cast<size_t>(nof_grids) * plan->args.nof_re * plan->nof_layers;
+  const size_t bytes = align_up(nsym * 8, 256) + align_up(nsym * 4, 256);
+  std::lock_guard<std::mutex> lock(dem->mtx);
+  hipError_t                  e = hipSetDevice(dem->device);
+  if (e == hipSuccess) {
+    e = dem->scratch.ensure(bytes);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH demodulator scratch");
+  }
+  auto*         base = dem->scratch.as<uint8_t>();
+  pusch_eq_args a    = plan->args;
+  a.grids            = d_grids;
+  a.grid_stride      = grid_stride;
+  a.estimates        = d_estimates;
+  a.est_stride       = est_stride;
+  a.stats            = d_stats;
+  a.eq_symbols       = reinterpret_cast<float2*>(base);
+  a.eq_noise_vars    = reinterpret_cast<float*>(base + align_up(nsym * 8, 256));
+  auto s             = static_cast<hipStream_t>(stream);
+  e                  = dem->order.begin(s);
+  if (e == hipSuccess) {
+    e = fused != nullptr ? launch_pusch_equalize_fused(a, *fused, plan->nof_ports, plan->nof_layers, plan->mmse,
+                                                       plan->span_subc, nof_grids, s)
+                         : launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->mmse, plan->nof_symbols,
+                                                 plan->span_subc, nof_grids, s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "pusch_equalize_kernel launch");
+  }
+  // soft demapper + descrambling (revert_scrambling) in one pass: LLRs straight into the caller's rows
+  int rc = demap_descramble_batch(dem->demapper, plan->qm, d_llrs, llr_stride,
+                                  reinterpret_cast<const float*>(a.eq_symbols), a.eq_noise_vars,
+                                  static_cast<uint32_t>(plan->args.nof_re * plan->nof_layers), plan->sym_counts,
+                                  nof_grids, dem->d_jump, plan->c_init, stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  e = dem->order.end(s);
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH demodulator completion event");
+}
+
+int srs_amd::pusch_demodulate_batch_fused(::srs_amd_pusch_demodulator*      dem,
+                                          const ::srs_amd_pusch_demod_plan* plan,
+                                          const uint32_t*                   d_grids,
+                                          uint64_t                          grid_stride,
+                                          const chest_args&                 chest_view,
+                                          const srs_amd_chest_port_stats*   d_stats,
+                                          int8_t*                           d_llrs,
+                                          uint64_t                          llr_stride,
+                                          uint32_t                          nof_grids,
+                                          void*                             stream)
+{
+  return demodulate_impl(dem, plan, d_grids, grid_stride, nullptr, 0, &chest_view, d_stats, d_llrs, llr_stride,
+                         nof_grids, stream);
+}
+
 extern "C" {
 
 int srs_amd_pusch_demodulator_create(srs_amd_pusch_demodulator** dem, int device)
@@ -198,7 +296,7 @@ int srs_amd_pusch_demod_plan_create(srs_amd_pusch_demodulator*        dem,
   p->device       = dem->device;
   p->nof_ports    = cfg->nof_rx_ports;
   p->nof_layers   = cfg->nof_tx_layers;
-  p->mmse         = cfg->equalizer == SRS_AMD_EQ_MMSE;
+  p->mmse         = cfg->equalizer == SRS_AMD_EQ_MMSE && cfg->nof_tx_layers > 1; // one layer: ZF (generic_impl:343)
   p->nof_symbols  = cfg->nof_symbols;
   p->span_subc    = (hi - lo) * 12;
   p->qm           = qm;
@@ -248,59 +346,8 @@ int srs_amd_pusch_demodulate_batch(srs_amd_pusch_demodulator*      dem,
                                    uint32_t                        nof_grids,
                                    void*                           stream)
 {
-  if (dem == nullptr || plan == nullptr) {
-    return fail(SRS_AMD_EINVAL, "null argument");
-  }
-  if (nof_grids == 0 || plan->args.nof_re == 0) {
-    return SRS_AMD_OK;
-  }
-  if (d_grids == nullptr || d_estimates == nullptr || d_stats == nullptr || d_llrs == nullptr) {
-    return fail(SRS_AMD_EINVAL, "null device buffer");
-  }
-  const uint32_t nllr = plan->nof_llrs();
-  const uint64_t plane = 14ull * plan->args.nof_subc;
-  if (nof_grids > 1 && (grid_stride < plan->nof_ports * plane || est_stride < plan->nof_ports * plan->nof_layers * plane ||
-                        llr_stride < nllr)) {
-    return fail(SRS_AMD_EINVAL, "grid, estimate or LLR stride too small");
-  }
-  const size_t nsym  = static_cast<size_t>(nof_grids) * plan->args.nof_re * plan->nof_layers;
-  const size_t bytes = align_up(nsym * 8, 256) + align_up(nsym * 4, 256);
-  std::lock_guard<std::mutex> lock(dem->mtx);
-  hipError_t                  e = hipSetDevice(dem->device);
-  if (e == hipSuccess) {
-    e = dem->scratch.ensure(bytes);
-  }
-  if (e != hipSuccess) {
-    return hip_fail(e, "PUSCH demodulator scratch");
-  }
-  auto*         base = dem->scratch.as<uint8_t>();
-  pusch_eq_args a    = plan->args;
-  a.grids            = d_grids;
-  a.grid_stride      = grid_stride;
-  a.estimates        = d_estimates;
-  a.est_stride       = est_stride;
-  a.stats            = d_stats;
-  a.eq_symbols       = reinterpret_cast<float2*>(base);
-  a.eq_noise_vars    = reinterpret_cast<float*>(base + align_up(nsym * 8, 256));
-  auto    s          = static_cast<hipStream_t>(stream);
-  e                  = dem->order.begin(s);
-  if (e == hipSuccess) {
-    e = launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->mmse, plan->nof_symbols, plan->span_subc,
-                              nof_grids, s);
-  }
-  if (e != hipSuccess) {
-    return hip_fail(e, "pusch_equalize_kernel launch");
-  }
-  // soft demapper + descrambling (revert_scrambling) in one pass: LLRs straight into the caller's rows
-  int rc = demap_descramble_batch(dem->demapper, plan->qm, d_llrs, llr_stride,
-                                  reinterpret_cast<const float*>(a.eq_symbols), a.eq_noise_vars,
-                                  static_cast<uint32_t>(plan->args.nof_re * plan->nof_layers), plan->sym_counts,
-                                  nof_grids, dem->d_jump, plan->c_init, stream);
-  if (rc != SRS_AMD_OK) {
-    return rc;
-  }
-  e = dem->order.end(s);
-  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH demodulator completion event");
+  return demodulate_impl(dem, plan, d_grids, grid_stride, d_estimates, est_stride, nullptr, d_stats, d_llrs,
+                         llr_stride, nof_grids, stream);
 }
 
 int srs_amd_pusch_demap_descramble_batch(srs_amd_pusch_demodulator*      dem,

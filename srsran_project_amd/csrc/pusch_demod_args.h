@@ -7,6 +7,8 @@
 #include <cstdint>
 
 #include "srsran_amd/pusch_chest.h"
+#include "srsran_amd/pusch_demodulator.h"
+#include "pusch_chest_args.h"
 
 namespace srs_amd {
 
@@ -29,5 +31,24 @@ struct pusch_eq_args {
 
 hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers, bool mmse,
                                  uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_grids, hipStream_t stream);
+
+// Estimator-fused equalizer (pusch_demod.hip pusch_equalize_fused_kernel): the channel coefficients of each data
+// RE rebuilt from the estimator's unexpanded output c (chest_estimate_batch_unexpanded); a.estimates unused.
+bool       pusch_equalize_fusable(uint32_t nof_ports, uint32_t nof_layers, bool mmse, uint32_t nof_lse);
+hipError_t launch_pusch_equalize_fused(const pusch_eq_args& a, const chest_args& c, uint32_t nof_ports,
+                                       uint32_t nof_layers, bool mmse, uint32_t span_subc, uint32_t nof_grids,
+                                       hipStream_t stream);
+
+// srs_amd_pusch_demodulate_batch with the estimator-fused equalizer (no estimate tensor).
+int pusch_demodulate_batch_fused(::srs_amd_pusch_demodulator*      dem,
+                                 const ::srs_amd_pusch_demod_plan* plan,
+                                 const uint32_t*                   d_grids,
+                                 uint64_t                          grid_stride,
+                                 const chest_args&                 chest_view,
+                                 const srs_amd_chest_port_stats*   d_stats,
+                                 int8_t*                           d_llrs,
+                                 uint64_t                          llr_stride,
+                                 uint32_t                          nof_grids,
+                                 void*                             stream);
 
 } // namespace srs_amd

@@ -9,9 +9,12 @@
 
 #include "api_common.h"
 #include "device_buffer.h"
+#include "pusch_chest_args.h"
+#include "pusch_demod_args.h"
 #include "pusch_processor_args.h"
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -27,6 +30,7 @@ struct srs_amd_pusch_processor {
   device_buffer                  estimates, stats, llrs, dec_results, host_io;
   stream_order                   order;
   std::mutex                     mtx;
+  bool                           fuse = true; // SRSRAN_AMD_PUSCH_FUSED=0: always expand the estimates
   ~srs_amd_pusch_processor()
   {
     (void)hipSetDevice(device);
@@ -49,6 +53,7 @@ struct srs_amd_pusch_processor_plan {
   srs_amd_sch_plan             sch{};
   srs_amd_pusch_decoder_config dec_cfg{};
   uint64_t                     soft_bytes = 0;
+  bool                         fusable    = false; // the fused estimator-equalizer path covers this PDU
   ~srs_amd_pusch_processor_plan() { srs_amd_pusch_demod_plan_destroy(demod_plan); }
 };
 
@@ -100,7 +105,10 @@ int srs_amd_pusch_processor_create(srs_amd_pusch_processor**             proc,
   auto* p   = new srs_amd_pusch_processor();
   p->device = device;
   p->cfg    = *cfg;
-  rc        = srs_amd_pusch_chest_create(&p->chest, device);
+  if (const char* v = std::getenv("SRSRAN_AMD_PUSCH_FUSED")) {
+    p->fuse = std::strcmp(v, "0") != 0;
+  }
+  rc = srs_amd_pusch_chest_create(&p->chest, device);
   if (rc == SRS_AMD_OK) {
     rc = srs_amd_pusch_demodulator_create(&p->demod, device);
   }
@@ -193,6 +201,14 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
   dc.nof_tx_layers               = pdu->nof_tx_layers;
   dc.nof_rx_ports                = pdu->nof_rx_ports;
   dc.equalizer                   = proc->cfg.equalizer;
+  {
+    // the fused equalizer keeps at most two LSE slices per subcarrier in registers
+    const uint32_t nof_lse = c.td_interpolation == SRS_AMD_CHEST_TD_AVERAGE
+                                 ? 1u
+                                 : static_cast<uint32_t>(__builtin_popcount(c.symbols_mask & 0x3fffu));
+    const bool mmse = proc->cfg.equalizer == SRS_AMD_EQ_MMSE && pdu->nof_tx_layers > 1;
+    pl->fusable     = pusch_equalize_fusable(pdu->nof_rx_ports, pdu->nof_tx_layers, mmse, nof_lse);
+  }
   int rc = srs_amd_pusch_demod_plan_create(proc->demod, &dc, nof_subc, &pl->demod_plan, &pl->nof_re);
   if (rc != SRS_AMD_OK) {
     delete pl;
@@ -256,6 +272,9 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   }
   const uint32_t G            = plan->sch.cw_length;
   const bool     own_est      = io == nullptr || io->d_estimates == nullptr;
+  // Without a caller estimate buffer the equalizer rebuilds each RE's estimate from the estimator's
+  // per-subcarrier output (pusch_demod.hip pusch_equalize_fused_kernel): no estimate tensor in HBM.
+  const bool     fused        = own_est && plan->fusable && proc->fuse;
   const bool     own_llrs     = io == nullptr || io->d_llrs == nullptr;
   const uint64_t est_stride   = own_est ? P * L * plane : io->est_stride;
   const uint32_t llr_stride   = own_llrs ? static_cast<uint32_t>(align_up(G, 64)) : io->llr_stride;
@@ -265,7 +284,7 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   auto           s          = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(proc->mtx);
   hipError_t                  e = hipSetDevice(proc->device);
-  if (e == hipSuccess && own_est) {
+  if (e == hipSuccess && own_est && !fused) {
     e = proc->estimates.ensure(nof_grids * est_stride * 4);
   }
   if (e == hipSuccess) {
@@ -286,11 +305,22 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   srs_amd_chest_port_stats* st   = (io && io->d_port_stats) ? io->d_port_stats : proc->stats.as<srs_amd_chest_port_stats>();
   uint32_t*                 est  = own_est ? proc->estimates.as<uint32_t>() : io->d_estimates;
   int8_t*                   llrs = own_llrs ? proc->llrs.as<int8_t>() : io->d_llrs;
-  int rc = srs_amd_pusch_chest_estimate_batch(proc->chest, &plan->chest_cfg, d_grids, grid_stride, P, plan->nof_subc,
-                                              nof_grids, est, est_stride, st, stream);
-  if (rc == SRS_AMD_OK) {
-    rc = srs_amd_pusch_demodulate_batch(proc->demod, plan->demod_plan, d_grids, grid_stride, est, est_stride, st, llrs,
-                                        llr_stride, nof_grids, stream);
+  int rc;
+  if (fused) {
+    chest_args view;
+    rc = chest_estimate_batch_unexpanded(proc->chest, &plan->chest_cfg, d_grids, grid_stride, P, plan->nof_subc,
+                                         nof_grids, st, stream, &view);
+    if (rc == SRS_AMD_OK) {
+      rc = pusch_demodulate_batch_fused(proc->demod, plan->demod_plan, d_grids, grid_stride, view, st, llrs, llr_stride,
+                                        nof_grids, stream);
+    }
+  } else {
+    rc = srs_amd_pusch_chest_estimate_batch(proc->chest, &plan->chest_cfg, d_grids, grid_stride, P, plan->nof_subc,
+                                            nof_grids, est, est_stride, st, stream);
+    if (rc == SRS_AMD_OK) {
+      rc = srs_amd_pusch_demodulate_batch(proc->demod, plan->demod_plan, d_grids, grid_stride, est, est_stride, st,
+                                          llrs, llr_stride, nof_grids, stream);
+    }
   }
   if (rc == SRS_AMD_OK) {
     rc = srs_amd_pusch_decode_batch(proc->dec, &plan->sch, &plan->dec_cfg, d_tbs, tb_stride,

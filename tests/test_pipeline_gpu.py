@@ -33,7 +33,7 @@ def run():
     import bench_pipeline as bp
 
     dev = torch.device("cuda", 0)
-    pl = bp.Pipeline(2, dev, ul_layers=2)  # the reference chain runs PUSCH with at most 2 layers
+    pl = bp.Pipeline(2, dev, ul_layers=2, keep_estimates=True)  # the reference chain runs PUSCH with at most 2 layers
     stream = torch.cuda.current_stream(dev)
     pl.step(stream)
     torch.cuda.synchronize(dev)
@@ -117,7 +117,7 @@ def test_pipeline_four_layer_pusch():
     from tests.pusch_demod_cases import assert_llrs_close
 
     dev = torch.device("cuda", 0)
-    pl = bp.Pipeline(2, dev, ul_layers=4)
+    pl = bp.Pipeline(2, dev, ul_layers=4, keep_estimates=True)
     assert pl.ul_equalizer == "mmse"
     stream = torch.cuda.current_stream(dev)
     pl.step(stream)
@@ -147,3 +147,27 @@ def test_pipeline_four_layer_pusch():
         assert_llrs_close(llr, want, "cell %d LLRs (4 x 4 MMSE)" % c)
         assert res[c].data.tb_crc_ok == 1
         assert np.array_equal(pl.tb_rx[c].cpu().numpy(), pl.tb_ul[c].cpu().numpy()), c
+
+
+@pytest.mark.parametrize("ul_layers", [2, 4])
+def test_pipeline_fused_estimates_identical(ul_layers):
+    """The estimator-fused equalizer (no estimate tensor: the bench path) rebuilds every RE's channel
+    estimate with the expansion kernel's own operations, so its LLRs, transport blocks and results are
+    bit-identical to the path that writes and re-reads the expanded estimates."""
+    import torch
+
+    import bench_pipeline as bp
+
+    dev = torch.device("cuda", 0)
+    out = []
+    for keep in (True, False):
+        pl = bp.Pipeline(2, dev, ul_layers=ul_layers, keep_estimates=keep)
+        stream = torch.cuda.current_stream(dev)
+        pl.step(stream)
+        torch.cuda.synchronize(dev)
+        G = pl.plan_ul.cw_length
+        out.append((pl.llr_ul[:, :G].cpu().numpy(), pl.tb_rx.cpu().numpy(), pl.res_ul.cpu().numpy(),
+                    pl.stats_ul.cpu().numpy()))
+        del pl
+    for a, b, what in zip(out[0], out[1], ("LLRs", "transport blocks", "results", "port stats")):
+        assert np.array_equal(a, b), what

@@ -126,3 +126,36 @@ def test_pusch_processor_batch_matches_host():
         h_tb, h_res = proc.process(grids[i], plan)
         assert np.array_equal(out[i], h_tb) and np.array_equal(out[i], tbs_in[i])
         assert res[i].data.tb_crc_ok and res[i].data.ldpc_iterations_sum == h_res.data.ldpc_iterations_sum
+
+
+@pytest.mark.parametrize("td,mask,eq", [(0, (1 << 2) | (1 << 11), 0), (1, (1 << 2) | (1 << 11), 0),
+                                         (0, 1 << 2, 1), (0, (1 << 2) | (1 << 7) | (1 << 11), 0)],
+                         ids=["interp_2dmrs_zf", "average_2dmrs_zf", "interp_1dmrs_mmse", "interp_3dmrs_expanded"])
+def test_pusch_processor_fused_equalizer_identical(td, mask, eq):
+    """Without a caller estimate buffer the processor fuses the estimate expansion into the equalizer
+    (one or two LSE slices per subcarrier; three DM-RS symbols interpolated keep the expanded path): LLRs,
+    transport blocks and results are bit-identical to the run that writes the estimates."""
+    import torch
+
+    name, over, nprb, ch, snr, iters = CASES[3]
+    pdu = dict(BASE, **over, dmrs_symbol_mask=mask)
+    tbs = _tbs(pdu)
+    tb = np.random.default_rng(3).integers(0, 256, tbs // 8, dtype=np.uint8)
+    grids = np.stack([pp.ue_transmit(tb, pdu, 12 * nprb, channel=ch, snr_db=snr, seed=i)[0] for i in range(2)])
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=iters, td_interpolation=td, equalizer=eq),
+                              device=0)
+    plan = proc.plan(amd.make_pdu(**dict(pdu, tbs=tbs)), 12 * nprb)
+    g = torch.from_numpy(grids.view(np.int32)).to("cuda:0")
+    P, L = pdu["nof_rx_ports"], pdu["nof_tx_layers"]
+    G = plan.sch.cw_length
+    got = []
+    for keep in (True, False):
+        est = torch.zeros((2, P, L, 14, 12 * nprb), dtype=torch.int32, device="cuda:0") if keep else None
+        llrs = torch.zeros((2, (G + 63) // 64 * 64), dtype=torch.int8, device="cuda:0")
+        out, res = proc.process_batch(g, plan, estimates=est, llrs=llrs)
+        torch.cuda.synchronize()
+        got.append((llrs[:, :G].cpu().numpy(), out.cpu().numpy(), res.cpu().numpy()))
+    for a, b, what in zip(got[0], got[1], ("LLRs", "transport blocks", "results")):
+        assert np.array_equal(a, b), what
+    assert all(r.data.tb_crc_ok for r in amd.pusch_processor.parse_results(got[1][2]))
+    assert np.array_equal(got[1][1][0], tb)
