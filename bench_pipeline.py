@@ -39,7 +39,7 @@ UL_START, UL_NSYM = 0, 14
 RNTI, N_ID, SLOT = 0x4601, 500, 0
 SNR_DB = 35.0
 # near the decoding threshold (tools/snr_sweep.py, mean LDPC iterations ~4): per PUSCH layer count
-LOW_SNR_DB = {2: 23.8, 4: 31.0}
+LOW_SNR_DB = {2: 23.8, 4: 32.0}
 LDPC_ITERS = 6
 # DM-RS amplitude relative to data: convert_dB_to_amplitude(-get_sch_to_dmrs_ratio_dB(2)) = 10^(3/20),
 # evaluated in float as the reference (sch_dmrs_power.h, math_utils.h:118)

@@ -16,41 +16,19 @@
 // one launch without any sequential pass.
 #include <hip/hip_runtime.h>
 
+#include "demap_device.h"
 #include "gold_sequence.h"
 #include "modulation_args.h"
 
 #pragma clang fp contract(off)
 
 namespace srs_amd {
+using namespace demap;
 namespace {
-
-constexpr float NEAR_ZERO = 1e-9f;
 
 __device__ __forceinline__ unsigned get_bit(const uint8_t* b, unsigned p)
 {
   return (b[p >> 3] >> (7 - (p & 7))) & 1u;
-}
-
-__device__ __forceinline__ float safe_rcp(float nv)
-{
-  return nv > 0.0f ? 1.0f / nv : 0.0f;
-}
-
-// quantize_ps (avx2_helpers.h:121): scale, clip to +-120, round half to even.
-__device__ __forceinline__ int q_simd(float v, float range)
-{
-  float x = v * (120.0f / range);
-  x       = x > 120.0f ? 120.0f : x;
-  x       = x < -120.0f ? -120.0f : x;
-  x       = __builtin_rintf(x);
-  return x != x ? 0 : static_cast<int>(x);
-}
-
-// log_likelihood_ratio::quantize: clip to the range, round half away from zero.
-__device__ __forceinline__ int q_scalar(float v, float range)
-{
-  const float c = fabsf(v) > range ? copysignf(range, v) : v;
-  return static_cast<int>(roundf(c / range * 120.0f));
 }
 
 } // namespace
@@ -77,120 +55,6 @@ __global__ __launch_bounds__(256) void modulate_kernel(modulate_args a)
     v = reinterpret_cast<const float2*>(a.table)[idx];
   }
   reinterpret_cast<float2*>(a.symbols)[i] = v;
-}
-
-// LLRs of one symbol into o[0 .. max(qm, 1)); i: the symbol's index in its demodulation call (the
-// pi/2-BPSK rotation parity), simd: the symbol lies in the reference's AVX2 blocks.
-__device__ __forceinline__ void demap_symbol(const demodulate_args& a, const float* lt, float2 s, float nv, uint32_t i,
-                                             bool simd, int8_t* o)
-{
-  const float  xs[2] = {s.x, s.y};
-  constexpr float SQRT2 = 1.41421356237309504880f;
-  if (a.qm <= 1) { // BPSK / pi/2-BPSK: scalar code only
-    float re = s.x, im = s.y;
-    if (a.qm == 0 && (i & 1)) {
-      const float t = re;
-      re            = im;
-      im            = -t;
-    }
-    o[0] = static_cast<int8_t>(nv > 0.0f ? q_scalar(2.0f * SQRT2 * (re + im) / nv, 24.0f) : 0);
-    return;
-  }
-  if (a.qm == 2) {
-    const float GAIN = 2.0f * SQRT2;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      o[c] = static_cast<int8_t>(simd ? q_simd((GAIN * xs[c]) * safe_rcp(nv), 24.0f)
-                                      : (nv > 0.0f ? q_scalar(GAIN * xs[c] / nv, 24.0f) : 0));
-    }
-    return;
-  }
-  if (a.qm == 4) {
-    const float S = a.qam16_scale;
-    const float G = 4.0f * S, TH = 2.0f * S;
-    if (simd) {
-      const float rcp = safe_rcp(nv);
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const float x   = xs[c];
-        const float f   = G * x;
-        float       l01 = fabsf(x) > TH ? (2.0f * f - copysignf(0.8f, x)) : f;
-        float       l23 = 0.8f - fabsf(f);
-        l01 *= rcp;
-        l23 *= rcp;
-        if (fabsf(x) <= NEAR_ZERO) {
-          l01 = 0.0f;
-          l23 = 0.0f;
-        }
-        o[c]     = static_cast<int8_t>(q_simd(l01, 20.0f));
-        o[2 + c] = static_cast<int8_t>(q_simd(l23, 20.0f));
-      }
-    } else {
-      const bool zero = (s.x * s.x + s.y * s.y) < NEAR_ZERO;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const float x = xs[c];
-        if (zero || !(nv > 0.0f)) {
-          o[c]     = 0;
-          o[2 + c] = 0;
-          continue;
-        }
-        float l = G * x;
-        if (fabsf(x) > TH) {
-          l = __builtin_fmaf(2.0f, l, -copysignf(0.8f, x));
-        }
-        o[c]           = static_cast<int8_t>(q_scalar(l / nv, 20.0f));
-        const float l2 = __builtin_fmaf(-G, fabsf(x), 0.8f);
-        o[2 + c]       = static_cast<int8_t>(q_scalar(l2 / nv, 20.0f));
-      }
-    }
-    return;
-  }
-  // 64QAM / 256QAM: interval functions.
-  const int  m    = a.qm / 2;
-  const bool zero = !simd && (s.x * s.x + s.y * s.y) < NEAR_ZERO;
-  const float rcp = safe_rcp(nv);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) { // compile-time k: the table fields are scalar loads
-    if (k >= m) {
-      break;
-    }
-    const demod_interval_table& t = a.tab[k];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const float x = xs[c];
-      int         q;
-      if (zero) {
-        q = 0;
-      } else if (simd) {
-        int idx = static_cast<int>(floorf(x * t.inv_width)) + t.n / 2;
-        idx     = idx < 0 ? 0 : (idx > t.n - 1 ? t.n - 1 : idx);
-        float l = (lt[(2 * k) * 16 + idx] * x + lt[(2 * k + 1) * 16 + idx]) * rcp;
-        if (fabsf(x) <= NEAR_ZERO) {
-          l = 0.0f;
-        }
-        q = q_simd(l, 20.0f);
-      } else {
-        int idx = static_cast<int>(floorf(x / t.width)) + t.n / 2;
-        idx     = idx < 0 ? 0 : (idx > t.n - 1 ? t.n - 1 : idx);
-        float l = __builtin_fmaf(lt[(2 * k) * 16 + idx], x, lt[(2 * k + 1) * 16 + idx]);
-        l *= rcp;
-        q = q_scalar(l, 20.0f);
-      }
-      o[2 * k + c] = static_cast<int8_t>(q);
-    }
-  }
-}
-
-// The interval tables' slopes and intercepts ([k][slope, icpt][16]) into LDS: per-lane lookups at a
-// data-dependent interval would otherwise be loads from the kernel-argument segment.
-__device__ __forceinline__ void stage_interval_tables(const demodulate_args& a, float* lt)
-{
-  for (uint32_t x = threadIdx.x; x < 4 * 2 * 16; x += blockDim.x) {
-    const uint32_t k = x / 32, w = (x / 16) % 2, j = x % 16;
-    lt[x]            = w == 0 ? a.tab[k].slope[j] : a.tab[k].icpt[j];
-  }
-  __syncthreads();
 }
 
 __global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
@@ -309,6 +173,31 @@ __global__ __launch_bounds__(256) void descramble_llrs_kernel(prbs_args a)
     const int v   = a.in_llrs[i];
     a.out_llrs[i] = static_cast<int8_t>(((c >> b) & 1u) ? -v : v);
   }
+}
+
+// Words 0 .. nof_words of the Gold sequence of c_init (c(32 w + b) at bit b of word w): the PUSCH
+// equalizer's descrambling table (pusch_demod.hip), generated once per demodulator plan.
+__global__ __launch_bounds__(256) void gold_words_kernel(const uint32_t* jump, uint32_t c_init, uint32_t* out,
+                                                         uint32_t nof_words)
+{
+  const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+  uint32_t       x1, x2;
+  gold_state_wave(jump, c_init, (w - (threadIdx.x & 63u)) * 32, (threadIdx.x & 63u) * 32, x1, x2);
+  const uint32_t c = gold_next32(x1, x2);
+  if (w < nof_words) {
+    out[w] = c;
+  }
+}
+
+hipError_t launch_gold_words(const uint32_t* jump, uint32_t c_init, uint32_t* out, uint32_t nof_words,
+                             hipStream_t stream)
+{
+  if (nof_words == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(gold_words_kernel, dim3((nof_words + 255) / 256), dim3(256), 0, stream, jump, c_init, out,
+                     nof_words);
+  return hipGetLastError();
 }
 
 hipError_t launch_modulate(const modulate_args& a, hipStream_t stream)

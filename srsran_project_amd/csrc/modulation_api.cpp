@@ -557,6 +557,20 @@ demodulate_args srs_amd::demodulate_args_for(const srs_amd_modulator* mod, int q
   return a;
 }
 
+uint32_t srs_amd::demap_symbol_bounds(int qm, const uint32_t* sym_counts, uint32_t* sym_lo, uint32_t* simd_hi)
+{
+  // one demapper call per OFDM symbol: SIMD blocks of avx2_block(qm) symbols from each symbol's start
+  const uint32_t blk = avx2_block(qm);
+  uint32_t       s0  = 0;
+  for (int l = 0; l < 14; ++l) {
+    const uint32_t n = sym_counts[l];
+    sym_lo[l]        = s0;
+    simd_hi[l]       = s0 + (blk ? (n / blk) * blk : 0);
+    s0 += n;
+  }
+  return s0;
+}
+
 int srs_amd::demap_descramble_batch(srs_amd_modulator* mod, int qm, int8_t* d_llrs, uint64_t llr_stride,
                                     const float* d_symbols, const float* d_noise_vars, uint32_t grid_symbols,
                                     const uint32_t* sym_counts, uint32_t nof_grids, const uint32_t* d_jump,
@@ -575,15 +589,7 @@ int srs_amd::demap_descramble_batch(srs_amd_modulator* mod, int qm, int8_t* d_ll
   d.llr_stride   = llr_stride;
   d.grid_symbols = grid_symbols;
   d.c_init       = c_init;
-  // one demapper call per OFDM symbol: SIMD blocks of avx2_block(qm) symbols from each symbol's start
-  const uint32_t blk = avx2_block(qm);
-  uint32_t       s0  = 0;
-  for (int l = 0; l < 14; ++l) {
-    const uint32_t n = sym_counts[l];
-    d.sym_lo[l]      = s0;
-    d.simd_hi[l]     = s0 + (blk ? (n / blk) * blk : 0);
-    s0 += n;
-  }
+  const uint32_t s0 = demap_symbol_bounds(qm, sym_counts, d.sym_lo, d.simd_hi);
   if (s0 != grid_symbols) {
     return fail(SRS_AMD_EINVAL, "per-symbol counts (%u) do not add up to the grid symbols (%u)", s0, grid_symbols);
   }

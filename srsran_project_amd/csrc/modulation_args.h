@@ -66,6 +66,9 @@ struct demap_descramble_args {
 };
 hipError_t launch_demap_descramble(const demodulate_args& a, const demap_descramble_args& d, uint32_t nof_grids,
                                    hipStream_t stream);
+// Gold-sequence words 0 .. nof_words of c_init into out (c(32 w + b) at bit b of word w).
+hipError_t launch_gold_words(const uint32_t* jump, uint32_t c_init, uint32_t* out, uint32_t nof_words,
+                             hipStream_t stream);
 
 } // namespace srs_amd
 
@@ -75,6 +78,9 @@ namespace srs_amd {
 
 // Demapper arguments (tables, AVX2 block end) for calls of nof_symbols symbols (modulation_api.cpp).
 demodulate_args demodulate_args_for(const srs_amd_modulator* mod, int qm, uint32_t nof_symbols);
+// The reference demaps each OFDM symbol in its own call: per OFDM symbol l (sym_counts[l] demapper symbols),
+// its first symbol sym_lo[l] and the end of its SIMD blocks simd_hi[l]; returns the total.
+uint32_t demap_symbol_bounds(int qm, const uint32_t* sym_counts, uint32_t* sym_lo, uint32_t* simd_hi);
 
 // Soft demapping of nof_grids x grid_symbols symbols and descrambling of each grid's LLRs with the
 // Gold sequence of c_init, one launch (the PUSCH demodulator's last two steps).

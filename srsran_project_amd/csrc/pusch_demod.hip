@@ -18,21 +18,89 @@
 #include <hip/hip_runtime.h>
 
 #include "chest_device.h"
+#include "demap_device.h"
 #include "equalizer_device.h"
 #include "pusch_demod_args.h"
 
 namespace srs_amd {
 namespace {
 
-// Equalizes data RE j of grid gi from its received samples y[P] and channel coefficients h[P][L] and writes
-// [j][layer] symbols and variances.
-template <int P, int L, bool MMSE>
-__device__ __forceinline__ void equalize_write(const pusch_eq_args& a, uint32_t gi, uint32_t j, const eq::cplx* y,
-                                               const eq::cplx* h)
+// Soft demapping and descrambling of the QM LLRs of codeword symbol i (= j L + layer) into the grid's LLR row:
+// demap_device.h's demapper (the SIMD or scalar arithmetic by the symbol's place in its OFDM symbol, as the
+// reference's per-OFDM-symbol demapper calls), the sign flipped where the Gold sequence bit is one.
+template <int QM>
+__device__ __forceinline__ void emit_symbol_llrs(const pusch_eq_args& a, const float* lt, int8_t* row, uint32_t i,
+                                                 bool simd, float2 s, float nv)
 {
-  const srs_amd_chest_port_stats* st  = a.stats + gi * P;
-  const uint64_t                  out = static_cast<uint64_t>(gi) * a.nof_re * L + static_cast<uint64_t>(j) * L;
-  if (L == 1) {
+  int8_t o[8];
+  demap::demap_symbol(a.dm, lt, s, nv, i, simd, o);
+  const uint32_t n0 = i * QM;
+  const uint64_t cc = static_cast<uint64_t>(a.scr[n0 / 32]) | (static_cast<uint64_t>(a.scr[n0 / 32 + 1]) << 32);
+  const uint32_t c  = static_cast<uint32_t>(cc >> (n0 % 32));
+  uint64_t       v  = 0;
+#pragma unroll
+  for (int k = 0; k < QM; ++k) {
+    const int x = ((c >> k) & 1u) ? -o[k] : o[k];
+    v |= static_cast<uint64_t>(static_cast<uint8_t>(x)) << (8 * k);
+  }
+  int8_t* dst = row + n0;
+  if constexpr (QM == 8) {
+    *reinterpret_cast<uint2*>(dst) = make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
+  } else if constexpr (QM == 6) {
+    uint16_t* d16 = reinterpret_cast<uint16_t*>(dst); // i * 6 is even
+    d16[0]        = static_cast<uint16_t>(v);
+    d16[1]        = static_cast<uint16_t>(v >> 16);
+    d16[2]        = static_cast<uint16_t>(v >> 32);
+  } else if constexpr (QM == 4) {
+    *reinterpret_cast<uint32_t*>(dst) = static_cast<uint32_t>(v);
+  } else if constexpr (QM == 2) {
+    *reinterpret_cast<uint16_t*>(dst) = static_cast<uint16_t>(v);
+  } else {
+    *dst = static_cast<int8_t>(v);
+  }
+}
+
+// The L equalized symbols of data RE j (OFDM symbol l) of grid gi straight to LLRs.
+template <int L>
+__device__ __forceinline__ void emit_llrs(const pusch_eq_args& a, const float* lt, uint32_t gi, uint32_t j, uint32_t l,
+                                          const float2 (&s)[L], const float (&nv)[L])
+{
+  int8_t*        row     = a.llrs + static_cast<uint64_t>(gi) * a.llr_stride;
+  const uint32_t simd_hi = a.simd_hi[l];
+#pragma unroll
+  for (int v = 0; v < L; ++v) {
+    const uint32_t i    = j * L + v;
+    const bool     simd = i < simd_hi;
+    switch (a.dm.qm) {
+      case 8:
+        emit_symbol_llrs<8>(a, lt, row, i, simd, s[v], nv[v]);
+        break;
+      case 6:
+        emit_symbol_llrs<6>(a, lt, row, i, simd, s[v], nv[v]);
+        break;
+      case 4:
+        emit_symbol_llrs<4>(a, lt, row, i, simd, s[v], nv[v]);
+        break;
+      case 2:
+        emit_symbol_llrs<2>(a, lt, row, i, simd, s[v], nv[v]);
+        break;
+      default:
+        emit_symbol_llrs<1>(a, lt, row, i, simd, s[v], nv[v]);
+        break;
+    }
+  }
+}
+
+// Equalizes data RE j (OFDM symbol l) of grid gi from its received samples y[P] and channel coefficients
+// h[P][L], then demaps and descrambles the L symbols into the grid's LLR row (no symbol round trip via HBM).
+template <int P, int L, bool MMSE>
+__device__ __forceinline__ void equalize_write(const pusch_eq_args& a, const float* lt, uint32_t gi, uint32_t j,
+                                               uint32_t l, const eq::cplx* y, const eq::cplx* h)
+{
+  const srs_amd_chest_port_stats* st = a.stats + gi * P;
+  float2                          so[L];
+  float                           nvo[L];
+  if constexpr (L == 1) {
     eq::cplx h0[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -48,8 +116,8 @@ __device__ __forceinline__ void equalize_write(const pusch_eq_args& a, uint32_t 
     eq::cplx s;
     float    nv;
     eq::equalize_1xn<P>(y, h0, nvp, valid, 1.0f, s, nv);
-    a.eq_symbols[out]    = make_float2(s.x, s.y);
-    a.eq_noise_vars[out] = nv;
+    so[0]  = make_float2(s.x, s.y);
+    nvo[0] = nv;
   } else {
     // channel_equalizer_generic_impl.cpp:304: the largest port variance (std::max_element order).
     float nmax = st[0].noise_var;
@@ -68,26 +136,29 @@ __device__ __forceinline__ void equalize_write(const pusch_eq_args& a, uint32_t 
       float4 s;
       float2 nv;
       eq::equalize_2xn<P>(y, h0, h1, nmax, ok, 1.0f, s, nv);
-      a.eq_symbols[out]        = make_float2(s.x, s.y);
-      a.eq_symbols[out + 1]    = make_float2(s.z, s.w);
-      a.eq_noise_vars[out]     = nv.x;
-      a.eq_noise_vars[out + 1] = nv.y;
+      so[0]  = make_float2(s.x, s.y);
+      so[1]  = make_float2(s.z, s.w);
+      nvo[0] = nv.x;
+      nvo[1] = nv.y;
     } else {
       eq::cplx s[L];
       float    nv[L];
       eq::equalize_mimo<P, L, MMSE>(y, h, nmax, ok, 1.0f, s, nv);
 #pragma unroll
-      for (int l = 0; l < L; ++l) {
-        a.eq_symbols[out + l]    = make_float2(s[l].x, s[l].y);
-        a.eq_noise_vars[out + l] = nv[l];
+      for (int v = 0; v < L; ++v) {
+        so[v]  = make_float2(s[v].x, s[v].y);
+        nvo[v] = nv[v];
       }
     }
   }
+  emit_llrs<L>(a, lt, gi, j, l, so, nvo);
 }
 
 template <int P, int L, bool MMSE>
 __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
 {
+  __shared__ float lt[4 * 2 * 16];
+  demap::stage_interval_tables(a.dm, lt);
   const uint32_t  l   = a.first_symbol + blockIdx.y;
   const uint32_t  sc  = a.first_subc + blockIdx.x * 256 + threadIdx.x;
   const uint32_t  gi  = blockIdx.z;
@@ -114,7 +185,7 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
       h[p * L + l] = eq::from_cbf16(est[static_cast<uint64_t>(p * L + l) * plane]);
     }
   }
-  equalize_write<P, L, MMSE>(a, gi, j, y, h);
+  equalize_write<P, L, MMSE>(a, lt, gi, j, l, y, h);
 }
 
 // Estimator-fused form: one thread per (grid, subcarrier, half of the OFDM symbols) rebuilds the channel
@@ -128,6 +199,8 @@ __global__ __launch_bounds__(256) void pusch_equalize_fused_kernel(pusch_eq_args
 {
   __shared__ float2 s_ph[P][CH_NSYMB];
   __shared__ int    s_rot[P];
+  __shared__ float  lt[4 * 2 * 16];
+  demap::stage_interval_tables(a.dm, lt); // (synchronizes)
   const uint32_t    gi = blockIdx.z;
   if (threadIdx.x < P * CH_NSYMB) {
     const uint32_t p   = threadIdx.x / CH_NSYMB, n = threadIdx.x % CH_NSYMB;
@@ -178,7 +251,7 @@ __global__ __launch_bounds__(256) void pusch_equalize_fused_kernel(pusch_eq_args
         h[p * L + v]     = eq::from_cbf16(u);
       }
     }
-    equalize_write<P, L, MMSE>(a, gi, j, y, h);
+    equalize_write<P, L, MMSE>(a, lt, gi, j, l, y, h);
   }
 }
 

@@ -56,10 +56,12 @@ struct srs_amd_pusch_demod_plan {
   uint32_t      c_init      = 0;
   uint32_t      sym_counts[14] = {}; // demapper symbols (data REs x layers) per OFDM symbol
   uint32_t*     d_table     = nullptr;
+  uint32_t*     d_scr       = nullptr; // Gold words of c_init over the codeword (+1)
   ~srs_amd_pusch_demod_plan()
   {
     (void)hipSetDevice(device);
     (void)hipFree(d_table);
+    (void)hipFree(d_scr);
   }
   uint32_t nof_llrs() const { return args.nof_re * nof_layers * (qm < 2 ? 1u : static_cast<uint32_t>(qm)); }
 };
@@ -134,46 +136,24 @@ static int demodulate_impl(srs_amd_pusch_demodulator*      dem,
       return fail(SRS_AMD_EINVAL, "channel estimator output does not match the demodulator plan");
     }
   }
-  const size_t nsym  = static_cast<size_t>(nof_grids) * plan->args.nof_re * plan->nof_layers;
-  const size_t bytes = align_up(nsym * 8, 256) + align_up(nsym * 4, 256);
-  std::lock_guard<std::mutex> lock(dem->mtx);
-  hipError_t                  e = hipSetDevice(dem->device);
-  if (e == hipSuccess) {
-    e = dem->scratch.ensure(bytes);
-  }
-  if (e != hipSuccess) {
-    return hip_fail(e, "PUSCH demodulator scratch");
-  }
-  auto*         base = dem->scratch.as<uint8_t>();
-  pusch_eq_args a    = plan->args;
-  a.grids            = d_grids;
-  a.grid_stride      = grid_stride;
-  a.estimates        = d_estimates;
-  a.est_stride       = est_stride;
-  a.stats            = d_stats;
-  a.eq_symbols       = reinterpret_cast<float2*>(base);
-  a.eq_noise_vars    = reinterpret_cast<float*>(base + align_up(nsym * 8, 256));
-  auto s             = static_cast<hipStream_t>(stream);
-  e                  = dem->order.begin(s);
+  // the equalizer demaps and descrambles its own symbols: LLRs straight into the caller's rows, no scratch
+  hipError_t    e = hipSetDevice(dem->device);
+  pusch_eq_args a = plan->args;
+  a.grids         = d_grids;
+  a.grid_stride   = grid_stride;
+  a.estimates     = d_estimates;
+  a.est_stride    = est_stride;
+  a.stats         = d_stats;
+  a.llrs          = d_llrs;
+  a.llr_stride    = llr_stride;
+  auto s          = static_cast<hipStream_t>(stream);
   if (e == hipSuccess) {
     e = fused != nullptr ? launch_pusch_equalize_fused(a, *fused, plan->nof_ports, plan->nof_layers, plan->mmse,
                                                        plan->span_subc, nof_grids, s)
                          : launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->mmse, plan->nof_symbols,
                                                  plan->span_subc, nof_grids, s);
   }
-  if (e != hipSuccess) {
-    return hip_fail(e, "pusch_equalize_kernel launch");
-  }
-  // soft demapper + descrambling (revert_scrambling) in one pass: LLRs straight into the caller's rows
-  int rc = demap_descramble_batch(dem->demapper, plan->qm, d_llrs, llr_stride,
-                                  reinterpret_cast<const float*>(a.eq_symbols), a.eq_noise_vars,
-                                  static_cast<uint32_t>(plan->args.nof_re * plan->nof_layers), plan->sym_counts,
-                                  nof_grids, dem->d_jump, plan->c_init, stream);
-  if (rc != SRS_AMD_OK) {
-    return rc;
-  }
-  e = dem->order.end(s);
-  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH demodulator completion event");
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_equalize_kernel launch");
 }
 
 int srs_amd::pusch_demodulate_batch_fused(::srs_amd_pusch_demodulator*      dem,
@@ -322,7 +302,25 @@ int srs_amd_pusch_demod_plan_create(srs_amd_pusch_demodulator*        dem,
     return hip_fail(e, "PUSCH demodulator plan");
   }
   a.re_table = p->d_table;
-  *plan      = p;
+  // demapper tables, per-OFDM-symbol SIMD bounds and the descrambling words of the equalizer's LLR output
+  const uint32_t grid_symbols = count * cfg->nof_tx_layers;
+  a.dm                        = demodulate_args_for(dem->demapper, qm, grid_symbols);
+  uint32_t sym_lo[14];
+  (void)demap_symbol_bounds(qm, p->sym_counts, sym_lo, a.simd_hi);
+  const uint32_t nof_words = (p->nof_llrs() + 31) / 32 + 1;
+  e                        = hipMalloc(&p->d_scr, nof_words * sizeof(uint32_t));
+  if (e == hipSuccess) {
+    e = launch_gold_words(dem->d_jump, p->c_init, p->d_scr, nof_words, nullptr);
+  }
+  if (e == hipSuccess) {
+    e = hipStreamSynchronize(nullptr);
+  }
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "PUSCH demodulator plan scrambling words");
+  }
+  a.scr = p->d_scr;
+  *plan = p;
   if (nof_re != nullptr) {
     *nof_re = count;
   }

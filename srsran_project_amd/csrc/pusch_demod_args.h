@@ -8,6 +8,7 @@
 
 #include "srsran_amd/pusch_chest.h"
 #include "srsran_amd/pusch_demodulator.h"
+#include "modulation_args.h"
 #include "pusch_chest_args.h"
 
 namespace srs_amd {
@@ -17,8 +18,6 @@ struct pusch_eq_args {
   const uint32_t*                 estimates; // cbf16 [grid][port][layer][14][subc]
   const srs_amd_chest_port_stats* stats;     // [grid][port]
   const uint32_t*                 re_table;  // [14][nof_prb]: data RE index << 12 | 12-bit mask
-  float2*                         eq_symbols;    // [grid][nof_re][layer]
-  float*                          eq_noise_vars; // [grid][nof_re][layer]
   uint64_t                        grid_stride;
   uint64_t                        est_stride;
   uint32_t                        nof_subc;
@@ -26,6 +25,14 @@ struct pusch_eq_args {
   uint32_t                        nof_re;
   uint32_t                        first_symbol;
   uint32_t                        first_subc;
+  // demapping + descrambling in the equalizer: LLR n of a grid at llrs[grid * llr_stride + n], codeword
+  // symbol i = j L + layer of data RE j; scr: Gold words of the plan's c_init (c(n) at bit n % 32 of word
+  // n / 32, one word past the codeword); symbols i < simd_hi[l] of OFDM symbol l take the SIMD demapper
+  int8_t*                         llrs;
+  const uint32_t*                 scr;
+  uint64_t                        llr_stride;
+  uint32_t                        simd_hi[14];
+  demodulate_args                 dm;
 };
 
 
