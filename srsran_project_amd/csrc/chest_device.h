@@ -53,40 +53,46 @@ __device__ __forceinline__ bool cfo_rotates(const chest_args& a, const float* ac
   return a.compensate_cfo && acc[3] != 0.0f;
 }
 
-// The cbf16 estimate of symbol l of a subcarrier inside the allocation from its LSE slices x[0 .. nof_lse):
-// the time-domain strategy (average or interpolation), bf16 rounding, then the CFO rotation and a second
-// rounding (do_compute, port_channel_estimator_average_impl.cpp:184-193 / 390-440).
-template <int NLSE>
-__device__ __forceinline__ uint32_t expand_value(const chest_args& a, const float2 (&x)[NLSE], uint32_t l, bool rot,
-                                                 float2 ph)
+// The cbf16 estimate of symbol l of a subcarrier inside the allocation from the LSE slices it reads
+// (x0 = slice i0 of the symbol -- td_i0[l], 0 when averaging -- and x1 = slice i0 + 1): the time-domain
+// strategy (average or interpolation), bf16 rounding, then the CFO rotation and a second rounding
+// (do_compute, port_channel_estimator_average_impl.cpp:184-193 / 390-440).
+__device__ __forceinline__ uint32_t expand_pair(const chest_args& a, float2 x0, float2 x1, uint32_t l, bool rot,
+                                                float2 ph)
 {
-  float2 e;
-  if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
-    e = x[0];
-  } else {
-    auto lse = [&](int i) { // x[i] without dynamic register indexing
-      float2 r = x[0];
-#pragma unroll
-      for (int s = 1; s < NLSE; ++s) {
-        r = i == s ? x[s] : r;
-      }
-      return r;
-    };
-    const int    i0 = a.td_i0[l];
-    const float2 x0 = lse(i0);
-    if (a.td_interp[l]) {
-      const float2 x1 = lse(i0 + 1);
-      const float  w  = a.td_w[l];
-      e               = make_float2(__builtin_fmaf(x1.x - x0.x, w, x0.x), __builtin_fmaf(x1.y - x0.y, w, x0.y));
-    } else {
-      e = x0;
-    }
+  float2 e = x0;
+  if (a.td != SRS_AMD_CHEST_TD_AVERAGE && a.td_interp[l]) {
+    const float w = a.td_w[l];
+    e             = make_float2(__builtin_fmaf(x1.x - x0.x, w, x0.x), __builtin_fmaf(x1.y - x0.y, w, x0.y));
   }
   uint32_t out = to_cbf16(e);
   if (rot) {
     out = to_cbf16(cmul(from_cbf16(out), ph));
   }
   return out;
+}
+
+// Slice index i0 of symbol l (the first of the two expand_pair reads).
+__device__ __forceinline__ int lse_index(const chest_args& a, uint32_t l)
+{
+  return a.td == SRS_AMD_CHEST_TD_AVERAGE ? 0 : a.td_i0[l];
+}
+
+// expand_pair with every LSE slice of the subcarrier in registers (x[0 .. nof_lse)).
+template <int NLSE>
+__device__ __forceinline__ uint32_t expand_value(const chest_args& a, const float2 (&x)[NLSE], uint32_t l, bool rot,
+                                                 float2 ph)
+{
+  auto lse = [&](int i) { // x[i] without dynamic register indexing
+    float2 r = x[0];
+#pragma unroll
+    for (int s = 1; s < NLSE; ++s) {
+      r = i == s ? x[s] : r;
+    }
+    return r;
+  };
+  const int i0 = lse_index(a, l);
+  return expand_pair(a, lse(i0), lse(i0 + 1), l, rot, ph);
 }
 
 } // namespace chdev

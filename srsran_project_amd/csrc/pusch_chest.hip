@@ -1,25 +1,21 @@
 // pusch_chest.hip -- MI355X PUSCH DM-RS channel estimator (dmrs_pusch_estimator_impl
 // + port_channel_estimator_average_impl, DM-RS type 1, one hop).
 //
-// Three launches per batch of grids:
-//   chest_pilot_kernel   one 1024-thread workgroup per (grid, rx port). The DM-RS
-//                        Gold words of every DM-RS symbol are generated into LDS
-//                        (jump-ahead, one word per thread); thread t owns pilots
-//                        t and t + 1024 and keeps their received values in
-//                        registers. Per layer: LSE (rx * conj(pilot)), CFO from
-//                        the first two DM-RS symbols (block reduction), CFO
-//                        compensation and time accumulation, CDM pair averaging
-//                        (lane shuffle), scaling, FD smoothing in LDS (mean, or
-//                        virtual pilots + raised-cosine FIR), RSRP, linear
-//                        interpolation to every RE of the allocation; then the
-//                        noise energy per CDM group
-//                        (port_channel_estimator_average_impl.cpp:130-506).
-//   chest_ta_kernel<N>   one workgroup per (grid, port): the N-point IDFT of every
-//                        (layer, LSE symbol) slice of smoothed pilots with the
-//                        fused Stockham engine, |.|^2 accumulated in LDS, peak
-//                        search and quadratic refinement
-//                        (time_alignment_estimator_dft_impl.cpp:122-310), and the
-//                        per-port measurements (noise variance, EPRE, RSRP, SNR, CFO).
+// Six launches per batch of grids (the last only when the per-RE estimates are wanted):
+//   chest_seq_kernel     one workgroup: the DM-RS Gold words of the batch (jump-ahead) for the kernels below.
+//   chest_cfo_kernel     one workgroup per (grid, rx port): EPRE and the CFO from the first two DM-RS symbols.
+//   chest_slice_kernel   one 256-thread workgroup per (grid, rx port, slice = layer x LSE symbol), so the
+//                        slices of a port run concurrently. DM-RS Gold words into LDS (jump-ahead);
+//                        LSE (rx * conj(pilot)), CFO compensation and time accumulation, CDM
+//                        pair averaging (lane shuffle), scaling, FD smoothing in LDS (mean, or virtual
+//                        pilots + raised-cosine FIR), the slice's RSRP share, linear interpolation to
+//                        every RE of the allocation (port_channel_estimator_average_impl.cpp:130-506).
+//   chest_ta_kernel<N>   one workgroup per (grid, port, slice): the N-point IDFT of the slice's smoothed
+//                        pilots with the fused Stockham engine, |.|^2 into the slice's correlation row
+//                        (time_alignment_estimator_dft_impl.cpp:122-200).
+//   chest_stats_kernel   one workgroup per (grid, port): noise energy per CDM group, the correlations
+//                        summed, peak search and quadratic refinement (:248-310), and the per-port
+//                        measurements (noise variance, EPRE, RSRP, SNR, CFO).
 //   chest_expand_kernel  one thread per (subcarrier, port, layer), every symbol: the time-domain strategy
 //                        (average or interpolation between DM-RS symbols), bf16
 //                        rounding and the CFO phase of the symbol -- the only
@@ -62,23 +58,6 @@ __device__ __forceinline__ float2 csub(float2 a, float2 b)
 __device__ __forceinline__ float2 cscale(float2 a, float s)
 {
   return make_float2(a.x * s, a.y * s);
-}
-
-// rx[g][d][k] with runtime indices through selects (no dynamic register indexing).
-__device__ __forceinline__ float2 rx_sel(const float2 (&rx)[2][CH_MAXDMRS][CH_PPT], int g, int d, int k)
-{
-  float2 r = rx[0][0][0];
-#pragma unroll
-  for (int gg = 0; gg < 2; ++gg) {
-#pragma unroll
-    for (int dd = 0; dd < CH_MAXDMRS; ++dd) {
-#pragma unroll
-      for (int kk = 0; kk < CH_PPT; ++kk) {
-        r = (gg == g && dd == d && kk == k) ? rx[gg][dd][kk] : r;
-      }
-    }
-  }
-  return r;
 }
 
 // Sum of 4 floats over the workgroup (result broadcast). red: >= 4 * 16 floats.
@@ -172,76 +151,82 @@ __device__ void virtual_pilots(float2* out, const float2* in, int n, bool is_sta
   }
 }
 
-__global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
+// Words of the DM-RS Gold sequences (bits 2 x 6 x prb_lo .. of every DM-RS symbol), shared by every grid
+// and port of the batch.
+__device__ __forceinline__ uint32_t dmrs_nof_words(const chest_args& a, uint32_t& w_first)
+{
+  const uint32_t bit_first = 12u * a.prb_lo;
+  w_first                  = bit_first / 32;
+  return (bit_first + 2 * a.npil + 31) / 32 - w_first;
+}
+
+// One workgroup: the DM-RS Gold words of the batch (jump-ahead, one word per thread) into a.dmrs_seq.
+__global__ __launch_bounds__(CS_THREADS) void chest_seq_kernel(chest_args a)
+{
+  uint32_t       w_first;
+  const uint32_t nwords = dmrs_nof_words(a, w_first);
+  for (uint32_t i = threadIdx.x; i < nwords * a.nds; i += CS_THREADS) {
+    const uint32_t d = i / nwords, w = i % nwords;
+    a.dmrs_seq[d * CH_SEQWORDS + w] = gold_word(a.jump, a.c_init[d], 32 * (w_first + w));
+  }
+}
+
+// The batch's DM-RS words into LDS; returns the bit offset of the first allocated pilot in word 0.
+__device__ __forceinline__ uint32_t dmrs_words(const chest_args& a, uint32_t (*seq)[CH_SEQWORDS])
+{
+  uint32_t       w_first;
+  const uint32_t nwords = dmrs_nof_words(a, w_first);
+  for (uint32_t i = threadIdx.x; i < nwords * a.nds; i += blockDim.x) {
+    const uint32_t d = i / nwords, w = i % nwords;
+    seq[d][w]        = a.dmrs_seq[d * CH_SEQWORDS + w];
+  }
+  return 12u * a.prb_lo - 32 * w_first;
+}
+
+// One workgroup per (grid, rx port): EPRE over every received DM-RS RE and the CFO from the first two DM-RS
+// symbols over every layer of every CDM group (preprocess_pilots_and_estimate_cfo, :390-445), for the
+// slice workgroups of the port.
+__global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a)
 {
   __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
-  __shared__ float2   enl_in[CH_MAXPIL + 2 * CH_MAXV];
-  __shared__ float2   enl_out[CH_MAXPIL + 2 * CH_MAXV];
   __shared__ float    red[4 * 16];
-  __shared__ float    s_cfo;
-  __shared__ int      s_has_cfo;
-  __shared__ float2   s_rot[CH_MAXDMRS];
-  __shared__ float2   s_rot_fwd[CH_MAXDMRS];
-  __shared__ uint32_t s_rx[2][CH_MAXDMRS][CH_MAXPIL]; // received pilots (cbf16) of every CDM group / DM-RS symbol
-
-  const uint32_t gp   = blockIdx.x; // grid * nof_ports + port
-  const uint32_t grid = gp / a.nof_ports;
-  const uint32_t port = gp % a.nof_ports;
-  const uint32_t tid  = threadIdx.x;
-  const uint32_t npil = a.npil;
-  const int      nds  = static_cast<int>(a.nds);
-  const int      L    = static_cast<int>(a.L);
-
-  // DM-RS Gold words: sequence bits 2 * 6 * prb_lo .. of every DM-RS symbol.
-  const uint32_t bit_first = 12u * a.prb_lo;
-  const uint32_t w_first   = bit_first / 32;
-  const uint32_t nwords    = (bit_first + 2 * npil + 31) / 32 - w_first;
-  for (uint32_t i = tid; i < nwords * static_cast<uint32_t>(nds); i += CH_THREADS) {
-    const uint32_t d = i / nwords, w = i % nwords;
-    seq[d][w]        = gold_word(a.jump, a.c_init[d], 32 * (w_first + w));
-  }
-  const uint32_t bit0 = bit_first - 32 * w_first;
-
-  // Received pilots of the owned indices: rx[g][d][k] at subcarrier 12 prb_lo + 2m + g.
-  const uint32_t* gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc;
-  // kept in LDS as the raw cbf16 words (lossless) rather than registers: the 1024-thread workgroup
-  // has 128 VGPRs per lane, and 32 of them for the pilots made the kernel spill to scratch
-  auto rxv = [&](int g, int d, int k) { return from_cbf16(s_rx[g][d][tid + k * CH_THREADS]); };
-  float           epre = 0;
+  const uint32_t      gp   = blockIdx.x;
+  const uint32_t      grid = gp / a.nof_ports;
+  const uint32_t      port = gp % a.nof_ports;
+  const uint32_t      tid  = threadIdx.x;
+  const uint32_t      npil = a.npil;
+  const int           nds  = static_cast<int>(a.nds);
+  const int           L    = static_cast<int>(a.L);
+  const uint32_t      bit0 = dmrs_words(a, seq);
+  const uint32_t*     gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc +
+                          12 * a.prb_lo;
+  auto rxv = [&](int gg, int d, uint32_t m) { return from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + gg]); };
+  float epre = 0;
 #pragma unroll
-  for (int k = 0; k < CH_PPT; ++k) {
-    const uint32_t m = tid + k * CH_THREADS;
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-#pragma unroll
-      for (int d = 0; d < CH_MAXDMRS; ++d) {
-        uint32_t u = 0;
-        if (m < npil && d < nds && g < static_cast<int>(a.ncdm)) {
-          u              = gridp[a.dmrs_sym[d] * a.nsubc + 12 * a.prb_lo + 2 * m + g];
-          const float2 v = from_cbf16(u);
-          epre           = __builtin_fmaf(v.x, v.x, __builtin_fmaf(v.y, v.y, epre));
-        }
-        if (m < CH_MAXPIL) {
-          s_rx[g][d][m] = u;
+  for (int k = 0; k < CS_PPT; ++k) {
+    const uint32_t m = tid + k * CS_THREADS;
+    if (m < npil) {
+      for (int gg = 0; gg < static_cast<int>(a.ncdm); ++gg) {
+        for (int d = 0; d < nds; ++d) {
+          const float2 u = rxv(gg, d, m);
+          epre           = __builtin_fmaf(u.x, u.x, __builtin_fmaf(u.y, u.y, epre));
         }
       }
     }
   }
   __syncthreads(); // seq ready
-
-  // CFO from the first two DM-RS symbols (preprocess_pilots_and_estimate_cfo, :390-445).
+  float4 acc = make_float4(0, 0, 0, 0); // (re, im) of CDM group 0, then 1
   if (nds >= 2) {
-    float4 acc = make_float4(0, 0, 0, 0); // (re, im) of CDM group 0, then 1
 #pragma unroll
-    for (int k = 0; k < CH_PPT; ++k) {
-      const uint32_t m = tid + k * CH_THREADS;
+    for (int k = 0; k < CS_PPT; ++k) {
+      const uint32_t m = tid + k * CS_THREADS;
       if (m < npil) {
-        for (int v = 0; v < L; ++v) {
-          const int    g  = v / 2;
-          const float2 p0 = cmulc(rxv(g, 0, k), pilot(seq, bit0, 0, v, m));
-          const float2 p1 = cmulc(rxv(g, 1, k), pilot(seq, bit0, 1, v, m));
+        for (int vv = 0; vv < L; ++vv) {
+          const int    gg = vv / 2;
+          const float2 p0 = cmulc(rxv(gg, 0, m), pilot(seq, bit0, 0, vv, m));
+          const float2 p1 = cmulc(rxv(gg, 1, m), pilot(seq, bit0, 1, vv, m));
           const float2 t  = cmulc(p1, p0);
-          if (g == 0) {
+          if (gg == 0) {
             acc.x += t.x;
             acc.y += t.y;
           } else {
@@ -252,169 +237,266 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
       }
     }
     acc = block_sum4(acc, red);
-    if (tid == 0) {
-      const float de  = a.epoch[a.dmrs_sym[1]] - a.epoch[a.dmrs_sym[0]];
-      float       cfo = atan2f(acc.y, acc.x) / TWOPI_F / de;
+  }
+  const float4 te = block_sum4(make_float4(epre, 0, 0, 0), red);
+  if (tid == 0) {
+    float* out = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
+    float  cfo = 0;
+    if (nds >= 2) {
+      const float de = a.epoch[a.dmrs_sym[1]] - a.epoch[a.dmrs_sym[0]];
+      cfo            = atan2f(acc.y, acc.x) / TWOPI_F / de;
       if (a.ncdm > 1) {
         cfo += atan2f(acc.w, acc.z) / TWOPI_F / de;
       }
       cfo /= static_cast<float>(a.ncdm);
-      s_cfo     = cfo;
-      s_has_cfo = 1;
-      for (int d = 0; d < nds; ++d) {
-        s_rot[d]     = a.compensate_cfo ? polar1(-TWOPI_F * a.epoch[a.dmrs_sym[d]] * cfo) : make_float2(1, 0);
-        s_rot_fwd[d] = polar1(TWOPI_F * a.epoch[a.dmrs_sym[d]] * cfo); // the noise predictor's phase
-      }
     }
-  } else if (tid == 0) {
-    s_cfo     = 0;
-    s_has_cfo = 0;
-    s_rot[0]  = make_float2(1, 0);
+    out[0] = te.x;
+    out[3] = nds >= 2 ? 1.0f : 0.0f;
+    out[4] = cfo;
   }
-  __syncthreads();
+}
+
+// One workgroup per (grid, rx port, slice = layer x LSE symbol): every slice of a port is estimated
+// concurrently, with the port's CFO from chest_cfo_kernel.  Per slice: LSE
+// (rx * conj(pilot)), CFO compensation and time accumulation, CDM pair averaging (lane shuffle), scaling, FD
+// smoothing in LDS (mean, or virtual pilots + raised-cosine FIR), the slice's RSRP share, linear
+// interpolation to every RE of the allocation (port_channel_estimator_average_impl.cpp:130-506).
+__global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a)
+{
+  __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
+  __shared__ float2   enl_in[CH_MAXPIL + 2 * CH_MAXV];
+  __shared__ float2   enl_out[CH_MAXPIL + 2 * CH_MAXV];
+  __shared__ float    red[4 * 16];
+  __shared__ int      s_has_cfo;
+  __shared__ float2   s_rot[CH_MAXDMRS];
+
+  const uint32_t gp    = blockIdx.x; // grid * nof_ports + port
+  const uint32_t slice = blockIdx.y; // layer * nof_lse + LSE symbol
+  const uint32_t grid  = gp / a.nof_ports;
+  const uint32_t port  = gp % a.nof_ports;
+  const uint32_t tid   = threadIdx.x;
+  const uint32_t npil  = a.npil;
+  const int      nds   = static_cast<int>(a.nds);
+  const int      L     = static_cast<int>(a.L);
+  const int      v     = static_cast<int>(slice / a.nof_lse);
+  const int      s     = static_cast<int>(slice % a.nof_lse);
+  const int      g     = v / 2;
+
+  const uint32_t  bit0  = dmrs_words(a, seq);
+  const uint32_t* gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc +
+                          12 * a.prb_lo;
+  // received pilot m of CDM group gg in DM-RS symbol d (subcarrier 12 prb_lo + 2m + gg)
+  auto rxv = [&](int gg, int d, uint32_t m) { return from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + gg]); };
+
+  if (tid < static_cast<uint32_t>(nds)) { // the port's CFO phases (chest_cfo_kernel)
+    const float* acc = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
+    s_rot[tid]       = (acc[3] != 0.0f && a.compensate_cfo) ? polar1(-TWOPI_F * a.epoch[a.dmrs_sym[tid]] * acc[4])
+                                                            : make_float2(1, 0);
+    if (tid == 0) {
+      s_has_cfo = acc[3] != 0.0f ? 1 : 0;
+    }
+  }
+  __syncthreads(); // seq, rotations ready
   const bool  has_cfo  = s_has_cfo != 0;
   const bool  rotate   = has_cfo && a.compensate_cfo;
   const float total    = a.td == SRS_AMD_CHEST_TD_AVERAGE ? (1.0f / a.beta) / static_cast<float>(nds) : 1.0f / a.beta;
   const float rsrp_nrm = a.beta * a.beta * static_cast<float>(nds) / static_cast<float>(a.nof_lse);
   // Pair averaging (average_pairs): one DM-RS symbol -> layers of two-layer CDM groups; more -> every layer if L > 1.
-  float2* filt = a.filt + static_cast<uint64_t>(gp) * a.L * a.nof_lse * npil;
-  float2* freq = a.freq + static_cast<uint64_t>(gp) * a.L * a.nof_lse * a.nof_re;
-  float   rsrp = 0;
+  const bool pair_avg = nds == 1 ? (2 * g + 2 <= L) : (L > 1);
 
-  for (int v = 0; v < L; ++v) {
-    const int  g        = v / 2;
-    const bool pair_avg = nds == 1 ? (2 * g + 2 <= L) : (L > 1);
-    for (int s = 0; s < static_cast<int>(a.nof_lse); ++s) {
-      float2 x[CH_PPT];
+  float2 x[CS_PPT];
 #pragma unroll
-      for (int k = 0; k < CH_PPT; ++k) {
-        const uint32_t m = tid + k * CH_THREADS;
-        float2         y = make_float2(0, 0);
-        if (m < npil) {
-          if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
-            y = cmulc(rxv(g, 0, k), pilot(seq, bit0, 0, v, m));
-            if (rotate) {
-              y = cmul(y, s_rot[0]);
-            }
-            for (int d = 1; d < nds; ++d) {
-              float2 t = cmulc(rxv(g, d, k), pilot(seq, bit0, d, v, m));
-              if (rotate) {
-                t = cmul(t, s_rot[d]);
-              }
-              y = cadd(y, t);
-            }
-          } else {
-            y = cmulc(rxv(g, s, k), pilot(seq, bit0, s, v, m));
-            if (rotate) {
-              y = cmul(y, s_rot[s]);
-            }
+  for (int k = 0; k < CS_PPT; ++k) {
+    const uint32_t m = tid + k * CS_THREADS;
+    float2         y = make_float2(0, 0);
+    if (m < npil) {
+      if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
+        y = cmulc(rxv(g, 0, m), pilot(seq, bit0, 0, v, m));
+        if (rotate) {
+          y = cmul(y, s_rot[0]);
+        }
+        for (int d = 1; d < nds; ++d) {
+          float2 t = cmulc(rxv(g, d, m), pilot(seq, bit0, d, v, m));
+          if (rotate) {
+            t = cmul(t, s_rot[d]);
           }
+          y = cadd(y, t);
         }
-        const float2 o = make_float2(__shfl_xor(y.x, 1), __shfl_xor(y.y, 1));
-        if (pair_avg && m < npil) {
-          const float2 sum = (m & 1) ? cadd(o, y) : cadd(y, o);
-          y                = make_float2(sum.x / 2.0f, sum.y / 2.0f);
+      } else {
+        y = cmulc(rxv(g, s, m), pilot(seq, bit0, s, v, m));
+        if (rotate) {
+          y = cmul(y, s_rot[s]);
         }
-        x[k] = cscale(y, total);
       }
+    }
+    const float2 o = make_float2(__shfl_xor(y.x, 1), __shfl_xor(y.y, 1));
+    if (pair_avg && m < npil) {
+      const float2 sum = (m & 1) ? cadd(o, y) : cadd(y, o);
+      y                = make_float2(sum.x / 2.0f, sum.y / 2.0f);
+    }
+    x[k] = cscale(y, total);
+  }
 
-      // FD smoothing (apply_fd_smoothing, port_channel_estimator_helpers.cpp:213-260).
-      if (a.fd == SRS_AMD_CHEST_FD_MEAN) {
-        float4 sm = make_float4(0, 0, 0, 0);
+  // FD smoothing (apply_fd_smoothing, port_channel_estimator_helpers.cpp:213-260).
+  if (a.fd == SRS_AMD_CHEST_FD_MEAN) {
+    float4 sm = make_float4(0, 0, 0, 0);
 #pragma unroll
-        for (int k = 0; k < CH_PPT; ++k) {
-          if (tid + k * CH_THREADS < npil) {
-            sm.x += x[k].x;
-            sm.y += x[k].y;
-          }
-        }
-        sm              = block_sum4(sm, red);
-        const float2 mu = make_float2(sm.x / npil, sm.y / npil);
-#pragma unroll
-        for (int k = 0; k < CH_PPT; ++k) {
-          x[k] = mu;
-        }
-      } else if (a.fd == SRS_AMD_CHEST_FD_FILTER) {
-        const int nv = a.nof_v;
-        for (uint32_t i = tid; i < npil + 2 * CH_MAXV; i += CH_THREADS) {
-          enl_in[i] = make_float2(0, 0);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < CH_PPT; ++k) {
-          const uint32_t m = tid + k * CH_THREADS;
-          if (m < npil) {
-            enl_in[CH_MAXV + m] = x[k];
-          }
-        }
-        __syncthreads();
-        if (tid == 0) {
-          virtual_pilots(enl_in + CH_MAXV - nv, enl_in + CH_MAXV, nv, true);
-        } else if (tid == 64) {
-          virtual_pilots(enl_in + CH_MAXV + npil, enl_in + CH_MAXV + npil - nv, nv, false);
-        }
-        __syncthreads();
-        const int half = a.nof_taps / 2;
-#pragma unroll
-        for (int k = 0; k < CH_PPT; ++k) {
-          const int m = static_cast<int>(tid + k * CH_THREADS);
-          if (m < static_cast<int>(npil)) {
-            float2 acc = make_float2(0, 0);
-            for (int j = 0; j < a.nof_taps; ++j) {
-              const int i = m + j - half; // convolution input index (pilot domain)
-              if (i >= -nv && i < static_cast<int>(npil) + nv) {
-                const float2 in = enl_in[CH_MAXV + i];
-                const float  c  = a.rc[a.nof_taps - 1 - j];
-                acc.x           = acc.x + in.x * c; // srsran_simd_f_mul then _add
-                acc.y           = acc.y + in.y * c;
-              }
-            }
-            x[k] = acc;
-          }
-        }
+    for (int k = 0; k < CS_PPT; ++k) {
+      if (tid + k * CS_THREADS < npil) {
+        sm.x += x[k].x;
+        sm.y += x[k].y;
       }
-
-      // RSRP, store the smoothed pilots, stage them for the interpolation.
+    }
+    sm              = block_sum4(sm, red);
+    const float2 mu = make_float2(sm.x / npil, sm.y / npil);
 #pragma unroll
-      for (int k = 0; k < CH_PPT; ++k) {
-        const uint32_t m = tid + k * CH_THREADS;
-        if (m < npil) {
-          rsrp = __builtin_fmaf(x[k].x * x[k].x + x[k].y * x[k].y, rsrp_nrm, rsrp);
-          filt[(static_cast<uint64_t>(v) * a.nof_lse + s) * npil + m] = x[k];
-          enl_out[m]                                                  = x[k];
-        }
+    for (int k = 0; k < CS_PPT; ++k) {
+      x[k] = mu;
+    }
+  } else if (a.fd == SRS_AMD_CHEST_FD_FILTER) {
+    const int nv = a.nof_v;
+    for (uint32_t i = tid; i < npil + 2 * CH_MAXV; i += CS_THREADS) {
+      enl_in[i] = make_float2(0, 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CS_PPT; ++k) {
+      const uint32_t m = tid + k * CS_THREADS;
+      if (m < npil) {
+        enl_in[CH_MAXV + m] = x[k];
       }
-      __syncthreads();
-      // Linear interpolation (interpolator_linear_impl.cpp): pilots at offset g + 2i.
-      float2* fr = freq + (static_cast<uint64_t>(v) * a.nof_lse + s) * a.nof_re;
-      for (uint32_t kk = tid; kk < a.nof_re; kk += CH_THREADS) {
-        float2 out;
-        if (kk <= static_cast<uint32_t>(g)) {
-          out = enl_out[0];
-        } else {
-          const uint32_t j = (kk - g) / 2, r = (kk - g) % 2;
-          if (j + 1 < npil) {
-            const float2 p0 = enl_out[j], p1 = enl_out[j + 1];
-            out = r ? make_float2((p1.x - p0.x) * 0.5f + p0.x, (p1.y - p0.y) * 0.5f + p0.y) : p0;
-          } else {
-            out = enl_out[npil - 1];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      virtual_pilots(enl_in + CH_MAXV - nv, enl_in + CH_MAXV, nv, true);
+    } else if (tid == 64) {
+      virtual_pilots(enl_in + CH_MAXV + npil, enl_in + CH_MAXV + npil - nv, nv, false);
+    }
+    __syncthreads();
+    const int half = a.nof_taps / 2;
+#pragma unroll
+    for (int k = 0; k < CS_PPT; ++k) {
+      const int m = static_cast<int>(tid + k * CS_THREADS);
+      if (m < static_cast<int>(npil)) {
+        float2 acc = make_float2(0, 0);
+        for (int j = 0; j < a.nof_taps; ++j) {
+          const int i = m + j - half; // convolution input index (pilot domain)
+          if (i >= -nv && i < static_cast<int>(npil) + nv) {
+            const float2 in = enl_in[CH_MAXV + i];
+            const float  c  = a.rc[a.nof_taps - 1 - j];
+            acc.x           = acc.x + in.x * c; // srsran_simd_f_mul then _add
+            acc.y           = acc.y + in.y * c;
           }
         }
-        fr[kk] = out;
+        x[k] = acc;
       }
-      __syncthreads(); // enl_in / enl_out reused
     }
   }
 
-  // Noise energy per CDM group (estimate_noise, :594-690).
-  float       noise0 = 0, noise1 = 0;
-  const float sf     = a.beta / static_cast<float>(a.nof_lse);
+  // RSRP share, store the smoothed pilots, stage them for the interpolation.
+  float   rsrp = 0;
+  float2* filt = a.filt + (static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice) * npil;
 #pragma unroll
-  for (int k = 0; k < CH_PPT; ++k) {
-    const uint32_t m = tid + k * CH_THREADS;
-    if (m >= npil) {
-      continue;
+  for (int k = 0; k < CS_PPT; ++k) {
+    const uint32_t m = tid + k * CS_THREADS;
+    if (m < npil) {
+      rsrp    = __builtin_fmaf(x[k].x * x[k].x + x[k].y * x[k].y, rsrp_nrm, rsrp);
+      filt[m] = x[k];
+      enl_out[m] = x[k];
     }
+  }
+  __syncthreads();
+  // Linear interpolation (interpolator_linear_impl.cpp): pilots at offset g + 2i.
+  float2* fr = a.freq + (static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice) * a.nof_re;
+  for (uint32_t kk = tid; kk < a.nof_re; kk += CS_THREADS) {
+    float2 out;
+    if (kk <= static_cast<uint32_t>(g)) {
+      out = enl_out[0];
+    } else {
+      const uint32_t j = (kk - g) / 2, r = (kk - g) % 2;
+      if (j + 1 < npil) {
+        const float2 p0 = enl_out[j], p1 = enl_out[j + 1];
+        out = r ? make_float2((p1.x - p0.x) * 0.5f + p0.x, (p1.y - p0.y) * 0.5f + p0.y) : p0;
+      } else {
+        out = enl_out[npil - 1];
+      }
+    }
+    fr[kk] = out;
+  }
+  const float4 tot = block_sum4(make_float4(rsrp, 0, 0, 0), red);
+  if (tid == 0) {
+    a.acc[static_cast<uint64_t>(gp) * CH_ACC + CH_ACC_RSRP + slice] = tot.x;
+  }
+}
+
+// Time alignment, one workgroup per (grid, port, slice): the N-point IDFT of the slice's smoothed pilots
+// with the fused Stockham engine and |.|^2 into the slice's correlation row
+// (time_alignment_estimator_dft_impl.cpp:122-200).
+template <int N>
+__global__ __launch_bounds__(dft::plan<N>::T) void chest_ta_kernel(chest_args a)
+{
+  using dft::cf;
+  __shared__ cf  lds[dft::lds_complex<N>()];
+  const uint32_t gp     = blockIdx.x;
+  const uint32_t slice  = blockIdx.y;
+  const uint32_t npil   = a.npil;
+  const uint64_t row    = static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice;
+  const float2*  in     = a.filt + row * npil;
+  float*         corr   = a.corr + row * N;
+  auto           load   = [&](int i) -> cf {
+    if (i < static_cast<int>(npil)) {
+      const float2 v = in[i];
+      return cf{v.x, v.y};
+    }
+    return cf{0, 0};
+  };
+  auto store = [&](int k, cf v) { corr[k] = v.x * v.x + v.y * v.y; };
+  dft::plan<N>::template engine<+1>::run(lds, reinterpret_cast<const cf*>(a.ta_tw), load, store);
+}
+
+// Per-port measurements, one workgroup per (grid, port): the noise energy per CDM group from the smoothed
+// pilots of every slice (estimate_noise, :594-690), the slices' correlations summed in slice order (the
+// reference accumulates them symbol-major; the sum is order-free up to rounding), the peak search and
+// quadratic refinement (time_alignment_estimator_dft_impl.cpp:248-310) and noise variance, EPRE, RSRP,
+// SNR and CFO (do_compute tail, port_channel_estimator_average_impl.cpp:160-199).
+__global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a)
+{
+  __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
+  __shared__ float    corr[CH_TA_MAXN];
+  __shared__ float    red[4 * 16];
+  const uint32_t      gp   = blockIdx.x;
+  const uint32_t      grid = gp / a.nof_ports;
+  const uint32_t      port = gp % a.nof_ports;
+  const uint32_t      tid  = threadIdx.x;
+  const uint32_t      npil = a.npil;
+  const int           nds  = static_cast<int>(a.nds);
+  const int           L    = static_cast<int>(a.L);
+  const uint32_t      N    = a.ta_n;
+  const float*        acc  = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
+  const uint32_t      bit0 = dmrs_words(a, seq);
+  const uint32_t      nsl  = a.L * a.nof_lse;
+  const float*        crow = a.corr + static_cast<uint64_t>(gp) * nsl * N;
+  for (uint32_t k = tid; k < N; k += ST_THREADS) {
+    float c = 0;
+    for (uint32_t sl = 0; sl < nsl; ++sl) {
+      c += crow[static_cast<uint64_t>(sl) * N + k];
+    }
+    corr[k] = c;
+  }
+  __syncthreads(); // seq, corr ready
+
+  const bool rotate = acc[3] != 0.0f && a.compensate_cfo;
+  float2     rot_fwd[CH_MAXDMRS]; // the noise predictor's phase
+#pragma unroll
+  for (int d = 0; d < CH_MAXDMRS; ++d) {
+    rot_fwd[d] = d < nds ? polar1(TWOPI_F * a.epoch[a.dmrs_sym[d]] * acc[4]) : make_float2(1, 0);
+  }
+  const uint32_t* gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc +
+                          12 * a.prb_lo;
+  const float2*   filt  = a.filt + static_cast<uint64_t>(gp) * a.L * a.nof_lse * npil;
+  float           noise0 = 0, noise1 = 0;
+  const float     sf     = a.beta / static_cast<float>(a.nof_lse);
+  for (uint32_t m = tid; m < npil; m += ST_THREADS) {
     for (int g = 0; g < static_cast<int>(a.ncdm); ++g) {
       const int v0 = 2 * g, v1 = min(2 * g + 2, L);
       float2    sc0 = make_float2(0, 0), sc1 = make_float2(0, 0);
@@ -430,20 +512,23 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
           sc1 = t;
         }
       }
-      for (int d = 0; d < nds; ++d) {
-        const float2 rot = s_rot_fwd[d];
+#pragma unroll
+      for (int d = 0; d < CH_MAXDMRS; ++d) {
+        if (d >= nds) {
+          break;
+        }
         float2 pred = cmul(sc0, pilot(seq, bit0, d, v0, m));
         if (rotate) {
-          pred = cmul(pred, rot);
+          pred = cmul(pred, rot_fwd[d]);
         }
         if (v1 - v0 == 2) {
           float2 po = cmul(sc1, pilot(seq, bit0, d, v0 + 1, m));
           if (rotate) {
-            po = cmul(po, rot);
+            po = cmul(po, rot_fwd[d]);
           }
           pred = cadd(pred, po);
         }
-        const float2 n = csub(rxv(g, d, k), pred);
+        const float2 n = csub(from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + g]), pred);
         const float  e = __builtin_fmaf(n.x, n.x, n.y * n.y);
         if (g == 0) {
           noise0 += e;
@@ -453,53 +538,18 @@ __global__ __launch_bounds__(CH_THREADS) void chest_pilot_kernel(chest_args a)
       }
     }
   }
-  const float4 tot = block_sum4(make_float4(epre, rsrp, noise0, noise1), red);
+  const float4 tot = block_sum4(make_float4(noise0, noise1, 0, 0), red);
+
   if (tid == 0) {
-    float* acc  = a.acc + static_cast<uint64_t>(gp) * 8;
-    float  nsum = 0;
-    nsum += (isnormal(tot.z) ? tot.z : 0.0f);
+    float nsum = 0;
+    nsum += (isnormal(tot.x) ? tot.x : 0.0f);
     if (a.ncdm > 1) {
-      nsum += (isnormal(tot.w) ? tot.w : 0.0f);
+      nsum += (isnormal(tot.y) ? tot.y : 0.0f);
     }
-    acc[0] = tot.x;
-    acc[1] = tot.y;
-    acc[2] = nsum;
-    acc[3] = has_cfo ? 1.0f : 0.0f;
-    acc[4] = s_cfo;
-  }
-}
-
-// Time alignment + per-port measurements, one workgroup per (grid, port).
-template <int N>
-__global__ __launch_bounds__(dft::plan<N>::T) void chest_ta_kernel(chest_args a)
-{
-  using dft::cf;
-  __shared__ cf    lds[dft::lds_complex<N>()];
-  __shared__ float corr[N];
-  const uint32_t   gp   = blockIdx.x;
-  const uint32_t   npil = a.npil;
-  const float2*    filt = a.filt + static_cast<uint64_t>(gp) * a.L * a.nof_lse * npil;
-  for (int i = threadIdx.x; i < N; i += blockDim.x) {
-    corr[i] = 0;
-  }
-  __syncthreads();
-  const uint32_t nslices = a.L * a.nof_lse;
-  for (uint32_t sl = 0; sl < nslices; ++sl) {
-    // estimate_time_alignment orders the slices symbol-major; the correlation sum is order-free.
-    const float2* in    = filt + static_cast<uint64_t>(sl) * npil;
-    auto          load  = [&](int i) -> cf {
-      if (i < static_cast<int>(npil)) {
-        const float2 v = in[i];
-        return cf{v.x, v.y};
-      }
-      return cf{0, 0};
-    };
-    auto store = [&](int k, cf v) { corr[k] += v.x * v.x + v.y * v.y; };
-    dft::plan<N>::template engine<+1>::run(lds, reinterpret_cast<const cf*>(a.ta_tw), load, store);
-    __syncthreads();
-  }
-
-  if (threadIdx.x == 0) {
+    float rsrp_sum = 0;
+    for (uint32_t sl = 0; sl < nsl; ++sl) {
+      rsrp_sum += acc[CH_ACC_RSRP + sl];
+    }
     // estimate_ta_correlation (time_alignment_estimator_dft_impl.cpp:248-310).
     const int max_taps = a.ta_max_taps;
     int       i_d = 0, i_a = 0;
@@ -545,11 +595,10 @@ __global__ __launch_bounds__(dft::plan<N>::T) void chest_ta_kernel(chest_args a)
     const long       tc  = tcx / 10 + (tcx % 10) / 5;
 
     // do_compute tail (port_channel_estimator_average_impl.cpp:160-199).
-    const float* acc   = a.acc + static_cast<uint64_t>(gp) * 8;
-    const float  npilt = static_cast<float>(npil * a.nds);
-    const float  rsrp  = acc[1] / (npilt * static_cast<float>(a.L));
-    const float  epre  = acc[0] / npilt;
-    float        nvar  = acc[2] / (npilt * static_cast<float>(a.ncdm) - 1.0f);
+    const float npilt  = static_cast<float>(npil * a.nds);
+    const float rsrp   = rsrp_sum / (npilt * static_cast<float>(a.L));
+    const float epre   = acc[0] / npilt;
+    float       nvar   = nsum / (npilt * static_cast<float>(a.ncdm) - 1.0f);
     nvar               = fmaxf(rsrp / 1e10f, nvar);
     const float datarp = rsrp * static_cast<float>(a.L) / a.beta / a.beta;
     const float snr    = isnormal(nvar) ? datarp / nvar : 0.0f;
@@ -579,7 +628,7 @@ __global__ __launch_bounds__(256) void chest_expand_kernel(chest_args a)
   const uint32_t    gp   = gpv / a.L;
   const uint32_t    v    = gpv % a.L;
   const uint32_t    grid = gp / a.nof_ports, port = gp % a.nof_ports;
-  const float*      acc  = a.acc + static_cast<uint64_t>(gp) * 8;
+  const float*      acc  = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
   const bool        rot  = chdev::cfo_rotates(a, acc);
   if (rot && threadIdx.x < a.nof_symbols) {
     const uint32_t l  = a.first_symbol + threadIdx.x;
@@ -626,15 +675,26 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   if (nb == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(chest_pilot_kernel, dim3(nb), dim3(CH_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(chest_seq_kernel, dim3(1), dim3(CS_THREADS), 0, stream, a);
   hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    return e;
+  }
+  hipLaunchKernelGGL(chest_cfo_kernel, dim3(nb), dim3(CS_THREADS), 0, stream, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) {
+    return e;
+  }
+  const dim3 slices(nb, a.L * a.nof_lse);
+  hipLaunchKernelGGL(chest_slice_kernel, slices, dim3(CS_THREADS), 0, stream, a);
+  e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
   }
   switch (a.ta_n) {
 #define SRS_TA_CASE(NN)                                                                                               \
   case NN:                                                                                                            \
-    hipLaunchKernelGGL(chest_ta_kernel<NN>, dim3(nb), dim3(dft::plan<NN>::T), 0, stream, a);                         \
+    hipLaunchKernelGGL(chest_ta_kernel<NN>, slices, dim3(dft::plan<NN>::T), 0, stream, a);                           \
     break;
     SRS_TA_CASE(128)
     SRS_TA_CASE(256)
@@ -646,6 +706,11 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
     default:
       return hipErrorInvalidValue;
   }
+  e = hipGetLastError();
+  if (e != hipSuccess) {
+    return e;
+  }
+  hipLaunchKernelGGL(chest_stats_kernel, dim3(nb), dim3(ST_THREADS), 0, stream, a);
   e = hipGetLastError();
   if (e != hipSuccess) {
     return e;

@@ -251,7 +251,8 @@ size_t scratch_bytes(const chest_args& a, uint32_t nof_grids)
 {
   const size_t gp = static_cast<size_t>(nof_grids) * a.nof_ports;
   return align_up(gp * a.L * a.nof_lse * a.npil * 8, 256) + align_up(gp * a.L * a.nof_lse * a.nof_re * 8, 256) +
-         gp * 8 * 4;
+         align_up(gp * CH_ACC * 4, 256) + align_up(gp * a.L * a.nof_lse * a.ta_n * 4, 256) +
+         CH_MAXDMRS * CH_SEQWORDS * 4;
 }
 
 } // namespace
@@ -353,6 +354,10 @@ static int estimate_batch_impl(srs_amd_pusch_chest*              chest,
   a.freq = reinterpret_cast<float2*>(base);
   base += align_up(gp * a.L * a.nof_lse * a.nof_re * 8, 256);
   a.acc         = reinterpret_cast<float*>(base);
+  base += align_up(gp * CH_ACC * 4, 256);
+  a.corr        = reinterpret_cast<float*>(base);
+  base += align_up(gp * a.L * a.nof_lse * a.ta_n * 4, 256);
+  a.dmrs_seq    = reinterpret_cast<uint32_t*>(base);
   a.grids       = d_grids;
   a.grid_stride = grid_stride;
   a.estimates   = d_estimates;

@@ -10,14 +10,20 @@
 
 namespace srs_amd {
 
-constexpr int CH_THREADS  = 1024;           // pilot kernel workgroup
 constexpr int CH_MAXPIL   = 2048;           // pilots per DM-RS symbol (type 1: 6 x 275 = 1650)
-constexpr int CH_PPT      = CH_MAXPIL / CH_THREADS;
+constexpr int CS_THREADS  = 256;            // slice and stats kernel workgroups
+constexpr int CS_PPT      = CH_MAXPIL / CS_THREADS;
+constexpr int ST_THREADS  = 1024;           // per-port statistics kernel workgroup
+constexpr int CH_TA_MAXN  = 4096;           // largest time-alignment IDFT
 constexpr int CH_MAXV     = 12;             // MAX_V_PILOTS
 constexpr int CH_MAXDMRS  = 4;              // DM-RS symbols per slot
 constexpr int CH_MAXL     = 4;              // layers
 constexpr int CH_SEQWORDS = 2 * CH_MAXPIL / 32 + 2;
 constexpr int CH_NSYMB    = 14;
+// per (grid, port) accumulators: [0] EPRE, [3] CFO valid, [4] CFO (normalised), [CH_ACC_RSRP + slice] the
+// slices' RSRP shares
+constexpr int CH_ACC_RSRP = 8;
+constexpr int CH_ACC      = CH_ACC_RSRP + CH_MAXL * CH_MAXDMRS;
 
 struct chest_args {
   // inputs / outputs
@@ -29,7 +35,9 @@ struct chest_args {
   // scratch (per grid and port)
   float2* filt; // [L][nof_lse][npil]
   float2* freq; // [L][nof_lse][nof_re]
-  float*  acc;  // [8]: epre, rsrp, noise, cfo valid, cfo
+  float*  acc;  // [CH_ACC]: epre, -, -, cfo valid, cfo, -, -, -, rsrp per slice
+  float*  corr; // [L][nof_lse][ta_n]: time-alignment correlation per slice
+  uint32_t* dmrs_seq; // [CH_MAXDMRS][CH_SEQWORDS]: DM-RS Gold words of the batch
   // constants
   const uint32_t* jump;    // Gold-sequence jump matrices
   const float2*   ta_tw;   // W_N^m table of the time-alignment IDFT size

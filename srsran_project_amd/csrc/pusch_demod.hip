@@ -25,38 +25,44 @@
 namespace srs_amd {
 namespace {
 
-// Soft demapping and descrambling of the QM LLRs of codeword symbol i (= j L + layer) into the grid's LLR row:
-// demap_device.h's demapper (the SIMD or scalar arithmetic by the symbol's place in its OFDM symbol, as the
-// reference's per-OFDM-symbol demapper calls), the sign flipped where the Gold sequence bit is one.
-template <int QM>
-__device__ __forceinline__ void emit_symbol_llrs(const pusch_eq_args& a, const float* lt, int8_t* row, uint32_t i,
-                                                 bool simd, float2 s, float nv)
+// Soft demapping and descrambling of the L x QM LLRs of data RE j (codeword symbols i = j L + layer) into
+// the grid's LLR row: demap_device.h's demapper (the SIMD or scalar arithmetic by the symbol's place in its
+// OFDM symbol, as the reference's per-OFDM-symbol demapper calls), the sign flipped where the Gold sequence
+// bit is one (the RE's L QM <= 32 sequence bits from two table words).
+template <int L, int QM>
+__device__ __forceinline__ void emit_re_llrs(const pusch_eq_args& a, const float* lt, int8_t* row, uint32_t j,
+                                             uint32_t simd_hi, const float2 (&s)[L], const float (&nv)[L])
 {
-  int8_t o[8];
-  demap::demap_symbol(a.dm, lt, s, nv, i, simd, o);
-  const uint32_t n0 = i * QM;
-  const uint64_t cc = static_cast<uint64_t>(a.scr[n0 / 32]) | (static_cast<uint64_t>(a.scr[n0 / 32 + 1]) << 32);
-  const uint32_t c  = static_cast<uint32_t>(cc >> (n0 % 32));
-  uint64_t       v  = 0;
+  const uint32_t b0 = j * L * QM;
+  const uint64_t cc = static_cast<uint64_t>(a.scr[b0 / 32]) | (static_cast<uint64_t>(a.scr[b0 / 32 + 1]) << 32);
+  const uint32_t cw = static_cast<uint32_t>(cc >> (b0 % 32));
 #pragma unroll
-  for (int k = 0; k < QM; ++k) {
-    const int x = ((c >> k) & 1u) ? -o[k] : o[k];
-    v |= static_cast<uint64_t>(static_cast<uint8_t>(x)) << (8 * k);
-  }
-  int8_t* dst = row + n0;
-  if constexpr (QM == 8) {
-    *reinterpret_cast<uint2*>(dst) = make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
-  } else if constexpr (QM == 6) {
-    uint16_t* d16 = reinterpret_cast<uint16_t*>(dst); // i * 6 is even
-    d16[0]        = static_cast<uint16_t>(v);
-    d16[1]        = static_cast<uint16_t>(v >> 16);
-    d16[2]        = static_cast<uint16_t>(v >> 32);
-  } else if constexpr (QM == 4) {
-    *reinterpret_cast<uint32_t*>(dst) = static_cast<uint32_t>(v);
-  } else if constexpr (QM == 2) {
-    *reinterpret_cast<uint16_t*>(dst) = static_cast<uint16_t>(v);
-  } else {
-    *dst = static_cast<int8_t>(v);
+  for (int v = 0; v < L; ++v) {
+    const uint32_t i = j * L + v;
+    int8_t         o[8];
+    demap::demap_symbol(a.dm, lt, s[v], nv[v], i, i < simd_hi, o);
+    const uint32_t c = cw >> (v * QM);
+    uint64_t       x = 0;
+#pragma unroll
+    for (int k = 0; k < QM; ++k) {
+      const int q = ((c >> k) & 1u) ? -o[k] : o[k];
+      x |= static_cast<uint64_t>(static_cast<uint8_t>(q)) << (8 * k);
+    }
+    int8_t* dst = row + i * QM;
+    if constexpr (QM == 8) {
+      *reinterpret_cast<uint2*>(dst) = make_uint2(static_cast<uint32_t>(x), static_cast<uint32_t>(x >> 32));
+    } else if constexpr (QM == 6) {
+      uint16_t* d16 = reinterpret_cast<uint16_t*>(dst); // i * 6 is even
+      d16[0]        = static_cast<uint16_t>(x);
+      d16[1]        = static_cast<uint16_t>(x >> 16);
+      d16[2]        = static_cast<uint16_t>(x >> 32);
+    } else if constexpr (QM == 4) {
+      *reinterpret_cast<uint32_t*>(dst) = static_cast<uint32_t>(x);
+    } else if constexpr (QM == 2) {
+      *reinterpret_cast<uint16_t*>(dst) = static_cast<uint16_t>(x);
+    } else {
+      *dst = static_cast<int8_t>(x);
+    }
   }
 }
 
@@ -67,27 +73,22 @@ __device__ __forceinline__ void emit_llrs(const pusch_eq_args& a, const float* l
 {
   int8_t*        row     = a.llrs + static_cast<uint64_t>(gi) * a.llr_stride;
   const uint32_t simd_hi = a.simd_hi[l];
-#pragma unroll
-  for (int v = 0; v < L; ++v) {
-    const uint32_t i    = j * L + v;
-    const bool     simd = i < simd_hi;
-    switch (a.dm.qm) {
-      case 8:
-        emit_symbol_llrs<8>(a, lt, row, i, simd, s[v], nv[v]);
-        break;
-      case 6:
-        emit_symbol_llrs<6>(a, lt, row, i, simd, s[v], nv[v]);
-        break;
-      case 4:
-        emit_symbol_llrs<4>(a, lt, row, i, simd, s[v], nv[v]);
-        break;
-      case 2:
-        emit_symbol_llrs<2>(a, lt, row, i, simd, s[v], nv[v]);
-        break;
-      default:
-        emit_symbol_llrs<1>(a, lt, row, i, simd, s[v], nv[v]);
-        break;
-    }
+  switch (a.dm.qm) {
+    case 8:
+      emit_re_llrs<L, 8>(a, lt, row, j, simd_hi, s, nv);
+      break;
+    case 6:
+      emit_re_llrs<L, 6>(a, lt, row, j, simd_hi, s, nv);
+      break;
+    case 4:
+      emit_re_llrs<L, 4>(a, lt, row, j, simd_hi, s, nv);
+      break;
+    case 2:
+      emit_re_llrs<L, 2>(a, lt, row, j, simd_hi, s, nv);
+      break;
+    default:
+      emit_re_llrs<L, 1>(a, lt, row, j, simd_hi, s, nv);
+      break;
   }
 }
 
@@ -188,71 +189,64 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
   equalize_write<P, L, MMSE>(a, lt, gi, j, l, y, h);
 }
 
-// Estimator-fused form: one thread per (grid, subcarrier, half of the OFDM symbols) rebuilds the channel
-// coefficients of each data RE from the estimator's per-subcarrier values (c.freq) and per-port CFO phases
-// with the expansion kernel's own operations (chest_device.h expand_value: identical cbf16 estimates), so
-// the P x L x 14 x subcarrier estimate tensor is neither written nor read.
-constexpr int EQ_SYM_GROUPS = 2;
+// Estimator-fused form: one thread per (grid, OFDM symbol, subcarrier) rebuilds the channel coefficients of
+// its data RE from the estimator's per-subcarrier values (c.freq: the one or two LSE slices the symbol
+// reads) and per-port CFO phases with the expansion kernel's own operations (chest_device.h expand_pair:
+// identical cbf16 estimates), so the P x L x 14 x subcarrier estimate tensor is neither written nor read.
+constexpr uint32_t EQ_XCDS = 8;
 
-template <int P, int L, bool MMSE, int NLSE>
+template <int P, int L, bool MMSE>
 __global__ __launch_bounds__(256) void pusch_equalize_fused_kernel(pusch_eq_args a, chest_args c)
 {
-  __shared__ float2 s_ph[P][CH_NSYMB];
+  __shared__ float2 s_ph[P];
   __shared__ int    s_rot[P];
   __shared__ float  lt[4 * 2 * 16];
-  demap::stage_interval_tables(a.dm, lt); // (synchronizes)
-  const uint32_t    gi = blockIdx.z;
-  if (threadIdx.x < P * CH_NSYMB) {
-    const uint32_t p   = threadIdx.x / CH_NSYMB, n = threadIdx.x % CH_NSYMB;
-    const float*   acc = c.acc + (static_cast<uint64_t>(gi) * P + p) * 8;
-    s_ph[p][n]         = n < c.nof_symbols ? chdev::cfo_phase(c, acc, c.first_symbol + n) : make_float2(1, 0);
-    if (n == 0) {
-      s_rot[p] = chdev::cfo_rotates(c, acc) ? 1 : 0;
-    }
+  // XCD-aware order: workgroups are dispatched to the 8 XCDs round-robin, so the symbols of one (grid,
+  // subcarrier tile) are placed on one XCD -- its L2 then serves their common LSE slices.
+  const uint32_t xcd  = blockIdx.x % EQ_XCDS, r = blockIdx.x / EQ_XCDS;
+  const uint32_t tile = xcd + EQ_XCDS * (r / c.nof_symbols);
+  if (tile >= a.nof_tiles) {
+    return;
   }
-  __syncthreads();
-  const uint32_t sc = a.first_subc + blockIdx.x * 256 + threadIdx.x;
+  const uint32_t gi = tile / a.tiles_x;
+  const uint32_t tx = tile % a.tiles_x;
+  const uint32_t l  = c.first_symbol + r % c.nof_symbols;
+  if (threadIdx.x < P) {
+    const float* acc    = c.acc + (static_cast<uint64_t>(gi) * P + threadIdx.x) * CH_ACC;
+    s_ph[threadIdx.x]  = chdev::cfo_phase(c, acc, l);
+    s_rot[threadIdx.x] = chdev::cfo_rotates(c, acc) ? 1 : 0;
+  }
+  demap::stage_interval_tables(a.dm, lt); // (synchronizes)
+  const uint32_t sc = a.first_subc + tx * 256 + threadIdx.x;
   const uint32_t kk = sc - 12 * c.prb_lo; // estimator allocation index (wraps below it)
   if (sc >= a.nof_subc || kk >= c.nof_re) {
     return;
   }
-  float2 x[P][L][NLSE];
+  const uint32_t e   = a.re_table[l * a.nof_prb + sc / 12];
+  const uint32_t bit = sc % 12;
+  if (((e >> bit) & 1u) == 0) {
+    return;
+  }
+  const uint32_t  j     = (e >> 12) + __builtin_popcount(e & ((1u << bit) - 1u));
+  const uint32_t* grid  = a.grids + gi * a.grid_stride + l * a.nof_subc + sc;
+  const uint32_t  plane = 14 * a.nof_subc;
+  const int       i0    = chdev::lse_index(c, l);
+  const bool      two   = c.td != SRS_AMD_CHEST_TD_AVERAGE && c.td_interp[l];
+  eq::cplx        y[P], h[P * L];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
+    y[p] = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane]);
 #pragma unroll
     for (int v = 0; v < L; ++v) {
-      const float2* fr = c.freq + ((static_cast<uint64_t>(gi) * P + p) * L + v) * c.nof_lse * c.nof_re + kk;
-#pragma unroll
-      for (int s = 0; s < NLSE; ++s) {
-        x[p][v][s] = fr[static_cast<uint64_t>(s) * c.nof_re];
-      }
+      const float2* fr =
+          c.freq + (((static_cast<uint64_t>(gi) * P + p) * L + v) * c.nof_lse + i0) * c.nof_re + kk;
+      const float2   x0 = fr[0];
+      const float2   x1 = two ? fr[c.nof_re] : x0;
+      const uint32_t u  = chdev::expand_pair(c, x0, x1, l, s_rot[p] != 0, s_ph[p]);
+      h[p * L + v]      = eq::from_cbf16(u);
     }
   }
-  const uint32_t* grid  = a.grids + gi * a.grid_stride + sc;
-  const uint32_t  plane = 14 * a.nof_subc;
-  const uint32_t  per   = (c.nof_symbols + EQ_SYM_GROUPS - 1) / EQ_SYM_GROUPS;
-  const uint32_t  n0    = blockIdx.y * per;
-  const uint32_t  n1    = min(c.nof_symbols, n0 + per);
-  for (uint32_t n = n0; n < n1; ++n) {
-    const uint32_t l   = c.first_symbol + n;
-    const uint32_t e   = a.re_table[l * a.nof_prb + sc / 12];
-    const uint32_t bit = sc % 12;
-    if (((e >> bit) & 1u) == 0) {
-      continue;
-    }
-    const uint32_t j = (e >> 12) + __builtin_popcount(e & ((1u << bit) - 1u));
-    eq::cplx       y[P], h[P * L];
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      y[p] = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane + l * a.nof_subc]);
-#pragma unroll
-      for (int v = 0; v < L; ++v) {
-        const uint32_t u = chdev::expand_value(c, x[p][v], l, s_rot[p] != 0, s_ph[p][n]);
-        h[p * L + v]     = eq::from_cbf16(u);
-      }
-    }
-    equalize_write<P, L, MMSE>(a, lt, gi, j, l, y, h);
-  }
+  equalize_write<P, L, MMSE>(a, lt, gi, j, l, y, h);
 }
 
 } // namespace
@@ -288,7 +282,7 @@ hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uin
 bool pusch_equalize_fusable(uint32_t nof_ports, uint32_t nof_layers, bool mmse, uint32_t nof_lse)
 {
   (void)mmse;
-  return nof_lse >= 1 && nof_lse <= 2 && nof_layers >= 1 && nof_layers <= 4 && nof_layers <= nof_ports &&
+  return nof_lse >= 1 && nof_lse <= CH_MAXDMRS && nof_layers >= 1 && nof_layers <= 4 && nof_layers <= nof_ports &&
          (nof_ports == 1 || nof_ports == 2 || nof_ports == 4) && !(nof_layers == 3 && nof_ports != 4);
 }
 
@@ -296,31 +290,31 @@ hipError_t launch_pusch_equalize_fused(const pusch_eq_args& a, const chest_args&
                                        uint32_t nof_layers, bool mmse, uint32_t span_subc, uint32_t nof_grids,
                                        hipStream_t stream)
 {
-  if (span_subc == 0 || nof_grids == 0) {
+  if (span_subc == 0 || nof_grids == 0 || c.nof_symbols == 0) {
     return hipSuccess;
   }
-  const dim3 grid((span_subc + 255) / 256, EQ_SYM_GROUPS, nof_grids);
-#define SRS_EQF_CASE(PP, LL, MM, NN)                                                                                  \
-  if (nof_ports == PP && nof_layers == LL && mmse == MM && c.nof_lse == NN) {                                         \
-    hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM, NN>), grid, dim3(256), 0, stream, a, c);             \
+  pusch_eq_args ax = a;
+  ax.tiles_x       = (span_subc + 255) / 256;
+  ax.nof_tiles     = ax.tiles_x * nof_grids;
+  const dim3 grid(EQ_XCDS * c.nof_symbols * ((ax.nof_tiles + EQ_XCDS - 1) / EQ_XCDS));
+#define SRS_EQF_CASE(PP, LL, MM)                                                                                      \
+  if (nof_ports == PP && nof_layers == LL && mmse == MM) {                                                            \
+    hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM>), grid, dim3(256), 0, stream, ax, c);                \
     return hipGetLastError();                                                                                         \
   }
-#define SRS_EQF_LSE(PP, LL, MM) SRS_EQF_CASE(PP, LL, MM, 1) SRS_EQF_CASE(PP, LL, MM, 2)
-  SRS_EQF_LSE(1, 1, false)
-  SRS_EQF_LSE(2, 1, false)
-  SRS_EQF_LSE(4, 1, false)
-  SRS_EQF_LSE(2, 2, false)
-  SRS_EQF_LSE(4, 2, false)
-  SRS_EQF_LSE(4, 3, false)
-  SRS_EQF_LSE(4, 4, false)
-  SRS_EQF_LSE(2, 2, true)
-  SRS_EQF_LSE(4, 2, true)
-  SRS_EQF_LSE(4, 3, true)
-  SRS_EQF_LSE(4, 4, true)
-#undef SRS_EQF_LSE
+  SRS_EQF_CASE(1, 1, false)
+  SRS_EQF_CASE(2, 1, false)
+  SRS_EQF_CASE(4, 1, false)
+  SRS_EQF_CASE(2, 2, false)
+  SRS_EQF_CASE(4, 2, false)
+  SRS_EQF_CASE(4, 3, false)
+  SRS_EQF_CASE(4, 4, false)
+  SRS_EQF_CASE(2, 2, true)
+  SRS_EQF_CASE(4, 2, true)
+  SRS_EQF_CASE(4, 3, true)
+  SRS_EQF_CASE(4, 4, true)
 #undef SRS_EQF_CASE
   return hipErrorInvalidValue;
 }
-
 
 } // namespace srs_amd

@@ -33,6 +33,8 @@ struct pusch_eq_args {
   uint64_t                        llr_stride;
   uint32_t                        simd_hi[14];
   demodulate_args                 dm;
+  uint32_t                        tiles_x;   // fused equalizer: 256-subcarrier tiles per grid
+  uint32_t                        nof_tiles; // tiles_x x grids
 };
 
 

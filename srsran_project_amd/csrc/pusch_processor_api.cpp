@@ -202,7 +202,7 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
   dc.nof_rx_ports                = pdu->nof_rx_ports;
   dc.equalizer                   = proc->cfg.equalizer;
   {
-    // the fused equalizer keeps at most two LSE slices per subcarrier in registers
+    // the fused equalizer reads the one or two LSE slices of each symbol (any number of DM-RS symbols)
     const uint32_t nof_lse = c.td_interpolation == SRS_AMD_CHEST_TD_AVERAGE
                                  ? 1u
                                  : static_cast<uint32_t>(__builtin_popcount(c.symbols_mask & 0x3fffu));

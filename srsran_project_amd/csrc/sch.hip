@@ -229,37 +229,43 @@ __device__ __forceinline__ const uint8_t* asm_source(const assemble_args& a, uin
   return a.msgs + static_cast<size_t>(t) * C * a.msg_stride;
 }
 
-struct tb_gather_write {
-  tb_gather g;
-  uint8_t*  tb;
-  __device__ uint32_t operator()(uint32_t j) const
-  {
-    const uint32_t b = g(j);
-    tb[j]            = static_cast<uint8_t>(b);
-    return b;
-  }
+struct lds_fetch {
+  const uint8_t* chunk;
+  uint32_t       first;
+  __device__ uint32_t operator()(uint32_t j) const { return chunk[j - first]; }
 };
 
 // C > 1, every codeblock OK: concatenation (concatenate_codeblocks, pusch_decoder_impl.cpp:460-503) and
-// TB CRC24A contributions, one workgroup per TB_CHUNK bytes of a TB.
+// TB CRC24A contributions, one workgroup per TB_CHUNK bytes of a TB: the chunk is gathered with consecutive
+// threads on consecutive bytes (coalesced codeblock reads and TB writes) into LDS, then each thread folds
+// its TB_PER contiguous bytes into a CRC contribution.
 __global__ __launch_bounds__(ASM_THREADS) void asm_tb_kernel(assemble_args a)
 {
   __shared__ uint32_t partial[ASM_THREADS / 64];
   __shared__ uint32_t T[256];
+  __shared__ uint8_t  s_chunk[ASM_TB_CHUNK];
   const uint32_t      t = blockIdx.y;
   if (a.results[t].nof_codeblocks_crc_ok != a.nof_segments) {
     return; // uniform over the workgroup
   }
   crc_table8_init<ASM_THREADS>(T, 24, CRC24A_POLY);
+  uint32_t        stride;
+  const uint8_t*  src    = asm_source(a, t, stride);
+  const tb_gather g{src, stride, a.cb_info_bits};
+  uint8_t*        tb     = a.tbs + static_cast<size_t>(t) * a.tb_stride;
+  const uint32_t  nbytes = a.tbs_bits / 8;
+  const uint32_t  c0     = blockIdx.x * ASM_TB_CHUNK;
+  const uint32_t  n      = min(ASM_TB_CHUNK, nbytes - c0);
+  for (uint32_t i = threadIdx.x; i < n; i += ASM_THREADS) {
+    const uint32_t b = g(c0 + i);
+    s_chunk[i]       = static_cast<uint8_t>(b);
+    tb[c0 + i]       = static_cast<uint8_t>(b);
+  }
   __syncthreads();
-  uint32_t            stride;
-  const uint8_t*      src = asm_source(a, t, stride);
-  const tb_gather_write f{tb_gather{src, stride, a.cb_info_bits}, a.tbs + static_cast<size_t>(t) * a.tb_stride};
-  const uint32_t      nbytes = a.tbs_bits / 8;
-  const uint32_t      b0     = blockIdx.x * ASM_TB_CHUNK + threadIdx.x * ASM_TB_PER;
-  const uint32_t      b1     = min(nbytes, b0 + ASM_TB_PER);
-  const uint32_t      v      = crc_block_xor<ASM_THREADS>(
-      crc_chunk_contrib(f, b0, b1, a.tbs_bits, 24, CRC24A_POLY, a.crc24a_table, T), partial);
+  const uint32_t b0 = c0 + threadIdx.x * ASM_TB_PER;
+  const uint32_t b1 = min(nbytes, b0 + ASM_TB_PER);
+  const uint32_t v  = crc_block_xor<ASM_THREADS>(
+      crc_chunk_contrib(lds_fetch{s_chunk, c0}, b0, b1, a.tbs_bits, 24, CRC24A_POLY, a.crc24a_table, T), partial);
   if (threadIdx.x == 0 && v != 0) {
     atomicXor(a.acc + t, v);
   }

@@ -130,11 +130,11 @@ def test_pusch_processor_batch_matches_host():
 
 @pytest.mark.parametrize("td,mask,eq", [(0, (1 << 2) | (1 << 11), 0), (1, (1 << 2) | (1 << 11), 0),
                                          (0, 1 << 2, 1), (0, (1 << 2) | (1 << 7) | (1 << 11), 0)],
-                         ids=["interp_2dmrs_zf", "average_2dmrs_zf", "interp_1dmrs_mmse", "interp_3dmrs_expanded"])
+                         ids=["interp_2dmrs_zf", "average_2dmrs_zf", "interp_1dmrs_mmse", "interp_3dmrs_zf"])
 def test_pusch_processor_fused_equalizer_identical(td, mask, eq):
     """Without a caller estimate buffer the processor fuses the estimate expansion into the equalizer
-    (one or two LSE slices per subcarrier; three DM-RS symbols interpolated keep the expanded path): LLRs,
-    transport blocks and results are bit-identical to the run that writes the estimates."""
+    (each OFDM symbol reads the one or two LSE slices its time-domain strategy needs): LLRs, transport blocks
+    and results are bit-identical to the run that writes the estimates."""
     import torch
 
     name, over, nprb, ch, snr, iters = CASES[3]
