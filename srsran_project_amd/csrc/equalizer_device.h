@@ -12,6 +12,11 @@
 
 #include <cstdint>
 
+// Contraction only within one source expression (fmuladd), never across statements: the results then do
+// not depend on how a kernel's control flow splits the code into blocks, so every kernel that inlines these
+// functions (the expanded-estimate and the estimator-fused equalizers) produces the same bits.
+#pragma clang fp contract(on)
+
 namespace srs_amd {
 namespace eq {
 
@@ -140,46 +145,71 @@ __device__ __forceinline__ void equalize_2xn(const cplx* y,
 // so the kernel stays HBM-bound and matrix cores would not shorten it.  A Cholesky pivot that is
 // not a normal number above 2^-20 times its diagonal entry (a singular channel in float32 terms),
 // an invalid sigma^2 or mu_l <= 2^-20 gives zero symbols with infinite variances for the RE, as the
-// reference does for abnormal 2 x N inputs.
-template <int P, int L, bool MMSE>
-__device__ __forceinline__ void equalize_mimo(const cplx* y,  // [P]
-                                              const cplx* h,  // [P][L]
-                                              float       noise_var,
-                                              bool        noise_ok,
-                                              float       tx_scaling,
-                                              cplx*       out, // [L]
-                                              float*      nv)  // [L]
+// reference does for abnormal 2 x N inputs (equalize_mimo below).
+
+// The normal equations of one RE, accumulated port by port (each entry sums its ports in port order), so a
+// caller can build them while it produces the channel coefficients of each port.
+template <int L>
+struct mimo_system {
+  cplx a[L][L]; // H^H H, lower triangle (row i >= column k)
+  cplx b[L];    // H^H y
+};
+
+template <int L>
+__device__ __forceinline__ void mimo_init(mimo_system<L>& s)
+{
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+#pragma unroll
+    for (int k = 0; k <= i; ++k) {
+      s.a[i][k] = {0.0f, 0.0f};
+    }
+    s.b[i] = {0.0f, 0.0f};
+  }
+}
+
+// Port p's terms: hp[L] its channel coefficients, yp its received sample.
+template <int L>
+__device__ __forceinline__ void mimo_add_port(mimo_system<L>& s, const cplx* hp, cplx yp)
+{
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+#pragma unroll
+    for (int k = 0; k <= i; ++k) {
+      const cplx t = mul_conj(hp[k], hp[i]); // (H^H H)_{i,k} = sum_p conj(H_pi) H_pk
+      s.a[i][k].x += t.x;
+      s.a[i][k].y += t.y;
+    }
+    const cplx t = mul_conj(yp, hp[i]); // conj(h_i) y
+    s.b[i].x += t.x;
+    s.b[i].y += t.y;
+  }
+}
+
+template <int L, bool MMSE>
+__device__ __forceinline__ void mimo_solve(mimo_system<L>& sys,
+                                           float           noise_var,
+                                           bool            noise_ok,
+                                           float           tx_scaling,
+                                           cplx*           out, // [L]
+                                           float*          nv)  // [L]
 {
   // A (lower triangle, row i >= column k) and the right-hand side
-  cplx a[L][L];
-  cplx b[L];
+  cplx(&a)[L][L] = sys.a;
+  cplx(&b)[L]    = sys.b;
   const float ga = MMSE ? tx_scaling * tx_scaling : 1.0f;
   const float gb = MMSE ? tx_scaling : 1.0f;
 #pragma unroll
   for (int i = 0; i < L; ++i) {
 #pragma unroll
     for (int k = 0; k <= i; ++k) {
-      cplx acc = {0.0f, 0.0f};
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const cplx t = mul_conj(h[p * L + k], h[p * L + i]); // (H^H H)_{i,k} = sum_p conj(H_pi) H_pk
-        acc.x += t.x;
-        acc.y += t.y;
-      }
-      a[i][k] = {acc.x * ga, acc.y * ga};
+      a[i][k] = {a[i][k].x * ga, a[i][k].y * ga};
     }
     a[i][i].y = 0.0f;
     if (MMSE) {
       a[i][i].x += noise_var;
     }
-    cplx acc = {0.0f, 0.0f};
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const cplx t = mul_conj(y[p], h[p * L + i]); // conj(h_i) y
-      acc.x += t.x;
-      acc.y += t.y;
-    }
-    b[i] = {acc.x * gb, acc.y * gb};
+    b[i] = {b[i].x * gb, b[i].y * gb};
   }
   // Cholesky A = C C^H (C lower, real diagonal), kept in a[][]; r[k] = 1 / C_kk
   float r[L];
@@ -275,6 +305,24 @@ __device__ __forceinline__ void equalize_mimo(const cplx* y,  // [P]
       nv[l]  = __builtin_inff();
     }
   }
+}
+
+template <int P, int L, bool MMSE>
+__device__ __forceinline__ void equalize_mimo(const cplx* y,  // [P]
+                                              const cplx* h,  // [P][L]
+                                              float       noise_var,
+                                              bool        noise_ok,
+                                              float       tx_scaling,
+                                              cplx*       out, // [L]
+                                              float*      nv)  // [L]
+{
+  mimo_system<L> sys;
+  mimo_init(sys);
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    mimo_add_port(sys, h + p * L, y[p]);
+  }
+  mimo_solve<L, MMSE>(sys, noise_var, noise_ok, tx_scaling, out, nv);
 }
 
 } // namespace eq

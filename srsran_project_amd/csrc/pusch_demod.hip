@@ -92,6 +92,19 @@ __device__ __forceinline__ void emit_llrs(const pusch_eq_args& a, const float* l
   }
 }
 
+// channel_equalizer_generic_impl.cpp:304: the largest port variance (std::max_element order) of grid gi.
+template <int P>
+__device__ __forceinline__ void port_noise_max(const pusch_eq_args& a, uint32_t gi, float& nmax, bool& ok)
+{
+  const srs_amd_chest_port_stats* st = a.stats + gi * P;
+  nmax                               = st[0].noise_var;
+#pragma unroll
+  for (int p = 1; p < P; ++p) {
+    nmax = (nmax < st[p].noise_var) ? st[p].noise_var : nmax;
+  }
+  ok = __builtin_isnormal(nmax) && nmax >= 0.0f;
+}
+
 // Equalizes data RE j (OFDM symbol l) of grid gi from its received samples y[P] and channel coefficients
 // h[P][L], then demaps and descrambles the L symbols into the grid's LLR row (no symbol round trip via HBM).
 template <int P, int L, bool MMSE>
@@ -120,13 +133,9 @@ __device__ __forceinline__ void equalize_write(const pusch_eq_args& a, const flo
     so[0]  = make_float2(s.x, s.y);
     nvo[0] = nv;
   } else {
-    // channel_equalizer_generic_impl.cpp:304: the largest port variance (std::max_element order).
-    float nmax = st[0].noise_var;
-#pragma unroll
-    for (int p = 1; p < P; ++p) {
-      nmax = (nmax < st[p].noise_var) ? st[p].noise_var : nmax;
-    }
-    const bool ok = __builtin_isnormal(nmax) && nmax >= 0.0f;
+    float nmax;
+    bool  ok;
+    port_noise_max<P>(a, gi, nmax, ok);
     if constexpr (L == 2 && !MMSE) {
       eq::cplx h0[P], h1[P];
 #pragma unroll
@@ -196,7 +205,8 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
 constexpr uint32_t EQ_XCDS = 8;
 
 template <int P, int L, bool MMSE>
-__global__ __launch_bounds__(256) void pusch_equalize_fused_kernel(pusch_eq_args a, chest_args c)
+// six waves per SIMD (<= 80 VGPRs, no spills for the 4 x 4 solve) to hide the per-RE memory latency
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void pusch_equalize_fused_kernel(pusch_eq_args a, chest_args c)
 {
   __shared__ float2 s_ph[P];
   __shared__ int    s_rot[P];
@@ -232,21 +242,51 @@ __global__ __launch_bounds__(256) void pusch_equalize_fused_kernel(pusch_eq_args
   const uint32_t  plane = 14 * a.nof_subc;
   const int       i0    = chdev::lse_index(c, l);
   const bool      two   = c.td != SRS_AMD_CHEST_TD_AVERAGE && c.td_interp[l];
-  eq::cplx        y[P], h[P * L];
+  // channel coefficient of port p, layer v
+  auto coef = [&](int p, int v) {
+    const float2*  fr = c.freq + (((static_cast<uint64_t>(gi) * P + p) * L + v) * c.nof_lse + i0) * c.nof_re + kk;
+    const float2   x0 = fr[0];
+    const float2   x1 = two ? fr[c.nof_re] : x0;
+    const uint32_t u  = chdev::expand_pair(c, x0, x1, l, s_rot[p] != 0, s_ph[p]);
+    return eq::from_cbf16(u);
+  };
+  if constexpr (L >= 3 || (L == 2 && MMSE)) {
+    // the normal equations built port by port as the coefficients are rebuilt (few live registers)
+    eq::mimo_system<L> sys;
+    eq::mimo_init(sys);
 #pragma unroll
-  for (int p = 0; p < P; ++p) {
-    y[p] = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane]);
+    for (int p = 0; p < P; ++p) {
+      eq::cplx hp[L];
+#pragma unroll
+      for (int v = 0; v < L; ++v) {
+        hp[v] = coef(p, v);
+      }
+      eq::mimo_add_port(sys, hp, eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane]));
+    }
+    float nmax;
+    bool  ok;
+    port_noise_max<P>(a, gi, nmax, ok);
+    eq::cplx s[L];
+    float    nv[L];
+    eq::mimo_solve<L, MMSE>(sys, nmax, ok, 1.0f, s, nv);
+    float2 so[L];
 #pragma unroll
     for (int v = 0; v < L; ++v) {
-      const float2* fr =
-          c.freq + (((static_cast<uint64_t>(gi) * P + p) * L + v) * c.nof_lse + i0) * c.nof_re + kk;
-      const float2   x0 = fr[0];
-      const float2   x1 = two ? fr[c.nof_re] : x0;
-      const uint32_t u  = chdev::expand_pair(c, x0, x1, l, s_rot[p] != 0, s_ph[p]);
-      h[p * L + v]      = eq::from_cbf16(u);
+      so[v] = make_float2(s[v].x, s[v].y);
     }
+    emit_llrs<L>(a, lt, gi, j, l, so, nv);
+  } else {
+    eq::cplx y[P], h[P * L];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      y[p] = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane]);
+#pragma unroll
+      for (int v = 0; v < L; ++v) {
+        h[p * L + v] = coef(p, v);
+      }
+    }
+    equalize_write<P, L, MMSE>(a, lt, gi, j, l, y, h);
   }
-  equalize_write<P, L, MMSE>(a, lt, gi, j, l, y, h);
 }
 
 } // namespace
