@@ -521,8 +521,7 @@ int srs_amd::rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
                                    uint32_t                          nof_cbs,
                                    void*                             stream,
                                    bool                              fresh,
-                                   uint32_t                          write_end,
-                                   uint32_t                          max_rm_length)
+                                   uint32_t                          write_end)
 {
   if (dm == nullptr) {
     return fail(SRS_AMD_EINVAL, "null rate dematcher");
@@ -550,7 +549,6 @@ int srs_amd::rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
   a.new_data    = new_data ? 1 : 0;
   a.fresh       = (fresh && new_data) ? 1 : 0;
   a.write_end   = (write_end == 0 || write_end > a.g.N) ? a.g.N : write_end;
-  a.max_rm_length = max_rm_length;
   std::lock_guard<std::mutex> lock(dm->mtx);
   hipError_t                  e = hipSetDevice(dm->device);
   if (e == hipSuccess) {

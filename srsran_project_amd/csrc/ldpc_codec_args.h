@@ -39,7 +39,6 @@ struct dematch_args {
   int32_t         new_data;
   int32_t         fresh;     // previous soft-buffer contents are known to be zero (not read)
   uint32_t        write_end; // soft-buffer bytes [write_end, N) are not written (nobody reads them); N: all
-  uint32_t        max_rm_length; // largest E of the batch (0: unknown)
   rm_geometry     g;
 };
 

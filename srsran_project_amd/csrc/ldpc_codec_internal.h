@@ -24,8 +24,7 @@ int rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
                           uint32_t                          nof_cbs,
                           void*                             stream,
                           bool                              fresh,
-                          uint32_t                          write_end     = 0,
-                          uint32_t                          max_rm_length = 0);
+                          uint32_t                          write_end = 0);
 
 // srs_amd_ldpc_encode_batch producing only the first max_bits of each shortened
 // codeword (the rows of the extension region beyond them are not computed and

@@ -33,6 +33,8 @@
 // following codeblocks' bits, so no two threads write one byte.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ldpc_common.h"
 #include "ldpc_codec_args.h"
 
@@ -108,7 +110,30 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
         const uint32_t i = divQ.div(x, j);
         s_in[j * Kq + i] = v;
       };
-      if (((reinterpret_cast<uintptr_t>(in) | E) & 15u) == 0) {
+      // one thread per modulation symbol i: its Qm LLRs (one load) to rows j = 0 .. Qm-1
+      auto by_symbol = [&](auto qm_tag) {
+        constexpr uint32_t QM = decltype(qm_tag)::value;
+        using word            = typename std::conditional<QM == 8, uint2, typename std::conditional<QM == 4, uint32_t, uint16_t>::type>::type;
+        for (uint32_t i = threadIdx.x; i < Kq; i += DEMATCH_THREADS) {
+          union {
+            word   w;
+            int8_t b[QM];
+          } u;
+          u.w = reinterpret_cast<const word*>(in)[i];
+#pragma unroll
+          for (uint32_t j = 0; j < QM; ++j) {
+            s_in[j * Kq + i] = u.b[j];
+          }
+        }
+      };
+      const uintptr_t ia = reinterpret_cast<uintptr_t>(in);
+      if (g.Qm == 8 && (ia & 7u) == 0) {
+        by_symbol(std::integral_constant<uint32_t, 8>{});
+      } else if (g.Qm == 4 && (ia & 3u) == 0) {
+        by_symbol(std::integral_constant<uint32_t, 4>{});
+      } else if (g.Qm == 2 && (ia & 1u) == 0) {
+        by_symbol(std::integral_constant<uint32_t, 2>{});
+      } else if (((reinterpret_cast<uintptr_t>(in) | E) & 15u) == 0) {
         for (uint32_t x = threadIdx.x; x < E / 16; x += DEMATCH_THREADS) {
           union {
             uint4  v;
@@ -308,67 +333,6 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
 }
 
 
-// New data into a fresh (zero) soft buffer without repetition (every E <= L - rank0) -- the common PUSCH
-// first transmission: each position of the written prefix is a pure function of its own input, so one
-// thread produces 16 consecutive soft-buffer bytes straight from the received LLRs (a strided byte gather
-// served by L1/L2: a codeblock's input is a few KB) with one 16-byte store, and a codeblock spreads over
-// as many workgroups as its prefix needs -- no LDS staging, no barrier, one memory round trip.
-// Same values as ldpc_rate_dematch_kernel's first pass: 0 before k0 / past the input, +inf on the
-// fillers, the deinterleaved input elsewhere, 0 from the tail zeroing on.
-__global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_gather_kernel(dematch_args a)
-{
-  const rm_geometry& g   = a.g;
-  const uint32_t     cb  = blockIdx.y;
-  const uint32_t     p0  = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD;
-  if (p0 >= a.write_end) {
-    return;
-  }
-  const uint32_t E   = a.rm_lengths[cb];
-  const int8_t*  in  = a.in + a.in_offsets[cb];
-  int8_t*        buf = a.soft + static_cast<size_t>(cb) * a.soft_stride;
-  const uint32_t Kq  = E / g.Qm;
-  const uint32_t L1  = g.L - g.rank0;
-  uint32_t       zero_from = g.N;
-  {
-    uint32_t tmp;
-    if (E == 0) {
-      tmp = g.k0;
-    } else if (g.rank0 < g.nof_info) {
-      const uint32_t n1 = min(g.nof_info - g.rank0, E);
-      tmp               = (g.nof_sys + (E - n1)) % g.Ncb;
-    } else {
-      tmp = (g.rank0 + g.F + E) % g.Ncb;
-    }
-    if (tmp != 0) {
-      zero_from = g.N - (g.Ncb - tmp);
-    }
-  }
-  union {
-    uint4  v;
-    int8_t b[16];
-  } out;
-  if (p0 >= zero_from) {
-    out.v = make_uint4(0, 0, 0, 0);
-  } else {
-    const fast_div divK(Kq > 0 ? Kq : 1u);
-#pragma unroll
-    for (int k = 0; k < DEMATCH_PER_THREAD; ++k) {
-      const uint32_t p      = p0 + k;
-      const bool     filler = p >= g.nof_info && p < g.nof_sys;
-      const uint32_t w      = p < g.nof_info ? p : p - g.F;
-      const uint32_t t      = w >= g.rank0 ? w - g.rank0 : w + L1;
-      int            v      = filler ? LLR_INFINITY : 0;
-      if (!filler && p < g.Ncb && t < E) {
-        uint32_t       i;
-        const uint32_t j = divK.div(t, i);
-        v                = in[i * g.Qm + j];
-      }
-      out.b[k] = static_cast<int8_t>(p >= zero_from ? 0 : v);
-    }
-  }
-  *reinterpret_cast<uint4*>(buf + p0) = out.v;
-}
-
 constexpr int      RATE_MATCH_THREADS = 256;
 constexpr uint32_t RM_MAX_CW_BYTES    = 66 * 384 / 8; // circular buffer of BG1, Z = 384
 
@@ -476,15 +440,6 @@ hipError_t launch_rate_dematch(const dematch_args& a, hipStream_t stream)
 {
   // one workgroup per codeblock: splitting a codeblock over several (each staging its input) measured
   // twice as slow
-  const rm_geometry& g = a.g;
-  if (a.fresh && a.new_data && a.max_rm_length > 0 && a.max_rm_length <= g.L - g.rank0 && g.Qm > 0 &&
-      (g.N & 15u) == 0 && (a.soft_stride & 15u) == 0 && (reinterpret_cast<uintptr_t>(a.soft) & 15u) == 0 &&
-      a.nof_cbs <= 65535u) {
-    const uint32_t per = DEMATCH_THREADS * DEMATCH_PER_THREAD;
-    dim3           grid((a.write_end + per - 1) / per, a.nof_cbs);
-    hipLaunchKernelGGL(ldpc_rate_dematch_gather_kernel, grid, dim3(DEMATCH_THREADS), 0, stream, a);
-    return hipGetLastError();
-  }
   dim3 grid(1, a.nof_cbs < 65535u ? a.nof_cbs : 65535u);
   hipLaunchKernelGGL(ldpc_rate_dematch_kernel, grid, dim3(DEMATCH_THREADS), 0, stream, a);
   return hipGetLastError();

@@ -89,7 +89,6 @@ __device__ __forceinline__ uint32_t codeword_word(const uint8_t* cw, uint32_t no
 }
 
 constexpr int MAX_WORDS = PDSCH_THREADS + 2; // 256 REs x 4 layers x 8 bits / 32 + 2
-constexpr uint32_t GOLD_RUN = 4;             // Gold words per scrambling thread
 
 __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args a)
 {
@@ -116,18 +115,10 @@ __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args
   if (a.qm >= 2 && threadIdx.x < (1u << a.qm)) {
     s_qam[threadIdx.x] = qam_point(threadIdx.x, a.qm);
   }
-  // GOLD_RUN consecutive words per thread: one jump-ahead, then word-parallel LFSR steps
+  // the block's codeword words XOR the plan's scrambling words (one word per thread)
   const uint32_t nw = w_hi - w_lo;
-  for (uint32_t q = threadIdx.x * GOLD_RUN; q < nw; q += PDSCH_THREADS * GOLD_RUN) {
-    uint32_t x1, x2;
-    gold_state(a.jump, a.c_init, 32 * (w_lo + q), x1, x2);
-#pragma unroll
-    for (uint32_t r = 0; r < GOLD_RUN; ++r) {
-      const uint32_t c = gold_next32(x1, x2);
-      if (q + r < nw) {
-        scrambled[q + r] = codeword_word(cw, nof_bytes, w_lo + q + r) ^ c;
-      }
-    }
+  for (uint32_t q = threadIdx.x; q < nw; q += PDSCH_THREADS) {
+    scrambled[q] = codeword_word(cw, nof_bytes, w_lo + q) ^ a.scr[w_lo + q];
   }
   __syncthreads();
 

@@ -18,6 +18,7 @@
 #include "api_common.h"
 #include "device_buffer.h"
 #include "gold_sequence.h"
+#include "modulation_args.h"
 #include "pdsch_modulator_args.h"
 #include <cmath>
 #include <mutex>
@@ -49,10 +50,12 @@ struct srs_amd_pdsch_mod_plan {
   uint32_t       span_subc   = 0;
   uint32_t       nof_re      = 0;
   uint32_t*      d_table     = nullptr;
+  uint32_t*      d_scr       = nullptr; // Gold words of c_init over the codeword (+1)
   ~srs_amd_pdsch_mod_plan()
   {
     (void)hipSetDevice(device);
     (void)hipFree(d_table);
+    (void)hipFree(d_scr);
   }
 };
 
@@ -259,10 +262,23 @@ int srs_amd_pdsch_mod_plan_create(srs_amd_pdsch_modulator*        mod,
   if (e == hipSuccess) {
     e = hipMemcpy(p->d_table, table.data(), table.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   }
+  // the scrambling sequence of the plan's c_init, generated once (the map kernel XORs table words)
+  const uint32_t bps       = cfg->modulation < 2 ? 1u : static_cast<uint32_t>(cfg->modulation);
+  const uint32_t nof_words = (count * cfg->nof_layers * bps + 31) / 32 + 1;
+  if (e == hipSuccess) {
+    e = hipMalloc(&p->d_scr, nof_words * sizeof(uint32_t));
+  }
+  if (e == hipSuccess) {
+    e = launch_gold_words(mod->d_jump, a.c_init, p->d_scr, nof_words, nullptr);
+  }
+  if (e == hipSuccess) {
+    e = hipStreamSynchronize(nullptr);
+  }
   if (e != hipSuccess) {
     delete p;
     return hip_fail(e, "PDSCH modulator plan");
   }
+  a.scr      = p->d_scr;
   a.re_table = p->d_table;
   *plan      = p;
   if (nof_re != nullptr) {

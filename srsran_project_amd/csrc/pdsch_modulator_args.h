@@ -18,6 +18,7 @@ struct pdsch_map_args {
   uint32_t*       grids;      // cbf16 REs
   const uint32_t* re_table;   // [14][nof_prb]: (data RE index of the PRB's first RE) << 12 | 12-bit data RE mask
   const uint32_t* jump;       // Gold-sequence jump matrices
+  const uint32_t* scr;        // Gold words of c_init (c(32 w + b) at bit b of word w), one past the codeword
   uint64_t        grid_stride;
   uint32_t        port_stride; // 14 * nof_subc
   uint32_t        nof_subc;

@@ -159,7 +159,7 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   const uint32_t prefix = llr_prefix(p, lay, cfg->new_data != 0, internal);
   int rc = rate_dematch_batch_ex(d->dm, &md, cfg->new_data ? 1 : 0, d_llrs, d->arrays.as<uint32_t>() + rows,
                                  d->arrays.as<uint32_t>(), d_soft, lay.row_bytes, rows, stream, internal,
-                                 internal ? prefix : 0, std::max(p->rm_length_long, p->rm_length_short));
+                                 internal ? prefix : 0);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
