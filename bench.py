@@ -82,12 +82,16 @@ def parse():
     return p.parse_args()
 
 
-def load_traffic(name):
+def load_traffic(name, kernel=None):
     """HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    (tools/gpu_check.sh traffic), committed under profiles/."""
+    (tools/gpu_check.sh traffic, tools/pmc_summary.py), committed under profiles/;
+    `kernel` picks one kernel of a multi-kernel summary."""
     tpath = os.path.join(ROOT, "profiles", name)
     if os.path.exists(tpath):
-        return json.load(open(tpath)).get("hbm_bytes_per_launch")
+        d = json.load(open(tpath))
+        if kernel is not None and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel].get("hbm_bytes_per_launch")
+        return d.get("hbm_bytes_per_launch")
     return None
 
 
@@ -397,7 +401,7 @@ def main():
         from bench_pipeline import run_pipeline
 
         line = run_pipeline(args, dist, world, rank, dev, timed, HBM_PEAK_GBS,
-                            load_traffic("r02_pipeline_ldpc_traffic.json"))
+                            load_traffic("r02_final_traffic.json", "ldpc_decode_hr_kernel"))
     else:
         run = run_ldpc if args.workload == "ldpc" else run_ofdm
         line = run(args, dist, world, rank, dev)
