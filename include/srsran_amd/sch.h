@@ -165,6 +165,33 @@ int srs_amd_pusch_decode_batch(srs_amd_pusch_decoder*              dec,
                                uint32_t                            nof_tbs,
                                void*                               stream);
 
+/* One UE's transport block of a heterogeneous slot batch (srs_amd_pusch_decode_slot). */
+typedef struct srs_amd_pusch_ue {
+  srs_amd_sch_plan plan;       /* computed with srs_amd_sch_plan_compute; any BG / Z / Qm / rv / Nref / TBS */
+  uint64_t         llr_offset; /* byte offset of this UE's plan.cw_length LLRs in d_llrs */
+  uint64_t         tb_offset;  /* byte offset of this UE's plan.tbs / 8 transport-block bytes in d_tbs */
+} srs_amd_pusch_ue;
+
+/* DEVICE, asynchronous: the new transmissions of nof_ues UEs with DIFFERENT plans (the PUSCH
+ * allocations of one slot: PRBs, MCS, layers, rv differ per UE), decoded as one launch sequence
+ * rather than one per UE -- what pusch_decoder_impl::new_data does once per PUSCH PDU of the slot
+ * (pusch_decoder_impl.cpp:89, called per PDU at pusch_processor_impl.cpp:343).  ues: HOST array; the codeword
+ * LLRs of UE u start at d_llrs + ues[u].llr_offset, its transport block is written at
+ * d_tbs + ues[u].tb_offset and its result to d_results[u].  Semantics per UE identical to
+ * srs_amd_pusch_decode_batch with new_data = 1 and internal soft buffers: cfg->new_data must be 1
+ * (HARQ retransmissions keep their caller soft buffers through srs_amd_pusch_decode_batch).
+ * One rate-dematching launch over every codeblock of the slot (per-codeblock geometry), one
+ * LDPC decoding launch per (base graph, lifting size, CRC, bounded LLR prefix) bucket, one assembly sequence
+ * (per-TB descriptors).  The LLR span of the batch must stay below 2^32 bytes. */
+int srs_amd_pusch_decode_slot(srs_amd_pusch_decoder*              dec,
+                              const srs_amd_pusch_decoder_config* cfg,
+                              const srs_amd_pusch_ue*             ues,
+                              uint32_t                            nof_ues,
+                              const int8_t*                       d_llrs,
+                              uint8_t*                            d_tbs,
+                              srs_amd_pusch_decoder_result*       d_results,
+                              void*                               stream);
+
 #ifdef __cplusplus
 }
 #endif

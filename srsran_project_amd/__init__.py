@@ -91,6 +91,7 @@ from .sch import (  # noqa: F401
     PuschDecoder,
     PuschDecoderConfig,
     PuschDecoderResult,
+    PuschUe,
     SchPlan,
     sch_plan,
     sch_segments,

@@ -231,7 +231,8 @@ int srs_amd::ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
                                   uint32_t                           nof_cbs,
                                   void*                              stream,
                                   const uint8_t*                     d_skip_flags,
-                                  uint32_t                           skip_stride)
+                                  uint32_t                           skip_stride,
+                                  const int32_t*                     d_fillers)
 {
   if (d == nullptr) {
     return fail(SRS_AMD_EINVAL, "null decoder");
@@ -290,6 +291,7 @@ int srs_amd::ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
   a.force_decoding  = d->force_decoding;
   a.skip_flags      = d_skip_flags;
   a.skip_stride     = skip_stride;
+  a.fillers         = d_fillers;
   const int grid    = static_cast<int>(nof_cbs < d->max_slots ? nof_cbs : d->max_slots);
   e = launch_ldpc_decode(a, g, d->arith, grid, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) {

@@ -557,6 +557,49 @@ int srs_amd::rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_rate_dematch_kernel launch");
 }
 
+int srs_amd::rate_dematch_ragged(srs_amd_ldpc_rate_dematcher* dm,
+                                 const int8_t*                d_input,
+                                 const uint32_t*              d_in_offsets,
+                                 const uint32_t*              d_rm_lengths,
+                                 const uint32_t*              d_row_geo,
+                                 const void*                  d_geos,
+                                 const uint32_t*              d_geo_write_end,
+                                 int8_t*                      d_soft,
+                                 uint32_t                     soft_stride,
+                                 uint32_t                     nof_cbs,
+                                 void*                        stream)
+{
+  if (dm == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null rate dematcher");
+  }
+  if (nof_cbs == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_input == nullptr || d_in_offsets == nullptr || d_rm_lengths == nullptr || d_row_geo == nullptr ||
+      d_geos == nullptr || d_geo_write_end == nullptr || d_soft == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  // the caller (srs_amd_pusch_decode_slot) checked every geometry and soft_stride >= every N
+  dematch_args a{};
+  a.in            = d_input;
+  a.in_offsets    = d_in_offsets;
+  a.rm_lengths    = d_rm_lengths;
+  a.soft          = d_soft;
+  a.soft_stride   = soft_stride;
+  a.nof_cbs       = nof_cbs;
+  a.new_data      = 1;
+  a.fresh         = 1;
+  a.row_geo       = d_row_geo;
+  a.geos          = static_cast<const rm_geometry*>(d_geos);
+  a.geo_write_end = d_geo_write_end;
+  std::lock_guard<std::mutex> lock(dm->mtx);
+  hipError_t                  e = hipSetDevice(dm->device);
+  if (e == hipSuccess) {
+    e = launch_rate_dematch(a, static_cast<hipStream_t>(stream));
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_rate_dematch_kernel launch");
+}
+
 extern "C" {
 
 int srs_amd_ldpc_rate_dematch(srs_amd_ldpc_rate_dematcher*      dm,

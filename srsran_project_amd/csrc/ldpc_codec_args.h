@@ -40,6 +40,10 @@ struct dematch_args {
   int32_t         fresh;     // previous soft-buffer contents are known to be zero (not read)
   uint32_t        write_end; // soft-buffer bytes [write_end, N) are not written (nobody reads them); N: all
   rm_geometry     g;
+  // optional per-codeblock geometry (replaces g / write_end): codeblock cb uses geos[row_geo[cb]]
+  const uint32_t*    row_geo;
+  const rm_geometry* geos;
+  const uint32_t*    geo_write_end;
 };
 
 struct rate_match_args {

@@ -57,6 +57,22 @@ int ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
                          uint32_t                           nof_cbs,
                          void*                              stream,
                          const uint8_t*                     d_skip_flags,
-                         uint32_t                           skip_stride);
+                         uint32_t                           skip_stride,
+                         const int32_t*                     d_fillers = nullptr);
+
+// Rate dematching of codeblocks with per-codeblock geometry (srs_amd_pusch_decode_slot): codeblock cb
+// uses geos[row_geo[cb]] and writes soft-buffer bytes [0, geo_write_end[row_geo[cb]]) of its row
+// (new data into fresh internal buffers, whose old contents are taken as zero).
+int rate_dematch_ragged(srs_amd_ldpc_rate_dematcher* dm,
+                        const int8_t*                d_input,
+                        const uint32_t*              d_in_offsets,
+                        const uint32_t*              d_rm_lengths,
+                        const uint32_t*              d_row_geo,
+                        const void*                  d_geos,
+                        const uint32_t*              d_geo_write_end,
+                        int8_t*                      d_soft,
+                        uint32_t                     soft_stride,
+                        uint32_t                     nof_cbs,
+                        void*                        stream);
 
 } // namespace srs_amd

@@ -68,6 +68,9 @@ struct decode_args {
   // passed earlier is only rate dematched (pusch_decoder_impl.cpp:330-345)
   const uint8_t*  skip_flags;
   uint32_t        skip_stride;
+  // optional per-codeblock filler-bit count (replaces nof_filler_bits): a launch over the codeblocks of
+  // several transport blocks with different segmentations (srs_amd_pusch_decode_slot)
+  const int32_t*  fillers;
 };
 constexpr int32_t LDPC_ITERS_SKIPPED = -2;
 

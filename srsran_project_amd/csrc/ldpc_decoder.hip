@@ -601,7 +601,7 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
       cb_len = msg_len + 4 * Z;
     }
     const int nof_layers = (cb_len + Z - 1) / Z - bg_traits<BG>::K;
-    const int nof_sig    = msg_len - a.nof_filler_bits;
+    const int nof_sig    = msg_len - (a.fillers ? a.fillers[cb] : a.nof_filler_bits);
     int       result     = -1;
 
     // check row of this lane (== j unless rows are spread 48 per wave)
@@ -1055,7 +1055,7 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
     }
     const int cb_len     = max(input_size + 2 * Z, K + 4 * Z);
     const int nof_layers = (cb_len + Z - 1) / Z - 22;
-    const int nof_sig    = K - a.nof_filler_bits;
+    const int nof_sig    = K - (a.fillers ? a.fillers[cb] : a.nof_filler_bits);
     int       result     = -1;
 
     hr_msgs<NE> c2v;

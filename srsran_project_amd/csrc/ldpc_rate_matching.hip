@@ -88,11 +88,16 @@ constexpr uint32_t DEMATCH_LDS   = 12288; // received LLRs of a codeblock staged
 
 // One workgroup per codeblock: the codeblock's received LLRs (deinterleaver input) are staged in LDS
 // with coalesced loads when they fit, then each thread produces 16 consecutive soft-buffer bytes.
+// RAGGED: per-codeblock geometry (a.row_geo / a.geos / a.geo_write_end), a separate instantiation so the
+// uniform launch keeps its geometry in kernel arguments.
+template <bool RAGGED>
 __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dematch_args a)
 {
   __shared__ __attribute__((aligned(16))) int8_t s_in[DEMATCH_LDS];
-  const rm_geometry& g = a.g;
   for (uint32_t cb = blockIdx.y; cb < a.nof_cbs; cb += gridDim.y) {
+    const uint32_t    gi        = RAGGED ? a.row_geo[cb] : 0u;
+    const rm_geometry g         = RAGGED ? a.geos[gi] : a.g;
+    const uint32_t    write_end = RAGGED ? a.geo_write_end[gi] : a.write_end;
     const uint32_t E   = a.rm_lengths[cb];
     const int8_t*  in  = a.in + a.in_offsets[cb];
     int8_t*        buf = a.soft + static_cast<size_t>(cb) * a.soft_stride;
@@ -197,7 +202,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
     if (staged && vec && first_pass && E <= L1) {
       // Single first pass (no combining), branch-free: every position selects between its old value,
       // zero, +inf (filler) and its input, whose LDS read is always issued at a clamped index.
-      for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < a.write_end; p0 += step) {
+      for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < write_end; p0 += step) {
         union {
           uint4  v;
           int8_t b[16];
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
       }
       continue;
     }
-    for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < a.write_end; p0 += step) {
+    for (uint32_t p0 = (blockIdx.x * DEMATCH_THREADS + threadIdx.x) * DEMATCH_PER_THREAD; p0 < write_end; p0 += step) {
       union {
         uint4  v;
         int8_t b[16];
@@ -441,7 +446,11 @@ hipError_t launch_rate_dematch(const dematch_args& a, hipStream_t stream)
   // one workgroup per codeblock: splitting a codeblock over several (each staging its input) measured
   // twice as slow
   dim3 grid(1, a.nof_cbs < 65535u ? a.nof_cbs : 65535u);
-  hipLaunchKernelGGL(ldpc_rate_dematch_kernel, grid, dim3(DEMATCH_THREADS), 0, stream, a);
+  if (a.row_geo != nullptr) {
+    hipLaunchKernelGGL(ldpc_rate_dematch_kernel<true>, grid, dim3(DEMATCH_THREADS), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(ldpc_rate_dematch_kernel<false>, grid, dim3(DEMATCH_THREADS), 0, stream, a);
+  }
   return hipGetLastError();
 }
 

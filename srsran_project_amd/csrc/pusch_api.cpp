@@ -24,7 +24,9 @@
 #include "sch_args.h"
 #include <cstring>
 #include <algorithm>
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <vector>
 
 using namespace srs_amd;
@@ -36,9 +38,14 @@ struct srs_amd_pusch_decoder {
   srs_amd_crc_calculator*      crc[3] = {nullptr, nullptr, nullptr}; // CRC16, CRC24A, CRC24B
   srs_amd_ldpc_rate_dematcher* dm     = nullptr;
   srs_amd_ldpc_decoder*        dec[2] = {nullptr, nullptr}; // force_decoding 0 / 1
-  device_buffer                soft, msgs, iters, checks, arrays, results, host_io, tb_acc;
+  device_buffer                soft, msgs, iters, checks, arrays, results, host_io, tb_acc, slot_desc;
   stream_order                 order; // scratch reuse across the callers' streams
   std::mutex                   mtx;
+  // srs_amd_pusch_decode_slot: descriptors staged in pinned memory, reused once their upload completed
+  void*                        h_stage      = nullptr;
+  size_t                       h_stage_size = 0;
+  hipEvent_t                   stage_done   = nullptr;
+  bool                         stage_used   = false;
   ~srs_amd_pusch_decoder()
   {
     (void)hipSetDevice(device);
@@ -46,6 +53,11 @@ struct srs_amd_pusch_decoder {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
     }
+    if (stage_done) {
+      (void)hipEventSynchronize(stage_done);
+      (void)hipEventDestroy(stage_done);
+    }
+    (void)hipHostFree(h_stage);
     for (auto* c : crc) {
       srs_amd_crc_calculator_destroy(c);
     }
@@ -91,6 +103,17 @@ uint32_t llr_prefix(const srs_amd_sch_plan* p, const soft_row_layout& lay, bool 
   const uint32_t end = std::max(e_max + g.F, g.nof_sys);
   const uint32_t lo  = (p->base_graph == 1 ? 24u : 12u) * Z; // ldpc_decoder_impl.cpp:78 minimum input length
   return std::min(lay.soft_bytes, std::max(lo, (end + Z - 1) / Z * Z));
+}
+
+// CRC polynomial of the decoder's early stop and of the CB check (select_crc, pusch_decoder_impl.cpp:35-46).
+int crc_poly_of(const srs_amd_sch_plan* p)
+{
+  return p->nof_segments > 1 ? 1 : (p->tbs > 3824 ? 0 : 3);
+}
+
+int crc_index_of(const srs_amd_sch_plan* p)
+{
+  return p->nof_segments > 1 ? 2 : (p->tbs > 3824 ? 1 : 0);
 }
 
 int check_plan(const srs_amd_sch_plan* p)
@@ -164,8 +187,8 @@ int decode_locked(srs_amd_pusch_decoder*              d,
     return rc;
   }
   // 2. LDPC decoding (select_crc, pusch_decoder_impl.cpp:35-46).
-  const int crc_index = C > 1 ? 2 : (p->tbs > 3824 ? 1 : 0);
-  const int crc_poly  = C > 1 ? 1 : (p->tbs > 3824 ? 0 : 3);
+  const int crc_index = crc_index_of(p);
+  const int crc_poly  = crc_poly_of(p);
   srs_amd_ldpc_decoder_config dc{};
   dc.base_graph      = p->base_graph;
   dc.lifting_size    = p->lifting_size;
@@ -210,6 +233,224 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   a.max_iterations = cfg->nof_ldpc_iterations;
   a.new_data       = cfg->new_data ? 1 : 0;
   he               = launch_assemble(a, nof_tbs, stream);
+  if (he == hipSuccess) {
+    he = d->order.end(stream);
+  }
+  return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "assemble_kernel launch");
+}
+
+// srs_amd_pusch_decode_slot: every codeblock of the slot is one row of the decoder scratch (soft rows of
+// stride S, message rows of stride M), rows grouped by LDPC decoder bucket (BG, Z, CRC, bounded prefix), each
+// UE's C rows
+// contiguous.  Descriptors built on the host, uploaded once from pinned memory.
+int decode_slot_locked(srs_amd_pusch_decoder*              d,
+                       const srs_amd_pusch_decoder_config* cfg,
+                       const srs_amd_pusch_ue*             ues,
+                       uint32_t                            U,
+                       const int8_t*                       d_llrs,
+                       uint8_t*                            d_tbs,
+                       srs_amd_pusch_decoder_result*       d_results,
+                       hipStream_t                         stream)
+{
+  struct bucket {
+    uint32_t              bg, Z;
+    int                   poly;
+    uint32_t              prefix = 0, row0 = 0, rows = 0;
+    std::vector<uint32_t> ues;
+  };
+  std::vector<bucket>                                  buckets;
+  std::map<std::tuple<uint32_t, uint32_t, int, bool>, size_t> bucket_of;
+  uint32_t                                             S = 0, M = 0, R = 0, max_tb_bits = 0;
+  for (uint32_t u = 0; u < U; ++u) {
+    const srs_amd_sch_plan* p  = &ues[u].plan;
+    int                     rc = check_plan(p);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+    rm_geometry g{};
+    if (const char* msg = make_rm_geometry(g, p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                                           p->nof_filler_bits)) {
+      return fail(SRS_AMD_EINVAL, "UE %u: %s", u, msg);
+    }
+    if (ues[u].llr_offset + p->cw_length > 0xffffffffull) {
+      return fail(SRS_AMD_EINVAL, "UE %u: LLR span exceeds 2^32 bytes", u);
+    }
+    const soft_row_layout lay    = layout_of(p);
+    const uint32_t        prefix = llr_prefix(p, lay, true, true);
+    // rows whose non-zero prefix is bounded decode apart from full rows: the bucket's LLR length is its
+    // longest prefix, and a bounded one selects the high-rate decoder kernel
+    const auto key = std::make_tuple(p->base_graph, p->lifting_size, crc_poly_of(p), prefix < lay.soft_bytes);
+    auto                  it  = bucket_of.find(key);
+    if (it == bucket_of.end()) {
+      it = bucket_of.emplace(key, buckets.size()).first;
+      buckets.push_back(bucket{p->base_graph, p->lifting_size, crc_poly_of(p)});
+    }
+    bucket& b = buckets[it->second];
+    b.ues.push_back(u);
+    b.rows += p->nof_segments;
+    b.prefix    = std::max(b.prefix, prefix);
+    S           = std::max(S, static_cast<uint32_t>(align_up(lay.soft_bytes, 64)));
+    M           = std::max(M, static_cast<uint32_t>(align_up((p->segment_length + 7) / 8, 64)));
+    R          += p->nof_segments;
+    max_tb_bits = std::max(max_tb_bits, p->tbs);
+  }
+  // host descriptors: per row E, input offset, geometry, filler bits; geometries + write ends; per-TB
+  std::vector<uint32_t>                                                              row_E(R), row_in(R), row_geo(R);
+  std::vector<int32_t>                                                               row_F(R);
+  std::vector<rm_geometry>                                                           geos;
+  std::vector<uint32_t>                                                              geo_end;
+  std::map<std::tuple<size_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t>     geo_of;
+  std::vector<tb_desc>                                                               tds(U);
+  std::vector<uint32_t>                                                              segE, segOff;
+  uint32_t                                                                           row = 0;
+  for (size_t bi = 0; bi < buckets.size(); ++bi) {
+    bucket& b = buckets[bi];
+    b.row0    = row;
+    for (uint32_t u : b.ues) {
+      const srs_amd_sch_plan* p = &ues[u].plan;
+      const auto gkey = std::make_tuple(bi, p->rv, p->modulation_order, p->Nref, p->nof_filler_bits);
+      auto       git  = geo_of.find(gkey);
+      if (git == geo_of.end()) {
+        rm_geometry g{};
+        (void)make_rm_geometry(g, p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                               p->nof_filler_bits);
+        git = geo_of.emplace(gkey, static_cast<uint32_t>(geos.size())).first;
+        geos.push_back(g);
+        geo_end.push_back(b.prefix);
+      }
+      segE.resize(p->nof_segments);
+      segOff.resize(p->nof_segments);
+      (void)srs_amd_sch_plan_segments(p, segE.data(), segOff.data());
+      tds[u] = tb_desc{ues[u].tb_offset, row, p->nof_segments, p->cb_info_bits, p->tbs};
+      for (uint32_t r = 0; r < p->nof_segments; ++r, ++row) {
+        row_E[row]   = segE[r];
+        row_in[row]  = static_cast<uint32_t>(ues[u].llr_offset) + segOff[r];
+        row_geo[row] = git->second;
+        row_F[row]   = static_cast<int32_t>(p->nof_filler_bits);
+      }
+    }
+  }
+  const size_t o_E   = 0;
+  const size_t o_in  = o_E + align_up(sizeof(uint32_t) * R, 16);
+  const size_t o_geo = o_in + align_up(sizeof(uint32_t) * R, 16);
+  const size_t o_F   = o_geo + align_up(sizeof(uint32_t) * R, 16);
+  const size_t o_G   = o_F + align_up(sizeof(int32_t) * R, 16);
+  const size_t o_GE  = o_G + align_up(sizeof(rm_geometry) * geos.size(), 16);
+  const size_t o_TD  = o_GE + align_up(sizeof(uint32_t) * geos.size(), 16);
+  const size_t total = o_TD + sizeof(tb_desc) * U;
+
+  hipError_t he = hipSetDevice(d->device);
+  // the pinned staging buffer is rewritten only once its previous upload completed
+  if (he == hipSuccess && d->stage_used) {
+    he = hipEventSynchronize(d->stage_done);
+  }
+  if (he == hipSuccess && d->stage_done == nullptr) {
+    he = hipEventCreateWithFlags(&d->stage_done, hipEventDisableTiming);
+  }
+  if (he == hipSuccess && d->h_stage_size < total) {
+    (void)hipHostFree(d->h_stage);
+    d->h_stage      = nullptr;
+    d->h_stage_size = 0;
+    he              = hipHostMalloc(&d->h_stage, total, hipHostMallocDefault);
+    if (he == hipSuccess) {
+      d->h_stage_size = total;
+    }
+  }
+  if (he == hipSuccess) {
+    he = d->slot_desc.ensure(total);
+  }
+  if (he == hipSuccess) {
+    he = d->soft.ensure(static_cast<size_t>(R) * S);
+  }
+  if (he == hipSuccess) {
+    he = d->msgs.ensure(static_cast<size_t>(R) * M);
+  }
+  if (he == hipSuccess) {
+    he = d->iters.ensure(sizeof(int32_t) * R);
+  }
+  if (he == hipSuccess) {
+    he = d->checks.ensure(sizeof(uint32_t) * R);
+  }
+  if (he == hipSuccess) {
+    he = d->tb_acc.ensure(sizeof(uint32_t) * U);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PUSCH slot decoder scratch");
+  }
+  auto* h = static_cast<uint8_t*>(d->h_stage);
+  std::memcpy(h + o_E, row_E.data(), sizeof(uint32_t) * R);
+  std::memcpy(h + o_in, row_in.data(), sizeof(uint32_t) * R);
+  std::memcpy(h + o_geo, row_geo.data(), sizeof(uint32_t) * R);
+  std::memcpy(h + o_F, row_F.data(), sizeof(int32_t) * R);
+  std::memcpy(h + o_G, geos.data(), sizeof(rm_geometry) * geos.size());
+  std::memcpy(h + o_GE, geo_end.data(), sizeof(uint32_t) * geo_end.size());
+  std::memcpy(h + o_TD, tds.data(), sizeof(tb_desc) * U);
+  auto* dd = d->slot_desc.as<uint8_t>();
+  he       = d->order.begin(stream);
+  if (he == hipSuccess) {
+    he = hipMemcpyAsync(dd, h, total, hipMemcpyHostToDevice, stream);
+  }
+  if (he == hipSuccess) {
+    he = hipEventRecord(d->stage_done, stream);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PUSCH slot descriptors upload");
+  }
+  d->stage_used = true;
+  // 1. Rate dematching of every codeblock of the slot, one launch.
+  int8_t* soft = d->soft.as<int8_t>();
+  int     rc   = rate_dematch_ragged(d->dm, d_llrs, reinterpret_cast<const uint32_t*>(dd + o_in),
+                                     reinterpret_cast<const uint32_t*>(dd + o_E), reinterpret_cast<const uint32_t*>(dd + o_geo),
+                                     dd + o_G, reinterpret_cast<const uint32_t*>(dd + o_GE), soft, S, R, stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  // 2. LDPC decoding, one launch per (BG, Z, CRC, bounded prefix) bucket.
+  const int32_t*        d_F  = reinterpret_cast<const int32_t*>(dd + o_F);
+  srs_amd_ldpc_decoder* ldpc = d->dec[cfg->force_decoding ? 1 : 0];
+  for (const bucket& b : buckets) {
+    srs_amd_ldpc_decoder_config dc{};
+    dc.base_graph     = b.bg;
+    dc.lifting_size   = b.Z;
+    dc.nof_crc_bits   = b.poly == 3 ? 16 : 24;
+    dc.max_iterations = cfg->nof_ldpc_iterations;
+    rc = ldpc_decode_batch_ex(ldpc, &dc, cfg->use_early_stop ? b.poly : SRS_AMD_NO_CRC,
+                              soft + static_cast<size_t>(b.row0) * S, S, nullptr, b.prefix,
+                              d->msgs.as<uint8_t>() + static_cast<size_t>(b.row0) * M, M,
+                              d->iters.as<int32_t>() + b.row0, nullptr, b.rows, stream, nullptr, 0, d_F + b.row0);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+  }
+  // Without early stop: CRC of each decoded message (pusch_codeblock_decoder.cpp:75-86), per UE.
+  if (!cfg->use_early_stop) {
+    for (uint32_t u = 0; u < U; ++u) {
+      const srs_amd_sch_plan* p = &ues[u].plan;
+      rc = srs_amd_crc_calculate_batch(d->crc[crc_index_of(p)], d->checks.as<uint32_t>() + tds[u].row0,
+                                       d->msgs.as<uint8_t>() + static_cast<size_t>(tds[u].row0) * M, M,
+                                       p->segment_length - p->nof_filler_bits, p->nof_segments, stream);
+      if (rc != SRS_AMD_OK) {
+        return rc;
+      }
+    }
+  }
+  // 3. Concatenation and TB CRC, per-TB descriptors.
+  assemble_args a{};
+  a.msgs           = d->msgs.as<uint8_t>();
+  a.iters          = d->iters.as<int32_t>();
+  a.crc_checks     = cfg->use_early_stop ? nullptr : d->checks.as<uint32_t>();
+  a.soft           = nullptr;
+  a.tbs            = d_tbs;
+  a.results        = d_results;
+  a.cb_iterations  = nullptr;
+  a.crc24a_table   = crc_device_table(d->crc[1]);
+  a.acc            = d->tb_acc.as<uint32_t>();
+  a.msg_stride     = M;
+  a.max_iterations = cfg->nof_ldpc_iterations;
+  a.new_data       = 1;
+  a.tds            = reinterpret_cast<const tb_desc*>(dd + o_TD);
+  a.max_tb_bits    = max_tb_bits;
+  he               = launch_assemble(a, U, stream);
   if (he == hipSuccess) {
     he = d->order.end(stream);
   }
@@ -337,6 +578,35 @@ int srs_amd_pusch_decode_batch(srs_amd_pusch_decoder*              dec,
   std::lock_guard<std::mutex> lock(dec->mtx);
   return decode_locked(dec, plan, cfg, d_tbs, tb_stride, d_results, d_llrs, llr_stride, d_soft, d_cb_iterations,
                        nof_tbs, static_cast<hipStream_t>(stream));
+}
+
+int srs_amd_pusch_decode_slot(srs_amd_pusch_decoder*              dec,
+                              const srs_amd_pusch_decoder_config* cfg,
+                              const srs_amd_pusch_ue*             ues,
+                              uint32_t                            nof_ues,
+                              const int8_t*                       d_llrs,
+                              uint8_t*                            d_tbs,
+                              srs_amd_pusch_decoder_result*       d_results,
+                              void*                               stream)
+{
+  if (dec == nullptr || cfg == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (cfg->nof_ldpc_iterations == 0) {
+    return fail(SRS_AMD_EINVAL, "The number of LDPC iterations must be positive.");
+  }
+  if (!cfg->new_data) {
+    return fail(SRS_AMD_EINVAL, "slot decoding serves new transmissions; HARQ retransmissions go through "
+                                "srs_amd_pusch_decode_batch with the caller's soft buffers");
+  }
+  if (nof_ues == 0) {
+    return SRS_AMD_OK;
+  }
+  if (ues == nullptr || d_llrs == nullptr || d_tbs == nullptr || d_results == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null buffer");
+  }
+  std::lock_guard<std::mutex> lock(dec->mtx);
+  return decode_slot_locked(dec, cfg, ues, nof_ues, d_llrs, d_tbs, d_results, static_cast<hipStream_t>(stream));
 }
 
 int srs_amd_pusch_decode(srs_amd_pusch_decoder*              dec,

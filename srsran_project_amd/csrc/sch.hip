@@ -132,6 +132,22 @@ __global__ __launch_bounds__(ASM_THREADS) void asm_copy_kernel(assemble_args a, 
   }
 }
 
+// Transport block t of a batch: uniform plan, or its descriptor in a heterogeneous batch.
+struct tb_view {
+  uint8_t* tb;
+  uint32_t row0, C, cbi, tbs_bits;
+};
+
+__device__ __forceinline__ tb_view view_of(const assemble_args& a, uint32_t t)
+{
+  if (a.tds != nullptr) {
+    const tb_desc d = a.tds[t];
+    return {a.tbs + d.tb_offset, d.row0, d.nof_segments, d.cb_info_bits, d.tbs_bits};
+  }
+  return {a.tbs + static_cast<size_t>(t) * a.tb_stride, t * a.nof_segments, a.nof_segments, a.cb_info_bits,
+          a.tbs_bits};
+}
+
 __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
 {
   __shared__ uint32_t s_ok, s_sum, s_min, s_max, s_tb_ok;
@@ -139,7 +155,8 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
   __shared__ uint8_t  s_cb_ok[SCH_MAX_SEGMENTS];
   __shared__ uint16_t s_stat[SCH_MAX_SEGMENTS]; // iterations of the freshly decoded codeblocks
   const uint32_t      t = blockIdx.x;
-  const uint32_t      C = a.nof_segments;
+  const tb_view       v = view_of(a, t);
+  const uint32_t      C = v.C;
   if (threadIdx.x == 0) {
     s_ok    = 0;
     s_sum   = 0;
@@ -150,7 +167,7 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
   __syncthreads();
   // 1. CB CRC status (pusch_decoder_impl.cpp:334-375) and LDPC statistics.
   for (uint32_t r = threadIdx.x; r < C; r += ASM_THREADS) {
-    const uint32_t cb   = t * C + r;
+    const uint32_t cb   = v.row0 + r;
     const uint8_t* srow = a.soft ? a.soft + static_cast<size_t>(cb) * a.lay.row_bytes : nullptr;
     // the soft-buffer flag of a codeblock OK from an earlier transmission holds that decoding's iteration
     // count, which the reference's statistics keep for it (cb_stats is not updated, :333-345)
@@ -177,22 +194,22 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
   }
   __syncthreads();
   // 2. HARQ: CRC flags of the freshly decoded codeblocks into the soft buffer.
-  const uint8_t* src = a.msgs + static_cast<size_t>(t) * C * a.msg_stride;
+  const uint8_t* src = a.msgs + static_cast<size_t>(v.row0) * a.msg_stride;
   if (a.soft) {
     // the fresh messages were copied by asm_copy_kernel (launched before this kernel, which then
     // overwrites the flags it read)
     for (uint32_t r = threadIdx.x; r < C; r += ASM_THREADS) {
       if (s_fresh[r]) {
-        *reinterpret_cast<int32_t*>(a.soft + static_cast<size_t>(t * C + r) * a.lay.row_bytes + a.lay.flag_offset) =
+        *reinterpret_cast<int32_t*>(a.soft + static_cast<size_t>(v.row0 + r) * a.lay.row_bytes + a.lay.flag_offset) =
             s_cb_ok[r] ? static_cast<int32_t>(s_stat[r]) : 0;
       }
     }
     __syncthreads();
-    src = a.soft + static_cast<size_t>(t) * C * a.lay.row_bytes + a.lay.msg_offset;
+    src = a.soft + static_cast<size_t>(v.row0) * a.lay.row_bytes + a.lay.msg_offset;
   }
   // 3. Transport block (pusch_decoder_impl.cpp:416-437).
-  uint8_t*       tb     = a.tbs + static_cast<size_t>(t) * a.tb_stride;
-  const uint32_t nbytes = a.tbs_bits / 8;
+  uint8_t*       tb     = v.tb;
+  const uint32_t nbytes = v.tbs_bits / 8;
   const bool     all_ok = s_ok == C;
   if (C == 1) {
     if (all_ok) {
@@ -218,15 +235,14 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
 }
 
 // Source of the concatenated codeblock messages of TB t (the soft-buffer copies when HARQ state is kept).
-__device__ __forceinline__ const uint8_t* asm_source(const assemble_args& a, uint32_t t, uint32_t& stride)
+__device__ __forceinline__ const uint8_t* asm_source(const assemble_args& a, const tb_view& v, uint32_t& stride)
 {
-  const uint32_t C = a.nof_segments;
   if (a.soft) {
     stride = a.lay.row_bytes;
-    return a.soft + static_cast<size_t>(t) * C * a.lay.row_bytes + a.lay.msg_offset;
+    return a.soft + static_cast<size_t>(v.row0) * a.lay.row_bytes + a.lay.msg_offset;
   }
   stride = a.msg_stride;
-  return a.msgs + static_cast<size_t>(t) * C * a.msg_stride;
+  return a.msgs + static_cast<size_t>(v.row0) * a.msg_stride;
 }
 
 struct lds_fetch {
@@ -245,16 +261,17 @@ __global__ __launch_bounds__(ASM_THREADS) void asm_tb_kernel(assemble_args a)
   __shared__ uint32_t T[256];
   __shared__ uint8_t  s_chunk[ASM_TB_CHUNK];
   const uint32_t      t = blockIdx.y;
-  if (a.results[t].nof_codeblocks_crc_ok != a.nof_segments) {
+  const tb_view       v = view_of(a, t);
+  const uint32_t      c0 = blockIdx.x * ASM_TB_CHUNK;
+  if (v.C == 1 || c0 >= v.tbs_bits / 8 || a.results[t].nof_codeblocks_crc_ok != v.C) {
     return; // uniform over the workgroup
   }
   crc_table8_init<ASM_THREADS>(T, 24, CRC24A_POLY);
   uint32_t        stride;
-  const uint8_t*  src    = asm_source(a, t, stride);
-  const tb_gather g{src, stride, a.cb_info_bits};
-  uint8_t*        tb     = a.tbs + static_cast<size_t>(t) * a.tb_stride;
-  const uint32_t  nbytes = a.tbs_bits / 8;
-  const uint32_t  c0     = blockIdx.x * ASM_TB_CHUNK;
+  const uint8_t*  src    = asm_source(a, v, stride);
+  const tb_gather g{src, stride, v.cbi};
+  uint8_t*        tb     = v.tb;
+  const uint32_t  nbytes = v.tbs_bits / 8;
   const uint32_t  n      = min(ASM_TB_CHUNK, nbytes - c0);
   for (uint32_t i = threadIdx.x; i < n; i += ASM_THREADS) {
     const uint32_t b = g(c0 + i);
@@ -264,10 +281,10 @@ __global__ __launch_bounds__(ASM_THREADS) void asm_tb_kernel(assemble_args a)
   __syncthreads();
   const uint32_t b0 = c0 + threadIdx.x * ASM_TB_PER;
   const uint32_t b1 = min(nbytes, b0 + ASM_TB_PER);
-  const uint32_t v  = crc_block_xor<ASM_THREADS>(
-      crc_chunk_contrib(lds_fetch{s_chunk, c0}, b0, b1, a.tbs_bits, 24, CRC24A_POLY, a.crc24a_table, T), partial);
-  if (threadIdx.x == 0 && v != 0) {
-    atomicXor(a.acc + t, v);
+  const uint32_t x  = crc_block_xor<ASM_THREADS>(
+      crc_chunk_contrib(lds_fetch{s_chunk, c0}, b0, b1, v.tbs_bits, 24, CRC24A_POLY, a.crc24a_table, T), partial);
+  if (threadIdx.x == 0 && x != 0) {
+    atomicXor(a.acc + t, x);
   }
 }
 
@@ -276,13 +293,17 @@ __global__ __launch_bounds__(ASM_THREADS) void asm_tb_kernel(assemble_args a)
 __global__ __launch_bounds__(64) void asm_final_kernel(assemble_args a, uint32_t nof_tbs)
 {
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-  const uint32_t C = a.nof_segments;
-  if (t >= nof_tbs || C == 1 || a.results[t].nof_codeblocks_crc_ok != C) {
+  if (t >= nof_tbs) {
+    return;
+  }
+  const tb_view  v = view_of(a, t);
+  const uint32_t C = v.C;
+  if (C == 1 || a.results[t].nof_codeblocks_crc_ok != C) {
     return;
   }
   uint32_t       stride;
-  const uint8_t* src = asm_source(a, t, stride);
-  const uint32_t off = a.tbs_bits - (C - 1) * a.cb_info_bits;
+  const uint8_t* src = asm_source(a, v, stride);
+  const uint32_t off = v.tbs_bits - (C - 1) * v.cbi;
   const uint8_t* m   = src + static_cast<size_t>(C - 1) * stride;
   uint32_t       chk = 0;
   for (uint32_t k = 0; k < 24; ++k) {
@@ -292,7 +313,7 @@ __global__ __launch_bounds__(64) void asm_final_kernel(assemble_args a, uint32_t
   a.results[t].tb_crc_ok  = ok ? 1 : 0;
   if (!ok && a.soft) {
     for (uint32_t r = 0; r < C; ++r) {
-      uint8_t* srow = a.soft + static_cast<size_t>(t * C + r) * a.lay.row_bytes;
+      uint8_t* srow = a.soft + static_cast<size_t>(v.row0 + r) * a.lay.row_bytes;
       *reinterpret_cast<int32_t*>(srow + a.lay.flag_offset) = 0;
     }
   }
@@ -343,14 +364,14 @@ hipError_t launch_assemble(const assemble_args& a, uint32_t nof_tbs, hipStream_t
   }
   hipLaunchKernelGGL(assemble_kernel, dim3(nof_tbs), dim3(ASM_THREADS), 0, stream, a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || a.nof_segments == 1) {
+  if (e != hipSuccess || (a.tds == nullptr && a.nof_segments == 1)) {
     return e;
   }
   e = hipMemsetAsync(a.acc, 0, sizeof(uint32_t) * nof_tbs, stream);
   if (e != hipSuccess) {
     return e;
   }
-  const uint32_t nbytes = a.tbs_bits / 8;
+  const uint32_t nbytes = (a.tds != nullptr ? a.max_tb_bits : a.tbs_bits) / 8;
   hipLaunchKernelGGL(asm_tb_kernel, dim3((nbytes + ASM_TB_CHUNK - 1) / ASM_TB_CHUNK, nof_tbs), dim3(ASM_THREADS), 0,
                      stream, a);
   e = hipGetLastError();

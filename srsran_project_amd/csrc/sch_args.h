@@ -35,6 +35,16 @@ struct soft_row_layout {
   uint32_t row_bytes;
 };
 
+// One transport block of a heterogeneous batch (srs_amd_pusch_decode_slot): its codeblock rows are
+// [row0, row0 + nof_segments) of the decoder scratch, its bytes go to tbs + tb_offset.
+struct tb_desc {
+  uint64_t tb_offset;
+  uint32_t row0;
+  uint32_t nof_segments;
+  uint32_t cb_info_bits;
+  uint32_t tbs_bits;
+};
+
 // pusch_decoder_impl.cpp:309-500 after the decoder: per-CB CRC status (kept in the
 // soft buffer across HARQ transmissions), statistics, codeblock concatenation
 // and the TB CRC check.
@@ -56,6 +66,10 @@ struct assemble_args {
   uint32_t                      tbs_bits;
   uint32_t                      max_iterations;
   int32_t                       new_data;
+  // optional per-TB descriptors (replace nof_segments / cb_info_bits / tbs_bits / tb_stride, rows of TB t
+  // start at tds[t].row0); soft must be null.  max_tb_bits: the largest tbs_bits (grid of asm_tb_kernel).
+  const tb_desc*                tds;
+  uint32_t                      max_tb_bits;
 };
 
 hipError_t launch_segment(const segment_args& a, hipStream_t stream);

@@ -45,6 +45,13 @@ class PuschDecoderResult(ctypes.Structure):
 RESULT_WORDS = ctypes.sizeof(PuschDecoderResult) // 4
 
 
+class PuschUe(ctypes.Structure):
+    """``srs_amd_pusch_ue``: one UE's transport block of a heterogeneous slot batch (its PUSCH PDU,
+    pusch_processor_impl.cpp:343)."""
+
+    _fields_ = [("plan", SchPlan), ("llr_offset", ctypes.c_uint64), ("tb_offset", ctypes.c_uint64)]
+
+
 def _declare(lib):
     c = ctypes
     P = c.c_void_p
@@ -65,6 +72,8 @@ def _declare(lib):
         "srs_amd_pusch_decode": (c.c_int, [P, P, c.POINTER(PuschDecoderResult), P, P, PP,
                                            c.POINTER(PuschDecoderConfig)]),
         "srs_amd_pusch_decode_batch": (c.c_int, [P, PP, c.POINTER(PuschDecoderConfig), P, u, P, P, u, P, P, u, P]),
+        "srs_amd_pusch_decode_slot": (c.c_int, [P, c.POINTER(PuschDecoderConfig), c.POINTER(PuschUe), u, P, P, P,
+                                                P]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -230,4 +239,31 @@ class PuschDecoder:
             llrs.data_ptr(), llrs.shape[1], None if soft is None else soft.data_ptr(),
             None if cb_iterations is None else cb_iterations.data_ptr(), n, _stream(stream, llrs)),
             "pusch decode_batch")
+        return tbs, res
+
+    def decode_slot(self, llrs, ues, cfg, tbs=None, stream=None):
+        """Device form over UEs with different plans (one slot's PUSCH PDUs, new transmissions):
+        llrs: int8 1-D tensor holding every UE's codeword; ues: list of (plan, llr_offset, tb_offset).
+        Returns (uint8 1-D TB tensor, results int32 [len(ues), 6])."""
+        import torch
+
+        if llrs.dim() != 1 or llrs.dtype != torch.int8 or not llrs.is_contiguous():
+            raise ValueError("llrs must be a contiguous int8 1-D tensor")
+        n = len(ues)
+        arr = (PuschUe * max(n, 1))()
+        tb_end = 0
+        for i, (plan, lo, to) in enumerate(ues):
+            if lo + plan.cw_length > llrs.numel():
+                raise ValueError("UE %d codeword beyond the LLR tensor" % i)
+            arr[i] = PuschUe(plan, int(lo), int(to))
+            tb_end = max(tb_end, int(to) + plan.tbs // 8)
+        dev = llrs.device
+        if tbs is None:
+            tbs = torch.zeros(tb_end, dtype=torch.uint8, device=dev)
+        elif tbs.numel() < tb_end:
+            raise ValueError("TB tensor too small")
+        res = torch.empty((n, RESULT_WORDS), dtype=torch.int32, device=dev)
+        _lib.check(self._lib.srs_amd_pusch_decode_slot(self._h, ctypes.byref(cfg), arr, n, llrs.data_ptr(),
+                                                       tbs.data_ptr(), res.data_ptr(), _stream(stream, llrs)),
+                   "pusch decode_slot")
         return tbs, res

@@ -1,0 +1,111 @@
+"""GPU parity: heterogeneous slot decoding (srs_amd_pusch_decode_slot) -- the new transmissions of
+UEs with different plans (TBS, base graph, lifting size, Qm, layers, rv, limited buffer) decoded as
+one launch sequence -- against oracle/sch.py per UE, itself bit-exact with the reference's
+pusch_decoder_impl (tests/test_oracle_vs_ref.py).  Bar: bit-exact TB bytes, TB CRC status and
+LDPC statistics for every UE, whatever its position, alignment or bucket in the batch."""
+import numpy as np
+import pytest
+
+import oracle.sch as osch
+from tests.sch_cases import SCH_CASES, noisy_llrs, tb_bytes
+
+pytestmark = pytest.mark.gpu
+
+# (tbs, base graph, Qm, layers, channel symbols, rv, Nref): SCH_CASES plus high-rate BG1 Z = 384
+# codeblocks of the 100 MHz slot (the LDPC high-rate kernel's bucket, CRC24B) with different Qm / F.
+SLOT_CASES = SCH_CASES + [
+    (8 * 20000, 1, 8, 2, 21504, 0, 0),     # 256QAM R ~ 0.93, C = 19
+    (8 * 9000, 1, 6, 2, 12960, 0, 0),      # 64QAM high rate, C = 9
+    (8 * 30000, 1, 8, 4, 32256, 0, 0),     # 256QAM 4 layers, C = 29
+    (8 * 6000, 1, 4, 1, 13000, 2, 0),      # rv 2 new data (k0 != 0: whole soft row)
+]
+
+
+def _ues(seed, order):
+    import srsran_project_amd as amd
+
+    rng = np.random.default_rng(seed)
+    ues, llr_chunks, want_tbs, pos, tpos = [], [], [], 0, 0
+    for k, ci in enumerate(order):
+        tbs, bg, qm, lay, nre, rv, nref = SLOT_CASES[ci]
+        p = amd.sch_plan(tbs, bg, rv, qm, nref, lay, nre)
+        op = osch.plan(tbs, bg, rv, qm, nref, lay, nre)
+        tb = tb_bytes(tbs, 1000 * seed + k)
+        sigma = [3, 6, 9, 30][k % 4]  # easy ... undecodable
+        llr = noisy_llrs(osch.pdsch_encode(tb, op), 10, sigma, seed=7 * seed + k)
+        pos += int(rng.integers(0, 40))  # arbitrary (also odd) codeword offsets
+        tpos += int(rng.integers(0, 9))
+        ues.append((p, pos, tpos, op, llr, tb))
+        pos += llr.size
+        tpos += tbs // 8
+    flat = np.zeros(pos + 64, np.int8)
+    for p, lo, _, _, llr, _ in ues:
+        flat[lo:lo + llr.size] = llr
+    return ues, flat, tpos
+
+
+@pytest.fixture(scope="module")
+def decs():
+    import srsran_project_amd as amd
+
+    return {"simd": amd.PuschDecoder("simd"), "generic": amd.PuschDecoder("generic")}
+
+
+@pytest.mark.parametrize("arith", ["simd", "generic"])
+@pytest.mark.parametrize("early", [True, False])
+def test_decode_slot_matches_oracle(decs, arith, early):
+    import torch
+
+    import srsran_project_amd as amd
+
+    n = len(SLOT_CASES)
+    # every case twice, interleaved so buckets and plans alternate along the batch
+    order = list(range(n)) + list(reversed(range(n)))
+    ues, flat, tb_total = _ues(3 + int(early), order)
+    cfg = amd.PuschDecoder.config(nof_ldpc_iterations=6, use_early_stop=early)
+    d_tb, res = decs[arith].decode_slot(torch.from_numpy(flat).cuda(), [(u[0], u[1], u[2]) for u in ues], cfg)
+    torch.cuda.synchronize()
+    d_tb, res = d_tb.cpu().numpy(), res.cpu().numpy()
+    for u, (p, _, to, op, llr, tb) in enumerate(ues):
+        h = osch.HarqBuffer(op)
+        out = np.zeros(p.tbs // 8, np.uint8)
+        ok, iters, stats = osch.pusch_decode(llr, op, h, out, 6, arith, use_early_stop=early)
+        msg = "UE %d (case %d)" % (u, order[u])
+        assert bool(res[u, 0]) == ok, msg
+        assert res[u, 1] == p.nof_segments, msg
+        assert (res[u, 2], res[u, 3], res[u, 4]) == (sum(stats), min(stats), max(stats)), msg
+        assert res[u, 5] == sum(i is not None for i in iters), msg
+        np.testing.assert_array_equal(d_tb[to:to + p.tbs // 8], out, err_msg=msg)
+        if u % 4 == 0 and SLOT_CASES[order[u]][5] == 0:
+            assert ok and np.array_equal(out, tb), msg
+
+
+def test_decode_slot_equals_uniform_batches(decs):
+    """A slot of many UEs equals decoding each UE alone through srs_amd_pusch_decode_batch."""
+    import torch
+
+    import srsran_project_amd as amd
+
+    order = [8, 9, 3, 10, 8, 4, 9, 7, 10, 8, 11, 5]
+    ues, flat, _ = _ues(11, order)
+    cfg = amd.PuschDecoder.config(nof_ldpc_iterations=6)
+    d_tb, res = decs["simd"].decode_slot(torch.from_numpy(flat).cuda(), [(u[0], u[1], u[2]) for u in ues], cfg)
+    for u, (p, _, to, _, llr, _) in enumerate(ues):
+        tb1, res1 = decs["simd"].decode_batch(torch.from_numpy(llr[None, :].copy()).cuda(), p, cfg)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(res[u].cpu().numpy(), res1[0].cpu().numpy(), err_msg="UE %d" % u)
+        np.testing.assert_array_equal(d_tb[to:to + p.tbs // 8].cpu().numpy(), tb1[0].cpu().numpy(),
+                                      err_msg="UE %d" % u)
+
+
+def test_decode_slot_rejects_retransmissions(decs):
+    import torch
+
+    import srsran_project_amd as amd
+
+    p = amd.sch_plan(*[SLOT_CASES[1][i] for i in (0, 1, 5, 2, 6, 3, 4)])
+    llrs = torch.zeros(p.cw_length, dtype=torch.int8, device="cuda")
+    with pytest.raises(ValueError):
+        decs["simd"].decode_slot(llrs, [(p, 0, 0)], amd.PuschDecoder.config(new_data=False))
+    tbs, res = decs["simd"].decode_slot(llrs, [], amd.PuschDecoder.config())
+    assert res.shape[0] == 0
