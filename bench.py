@@ -59,7 +59,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="pipeline", choices=["pipeline", "ldpc", "ofdm"])
+    p.add_argument("--workload", default="pipeline", choices=["pipeline", "ldpc", "ofdm", "sch_slot"])
     p.add_argument("--batch", type=int, default=4096, help="ldpc: codeblocks per rank per step")
     p.add_argument("--slots", type=int, default=160, help="ofdm: slots per rank per step (x 4 ports)")
     p.add_argument("--slots-pipeline", type=int, default=64,
@@ -78,7 +78,9 @@ def parse():
                    help="pipeline: PUSCH layers (4: MMSE 4x4, parity unpinned; 2: the reference-pinned ZF 2x4)")
     p.add_argument("--ingest", action="store_true",
                    help="pipeline, N > 1: rank 0 holds all cells' slot inputs; RCCL scatter / gather every step")
-    p.add_argument("--no-latency", action="store_true", help="pipeline: skip the 1 / 8 cell latency figures")
+    p.add_argument("--no-latency", action="store_true",
+                   help="pipeline: skip the 1 / 8 cell latency figures; sch_slot: skip the per-UE launch timing")
+    p.add_argument("--ues-per-cell", type=int, default=8, help="sch_slot: UEs sharing each cell's 273 PRBs")
     return p.parse_args()
 
 
@@ -402,6 +404,10 @@ def main():
 
         line = run_pipeline(args, dist, world, rank, dev, timed, HBM_PEAK_GBS,
                             load_traffic("r02_final_traffic.json", "ldpc_decode_hr_kernel"))
+    elif args.workload == "sch_slot":
+        from bench_slot import run_sch_slot
+
+        line = run_sch_slot(args, dist, world, rank, dev, timed)
     else:
         run = run_ldpc if args.workload == "ldpc" else run_ofdm
         line = run(args, dist, world, rank, dev)

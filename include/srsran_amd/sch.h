@@ -100,6 +100,26 @@ int srs_amd_pdsch_encode_batch(srs_amd_pdsch_encoder*  enc,
                                uint32_t                nof_tbs,
                                void*                   stream);
 
+/* One UE's transport block of a heterogeneous slot batch (srs_amd_pdsch_encode_slot). */
+typedef struct srs_amd_pdsch_ue {
+  srs_amd_sch_plan plan;      /* computed with srs_amd_sch_plan_compute; any BG / Z / Qm / rv / Nref / TBS */
+  uint64_t         tb_offset; /* byte offset of this UE's plan.tbs / 8 transport-block bytes in d_tbs */
+  uint64_t         cw_offset; /* byte offset of its packed codeword (ceil(G / 8) bytes, MSB first) in d_codewords */
+} srs_amd_pdsch_ue;
+
+/* DEVICE, asynchronous: the transport blocks of nof_ues UEs with DIFFERENT plans (the PDSCH PDUs of one
+ * slot, pdsch_processor_impl calling pdsch_encoder::encode once per codeword,
+ * pdsch_encoder.h:61) encoded as one launch sequence: TB CRCs, segmentation and codeblock CRCs with
+ * per-TB descriptors, one LDPC encoding launch per (base graph, lifting size), one rate-matching launch
+ * (per-codeblock geometry).  Each codeword is bit-exact with srs_amd_pdsch_encode_batch of its plan.
+ * ues: HOST array.  The codeword bit span of the batch must stay below 2^32 bits. */
+int srs_amd_pdsch_encode_slot(srs_amd_pdsch_encoder*  enc,
+                              const srs_amd_pdsch_ue* ues,
+                              uint32_t                nof_ues,
+                              const uint8_t*          d_tbs,
+                              uint8_t*                d_codewords,
+                              void*                   stream);
+
 /* ---- PUSCH decoder -------------------------------------------------------- */
 typedef struct srs_amd_pusch_decoder srs_amd_pusch_decoder;
 

@@ -88,6 +88,7 @@ from .pusch_processor import (  # noqa: F401
 
 from .sch import (  # noqa: F401
     PdschEncoder,
+    PdschUe,
     PuschDecoder,
     PuschDecoderConfig,
     PuschDecoderResult,

@@ -238,3 +238,13 @@ const uint32_t* srs_amd::crc_device_table(const srs_amd_crc_calculator* crc)
 {
   return crc ? crc->d_table : nullptr;
 }
+
+uint32_t srs_amd::crc_polynom(const srs_amd_crc_calculator* crc)
+{
+  return crc ? crc->polynom : 0;
+}
+
+uint32_t srs_amd::crc_order(const srs_amd_crc_calculator* crc)
+{
+  return crc ? static_cast<uint32_t>(crc->order) : 0;
+}

@@ -67,6 +67,72 @@ struct stream_order {
   }
 };
 
+// Fans independent launches of one call out over up to FAN_STREAMS helper streams and joins them back into
+// the caller's stream (events only, no host synchronisation): the small per-bucket LDPC launches of a
+// heterogeneous slot run concurrently instead of one after the other on a mostly idle GPU.
+struct stream_fan {
+  static constexpr int FAN_STREAMS = 4;
+  hipStream_t          s[FAN_STREAMS]    = {};
+  hipEvent_t           join[FAN_STREAMS] = {};
+  hipEvent_t           fork              = nullptr;
+  int                  n                 = 0;
+  stream_fan()                           = default;
+  stream_fan(const stream_fan&)            = delete;
+  stream_fan& operator=(const stream_fan&) = delete;
+  ~stream_fan()
+  {
+    for (int i = 0; i < FAN_STREAMS; ++i) {
+      if (s[i]) {
+        (void)hipStreamSynchronize(s[i]);
+        (void)hipStreamDestroy(s[i]);
+      }
+      if (join[i]) {
+        (void)hipEventDestroy(join[i]);
+      }
+    }
+    if (fork) {
+      (void)hipEventDestroy(fork);
+    }
+  }
+  // The next `count` launches go to stream(i), i < count; count <= 1 keeps them on `main`.
+  hipError_t begin(hipStream_t main, int count)
+  {
+    n            = count > FAN_STREAMS ? FAN_STREAMS : (count > 1 ? count : 0);
+    hipError_t e = hipSuccess;
+    if (n > 0 && fork == nullptr) {
+      e = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+    }
+    for (int i = 0; i < n && e == hipSuccess; ++i) {
+      if (s[i] == nullptr) {
+        e = hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking);
+        if (e == hipSuccess) {
+          e = hipEventCreateWithFlags(&join[i], hipEventDisableTiming);
+        }
+      }
+    }
+    if (n > 0 && e == hipSuccess) {
+      e = hipEventRecord(fork, main);
+    }
+    for (int i = 0; i < n && e == hipSuccess; ++i) {
+      e = hipStreamWaitEvent(s[i], fork, 0);
+    }
+    return e;
+  }
+  hipStream_t stream(hipStream_t main, int i) const { return n > 0 ? s[i % n] : main; }
+  hipError_t  end(hipStream_t main)
+  {
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < n && e == hipSuccess; ++i) {
+      e = hipEventRecord(join[i], s[i]);
+      if (e == hipSuccess) {
+        e = hipStreamWaitEvent(main, join[i], 0);
+      }
+    }
+    n = 0;
+    return e;
+  }
+};
+
 inline size_t align_up(size_t n, size_t a)
 {
   return (n + a - 1) / a * a;

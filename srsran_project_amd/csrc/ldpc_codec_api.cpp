@@ -557,6 +557,45 @@ int srs_amd::rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_rate_dematch_kernel launch");
 }
 
+int srs_amd::rate_match_ragged(srs_amd_ldpc_rate_matcher* rm,
+                               const uint8_t*             d_codeblocks,
+                               uint32_t                   cb_stride,
+                               const uint32_t*            d_rm_lengths,
+                               const uint32_t*            d_out_offsets,
+                               const uint32_t*            d_row_geo,
+                               const void*                d_geos,
+                               uint8_t*                   d_output,
+                               uint32_t                   nof_cbs,
+                               void*                      stream)
+{
+  if (rm == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null rate matcher");
+  }
+  if (nof_cbs == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_codeblocks == nullptr || d_rm_lengths == nullptr || d_out_offsets == nullptr || d_row_geo == nullptr ||
+      d_geos == nullptr || d_output == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  // the caller (srs_amd_pdsch_encode_slot) checked every geometry and cb_stride
+  rate_match_args a{};
+  a.cw          = d_codeblocks;
+  a.cw_stride   = cb_stride;
+  a.rm_lengths  = d_rm_lengths;
+  a.out_offsets = d_out_offsets;
+  a.out         = d_output;
+  a.nof_cbs     = nof_cbs;
+  a.row_geo     = d_row_geo;
+  a.geos        = static_cast<const rm_geometry*>(d_geos);
+  std::lock_guard<std::mutex> lock(rm->mtx);
+  hipError_t                  e = hipSetDevice(rm->device);
+  if (e == hipSuccess) {
+    e = launch_rate_match(a, 0, static_cast<hipStream_t>(stream));
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_rate_match_kernel launch");
+}
+
 int srs_amd::rate_dematch_ragged(srs_amd_ldpc_rate_dematcher* dm,
                                  const int8_t*                d_input,
                                  const uint32_t*              d_in_offsets,

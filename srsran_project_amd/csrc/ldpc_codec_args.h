@@ -54,6 +54,10 @@ struct rate_match_args {
   uint8_t*        out;
   uint32_t        nof_cbs;
   rm_geometry     g;
+  // optional per-codeblock geometry (replaces g): codeblock cb uses geos[row_geo[cb]]; the codeblocks
+  // of one codeword share a geometry and the codewords of different geometries share no byte
+  const uint32_t*    row_geo;
+  const rm_geometry* geos;
 };
 
 hipError_t launch_ldpc_encode(const encode_args& a, int grid, hipStream_t stream);

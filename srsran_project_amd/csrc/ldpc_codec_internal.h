@@ -60,6 +60,19 @@ int ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
                          uint32_t                           skip_stride,
                          const int32_t*                     d_fillers = nullptr);
 
+// Rate matching of codeblocks with per-codeblock geometry (srs_amd_pdsch_encode_slot): codeblock cb uses
+// geos[row_geo[cb]]; d_out_offsets are bit offsets into d_output.
+int rate_match_ragged(srs_amd_ldpc_rate_matcher* rm,
+                      const uint8_t*             d_codeblocks,
+                      uint32_t                   cb_stride,
+                      const uint32_t*            d_rm_lengths,
+                      const uint32_t*            d_out_offsets,
+                      const uint32_t*            d_row_geo,
+                      const void*                d_geos,
+                      uint8_t*                   d_output,
+                      uint32_t                   nof_cbs,
+                      void*                      stream);
+
 // Rate dematching of codeblocks with per-codeblock geometry (srs_amd_pusch_decode_slot): codeblock cb
 // uses geos[row_geo[cb]] and writes soft-buffer bytes [0, geo_write_end[row_geo[cb]]) of its row
 // (new data into fresh internal buffers, whose old contents are taken as zero).

@@ -343,9 +343,9 @@ constexpr uint32_t RM_MAX_CW_BYTES    = 66 * 384 / 8; // circular buffer of BG1,
 
 // Output byte b of the concatenated codeword, bits of segment cb and (when it straddles) the following
 // segments.
-__device__ uint32_t rm_byte(const rate_match_args& a, const fast_div& divL, uint32_t cb, uint32_t b)
+__device__ uint32_t rm_byte(const rate_match_args& a, const rm_geometry& g, const fast_div& divL, uint32_t cb,
+                            uint32_t b)
 {
-  const rm_geometry& g = a.g;
   uint32_t c = cb, off_c = a.out_offsets[cb], E_c = a.rm_lengths[cb];
   uint32_t byte = 0;
   for (int k = 0; k < 8; ++k) {
@@ -388,13 +388,14 @@ __device__ uint32_t rm_byte(const rate_match_args& a, const fast_div& divL, uint
 // One workgroup per codeblock: the circular buffer (Ncb bits of the packed codeword) is staged in LDS
 // with coalesced loads, then one thread per output byte gathers its 8 bits from LDS (bit selection +
 // interleaver as index arithmetic). A byte straddling the next segment is built from global memory.
+template <bool RAGGED>
 __global__ __launch_bounds__(RATE_MATCH_THREADS) void ldpc_rate_match_kernel(rate_match_args a)
 {
   __shared__ uint8_t s_cw[RM_MAX_CW_BYTES];
-  const rm_geometry& g = a.g;
-  const fast_div     divL(g.L);
-  const uint32_t     cw_bytes = (g.Ncb + 7) / 8;
   for (uint32_t cb = blockIdx.y; cb < a.nof_cbs; cb += gridDim.y) {
+    const rm_geometry g = RAGGED ? a.geos[a.row_geo[cb]] : a.g;
+    const fast_div    divL(g.L);
+    const uint32_t    cw_bytes = (g.Ncb + 7) / 8;
     const uint32_t off   = a.out_offsets[cb];
     const uint32_t E     = a.rm_lengths[cb];
     const uint32_t first = (off + 7) / 8;
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(RATE_MATCH_THREADS) void ldpc_rate_match_kernel(rat
     for (uint32_t b = first + blockIdx.x * RATE_MATCH_THREADS + threadIdx.x; b < last;
          b += gridDim.x * RATE_MATCH_THREADS) {
       if (b >= whole) {
-        a.out[b] = static_cast<uint8_t>(rm_byte(a, divL, cb, b));
+        a.out[b] = static_cast<uint8_t>(rm_byte(a, g, divL, cb, b));
         continue;
       }
       uint32_t byte = 0;
@@ -459,7 +460,11 @@ hipError_t launch_rate_match(const rate_match_args& a, uint32_t max_rm_length, h
   // one workgroup per codeblock: the staged circular buffer is loaded once
   (void)max_rm_length;
   dim3 grid(1, a.nof_cbs < 65535u ? a.nof_cbs : 65535u);
-  hipLaunchKernelGGL(ldpc_rate_match_kernel, grid, dim3(RATE_MATCH_THREADS), 0, stream, a);
+  if (a.row_geo != nullptr) {
+    hipLaunchKernelGGL(ldpc_rate_match_kernel<true>, grid, dim3(RATE_MATCH_THREADS), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(ldpc_rate_match_kernel<false>, grid, dim3(RATE_MATCH_THREADS), 0, stream, a);
+  }
   return hipGetLastError();
 }
 

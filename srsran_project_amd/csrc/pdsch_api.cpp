@@ -21,7 +21,9 @@
 #include "sch_args.h"
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <vector>
 
 using namespace srs_amd;
@@ -34,9 +36,15 @@ struct srs_amd_pdsch_encoder {
   srs_amd_crc_calculator*    crc24b = nullptr;
   srs_amd_ldpc_encoder*      enc    = nullptr;
   srs_amd_ldpc_rate_matcher* rm     = nullptr;
-  device_buffer              tb_crcs, msgs, coded, rm_arrays, host_io;
+  device_buffer              tb_crcs, msgs, coded, rm_arrays, host_io, slot_desc;
   stream_order               order; // scratch reuse across the callers' streams
+  stream_fan                 fan;   // srs_amd_pdsch_encode_slot: concurrent LDPC encoder bucket launches
   std::mutex                 mtx;
+  // srs_amd_pdsch_encode_slot: descriptors staged in pinned memory, reused once their upload completed
+  void*                      h_stage      = nullptr;
+  size_t                     h_stage_size = 0;
+  hipEvent_t                 stage_done   = nullptr;
+  bool                       stage_used   = false;
   ~srs_amd_pdsch_encoder()
   {
     (void)hipSetDevice(device);
@@ -44,6 +52,11 @@ struct srs_amd_pdsch_encoder {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
     }
+    if (stage_done) {
+      (void)hipEventSynchronize(stage_done);
+      (void)hipEventDestroy(stage_done);
+    }
+    (void)hipHostFree(h_stage);
     srs_amd_crc_calculator_destroy(crc16);
     srs_amd_crc_calculator_destroy(crc24a);
     srs_amd_crc_calculator_destroy(crc24b);
@@ -160,9 +173,224 @@ int encode_locked(srs_amd_pdsch_encoder* e,
   return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "PDSCH encoder completion event");
 }
 
+// srs_amd_pdsch_encode_slot: one message row (stride MS) and one coded row (stride CS) per codeblock of the
+// slot, rows grouped by LDPC encoder bucket (BG, Z), each UE's C rows contiguous.
+int encode_slot_locked(srs_amd_pdsch_encoder*  e,
+                       const srs_amd_pdsch_ue* ues,
+                       uint32_t                U,
+                       const uint8_t*          d_tbs,
+                       uint8_t*                d_cw,
+                       hipStream_t             stream)
+{
+  struct bucket {
+    uint32_t              bg, Z;
+    uint32_t              max_bits = 0, row0 = 0, rows = 0;
+    std::vector<uint32_t> ues;
+  };
+  std::vector<bucket>                         buckets;
+  std::map<std::pair<uint32_t, uint32_t>, size_t> bucket_of;
+  std::vector<rm_geometry>                    ug(U);
+  uint32_t MS = 0, CS = 0, R = 0, max_tb_bytes = 0, max_msg_bytes = 0;
+  for (uint32_t u = 0; u < U; ++u) {
+    const srs_amd_sch_plan* p  = &ues[u].plan;
+    int                     rc = check_plan(p);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+    if (const char* msg = make_rm_geometry(ug[u], p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                                           p->nof_filler_bits)) {
+      return fail(SRS_AMD_EINVAL, "UE %u: %s", u, msg);
+    }
+    if ((ues[u].cw_offset + (p->cw_length + 7) / 8) * 8 > 0xffffffffull) {
+      return fail(SRS_AMD_EINVAL, "UE %u: codeword span exceeds 2^32 bits", u);
+    }
+    const auto key = std::make_pair(p->base_graph, p->lifting_size);
+    auto       it  = bucket_of.find(key);
+    if (it == bucket_of.end()) {
+      it = bucket_of.emplace(key, buckets.size()).first;
+      buckets.push_back(bucket{p->base_graph, p->lifting_size});
+    }
+    bucket& b = buckets[it->second];
+    b.ues.push_back(u);
+    b.rows += p->nof_segments;
+    // only the circular-buffer window the rate matcher reads is encoded (ldpc_rate_matcher_impl.cpp:95-130)
+    const uint64_t window = static_cast<uint64_t>(ug[u].k0) + std::max(p->rm_length_long, p->rm_length_short) +
+                            ug[u].F;
+    b.max_bits    = std::max(b.max_bits, window >= ug[u].Ncb ? ug[u].Ncb : static_cast<uint32_t>(window));
+    const uint32_t N = srs_amd_ldpc_codeblock_length(p->base_graph, p->lifting_size);
+    MS            = std::max(MS, static_cast<uint32_t>(align_up((p->segment_length + 7) / 8, 64)));
+    CS            = std::max(CS, static_cast<uint32_t>(align_up((N + 7) / 8, 64)));
+    R            += p->nof_segments;
+    max_tb_bytes  = std::max(max_tb_bytes, p->tbs / 8);
+    max_msg_bytes = std::max(max_msg_bytes, (p->segment_length + 7) / 8);
+  }
+  if (R > 65535) {
+    return fail(SRS_AMD_EINVAL, "%u codeblocks exceed the 65535 of one slot batch", R);
+  }
+  std::vector<uint32_t>                                                          row_E(R), row_out(R), row_geo(R), row_tb(R);
+  std::vector<rm_geometry>                                                       geos;
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> geo_of;
+  std::vector<tb_desc>                                                           tds(U);
+  std::vector<uint32_t>                                                          segE, segOff;
+  uint32_t                                                                       row = 0;
+  for (bucket& b : buckets) {
+    b.row0 = row;
+    for (uint32_t u : b.ues) {
+      const srs_amd_sch_plan* p    = &ues[u].plan;
+      const auto              gkey = std::make_tuple(p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                                                     p->nof_filler_bits, 0u);
+      auto                    git  = geo_of.find(gkey);
+      if (git == geo_of.end()) {
+        git = geo_of.emplace(gkey, static_cast<uint32_t>(geos.size())).first;
+        geos.push_back(ug[u]);
+      }
+      segE.resize(p->nof_segments);
+      segOff.resize(p->nof_segments);
+      (void)srs_amd_sch_plan_segments(p, segE.data(), segOff.data());
+      tds[u] = tb_desc{ues[u].tb_offset, row,         p->nof_segments, p->cb_info_bits, p->tbs, p->nof_tb_crc_bits,
+                       p->zero_pad,       (p->segment_length + 7) / 8, 0};
+      for (uint32_t r = 0; r < p->nof_segments; ++r, ++row) {
+        row_E[row]   = segE[r];
+        row_out[row] = static_cast<uint32_t>(ues[u].cw_offset * 8) + segOff[r];
+        row_geo[row] = git->second;
+        row_tb[row]  = u;
+      }
+    }
+  }
+  const size_t o_E   = 0;
+  const size_t o_out = o_E + align_up(sizeof(uint32_t) * R, 16);
+  const size_t o_geo = o_out + align_up(sizeof(uint32_t) * R, 16);
+  const size_t o_tb  = o_geo + align_up(sizeof(uint32_t) * R, 16);
+  const size_t o_G   = o_tb + align_up(sizeof(uint32_t) * R, 16);
+  const size_t o_TD  = o_G + align_up(sizeof(rm_geometry) * geos.size(), 16);
+  const size_t total = o_TD + sizeof(tb_desc) * U;
+
+  hipError_t he = hipSetDevice(e->device);
+  // the pinned staging buffer is rewritten only once its previous upload completed
+  if (he == hipSuccess && e->stage_used) {
+    he = hipEventSynchronize(e->stage_done);
+  }
+  if (he == hipSuccess && e->stage_done == nullptr) {
+    he = hipEventCreateWithFlags(&e->stage_done, hipEventDisableTiming);
+  }
+  if (he == hipSuccess && e->h_stage_size < total) {
+    (void)hipHostFree(e->h_stage);
+    e->h_stage      = nullptr;
+    e->h_stage_size = 0;
+    he              = hipHostMalloc(&e->h_stage, total, hipHostMallocDefault);
+    if (he == hipSuccess) {
+      e->h_stage_size = total;
+    }
+  }
+  if (he == hipSuccess) {
+    he = e->slot_desc.ensure(total);
+  }
+  if (he == hipSuccess) {
+    he = e->tb_crcs.ensure(sizeof(uint32_t) * U);
+  }
+  if (he == hipSuccess) {
+    he = e->msgs.ensure(static_cast<size_t>(R) * MS);
+  }
+  if (he == hipSuccess) {
+    he = e->coded.ensure(static_cast<size_t>(R) * CS);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH slot encoder scratch");
+  }
+  auto* h = static_cast<uint8_t*>(e->h_stage);
+  std::memcpy(h + o_E, row_E.data(), sizeof(uint32_t) * R);
+  std::memcpy(h + o_out, row_out.data(), sizeof(uint32_t) * R);
+  std::memcpy(h + o_geo, row_geo.data(), sizeof(uint32_t) * R);
+  std::memcpy(h + o_tb, row_tb.data(), sizeof(uint32_t) * R);
+  std::memcpy(h + o_G, geos.data(), sizeof(rm_geometry) * geos.size());
+  std::memcpy(h + o_TD, tds.data(), sizeof(tb_desc) * U);
+  auto* dd = e->slot_desc.as<uint8_t>();
+  he       = e->order.begin(stream);
+  if (he == hipSuccess) {
+    he = hipMemcpyAsync(dd, h, total, hipMemcpyHostToDevice, stream);
+  }
+  if (he == hipSuccess) {
+    he = hipEventRecord(e->stage_done, stream);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH slot descriptors upload");
+  }
+  e->stage_used = true;
+  // 1-3. TB CRCs, segmentation, codeblock CRCs.
+  tx_slot_args ta{};
+  ta.tbs           = d_tbs;
+  ta.tds           = reinterpret_cast<const tb_desc*>(dd + o_TD);
+  ta.row_tb        = reinterpret_cast<const uint32_t*>(dd + o_tb);
+  ta.acc           = e->tb_crcs.as<uint32_t>();
+  ta.msgs          = e->msgs.as<uint8_t>();
+  ta.crc16_table   = crc_device_table(e->crc16);
+  ta.crc24a_table  = crc_device_table(e->crc24a);
+  ta.crc24b_table  = crc_device_table(e->crc24b);
+  ta.crc16_poly    = crc_polynom(e->crc16);
+  ta.crc24a_poly   = crc_polynom(e->crc24a);
+  ta.crc24b_poly   = crc_polynom(e->crc24b);
+  ta.msg_stride    = MS;
+  ta.nof_tbs       = U;
+  ta.nof_rows      = R;
+  ta.max_tb_bytes  = max_tb_bytes;
+  ta.max_msg_bytes = max_msg_bytes;
+  he               = launch_tx_slot_segment(ta, stream);
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH slot segmentation launch");
+  }
+  // 4. LDPC encoding, one launch per (BG, Z) bucket, fanned out over helper streams.
+  he = e->fan.begin(stream, static_cast<int>(buckets.size()));
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH slot encoder stream fan-out");
+  }
+  for (size_t bi = 0; bi < buckets.size(); ++bi) {
+    const bucket&               b = buckets[bi];
+    srs_amd_ldpc_encoder_config ec{b.bg, b.Z, 0};
+    int rc = ldpc_encode_batch_ex(e->enc, &ec, e->msgs.as<uint8_t>() + static_cast<size_t>(b.row0) * MS, MS,
+                                  e->coded.as<uint8_t>() + static_cast<size_t>(b.row0) * CS, CS, b.rows,
+                                  e->fan.stream(stream, static_cast<int>(bi)), b.max_bits);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+  }
+  he = e->fan.end(stream);
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH slot encoder stream join");
+  }
+  // 5. Rate matching of every codeblock into the codewords, one launch.
+  int rc = rate_match_ragged(e->rm, e->coded.as<uint8_t>(), CS, reinterpret_cast<const uint32_t*>(dd + o_E),
+                             reinterpret_cast<const uint32_t*>(dd + o_out), reinterpret_cast<const uint32_t*>(dd + o_geo),
+                             dd + o_G, d_cw, R, stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  he = e->order.end(stream);
+  return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "PDSCH encoder completion event");
+}
+
 } // namespace
 
 extern "C" {
+
+int srs_amd_pdsch_encode_slot(srs_amd_pdsch_encoder*  enc,
+                              const srs_amd_pdsch_ue* ues,
+                              uint32_t                nof_ues,
+                              const uint8_t*          d_tbs,
+                              uint8_t*                d_codewords,
+                              void*                   stream)
+{
+  if (enc == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null encoder");
+  }
+  if (nof_ues == 0) {
+    return SRS_AMD_OK;
+  }
+  if (ues == nullptr || d_tbs == nullptr || d_codewords == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null buffer");
+  }
+  std::lock_guard<std::mutex> lock(enc->mtx);
+  return encode_slot_locked(enc, ues, nof_ues, d_tbs, d_codewords, static_cast<hipStream_t>(stream));
+}
 
 int srs_amd_pdsch_encoder_create(srs_amd_pdsch_encoder** out, int device)
 {

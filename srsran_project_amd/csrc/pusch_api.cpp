@@ -40,6 +40,7 @@ struct srs_amd_pusch_decoder {
   srs_amd_ldpc_decoder*        dec[2] = {nullptr, nullptr}; // force_decoding 0 / 1
   device_buffer                soft, msgs, iters, checks, arrays, results, host_io, tb_acc, slot_desc;
   stream_order                 order; // scratch reuse across the callers' streams
+  stream_fan                   fan;   // srs_amd_pusch_decode_slot: concurrent LDPC bucket launches
   std::mutex                   mtx;
   // srs_amd_pusch_decode_slot: descriptors staged in pinned memory, reused once their upload completed
   void*                        h_stage      = nullptr;
@@ -321,7 +322,8 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
       segE.resize(p->nof_segments);
       segOff.resize(p->nof_segments);
       (void)srs_amd_sch_plan_segments(p, segE.data(), segOff.data());
-      tds[u] = tb_desc{ues[u].tb_offset, row, p->nof_segments, p->cb_info_bits, p->tbs};
+      tds[u] = tb_desc{ues[u].tb_offset, row,         p->nof_segments, p->cb_info_bits, p->tbs, p->nof_tb_crc_bits,
+                       p->zero_pad,       (p->segment_length + 7) / 8, 0};
       for (uint32_t r = 0; r < p->nof_segments; ++r, ++row) {
         row_E[row]   = segE[r];
         row_in[row]  = static_cast<uint32_t>(ues[u].llr_offset) + segOff[r];
@@ -405,10 +407,30 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   if (rc != SRS_AMD_OK) {
     return rc;
   }
-  // 2. LDPC decoding, one launch per (BG, Z, CRC, bounded prefix) bucket.
+  // 2. LDPC decoding, one launch per (BG, Z, CRC, bounded prefix) bucket, fanned out over helper streams
+  //    (largest buckets first, each to the least loaded stream).
   const int32_t*        d_F  = reinterpret_cast<const int32_t*>(dd + o_F);
   srs_amd_ldpc_decoder* ldpc = d->dec[cfg->force_decoding ? 1 : 0];
-  for (const bucket& b : buckets) {
+  std::vector<size_t>   by_size(buckets.size());
+  for (size_t i = 0; i < by_size.size(); ++i) {
+    by_size[i] = i;
+  }
+  std::sort(by_size.begin(), by_size.end(), [&](size_t x, size_t y) {
+    return static_cast<uint64_t>(buckets[x].rows) * buckets[x].Z > static_cast<uint64_t>(buckets[y].rows) * buckets[y].Z;
+  });
+  he = d->fan.begin(stream, static_cast<int>(buckets.size()));
+  if (he != hipSuccess) {
+    return hip_fail(he, "PUSCH slot decoder stream fan-out");
+  }
+  uint64_t load[stream_fan::FAN_STREAMS] = {};
+  for (size_t bi : by_size) {
+    const bucket& b  = buckets[bi];
+    int           si = 0;
+    for (int k = 1; k < stream_fan::FAN_STREAMS; ++k) {
+      si = load[k] < load[si] ? k : si;
+    }
+    load[si] += static_cast<uint64_t>(b.rows) * b.Z;
+    const hipStream_t bs = d->fan.stream(stream, si);
     srs_amd_ldpc_decoder_config dc{};
     dc.base_graph     = b.bg;
     dc.lifting_size   = b.Z;
@@ -417,10 +439,14 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     rc = ldpc_decode_batch_ex(ldpc, &dc, cfg->use_early_stop ? b.poly : SRS_AMD_NO_CRC,
                               soft + static_cast<size_t>(b.row0) * S, S, nullptr, b.prefix,
                               d->msgs.as<uint8_t>() + static_cast<size_t>(b.row0) * M, M,
-                              d->iters.as<int32_t>() + b.row0, nullptr, b.rows, stream, nullptr, 0, d_F + b.row0);
+                              d->iters.as<int32_t>() + b.row0, nullptr, b.rows, bs, nullptr, 0, d_F + b.row0);
     if (rc != SRS_AMD_OK) {
       return rc;
     }
+  }
+  he = d->fan.end(stream);
+  if (he != hipSuccess) {
+    return hip_fail(he, "PUSCH slot decoder stream join");
   }
   // Without early stop: CRC of each decoded message (pusch_codeblock_decoder.cpp:75-86), per UE.
   if (!cfg->use_early_stop) {

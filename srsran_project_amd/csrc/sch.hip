@@ -34,21 +34,10 @@ __device__ __forceinline__ uint32_t bit_at(const uint8_t* b, uint32_t p)
   return (b[p >> 3] >> (7 - (p & 7))) & 1u;
 }
 
-__global__ __launch_bounds__(SEG_THREADS) void segment_kernel(segment_args a)
+// Byte j of segment message row: n_data TB bits from bit tb_off, then (last segment) the TB CRC, zeros after.
+__device__ __forceinline__ uint8_t segment_byte(const uint8_t* tb, uint32_t tb_off, uint32_t n_data, bool last,
+                                                uint32_t crc, uint32_t tb_crc_bits, uint32_t j)
 {
-  const uint32_t row = blockIdx.y;
-  const uint32_t j   = blockIdx.x * SEG_THREADS + threadIdx.x;
-  if (row >= a.nof_rows || j >= a.msg_bytes) {
-    return;
-  }
-  const uint32_t t       = row / a.nof_segments;
-  const uint32_t r       = row - t * a.nof_segments;
-  const bool     last    = r == a.nof_segments - 1;
-  const uint32_t n_data  = last ? a.last_data_bits : a.cb_info_bits;
-  const uint32_t tb_off  = r * a.cb_info_bits;
-  const uint8_t* tb      = a.tbs + static_cast<size_t>(t) * a.tb_stride;
-  const uint32_t crc     = a.tb_crcs[t];
-  uint32_t       byte    = 0;
   if (8 * j + 8 <= n_data) {
     // all 8 bits from the TB: one or two byte loads
     const uint32_t q  = tb_off + 8 * j;
@@ -57,20 +46,112 @@ __global__ __launch_bounds__(SEG_THREADS) void segment_kernel(segment_args a)
     if (sh != 0) {
       w |= tb[(q >> 3) + 1];
     }
-    a.msgs[static_cast<size_t>(row) * a.msg_stride + j] = static_cast<uint8_t>(w >> (8 - sh));
-    return;
+    return static_cast<uint8_t>(w >> (8 - sh));
   }
+  uint32_t byte = 0;
   for (int k = 0; k < 8; ++k) {
     const uint32_t p = 8 * j + k;
     uint32_t       v = 0;
     if (p < n_data) {
       v = bit_at(tb, tb_off + p);
-    } else if (last && p < n_data + a.tb_crc_bits) {
-      v = (crc >> (a.tb_crc_bits - 1 - (p - n_data))) & 1u;
+    } else if (last && p < n_data + tb_crc_bits) {
+      v = (crc >> (tb_crc_bits - 1 - (p - n_data))) & 1u;
     }
     byte |= v << (7 - k);
   }
-  a.msgs[static_cast<size_t>(row) * a.msg_stride + j] = static_cast<uint8_t>(byte);
+  return static_cast<uint8_t>(byte);
+}
+
+__global__ __launch_bounds__(SEG_THREADS) void segment_kernel(segment_args a)
+{
+  const uint32_t row = blockIdx.y;
+  const uint32_t j   = blockIdx.x * SEG_THREADS + threadIdx.x;
+  if (row >= a.nof_rows || j >= a.msg_bytes) {
+    return;
+  }
+  const uint32_t t      = row / a.nof_segments;
+  const uint32_t r      = row - t * a.nof_segments;
+  const bool     last   = r == a.nof_segments - 1;
+  const uint32_t n_data = last ? a.last_data_bits : a.cb_info_bits;
+  const uint8_t* tb     = a.tbs + static_cast<size_t>(t) * a.tb_stride;
+  a.msgs[static_cast<size_t>(row) * a.msg_stride + j] =
+      segment_byte(tb, r * a.cb_info_bits, n_data, last, a.tb_crcs[t], a.tb_crc_bits, j);
+}
+
+// ---- PDSCH encoder of a heterogeneous batch (srs_amd_pdsch_encode_slot) ----
+
+// TB CRC (CRC16 / CRC24A per TB): one workgroup per ASM_TB_CHUNK bytes of a TB, partials XOR-ed into acc[t].
+__global__ __launch_bounds__(ASM_THREADS) void tx_tb_crc_kernel(tx_slot_args a)
+{
+  __shared__ uint32_t partial[ASM_THREADS / 64];
+  __shared__ uint32_t T[256];
+  const uint32_t      t      = blockIdx.y;
+  const tb_desc       d      = a.tds[t];
+  const uint32_t      nbytes = d.tbs_bits / 8;
+  const uint32_t      c0     = blockIdx.x * ASM_TB_CHUNK;
+  if (c0 >= nbytes) {
+    return; // uniform over the workgroup
+  }
+  const bool      c16   = d.tb_crc_bits == 16;
+  const uint32_t  poly  = c16 ? a.crc16_poly : a.crc24a_poly;
+  const uint32_t* table = c16 ? a.crc16_table : a.crc24a_table;
+  crc_table8_init<ASM_THREADS>(T, d.tb_crc_bits, poly);
+  __syncthreads();
+  const uint32_t b0 = c0 + threadIdx.x * ASM_TB_PER;
+  const uint32_t b1 = min(nbytes, b0 + ASM_TB_PER);
+  const uint32_t x  = crc_block_xor<ASM_THREADS>(
+      crc_chunk_contrib(row_fetch{a.tbs + d.tb_offset}, b0, b1, d.tbs_bits, d.tb_crc_bits, poly, table, T), partial);
+  if (threadIdx.x == 0 && x != 0) {
+    atomicXor(a.acc + t, x);
+  }
+}
+
+// Segmentation (ldpc_segmenter_tx_impl.cpp:137-207) with per-TB geometry: one thread per message byte.
+__global__ __launch_bounds__(SEG_THREADS) void tx_segment_kernel(tx_slot_args a)
+{
+  const uint32_t row = blockIdx.y;
+  const uint32_t j   = blockIdx.x * SEG_THREADS + threadIdx.x;
+  const uint32_t t   = a.row_tb[row];
+  const tb_desc  d   = a.tds[t];
+  if (j >= d.msg_bytes) {
+    return;
+  }
+  const uint32_t r      = row - d.row0;
+  const bool     last   = r == d.nof_segments - 1;
+  const uint32_t n_data = last ? d.cb_info_bits - d.tb_crc_bits - d.zero_pad : d.cb_info_bits;
+  a.msgs[static_cast<size_t>(row) * a.msg_stride + j] =
+      segment_byte(a.tbs + d.tb_offset, r * d.cb_info_bits, n_data, last, a.acc[t], d.tb_crc_bits, j);
+}
+
+// CRC24B attachment to the codeblocks of segmented TBs (ldpc_segmenter_tx_impl.cpp:196): one wave per row,
+// the CRC bits MSB-first into message bits [cb_info_bits, cb_info_bits + 24).
+__global__ __launch_bounds__(64) void tx_cb_crc_kernel(tx_slot_args a)
+{
+  __shared__ uint32_t partial[1];
+  __shared__ uint32_t T[256];
+  const uint32_t      row = blockIdx.x;
+  const tb_desc       d   = a.tds[a.row_tb[row]];
+  if (d.nof_segments == 1) {
+    return;
+  }
+  crc_table8_init<64>(T, 24, a.crc24b_poly);
+  __syncthreads();
+  uint8_t*       m   = a.msgs + static_cast<size_t>(row) * a.msg_stride;
+  const uint32_t n   = d.cb_info_bits;
+  const uint32_t crc = block_crc_bytes<64>(row_fetch{m}, n, 24, a.crc24b_poly, a.crc24b_table, T, partial);
+  if (threadIdx.x == 0) {
+    for (uint32_t q = n >> 3; q <= (n + 23) >> 3; ++q) {
+      uint32_t byte = m[q];
+      for (uint32_t b = 0; b < 8; ++b) {
+        const uint32_t pos = 8 * q + b;
+        if (pos >= n && pos < n + 24) {
+          const uint32_t mask = 0x80u >> b;
+          byte                = (byte & ~mask) | (((crc >> (23 - (pos - n))) & 1u) ? mask : 0u);
+        }
+      }
+      m[q] = static_cast<uint8_t>(byte);
+    }
+  }
 }
 
 // TB byte j (bits 8j..8j+7) gathered from the concatenated codeblock data bits.
@@ -348,6 +429,23 @@ hipError_t launch_segment(const segment_args& a, hipStream_t stream)
   }
   dim3 grid((a.msg_bytes + SEG_THREADS - 1) / SEG_THREADS, a.nof_rows);
   hipLaunchKernelGGL(segment_kernel, grid, dim3(SEG_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_tx_slot_segment(const tx_slot_args& a, hipStream_t stream)
+{
+  if (a.nof_tbs == 0) {
+    return hipSuccess;
+  }
+  hipError_t e = hipMemsetAsync(a.acc, 0, sizeof(uint32_t) * a.nof_tbs, stream);
+  if (e != hipSuccess) {
+    return e;
+  }
+  hipLaunchKernelGGL(tx_tb_crc_kernel, dim3((a.max_tb_bytes + ASM_TB_CHUNK - 1) / ASM_TB_CHUNK, a.nof_tbs),
+                     dim3(ASM_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(tx_segment_kernel, dim3((a.max_msg_bytes + SEG_THREADS - 1) / SEG_THREADS, a.nof_rows),
+                     dim3(SEG_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(tx_cb_crc_kernel, dim3(a.nof_rows), dim3(64), 0, stream, a);
   return hipGetLastError();
 }
 

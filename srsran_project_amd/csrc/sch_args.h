@@ -35,15 +35,39 @@ struct soft_row_layout {
   uint32_t row_bytes;
 };
 
-// One transport block of a heterogeneous batch (srs_amd_pusch_decode_slot): its codeblock rows are
-// [row0, row0 + nof_segments) of the decoder scratch, its bytes go to tbs + tb_offset.
+// One transport block of a heterogeneous batch (srs_amd_pusch_decode_slot / srs_amd_pdsch_encode_slot): its
+// codeblock rows are [row0, row0 + nof_segments) of the scratch, its bytes at tbs + tb_offset.
 struct tb_desc {
   uint64_t tb_offset;
   uint32_t row0;
   uint32_t nof_segments;
   uint32_t cb_info_bits;
   uint32_t tbs_bits;
+  uint32_t tb_crc_bits; // 16 / 24
+  uint32_t zero_pad;
+  uint32_t msg_bytes;   // ceil(K / 8)
+  uint32_t pad;
 };
+
+// PDSCH encoder of a heterogeneous batch: TB CRCs (CRC16 or CRC24A per TB, linear CRC over chunks XOR-ed
+// into acc[t]), segmentation, and the CRC24B of the codeblocks of segmented TBs (per-row lengths).
+struct tx_slot_args {
+  const uint8_t*  tbs;        // TB bytes (tds[t].tb_offset)
+  const tb_desc*  tds;
+  const uint32_t* row_tb;     // TB of each message row
+  uint32_t*       acc;        // per-TB CRC accumulators (zeroed before tx_tb_crc_kernel)
+  uint8_t*        msgs;       // message rows of msg_stride bytes
+  const uint32_t* crc16_table;
+  const uint32_t* crc24a_table;
+  const uint32_t* crc24b_table;
+  uint32_t        crc16_poly, crc24a_poly, crc24b_poly;
+  uint32_t        msg_stride;
+  uint32_t        nof_tbs;
+  uint32_t        nof_rows;
+  uint32_t        max_tb_bytes;
+  uint32_t        max_msg_bytes;
+};
+hipError_t launch_tx_slot_segment(const tx_slot_args& a, hipStream_t stream);
 
 // pusch_decoder_impl.cpp:309-500 after the decoder: per-CB CRC status (kept in the
 // soft buffer across HARQ transmissions), statistics, codeblock concatenation

@@ -45,6 +45,13 @@ class PuschDecoderResult(ctypes.Structure):
 RESULT_WORDS = ctypes.sizeof(PuschDecoderResult) // 4
 
 
+class PdschUe(ctypes.Structure):
+    """``srs_amd_pdsch_ue``: one UE's transport block of a heterogeneous slot batch (one PDSCH PDU codeword,
+    pdsch_encoder.h:61)."""
+
+    _fields_ = [("plan", SchPlan), ("tb_offset", ctypes.c_uint64), ("cw_offset", ctypes.c_uint64)]
+
+
 class PuschUe(ctypes.Structure):
     """``srs_amd_pusch_ue``: one UE's transport block of a heterogeneous slot batch (its PUSCH PDU,
     pusch_processor_impl.cpp:343)."""
@@ -65,6 +72,7 @@ def _declare(lib):
         "srs_amd_pdsch_encoder_destroy": (None, [P]),
         "srs_amd_pdsch_encode": (c.c_int, [P, P, P, PP]),
         "srs_amd_pdsch_encode_batch": (c.c_int, [P, PP, P, u, P, u, u, P]),
+        "srs_amd_pdsch_encode_slot": (c.c_int, [P, c.POINTER(PdschUe), u, P, P, P]),
         "srs_amd_pusch_decoder_create": (c.c_int, [c.POINTER(P), c.c_int, c.c_int]),
         "srs_amd_pusch_decoder_destroy": (None, [P]),
         "srs_amd_pusch_soft_buffer_size": (c.c_uint64, [PP]),
@@ -182,6 +190,34 @@ class PdschEncoder:
                                                         tbs.data_ptr(), tbs.shape[1], n, _stream(stream, tbs)),
                    "pdsch encode_batch")
         return out
+
+
+def _encode_slot(self, tbs, ues, out=None, stream=None):
+    """Device form over UEs with different plans (one slot's PDSCH codewords): tbs: uint8 1-D tensor
+    holding every UE's transport block; ues: list of (plan, tb_offset, cw_offset).  Returns the uint8
+    1-D codeword tensor (packed MSB-first, each UE's codeword at its cw_offset)."""
+    import torch
+
+    if tbs.dim() != 1 or tbs.dtype != torch.uint8 or not tbs.is_contiguous():
+        raise ValueError("tbs must be a contiguous uint8 1-D tensor")
+    n = len(ues)
+    arr = (PdschUe * max(n, 1))()
+    cw_end = 0
+    for i, (plan, to, co) in enumerate(ues):
+        if to + plan.tbs // 8 > tbs.numel():
+            raise ValueError("UE %d transport block beyond the TB tensor" % i)
+        arr[i] = PdschUe(plan, int(to), int(co))
+        cw_end = max(cw_end, int(co) + (plan.cw_length + 7) // 8)
+    if out is None:
+        out = torch.zeros(cw_end, dtype=torch.uint8, device=tbs.device)
+    elif out.numel() < cw_end:
+        raise ValueError("codeword tensor too small")
+    _lib.check(self._lib.srs_amd_pdsch_encode_slot(self._h, arr, n, tbs.data_ptr(), out.data_ptr(),
+                                                   _stream(stream, tbs)), "pdsch encode_slot")
+    return out
+
+
+PdschEncoder.encode_slot = _encode_slot
 
 
 class PuschDecoder:

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Heterogeneous slot batches: parity tests (+ the SCH / codec / pipeline regressions) and the sch_slot bench.
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -6 "gpurun_out/$name.log"
+  [ $rc -eq 0 ] || exit $rc
+}
+run t_slot 600 python -u -m pytest tests/test_sch_slot_gpu.py tests/test_sch_gpu.py tests/test_ldpc_codec_gpu.py tests/test_crc_gpu.py tests/test_pipeline_gpu.py -x -q --timeout 200 --timeout-method thread -m gpu
+run b_slot 300 python bench.py --workload sch_slot --steps 20 --warmup 3
