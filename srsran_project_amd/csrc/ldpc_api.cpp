@@ -300,6 +300,70 @@ int srs_amd::ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
   return SRS_AMD_OK;
 }
 
+void srs_amd::ldpc_mixed_row(void* row, uint32_t bg, uint32_t Z, int crc_poly)
+{
+  ldpc_row_desc r{};
+  r.Z        = Z;
+  r.edge_off = static_cast<uint32_t>(lifted_edges_offset(static_cast<int>(bg), static_cast<int>(Z)));
+  r.crc_off  = crc_poly == SRS_AMD_NO_CRC ? NO_CRC_ROW : static_cast<uint32_t>(crc_poly) * MAX_CRC_BITS_LEN;
+  std::memcpy(row, &r, sizeof(r));
+}
+
+int srs_amd::ldpc_decode_mixed(srs_amd_ldpc_decoder* d,
+                               uint32_t              bg,
+                               uint32_t              max_z,
+                               uint32_t              max_iterations,
+                               const int8_t*         d_llrs,
+                               uint32_t              llr_stride,
+                               const uint32_t*       d_llr_lens,
+                               uint8_t*              d_output,
+                               uint32_t              out_stride,
+                               int32_t*              d_nof_iters,
+                               uint32_t              nof_cbs,
+                               void*                 stream,
+                               const int32_t*        d_fillers,
+                               const void*           d_rows)
+{
+  if (d == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null decoder");
+  }
+  if ((bg != 1 && bg != 2) || lifting_index(static_cast<int>(max_z)) < 0 || max_z >= 384 || max_iterations == 0) {
+    return fail(SRS_AMD_EINVAL, "invalid mixed-Z decoding (bg %u, max Z %u)", bg, max_z);
+  }
+  if (nof_cbs == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_llrs == nullptr || d_llr_lens == nullptr || d_output == nullptr || d_nof_iters == nullptr ||
+      d_fillers == nullptr || d_rows == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  std::lock_guard<std::mutex> lock(d->mtx);
+  hipError_t                  e = hipSetDevice(d->device);
+  if (e != hipSuccess) {
+    return hip_fail(e, "hipSetDevice");
+  }
+  // the launch shape (threads, LDS) of the largest lifting size; each codeblock reads its own graph
+  const lifted_graph& g = get_graph(d, static_cast<int>(bg), static_cast<int>(max_z));
+  decode_args         a{};
+  a.llrs           = d_llrs;
+  a.llr_lens       = d_llr_lens;
+  a.out            = d_output;
+  a.nof_iters      = d_nof_iters;
+  a.crc_table      = d->crc_tables;
+  a.edges          = d->edges;
+  a.llr_stride     = llr_stride;
+  a.aligned4       = ((reinterpret_cast<uintptr_t>(d_llrs) | llr_stride) & 3u) == 0 ? 1 : 0;
+  a.out_stride     = out_stride;
+  a.nof_cbs        = nof_cbs;
+  a.max_iterations = static_cast<int32_t>(max_iterations);
+  a.force_decoding = d->force_decoding;
+  a.fillers        = d_fillers;
+  a.rows           = static_cast<const ldpc_row_desc*>(d_rows);
+  const int grid   = static_cast<int>(nof_cbs < d->max_slots ? nof_cbs : d->max_slots);
+  e                = launch_ldpc_decode(a, g, d->arith, grid, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_decode_kernel launch");
+}
+
 extern "C" {
 
 int srs_amd_ldpc_decode(srs_amd_ldpc_decoder*              d,

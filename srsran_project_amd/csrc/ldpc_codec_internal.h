@@ -60,6 +60,27 @@ int ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
                          uint32_t                           skip_stride,
                          const int32_t*                     d_fillers = nullptr);
 
+// LDPC decoding of codeblocks of one base graph with per-codeblock lifting sizes (srs_amd_pusch_decode_slot):
+// row cb has lifting size row_z[cb] <= max_z < 384, input length llr_lens[cb], filler bits fillers[cb] and
+// CRC polynomial row_crc[cb] (SRS_AMD_NO_CRC: none), its soft row at d_llrs + cb * llr_stride.
+int ldpc_decode_mixed(srs_amd_ldpc_decoder* d,
+                      uint32_t              bg,
+                      uint32_t              max_z,
+                      uint32_t              max_iterations,
+                      const int8_t*         d_llrs,
+                      uint32_t              llr_stride,
+                      const uint32_t*       d_llr_lens,
+                      uint8_t*              d_output,
+                      uint32_t              out_stride,
+                      int32_t*              d_nof_iters,
+                      uint32_t              nof_cbs,
+                      void*                 stream,
+                      const int32_t*        d_fillers,
+                      const void*           d_rows);
+
+// Device row descriptor of ldpc_decode_mixed (16 bytes) for a codeblock of lifting size Z and CRC poly.
+void ldpc_mixed_row(void* row, uint32_t bg, uint32_t Z, int crc_poly);
+
 // Rate matching of codeblocks with per-codeblock geometry (srs_amd_pdsch_encode_slot): codeblock cb uses
 // geos[row_geo[cb]]; d_out_offsets are bit offsets into d_output.
 int rate_match_ragged(srs_amd_ldpc_rate_matcher* rm,

@@ -71,7 +71,19 @@ struct decode_args {
   // optional per-codeblock filler-bit count (replaces nof_filler_bits): a launch over the codeblocks of
   // several transport blocks with different segmentations (srs_amd_pusch_decode_slot)
   const int32_t*  fillers;
+  // optional per-codeblock graph (runtime-Z kernel only): codeblock cb has lifting size rows[cb].Z, its
+  // edges at edges + rows[cb].edge_off and its CRC table at crc_table + rows[cb].crc_off (NO_CRC_ROW: none)
+  const struct ldpc_row_desc* rows;
 };
+
+// Per-codeblock graph of a mixed-lifting-size launch (srs_amd_pusch_decode_slot).
+struct ldpc_row_desc {
+  uint32_t Z;
+  uint32_t edge_off;
+  uint32_t crc_off;
+  uint32_t pad;
+};
+constexpr uint32_t NO_CRC_ROW = 0xffffffffu;
 constexpr int32_t LDPC_ITERS_SKIPPED = -2;
 
 // Position of a lifting size in the 51-entry list (ldpc.h all_lifting_sizes), -1 if invalid.

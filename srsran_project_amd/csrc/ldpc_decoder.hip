@@ -464,17 +464,25 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
 {
   constexpr int NW      = reg_words<BG>();
   constexpr int N_FULL  = bg_traits<BG>::N_FULL;
-  const int     Z       = ZC > 0 ? ZC : g.Z;
   lds_i32*      red     = (lds_i32*)(uintptr_t)LDS_RED_OFFSET;
   lds_i8*       soft    = (lds_i8*)(uintptr_t)LDS_SOFT_OFFSET;
-  lds_i8*       c2v_lds = soft + lds_soft_bytes<BG>(Z);
 
   const int  nthr    = blockDim.x;
   constexpr int CPW  = checks_per_wave<ZC>();
-  const int  msg_len = bg_traits<BG>::K * Z;
-  const int  NZ      = N_FULL * Z;
 
   for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
+    // lifting size, graph and CRC of this codeblock: the launch's, or its row descriptor's (mixed Z)
+    // (row fields made wave-uniform explicitly: they feed scalar operands of the layer code)
+    const bool      mixed     = ZC == 0 && a.rows != nullptr;
+    const uint32_t  row_z     = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].Z) : 0u;
+    const uint32_t  row_e     = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].edge_off) : 0u;
+    const uint32_t  row_c     = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].crc_off) : 0u;
+    const int       Z         = ZC > 0 ? ZC : (mixed ? static_cast<int>(row_z) : g.Z);
+    const uint32_t* edges     = mixed ? a.edges + row_e : a.edges;
+    const uint32_t* crc_table = mixed ? (row_c == NO_CRC_ROW ? nullptr : a.crc_table + row_c) : a.crc_table;
+    lds_i8*         c2v_lds   = soft + lds_soft_bytes<BG>(Z);
+    const int       msg_len   = bg_traits<BG>::K * Z;
+    const int       NZ        = N_FULL * Z;
     if (a.skip_flags && *reinterpret_cast<const int32_t*>(a.skip_flags + static_cast<size_t>(cb) * a.skip_stride)) {
       if (threadIdx.x == 0) {
         a.nof_iters[cb] = LDPC_ITERS_SKIPPED; // uniform over the workgroup
@@ -562,7 +570,7 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
     if (input_size < msg_len && a.force_decoding) {
       // ldpc_decoder_impl.cpp:92: not enough soft bits -- all ones when no CRC,
       // output left untouched when a CRC is given (as the reference).
-      for (int b = j; b < obytes && !a.crc_table; b += nthr) {
+      for (int b = j; b < obytes && !crc_table; b += nthr) {
         uint8_t v = 0xff;
         if (b == obytes - 1 && (msg_len & 7)) {
           v &= static_cast<uint8_t>(0xff << (8 - (msg_len & 7)));
@@ -620,9 +628,9 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
     __syncthreads();
 
     for (int it = 0; it < a.max_iterations; ++it) {
-      run_layers<BG, ZC, 0, ARITH>(soft, c2v_lds, c2v, (const_u32_ptr)(a.edges), Z, jc, idle_slot, nof_layers);
+      run_layers<BG, ZC, 0, ARITH>(soft, c2v_lds, c2v, (const_u32_ptr)(edges), Z, jc, idle_slot, nof_layers);
 
-      if (a.crc_table) {
+      if (crc_table) {
         // get_hard_bits + CRC early stop (ldpc_decoder_impl.cpp:125): linear
         // CRC, every lane XORs the remainders of its set bits into LDS.
         int jj = threadIdx.x;
@@ -643,7 +651,7 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
             const int i  = 4 * q + b;
             zero |= (sb == 0);
             if (i < nof_sig && sb <= 0) {
-              crc ^= a.crc_table[nof_sig - 1 - i];
+              crc ^= crc_table[nof_sig - 1 - i];
             }
           }
         }
@@ -651,7 +659,7 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
           const int sb = soft[i];
           zero |= (sb == 0);
           if (i < nof_sig && sb <= 0) {
-            crc ^= a.crc_table[nof_sig - 1 - i];
+            crc ^= crc_table[nof_sig - 1 - i];
           }
         }
         if (crc != 0) {

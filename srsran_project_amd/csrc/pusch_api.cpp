@@ -20,6 +20,7 @@
 #include "crc_internal.h"
 #include "device_buffer.h"
 #include "ldpc_codec_internal.h"
+#include "ldpc_common.h"
 #include "rate_matching_common.h"
 #include "sch_args.h"
 #include <cstring>
@@ -253,14 +254,19 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
                        srs_amd_pusch_decoder_result*       d_results,
                        hipStream_t                         stream)
 {
+  // Z = 384 rows: one uniform launch per (BG, CRC, bounded prefix) -- the compile-time Z = 384 kernels,
+  // the high-rate one for bounded prefixes; Z < 384 rows: one mixed-Z launch per (BG, waves per
+  // codeblock), each row with its own Z, CRC, input length and filler bits.
   struct bucket {
-    uint32_t              bg, Z;
-    int                   poly;
+    uint32_t              bg, Z; // Z: the lifting size (uniform) or the largest one (mixed)
+    int                   poly;  // uniform buckets
+    bool                  mixed;
     uint32_t              prefix = 0, row0 = 0, rows = 0;
     std::vector<uint32_t> ues;
   };
-  std::vector<bucket>                                  buckets;
+  std::vector<bucket>                                          buckets;
   std::map<std::tuple<uint32_t, uint32_t, int, bool>, size_t> bucket_of;
+  std::vector<uint32_t>                                        ue_prefix(U);
   uint32_t                                             S = 0, M = 0, R = 0, max_tb_bits = 0;
   for (uint32_t u = 0; u < U; ++u) {
     const srs_amd_sch_plan* p  = &ues[u].plan;
@@ -278,15 +284,19 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     }
     const soft_row_layout lay    = layout_of(p);
     const uint32_t        prefix = llr_prefix(p, lay, true, true);
+    ue_prefix[u]                = prefix;
     // rows whose non-zero prefix is bounded decode apart from full rows: the bucket's LLR length is its
     // longest prefix, and a bounded one selects the high-rate decoder kernel
-    const auto key = std::make_tuple(p->base_graph, p->lifting_size, crc_poly_of(p), prefix < lay.soft_bytes);
-    auto                  it  = bucket_of.find(key);
+    const bool mixed = p->lifting_size < 384;
+    const auto key   = mixed ? std::make_tuple(p->base_graph, (p->lifting_size + 63) / 64, -1, false)
+                             : std::make_tuple(p->base_graph, p->lifting_size, crc_poly_of(p), prefix < lay.soft_bytes);
+    auto       it    = bucket_of.find(key);
     if (it == bucket_of.end()) {
       it = bucket_of.emplace(key, buckets.size()).first;
-      buckets.push_back(bucket{p->base_graph, p->lifting_size, crc_poly_of(p)});
+      buckets.push_back(bucket{p->base_graph, p->lifting_size, mixed ? -1 : crc_poly_of(p), mixed});
     }
     bucket& b = buckets[it->second];
+    b.Z       = std::max(b.Z, p->lifting_size);
     b.ues.push_back(u);
     b.rows += p->nof_segments;
     b.prefix    = std::max(b.prefix, prefix);
@@ -297,10 +307,12 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   }
   // host descriptors: per row E, input offset, geometry, filler bits; geometries + write ends; per-TB
   std::vector<uint32_t>                                                              row_E(R), row_in(R), row_geo(R);
+  std::vector<uint32_t>                                                              row_len(R);
   std::vector<int32_t>                                                               row_F(R);
+  std::vector<ldpc_row_desc>                                                         row_desc(R);
   std::vector<rm_geometry>                                                           geos;
   std::vector<uint32_t>                                                              geo_end;
-  std::map<std::tuple<size_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t>     geo_of;
+  std::map<std::tuple<size_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> geo_of;
   std::vector<tb_desc>                                                               tds(U);
   std::vector<uint32_t>                                                              segE, segOff;
   uint32_t                                                                           row = 0;
@@ -309,7 +321,10 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     b.row0    = row;
     for (uint32_t u : b.ues) {
       const srs_amd_sch_plan* p = &ues[u].plan;
-      const auto gkey = std::make_tuple(bi, p->rv, p->modulation_order, p->Nref, p->nof_filler_bits);
+      // dematcher write end: the longest prefix of a uniform bucket (its decoder reads that many LLRs of
+      // every row), each UE's own prefix in a mixed bucket (per-row input lengths)
+      const uint32_t wend = b.mixed ? ue_prefix[u] : b.prefix;
+      const auto     gkey = std::make_tuple(bi, p->rv, p->modulation_order, p->Nref, p->nof_filler_bits, wend);
       auto       git  = geo_of.find(gkey);
       if (git == geo_of.end()) {
         rm_geometry g{};
@@ -317,7 +332,7 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
                                p->nof_filler_bits);
         git = geo_of.emplace(gkey, static_cast<uint32_t>(geos.size())).first;
         geos.push_back(g);
-        geo_end.push_back(b.prefix);
+        geo_end.push_back(wend);
       }
       segE.resize(p->nof_segments);
       segOff.resize(p->nof_segments);
@@ -329,6 +344,9 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
         row_in[row]  = static_cast<uint32_t>(ues[u].llr_offset) + segOff[r];
         row_geo[row] = git->second;
         row_F[row]   = static_cast<int32_t>(p->nof_filler_bits);
+        row_len[row] = wend;
+        ldpc_mixed_row(&row_desc[row], p->base_graph, p->lifting_size,
+                       cfg->use_early_stop ? crc_poly_of(p) : SRS_AMD_NO_CRC);
       }
     }
   }
@@ -339,7 +357,9 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   const size_t o_G   = o_F + align_up(sizeof(int32_t) * R, 16);
   const size_t o_GE  = o_G + align_up(sizeof(rm_geometry) * geos.size(), 16);
   const size_t o_TD  = o_GE + align_up(sizeof(uint32_t) * geos.size(), 16);
-  const size_t total = o_TD + sizeof(tb_desc) * U;
+  const size_t o_LEN = o_TD + align_up(sizeof(tb_desc) * U, 16);
+  const size_t o_RD  = o_LEN + align_up(sizeof(uint32_t) * R, 16);
+  const size_t total = o_RD + sizeof(ldpc_row_desc) * R;
 
   hipError_t he = hipSetDevice(d->device);
   // the pinned staging buffer is rewritten only once its previous upload completed
@@ -387,6 +407,8 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   std::memcpy(h + o_G, geos.data(), sizeof(rm_geometry) * geos.size());
   std::memcpy(h + o_GE, geo_end.data(), sizeof(uint32_t) * geo_end.size());
   std::memcpy(h + o_TD, tds.data(), sizeof(tb_desc) * U);
+  std::memcpy(h + o_LEN, row_len.data(), sizeof(uint32_t) * R);
+  std::memcpy(h + o_RD, row_desc.data(), sizeof(ldpc_row_desc) * R);
   auto* dd = d->slot_desc.as<uint8_t>();
   he       = d->order.begin(stream);
   if (he == hipSuccess) {
@@ -431,6 +453,17 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     }
     load[si] += static_cast<uint64_t>(b.rows) * b.Z;
     const hipStream_t bs = d->fan.stream(stream, si);
+    if (b.mixed) {
+      rc = ldpc_decode_mixed(ldpc, b.bg, b.Z, cfg->nof_ldpc_iterations, soft + static_cast<size_t>(b.row0) * S, S,
+                             reinterpret_cast<const uint32_t*>(dd + o_LEN) + b.row0,
+                             d->msgs.as<uint8_t>() + static_cast<size_t>(b.row0) * M, M,
+                             d->iters.as<int32_t>() + b.row0, b.rows, bs, d_F + b.row0,
+                             dd + o_RD + sizeof(ldpc_row_desc) * b.row0);
+      if (rc != SRS_AMD_OK) {
+        return rc;
+      }
+      continue;
+    }
     srs_amd_ldpc_decoder_config dc{};
     dc.base_graph     = b.bg;
     dc.lifting_size   = b.Z;

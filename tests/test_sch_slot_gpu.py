@@ -173,3 +173,40 @@ def test_encode_slot_equals_uniform_batch(enc):
     got = enc.encode_slot(d_rows.reshape(-1), [(p, k * tbb, k * cwb) for k in range(m)]).cpu().numpy()
     for k in range(m):
         np.testing.assert_array_equal(got[k * cwb:(k + 1) * cwb], want[k, :cwb], err_msg="TB %d" % k)
+
+
+@pytest.mark.parametrize("early", [True, False])
+def test_realistic_slot_equals_per_ue(decs, enc, early):
+    """A slot as bench.py --workload sch_slot builds it (4 cells x 8 UEs: random PRB split, MCS QPSK..256QAM,
+    1-4 layers; ~20 lifting sizes, mixed-Z decoder launches) encodes and decodes exactly as one per-plan
+    batch per UE."""
+    import torch
+
+    import bench_slot
+    import srsran_project_amd as amd
+
+    plans = bench_slot.make_slot(amd, 4, 8, 77)
+    tx, rx, tpos, cpos = [], [], 0, 0
+    for p in plans:
+        tx.append((p, tpos, cpos))
+        rx.append((p, 8 * cpos, tpos))
+        tpos += p.tbs // 8
+        cpos += (p.cw_length + 7) // 8
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    tbs = torch.randint(0, 256, (tpos,), device="cuda", generator=g, dtype=torch.uint8)
+    cws = enc.encode_slot(tbs, tx)
+    bits = ((cws[:, None] >> torch.arange(7, -1, -1, device="cuda", dtype=torch.uint8)) & 1).reshape(-1).float()
+    sigma = torch.rand(bits.shape, device="cuda", generator=g) * 12  # from clean to undecodable
+    llrs = ((1 - 2 * bits) * 10 + sigma * torch.randn(bits.shape, device="cuda", generator=g)).round()
+    llrs = llrs.clamp(-120, 120).to(torch.int8)
+    cfg = amd.PuschDecoder.config(nof_ldpc_iterations=6, use_early_stop=early)
+    d_tb, res = decs["simd"].decode_slot(llrs, rx, cfg)
+    torch.cuda.synchronize()
+    for u, ((p, to, co), (_, lo, _)) in enumerate(zip(tx, rx)):
+        cw1 = enc.encode_batch(tbs[to:to + p.tbs // 8].view(1, -1), p)
+        nb = (p.cw_length + 7) // 8
+        assert torch.equal(cw1[0, :nb], cws[co:co + nb]), "UE %d codeword" % u
+        tb1, res1 = decs["simd"].decode_batch(llrs[lo:lo + p.cw_length].view(1, -1), p, cfg)
+        assert torch.equal(res[u], res1[0]), "UE %d: %s vs %s" % (u, res[u].tolist(), res1[0].tolist())
+        assert torch.equal(d_tb[to:to + p.tbs // 8], tb1[0]), "UE %d TB" % u
