@@ -10,7 +10,8 @@
  *       include/srsran/phy/upper/channel_processors/pusch/pusch_demodulator.h:95
  *       (impl lib/phy/upper/channel_processors/pusch/pusch_demodulator_impl.cpp:203-330)
  *
- * Scope: no transform precoding, no UCI multiplexing (the codeword is all
+ * Scope: transform precoding (DFT-s-OFDM, pusch_demodulator_impl.cpp:344-351: equalized symbols ->
+ * transform_precoding.h deprecoder -> demapper), no UCI multiplexing (the codeword is all
  * UL-SCH), the equalizers of equalizer.h: the open-source reference's (ZF 1 layer x
  * {1,2,4} ports, ZF 2 layers x {2,4} ports, MMSE 1 layer) and the L-layer ZF 3x4 / 4x4 and
  * MMSE 2x2 / 2x4 / 3x4 / 4x4 solves (parity unpinned). The post-equalization SINR / EVM
@@ -51,6 +52,8 @@ typedef struct srs_amd_pusch_demod_config {
   uint32_t nof_tx_layers;              /* 1 to 4 (no more than nof_rx_ports) */
   uint32_t nof_rx_ports;               /* 1, 2 or 4 */
   int32_t  equalizer;                  /* SRS_AMD_EQ_ZF or SRS_AMD_EQ_MMSE */
+  uint32_t transform_precoding;        /* enable_transform_precoding: DFT-s-OFDM, one layer, every data OFDM
+                                          symbol 12 x M_rb REs with M_rb valid (transform_precoding.h) */
 } srs_amd_pusch_demod_config;
 
 typedef struct srs_amd_pusch_demodulator srs_amd_pusch_demodulator;

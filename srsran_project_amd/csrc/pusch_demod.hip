@@ -71,6 +71,14 @@ template <int L>
 __device__ __forceinline__ void emit_llrs(const pusch_eq_args& a, const float* lt, uint32_t gi, uint32_t j, uint32_t l,
                                           const float2 (&s)[L], const float (&nv)[L])
 {
+  if (a.eq_out != nullptr) {
+#pragma unroll
+    for (int v = 0; v < L; ++v) {
+      a.eq_out[gi * a.eq_stride + j * L + v] = s[v];
+      a.nv_out[gi * a.eq_stride + j * L + v] = nv[v];
+    }
+    return;
+  }
   int8_t*        row     = a.llrs + static_cast<uint64_t>(gi) * a.llr_stride;
   const uint32_t simd_hi = a.simd_hi[l];
   switch (a.dm.qm) {

@@ -8,6 +8,7 @@
 // gather), soft demapping (the modulator object's kernel, modulation.h) and
 // descrambling, three launches on the caller's stream.
 #include "srsran_amd/pusch_demodulator.h"
+#include "srsran_amd/transform_precoding.h"
 
 #include <hip/hip_runtime.h>
 
@@ -30,6 +31,7 @@ struct srs_amd_pusch_demodulator {
   srs_amd_modulator*  demapper = nullptr;
   device_buffer       scratch;
   stream_order        order; // scratch reuse across the callers' streams
+  srs_amd_transform_precoder* tp = nullptr; // transform precoding plans, created on first use
   device_buffer       host_io;
   std::mutex          mtx;
   ~srs_amd_pusch_demodulator()
@@ -40,6 +42,7 @@ struct srs_amd_pusch_demodulator {
       (void)hipStreamDestroy(stream);
     }
     srs_amd_modulator_destroy(demapper);
+    srs_amd_transform_precoder_destroy(tp);
     (void)hipFree(d_jump);
   }
 };
@@ -55,6 +58,7 @@ struct srs_amd_pusch_demod_plan {
   int32_t       qm          = 0;
   uint32_t      c_init      = 0;
   uint32_t      sym_counts[14] = {}; // demapper symbols (data REs x layers) per OFDM symbol
+  uint32_t      tp_subc     = 0;     // transform precoding: subcarriers per data OFDM symbol (0: off)
   uint32_t*     d_table     = nullptr;
   uint32_t*     d_scr       = nullptr; // Gold words of c_init over the codeword (+1)
   ~srs_amd_pusch_demod_plan()
@@ -136,9 +140,33 @@ static int demodulate_impl(srs_amd_pusch_demodulator*      dem,
       return fail(SRS_AMD_EINVAL, "channel estimator output does not match the demodulator plan");
     }
   }
-  // the equalizer demaps and descrambles its own symbols: LLRs straight into the caller's rows, no scratch
+  // the equalizer demaps and descrambles its own symbols: LLRs straight into the caller's rows, no scratch;
+  // with transform precoding it writes equalized symbols to scratch for the deprecoder and the demapper
   hipError_t    e = hipSetDevice(dem->device);
   pusch_eq_args a = plan->args;
+  auto          s = static_cast<hipStream_t>(stream);
+  const bool    tp = plan->tp_subc != 0;
+  if (tp) {
+    const uint64_t n = static_cast<uint64_t>(nof_grids) * plan->args.nof_re; // one layer
+    if (e == hipSuccess && dem->tp == nullptr) {
+      int rc = srs_amd_transform_precoder_create(&dem->tp, dem->device);
+      if (rc != SRS_AMD_OK) {
+        return rc;
+      }
+    }
+    if (e == hipSuccess) {
+      e = dem->scratch.ensure(n * (sizeof(float2) + sizeof(float)));
+    }
+    if (e == hipSuccess) {
+      e = dem->order.begin(s);
+    }
+    if (e != hipSuccess) {
+      return hip_fail(e, "PUSCH demodulator transform-precoding scratch");
+    }
+    a.eq_out    = dem->scratch.as<float2>();
+    a.nv_out    = reinterpret_cast<float*>(dem->scratch.as<float2>() + n);
+    a.eq_stride = plan->args.nof_re;
+  }
   a.grids         = d_grids;
   a.grid_stride   = grid_stride;
   a.estimates     = d_estimates;
@@ -146,14 +174,33 @@ static int demodulate_impl(srs_amd_pusch_demodulator*      dem,
   a.stats         = d_stats;
   a.llrs          = d_llrs;
   a.llr_stride    = llr_stride;
-  auto s          = static_cast<hipStream_t>(stream);
   if (e == hipSuccess) {
     e = fused != nullptr ? launch_pusch_equalize_fused(a, *fused, plan->nof_ports, plan->nof_layers, plan->mmse,
                                                        plan->span_subc, nof_grids, s)
                          : launch_pusch_equalize(a, plan->nof_ports, plan->nof_layers, plan->mmse, plan->nof_symbols,
                                                  plan->span_subc, nof_grids, s);
   }
-  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_equalize_kernel launch");
+  if (e != hipSuccess) {
+    return hip_fail(e, "pusch_equalize_kernel launch");
+  }
+  if (!tp) {
+    return SRS_AMD_OK;
+  }
+  // transform deprecoding of every data OFDM symbol (rows of tp_subc symbols, pusch_demodulator_impl.cpp:344-351),
+  // then demapping + descrambling per OFDM symbol
+  const uint32_t rows = nof_grids * (plan->args.nof_re / plan->tp_subc);
+  int rc = srs_amd_transform_deprecode_batch(dem->tp, reinterpret_cast<float*>(a.eq_out), plan->tp_subc, a.nv_out,
+                                             plan->tp_subc, plan->tp_subc, rows, stream);
+  if (rc == SRS_AMD_OK) {
+    rc = demap_descramble_batch(dem->demapper, plan->qm, d_llrs, llr_stride, reinterpret_cast<const float*>(a.eq_out),
+                                a.nv_out, plan->args.nof_re, plan->sym_counts, nof_grids, dem->d_jump, plan->c_init,
+                                stream);
+  }
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  e = dem->order.end(s);
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH demodulator completion event");
 }
 
 int srs_amd::pusch_demodulate_batch_fused(::srs_amd_pusch_demodulator*      dem,
@@ -272,7 +319,27 @@ int srs_amd_pusch_demod_plan_create(srs_amd_pusch_demodulator*        dem,
     }
     sym_counts[l] = count - sym_start;
   }
+  uint32_t tp_subc = 0;
+  if (cfg->transform_precoding) {
+    // pusch_demodulator_impl.cpp:345-349 and transform_precoder_dft_impl.cpp:35-41
+    if (cfg->nof_tx_layers != 1) {
+      return fail(SRS_AMD_EINVAL, "Transform precoding is only possible with one layer (i.e. %u).", cfg->nof_tx_layers);
+    }
+    for (uint32_t l = 0; l < 14; ++l) {
+      if (sym_counts[l] == 0) {
+        continue;
+      }
+      if (tp_subc != 0 && sym_counts[l] != tp_subc) {
+        return fail(SRS_AMD_EINVAL, "transform precoding: OFDM symbols with %u and %u data REs", tp_subc, sym_counts[l]);
+      }
+      tp_subc = sym_counts[l];
+    }
+    if (tp_subc % 12 != 0 || !srs_amd_transform_precoding_nof_prbs_valid(tp_subc / 12)) {
+      return fail(SRS_AMD_EINVAL, "The number of PRB (i.e., %u) is not valid.", tp_subc / 12);
+    }
+  }
   auto* p         = new srs_amd_pusch_demod_plan();
+  p->tp_subc      = tp_subc;
   p->device       = dem->device;
   p->nof_ports    = cfg->nof_rx_ports;
   p->nof_layers   = cfg->nof_tx_layers;

@@ -33,6 +33,11 @@ struct pusch_eq_args {
   uint64_t                        llr_stride;
   uint32_t                        simd_hi[14];
   demodulate_args                 dm;
+  // transform precoding: the equalizer writes its symbols / noise variances (grid rows of eq_stride
+  // codeword symbols) instead of LLRs; the deprecoder and the demapper follow
+  float2*                         eq_out;
+  float*                          nv_out;
+  uint64_t                        eq_stride;
   uint32_t                        tiles_x;   // fused equalizer: 256-subcarrier tiles per grid
   uint32_t                        nof_tiles; // tiles_x x grids
 };

@@ -25,12 +25,13 @@ class _Config(ctypes.Structure):
                 ("start_symbol", ctypes.c_uint32), ("nof_symbols", ctypes.c_uint32),
                 ("dmrs_symbol_mask", ctypes.c_uint32), ("dmrs_type", ctypes.c_uint32),
                 ("nof_cdm_groups_without_data", ctypes.c_uint32), ("nof_tx_layers", ctypes.c_uint32),
-                ("nof_rx_ports", ctypes.c_uint32), ("equalizer", ctypes.c_int32)]
+                ("nof_rx_ports", ctypes.c_uint32), ("equalizer", ctypes.c_int32),
+                ("transform_precoding", ctypes.c_uint32)]
 
 
 @dataclass
 class PuschDemodulatorConfig:
-    """pusch_demodulator::configuration (rb_mask as CRB indices; no transform precoding)."""
+    """pusch_demodulator::configuration (rb_mask as CRB indices)."""
 
     rnti: int
     crbs: list
@@ -44,11 +45,13 @@ class PuschDemodulatorConfig:
     dmrs_type: int = 1
     nof_cdm_groups_without_data: int = 2
     equalizer: int = 0  # ChannelEqualizerAlgorithmType
+    enable_transform_precoding: bool = False
 
     def _c(self):
         return _Config(self.rnti, self.n_id, self.modulation, _mask_bytes(self.crbs), 0, self.start_symbol,
                        self.nof_symbols, self.dmrs_symb_pos, self.dmrs_type, self.nof_cdm_groups_without_data,
-                       self.nof_tx_layers, self.nof_rx_ports, int(self.equalizer))
+                       self.nof_tx_layers, self.nof_rx_ports, int(self.equalizer),
+                       int(self.enable_transform_precoding))
 
 
 def _declare(lib):
