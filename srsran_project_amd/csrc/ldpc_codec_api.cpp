@@ -557,6 +557,71 @@ int srs_amd::rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_rate_dematch_kernel launch");
 }
 
+uint32_t srs_amd::ldpc_encode_mixed_row(void* row, uint32_t bg, uint32_t Z, uint32_t max_bits)
+{
+  lifted_graph g{};
+  encode_args  a{};
+  build_lifted_graph(g, static_cast<int>(bg), static_cast<int>(Z));
+  (void)build_encode_params(a, g);
+  // as ldpc_encode_batch_ex: rows whose parity columns hold shortened-codeword positions < max_bits
+  const uint32_t full_bits = static_cast<uint32_t>(g.N_short * g.Z);
+  max_bits                 = std::min(max_bits, full_bits);
+  const int cols           = static_cast<int>((max_bits + Z - 1) / Z) + 2;
+  enc_row_desc r{};
+  r.Z         = Z;
+  r.edge_off  = static_cast<uint32_t>(lifted_edges_offset(static_cast<int>(bg), static_cast<int>(Z)));
+  r.M_eff     = static_cast<uint32_t>(std::max(4, std::min(a.M, cols - a.K)));
+  r.pack_bits = max_bits == full_bits ? full_bits : std::min(full_bits, (max_bits + 7) / 8 * 8);
+  r.p0_shift  = static_cast<uint32_t>(a.p0_shift);
+  for (int c = 0; c < 3; ++c) {
+    r.core_a[c] = static_cast<uint32_t>(a.core_a[c]);
+  }
+  static_assert(sizeof(r) == LDPC_ENCODE_ROW_BYTES, "row descriptor size");
+  std::memcpy(row, &r, sizeof(r));
+  return r.M_eff;
+}
+
+int srs_amd::ldpc_encode_mixed(srs_amd_ldpc_encoder* enc,
+                               uint32_t              bg,
+                               uint32_t              max_z,
+                               uint32_t              max_rows_eff,
+                               const uint8_t*        d_messages,
+                               uint32_t              msg_stride,
+                               uint8_t*              d_codeblocks,
+                               uint32_t              cb_stride,
+                               uint32_t              nof_cbs,
+                               void*                 stream,
+                               const void*           d_rows)
+{
+  if (enc == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null encoder");
+  }
+  if (nof_cbs == 0) {
+    return SRS_AMD_OK;
+  }
+  lifted_graph g{};
+  if ((bg != 1 && bg != 2) || !build_lifted_graph(g, static_cast<int>(bg), static_cast<int>(max_z)) || max_z < 32 ||
+      d_messages == nullptr || d_codeblocks == nullptr || d_rows == nullptr) {
+    return fail(SRS_AMD_EINVAL, "invalid mixed-Z encoding (bg %u, max Z %u)", bg, max_z);
+  }
+  encode_args a{};
+  (void)build_encode_params(a, g);
+  a.msgs       = d_messages;
+  a.cws        = d_codeblocks;
+  a.edges      = enc->edges;
+  a.msg_stride = msg_stride;
+  a.cw_stride  = cb_stride;
+  a.nof_cbs    = nof_cbs;
+  a.M_eff      = static_cast<int32_t>(max_rows_eff);
+  a.rows       = static_cast<const enc_row_desc*>(d_rows);
+  std::lock_guard<std::mutex> lock(enc->mtx);
+  hipError_t                  e = hipSetDevice(enc->device);
+  if (e == hipSuccess) {
+    e = launch_ldpc_encode(a, static_cast<int>(std::min(nof_cbs, ENCODE_GRID_CAP)), static_cast<hipStream_t>(stream));
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_encode_kernel launch");
+}
+
 int srs_amd::rate_match_ragged(srs_amd_ldpc_rate_matcher* rm,
                                const uint8_t*             d_codeblocks,
                                uint32_t                   cb_stride,

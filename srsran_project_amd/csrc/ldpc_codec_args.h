@@ -27,6 +27,19 @@ struct encode_args {
   int32_t         p0_shift;  // s: p0 = P^-s (sum of lambdas)
   int32_t         core_a[4]; // shift of column K_bg in rows 0..3 (0 where absent)
   int32_t         row_start[MAX_BG_M + 1];
+  // optional per-codeblock lifting size (bit-sliced kernel, every Z >= 32 of one base graph): codeblock cb
+  // uses rows[cb] and its edges at edges + rows[cb].edge_off; Z / M_eff above are then the launch maxima
+  const struct enc_row_desc* rows;
+};
+
+// Per-codeblock graph of a mixed-lifting-size encoder launch (srs_amd_pdsch_encode_slot).
+struct enc_row_desc {
+  uint32_t Z;
+  uint32_t edge_off;
+  uint32_t M_eff;
+  uint32_t pack_bits;
+  uint32_t p0_shift;
+  uint32_t core_a[3];
 };
 
 struct dematch_args {

@@ -81,6 +81,26 @@ int ldpc_decode_mixed(srs_amd_ldpc_decoder* d,
 // Device row descriptor of ldpc_decode_mixed (16 bytes) for a codeblock of lifting size Z and CRC poly.
 void ldpc_mixed_row(void* row, uint32_t bg, uint32_t Z, int crc_poly);
 
+// LDPC encoding of codeblocks of one base graph with per-codeblock lifting sizes (all >= 32) in one launch
+// (srs_amd_pdsch_encode_slot): d_rows holds ldpc_encode_mixed_row descriptors; max_z / max_rows_eff size the
+// launch (the largest Z and extension row count of the batch).
+int ldpc_encode_mixed(srs_amd_ldpc_encoder* enc,
+                      uint32_t              bg,
+                      uint32_t              max_z,
+                      uint32_t              max_rows_eff,
+                      const uint8_t*        d_messages,
+                      uint32_t              msg_stride,
+                      uint8_t*              d_codeblocks,
+                      uint32_t              cb_stride,
+                      uint32_t              nof_cbs,
+                      void*                 stream,
+                      const void*           d_rows);
+
+// Row descriptor (32 bytes) of ldpc_encode_mixed for a codeblock of lifting size Z whose rate matcher reads
+// the first max_bits of the shortened codeword; returns the extension rows it computes (M_eff).
+uint32_t ldpc_encode_mixed_row(void* row, uint32_t bg, uint32_t Z, uint32_t max_bits);
+constexpr size_t LDPC_ENCODE_ROW_BYTES = 32;
+
 // Rate matching of codeblocks with per-codeblock geometry (srs_amd_pdsch_encode_slot): codeblock cb uses
 // geos[row_geo[cb]]; d_out_offsets are bit offsets into d_output.
 int rate_match_ragged(srs_amd_ldpc_rate_matcher* rm,

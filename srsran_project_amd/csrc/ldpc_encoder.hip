@@ -192,18 +192,32 @@ __device__ __forceinline__ void lds_or_bits(uint32_t* W, uint32_t off, uint32_t 
 __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(encode_args a)
 {
   extern __shared__ uint32_t lw[];
-  const uint32_t Z   = static_cast<uint32_t>(a.Z);
-  const uint32_t K   = static_cast<uint32_t>(a.K);
-  const uint32_t kz  = K * Z;
-  const uint32_t nq  = (Z + 31) / 32;
-  const uint32_t tot = (K + static_cast<uint32_t>(a.M_eff)) * Z;
-  const uint32_t ncw = (tot + 31) / 32 + 2;
-  uint32_t*      cw  = lw;            // [ncw] codeword bits
-  uint32_t*      lam = lw + ncw;      // [4][nq] systematic part of the high-rate rows
-  uint32_t*      ls  = lam + 4 * nq;  // [nq + 2] lambda sum as a column at bit 0
-  const uint32_t j   = threadIdx.x;
+  const uint32_t K = static_cast<uint32_t>(a.K);
+  const uint32_t j = threadIdx.x;
 
   for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
+    // lifting size and graph of this codeblock: the launch's, or its row descriptor's (mixed Z; the
+    // launch's LDS is sized for the largest), made wave-uniform explicitly
+    const bool      mixed     = a.rows != nullptr;
+    const uint32_t  Z         = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].Z) : static_cast<uint32_t>(a.Z);
+    const uint32_t* edges     = mixed ? a.edges + __builtin_amdgcn_readfirstlane(a.rows[cb].edge_off) : a.edges;
+    const uint32_t  M_eff     = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].M_eff) : static_cast<uint32_t>(a.M_eff);
+    const uint32_t  pack_bits = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].pack_bits)
+                                      : static_cast<uint32_t>(a.pack_bits);
+    const int32_t   p0_shift  = mixed ? static_cast<int32_t>(__builtin_amdgcn_readfirstlane(a.rows[cb].p0_shift))
+                                      : a.p0_shift;
+    int32_t         core_a[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      core_a[c] = mixed ? static_cast<int32_t>(__builtin_amdgcn_readfirstlane(a.rows[cb].core_a[c])) : a.core_a[c];
+    }
+    const uint32_t kz  = K * Z;
+    const uint32_t nq  = (Z + 31) / 32;
+    const uint32_t tot = (K + M_eff) * Z;
+    const uint32_t ncw = (tot + 31) / 32 + 2;
+    uint32_t*      cw  = lw;            // [ncw] codeword bits
+    uint32_t*      lam = lw + ncw;      // [4][nq] systematic part of the high-rate rows
+    uint32_t*      ls  = lam + 4 * nq;  // [nq + 2] lambda sum as a column at bit 0
     // 1. Message words (bit reversal of 4 MSB-first bytes), the rest zeroed.
     const uint8_t* msg    = a.msgs + static_cast<size_t>(cb) * a.msg_stride;
     const uint32_t nbytes = (kz + 7) / 8;
@@ -234,7 +248,7 @@ __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(enco
       const uint32_t r = task / nq, x0 = 32 * (task - r * nq);
       uint32_t       acc = 0;
       for (int e = a.row_start[r]; e < a.row_start[r + 1]; ++e) {
-        const uint32_t ed   = a.edges[e];
+        const uint32_t ed   = edges[e];
         const uint32_t base = ed & 0xffffu;
         if (base >= kz) {
           break; // edges are sorted by column
@@ -252,7 +266,7 @@ __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(enco
     __syncthreads();
 
     // 3. p0 = P^-s (lambda sum): row x takes the sum's row (x - s) mod Z.
-    const uint32_t sh0 = (Z - static_cast<uint32_t>(a.p0_shift) % Z) % Z;
+    const uint32_t sh0 = (Z - static_cast<uint32_t>(p0_shift) % Z) % Z;
     for (uint32_t q = j; q < nq; q += ENC_BITS_THREADS) {
       lds_or_bits(cw, kz + 32 * q, cyc32(ls, 0, Z, 32 * q, sh0), min(32u, Z - 32 * q));
     }
@@ -263,13 +277,13 @@ __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(enco
       const uint32_t x0 = 32 * q, n = min(32u, Z - x0);
       auto           at = [&](int s) { return cyc32(cw, kz, Z, x0, static_cast<uint32_t>(s)); };
       uint32_t       p1, p2, p3;
-      p1 = lam[q] ^ at(a.core_a[0]);
+      p1 = lam[q] ^ at(core_a[0]);
       if (a.bg == 1) {
-        p2 = lam[nq + q] ^ at(a.core_a[1]) ^ p1;
+        p2 = lam[nq + q] ^ at(core_a[1]) ^ p1;
         p3 = lam[2 * nq + q] ^ p2;
       } else {
         p2 = lam[nq + q] ^ p1;
-        p3 = lam[2 * nq + q] ^ at(a.core_a[2]) ^ p2;
+        p3 = lam[2 * nq + q] ^ at(core_a[2]) ^ p2;
       }
       lds_or_bits(cw, kz + Z + x0, p1, n);
       lds_or_bits(cw, kz + 2 * Z + x0, p2, n);
@@ -279,11 +293,11 @@ __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(enco
 
     // 5. Extension rows: independent single-parity rows over columns < K + 4.
     const uint32_t hz = kz + 4 * Z;
-    for (uint32_t task = j; task < (static_cast<uint32_t>(a.M_eff) - 4) * nq; task += ENC_BITS_THREADS) {
+    for (uint32_t task = j; task < (M_eff - 4) * nq; task += ENC_BITS_THREADS) {
       const uint32_t rr = task / nq, r = 4 + rr, x0 = 32 * (task - rr * nq);
       uint32_t       acc = 0;
       for (int e = a.row_start[r]; e < a.row_start[r + 1]; ++e) {
-        const uint32_t ed   = a.edges[e];
+        const uint32_t ed   = edges[e];
         const uint32_t base = ed & 0xffffu;
         if (base >= hz) {
           break;
@@ -296,7 +310,7 @@ __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(enco
 
     // 6. Pack the shortened codeword (from bit 2Z), MSB-first.
     uint8_t*       out   = a.cws + static_cast<size_t>(cb) * a.cw_stride;
-    const uint32_t nbits = static_cast<uint32_t>(a.pack_bits);
+    const uint32_t nbits = pack_bits;
     const uint32_t nb    = (nbits + 7) / 8;
     const bool     al    = ((reinterpret_cast<uintptr_t>(out)) & 3u) == 0;
     for (uint32_t m = j; 4 * m < nb; m += ENC_BITS_THREADS) {
@@ -324,7 +338,8 @@ size_t ldpc_encode_lds_bytes(int K, int M_eff, int Z)
 
 hipError_t launch_ldpc_encode(const encode_args& a, int grid, hipStream_t stream)
 {
-  if (a.Z >= 32) {
+  // (mixed Z: a.Z / a.M_eff are the largest of the launch, for the LDS size)
+  if (a.Z >= 32 || a.rows != nullptr) {
     const size_t nq    = (a.Z + 31) / 32;
     const size_t words = ((static_cast<size_t>(a.K) + a.M_eff) * a.Z + 31) / 32 + 2 + 4 * nq + nq + 2;
     hipLaunchKernelGGL(ldpc_encode_bits_kernel, dim3(grid), dim3(ENC_BITS_THREADS), words * 4, stream, a);

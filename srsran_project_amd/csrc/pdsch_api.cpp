@@ -182,14 +182,18 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
                        uint8_t*                d_cw,
                        hipStream_t             stream)
 {
+  // Z < 32: one uniform launch per (BG, Z) (the byte-per-bit kernel); Z >= 32: one mixed-Z launch per BG
+  // (the bit-sliced kernel reads each codeblock's Z, graph and encoded window from a row descriptor)
   struct bucket {
-    uint32_t              bg, Z;
-    uint32_t              max_bits = 0, row0 = 0, rows = 0;
+    uint32_t              bg, Z; // Z: the lifting size (uniform) or the largest (mixed)
+    bool                  mixed;
+    uint32_t              max_bits = 0, row0 = 0, rows = 0, max_rows_eff = 0;
     std::vector<uint32_t> ues;
   };
   std::vector<bucket>                         buckets;
   std::map<std::pair<uint32_t, uint32_t>, size_t> bucket_of;
   std::vector<rm_geometry>                    ug(U);
+  std::vector<uint32_t>                       ue_window(U);
   uint32_t MS = 0, CS = 0, R = 0, max_tb_bytes = 0, max_msg_bytes = 0;
   for (uint32_t u = 0; u < U; ++u) {
     const srs_amd_sch_plan* p  = &ues[u].plan;
@@ -204,19 +208,22 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
     if ((ues[u].cw_offset + (p->cw_length + 7) / 8) * 8 > 0xffffffffull) {
       return fail(SRS_AMD_EINVAL, "UE %u: codeword span exceeds 2^32 bits", u);
     }
-    const auto key = std::make_pair(p->base_graph, p->lifting_size);
-    auto       it  = bucket_of.find(key);
+    const bool mixed = p->lifting_size >= 32;
+    const auto key   = std::make_pair(p->base_graph, mixed ? 0u : p->lifting_size);
+    auto       it    = bucket_of.find(key);
     if (it == bucket_of.end()) {
       it = bucket_of.emplace(key, buckets.size()).first;
-      buckets.push_back(bucket{p->base_graph, p->lifting_size});
+      buckets.push_back(bucket{p->base_graph, p->lifting_size, mixed});
     }
     bucket& b = buckets[it->second];
+    b.Z       = std::max(b.Z, p->lifting_size);
     b.ues.push_back(u);
     b.rows += p->nof_segments;
     // only the circular-buffer window the rate matcher reads is encoded (ldpc_rate_matcher_impl.cpp:95-130)
     const uint64_t window = static_cast<uint64_t>(ug[u].k0) + std::max(p->rm_length_long, p->rm_length_short) +
                             ug[u].F;
-    b.max_bits    = std::max(b.max_bits, window >= ug[u].Ncb ? ug[u].Ncb : static_cast<uint32_t>(window));
+    ue_window[u]  = window >= ug[u].Ncb ? ug[u].Ncb : static_cast<uint32_t>(window);
+    b.max_bits    = std::max(b.max_bits, ue_window[u]);
     const uint32_t N = srs_amd_ldpc_codeblock_length(p->base_graph, p->lifting_size);
     MS            = std::max(MS, static_cast<uint32_t>(align_up((p->segment_length + 7) / 8, 64)));
     CS            = std::max(CS, static_cast<uint32_t>(align_up((N + 7) / 8, 64)));
@@ -231,6 +238,9 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   std::vector<rm_geometry>                                                       geos;
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> geo_of;
   std::vector<tb_desc>                                                           tds(U);
+  std::vector<uint8_t>                                                           enc_rows(R * LDPC_ENCODE_ROW_BYTES);
+  // encoder row descriptors per (BG, Z, window): built once (a lifted graph each), copied to every row
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::pair<std::vector<uint8_t>, uint32_t>> enc_desc;
   std::vector<uint32_t>                                                          segE, segOff;
   uint32_t                                                                       row = 0;
   for (bucket& b : buckets) {
@@ -254,6 +264,17 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
         row_out[row] = static_cast<uint32_t>(ues[u].cw_offset * 8) + segOff[r];
         row_geo[row] = git->second;
         row_tb[row]  = u;
+        if (b.mixed) {
+          const auto dkey = std::make_tuple(p->base_graph, p->lifting_size, ue_window[u]);
+          auto       dit  = enc_desc.find(dkey);
+          if (dit == enc_desc.end()) {
+            std::vector<uint8_t> d(LDPC_ENCODE_ROW_BYTES);
+            const uint32_t       m = ldpc_encode_mixed_row(d.data(), p->base_graph, p->lifting_size, ue_window[u]);
+            dit                    = enc_desc.emplace(dkey, std::make_pair(std::move(d), m)).first;
+          }
+          std::memcpy(&enc_rows[row * LDPC_ENCODE_ROW_BYTES], dit->second.first.data(), LDPC_ENCODE_ROW_BYTES);
+          b.max_rows_eff = std::max(b.max_rows_eff, dit->second.second);
+        }
       }
     }
   }
@@ -263,7 +284,8 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   const size_t o_tb  = o_geo + align_up(sizeof(uint32_t) * R, 16);
   const size_t o_G   = o_tb + align_up(sizeof(uint32_t) * R, 16);
   const size_t o_TD  = o_G + align_up(sizeof(rm_geometry) * geos.size(), 16);
-  const size_t total = o_TD + sizeof(tb_desc) * U;
+  const size_t o_ER  = o_TD + align_up(sizeof(tb_desc) * U, 16);
+  const size_t total = o_ER + enc_rows.size();
 
   hipError_t he = hipSetDevice(e->device);
   // the pinned staging buffer is rewritten only once its previous upload completed
@@ -304,6 +326,7 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   std::memcpy(h + o_tb, row_tb.data(), sizeof(uint32_t) * R);
   std::memcpy(h + o_G, geos.data(), sizeof(rm_geometry) * geos.size());
   std::memcpy(h + o_TD, tds.data(), sizeof(tb_desc) * U);
+  std::memcpy(h + o_ER, enc_rows.data(), enc_rows.size());
   auto* dd = e->slot_desc.as<uint8_t>();
   he       = e->order.begin(stream);
   if (he == hipSuccess) {
@@ -344,11 +367,22 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
     return hip_fail(he, "PDSCH slot encoder stream fan-out");
   }
   for (size_t bi = 0; bi < buckets.size(); ++bi) {
-    const bucket&               b = buckets[bi];
+    const bucket&     b  = buckets[bi];
+    const hipStream_t bs = e->fan.stream(stream, static_cast<int>(bi));
+    if (b.mixed) {
+      int rc = ldpc_encode_mixed(e->enc, b.bg, b.Z, b.max_rows_eff,
+                                 e->msgs.as<uint8_t>() + static_cast<size_t>(b.row0) * MS, MS,
+                                 e->coded.as<uint8_t>() + static_cast<size_t>(b.row0) * CS, CS, b.rows, bs,
+                                 dd + o_ER + LDPC_ENCODE_ROW_BYTES * b.row0);
+      if (rc != SRS_AMD_OK) {
+        return rc;
+      }
+      continue;
+    }
     srs_amd_ldpc_encoder_config ec{b.bg, b.Z, 0};
     int rc = ldpc_encode_batch_ex(e->enc, &ec, e->msgs.as<uint8_t>() + static_cast<size_t>(b.row0) * MS, MS,
-                                  e->coded.as<uint8_t>() + static_cast<size_t>(b.row0) * CS, CS, b.rows,
-                                  e->fan.stream(stream, static_cast<int>(bi)), b.max_bits);
+                                  e->coded.as<uint8_t>() + static_cast<size_t>(b.row0) * CS, CS, b.rows, bs,
+                                  b.max_bits);
     if (rc != SRS_AMD_OK) {
       return rc;
     }

@@ -52,6 +52,24 @@ class PdschUe(ctypes.Structure):
     _fields_ = [("plan", SchPlan), ("tb_offset", ctypes.c_uint64), ("cw_offset", ctypes.c_uint64)]
 
 
+class SlotUes:
+    """The C descriptor array of a slot's UEs (PdschUe / PuschUe), built once and reusable across calls:
+    ues is a list of (plan, first offset, second offset) as the slot entry points take them."""
+
+    def __init__(self, kind, ues):
+        self.n = len(ues)
+        self.arr = (kind * max(self.n, 1))()
+        self.data_end = self.out_end = 0
+        for i, (plan, o1, o2) in enumerate(ues):
+            self.arr[i] = kind(plan, int(o1), int(o2))
+            if kind is PdschUe:  # (plan, tb_offset, cw_offset)
+                self.data_end = max(self.data_end, int(o1) + plan.tbs // 8)
+                self.out_end = max(self.out_end, int(o2) + (plan.cw_length + 7) // 8)
+            else:  # (plan, llr_offset, tb_offset)
+                self.data_end = max(self.data_end, int(o1) + plan.cw_length)
+                self.out_end = max(self.out_end, int(o2) + plan.tbs // 8)
+
+
 class PuschUe(ctypes.Structure):
     """``srs_amd_pusch_ue``: one UE's transport block of a heterogeneous slot batch (its PUSCH PDU,
     pusch_processor_impl.cpp:343)."""
@@ -200,19 +218,16 @@ def _encode_slot(self, tbs, ues, out=None, stream=None):
 
     if tbs.dim() != 1 or tbs.dtype != torch.uint8 or not tbs.is_contiguous():
         raise ValueError("tbs must be a contiguous uint8 1-D tensor")
-    n = len(ues)
-    arr = (PdschUe * max(n, 1))()
-    cw_end = 0
-    for i, (plan, to, co) in enumerate(ues):
-        if to + plan.tbs // 8 > tbs.numel():
-            raise ValueError("UE %d transport block beyond the TB tensor" % i)
-        arr[i] = PdschUe(plan, int(to), int(co))
-        cw_end = max(cw_end, int(co) + (plan.cw_length + 7) // 8)
+    arr = ues if isinstance(ues, SlotUes) else SlotUes(PdschUe, ues)
+    n = arr.n
+    if arr.data_end > tbs.numel():
+        raise ValueError("a transport block lies beyond the TB tensor")
+    cw_end = arr.out_end
     if out is None:
         out = torch.zeros(cw_end, dtype=torch.uint8, device=tbs.device)
     elif out.numel() < cw_end:
         raise ValueError("codeword tensor too small")
-    _lib.check(self._lib.srs_amd_pdsch_encode_slot(self._h, arr, n, tbs.data_ptr(), out.data_ptr(),
+    _lib.check(self._lib.srs_amd_pdsch_encode_slot(self._h, arr.arr, n, tbs.data_ptr(), out.data_ptr(),
                                                    _stream(stream, tbs)), "pdsch encode_slot")
     return out
 
@@ -285,21 +300,18 @@ class PuschDecoder:
 
         if llrs.dim() != 1 or llrs.dtype != torch.int8 or not llrs.is_contiguous():
             raise ValueError("llrs must be a contiguous int8 1-D tensor")
-        n = len(ues)
-        arr = (PuschUe * max(n, 1))()
-        tb_end = 0
-        for i, (plan, lo, to) in enumerate(ues):
-            if lo + plan.cw_length > llrs.numel():
-                raise ValueError("UE %d codeword beyond the LLR tensor" % i)
-            arr[i] = PuschUe(plan, int(lo), int(to))
-            tb_end = max(tb_end, int(to) + plan.tbs // 8)
+        arr = ues if isinstance(ues, SlotUes) else SlotUes(PuschUe, ues)
+        n = arr.n
+        if arr.data_end > llrs.numel():
+            raise ValueError("a codeword lies beyond the LLR tensor")
+        tb_end = arr.out_end
         dev = llrs.device
         if tbs is None:
             tbs = torch.zeros(tb_end, dtype=torch.uint8, device=dev)
         elif tbs.numel() < tb_end:
             raise ValueError("TB tensor too small")
         res = torch.empty((n, RESULT_WORDS), dtype=torch.int32, device=dev)
-        _lib.check(self._lib.srs_amd_pusch_decode_slot(self._h, ctypes.byref(cfg), arr, n, llrs.data_ptr(),
+        _lib.check(self._lib.srs_amd_pusch_decode_slot(self._h, ctypes.byref(cfg), arr.arr, n, llrs.data_ptr(),
                                                        tbs.data_ptr(), res.data_ptr(), _stream(stream, llrs)),
                    "pusch decode_slot")
         return tbs, res
