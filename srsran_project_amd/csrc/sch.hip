@@ -12,6 +12,11 @@
 //                    they are produced, 2 KiB of a TB per workgroup (linear
 //                    CRC, crc_device.h, partials XOR-ed with atomics);
 //   asm_final_kernel the TB CRC verdict and the HARQ flag reset.
+// Heterogeneous slots (srs_amd_pdsch_encode_slot / srs_amd_pusch_decode_slot) read per-TB descriptors
+// (tb_desc): the assembly kernels above through view_of(), and the TX kernels
+//   tx_tb_crc_kernel  TB CRC16 / CRC24A per TB, 8 KiB of a TB per workgroup, partials XOR-ed per TB;
+//   tx_segment_kernel segmentation with per-TB geometry, one thread per message byte;
+//   tx_cb_crc_kernel  CRC24B attachment of the codeblocks of segmented TBs, one wave per codeblock.
 // Both are byte-gather kernels far below any roofline next to the LDPC
 // kernels they sit between (a few hundred KB per slot).
 #include <hip/hip_runtime.h>
