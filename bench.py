@@ -18,6 +18,10 @@ batch of slots of the 100 MHz numerology-1 carrier (273 PRB, 4096-point DFT,
 normal CP): 4 antenna ports x `--slots` slots, cbf16 resource grids to complex
 float baseband and back (ofdm_slot_modulator / ofdm_slot_demodulator).
 
+`--workload sch_slot` (heterogeneous slots, not a BASELINE.json config): one step PDSCH-encodes and
+PUSCH-decodes the transport blocks of `--slots-pipeline` cells x `--ues-per-cell` UEs with different PRB
+shares, MCS and layer counts through the slot-level entry points -- see bench_slot.py.
+
 Inputs are resident in HBM before the timed region.  Multi-GPU: `--gpus N`
 starts N ranks itself (one process per GPU, before any GPU call), or runs under
 torch.distributed.run; cells / codeblocks / slots are independent, so every
