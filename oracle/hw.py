@@ -23,6 +23,8 @@ def lib():
         L.srs_ref_hw_ctx_create.restype = P
         L.srs_ref_hw_ctx_create.argtypes = [i, i]
         L.srs_ref_hw_ctx_destroy.argtypes = [P]
+        L.srs_ref_hw_ctx_sibling.restype = P
+        L.srs_ref_hw_ctx_sibling.argtypes = [P, i]
         L.srs_ref_hw_rx_buffer_create.restype = P
         L.srs_ref_hw_rx_buffer_create.argtypes = [u, u]
         L.srs_ref_hw_rx_buffer_destroy.argtypes = [P]
@@ -35,8 +37,12 @@ def lib():
 class HwPuschDecoder:
     """pusch_decoder_hw_impl + the MI355X hal::hw_accelerator_pusch_dec (external HARQ in HBM)."""
 
-    def __init__(self, device=0, generic=False):
-        self.h = lib().srs_ref_hw_ctx_create(int(device), int(generic))
+    def __init__(self, device=0, generic=False, sibling_of=None):
+        if sibling_of is not None:  # another accelerator of the same factory (shared HBM HARQ pool)
+            self.h = lib().srs_ref_hw_ctx_sibling(sibling_of.h, int(generic))
+            self._base = sibling_of  # keeps the factory's owner alive
+        else:
+            self.h = lib().srs_ref_hw_ctx_create(int(device), int(generic))
 
     def close(self):
         if getattr(self, "h", None):

@@ -109,6 +109,25 @@ void* srs_ref_hw_ctx_create(int device, int generic)
   return ctx;
 }
 
+/* A second pusch_decoder_hw_impl whose accelerator comes from the SAME factory as ctx's (one shared HBM
+ * HARQ pool), for concurrent transport blocks on two threads. */
+void* srs_ref_hw_ctx_sibling(void* base, int generic)
+{
+  auto* b   = static_cast<hw_context*>(base);
+  auto* ctx = new hw_context();
+  ctx->factory = b->factory;
+  std::vector<std::unique_ptr<hal::hw_accelerator_pusch_dec>> hw(1);
+  hw[0]     = ctx->factory->create();
+  auto pool = std::make_shared<pusch_decoder_hw_impl::hw_decoder_pool>(hw);
+  const auto   choice = generic ? srs_ref::impl::generic : srs_ref::impl::automatic;
+  pusch_decoder_hw_impl::sch_crc crcs;
+  crcs.crc16   = srs_ref::make_crc(crc_generator_poly::CRC16, choice);
+  crcs.crc24A  = srs_ref::make_crc(crc_generator_poly::CRC24A, choice);
+  crcs.crc24B  = srs_ref::make_crc(crc_generator_poly::CRC24B, choice);
+  ctx->decoder = std::make_unique<pusch_decoder_hw_impl>(std::make_unique<ldpc_segmenter_rx_impl>(), crcs, pool, nullptr);
+  return ctx;
+}
+
 void srs_ref_hw_ctx_destroy(void* ctx)
 {
   delete static_cast<hw_context*>(ctx);

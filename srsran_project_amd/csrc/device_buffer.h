@@ -133,6 +133,32 @@ struct stream_fan {
   }
 };
 
+// Closes a call begun with stream_order::begin on every exit path, errors included: a pending fan-out is
+// joined back into the caller's stream and the completion event recorded, so an early return never leaves
+// helper streams forked (still using the scratch) while the next call waits on a stale event.
+struct call_scope {
+  stream_order& order;
+  stream_fan*   fan;
+  hipStream_t   s;
+  bool          open = true;
+  call_scope(stream_order& o, stream_fan* f, hipStream_t st) : order(o), fan(f), s(st) {}
+  call_scope(const call_scope&)            = delete;
+  call_scope& operator=(const call_scope&) = delete;
+  hipError_t close()
+  {
+    open               = false;
+    const hipError_t e = fan != nullptr ? fan->end(s) : hipSuccess;
+    const hipError_t o = order.end(s);
+    return e != hipSuccess ? e : o;
+  }
+  ~call_scope()
+  {
+    if (open) {
+      (void)close();
+    }
+  }
+};
+
 inline size_t align_up(size_t n, size_t a)
 {
   return (n + a - 1) / a * a;

@@ -752,7 +752,6 @@ typedef short pk16 __attribute__((ext_vector_type(2)));
 
 constexpr int HR_Z       = 384;
 constexpr int HR_HALF    = HR_Z / 2; // lanes per codeblock
-constexpr int HR_THREADS = HR_HALF;
 
 __device__ __forceinline__ pk16 pk_splat(int v)
 {
@@ -951,8 +950,14 @@ __device__ __forceinline__ void hr_layers(lds_i8* lds, MSGS& c2v, uint32_t t, in
     if (L < 4 || L < nof_layers) {
       asm volatile("" : "+v"(t));
       hr_layer<L, ARITH, NP>(lds, c2v, t, std::make_integer_sequence<int, bg_traits<1>::deg(L)>{});
-      // one wave per codeblock (NP = 3): the wave's LDS accesses are processed in order, no barrier
-      __syncthreads();
+      if constexpr (NP == 1) {
+        __syncthreads();
+      } else {
+        // one wave per codeblock: the wave's LDS instructions execute in issue order, so the next layer's
+        // gathers see this layer's scatters of every lane; only the compiler must not move LDS accesses
+        // across the layer boundary (it cannot see the cross-lane dependencies)
+        asm volatile("" ::: "memory");
+      }
     }
     hr_layers<L + 1, MAXL, ARITH, NP>(lds, c2v, t, nof_layers);
   }
@@ -995,12 +1000,15 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
 
     // ---- input scan (last non-zero LLR, ldpc_decoder_impl.cpp:86) fused with the soft-bit load
     // (:160): clamped full nodes, the partial tail node unclamped, zeros elsewhere.
-    if (t == 0) {
-      red[0] = -1;
-      red[1] = 0;
-      red[2] = 0;
+    if constexpr (NT > 64) {
+      if (t == 0) {
+        red[0] = -1;
+        red[1] = 0;
+        red[2] = 0;
+      }
+      __syncthreads();
     }
-    __syncthreads();
+    int input_size;
     {
       const int      nw  = n_llrs >> 2;
       const int      B4  = (n_llrs / Z) * Z >> 2;
@@ -1043,12 +1051,16 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
       for (int w = t; w < 2 * Z / 4; w += NT) {
         soft4[w] = 0;
       }
-      if (last >= 0) {
-        __hip_atomic_fetch_max(&red[0], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if constexpr (NT == 64) {
+        input_size = __builtin_amdgcn_readfirstlane(wave_max(last) + 1);
+      } else {
+        if (last >= 0) {
+          __hip_atomic_fetch_max(&red[0], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        input_size = __builtin_amdgcn_readfirstlane(red[0] + 1);
       }
     }
-    __syncthreads();
-    const int input_size = __builtin_amdgcn_readfirstlane(red[0] + 1);
 
     if (input_size < K && a.force_decoding) {
       // ldpc_decoder_impl.cpp:92 (see ldpc_decode_kernel)
@@ -1058,7 +1070,9 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
       if (t == 0) {
         a.nof_iters[cb] = -1;
       }
-      __syncthreads();
+      if constexpr (NT > 64) {
+        __syncthreads();
+      }
       continue;
     }
     const int cb_len     = max(input_size + 2 * Z, K + 4 * Z);
@@ -1099,6 +1113,16 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
               crc ^= rr[b];
             }
           }
+        }
+        if constexpr (NT == 64) {
+          // one wave: shuffle reductions, no LDS round trip and no barrier
+          const uint32_t c_all = __builtin_amdgcn_readfirstlane(wave_xor(crc));
+          const uint32_t z_all = __builtin_amdgcn_readfirstlane(wave_or(zero));
+          if (z_all == 0 && c_all == 0) {
+            result = it + 1;
+            break;
+          }
+          continue;
         }
         lds_u32* acc = reinterpret_cast<lds_u32*>(&red[1 + 2 * (it & 1)]);
         if (crc != 0) {
@@ -1156,7 +1180,11 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
     if (te == 0) {
       a.nof_iters[cb] = result;
     }
-    __syncthreads();
+    if constexpr (NT > 64) {
+      __syncthreads();
+    } else {
+      asm volatile("" ::: "memory"); // the next codeblock's soft-bit stores follow this one's reads
+    }
   }
 }
 

@@ -107,6 +107,7 @@ int encode_locked(srs_amd_pdsch_encoder* e,
     return hip_fail(he, "PDSCH encoder scratch");
   }
   // Rate-matching lengths and codeword offsets, uploaded when the geometry changes.
+  call_scope scope(e->order, nullptr, stream);
   he = e->order.begin(stream);
   if (he == hipSuccess) {
     he = launch_rm_arrays(e->rm_arrays.as<uint32_t>(), nof_tbs, C, p->nof_short_segments, p->rm_length_short,
@@ -169,7 +170,7 @@ int encode_locked(srs_amd_pdsch_encoder* e,
   if (rc != SRS_AMD_OK) {
     return rc;
   }
-  he = e->order.end(stream);
+  he = scope.close();
   return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "PDSCH encoder completion event");
 }
 
@@ -231,8 +232,8 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
     max_tb_bytes  = std::max(max_tb_bytes, p->tbs / 8);
     max_msg_bytes = std::max(max_msg_bytes, (p->segment_length + 7) / 8);
   }
-  if (R > 65535) {
-    return fail(SRS_AMD_EINVAL, "%u codeblocks exceed the 65535 of one slot batch", R);
+  if (U > 65535 || R > 65535) {
+    return fail(SRS_AMD_EINVAL, "%u UEs / %u codeblocks exceed the 65535 of one slot batch", U, R);
   }
   std::vector<uint32_t>                                                          row_E(R), row_out(R), row_geo(R), row_tb(R);
   std::vector<rm_geometry>                                                       geos;
@@ -327,8 +328,9 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   std::memcpy(h + o_G, geos.data(), sizeof(rm_geometry) * geos.size());
   std::memcpy(h + o_TD, tds.data(), sizeof(tb_desc) * U);
   std::memcpy(h + o_ER, enc_rows.data(), enc_rows.size());
-  auto* dd = e->slot_desc.as<uint8_t>();
-  he       = e->order.begin(stream);
+  auto*      dd = e->slot_desc.as<uint8_t>();
+  call_scope scope(e->order, &e->fan, stream);
+  he = e->order.begin(stream);
   if (he == hipSuccess) {
     he = hipMemcpyAsync(dd, h, total, hipMemcpyHostToDevice, stream);
   }
@@ -398,7 +400,7 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   if (rc != SRS_AMD_OK) {
     return rc;
   }
-  he = e->order.end(stream);
+  he = scope.close();
   return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "PDSCH encoder completion event");
 }
 

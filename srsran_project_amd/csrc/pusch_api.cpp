@@ -167,6 +167,7 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH decoder scratch");
   }
+  call_scope scope(d->order, nullptr, stream);
   he = d->order.begin(stream);
   if (he == hipSuccess) {
     he = launch_rm_arrays(d->arrays.as<uint32_t>(), nof_tbs, C, p->nof_short_segments, p->rm_length_short,
@@ -236,7 +237,7 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   a.new_data       = cfg->new_data ? 1 : 0;
   he               = launch_assemble(a, nof_tbs, stream);
   if (he == hipSuccess) {
-    he = d->order.end(stream);
+    he = scope.close();
   }
   return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "assemble_kernel launch");
 }
@@ -305,6 +306,10 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     R          += p->nof_segments;
     max_tb_bits = std::max(max_tb_bits, p->tbs);
   }
+  // the TB assembly runs one grid row per UE, the codeblock kernels one grid row per codeblock
+  if (U > 65535 || R > 65535) {
+    return fail(SRS_AMD_EINVAL, "%u UEs / %u codeblocks exceed the 65535 of one slot batch", U, R);
+  }
   // host descriptors: per row E, input offset, geometry, filler bits; geometries + write ends; per-TB
   std::vector<uint32_t>                                                              row_E(R), row_in(R), row_geo(R);
   std::vector<uint32_t>                                                              row_len(R);
@@ -312,7 +317,7 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   std::vector<ldpc_row_desc>                                                         row_desc(R);
   std::vector<rm_geometry>                                                           geos;
   std::vector<uint32_t>                                                              geo_end;
-  std::map<std::tuple<size_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> geo_of;
+  std::map<std::tuple<size_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> geo_of;
   std::vector<tb_desc>                                                               tds(U);
   std::vector<uint32_t>                                                              segE, segOff;
   uint32_t                                                                           row = 0;
@@ -324,7 +329,9 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
       // dematcher write end: the longest prefix of a uniform bucket (its decoder reads that many LLRs of
       // every row), each UE's own prefix in a mixed bucket (per-row input lengths)
       const uint32_t wend = b.mixed ? ue_prefix[u] : b.prefix;
-      const auto     gkey = std::make_tuple(bi, p->rv, p->modulation_order, p->Nref, p->nof_filler_bits, wend);
+      // (a mixed-Z bucket holds several lifting sizes whose write ends can coincide: Z is part of the key)
+      const auto     gkey = std::make_tuple(bi, p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                                            p->nof_filler_bits, wend);
       auto       git  = geo_of.find(gkey);
       if (git == geo_of.end()) {
         rm_geometry g{};
@@ -409,8 +416,9 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   std::memcpy(h + o_TD, tds.data(), sizeof(tb_desc) * U);
   std::memcpy(h + o_LEN, row_len.data(), sizeof(uint32_t) * R);
   std::memcpy(h + o_RD, row_desc.data(), sizeof(ldpc_row_desc) * R);
-  auto* dd = d->slot_desc.as<uint8_t>();
-  he       = d->order.begin(stream);
+  auto*      dd = d->slot_desc.as<uint8_t>();
+  call_scope scope(d->order, &d->fan, stream);
+  he = d->order.begin(stream);
   if (he == hipSuccess) {
     he = hipMemcpyAsync(dd, h, total, hipMemcpyHostToDevice, stream);
   }
@@ -511,7 +519,7 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   a.max_tb_bits    = max_tb_bits;
   he               = launch_assemble(a, U, stream);
   if (he == hipSuccess) {
-    he = d->order.end(stream);
+    he = scope.close();
   }
   return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "assemble_kernel launch");
 }

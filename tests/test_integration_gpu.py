@@ -21,6 +21,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def hw():
+    import torch
+
+    torch.cuda.init()  # torch's HIP runtime first, whatever test file ran before
     from oracle import hw as ohw
 
     return ohw, ohw.HwPuschDecoder(0)
@@ -89,3 +92,66 @@ def test_hw_plugin_no_early_stop(hw):
     want = oracle.ref_pusch_decode(llr, p, oracle.RefRxBuffer(p["nof_segments"]), want_tb, use_early_stop=False)
     assert got == want
     np.testing.assert_array_equal(got_tb, want_tb)
+
+
+def test_hw_plugin_concurrent_instances(hw):
+    """Two accelerator instances of ONE factory (one shared HBM HARQ pool) decode transport blocks on two
+    threads at once, as the reference's decoder pool does (pusch_decoder_hw_impl::hw_decoder_pool): rows are
+    reserved per transport block under the pool's lock, so neither thread takes the other's rows."""
+    import threading
+
+    ohw, dec = hw
+    dec2 = ohw.HwPuschDecoder(0, sibling_of=dec)
+    case = (8 * 6000, 1, 6, 2, 9000, 0, 0)
+    p = _plan(case)
+    C = p["nof_segments"]
+    assert C > 1
+    jobs = []
+    for k in range(12):
+        tb = tb_bytes(case[0], 300 + k)
+        llr = noisy_llrs(osch.pdsch_encode(tb, p), 8, 3.0 if k % 3 else 9.0, seed=500 + k)
+        want_tb = np.zeros(case[0] // 8, np.uint8)
+        want = oracle.ref_pusch_decode(llr, p, oracle.RefRxBuffer(C), want_tb)
+        jobs.append((llr, want, want_tb))
+    results = [None] * len(jobs)
+
+    def worker(d, idx):
+        for k in idx:
+            got_tb = np.zeros(case[0] // 8, np.uint8)
+            got = ohw.hw_pusch_decode(d, jobs[k][0], p, ohw.HwRxBuffer(C, 200000 + 64 * k), got_tb)
+            results[k] = (got, got_tb)
+
+    th = [threading.Thread(target=worker, args=(d, range(i, len(jobs), 2))) for i, d in enumerate((dec, dec2))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for k, (llr, want, want_tb) in enumerate(jobs):
+        got, got_tb = results[k]
+        assert got == want, (k, got, want)
+        np.testing.assert_array_equal(got_tb, want_tb)
+    dec2.close()
+
+
+def test_hw_plugin_abandoned_harq_process(hw):
+    """A HARQ process that never passed its CRC keeps its rows (the reference frees them only on a TB CRC pass);
+    its absolute codeblock ids are then reused by a new transport block with MORE codeblocks (new data): the
+    plug-in remaps the stale ids instead of failing, and still equals pusch_decoder_impl."""
+    ohw, dec = hw
+    small = (8 * 3000, 1, 4, 1, 8000, 0, 0)
+    big = (8 * 9000, 1, 6, 2, 14000, 0, 0)
+    ps, pb = _plan(small), _plan(big)
+    assert pb["nof_segments"] > ps["nof_segments"] > 1
+    tb = tb_bytes(small[0], 11)
+    got_tb = np.zeros(small[0] // 8, np.uint8)
+    got = ohw.hw_pusch_decode(dec, noisy_llrs(osch.pdsch_encode(tb, ps), 8, 14.0, seed=1), ps,
+                              ohw.HwRxBuffer(ps["nof_segments"], 300001), got_tb)
+    assert not got[0]  # abandoned: rows stay mapped
+    tb = tb_bytes(big[0], 12)
+    llr = noisy_llrs(osch.pdsch_encode(tb, pb), 8, 2.0, seed=2)
+    got_tb = np.zeros(big[0] // 8, np.uint8)
+    want_tb = np.zeros(big[0] // 8, np.uint8)
+    got = ohw.hw_pusch_decode(dec, llr, pb, ohw.HwRxBuffer(pb["nof_segments"], 300000), got_tb)
+    want = oracle.ref_pusch_decode(llr, pb, oracle.RefRxBuffer(pb["nof_segments"]), want_tb)
+    assert got == want and got[0]
+    np.testing.assert_array_equal(got_tb, tb)

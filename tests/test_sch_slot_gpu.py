@@ -19,6 +19,11 @@ SLOT_CASES = SCH_CASES + [
     (8 * 9000, 1, 6, 2, 12960, 0, 0),      # 64QAM high rate, C = 9
     (8 * 30000, 1, 8, 4, 32256, 0, 0),     # 256QAM 4 layers, C = 29
     (8 * 6000, 1, 4, 1, 13000, 2, 0),      # rv 2 new data (k0 != 0: whole soft row)
+    # one mixed-Z bucket, same rv / Qm / Nref / F = 0, equal dematcher write ends: Z = 32 with E > Ncb
+    # (whole row, 66 x 32 = 2112) and Z = 64 whose bounded prefix is also 2112 = 33 x 64 -- their
+    # rate-matching geometries must stay apart
+    (688, 1, 2, 1, 1100, 0, 0),
+    (1392, 1, 2, 1, 1025, 0, 0),
 ]
 
 
