@@ -78,6 +78,9 @@ def parse():
                    help="pipeline: also report a line at this SNR, near the 256QAM R=0.93 decoding threshold where "
                         "the decoder runs ~4 iterations per codeblock (default per PUSCH layers, from "
                         "tools/snr_sweep.py: 31.0 dB for 4 layers, 23.8 dB for 2; < 0 disables)")
+    p.add_argument("--mimo", default="4x4", choices=["4x4", "2x2"],
+                   help="pipeline: 4x4 (headline: PDSCH 4 layers x 4 ports, PUSCH --ul-layers x 4 rx) or 2x2 "
+                        "(configs[3]: PDSCH 2 layers x 2 ports, PUSCH 2 layers x 2 rx, reference-pinned ZF)")
     p.add_argument("--ul-layers", type=int, default=4, choices=[1, 2, 3, 4],
                    help="pipeline: PUSCH layers (4: MMSE 4x4, parity unpinned; 2: the reference-pinned ZF 2x4)")
     p.add_argument("--ingest", action="store_true",

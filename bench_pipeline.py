@@ -39,7 +39,7 @@ UL_START, UL_NSYM = 0, 14
 RNTI, N_ID, SLOT = 0x4601, 500, 0
 SNR_DB = 35.0
 # near the decoding threshold (tools/snr_sweep.py, mean LDPC iterations ~4): per PUSCH layer count
-LOW_SNR_DB = {2: 23.8, 4: 32.0}
+LOW_SNR_DB = {(2, 4): 23.8, (4, 4): 32.0}  # (PUSCH layers, rx ports)
 LDPC_ITERS = 6
 # DM-RS amplitude relative to data: convert_dB_to_amplitude(-get_sch_to_dmrs_ratio_dB(2)) = 10^(3/20),
 # evaluated in float as the reference (sch_dmrs_power.h, math_utils.h:118)
@@ -53,18 +53,33 @@ def base_graph(tbs, r):
     return 1
 
 
-def dl_weights():
-    k = np.arange(DL_PORTS)
-    return (np.exp(-2j * np.pi * np.outer(np.arange(DL_LAYERS), k) / DL_PORTS) / 2.0).astype(np.complex64)
+# MIMO shapes of the pipeline: "4x4" (the BASELINE.json headline: PDSCH 4 layers x 4 ports, PUSCH 4 layers x 4 rx
+# ports) and "2x2" (configs[3]: PDSCH 2 layers x 2 ports, PUSCH 2 layers x 2 rx ports)
+MIMO = {"4x4": (4, 4, 4, 4), "2x2": (2, 2, 2, 2)}  # dl layers, dl ports, ul layers, ul rx ports
 
 
-def ul_channel(layers):
+def shape_kw(args):
+    """Pipeline keyword arguments of bench.py's --mimo / --ul-layers."""
+    dl_l, dl_p, ul_l, ul_p = MIMO[getattr(args, "mimo", "4x4")]
+    if getattr(args, "mimo", "4x4") == "4x4":
+        ul_l = args.ul_layers
+    return dict(dl_layers=dl_l, dl_ports=dl_p, ul_layers=ul_l, ul_ports=ul_p)
+
+
+def dl_weights(layers=DL_LAYERS, ports=DL_PORTS):
+    """[layer][port] DFT precoder, unit power per layer."""
+    k = np.arange(ports)
+    return (np.exp(-2j * np.pi * np.outer(np.arange(layers), k) / ports) /
+            np.sqrt(np.float32(ports))).astype(np.complex64)
+
+
+def ul_channel(layers, ports=UL_PORTS):
     """[layer][rx port]: the MIMO channel the UE transmission goes through."""
     h = np.array([[1.0, 0.2j, 0.7 + 0.1j, 0.3],
                   [0.1, 0.9, -0.2j, 0.8 - 0.2j],
                   [0.3j, -0.2, 0.9, 0.1 + 0.2j],
                   [0.2, 0.1 - 0.3j, 0.2, 0.9]], np.complex64)
-    return h[:layers] * np.float32(0.8)
+    return h[:layers, :ports] * np.float32(0.8)
 
 
 def ul_tbs(amd, layers):
@@ -72,37 +87,39 @@ def ul_tbs(amd, layers):
     return amd.tbs_calculator_calculate(UL_NSYM, ndmrs, 0, QM, RATE, layers, 0, NPRB)
 
 
-def ul_pdu(amd, layers, tbs):
+def ul_pdu(amd, layers, tbs, ports=UL_PORTS):
     return amd.make_pdu(numerology=MU, slot_index=SLOT, rnti=RNTI, bwp_start_rb=0, bwp_size_rb=NPRB, modulation=QM,
                         target_code_rate=RATE, rv=0, base_graph=base_graph(tbs, RATE / 1024), new_data=1, n_id=N_ID,
-                        nof_tx_layers=layers, nof_rx_ports=UL_PORTS, dmrs_symbol_mask=DMRS_MASK, scrambling_id=N_ID,
+                        nof_tx_layers=layers, nof_rx_ports=ports, dmrs_symbol_mask=DMRS_MASK, scrambling_id=N_ID,
                         n_scid=0, nof_cdm_groups_without_data=NCDM, rb_start=0, rb_count=NPRB,
                         start_symbol_index=UL_START, nof_symbols=UL_NSYM, tbs=tbs)
 
 
 class Pipeline:
     def __init__(self, slots, dev, iters=LDPC_ITERS, snr_db=SNR_DB, ul_layers=UL_LAYERS, seed=0, ul_equalizer=None,
-                 keep_estimates=False):
+                 keep_estimates=False, dl_layers=DL_LAYERS, dl_ports=DL_PORTS, ul_ports=UL_PORTS):
         import torch
 
         import srsran_project_amd as amd
 
         self.torch, self.dev, self.S = torch, dev, slots
         self.ul_layers, self.snr_db, self.iters = ul_layers, snr_db, iters
+        self.dl_layers, self.dl_ports, self.ul_ports = dl_layers, dl_ports, ul_ports
+        assert dl_layers <= dl_ports and ul_layers <= ul_ports
         # the reference-pinned ZF for two layers, MMSE (parity unpinned) for four unless asked otherwise
         self.ul_equalizer = ul_equalizer or ("zf" if ul_layers <= 2 else UL_EQ)
         self.ul_stream = None
         d = dev.index
         all_crbs = list(range(NPRB))
         # ---- plans -------------------------------------------------------------------------
-        self.tbs_dl = amd.tbs_calculator_calculate(DL_NSYM, 24, 0, QM, RATE, DL_LAYERS, 0, NPRB)
+        self.tbs_dl = amd.tbs_calculator_calculate(DL_NSYM, 24, 0, QM, RATE, dl_layers, 0, NPRB)
         self.tbs_ul = ul_tbs(amd, ul_layers)
         nre_dl = NPRB * 12 * (DL_NSYM - 2)
-        self.plan_dl = amd.sch_plan(self.tbs_dl, base_graph(self.tbs_dl, RATE / 1024), 0, QM, 0, DL_LAYERS,
-                                    nre_dl * DL_LAYERS)
+        self.plan_dl = amd.sch_plan(self.tbs_dl, base_graph(self.tbs_dl, RATE / 1024), 0, QM, 0, dl_layers,
+                                    nre_dl * dl_layers)
         self.enc = amd.PdschEncoder(device=d)
         self.mod = amd.PdschModulator(device=d)
-        wdl = dl_weights()
+        wdl = dl_weights(dl_layers, dl_ports)
         self.mod_plan_dl = self.mod.plan(amd.PdschModulatorConfig(
             rnti=RNTI, bwp_start=0, bwp_size=NPRB, modulation=QM, crbs=all_crbs, start_symbol=DL_START,
             nof_symbols=DL_NSYM, dmrs_symb_pos=DMRS_MASK, dmrs_type=1, nof_cdm_groups_without_data=NCDM, n_id=N_ID,
@@ -120,7 +137,7 @@ class Pipeline:
             dec_nof_iterations=iters, dec_enable_early_stop=True, fd_smoothing=2, td_interpolation=0,
             compensate_cfo=True, equalizer=int(getattr(amd.ChannelEqualizerAlgorithmType, self.ul_equalizer))),
             device=d)
-        self.pdu_ul = ul_pdu(amd, ul_layers, self.tbs_ul)
+        self.pdu_ul = ul_pdu(amd, ul_layers, self.tbs_ul, ul_ports)
         self.proc_plan = self.proc.plan(self.pdu_ul, NSUBC)
         self.plan_ul = self.proc_plan.sch  # the processor's UL-SCH plan (Nref from tbs_lbrm_default)
 
@@ -131,15 +148,15 @@ class Pipeline:
         self.tb_dl = torch.randint(0, 256, (S, self.tbs_dl // 8), device=dev, dtype=torch.uint8, generator=g)
         self.tb_ul = torch.randint(0, 256, (S, self.tbs_ul // 8), device=dev, dtype=torch.uint8, generator=g)
         self.cw_dl = torch.empty((S, (self.plan_dl.cw_length + 7) // 8), dtype=torch.uint8, device=dev)
-        self.grid_dl = torch.zeros((S, DL_PORTS, 14, NSUBC), dtype=torch.int32, device=dev)
+        self.grid_dl = torch.zeros((S, dl_ports, 14, NSUBC), dtype=torch.int32, device=dev)
         stride = self.ofdm_mod.max_slot_size()
-        self.samp_dl = torch.empty((S, DL_PORTS, stride), dtype=torch.complex64, device=dev)
-        self.grid_ul = torch.zeros((S, UL_PORTS, 14, NSUBC), dtype=torch.int32, device=dev)
+        self.samp_dl = torch.empty((S, dl_ports, stride), dtype=torch.complex64, device=dev)
+        self.grid_ul = torch.zeros((S, ul_ports, 14, NSUBC), dtype=torch.int32, device=dev)
         # keep_estimates: the processor also writes the expanded channel estimates (tests check them); without
         # it the equalizer rebuilds them per RE from the estimator's per-subcarrier output (no HBM tensor)
-        self.est_ul = (torch.zeros((S, UL_PORTS, ul_layers, 14, NSUBC), dtype=torch.int32, device=dev)
+        self.est_ul = (torch.zeros((S, ul_ports, ul_layers, 14, NSUBC), dtype=torch.int32, device=dev)
                        if keep_estimates else None)
-        self.stats_ul = torch.zeros((S, UL_PORTS, 6), dtype=torch.float32, device=dev)
+        self.stats_ul = torch.zeros((S, ul_ports, 6), dtype=torch.float32, device=dev)
         self.llr_ul = torch.empty((S, (self.plan_ul.cw_length + 63) // 64 * 64), dtype=torch.int8, device=dev)
         self.tb_rx = torch.zeros((S, self.tbs_ul // 8), dtype=torch.uint8, device=dev)
         self.res_ul = torch.zeros((S, amd.pusch_processor.RESULT_BYTES), dtype=torch.uint8, device=dev)
@@ -150,19 +167,19 @@ class Pipeline:
         modulation and type-1 DM-RS use the same TS 38.211 / 38.212 chains as the PDSCH TX kernels; DM-RS at the
         amplitude the processor's estimator expects (DMRS_AMP)."""
         torch, dev, S = self.torch, self.dev, self.S
-        h = ul_channel(self.ul_layers)
+        h = ul_channel(self.ul_layers, self.ul_ports)
         ue_mod_plan = self.mod.plan(amd.PdschModulatorConfig(
             rnti=RNTI, bwp_start=0, bwp_size=NPRB, modulation=QM, crbs=list(range(NPRB)), start_symbol=UL_START,
             nof_symbols=UL_NSYM, dmrs_symb_pos=DMRS_MASK, dmrs_type=1, nof_cdm_groups_without_data=NCDM, n_id=N_ID,
             precoding=h), NSUBC)
         assert ue_mod_plan.nof_bits == self.plan_ul.cw_length
         cw = self.enc.encode_batch(self.tb_ul, self.plan_ul)
-        grid = torch.zeros((S, UL_PORTS, 14, NSUBC), dtype=torch.int32, device=dev)
+        grid = torch.zeros((S, self.ul_ports, 14, NSUBC), dtype=torch.int32, device=dev)
         self.mod.modulate_batch(grid, cw, ue_mod_plan)
         self.mod.map_dmrs_batch(grid, amd.DmrsPdschConfig(
             slot_index=SLOT, reference_point_k_rb=0, type=1, scrambling_id=N_ID, n_scid=False, amplitude=DMRS_AMP,
             symbols_mask=DMRS_MASK, crbs=list(range(NPRB)), precoding=h))
-        samp = self.ofdm_mod.modulate_batch(grid.view(torch.int16).view(S, UL_PORTS, 14, 2 * NSUBC), SLOT)
+        samp = self.ofdm_mod.modulate_batch(grid.view(torch.int16).view(S, self.ul_ports, 14, 2 * NSUBC), SLOT)
         # AWGN at snr_db relative to the mean sample power
         p = float(torch.mean(torch.abs(samp) ** 2).item())
         sigma = np.sqrt(p / 10 ** (self.snr_db / 10) / 2)
@@ -178,13 +195,13 @@ class Pipeline:
         self.enc.encode_batch(self.tb_dl, self.plan_dl, out=self.cw_dl, stream=stream)
         self.mod.modulate_batch(self.grid_dl, self.cw_dl, self.mod_plan_dl, stream=stream)
         self.mod.map_dmrs_batch(self.grid_dl, self.dmrs_dl, stream=stream)
-        self.ofdm_mod.modulate_batch(self.grid_dl.view(t.int16).view(self.S, DL_PORTS, 14, 2 * NSUBC), SLOT,
+        self.ofdm_mod.modulate_batch(self.grid_dl.view(t.int16).view(self.S, self.dl_ports, 14, 2 * NSUBC), SLOT,
                                      out=self.samp_dl, stream=stream)
 
     def pusch(self, stream):
         t = self.torch
         self.ofdm_dem.demodulate_batch(self.samp_ul, SLOT,
-                                       grid=self.grid_ul.view(t.int16).view(self.S, UL_PORTS, 14, 2 * NSUBC),
+                                       grid=self.grid_ul.view(t.int16).view(self.S, self.ul_ports, 14, 2 * NSUBC),
                                        stream=stream)
         self.proc.process_batch(self.grid_ul, self.proc_plan, tbs=self.tb_rx, results=self.res_ul,
                                 port_stats=self.stats_ul, estimates=self.est_ul, llrs=self.llr_ul, stream=stream)
@@ -272,11 +289,11 @@ class Pipeline:
             ev[2].record(stream)
             self.mod.map_dmrs_batch(self.grid_dl, self.dmrs_dl, stream=stream)
             ev[3].record(stream)
-            self.ofdm_mod.modulate_batch(self.grid_dl.view(t.int16).view(self.S, DL_PORTS, 14, 2 * NSUBC), SLOT,
+            self.ofdm_mod.modulate_batch(self.grid_dl.view(t.int16).view(self.S, self.dl_ports, 14, 2 * NSUBC), SLOT,
                                          out=self.samp_dl, stream=stream)
             ev[4].record(stream)
             self.ofdm_dem.demodulate_batch(self.samp_ul, SLOT,
-                                           grid=self.grid_ul.view(t.int16).view(self.S, UL_PORTS, 14, 2 * NSUBC),
+                                           grid=self.grid_ul.view(t.int16).view(self.S, self.ul_ports, 14, 2 * NSUBC),
                                            stream=stream)
             ev[5].record(stream)
             self.proc.process_batch(self.grid_ul, self.proc_plan, tbs=self.tb_rx, results=self.res_ul,
@@ -292,19 +309,19 @@ def chain_config(pl, choice="auto"):
     from oracle import chain as oc
 
     return oc.make_config(numerology=MU, slot=SLOT, nof_prb=NPRB, dft_size=NFFT, rnti=RNTI, n_id=N_ID, qm=QM,
-                          dmrs_symbol_mask=DMRS_MASK, nof_cdm_groups_without_data=NCDM, dl_layers=DL_LAYERS,
-                          dl_ports=DL_PORTS, dl_start=DL_START, dl_nsym=DL_NSYM, dl_tbs=pl.tbs_dl,
-                          dl_bg=pl.plan_dl.base_graph, dl_weights=dl_weights(), dl_dmrs_amplitude=DMRS_AMP,
-                          ul_layers=pl.ul_layers, ul_ports=UL_PORTS, ul_start=UL_START, ul_nsym=UL_NSYM,
+                          dmrs_symbol_mask=DMRS_MASK, nof_cdm_groups_without_data=NCDM, dl_layers=pl.dl_layers,
+                          dl_ports=pl.dl_ports, dl_start=DL_START, dl_nsym=DL_NSYM, dl_tbs=pl.tbs_dl,
+                          dl_bg=pl.plan_dl.base_graph, dl_weights=dl_weights(pl.dl_layers, pl.dl_ports),
+                          dl_dmrs_amplitude=DMRS_AMP, ul_layers=pl.ul_layers, ul_ports=pl.ul_ports, ul_start=UL_START, ul_nsym=UL_NSYM,
                           ul_tbs=pl.tbs_ul, ul_bg=pl.plan_ul.base_graph, ul_iterations=pl.iters,
                           ul_target_code_rate=RATE, choice={"generic": 0, "avx2": 1, "auto": 2}[choice])
 
 
-def latency_ms(dev, cells, steps=10, warmup=3, ul_layers=UL_LAYERS):
+def latency_ms(dev, cells, steps=10, warmup=3, **shape):
     """Wall time of one step (both chains of `cells` cells) measured step by step (synchronized each step)."""
     import torch
 
-    pl = Pipeline(cells, dev, ul_layers=ul_layers)
+    pl = Pipeline(cells, dev, **shape)
     stream = torch.cuda.current_stream(dev)
     for _ in range(warmup):
         pl.step(stream)
@@ -324,7 +341,7 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
     from srsran_project_amd.cell_fanout import SlotFanout
 
     stream = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
-    pl = Pipeline(args.slots_pipeline, dev, snr_db=args.snr_db, ul_layers=args.ul_layers)
+    pl = Pipeline(args.slots_pipeline, dev, snr_db=args.snr_db, **shape_kw(args))
     S = pl.S
     ingest_ms = None
     if args.ingest and world > 1:
@@ -357,18 +374,18 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
     value = cbs / elapsed
     dec_ms, dec_bytes, dec_cbs, dec_its = pl.ldpc_decoder_ms(stream)
     # algorithmic HBM bytes of each stage per step (inputs read once, outputs written once)
-    samp_dl = S * DL_PORTS * pl.ofdm_mod.get_slot_size(SLOT) * 8
-    samp_ul = S * UL_PORTS * pl.ofdm_dem.get_slot_size(SLOT) * 8
+    samp_dl = S * pl.dl_ports * pl.ofdm_mod.get_slot_size(SLOT) * 8
+    samp_ul = S * pl.ul_ports * pl.ofdm_dem.get_slot_size(SLOT) * 8
     grid_b = lambda ports: S * ports * 14 * NSUBC * 4  # noqa: E731
     L = pl.ul_layers
     alg_bytes = {
         "pdsch_encode": S * (pl.tbs_dl // 8 + (pl.plan_dl.cw_length + 7) // 8),
-        "pdsch_modulate": S * ((pl.plan_dl.cw_length + 7) // 8) + grid_b(DL_PORTS) * 11 // 14,
-        "dmrs_pdsch": grid_b(DL_PORTS) * 2 // 14,
-        "ofdm_modulate": grid_b(DL_PORTS) + samp_dl,
-        "ofdm_demodulate": samp_ul + grid_b(UL_PORTS),
+        "pdsch_modulate": S * ((pl.plan_dl.cw_length + 7) // 8) + grid_b(pl.dl_ports) * 11 // 14,
+        "dmrs_pdsch": grid_b(pl.dl_ports) * 2 // 14,
+        "ofdm_modulate": grid_b(pl.dl_ports) + samp_dl,
+        "ofdm_demodulate": samp_ul + grid_b(pl.ul_ports),
         # estimator: DM-RS REs in, estimates out; demodulator: grid + estimates in, LLRs out; decoder: LLRs in, TB out
-        "pusch_process": (grid_b(UL_PORTS) * 2 // 14 + grid_b(UL_PORTS) * L) + (grid_b(UL_PORTS) * (1 + L)
+        "pusch_process": (grid_b(pl.ul_ports) * 2 // 14 + grid_b(pl.ul_ports) * L) + (grid_b(pl.ul_ports) * (1 + L)
                                                                               + S * pl.plan_ul.cw_length)
         + S * pl.plan_ul.cw_length + S * pl.tbs_ul // 8,
     }
@@ -381,17 +398,18 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         return None
     lat = None
     if world == 1 and not args.no_latency:
-        lat = {"1_cell": latency_ms(dev, 1, ul_layers=L), "8_cells": latency_ms(dev, 8, ul_layers=L)}
+        lat = {"1_cell": latency_ms(dev, 1, **shape_kw(args)), "8_cells": latency_ms(dev, 8, **shape_kw(args))}
     low = None
     if args.low_snr_db is None:
-        args.low_snr_db = LOW_SNR_DB.get(L, -1.0)
+        args.low_snr_db = LOW_SNR_DB.get((L, pl.ul_ports), -1.0)
     if world == 1 and args.low_snr_db >= 0:
         low = low_snr_line(args, dev, timed, dist)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = pipeline_cpu_baseline(args, pl)
     return {
-        "metric": "PDSCH+PUSCH codeblocks/s @ 100 MHz 273-PRB 4x4 MIMO (PDSCH 4 layers, PUSCH %d layers x 4 rx)" % L,
+        "metric": "PDSCH+PUSCH codeblocks/s @ 100 MHz 273-PRB %dx%d MIMO (PDSCH %d layers, PUSCH %d layers x %d rx)"
+                  % (pl.dl_ports, pl.ul_ports, pl.dl_layers, L, pl.ul_ports),
         "value": value,
         "unit": "codeblocks/s",
         "n_gpus": world,
@@ -408,8 +426,8 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
             "workload": "configs[3]/headline: full PDSCH+PUSCH slot pipeline, 100 MHz numerology-1 273 PRB, "
                         "256QAM R=948/1024",
             "cells_per_step_per_gpu": S,
-            "pdsch": {"layers": DL_LAYERS, "ports": DL_PORTS, "tbs": pl.tbs_dl, "codeblocks": cbs_dl},
-            "pusch": {"layers": L, "rx_ports": UL_PORTS, "tbs": pl.tbs_ul, "codeblocks": cbs_ul,
+            "pdsch": {"layers": pl.dl_layers, "ports": pl.dl_ports, "tbs": pl.tbs_dl, "codeblocks": cbs_dl},
+            "pusch": {"layers": L, "rx_ports": pl.ul_ports, "tbs": pl.tbs_ul, "codeblocks": cbs_ul,
                       "equalizer": pl.ul_equalizer,
                       "equalizer_parity": "pinned (reference ZF)" if (L <= 2 and pl.ul_equalizer == "zf") or L == 1
                       else "unpinned: the open reference asserts for this topology; fp64 solve within stated "
@@ -472,7 +490,7 @@ def low_snr_line(args, dev, timed, dist):
     iterations per codeblock (the headline runs at 35 dB, ~2 iterations)."""
     import torch
 
-    pl = Pipeline(args.slots_pipeline, dev, snr_db=args.low_snr_db, seed=1, ul_layers=args.ul_layers)
+    pl = Pipeline(args.slots_pipeline, dev, snr_db=args.low_snr_db, seed=1, **shape_kw(args))
     stream = torch.cuda.current_stream(dev)
     elapsed, _ = timed(args, dist, 1, dev, stream, lambda: pl.step(stream))
     ok, its = pl.check()
@@ -501,7 +519,8 @@ def pipeline_cpu_baseline(args, pl):
     # The open reference's PUSCH processor runs at most two layers (its equalizer asserts for 3 / 4,
     # channel_equalizer_generic_impl.cpp:197-247): for a 4-layer GPU line the CPU chain processes the same cell
     # with a 2-layer PUSCH (inputs from a 1-cell 2-layer pipeline); codeblocks/s is normalised per codeblock.
-    ref_pl = pl if pl.ul_layers <= 2 else Pipeline(1, pl.dev, snr_db=pl.snr_db, ul_layers=2)
+    ref_pl = pl if pl.ul_layers <= 2 else Pipeline(1, pl.dev, snr_db=pl.snr_db, ul_layers=2, dl_layers=pl.dl_layers,
+                                                   dl_ports=pl.dl_ports, ul_ports=pl.ul_ports)
     cfg = chain_config(ref_pl)
     tb = ref_pl.tb_dl[0].cpu().numpy()
     n = oc.slot_size(cfg)
@@ -517,8 +536,17 @@ def pipeline_cpu_baseline(args, pl):
     per_slot = w1 / n1
     nmt = max(2 * threads, int(args.cpu_seconds * threads / per_slot / 2))
     wm, stm, okm, itm = oc.many(cfg, tb, samp, nmt, threads)
-    return {"value": nmt * cbs / wm, "unit": "codeblocks/s", "cores": threads, "kind": "reference",
-            "host_logical_cpus": logical, "host_physical_cores": physical, "os_cpu_count": os.cpu_count(),
+    value = nmt * cbs / wm
+    return {"value": value, "unit": "codeblocks/s", "cores": threads, "kind": "reference",
+            "cores_used": threads, "host_logical_cpus": logical, "host_physical_cores": physical,
+            "os_cpu_count": os.cpu_count(),
+            "per_gpu_share_rationale": "%d threads = this process's CPU share on the GPU box (OMP_NUM_THREADS; the "
+                                       "harness gives each GPU of an 8-GPU node 1/8 of the host), i.e. the host cores "
+                                       "that stand beside ONE MI355X; the whole host is not this process's to use"
+                                       % threads,
+            "whole_host_extrapolated_value": value / threads * physical,
+            "whole_host_extrapolation": "measured %d-thread rate scaled linearly to all %d physical host cores (an "
+                                        "upper bound: no memory-bandwidth contention)" % (threads, physical),
             "single_thread_value": n1 * cbs / w1,
             "impl": opp.describe("auto") + ", precoder " + ("avx512" if "avx512" in opp.describe("auto") else "avx2")
                     + ", LDPC encoder avx2, DFT generic (FFTW absent)",
@@ -528,9 +556,10 @@ def pipeline_cpu_baseline(args, pl):
                       "dmrs_pdsch_processor_impl, ofdm_slot_modulator_impl / ofdm_slot_demodulator_impl, "
                       "pusch_processor_impl (dmrs_pusch_estimator_impl, pusch_demodulator_impl, "
                       "ulsch_demultiplex_impl, pusch_decoder_impl) with the \"auto\" factory implementations "
-                      "(%s); PUSCH TB CRC ok in %d of %d slots; per cell PDSCH 4 layers x 4 ports and PUSCH "
-                      "%d layers x 4 rx (%d codeblocks)%s"
-                      % (nmt, threads, wm, n1, w1, opp.describe("auto"), okm, nmt, ref_pl.ul_layers, cbs,
+                      "(%s); PUSCH TB CRC ok in %d of %d slots; per cell PDSCH %d layers x %d ports and PUSCH "
+                      "%d layers x %d rx (%d codeblocks)%s"
+                      % (nmt, threads, wm, n1, w1, opp.describe("auto"), okm, nmt, ref_pl.dl_layers, ref_pl.dl_ports,
+                         ref_pl.ul_layers, ref_pl.ul_ports, cbs,
                          "" if ref_pl is pl else "; the open reference cannot run the GPU line's %d-layer PUSCH "
                          "(its equalizer asserts), so its chain runs the 2-layer PUSCH of the same cell"
                          % pl.ul_layers),

@@ -871,9 +871,18 @@ __device__ __forceinline__ pk16 pk_scale(pk16 m)
 #ifndef HR_CHUNK2
 #define HR_CHUNK2 5
 #endif
+#ifndef HR_PIN_X
+#define HR_PIN_X 0
+#endif
 
 // One layer (base-graph row L, global edges E0 .. E0 + DEG - 1) for the NP row pairs of lane t:
 // rows t + k T and t + k T + 192, T = 192 / NP, k < NP (message of edge e, pair k: index e NP + k).
+//
+// Instruction scheduling (gfx950): a packed-math (VOP3P) result read by the very next VOP3P instruction costs a
+// hazard s_nop, and those nops took ~35 % of the issue slots of a dependent v_pk_* chain at 4 waves per SIMD
+// (scratch microbenchmark; the kernel is VALU-issue bound at ~4.3 cycles per v_pk_* wave instruction).  So the
+// check-node reduction runs as two independent chains (even / odd edges, merged at the end of pass 1), and pass 2
+// leaves the scheduler free to interleave consecutive edges (no ordering fence between them).
 template <int L, int ARITH, int NP, typename MSGS, int... E>
 __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std::integer_sequence<int, E...>)
 {
@@ -881,12 +890,12 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
   constexpr int DEG = sizeof...(E);
   constexpr int T   = HR_HALF / NP;
   pk16          v[DEG][NP];
-  pk16          min1[NP], min2[NP], sgn[NP];
+  pk16          min1[2][NP], min2[2][NP], sgn[NP];
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    min1[k] = pk_splat(LLR_MAX);
-    min2[k] = pk_splat(LLR_MAX);
-    sgn[k]  = pk_splat(0);
+    min1[0][k] = min1[1][k] = pk_splat(LLR_MAX);
+    min2[0][k] = min2[1][k] = pk_splat(LLR_MAX);
+    sgn[k]                  = pk_splat(0);
   }
   // pass 1 (ldpc_decoder_impl.cpp:235 / :290): v2c and the check-node statistics
   (
@@ -896,25 +905,29 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
         }
         static_for<NP>([&](auto kc) {
           constexpr int k = decltype(kc)::value;
+          constexpr int h = E & 1; // reduction chain
           const pk16    s = pk16{static_cast<short>(lds[hr_addr<E0 + E, 0, k * T>(t)]),
                               static_cast<short>(lds[hr_addr<E0 + E, HR_HALF, k * T>(t)])};
           const pk16 sat = pk_clamp(s, LLR_MAX);
           // infinite soft bits (+-127) push |v2c| beyond 220 (see edge_pass1)
           const pk16 x = (s - sat) * pk_splat(27) + pk_clamp(s - c2v.template get<(E0 + E) * NP + k>(), LLR_MAX);
           const pk16 ax = __builtin_elementwise_abs(x);
-          min2[k]       = pk_max(min1[k], pk_min(ax, min2[k])); // median(min1, |v|, min2)
-          min1[k]       = pk_min(min1[k], ax);
+          min2[h][k]    = pk_max(min1[h][k], pk_min(ax, min2[h][k])); // median(min1, |v|, min2)
+          min1[h][k]    = pk_min(min1[h][k], ax);
           sgn[k] ^= x;
           v[E][k] = x;
         });
       }(),
       ...);
   __builtin_amdgcn_sched_barrier(0);
-  pk16 s1[NP], s2[NP], d12[NP];
+  pk16 m1[NP], s1[NP], s2[NP], d12[NP];
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    s1[k]  = pk_scale<ARITH>(min1[k]);
-    s2[k]  = pk_scale<ARITH>(min2[k]);
+    // merge the two chains: min1 = min(a1, b1), min2 = min(max(a1, b1), min(a2, b2))
+    m1[k]  = pk_min(min1[0][k], min1[1][k]);
+    const pk16 mn2 = pk_min(pk_max(min1[0][k], min1[1][k]), pk_min(min2[0][k], min2[1][k]));
+    s1[k]  = pk_scale<ARITH>(m1[k]);
+    s2[k]  = pk_scale<ARITH>(mn2);
     d12[k] = s1[k] - s2[k];
   }
   // pass 2 (ldpc_decoder_impl.cpp:310, :270): new message and promotion sum
@@ -926,9 +939,11 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
         static_for<NP>([&](auto kc) {
           constexpr int k = decltype(kc)::value;
           pk16          x = v[E][k];
+#if HR_PIN_X
           // opaque: otherwise |x| of pass 1 is kept live (19 more VGPRs) instead of being recomputed
           asm volatile("" : "+v"(x));
-          const pk16 f   = pk_min(__builtin_elementwise_abs(x) - min1[k], pk_splat(1)); // 0: this edge holds min1
+#endif
+          const pk16 f   = pk_min(__builtin_elementwise_abs(x) - m1[k], pk_splat(1)); // 0: this edge holds min1
           const pk16 mag = f * d12[k] + s2[k];
           const pk16 neg = (sgn[k] ^ x) >> 15;
           const pk16 c   = (mag ^ neg) - neg;
@@ -1105,12 +1120,24 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
           const uint32_t w4 = static_cast<uint32_t>(soft4[q]);
           const uint4    r  = *reinterpret_cast<const uint4*>(a.crc_table + (K - 4 - 4 * q));
           zero |= (w4 - 0x01010101u) & ~w4 & 0x80808080u; // some byte is zero
+          // bit 8b + 7 of d: soft bit 4q + b <= 0 (per-byte sign of x - 1, SWAR without borrows)
+          const uint32_t d     = ((w4 | 0x80808080u) - 0x01010101u) ^ (~w4 & 0x80808080u);
           const uint32_t rr[4] = {r.w, r.z, r.y, r.x};
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
-            const int sb = static_cast<int8_t>(w4 >> (8 * b));
-            if (sb <= 0 && (4 * q + b < nof_sig)) {
-              crc ^= rr[b];
+            // one bit-field extract (sign-extended) as the select mask: no compare / v_cndmask per bit
+            crc ^= rr[b] & static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(d), 8 * b + 7, 1));
+          }
+        }
+        // filler bits (positions >= nof_sig) take no part in the CRC: cancel what the loop above added for them
+        // (at most one word per lane; with the PUSCH's +infinity fillers nothing is set)
+        for (int q = (nof_sig >> 2) + static_cast<int>(tq); q < K / 4; q += NT) {
+          const uint32_t w4 = static_cast<uint32_t>(soft4[q]);
+          const uint32_t d  = ((w4 | 0x80808080u) - 0x01010101u) ^ (~w4 & 0x80808080u);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            if (4 * q + b >= nof_sig && ((d >> (8 * b + 7)) & 1u)) {
+              crc ^= a.crc_table[K - 1 - (4 * q + b)];
             }
           }
         }

@@ -26,34 +26,39 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def run():
-    import torch
-
-    import bench_pipeline as bp
-
-    dev = torch.device("cuda", 0)
-    pl = bp.Pipeline(2, dev, ul_layers=2, keep_estimates=True)  # the reference chain runs PUSCH with at most 2 layers
-    stream = torch.cuda.current_stream(dev)
-    pl.step(stream)
-    torch.cuda.synchronize(dev)
-    return bp, pl
+# (name, Pipeline keyword arguments, cells, cells checked stage by stage): the headline's PDSCH 4 x 4 with the
+# reference-runnable 2-layer PUSCH (the reference chain runs PUSCH with at most 2 layers), configs[3] as stated
+# (PDSCH 2 layers x 2 ports, PUSCH 2 layers x 2 rx ports), and a 16-cell batch (cross-cell indexing: every cell's
+# DL grid and TB against the reference chain, three cells stage by stage)
+CHAIN_CASES = [
+    ("dl4x4_ul2x4", dict(ul_layers=2), 2, (0, 1)),
+    ("2x2", dict(dl_layers=2, dl_ports=2, ul_layers=2, ul_ports=2), 2, (0, 1)),
+    ("dl4x4_ul2x4_16cells", dict(ul_layers=2), 16, (0, 7, 15)),
+]
 
 
 def _bf16(u16):
     return (np.asarray(u16, np.uint32) << 16).view(np.float32)
 
 
-def test_pipeline_vs_reference_chain(run):
+@pytest.mark.parametrize("case", CHAIN_CASES, ids=[c[0] for c in CHAIN_CASES])
+def test_pipeline_vs_reference_chain(case):
+    import torch
+
+    import bench_pipeline as bp
+    import oracle
     from oracle import chain as oc
     from oracle import chest as och
     from oracle import pusch_demod as od
     from tests.chest_cases import assert_estimates_close, assert_stats_close
     from tests.pusch_demod_cases import assert_llrs_close
 
-    import oracle
-
-    bp, pl = run
+    _, kw, cells, staged = case
+    dev = torch.device("cuda", 0)
+    pl = bp.Pipeline(cells, dev, keep_estimates=True, **kw)
+    stream = torch.cuda.current_stream(dev)
+    pl.step(stream)
+    torch.cuda.synchronize(dev)
     cfg = bp.chain_config(pl)
     n = oc.slot_size(cfg)
     res = pl.results()
@@ -63,7 +68,16 @@ def test_pipeline_vs_reference_chain(run):
         grid_ref, samp_ref, tb_ref, ok_ref, it_ref = oc.run(cfg, tb_dl, samp_ul)
         # DL grid: bit-exact
         grid = pl.grid_dl[c].cpu().numpy().view(np.uint32)
+        assert grid.shape == grid_ref.shape == (pl.dl_ports, 14, bp.NSUBC)
         assert np.array_equal(grid, grid_ref), "cell %d: DL grid differs in %d REs" % (c, int((grid != grid_ref).sum()))
+        # UL transport block and CRC
+        tb = pl.tb_rx[c].cpu().numpy()
+        assert bool(res[c].data.tb_crc_ok) == ok_ref, c
+        assert np.array_equal(tb, tb_ref), "cell %d: decoded TB differs from the reference chain" % c
+        assert ok_ref and np.array_equal(tb, pl.tb_ul[c].cpu().numpy()), c
+        assert res[c].data.ldpc_iterations_sum == it_ref, (c, res[c].data.ldpc_iterations_sum, it_ref)
+        if c not in staged:
+            continue
         # DL baseband
         samp = pl.samp_dl[c, :, :n].cpu().numpy()
         rms = np.sqrt(np.mean(np.abs(samp_ref) ** 2))
@@ -71,7 +85,7 @@ def test_pipeline_vs_reference_chain(run):
         assert err <= 3e-5 * rms, "cell %d: DL baseband max error %.3g x RMS" % (c, err / rms)
         # UL grid (OFDM demodulator)
         gul = pl.grid_ul[c].cpu().numpy().view(np.uint32)
-        for p in range(bp.UL_PORTS):
+        for p in range(pl.ul_ports):
             ref = oracle.ref_ofdm_demodulate_slot(samp_ul[p], bp.SLOT, bp.MU, bp.NPRB, bp.NFFT, 1.0, 3.5e9)
             ref = ref.view(np.uint32).reshape(14, bp.NSUBC)
             same = gul[p] == ref
@@ -98,12 +112,6 @@ def test_pipeline_vs_reference_chain(run):
         want = od.ref_pusch_demodulate(gul, est, st[:, 0], bp.RNTI, bp.N_ID, bp.QM, list(range(bp.NPRB)),
                                        bp.UL_START, bp.UL_NSYM, bp.DMRS_MASK, False, bp.NCDM, pl.ul_layers)
         assert_llrs_close(llr, want, "cell %d LLRs" % c)
-        # UL transport block and CRC
-        tb = pl.tb_rx[c].cpu().numpy()
-        assert bool(res[c].data.tb_crc_ok) == ok_ref, c
-        assert np.array_equal(tb, tb_ref), "cell %d: decoded TB differs from the reference chain" % c
-        assert ok_ref and np.array_equal(tb, pl.tb_ul[c].cpu().numpy()), c
-        assert res[c].data.ldpc_iterations_sum == it_ref, (c, res[c].data.ldpc_iterations_sum, it_ref)
 
 
 def test_pipeline_four_layer_pusch():
@@ -128,7 +136,7 @@ def test_pipeline_four_layer_pusch():
     for c in range(pl.S):
         gul = pl.grid_ul[c].cpu().numpy().view(np.uint32)
         samp_ul = pl.samp_ul[c].cpu().numpy()
-        for p in range(bp.UL_PORTS):
+        for p in range(pl.ul_ports):
             ref = oracle.ref_ofdm_demodulate_slot(samp_ul[p], bp.SLOT, bp.MU, bp.NPRB, bp.NFFT, 1.0, 3.5e9)
             same = gul[p] == ref.view(np.uint32).reshape(14, bp.NSUBC)
             assert same.mean() >= 0.99, (c, p, same.mean())
