@@ -30,6 +30,18 @@ def lib():
         L.srs_ref_hw_rx_buffer_destroy.argtypes = [P]
         L.srs_ref_hw_pusch_decode.restype = i
         L.srs_ref_hw_pusch_decode.argtypes = [P, P, P, u, P, u] + [u] * 6 + [i, i, P]
+        # adapter_harness.cpp
+        f, d = ctypes.c_float, ctypes.c_double
+        L.srs_ref_hw_pdsch_encode.restype = i
+        L.srs_ref_hw_pdsch_encode.argtypes = [i, i, P, u] + [u] * 6 + [P]
+        L.srs_ref_hip_ofdm_modulate_slot.restype = i
+        L.srs_ref_hip_ofdm_modulate_slot.argtypes = [i, u, u, u, i, f, d, u, P, P]
+        L.srs_ref_hip_ofdm_demodulate_slot.restype = i
+        L.srs_ref_hip_ofdm_demodulate_slot.argtypes = [i, u, u, u, i, u, f, d, u, P, P]
+        L.srs_ref_hip_pusch_demodulate.restype = i
+        L.srs_ref_hip_pusch_demodulate.argtypes = [i, P, u, u, P, u, P, u, u, i, P, u, u, u, i, u, i, i, i, P, u, P]
+        L.srs_ref_hip_ldpc_pusch_decode.restype = i
+        L.srs_ref_hip_ldpc_pusch_decode.argtypes = [i, P, P, u, P, u] + [u] * 6 + [i] * 4 + [P]
         _lib = L
     return _lib
 
@@ -77,4 +89,76 @@ def hw_pusch_decode(dec, llrs, p, rxbuf, tb_out, max_iterations=6, use_early_sto
                                       max_iterations, int(use_early_stop), int(new_data), res.ctypes.data)
     if r != 0:
         raise RuntimeError("pusch_decoder_hw_impl did not notify")
+    return bool(res[0]), int(res[1]), int(res[2]), int(round(res[3])), int(res[4]), int(res[5])
+
+
+def _p(a):
+    return a.ctypes.data
+
+
+def hw_pdsch_encode(tb_bytes, p, cb_mode=False, device=0):
+    """The reference's pdsch_encoder_hw_impl with the MI355X hal::hw_accelerator_pdsch_enc (TB mode, or CB mode).
+    p: an oracle.sch.plan() dict. Codeword bits, one per byte (as oracle.ref_pdsch_encode)."""
+    tb = np.ascontiguousarray(tb_bytes, dtype=np.uint8)
+    cw = np.zeros(p["cw_length"], np.uint8)
+    lib().srs_ref_hw_pdsch_encode(device, int(cb_mode), _p(tb), tb.size, p["base_graph"], p["rv"],
+                                  p["modulation_order"], p["Nref"], p["nof_layers"], p["nof_ch_symbols"], _p(cw))
+    return cw
+
+
+def hip_ofdm_modulate_slot(grid_u16, slot, numerology, bw_rb, dft_size, scale, fc, n, device=0):
+    """ofdm_slot_modulator_impl (one port) with the MI355X dft_processor; n = the slot size in samples."""
+    g = np.ascontiguousarray(grid_u16, dtype=np.uint16)
+    out = np.zeros(n, np.complex64)
+    if lib().srs_ref_hip_ofdm_modulate_slot(device, numerology, bw_rb, dft_size, 0, scale, fc, slot, _p(g), _p(out)):
+        raise ValueError("the MI355X dft_processor refused size %d" % dft_size)
+    return out
+
+
+def hip_ofdm_demodulate_slot(samples, slot, numerology, bw_rb, dft_size, scale, fc, device=0):
+    """ofdm_slot_demodulator_impl (one port) with the MI355X dft_processor; grid uint16 [14][2 * 12 * bw_rb]."""
+    x = np.ascontiguousarray(samples, dtype=np.complex64)
+    grid = np.zeros((14, 2 * bw_rb * 12), np.uint16)
+    if lib().srs_ref_hip_ofdm_demodulate_slot(device, numerology, bw_rb, dft_size, 0, 0, scale, fc, slot, _p(x),
+                                              _p(grid)):
+        raise ValueError("the MI355X dft_processor refused size %d" % dft_size)
+    return grid
+
+
+def hip_pusch_demodulate(grid, estimates, noise_vars, rnti, n_id, qm, crbs, start_symbol, nof_symbols, dmrs_symb_mask,
+                         dmrs_type2, nof_cdm_groups_without_data, nof_layers, mmse=False, device=0):
+    """pusch_demodulator_impl with the MI355X channel_equalizer (arguments as oracle.pusch_demod.ref_pusch_demodulate)."""
+    from .pusch_demod import data_re_mask
+
+    P, _, nsubc = grid.shape
+    mask = data_re_mask(nsubc, crbs, start_symbol, nof_symbols, dmrs_symb_mask, dmrs_type2,
+                        nof_cdm_groups_without_data)
+    nllr = int(mask.sum()) * nof_layers * qm
+    g = np.ascontiguousarray(grid, np.uint32)
+    e = np.ascontiguousarray(estimates, np.uint32)
+    nv = np.ascontiguousarray(noise_vars, np.float32)
+    cr = np.zeros(nsubc // 12, np.uint8)
+    cr[list(crbs)] = 1
+    out = np.zeros(nllr, np.int8)
+    sinr = np.zeros(15, np.float32)
+    r = lib().srs_ref_hip_pusch_demodulate(device, _p(g), P, nsubc, _p(e), nof_layers, _p(nv), rnti, n_id, qm, _p(cr),
+                                           start_symbol, nof_symbols, dmrs_symb_mask, int(dmrs_type2),
+                                           nof_cdm_groups_without_data, int(mmse), 0, 0, _p(out), nllr, _p(sinr))
+    if r < 0:
+        raise RuntimeError("pusch_demodulator_impl with the MI355X equalizer failed (%d)" % r)
+    return out
+
+
+def hip_ldpc_pusch_decode(llrs, p, rxbuf, tb_out, max_iterations=6, generic=False, use_early_stop=True,
+                          force_decoding=False, new_data=True, device=0):
+    """The reference's pusch_decoder_impl whose pusch_codeblock_decoder runs the MI355X ldpc_decoder adapter
+    (integration/ldpc_decoder_hip). rxbuf: an oracle.RefRxBuffer. Result as oracle.ref_pusch_decode."""
+    llrs = np.ascontiguousarray(llrs, dtype=np.int8)
+    res = np.zeros(6, np.float64)
+    r = lib().srs_ref_hip_ldpc_pusch_decode(device, rxbuf.h, _p(llrs), llrs.size, _p(tb_out), tb_out.size,
+                                            p["base_graph"], p["rv"], p["modulation_order"], p["Nref"],
+                                            p["nof_layers"], max_iterations, int(force_decoding), int(use_early_stop),
+                                            int(new_data), int(generic), _p(res))
+    if r != 0:
+        raise RuntimeError("pusch_decoder_impl did not notify")
     return bool(res[0]), int(res[1]), int(res[2]), int(round(res[3])), int(res[4]), int(res[5])

@@ -227,12 +227,17 @@ inline std::unique_ptr<transform_precoder> make_transform_precoder(unsigned max_
 }
 
 // eq: 0 ZF, 1 MMSE (channel_equalizer_algorithm_type).
-inline std::unique_ptr<pusch_demodulator_impl>
-make_pusch_demodulator(int eq, unsigned max_nof_rb, bool compute_post_eq_sinr, bool with_transform_precoder)
+// custom: an equalizer to use instead of channel_equalizer_generic_impl (the harness's MI355X adapter).
+inline std::unique_ptr<pusch_demodulator_impl> make_pusch_demodulator(int                                eq,
+                                                                      unsigned                           max_nof_rb,
+                                                                      bool                               compute_post_eq_sinr,
+                                                                      bool                               with_transform_precoder,
+                                                                      std::unique_ptr<channel_equalizer> custom = nullptr)
 {
   return std::make_unique<pusch_demodulator_impl>(
-      std::make_unique<channel_equalizer_generic_impl>(eq == 0 ? channel_equalizer_algorithm_type::zf
-                                                               : channel_equalizer_algorithm_type::mmse),
+      custom ? std::move(custom)
+             : std::make_unique<channel_equalizer_generic_impl>(eq == 0 ? channel_equalizer_algorithm_type::zf
+                                                                        : channel_equalizer_algorithm_type::mmse),
       with_transform_precoder ? make_transform_precoder(max_nof_rb) : nullptr,
       std::make_unique<demodulation_mapper_impl>(),
       nullptr,
@@ -280,5 +285,23 @@ make_pusch_processor(impl choice, unsigned max_nof_rb, unsigned nof_rx_ports, un
   b->proc                   = std::make_unique<pusch_processor_impl>(cfg);
   return b;
 }
+
+// ---- defined in the wrappers (libsrsran_ref.so); the adapter harness (adapter_harness.cpp) runs the reference's
+// own classes with the MI355X adapters of integration/ injected through them.
+std::unique_ptr<pusch_decoder_impl> make_pusch_decoder_with(std::unique_ptr<ldpc_decoder> dec, bool generic);
+int pusch_decode_on(pusch_decoder_impl& dec, void* rx_buffer, const int8_t* llrs, unsigned nof_llrs, uint8_t* tb,
+                    unsigned tb_bytes, unsigned bg, unsigned rv, unsigned qm, unsigned Nref, unsigned nof_layers,
+                    unsigned nof_iterations, int force_decoding, int use_early_stop, int new_data, double* result);
+int ofdm_modulate_slot_with(std::unique_ptr<dft_processor> dft, unsigned numerology, unsigned bw_rb, unsigned dft_size,
+                            int extended_cp, float scale, double fc, unsigned slot, const uint16_t* grid, float* out);
+int ofdm_demodulate_slot_with(std::unique_ptr<dft_processor> dft, unsigned numerology, unsigned bw_rb,
+                              unsigned dft_size, int extended_cp, unsigned window_offset, float scale, double fc,
+                              unsigned slot, const float* in, uint16_t* grid);
+int pusch_demodulate_with(std::unique_ptr<channel_equalizer> eq_impl, const uint32_t* grid, unsigned nof_rx_ports,
+                          unsigned nsubc, const uint32_t* estimates, unsigned nof_layers, const float* noise_vars,
+                          unsigned rnti, unsigned n_id, int qm, const uint8_t* crbs, unsigned start_symbol,
+                          unsigned nof_symbols, unsigned dmrs_symb_mask, int dmrs_type2,
+                          unsigned nof_cdm_groups_without_data, int eq, int transform_precoding, int post_eq_sinr,
+                          int8_t* llrs, unsigned nof_llrs, float* sinr_out);
 
 } // namespace srs_ref

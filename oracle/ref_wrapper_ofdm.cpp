@@ -18,6 +18,7 @@
 #include "phy/lower/modulation/ofdm_modulator_impl.h"
 #include "srsran/phy/support/resource_grid_reader.h"
 #include "srsran/phy/support/resource_grid_writer.h"
+#include "ref_builders.h"
 #include <chrono>
 #include <cstring>
 #include <memory>
@@ -101,8 +102,13 @@ private:
   unsigned nsymb, nsubc;
 };
 
-std::unique_ptr<ofdm_slot_modulator>
-make_modulator(unsigned numerology, unsigned bw_rb, unsigned dft_size, int extended_cp, float scale, double fc)
+std::unique_ptr<ofdm_slot_modulator> make_modulator(unsigned                       numerology,
+                                                    unsigned                       bw_rb,
+                                                    unsigned                       dft_size,
+                                                    int                            extended_cp,
+                                                    float                          scale,
+                                                    double                         fc,
+                                                    std::unique_ptr<dft_processor> dft = nullptr)
 {
   ofdm_modulator_configuration cfg;
   cfg.numerology     = numerology;
@@ -112,8 +118,9 @@ make_modulator(unsigned numerology, unsigned bw_rb, unsigned dft_size, int exten
   cfg.scale          = scale;
   cfg.center_freq_Hz = fc;
   ofdm_modulator_common_configuration common;
-  common.dft = std::make_unique<dft_processor_generic_impl>(
-      dft_processor::configuration{dft_size, dft_processor::direction::INVERSE});
+  common.dft = dft ? std::move(dft)
+                   : std::make_unique<dft_processor_generic_impl>(
+                         dft_processor::configuration{dft_size, dft_processor::direction::INVERSE});
   auto sym = std::make_unique<ofdm_symbol_modulator_impl>(common, cfg);
   return std::make_unique<ofdm_slot_modulator_impl>(cfg, std::move(sym));
 }
@@ -124,7 +131,8 @@ std::unique_ptr<ofdm_slot_demodulator> make_demodulator(unsigned numerology,
                                                         int      extended_cp,
                                                         unsigned window_offset,
                                                         float    scale,
-                                                        double   fc)
+                                                        double   fc,
+                                                        std::unique_ptr<dft_processor> dft = nullptr)
 {
   ofdm_demodulator_configuration cfg;
   cfg.numerology                = numerology;
@@ -135,13 +143,61 @@ std::unique_ptr<ofdm_slot_demodulator> make_demodulator(unsigned numerology,
   cfg.scale                     = scale;
   cfg.center_freq_Hz            = fc;
   ofdm_demodulator_common_configuration common;
-  common.dft = std::make_unique<dft_processor_generic_impl>(
-      dft_processor::configuration{dft_size, dft_processor::direction::DIRECT});
+  common.dft = dft ? std::move(dft)
+                   : std::make_unique<dft_processor_generic_impl>(
+                         dft_processor::configuration{dft_size, dft_processor::direction::DIRECT});
   auto sym = std::make_unique<ofdm_symbol_demodulator_impl>(common, cfg);
   return std::make_unique<ofdm_slot_demodulator_impl>(cfg, std::move(sym));
 }
 
 } // namespace
+
+// ofdm_slot_modulator_impl / ofdm_slot_demodulator_impl of one port with a given DFT (the harness's MI355X
+// dft_processor adapter); layouts as srs_ref_ofdm_modulate_slot / srs_ref_ofdm_demodulate_slot.
+int srs_ref::ofdm_modulate_slot_with(std::unique_ptr<dft_processor> dft,
+                                     unsigned                       numerology,
+                                     unsigned                       bw_rb,
+                                     unsigned                       dft_size,
+                                     int                            extended_cp,
+                                     float                          scale,
+                                     double                         fc,
+                                     unsigned                       slot,
+                                     const uint16_t*                grid,
+                                     float*                         out)
+{
+  if (!dft) {
+    return -1;
+  }
+  auto              mod   = make_modulator(numerology, bw_rb, dft_size, extended_cp, scale, fc, std::move(dft));
+  unsigned          nsymb = extended_cp ? 12 : 14;
+  unsigned          n     = mod->get_slot_size(slot);
+  dense_grid_reader rd(reinterpret_cast<const cbf16_t*>(grid), nsymb, bw_rb * NRE);
+  mod->modulate(span<cf_t>(reinterpret_cast<cf_t*>(out), n), rd, 0, slot);
+  return 0;
+}
+
+int srs_ref::ofdm_demodulate_slot_with(std::unique_ptr<dft_processor> dft,
+                                       unsigned                       numerology,
+                                       unsigned                       bw_rb,
+                                       unsigned                       dft_size,
+                                       int                            extended_cp,
+                                       unsigned                       window_offset,
+                                       float                          scale,
+                                       double                         fc,
+                                       unsigned                       slot,
+                                       const float*                   in,
+                                       uint16_t*                      grid)
+{
+  if (!dft) {
+    return -1;
+  }
+  auto dem = make_demodulator(numerology, bw_rb, dft_size, extended_cp, window_offset, scale, fc, std::move(dft));
+  unsigned          nsymb = extended_cp ? 12 : 14;
+  unsigned          n     = dem->get_slot_size(slot);
+  dense_grid_writer wr(reinterpret_cast<cbf16_t*>(grid), nsymb, bw_rb * NRE);
+  dem->demodulate(wr, span<const cf_t>(reinterpret_cast<const cf_t*>(in), n), 0, slot);
+  return 0;
+}
 
 extern "C" {
 

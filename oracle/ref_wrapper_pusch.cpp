@@ -127,38 +127,34 @@ public:
 
 } // namespace
 
-extern "C" {
-
-// pusch_demodulator::demodulate (pusch_demodulator_impl.cpp:203-445) of one grid [P][14][nsubc]
-// with channel estimates [P][L][14][nsubc] (cbf16 as uint32) and per-port noise variances.
-// crbs: 0/1 bytes [nsubc / 12]. eq: 0 ZF, 1 MMSE. llrs: nof_llrs (= data REs x L x Qm) int8.
-// sinr_out[15]: per-OFDM-symbol provisional SINR (dB, NaN when not notified) then the final one
-// (computed only when post_eq_sinr != 0). Returns the number of codeword blocks the demodulator
-// produced, or -1 on a size mismatch.
-int srs_ref_pusch_demodulate(const uint32_t* grid,
-                             unsigned        nof_rx_ports,
-                             unsigned        nsubc,
-                             const uint32_t* estimates,
-                             unsigned        nof_layers,
-                             const float*    noise_vars,
-                             unsigned        rnti,
-                             unsigned        n_id,
-                             int             qm,
-                             const uint8_t*  crbs,
-                             unsigned        start_symbol,
-                             unsigned        nof_symbols,
-                             unsigned        dmrs_symb_mask,
-                             int             dmrs_type2,
-                             unsigned        nof_cdm_groups_without_data,
-                             int             eq,
-                             int             transform_precoding,
-                             int             post_eq_sinr,
-                             int8_t*         llrs,
-                             unsigned        nof_llrs,
-                             float*          sinr_out)
+// pusch_demodulator_impl with a given channel equalizer (nullptr: channel_equalizer_generic_impl); the harness runs
+// it with the MI355X channel_equalizer adapter. Arguments as srs_ref_pusch_demodulate.
+int srs_ref::pusch_demodulate_with(std::unique_ptr<channel_equalizer> eq_impl,
+                                   const uint32_t*                    grid,
+                                   unsigned                           nof_rx_ports,
+                                   unsigned                           nsubc,
+                                   const uint32_t*                    estimates,
+                                   unsigned                           nof_layers,
+                                   const float*                       noise_vars,
+                                   unsigned                           rnti,
+                                   unsigned                           n_id,
+                                   int                                qm,
+                                   const uint8_t*                     crbs,
+                                   unsigned                           start_symbol,
+                                   unsigned                           nof_symbols,
+                                   unsigned                           dmrs_symb_mask,
+                                   int                                dmrs_type2,
+                                   unsigned                           nof_cdm_groups_without_data,
+                                   int                                eq,
+                                   int                                transform_precoding,
+                                   int                                post_eq_sinr,
+                                   int8_t*                            llrs,
+                                   unsigned                           nof_llrs,
+                                   float*                             sinr_out)
 {
   const unsigned nof_prb = nsubc / NRE;
-  auto           demod   = make_pusch_demodulator(eq, nof_prb, post_eq_sinr != 0, transform_precoding != 0);
+  auto           demod   = make_pusch_demodulator(eq, nof_prb, post_eq_sinr != 0, transform_precoding != 0,
+                                                  std::move(eq_impl));
 
   grid_tensor data({nsubc, MAX_NSYMB_PER_SLOT, nof_rx_ports});
   load_grid(data, grid, nof_rx_ports, nsubc);
@@ -215,6 +211,42 @@ int srs_ref_pusch_demodulate(const uint32_t* grid,
     sinr_out[MAX_NSYMB_PER_SLOT] = notifier.end_sinr;
   }
   return static_cast<int>(buf.nof_blocks);
+}
+
+extern "C" {
+
+// pusch_demodulator::demodulate (pusch_demodulator_impl.cpp:203-445) of one grid [P][14][nsubc]
+// with channel estimates [P][L][14][nsubc] (cbf16 as uint32) and per-port noise variances.
+// crbs: 0/1 bytes [nsubc / 12]. eq: 0 ZF, 1 MMSE. llrs: nof_llrs (= data REs x L x Qm) int8.
+// sinr_out[15]: per-OFDM-symbol provisional SINR (dB, NaN when not notified) then the final one
+// (computed only when post_eq_sinr != 0). Returns the number of codeword blocks the demodulator
+// produced, or -1 on a size mismatch.
+int srs_ref_pusch_demodulate(const uint32_t* grid,
+                             unsigned        nof_rx_ports,
+                             unsigned        nsubc,
+                             const uint32_t* estimates,
+                             unsigned        nof_layers,
+                             const float*    noise_vars,
+                             unsigned        rnti,
+                             unsigned        n_id,
+                             int             qm,
+                             const uint8_t*  crbs,
+                             unsigned        start_symbol,
+                             unsigned        nof_symbols,
+                             unsigned        dmrs_symb_mask,
+                             int             dmrs_type2,
+                             unsigned        nof_cdm_groups_without_data,
+                             int             eq,
+                             int             transform_precoding,
+                             int             post_eq_sinr,
+                             int8_t*         llrs,
+                             unsigned        nof_llrs,
+                             float*          sinr_out)
+{
+  return srs_ref::pusch_demodulate_with(nullptr, grid, nof_rx_ports, nsubc, estimates, nof_layers, noise_vars, rnti,
+                                        n_id, qm, crbs, start_symbol, nof_symbols, dmrs_symb_mask, dmrs_type2,
+                                        nof_cdm_groups_without_data, eq, transform_precoding, post_eq_sinr, llrs,
+                                        nof_llrs, sinr_out);
 }
 
 // pusch_processor::process (pusch_processor_impl.cpp:134-386) of one PDU on a received grid

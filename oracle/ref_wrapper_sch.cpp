@@ -86,7 +86,7 @@ public:
   bool                 done = false;
 };
 
-std::unique_ptr<pusch_decoder_impl> make_pusch_decoder(bool generic)
+std::unique_ptr<pusch_decoder_impl> make_pusch_decoder(bool generic, std::unique_ptr<ldpc_decoder> custom = nullptr)
 {
   std::vector<std::unique_ptr<pusch_codeblock_decoder>> cbdec;
   pusch_codeblock_decoder::sch_crc                      c;
@@ -102,6 +102,9 @@ std::unique_ptr<pusch_decoder_impl> make_pusch_decoder(bool generic)
     dec = std::make_unique<ldpc_decoder_avx2>(false);
     dm  = std::make_unique<ldpc_rate_dematcher_avx2_impl>();
   }
+  if (custom) {
+    dec = std::move(custom); // the decoder under test (srs_ref::make_pusch_decoder_with)
+  }
   cbdec.emplace_back(std::make_unique<pusch_codeblock_decoder>(std::move(dm), std::move(dec), c));
   auto pool = std::make_shared<pusch_decoder_impl::codeblock_decoder_pool>(cbdec);
   pusch_decoder_impl::sch_crc crcs;
@@ -113,6 +116,59 @@ std::unique_ptr<pusch_decoder_impl> make_pusch_decoder(bool generic)
 }
 
 } // namespace
+
+// pusch_decoder_impl (pusch_codeblock_decoder with the generic or AVX2 rate dematcher) around a given LDPC decoder:
+// the harness runs the reference decoder chain with the MI355X ldpc_decoder adapter (integration/ldpc_decoder_hip).
+std::unique_ptr<pusch_decoder_impl> srs_ref::make_pusch_decoder_with(std::unique_ptr<ldpc_decoder> dec, bool generic)
+{
+  return ::make_pusch_decoder(generic, std::move(dec));
+}
+
+// new_data + on_new_softbits + on_end_softbits on `dec`; result as srs_ref_pusch_decode.
+int srs_ref::pusch_decode_on(pusch_decoder_impl& dec,
+                             void*               rx_buffer,
+                             const int8_t*       llrs,
+                             unsigned            nof_llrs,
+                             uint8_t*            tb,
+                             unsigned            tb_bytes,
+                             unsigned            bg,
+                             unsigned            rv,
+                             unsigned            qm,
+                             unsigned            Nref,
+                             unsigned            nof_layers,
+                             unsigned            nof_iterations,
+                             int                 force_decoding,
+                             int                 use_early_stop,
+                             int                 new_data,
+                             double*             result)
+{
+  pusch_decoder::configuration cfg;
+  cfg.base_graph          = bg == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
+  cfg.rv                  = rv;
+  cfg.mod                 = scheme_of(qm);
+  cfg.Nref                = Nref;
+  cfg.nof_layers          = nof_layers;
+  cfg.nof_ldpc_iterations = nof_iterations;
+  cfg.force_decoding      = force_decoding != 0;
+  cfg.use_early_stop      = use_early_stop != 0;
+  cfg.new_data            = new_data != 0;
+  result_catcher   notifier;
+  unique_rx_buffer buf(*static_cast<ref_rx_buffer*>(rx_buffer));
+  pusch_decoder_buffer& in = dec.new_data(span<uint8_t>(tb, tb_bytes), std::move(buf), notifier, cfg);
+  in.on_new_softbits(span<const log_likelihood_ratio>(reinterpret_cast<const log_likelihood_ratio*>(llrs), nof_llrs));
+  in.on_end_softbits();
+  if (!notifier.done) {
+    return -1;
+  }
+  const auto& st = notifier.result.ldpc_decoder_stats;
+  result[0]      = notifier.result.tb_crc_ok ? 1 : 0;
+  result[1]      = notifier.result.nof_codeblocks_total;
+  result[2]      = st.get_nof_observations();
+  result[3]      = st.get_mean() * st.get_nof_observations();
+  result[4]      = st.get_min();
+  result[5]      = st.get_max();
+  return 0;
+}
 
 extern "C" {
 
@@ -172,32 +228,8 @@ int srs_ref_pusch_decode(void*         rx_buffer,
   static thread_local std::unique_ptr<pusch_decoder_impl> dec_simd    = make_pusch_decoder(false);
   static thread_local std::unique_ptr<pusch_decoder_impl> dec_generic = make_pusch_decoder(true);
   pusch_decoder_impl&                                     dec         = generic ? *dec_generic : *dec_simd;
-  pusch_decoder::configuration                            cfg;
-  cfg.base_graph          = bg == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
-  cfg.rv                  = rv;
-  cfg.mod                 = scheme_of(qm);
-  cfg.Nref                = Nref;
-  cfg.nof_layers          = nof_layers;
-  cfg.nof_ldpc_iterations = nof_iterations;
-  cfg.force_decoding      = force_decoding != 0;
-  cfg.use_early_stop      = use_early_stop != 0;
-  cfg.new_data            = new_data != 0;
-  result_catcher   notifier;
-  unique_rx_buffer buf(*static_cast<ref_rx_buffer*>(rx_buffer));
-  pusch_decoder_buffer& in = dec.new_data(span<uint8_t>(tb, tb_bytes), std::move(buf), notifier, cfg);
-  in.on_new_softbits(span<const log_likelihood_ratio>(reinterpret_cast<const log_likelihood_ratio*>(llrs), nof_llrs));
-  in.on_end_softbits();
-  if (!notifier.done) {
-    return -1;
-  }
-  const auto& st = notifier.result.ldpc_decoder_stats;
-  result[0]      = notifier.result.tb_crc_ok ? 1 : 0;
-  result[1]      = notifier.result.nof_codeblocks_total;
-  result[2]      = st.get_nof_observations();
-  result[3]      = st.get_mean() * st.get_nof_observations();
-  result[4]      = st.get_min();
-  result[5]      = st.get_max();
-  return 0;
+  return srs_ref::pusch_decode_on(dec, rx_buffer, llrs, nof_llrs, tb, tb_bytes, bg, rv, qm, Nref, nof_layers,
+                                  nof_iterations, force_decoding, use_early_stop, new_data, result);
 }
 
 } // extern "C"

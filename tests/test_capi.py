@@ -140,7 +140,7 @@ def test_sch_plan_host_only():
 
 def test_integration_plugins_built_against_reference_headers():
     """integration/_build/libsrsran_amd_hal.so -- the srsRAN plug-ins over the C-ABI (hal::hw_accelerator_pusch_dec
-    and its factory, the ldpc_decoder "hip" factory), compiled against the reference's own headers -- exists, links
+    and its factory, the PDSCH encoder plug-in, the ldpc_decoder / dft_processor / channel_equalizer factories), compiled against the reference's own headers -- exists, links
     with no undefined symbols (-Wl,--no-undefined) and exports the factory entry points."""
     import subprocess
 
@@ -150,4 +150,7 @@ def test_integration_plugins_built_against_reference_headers():
     out = subprocess.run(["nm", "-D", "-C", "--defined-only", path], capture_output=True, text=True, check=True).stdout
     assert "srsran::hip::create_hip_pusch_dec_acc_factory(srsran::hip::pusch_dec_accelerator_config const&)" in out
     assert "srsran::hip::create_ldpc_decoder_factory_hip(" in out
+    assert "srsran::hip::create_hip_pdsch_enc_acc_factory(srsran::hip::pdsch_enc_accelerator_config const&)" in out
+    assert "srsran::hip::create_dft_processor_factory_hip(int)" in out
+    assert "srsran::hip::create_channel_equalizer_factory_hip(srsran::channel_equalizer_algorithm_type, int)" in out
     ctypes.CDLL(path)  # loads with libsrsran_amd.so found through its rpath

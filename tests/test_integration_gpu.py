@@ -1,5 +1,5 @@
 """The reference-side boundary, compiled against the reference's own headers (integration/Makefile) and
-exercised through the reference's own code:
+exercised through the reference's own code (oracle/hw_harness.cpp, oracle/adapter_harness.cpp):
 
   * the REFERENCE's hardware-accelerated PUSCH decoder, pusch_decoder_hw_impl
     (lib/phy/upper/channel_processors/pusch/pusch_decoder_hw_impl.cpp), driving the MI355X plug-in
@@ -7,13 +7,20 @@ exercised through the reference's own code:
     rate-dematch + LDPC batch per transport block), must give the same transport block, TB CRC verdict and
     LDPC statistics as the reference's software pusch_decoder_impl (oracle ref_wrapper_sch.cpp) on the same
     LLRs -- new data, HARQ combining across redundancy versions, single- and multi-codeblock TBs (CRC16 /
-    CRC24A / CRC24B), BG1 / BG2, limited-buffer rate matching.
+    CRC24A / CRC24B), BG1 / BG2, limited-buffer rate matching; two accelerator instances of one factory on two
+    threads; a HARQ process abandoned without a CRC pass;
+  * the reference's pdsch_encoder_hw_impl driving hal::hw_accelerator_pdsch_enc (TB and CB mode) must equal
+    pdsch_encoder_impl bit-exactly;
+  * the reference's OFDM slot modulator / demodulator built with the dft_processor adapter, its
+    pusch_demodulator_impl with the channel_equalizer adapter, and its pusch_decoder_impl with the ldpc_decoder
+    adapter must match the generic builds within the float tolerances stated per test (bit-exact for the decoder).
 """
 import numpy as np
 import pytest
 
 import oracle
 import oracle.sch as osch
+from tests.pusch_demod_cases import CASES as DEMOD_CASES
 from tests.sch_cases import SCH_CASES, noisy_llrs, tb_bytes
 
 pytestmark = pytest.mark.gpu
@@ -155,3 +162,88 @@ def test_hw_plugin_abandoned_harq_process(hw):
     want = oracle.ref_pusch_decode(llr, pb, oracle.RefRxBuffer(pb["nof_segments"]), want_tb)
     assert got == want and got[0]
     np.testing.assert_array_equal(got_tb, tb)
+
+
+# ---- the other reference-side adapters, each driven by the REFERENCE's own class (oracle/adapter_harness.cpp) ----
+
+@pytest.mark.parametrize("cb_mode", [False, True], ids=["tb_mode", "cb_mode"])
+@pytest.mark.parametrize("ci", range(len(SCH_CASES)))
+def test_hw_pdsch_enc_plugin_matches_pdsch_encoder_impl(hw, ci, cb_mode):
+    """pdsch_encoder_hw_impl (pdsch_encoder_hw_impl.cpp) with the MI355X hal::hw_accelerator_pdsch_enc: the same
+    codeword bits as the reference's software pdsch_encoder_impl, bit-exact (TB mode: one GPU batch per transport
+    block; CB mode: the reference segments, the GPU LDPC-encodes and rate-matches each codeblock)."""
+    ohw, _ = hw
+    p = _plan(SCH_CASES[ci])
+    for seed in (0, 1):
+        tb = tb_bytes(p["tbs"], 700 + 10 * ci + seed)
+        got = ohw.hw_pdsch_encode(tb, p, cb_mode=cb_mode)
+        want = oracle.ref_pdsch_encode(tb, p)
+        assert np.array_equal(got, want), (SCH_CASES[ci], cb_mode, int((got != want).sum()))
+
+
+DFT_OFDM_CASES = [(1, 273, 4096, 1.0, 3.5e9), (0, 52, 1024, 0.5, 1.8e9), (1, 106, 1536, 0.7, 2.6e9)]
+
+
+@pytest.mark.parametrize("case", DFT_OFDM_CASES)
+def test_dft_adapter_through_ofdm_modulator(hw, case):
+    """ofdm_slot_modulator_impl / ofdm_slot_demodulator_impl (ofdm_modulator_impl.cpp / ofdm_demodulator_impl.cpp)
+    built with the MI355X dft_processor instead of dft_processor_generic_impl: baseband samples within 4e-5 x RMS of
+    the generic build (each float DFT sits within 2e-5 x RMS of the exact transform), resource grids within one bf16
+    ulp (+ 3e-5 x RMS near zero) and >= 99 % identical."""
+    from oracle import ofdm as oofdm
+
+    ohw, _ = hw
+    mu, bw, N, scale, fc = case
+    rng = np.random.default_rng(N + bw)
+    for slot in (0, (1 << mu) - 1):
+        g = oofdm.random_grid(rng, 14, bw * 12)
+        want = oracle.ref_ofdm_modulate_slot(g, slot, mu, bw, N, scale, fc)
+        got = ohw.hip_ofdm_modulate_slot(g, slot, mu, bw, N, scale, fc, want.size)
+        rms = float(np.sqrt(np.mean(np.abs(want) ** 2)))
+        assert np.max(np.abs(got - want)) <= 4e-5 * rms, (case, slot, np.max(np.abs(got - want)) / rms)
+        rx = (want + (rng.normal(0, 0.05, want.size) + 1j * rng.normal(0, 0.05, want.size)) * rms).astype(np.complex64)
+        gw = oracle.ref_ofdm_demodulate_slot(rx, slot, mu, bw, N, scale, fc).view(np.uint32)
+        gg = ohw.hip_ofdm_demodulate_slot(rx, slot, mu, bw, N, scale, fc).view(np.uint32)
+        a = (gg.view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+        b = (gw.view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+        tol = 2.0 ** -7 * np.maximum(np.abs(a), np.abs(b)) + 3e-5 * np.sqrt(np.mean(b ** 2))
+        assert (np.abs(a - b) <= tol).all(), case
+        assert (gg == gw).mean() >= 0.99, (case, (gg == gw).mean())
+
+
+@pytest.mark.parametrize("ci", range(len(DEMOD_CASES)))
+def test_equalizer_adapter_through_pusch_demodulator(hw, ci):
+    """pusch_demodulator_impl (pusch_demodulator_impl.cpp:203-445) built with the MI355X channel_equalizer instead of
+    channel_equalizer_generic_impl: the LLRs of the whole demodulator within |dLLR| <= 1, >= 97 % identical (the
+    reference's AVX2 ZF path multiplies by an approximate reciprocal, tests/pusch_demod_cases.py)."""
+    from oracle import pusch_demod as od
+    from tests.pusch_demod_cases import assert_llrs_close, demod_args, make_case
+
+    ohw, _ = hw
+    case = DEMOD_CASES[ci]
+    grid, est, nv, crbs = make_case(case, seed=40 + ci)
+    args = demod_args(case)
+    want = od.ref_pusch_demodulate(grid, est, nv, 0x4601, 500, crbs=crbs, **args)
+    got = ohw.hip_pusch_demodulate(grid, est, nv, 0x4601, 500, crbs=crbs, **args)
+    assert_llrs_close(got, want, case[0], min_equal=0.97)
+
+
+@pytest.mark.parametrize("generic", [False, True], ids=["hip", "hip-generic"])
+@pytest.mark.parametrize("ci", range(len(SCH_CASES)))
+def test_ldpc_decoder_adapter_through_pusch_decoder(hw, ci, generic):
+    """pusch_decoder_impl + pusch_codeblock_decoder (pusch_codeblock_decoder.cpp:35-69) whose ldpc_decoder is the
+    MI355X adapter (integration/ldpc_decoder_hip, the "hip" / "hip-generic" decoder types): transport block, TB CRC
+    and LDPC statistics identical to the reference's AVX2 / generic decoders, new data and HARQ combining."""
+    ohw, _ = hw
+    p = _plan(SCH_CASES[ci])
+    tb = tb_bytes(p["tbs"], 900 + ci)
+    cw = osch.pdsch_encode(tb, p)
+    rx_a, rx_b = oracle.RefRxBuffer(p["nof_segments"]), oracle.RefRxBuffer(p["nof_segments"])
+    for k, (sigma, new) in enumerate(((9.0, True), (6.0, False), (3.0, True))):
+        llr = noisy_llrs(cw, 8, sigma, seed=ci * 17 + k)
+        got_tb = np.zeros(p["tbs"] // 8, np.uint8)
+        want_tb = np.zeros(p["tbs"] // 8, np.uint8)
+        got = ohw.hip_ldpc_pusch_decode(llr, p, rx_a, got_tb, generic=generic, new_data=new)
+        want = oracle.ref_pusch_decode(llr, p, rx_b, want_tb, generic=generic, new_data=new)
+        assert got == want, (SCH_CASES[ci], sigma, got, want)
+        np.testing.assert_array_equal(got_tb, want_tb)
