@@ -143,6 +143,35 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
                                 const srs_amd_pusch_intermediates*  io,
                                 void*                               stream);
 
+/* One PUSCH PDU of a slot (srs_amd_pusch_process_slot). */
+typedef struct srs_amd_pusch_slot_pdu {
+  const srs_amd_pusch_processor_plan* plan;      /* a plan of this processor */
+  uint32_t                            grid;      /* index of the received grid the PDU occupies in d_grids */
+  uint32_t                            reserved;  /* 0 */
+  uint64_t                            tb_offset; /* byte offset of its tbs / 8 transport-block bytes in d_tbs */
+} srs_amd_pusch_slot_pdu;
+
+/* DEVICE, asynchronous: every PUSCH PDU of a slot -- several UEs on disjoint PRBs of one received grid (or of
+ * several grids), each with its own PRB range, layers, modulation, DM-RS symbols and scrambling, rnti / n_id
+ * and code rate -- as ONE launch sequence: one channel-estimator sequence over all PDUs (per-PDU argument
+ * blocks), one fused equalizer-demapper launch per (ports, layers, equalizer) kind, one slot decoder sequence
+ * (srs_amd_pusch_decode_slot) and one result launch.  What uplink_processor_impl::process_pusch
+ * (uplink_processor_impl.cpp:270-326) does by calling pusch_processor_impl::process once per PDU.  Result of
+ * pdus[i] in d_results[i], transport block at d_tbs + pdus[i].tb_offset; per PDU identical to
+ * srs_amd_pusch_process_batch on that PDU's grid.  Scope: new transmissions (pdu.new_data = 1; HARQ
+ * retransmissions go through srs_amd_pusch_process_batch with caller soft buffers), no transform precoding,
+ * every plan covered by the fused estimator-equalizer (1, 2 or 4 receive ports, layers <= ports), plans
+ * created for the same nof_subc. */
+int srs_amd_pusch_process_slot(srs_amd_pusch_processor*        proc,
+                               const srs_amd_pusch_slot_pdu*   pdus,
+                               uint32_t                        nof_pdus,
+                               const uint32_t*                 d_grids,
+                               uint64_t                        grid_stride,
+                               uint32_t                        nof_grids,
+                               uint8_t*                        d_tbs,
+                               srs_amd_pusch_processor_result* d_results,
+                               void*                           stream);
+
 /* HOST, synchronous: one grid [port][14][nof_subc]; tb gets tbs/8 bytes;
  * soft_buffer: HOST HARQ buffer of soft_buffer_bytes (or NULL for new data only). */
 int srs_amd_pusch_process(srs_amd_pusch_processor*            proc,

@@ -81,6 +81,7 @@ from .pusch_processor import (  # noqa: F401
     PuschPdu,
     PuschProcessor,
     PuschProcessorConfig,
+    PuschSlotPdu,
     PuschProcessorPlan,
     PuschProcessorResult,
     make_pdu,

@@ -159,6 +159,58 @@ struct call_scope {
   }
 };
 
+// Host-built launch descriptors (per-item argument blocks of a slot call) staged in pinned memory and
+// uploaded on the call's stream: the buffer is rewritten only once its previous upload has completed.
+struct pinned_stage {
+  void*      h    = nullptr;
+  size_t     size = 0;
+  hipEvent_t done = nullptr;
+  bool       used = false;
+  pinned_stage()                               = default;
+  pinned_stage(const pinned_stage&)            = delete;
+  pinned_stage& operator=(const pinned_stage&) = delete;
+  ~pinned_stage()
+  {
+    if (done) {
+      (void)hipEventSynchronize(done);
+      (void)hipEventDestroy(done);
+    }
+    (void)hipHostFree(h);
+  }
+  // Waits for the previous upload and grows the buffer to n bytes; the host pointer is then writable.
+  hipError_t acquire(size_t n)
+  {
+    hipError_t e = used ? hipEventSynchronize(done) : hipSuccess;
+    used         = false;
+    if (e == hipSuccess && done == nullptr) {
+      e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    }
+    if (e == hipSuccess && size < n) {
+      (void)hipHostFree(h);
+      h    = nullptr;
+      size = 0;
+      e    = hipHostMalloc(&h, n, hipHostMallocDefault);
+      size = e == hipSuccess ? n : 0;
+    }
+    return e;
+  }
+  template <typename T>
+  T* at(size_t offset) const
+  {
+    return reinterpret_cast<T*>(static_cast<unsigned char*>(h) + offset);
+  }
+  // Copies the first n bytes to device memory d on stream s.
+  hipError_t upload(void* d, size_t n, hipStream_t s)
+  {
+    hipError_t e = hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+      e = hipEventRecord(done, s);
+    }
+    used = e == hipSuccess;
+    return e;
+  }
+};
+
 inline size_t align_up(size_t n, size_t a)
 {
   return (n + a - 1) / a * a;

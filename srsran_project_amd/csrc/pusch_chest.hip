@@ -161,8 +161,10 @@ __device__ __forceinline__ uint32_t dmrs_nof_words(const chest_args& a, uint32_t
 }
 
 // One workgroup: the DM-RS Gold words of the batch (jump-ahead, one word per thread) into a.dmrs_seq.
-__global__ __launch_bounds__(CS_THREADS) void chest_seq_kernel(chest_args a)
+template <bool MULTI>
+__global__ __launch_bounds__(CS_THREADS) void chest_seq_kernel(chest_args a_in, chest_items items)
 {
+  const chest_args& a = item_args<MULTI>(a_in, items);
   uint32_t       w_first;
   const uint32_t nwords = dmrs_nof_words(a, w_first);
   for (uint32_t i = threadIdx.x; i < nwords * a.nds; i += CS_THREADS) {
@@ -186,8 +188,13 @@ __device__ __forceinline__ uint32_t dmrs_words(const chest_args& a, uint32_t (*s
 // One workgroup per (grid, rx port): EPRE over every received DM-RS RE and the CFO from the first two DM-RS
 // symbols over every layer of every CDM group (preprocess_pilots_and_estimate_cfo, :390-445), for the
 // slice workgroups of the port.
-__global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a)
+template <bool MULTI>
+__global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a_in, chest_items items)
 {
+  const chest_args& a = item_args<MULTI>(a_in, items);
+  if (MULTI && blockIdx.x >= a.nof_ports) {
+    return; // slot form: the launch covers the largest item
+  }
   __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
   __shared__ float    red[4 * 16];
   const uint32_t      gp   = blockIdx.x;
@@ -261,8 +268,13 @@ __global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a)
 // (rx * conj(pilot)), CFO compensation and time accumulation, CDM pair averaging (lane shuffle), scaling, FD
 // smoothing in LDS (mean, or virtual pilots + raised-cosine FIR), the slice's RSRP share, linear
 // interpolation to every RE of the allocation (port_channel_estimator_average_impl.cpp:130-506).
-__global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a)
+template <bool MULTI>
+__global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in, chest_items items)
 {
+  const chest_args& a = item_args<MULTI>(a_in, items);
+  if (MULTI && (blockIdx.x >= a.nof_ports || blockIdx.y >= a.L * a.nof_lse)) {
+    return;
+  }
   __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
   __shared__ float2   enl_in[CH_MAXPIL + 2 * CH_MAXV];
   __shared__ float2   enl_out[CH_MAXPIL + 2 * CH_MAXV];
@@ -432,9 +444,13 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a)
 // Time alignment, one workgroup per (grid, port, slice): the N-point IDFT of the slice's smoothed pilots
 // with the fused Stockham engine and |.|^2 into the slice's correlation row
 // (time_alignment_estimator_dft_impl.cpp:122-200).
-template <int N>
-__global__ __launch_bounds__(dft::plan<N>::T) void chest_ta_kernel(chest_args a)
+template <int N, bool MULTI>
+__global__ __launch_bounds__(dft::plan<N>::T) void chest_ta_kernel(chest_args a_in, chest_items items)
 {
+  const chest_args& a = item_args<MULTI>(a_in, items);
+  if (MULTI && (blockIdx.x >= a.nof_ports || blockIdx.y >= a.L * a.nof_lse)) {
+    return;
+  }
   using dft::cf;
   __shared__ cf  lds[dft::lds_complex<N>()];
   const uint32_t gp     = blockIdx.x;
@@ -459,8 +475,13 @@ __global__ __launch_bounds__(dft::plan<N>::T) void chest_ta_kernel(chest_args a)
 // reference accumulates them symbol-major; the sum is order-free up to rounding), the peak search and
 // quadratic refinement (time_alignment_estimator_dft_impl.cpp:248-310) and noise variance, EPRE, RSRP,
 // SNR and CFO (do_compute tail, port_channel_estimator_average_impl.cpp:160-199).
-__global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a)
+template <bool MULTI>
+__global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in, chest_items items)
 {
+  const chest_args& a = item_args<MULTI>(a_in, items);
+  if (MULTI && blockIdx.x >= a.nof_ports) {
+    return;
+  }
   __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
   __shared__ float    corr[CH_TA_MAXN];
   __shared__ float    red[4 * 16];
@@ -618,8 +639,13 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a)
 // allocation the time-domain strategy and bf16 rounding; the CFO phase then multiplies the
 // whole OFDM symbol (do_compute, port_channel_estimator_average_impl.cpp:184-193), so REs
 // outside the allocation are rotated in place, as the reference does.
-__global__ __launch_bounds__(256) void chest_expand_kernel(chest_args a)
+template <bool MULTI>
+__global__ __launch_bounds__(256) void chest_expand_kernel(chest_args a_in, chest_items items)
 {
+  const chest_args& a = item_args<MULTI>(a_in, items);
+  if (MULTI && blockIdx.y >= a.nof_ports * a.L) {
+    return;
+  }
   // one thread per subcarrier and (grid, port, layer): the LSE estimates of the subcarrier are read
   // once and every OFDM symbol of the allocation written from them
   __shared__ float2 s_ph[CH_NSYMB];
@@ -675,18 +701,18 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   if (nb == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(chest_seq_kernel, dim3(1), dim3(CS_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(chest_seq_kernel<false>, dim3(1), dim3(CS_THREADS), 0, stream, a, chest_items{});
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
   }
-  hipLaunchKernelGGL(chest_cfo_kernel, dim3(nb), dim3(CS_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(chest_cfo_kernel<false>, dim3(nb), dim3(CS_THREADS), 0, stream, a, chest_items{});
   e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
   }
   const dim3 slices(nb, a.L * a.nof_lse);
-  hipLaunchKernelGGL(chest_slice_kernel, slices, dim3(CS_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(chest_slice_kernel<false>, slices, dim3(CS_THREADS), 0, stream, a, chest_items{});
   e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
@@ -694,7 +720,7 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   switch (a.ta_n) {
 #define SRS_TA_CASE(NN)                                                                                               \
   case NN:                                                                                                            \
-    hipLaunchKernelGGL(chest_ta_kernel<NN>, slices, dim3(dft::plan<NN>::T), 0, stream, a);                           \
+    hipLaunchKernelGGL((chest_ta_kernel<NN, false>), slices, dim3(dft::plan<NN>::T), 0, stream, a, chest_items{});                           \
     break;
     SRS_TA_CASE(128)
     SRS_TA_CASE(256)
@@ -710,7 +736,7 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   if (e != hipSuccess) {
     return e;
   }
-  hipLaunchKernelGGL(chest_stats_kernel, dim3(nb), dim3(ST_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(chest_stats_kernel<false>, dim3(nb), dim3(ST_THREADS), 0, stream, a, chest_items{});
   e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
@@ -718,8 +744,61 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   if (!expand) {
     return hipSuccess; // the consumer rebuilds the estimates from a.freq / a.acc (chest_device.h)
   }
-  hipLaunchKernelGGL(chest_expand_kernel, dim3((a.nsubc + 255) / 256, nb * a.L), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(chest_expand_kernel<false>, dim3((a.nsubc + 255) / 256, nb * a.L), dim3(256), 0, stream, a,
+                     chest_items{});
   return hipGetLastError();
+}
+
+hipError_t launch_chest_items(const chest_items&                       items,
+                              uint32_t                                 nof_items,
+                              uint32_t                                 max_ports,
+                              uint32_t                                 max_slices,
+                              const std::vector<chest_ta_group>&       ta_groups,
+                              hipStream_t                              stream)
+{
+  if (nof_items == 0) {
+    return hipSuccess;
+  }
+  const chest_args none{};
+  hipLaunchKernelGGL(chest_seq_kernel<true>, dim3(1, 1, nof_items), dim3(CS_THREADS), 0, stream, none, items);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(chest_cfo_kernel<true>, dim3(max_ports, 1, nof_items), dim3(CS_THREADS), 0, stream, none,
+                       items);
+    e = hipGetLastError();
+  }
+  const dim3 slices(max_ports, max_slices, nof_items);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(chest_slice_kernel<true>, slices, dim3(CS_THREADS), 0, stream, none, items);
+    e = hipGetLastError();
+  }
+  // time alignment: one launch per IDFT size, over the items of that size (ids)
+  for (const chest_ta_group& g : ta_groups) {
+    if (e != hipSuccess) {
+      break;
+    }
+    const chest_items sub{items.items, g.ids};
+    const dim3        gs(max_ports, max_slices, g.count);
+    switch (g.n) {
+#define SRS_TA_CASE(NN)                                                                                                 case NN:                                                                                                                hipLaunchKernelGGL((chest_ta_kernel<NN, true>), gs, dim3(dft::plan<NN>::T), 0, stream, none, sub);                   break;
+      SRS_TA_CASE(128)
+      SRS_TA_CASE(256)
+      SRS_TA_CASE(512)
+      SRS_TA_CASE(1024)
+      SRS_TA_CASE(2048)
+      SRS_TA_CASE(4096)
+#undef SRS_TA_CASE
+      default:
+        return hipErrorInvalidValue;
+    }
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(chest_stats_kernel<true>, dim3(max_ports, 1, nof_items), dim3(ST_THREADS), 0, stream, none,
+                       items);
+    e = hipGetLastError();
+  }
+  return e;
 }
 
 } // namespace srs_amd

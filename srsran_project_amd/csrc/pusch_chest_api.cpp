@@ -19,6 +19,7 @@
 #include "pusch_chest_args.h"
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -66,6 +67,7 @@ struct srs_amd_pusch_chest {
   device_buffer scratch;
   device_buffer host_io;
   stream_order  order; // scratch reuse across the callers' streams
+  pinned_stage  stage; // slot form: per-PDU argument blocks
   std::mutex    mtx;
   ~srs_amd_pusch_chest()
   {
@@ -391,6 +393,110 @@ int srs_amd::chest_estimate_batch_unexpanded(::srs_amd_pusch_chest*            c
 {
   return estimate_batch_impl(chest, cfg, d_grids, grid_stride, nof_ports, nof_subc, nof_grids, nullptr, 0, d_stats,
                              stream, false, view);
+}
+
+int srs_amd::chest_estimate_slot_unexpanded(::srs_amd_pusch_chest* chest,
+                                            const chest_slot_item* items,
+                                            uint32_t               nof_items,
+                                            uint32_t               nof_subc,
+                                            void*                  stream,
+                                            chest_args*            views)
+{
+  if (chest == nullptr || (nof_items != 0 && (items == nullptr || views == nullptr))) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_items == 0) {
+    return SRS_AMD_OK;
+  }
+  // host argument blocks; per-PDU scratch laid out back to back (offsets first, pointers once allocated)
+  std::vector<size_t> offset(nof_items);
+  size_t              total      = 0;
+  uint32_t            max_ports  = 0;
+  uint32_t            max_slices = 0;
+  for (uint32_t i = 0; i != nof_items; ++i) {
+    int rc = make_args(views[i], items[i].cfg, items[i].nof_ports, nof_subc);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+    if (items[i].d_grid == nullptr || items[i].d_stats == nullptr) {
+      return fail(SRS_AMD_EINVAL, "null device buffer");
+    }
+    offset[i] = total;
+    total += align_up(scratch_bytes(views[i], 1), 256);
+    max_ports  = std::max(max_ports, views[i].nof_ports);
+    max_slices = std::max(max_slices, views[i].L * views[i].nof_lse);
+  }
+  // TA groups: item ids per IDFT size, after the argument blocks
+  std::vector<uint32_t> sizes;
+  for (uint32_t i = 0; i != nof_items; ++i) {
+    if (std::find(sizes.begin(), sizes.end(), views[i].ta_n) == sizes.end()) {
+      sizes.push_back(views[i].ta_n);
+    }
+  }
+  const size_t o_args = total;
+  const size_t o_ids  = o_args + align_up(sizeof(chest_args) * nof_items, 256);
+  const size_t stage  = o_ids - o_args + sizeof(uint32_t) * nof_items;
+  std::lock_guard<std::mutex> lock(chest->mtx);
+  hipError_t                  e = hipSetDevice(chest->device);
+  if (e == hipSuccess) {
+    e = chest->scratch.ensure(o_ids + sizeof(uint32_t) * nof_items);
+  }
+  if (e == hipSuccess) {
+    e = chest->stage.acquire(stage);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH channel estimator slot scratch");
+  }
+  auto*                       base = chest->scratch.as<uint8_t>();
+  auto*                       ids  = reinterpret_cast<uint32_t*>(base + o_ids);
+  std::vector<chest_ta_group> groups;
+  uint32_t*                   h_ids = chest->stage.at<uint32_t>(o_ids - o_args);
+  uint32_t                    n_ids = 0;
+  for (uint32_t n : sizes) {
+    chest_ta_group g{n, 0, ids + n_ids};
+    for (uint32_t i = 0; i != nof_items; ++i) {
+      if (views[i].ta_n == n) {
+        h_ids[n_ids++] = i;
+        ++g.count;
+      }
+    }
+    groups.push_back(g);
+  }
+  for (uint32_t i = 0; i != nof_items; ++i) {
+    chest_args& a = views[i];
+    uint8_t*    b = base + offset[i];
+    a.filt        = reinterpret_cast<float2*>(b);
+    b += align_up(static_cast<size_t>(a.nof_ports) * a.L * a.nof_lse * a.npil * 8, 256);
+    a.freq = reinterpret_cast<float2*>(b);
+    b += align_up(static_cast<size_t>(a.nof_ports) * a.L * a.nof_lse * a.nof_re * 8, 256);
+    a.acc = reinterpret_cast<float*>(b);
+    b += align_up(static_cast<size_t>(a.nof_ports) * CH_ACC * 4, 256);
+    a.corr = reinterpret_cast<float*>(b);
+    b += align_up(static_cast<size_t>(a.nof_ports) * a.L * a.nof_lse * a.ta_n * 4, 256);
+    a.dmrs_seq    = reinterpret_cast<uint32_t*>(b);
+    a.grids       = items[i].d_grid;
+    a.grid_stride = 0;
+    a.estimates   = nullptr;
+    a.est_stride  = 0;
+    a.stats       = items[i].d_stats;
+    a.jump        = chest->d_jump;
+    a.ta_tw       = chest->tw(a.ta_n);
+  }
+  std::memcpy(chest->stage.at<chest_args>(0), views, sizeof(chest_args) * nof_items);
+  auto s = static_cast<hipStream_t>(stream);
+  e      = chest->order.begin(s);
+  if (e != hipSuccess) {
+    return hip_fail(e, "channel estimator slot launch");
+  }
+  call_scope scope(chest->order, nullptr, s);
+  e = chest->stage.upload(base + o_args, stage, s);
+  if (e == hipSuccess) {
+    const chest_items all{reinterpret_cast<const chest_args*>(base + o_args), nullptr};
+    e = launch_chest_items(all, nof_items, max_ports, max_slices, groups, s);
+  }
+  const hipError_t done = scope.close();
+  e                     = e != hipSuccess ? e : done;
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "channel estimator slot launch");
 }
 
 extern "C" {

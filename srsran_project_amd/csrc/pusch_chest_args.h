@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "srsran_amd/pusch_chest.h"
 
@@ -74,6 +75,44 @@ struct chest_args {
   float    scs_hz;
 };
 
+// Slot form (several PDUs of one grid, srs_amd_pusch_process_slot): one argument block per work item (one PDU on
+// one grid, nof_ports of its own, grids / scratch / stats pointers of its own) in device memory; the kernels of a
+// launch take item ids[blockIdx.z] (ids == nullptr: item blockIdx.z), so launches grouped by a template parameter
+// (the time-alignment IDFT size) cover a subset of the items.
+struct chest_items {
+  const chest_args* items = nullptr;
+  const uint32_t*   ids   = nullptr;
+};
+
+// The argument block of this workgroup: the launch's own (batch forms) or its item's (slot form); uniform
+// addresses of memory no kernel of the launch writes, so the fields are scalar loads.
+template <bool MULTI>
+__device__ __forceinline__ const chest_args& item_args(const chest_args& a, const chest_items& m)
+{
+  if constexpr (MULTI) {
+    const uint32_t z = m.ids != nullptr ? m.ids[blockIdx.z] : blockIdx.z;
+    return m.items[z];
+  } else {
+    return a;
+  }
+}
+
+// Items sharing one time-alignment IDFT size (ids: device array of count item indices).
+struct chest_ta_group {
+  uint32_t        n;
+  uint32_t        count;
+  const uint32_t* ids;
+};
+
+// The slot form's pilot, time-alignment and statistics kernels over nof_items items (no expansion: the fused
+// equalizer consumes freq / acc).  max_ports / max_slices: the largest nof_ports / L x nof_lse of the items.
+hipError_t launch_chest_items(const chest_items&                 items,
+                              uint32_t                           nof_items,
+                              uint32_t                           max_ports,
+                              uint32_t                           max_slices,
+                              const std::vector<chest_ta_group>& ta_groups,
+                              hipStream_t                        stream);
+
 // expand = false: pilot and time-alignment kernels only -- the per-subcarrier estimates (freq) and the
 // per-port accumulators (acc) stay in the estimator's scratch for a consumer that rebuilds each RE's
 // estimate itself (the PUSCH demodulator's fused equalizer, chest_device.h).
@@ -92,5 +131,24 @@ int chest_estimate_batch_unexpanded(::srs_amd_pusch_chest*            chest,
                                     srs_amd_chest_port_stats*         d_stats,
                                     void*                             stream,
                                     chest_args*                       view);
+
+// One PDU of a slot (srs_amd_pusch_process_slot): its estimator configuration, the grid it occupies
+// (cbf16 [port][14][nof_subc], shared with the slot's other PDUs) and its nof_ports port measurements.
+struct chest_slot_item {
+  const srs_amd_pusch_chest_config* cfg;
+  const uint32_t*                   d_grid;
+  uint32_t                          nof_ports;
+  srs_amd_chest_port_stats*         d_stats;
+};
+
+// The unexpanded estimate of every PDU of a slot in one launch sequence (chest_items): per-PDU scratch and
+// argument blocks, TA launches grouped by IDFT size.  views[i] receives PDU i's argument block (host copy)
+// for the fused equalizer, valid until the next call on this estimator.
+int chest_estimate_slot_unexpanded(::srs_amd_pusch_chest*  chest,
+                                   const chest_slot_item*  items,
+                                   uint32_t                nof_items,
+                                   uint32_t                nof_subc,
+                                   void*                   stream,
+                                   chest_args*             views);
 
 } // namespace srs_amd

@@ -212,10 +212,25 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
 // identical cbf16 estimates), so the P x L x 14 x subcarrier estimate tensor is neither written nor read.
 constexpr uint32_t EQ_XCDS = 8;
 
-template <int P, int L, bool MMSE>
-// six waves per SIMD (<= 80 VGPRs, no spills for the 4 x 4 solve) to hide the per-RE memory latency
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void pusch_equalize_fused_kernel(pusch_eq_args a, chest_args c)
+template <bool MULTI>
+__device__ __forceinline__ const eq_item& eq_item_of(const eq_item& own, const eq_items& m)
 {
+  if constexpr (MULTI) {
+    const uint32_t z = m.ids != nullptr ? m.ids[blockIdx.y] : blockIdx.y;
+    return m.items[z];
+  } else {
+    return own;
+  }
+}
+
+template <int P, int L, bool MMSE, bool MULTI>
+// six waves per SIMD (<= 80 VGPRs, no spills for the 4 x 4 solve) to hide the per-RE memory latency
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void pusch_equalize_fused_kernel(eq_item own, eq_items items)
+{
+  // batch form: the launch's argument pair; slot form: the pair of PDU ids[blockIdx.y] (one grid per PDU)
+  const eq_item&       it = eq_item_of<MULTI>(own, items);
+  const pusch_eq_args& a  = it.a;
+  const chest_args&    c  = it.c;
   __shared__ float2 s_ph[P];
   __shared__ int    s_rot[P];
   __shared__ float  lt[4 * 2 * 16];
@@ -334,6 +349,11 @@ bool pusch_equalize_fusable(uint32_t nof_ports, uint32_t nof_layers, bool mmse, 
          (nof_ports == 1 || nof_ports == 2 || nof_ports == 4) && !(nof_layers == 3 && nof_ports != 4);
 }
 
+uint32_t pusch_equalize_fused_blocks(uint32_t nof_symbols, uint32_t nof_tiles)
+{
+  return EQ_XCDS * nof_symbols * ((nof_tiles + EQ_XCDS - 1) / EQ_XCDS);
+}
+
 hipError_t launch_pusch_equalize_fused(const pusch_eq_args& a, const chest_args& c, uint32_t nof_ports,
                                        uint32_t nof_layers, bool mmse, uint32_t span_subc, uint32_t nof_grids,
                                        hipStream_t stream)
@@ -344,10 +364,39 @@ hipError_t launch_pusch_equalize_fused(const pusch_eq_args& a, const chest_args&
   pusch_eq_args ax = a;
   ax.tiles_x       = (span_subc + 255) / 256;
   ax.nof_tiles     = ax.tiles_x * nof_grids;
-  const dim3 grid(EQ_XCDS * c.nof_symbols * ((ax.nof_tiles + EQ_XCDS - 1) / EQ_XCDS));
+  const dim3 grid(pusch_equalize_fused_blocks(c.nof_symbols, ax.nof_tiles));
 #define SRS_EQF_CASE(PP, LL, MM)                                                                                      \
   if (nof_ports == PP && nof_layers == LL && mmse == MM) {                                                            \
-    hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM>), grid, dim3(256), 0, stream, ax, c);                \
+    hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM, false>), grid, dim3(256), 0, stream, eq_item{ax, c},   \
+                       eq_items{});                                                                                   \
+    return hipGetLastError();                                                                                         \
+  }
+  SRS_EQF_CASE(1, 1, false)
+  SRS_EQF_CASE(2, 1, false)
+  SRS_EQF_CASE(4, 1, false)
+  SRS_EQF_CASE(2, 2, false)
+  SRS_EQF_CASE(4, 2, false)
+  SRS_EQF_CASE(4, 3, false)
+  SRS_EQF_CASE(4, 4, false)
+  SRS_EQF_CASE(2, 2, true)
+  SRS_EQF_CASE(4, 2, true)
+  SRS_EQF_CASE(4, 3, true)
+  SRS_EQF_CASE(4, 4, true)
+#undef SRS_EQF_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_pusch_equalize_fused_items(const eq_items& items, uint32_t count, uint32_t nof_ports,
+                                             uint32_t nof_layers, bool mmse, uint32_t max_blocks, hipStream_t stream)
+{
+  if (count == 0 || max_blocks == 0) {
+    return hipSuccess;
+  }
+  const dim3    grid(max_blocks, count);
+  const eq_item none{};
+#define SRS_EQF_CASE(PP, LL, MM)                                                                                      \
+  if (nof_ports == PP && nof_layers == LL && mmse == MM) {                                                            \
+    hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM, true>), grid, dim3(256), 0, stream, none, items);     \
     return hipGetLastError();                                                                                         \
   }
   SRS_EQF_CASE(1, 1, false)

@@ -19,6 +19,7 @@
 #include "pusch_demod_args.h"
 #include "srsran_amd/modulation.h"
 #include <algorithm>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -33,6 +34,8 @@ struct srs_amd_pusch_demodulator {
   stream_order        order; // scratch reuse across the callers' streams
   srs_amd_transform_precoder* tp = nullptr; // transform precoding plans, created on first use
   device_buffer       host_io;
+  device_buffer       slot_items; // slot form: per-PDU argument pairs
+  pinned_stage        stage;
   std::mutex          mtx;
   ~srs_amd_pusch_demodulator()
   {
@@ -216,6 +219,115 @@ int srs_amd::pusch_demodulate_batch_fused(::srs_amd_pusch_demodulator*      dem,
 {
   return demodulate_impl(dem, plan, d_grids, grid_stride, nullptr, 0, &chest_view, d_stats, d_llrs, llr_stride,
                          nof_grids, stream);
+}
+
+int srs_amd::pusch_demodulate_slot_fused(::srs_amd_pusch_demodulator* dem,
+                                         const demod_slot_item*       items,
+                                         uint32_t                     nof_items,
+                                         void*                        stream)
+{
+  if (dem == nullptr || (nof_items != 0 && items == nullptr)) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  // kernel groups (ports, layers, MMSE): item ids of each group, back to back
+  struct group {
+    uint32_t P, L;
+    bool     mmse;
+    uint32_t first, count, max_blocks;
+  };
+  std::vector<group>    groups;
+  std::vector<uint32_t> order;
+  std::vector<eq_item>  pairs(nof_items);
+  for (uint32_t i = 0; i != nof_items; ++i) {
+    const demod_slot_item& it = items[i];
+    const auto*            pl = it.plan;
+    if (pl == nullptr || it.chest_view == nullptr) {
+      return fail(SRS_AMD_EINVAL, "null argument");
+    }
+    if (it.d_grid == nullptr || it.d_stats == nullptr || (pl->args.nof_re != 0 && it.d_llrs == nullptr)) {
+      return fail(SRS_AMD_EINVAL, "null device buffer");
+    }
+    const chest_args& c = *it.chest_view;
+    if (pl->tp_subc != 0) {
+      return fail(SRS_AMD_EINVAL, "transform precoding is not supported by the slot form");
+    }
+    if (c.nof_ports != pl->nof_ports || c.L != pl->nof_layers || c.nsubc != pl->args.nof_subc ||
+        c.first_symbol != pl->args.first_symbol || c.nof_symbols != pl->nof_symbols ||
+        pl->args.first_subc < 12 * c.prb_lo || pl->args.first_subc + pl->span_subc > 12 * c.prb_lo + c.nof_re ||
+        !pusch_equalize_fusable(pl->nof_ports, pl->nof_layers, pl->mmse, c.nof_lse)) {
+      return fail(SRS_AMD_EINVAL, "channel estimator output does not match the demodulator plan");
+    }
+    pusch_eq_args a = pl->args;
+    a.grids         = it.d_grid;
+    a.grid_stride   = 0;
+    a.estimates     = nullptr;
+    a.est_stride    = 0;
+    a.stats         = it.d_stats;
+    a.llrs          = it.d_llrs;
+    a.llr_stride    = 0;
+    a.tiles_x       = (pl->span_subc + 255) / 256;
+    a.nof_tiles     = a.tiles_x;
+    pairs[i]        = eq_item{a, c};
+  }
+  for (uint32_t i = 0; i != nof_items; ++i) {
+    const auto* pl = items[i].plan;
+    if (pl->args.nof_re == 0 || pl->span_subc == 0) {
+      continue; // nothing to equalize
+    }
+    bool seen = false;
+    for (const group& g : groups) {
+      seen |= g.P == pl->nof_ports && g.L == pl->nof_layers && g.mmse == pl->mmse;
+    }
+    if (seen) {
+      continue;
+    }
+    group g{pl->nof_ports, pl->nof_layers, pl->mmse, static_cast<uint32_t>(order.size()), 0, 0};
+    for (uint32_t k = i; k != nof_items; ++k) {
+      const auto* q = items[k].plan;
+      if (q->args.nof_re != 0 && q->span_subc != 0 && q->nof_ports == g.P && q->nof_layers == g.L &&
+          q->mmse == g.mmse) {
+        order.push_back(k);
+        ++g.count;
+        g.max_blocks = std::max(g.max_blocks, pusch_equalize_fused_blocks(pairs[k].c.nof_symbols, pairs[k].a.nof_tiles));
+      }
+    }
+    groups.push_back(g);
+  }
+  if (groups.empty()) {
+    return SRS_AMD_OK;
+  }
+  const size_t o_ids = align_up(sizeof(eq_item) * nof_items, 256);
+  const size_t total = o_ids + sizeof(uint32_t) * order.size();
+  auto         s     = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(dem->mtx);
+  hipError_t                  e = hipSetDevice(dem->device);
+  if (e == hipSuccess) {
+    e = dem->slot_items.ensure(total);
+  }
+  if (e == hipSuccess) {
+    e = dem->stage.acquire(total);
+  }
+  if (e == hipSuccess) {
+    e = dem->order.begin(s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH demodulator slot descriptors");
+  }
+  call_scope scope(dem->order, nullptr, s);
+  std::memcpy(dem->stage.at<eq_item>(0), pairs.data(), sizeof(eq_item) * nof_items);
+  std::memcpy(dem->stage.at<uint32_t>(o_ids), order.data(), sizeof(uint32_t) * order.size());
+  auto* d = dem->slot_items.as<uint8_t>();
+  e       = dem->stage.upload(d, total, s);
+  for (const group& g : groups) {
+    if (e != hipSuccess) {
+      break;
+    }
+    const eq_items m{reinterpret_cast<const eq_item*>(d), reinterpret_cast<const uint32_t*>(d + o_ids) + g.first};
+    e = launch_pusch_equalize_fused_items(m, g.count, g.P, g.L, g.mmse, g.max_blocks, s);
+  }
+  const hipError_t done = scope.close();
+  e                     = e != hipSuccess ? e : done;
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_equalize_fused_kernel slot launch");
 }
 
 extern "C" {

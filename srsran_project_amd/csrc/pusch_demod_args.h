@@ -53,6 +53,35 @@ hipError_t launch_pusch_equalize_fused(const pusch_eq_args& a, const chest_args&
                                        uint32_t nof_layers, bool mmse, uint32_t span_subc, uint32_t nof_grids,
                                        hipStream_t stream);
 
+// Slot form of the fused equalizer (srs_amd_pusch_process_slot): one (equalizer, estimator) argument pair per
+// PDU, each on one grid (a.nof_tiles = a.tiles_x); a launch covers the PDUs ids[blockIdx.y] (ids == nullptr:
+// PDU blockIdx.y) of one (ports, layers, MMSE) kernel; max_blocks = the largest PDU's blockIdx.x extent.
+struct eq_item {
+  pusch_eq_args a;
+  chest_args    c;
+};
+struct eq_items {
+  const eq_item*  items = nullptr;
+  const uint32_t* ids   = nullptr;
+};
+hipError_t launch_pusch_equalize_fused_items(const eq_items& items, uint32_t count, uint32_t nof_ports,
+                                             uint32_t nof_layers, bool mmse, uint32_t max_blocks, hipStream_t stream);
+uint32_t   pusch_equalize_fused_blocks(uint32_t nof_symbols, uint32_t nof_tiles);
+
+// One PDU of a slot for pusch_demodulate_slot_fused: its plan, the estimator view of its unexpanded
+// estimates (chest_estimate_slot_unexpanded), its grid, port measurements and codeword LLR row.
+struct demod_slot_item {
+  const ::srs_amd_pusch_demod_plan* plan;
+  const chest_args*                 chest_view;
+  const uint32_t*                   d_grid;
+  const srs_amd_chest_port_stats*   d_stats;
+  int8_t*                           d_llrs;
+};
+int pusch_demodulate_slot_fused(::srs_amd_pusch_demodulator* dem,
+                                const demod_slot_item*       items,
+                                uint32_t                     nof_items,
+                                void*                        stream);
+
 // srs_amd_pusch_demodulate_batch with the estimator-fused equalizer (no estimate tensor).
 int pusch_demodulate_batch_fused(::srs_amd_pusch_demodulator*      dem,
                                  const ::srs_amd_pusch_demod_plan* plan,

@@ -13,10 +13,11 @@ __global__ __launch_bounds__(64) void pusch_result_kernel(pusch_result_args a)
   if (g >= a.nof_grids) {
     return;
   }
-  const srs_amd_chest_port_stats* st = a.stats + static_cast<size_t>(g) * a.nof_ports;
+  const uint32_t                  P  = a.port_counts != nullptr ? a.port_counts[g] : a.nof_ports;
+  const srs_amd_chest_port_stats* st = a.stats + static_cast<size_t>(g) * (a.stats_stride ? a.stats_stride : P);
   float    noise = 0.0f, rsrp = 0.0f, epre = 0.0f, best_snr = 0.0f;
   uint32_t best  = 0;
-  for (uint32_t p = 0; p < a.nof_ports; ++p) {
+  for (uint32_t p = 0; p < P; ++p) {
     noise += st[p].noise_var;
     rsrp += st[p].rsrp;
     epre += st[p].epre;
@@ -29,8 +30,8 @@ __global__ __launch_bounds__(64) void pusch_result_kernel(pusch_result_args a)
   r.data             = a.dec_results[g];
   const bool normal  = isfinite(noise) && fabsf(noise) >= 1.17549435e-38f;
   r.sinr_db          = 10.0f * log10f(normal ? rsrp / noise : 0.0f);
-  r.epre_db          = 10.0f * log10f(epre / static_cast<float>(a.nof_ports));
-  r.rsrp_db          = 10.0f * log10f(rsrp / static_cast<float>(a.nof_ports));
+  r.epre_db          = 10.0f * log10f(epre / static_cast<float>(P));
+  r.rsrp_db          = 10.0f * log10f(rsrp / static_cast<float>(P));
   r.time_alignment_s = st[best].time_alignment_s;
   a.results[g]       = r;
 }

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 using namespace srs_amd;
 
@@ -27,8 +28,9 @@ struct srs_amd_pusch_processor {
   srs_amd_pusch_demodulator*     demod  = nullptr;
   srs_amd_pusch_decoder*         dec    = nullptr;
   hipStream_t                    stream = nullptr; // host-call stream
-  device_buffer                  estimates, stats, llrs, dec_results, host_io;
+  device_buffer                  estimates, stats, llrs, dec_results, host_io, slot_ports;
   stream_order                   order;
+  pinned_stage                   stage; // slot form: per-PDU port counts
   std::mutex                     mtx;
   bool                           fuse = true; // SRSRAN_AMD_PUSCH_FUSED=0: always expand the estimates
   ~srs_amd_pusch_processor()
@@ -341,6 +343,131 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
     e = proc->order.end(s);
   }
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_result_kernel launch");
+}
+
+int srs_amd_pusch_process_slot(srs_amd_pusch_processor*        proc,
+                               const srs_amd_pusch_slot_pdu*   pdus,
+                               uint32_t                        nof_pdus,
+                               const uint32_t*                 d_grids,
+                               uint64_t                        grid_stride,
+                               uint32_t                        nof_grids,
+                               uint8_t*                        d_tbs,
+                               srs_amd_pusch_processor_result* d_results,
+                               void*                           stream)
+{
+  if (proc == nullptr || (nof_pdus != 0 && pdus == nullptr)) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_pdus == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_grids == nullptr || d_tbs == nullptr || d_results == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  constexpr uint32_t STATS_STRIDE = 4; // port measurements per PDU (at most four receive ports)
+  const uint32_t     nof_subc     = pdus[0].plan != nullptr ? pdus[0].plan->nof_subc : 0;
+  std::vector<size_t> llr_off(nof_pdus);
+  size_t              llr_bytes = 0;
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    const srs_amd_pusch_processor_plan* pl = pdus[i].plan;
+    if (pl == nullptr) {
+      return fail(SRS_AMD_EINVAL, "null plan");
+    }
+    const uint32_t P = pl->pdu.nof_rx_ports;
+    if (!pl->fusable || P > STATS_STRIDE) {
+      return fail(SRS_AMD_EINVAL, "PDU %u: the slot form needs the fused estimator-equalizer path", i);
+    }
+    if (!pl->dec_cfg.new_data) {
+      return fail(SRS_AMD_EINVAL, "PDU %u: HARQ retransmissions go through srs_amd_pusch_process_batch", i);
+    }
+    if (pl->nof_subc != nof_subc) {
+      return fail(SRS_AMD_EINVAL, "PDU %u: plans of different grid sizes", i);
+    }
+    if (pdus[i].grid >= nof_grids || (nof_grids > 1 && grid_stride < 14ull * nof_subc * P)) {
+      return fail(SRS_AMD_EINVAL, "PDU %u: grid index or grid stride out of range", i);
+    }
+    llr_off[i] = llr_bytes;
+    llr_bytes += align_up(pl->sch.cw_length, 64);
+  }
+  auto                        s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(proc->mtx);
+  hipError_t                  e = hipSetDevice(proc->device);
+  if (e == hipSuccess) {
+    e = proc->stats.ensure(static_cast<size_t>(nof_pdus) * STATS_STRIDE * sizeof(srs_amd_chest_port_stats));
+  }
+  if (e == hipSuccess) {
+    e = proc->llrs.ensure(std::max<size_t>(llr_bytes, 64));
+  }
+  if (e == hipSuccess) {
+    e = proc->dec_results.ensure(static_cast<size_t>(nof_pdus) * sizeof(srs_amd_pusch_decoder_result));
+  }
+  if (e == hipSuccess) {
+    e = proc->slot_ports.ensure(sizeof(uint32_t) * nof_pdus);
+  }
+  if (e == hipSuccess) {
+    e = proc->stage.acquire(sizeof(uint32_t) * nof_pdus);
+  }
+  if (e == hipSuccess) {
+    e = proc->order.begin(s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH processor slot scratch");
+  }
+  call_scope scope(proc->order, nullptr, s);
+  auto*      st   = proc->stats.as<srs_amd_chest_port_stats>();
+  auto*      llrs = proc->llrs.as<int8_t>();
+  // 1. channel estimation of every PDU (one launch sequence)
+  std::vector<chest_slot_item> citems(nof_pdus);
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    const srs_amd_pusch_processor_plan* pl = pdus[i].plan;
+    citems[i] = chest_slot_item{&pl->chest_cfg, d_grids + pdus[i].grid * grid_stride, pl->pdu.nof_rx_ports,
+                                st + static_cast<size_t>(i) * STATS_STRIDE};
+  }
+  std::vector<chest_args> views(nof_pdus);
+  int rc = chest_estimate_slot_unexpanded(proc->chest, citems.data(), nof_pdus, nof_subc, stream, views.data());
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  // 2. equalization, demapping and descrambling into each PDU's codeword LLR row (one launch per kernel kind)
+  std::vector<demod_slot_item> ditems(nof_pdus);
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    ditems[i] = demod_slot_item{pdus[i].plan->demod_plan, &views[i], citems[i].d_grid, citems[i].d_stats,
+                                llrs + llr_off[i]};
+  }
+  rc = pusch_demodulate_slot_fused(proc->demod, ditems.data(), nof_pdus, stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  // 3. UL-SCH decoding of every transport block of the slot (srs_amd_pusch_decode_slot)
+  std::vector<srs_amd_pusch_ue> ues(nof_pdus);
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    ues[i] = srs_amd_pusch_ue{pdus[i].plan->sch, llr_off[i], pdus[i].tb_offset};
+  }
+  rc = srs_amd_pusch_decode_slot(proc->dec, &pdus[0].plan->dec_cfg, ues.data(), nof_pdus, llrs, d_tbs,
+                                 proc->dec_results.as<srs_amd_pusch_decoder_result>(), stream);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  // 4. per-PDU results (decoder result + CSI from the PDU's own port measurements)
+  auto* h_ports = proc->stage.at<uint32_t>(0);
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    h_ports[i] = pdus[i].plan->pdu.nof_rx_ports;
+  }
+  e = proc->stage.upload(proc->slot_ports.ptr, sizeof(uint32_t) * nof_pdus, s);
+  if (e == hipSuccess) {
+    pusch_result_args a{};
+    a.dec_results  = proc->dec_results.as<srs_amd_pusch_decoder_result>();
+    a.stats        = st;
+    a.results      = d_results;
+    a.nof_grids    = nof_pdus;
+    a.nof_ports    = 0;
+    a.port_counts  = proc->slot_ports.as<uint32_t>();
+    a.stats_stride = STATS_STRIDE;
+    e              = launch_pusch_result(a, s);
+  }
+  const hipError_t done = scope.close();
+  e                     = e != hipSuccess ? e : done;
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_result_kernel slot launch");
 }
 
 int srs_amd_pusch_process(srs_amd_pusch_processor*            proc,

@@ -16,6 +16,9 @@ struct pusch_result_args {
   srs_amd_pusch_processor_result*     results;     // [grid]
   uint32_t                            nof_grids;
   uint32_t                            nof_ports;
+  // slot form: PDU g has port_counts[g] ports, its stats at stats + g * stats_stride
+  const uint32_t*                     port_counts  = nullptr;
+  uint32_t                            stats_stride = 0;
 };
 
 hipError_t launch_pusch_result(const pusch_result_args& a, hipStream_t stream);

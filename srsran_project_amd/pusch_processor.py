@@ -65,6 +65,13 @@ class PuschIntermediates(ctypes.Structure):
                 ("d_llrs", ctypes.c_void_p), ("llr_stride", ctypes.c_uint32)]
 
 
+class PuschSlotPdu(ctypes.Structure):
+    """``srs_amd_pusch_slot_pdu``: one PDU of srs_amd_pusch_process_slot."""
+
+    _fields_ = [("plan", ctypes.c_void_p), ("grid", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("tb_offset", ctypes.c_uint64)]
+
+
 def make_pdu(**kw):
     """PuschPdu with the reference benchmark's defaults (pusch_processor_benchmark.cpp:396-431)."""
     d = dict(numerology=1, slot_index=0, rnti=1, bwp_start_rb=0, bwp_size_rb=51, modulation=2,
@@ -93,6 +100,7 @@ def _declare(lib):
         "srs_amd_pusch_processor_plan_destroy": (None, [P]),
         "srs_amd_pusch_process_batch": (c.c_int, [P, P, P, c.c_uint64, u, P, u, P, P, P, P]),
         "srs_amd_pusch_process": (c.c_int, [P, P, P, P, c.POINTER(PuschProcessorResult), P]),
+        "srs_amd_pusch_process_slot": (c.c_int, [P, c.POINTER(PuschSlotPdu), u, P, c.c_uint64, u, P, P, P]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -207,6 +215,31 @@ class PuschProcessor:
             None if io is None else ctypes.byref(io), ctypes.c_void_p(stream.cuda_stream)),
             "pusch_process_batch")
         return tbs, results
+
+    def process_slot(self, grids, pdus, tbs=None, results=None, stream=None):
+        """Device: every PDU of a slot in one launch sequence (uplink_processor_impl::process_pusch per PDU).
+        grids int32 [n][P][14][nsubc]; pdus: list of (plan, grid index). Returns (tbs uint8 flat, tb offsets,
+        results uint8 [len(pdus)][RESULT_BYTES])."""
+        import torch
+
+        dev = grids.device
+        offs, total = [], 0
+        for plan, _ in pdus:
+            offs.append(total)
+            total += (plan.tb_bytes + 63) // 64 * 64
+        if tbs is None:
+            tbs = torch.zeros(max(total, 1), dtype=torch.uint8, device=dev)
+        if results is None:
+            results = torch.zeros((len(pdus), RESULT_BYTES), dtype=torch.uint8, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        arr = (PuschSlotPdu * max(len(pdus), 1))()
+        for i, ((plan, g), off) in enumerate(zip(pdus, offs)):
+            arr[i] = PuschSlotPdu(plan._h.value, int(g), 0, off)
+        _lib.check(self._lib.srs_amd_pusch_process_slot(
+            self._h, arr, len(pdus), grids.data_ptr(), grids.stride(0), grids.shape[0], tbs.data_ptr(),
+            results.data_ptr(), ctypes.c_void_p(stream.cuda_stream)), "pusch_process_slot")
+        return tbs, offs, results
 
 
 def parse_results(results):

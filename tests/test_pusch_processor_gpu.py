@@ -159,3 +159,114 @@ def test_pusch_processor_fused_equalizer_identical(td, mask, eq):
         assert np.array_equal(a, b), what
     assert all(r.data.tb_crc_ok for r in amd.pusch_processor.parse_results(got[1][2]))
     assert np.array_equal(got[1][1][0], tb)
+
+
+def _to_complex(g):
+    f = np.stack([((g & 0xFFFF) << 16).view(np.float32), ((g >> 16) << 16).view(np.float32)], -1)
+    return f[..., 0] + 1j * f[..., 1]
+
+
+def _from_complex(z):
+    from oracle.pdsch_mod import to_bf16
+    return np.ascontiguousarray(to_bf16(z.real.astype(np.float32)).astype(np.uint32)
+                                | (to_bf16(z.imag.astype(np.float32)).astype(np.uint32) << 16))
+
+
+def _chan(L, P, seed):
+    rng = np.random.default_rng(seed)
+    h = np.eye(L, P) + 0.25 * (rng.normal(size=(L, P)) + 1j * rng.normal(size=(L, P)))
+    return (0.8 * h).astype(np.complex64)
+
+
+# Four UEs of one 273-PRB slot on four receive ports, disjoint PRBs, each with its own layers, modulation, code
+# rate, DM-RS symbols / CDM groups / scrambling identity / n_SCID, time allocation, rnti and n_id.
+SLOT_UES = [
+    dict(rnti=0x4601, n_id=1, scrambling_id=11, rb_start=0, rb_count=60, modulation=2, target_code_rate=679.0,
+         nof_tx_layers=1),
+    dict(rnti=0x4602, n_id=2, scrambling_id=22, n_scid=1, rb_start=60, rb_count=80, modulation=6,
+         target_code_rate=567.0, nof_tx_layers=2, dmrs_symbol_mask=(1 << 2) | (1 << 7) | (1 << 11)),
+    dict(rnti=0x4603, n_id=3, scrambling_id=33, rb_start=140, rb_count=60, modulation=4, target_code_rate=490.0,
+         nof_tx_layers=1, nof_cdm_groups_without_data=1, dmrs_symbol_mask=1 << 3, start_symbol_index=1,
+         nof_symbols=12),
+    dict(rnti=0x4604, n_id=4, scrambling_id=44, rb_start=200, rb_count=73, modulation=4, target_code_rate=378.0,
+         nof_tx_layers=2),
+]
+
+
+def _slot_case(slot_index=5, snr=28.0, seed=0, ue3_layers=2):
+    pdus, txs = [], []
+    z = 0
+    for u, over in enumerate(SLOT_UES):
+        pdu = dict(BASE, bwp_size_rb=273, nof_rx_ports=4, slot_index=slot_index, **over)
+        if u == 3:
+            pdu["nof_tx_layers"] = ue3_layers
+        tbs = _tbs(pdu)
+        pdu["base_graph"] = 2 if (tbs <= 292 or (tbs <= 3824 and pdu["target_code_rate"] / 1024 <= 0.67)
+                                  or pdu["target_code_rate"] / 1024 <= 0.25) else 1
+        pdu["tbs"] = tbs
+        tb = np.random.default_rng(seed * 10 + u).integers(0, 256, tbs // 8, dtype=np.uint8)
+        g, _ = pp.ue_transmit(tb, pdu, 12 * 273, channel=_chan(pdu["nof_tx_layers"], 4, 40 + u))
+        z = z + _to_complex(g)
+        pdus.append(pdu)
+        txs.append(tb)
+    occ = np.abs(z) > 0
+    sigma = np.sqrt(float(np.mean(np.abs(z[occ]) ** 2)) / 10 ** (snr / 10) / 2)
+    rng = np.random.default_rng(100 + seed)
+    grid = _from_complex(z + sigma * (rng.normal(size=z.shape) + 1j * rng.normal(size=z.shape)))
+    return grid, pdus, txs
+
+
+@pytest.mark.parametrize("eq", [0, 1], ids=["zf", "mmse"])
+def test_pusch_slot_4ue_grid_vs_reference(eq):
+    """four PUSCH PDUs of one grid through srs_amd_pusch_process_slot (one launch sequence)
+    against the reference pusch_processor_impl called once per PDU on the same grid
+    (uplink_processor_impl.cpp:270-326): transport blocks, CRC flags and LDPC iteration statistics identical,
+    CSI within the estimator tolerances.  The MMSE run (no reference counterpart in the compiled processor)
+    gives UE 3 four layers (the 4 x 4 solve) and is pinned to the single-PDU batch form."""
+    import torch
+
+    iters = 6
+    grid, pdus, txs = _slot_case(ue3_layers=2 if eq == 0 else 4)
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=iters, equalizer=eq), device=0)
+    plans = [proc.plan(amd.make_pdu(**p), 12 * 273) for p in pdus]
+    g = torch.from_numpy(grid.view(np.int32)[None]).to("cuda:0")
+    out, offs, res = proc.process_slot(g, [(pl, 0) for pl in plans])
+    torch.cuda.synchronize()
+    out = out.cpu().numpy()
+    res = amd.pusch_processor.parse_results(res.cpu().numpy())
+    for u, (pdu, pl) in enumerate(zip(pdus, plans)):
+        got_tb = out[offs[u]:offs[u] + pl.tb_bytes]
+        if eq == 0:
+            want_tb, want = pp.ref_pusch_process(grid, pdu, pl.tb_bytes, iterations=iters)
+            assert bool(res[u].data.tb_crc_ok) == want["tb_crc_ok"], u
+            assert np.array_equal(got_tb, want_tb), u
+            assert res[u].data.nof_codeblocks_total == want["nof_codeblocks_total"], u
+            assert res[u].data.ldpc_iterations_sum == want["iterations_sum"], (u, res[u].data.ldpc_iterations_sum,
+                                                                                 want)
+            assert res[u].data.ldpc_iterations_max == want["iterations_max"], u
+            _check_csi(res[u], want, "ue%d" % u)
+        assert res[u].data.tb_crc_ok and np.array_equal(got_tb, txs[u]), u
+        # per PDU identical to the single-PDU batch form on the same grid
+        b_tb, b_res = proc.process_batch(g, pl)
+        torch.cuda.synchronize()
+        b = amd.pusch_processor.parse_results(b_res.cpu().numpy())[0]
+        assert np.array_equal(b_tb[0].cpu().numpy(), got_tb), u
+        for k in ("sinr_db", "epre_db", "rsrp_db", "time_alignment_s"):
+            assert getattr(b, k) == getattr(res[u], k), (u, k)
+        assert b.data.ldpc_iterations_sum == res[u].data.ldpc_iterations_sum, u
+
+
+def test_pusch_slot_rejects_unsupported():
+    import torch
+
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(), device=0)
+    pdu = dict(BASE, tbs=_tbs(BASE))
+    g = torch.zeros((1, 1, 14, 12 * 51), dtype=torch.int32, device="cuda:0")
+    retx = proc.plan(amd.make_pdu(**dict(pdu, new_data=0)), 12 * 51)
+    with pytest.raises(ValueError):
+        proc.process_slot(g, [(retx, 0)])
+    ok = proc.plan(amd.make_pdu(**pdu), 12 * 51)
+    with pytest.raises(ValueError):
+        proc.process_slot(g, [(ok, 1)])  # grid index out of range
+    tbs, offs, res = proc.process_slot(g, [])
+    assert offs == [] and res.shape[0] == 0
