@@ -133,3 +133,207 @@ def run_sch_slot(args, dist, world, rank, dev, timed):
         "pusch_tbs_equal_sent": tb_equal,
         "per_ue_launches": per_ue,
     }
+
+
+class SlotPipeline:
+    """`bench.py --workload slot_pipeline`: the full PDSCH + PUSCH chains of cells whose 273 PRBs are shared by
+    `ues_per_cell` UEs (own PRBs, MCS, layers, rnti).  Per step and rank:
+      PDSCH  every UE's TB -> srs_amd_pdsch_encode_slot (one launch sequence) -> srs_amd_pdsch_modulate_slot
+             (data + DM-RS of every PDU of every cell: two launches) -> OFDM modulator (4 ports per cell);
+      PUSCH  OFDM demodulator (4 rx ports per cell) -> srs_amd_pusch_process_slot (estimator, fused equalizer,
+             slot decoder, results of every PDU of every cell: one launch sequence).
+    DL: 1-4 layers on 4 ports (DFT precoding), symbols 1-13.  UL: 1-2 layers (the reference-pinned ZF) through a
+    fixed channel + AWGN, symbols 0-13; the UE transmissions are synthesised before the timed region (the PDSCH
+    modulator as the UE transmitter, per-UE channel as its precoder) and every run checks the decoded TBs."""
+
+    def __init__(self, cells, ues_per_cell, dev, seed=0, iters=6, snr_db=35.0, ul_max_layers=2):
+        import torch
+
+        import bench_pipeline as bp
+        import srsran_project_amd as amd
+
+        self.torch, self.dev, self.S = torch, dev, cells
+        d = dev.index
+        rng = np.random.default_rng(777 + seed)
+        self.enc = amd.PdschEncoder(device=d)
+        self.mod = amd.PdschModulator(device=d)
+        self.proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=iters), device=d)
+        self.ofdm_mod = amd.OfdmSlotModulator(amd.OfdmModulatorConfiguration(bp.MU, NOF_PRB, bp.NFFT, 0, 1.0, 3.5e9),
+                                              device=d)
+        self.ofdm_dem = amd.OfdmSlotDemodulator(
+            amd.OfdmDemodulatorConfiguration(bp.MU, NOF_PRB, bp.NFFT, 0, 1.0, 3.5e9, 0), device=d)
+        nsubc = 12 * NOF_PRB
+        dl, ul, ue_tx = [], [], []   # (sch plan, mod plan, dmrs, cell) / (processor plan, cell) / UE TX
+        for c in range(cells):
+            n_id = int(rng.integers(0, 1008))
+            for side in ("dl", "ul"):
+                cuts = np.sort(rng.choice(np.arange(1, NOF_PRB), ues_per_cell - 1, replace=False))
+                edges = np.concatenate([[0], cuts, [NOF_PRB]])
+                for u in range(ues_per_cell):
+                    lo, hi = int(edges[u]), int(edges[u + 1])
+                    crbs = list(range(lo, hi))
+                    qm, r = MCS[rng.integers(len(MCS))]
+                    rnti = int(rng.integers(1, 65520))
+                    if side == "dl":
+                        layers = int(rng.integers(1, 5))
+                        w = bp.dl_weights(layers, 4)
+                        mp = self.mod.plan(amd.PdschModulatorConfig(
+                            rnti=rnti, bwp_start=0, bwp_size=NOF_PRB, modulation=qm, crbs=crbs, start_symbol=1,
+                            nof_symbols=13, dmrs_symb_pos=bp.DMRS_MASK, dmrs_type=1, nof_cdm_groups_without_data=2,
+                            n_id=n_id, precoding=w), nsubc)
+                        tbs = amd.tbs_calculator_calculate(13, 24, 0, qm, r, layers, 0, hi - lo)
+                        sp = amd.sch_plan(tbs, base_graph(tbs, r / 1024), 0, qm, 0, layers, mp.nof_re * layers)
+                        assert sp.cw_length == mp.nof_bits
+                        dm = amd.DmrsPdschConfig(slot_index=bp.SLOT, reference_point_k_rb=0, type=1,
+                                                 scrambling_id=n_id, n_scid=False, amplitude=bp.DMRS_AMP,
+                                                 symbols_mask=bp.DMRS_MASK, crbs=crbs, precoding=w)
+                        dl.append((sp, mp, dm, c))
+                    else:
+                        layers = int(rng.integers(1, ul_max_layers + 1))
+                        tbs = amd.tbs_calculator_calculate(14, 24, 0, qm, r, layers, 0, hi - lo)
+                        pdu = amd.make_pdu(numerology=bp.MU, slot_index=bp.SLOT, rnti=rnti, bwp_start_rb=0,
+                                           bwp_size_rb=NOF_PRB, modulation=qm, target_code_rate=r, rv=0,
+                                           base_graph=base_graph(tbs, r / 1024), new_data=1, n_id=n_id,
+                                           nof_tx_layers=layers, nof_rx_ports=4, dmrs_symbol_mask=bp.DMRS_MASK,
+                                           scrambling_id=n_id, n_scid=0, nof_cdm_groups_without_data=2, rb_start=lo,
+                                           rb_count=hi - lo, start_symbol_index=0, nof_symbols=14, tbs=tbs)
+                        pp = self.proc.plan(pdu, nsubc)
+                        h = bp.ul_channel(layers, 4)
+                        mp = self.mod.plan(amd.PdschModulatorConfig(
+                            rnti=rnti, bwp_start=0, bwp_size=NOF_PRB, modulation=qm, crbs=crbs, start_symbol=0,
+                            nof_symbols=14, dmrs_symb_pos=bp.DMRS_MASK, dmrs_type=1, nof_cdm_groups_without_data=2,
+                            n_id=n_id, precoding=h), nsubc)
+                        assert mp.nof_bits == pp.sch.cw_length
+                        dm = amd.DmrsPdschConfig(slot_index=bp.SLOT, reference_point_k_rb=0, type=1,
+                                                 scrambling_id=n_id, n_scid=False, amplitude=bp.DMRS_AMP,
+                                                 symbols_mask=bp.DMRS_MASK, crbs=crbs, precoding=h)
+                        ul.append((pp, c))
+                        ue_tx.append((pp.sch, mp, dm, c))
+        self.dl, self.ul = dl, ul
+        g = torch.Generator(device=dev)
+        g.manual_seed(4242 + d + 7919 * seed)
+        # ---- PDSCH: TBs, codewords, grids, samples ------------------------------------------------------------
+        self.tx_ues, tpos, cpos = [], 0, 0
+        for sp, _, _, _ in dl:
+            self.tx_ues.append((sp, tpos, cpos))
+            tpos += sp.tbs // 8
+            cpos += (sp.cw_length + 7) // 8 + 64
+        self.tb_dl = torch.randint(0, 256, (tpos,), device=dev, dtype=torch.uint8, generator=g)
+        self.cw_dl = torch.zeros(cpos, dtype=torch.uint8, device=dev)
+        self.tx_desc = amd.SlotUes(amd.PdschUe, self.tx_ues)
+        self.dl_slot = amd.PdschSlot([(mp, dm, c, co) for (sp, mp, dm, c), (_, _, co) in zip(dl, self.tx_ues)])
+        self.grid_dl = torch.zeros((cells, 4, 14, nsubc), dtype=torch.int32, device=dev)
+        self.samp_dl = torch.empty((cells, 4, self.ofdm_mod.max_slot_size()), dtype=torch.complex64, device=dev)
+        # ---- PUSCH: the UE transmissions (untimed), received grids, results -------------------------------------
+        ul_ues, tpos, cpos = [], 0, 0
+        for sp, _, _, _ in ue_tx:
+            ul_ues.append((sp, tpos, cpos))
+            tpos += sp.tbs // 8
+            cpos += (sp.cw_length + 7) // 8 + 64
+        self.tb_ul = torch.randint(0, 256, (tpos,), device=dev, dtype=torch.uint8, generator=g)
+        cw_ul = torch.zeros(cpos, dtype=torch.uint8, device=dev)
+        self.enc.encode_slot(self.tb_ul, ul_ues, out=cw_ul)
+        grid = torch.zeros((cells, 4, 14, nsubc), dtype=torch.int32, device=dev)
+        self.mod.modulate_slot(grid, amd.PdschSlot([(mp, dm, c, co) for (sp, mp, dm, c), (_, _, co)
+                                                    in zip(ue_tx, ul_ues)]), codewords=cw_ul)
+        samp = self.ofdm_mod.modulate_batch(grid.view(torch.int16).view(cells, 4, 14, 2 * nsubc), bp.SLOT)
+        p = float(torch.mean(torch.abs(samp) ** 2).item())
+        sigma = np.sqrt(p / 10 ** (snr_db / 10) / 2)
+        noise = torch.complex(torch.randn(samp.shape, device=dev, generator=g),
+                              torch.randn(samp.shape, device=dev, generator=g)) * sigma
+        self.samp_ul = (samp + noise.to(torch.complex64)).contiguous()
+        self.ul_tb_off = [to for _, to, _ in ul_ues]
+        self.ul_slot = amd.PuschSlot(ul)
+        self.grid_ul = torch.zeros((cells, 4, 14, nsubc), dtype=torch.int32, device=dev)
+        self.tb_rx = torch.zeros(max(self.ul_slot.tb_total, 1), dtype=torch.uint8, device=dev)
+        self.res_ul = torch.zeros((len(ul), amd.pusch_processor.RESULT_BYTES), dtype=torch.uint8, device=dev)
+        self.ul_stream = None
+        torch.cuda.synchronize(dev)
+
+    def pdsch(self, stream):
+        import bench_pipeline as bp
+
+        t = self.torch
+        self.enc.encode_slot(self.tb_dl, self.tx_desc, out=self.cw_dl, stream=stream)
+        self.mod.modulate_slot(self.grid_dl, self.dl_slot, codewords=self.cw_dl, stream=stream)
+        self.ofdm_mod.modulate_batch(self.grid_dl.view(t.int16).view(self.S, 4, 14, 2 * 12 * NOF_PRB), bp.SLOT,
+                                     out=self.samp_dl, stream=stream)
+
+    def pusch(self, stream):
+        import bench_pipeline as bp
+
+        t = self.torch
+        self.ofdm_dem.demodulate_batch(self.samp_ul, bp.SLOT,
+                                       grid=self.grid_ul.view(t.int16).view(self.S, 4, 14, 2 * 12 * NOF_PRB),
+                                       stream=stream)
+        self.proc.process_slot(self.grid_ul, self.ul_slot, tbs=self.tb_rx, results=self.res_ul, stream=stream)
+
+    def step(self, stream):
+        """Both chains of every cell, concurrently on two HIP streams (fork / join on `stream`)."""
+        t = self.torch
+        if self.ul_stream is None:
+            self.ul_stream = t.cuda.Stream(self.dev)
+            self.ev_fork, self.ev_join = t.cuda.Event(), t.cuda.Event()
+        self.ev_fork.record(stream)
+        self.ul_stream.wait_event(self.ev_fork)
+        with t.cuda.stream(stream):
+            self.pdsch(stream)
+        with t.cuda.stream(self.ul_stream):
+            self.pusch(self.ul_stream)
+        self.ev_join.record(self.ul_stream)
+        stream.wait_event(self.ev_join)
+
+    def check(self):
+        """Fraction of PUSCH TBs with CRC ok and equal to what the UE sent, mean LDPC iterations per codeblock."""
+        import srsran_project_amd as amd
+
+        res = amd.pusch_processor.parse_results(self.res_ul.cpu().numpy())
+        rx, tx = self.tb_rx.cpu().numpy(), self.tb_ul.cpu().numpy()
+        ok = []
+        for (pp, _), r, off, toff in zip(self.ul, res, self.ul_slot.offsets, self.ul_tb_off):
+            n = pp.tb_bytes
+            ok.append(bool(r.data.tb_crc_ok) and np.array_equal(rx[off:off + n], tx[toff:toff + n]))
+        its = sum(r.data.ldpc_iterations_sum for r in res) / max(1, sum(r.data.nof_codeblocks_total for r in res))
+        return float(np.mean(ok)), float(its)
+
+    def codeblocks(self):
+        return (sum(sp.nof_segments for sp, _, _, _ in self.dl), sum(pp.sch.nof_segments for pp, _ in self.ul))
+
+
+def run_slot_pipeline(args, dist, world, rank, dev, timed):
+    import torch
+
+    cells = args.slots_pipeline
+    pl = SlotPipeline(cells, args.ues_per_cell, dev, seed=rank, iters=args.iters, snr_db=args.snr_db)
+    stream = torch.cuda.current_stream(dev)
+    elapsed, step_ms = timed(args, dist, world, dev, stream, lambda: pl.step(stream))
+    torch.cuda.synchronize(dev)
+    ok, its = pl.check()
+    cb_dl, cb_ul = pl.codeblocks()
+    if rank != 0:
+        return None
+    return {
+        "metric": "PDSCH+PUSCH codeblocks/s, multi-UE slots (per-UE PRBs / MCS / layers / rnti on shared grids)",
+        "value": (cb_dl + cb_ul) * args.steps * world / elapsed,
+        "unit": "codeblocks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8 LLR / bf16 grid / f32 DSP",
+        "data": "synthetic (random TBs; UE transmissions through fixed channels + AWGN at %.1f dB)" % args.snr_db,
+        "config": {
+            "workload": "slot_pipeline: %d cells x %d DL + %d UL UEs (273 PRB split at random, MCS QPSK..256QAM, "
+                        "DL 1-4 layers x 4 ports, UL 1-2 layers x 4 rx ports, ZF)"
+                        % (cells, args.ues_per_cell, args.ues_per_cell),
+            "pdus_per_step_per_gpu": len(pl.dl) + len(pl.ul),
+            "codeblocks_per_step_per_gpu": {"pdsch": cb_dl, "pusch": cb_ul},
+            "parallelism": "cells sharded over ranks" if world > 1 else "single GPU",
+        },
+        "step_event_ms": step_ms,
+        "pusch_tb_ok_fraction": ok,
+        "pusch_mean_ldpc_iterations": its,
+    }

@@ -138,6 +138,34 @@ int srs_amd_dmrs_pdsch_map_batch(srs_amd_pdsch_modulator*         mod,
                                  uint32_t                         nof_grids,
                                  void*                            stream);
 
+/* One PDSCH PDU of a slot (srs_amd_pdsch_modulate_slot): its data (plan + codeword) and its DM-RS. */
+typedef struct srs_amd_pdsch_slot_pdu {
+  const srs_amd_pdsch_mod_plan*    plan;      /* NULL: no data (DM-RS only) */
+  const srs_amd_dmrs_pdsch_config* dmrs;      /* NULL: no DM-RS */
+  uint32_t                         grid;      /* index of the grid in d_grids */
+  uint32_t                         nof_bits;  /* codeword length (nof_re x layers x Qm) */
+  uint64_t                         cw_offset; /* byte offset of the packed codeword in d_codewords */
+} srs_amd_pdsch_slot_pdu;
+
+/* DEVICE, asynchronous: every PDSCH PDU of a slot -- several UEs on disjoint PRBs of one grid (or of several
+ * grids), each with its own PRBs, symbols, layers, modulation, precoding, rnti / n_id, reserved REs and DM-RS
+ * configuration -- as TWO launches (all data REs, then all DM-RS), per-PDU argument blocks in device memory.
+ * Replaces calling pdsch_modulator::modulate and dmrs_pdsch_processor::map once per PDU
+ * (pdsch_processor_impl.cpp:80 modulate + DM-RS per PDU, reached once per PDU from
+ * downlink_processor_multi_executor_impl.cpp:104 process_pdsch).  Grid writes
+ * per PDU identical to srs_amd_pdsch_modulate_batch / srs_amd_dmrs_pdsch_map_batch on that grid; PDUs
+ * sharing a grid must not write the same RE (the order between them is unspecified).  Plans created for
+ * nof_subc subcarriers. */
+int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
+                                const srs_amd_pdsch_slot_pdu* pdus,
+                                uint32_t                      nof_pdus,
+                                uint32_t*                     d_grids,
+                                uint64_t                      grid_stride,
+                                uint32_t                      nof_grids,
+                                uint32_t                      nof_subc,
+                                const uint8_t*                d_codewords,
+                                void*                         stream);
+
 #ifdef __cplusplus
 }
 #endif

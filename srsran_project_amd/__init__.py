@@ -64,6 +64,8 @@ from .pdsch_modulator import (  # noqa: F401
     PdschModPlan,
     PdschModulator,
     PdschModulatorConfig,
+    PdschSlot,
+    PdschSlotPdu,
     ReservedPattern,
 )
 
@@ -81,6 +83,7 @@ from .pusch_processor import (  # noqa: F401
     PuschPdu,
     PuschProcessor,
     PuschProcessorConfig,
+    PuschSlot,
     PuschSlotPdu,
     PuschProcessorPlan,
     PuschProcessorResult,

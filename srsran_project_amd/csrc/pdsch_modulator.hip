@@ -90,8 +90,24 @@ __device__ __forceinline__ uint32_t codeword_word(const uint8_t* cw, uint32_t no
 
 constexpr int MAX_WORDS = PDSCH_THREADS + 2; // 256 REs x 4 layers x 8 bits / 32 + 2
 
-__global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args a)
+// The argument block of this workgroup: the launch's own (batch form) or that of PDU blockIdx.z (slot form).
+template <bool MULTI, typename T>
+__device__ __forceinline__ const T& item_of(const T& own, const T* items)
 {
+  if constexpr (MULTI) {
+    return items[blockIdx.z];
+  } else {
+    return own;
+  }
+}
+
+template <bool MULTI>
+__global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args own, const pdsch_map_args* items)
+{
+  const pdsch_map_args& a = item_of<MULTI>(own, items);
+  if (MULTI && (blockIdx.x >= a.nof_tiles || blockIdx.y >= a.nof_symbols)) {
+    return;
+  }
   __shared__ uint32_t scrambled[MAX_WORDS];
   __shared__ float2   s_qam[256]; // constellation point of every Qm-bit index (qm >= 2)
 
@@ -171,10 +187,12 @@ __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args
   }
 }
 
-__global__ __launch_bounds__(64) void dmrs_pdsch_kernel(dmrs_pdsch_args a)
+template <bool MULTI>
+__global__ __launch_bounds__(64) void dmrs_pdsch_kernel(dmrs_pdsch_args own, const dmrs_pdsch_args* items)
 {
-  const uint32_t i = blockIdx.x * 64 + threadIdx.x; // allocated CRB
-  if (i >= a.nof_crb) {
+  const dmrs_pdsch_args& a = item_of<MULTI>(own, items);
+  const uint32_t         i = blockIdx.x * 64 + threadIdx.x; // allocated CRB
+  if (i >= a.nof_crb || (MULTI && blockIdx.y >= a.nof_dmrs_symbols)) {
     return;
   }
   const uint32_t l   = a.symbol[blockIdx.y];
@@ -224,7 +242,7 @@ hipError_t launch_pdsch_map(const pdsch_map_args& a, uint32_t nof_symbols, uint3
     return hipSuccess;
   }
   const dim3 grid((span_subc + PDSCH_THREADS - 1) / PDSCH_THREADS, nof_symbols, nof_cws);
-  hipLaunchKernelGGL(pdsch_map_kernel, grid, dim3(PDSCH_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(pdsch_map_kernel<false>, grid, dim3(PDSCH_THREADS), 0, stream, a, nullptr);
   return hipGetLastError();
 }
 
@@ -234,7 +252,29 @@ hipError_t launch_dmrs_pdsch(const dmrs_pdsch_args& a, uint32_t nof_grids, hipSt
     return hipSuccess;
   }
   const dim3 grid((a.nof_crb + 63) / 64, a.nof_dmrs_symbols, nof_grids);
-  hipLaunchKernelGGL(dmrs_pdsch_kernel, grid, dim3(64), 0, stream, a);
+  hipLaunchKernelGGL(dmrs_pdsch_kernel<false>, grid, dim3(64), 0, stream, a, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_pdsch_map_items(const pdsch_map_args* items, uint32_t count, uint32_t max_tiles,
+                                  uint32_t max_symbols, hipStream_t stream)
+{
+  if (count == 0 || max_tiles == 0 || max_symbols == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(pdsch_map_kernel<true>, dim3(max_tiles, max_symbols, count), dim3(PDSCH_THREADS), 0, stream,
+                     pdsch_map_args{}, items);
+  return hipGetLastError();
+}
+
+hipError_t launch_dmrs_pdsch_items(const dmrs_pdsch_args* items, uint32_t count, uint32_t max_crb_blocks,
+                                   uint32_t max_symbols, hipStream_t stream)
+{
+  if (count == 0 || max_crb_blocks == 0 || max_symbols == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(dmrs_pdsch_kernel<true>, dim3(max_crb_blocks, max_symbols, count), dim3(64), 0, stream,
+                     dmrs_pdsch_args{}, items);
   return hipGetLastError();
 }
 

@@ -20,7 +20,9 @@
 #include "gold_sequence.h"
 #include "modulation_args.h"
 #include "pdsch_modulator_args.h"
+#include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -31,6 +33,9 @@ struct srs_amd_pdsch_modulator {
   hipStream_t   stream = nullptr;
   uint32_t*     d_jump = nullptr;
   device_buffer scratch;
+  device_buffer slot_items; // slot form: per-PDU argument blocks
+  pinned_stage  stage;
+  stream_order  order;
   std::mutex    mtx;
   ~srs_amd_pdsch_modulator()
   {
@@ -245,6 +250,8 @@ int srs_amd_pdsch_mod_plan_create(srs_amd_pdsch_modulator*        mod,
   a.nof_layers            = static_cast<int32_t>(cfg->nof_layers);
   a.nof_ports             = static_cast<int32_t>(cfg->nof_ports);
   a.first_subc            = lo * 12;
+  a.nof_symbols           = cfg->nof_symbols;
+  a.nof_tiles             = (p->span_subc + PDSCH_THREADS - 1) / PDSCH_THREADS;
   float scaling           = modulation_scaling(cfg->modulation);
   if (std::isnormal(cfg->scaling)) {
     scaling *= cfg->scaling;
@@ -382,17 +389,12 @@ int srs_amd_pdsch_modulate(srs_amd_pdsch_modulator*      mod,
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PDSCH modulator download");
 }
 
-int srs_amd_dmrs_pdsch_map_batch(srs_amd_pdsch_modulator*         mod,
-                                 const srs_amd_dmrs_pdsch_config* cfg,
-                                 uint32_t*                        d_grids,
-                                 uint64_t                         grid_stride,
-                                 uint32_t                         nof_subc,
-                                 uint32_t                         nof_grids,
-                                 void*                            stream)
+} // extern "C"
+
+// The DM-RS argument block of cfg (dmrs_pdsch_processor_impl.cpp:40-90) for grids of nof_subc subcarriers.
+static int make_dmrs_args(const srs_amd_pdsch_modulator* mod, const srs_amd_dmrs_pdsch_config* cfg, uint32_t nof_subc,
+                          dmrs_pdsch_args& a)
 {
-  if (mod == nullptr || cfg == nullptr) {
-    return fail(SRS_AMD_EINVAL, "null argument");
-  }
   int rc = check_weights(cfg->nof_layers, cfg->nof_ports);
   if (rc != SRS_AMD_OK) {
     return rc;
@@ -403,10 +405,8 @@ int srs_amd_dmrs_pdsch_map_batch(srs_amd_pdsch_modulator*         mod,
   if (nof_subc == 0 || nof_subc % 12 != 0 || nof_subc > 12 * SRS_AMD_MAX_RB) {
     return fail(SRS_AMD_EINVAL, "Invalid number of grid subcarriers (i.e., %u).", nof_subc);
   }
-  dmrs_pdsch_args a{};
+  a = dmrs_pdsch_args{};
   a.jump                 = mod->d_jump;
-  a.grids                = d_grids;
-  a.grid_stride          = grid_stride;
   a.port_stride          = PDSCH_NSYMB * nof_subc;
   a.reference_point_k_rb = cfg->reference_point_k_rb;
   a.type2                = cfg->type == 2 ? 1 : 0;
@@ -442,6 +442,29 @@ int srs_amd_dmrs_pdsch_map_batch(srs_amd_pdsch_modulator*         mod,
       a.w[v][q][1] = cfg->weights[v][q][1];
     }
   }
+  return SRS_AMD_OK;
+}
+
+extern "C" {
+
+int srs_amd_dmrs_pdsch_map_batch(srs_amd_pdsch_modulator*         mod,
+                                 const srs_amd_dmrs_pdsch_config* cfg,
+                                 uint32_t*                        d_grids,
+                                 uint64_t                         grid_stride,
+                                 uint32_t                         nof_subc,
+                                 uint32_t                         nof_grids,
+                                 void*                            stream)
+{
+  if (mod == nullptr || cfg == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  dmrs_pdsch_args a;
+  int             rc = make_dmrs_args(mod, cfg, nof_subc, a);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  a.grids       = d_grids;
+  a.grid_stride = grid_stride;
   if (nof_grids == 0 || a.nof_crb == 0 || a.nof_dmrs_symbols == 0) {
     return SRS_AMD_OK;
   }
@@ -493,6 +516,116 @@ int srs_amd_dmrs_pdsch_map(srs_amd_pdsch_modulator*         mod,
     e = hipStreamSynchronize(mod->stream);
   }
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "DM-RS download");
+}
+
+int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
+                                const srs_amd_pdsch_slot_pdu* pdus,
+                                uint32_t                      nof_pdus,
+                                uint32_t*                     d_grids,
+                                uint64_t                      grid_stride,
+                                uint32_t                      nof_grids,
+                                uint32_t                      nof_subc,
+                                const uint8_t*                d_codewords,
+                                void*                         stream)
+{
+  if (mod == nullptr || (nof_pdus != 0 && pdus == nullptr)) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_pdus == 0) {
+    return SRS_AMD_OK;
+  }
+  if (d_grids == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  std::vector<pdsch_map_args>  maps;
+  std::vector<dmrs_pdsch_args> dmrs;
+  uint32_t                     max_tiles = 0, max_symbols = 0, max_blocks = 0, max_dmrs_symbols = 0;
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    const srs_amd_pdsch_slot_pdu& u = pdus[i];
+    if (u.grid >= nof_grids) {
+      return fail(SRS_AMD_EINVAL, "PDU %u: grid index %u out of range.", i, u.grid);
+    }
+    uint32_t* grid = d_grids + u.grid * grid_stride;
+    if (u.plan != nullptr) {
+      const pdsch_map_args& pa  = u.plan->args;
+      const uint32_t        bps = pa.qm < 2 ? 1u : static_cast<uint32_t>(pa.qm);
+      if (pa.nof_subc != nof_subc) {
+        return fail(SRS_AMD_EINVAL, "PDU %u: plan for %u subcarriers, grid of %u.", i, pa.nof_subc, nof_subc);
+      }
+      if (static_cast<uint64_t>(u.nof_bits) != static_cast<uint64_t>(u.plan->nof_re) * pa.nof_layers * bps) {
+        return fail(SRS_AMD_EINVAL, "PDU %u: the codeword length (i.e., %u bits) does not match the allocation.", i,
+                    u.nof_bits);
+      }
+      if (nof_grids > 1 && grid_stride < static_cast<uint64_t>(pa.nof_ports) * pa.port_stride) {
+        return fail(SRS_AMD_EINVAL, "grid stride too small");
+      }
+      if (d_codewords == nullptr) {
+        return fail(SRS_AMD_EINVAL, "null device buffer");
+      }
+      pdsch_map_args a = pa;
+      a.codewords      = d_codewords + u.cw_offset;
+      a.grids          = grid;
+      a.grid_stride    = 0;
+      a.cw_stride      = 0;
+      a.nof_bits       = u.nof_bits;
+      maps.push_back(a);
+      max_tiles   = std::max(max_tiles, a.nof_tiles);
+      max_symbols = std::max(max_symbols, a.nof_symbols);
+    }
+    if (u.dmrs != nullptr) {
+      dmrs_pdsch_args a;
+      int             rc = make_dmrs_args(mod, u.dmrs, nof_subc, a);
+      if (rc != SRS_AMD_OK) {
+        return rc;
+      }
+      if (nof_grids > 1 && grid_stride < static_cast<uint64_t>(a.nof_ports) * a.port_stride) {
+        return fail(SRS_AMD_EINVAL, "grid stride too small");
+      }
+      a.grids       = grid;
+      a.grid_stride = 0;
+      if (a.nof_crb != 0 && a.nof_dmrs_symbols != 0) {
+        dmrs.push_back(a);
+        max_blocks       = std::max(max_blocks, (a.nof_crb + 63) / 64);
+        max_dmrs_symbols = std::max(max_dmrs_symbols, a.nof_dmrs_symbols);
+      }
+    }
+  }
+  const size_t o_dmrs = align_up(sizeof(pdsch_map_args) * maps.size(), 256);
+  const size_t total  = o_dmrs + sizeof(dmrs_pdsch_args) * dmrs.size();
+  if (total == 0) {
+    return SRS_AMD_OK;
+  }
+  auto                        s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(mod->mtx);
+  hipError_t                  e = hipSetDevice(mod->device);
+  if (e == hipSuccess) {
+    e = mod->slot_items.ensure(total);
+  }
+  if (e == hipSuccess) {
+    e = mod->stage.acquire(total);
+  }
+  if (e == hipSuccess) {
+    e = mod->order.begin(s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PDSCH modulator slot descriptors");
+  }
+  call_scope scope(mod->order, nullptr, s);
+  std::memcpy(mod->stage.at<pdsch_map_args>(0), maps.data(), sizeof(pdsch_map_args) * maps.size());
+  std::memcpy(mod->stage.at<dmrs_pdsch_args>(o_dmrs), dmrs.data(), sizeof(dmrs_pdsch_args) * dmrs.size());
+  auto* d = mod->slot_items.as<uint8_t>();
+  e       = mod->stage.upload(d, total, s);
+  if (e == hipSuccess) {
+    e = launch_pdsch_map_items(reinterpret_cast<const pdsch_map_args*>(d), static_cast<uint32_t>(maps.size()),
+                               max_tiles, max_symbols, s);
+  }
+  if (e == hipSuccess) {
+    e = launch_dmrs_pdsch_items(reinterpret_cast<const dmrs_pdsch_args*>(d + o_dmrs),
+                                static_cast<uint32_t>(dmrs.size()), max_blocks, max_dmrs_symbols, s);
+  }
+  const hipError_t done = scope.close();
+  e                     = e != hipSuccess ? e : done;
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PDSCH modulator slot launch");
 }
 
 } // extern "C"

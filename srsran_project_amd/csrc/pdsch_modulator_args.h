@@ -31,6 +31,8 @@ struct pdsch_map_args {
   int32_t         nof_layers;
   int32_t         nof_ports;
   uint32_t        first_subc;  // first allocated subcarrier (grid.x offset)
+  uint32_t        nof_symbols; // slot form: blockIdx.y extent of this PDU
+  uint32_t        nof_tiles;   // slot form: blockIdx.x extent of this PDU
   float           w[4][4][2];  // [layer][port] weights x modulation scaling x config scaling
 };
 
@@ -56,5 +58,13 @@ struct dmrs_pdsch_args {
 hipError_t launch_pdsch_map(const pdsch_map_args& a, uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_cws,
                             hipStream_t stream);
 hipError_t launch_dmrs_pdsch(const dmrs_pdsch_args& a, uint32_t nof_grids, hipStream_t stream);
+
+// Slot form (srs_amd_pdsch_modulate_slot): one argument block per PDU in device memory (each on one grid and
+// codeword, strides 0), PDU blockIdx.z; the launch covers the largest PDU (max_tiles x max_symbols
+// workgroups, max_crb_blocks x max_symbols for the DM-RS) and each PDU's workgroups past its own extent exit.
+hipError_t launch_pdsch_map_items(const pdsch_map_args* items, uint32_t count, uint32_t max_tiles,
+                                  uint32_t max_symbols, hipStream_t stream);
+hipError_t launch_dmrs_pdsch_items(const dmrs_pdsch_args* items, uint32_t count, uint32_t max_crb_blocks,
+                                   uint32_t max_symbols, hipStream_t stream);
 
 } // namespace srs_amd

@@ -153,6 +153,13 @@ class DmrsPdschConfig:
         return c
 
 
+class PdschSlotPdu(ctypes.Structure):
+    """``srs_amd_pdsch_slot_pdu``: one PDU of srs_amd_pdsch_modulate_slot."""
+
+    _fields_ = [("plan", ctypes.c_void_p), ("dmrs", ctypes.c_void_p), ("grid", ctypes.c_uint32),
+                ("nof_bits", ctypes.c_uint32), ("cw_offset", ctypes.c_uint64)]
+
+
 def _declare(lib):
     c = ctypes
     P = c.c_void_p
@@ -166,6 +173,7 @@ def _declare(lib):
         "srs_amd_pdsch_modulate_batch": (c.c_int, [P, P, P, c.c_uint64, P, u, u, u, P]),
         "srs_amd_dmrs_pdsch_map": (c.c_int, [P, c.POINTER(_DmrsConfig), P, u, u]),
         "srs_amd_dmrs_pdsch_map_batch": (c.c_int, [P, c.POINTER(_DmrsConfig), P, c.c_uint64, u, u, P]),
+        "srs_amd_pdsch_modulate_slot": (c.c_int, [P, c.POINTER(PdschSlotPdu), u, P, c.c_uint64, u, u, P, P]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -285,3 +293,51 @@ class PdschModulator:
                                                           grids.shape[3], grids.shape[0],
                                                           ctypes.c_void_p(stream.cuda_stream)), "dmrs_pdsch_map_batch")
         return grids
+
+    def modulate_slot(self, grids, pdus, codewords=None, stream=None):
+        """Every PDSCH PDU of a slot in two launches. grids: torch int32 [n][ports][14][nof_subc].
+        pdus: a PdschSlot over the device codeword buffer `codewords` (uint8), or a list of (plan or None,
+        DmrsPdschConfig or None, grid index, packed host codeword bytes or None), staged here."""
+        import torch
+
+        if isinstance(pdus, PdschSlot):
+            slot = pdus
+        else:
+            offs, total = [], 0
+            for plan, _, _, _ in pdus:
+                offs.append(total)
+                total += 0 if plan is None else (plan.nof_bits // 8 + 64) // 64 * 64
+            host = np.zeros(max(total, 1), np.uint8)
+            for (plan, _, _, cw), off in zip(pdus, offs):
+                if plan is not None:
+                    b = np.ascontiguousarray(cw, np.uint8)
+                    if b.size * 8 < plan.nof_bits:
+                        raise ValueError("codeword shorter than the allocation")
+                    host[off:off + b.size] = b
+            codewords = torch.from_numpy(host).to(grids.device)
+            slot = PdschSlot([(p, d, g, o) for (p, d, g, _), o in zip(pdus, offs)])
+        if stream is None:
+            stream = torch.cuda.current_stream(grids.device)
+        _lib.check(self._lib.srs_amd_pdsch_modulate_slot(
+            self._h, slot.arr, slot.n, grids.data_ptr(), grids.stride(0), grids.shape[0], grids.shape[3],
+            None if codewords is None else codewords.data_ptr(), ctypes.c_void_p(stream.cuda_stream)),
+            "pdsch_modulate_slot")
+        if not isinstance(pdus, PdschSlot):
+            stream.synchronize()  # the staged codewords are released on return
+        return grids
+
+
+class PdschSlot:
+    """The srs_amd_pdsch_slot_pdu array of a slot, built once per slot configuration: pdus = list of
+    (plan or None, DmrsPdschConfig or None, grid index, codeword byte offset)."""
+
+    def __init__(self, pdus):
+        self.plans = [p for p, _, _, _ in pdus]  # keep the plans alive
+        self.dmrs = [None if d is None else d._c() for _, d, _, _ in pdus]
+        self.n = len(pdus)
+        self.arr = (PdschSlotPdu * max(self.n, 1))()
+        for i, (plan, _, g, off) in enumerate(pdus):
+            d = self.dmrs[i]
+            self.arr[i] = PdschSlotPdu(None if plan is None else plan._h.value,
+                                       None if d is None else ctypes.addressof(d), int(g),
+                                       0 if plan is None else plan.nof_bits, int(off))

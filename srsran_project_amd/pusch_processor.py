@@ -218,28 +218,39 @@ class PuschProcessor:
 
     def process_slot(self, grids, pdus, tbs=None, results=None, stream=None):
         """Device: every PDU of a slot in one launch sequence (uplink_processor_impl::process_pusch per PDU).
-        grids int32 [n][P][14][nsubc]; pdus: list of (plan, grid index). Returns (tbs uint8 flat, tb offsets,
-        results uint8 [len(pdus)][RESULT_BYTES])."""
+        grids int32 [n][P][14][nsubc]; pdus: a PuschSlot or a list of (plan, grid index). Returns (tbs uint8 flat,
+        tb offsets, results uint8 [len(pdus)][RESULT_BYTES])."""
         import torch
 
+        slot = pdus if isinstance(pdus, PuschSlot) else PuschSlot(pdus)
         dev = grids.device
-        offs, total = [], 0
-        for plan, _ in pdus:
-            offs.append(total)
-            total += (plan.tb_bytes + 63) // 64 * 64
         if tbs is None:
-            tbs = torch.zeros(max(total, 1), dtype=torch.uint8, device=dev)
+            tbs = torch.zeros(max(slot.tb_total, 1), dtype=torch.uint8, device=dev)
         if results is None:
-            results = torch.zeros((len(pdus), RESULT_BYTES), dtype=torch.uint8, device=dev)
+            results = torch.zeros((slot.n, RESULT_BYTES), dtype=torch.uint8, device=dev)
         if stream is None:
             stream = torch.cuda.current_stream(dev)
-        arr = (PuschSlotPdu * max(len(pdus), 1))()
-        for i, ((plan, g), off) in enumerate(zip(pdus, offs)):
-            arr[i] = PuschSlotPdu(plan._h.value, int(g), 0, off)
         _lib.check(self._lib.srs_amd_pusch_process_slot(
-            self._h, arr, len(pdus), grids.data_ptr(), grids.stride(0), grids.shape[0], tbs.data_ptr(),
+            self._h, slot.arr, slot.n, grids.data_ptr(), grids.stride(0), grids.shape[0], tbs.data_ptr(),
             results.data_ptr(), ctypes.c_void_p(stream.cuda_stream)), "pusch_process_slot")
-        return tbs, offs, results
+        return tbs, slot.offsets, results
+
+
+class PuschSlot:
+    """The srs_amd_pusch_slot_pdu array of a slot, built once per slot configuration: pdus = list of
+    (plan, grid index); transport block u at byte offsets[u] (64-byte aligned) of a tb_total-byte buffer."""
+
+    def __init__(self, pdus):
+        self.plans = [p for p, _ in pdus]  # keep the plans alive
+        self.n = len(pdus)
+        self.offsets, total = [], 0
+        for plan, _ in pdus:
+            self.offsets.append(total)
+            total += (plan.tb_bytes + 63) // 64 * 64
+        self.tb_total = total
+        self.arr = (PuschSlotPdu * max(self.n, 1))()
+        for i, ((plan, g), off) in enumerate(zip(pdus, self.offsets)):
+            self.arr[i] = PuschSlotPdu(plan._h.value, int(g), 0, off)
 
 
 def parse_results(results):
