@@ -446,7 +446,7 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         "ingest_ms_per_step": ingest_ms,
         "low_snr": low,
         "roofline": {
-            "bound": "valu",
+            "bound": "hbm",
             "kernel": "ldpc_decode_hr_kernel (PUSCH codeblocks of one step, BG%d Z=%d, CRC24B early stop, <= %d it; "
                       "the decoder reads the %d-LLR non-zero prefix of each soft-buffer row)"
                       % (pl.plan_ul.base_graph, pl.plan_ul.lifting_size, pl.iters,
@@ -458,20 +458,23 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
             "traffic": traffic,
             "kernel_ms": dec_ms,
             "algorithmic_bytes_per_launch": dec_bytes,
-            "valu_issue": valu,
-            "note": "HBM fraction of the decoder (algorithmic bytes / kernel time / 8 TB/s; PMC traffic = algorithmic, "
-                    "no re-reads). The kernel is latency-bound: valu_issue is its VALU-issue fraction (measured VALU "
-                    "wave-instructions x 2 cycles per wave64 instruction over 1,024 SIMDs at 2.4 GHz, "
-                    "profiles/ldpc_valu_model.json); PMC: ~40 % of wave time waiting on barriers / LDS",
+            "limiter": "valu",
+            "valu": valu,
+            "note": "bound/achieved/peak/frac: the decoder's HBM roofline (algorithmic bytes / measured kernel time / "
+                    "8 TB/s; PMC traffic = algorithmic bytes, no re-reads) -- far from HBM-bound.  Its limiter is VALU "
+                    "issue: valu.achieved_frac_of_peak_issue = modelled VALU issue cycles (PMC SQ_ACTIVE_INST_VALU "
+                    "per codeblock and iteration, profiles/ldpc_valu_model.json) / (1,024 SIMDs x 2.4 GHz x kernel "
+                    "time); the PMC-measured busy fraction of the same command is in profiles/r03_pmc_table.json",
         },
         "cpu_baseline": cpu,
     }
 
 
 def valu_bound(cbs, its_mean, kernel_ms):
-    """VALU-issue roofline of ldpc_decode_kernel from the committed PMC profile (profiles/*_ldpc_pmc.json:
-    VALU instructions per codeblock-iteration and per codeblock fixed): instructions x 2 cycles / (1024 SIMDs x
-    2.4 GHz) against the measured kernel time."""
+    """VALU-issue roofline of ldpc_decode_hr_kernel from the committed PMC model (profiles/ldpc_valu_model.json,
+    tools/pmc_valu_model.py: SQ_ACTIVE_INST_VALU issue cycles per codeblock, fixed + per iteration) scaled to this
+    launch's codeblocks and measured mean iterations: issue bound = cycles / (1,024 SIMDs x 2.4 GHz), frac = issue
+    bound / measured kernel time (1.0 = every SIMD issues VALU work every cycle of the kernel)."""
     import json
     import os
 
@@ -479,10 +482,16 @@ def valu_bound(cbs, its_mean, kernel_ms):
     if not os.path.exists(path):
         return None
     m = json.load(open(path))
-    valu_wave_instr = cbs * (m["valu_per_cb_fixed"] + m["valu_per_cb_iteration"] * its_mean)
-    issue_s = valu_wave_instr * 2 / (1024 * 2.4e9)
-    return {"valu_wave_instructions": valu_wave_instr, "issue_bound_ms": issue_s * 1e3,
-            "frac": issue_s * 1e3 / kernel_ms, "model": os.path.basename(path), "iterations_mean": its_mean}
+    if "valu_cycles_per_cb_fixed" in m:
+        cycles = cbs * (m["valu_cycles_per_cb_fixed"] + m["valu_cycles_per_cb_iteration"] * its_mean)
+        basis = "SQ_ACTIVE_INST_VALU issue cycles"
+    else:  # older model: instruction counts at 2 cycles per wave64 VALU instruction
+        cycles = 2 * cbs * (m["valu_per_cb_fixed"] + m["valu_per_cb_iteration"] * its_mean)
+        basis = "SQ_INSTS_VALU x 2 cycles"
+    issue_s = cycles / (1024 * 2.4e9)
+    return {"achieved_frac_of_peak_issue": issue_s * 1e3 / kernel_ms, "issue_bound_ms": issue_s * 1e3,
+            "kernel_ms": kernel_ms, "valu_issue_cycles": cycles, "basis": basis, "model": os.path.basename(path),
+            "iterations_mean": its_mean}
 
 
 def low_snr_line(args, dev, timed, dist):
