@@ -8,8 +8,11 @@
  *       (impl lib/phy/upper/signal_processors/pusch/dmrs_pusch_estimator_impl.cpp:28-184 with
  *        port_channel_estimator_average_impl.cpp, the channel estimator the PUSCH processor uses)
  *
- * Scope: pseudo-random DM-RS sequence (no transform precoding), DM-RS type 1,
- * 1..4 layers, 1..4 DM-RS symbols, one hop (no intra-slot frequency hopping),
+ * Scope: pseudo-random DM-RS sequence or, with transform precoding, the low-PAPR
+ * sequence (low_papr = 1: one layer, include/srsran_amd/low_papr.h), DM-RS type 1,
+ * 1..4 layers, 1..4 DM-RS symbols, one hop (the reference's PUSCH estimator has no
+ * hopping: dmrs_pusch_estimator::configuration carries one rb_mask and
+ * dmrs_pusch_estimator_impl.cpp:177-180 never sets a hopping symbol),
  * contiguous PRB allocation, all smoothing / interpolation / CFO options of
  * port_channel_estimator_average_impl. Type 2 is rejected: the reference's
  * linear interpolator reads past its pilot buffer for that pattern
@@ -60,6 +63,9 @@ typedef struct srs_amd_pusch_chest_config {
   int32_t  fd_smoothing;     /* SRS_AMD_CHEST_FD_* (PUSCH default: filter) */
   int32_t  td_interpolation; /* SRS_AMD_CHEST_TD_* (PUSCH default: average) */
   int32_t  compensate_cfo;   /* default 1 */
+  int32_t  low_papr;         /* transform precoding: low_papr_sequence_configuration (dmrs_pusch_estimator.h:67-77),
+                                one layer, sequence group n_rs_id mod 30, no scrambling_id / n_scid */
+  uint32_t n_rs_id;          /* {0 .. 1007} */
 } srs_amd_pusch_chest_config;
 
 /* channel_estimate per-port measurements (channel_estimation.h:125-190); rsrp,

@@ -23,9 +23,11 @@
  * get_ulsch_information without UCI (all data REs x layers), rb_mask of the
  * type-1 allocation relative to the BWP (:166).
  * Scope: data-only PUSCH (no UCI multiplexing, the pdu carries a codeword),
- * pseudo-random DM-RS type 1 (no transform precoding), no intra-slot frequency
- * hopping, no DC-carrier zeroing (pdu.dc_position unset), as the estimator and
- * demodulator C-ABIs support.
+ * DM-RS type 1 with the pseudo-random sequence, or transform precoding with the
+ * low-PAPR DM-RS (pusch_processor_impl.cpp:172-196, validator :148-174), no DC-carrier
+ * zeroing (pdu.dc_position unset). DM-RS type 2 is rejected as the reference's own
+ * validator rejects it (pusch_processor_validator_impl.cpp:151-154); the reference
+ * PUSCH has no intra-slot frequency hopping.
  */
 #ifndef SRSRAN_AMD_PUSCH_PROCESSOR_H
 #define SRSRAN_AMD_PUSCH_PROCESSOR_H
@@ -79,6 +81,10 @@ typedef struct srs_amd_pusch_pdu {
   uint32_t nof_symbols;
   uint32_t tbs_lbrm_bytes;    /* 0: tbs_lbrm_default (159749) */
   uint32_t tbs;               /* transport block size in bits (data.size() * 8) */
+  uint32_t transform_precoding; /* dmrs = dmrs_transform_precoding_configuration (DFT-s-OFDM): one layer, valid
+                                   PRB count, low-PAPR DM-RS of n_rs_id; dmrs_type / scrambling_id / n_scid /
+                                   nof_cdm_groups_without_data are then unused (two CDM groups, as the reference) */
+  uint32_t n_rs_id;           /* {0 .. 1007} */
 } srs_amd_pusch_pdu;
 
 /* Per-transport-block results: pusch_decoder_result (sch.h) and the channel

@@ -379,6 +379,18 @@ if REF is not None and hasattr(REF, "srs_ref_pusch_chest"):
                                              _c.c_void_p, _c.c_uint, _c.c_uint, _c.c_uint, _c.c_uint]
 
 
+if REF is not None and hasattr(REF, "srs_ref_low_papr"):
+    REF.srs_ref_low_papr.restype = None
+    REF.srs_ref_low_papr.argtypes = [_c.c_void_p, _c.c_uint, _c.c_uint, _c.c_uint]
+
+
+def ref_low_papr(M, u, v=0):
+    """The reference's low_papr_sequence_generator_impl::generate(sequence, u, v, 0, 1): complex64 [M]."""
+    out = np.zeros(M, np.complex64)
+    REF.srs_ref_low_papr(_ptr(out), M, u, v)
+    return out
+
+
 def ref_pusch_chest(grid, slot_index, type2, nof_layers, scrambling_id, n_scid, scaling, symbols_mask, prb_lo, prb_hi,
                     first_symbol, nof_symbols, fd=2, td=1, compensate_cfo=True, numerology=1, estimates=None):
     g = np.ascontiguousarray(grid, dtype=np.uint32)

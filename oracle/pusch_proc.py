@@ -56,11 +56,13 @@ def describe(choice="auto"):
 
 
 def ref_pusch_process(grid, pdu, tb_bytes, iterations=2, choice="auto", rx_buffer=None):
-    """grid uint32 [P][14][nsubc]; pdu: dict with the PuschPdu fields. Returns (tb, result dict)."""
+    """grid uint32 [P][14][nsubc]; pdu: dict with the PuschPdu fields (transform_precoding / n_rs_id: the
+    dmrs_transform_precoding_configuration). Returns (tb, result dict)."""
     if REF is None:
         raise RuntimeError("oracle/_ref not built")
     g = np.ascontiguousarray(grid, np.uint32)
     P, _, nsubc = g.shape
+    tp = bool(pdu.get("transform_precoding", 0))
     C = nof_codeblocks(tb_bytes * 8, pdu["base_graph"])
     buf = rx_buffer or RefRxBuffer(C)
     tb = np.zeros(tb_bytes, np.uint8)
@@ -69,7 +71,8 @@ def ref_pusch_process(grid, pdu, tb_bytes, iterations=2, choice="auto", rx_buffe
     r = REF.srs_ref_pusch_process(
         _ptr(g), P, nsubc, pdu["numerology"], pdu["slot_index"], pdu["rnti"], pdu["bwp_start_rb"], pdu["bwp_size_rb"],
         pdu["modulation"], float(pdu["target_code_rate"]), pdu["rv"], pdu["base_graph"], int(pdu["new_data"]),
-        pdu["n_id"], pdu["nof_tx_layers"], pdu["dmrs_symbol_mask"], 0, pdu["scrambling_id"], int(pdu["n_scid"]),
+        pdu["n_id"], pdu["nof_tx_layers"], pdu["dmrs_symbol_mask"], 2 if tp else 0,
+        pdu.get("n_rs_id", 0) if tp else pdu["scrambling_id"], int(pdu["n_scid"]),
         pdu["nof_cdm_groups_without_data"], pdu["rb_start"], pdu["rb_count"], pdu["start_symbol_index"],
         pdu["nof_symbols"], pdu.get("tbs_lbrm_bytes", 0), iterations, CHOICE[choice], buf.h, _ptr(tb), tb_bytes,
         _ptr(res), _ptr(csi))
@@ -120,4 +123,50 @@ def ue_transmit(tb, pdu, nsubc, channel=None, snr_db=None, seed=0, nof_rx_ports=
         z = z + sigma * (rng.normal(size=z.shape) + 1j * rng.normal(size=z.shape))
         g = (to_bf16(z.real.astype(np.float32)).astype(np.uint32)
              | (to_bf16(z.imag.astype(np.float32)).astype(np.uint32) << 16))
+    return np.ascontiguousarray(g), p
+
+
+def ue_transmit_tp(tb, pdu, nsubc, channel=None, snr_db=None, seed=0):
+    """UE PUSCH transmission with transform precoding (DFT-s-OFDM, TS 38.211 6.3.1.4 / 6.4.1.1.1.2): the
+    reference's PDSCH-style encoder chain for the codeword, the reference's Gold sequence and modulation mapper,
+    an M-point forward DFT scaled by 1/sqrt(M) per data OFDM symbol (numpy, float64 then float32), and the
+    reference's low-PAPR DM-RS (r_{n_rs_id mod 30, 0}) on the even subcarriers of the DM-RS symbols at the
+    two-CDM-group DM-RS amplitude; one layer through `channel` (complex [rx ports]) plus AWGN.
+    Returns the received grid uint32 [P][14][nsubc] (cbf16) and the UL-SCH plan."""
+    from . import ref_modulate, ref_prbs
+    from .chest import ref_low_papr
+    from .pdsch_mod import to_bf16
+
+    P = pdu["nof_rx_ports"]
+    channel = np.ones(P, np.complex64) if channel is None else np.asarray(channel, np.complex64).reshape(P)
+    crb0 = pdu["bwp_start_rb"] + pdu["rb_start"]
+    nrb = pdu["rb_count"]
+    M = 12 * nrb
+    dmrs = pdu["dmrs_symbol_mask"]
+    data_syms = [l for l in range(pdu["start_symbol_index"], pdu["start_symbol_index"] + pdu["nof_symbols"])
+                 if not (dmrs >> l) & 1]
+    qm = pdu["modulation"]
+    tbs = len(tb) * 8
+    p = osch.plan(tbs, pdu["base_graph"], pdu["rv"], qm, nref(tbs, pdu["base_graph"], pdu.get("tbs_lbrm_bytes", 0)),
+                  1, M * len(data_syms))
+    cw = ref_pdsch_encode(np.asarray(tb, np.uint8), p)
+    scr = cw ^ ref_prbs((pdu["rnti"] << 15) + pdu["n_id"], cw.size)
+    x = ref_modulate(np.packbits(scr), cw.size // qm, qm).reshape(len(data_syms), M)
+    y = (np.fft.fft(x.astype(np.complex128), axis=1) / np.sqrt(M)).astype(np.complex64)
+    z = np.zeros((P, 14, nsubc), np.complex64)
+    k0 = 12 * crb0
+    for i, l in enumerate(data_syms):
+        z[:, l, k0:k0 + M] = channel[:, None] * y[i][None, :]
+    amp = np.float32(dmrs_scaling(2))
+    r = ref_low_papr(M // 2, pdu.get("n_rs_id", 0) % 30, 0)
+    for l in range(14):
+        if (dmrs >> l) & 1:
+            z[:, l, k0:k0 + M:2] = channel[:, None] * (amp * r)[None, :]
+    if snr_db is not None:
+        occ = np.abs(z) > 0
+        pw = float(np.mean(np.abs(z[occ]) ** 2))
+        rng = np.random.default_rng(seed)
+        sigma = np.sqrt(pw / 10 ** (snr_db / 10) / 2)
+        z = z + sigma * (rng.normal(size=z.shape) + 1j * rng.normal(size=z.shape))
+    g = (to_bf16(z.real.astype(np.float32)).astype(np.uint32) | (to_bf16(z.imag.astype(np.float32)).astype(np.uint32) << 16))
     return np.ascontiguousarray(g), p

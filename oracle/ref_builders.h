@@ -14,8 +14,6 @@
 // Glue (interfaces implemented here; nothing of the reference is replaced):
 //   inline_executor       task_executor that runs tasks inline
 //                         (the benchmark's inline_task_executor);
-//   no_low_papr_generator low_papr_sequence_generator (only transform-precoded
-//                         DM-RS would call it; not used by the wrapped cases);
 //   no_uci_decoder        uci_decoder (the wrapped PDUs carry no UCI);
 //   ref_rx_buffer         unique_rx_buffer::callback over host vectors (the role
 //                         of lib/phy/upper/rx_buffer_impl.h), one HARQ process.
@@ -43,6 +41,7 @@
 #include "phy/upper/equalization/channel_equalizer_generic_impl.h"
 #include "phy/upper/sequence_generators/pseudo_random_generator_impl.h"
 #include "phy/upper/signal_processors/channel_estimator/port_channel_estimator_average_impl.h"
+#include "phy/upper/sequence_generators/low_papr_sequence_generator_impl.h"
 #include "phy/upper/signal_processors/pusch/dmrs_pusch_estimator_impl.h"
 #include "srsran/phy/upper/unique_rx_buffer.h"
 #include "srsran/support/cpu_features.h"
@@ -85,11 +84,6 @@ public:
   }
 };
 
-class no_low_papr_generator : public low_papr_sequence_generator
-{
-public:
-  void generate(span<cf_t>, unsigned, unsigned, unsigned, unsigned) override { std::abort(); }
-};
 
 class no_uci_decoder : public uci_decoder
 {
@@ -268,7 +262,7 @@ make_pusch_processor(impl choice, unsigned max_nof_rb, unsigned nof_rx_ports, un
   std::vector<std::unique_ptr<pusch_processor_impl::concurrent_dependencies>> deps;
   deps.emplace_back(std::make_unique<pusch_processor_impl::concurrent_dependencies>(
       std::make_unique<dmrs_pusch_estimator_impl>(std::make_unique<pseudo_random_generator_impl>(),
-                                                  std::make_unique<no_low_papr_generator>(),
+                                                  std::make_unique<low_papr_sequence_generator_impl>(),
                                                   make_port_estimator(fd, td, cfo),
                                                   b->exec),
       make_pusch_demodulator(eq, max_nof_rb, false, true),

@@ -9,8 +9,6 @@
 // Glue (interfaces implemented here, nothing of the reference replaced):
 //   inline_executor            task_executor that refuses deferral, so the estimator
 //                              runs each port inline (dmrs_pusch_estimator_impl.cpp:62-66);
-//   no_low_papr_generator      low_papr_sequence_generator for the constructor; only the
-//                              transform-precoding sequence path would call it (not wrapped);
 //   counting_notifier          dmrs_pusch_estimator_notifier.
 // The grid is the reference's own resource_grid_reader_impl over its tensor.
 #include "phy/generic_functions/dft_processor_generic_impl.h"
@@ -19,6 +17,7 @@
 #include "phy/support/time_alignment_estimator/time_alignment_estimator_dft_impl.h"
 #include "phy/upper/sequence_generators/pseudo_random_generator_impl.h"
 #include "phy/upper/signal_processors/channel_estimator/port_channel_estimator_average_impl.h"
+#include "phy/upper/sequence_generators/low_papr_sequence_generator_impl.h"
 #include "phy/upper/signal_processors/pusch/dmrs_pusch_estimator_impl.h"
 #include "srsran/adt/tensor.h"
 #include <atomic>
@@ -43,11 +42,6 @@ public:
   bool defer(unique_task) override { return false; }
 };
 
-class no_low_papr_generator : public low_papr_sequence_generator
-{
-public:
-  void generate(span<cf_t>, unsigned, unsigned, unsigned, unsigned) override { std::abort(); }
-};
 
 class counting_notifier : public dmrs_pusch_estimator_notifier
 {
@@ -83,7 +77,7 @@ struct chest_ctx {
   chest_ctx(int fd, int td, int cfo)
   {
     est = std::make_unique<dmrs_pusch_estimator_impl>(std::make_unique<pseudo_random_generator_impl>(),
-                                                      std::make_unique<no_low_papr_generator>(),
+                                                      std::make_unique<low_papr_sequence_generator_impl>(),
                                                       make_port_estimator(fd, td, cfo),
                                                       exec);
   }
@@ -105,12 +99,17 @@ dmrs_pusch_estimator::configuration make_config(unsigned       numerology,
 {
   dmrs_pusch_estimator::configuration cfg;
   cfg.slot = slot_point(numerology, slot_index);
-  dmrs_pusch_estimator::pseudo_random_sequence_configuration seq;
-  seq.type            = type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
-  seq.nof_tx_layers   = nof_layers;
-  seq.scrambling_id   = scrambling_id;
-  seq.n_scid          = n_scid != 0;
-  cfg.sequence_config = seq;
+  if (type2 == 2) {
+    // transform precoding: low-PAPR sequence of identifier n_rs_id (passed as scrambling_id)
+    cfg.sequence_config = dmrs_pusch_estimator::low_papr_sequence_configuration{scrambling_id};
+  } else {
+    dmrs_pusch_estimator::pseudo_random_sequence_configuration seq;
+    seq.type            = type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
+    seq.nof_tx_layers   = nof_layers;
+    seq.scrambling_id   = scrambling_id;
+    seq.n_scid          = n_scid != 0;
+    cfg.sequence_config = seq;
+  }
   cfg.scaling         = scaling;
   cfg.c_prefix        = cyclic_prefix::NORMAL;
   cfg.symbols_mask    = bounded_bitset<MAX_NSYMB_PER_SLOT>(MAX_NSYMB_PER_SLOT);
@@ -149,6 +148,7 @@ extern "C" {
 
 // dmrs_pusch_estimator::estimate (dmrs_pusch_estimator_impl.cpp:28-70) for all
 // nof_rx_ports ports of a grid [nof_rx_ports][14][nsubc] (cbf16 as uint32).
+// type2: 0 DM-RS type 1, 1 type 2, 2 the low-PAPR sequence of transform precoding with n_rs_id = scrambling_id.
 // fd: 0 none, 1 mean, 2 filter; td: 0 interpolate, 1 average (the reference enums).
 // Outputs: estimates uint32 [port][layer][14][nsubc] (only the REs the
 // reference writes are changed), per port noise_var, epre, snr, per
@@ -221,6 +221,13 @@ int srs_ref_pusch_chest(const uint32_t* grid,
     }
   }
   return 0;
+}
+
+// low_papr_sequence_generator_impl::generate(sequence, u, v, 0, 1): M interleaved (re, im) floats.
+void srs_ref_low_papr(float* out, unsigned M, unsigned u, unsigned v)
+{
+  low_papr_sequence_generator_impl gen;
+  gen.generate(span<cf_t>(reinterpret_cast<cf_t*>(out), M), u, v, 0, 1);
 }
 
 // CPU baseline: `iterations` estimations of the same grid on `threads` threads

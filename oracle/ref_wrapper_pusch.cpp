@@ -252,6 +252,7 @@ int srs_ref_pusch_demodulate(const uint32_t* grid,
 // pusch_processor::process (pusch_processor_impl.cpp:134-386) of one PDU on a received grid
 // [P][14][nsubc] (cbf16 as uint32), configured as the reference PUSCH processor benchmark.
 // Type-1 contiguous allocation [rb_start, rb_start + rb_count) of a BWP [bwp_start, +bwp_size).
+// dmrs_type2: 0 type 1, 1 type 2, 2 transform precoding (low-PAPR DM-RS, n_rs_id = scrambling_id).
 // choice: 0 generic, 1 AVX2, 2 the "auto" factory choice (ref_builders.h).
 // rx_buffer: srs_ref_rx_buffer_create handle (HARQ process). tb: tb_bytes output bytes.
 // result[0..5] = tb_crc_ok, nof_codeblocks_total, LDPC observations, sum, min, max;
@@ -319,10 +320,15 @@ int srs_ref_pusch_process(const uint32_t* grid,
     pdu.rx_ports.push_back(static_cast<uint8_t>(p));
   }
   pdu.dmrs_symbol_mask   = to_symbols(dmrs_symb_mask);
-  pdu.dmrs               = pusch_processor::dmrs_configuration{.dmrs          = dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1,
-                                                               .scrambling_id = scrambling_id,
-                                                               .n_scid        = n_scid != 0,
-                                                               .nof_cdm_groups_without_data = nof_cdm_groups_without_data};
+  if (dmrs_type2 == 2) {
+    // transform precoding (DFT-s-OFDM): low-PAPR DM-RS of identifier n_rs_id, passed as scrambling_id
+    pdu.dmrs = pusch_processor::dmrs_transform_precoding_configuration{.n_rs_id = scrambling_id};
+  } else {
+    pdu.dmrs = pusch_processor::dmrs_configuration{.dmrs          = dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1,
+                                                   .scrambling_id = scrambling_id,
+                                                   .n_scid        = n_scid != 0,
+                                                   .nof_cdm_groups_without_data = nof_cdm_groups_without_data};
+  }
   pdu.freq_alloc         = rb_allocation::make_type1(rb_start, rb_count);
   pdu.start_symbol_index = start_symbol;
   pdu.nof_symbols        = nof_symbols;

@@ -75,6 +75,8 @@ from .pusch_chest import (  # noqa: F401
     DmrsPuschEstimatorConfig,
     FdSmoothingStrategy,
     TdInterpolationStrategy,
+    low_papr_length_valid,
+    low_papr_sequence,
 )
 
 from .pusch_demodulator import PuschDemodPlan, PuschDemodulator, PuschDemodulatorConfig  # noqa: F401

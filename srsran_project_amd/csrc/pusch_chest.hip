@@ -90,9 +90,14 @@ __device__ float4 block_sum4(float4 v, float* red)
 }
 
 // Pilot of layer v at DM-RS symbol d, index m (dmrs_pusch_estimator_impl.cpp:72-184): amplitude
-// M_SQRT1_2, w_f = -1 on odd indices of odd layers (w_t = +1 for layers < 4).
-__device__ __forceinline__ float2 pilot(const uint32_t (*seq)[CH_SEQWORDS], uint32_t bit0, int d, int v, uint32_t m)
+// M_SQRT1_2, w_f = -1 on odd indices of odd layers (w_t = +1 for layers < 4).  Transform precoding: the
+// low-PAPR sequence of the allocation, one layer, the same in every DM-RS symbol (:86-92).
+__device__ __forceinline__ float2 pilot(const chest_args& a, const uint32_t (*seq)[CH_SEQWORDS], uint32_t bit0, int d,
+                                        int v, uint32_t m)
 {
+  if (a.lp_seq != nullptr) {
+    return a.lp_seq[m];
+  }
   const uint32_t b  = bit0 + 2 * m;
   const uint32_t c0 = (seq[d][b >> 5] >> (b & 31)) & 1u;
   const uint32_t c1 = (seq[d][(b + 1) >> 5] >> ((b + 1) & 31)) & 1u;
@@ -230,8 +235,8 @@ __global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a_in, 
       if (m < npil) {
         for (int vv = 0; vv < L; ++vv) {
           const int    gg = vv / 2;
-          const float2 p0 = cmulc(rxv(gg, 0, m), pilot(seq, bit0, 0, vv, m));
-          const float2 p1 = cmulc(rxv(gg, 1, m), pilot(seq, bit0, 1, vv, m));
+          const float2 p0 = cmulc(rxv(gg, 0, m), pilot(a, seq, bit0, 0, vv, m));
+          const float2 p1 = cmulc(rxv(gg, 1, m), pilot(a, seq, bit0, 1, vv, m));
           const float2 t  = cmulc(p1, p0);
           if (gg == 0) {
             acc.x += t.x;
@@ -323,19 +328,19 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
     float2         y = make_float2(0, 0);
     if (m < npil) {
       if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
-        y = cmulc(rxv(g, 0, m), pilot(seq, bit0, 0, v, m));
+        y = cmulc(rxv(g, 0, m), pilot(a, seq, bit0, 0, v, m));
         if (rotate) {
           y = cmul(y, s_rot[0]);
         }
         for (int d = 1; d < nds; ++d) {
-          float2 t = cmulc(rxv(g, d, m), pilot(seq, bit0, d, v, m));
+          float2 t = cmulc(rxv(g, d, m), pilot(a, seq, bit0, d, v, m));
           if (rotate) {
             t = cmul(t, s_rot[d]);
           }
           y = cadd(y, t);
         }
       } else {
-        y = cmulc(rxv(g, s, m), pilot(seq, bit0, s, v, m));
+        y = cmulc(rxv(g, s, m), pilot(a, seq, bit0, s, v, m));
         if (rotate) {
           y = cmul(y, s_rot[s]);
         }
@@ -538,12 +543,12 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
         if (d >= nds) {
           break;
         }
-        float2 pred = cmul(sc0, pilot(seq, bit0, d, v0, m));
+        float2 pred = cmul(sc0, pilot(a, seq, bit0, d, v0, m));
         if (rotate) {
           pred = cmul(pred, rot_fwd[d]);
         }
         if (v1 - v0 == 2) {
-          float2 po = cmul(sc1, pilot(seq, bit0, d, v0 + 1, m));
+          float2 po = cmul(sc1, pilot(a, seq, bit0, d, v0 + 1, m));
           if (rotate) {
             po = cmul(po, rot_fwd[d]);
           }

@@ -10,6 +10,7 @@
 //   the time-alignment IDFT size, sampling rate and search window
 //     (time_alignment_estimator_dft_impl.cpp:230-275).
 #include "srsran_amd/pusch_chest.h"
+#include "srsran_amd/low_papr.h"
 
 #include <hip/hip_runtime.h>
 
@@ -20,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -69,6 +71,8 @@ struct srs_amd_pusch_chest {
   stream_order  order; // scratch reuse across the callers' streams
   pinned_stage  stage; // slot form: per-PDU argument blocks
   std::mutex    mtx;
+  // transform precoding: low-PAPR pilot sequences by (length, group), generated on first use and kept
+  std::map<uint64_t, float2*> lp_tables;
   ~srs_amd_pusch_chest()
   {
     (void)hipSetDevice(device);
@@ -78,6 +82,34 @@ struct srs_amd_pusch_chest {
     }
     (void)hipFree(d_jump);
     (void)hipFree(d_tw);
+    for (auto& t : lp_tables) {
+      (void)hipFree(t.second);
+    }
+  }
+  // The device copy of r_{u,0}(n), n < M (caller holds mtx); nullptr on failure (the error is recorded).
+  const float2* low_papr(uint32_t M, uint32_t u)
+  {
+    const uint64_t key = (static_cast<uint64_t>(M) << 8) | u;
+    auto           it  = lp_tables.find(key);
+    if (it != lp_tables.end()) {
+      return it->second;
+    }
+    std::vector<float> h(2 * M);
+    if (srs_amd_low_papr_sequence(h.data(), M, u, 0) != SRS_AMD_OK) {
+      return nullptr;
+    }
+    float2*    d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(float2) * M);
+    if (e == hipSuccess) {
+      e = hipMemcpy(d, h.data(), sizeof(float2) * M, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+      (void)hipFree(d);
+      hip_fail(e, "low-PAPR sequence upload");
+      return nullptr;
+    }
+    lp_tables.emplace(key, d);
+    return d;
   }
   const float2* tw(uint32_t N) const
   {
@@ -98,6 +130,13 @@ int make_args(chest_args& a, const srs_amd_pusch_chest_config* cfg, uint32_t nof
   }
   if (cfg->nof_tx_layers < 1 || cfg->nof_tx_layers > CH_MAXL) {
     return fail(SRS_AMD_EINVAL, "The number of Tx layers is %u, max %d supported.", cfg->nof_tx_layers, CH_MAXL);
+  }
+  if (cfg->low_papr && (cfg->nof_tx_layers != 1 || cfg->n_rs_id > 1007)) {
+    return fail(SRS_AMD_EINVAL, "Transform precoding is only possible with one layer and n_rs_id <= 1007.");
+  }
+  if (cfg->low_papr && !srs_amd_low_papr_length_valid(6 * cfg->rb_count)) {
+    return fail(SRS_AMD_EINVAL, "No low-PAPR sequence of length %u (transform precoding with %u PRB).",
+                6 * cfg->rb_count, cfg->rb_count);
   }
   if (!(cfg->scaling > 0)) {
     return fail(SRS_AMD_EINVAL, "The DM-RS to data scaling factor should be a positive number.");
@@ -367,6 +406,13 @@ static int estimate_batch_impl(srs_amd_pusch_chest*              chest,
   a.stats       = d_stats;
   a.jump        = chest->d_jump;
   a.ta_tw       = chest->tw(a.ta_n);
+  a.lp_seq      = nullptr;
+  if (cfg->low_papr) {
+    a.lp_seq = chest->low_papr(a.npil, cfg->n_rs_id % 30);
+    if (a.lp_seq == nullptr) {
+      return SRS_AMD_EHIP;
+    }
+  }
   e             = chest->order.begin(static_cast<hipStream_t>(stream));
   if (e == hipSuccess) {
     e = launch_chest(a, nof_grids, static_cast<hipStream_t>(stream), expand);
@@ -481,6 +527,13 @@ int srs_amd::chest_estimate_slot_unexpanded(::srs_amd_pusch_chest* chest,
     a.stats       = items[i].d_stats;
     a.jump        = chest->d_jump;
     a.ta_tw       = chest->tw(a.ta_n);
+    a.lp_seq      = nullptr;
+    if (items[i].cfg->low_papr) {
+      a.lp_seq = chest->low_papr(a.npil, items[i].cfg->n_rs_id % 30);
+      if (a.lp_seq == nullptr) {
+        return SRS_AMD_EHIP;
+      }
+    }
   }
   std::memcpy(chest->stage.at<chest_args>(0), views, sizeof(chest_args) * nof_items);
   auto s = static_cast<hipStream_t>(stream);

@@ -39,6 +39,7 @@ struct chest_args {
   float*  acc;  // [CH_ACC]: epre, -, -, cfo valid, cfo, -, -, -, rsrp per slice
   float*  corr; // [L][nof_lse][ta_n]: time-alignment correlation per slice
   uint32_t* dmrs_seq; // [CH_MAXDMRS][CH_SEQWORDS]: DM-RS Gold words of the batch
+  const float2* lp_seq; // transform precoding: the low-PAPR pilot sequence [npil] (nullptr: Gold sequence)
   // constants
   const uint32_t* jump;    // Gold-sequence jump matrices
   const float2*   ta_tw;   // W_N^m table of the time-alignment IDFT size

@@ -4,6 +4,7 @@
 // DM-RS channel estimation, demodulation, UL-SCH decoding -- over a batch of
 // grids, with the processor's own HBM scratch between them.
 #include "srsran_amd/pusch_processor.h"
+#include "srsran_amd/transform_precoding.h"
 
 #include <hip/hip_runtime.h>
 
@@ -148,13 +149,28 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
   }
   *plan = nullptr;
   // pusch_processor_validator_impl.cpp checks, where the C-ABI subset narrows them
-  if (pdu->dmrs_type != 1) {
-    return fail(SRS_AMD_EINVAL, "Only DM-RS type 1 is supported.");
+  const bool tp = pdu->transform_precoding != 0;
+  if (tp) {
+    if (pdu->nof_tx_layers != 1) {
+      return fail(SRS_AMD_EINVAL, "Transform precoding is only possible with one layer.");
+    }
+    if (!srs_amd_transform_precoding_nof_prbs_valid(pdu->rb_count)) {
+      return fail(SRS_AMD_EINVAL, "Transform precoding is only possible with a valid number of PRB.");
+    }
+    if (pdu->n_rs_id > 1007) {
+      return fail(SRS_AMD_EINVAL, "Invalid n_rs_id %u.", pdu->n_rs_id);
+    }
+  } else {
+    if (pdu->dmrs_type != 1) {
+      return fail(SRS_AMD_EINVAL, "Only DM-RS type 1 is supported.");
+    }
+    if (pdu->nof_cdm_groups_without_data < 1 || pdu->nof_cdm_groups_without_data > 2) {
+      return fail(SRS_AMD_EINVAL, "Invalid number of CDM groups without data (i.e., %u).",
+                  pdu->nof_cdm_groups_without_data);
+    }
   }
-  if (pdu->nof_cdm_groups_without_data < 1 || pdu->nof_cdm_groups_without_data > 2) {
-    return fail(SRS_AMD_EINVAL, "Invalid number of CDM groups without data (i.e., %u).",
-                pdu->nof_cdm_groups_without_data);
-  }
+  // transform precoding keeps the default of two CDM groups without data (pusch_processor_impl.cpp:176)
+  const uint32_t ncdm = tp ? 2u : pdu->nof_cdm_groups_without_data;
   if (pdu->rb_count == 0 || pdu->rb_start + pdu->rb_count > pdu->bwp_size_rb) {
     return fail(SRS_AMD_EINVAL, "Invalid frequency allocation.");
   }
@@ -178,7 +194,7 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
   c.scrambling_id           = pdu->scrambling_id;
   c.n_scid                  = pdu->n_scid;
   c.nof_tx_layers           = pdu->nof_tx_layers;
-  c.scaling                 = dmrs_scaling(pdu->nof_cdm_groups_without_data);
+  c.scaling                 = dmrs_scaling(ncdm);
   c.symbols_mask            = pdu->dmrs_symbol_mask;
   c.rb_start                = crb0;
   c.rb_count                = pdu->rb_count;
@@ -187,6 +203,8 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
   c.fd_smoothing            = proc->cfg.fd_smoothing;
   c.td_interpolation        = proc->cfg.td_interpolation;
   c.compensate_cfo          = proc->cfg.compensate_cfo;
+  c.low_papr                = tp ? 1 : 0;
+  c.n_rs_id                 = pdu->n_rs_id;
   // demodulator configuration (pusch_processor_impl.cpp:368-383)
   srs_amd_pusch_demod_config dc{};
   dc.rnti = pdu->rnti;
@@ -198,8 +216,9 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
   dc.start_symbol                = pdu->start_symbol_index;
   dc.nof_symbols                 = pdu->nof_symbols;
   dc.dmrs_symbol_mask            = pdu->dmrs_symbol_mask;
-  dc.dmrs_type                   = pdu->dmrs_type;
-  dc.nof_cdm_groups_without_data = pdu->nof_cdm_groups_without_data;
+  dc.dmrs_type                   = tp ? 1u : pdu->dmrs_type;
+  dc.nof_cdm_groups_without_data = ncdm;
+  dc.transform_precoding         = tp ? 1u : 0u;
   dc.nof_tx_layers               = pdu->nof_tx_layers;
   dc.nof_rx_ports                = pdu->nof_rx_ports;
   dc.equalizer                   = proc->cfg.equalizer;

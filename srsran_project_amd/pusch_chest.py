@@ -41,7 +41,7 @@ class _Config(ctypes.Structure):
                 ("symbols_mask", ctypes.c_uint32), ("rb_start", ctypes.c_uint32), ("rb_count", ctypes.c_uint32),
                 ("first_symbol", ctypes.c_uint32), ("nof_symbols", ctypes.c_uint32),
                 ("fd_smoothing", ctypes.c_int32), ("td_interpolation", ctypes.c_int32),
-                ("compensate_cfo", ctypes.c_int32)]
+                ("compensate_cfo", ctypes.c_int32), ("low_papr", ctypes.c_int32), ("n_rs_id", ctypes.c_uint32)]
 
 
 class ChestPortStats(ctypes.Structure):
@@ -72,12 +72,14 @@ class DmrsPuschEstimatorConfig:
     fd_smoothing: FdSmoothingStrategy = FdSmoothingStrategy.filter
     td_interpolation: TdInterpolationStrategy = TdInterpolationStrategy.average
     compensate_cfo: bool = True
+    low_papr: bool = False  # transform precoding: low-PAPR sequence of n_rs_id (one layer)
+    n_rs_id: int = 0
 
     def _c(self):
         return _Config(self.numerology, self.slot_index, self.scrambling_id, int(bool(self.n_scid)),
                        self.nof_tx_layers, self.scaling, self.symbols_mask, self.rb_start, self.rb_count,
                        self.first_symbol, self.nof_symbols, int(self.fd_smoothing), int(self.td_interpolation),
-                       int(bool(self.compensate_cfo)))
+                       int(bool(self.compensate_cfo)), int(bool(self.low_papr)), self.n_rs_id)
 
 
 def _declare(lib):
@@ -86,6 +88,8 @@ def _declare(lib):
     u = c.c_uint32
     sigs = {
         "srs_amd_pusch_chest_create": (c.c_int, [c.POINTER(P), c.c_int]),
+        "srs_amd_low_papr_length_valid": (c.c_int, [u]),
+        "srs_amd_low_papr_sequence": (c.c_int, [P, u, u, u]),
         "srs_amd_pusch_chest_destroy": (None, [P]),
         "srs_amd_pusch_chest_estimate": (c.c_int, [P, c.POINTER(_Config), P, u, u, P, P]),
         "srs_amd_pusch_chest_estimate_batch": (c.c_int, [P, c.POINTER(_Config), P, c.c_uint64, u, u, u, P,
@@ -108,6 +112,20 @@ def _L():
         _declare(lib)
         _declared = True
     return lib
+
+
+def low_papr_sequence(M, u, v=0):
+    """low_papr_sequence_generator::generate(sequence, u, v, 0, 1) (include/srsran_amd/low_papr.h): complex64 [M]."""
+    import numpy as np
+
+    lib = _L()
+    out = np.zeros(M, np.complex64)
+    _lib.check(lib.srs_amd_low_papr_sequence(out.ctypes.data, M, u, v), "low_papr_sequence")
+    return out
+
+
+def low_papr_length_valid(M):
+    return bool(_L().srs_amd_low_papr_length_valid(M))
 
 
 class DmrsPuschEstimator:

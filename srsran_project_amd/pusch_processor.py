@@ -45,7 +45,8 @@ class PuschPdu(ctypes.Structure):
          ("base_graph", ctypes.c_uint32), ("new_data", ctypes.c_int32)] + \
         [(n, ctypes.c_uint32) for n in ("n_id", "nof_tx_layers", "nof_rx_ports", "dmrs_symbol_mask", "dmrs_type",
                                         "scrambling_id", "n_scid", "nof_cdm_groups_without_data", "rb_start",
-                                        "rb_count", "start_symbol_index", "nof_symbols", "tbs_lbrm_bytes", "tbs")]
+                                        "rb_count", "start_symbol_index", "nof_symbols", "tbs_lbrm_bytes", "tbs",
+                                        "transform_precoding", "n_rs_id")]
 
 
 class PuschProcessorResult(ctypes.Structure):
@@ -78,7 +79,7 @@ def make_pdu(**kw):
              target_code_rate=679.0, rv=0, base_graph=1, new_data=1, n_id=0, nof_tx_layers=1, nof_rx_ports=1,
              dmrs_symbol_mask=(1 << 2) | (1 << 11), dmrs_type=1, scrambling_id=0, n_scid=0,
              nof_cdm_groups_without_data=2, rb_start=0, rb_count=None, start_symbol_index=0, nof_symbols=14,
-             tbs_lbrm_bytes=0, tbs=0)
+             tbs_lbrm_bytes=0, tbs=0, transform_precoding=0, n_rs_id=0)
     d.update(kw)
     if d["rb_count"] is None:
         d["rb_count"] = d["bwp_size_rb"] - d["rb_start"]

@@ -83,3 +83,44 @@ def test_pusch_chest_rejects_unsupported(est):
     cfg.nof_tx_layers = 5
     with pytest.raises(ValueError):
         est.estimate(grid, cfg)
+
+
+# Transform precoding: the low-PAPR DM-RS sequence (one layer), against the compiled reference estimator
+# configured with low_papr_sequence_configuration (dmrs_pusch_estimator_impl.cpp:86-92).
+# (name, ports, nof_prb, rb_start, rb_count, dmrs mask, td, n_rs_id)
+LP_CASES = [
+    ("lp_1rb_M6", 1, 25, 3, 1, (1 << 2) | (1 << 11), 1, 5),
+    ("lp_5rb_M30", 2, 52, 10, 5, (1 << 2) | (1 << 11), 1, 77),
+    ("lp_25rb_M150_interp", 4, 52, 20, 25, (1 << 2) | (1 << 7) | (1 << 11), 0, 1007),
+    ("lp_270rb_M1620", 2, 273, 2, 270, 1 << 2, 1, 301),
+]
+
+
+@pytest.mark.skipif(oracle.REF is None, reason="oracle/_ref not built")
+@pytest.mark.parametrize("case", LP_CASES, ids=[c[0] for c in LP_CASES])
+def test_pusch_chest_low_papr_vs_reference(est, case):
+    name, P, nprb, lo, cnt, mask, td, n_rs_id = case
+    grid = cc.make_grid(P, nprb, 0.05, seed=cnt)
+    kw = dict(slot_index=4, type2=2, nof_layers=1, scrambling_id=n_rs_id, n_scid=0, scaling=1.41, symbols_mask=mask,
+              prb_lo=lo, prb_hi=lo + cnt, first_symbol=0, nof_symbols=14, fd=2, td=td, compensate_cfo=True,
+              numerology=1)
+    est0 = cc.stale_estimates(grid.shape, 1, seed=3)
+    want, ws = chest.ref_pusch_chest(grid, estimates=est0, **kw)
+    cfg = _config(dict(kw, scrambling_id=0))
+    cfg.low_papr, cfg.n_rs_id = True, n_rs_id
+    got, gs = est.estimate(grid, cfg, estimates=est0)
+    cc.assert_estimates_close(got, want, name)
+    cc.assert_stats_close(gs, ws, name)
+
+
+def test_pusch_chest_low_papr_rejects(est):
+    grid = cc.make_grid(1, 52, 0.05, seed=0)
+    kw = dict(slot_index=0, type2=False, nof_layers=2, scrambling_id=0, n_scid=0, scaling=1.41, symbols_mask=1 << 2,
+              prb_lo=0, prb_hi=7, first_symbol=0, nof_symbols=14, fd=2, td=1, compensate_cfo=True, numerology=1)
+    cfg = _config(kw)
+    cfg.low_papr = True
+    with pytest.raises(ValueError):  # two layers
+        est.estimate(grid, cfg)
+    cfg.nof_tx_layers = 1
+    with pytest.raises(ValueError):  # 7 PRB: no low-PAPR sequence of length 42
+        est.estimate(grid, cfg)

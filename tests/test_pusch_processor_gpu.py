@@ -270,3 +270,51 @@ def test_pusch_slot_rejects_unsupported():
         proc.process_slot(g, [(ok, 1)])  # grid index out of range
     tbs, offs, res = proc.process_slot(g, [])
     assert offs == [] and res.shape[0] == 0
+
+
+# Transform precoding (DFT-s-OFDM): low-PAPR DM-RS in the estimator, deprecoding in the demodulator, against the
+# compiled pusch_processor_impl with dmrs_transform_precoding_configuration (pusch_processor_impl.cpp:172-196).
+# (name, pdu overrides, grid PRBs, channel [rx ports], SNR dB)
+TP_CASES = [
+    ("tp_1rb_qpsk", dict(rb_start=3, rb_count=1, modulation=2, target_code_rate=308.0, n_rs_id=5), 52, None, 20.0),
+    ("tp_5rb_16qam_2rx", dict(rb_start=10, rb_count=5, modulation=4, target_code_rate=434.0, nof_rx_ports=2,
+                              n_rs_id=77, rnti=0x1234, n_id=33), 52, np.array([0.9, 0.4 - 0.3j]), 25.0),
+    ("tp_25rb_64qam_4rx_3dmrs", dict(rb_start=20, rb_count=25, modulation=6, target_code_rate=567.0,
+                                     nof_rx_ports=4, n_rs_id=1007, dmrs_symbol_mask=(1 << 2) | (1 << 7) | (1 << 11)),
+     52, np.array([0.8, 0.3j, -0.5, 0.6 + 0.2j]), 30.0),
+    ("tp_270rb_16qam_2rx", dict(bwp_size_rb=273, rb_start=2, rb_count=270, modulation=4, target_code_rate=490.0,
+                                nof_rx_ports=2, n_rs_id=301), 273, np.array([1.0, 0.5j]), 25.0),
+]
+
+
+@pytest.mark.parametrize("case", TP_CASES, ids=[c[0] for c in TP_CASES])
+def test_pusch_processor_transform_precoding_vs_reference(case):
+    """DFT-s-OFDM PUSCH through the processor (low-PAPR DM-RS estimate, equalizer, transform
+    deprecoder, demapper, decoder) against the compiled pusch_processor_impl on the same grid."""
+    name, over, nprb, ch, snr = case
+    pdu = dict(BASE, **over, transform_precoding=1)
+    nd = bin(pdu["dmrs_symbol_mask"]).count("1")
+    tbs = amd.tbs_calculator_calculate(pdu["nof_symbols"], 12 * nd, 0, pdu["modulation"], pdu["target_code_rate"],
+                                       1, 0, pdu["rb_count"])
+    r = pdu["target_code_rate"] / 1024
+    pdu["base_graph"] = 2 if (tbs <= 292 or (tbs <= 3824 and r <= 0.67) or r <= 0.25) else 1
+    tb = np.random.default_rng(len(name)).integers(0, 256, tbs // 8, dtype=np.uint8)
+    grid, _ = pp.ue_transmit_tp(tb, pdu, 12 * nprb, channel=ch, snr_db=snr, seed=3)
+    want_tb, want = pp.ref_pusch_process(grid, pdu, tbs // 8, iterations=6)
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=6), device=0)
+    plan = proc.plan(amd.make_pdu(**dict(pdu, tbs=tbs)), 12 * nprb)
+    got_tb, got = proc.process(grid, plan)
+    assert want["tb_crc_ok"] and np.array_equal(want_tb, tb), name  # the synthetic UE transmission is valid
+    assert bool(got.data.tb_crc_ok) == want["tb_crc_ok"], name
+    assert np.array_equal(got_tb, want_tb), name
+    assert got.data.nof_codeblocks_total == want["nof_codeblocks_total"]
+    assert got.data.ldpc_iterations_sum == want["iterations_sum"], (name, got.data.ldpc_iterations_sum, want)
+    _check_csi(got, want, name)
+
+
+def test_pusch_processor_transform_precoding_rejects():
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(), device=0)
+    for over in (dict(nof_tx_layers=2, nof_rx_ports=2), dict(rb_count=7)):
+        pdu = dict(BASE, **over, transform_precoding=1, tbs=1024)
+        with pytest.raises(ValueError):
+            proc.plan(amd.make_pdu(**pdu), 12 * 51)
