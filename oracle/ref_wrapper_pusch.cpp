@@ -14,6 +14,7 @@
 // pusch_decoder_impl.cpp:140-157) so the demodulator splits its demapper calls
 // per OFDM symbol as in the real chain; notifiers that record the results.
 #include "ref_builders.h"
+#include "srsran/ran/pusch/ulsch_info.h"
 #include "phy/support/resource_grid_reader_impl.h"
 #include "srsran/adt/tensor.h"
 #include "srsran/phy/upper/channel_processors/pusch/pusch_codeword_buffer.h"
@@ -356,6 +357,58 @@ int srs_ref_pusch_process(const uint32_t* grid,
     csi[3]                             = c.get_time_alignment().has_value() ? c.get_time_alignment()->to_seconds() : NAN;
   }
   return 0;
+}
+
+// get_ulsch_information (lib/ran/pusch/ulsch_info.cpp:158-358). out[15] = nof_ul_sch_bits, nof_harq_ack_bits,
+// nof_harq_ack_rvd, nof_csi_part1_bits, nof_csi_part2_bits, nof_harq_ack_re, nof_csi_part1_re, nof_csi_part2_re,
+// nof_dc_overlap_bits, then the UL-SCH segmentation: tb_crc_size, base graph, nof_cb, lifting_size,
+// nof_bits_per_cb, nof_filler_bits_per_cb (0 without UL-SCH).
+void srs_ref_ulsch_information(unsigned tbs, int qm, float target_code_rate, unsigned nof_harq_ack_bits,
+                               unsigned nof_csi_part1_bits, unsigned nof_csi_part2_bits, float alpha_scaling,
+                               float beta_ack, float beta_csi1, float beta_csi2, unsigned nof_rb,
+                               unsigned start_symbol, unsigned nof_symbols, int dmrs_type2, unsigned dmrs_symbol_mask,
+                               unsigned nof_cdm_groups_without_data, unsigned nof_layers, int contains_dc,
+                               unsigned* out)
+{
+  ulsch_configuration c;
+  c.tbs                         = units::bits(tbs);
+  c.mcs_descr                   = sch_mcs_description{scheme_of(qm), target_code_rate};
+  c.nof_harq_ack_bits           = units::bits(nof_harq_ack_bits);
+  c.nof_csi_part1_bits          = units::bits(nof_csi_part1_bits);
+  c.nof_csi_part2_bits          = units::bits(nof_csi_part2_bits);
+  c.alpha_scaling               = alpha_scaling;
+  c.beta_offset_harq_ack        = beta_ack;
+  c.beta_offset_csi_part1       = beta_csi1;
+  c.beta_offset_csi_part2       = beta_csi2;
+  c.nof_rb                      = nof_rb;
+  c.start_symbol_index          = start_symbol;
+  c.nof_symbols                 = nof_symbols;
+  c.dmrs_type                   = dmrs_type2 ? dmrs_config_type::type2 : dmrs_config_type::type1;
+  c.dmrs_symbol_mask            = to_symbols(dmrs_symbol_mask);
+  c.nof_cdm_groups_without_data = nof_cdm_groups_without_data;
+  c.nof_layers                  = nof_layers;
+  c.contains_dc                 = contains_dc != 0;
+  const ulsch_information r     = get_ulsch_information(c);
+  out[0]                        = r.nof_ul_sch_bits.value();
+  out[1]                        = r.nof_harq_ack_bits.value();
+  out[2]                        = r.nof_harq_ack_rvd.value();
+  out[3]                        = r.nof_csi_part1_bits.value();
+  out[4]                        = r.nof_csi_part2_bits.value();
+  out[5]                        = r.nof_harq_ack_re;
+  out[6]                        = r.nof_csi_part1_re;
+  out[7]                        = r.nof_csi_part2_re;
+  out[8]                        = r.nof_dc_overlap_bits.value();
+  for (unsigned i = 9; i != 15; ++i) {
+    out[i] = 0;
+  }
+  if (r.sch.has_value()) {
+    out[9]  = r.sch->tb_crc_size.value();
+    out[10] = r.sch->base_graph == ldpc_base_graph_type::BG1 ? 1 : 2;
+    out[11] = r.sch->nof_cb;
+    out[12] = r.sch->lifting_size;
+    out[13] = r.sch->nof_bits_per_cb.value();
+    out[14] = r.sch->nof_filler_bits_per_cb.value();
+  }
 }
 
 // Describes what choice 2 ("auto") selects on this host.

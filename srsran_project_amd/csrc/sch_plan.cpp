@@ -220,3 +220,167 @@ extern "C" uint32_t srs_amd_tbs_calculate(uint32_t nof_symb_sh,
                          static_cast<float>(nof_layers);
   return nof_info <= 3824 ? tbs_step3(nof_info) : tbs_step4(nof_info, tcr);
 }
+
+// ---- get_ulsch_information (lib/ran/pusch/ulsch_info.cpp) -------------------------------------------------------
+#include "srsran_amd/ulsch_info.h"
+
+#include <algorithm>
+#include <cmath>
+
+#pragma clang fp contract(off)
+
+namespace {
+
+// get_uci_crc_size (include/srsran/ran/uci/uci_info.h:54-65)
+uint32_t uci_crc_size(uint32_t a)
+{
+  return a < 12 ? 0u : (a < 20 ? 6u : 11u);
+}
+
+// calculate_nof_re_harq_ack (ulsch_info.cpp:30-48), float as the reference
+uint32_t re_harq_ack(uint32_t o, float beta, uint32_t nre_uci, uint32_t sum_cb, float alpha, uint32_t nre_l0)
+{
+  if (o == 0) {
+    return 0;
+  }
+  const uint32_t left  = static_cast<uint32_t>(std::ceil(static_cast<float>(o + uci_crc_size(o)) * beta *
+                                                        static_cast<float>(nre_uci) / static_cast<float>(sum_cb)));
+  const uint32_t right = static_cast<uint32_t>(std::ceil(alpha * static_cast<float>(nre_l0)));
+  return std::min(left, right);
+}
+
+// calculate_nof_re_harq_ack_without_sch (:50-68)
+uint32_t re_harq_ack_no_sch(uint32_t o, float beta, float rate, uint32_t qm, float alpha, uint32_t nre_l0)
+{
+  if (o == 0) {
+    return 0;
+  }
+  const uint32_t left  = static_cast<uint32_t>(
+      std::ceil(static_cast<float>(o + uci_crc_size(o)) * beta / (rate * static_cast<float>(qm))));
+  const uint32_t right = static_cast<uint32_t>(std::ceil(alpha * static_cast<float>(nre_l0)));
+  return std::min(left, right);
+}
+
+// calculate_nof_re_csi_part1 (:70-89)
+uint32_t re_csi1(uint32_t o, float beta, uint32_t nre_uci, uint32_t nre_ack, uint32_t sum_cb, float alpha)
+{
+  if (o == 0) {
+    return 0;
+  }
+  const uint32_t left  = static_cast<uint32_t>(std::ceil(static_cast<float>(o + uci_crc_size(o)) * beta *
+                                                        static_cast<float>(nre_uci) / static_cast<float>(sum_cb)));
+  const uint32_t right = static_cast<uint32_t>(std::ceil(alpha * static_cast<float>(nre_uci))) - nre_ack;
+  return std::min(left, right);
+}
+
+// calculate_nof_re_csi_part1_without_sch (:91-118)
+uint32_t re_csi1_no_sch(uint32_t o, uint32_t o2, uint32_t nre_uci, uint32_t nre_ack, float beta, float rate, uint32_t qm)
+{
+  if (o == 0) {
+    return 0;
+  }
+  if (o2 == 0) {
+    return nre_uci - nre_ack;
+  }
+  const uint32_t left = static_cast<uint32_t>(
+      std::ceil(static_cast<float>(o + uci_crc_size(o)) * beta / (rate * static_cast<float>(qm))));
+  return std::min(left, nre_uci - nre_ack);
+}
+
+// calculate_nof_re_csi_part2 (:120-141)
+uint32_t re_csi2(uint32_t o, float beta, uint32_t nre_uci, uint32_t nre_ack, uint32_t nre_csi1, uint32_t sum_cb,
+                 float alpha)
+{
+  if (o == 0) {
+    return 0;
+  }
+  const uint32_t left  = static_cast<uint32_t>(std::ceil(static_cast<float>(o + uci_crc_size(o)) * beta *
+                                                        static_cast<float>(nre_uci) / static_cast<float>(sum_cb)));
+  const uint32_t right =
+      static_cast<uint32_t>(std::ceil(alpha * static_cast<float>(nre_uci))) - nre_ack - nre_csi1;
+  return std::min(left, right);
+}
+
+} // namespace
+
+extern "C" int srs_amd_ulsch_information(const srs_amd_ulsch_config* c, srs_amd_ulsch_info* r)
+{
+  if (c == nullptr || r == nullptr) {
+    return srs_amd::fail(SRS_AMD_EINVAL, "null argument");
+  }
+  *r                  = srs_amd_ulsch_info{};
+  const float    rate = c->target_code_rate * (1.F / 1024);
+  const uint32_t qm   = c->modulation < 2 ? 1u : static_cast<uint32_t>(c->modulation);
+  const uint32_t max_cdm = c->dmrs_type == 1 ? 2u : 3u;
+  if (c->dmrs_type < 1 || c->dmrs_type > 2 || c->nof_cdm_groups_without_data < 1 ||
+      c->nof_cdm_groups_without_data > max_cdm) {
+    return srs_amd::fail(SRS_AMD_EINVAL, "Invalid DM-RS type / CDM groups without data.");
+  }
+  const uint32_t end  = c->start_symbol_index + c->nof_symbols;
+  const uint32_t mask = c->dmrs_symbol_mask & 0x3fffu;
+  if (mask == 0 || end > 14 || static_cast<uint32_t>(__builtin_ctz(mask)) < c->start_symbol_index ||
+      static_cast<uint32_t>(31 - __builtin_clz(mask)) >= end) {
+    return srs_amd::fail(SRS_AMD_EINVAL, "DM-RS symbols outside the time allocation.");
+  }
+  uint32_t sum_cb = 0;
+  if (c->tbs > 0) {
+    if (!(rate > 0.F && rate < 1.F)) {
+      return srs_amd::fail(SRS_AMD_EINVAL, "Invalid target code rate.");
+    }
+    // get_sch_segmentation_info (lib/ran/sch/sch_segmentation.cpp:30-63), get_ldpc_base_graph (ldpc_base_graph.h:38)
+    const uint32_t bg = (c->tbs <= 292 || rate <= 0.25F || (c->tbs <= 3824 && rate <= 0.67F)) ? 2u : 1u;
+    const uint32_t C  = nof_codeblocks(c->tbs, bg);
+    const uint32_t Z  = lifting_size(c->tbs, bg, C);
+    const uint32_t K  = (bg == 1 ? 22u : 10u) * Z;
+    uint32_t       per_cb = (c->tbs + tb_crc_size(c->tbs)) / C;
+    if (C > 1) {
+      per_cb += SEG_CRC_LENGTH;
+    }
+    r->sch_tb_crc_size            = tb_crc_size(c->tbs);
+    r->sch_base_graph             = bg;
+    r->sch_nof_cb                 = C;
+    r->sch_lifting_size           = Z;
+    r->sch_nof_bits_per_cb        = K;
+    r->sch_nof_filler_bits_per_cb = K - per_cb;
+    sum_cb                        = C * K;
+  }
+  const uint32_t nds        = static_cast<uint32_t>(__builtin_popcount(mask));
+  const uint32_t dmrs_re_rb = nds * c->nof_cdm_groups_without_data * (c->dmrs_type == 1 ? 6u : 4u);
+  const uint32_t re_total   = c->nof_rb * (c->nof_symbols * 12 - dmrs_re_rb);
+  const uint32_t re_uci     = (c->nof_symbols - nds) * c->nof_rb * 12;
+  uint32_t       re_uci_l0  = 0;
+  for (uint32_t l = static_cast<uint32_t>(__builtin_ctz(mask)); l < end; ++l) {
+    re_uci_l0 += ((mask >> l) & 1u) ? 0u : c->nof_rb * 12;
+  }
+  const bool sch = c->tbs > 0;
+  r->nof_harq_ack_re = sch ? re_harq_ack(c->nof_harq_ack_bits, c->beta_offset_harq_ack, re_uci, sum_cb,
+                                         c->alpha_scaling, re_uci_l0)
+                           : re_harq_ack_no_sch(c->nof_harq_ack_bits, c->beta_offset_harq_ack, rate, qm,
+                                                c->alpha_scaling, re_uci_l0);
+  uint32_t rvd_re = 0;
+  if (c->nof_harq_ack_bits < 2) {
+    rvd_re = sch ? re_harq_ack(2, c->beta_offset_harq_ack, re_uci, sum_cb, c->alpha_scaling, re_uci_l0)
+                 : re_harq_ack_no_sch(2, c->beta_offset_harq_ack, rate, qm, c->alpha_scaling, re_uci_l0);
+  } else if (c->nof_harq_ack_bits == 2) {
+    rvd_re = r->nof_harq_ack_re;
+  }
+  const uint32_t ack_for_csi1 = c->nof_harq_ack_bits <= 2 ? rvd_re : r->nof_harq_ack_re;
+  r->nof_csi_part1_re = sch ? re_csi1(c->nof_csi_part1_bits, c->beta_offset_csi_part1, re_uci, ack_for_csi1, sum_cb,
+                                      c->alpha_scaling)
+                            : re_csi1_no_sch(c->nof_csi_part1_bits, c->nof_csi_part2_bits, re_uci, ack_for_csi1,
+                                             c->beta_offset_csi_part1, rate, qm);
+  const uint32_t ack_for_csi2 = c->nof_harq_ack_bits <= 2 ? 0u : r->nof_harq_ack_re;
+  r->nof_csi_part2_re = sch ? re_csi2(c->nof_csi_part2_bits, c->beta_offset_csi_part2, re_uci, ack_for_csi2,
+                                      r->nof_csi_part1_re, sum_cb, c->alpha_scaling)
+                            : (c->nof_csi_part2_bits == 0 ? 0u : re_uci - ack_for_csi2 - r->nof_csi_part1_re);
+  const uint32_t ack_re = c->nof_harq_ack_bits > 2 ? r->nof_harq_ack_re : 0u;
+  const uint32_t sch_re = sch ? re_total - ack_re - r->nof_csi_part1_re - r->nof_csi_part2_re : 0u;
+  const uint32_t bpre   = c->nof_layers * qm;
+  r->nof_ul_sch_bits     = sch_re * bpre;
+  r->nof_harq_ack_bits   = r->nof_harq_ack_re * bpre;
+  r->nof_harq_ack_rvd    = rvd_re * bpre;
+  r->nof_csi_part1_bits  = r->nof_csi_part1_re * bpre;
+  r->nof_csi_part2_bits  = r->nof_csi_part2_re * bpre;
+  r->nof_dc_overlap_bits = c->contains_dc ? c->nof_symbols * qm : 0u;
+  return SRS_AMD_OK;
+}

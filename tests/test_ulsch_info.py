@@ -1,0 +1,82 @@
+"""UL-SCH / UCI multiplexing geometry (include/srsran_amd/ulsch_info.h, host code) against the compiled
+reference get_ulsch_information (lib/ran/pusch/ulsch_info.cpp) over random configurations: HARQ-ACK 0-40 bits
+(the <= 2-bit reserved-RE rules included), CSI part 1 / part 2, with and without UL-SCH, DM-RS types and CDM
+groups, 1-4 layers, every modulation -- every field equal.  Runs on the CPU."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+import srsran_project_amd as amd
+from srsran_project_amd import _lib
+
+pytestmark = pytest.mark.skipif(oracle.REF is None, reason="oracle/_ref not built")
+
+FIELDS = ["nof_ul_sch_bits", "nof_harq_ack_bits", "nof_harq_ack_rvd", "nof_csi_part1_bits", "nof_csi_part2_bits",
+          "nof_harq_ack_re", "nof_csi_part1_re", "nof_csi_part2_re", "nof_dc_overlap_bits", "sch_tb_crc_size",
+          "sch_base_graph", "sch_nof_cb", "sch_lifting_size", "sch_nof_bits_per_cb", "sch_nof_filler_bits_per_cb"]
+
+
+def _ref(c):
+    R = oracle.REF
+    R.srs_ref_ulsch_information.restype = None
+    R.srs_ref_ulsch_information.argtypes = ([ctypes.c_uint, ctypes.c_int, ctypes.c_float] + [ctypes.c_uint] * 3
+                                            + [ctypes.c_float] * 4 + [ctypes.c_uint] * 3 + [ctypes.c_int]
+                                            + [ctypes.c_uint] * 3 + [ctypes.c_int, ctypes.c_void_p])
+    out = np.zeros(15, np.uint32)
+    R.srs_ref_ulsch_information(c.tbs, c.modulation, c.target_code_rate, c.nof_harq_ack_bits, c.nof_csi_part1_bits,
+                                c.nof_csi_part2_bits, c.alpha_scaling, c.beta_offset_harq_ack,
+                                c.beta_offset_csi_part1, c.beta_offset_csi_part2, c.nof_rb, c.start_symbol_index,
+                                c.nof_symbols, int(c.dmrs_type == 2), c.dmrs_symbol_mask,
+                                c.nof_cdm_groups_without_data, c.nof_layers, c.contains_dc, out.ctypes.data)
+    return dict(zip(FIELDS, out.tolist()))
+
+
+def test_ulsch_information_matches_reference():
+    rng = np.random.default_rng(2)
+    mcs = [(2, 120.0), (2, 679.0), (4, 378.0), (6, 567.0), (8, 948.0), (1, 120.0)]
+    n = 0
+    for _ in range(3000):
+        qm, r = mcs[rng.integers(len(mcs))]
+        t2 = bool(rng.integers(2))
+        start = int(rng.integers(0, 4))
+        nsym = int(rng.integers(4, 15 - start))
+        first_dmrs = start + int(rng.integers(0, min(3, nsym)))
+        mask = 1 << first_dmrs
+        for extra in rng.choice(np.arange(first_dmrs + 1, start + nsym), min(2, start + nsym - first_dmrs - 1),
+                                replace=False):
+            if rng.integers(2):
+                mask |= 1 << int(extra)
+        if mask.bit_count() == nsym:
+            continue
+        nrb = int(rng.integers(1, 274))
+        layers = int(rng.integers(1, 5))
+        with_sch = rng.integers(5) != 0
+        nds = mask.bit_count()
+        tbs = amd.tbs_calculator_calculate(nsym, 6 * nds, 0, qm if qm > 1 else 2, r, layers, 0, nrb) if with_sch else 0
+        c = amd.UlschConfig(tbs=tbs, modulation=qm, target_code_rate=r,
+                            nof_harq_ack_bits=int(rng.choice([0, 1, 2, 3, 5, 11, 12, 19, 20, 40])),
+                            nof_csi_part1_bits=int(rng.choice([0, 1, 2, 7, 12, 30])),
+                            nof_csi_part2_bits=int(rng.choice([0, 0, 4, 25])),
+                            alpha_scaling=float(rng.choice([0.5, 0.65, 0.8, 1.0])),
+                            beta_offset_harq_ack=float(rng.choice([2.0, 5.0, 20.0])),
+                            beta_offset_csi_part1=float(rng.choice([1.125, 5.0, 6.25])),
+                            beta_offset_csi_part2=float(rng.choice([1.0, 5.0])), nof_rb=nrb, start_symbol_index=start,
+                            nof_symbols=nsym, dmrs_type=2 if t2 else 1, dmrs_symbol_mask=mask,
+                            nof_cdm_groups_without_data=int(rng.integers(1, 4 if t2 else 3)), nof_layers=layers,
+                            contains_dc=int(rng.integers(2)))
+        if tbs == 0 and c.nof_harq_ack_bits == 0 and c.nof_csi_part1_bits == 0:
+            continue
+        got = amd.ulsch_information(c)
+        assert got == _ref(c), (c.as_dict(), got)
+        n += 1
+    assert n > 2000
+
+
+def test_ulsch_information_rejects():
+    c = amd.UlschConfig(tbs=1024, modulation=2, target_code_rate=500.0, nof_rb=10, start_symbol_index=2,
+                        nof_symbols=10, dmrs_type=1, dmrs_symbol_mask=1 << 1, nof_cdm_groups_without_data=2,
+                        nof_layers=1)
+    with pytest.raises(ValueError):  # DM-RS before the allocation
+        amd.ulsch_information(c)
