@@ -170,3 +170,25 @@ def ue_transmit_tp(tb, pdu, nsubc, channel=None, snr_db=None, seed=0):
         z = z + sigma * (rng.normal(size=z.shape) + 1j * rng.normal(size=z.shape))
     g = (to_bf16(z.real.astype(np.float32)).astype(np.uint32) | (to_bf16(z.imag.astype(np.float32)).astype(np.uint32) << 16))
     return np.ascontiguousarray(g), p
+
+
+if REF is not None and hasattr(REF, "srs_ref_ulsch_demultiplex"):
+    REF.srs_ref_ulsch_demultiplex.restype = _c.c_int
+    REF.srs_ref_ulsch_demultiplex.argtypes = ([_c.c_int] + [_c.c_uint] * 5 + [_c.c_int] + [_c.c_uint] * 7
+                                              + [_c.c_void_p, _c.c_uint] + [_c.c_void_p] * 4)
+
+
+def ref_ulsch_demultiplex(llrs, qm, nof_layers, nof_prb, start_symbol, nof_symbols, nof_harq_ack_rvd, dmrs_type2,
+                          dmrs_mask, nof_cdm_groups_without_data, nof_harq_ack_bits, nof_enc_harq_ack_bits,
+                          nof_csi_part1_bits, nof_enc_csi_part1_bits, c_init):
+    """The reference ulsch_demultiplex_impl over one codeword: (UL-SCH, HARQ-ACK, CSI part 1) int8 streams."""
+    x = np.ascontiguousarray(llrs, np.int8)
+    sch, ack, csi1 = (np.zeros(x.size, np.int8) for _ in range(3))
+    counts = np.zeros(3, np.uint32)
+    r = REF.srs_ref_ulsch_demultiplex(qm, nof_layers, nof_prb, start_symbol, nof_symbols, nof_harq_ack_rvd,
+                                      int(dmrs_type2), dmrs_mask, nof_cdm_groups_without_data, nof_harq_ack_bits,
+                                      nof_enc_harq_ack_bits, nof_csi_part1_bits, nof_enc_csi_part1_bits, c_init,
+                                      _ptr(x), x.size, _ptr(sch), _ptr(ack), _ptr(csi1), _ptr(counts))
+    if r != 0:
+        raise RuntimeError("reference demultiplexer did not end every stream")
+    return sch[:counts[0]], ack[:counts[1]], csi1[:counts[2]]

@@ -112,3 +112,4 @@ __version__ = "0.1.0"
 from .transform_precoding import TransformPrecoder, is_nof_prbs_valid as transform_precoding_nof_prbs_valid  # noqa: F401,E402
 
 from .ulsch_info import UlschConfig, UlschInfo, ulsch_information  # noqa: F401,E402
+from .ulsch_demux import UlschDemux, UlschDemuxConfig, UlschDemuxPlan  # noqa: F401,E402
