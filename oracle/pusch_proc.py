@@ -192,3 +192,56 @@ def ref_ulsch_demultiplex(llrs, qm, nof_layers, nof_prb, start_symbol, nof_symbo
     if r != 0:
         raise RuntimeError("reference demultiplexer did not end every stream")
     return sch[:counts[0]], ack[:counts[1]], csi1[:counts[2]]
+
+
+if REF is not None and hasattr(REF, "srs_ref_uci_decode"):
+    REF.srs_ref_uci_decode.restype = _c.c_int
+    REF.srs_ref_uci_decode.argtypes = [_c.c_void_p, _c.c_uint, _c.c_uint, _c.c_int, _c.c_void_p]
+    REF.srs_ref_short_block_encode.restype = None
+    REF.srs_ref_short_block_encode.argtypes = [_c.c_void_p, _c.c_uint, _c.c_uint, _c.c_int, _c.c_void_p]
+
+
+def ref_uci_decode(llrs, K, qm):
+    """The reference uci_decoder_impl: (message bits, uci_status)."""
+    x = np.ascontiguousarray(llrs, np.int8)
+    msg = np.zeros(K, np.uint8)
+    st = REF.srs_ref_uci_decode(_ptr(x), x.size, K, qm, _ptr(msg))
+    return msg, st
+
+
+def _uci_crc(bits, L):
+    poly = 0x21 if L == 6 else 0x621
+    crc = 0
+    for b in bits:
+        fb = ((crc >> (L - 1)) & 1) ^ int(b)
+        crc = (crc << 1) & ((1 << L) - 1)
+        if fb:
+            crc ^= poly
+    return [(crc >> (L - 1 - i)) & 1 for i in range(L)]
+
+
+def uci_encode(msg, E, qm):
+    """UE-side UCI encoding (TS 38.212 6.3.1.2-6.3.1.4) for test inputs: the reference's short_block_encoder_impl for
+    <= 11 bits (placeholders 255 / 254 kept), else code block segmentation with filler bits, CRC6 / CRC11 and the
+    reference's polar chain (nMax 10, channel interleaver) per codeblock."""
+    msg = np.asarray(msg, np.uint8)
+    A = msg.size
+    out = np.zeros(E, np.uint8)
+    if A <= 11:
+        REF.srs_ref_short_block_encode(_ptr(np.ascontiguousarray(msg)), A, E, qm, _ptr(out))
+        return out
+    from . import ref_polar_encode_chain
+
+    C = 2 if (A >= 360 and E >= 1088) or A >= 1013 else 1
+    L = 6 if A < 20 else 11
+    F = (-A) % C
+    a = np.concatenate([np.zeros(F, np.uint8), msg])
+    per = a.size // C
+    pos = 0
+    for r in range(C):
+        cb = a[r * per:(r + 1) * per]
+        cb = np.concatenate([cb, np.array(_uci_crc(cb, L), np.uint8)])
+        e = E // C
+        out[pos:pos + e] = ref_polar_encode_chain(cb, e, 10, ibil=True)
+        pos += e
+    return out

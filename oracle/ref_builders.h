@@ -14,7 +14,6 @@
 // Glue (interfaces implemented here; nothing of the reference is replaced):
 //   inline_executor       task_executor that runs tasks inline
 //                         (the benchmark's inline_task_executor);
-//   no_uci_decoder        uci_decoder (the wrapped PDUs carry no UCI);
 //   ref_rx_buffer         unique_rx_buffer::callback over host vectors (the role
 //                         of lib/phy/upper/rx_buffer_impl.h), one HARQ process.
 #pragma once
@@ -42,6 +41,13 @@
 #include "phy/upper/sequence_generators/pseudo_random_generator_impl.h"
 #include "phy/upper/signal_processors/channel_estimator/port_channel_estimator_average_impl.h"
 #include "phy/upper/sequence_generators/low_papr_sequence_generator_impl.h"
+#include "phy/upper/channel_coding/polar/polar_code_impl.h"
+#include "phy/upper/channel_coding/polar/polar_deallocator_impl.h"
+#include "phy/upper/channel_coding/polar/polar_decoder_impl.h"
+#include "phy/upper/channel_coding/polar/polar_encoder_impl.h"
+#include "phy/upper/channel_coding/polar/polar_rate_dematcher_impl.h"
+#include "phy/upper/channel_coding/short/short_block_detector_impl.h"
+#include "phy/upper/channel_processors/uci/uci_decoder_impl.h"
 #include "phy/upper/signal_processors/pusch/dmrs_pusch_estimator_impl.h"
 #include "srsran/phy/upper/unique_rx_buffer.h"
 #include "srsran/support/cpu_features.h"
@@ -85,14 +91,20 @@ public:
 };
 
 
-class no_uci_decoder : public uci_decoder
+// uci_decoder_impl as create_uci_decoder_factory_generic builds it (uci/factories.cpp:44-55) from the short block
+// detector, the polar chain (nMax = 10) and the CRC6 / CRC11 calculators (the CRC factory takes the generic
+// calculator for CRC6, channel_coding_factories.cpp:70-72).
+inline std::unique_ptr<uci_decoder> make_uci_decoder()
 {
-public:
-  uci_status decode(span<uint8_t>, span<const log_likelihood_ratio>, const configuration&) override
-  {
-    std::abort();
-  }
-};
+  return std::make_unique<uci_decoder_impl>(std::make_unique<short_block_detector_impl>(),
+                                            std::make_unique<polar_code_impl>(),
+                                            std::make_unique<polar_rate_dematcher_impl>(),
+                                            std::make_unique<polar_decoder_impl>(std::make_unique<polar_encoder_impl>(),
+                                                                                 polar_code::NMAX_LOG),
+                                            std::make_unique<polar_deallocator_impl>(),
+                                            std::make_unique<crc_calculator_generic_impl>(crc_generator_poly::CRC6),
+                                            std::make_unique<crc_calculator_lut_impl>(crc_generator_poly::CRC11));
+}
 
 class ref_rx_buffer : public unique_rx_buffer::callback
 {
@@ -267,7 +279,7 @@ make_pusch_processor(impl choice, unsigned max_nof_rb, unsigned nof_rx_ports, un
                                                   b->exec),
       make_pusch_demodulator(eq, max_nof_rb, false, true),
       std::make_unique<ulsch_demultiplex_impl>(),
-      std::make_unique<no_uci_decoder>(),
+      make_uci_decoder(),
       dims));
   pusch_processor_impl::configuration cfg;
   cfg.dependencies_pool     = std::make_shared<pusch_processor_impl::concurrent_dependencies_pool_type>(deps);

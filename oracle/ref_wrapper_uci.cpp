@@ -4,6 +4,8 @@
 //
 // Glue (interfaces implemented here, nothing of the reference replaced):
 //   recording_buffer   pusch_decoder_buffer that appends every soft bit it is given.
+#include "ref_builders.h"
+#include "phy/upper/channel_coding/short/short_block_encoder_impl.h"
 #include "phy/upper/channel_processors/pusch/ulsch_demultiplex_impl.h"
 #include "phy/upper/sequence_generators/pseudo_random_generator_impl.h"
 #include "srsran/adt/bit_buffer.h"
@@ -33,7 +35,7 @@ public:
   bool                              ended = false;
 };
 
-modulation_scheme scheme(int qm)
+modulation_scheme scheme_uci(int qm)
 {
   switch (qm) {
     case 0:
@@ -66,7 +68,7 @@ int srs_ref_ulsch_demultiplex(int qm, unsigned nof_layers, unsigned nof_prb, uns
                               int8_t* sch, int8_t* ack, int8_t* csi1, unsigned* counts)
 {
   ulsch_demultiplex::configuration cfg;
-  cfg.modulation         = scheme(qm);
+  cfg.modulation         = scheme_uci(qm);
   cfg.nof_layers         = nof_layers;
   cfg.nof_prb            = nof_prb;
   cfg.start_symbol_index = start_symbol;
@@ -111,6 +113,26 @@ int srs_ref_ulsch_demultiplex(int qm, unsigned nof_layers, unsigned nof_prb, uns
   }
   const bool ok = b_sch.ended && (nof_harq_ack_bits == 0 || b_ack.ended) && (nof_csi_part1_bits == 0 || b_csi1.ended);
   return ok ? 0 : -1;
+}
+
+// uci_decoder_impl::decode (uci_decoder_impl.cpp:117-129) of E LLRs into K message bits; returns the uci_status.
+int srs_ref_uci_decode(const int8_t* llrs, unsigned E, unsigned K, int qm, uint8_t* message)
+{
+  auto                        dec = srs_ref::make_uci_decoder();
+  uci_decoder::configuration  cfg;
+  cfg.modulation = scheme_uci(qm);
+  return static_cast<int>(dec->decode(span<uint8_t>(message, K),
+                                      span<const log_likelihood_ratio>(
+                                          reinterpret_cast<const log_likelihood_ratio*>(llrs), E),
+                                      cfg));
+}
+
+// short_block_encoder_impl::encode (short_block_encoder_impl.cpp): K <= 11 message bits into E coded bits
+// (placeholders as the encoder writes them: 255 = x "one", 254 = y "repeat").
+void srs_ref_short_block_encode(const uint8_t* message, unsigned K, unsigned E, int qm, uint8_t* out)
+{
+  short_block_encoder_impl enc;
+  enc.encode(span<uint8_t>(out, E), span<const uint8_t>(message, K), scheme_uci(qm));
 }
 
 } // extern "C"
