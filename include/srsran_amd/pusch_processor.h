@@ -22,7 +22,9 @@
  * Nref = compute_N_ref(tbs_lbrm, C) (ldpc.h:225), nof_ch_symbols from
  * get_ulsch_information without UCI (all data REs x layers), rb_mask of the
  * type-1 allocation relative to the BWP (:166).
- * Scope: data-only PUSCH (no UCI multiplexing, the pdu carries a codeword),
+ * Scope: PUSCH with a codeword and, optionally, HARQ-ACK and CSI part 1 multiplexed on it
+ * (ulsch_demux.h, uci_decoder.h: ulsch_demultiplex_impl + uci_decoder_impl as pusch_processor_impl.cpp:252-334
+ * wires them; no CSI part 2, no UCI-only PUSCH),
  * DM-RS type 1 with the pseudo-random sequence, or transform precoding with the
  * low-PAPR DM-RS (pusch_processor_impl.cpp:172-196, validator :148-174), no DC-carrier
  * zeroing (pdu.dc_position unset). DM-RS type 2 is rejected as the reference's own
@@ -85,9 +87,16 @@ typedef struct srs_amd_pusch_pdu {
                                    PRB count, low-PAPR DM-RS of n_rs_id; dmrs_type / scrambling_id / n_scid /
                                    nof_cdm_groups_without_data are then unused (two CDM groups, as the reference) */
   uint32_t n_rs_id;           /* {0 .. 1007} */
+  /* uci_description (pusch_processor.h:64-90): HARQ-ACK and CSI part 1 payloads multiplexed with the UL-SCH
+     (0: none), the scaling and beta offsets of TS 38.213 9.3; CSI part 2 is not supported */
+  uint32_t nof_harq_ack;
+  uint32_t nof_csi_part1;
+  float    alpha_scaling;
+  float    beta_offset_harq_ack;
+  float    beta_offset_csi_part1;
 } srs_amd_pusch_pdu;
 
-/* Per-transport-block results: pusch_decoder_result (sch.h) and the channel
+/* Per-transport-block results: pusch_decoder_result (sch.h), the UCI statuses and the channel
  * state information channel_estimate::get_channel_state_information derives
  * (channel_estimation.h:244-286): SINR from the channel estimator
  * (layer-0 RSRP summed over ports / noise variances summed over ports), EPRE
@@ -98,6 +107,8 @@ typedef struct srs_amd_pusch_processor_result {
   float                        epre_db;
   float                        rsrp_db;
   float                        time_alignment_s;
+  int32_t                      harq_ack_status;  /* SRS_AMD_UCI_* (uci_decoder.h); 0 without HARQ-ACK */
+  int32_t                      csi_part1_status; /* SRS_AMD_UCI_*; 0 without CSI part 1 */
 } srs_amd_pusch_processor_result;
 
 typedef struct srs_amd_pusch_processor      srs_amd_pusch_processor;
@@ -130,6 +141,12 @@ typedef struct srs_amd_pusch_intermediates {
   srs_amd_chest_port_stats* d_port_stats;
   int8_t*                   d_llrs;
   uint32_t                  llr_stride;
+  /* UCI payloads (one bit per byte, pusch_processor_result_control::harq_ack / csi_part1): rows of nof_harq_ack /
+     nof_csi_part1 bytes, *_stride apart; NULL: not returned (the statuses are in the results either way) */
+  uint8_t*                  d_harq_ack;
+  uint32_t                  harq_ack_stride;
+  uint8_t*                  d_csi_part1;
+  uint32_t                  csi_part1_stride;
 } srs_amd_pusch_intermediates;
 
 /* DEVICE, asynchronous: nof_grids received grids cbf16 [grid][port][14][nof_subc]

@@ -31,7 +31,9 @@ if REF is not None and hasattr(REF, "srs_ref_pusch_process"):
                                                                              _c.c_uint, _c.c_uint, _c.c_int, _c.c_uint,
                                                                              _c.c_int, _c.c_uint]
                                           + [_c.c_uint] * 6 + [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_uint,
-                                                               _c.c_void_p, _c.c_void_p])
+                                                               _c.c_void_p, _c.c_void_p]
+                                          + [_c.c_uint, _c.c_uint, _c.c_float, _c.c_float, _c.c_float]
+                                          + [_c.c_void_p] * 3)
     REF.srs_ref_describe_choice.restype = _c.c_char_p
     REF.srs_ref_describe_choice.argtypes = [_c.c_int]
 
@@ -68,6 +70,9 @@ def ref_pusch_process(grid, pdu, tb_bytes, iterations=2, choice="auto", rx_buffe
     tb = np.zeros(tb_bytes, np.uint8)
     res = np.zeros(6, np.float64)
     csi = np.zeros(4, np.float64)
+    ack = np.zeros(max(1, pdu.get("nof_harq_ack", 0)), np.uint8)
+    csi1 = np.zeros(max(1, pdu.get("nof_csi_part1", 0)), np.uint8)
+    ust = np.zeros(2, np.int32)
     r = REF.srs_ref_pusch_process(
         _ptr(g), P, nsubc, pdu["numerology"], pdu["slot_index"], pdu["rnti"], pdu["bwp_start_rb"], pdu["bwp_size_rb"],
         pdu["modulation"], float(pdu["target_code_rate"]), pdu["rv"], pdu["base_graph"], int(pdu["new_data"]),
@@ -75,17 +80,22 @@ def ref_pusch_process(grid, pdu, tb_bytes, iterations=2, choice="auto", rx_buffe
         pdu.get("n_rs_id", 0) if tp else pdu["scrambling_id"], int(pdu["n_scid"]),
         pdu["nof_cdm_groups_without_data"], pdu["rb_start"], pdu["rb_count"], pdu["start_symbol_index"],
         pdu["nof_symbols"], pdu.get("tbs_lbrm_bytes", 0), iterations, CHOICE[choice], buf.h, _ptr(tb), tb_bytes,
-        _ptr(res), _ptr(csi))
+        _ptr(res), _ptr(csi), pdu.get("nof_harq_ack", 0), pdu.get("nof_csi_part1", 0),
+        float(pdu.get("alpha_scaling", 1.0)), float(pdu.get("beta_offset_harq_ack", 5.0)),
+        float(pdu.get("beta_offset_csi_part1", 5.0)), _ptr(ack), _ptr(csi1), _ptr(ust))
     if r != 0:
         raise RuntimeError("reference PUSCH processor did not notify")
     return tb, dict(tb_crc_ok=bool(res[0]), nof_codeblocks_total=int(res[1]), nof_observations=int(res[2]),
                     iterations_sum=int(round(res[3])), iterations_min=int(res[4]), iterations_max=int(res[5]),
-                    sinr_db=csi[0], epre_db=csi[1], rsrp_db=csi[2], time_alignment_s=csi[3])
+                    sinr_db=csi[0], epre_db=csi[1], rsrp_db=csi[2], time_alignment_s=csi[3],
+                    harq_ack=ack[:pdu.get("nof_harq_ack", 0)], csi_part1=csi1[:pdu.get("nof_csi_part1", 0)],
+                    harq_ack_status=int(ust[0]), csi_part1_status=int(ust[1]))
 
 
-def ue_transmit(tb, pdu, nsubc, channel=None, snr_db=None, seed=0, nof_rx_ports=None):
+def ue_transmit(tb, pdu, nsubc, channel=None, snr_db=None, seed=0, nof_rx_ports=None, uci=None):
     """UE PUSCH transmission of transport block bytes `tb` for `pdu` (dict), through `channel`
-    (complex [layer][rx port], default identity) plus AWGN at snr_db (None: noiseless).
+    (complex [layer][rx port], default identity) plus AWGN at snr_db (None: noiseless).  uci: optional
+    (HARQ-ACK bits, CSI part 1 bits) multiplexed with the UL-SCH (ue_multiplex_uci).
     Returns the received grid uint32 [rx ports][14][nsubc] (cbf16) and the UL-SCH plan."""
     from .pdsch_mod import ref_dmrs_pdsch_map, ref_pdsch_modulate, to_bf16
     from .pusch_demod import data_re_mask
@@ -101,10 +111,17 @@ def ue_transmit(tb, pdu, nsubc, channel=None, snr_db=None, seed=0, nof_rx_ports=
                         pdu["nof_cdm_groups_without_data"])
     nre = int(mask.sum())
     tbs = len(tb) * 8
+    nch = nre * L
+    info = None
+    if uci is not None:
+        info = ref_ulsch_information(pdu, tbs)
+        nch = info["nof_ul_sch_bits"] // pdu["modulation"]
     p = osch.plan(tbs, pdu["base_graph"], pdu["rv"], pdu["modulation"], nref(tbs, pdu["base_graph"],
                                                                             pdu.get("tbs_lbrm_bytes", 0)),
-                  L, nre * L)
+                  L, nch)
     cw = ref_pdsch_encode(np.asarray(tb, np.uint8), p)
+    if uci is not None:
+        cw = ue_multiplex_uci(cw, pdu, info, nre * L * pdu["modulation"], uci[0], uci[1])
     grid = np.zeros((P, 14, nsubc, 2), np.uint16)
     ref_pdsch_modulate(grid, cw, pdu["rnti"], pdu["n_id"], pdu["modulation"], crbs, pdu["start_symbol_index"],
                        pdu["nof_symbols"], pdu["dmrs_symbol_mask"], False, pdu["nof_cdm_groups_without_data"], [],
@@ -245,3 +262,76 @@ def uci_encode(msg, E, qm):
         out[pos:pos + e] = ref_polar_encode_chain(cb, e, 10, ibil=True)
         pos += e
     return out
+
+
+if REF is not None and hasattr(REF, "srs_ref_ulsch_information"):
+    REF.srs_ref_ulsch_information.restype = None
+    REF.srs_ref_ulsch_information.argtypes = ([_c.c_uint, _c.c_int, _c.c_float] + [_c.c_uint] * 3 + [_c.c_float] * 4
+                                              + [_c.c_uint] * 3 + [_c.c_int] + [_c.c_uint] * 3
+                                              + [_c.c_int, _c.c_void_p])
+
+ULSCH_INFO_FIELDS = ["nof_ul_sch_bits", "nof_harq_ack_bits", "nof_harq_ack_rvd", "nof_csi_part1_bits",
+                     "nof_csi_part2_bits", "nof_harq_ack_re", "nof_csi_part1_re", "nof_csi_part2_re",
+                     "nof_dc_overlap_bits", "sch_tb_crc_size", "sch_base_graph", "sch_nof_cb", "sch_lifting_size",
+                     "sch_nof_bits_per_cb", "sch_nof_filler_bits_per_cb"]
+
+
+def ref_ulsch_information(pdu, tbs):
+    """The reference get_ulsch_information for a PUSCH pdu dict (type-1 DM-RS, no CSI part 2, no DC)."""
+    out = np.zeros(15, np.uint32)
+    REF.srs_ref_ulsch_information(tbs, pdu["modulation"], float(pdu["target_code_rate"]), pdu.get("nof_harq_ack", 0),
+                                  pdu.get("nof_csi_part1", 0), 0, float(pdu.get("alpha_scaling", 1.0)),
+                                  float(pdu.get("beta_offset_harq_ack", 5.0)),
+                                  float(pdu.get("beta_offset_csi_part1", 5.0)), 5.0, pdu["rb_count"],
+                                  pdu["start_symbol_index"], pdu["nof_symbols"], 0, pdu["dmrs_symbol_mask"],
+                                  pdu["nof_cdm_groups_without_data"], pdu["nof_tx_layers"], 0, _ptr(out))
+    return dict(zip(ULSCH_INFO_FIELDS, out.tolist()))
+
+
+def ue_multiplex_uci(sch_cw, pdu, info, nof_cw_bits, ack_bits, csi1_bits):
+    """UE-side UL-SCH / UCI multiplexing for test inputs (TS 38.212 6.2.7 + 6.3.2.1): the UCI encoded with
+    uci_encode, the RE placement read off the reference's own demultiplexer (three probe passes with the RE index
+    coded in the LLR values), the ACK of <= 2 bits puncturing the UL-SCH, and the scrambler's placeholder rules
+    (x -> 1, y -> the previous scrambled bit) folded in by pre-XOR-ing the Gold sequence, so that a modulator that
+    scrambles every bit produces the UE's symbols.  Returns the codeword to hand to the modulator."""
+    from . import ref_prbs
+
+    qm, L = pdu["modulation"], pdu["nof_tx_layers"]
+    bpre = qm * L
+    nre = nof_cw_bits // bpre
+    K_ack, K_csi1 = len(ack_bits), len(csi1_bits)
+    enc_ack = uci_encode(ack_bits, info["nof_harq_ack_bits"], qm) if K_ack else np.zeros(0, np.uint8)
+    enc_csi1 = uci_encode(csi1_bits, info["nof_csi_part1_bits"], qm) if K_csi1 else np.zeros(0, np.uint8)
+    c_init = (pdu["rnti"] << 15) + pdu["n_id"]
+    args = (qm, L, pdu["rb_count"], pdu["start_symbol_index"], pdu["nof_symbols"], info["nof_harq_ack_rvd"], False,
+            pdu["dmrs_symbol_mask"], pdu["nof_cdm_groups_without_data"], K_ack, info["nof_harq_ack_bits"], K_csi1,
+            info["nof_csi_part1_bits"], 0)
+    src = [None, None, None]
+    for k in range(3):
+        code = (((np.arange(nre) >> (7 * k)) & 0x7F) + 1).astype(np.int8)
+        streams = ref_ulsch_demultiplex(np.repeat(code, bpre), *args)
+        for i, st in enumerate(streams):
+            v = (np.abs(st.astype(np.int32)) - 1).clip(min=0) << (7 * k)
+            src[i] = v if src[i] is None else src[i] + v
+    out = np.zeros(nof_cw_bits, np.uint8)
+    pos = np.arange(bpre)
+    # UL-SCH REs (the zero LLRs of the demultiplexer's SCH stream are the REs an ACK of <= 2 bits punctures)
+    sch_src = src[0].reshape(-1, bpre)[:, 0]
+    for j, r in enumerate(sch_src):
+        out[r * bpre + pos] = sch_cw[j * bpre + pos]
+    for s_i, enc in ((1, enc_ack), (2, enc_csi1)):
+        if enc.size:
+            for j, r in enumerate(src[s_i].reshape(-1, bpre)[:, 0]):
+                out[r * bpre + pos] = enc[j * bpre + pos]
+    # scrambling with placeholders (TS 38.211 6.3.1.1), expressed as the bits a plain scrambler receives
+    c = ref_prbs(c_init, nof_cw_bits)
+    scr = np.zeros(nof_cw_bits, np.uint8)
+    for i in range(nof_cw_bits):
+        b = out[i]
+        if b == 255:
+            scr[i] = 1
+        elif b == 254:
+            scr[i] = scr[i - 1]
+        else:
+            scr[i] = b ^ c[i]
+    return scr ^ c

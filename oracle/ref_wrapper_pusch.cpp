@@ -22,6 +22,7 @@
 #include "srsran/phy/upper/channel_processors/pusch/pusch_processor_result_notifier.h"
 #include "srsran/ran/sch/sch_constants.h"
 #include <atomic>
+#include <vector>
 #include <cmath>
 #include <cstring>
 
@@ -115,7 +116,20 @@ public:
 class result_notifier : public pusch_processor_result_notifier
 {
 public:
-  void on_uci(const pusch_processor_result_control&) override { ++nof_uci; }
+  void on_uci(const pusch_processor_result_control& uci) override
+  {
+    ++nof_uci;
+    harq_ack_status = static_cast<int>(uci.harq_ack.status);
+    csi1_status     = static_cast<int>(uci.csi_part1.status);
+    harq_ack.resize(uci.harq_ack.payload.size());
+    for (size_t i = 0; i != harq_ack.size(); ++i) {
+      harq_ack[i] = uci.harq_ack.payload.test(i) ? 1 : 0;
+    }
+    csi1.resize(uci.csi_part1.payload.size());
+    for (size_t i = 0; i != csi1.size(); ++i) {
+      csi1[i] = uci.csi_part1.payload.test(i) ? 1 : 0;
+    }
+  }
   void on_sch(const pusch_processor_result_data& sch) override
   {
     result = sch;
@@ -124,6 +138,8 @@ public:
   pusch_processor_result_data result;
   bool                        done    = false;
   unsigned                    nof_uci = 0;
+  int                         harq_ack_status = 0, csi1_status = 0;
+  std::vector<uint8_t>        harq_ack, csi1;
 };
 
 } // namespace
@@ -256,6 +272,9 @@ int srs_ref_pusch_demodulate(const uint32_t* grid,
 // dmrs_type2: 0 type 1, 1 type 2, 2 transform precoding (low-PAPR DM-RS, n_rs_id = scrambling_id).
 // choice: 0 generic, 1 AVX2, 2 the "auto" factory choice (ref_builders.h).
 // rx_buffer: srs_ref_rx_buffer_create handle (HARQ process). tb: tb_bytes output bytes.
+// UCI: nof_harq_ack / nof_csi_part1 payload bits with their alpha / beta offsets; the decoded payloads (one bit per
+// byte) and uci_status values (0 unknown, 1 valid, 2 invalid) come back in harq_ack_out / csi_part1_out /
+// uci_status_out[2].
 // result[0..5] = tb_crc_ok, nof_codeblocks_total, LDPC observations, sum, min, max;
 // csi[0..3] = SINR (channel estimator, dB), EPRE dB, RSRP dB, time alignment (s).
 int srs_ref_pusch_process(const uint32_t* grid,
@@ -289,7 +308,15 @@ int srs_ref_pusch_process(const uint32_t* grid,
                           uint8_t*        tb,
                           unsigned        tb_bytes,
                           double*         result,
-                          double*         csi)
+                          double*         csi,
+                          unsigned        nof_harq_ack,
+                          unsigned        nof_csi_part1,
+                          float           alpha_scaling,
+                          float           beta_harq_ack,
+                          float           beta_csi_part1,
+                          uint8_t*        harq_ack_out,
+                          uint8_t*        csi_part1_out,
+                          int*            uci_status_out)
 {
   const unsigned nof_prb = nsubc / NRE;
   auto           bundle  = make_pusch_processor(
@@ -309,12 +336,12 @@ int srs_ref_pusch_process(const uint32_t* grid,
   pdu.mcs_descr              = sch_mcs_description{scheme_of(qm), target_code_rate};
   pdu.codeword.emplace(pusch_processor::codeword_description{
       rv, base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2, new_data != 0});
-  pdu.uci.alpha_scaling         = 1.0;
-  pdu.uci.beta_offset_harq_ack  = 5.0;
-  pdu.uci.beta_offset_csi_part1 = 5.0;
+  pdu.uci.alpha_scaling         = alpha_scaling;
+  pdu.uci.beta_offset_harq_ack  = beta_harq_ack;
+  pdu.uci.beta_offset_csi_part1 = beta_csi_part1;
   pdu.uci.beta_offset_csi_part2 = 5.0;
-  pdu.uci.nof_harq_ack          = 0;
-  pdu.uci.nof_csi_part1         = 0;
+  pdu.uci.nof_harq_ack          = nof_harq_ack;
+  pdu.uci.nof_csi_part1         = nof_csi_part1;
   pdu.n_id                      = n_id;
   pdu.nof_tx_layers             = nof_layers;
   for (unsigned p = 0; p != nof_rx_ports; ++p) {
@@ -340,6 +367,16 @@ int srs_ref_pusch_process(const uint32_t* grid,
   bundle->proc->process(span<uint8_t>(tb, tb_bytes), std::move(buf), notifier, reader, pdu);
   if (!notifier.done) {
     return -1;
+  }
+  if (uci_status_out != nullptr) {
+    uci_status_out[0] = notifier.harq_ack_status;
+    uci_status_out[1] = notifier.csi1_status;
+    for (size_t i = 0; i != notifier.harq_ack.size() && harq_ack_out != nullptr; ++i) {
+      harq_ack_out[i] = notifier.harq_ack[i];
+    }
+    for (size_t i = 0; i != notifier.csi1.size() && csi_part1_out != nullptr; ++i) {
+      csi_part1_out[i] = notifier.csi1[i];
+    }
   }
   const pusch_decoder_result& r  = notifier.result.data;
   const auto&                 st = r.ldpc_decoder_stats;

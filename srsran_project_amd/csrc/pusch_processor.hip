@@ -33,6 +33,8 @@ __global__ __launch_bounds__(64) void pusch_result_kernel(pusch_result_args a)
   r.epre_db          = 10.0f * log10f(epre / static_cast<float>(P));
   r.rsrp_db          = 10.0f * log10f(rsrp / static_cast<float>(P));
   r.time_alignment_s = st[best].time_alignment_s;
+  r.harq_ack_status  = (a.uci_mask & 1u) ? a.uci_status[2 * g] : 0;
+  r.csi_part1_status = (a.uci_mask & 2u) ? a.uci_status[2 * g + 1] : 0;
   a.results[g]       = r;
 }
 

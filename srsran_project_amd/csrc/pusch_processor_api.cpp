@@ -5,6 +5,9 @@
 // grids, with the processor's own HBM scratch between them.
 #include "srsran_amd/pusch_processor.h"
 #include "srsran_amd/transform_precoding.h"
+#include "srsran_amd/uci_decoder.h"
+#include "srsran_amd/ulsch_demux.h"
+#include "srsran_amd/ulsch_info.h"
 
 #include <hip/hip_runtime.h>
 
@@ -28,6 +31,9 @@ struct srs_amd_pusch_processor {
   srs_amd_pusch_chest*           chest  = nullptr;
   srs_amd_pusch_demodulator*     demod  = nullptr;
   srs_amd_pusch_decoder*         dec    = nullptr;
+  srs_amd_ulsch_demux*           demux  = nullptr; // UCI on PUSCH: demultiplexer and decoder
+  srs_amd_uci_decoder*           uci    = nullptr;
+  device_buffer                  cw_llrs, uci_llrs, uci_payload, uci_status;
   hipStream_t                    stream = nullptr; // host-call stream
   device_buffer                  estimates, stats, llrs, dec_results, host_io, slot_ports;
   stream_order                   order;
@@ -44,6 +50,8 @@ struct srs_amd_pusch_processor {
     srs_amd_pusch_chest_destroy(chest);
     srs_amd_pusch_demodulator_destroy(demod);
     srs_amd_pusch_decoder_destroy(dec);
+    srs_amd_ulsch_demux_destroy(demux);
+    srs_amd_uci_decoder_destroy(uci);
   }
 };
 
@@ -57,7 +65,16 @@ struct srs_amd_pusch_processor_plan {
   srs_amd_pusch_decoder_config dec_cfg{};
   uint64_t                     soft_bytes = 0;
   bool                         fusable    = false; // the fused estimator-equalizer path covers this PDU
-  ~srs_amd_pusch_processor_plan() { srs_amd_pusch_demod_plan_destroy(demod_plan); }
+  // UCI on PUSCH: multiplexing geometry (get_ulsch_information), demultiplexer plan, codeword bits
+  bool                         uci        = false;
+  srs_amd_ulsch_info           info{};
+  srs_amd_ulsch_demux_plan*    demux_plan = nullptr;
+  uint32_t                     cw_bits    = 0;
+  ~srs_amd_pusch_processor_plan()
+  {
+    srs_amd_pusch_demod_plan_destroy(demod_plan);
+    srs_amd_ulsch_demux_plan_destroy(demux_plan);
+  }
 };
 
 namespace {
@@ -117,6 +134,12 @@ int srs_amd_pusch_processor_create(srs_amd_pusch_processor**             proc,
   }
   if (rc == SRS_AMD_OK) {
     rc = srs_amd_pusch_decoder_create(&p->dec, cfg->ldpc_arith, device);
+  }
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_ulsch_demux_create(&p->demux, device);
+  }
+  if (rc == SRS_AMD_OK) {
+    rc = srs_amd_uci_decoder_create(&p->uci, device);
   }
   if (rc == SRS_AMD_OK) {
     hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
@@ -235,11 +258,63 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
     delete pl;
     return rc;
   }
-  // decoder configuration (pusch_processor_impl.cpp:322-347): UL-SCH without UCI gets every data RE
+  // UCI multiplexing (pusch_processor_impl.cpp:252-299): the geometry of get_ulsch_information, the
+  // demultiplexer's placement; the UL-SCH then gets nof_ul_sch_bits of the codeword's bits
+  const uint32_t qm_bits  = pdu->modulation < 2 ? 1u : static_cast<uint32_t>(pdu->modulation);
+  pl->cw_bits             = pl->nof_re * pdu->nof_tx_layers * qm_bits;
+  uint32_t       sch_bits = pl->cw_bits;
+  pl->uci                 = pdu->nof_harq_ack != 0 || pdu->nof_csi_part1 != 0;
+  if (pl->uci) {
+    srs_amd_ulsch_config uc{};
+    uc.tbs                         = pdu->tbs;
+    uc.modulation                  = pdu->modulation;
+    uc.target_code_rate            = pdu->target_code_rate;
+    uc.nof_harq_ack_bits           = pdu->nof_harq_ack;
+    uc.nof_csi_part1_bits          = pdu->nof_csi_part1;
+    uc.alpha_scaling               = pdu->alpha_scaling;
+    uc.beta_offset_harq_ack        = pdu->beta_offset_harq_ack;
+    uc.beta_offset_csi_part1       = pdu->beta_offset_csi_part1;
+    uc.nof_rb                      = pdu->rb_count;
+    uc.start_symbol_index          = pdu->start_symbol_index;
+    uc.nof_symbols                 = pdu->nof_symbols;
+    uc.dmrs_type                   = 1;
+    uc.dmrs_symbol_mask            = pdu->dmrs_symbol_mask;
+    uc.nof_cdm_groups_without_data = ncdm;
+    uc.nof_layers                  = pdu->nof_tx_layers;
+    rc                             = srs_amd_ulsch_information(&uc, &pl->info);
+    srs_amd_ulsch_demux_config dx{};
+    dx.modulation                  = pdu->modulation;
+    dx.nof_layers                  = pdu->nof_tx_layers;
+    dx.nof_prb                     = pdu->rb_count;
+    dx.start_symbol_index          = pdu->start_symbol_index;
+    dx.nof_symbols                 = pdu->nof_symbols;
+    dx.nof_harq_ack_rvd            = pl->info.nof_harq_ack_rvd;
+    dx.dmrs_type                   = 1;
+    dx.dmrs_symbol_mask            = pdu->dmrs_symbol_mask;
+    dx.nof_cdm_groups_without_data = ncdm;
+    dx.nof_harq_ack_bits           = pdu->nof_harq_ack;
+    dx.nof_enc_harq_ack_bits       = pl->info.nof_harq_ack_bits;
+    dx.nof_csi_part1_bits          = pdu->nof_csi_part1;
+    dx.nof_enc_csi_part1_bits      = pl->info.nof_csi_part1_bits;
+    dx.c_init                      = (pdu->rnti << 15) + pdu->n_id;
+    uint32_t total                 = 0;
+    if (rc == SRS_AMD_OK) {
+      rc = srs_amd_ulsch_demux_plan_create(proc->demux, &dx, &pl->demux_plan, &total, &sch_bits);
+    }
+    if (rc == SRS_AMD_OK && (total != pl->cw_bits || sch_bits != pl->info.nof_ul_sch_bits)) {
+      rc = fail(SRS_AMD_EINVAL, "UCI multiplexing geometry mismatch (%u / %u codeword bits, %u / %u UL-SCH bits).",
+                total, pl->cw_bits, sch_bits, pl->info.nof_ul_sch_bits);
+    }
+    if (rc != SRS_AMD_OK) {
+      delete pl;
+      return rc;
+    }
+  }
+  // decoder configuration (pusch_processor_impl.cpp:322-347): the UL-SCH's share of the codeword
   const uint32_t C       = nof_codeblocks(pdu->tbs, pdu->base_graph);
   const uint32_t tbs_lbrm = pdu->tbs_lbrm_bytes ? pdu->tbs_lbrm_bytes : 159749u; // tbs_lbrm_default
   rc = srs_amd_sch_plan_compute(&pl->sch, pdu->tbs, pdu->base_graph, pdu->rv, static_cast<uint32_t>(pdu->modulation),
-                                compute_N_ref(tbs_lbrm, C), pdu->nof_tx_layers, pl->nof_re * pdu->nof_tx_layers);
+                                compute_N_ref(tbs_lbrm, C), pdu->nof_tx_layers, sch_bits / qm_bits);
   if (rc != SRS_AMD_OK) {
     delete pl;
     return rc;
@@ -292,6 +367,7 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
     return fail(SRS_AMD_EINVAL, "grid or transport block stride too small");
   }
   const uint32_t G            = plan->sch.cw_length;
+  const bool     uci          = plan->uci;
   const bool     own_est      = io == nullptr || io->d_estimates == nullptr;
   // Without a caller estimate buffer the equalizer rebuilds each RE's estimate from the estimator's
   // per-subcarrier output (pusch_demod.hip pusch_equalize_fused_kernel): no estimate tensor in HBM.
@@ -317,6 +393,23 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   if (e == hipSuccess) {
     e = proc->dec_results.ensure(static_cast<size_t>(nof_grids) * sizeof(srs_amd_pusch_decoder_result));
   }
+  // UCI: the whole codeword's LLRs before the demultiplexer, the UCI streams, payloads and statuses
+  const uint64_t cw_stride  = align_up(plan->cw_bits, 64);
+  const uint64_t ack_e      = plan->info.nof_harq_ack_bits, csi1_e = plan->info.nof_csi_part1_bits;
+  const uint64_t uci_stride = align_up(ack_e + csi1_e, 64);
+  const uint32_t K_ack = plan->pdu.nof_harq_ack, K_csi1 = plan->pdu.nof_csi_part1;
+  if (e == hipSuccess && uci) {
+    e = proc->cw_llrs.ensure(nof_grids * cw_stride);
+  }
+  if (e == hipSuccess && uci) {
+    e = proc->uci_llrs.ensure(nof_grids * uci_stride);
+  }
+  if (e == hipSuccess && uci) {
+    e = proc->uci_payload.ensure(nof_grids * align_up(K_ack + K_csi1, 64));
+  }
+  if (e == hipSuccess && uci) {
+    e = proc->uci_status.ensure(static_cast<size_t>(nof_grids) * 2 * sizeof(int32_t));
+  }
   if (e == hipSuccess) {
     e = proc->order.begin(s);
   }
@@ -326,22 +419,46 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   srs_amd_chest_port_stats* st   = (io && io->d_port_stats) ? io->d_port_stats : proc->stats.as<srs_amd_chest_port_stats>();
   uint32_t*                 est  = own_est ? proc->estimates.as<uint32_t>() : io->d_estimates;
   int8_t*                   llrs = own_llrs ? proc->llrs.as<int8_t>() : io->d_llrs;
+  // the demodulator's rows: the UL-SCH LLRs directly, or with UCI the whole codeword for the demultiplexer
+  int8_t*        dem_rows   = uci ? proc->cw_llrs.as<int8_t>() : llrs;
+  const uint64_t dem_stride = uci ? cw_stride : llr_stride;
   int rc;
   if (fused) {
     chest_args view;
     rc = chest_estimate_batch_unexpanded(proc->chest, &plan->chest_cfg, d_grids, grid_stride, P, plan->nof_subc,
                                          nof_grids, st, stream, &view);
     if (rc == SRS_AMD_OK) {
-      rc = pusch_demodulate_batch_fused(proc->demod, plan->demod_plan, d_grids, grid_stride, view, st, llrs, llr_stride,
-                                        nof_grids, stream);
+      rc = pusch_demodulate_batch_fused(proc->demod, plan->demod_plan, d_grids, grid_stride, view, st, dem_rows,
+                                        dem_stride, nof_grids, stream);
     }
   } else {
     rc = srs_amd_pusch_chest_estimate_batch(proc->chest, &plan->chest_cfg, d_grids, grid_stride, P, plan->nof_subc,
                                             nof_grids, est, est_stride, st, stream);
     if (rc == SRS_AMD_OK) {
       rc = srs_amd_pusch_demodulate_batch(proc->demod, plan->demod_plan, d_grids, grid_stride, est, est_stride, st,
-                                          llrs, llr_stride, nof_grids, stream);
+                                          dem_rows, dem_stride, nof_grids, stream);
     }
+  }
+  // UL-SCH / HARQ-ACK / CSI part 1 (ulsch_demultiplex_impl), then the UCI decoders (uci_decoder_impl)
+  int8_t* uci_rows = proc->uci_llrs.as<int8_t>();
+  if (rc == SRS_AMD_OK && uci) {
+    rc = srs_amd_ulsch_demultiplex_batch(proc->demux, plan->demux_plan, dem_rows, cw_stride, llrs, llr_stride,
+                                         uci_rows, uci_stride, uci_rows + ack_e, uci_stride, nof_grids, stream);
+  }
+  if (rc == SRS_AMD_OK && uci && K_ack != 0) {
+    const bool out = io != nullptr && io->d_harq_ack != nullptr;
+    rc = srs_amd_uci_decode_batch(proc->uci, uci_rows, uci_stride, static_cast<uint32_t>(ack_e), K_ack,
+                                  plan->pdu.modulation, out ? io->d_harq_ack : proc->uci_payload.as<uint8_t>(),
+                                  out ? io->harq_ack_stride : align_up(K_ack + K_csi1, 64),
+                                  proc->uci_status.as<int32_t>(), 2 * sizeof(int32_t), nof_grids, stream);
+  }
+  if (rc == SRS_AMD_OK && uci && K_csi1 != 0) {
+    const bool out = io != nullptr && io->d_csi_part1 != nullptr;
+    rc = srs_amd_uci_decode_batch(proc->uci, uci_rows + ack_e, uci_stride, static_cast<uint32_t>(csi1_e), K_csi1,
+                                  plan->pdu.modulation,
+                                  out ? io->d_csi_part1 : proc->uci_payload.as<uint8_t>() + K_ack,
+                                  out ? io->csi_part1_stride : align_up(K_ack + K_csi1, 64),
+                                  proc->uci_status.as<int32_t>() + 1, 2 * sizeof(int32_t), nof_grids, stream);
   }
   if (rc == SRS_AMD_OK) {
     rc = srs_amd_pusch_decode_batch(proc->dec, &plan->sch, &plan->dec_cfg, d_tbs, tb_stride,
@@ -357,6 +474,10 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   a.results     = d_results;
   a.nof_grids   = nof_grids;
   a.nof_ports   = P;
+  if (uci) {
+    a.uci_status = proc->uci_status.as<int32_t>();
+    a.uci_mask   = (K_ack != 0 ? 1 : 0) | (K_csi1 != 0 ? 2 : 0);
+  }
   e             = launch_pusch_result(a, s);
   if (e == hipSuccess) {
     e = proc->order.end(s);
@@ -398,6 +519,9 @@ int srs_amd_pusch_process_slot(srs_amd_pusch_processor*        proc,
     }
     if (!pl->dec_cfg.new_data) {
       return fail(SRS_AMD_EINVAL, "PDU %u: HARQ retransmissions go through srs_amd_pusch_process_batch", i);
+    }
+    if (pl->uci) {
+      return fail(SRS_AMD_EINVAL, "PDU %u: UCI on PUSCH goes through srs_amd_pusch_process_batch", i);
     }
     if (pl->nof_subc != nof_subc) {
       return fail(SRS_AMD_EINVAL, "PDU %u: plans of different grid sizes", i);

@@ -19,6 +19,9 @@ struct pusch_result_args {
   // slot form: PDU g has port_counts[g] ports, its stats at stats + g * stats_stride
   const uint32_t*                     port_counts  = nullptr;
   uint32_t                            stats_stride = 0;
+  // UCI on PUSCH: statuses [grid][2] (HARQ-ACK, CSI part 1) of the fields set in uci_mask (bit 0, bit 1)
+  const int32_t*                      uci_status   = nullptr;
+  uint32_t                            uci_mask     = 0;
 };
 
 hipError_t launch_pusch_result(const pusch_result_args& a, hipStream_t stream);

@@ -46,14 +46,17 @@ class PuschPdu(ctypes.Structure):
         [(n, ctypes.c_uint32) for n in ("n_id", "nof_tx_layers", "nof_rx_ports", "dmrs_symbol_mask", "dmrs_type",
                                         "scrambling_id", "n_scid", "nof_cdm_groups_without_data", "rb_start",
                                         "rb_count", "start_symbol_index", "nof_symbols", "tbs_lbrm_bytes", "tbs",
-                                        "transform_precoding", "n_rs_id")]
+                                        "transform_precoding", "n_rs_id", "nof_harq_ack", "nof_csi_part1")] + \
+        [("alpha_scaling", ctypes.c_float), ("beta_offset_harq_ack", ctypes.c_float),
+         ("beta_offset_csi_part1", ctypes.c_float)]
 
 
 class PuschProcessorResult(ctypes.Structure):
     """``srs_amd_pusch_processor_result``: pusch_decoder_result + channel state information."""
 
     _fields_ = [("data", PuschDecoderResult), ("sinr_db", ctypes.c_float), ("epre_db", ctypes.c_float),
-                ("rsrp_db", ctypes.c_float), ("time_alignment_s", ctypes.c_float)]
+                ("rsrp_db", ctypes.c_float), ("time_alignment_s", ctypes.c_float),
+                ("harq_ack_status", ctypes.c_int32), ("csi_part1_status", ctypes.c_int32)]
 
 
 RESULT_BYTES = ctypes.sizeof(PuschProcessorResult)
@@ -63,7 +66,9 @@ class PuschIntermediates(ctypes.Structure):
     """``srs_amd_pusch_intermediates``: caller-owned buffers for the processor's intermediate results."""
 
     _fields_ = [("d_estimates", ctypes.c_void_p), ("est_stride", ctypes.c_uint64), ("d_port_stats", ctypes.c_void_p),
-                ("d_llrs", ctypes.c_void_p), ("llr_stride", ctypes.c_uint32)]
+                ("d_llrs", ctypes.c_void_p), ("llr_stride", ctypes.c_uint32),
+                ("d_harq_ack", ctypes.c_void_p), ("harq_ack_stride", ctypes.c_uint32),
+                ("d_csi_part1", ctypes.c_void_p), ("csi_part1_stride", ctypes.c_uint32)]
 
 
 class PuschSlotPdu(ctypes.Structure):
@@ -79,7 +84,8 @@ def make_pdu(**kw):
              target_code_rate=679.0, rv=0, base_graph=1, new_data=1, n_id=0, nof_tx_layers=1, nof_rx_ports=1,
              dmrs_symbol_mask=(1 << 2) | (1 << 11), dmrs_type=1, scrambling_id=0, n_scid=0,
              nof_cdm_groups_without_data=2, rb_start=0, rb_count=None, start_symbol_index=0, nof_symbols=14,
-             tbs_lbrm_bytes=0, tbs=0, transform_precoding=0, n_rs_id=0)
+             tbs_lbrm_bytes=0, tbs=0, transform_precoding=0, n_rs_id=0, nof_harq_ack=0, nof_csi_part1=0,
+             alpha_scaling=1.0, beta_offset_harq_ack=5.0, beta_offset_csi_part1=5.0)
     d.update(kw)
     if d["rb_count"] is None:
         d["rb_count"] = d["bwp_size_rb"] - d["rb_start"]
@@ -190,10 +196,11 @@ class PuschProcessor:
         return tb, res
 
     def process_batch(self, grids, plan, tbs=None, results=None, soft=None, port_stats=None, estimates=None,
-                      llrs=None, stream=None):
+                      llrs=None, stream=None, harq_ack=None, csi_part1=None):
         """Device: grids int32 [n][P][14][nsubc] -> tbs uint8 [n][tbs/8], results uint8 [n][RESULT_BYTES].
         Optional caller buffers for the intermediates: port_stats float32 [n][P][6], estimates int32
-        [n][P][L][14][nsubc], llrs int8 [n][>= codeword length]."""
+        [n][P][L][14][nsubc], llrs int8 [n][>= UL-SCH codeword length]; UCI payloads harq_ack uint8
+        [n][nof_harq_ack], csi_part1 uint8 [n][nof_csi_part1] (one bit per byte)."""
         import torch
 
         n = grids.shape[0]
@@ -205,11 +212,13 @@ class PuschProcessor:
         if stream is None:
             stream = torch.cuda.current_stream(dev)
         io = None
-        if port_stats is not None or estimates is not None or llrs is not None:
+        if any(x is not None for x in (port_stats, estimates, llrs, harq_ack, csi_part1)):
             io = PuschIntermediates(
                 None if estimates is None else estimates.data_ptr(), 0 if estimates is None else estimates.stride(0),
                 None if port_stats is None else port_stats.data_ptr(), None if llrs is None else llrs.data_ptr(),
-                0 if llrs is None else llrs.stride(0))
+                0 if llrs is None else llrs.stride(0), None if harq_ack is None else harq_ack.data_ptr(),
+                0 if harq_ack is None else harq_ack.stride(0), None if csi_part1 is None else csi_part1.data_ptr(),
+                0 if csi_part1 is None else csi_part1.stride(0))
         _lib.check(self._lib.srs_amd_pusch_process_batch(
             self._h, plan._h, grids.data_ptr(), grids.stride(0), n, tbs.data_ptr(), tbs.stride(0),
             results.data_ptr(), None if soft is None else soft.data_ptr(),

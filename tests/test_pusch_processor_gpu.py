@@ -318,3 +318,64 @@ def test_pusch_processor_transform_precoding_rejects():
         pdu = dict(BASE, **over, transform_precoding=1, tbs=1024)
         with pytest.raises(ValueError):
             proc.plan(amd.make_pdu(**pdu), 12 * 51)
+
+
+# UCI on PUSCH: HARQ-ACK / CSI part 1 multiplexed with the UL-SCH by the UE (oracle ue_multiplex_uci: the
+# reference's own UCI encoders and RE placement), against the compiled pusch_processor_impl with its
+# ulsch_demultiplex_impl and uci_decoder_impl.  (name, pdu overrides, HARQ-ACK bits, CSI part 1 bits, SNR dB)
+UCI_CASES = [
+    ("ack1_16qam", dict(modulation=4, target_code_rate=490.0), 1, 0, 25.0),
+    ("ack2_csi1_2", dict(modulation=4, target_code_rate=490.0, rnti=0x1234, n_id=11), 2, 2, 25.0),
+    ("ack5_csi9_qpsk", dict(modulation=2, target_code_rate=679.0), 5, 9, 20.0),
+    ("ack20_csi40_64qam_2rx", dict(modulation=6, target_code_rate=567.0, nof_rx_ports=2), 20, 40, 28.0),
+    ("ack11_csi12_2layer", dict(modulation=4, target_code_rate=490.0, nof_tx_layers=2, nof_rx_ports=2,
+                                dmrs_symbol_mask=(1 << 2) | (1 << 7) | (1 << 11)), 11, 12, 28.0),
+    ("ack2_csi400_256qam_4rx", dict(bwp_size_rb=106, rb_count=106, modulation=8, target_code_rate=797.0,
+                                    nof_rx_ports=4), 2, 400, 35.0),
+    ("ack3_lowsnr", dict(modulation=4, target_code_rate=658.0), 3, 20, 3.0),
+]
+
+
+@pytest.mark.parametrize("case", UCI_CASES, ids=[c[0] for c in UCI_CASES])
+def test_pusch_processor_uci_vs_reference(case):
+    """UCI bits on PUSCH -- demultiplexing, HARQ-ACK / CSI part 1 decoding and the UL-SCH around
+    them -- identical to the compiled reference processor: TB, CRC, LDPC statistics, UCI payloads and statuses."""
+    import torch
+
+    name, over, n_ack, n_csi1, snr = case
+    pdu = dict(BASE, **over, nof_harq_ack=n_ack, nof_csi_part1=n_csi1, beta_offset_harq_ack=8.0,
+               beta_offset_csi_part1=6.25, alpha_scaling=1.0)
+    nprb = pdu["bwp_size_rb"]
+    tbs = _tbs(pdu)
+    r = pdu["target_code_rate"] / 1024
+    pdu["base_graph"] = 2 if (tbs <= 292 or (tbs <= 3824 and r <= 0.67) or r <= 0.25) else 1
+    rng = np.random.default_rng(len(name))
+    tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+    ack = rng.integers(0, 2, n_ack).astype(np.uint8)
+    csi1 = rng.integers(0, 2, n_csi1).astype(np.uint8)
+    L, P = pdu["nof_tx_layers"], pdu["nof_rx_ports"]
+    ch = (np.eye(L, P) + 0.2j * np.ones((L, P))).astype(np.complex64)
+    grid, _ = pp.ue_transmit(tb, pdu, 12 * nprb, channel=ch, snr_db=snr, seed=2, uci=(ack, csi1))
+    want_tb, want = pp.ref_pusch_process(grid, pdu, tbs // 8, iterations=6)
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=6), device=0)
+    plan = proc.plan(amd.make_pdu(**dict(pdu, tbs=tbs)), 12 * nprb)
+    g = torch.from_numpy(grid.view(np.int32)[None]).to("cuda:0")
+    d_ack = torch.zeros((1, max(n_ack, 1)), dtype=torch.uint8, device="cuda:0")
+    d_csi = torch.zeros((1, max(n_csi1, 1)), dtype=torch.uint8, device="cuda:0")
+    out, res = proc.process_batch(g, plan, harq_ack=d_ack if n_ack else None, csi_part1=d_csi if n_csi1 else None)
+    torch.cuda.synchronize()
+    got = amd.pusch_processor.parse_results(res.cpu().numpy())[0]
+    got_tb = out[0].cpu().numpy()
+    assert bool(got.data.tb_crc_ok) == want["tb_crc_ok"], name
+    assert np.array_equal(got_tb, want_tb), name
+    assert got.data.ldpc_iterations_sum == want["iterations_sum"], (name, got.data.ldpc_iterations_sum, want)
+    assert got.harq_ack_status == want["harq_ack_status"], (name, got.harq_ack_status, want["harq_ack_status"])
+    assert got.csi_part1_status == want["csi_part1_status"], (name, got.csi_part1_status, want["csi_part1_status"])
+    if n_ack:
+        np.testing.assert_array_equal(d_ack[0, :n_ack].cpu().numpy(), want["harq_ack"], err_msg=name)
+    if n_csi1:
+        np.testing.assert_array_equal(d_csi[0, :n_csi1].cpu().numpy(), want["csi_part1"], err_msg=name)
+    _check_csi(got, want, name)
+    if snr >= 20:
+        assert want["tb_crc_ok"] and want["harq_ack_status"] in (0, 1) and want["csi_part1_status"] in (0, 1), name
+        assert np.array_equal(want["harq_ack"], ack) and np.array_equal(want["csi_part1"], csi1), name
