@@ -8,6 +8,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "bf16_device.h"
+
 #include <cstdint>
 
 #include "pusch_chest_args.h"
@@ -33,7 +35,7 @@ __device__ __forceinline__ uint32_t bf16_bits(float f)
 }
 __device__ __forceinline__ uint32_t to_cbf16(float2 v)
 {
-  return bf16_bits(v.x) | (bf16_bits(v.y) << 16);
+  return cbf16_pack(v.x, v.y); // == bf16_bits(v.x) | bf16_bits(v.y) << 16 (bf16_device.h)
 }
 __device__ __forceinline__ float2 polar1(float theta)
 {

@@ -31,20 +31,8 @@ __device__ void write_crc(const crc_args& a, uint32_t row_index, uint32_t crc)
   if (a.attach) {
     // CRC bits MSB-first into bits [n, n + L); other bits of the touched bytes kept.
     // each touched byte read and written once (at most 4 bytes for a 24-bit CRC)
-    uint8_t*       row   = a.bits + static_cast<size_t>(row_index) * a.stride;
-    const uint32_t first = a.nof_bits >> 3, last = (a.nof_bits + a.order - 1) >> 3;
-    for (uint32_t q = first; q <= last; ++q) {
-      uint32_t byte = row[q];
-      for (uint32_t b = 0; b < 8; ++b) {
-        const uint32_t pos = 8 * q + b;
-        if (pos >= a.nof_bits && pos < a.nof_bits + a.order) {
-          const uint32_t bit  = (crc >> (a.order - 1 - (pos - a.nof_bits))) & 1u;
-          const uint32_t mask = 0x80u >> b;
-          byte                = (byte & ~mask) | (bit ? mask : 0u);
-        }
-      }
-      row[q] = static_cast<uint8_t>(byte);
-    }
+    uint8_t* row = a.bits + static_cast<size_t>(row_index) * a.stride;
+    attach_crc_bits(row, a.nof_bits, a.order, crc);
   }
 }
 
@@ -69,16 +57,23 @@ __global__ void __launch_bounds__(CRC_THREADS) crc_chunk_kernel(crc_args a)
 {
   __shared__ uint32_t partial[CRC_THREADS / 64];
   __shared__ uint32_t T[256];
+  __shared__ __attribute__((aligned(16))) uint8_t s_chunk[CRC_CHUNK];
   crc_table8_init<CRC_THREADS>(T, a.order, a.polynom);
-  __syncthreads();
   const uint8_t* row    = a.bits + static_cast<size_t>(blockIdx.y) * a.stride;
   const uint32_t nbytes = (a.nof_bits + 7) / 8;
-  const uint32_t b0     = blockIdx.x * CRC_CHUNK + threadIdx.x * CRC_PER;
+  const uint32_t c0     = blockIdx.x * CRC_CHUNK;
+  // the chunk staged in LDS with coalesced loads (each thread then divides 32 contiguous bytes)
+  crc_stage_bytes<CRC_THREADS>(s_chunk, row, c0, min(CRC_CHUNK, nbytes - c0));
+  __syncthreads();
+  const uint32_t b0     = c0 + threadIdx.x * CRC_PER;
   const uint32_t b1     = min(nbytes, b0 + CRC_PER);
+  // contributions summed at the end of the workgroup's chunk, then moved to the message end once
+  const uint32_t to     = min(a.nof_bits, (blockIdx.x + 1) * CRC_CHUNK * 8);
   const uint32_t v      = crc_block_xor<CRC_THREADS>(
-      crc_chunk_contrib(row_fetch{row}, b0, b1, a.nof_bits, a.order, a.polynom, a.table, T), partial);
+      crc_chunk_contrib(lds_chunk_fetch{s_chunk, c0}, b0, b1, a.nof_bits, a.order, a.polynom, a.table, T, to),
+      partial);
   if (threadIdx.x == 0 && v != 0) {
-    atomicXor(a.acc + blockIdx.y, v);
+    atomicXor(a.acc + blockIdx.y, crc_move(v, a.nof_bits - to, a.order, a.table));
   }
 }
 

@@ -26,11 +26,18 @@ __device__ __forceinline__ float safe_rcp(float nv)
 __device__ __forceinline__ int q_simd(float v, float range)
 {
 #pragma clang fp contract(off)
-  float x = v * (120.0f / range);
-  x       = x > 120.0f ? 120.0f : x;
-  x       = x < -120.0f ? -120.0f : x;
-  x       = __builtin_rintf(x);
-  return x != x ? 0 : static_cast<int>(x);
+  const float x = v * (120.0f / range);
+  // clip as one v_med3_f32 (equal to the two compares for every non-NaN x; a NaN x gives 0 below)
+  const float c = __builtin_rintf(__builtin_amdgcn_fmed3f(x, -120.0f, 120.0f));
+  return x != x ? 0 : static_cast<int>(c);
+}
+
+// median(x, lo, hi) as one v_med3_i32 (lo <= hi)
+__device__ __forceinline__ int med3_int(int x, int lo, int hi)
+{
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+  return r;
 }
 
 // log_likelihood_ratio::quantize: clip to the range, round half away from zero.
@@ -109,12 +116,33 @@ __device__ __forceinline__ void demap_symbol(const demodulate_args& a, const flo
     }
     return;
   }
-  // 64QAM / 256QAM: interval functions.
-  const int  m    = a.qm / 2;
-  const bool zero = !simd && (s.x * s.x + s.y * s.y) < NEAR_ZERO;
+  // 64QAM / 256QAM: interval functions.  One branch per symbol around the whole loop (the SIMD-block
+  // arithmetic or the scalar tail's): a branch per LLR costs its exec-mask bookkeeping 2 qm times.
+  const int   m   = a.qm / 2;
   const float rcp = safe_rcp(nv);
+  if (simd) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) { // compile-time k: the table fields are scalar loads
+    for (int k = 0; k < 4; ++k) { // compile-time k: the table fields are scalar loads
+      if (k >= m) {
+        break;
+      }
+      const demod_interval_table& t = a.tab[k];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float x   = xs[c];
+        const int   idx = med3_int(static_cast<int>(floorf(x * t.inv_width)) + t.n / 2, 0, t.n - 1);
+        float l         = (lt[(2 * k) * 16 + idx] * x + lt[(2 * k + 1) * 16 + idx]) * rcp;
+        if (fabsf(x) <= NEAR_ZERO) {
+          l = 0.0f;
+        }
+        o[2 * k + c] = static_cast<int8_t>(q_simd(l, 20.0f));
+      }
+    }
+    return;
+  }
+  const bool zero = (s.x * s.x + s.y * s.y) < NEAR_ZERO;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
     if (k >= m) {
       break;
     }
@@ -122,18 +150,8 @@ __device__ __forceinline__ void demap_symbol(const demodulate_args& a, const flo
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const float x = xs[c];
-      int         q;
-      if (zero) {
-        q = 0;
-      } else if (simd) {
-        int idx = static_cast<int>(floorf(x * t.inv_width)) + t.n / 2;
-        idx     = idx < 0 ? 0 : (idx > t.n - 1 ? t.n - 1 : idx);
-        float l = (lt[(2 * k) * 16 + idx] * x + lt[(2 * k + 1) * 16 + idx]) * rcp;
-        if (fabsf(x) <= NEAR_ZERO) {
-          l = 0.0f;
-        }
-        q = q_simd(l, 20.0f);
-      } else {
+      int         q = 0;
+      if (!zero) {
         int idx = static_cast<int>(floorf(x / t.width)) + t.n / 2;
         idx     = idx < 0 ? 0 : (idx > t.n - 1 ? t.n - 1 : idx);
         float l = __builtin_fmaf(lt[(2 * k) * 16 + idx], x, lt[(2 * k + 1) * 16 + idx]);

@@ -36,6 +36,34 @@ struct device_buffer {
   }
 };
 
+// Remembers the geometry last written into a device array by a generator kernel (the per-codeblock
+// rate-matching lengths / offsets of rm_arrays_kernel): a call with the same geometry on the same buffer
+// skips the launch.  The buffer is written only by that kernel, and stream_order makes a call wait for the
+// previous call's completion, so the skipped launch's contents are in place.
+struct geometry_cache {
+  const void* ptr = nullptr;
+  uint32_t    key[8] = {};
+  bool        valid  = false;
+  // true when the generator must run for (p, k[0..n)); records the new state
+  bool stale(const void* p, const uint32_t* k, int n)
+  {
+    bool same = valid && p == ptr;
+    for (int i = 0; i < n && same; ++i) {
+      same = key[i] == k[i];
+    }
+    if (same) {
+      return false;
+    }
+    ptr   = p;
+    valid = true;
+    for (int i = 0; i < n; ++i) {
+      key[i] = k[i];
+    }
+    return true;
+  }
+  void invalidate() { valid = false; }
+};
+
 // Orders the reuse of an object's device scratch across the caller's streams: a batch call on stream s
 // first waits for the previous call's completion event when that call ran on another stream, so two
 // calls on different streams never overwrite each other's in-flight scratch.

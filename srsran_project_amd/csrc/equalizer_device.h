@@ -222,9 +222,11 @@ __device__ __forceinline__ void mimo_solve(mimo_system<L>& sys,
       d -= norm(a[k][j]);
     }
     // singular in float terms: a pivot below 2^-20 of its diagonal entry (or not a positive normal number)
-    ok            = ok && __builtin_isnormal(d) && d > 0x1p-20f * a[k][k].x;
-    const float c = __builtin_sqrtf(d);
-    r[k]          = 1.0f / c;
+    ok = ok && __builtin_isnormal(d) && d > 0x1p-20f * a[k][k].x;
+    // 1 / C_kk as one hardware reciprocal square root (v_rsq_f32, ~1 ulp): this solve has no reference to
+    // be bit-exact with (parity unpinned, fp64 tolerance), and the correctly rounded sqrt + IEEE division
+    // cost ~20 VALU instructions each
+    r[k] = __builtin_amdgcn_rsqf(d);
 #pragma unroll
     for (int i = k + 1; i < L; ++i) {
       cplx s = a[i][k];
@@ -289,7 +291,7 @@ __device__ __forceinline__ void mimo_solve(mimo_system<L>& sys,
       const float mu = 1.0f - noise_var * dinv[l];
       // mu_l = SINR / (1 + SINR) of the layer: below 2^-20 (no signal) the RE is abnormal
       ok             = ok && __builtin_isnormal(mu) && mu > 0x1p-20f;
-      const float rm = 1.0f / mu;
+      const float rm = __builtin_amdgcn_rcpf(mu); // v_rcp_f32 (~1 ulp), see r[k] above
       out[l]         = {x[l].x * rm, x[l].y * rm};
       nv[l]          = noise_var * dinv[l] * rm;
     } else {

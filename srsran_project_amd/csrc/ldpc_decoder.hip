@@ -155,12 +155,16 @@ __device__ __forceinline__ int sat120(int x)
   asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(-LLR_MAX), "v"(LLR_MAX));
   return r;
 }
-// a * K + b with a 24-bit signed multiply (K an inline constant)
+// a * K + b with a 24-bit signed multiply
 template <int K>
 __device__ __forceinline__ int mad24(int a, int b)
 {
   int r;
-  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(K), "v"(b));
+  if constexpr (K >= -16 && K <= 64) {
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(K), "v"(b));
+  } else { // not an inline constant: from an SGPR (VOP3 takes no literal here)
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(K), "v"(b));
+  }
   return r;
 }
 // median(x, -1, 1)
@@ -169,6 +173,31 @@ __device__ __forceinline__ int sign3(int x)
   int r;
   asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(x));
   return r;
+}
+
+// Soft bits in LDS encode the reference's +-LLR_INFINITY (127) as +-SOFT_INF = +-121, the first value past
+// +-LLR_MAX: the promotion sum (log_likelihood_ratio.cpp:75: |a + b| > LLR_MAX -> +-infinity) is then a single
+// clamp of a + b to +-SOFT_INF, and an infinite soft bit is the only value outside +-LLR_MAX.  Values are
+// mapped at the two borders: the partial tail node of the input is clamped to +-SOFT_INF on load (a valid LLR
+// is in +-LLR_MAX or +-127), and +-SOFT_INF is written out as +-127 in the soft-bit export.
+constexpr int SOFT_INF = LLR_MAX + 1;
+// v2c of an infinite soft bit: (s - sat(s)) * INF_BOOST + sat(s - c2v), |.| >= 200 + 25 (|c2v| <= 96), so it is
+// never a minimum (> LLR_MAX), keeps its sign, and c2v + v2c always saturates back to +-SOFT_INF.
+constexpr int INF_BOOST = 200;
+
+// byte -> the reference's LLR value (+-SOFT_INF -> +-LLR_INFINITY)
+__device__ __forceinline__ int soft_export(int v)
+{
+  return v == SOFT_INF ? LLR_INFINITY : (v == -SOFT_INF ? -LLR_INFINITY : v);
+}
+__device__ __forceinline__ uint32_t soft_export4(uint32_t w)
+{
+  uint32_t o = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    o |= (static_cast<uint32_t>(soft_export(static_cast<int8_t>(w >> (8 * b)))) & 0xffu) << (8 * b);
+  }
+  return o;
 }
 
 template <int ARITH>
@@ -235,9 +264,9 @@ __device__ __forceinline__ int c2v_old(const uint32_t (&c2v)[NW], const int (&cl
 
 // Pass 1 for edge E: v2c from the gathered soft bit and the old message, plus
 // the check-node statistics (ldpc_decoder_impl.cpp:235 / :290).  An infinite
-// soft bit (+-127) yields |v2c| >= 220 here: it can never be a minimum (> 120),
+// soft bit (+-SOFT_INF) yields |v2c| >= 225 here: it can never be a minimum (> 120),
 // its sign is right, and in pass 2 c2v + v2c always lands beyond +-120, so the
-// promotion sum returns +-127 with no separate infinity test.
+// promotion sum returns +-SOFT_INF with no separate infinity test.
 template <int BG, int E0, int E, int NW, int DEG>
 __device__ __forceinline__ int edge_pass1(int            s,
                                           const uint32_t (&c2v)[NW],
@@ -248,10 +277,10 @@ __device__ __forceinline__ int edge_pass1(int            s,
                                           int&           sgn)
 {
   // v2c = soft - c2v saturated to +-LLR_MAX; infinite soft bits stay infinite.
-  // Branch-free: s - med3(s, +-120) is 0 for a finite soft bit and +-7 for an
-  // infinite one, which pushes v2c to +-[220, 309] (|v2c| > 120: never a
-  // minimum; |c2v + v2c| >= 124: always promoted to +-127 in pass 2).
-  const int  v   = mad24<27>(s - sat120(s), sat120(s - c2v_old<BG, E0 + E>(c2v, cl, E)));
+  // Branch-free: s - med3(s, +-120) is 0 for a finite soft bit and +-1 for an
+  // infinite one, which pushes v2c to +-[225, 320] (|v2c| > 120: never a
+  // minimum; |c2v + v2c| >= 129: always promoted to +-SOFT_INF in pass 2).
+  const int  v   = mad24<INF_BOOST>(s - sat120(s), sat120(s - c2v_old<BG, E0 + E>(c2v, cl, E)));
   const int  av  = v < 0 ? -v : v;
   const bool lt1 = av < min1;
   idx            = lt1 ? E : idx;
@@ -273,13 +302,10 @@ __device__ __forceinline__ int edge_pass2(int v, uint32_t (&c2v)[NW], int (&cl)[
   // extrinsic sign: negate when the sign product without this edge is negative
   const int neg = (sgn ^ v) >> 31;
   const int c   = (mag ^ neg) - neg;
-  // promotion sum (log_likelihood_ratio.cpp:75) without compares: m is the
-  // +-120 saturation, (t - m) clamped to [-1, 1] flags an overflow, which moves
-  // m on to +-127.  c is always finite, c == -v gives 0 through the plain sum,
-  // an infinite v2c (|v| >= 220) always overflows.
-  const int t   = c + v;
-  const int m   = sat120(t);
-  const int out = mad24<LLR_INFINITY - LLR_MAX>(sign3(t - m), m);
+  // promotion sum (log_likelihood_ratio.cpp:75) as one median: |t| > 120 is
+  // +-SOFT_INF.  c is always finite, c == -v gives 0 through the plain sum,
+  // an infinite v2c (|v| >= 225) always overflows.
+  const int out = med3_op(c + v, -SOFT_INF, SOFT_INF);
   if constexpr (E0 + E < bg_traits<BG>::LDS_EDGES) {
     cl[E] = c;
   } else {
@@ -523,14 +549,13 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
         if (v != 0) {
           last = 4 * w + (31 - __builtin_clz(v)) / 8;
         }
-        uint32_t o = v;
-        if (w < B4) {
-          o = 0;
+        // full nodes clamped to +-SOFT_CLAMP, the partial tail node to the soft-bit range
+        const int lim = w < B4 ? SOFT_CLAMP : SOFT_INF;
+        uint32_t  o   = 0;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const int x = static_cast<int8_t>(v >> (8 * b));
-            o |= (static_cast<uint32_t>(med3_i(x, -SOFT_CLAMP, SOFT_CLAMP)) & 0xffu) << (8 * b);
-          }
+        for (int b = 0; b < 4; ++b) {
+          const int x = static_cast<int8_t>(v >> (8 * b));
+          o |= (static_cast<uint32_t>(med3_i(x, -lim, lim)) & 0xffu) << (8 * b);
         }
         s4[off4 + w] = static_cast<int32_t>(o);
       }
@@ -541,7 +566,7 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
         if (v != 0) {
           last = max(last, tb0 + j);
         }
-        soft[2 * Z + tb0 + j] = static_cast<int8_t>(v); // inside the partial tail node: unclamped
+        soft[2 * Z + tb0 + j] = static_cast<int8_t>(med3_i(v, -SOFT_INF, SOFT_INF)); // partial tail node
       }
       const int z0 = 2 * Z + n_llrs; // first byte after the data
       for (int i = z0 + j; i < ((z0 + 3) & ~3) && i < NZ; i += nthr) {
@@ -594,7 +619,7 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
           if (node >= 2 && node < nof_full_nodes) {
             v = med3_i(in[(node - 2) * Z + p], -SOFT_CLAMP, SOFT_CLAMP);
           } else if (node == nof_full_nodes && p < tail) {
-            v = in[(node - 2) * Z + p];
+            v = med3_i(in[(node - 2) * Z + p], -SOFT_INF, SOFT_INF);
           }
           soft[node * Z + p] = static_cast<int8_t>(v);
         }
@@ -709,7 +734,7 @@ __global__ void __launch_bounds__(max_threads<ZC>(), (waves_per_simd<BG, ZC>()))
     if (a.soft_out) {
       int8_t* so = a.soft_out + static_cast<size_t>(cb) * NZ;
       for (int i = je; i < NZ; i += nthr) {
-        so[i] = soft[i];
+        so[i] = static_cast<int8_t>(soft_export(soft[i]));
       }
     }
     if (je == 0) {
@@ -909,8 +934,8 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
           const pk16    s = pk16{static_cast<short>(lds[hr_addr<E0 + E, 0, k * T>(t)]),
                               static_cast<short>(lds[hr_addr<E0 + E, HR_HALF, k * T>(t)])};
           const pk16 sat = pk_clamp(s, LLR_MAX);
-          // infinite soft bits (+-127) push |v2c| beyond 220 (see edge_pass1)
-          const pk16 x = (s - sat) * pk_splat(27) + pk_clamp(s - c2v.template get<(E0 + E) * NP + k>(), LLR_MAX);
+          // infinite soft bits (+-SOFT_INF) push |v2c| beyond 220 (see edge_pass1)
+          const pk16 x = (s - sat) * pk_splat(INF_BOOST) + pk_clamp(s - c2v.template get<(E0 + E) * NP + k>(), LLR_MAX);
           const pk16 ax = __builtin_elementwise_abs(x);
           min2[h][k]    = pk_max(min1[h][k], pk_min(ax, min2[h][k])); // median(min1, |v|, min2)
           min1[h][k]    = pk_min(min1[h][k], ax);
@@ -947,9 +972,8 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
           const pk16 mag = f * d12[k] + s2[k];
           const pk16 neg = (sgn[k] ^ x) >> 15;
           const pk16 c   = (mag ^ neg) - neg;
-          const pk16 sum = c + x;
-          const pk16 m   = pk_clamp(sum, LLR_MAX);
-          const pk16 out = (pk_clamp(sum, LLR_MAX + 1) - m) * pk_splat(LLR_INFINITY - LLR_MAX) + m;
+          // promotion sum: |c + x| > LLR_MAX is +-SOFT_INF (see edge_pass2)
+          const pk16 out = pk_clamp(c + x, SOFT_INF);
           c2v.template set<(E0 + E) * NP + k>(c);
           lds[hr_addr<E0 + E, 0, k * T>(t)]       = static_cast<int8_t>(out.x);
           lds[hr_addr<E0 + E, HR_HALF, k * T>(t)] = static_cast<int8_t>(out.y);
@@ -980,10 +1004,13 @@ __device__ __forceinline__ void hr_layers(lds_i8* lds, MSGS& c2v, uint32_t t, in
 
 // NP row pairs per lane: NP = 1 -> 192 threads (3 waves) per codeblock, NP = 3 -> one wave per codeblock
 // (no workgroup barriers, three independent pair streams per lane).
+#ifndef HR_WAVES
+#define HR_WAVES 4
+#endif
 template <int NP>
 constexpr int hr_waves_per_simd()
 {
-  return NP == 1 ? 4 : 2;
+  return NP == 1 ? HR_WAVES : 2;
 }
 
 template <int ARITH, int MAXL, int NP>
@@ -1049,14 +1076,13 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
         if (v != 0) {
           last = 4 * w + (31 - __builtin_clz(v)) / 8;
         }
-        uint32_t o = v;
-        if (w < B4) {
-          o = 0;
+        // full nodes clamped to +-SOFT_CLAMP, the partial tail node to the soft-bit range
+        const int lim = w < B4 ? SOFT_CLAMP : SOFT_INF;
+        uint32_t  o   = 0;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const int x = static_cast<int8_t>(v >> (8 * b));
-            o |= (static_cast<uint32_t>(med3_i(x, -SOFT_CLAMP, SOFT_CLAMP)) & 0xffu) << (8 * b);
-          }
+        for (int b = 0; b < 4; ++b) {
+          const int x = static_cast<int8_t>(v >> (8 * b));
+          o |= (static_cast<uint32_t>(med3_i(x, -lim, lim)) & 0xffu) << (8 * b);
         }
         if (w < (NODES - 2) * Z / 4) {
           soft4[(2 * Z) / 4 + w] = static_cast<int32_t>(o); // words past nw hold zeros
@@ -1201,7 +1227,7 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
     if (a.soft_out) {
       int32_t* so = reinterpret_cast<int32_t*>(a.soft_out + static_cast<size_t>(cb) * (68 * Z));
       for (int i = te; i < 68 * Z / 4; i += NT) {
-        so[i] = i < NODES * Z / 4 ? soft4[i] : 0;
+        so[i] = i < NODES * Z / 4 ? static_cast<int32_t>(soft_export4(static_cast<uint32_t>(soft4[i]))) : 0;
       }
     }
     if (te == 0) {

@@ -157,6 +157,7 @@ __global__ __launch_bounds__(MAX_LIFTING_SIZE) void ldpc_encode_kernel(encode_ar
 // the window wraps), XOR-ed into the row's accumulator.  One wave per codeblock: the four high-rate
 // rows of BG1 Z = 384 are 48 lane tasks.
 constexpr int ENC_BITS_THREADS = 64;
+constexpr uint32_t ENC_MSG_UNROLL = 5; // 1,056-byte BG1 Z = 384 message: 264 words, five per lane
 
 __device__ __forceinline__ uint32_t lds_bits32(const uint32_t* W, uint32_t off)
 {
@@ -222,21 +223,40 @@ __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(enco
     const uint8_t* msg    = a.msgs + static_cast<size_t>(cb) * a.msg_stride;
     const uint32_t nbytes = (kz + 7) / 8;
     const uint32_t nmw    = (kz + 31) / 32;
-    for (uint32_t w = j; w < ncw; w += ENC_BITS_THREADS) {
-      uint32_t v = 0;
-      if (w < nmw) {
-        uint32_t be = 0;
+    // message words: every load of a lane issued before its LDS stores (ENC_MSG_UNROLL rounds of the wave)
+    const bool al4 = (reinterpret_cast<uintptr_t>(msg) & 3u) == 0;
+    for (uint32_t w0 = j; w0 < nmw; w0 += ENC_MSG_UNROLL * ENC_BITS_THREADS) {
+      uint32_t be[ENC_MSG_UNROLL];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const uint32_t q = 4 * w + b;
-          be |= (q < nbytes ? static_cast<uint32_t>(msg[q]) : 0u) << (24 - 8 * b);
-        }
-        v = __builtin_bitreverse32(be);
-        if (32 * w + 32 > kz) {
-          v &= (1u << (kz - 32 * w)) - 1u;
+      for (uint32_t r = 0; r < ENC_MSG_UNROLL; ++r) {
+        const uint32_t w = w0 + r * ENC_BITS_THREADS;
+        be[r]            = 0;
+        if (w < nmw) {
+          if (al4 && 4 * w + 4 <= nbytes) {
+            be[r] = __builtin_bswap32(reinterpret_cast<const uint32_t*>(msg)[w]);
+          } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const uint32_t q = 4 * w + b;
+              be[r] |= (q < nbytes ? static_cast<uint32_t>(msg[q]) : 0u) << (24 - 8 * b);
+            }
+          }
         }
       }
-      cw[w] = v;
+#pragma unroll
+      for (uint32_t r = 0; r < ENC_MSG_UNROLL; ++r) {
+        const uint32_t w = w0 + r * ENC_BITS_THREADS;
+        if (w < nmw) {
+          uint32_t v = __builtin_bitreverse32(be[r]);
+          if (32 * w + 32 > kz) {
+            v &= (1u << (kz - 32 * w)) - 1u;
+          }
+          cw[w] = v;
+        }
+      }
+    }
+    for (uint32_t w = nmw + j; w < ncw; w += ENC_BITS_THREADS) {
+      cw[w] = 0;
     }
     for (uint32_t w = j; w < nq + 2; w += ENC_BITS_THREADS) {
       ls[w] = 0;

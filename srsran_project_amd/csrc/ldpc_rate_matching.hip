@@ -84,6 +84,7 @@ __device__ __forceinline__ int llr_sum(int a, int b)
 
 constexpr int DEMATCH_THREADS   = 256;
 constexpr int DEMATCH_PER_THREAD = 16;
+constexpr uint32_t DEMATCH_UNROLL = 4; // staging loads in flight per thread
 constexpr uint32_t DEMATCH_LDS   = 12288; // received LLRs of a codeblock staged in LDS up to this length (8 resident workgroups per CU)
 
 // One workgroup per codeblock: the codeblock's received LLRs (deinterleaver input) are staged in LDS
@@ -119,20 +120,64 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
       auto by_symbol = [&](auto qm_tag) {
         constexpr uint32_t QM = decltype(qm_tag)::value;
         using word            = typename std::conditional<QM == 8, uint2, typename std::conditional<QM == 4, uint32_t, uint16_t>::type>::type;
-        for (uint32_t i = threadIdx.x; i < Kq; i += DEMATCH_THREADS) {
+        // DEMATCH_UNROLL symbols per thread per round, all loads issued before the LDS stores (a
+        // load-then-store loop waits one memory latency per symbol)
+        for (uint32_t i0 = threadIdx.x; i0 < Kq; i0 += DEMATCH_UNROLL * DEMATCH_THREADS) {
           union {
             word   w;
             int8_t b[QM];
-          } u;
-          u.w = reinterpret_cast<const word*>(in)[i];
+          } u[DEMATCH_UNROLL];
 #pragma unroll
-          for (uint32_t j = 0; j < QM; ++j) {
-            s_in[j * Kq + i] = u.b[j];
+          for (uint32_t r = 0; r < DEMATCH_UNROLL; ++r) {
+            const uint32_t i = i0 + r * DEMATCH_THREADS;
+            u[r].w           = i < Kq ? reinterpret_cast<const word*>(in)[i] : word{};
+          }
+#pragma unroll
+          for (uint32_t r = 0; r < DEMATCH_UNROLL; ++r) {
+            const uint32_t i = i0 + r * DEMATCH_THREADS;
+            if (i < Kq) {
+#pragma unroll
+              for (uint32_t j = 0; j < QM; ++j) {
+                s_in[j * Kq + i] = u[r].b[j];
+              }
+            }
           }
         }
       };
       const uintptr_t ia = reinterpret_cast<uintptr_t>(in);
-      if (g.Qm == 8 && (ia & 7u) == 0) {
+      if (g.Qm == 8 && (ia & 15u) == 0 && (Kq & 3u) == 0) {
+        // four symbols per thread and round: 32 LLR bytes (two 16-byte loads), transposed into the eight
+        // rows' 4-byte words (v_perm_b32) and stored with one aligned ds_write_b32 per row -- byte stores put
+        // four lanes on every LDS dword
+        const uint32_t ng = Kq / 4;
+        for (uint32_t q0 = threadIdx.x; q0 < ng; q0 += DEMATCH_UNROLL * DEMATCH_THREADS) {
+          uint4 u[DEMATCH_UNROLL][2];
+#pragma unroll
+          for (uint32_t r = 0; r < DEMATCH_UNROLL; ++r) {
+            const uint32_t q = q0 + r * DEMATCH_THREADS;
+            u[r][0]          = q < ng ? reinterpret_cast<const uint4*>(in)[2 * q] : uint4{};
+            u[r][1]          = q < ng ? reinterpret_cast<const uint4*>(in)[2 * q + 1] : uint4{};
+          }
+#pragma unroll
+          for (uint32_t r = 0; r < DEMATCH_UNROLL; ++r) {
+            const uint32_t q = q0 + r * DEMATCH_THREADS;
+            if (q < ng) {
+              // symbol s of the group: LLR bytes s0 = (u[s/2] word 2(s%2)), s1 = (word 2(s%2) + 1)
+              const uint32_t lo[4] = {u[r][0].x, u[r][0].z, u[r][1].x, u[r][1].z}; // LLRs 0-3 of symbols 0-3
+              const uint32_t hi[4] = {u[r][0].y, u[r][0].w, u[r][1].y, u[r][1].w}; // LLRs 4-7
+#pragma unroll
+              for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t* w  = j < 4 ? lo : hi;
+                const uint32_t  b  = j & 3u;
+                // bytes b of w[0], w[1] into the low half, of w[2], w[3] into the high half
+                const uint32_t  p01 = __builtin_amdgcn_perm(w[1], w[0], (b) | ((4 + b) << 8) | 0x0c0c0000u);
+                const uint32_t  p23 = __builtin_amdgcn_perm(w[3], w[2], (b) | ((4 + b) << 8) | 0x0c0c0000u);
+                reinterpret_cast<uint32_t*>(s_in + j * Kq)[q] = p01 | (p23 << 16);
+              }
+            }
+          }
+        }
+      } else if (g.Qm == 8 && (ia & 7u) == 0) {
         by_symbol(std::integral_constant<uint32_t, 8>{});
       } else if (g.Qm == 4 && (ia & 3u) == 0) {
         by_symbol(std::integral_constant<uint32_t, 4>{});
@@ -385,13 +430,49 @@ __device__ uint32_t rm_byte(const rate_match_args& a, const rm_geometry& g, cons
   return byte;
 }
 
+// 8 x 8 bit transpose: byte j (from the most significant) = row j, bit 7 - k = column k  ->  byte k = column k,
+// its bit 7 - j = row j.
+__device__ __forceinline__ uint64_t transpose8x8(uint64_t x)
+{
+  uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+  x          = x ^ t ^ (t << 7);
+  t          = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+  x          = x ^ t ^ (t << 14);
+  t          = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+  return x ^ t ^ (t << 28);
+}
+
+// Bits e[w], e[w + 1], .. e[w + 7] of the walk (w < L), MSB first, from the staged circular buffer: one
+// two-byte read when the run neither wraps nor crosses the filler gap, else bit by bit.
+__device__ __forceinline__ uint32_t rm_walk_byte(const uint8_t* s_cw, const rm_geometry& g, uint32_t w)
+{
+  if (w + 7 < g.L && (w + 7 < g.nof_info || w >= g.nof_info)) {
+    const uint32_t p = w < g.nof_info ? w : w + g.F;
+    const uint32_t v = (static_cast<uint32_t>(s_cw[p >> 3]) << 8) | s_cw[(p >> 3) + 1];
+    return (v >> (8 - (p & 7))) & 0xffu;
+  }
+  uint32_t row = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    uint32_t ww = w + k;
+    ww          = ww >= g.L ? ww - g.L : ww;
+    const uint32_t p = ww < g.nof_info ? ww : ww + g.F;
+    row |= ((s_cw[p >> 3] >> (7 - (p & 7))) & 1u) << (7 - k);
+  }
+  return row;
+}
+
 // One workgroup per codeblock: the circular buffer (Ncb bits of the packed codeword) is staged in LDS
-// with coalesced loads, then one thread per output byte gathers its 8 bits from LDS (bit selection +
-// interleaver as index arithmetic). A byte straddling the next segment is built from global memory.
+// with coalesced loads.  When the segment starts on a byte boundary, one thread per group of 8 modulation
+// symbols (Qm output bytes): for each interleaver row j < Qm the 8 bits of the group are 8 consecutive walk
+// positions (one two-byte LDS read), and an 8 x 8 bit transpose turns rows into symbols.  The remaining
+// bytes (partial last group, unaligned segments, Qm = 1): one thread per output byte gathering its 8 bits
+// (bit selection + interleaver as index arithmetic); a byte straddling the next segment is built from global
+// memory.
 template <bool RAGGED>
 __global__ __launch_bounds__(RATE_MATCH_THREADS) void ldpc_rate_match_kernel(rate_match_args a)
 {
-  __shared__ uint8_t s_cw[RM_MAX_CW_BYTES];
+  __shared__ uint8_t s_cw[RM_MAX_CW_BYTES + 4]; // + the second byte of a two-byte read at the end
   for (uint32_t cb = blockIdx.y; cb < a.nof_cbs; cb += gridDim.y) {
     const rm_geometry g = RAGGED ? a.geos[a.row_geo[cb]] : a.g;
     const fast_div    divL(g.L);
@@ -404,11 +485,56 @@ __global__ __launch_bounds__(RATE_MATCH_THREADS) void ldpc_rate_match_kernel(rat
     const uint32_t Kq    = E / g.Qm;
     const uint8_t* src   = a.cw + static_cast<size_t>(cb) * a.cw_stride;
     __syncthreads(); // s_cw of the previous codeblock is no longer read
-    for (uint32_t x = threadIdx.x; x < cw_bytes; x += RATE_MATCH_THREADS) {
+    const uint32_t nw4 = (reinterpret_cast<uintptr_t>(src) & 3u) == 0 ? cw_bytes / 4 : 0;
+    for (uint32_t x0 = threadIdx.x; x0 < nw4; x0 += 4 * RATE_MATCH_THREADS) {
+      uint32_t v[4]; // every load of the round in flight before the LDS stores
+#pragma unroll
+      for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t x = x0 + r * RATE_MATCH_THREADS;
+        v[r]             = x < nw4 ? reinterpret_cast<const uint32_t*>(src)[x] : 0u;
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t x = x0 + r * RATE_MATCH_THREADS;
+        if (x < nw4) {
+          reinterpret_cast<uint32_t*>(s_cw)[x] = v[r];
+        }
+      }
+    }
+    for (uint32_t x = 4 * nw4 + threadIdx.x; x < cw_bytes; x += RATE_MATCH_THREADS) {
       s_cw[x] = src[x];
     }
     __syncthreads();
-    for (uint32_t b = first + blockIdx.x * RATE_MATCH_THREADS + threadIdx.x; b < last;
+    // groups of 8 symbols (Qm bytes each) of a byte-aligned segment
+    const uint32_t G        = ((off & 7u) == 0 && g.Qm >= 2) ? Kq / 8 : 0;
+    const uint32_t fast_end = first + G * g.Qm;
+    for (uint32_t gi = blockIdx.x * RATE_MATCH_THREADS + threadIdx.x; gi < G; gi += gridDim.x * RATE_MATCH_THREADS) {
+      uint64_t x = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        if (j < g.Qm) {
+          uint32_t w = g.rank0 + j * Kq + 8 * gi;
+          if (w >= g.L) {
+            w -= g.L;
+            if (w >= g.L) {
+              divL.div(w, w); // repetition beyond one more turn
+            }
+          }
+          x |= static_cast<uint64_t>(rm_walk_byte(s_cw, g, w)) << (56 - 8 * j);
+        }
+      }
+      x = transpose8x8(x); // byte s: bits j = 0 .. Qm - 1 of symbol 8 gi + s, MSB first
+      uint64_t acc = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 8; ++q) {
+        acc = (acc << g.Qm) | ((x >> (64 - 8 * q - g.Qm)) & ((1u << g.Qm) - 1u));
+      }
+      uint8_t* o = a.out + fast_end - (G - gi) * g.Qm;
+      for (uint32_t q = 0; q < g.Qm; ++q) {
+        o[q] = static_cast<uint8_t>(acc >> (8 * (g.Qm - 1 - q)));
+      }
+    }
+    for (uint32_t b = fast_end + blockIdx.x * RATE_MATCH_THREADS + threadIdx.x; b < last;
          b += gridDim.x * RATE_MATCH_THREADS) {
       if (b >= whole) {
         a.out[b] = static_cast<uint8_t>(rm_byte(a, g, divL, cb, b));

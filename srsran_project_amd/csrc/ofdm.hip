@@ -17,6 +17,8 @@
 // 8*(N + cp) (samples) bytes, demodulation 8*N + 4*rg bytes.
 #include <hip/hip_runtime.h>
 
+#include "bf16_device.h"
+
 #include "dft_engine.h"
 #include "ofdm_args.h"
 
@@ -58,10 +60,11 @@ __device__ __forceinline__ void stream_store(T* p, T v)
   }
 }
 
+// a complex sample as ONE 8-byte access (global_store_dwordx2 / global_load_dwordx2): two 4-byte accesses per
+// sample issue twice the memory instructions, each with every other dword of its lanes' span
 __device__ __forceinline__ void stream_store(cf* p, cf v)
 {
-  stream_store(reinterpret_cast<float*>(p), v.x);
-  stream_store(reinterpret_cast<float*>(p) + 1, v.y);
+  stream_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v));
 }
 
 #ifndef OFDM_NT_LOADS
@@ -79,12 +82,12 @@ __device__ __forceinline__ T stream_load(const T* p)
 
 __device__ __forceinline__ cf stream_load(const cf* p)
 {
-  return {stream_load(reinterpret_cast<const float*>(p)), stream_load(reinterpret_cast<const float*>(p) + 1)};
+  return __builtin_bit_cast(cf, stream_load(reinterpret_cast<const uint64_t*>(p)));
 }
 
 __device__ __forceinline__ uint32_t to_cbf16(cf v)
 {
-  return bf16_bits(v.x) | (bf16_bits(v.y) << 16);
+  return cbf16_pack(v.x, v.y); // == bf16_bits(v.x) | bf16_bits(v.y) << 16 (bf16_device.h)
 }
 
 template <int N>

@@ -37,6 +37,7 @@ struct srs_amd_pdsch_encoder {
   srs_amd_ldpc_encoder*      enc    = nullptr;
   srs_amd_ldpc_rate_matcher* rm     = nullptr;
   device_buffer              tb_crcs, msgs, coded, rm_arrays, host_io, slot_desc;
+  geometry_cache             rm_geo; // last geometry written into rm_arrays
   stream_order               order; // scratch reuse across the callers' streams
   stream_fan                 fan;   // srs_amd_pdsch_encode_slot: concurrent LDPC encoder bucket launches
   std::mutex                 mtx;
@@ -110,8 +111,14 @@ int encode_locked(srs_amd_pdsch_encoder* e,
   call_scope scope(e->order, nullptr, stream);
   he = e->order.begin(stream);
   if (he == hipSuccess) {
-    he = launch_rm_arrays(e->rm_arrays.as<uint32_t>(), nof_tbs, C, p->nof_short_segments, p->rm_length_short,
-                          p->rm_length_long, cw_stride * 8, stream);
+    const uint32_t key[6] = {nof_tbs, C, p->nof_short_segments, p->rm_length_short, p->rm_length_long, cw_stride * 8};
+    if (e->rm_geo.stale(e->rm_arrays.ptr, key, 6)) {
+      he = launch_rm_arrays(e->rm_arrays.as<uint32_t>(), nof_tbs, C, p->nof_short_segments, p->rm_length_short,
+                            p->rm_length_long, cw_stride * 8, stream);
+      if (he != hipSuccess) {
+        e->rm_geo.invalidate();
+      }
+    }
   }
   if (he != hipSuccess) {
     return hip_fail(he, "PDSCH encoder rate-matching arrays");
@@ -135,12 +142,14 @@ int encode_locked(srs_amd_pdsch_encoder* e,
   sa.last_data_bits = p->cb_info_bits - p->nof_tb_crc_bits - p->zero_pad;
   sa.tb_crc_bits    = p->nof_tb_crc_bits;
   sa.nof_rows       = rows;
-  he                = launch_segment(sa, stream);
+  // 3. Codeblock CRC (C > 1), fused into the segmentation pass when the message fits one wave's registers.
+  sa.cb_crc_table = C > 1 ? crc_device_table(e->crc24b) : nullptr;
+  sa.cb_crc_poly  = C > 1 ? crc_polynom(e->crc24b) : 0u;
+  he              = launch_segment(sa, stream);
   if (he != hipSuccess) {
     return hip_fail(he, "segment_kernel launch");
   }
-  // 3. Codeblock CRC.
-  if (C > 1) {
+  if (C > 1 && !segment_attaches_crc(sa)) {
     rc = srs_amd_crc_attach_batch(e->crc24b, e->msgs.as<uint8_t>(), msg_stride, p->cb_info_bits, rows, stream);
     if (rc != SRS_AMD_OK) {
       return rc;

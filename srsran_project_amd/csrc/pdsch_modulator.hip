@@ -13,14 +13,15 @@
 // every thread gathers its L x Qm bits, builds the integer points and writes
 // the precoded cbf16 RE of every port (coalesced 4-byte stores).
 //
-// dmrs_pdsch_kernel: one thread per (grid, DM-RS symbol, allocated CRB); the
-// 2 x 6 (type 1) / 2 x 4 (type 2) sequence bits of its RB from at most two
-// Gold words, CDM codes w_f / w_t (dmrs_helper.cpp:34-56), precoding with the
-// same SIMD complex product, DM-RS REs of every CDM group and port.
+// dmrs_pdsch_kernel: one thread per (DM-RS symbol, RE of an allocated CRB), several grids per
+// workgroup; the workgroup's Gold words computed once into LDS, CDM codes w_f / w_t
+// (dmrs_helper.cpp:34-56), precoding with the same SIMD complex product, coalesced stores.
 //
 // Both are HBM-store bound: 4 bytes per RE and port written, Qm * L / 8 bytes
 // per RE read.
 #include <hip/hip_runtime.h>
+
+#include "bf16_device.h"
 
 #include "gold_sequence.h"
 #include "pdsch_modulator_args.h"
@@ -46,7 +47,7 @@ __device__ __forceinline__ uint32_t to_bf16(float f)
 
 __device__ __forceinline__ uint32_t pack_cbf16(float2 v)
 {
-  return to_bf16(v.x) | (to_bf16(v.y) << 16);
+  return cbf16_pack(v.x, v.y); // == to_bf16(v.x) | to_bf16(v.y) << 16 (bf16_device.h)
 }
 
 // Integer constellation point of a Qm-bit index (modulation_mapper_lut_impl.cpp:44-56).
@@ -187,47 +188,90 @@ __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args
   }
 }
 
+// DM-RS: one thread per resource element of an allocated CRB (12 per CRB, consecutive threads on consecutive
+// subcarriers: coalesced stores), DMRS_GRIDS_PER_WG grids per workgroup (batch form: every grid of a launch
+// carries the same sequence, so the Gold words are computed once per workgroup and written to several grids).
+// The sequence words of the workgroup's CRBs are computed cooperatively (one jump per word, into LDS); a
+// workgroup whose CRBs are spread over more than DMRS_MAX_WORDS words jumps per thread instead.
+constexpr int DMRS_THREADS      = 256;
+constexpr int DMRS_GRIDS_PER_WG = 4;
+constexpr int DMRS_MAX_WORDS    = 64;
+
 template <bool MULTI>
-__global__ __launch_bounds__(64) void dmrs_pdsch_kernel(dmrs_pdsch_args own, const dmrs_pdsch_args* items)
+__global__ __launch_bounds__(DMRS_THREADS) void dmrs_pdsch_kernel(dmrs_pdsch_args own, const dmrs_pdsch_args* items,
+                                                                 uint32_t nof_grids)
 {
   const dmrs_pdsch_args& a = item_of<MULTI>(own, items);
-  const uint32_t         i = blockIdx.x * 64 + threadIdx.x; // allocated CRB
-  if (i >= a.nof_crb || (MULTI && blockIdx.y >= a.nof_dmrs_symbols)) {
+  __shared__ uint32_t    s_words[DMRS_MAX_WORDS];
+  const uint32_t         e0 = blockIdx.x * DMRS_THREADS;
+  if (e0 >= a.nof_crb * PDSCH_NRE || (MULTI && blockIdx.y >= a.nof_dmrs_symbols)) {
+    return; // uniform over the workgroup
+  }
+  const int      nd = a.type2 ? 4 : 6;
+  const uint32_t l  = a.symbol[blockIdx.y];
+  // sequence words covering the workgroup's CRBs (dmrs_helper.cpp:70-90: bits 2 nd (crb - ref) ..)
+  const uint32_t i_lo   = e0 / PDSCH_NRE;
+  const uint32_t i_hi   = min(a.nof_crb, (e0 + DMRS_THREADS + PDSCH_NRE - 1) / PDSCH_NRE) - 1;
+  const uint32_t w_lo   = 2u * nd * (a.crbs[i_lo] - a.reference_point_k_rb) / 32;
+  const uint32_t w_hi   = (2u * nd * (a.crbs[i_hi] - a.reference_point_k_rb) + 2u * nd - 1) / 32;
+  const bool     shared = w_hi - w_lo < DMRS_MAX_WORDS;
+  if (shared && threadIdx.x <= w_hi - w_lo) {
+    uint32_t x1, x2;
+    gold_state(a.jump, a.c_init[blockIdx.y], 32 * (w_lo + threadIdx.x), x1, x2);
+    s_words[threadIdx.x] = gold_next32(x1, x2);
+  }
+  __syncthreads();
+  const uint32_t e = e0 + threadIdx.x;
+  const uint32_t i = e / PDSCH_NRE;
+  const uint32_t r = e - i * PDSCH_NRE;
+  if (i >= a.nof_crb) {
     return;
   }
-  const uint32_t l   = a.symbol[blockIdx.y];
-  const int      nd  = a.type2 ? 4 : 6;
+  // resource element r of the CRB: CDM group g, sequence index t within the RB
+  const uint32_t g = a.type2 ? (r % 6) / 2 : (r & 1u);
+  const uint32_t t = a.type2 ? (r & 1u) + 2 * (r / 6) : (r >> 1);
+  if (2 * static_cast<int>(g) >= a.nof_layers) {
+    return; // no port of this PDU in CDM group g
+  }
   const uint32_t crb = a.crbs[i];
-
-  // Sequence bits 2 * nd * (crb - reference) .. + 2 * nd - 1 (dmrs_helper.cpp:70-90).
-  const uint32_t b0 = 2u * nd * (crb - a.reference_point_k_rb);
-  const uint32_t w0 = b0 / 32;
-  uint32_t       x1, x2;
-  gold_state(a.jump, a.c_init[blockIdx.y], 32 * w0, x1, x2);
-  uint64_t c = gold_next32(x1, x2);
-  c |= static_cast<uint64_t>(gold_next32(x1, x2)) << 32;
-  const uint32_t bits = static_cast<uint32_t>(c >> (b0 % 32));
-
-  uint32_t* grid = a.grids + static_cast<uint64_t>(blockIdx.z) * a.grid_stride + l * (a.port_stride / 14);
-  for (int g = 0; 2 * g < a.nof_layers; ++g) {
-    for (int t = 0; t < nd; ++t) {
-      const float  amp = a.amplitude;
-      const float2 base =
-          make_float2(((bits >> (2 * t)) & 1u) ? -amp : amp, ((bits >> (2 * t + 1)) & 1u) ? -amp : amp);
-      // Ports 2g and 2g+1 of the CDM group: w_f = -1 on odd sequence indices for the odd port,
-      // w_t = +1 for every port < 4 (type 1) / < 6 (type 2) and every DM-RS symbol.
-      float2 seq[2];
-      seq[0] = base;
-      seq[1] = (t & 1) ? make_float2(-base.x, -base.y) : base;
-      const uint32_t sc = crb * PDSCH_NRE + (a.type2 ? (2 * g + (t & 1) + 6 * (t >> 1)) : (2 * t + g));
-      for (int p = 0; p < a.nof_ports; ++p) {
-        float2 y = cmul_simd(seq[0], a.w[2 * g][p][0], a.w[2 * g][p][1]);
-        if (2 * g + 1 < a.nof_layers) {
-          const float2 u = cmul_simd(seq[1], a.w[2 * g + 1][p][0], a.w[2 * g + 1][p][1]);
-          y.x            = y.x + u.x;
-          y.y            = y.y + u.y;
-        }
-        grid[static_cast<uint64_t>(p) * a.port_stride + sc] = pack_cbf16(y);
+  const uint32_t b   = 2u * nd * (crb - a.reference_point_k_rb) + 2 * t;
+  uint32_t       word;
+  if (shared) {
+    word = s_words[b / 32 - w_lo];
+  } else {
+    uint32_t x1, x2;
+    gold_state(a.jump, a.c_init[blockIdx.y], 32 * (b / 32), x1, x2);
+    word = gold_next32(x1, x2);
+  }
+  const uint32_t bits = word >> (b % 32);
+  const float    amp  = a.amplitude;
+  const float2   base = make_float2((bits & 1u) ? -amp : amp, (bits & 2u) ? -amp : amp);
+  // ports 2g and 2g+1 of the CDM group: w_f = -1 on odd sequence indices for the odd port, w_t = +1 for every
+  // port < 4 (type 1) / < 6 (type 2) and every DM-RS symbol (dmrs_helper.cpp:34-56)
+  const float2   seq1 = (t & 1u) ? make_float2(-base.x, -base.y) : base;
+  const uint32_t sc   = crb * PDSCH_NRE + r;
+  const uint32_t z0   = MULTI ? 0u : blockIdx.z * DMRS_GRIDS_PER_WG;
+  const uint32_t z1   = MULTI ? 1u : min(nof_grids, z0 + DMRS_GRIDS_PER_WG);
+  uint32_t       y[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (p < a.nof_ports) {
+      float2 v = cmul_simd(base, a.w[2 * g][p][0], a.w[2 * g][p][1]);
+      if (2 * static_cast<int>(g) + 1 < a.nof_layers) {
+        const float2 u = cmul_simd(seq1, a.w[2 * g + 1][p][0], a.w[2 * g + 1][p][1]);
+        v.x            = v.x + u.x;
+        v.y            = v.y + u.y;
+      }
+      y[p] = pack_cbf16(v);
+    }
+  }
+  for (uint32_t z = z0; z < z1; ++z) {
+    uint32_t* grid = a.grids + static_cast<uint64_t>(MULTI ? blockIdx.z : z) * a.grid_stride +
+                     l * (a.port_stride / 14) + sc;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p < a.nof_ports) {
+        grid[static_cast<uint64_t>(p) * a.port_stride] = y[p];
       }
     }
   }
@@ -251,8 +295,9 @@ hipError_t launch_dmrs_pdsch(const dmrs_pdsch_args& a, uint32_t nof_grids, hipSt
   if (a.nof_crb == 0 || a.nof_dmrs_symbols == 0 || nof_grids == 0) {
     return hipSuccess;
   }
-  const dim3 grid((a.nof_crb + 63) / 64, a.nof_dmrs_symbols, nof_grids);
-  hipLaunchKernelGGL(dmrs_pdsch_kernel<false>, grid, dim3(64), 0, stream, a, nullptr);
+  const dim3 grid((a.nof_crb * PDSCH_NRE + DMRS_THREADS - 1) / DMRS_THREADS, a.nof_dmrs_symbols,
+                  (nof_grids + DMRS_GRIDS_PER_WG - 1) / DMRS_GRIDS_PER_WG);
+  hipLaunchKernelGGL(dmrs_pdsch_kernel<false>, grid, dim3(DMRS_THREADS), 0, stream, a, nullptr, nof_grids);
   return hipGetLastError();
 }
 
@@ -273,8 +318,8 @@ hipError_t launch_dmrs_pdsch_items(const dmrs_pdsch_args* items, uint32_t count,
   if (count == 0 || max_crb_blocks == 0 || max_symbols == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(dmrs_pdsch_kernel<true>, dim3(max_crb_blocks, max_symbols, count), dim3(64), 0, stream,
-                     dmrs_pdsch_args{}, items);
+  hipLaunchKernelGGL(dmrs_pdsch_kernel<true>, dim3(max_crb_blocks, max_symbols, count), dim3(DMRS_THREADS), 0,
+                     stream, dmrs_pdsch_args{}, items, 1u);
   return hipGetLastError();
 }
 

@@ -585,7 +585,7 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
       a.grid_stride = 0;
       if (a.nof_crb != 0 && a.nof_dmrs_symbols != 0) {
         dmrs.push_back(a);
-        max_blocks       = std::max(max_blocks, (a.nof_crb + 63) / 64);
+        max_blocks       = std::max(max_blocks, (a.nof_crb * PDSCH_NRE + 255) / 256); // dmrs_pdsch_kernel REs per WG
         max_dmrs_symbols = std::max(max_dmrs_symbols, a.nof_dmrs_symbols);
       }
     }

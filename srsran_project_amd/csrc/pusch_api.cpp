@@ -40,6 +40,7 @@ struct srs_amd_pusch_decoder {
   srs_amd_ldpc_rate_dematcher* dm     = nullptr;
   srs_amd_ldpc_decoder*        dec[2] = {nullptr, nullptr}; // force_decoding 0 / 1
   device_buffer                soft, msgs, iters, checks, arrays, results, host_io, tb_acc, slot_desc;
+  geometry_cache               rm_geo; // last geometry written into arrays (rm_arrays_kernel)
   stream_order                 order; // scratch reuse across the callers' streams
   stream_fan                   fan;   // srs_amd_pusch_decode_slot: concurrent LDPC bucket launches
   std::mutex                   mtx;
@@ -170,8 +171,14 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   call_scope scope(d->order, nullptr, stream);
   he = d->order.begin(stream);
   if (he == hipSuccess) {
-    he = launch_rm_arrays(d->arrays.as<uint32_t>(), nof_tbs, C, p->nof_short_segments, p->rm_length_short,
-                          p->rm_length_long, llr_stride, stream);
+    const uint32_t key[6] = {nof_tbs, C, p->nof_short_segments, p->rm_length_short, p->rm_length_long, llr_stride};
+    if (d->rm_geo.stale(d->arrays.ptr, key, 6)) {
+      he = launch_rm_arrays(d->arrays.as<uint32_t>(), nof_tbs, C, p->nof_short_segments, p->rm_length_short,
+                            p->rm_length_long, llr_stride, stream);
+      if (he != hipSuccess) {
+        d->rm_geo.invalidate();
+      }
+    }
   }
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH decoder rate-matching arrays");

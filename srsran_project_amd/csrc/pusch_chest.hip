@@ -108,35 +108,55 @@ __device__ __forceinline__ float2 pilot(const chest_args& a, const uint32_t (*se
   return p;
 }
 
-// compute_v_pilots (port_channel_estimator_helpers.cpp:334-378), sequential over n <= 12 values.
-__device__ void virtual_pilots(float2* out, const float2* in, int n, bool is_start)
+// compute_v_pilots (port_channel_estimator_helpers.cpp:334-378) over one wave: lane i < n <= 12 computes the
+// modulus / argument of value i and output value i; the short serial parts (phase unwrapping, the four
+// sums) run redundantly in every lane on the shuffled values, in the reference's order.  One lane running
+// the whole function was a chain of 3 n transcendental functions on the slice kernel's critical path.
+__device__ void virtual_pilots_wave(float2* out, const float2* in, int n, bool is_start)
 {
+  const int lane = static_cast<int>(threadIdx.x & 63u);
+  float     av = 0, gv = 0;
+  if (lane < n) {
+    av = sqrtf(in[lane].x * in[lane].x + in[lane].y * in[lane].y);
+    gv = atan2f(in[lane].y, in[lane].x);
+  }
   float absv[CH_MAXV], argv[CH_MAXV];
-  for (int i = 0; i < n; ++i) {
-    absv[i] = sqrtf(in[i].x * in[i].x + in[i].y * in[i].y);
-    argv[i] = atan2f(in[i].y, in[i].x);
+#pragma unroll
+  for (int i = 0; i < CH_MAXV; ++i) {
+    absv[i] = __shfl(av, i);
+    argv[i] = __shfl(gv, i);
   }
   // unwrap_list (unwrap.cpp:42-62)
   const float width = 3.14159265358979323846f;
   float       k     = 0;
-  for (int i = 0; i < n - 1; ++i) {
-    const float old_a = argv[i], next_a = argv[i + 1];
-    argv[i] += 2.0f * k * width;
-    const float jump = next_a - old_a;
-    if (fabsf(jump) > width) {
-      k = k - copysignf(1.0f, jump);
+#pragma unroll
+  for (int i = 0; i < CH_MAXV - 1; ++i) {
+    if (i < n - 1) {
+      const float old_a = argv[i], next_a = argv[i + 1];
+      argv[i] += 2.0f * k * width;
+      const float jump = next_a - old_a;
+      if (fabsf(jump) > width) {
+        k = k - copysignf(1.0f, jump);
+      }
     }
   }
-  argv[n - 1] += 2.0f * k * width;
-
+#pragma unroll
+  for (int i = 0; i < CH_MAXV; ++i) {
+    if (i == n - 1) {
+      argv[i] += 2.0f * k * width;
+    }
+  }
   const float mean_x    = static_cast<float>(n * (n - 1)) / 2.0f / n;
   const float norm_x_sq = static_cast<float>((n - 1) * n * (2 * n - 1)) / 6.0f;
   float       sa = 0, sg = 0, ma = 0, mg = 0;
-  for (int i = 0; i < n; ++i) {
-    ma += absv[i];
-    mg += argv[i];
-    sa += absv[i] * static_cast<float>(i);
-    sg += argv[i] * static_cast<float>(i);
+#pragma unroll
+  for (int i = 0; i < CH_MAXV; ++i) {
+    if (i < n) {
+      ma += absv[i];
+      mg += argv[i];
+      sa += absv[i] * static_cast<float>(i);
+      sg += argv[i] * static_cast<float>(i);
+    }
   }
   ma /= n;
   mg /= n;
@@ -147,12 +167,12 @@ __device__ void virtual_pilots(float2* out, const float2* in, int n, bool is_sta
   const float ia  = ma - sa * mean_x;
   const float ig  = mg - sg * mean_x;
   const int   off = is_start ? -n : n;
-  for (int i = 0; i < n; ++i) {
-    const int   iv  = i + off;
+  if (lane < n) {
+    const int   iv  = lane + off;
     const float rho = sa * iv + ia;
     const float ph  = sg * iv + ig + ((rho > 0) ? 0.0f : 3.14159265358979323846f);
     const float r   = fabsf(rho);
-    out[i]          = make_float2(r * cosf(ph), r * sinf(ph));
+    out[lane]       = make_float2(r * cosf(ph), r * sinf(ph));
   }
 }
 
@@ -218,10 +238,16 @@ __global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a_in, 
   for (int k = 0; k < CS_PPT; ++k) {
     const uint32_t m = tid + k * CS_THREADS;
     if (m < npil) {
-      for (int gg = 0; gg < static_cast<int>(a.ncdm); ++gg) {
-        for (int d = 0; d < nds; ++d) {
-          const float2 u = rxv(gg, d, m);
-          epre           = __builtin_fmaf(u.x, u.x, __builtin_fmaf(u.y, u.y, epre));
+      // compile-time bounds (CDM groups of type 1, DM-RS symbols): every load of the thread is issued
+      // before the first is used
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+#pragma unroll
+        for (int d = 0; d < CH_MAXDMRS; ++d) {
+          if (gg < static_cast<int>(a.ncdm) && d < nds) {
+            const float2 u = rxv(gg, d, m);
+            epre           = __builtin_fmaf(u.x, u.x, __builtin_fmaf(u.y, u.y, epre));
+          }
         }
       }
     }
@@ -233,7 +259,11 @@ __global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a_in, 
     for (int k = 0; k < CS_PPT; ++k) {
       const uint32_t m = tid + k * CS_THREADS;
       if (m < npil) {
-        for (int vv = 0; vv < L; ++vv) {
+#pragma unroll
+        for (int vv = 0; vv < CH_MAXL; ++vv) {
+          if (vv >= L) {
+            break;
+          }
           const int    gg = vv / 2;
           const float2 p0 = cmulc(rxv(gg, 0, m), pilot(a, seq, bit0, 0, vv, m));
           const float2 p1 = cmulc(rxv(gg, 1, m), pilot(a, seq, bit0, 1, vv, m));
@@ -332,7 +362,11 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
         if (rotate) {
           y = cmul(y, s_rot[0]);
         }
-        for (int d = 1; d < nds; ++d) {
+#pragma unroll
+        for (int d = 1; d < CH_MAXDMRS; ++d) {
+          if (d >= nds) {
+            break;
+          }
           float2 t = cmulc(rxv(g, d, m), pilot(a, seq, bit0, d, v, m));
           if (rotate) {
             t = cmul(t, s_rot[d]);
@@ -384,10 +418,10 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
       }
     }
     __syncthreads();
-    if (tid == 0) {
-      virtual_pilots(enl_in + CH_MAXV - nv, enl_in + CH_MAXV, nv, true);
-    } else if (tid == 64) {
-      virtual_pilots(enl_in + CH_MAXV + npil, enl_in + CH_MAXV + npil - nv, nv, false);
+    if (tid < 64) {
+      virtual_pilots_wave(enl_in + CH_MAXV - nv, enl_in + CH_MAXV, nv, true);
+    } else if (tid < 128) {
+      virtual_pilots_wave(enl_in + CH_MAXV + npil, enl_in + CH_MAXV + npil - nv, nv, false);
     }
     __syncthreads();
     const int half = a.nof_taps / 2;

@@ -83,6 +83,100 @@ __global__ __launch_bounds__(SEG_THREADS) void segment_kernel(segment_args a)
       segment_byte(tb, r * a.cb_info_bits, n_data, last, a.tb_crcs[t], a.tb_crc_bits, j);
 }
 
+// Segmentation and CRC24B attachment in one pass (C > 1): one wave per (TB, segment) row.  Lane l builds
+// the contiguous message bytes [l per, (l + 1) per) in registers (segment_byte), divides them into its CRC
+// contribution, the wave XOR-reduces the codeblock CRC, every lane patches the CRC bits that fall into its
+// own bytes and stores them: the message row is written once and never read back.
+constexpr int      SEGCRC_THREADS = 64;
+constexpr uint32_t SEGCRC_PER     = 20; // bytes per lane: 64 x 20 >= 1,056 (BG1 K = 8,448 bits)
+
+__global__ __launch_bounds__(SEGCRC_THREADS) void segment_crc_kernel(segment_args a)
+{
+  __shared__ uint32_t T[256];
+  // the segment's TB bytes (coalesced loads), then the message row (coalesced stores)
+  __shared__ __attribute__((aligned(16))) uint8_t s_io[SEGCRC_THREADS * SEGCRC_PER + 8];
+  crc_table8_init<SEGCRC_THREADS>(T, 24, a.cb_crc_poly);
+  const uint32_t row = blockIdx.x;
+  const uint32_t t   = row / a.nof_segments;
+  const uint32_t r   = row - t * a.nof_segments;
+  const bool     last   = r == a.nof_segments - 1;
+  const uint32_t n_data = last ? a.last_data_bits : a.cb_info_bits;
+  const uint8_t* tb     = a.tbs + static_cast<size_t>(t) * a.tb_stride;
+  const uint32_t crc_t  = a.tb_crcs[t];
+  const uint32_t b0     = threadIdx.x * SEGCRC_PER;
+  const uint32_t off    = r * a.cb_info_bits;        // first TB bit of the segment
+  const uint32_t q0     = off >> 3;                   // its byte
+  const uint32_t nsrc   = (off + n_data + 7) / 8 - q0; // TB bytes the segment touches (<= msg_bytes + 1)
+  for (uint32_t i = threadIdx.x; i < nsrc; i += SEGCRC_THREADS) {
+    s_io[i] = tb[q0 + i];
+  }
+  __syncthreads(); // T, s_io ready
+  uint32_t v[SEGCRC_PER];
+#pragma unroll
+  for (uint32_t k = 0; k < SEGCRC_PER; ++k) {
+    const uint32_t j = b0 + k;
+    v[k]             = j < a.msg_bytes ? segment_byte(s_io, off & 7u, n_data, last, crc_t, a.tb_crc_bits, j) : 0u;
+  }
+  // CRC contribution of this lane's bits below n = cb_info_bits, moved to n (crc_device.h)
+  const uint32_t n    = a.cb_info_bits;
+  const uint32_t full = n / 8;
+  uint32_t       rem  = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < SEGCRC_PER; ++k) {
+    const uint32_t j = b0 + k;
+    if (j < full) {
+      rem = T[rem >> 16] ^ ((rem << 8) & 0xffffffu) ^ v[k];
+    } else if (j == full && (n & 7u) != 0) {
+      for (uint32_t i = 0; i < (n & 7u); ++i) {
+        rem = (rem << 1) | ((v[k] >> (7 - i)) & 1u);
+        if (rem & 0x1000000u) {
+          rem ^= a.cb_crc_poly;
+        }
+      }
+    }
+  }
+  uint32_t contrib = 0;
+  if (b0 * 8 < n) {
+    const uint32_t e = min(n, (b0 + SEGCRC_PER) * 8);
+#pragma unroll
+    for (uint32_t i = 0; i < 24; ++i) {
+      contrib ^= a.cb_crc_table[n - e + i] & (0u - ((rem >> i) & 1u));
+    }
+  }
+  const uint32_t crc = crc_wave_xor(contrib);
+  // the CRC bits [n, n + 24) that land in this lane's bytes
+#pragma unroll
+  for (uint32_t k = 0; k < SEGCRC_PER; ++k) {
+    const uint32_t j = b0 + k;
+    if (8 * j + 8 > n && 8 * j < n + 24) {
+#pragma unroll
+      for (uint32_t b = 0; b < 8; ++b) {
+        const uint32_t pos = 8 * j + b;
+        if (pos >= n && pos < n + 24) {
+          const uint32_t mask = 0x80u >> b;
+          v[k]                = (v[k] & ~mask) | (((crc >> (23 - (pos - n))) & 1u) ? mask : 0u);
+        }
+      }
+    }
+  }
+  __syncthreads(); // every lane has read its TB bytes from s_io
+#pragma unroll
+  for (uint32_t k = 0; k < SEGCRC_PER; ++k) {
+    s_io[b0 + k] = static_cast<uint8_t>(v[k]);
+  }
+  __syncthreads();
+  uint8_t* m = a.msgs + static_cast<size_t>(row) * a.msg_stride;
+  if ((reinterpret_cast<uintptr_t>(m) & 3u) == 0) {
+    for (uint32_t w = threadIdx.x; w < (a.msg_bytes + 3) / 4; w += SEGCRC_THREADS) {
+      reinterpret_cast<uint32_t*>(m)[w] = reinterpret_cast<const uint32_t*>(s_io)[w]; // row padded to 64 B
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < a.msg_bytes; i += SEGCRC_THREADS) {
+      m[i] = s_io[i];
+    }
+  }
+}
+
 // ---- PDSCH encoder of a heterogeneous batch (srs_amd_pdsch_encode_slot) ----
 
 // TB CRC (CRC16 / CRC24A per TB): one workgroup per ASM_TB_CHUNK bytes of a TB, partials XOR-ed into acc[t].
@@ -100,14 +194,18 @@ __global__ __launch_bounds__(ASM_THREADS) void tx_tb_crc_kernel(tx_slot_args a)
   const bool      c16   = d.tb_crc_bits == 16;
   const uint32_t  poly  = c16 ? a.crc16_poly : a.crc24a_poly;
   const uint32_t* table = c16 ? a.crc16_table : a.crc24a_table;
+  __shared__ __attribute__((aligned(16))) uint8_t s_chunk[ASM_TB_CHUNK];
   crc_table8_init<ASM_THREADS>(T, d.tb_crc_bits, poly);
+  crc_stage_bytes<ASM_THREADS>(s_chunk, a.tbs + d.tb_offset, c0, min(ASM_TB_CHUNK, nbytes - c0)); // coalesced
   __syncthreads();
   const uint32_t b0 = c0 + threadIdx.x * ASM_TB_PER;
   const uint32_t b1 = min(nbytes, b0 + ASM_TB_PER);
+  const uint32_t to = min(d.tbs_bits, (c0 + ASM_TB_CHUNK) * 8); // moved to the TB end once per workgroup
   const uint32_t x  = crc_block_xor<ASM_THREADS>(
-      crc_chunk_contrib(row_fetch{a.tbs + d.tb_offset}, b0, b1, d.tbs_bits, d.tb_crc_bits, poly, table, T), partial);
+      crc_chunk_contrib(lds_chunk_fetch{s_chunk, c0}, b0, b1, d.tbs_bits, d.tb_crc_bits, poly, table, T, to),
+      partial);
   if (threadIdx.x == 0 && x != 0) {
-    atomicXor(a.acc + t, x);
+    atomicXor(a.acc + t, crc_move(x, d.tbs_bits - to, d.tb_crc_bits, table));
   }
 }
 
@@ -145,17 +243,7 @@ __global__ __launch_bounds__(64) void tx_cb_crc_kernel(tx_slot_args a)
   const uint32_t n   = d.cb_info_bits;
   const uint32_t crc = block_crc_bytes<64>(row_fetch{m}, n, 24, a.crc24b_poly, a.crc24b_table, T, partial);
   if (threadIdx.x == 0) {
-    for (uint32_t q = n >> 3; q <= (n + 23) >> 3; ++q) {
-      uint32_t byte = m[q];
-      for (uint32_t b = 0; b < 8; ++b) {
-        const uint32_t pos = 8 * q + b;
-        if (pos >= n && pos < n + 24) {
-          const uint32_t mask = 0x80u >> b;
-          byte                = (byte & ~mask) | (((crc >> (23 - (pos - n))) & 1u) ? mask : 0u);
-        }
-      }
-      m[q] = static_cast<uint8_t>(byte);
-    }
+    attach_crc_bits(m, n, 24, crc);
   }
 }
 
@@ -359,18 +447,32 @@ __global__ __launch_bounds__(ASM_THREADS) void asm_tb_kernel(assemble_args a)
   uint8_t*        tb     = v.tb;
   const uint32_t  nbytes = v.tbs_bits / 8;
   const uint32_t  n      = min(ASM_TB_CHUNK, nbytes - c0);
-  for (uint32_t i = threadIdx.x; i < n; i += ASM_THREADS) {
-    const uint32_t b = g(c0 + i);
-    s_chunk[i]       = static_cast<uint8_t>(b);
-    tb[c0 + i]       = static_cast<uint8_t>(b);
+  constexpr uint32_t U = 8; // gathers in flight per thread before their stores
+  for (uint32_t i0 = threadIdx.x; i0 < n; i0 += U * ASM_THREADS) {
+    uint32_t v[U];
+#pragma unroll
+    for (uint32_t r = 0; r < U; ++r) {
+      const uint32_t i = i0 + r * ASM_THREADS;
+      v[r]             = i < n ? g(c0 + i) : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < U; ++r) {
+      const uint32_t i = i0 + r * ASM_THREADS;
+      if (i < n) {
+        s_chunk[i] = static_cast<uint8_t>(v[r]);
+        tb[c0 + i] = static_cast<uint8_t>(v[r]);
+      }
+    }
   }
   __syncthreads();
   const uint32_t b0 = c0 + threadIdx.x * ASM_TB_PER;
   const uint32_t b1 = min(nbytes, b0 + ASM_TB_PER);
+  const uint32_t to = min(v.tbs_bits, (c0 + ASM_TB_CHUNK) * 8); // moved to the TB end once per workgroup
   const uint32_t x  = crc_block_xor<ASM_THREADS>(
-      crc_chunk_contrib(lds_fetch{s_chunk, c0}, b0, b1, v.tbs_bits, 24, CRC24A_POLY, a.crc24a_table, T), partial);
+      crc_chunk_contrib(lds_fetch{s_chunk, c0}, b0, b1, v.tbs_bits, 24, CRC24A_POLY, a.crc24a_table, T, to),
+      partial);
   if (threadIdx.x == 0 && x != 0) {
-    atomicXor(a.acc + t, x);
+    atomicXor(a.acc + t, crc_move(x, v.tbs_bits - to, 24, a.crc24a_table));
   }
 }
 
@@ -427,10 +529,19 @@ hipError_t launch_rm_arrays(uint32_t* arrays, uint32_t nof_tbs, uint32_t C, uint
   return hipGetLastError();
 }
 
+bool segment_attaches_crc(const segment_args& a)
+{
+  return a.cb_crc_table != nullptr && a.msg_bytes <= SEGCRC_THREADS * SEGCRC_PER;
+}
+
 hipError_t launch_segment(const segment_args& a, hipStream_t stream)
 {
   if (a.nof_rows == 0) {
     return hipSuccess;
+  }
+  if (segment_attaches_crc(a)) {
+    hipLaunchKernelGGL(segment_crc_kernel, dim3(a.nof_rows), dim3(SEGCRC_THREADS), 0, stream, a);
+    return hipGetLastError();
   }
   dim3 grid((a.msg_bytes + SEG_THREADS - 1) / SEG_THREADS, a.nof_rows);
   hipLaunchKernelGGL(segment_kernel, grid, dim3(SEG_THREADS), 0, stream, a);

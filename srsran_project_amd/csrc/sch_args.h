@@ -25,6 +25,10 @@ struct segment_args {
   uint32_t        last_data_bits; // TB bits in the last segment
   uint32_t        tb_crc_bits;
   uint32_t        nof_rows;   // nof_tbs * C
+  // CRC24B attachment in the same pass (C > 1): the codeblock CRC over bits [0, cb_info_bits) written at
+  // bit cb_info_bits (ldpc_segmenter_tx_impl.cpp:196); null table: segmentation only
+  const uint32_t* cb_crc_table; // x^(k+24) mod g (crc_linear_table)
+  uint32_t        cb_crc_poly;
 };
 
 // Per-CB soft-buffer row (HARQ rx_buffer): [soft LLRs | saved message | CRC flag].
@@ -97,6 +101,8 @@ struct assemble_args {
 };
 
 hipError_t launch_segment(const segment_args& a, hipStream_t stream);
+// true when launch_segment also attaches the codeblock CRCs (segment_crc_kernel)
+bool       segment_attaches_crc(const segment_args& a);
 // Per-codeblock rate-matching lengths and codeword offsets of nof_tbs transport blocks of one plan
 // (srs_amd_sch_plan_segments per TB), written on the device: arrays[row] = E_r, arrays[rows + row] =
 // tb * tb_units + offset_r, row = tb * C + r.  No host upload, so a plan change never blocks the host.
