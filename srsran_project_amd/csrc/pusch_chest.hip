@@ -430,9 +430,11 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
       const int m = static_cast<int>(tid + k * CS_THREADS);
       if (m < static_cast<int>(npil)) {
         float2 acc = make_float2(0, 0);
-        for (int j = 0; j < a.nof_taps; ++j) {
+        // compile-time tap bound: the LDS reads of every tap are issued together (same summation order)
+#pragma unroll
+        for (int j = 0; j < CH_MAXV + 4; ++j) {
           const int i = m + j - half; // convolution input index (pilot domain)
-          if (i >= -nv && i < static_cast<int>(npil) + nv) {
+          if (j < a.nof_taps && i >= -nv && i < static_cast<int>(npil) + nv) {
             const float2 in = enl_in[CH_MAXV + i];
             const float  c  = a.rc[a.nof_taps - 1 - j];
             acc.x           = acc.x + in.x * c; // srsran_simd_f_mul then _add
@@ -459,20 +461,30 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
   __syncthreads();
   // Linear interpolation (interpolator_linear_impl.cpp): pilots at offset g + 2i.
   float2* fr = a.freq + (static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice) * a.nof_re;
-  for (uint32_t kk = tid; kk < a.nof_re; kk += CS_THREADS) {
-    float2 out;
-    if (kk <= static_cast<uint32_t>(g)) {
-      out = enl_out[0];
-    } else {
-      const uint32_t j = (kk - g) / 2, r = (kk - g) % 2;
-      if (j + 1 < npil) {
-        const float2 p0 = enl_out[j], p1 = enl_out[j + 1];
-        out = r ? make_float2((p1.x - p0.x) * 0.5f + p0.x, (p1.y - p0.y) * 0.5f + p0.y) : p0;
+  constexpr uint32_t IU = 4; // outputs per thread and round: their LDS reads issued together
+  for (uint32_t k0 = tid; k0 < a.nof_re; k0 += IU * CS_THREADS) {
+    float2 out[IU];
+#pragma unroll
+    for (uint32_t u = 0; u < IU; ++u) {
+      const uint32_t kk = min(k0 + u * CS_THREADS, a.nof_re - 1);
+      if (kk <= static_cast<uint32_t>(g)) {
+        out[u] = enl_out[0];
       } else {
-        out = enl_out[npil - 1];
+        const uint32_t j = (kk - g) / 2, r = (kk - g) % 2;
+        if (j + 1 < npil) {
+          const float2 p0 = enl_out[j], p1 = enl_out[j + 1];
+          out[u] = r ? make_float2((p1.x - p0.x) * 0.5f + p0.x, (p1.y - p0.y) * 0.5f + p0.y) : p0;
+        } else {
+          out[u] = enl_out[npil - 1];
+        }
       }
     }
-    fr[kk] = out;
+#pragma unroll
+    for (uint32_t u = 0; u < IU; ++u) {
+      if (k0 + u * CS_THREADS < a.nof_re) {
+        fr[k0 + u * CS_THREADS] = out[u];
+      }
+    }
   }
   const float4 tot = block_sum4(make_float4(rsrp, 0, 0, 0), red);
   if (tid == 0) {

@@ -252,12 +252,25 @@ struct tb_gather {
   const uint8_t* base;
   uint32_t       stride;
   uint32_t       cbi;
+  float          rcp; // 1 / cbi: the codeblock of bit b from a float estimate and one correction (b < 2^24)
+  __device__ tb_gather(const uint8_t* base_, uint32_t stride_, uint32_t cbi_) :
+    base(base_), stride(stride_), cbi(cbi_), rcp(1.0f / static_cast<float>(cbi_))
+  {
+  }
   __device__ uint32_t operator()(uint32_t j) const
   {
     uint32_t byte = 0;
     uint32_t b    = 8 * j;
-    uint32_t r    = b / cbi;
-    uint32_t o    = b - r * cbi;
+    uint32_t r    = static_cast<uint32_t>(static_cast<float>(b) * rcp);
+    int32_t  x    = static_cast<int32_t>(b - r * cbi);
+    if (x < 0) {
+      r -= 1;
+      x += static_cast<int32_t>(cbi);
+    } else if (x >= static_cast<int32_t>(cbi)) {
+      r += 1;
+      x -= static_cast<int32_t>(cbi);
+    }
+    uint32_t o = static_cast<uint32_t>(x);
     if (o + 8 <= cbi) {
       // the 8 bits lie in one codeblock: one or two byte loads
       const uint8_t* m  = base + static_cast<size_t>(r) * stride + (o >> 3);
@@ -330,6 +343,9 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
   __shared__ uint16_t s_stat[SCH_MAX_SEGMENTS]; // iterations of the freshly decoded codeblocks
   const uint32_t      t = blockIdx.x;
   const tb_view       v = view_of(a, t);
+  if (threadIdx.x == 0 && a.acc != nullptr) {
+    a.acc[t] = 0; // the TB CRC accumulator of asm_tb_kernel (launched after this kernel): no memset launch
+  }
   const uint32_t      C = v.C;
   if (threadIdx.x == 0) {
     s_ok    = 0;
@@ -581,10 +597,7 @@ hipError_t launch_assemble(const assemble_args& a, uint32_t nof_tbs, hipStream_t
   if (e != hipSuccess || (a.tds == nullptr && a.nof_segments == 1)) {
     return e;
   }
-  e = hipMemsetAsync(a.acc, 0, sizeof(uint32_t) * nof_tbs, stream);
-  if (e != hipSuccess) {
-    return e;
-  }
+  // a.acc was zeroed by assemble_kernel
   const uint32_t nbytes = (a.tds != nullptr ? a.max_tb_bits : a.tbs_bits) / 8;
   hipLaunchKernelGGL(asm_tb_kernel, dim3((nbytes + ASM_TB_CHUNK - 1) / ASM_TB_CHUNK, nof_tbs), dim3(ASM_THREADS), 0,
                      stream, a);
