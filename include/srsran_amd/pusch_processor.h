@@ -39,6 +39,7 @@
 #include "srsran_amd/pusch_chest.h"
 #include "srsran_amd/pusch_demodulator.h"
 #include "srsran_amd/sch.h"
+#include "srsran_amd/uci_decoder.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -88,12 +89,18 @@ typedef struct srs_amd_pusch_pdu {
                                    nof_cdm_groups_without_data are then unused (two CDM groups, as the reference) */
   uint32_t n_rs_id;           /* {0 .. 1007} */
   /* uci_description (pusch_processor.h:64-90): HARQ-ACK and CSI part 1 payloads multiplexed with the UL-SCH
-     (0: none), the scaling and beta offsets of TS 38.213 9.3; CSI part 2 is not supported */
+     (0: none), the scaling and beta offsets of TS 38.213 9.3 */
   uint32_t nof_harq_ack;
   uint32_t nof_csi_part1;
   float    alpha_scaling;
   float    beta_offset_harq_ack;
   float    beta_offset_csi_part1;
+  /* CSI part 2 (uci_description::csi_part2_size, beta_offset_csi_part2): its size comes from the decoded CSI part 1
+     (uci_part2_get_size, pusch_processor_impl.cpp:73-103); no entries: none.  srs_amd_pusch_process_batch then
+     decodes CSI part 1 first, reads it back (one host synchronisation) and demultiplexes and decodes CSI part 2
+     and the UL-SCH of each grid with the geometry of its CSI part 2 size. */
+  float                              beta_offset_csi_part2;
+  srs_amd_uci_part2_size_description csi_part2_size;
 } srs_amd_pusch_pdu;
 
 /* Per-transport-block results: pusch_decoder_result (sch.h), the UCI statuses and the channel
@@ -109,6 +116,8 @@ typedef struct srs_amd_pusch_processor_result {
   float                        time_alignment_s;
   int32_t                      harq_ack_status;  /* SRS_AMD_UCI_* (uci_decoder.h); 0 without HARQ-ACK */
   int32_t                      csi_part1_status; /* SRS_AMD_UCI_*; 0 without CSI part 1 */
+  int32_t                      csi_part2_status; /* SRS_AMD_UCI_*; 0 without CSI part 2 */
+  uint32_t                     nof_csi_part2;    /* CSI part 2 payload bits (from the decoded CSI part 1) */
 } srs_amd_pusch_processor_result;
 
 typedef struct srs_amd_pusch_processor      srs_amd_pusch_processor;
@@ -147,6 +156,9 @@ typedef struct srs_amd_pusch_intermediates {
   uint32_t                  harq_ack_stride;
   uint8_t*                  d_csi_part1;
   uint32_t                  csi_part1_stride;
+  /* CSI part 2 payloads: rows of csi_part2_stride bytes (at least the largest size the description allows) */
+  uint8_t*                  d_csi_part2;
+  uint32_t                  csi_part2_stride;
 } srs_amd_pusch_intermediates;
 
 /* DEVICE, asynchronous: nof_grids received grids cbf16 [grid][port][14][nof_subc]

@@ -52,6 +52,31 @@ int srs_amd_uci_decode_batch(srs_amd_uci_decoder* dec,
 int srs_amd_uci_decode(srs_amd_uci_decoder* dec, uint8_t* message, uint32_t K, const int8_t* llrs, uint32_t E,
                        int32_t modulation);
 
+/* uci_part2_size_description (include/srsran/ran/uci/uci_part2_size_description.h:30-95): at most two entries, each
+ * combining at most two CSI part 1 fields (bit offset, width; at most four bits in all) into an index of its map of
+ * CSI part 2 sizes. */
+typedef struct srs_amd_uci_part2_parameter {
+  uint16_t offset; /* bit offset in CSI part 1 */
+  uint16_t width;
+} srs_amd_uci_part2_parameter;
+typedef struct srs_amd_uci_part2_entry {
+  uint32_t                    nof_parameters;
+  srs_amd_uci_part2_parameter parameters[2];
+  uint32_t                    map_size; /* 1 << (sum of the widths) */
+  uint16_t                    map[16];
+} srs_amd_uci_part2_entry;
+typedef struct srs_amd_uci_part2_size_description {
+  uint32_t                nof_entries; /* 0: no CSI part 2 */
+  srs_amd_uci_part2_entry entries[2];
+} srs_amd_uci_part2_size_description;
+
+/* HOST: uci_part2_get_size (lib/ran/uci/uci_part2_size_calculator.cpp:53-89): the CSI part 2 payload size of a decoded
+ * CSI part 1 (one bit per byte), each field read MSB first.  Returns the size, or -1 for a field past the payload or
+ * a map of the wrong size (the reference asserts). */
+int32_t srs_amd_uci_part2_get_size(const uint8_t*                            part1,
+                                   uint32_t                                  nof_part1_bits,
+                                   const srs_amd_uci_part2_size_description* descr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,8 +12,11 @@
  *        HARQ-ACK REs in the reserved set, each chosen every d-th RE; placeholders x / y un-scrambled;
  *        the UL-SCH copy of a 1/2-bit HARQ-ACK RE zeroed)
  * The placement is resolved once per plan on the host into a per-RE table; the device pass reads every
- * codeword LLR once and writes each stream once.  Bit-exact.  Scope: no CSI part 2 (the reference multiplexes
- * it only after decoding CSI part 1, set_csi_part2).
+ * codeword LLR once and writes each stream once.  Bit-exact.
+ * CSI part 2 (ulsch_demultiplex::set_csi_part2, ulsch_demultiplex_impl.cpp:241-251, 450-472): its size comes from the
+ * decoded CSI part 1, and the reference sets it while demultiplexing the OFDM symbol in which CSI part 1 ends, so
+ * its REs start in that symbol (every d-th remaining UCI RE, reserved HARQ-ACK REs included; where a 1/2-bit
+ * HARQ-ACK shares the RE the CSI part 2 LLRs are zero).  A plan with nof_csi_part2_bits != 0 places it the same way.
  */
 #ifndef SRSRAN_AMD_ULSCH_DEMUX_H
 #define SRSRAN_AMD_ULSCH_DEMUX_H
@@ -43,6 +46,8 @@ typedef struct srs_amd_ulsch_demux_config {
   uint32_t nof_csi_part1_bits;
   uint32_t nof_enc_csi_part1_bits;
   uint32_t c_init;
+  uint32_t nof_csi_part2_bits;          /* payload (0: no CSI part 2) */
+  uint32_t nof_enc_csi_part2_bits;      /* rate matched (ulsch_information::nof_csi_part2_bits) */
 } srs_amd_ulsch_demux_config;
 
 typedef struct srs_amd_ulsch_demux      srs_amd_ulsch_demux;
@@ -82,6 +87,30 @@ int srs_amd_ulsch_demultiplex(srs_amd_ulsch_demux*            demux,
                               int8_t*                         sch,
                               int8_t*                         ack,
                               int8_t*                         csi1);
+
+/* As srs_amd_ulsch_demultiplex_batch / srs_amd_ulsch_demultiplex, plus the CSI part 2 rows (csi2_stride apart,
+ * nof_enc_csi_part2_bits each).  The forms above require a plan without CSI part 2. */
+int srs_amd_ulsch_demultiplex_csi2_batch(srs_amd_ulsch_demux*            demux,
+                                         const srs_amd_ulsch_demux_plan* plan,
+                                         const int8_t*                   d_cws,
+                                         uint64_t                        cw_stride,
+                                         int8_t*                         d_sch,
+                                         uint64_t                        sch_stride,
+                                         int8_t*                         d_ack,
+                                         uint64_t                        ack_stride,
+                                         int8_t*                         d_csi1,
+                                         uint64_t                        csi1_stride,
+                                         int8_t*                         d_csi2,
+                                         uint64_t                        csi2_stride,
+                                         uint32_t                        nof_cws,
+                                         void*                           stream);
+int srs_amd_ulsch_demultiplex_csi2(srs_amd_ulsch_demux*            demux,
+                                   const srs_amd_ulsch_demux_plan* plan,
+                                   const int8_t*                   codeword,
+                                   int8_t*                         sch,
+                                   int8_t*                         ack,
+                                   int8_t*                         csi1,
+                                   int8_t*                         csi2);
 
 #ifdef __cplusplus
 }

@@ -73,6 +73,13 @@ def ref_pusch_process(grid, pdu, tb_bytes, iterations=2, choice="auto", rx_buffe
     ack = np.zeros(max(1, pdu.get("nof_harq_ack", 0)), np.uint8)
     csi1 = np.zeros(max(1, pdu.get("nof_csi_part1", 0)), np.uint8)
     ust = np.zeros(2, np.int32)
+    part2 = pdu.get("csi_part2_size")
+    if part2:
+        f = REF.srs_ref_pusch_set_csi_part2
+        f.restype = None
+        f.argtypes = [_c.c_void_p, _c.c_uint, _c.c_float]
+        w = part2_words(part2)
+        f(_ptr(w), w.size, float(pdu.get("beta_offset_csi_part2", 5.0)))
     r = REF.srs_ref_pusch_process(
         _ptr(g), P, nsubc, pdu["numerology"], pdu["slot_index"], pdu["rnti"], pdu["bwp_start_rb"], pdu["bwp_size_rb"],
         pdu["modulation"], float(pdu["target_code_rate"]), pdu["rv"], pdu["base_graph"], int(pdu["new_data"]),
@@ -85,7 +92,13 @@ def ref_pusch_process(grid, pdu, tb_bytes, iterations=2, choice="auto", rx_buffe
         float(pdu.get("beta_offset_csi_part1", 5.0)), _ptr(ack), _ptr(csi1), _ptr(ust))
     if r != 0:
         raise RuntimeError("reference PUSCH processor did not notify")
-    return tb, dict(tb_crc_ok=bool(res[0]), nof_codeblocks_total=int(res[1]), nof_observations=int(res[2]),
+    csi2, st2 = np.zeros(4096, np.uint8), np.zeros(1, np.int32)
+    g = REF.srs_ref_pusch_get_csi_part2
+    g.restype = _c.c_int
+    g.argtypes = [_c.c_void_p, _c.c_uint, _c.c_void_p]
+    n2 = g(_ptr(csi2), csi2.size, _ptr(st2))
+    return tb, dict(csi_part2=csi2[:n2].copy(), csi_part2_status=int(st2[0]),
+                    tb_crc_ok=bool(res[0]), nof_codeblocks_total=int(res[1]), nof_observations=int(res[2]),
                     iterations_sum=int(round(res[3])), iterations_min=int(res[4]), iterations_max=int(res[5]),
                     sinr_db=csi[0], epre_db=csi[1], rsrp_db=csi[2], time_alignment_s=csi[3],
                     harq_ack=ack[:pdu.get("nof_harq_ack", 0)], csi_part1=csi1[:pdu.get("nof_csi_part1", 0)],
@@ -114,14 +127,15 @@ def ue_transmit(tb, pdu, nsubc, channel=None, snr_db=None, seed=0, nof_rx_ports=
     nch = nre * L
     info = None
     if uci is not None:
-        info = ref_ulsch_information(pdu, tbs)
+        info = ref_ulsch_information(pdu, tbs, len(uci[2]) if len(uci) > 2 else 0)
         nch = info["nof_ul_sch_bits"] // pdu["modulation"]
     p = osch.plan(tbs, pdu["base_graph"], pdu["rv"], pdu["modulation"], nref(tbs, pdu["base_graph"],
                                                                             pdu.get("tbs_lbrm_bytes", 0)),
                   L, nch)
     cw = ref_pdsch_encode(np.asarray(tb, np.uint8), p)
     if uci is not None:
-        cw = ue_multiplex_uci(cw, pdu, info, nre * L * pdu["modulation"], uci[0], uci[1])
+        cw = ue_multiplex_uci(cw, pdu, info, nre * L * pdu["modulation"], uci[0], uci[1],
+                              uci[2] if len(uci) > 2 else ())
     grid = np.zeros((P, 14, nsubc, 2), np.uint16)
     ref_pdsch_modulate(grid, cw, pdu["rnti"], pdu["n_id"], pdu["modulation"], crbs, pdu["start_symbol_index"],
                        pdu["nof_symbols"], pdu["dmrs_symbol_mask"], False, pdu["nof_cdm_groups_without_data"], [],
@@ -211,6 +225,53 @@ def ref_ulsch_demultiplex(llrs, qm, nof_layers, nof_prb, start_symbol, nof_symbo
     return sch[:counts[0]], ack[:counts[1]], csi1[:counts[2]]
 
 
+if REF is not None and hasattr(REF, "srs_ref_ulsch_demultiplex2"):
+    REF.srs_ref_ulsch_demultiplex2.restype = _c.c_int
+    REF.srs_ref_ulsch_demultiplex2.argtypes = ([_c.c_int] + [_c.c_uint] * 5 + [_c.c_int] + [_c.c_uint] * 9
+                                               + [_c.c_void_p, _c.c_uint] + [_c.c_void_p] * 5)
+
+
+def ref_ulsch_demultiplex2(llrs, qm, nof_layers, nof_prb, start_symbol, nof_symbols, nof_harq_ack_rvd, dmrs_type2,
+                           dmrs_mask, nof_cdm_groups_without_data, nof_harq_ack_bits, nof_enc_harq_ack_bits,
+                           nof_csi_part1_bits, nof_enc_csi_part1_bits, nof_csi_part2_bits, nof_enc_csi_part2_bits,
+                           c_init):
+    """The reference ulsch_demultiplex_impl with CSI part 2 configured when the CSI part 1 stream ends (as its PUSCH
+    processor does): (UL-SCH, HARQ-ACK, CSI part 1, CSI part 2) int8 streams."""
+    x = np.ascontiguousarray(llrs, np.int8)
+    sch, ack, csi1, csi2 = (np.zeros(x.size, np.int8) for _ in range(4))
+    counts = np.zeros(4, np.uint32)
+    r = REF.srs_ref_ulsch_demultiplex2(qm, nof_layers, nof_prb, start_symbol, nof_symbols, nof_harq_ack_rvd,
+                                       int(dmrs_type2), dmrs_mask, nof_cdm_groups_without_data, nof_harq_ack_bits,
+                                       nof_enc_harq_ack_bits, nof_csi_part1_bits, nof_enc_csi_part1_bits,
+                                       nof_csi_part2_bits, nof_enc_csi_part2_bits, c_init, _ptr(x), x.size, _ptr(sch),
+                                       _ptr(ack), _ptr(csi1), _ptr(csi2), _ptr(counts))
+    if r != 0:
+        raise RuntimeError("reference demultiplexer did not end every stream")
+    return sch[:counts[0]], ack[:counts[1]], csi1[:counts[2]], csi2[:counts[3]]
+
+
+def part2_words(entries):
+    """A uci_part2_size_description [([(offset, width), ...], [sizes]), ...] as the glue's flat uint16 words."""
+    w = [len(entries)]
+    for params, sizes in entries:
+        x = [len(params)] + [0] * 4 + [len(sizes)] + [0] * 16
+        for q, (off, wd) in enumerate(params):
+            x[1 + 2 * q], x[2 + 2 * q] = off, wd
+        x[6:6 + len(sizes)] = sizes
+        w += x
+    return np.ascontiguousarray(w, np.uint16)
+
+
+def ref_uci_part2_get_size(part1, entries):
+    """The reference uci_part2_get_size."""
+    b = np.ascontiguousarray(part1, np.uint8)
+    w = part2_words(entries)
+    f = REF.srs_ref_uci_part2_get_size
+    f.restype = _c.c_uint
+    f.argtypes = [_c.c_void_p, _c.c_uint, _c.c_void_p]
+    return int(f(_ptr(b), b.size, _ptr(w)))
+
+
 if REF is not None and hasattr(REF, "srs_ref_uci_decode"):
     REF.srs_ref_uci_decode.restype = _c.c_int
     REF.srs_ref_uci_decode.argtypes = [_c.c_void_p, _c.c_uint, _c.c_uint, _c.c_int, _c.c_void_p]
@@ -276,19 +337,21 @@ ULSCH_INFO_FIELDS = ["nof_ul_sch_bits", "nof_harq_ack_bits", "nof_harq_ack_rvd",
                      "sch_nof_bits_per_cb", "sch_nof_filler_bits_per_cb"]
 
 
-def ref_ulsch_information(pdu, tbs):
-    """The reference get_ulsch_information for a PUSCH pdu dict (type-1 DM-RS, no CSI part 2, no DC)."""
+def ref_ulsch_information(pdu, tbs, nof_csi_part2=0):
+    """The reference get_ulsch_information for a PUSCH pdu dict (type-1 DM-RS, no DC), with nof_csi_part2 CSI part 2
+    payload bits."""
     out = np.zeros(15, np.uint32)
     REF.srs_ref_ulsch_information(tbs, pdu["modulation"], float(pdu["target_code_rate"]), pdu.get("nof_harq_ack", 0),
-                                  pdu.get("nof_csi_part1", 0), 0, float(pdu.get("alpha_scaling", 1.0)),
+                                  pdu.get("nof_csi_part1", 0), nof_csi_part2, float(pdu.get("alpha_scaling", 1.0)),
                                   float(pdu.get("beta_offset_harq_ack", 5.0)),
-                                  float(pdu.get("beta_offset_csi_part1", 5.0)), 5.0, pdu["rb_count"],
+                                  float(pdu.get("beta_offset_csi_part1", 5.0)),
+                                  float(pdu.get("beta_offset_csi_part2", 5.0)), pdu["rb_count"],
                                   pdu["start_symbol_index"], pdu["nof_symbols"], 0, pdu["dmrs_symbol_mask"],
                                   pdu["nof_cdm_groups_without_data"], pdu["nof_tx_layers"], 0, _ptr(out))
     return dict(zip(ULSCH_INFO_FIELDS, out.tolist()))
 
 
-def ue_multiplex_uci(sch_cw, pdu, info, nof_cw_bits, ack_bits, csi1_bits):
+def ue_multiplex_uci(sch_cw, pdu, info, nof_cw_bits, ack_bits, csi1_bits, csi2_bits=()):
     """UE-side UL-SCH / UCI multiplexing for test inputs (TS 38.212 6.2.7 + 6.3.2.1): the UCI encoded with
     uci_encode, the RE placement read off the reference's own demultiplexer (three probe passes with the RE index
     coded in the LLR values), the ACK of <= 2 bits puncturing the UL-SCH, and the scrambler's placeholder rules
@@ -299,30 +362,39 @@ def ue_multiplex_uci(sch_cw, pdu, info, nof_cw_bits, ack_bits, csi1_bits):
     qm, L = pdu["modulation"], pdu["nof_tx_layers"]
     bpre = qm * L
     nre = nof_cw_bits // bpre
-    K_ack, K_csi1 = len(ack_bits), len(csi1_bits)
+    K_ack, K_csi1, K_csi2 = len(ack_bits), len(csi1_bits), len(csi2_bits)
     enc_ack = uci_encode(ack_bits, info["nof_harq_ack_bits"], qm) if K_ack else np.zeros(0, np.uint8)
     enc_csi1 = uci_encode(csi1_bits, info["nof_csi_part1_bits"], qm) if K_csi1 else np.zeros(0, np.uint8)
+    enc_csi2 = (uci_encode(np.asarray(csi2_bits, np.uint8), info["nof_csi_part2_bits"], qm) if K_csi2
+                else np.zeros(0, np.uint8))
     c_init = (pdu["rnti"] << 15) + pdu["n_id"]
     args = (qm, L, pdu["rb_count"], pdu["start_symbol_index"], pdu["nof_symbols"], info["nof_harq_ack_rvd"], False,
             pdu["dmrs_symbol_mask"], pdu["nof_cdm_groups_without_data"], K_ack, info["nof_harq_ack_bits"], K_csi1,
-            info["nof_csi_part1_bits"], 0)
-    src = [None, None, None]
+            info["nof_csi_part1_bits"])
+    src = [None, None, None, None]
     for k in range(3):
         code = (((np.arange(nre) >> (7 * k)) & 0x7F) + 1).astype(np.int8)
-        streams = ref_ulsch_demultiplex(np.repeat(code, bpre), *args)
+        if K_csi2:
+            streams = ref_ulsch_demultiplex2(np.repeat(code, bpre), *args, K_csi2, info["nof_csi_part2_bits"], 0)
+        else:
+            streams = ref_ulsch_demultiplex(np.repeat(code, bpre), *args, 0) + (np.zeros(0, np.int8),)
         for i, st in enumerate(streams):
-            v = (np.abs(st.astype(np.int32)) - 1).clip(min=0) << (7 * k)
+            a = np.abs(st.astype(np.int64)) - 1  # -1: a zeroed LLR (a RE a 1/2-bit HARQ-ACK punctures)
+            v = np.where(a < 0, -(1 << 40), a << (7 * k))
             src[i] = v if src[i] is None else src[i] + v
     out = np.zeros(nof_cw_bits, np.uint8)
     pos = np.arange(bpre)
     # UL-SCH REs (the zero LLRs of the demultiplexer's SCH stream are the REs an ACK of <= 2 bits punctures)
     sch_src = src[0].reshape(-1, bpre)[:, 0]
     for j, r in enumerate(sch_src):
-        out[r * bpre + pos] = sch_cw[j * bpre + pos]
-    for s_i, enc in ((1, enc_ack), (2, enc_csi1)):
+        if r >= 0:
+            out[r * bpre + pos] = sch_cw[j * bpre + pos]
+    # CSI part 2 first: where a 1/2-bit HARQ-ACK shares a reserved RE with it, the HARQ-ACK is what is sent
+    for s_i, enc in ((3, enc_csi2), (1, enc_ack), (2, enc_csi1)):
         if enc.size:
             for j, r in enumerate(src[s_i].reshape(-1, bpre)[:, 0]):
-                out[r * bpre + pos] = enc[j * bpre + pos]
+                if r >= 0:
+                    out[r * bpre + pos] = enc[j * bpre + pos]
     # scrambling with placeholders (TS 38.211 6.3.1.1), expressed as the bits a plain scrambler receives
     c = ref_prbs(c_init, nof_cw_bits)
     scr = np.zeros(nof_cw_bits, np.uint8)

@@ -121,6 +121,11 @@ public:
     ++nof_uci;
     harq_ack_status = static_cast<int>(uci.harq_ack.status);
     csi1_status     = static_cast<int>(uci.csi_part1.status);
+    csi2_status     = static_cast<int>(uci.csi_part2.status);
+    csi2.resize(uci.csi_part2.payload.size());
+    for (size_t i = 0; i != csi2.size(); ++i) {
+      csi2[i] = uci.csi_part2.payload.test(i) ? 1 : 0;
+    }
     harq_ack.resize(uci.harq_ack.payload.size());
     for (size_t i = 0; i != harq_ack.size(); ++i) {
       harq_ack[i] = uci.harq_ack.payload.test(i) ? 1 : 0;
@@ -138,8 +143,8 @@ public:
   pusch_processor_result_data result;
   bool                        done    = false;
   unsigned                    nof_uci = 0;
-  int                         harq_ack_status = 0, csi1_status = 0;
-  std::vector<uint8_t>        harq_ack, csi1;
+  int                         harq_ack_status = 0, csi1_status = 0, csi2_status = 0;
+  std::vector<uint8_t>        harq_ack, csi1, csi2;
 };
 
 } // namespace
@@ -230,7 +235,31 @@ int srs_ref::pusch_demodulate_with(std::unique_ptr<channel_equalizer> eq_impl,
   return static_cast<int>(buf.nof_blocks);
 }
 
+// CSI part 2 of the next srs_ref_pusch_process call (test glue: the call's argument list stays as it is): the
+// uci_part2_size_description as flat uint16 words [nof_entries, then per entry nof_parameters, offset0, width0,
+// offset1, width1, map_size, map[16]] and its beta offset; the decoded payload and status of that call.
+std::vector<uint16_t> g_part2_descr;
+float                 g_part2_beta = 5.0F;
+std::vector<uint8_t>  g_part2_out;
+int                   g_part2_status = 0;
+
 extern "C" {
+
+void srs_ref_pusch_set_csi_part2(const uint16_t* descr, unsigned nof_words, float beta)
+{
+  g_part2_descr.assign(descr, descr + nof_words);
+  g_part2_beta = beta;
+}
+
+// the last call's CSI part 2 payload (one bit per byte) into out[max_bits]; returns its size, status in *status
+int srs_ref_pusch_get_csi_part2(uint8_t* out, unsigned max_bits, int* status)
+{
+  *status = g_part2_status;
+  for (size_t i = 0; i != g_part2_out.size() && i < max_bits; ++i) {
+    out[i] = g_part2_out[i];
+  }
+  return static_cast<int>(g_part2_out.size());
+}
 
 // pusch_demodulator::demodulate (pusch_demodulator_impl.cpp:203-445) of one grid [P][14][nsubc]
 // with channel estimates [P][L][14][nsubc] (cbf16 as uint32) and per-port noise variances.
@@ -339,7 +368,20 @@ int srs_ref_pusch_process(const uint32_t* grid,
   pdu.uci.alpha_scaling         = alpha_scaling;
   pdu.uci.beta_offset_harq_ack  = beta_harq_ack;
   pdu.uci.beta_offset_csi_part1 = beta_csi_part1;
-  pdu.uci.beta_offset_csi_part2 = 5.0;
+  pdu.uci.beta_offset_csi_part2 = g_part2_beta;
+  if (!g_part2_descr.empty()) {
+    const uint16_t* w = g_part2_descr.data();
+    for (unsigned e = 0; e != w[0]; ++e) {
+      const uint16_t*                    x  = w + 1 + e * 22;
+      uci_part2_size_description::entry& en = pdu.uci.csi_part2_size.entries.emplace_back();
+      for (unsigned q = 0; q != x[0]; ++q) {
+        en.parameters.push_back(uci_part2_size_description::parameter{x[1 + 2 * q], static_cast<uint8_t>(x[2 + 2 * q])});
+      }
+      for (unsigned m = 0; m != x[5]; ++m) {
+        en.map.push_back(x[6 + m]);
+      }
+    }
+  }
   pdu.uci.nof_harq_ack          = nof_harq_ack;
   pdu.uci.nof_csi_part1         = nof_csi_part1;
   pdu.n_id                      = n_id;
@@ -365,6 +407,10 @@ int srs_ref_pusch_process(const uint32_t* grid,
   result_notifier  notifier;
   unique_rx_buffer buf(*static_cast<ref_rx_buffer*>(rx_buffer));
   bundle->proc->process(span<uint8_t>(tb, tb_bytes), std::move(buf), notifier, reader, pdu);
+  g_part2_descr.clear();
+  g_part2_beta   = 5.0F;
+  g_part2_out    = notifier.csi2;
+  g_part2_status = notifier.csi2_status;
   if (!notifier.done) {
     return -1;
   }

@@ -89,7 +89,10 @@ from .pusch_processor import (  # noqa: F401
     PuschSlotPdu,
     PuschProcessorPlan,
     PuschProcessorResult,
+    UciPart2SizeDescription,
     make_pdu,
+    uci_part2_description,
+    uci_part2_get_size,
 )
 
 from .sch import (  # noqa: F401

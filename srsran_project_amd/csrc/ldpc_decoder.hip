@@ -473,7 +473,10 @@ constexpr int waves_per_simd()
 // kernel, which may spread its 384 rows over 8 waves of 48 (lanes 48-63 then
 // duplicate rows 32-47: identical values to identical addresses), so that two
 // workgroups put exactly 2 + 2 waves on every SIMD instead of 2/2/1/1 + 1/1/2/2.
-constexpr int Z384_CHECKS_PER_WAVE = 48;
+#ifndef Z384_CPW
+#define Z384_CPW 48
+#endif
+constexpr int Z384_CHECKS_PER_WAVE = Z384_CPW;
 template <int ZC>
 constexpr int checks_per_wave()
 {

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -70,10 +71,27 @@ struct srs_amd_pusch_processor_plan {
   srs_amd_ulsch_info           info{};
   srs_amd_ulsch_demux_plan*    demux_plan = nullptr;
   uint32_t                     cw_bits    = 0;
+  // CSI part 2 (its size known only once CSI part 1 is decoded): the multiplexing / demultiplexing / UL-SCH
+  // configurations to recompute, and their results per CSI part 2 size (filled on first use)
+  bool                         csi2       = false;
+  uint32_t                     max_csi2   = 0; // largest size the description allows
+  srs_amd_ulsch_config         ucfg{};
+  srs_amd_ulsch_demux_config   dxcfg{};
+  uint32_t                     nref       = 0;
+  struct part2_geometry {
+    srs_amd_ulsch_info        info{};
+    srs_amd_ulsch_demux_plan* demux = nullptr;
+    srs_amd_sch_plan          sch{};
+  };
+  mutable std::map<uint32_t, part2_geometry> part2;
+  mutable std::mutex                         part2_mtx;
   ~srs_amd_pusch_processor_plan()
   {
     srs_amd_pusch_demod_plan_destroy(demod_plan);
     srs_amd_ulsch_demux_plan_destroy(demux_plan);
+    for (auto& kv : part2) {
+      srs_amd_ulsch_demux_plan_destroy(kv.second.demux);
+    }
   }
 };
 
@@ -101,6 +119,51 @@ float dmrs_scaling(uint32_t nof_cdm_groups_without_data)
   static const float beta_dmrs_db[4] = {NAN, 0.0F, -3.0F, -4.77F};
   const float        v               = -beta_dmrs_db[nof_cdm_groups_without_data];
   return std::pow(10.0F, v / 20.0F);
+}
+
+// The multiplexing geometry, demultiplexer plan and UL-SCH plan of `pl` with n2 CSI part 2 bits
+// (pusch_processor_impl.cpp:73-103: get_ulsch_information again, set_csi_part2, set_nof_softbits), cached per size.
+int plan_part2(srs_amd_pusch_processor*                                    proc,
+               const srs_amd_pusch_processor_plan*                         pl,
+               uint32_t                                                    n2,
+               const srs_amd_pusch_processor_plan::part2_geometry**        out)
+{
+  std::lock_guard<std::mutex> lock(pl->part2_mtx);
+  auto                        it = pl->part2.find(n2);
+  if (it != pl->part2.end()) {
+    *out = &it->second;
+    return SRS_AMD_OK;
+  }
+  srs_amd_pusch_processor_plan::part2_geometry g;
+  srs_amd_ulsch_config                         uc = pl->ucfg;
+  uc.nof_csi_part2_bits                           = n2;
+  int rc                                          = srs_amd_ulsch_information(&uc, &g.info);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  srs_amd_ulsch_demux_config dx = pl->dxcfg;
+  dx.nof_csi_part2_bits         = n2;
+  dx.nof_enc_csi_part2_bits     = g.info.nof_csi_part2_bits;
+  uint32_t total = 0, sch_bits = 0;
+  rc             = srs_amd_ulsch_demux_plan_create(proc->demux, &dx, &g.demux, &total, &sch_bits);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  const uint32_t qm_bits = pl->pdu.modulation < 2 ? 1u : static_cast<uint32_t>(pl->pdu.modulation);
+  if (total != pl->cw_bits || sch_bits != g.info.nof_ul_sch_bits) {
+    srs_amd_ulsch_demux_plan_destroy(g.demux);
+    return fail(SRS_AMD_EINVAL, "CSI part 2 multiplexing geometry mismatch (%u / %u UL-SCH bits).", sch_bits,
+                g.info.nof_ul_sch_bits);
+  }
+  rc = srs_amd_sch_plan_compute(&g.sch, pl->pdu.tbs, pl->pdu.base_graph, pl->pdu.rv,
+                                static_cast<uint32_t>(pl->pdu.modulation), pl->nref, pl->pdu.nof_tx_layers,
+                                sch_bits / qm_bits);
+  if (rc != SRS_AMD_OK) {
+    srs_amd_ulsch_demux_plan_destroy(g.demux);
+    return rc;
+  }
+  *out = &pl->part2.emplace(n2, g).first->second;
+  return SRS_AMD_OK;
 }
 
 } // namespace
@@ -264,6 +327,30 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
   pl->cw_bits             = pl->nof_re * pdu->nof_tx_layers * qm_bits;
   uint32_t       sch_bits = pl->cw_bits;
   pl->uci                 = pdu->nof_harq_ack != 0 || pdu->nof_csi_part1 != 0;
+  pl->csi2                = pdu->nof_csi_part1 != 0 && pdu->csi_part2_size.nof_entries != 0;
+  if (pdu->csi_part2_size.nof_entries > 2) {
+    delete pl;
+    return fail(SRS_AMD_EINVAL, "At most two CSI part 2 size entries.");
+  }
+  for (uint32_t e = 0; e < pdu->csi_part2_size.nof_entries && pl->csi2; ++e) {
+    const srs_amd_uci_part2_entry& en = pdu->csi_part2_size.entries[e];
+    uint32_t                       w  = 0, mx = 0;
+    for (uint32_t q = 0; q < en.nof_parameters && q < 2; ++q) {
+      w += en.parameters[q].width;
+      if (static_cast<uint32_t>(en.parameters[q].offset) + en.parameters[q].width > pdu->nof_csi_part1) {
+        delete pl;
+        return fail(SRS_AMD_EINVAL, "CSI part 2 size parameter beyond the CSI part 1 payload.");
+      }
+    }
+    if (en.nof_parameters > 2 || w > 4 || en.map_size != (1u << w)) {
+      delete pl;
+      return fail(SRS_AMD_EINVAL, "Invalid CSI part 2 size entry (parameters, widths or map size).");
+    }
+    for (uint32_t m = 0; m < en.map_size; ++m) {
+      mx = std::max<uint32_t>(mx, en.map[m]);
+    }
+    pl->max_csi2 += mx;
+  }
   if (pl->uci) {
     srs_amd_ulsch_config uc{};
     uc.tbs                         = pdu->tbs;
@@ -281,7 +368,9 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
     uc.dmrs_symbol_mask            = pdu->dmrs_symbol_mask;
     uc.nof_cdm_groups_without_data = ncdm;
     uc.nof_layers                  = pdu->nof_tx_layers;
+    uc.beta_offset_csi_part2       = pdu->beta_offset_csi_part2;
     rc                             = srs_amd_ulsch_information(&uc, &pl->info);
+    pl->ucfg                       = uc;
     srs_amd_ulsch_demux_config dx{};
     dx.modulation                  = pdu->modulation;
     dx.nof_layers                  = pdu->nof_tx_layers;
@@ -297,6 +386,7 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
     dx.nof_csi_part1_bits          = pdu->nof_csi_part1;
     dx.nof_enc_csi_part1_bits      = pl->info.nof_csi_part1_bits;
     dx.c_init                      = (pdu->rnti << 15) + pdu->n_id;
+    pl->dxcfg                      = dx;
     uint32_t total                 = 0;
     if (rc == SRS_AMD_OK) {
       rc = srs_amd_ulsch_demux_plan_create(proc->demux, &dx, &pl->demux_plan, &total, &sch_bits);
@@ -313,8 +403,9 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
   // decoder configuration (pusch_processor_impl.cpp:322-347): the UL-SCH's share of the codeword
   const uint32_t C       = nof_codeblocks(pdu->tbs, pdu->base_graph);
   const uint32_t tbs_lbrm = pdu->tbs_lbrm_bytes ? pdu->tbs_lbrm_bytes : 159749u; // tbs_lbrm_default
+  pl->nref = compute_N_ref(tbs_lbrm, C);
   rc = srs_amd_sch_plan_compute(&pl->sch, pdu->tbs, pdu->base_graph, pdu->rv, static_cast<uint32_t>(pdu->modulation),
-                                compute_N_ref(tbs_lbrm, C), pdu->nof_tx_layers, sch_bits / qm_bits);
+                                pl->nref, pdu->nof_tx_layers, sch_bits / qm_bits);
   if (rc != SRS_AMD_OK) {
     delete pl;
     return rc;
@@ -398,20 +489,27 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   const uint64_t ack_e      = plan->info.nof_harq_ack_bits, csi1_e = plan->info.nof_csi_part1_bits;
   const uint64_t uci_stride = align_up(ack_e + csi1_e, 64);
   const uint32_t K_ack = plan->pdu.nof_harq_ack, K_csi1 = plan->pdu.nof_csi_part1;
+  // payload rows: HARQ-ACK | CSI part 1 | CSI part 2 (largest size); statuses [grid][4] (pusch_result_args)
+  const uint64_t pay_stride = align_up(K_ack + K_csi1 + plan->max_csi2, 64);
+  // CSI part 2 LLR rows: the largest encoded size any CSI part 2 size can take is below the codeword length
+  const uint64_t csi2_stride = plan->csi2 ? cw_stride : 0;
   if (e == hipSuccess && uci) {
     e = proc->cw_llrs.ensure(nof_grids * cw_stride);
   }
   if (e == hipSuccess && uci) {
-    e = proc->uci_llrs.ensure(nof_grids * uci_stride);
+    e = proc->uci_llrs.ensure(nof_grids * (uci_stride + csi2_stride));
   }
   if (e == hipSuccess && uci) {
-    e = proc->uci_payload.ensure(nof_grids * align_up(K_ack + K_csi1, 64));
+    e = proc->uci_payload.ensure(nof_grids * pay_stride);
   }
   if (e == hipSuccess && uci) {
-    e = proc->uci_status.ensure(static_cast<size_t>(nof_grids) * 2 * sizeof(int32_t));
+    e = proc->uci_status.ensure(static_cast<size_t>(nof_grids) * 4 * sizeof(int32_t));
   }
   if (e == hipSuccess) {
     e = proc->order.begin(s);
+  }
+  if (e == hipSuccess && uci) { // after begin: a previous call on another stream may still read the statuses
+    e = hipMemsetAsync(proc->uci_status.ptr, 0, static_cast<size_t>(nof_grids) * 4 * sizeof(int32_t), s);
   }
   if (e != hipSuccess) {
     return hip_fail(e, "PUSCH processor scratch");
@@ -449,21 +547,95 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
     const bool out = io != nullptr && io->d_harq_ack != nullptr;
     rc = srs_amd_uci_decode_batch(proc->uci, uci_rows, uci_stride, static_cast<uint32_t>(ack_e), K_ack,
                                   plan->pdu.modulation, out ? io->d_harq_ack : proc->uci_payload.as<uint8_t>(),
-                                  out ? io->harq_ack_stride : align_up(K_ack + K_csi1, 64),
-                                  proc->uci_status.as<int32_t>(), 2 * sizeof(int32_t), nof_grids, stream);
+                                  out ? io->harq_ack_stride : pay_stride, proc->uci_status.as<int32_t>(),
+                                  4 * sizeof(int32_t), nof_grids, stream);
   }
   if (rc == SRS_AMD_OK && uci && K_csi1 != 0) {
     const bool out = io != nullptr && io->d_csi_part1 != nullptr;
     rc = srs_amd_uci_decode_batch(proc->uci, uci_rows + ack_e, uci_stride, static_cast<uint32_t>(csi1_e), K_csi1,
                                   plan->pdu.modulation,
                                   out ? io->d_csi_part1 : proc->uci_payload.as<uint8_t>() + K_ack,
-                                  out ? io->csi_part1_stride : align_up(K_ack + K_csi1, 64),
-                                  proc->uci_status.as<int32_t>() + 1, 2 * sizeof(int32_t), nof_grids, stream);
+                                  out ? io->csi_part1_stride : pay_stride, proc->uci_status.as<int32_t>() + 1,
+                                  4 * sizeof(int32_t), nof_grids, stream);
   }
-  if (rc == SRS_AMD_OK) {
+  // CSI part 2 sizes from the decoded CSI part 1 (one readback), grids without CSI part 2 keep the plan's geometry
+  std::vector<uint32_t> n2(nof_grids, 0);
+  if (rc == SRS_AMD_OK && plan->csi2) {
+    const bool     out1 = io != nullptr && io->d_csi_part1 != nullptr;
+    const uint8_t* p1   = out1 ? io->d_csi_part1 : proc->uci_payload.as<uint8_t>() + K_ack;
+    const uint64_t p1s  = out1 ? io->csi_part1_stride : pay_stride;
+    std::vector<int32_t> st1(static_cast<size_t>(nof_grids) * 4);
+    std::vector<uint8_t> part1(static_cast<size_t>(nof_grids) * K_csi1);
+    e = hipMemcpyAsync(st1.data(), proc->uci_status.ptr, st1.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) {
+      e = hipMemcpy2DAsync(part1.data(), K_csi1, p1, p1s, K_csi1, nof_grids, hipMemcpyDeviceToHost, s);
+    }
+    if (e == hipSuccess) {
+      e = hipStreamSynchronize(s);
+    }
+    if (e != hipSuccess) {
+      return hip_fail(e, "CSI part 1 readback");
+    }
+    for (uint32_t g = 0; g < nof_grids && rc == SRS_AMD_OK; ++g) {
+      if (st1[4 * g + 1] == SRS_AMD_UCI_VALID) { // on_csi_part1 feeds back only a valid CSI part 1
+        const int32_t v = srs_amd_uci_part2_get_size(part1.data() + static_cast<size_t>(g) * K_csi1, K_csi1,
+                                                      &plan->pdu.csi_part2_size);
+        rc              = v < 0 ? fail(SRS_AMD_EINVAL, "CSI part 2 size description does not fit CSI part 1") : rc;
+        n2[g]           = v < 0 ? 0u : static_cast<uint32_t>(v);
+      }
+    }
+  }
+  const bool any2 = std::any_of(n2.begin(), n2.end(), [](uint32_t v) { return v != 0; });
+  if (rc == SRS_AMD_OK && !any2) {
     rc = srs_amd_pusch_decode_batch(proc->dec, &plan->sch, &plan->dec_cfg, d_tbs, tb_stride,
                                     proc->dec_results.as<srs_amd_pusch_decoder_result>(), llrs, llr_stride, d_soft,
                                     nullptr, nof_grids, stream);
+  }
+  // grid by grid when some CSI part 2 is present: each size has its own UL-SCH geometry
+  for (uint32_t g = 0; g < nof_grids && rc == SRS_AMD_OK && any2; ++g) {
+    const srs_amd_sch_plan* sch = &plan->sch;
+    int8_t*                 row = llrs + static_cast<uint64_t>(g) * llr_stride;
+    if (n2[g] != 0) {
+      const srs_amd_pusch_processor_plan::part2_geometry* geo = nullptr;
+      rc = plan_part2(proc, plan, n2[g], &geo);
+      if (rc != SRS_AMD_OK) {
+        break;
+      }
+      sch                = &geo->sch;
+      int8_t*        c2  = uci_rows + static_cast<uint64_t>(nof_grids) * uci_stride + g * csi2_stride;
+      const uint64_t e2  = geo->info.nof_csi_part2_bits;
+      int8_t*        u1  = uci_rows + static_cast<uint64_t>(g) * uci_stride;
+      rc = srs_amd_ulsch_demultiplex_csi2_batch(proc->demux, geo->demux, dem_rows + g * cw_stride, cw_stride, row,
+                                                llr_stride, u1, uci_stride, u1 + ack_e, uci_stride, c2, csi2_stride, 1,
+                                                stream);
+      const bool out2 = io != nullptr && io->d_csi_part2 != nullptr;
+      if (rc == SRS_AMD_OK && out2 && io->csi_part2_stride < n2[g]) {
+        rc = fail(SRS_AMD_EINVAL, "CSI part 2 payload stride too small (%u bits)", n2[g]);
+      }
+      if (rc == SRS_AMD_OK) {
+        rc = srs_amd_uci_decode_batch(proc->uci, c2, csi2_stride, static_cast<uint32_t>(e2), n2[g],
+                                      plan->pdu.modulation,
+                                      out2 ? io->d_csi_part2 + static_cast<uint64_t>(g) * io->csi_part2_stride
+                                           : proc->uci_payload.as<uint8_t>() + g * pay_stride + K_ack + K_csi1,
+                                      pay_stride, proc->uci_status.as<int32_t>() + 4 * g + 2, 4 * sizeof(int32_t), 1,
+                                      stream);
+      }
+      if (rc == SRS_AMD_OK) {
+        const int32_t nb = static_cast<int32_t>(n2[g]);
+        e  = hipMemcpyAsync(proc->uci_status.as<int32_t>() + 4 * g + 3, &nb, sizeof(nb), hipMemcpyHostToDevice, s);
+        rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "CSI part 2 size upload");
+        if (rc == SRS_AMD_OK) {
+          e  = hipStreamSynchronize(s); // nb lives on this stack frame
+          rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "CSI part 2 size upload");
+        }
+      }
+    }
+    if (rc == SRS_AMD_OK) {
+      rc = srs_amd_pusch_decode_batch(proc->dec, sch, &plan->dec_cfg, d_tbs + static_cast<uint64_t>(g) * tb_stride,
+                                      tb_stride, proc->dec_results.as<srs_amd_pusch_decoder_result>() + g, row,
+                                      llr_stride, d_soft ? d_soft + g * plan->soft_bytes : nullptr, nullptr, 1,
+                                      stream);
+    }
   }
   if (rc != SRS_AMD_OK) {
     return rc;
@@ -476,7 +648,7 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   a.nof_ports   = P;
   if (uci) {
     a.uci_status = proc->uci_status.as<int32_t>();
-    a.uci_mask   = (K_ack != 0 ? 1 : 0) | (K_csi1 != 0 ? 2 : 0);
+    a.uci_mask   = (K_ack != 0 ? 1 : 0) | (K_csi1 != 0 ? 2 : 0) | (plan->csi2 ? 4 : 0);
   }
   e             = launch_pusch_result(a, s);
   if (e == hipSuccess) {

@@ -19,7 +19,8 @@ struct pusch_result_args {
   // slot form: PDU g has port_counts[g] ports, its stats at stats + g * stats_stride
   const uint32_t*                     port_counts  = nullptr;
   uint32_t                            stats_stride = 0;
-  // UCI on PUSCH: statuses [grid][2] (HARQ-ACK, CSI part 1) of the fields set in uci_mask (bit 0, bit 1)
+  // UCI on PUSCH: [grid][4] = HARQ-ACK, CSI part 1, CSI part 2 statuses of the fields set in uci_mask (bits 0-2),
+  // CSI part 2 payload bits
   const int32_t*                      uci_status   = nullptr;
   uint32_t                            uci_mask     = 0;
 };

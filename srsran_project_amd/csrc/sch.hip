@@ -144,25 +144,14 @@ __global__ __launch_bounds__(SEGCRC_THREADS) void segment_crc_kernel(segment_arg
     }
   }
   const uint32_t crc = crc_wave_xor(contrib);
-  // the CRC bits [n, n + 24) that land in this lane's bytes
-#pragma unroll
-  for (uint32_t k = 0; k < SEGCRC_PER; ++k) {
-    const uint32_t j = b0 + k;
-    if (8 * j + 8 > n && 8 * j < n + 24) {
-#pragma unroll
-      for (uint32_t b = 0; b < 8; ++b) {
-        const uint32_t pos = 8 * j + b;
-        if (pos >= n && pos < n + 24) {
-          const uint32_t mask = 0x80u >> b;
-          v[k]                = (v[k] & ~mask) | (((crc >> (23 - (pos - n))) & 1u) ? mask : 0u);
-        }
-      }
-    }
-  }
   __syncthreads(); // every lane has read its TB bytes from s_io
 #pragma unroll
   for (uint32_t k = 0; k < SEGCRC_PER; ++k) {
     s_io[b0 + k] = static_cast<uint8_t>(v[k]);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    attach_crc_bits(s_io, n, 24, crc); // the CRC bits [n, n + 24): at most four LDS bytes
   }
   __syncthreads();
   uint8_t* m = a.msgs + static_cast<size_t>(row) * a.msg_stride;

@@ -211,4 +211,38 @@ int srs_amd_uci_decode(srs_amd_uci_decoder* dec, uint8_t* message, uint32_t K, c
   return e == hipSuccess ? status : hip_fail(e, "UCI decoder download");
 }
 
+int32_t srs_amd_uci_part2_get_size(const uint8_t*                            part1,
+                                   uint32_t                                  nof_part1_bits,
+                                   const srs_amd_uci_part2_size_description* descr)
+{
+  if (descr == nullptr || descr->nof_entries > 2 || (nof_part1_bits != 0 && part1 == nullptr)) {
+    return -1;
+  }
+  uint32_t result = 0;
+  for (uint32_t e = 0; e < descr->nof_entries; ++e) {
+    const srs_amd_uci_part2_entry& en = descr->entries[e];
+    if (en.nof_parameters > 2) {
+      return -1;
+    }
+    uint32_t index = 0, bits = 0;
+    for (uint32_t q = 0; q < en.nof_parameters; ++q) {
+      const srs_amd_uci_part2_parameter& prm = en.parameters[q];
+      if (static_cast<uint32_t>(prm.offset) + prm.width > nof_part1_bits) {
+        return -1;
+      }
+      uint32_t value = 0; // the field's first bit is its most significant (extract_parameter, :28-51)
+      for (uint32_t b = 0; b < prm.width; ++b) {
+        value = (value << 1) | (part1[prm.offset + b] & 1u);
+      }
+      index = (index << prm.width) | value;
+      bits += prm.width;
+    }
+    if (bits > 4 || en.map_size != (1u << bits) || index >= en.map_size) {
+      return -1;
+    }
+    result += en.map[index];
+  }
+  return static_cast<int32_t>(result);
+}
+
 } // extern "C"

@@ -32,14 +32,11 @@ __global__ __launch_bounds__(DMX_THREADS) void ulsch_demux_kernel(demux_args a)
   for (uint32_t b = 0; b < a.bpre; ++b) {
     v[b] = in[b];
   }
-  if (u != DMX_NONE) {
-    const uint32_t kind = u >> DMX_KIND_SHIFT;
-    const uint32_t ph   = kind == DMX_ACK ? a.ack_ph : a.csi1_ph;
-    int8_t*        out  = kind == DMX_ACK ? a.ack + row * a.ack_stride : a.csi1 + row * a.csi1_stride;
-    out += static_cast<uint64_t>(u & DMX_INDEX_MASK) * a.bpre;
-    const uint32_t n0 = re * a.bpre; // codeword bit of the RE's first LLR
+  const uint32_t n0 = re * a.bpre; // codeword bit of the RE's first LLR
+  // one UCI stream's copy of the RE, the placeholder scrambling of a 1/2-bit payload reverted
+  auto put_uci = [&](int8_t* out, uint32_t ph, bool zero) {
     for (uint32_t b = 0; b < a.bpre; ++b) {
-      int8_t x = v[b];
+      int8_t x = zero ? int8_t(0) : v[b];
       if (ph != 0 && a.qm > 1) {
         const uint32_t k = b % a.qm; // bit of the modulation symbol
         if (k >= 2) {
@@ -51,6 +48,19 @@ __global__ __launch_bounds__(DMX_THREADS) void ulsch_demux_kernel(demux_args a)
         }
       }
       out[b] = x;
+    }
+  };
+  if (u != DMX_NONE) {
+    const uint32_t kind = u >> DMX_KIND_SHIFT;
+    int8_t*        out  = kind == DMX_ACK ? a.ack + row * a.ack_stride : a.csi1 + row * a.csi1_stride;
+    put_uci(out + static_cast<uint64_t>(u & DMX_INDEX_MASK) * a.bpre, kind == DMX_ACK ? a.ack_ph : a.csi1_ph, false);
+  }
+  if (a.csi2_map != nullptr) {
+    // CSI part 2 after HARQ-ACK: a RE it shares with a 1/2-bit HARQ-ACK was zeroed by the HARQ-ACK extraction
+    const uint32_t c2 = a.csi2_map[re];
+    if (c2 != DMX_NONE) {
+      put_uci(a.csi2 + row * a.csi2_stride + static_cast<uint64_t>(c2 & ~DMX_ZERO) * a.bpre, a.csi2_ph,
+              (c2 & DMX_ZERO) != 0);
     }
   }
   if (s != DMX_NONE) {

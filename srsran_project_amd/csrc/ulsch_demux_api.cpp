@@ -1,7 +1,7 @@
 // ulsch_demux_api.cpp -- C-ABI of the MI355X UL-SCH demultiplexer (include/srsran_amd/ulsch_demux.h): the host
-// resolves the placement of ulsch_demultiplex_impl (ulsch_demultiplex_impl.cpp:285-444, one OFDM symbol at a
-// time: reserved HARQ-ACK REs, HARQ-ACK > 2 bits, CSI part 1, UL-SCH, HARQ-ACK <= 2 bits in the reserved REs,
-// each taken every d-th RE of its candidate set) into per-RE tables once per plan; the device pass
+// resolves the placement of ulsch_demultiplex_impl (ulsch_demultiplex_impl.cpp:285-472, one OFDM symbol at a
+// time: reserved HARQ-ACK REs, HARQ-ACK > 2 bits, CSI part 1, CSI part 2, UL-SCH, HARQ-ACK <= 2 bits in the
+// reserved REs, each taken every d-th RE of its candidate set) into per-RE tables once per plan; the device pass
 // (ulsch_demux.hip) moves the LLRs.
 #include "srsran_amd/ulsch_demux.h"
 
@@ -106,7 +106,11 @@ int srs_amd::build_demux_placement(const srs_amd_ulsch_demux_config& c, demux_pl
   const uint32_t nof_re_dmrs =
       (12 - c.nof_cdm_groups_without_data * (c.dmrs_type == 1 ? 6u : 4u)) * c.nof_prb; // get_..._nof_re_prb_dmrs
   out = demux_placement{};
-  uint32_t m_rvd = 0, m_ack = 0, m_csi1 = 0;
+  uint32_t m_rvd = 0, m_ack = 0, m_csi1 = 0, m_csi2 = 0;
+  // CSI part 2 is configured (set_csi_part2) once CSI part 1 has been decoded, i.e. while demultiplexing the
+  // OFDM symbol in which the CSI part 1 REs end (ulsch_demultiplex_impl.cpp:241-251): it starts in that symbol
+  const bool     has_csi2  = c.nof_csi_part2_bits != 0 && c.nof_csi_part1_bits != 0;
+  bool           csi2_live = false;
   for (uint32_t l = c.start_symbol_index; l < end; ++l) {
     const bool     dmrs = (mask >> l) & 1u;
     const uint32_t M    = dmrs ? nof_re_dmrs : c.nof_prb * 12;
@@ -154,6 +158,22 @@ int srs_amd::build_demux_placement(const srs_amd_ulsch_demux_config& c, demux_pl
       }
       m_csi1 += m * bpre;
     }
+    // step 3bis: CSI part 2 (configure_csi_part2_current_ofdm_symbol, :450-472), from the symbol where CSI part 1
+    // completes, every d-th of the remaining UCI REs (reserved REs included)
+    csi2_live          = csi2_live || (has_csi2 && m_csi1 == c.nof_enc_csi_part1_bits);
+    re_set         csi2(M, 0);
+    const uint32_t M_uci2   = count(uci);
+    const uint32_t rem_csi2 = csi2_live ? (c.nof_enc_csi_part2_bits - m_csi2) / bpre : 0u;
+    if (l >= l1_csi && M_uci2 > 0 && rem_csi2 > 0) {
+      const uint32_t d = rem_csi2 < M_uci2 ? M_uci2 / rem_csi2 : 1;
+      const uint32_t m = rem_csi2 < M_uci2 ? rem_csi2 : M_uci2;
+      csi2             = select(uci, d, m);
+      for (uint32_t i = 0; i < M; ++i) {
+        ulsch[i] &= !csi2[i];
+        uci[i] &= !csi2[i];
+      }
+      m_csi2 += m * bpre;
+    }
     // step 5: HARQ-ACK of one or two bits in the reserved REs (they stay UL-SCH REs, zeroed there)
     if (M_rvd > 0 && c.nof_harq_ack_bits <= 2 && rem_ack > 0) {
       const uint32_t d = rem_ack < M_rvd ? M_rvd / rem_ack : 1;
@@ -171,15 +191,23 @@ int srs_amd::build_demux_placement(const srs_amd_ulsch_demux_config& c, demux_pl
       if (ulsch[i]) {
         s = out.nof_sch_re++ | ((ack[i] && c.nof_harq_ack_bits <= 2) ? DMX_ZERO : 0u);
       }
+      uint32_t v2 = DMX_NONE;
+      if (csi2[i]) {
+        v2 = out.nof_csi2_re++ | ((ack[i] && c.nof_harq_ack_bits <= 2) ? DMX_ZERO : 0u);
+      }
       out.sch_map.push_back(s);
       out.uci_map.push_back(u);
+      out.csi2_map.push_back(v2);
     }
   }
   out.nof_re = static_cast<uint32_t>(out.sch_map.size());
   if (out.nof_ack_re * bpre != (c.nof_harq_ack_bits ? c.nof_enc_harq_ack_bits : 0u) ||
-      out.nof_csi1_re * bpre != (c.nof_csi_part1_bits ? c.nof_enc_csi_part1_bits : 0u)) {
-    return fail(SRS_AMD_EINVAL, "The UCI does not fit the allocation (HARQ-ACK %u of %u bits, CSI part 1 %u of %u).",
-                out.nof_ack_re * bpre, c.nof_enc_harq_ack_bits, out.nof_csi1_re * bpre, c.nof_enc_csi_part1_bits);
+      out.nof_csi1_re * bpre != (c.nof_csi_part1_bits ? c.nof_enc_csi_part1_bits : 0u) ||
+      out.nof_csi2_re * bpre != (has_csi2 ? c.nof_enc_csi_part2_bits : 0u)) {
+    return fail(SRS_AMD_EINVAL,
+                "The UCI does not fit the allocation (HARQ-ACK %u of %u bits, CSI part 1 %u of %u, CSI part 2 %u of %u).",
+                out.nof_ack_re * bpre, c.nof_enc_harq_ack_bits, out.nof_csi1_re * bpre, c.nof_enc_csi_part1_bits,
+                out.nof_csi2_re * bpre, c.nof_enc_csi_part2_bits);
   }
   return SRS_AMD_OK;
 }
@@ -242,13 +270,17 @@ int srs_amd_ulsch_demux_plan_create(srs_amd_ulsch_demux*              demux,
   const uint32_t nwords   = cw_bits / 32 + 2;
   hipError_t     e        = hipSetDevice(demux->device);
   if (e == hipSuccess) {
-    e = hipMalloc(&p->d_maps, sizeof(uint32_t) * 2 * std::max(p->pl.nof_re, 1u));
+    e = hipMalloc(&p->d_maps, sizeof(uint32_t) * 3 * std::max(p->pl.nof_re, 1u));
   }
   if (e == hipSuccess && p->pl.nof_re != 0) {
     e = hipMemcpy(p->d_maps, p->pl.sch_map.data(), sizeof(uint32_t) * p->pl.nof_re, hipMemcpyHostToDevice);
   }
   if (e == hipSuccess && p->pl.nof_re != 0) {
     e = hipMemcpy(p->d_maps + p->pl.nof_re, p->pl.uci_map.data(), sizeof(uint32_t) * p->pl.nof_re,
+                  hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess && p->pl.nof_re != 0) {
+    e = hipMemcpy(p->d_maps + 2 * p->pl.nof_re, p->pl.csi2_map.data(), sizeof(uint32_t) * p->pl.nof_re,
                   hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) {
@@ -292,6 +324,25 @@ int srs_amd_ulsch_demultiplex_batch(srs_amd_ulsch_demux*            demux,
                                     uint32_t                        nof_cws,
                                     void*                           stream)
 {
+  return srs_amd_ulsch_demultiplex_csi2_batch(demux, plan, d_cws, cw_stride, d_sch, sch_stride, d_ack, ack_stride,
+                                              d_csi1, csi1_stride, nullptr, 0, nof_cws, stream);
+}
+
+int srs_amd_ulsch_demultiplex_csi2_batch(srs_amd_ulsch_demux*            demux,
+                                         const srs_amd_ulsch_demux_plan* plan,
+                                         const int8_t*                   d_cws,
+                                         uint64_t                        cw_stride,
+                                         int8_t*                         d_sch,
+                                         uint64_t                        sch_stride,
+                                         int8_t*                         d_ack,
+                                         uint64_t                        ack_stride,
+                                         int8_t*                         d_csi1,
+                                         uint64_t                        csi1_stride,
+                                         int8_t*                         d_csi2,
+                                         uint64_t                        csi2_stride,
+                                         uint32_t                        nof_cws,
+                                         void*                           stream)
+{
   if (demux == nullptr || plan == nullptr) {
     return fail(SRS_AMD_EINVAL, "null argument");
   }
@@ -300,12 +351,13 @@ int srs_amd_ulsch_demultiplex_batch(srs_amd_ulsch_demux*            demux,
   }
   const uint32_t bpre = bits_per_symbol(plan->cfg.modulation) * plan->cfg.nof_layers;
   if (d_cws == nullptr || (plan->pl.nof_sch_re && d_sch == nullptr) || (plan->pl.nof_ack_re && d_ack == nullptr) ||
-      (plan->pl.nof_csi1_re && d_csi1 == nullptr)) {
-    return fail(SRS_AMD_EINVAL, "null device buffer");
+      (plan->pl.nof_csi1_re && d_csi1 == nullptr) || (plan->pl.nof_csi2_re && d_csi2 == nullptr)) {
+    return fail(SRS_AMD_EINVAL, "null device buffer (a plan with CSI part 2 needs its rows)");
   }
   if (nof_cws > 1 && (cw_stride < uint64_t(plan->pl.nof_re) * bpre || sch_stride < uint64_t(plan->pl.nof_sch_re) * bpre ||
                       ack_stride < uint64_t(plan->pl.nof_ack_re) * bpre ||
-                      csi1_stride < uint64_t(plan->pl.nof_csi1_re) * bpre)) {
+                      csi1_stride < uint64_t(plan->pl.nof_csi1_re) * bpre ||
+                      csi2_stride < uint64_t(plan->pl.nof_csi2_re) * bpre)) {
     return fail(SRS_AMD_EINVAL, "stride too small");
   }
   demux_args a{};
@@ -325,6 +377,10 @@ int srs_amd_ulsch_demultiplex_batch(srs_amd_ulsch_demux*            demux,
   a.bpre        = bpre;
   a.ack_ph      = plan->cfg.nof_harq_ack_bits <= 2 ? plan->cfg.nof_harq_ack_bits : 0u;
   a.csi1_ph     = plan->cfg.nof_csi_part1_bits <= 2 ? plan->cfg.nof_csi_part1_bits : 0u;
+  a.csi2_map    = plan->pl.nof_csi2_re != 0 ? plan->d_maps + 2 * plan->pl.nof_re : nullptr;
+  a.csi2        = d_csi2;
+  a.csi2_stride = csi2_stride;
+  a.csi2_ph     = plan->cfg.nof_csi_part2_bits <= 2 ? plan->cfg.nof_csi_part2_bits : 0u;
   hipError_t e  = hipSetDevice(demux->device);
   if (e == hipSuccess) {
     e = launch_ulsch_demux(a, nof_cws, static_cast<hipStream_t>(stream));
@@ -339,6 +395,17 @@ int srs_amd_ulsch_demultiplex(srs_amd_ulsch_demux*            demux,
                               int8_t*                         ack,
                               int8_t*                         csi1)
 {
+  return srs_amd_ulsch_demultiplex_csi2(demux, plan, codeword, sch, ack, csi1, nullptr);
+}
+
+int srs_amd_ulsch_demultiplex_csi2(srs_amd_ulsch_demux*            demux,
+                                   const srs_amd_ulsch_demux_plan* plan,
+                                   const int8_t*                   codeword,
+                                   int8_t*                         sch,
+                                   int8_t*                         ack,
+                                   int8_t*                         csi1,
+                                   int8_t*                         csi2)
+{
   if (demux == nullptr || plan == nullptr || codeword == nullptr) {
     return fail(SRS_AMD_EINVAL, "null argument");
   }
@@ -347,15 +414,17 @@ int srs_amd_ulsch_demultiplex(srs_amd_ulsch_demux*            demux,
   const size_t   n_sch  = size_t(plan->pl.nof_sch_re) * bpre;
   const size_t   n_ack  = size_t(plan->pl.nof_ack_re) * bpre;
   const size_t   n_csi1 = size_t(plan->pl.nof_csi1_re) * bpre;
-  if ((n_sch && sch == nullptr) || (n_ack && ack == nullptr) || (n_csi1 && csi1 == nullptr)) {
+  const size_t   n_csi2 = size_t(plan->pl.nof_csi2_re) * bpre;
+  if ((n_sch && sch == nullptr) || (n_ack && ack == nullptr) || (n_csi1 && csi1 == nullptr) ||
+      (n_csi2 && csi2 == nullptr)) {
     return fail(SRS_AMD_EINVAL, "null output");
   }
   std::lock_guard<std::mutex> lock(demux->mtx);
   const size_t                o_sch = align_up(n_cw, 256), o_ack = o_sch + align_up(n_sch, 256),
-                o_csi1 = o_ack + align_up(n_ack, 256);
+                o_csi1 = o_ack + align_up(n_ack, 256), o_csi2 = o_csi1 + align_up(n_csi1, 256);
   hipError_t e         = hipSetDevice(demux->device);
   if (e == hipSuccess) {
-    e = demux->host_io.ensure(o_csi1 + n_csi1 + 256);
+    e = demux->host_io.ensure(o_csi2 + n_csi2 + 256);
   }
   auto* b = demux->host_io.as<int8_t>();
   if (e == hipSuccess && n_cw) {
@@ -364,8 +433,8 @@ int srs_amd_ulsch_demultiplex(srs_amd_ulsch_demux*            demux,
   if (e != hipSuccess) {
     return hip_fail(e, "UL-SCH demultiplexer upload");
   }
-  int rc = srs_amd_ulsch_demultiplex_batch(demux, plan, b, n_cw, b + o_sch, n_sch, b + o_ack, n_ack, b + o_csi1, n_csi1,
-                                           1, demux->stream);
+  int rc = srs_amd_ulsch_demultiplex_csi2_batch(demux, plan, b, n_cw, b + o_sch, n_sch, b + o_ack, n_ack, b + o_csi1,
+                                                n_csi1, b + o_csi2, n_csi2, 1, demux->stream);
   if (rc != SRS_AMD_OK) {
     (void)hipStreamSynchronize(demux->stream);
     return rc;
@@ -378,6 +447,9 @@ int srs_amd_ulsch_demultiplex(srs_amd_ulsch_demux*            demux,
   }
   if (e == hipSuccess && n_csi1) {
     e = hipMemcpyAsync(csi1, b + o_csi1, n_csi1, hipMemcpyDeviceToHost, demux->stream);
+  }
+  if (e == hipSuccess && n_csi2) {
+    e = hipMemcpyAsync(csi2, b + o_csi2, n_csi2, hipMemcpyDeviceToHost, demux->stream);
   }
   if (e == hipSuccess) {
     e = hipStreamSynchronize(demux->stream);

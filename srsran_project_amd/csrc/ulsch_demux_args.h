@@ -25,22 +25,26 @@ struct demux_args {
   int8_t*         csi1;
   const uint32_t* sch_map; // [nof_re]: UL-SCH RE index | DMX_ZERO, or DMX_NONE
   const uint32_t* uci_map; // [nof_re]: kind << 28 | stream RE index, or DMX_NONE
+  const uint32_t* csi2_map; // [nof_re]: CSI part 2 RE index | DMX_ZERO, or DMX_NONE (null: no CSI part 2)
+  int8_t*         csi2;
   const uint32_t* scr;     // Gold words of c_init over the codeword
   uint64_t        cw_stride;
   uint64_t        sch_stride;
   uint64_t        ack_stride;
   uint64_t        csi1_stride;
+  uint64_t        csi2_stride;
   uint32_t        nof_re;
   uint32_t        qm;
   uint32_t        bpre;    // bits per RE: Qm x layers
   uint32_t        ack_ph;  // HARQ-ACK payload bits when 1 or 2 (placeholders), else 0
   uint32_t        csi1_ph; // CSI part 1 payload bits when 1 or 2, else 0
+  uint32_t        csi2_ph; // CSI part 2 payload bits when 1 or 2, else 0
 };
 
 // Host placement (ulsch_demultiplex_impl.cpp:285-444) of every data RE of the codeword, in demodulator order.
 struct demux_placement {
-  std::vector<uint32_t> sch_map, uci_map;
-  uint32_t              nof_re = 0, nof_sch_re = 0, nof_ack_re = 0, nof_csi1_re = 0;
+  std::vector<uint32_t> sch_map, uci_map, csi2_map;
+  uint32_t              nof_re = 0, nof_sch_re = 0, nof_ack_re = 0, nof_csi1_re = 0, nof_csi2_re = 0;
 };
 int build_demux_placement(const srs_amd_ulsch_demux_config& cfg, demux_placement& out);
 

@@ -37,6 +37,49 @@ class PuschProcessorConfig(ctypes.Structure):
                          fd_smoothing, td_interpolation, int(compensate_cfo), ldpc_arith)
 
 
+class UciPart2Parameter(ctypes.Structure):
+    """``srs_amd_uci_part2_parameter``."""
+
+    _fields_ = [("offset", ctypes.c_uint16), ("width", ctypes.c_uint16)]
+
+
+class UciPart2Entry(ctypes.Structure):
+    """``srs_amd_uci_part2_entry``."""
+
+    _fields_ = [("nof_parameters", ctypes.c_uint32), ("parameters", UciPart2Parameter * 2),
+                ("map_size", ctypes.c_uint32), ("map", ctypes.c_uint16 * 16)]
+
+
+class UciPart2SizeDescription(ctypes.Structure):
+    """``srs_amd_uci_part2_size_description`` (uci_part2_size_description)."""
+
+    _fields_ = [("nof_entries", ctypes.c_uint32), ("entries", UciPart2Entry * 2)]
+
+
+def uci_part2_description(entries):
+    """entries: [([(offset, width), ...], [size per index]), ...] -> UciPart2SizeDescription."""
+    d = UciPart2SizeDescription()
+    d.nof_entries = len(entries)
+    for e, (params, sizes) in enumerate(entries):
+        d.entries[e].nof_parameters = len(params)
+        for q, (off, w) in enumerate(params):
+            d.entries[e].parameters[q].offset = off
+            d.entries[e].parameters[q].width = w
+        d.entries[e].map_size = len(sizes)
+        for m, v in enumerate(sizes):
+            d.entries[e].map[m] = v
+    return d
+
+
+def uci_part2_get_size(part1, descr):
+    """srs_amd_uci_part2_get_size: the CSI part 2 size of a CSI part 1 payload (one bit per byte)."""
+    import numpy as np
+
+    lib = _L()
+    b = np.ascontiguousarray(part1, np.uint8)
+    return int(lib.srs_amd_uci_part2_get_size(b.ctypes.data, b.size, ctypes.byref(descr)))
+
+
 class PuschPdu(ctypes.Structure):
     """``srs_amd_pusch_pdu`` (pusch_processor::pdu_t, data-only subset)."""
 
@@ -48,7 +91,8 @@ class PuschPdu(ctypes.Structure):
                                         "rb_count", "start_symbol_index", "nof_symbols", "tbs_lbrm_bytes", "tbs",
                                         "transform_precoding", "n_rs_id", "nof_harq_ack", "nof_csi_part1")] + \
         [("alpha_scaling", ctypes.c_float), ("beta_offset_harq_ack", ctypes.c_float),
-         ("beta_offset_csi_part1", ctypes.c_float)]
+         ("beta_offset_csi_part1", ctypes.c_float), ("beta_offset_csi_part2", ctypes.c_float),
+         ("csi_part2_size", UciPart2SizeDescription)]
 
 
 class PuschProcessorResult(ctypes.Structure):
@@ -56,7 +100,8 @@ class PuschProcessorResult(ctypes.Structure):
 
     _fields_ = [("data", PuschDecoderResult), ("sinr_db", ctypes.c_float), ("epre_db", ctypes.c_float),
                 ("rsrp_db", ctypes.c_float), ("time_alignment_s", ctypes.c_float),
-                ("harq_ack_status", ctypes.c_int32), ("csi_part1_status", ctypes.c_int32)]
+                ("harq_ack_status", ctypes.c_int32), ("csi_part1_status", ctypes.c_int32),
+                ("csi_part2_status", ctypes.c_int32), ("nof_csi_part2", ctypes.c_uint32)]
 
 
 RESULT_BYTES = ctypes.sizeof(PuschProcessorResult)
@@ -68,7 +113,8 @@ class PuschIntermediates(ctypes.Structure):
     _fields_ = [("d_estimates", ctypes.c_void_p), ("est_stride", ctypes.c_uint64), ("d_port_stats", ctypes.c_void_p),
                 ("d_llrs", ctypes.c_void_p), ("llr_stride", ctypes.c_uint32),
                 ("d_harq_ack", ctypes.c_void_p), ("harq_ack_stride", ctypes.c_uint32),
-                ("d_csi_part1", ctypes.c_void_p), ("csi_part1_stride", ctypes.c_uint32)]
+                ("d_csi_part1", ctypes.c_void_p), ("csi_part1_stride", ctypes.c_uint32),
+                ("d_csi_part2", ctypes.c_void_p), ("csi_part2_stride", ctypes.c_uint32)]
 
 
 class PuschSlotPdu(ctypes.Structure):
@@ -85,12 +131,17 @@ def make_pdu(**kw):
              dmrs_symbol_mask=(1 << 2) | (1 << 11), dmrs_type=1, scrambling_id=0, n_scid=0,
              nof_cdm_groups_without_data=2, rb_start=0, rb_count=None, start_symbol_index=0, nof_symbols=14,
              tbs_lbrm_bytes=0, tbs=0, transform_precoding=0, n_rs_id=0, nof_harq_ack=0, nof_csi_part1=0,
-             alpha_scaling=1.0, beta_offset_harq_ack=5.0, beta_offset_csi_part1=5.0)
+             alpha_scaling=1.0, beta_offset_harq_ack=5.0, beta_offset_csi_part1=5.0, beta_offset_csi_part2=5.0,
+             csi_part2_size=None)
     d.update(kw)
     if d["rb_count"] is None:
         d["rb_count"] = d["bwp_size_rb"] - d["rb_start"]
     p = PuschPdu()
     for k, v in d.items():
+        if k == "csi_part2_size":
+            if v is not None:
+                p.csi_part2_size = v if isinstance(v, UciPart2SizeDescription) else uci_part2_description(v)
+            continue
         setattr(p, k, v)
     return p
 
@@ -108,6 +159,7 @@ def _declare(lib):
         "srs_amd_pusch_process_batch": (c.c_int, [P, P, P, c.c_uint64, u, P, u, P, P, P, P]),
         "srs_amd_pusch_process": (c.c_int, [P, P, P, P, c.POINTER(PuschProcessorResult), P]),
         "srs_amd_pusch_process_slot": (c.c_int, [P, c.POINTER(PuschSlotPdu), u, P, c.c_uint64, u, P, P, P]),
+        "srs_amd_uci_part2_get_size": (c.c_int32, [P, u, c.POINTER(UciPart2SizeDescription)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -196,11 +248,12 @@ class PuschProcessor:
         return tb, res
 
     def process_batch(self, grids, plan, tbs=None, results=None, soft=None, port_stats=None, estimates=None,
-                      llrs=None, stream=None, harq_ack=None, csi_part1=None):
+                      llrs=None, stream=None, harq_ack=None, csi_part1=None, csi_part2=None):
         """Device: grids int32 [n][P][14][nsubc] -> tbs uint8 [n][tbs/8], results uint8 [n][RESULT_BYTES].
         Optional caller buffers for the intermediates: port_stats float32 [n][P][6], estimates int32
         [n][P][L][14][nsubc], llrs int8 [n][>= UL-SCH codeword length]; UCI payloads harq_ack uint8
-        [n][nof_harq_ack], csi_part1 uint8 [n][nof_csi_part1] (one bit per byte)."""
+        [n][nof_harq_ack], csi_part1 uint8 [n][nof_csi_part1], csi_part2 uint8 [n][largest CSI part 2 size] (one bit
+        per byte; the size each grid's CSI part 1 selected is in its result's nof_csi_part2)."""
         import torch
 
         n = grids.shape[0]
@@ -212,13 +265,14 @@ class PuschProcessor:
         if stream is None:
             stream = torch.cuda.current_stream(dev)
         io = None
-        if any(x is not None for x in (port_stats, estimates, llrs, harq_ack, csi_part1)):
+        if any(x is not None for x in (port_stats, estimates, llrs, harq_ack, csi_part1, csi_part2)):
             io = PuschIntermediates(
                 None if estimates is None else estimates.data_ptr(), 0 if estimates is None else estimates.stride(0),
                 None if port_stats is None else port_stats.data_ptr(), None if llrs is None else llrs.data_ptr(),
                 0 if llrs is None else llrs.stride(0), None if harq_ack is None else harq_ack.data_ptr(),
                 0 if harq_ack is None else harq_ack.stride(0), None if csi_part1 is None else csi_part1.data_ptr(),
-                0 if csi_part1 is None else csi_part1.stride(0))
+                0 if csi_part1 is None else csi_part1.stride(0), None if csi_part2 is None else csi_part2.data_ptr(),
+                0 if csi_part2 is None else csi_part2.stride(0))
         _lib.check(self._lib.srs_amd_pusch_process_batch(
             self._h, plan._h, grids.data_ptr(), grids.stride(0), n, tbs.data_ptr(), tbs.stride(0),
             results.data_ptr(), None if soft is None else soft.data_ptr(),

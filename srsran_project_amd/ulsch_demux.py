@@ -8,7 +8,7 @@ from . import _lib
 
 _FIELDS = ["modulation", "nof_layers", "nof_prb", "start_symbol_index", "nof_symbols", "nof_harq_ack_rvd", "dmrs_type",
            "dmrs_symbol_mask", "nof_cdm_groups_without_data", "nof_harq_ack_bits", "nof_enc_harq_ack_bits",
-           "nof_csi_part1_bits", "nof_enc_csi_part1_bits", "c_init"]
+           "nof_csi_part1_bits", "nof_enc_csi_part1_bits", "c_init", "nof_csi_part2_bits", "nof_enc_csi_part2_bits"]
 
 
 class UlschDemuxConfig(ctypes.Structure):
@@ -30,6 +30,8 @@ def _declare(lib):
         "srs_amd_ulsch_demux_plan_destroy": (None, [P]),
         "srs_amd_ulsch_demultiplex_batch": (c.c_int, [P, P, P, u64, P, u64, P, u64, P, u64, u, P]),
         "srs_amd_ulsch_demultiplex": (c.c_int, [P, P, P, P, P, P]),
+        "srs_amd_ulsch_demultiplex_csi2_batch": (c.c_int, [P, P, P, u64, P, u64, P, u64, P, u64, P, u64, u, P]),
+        "srs_amd_ulsch_demultiplex_csi2": (c.c_int, [P, P, P, P, P, P, P]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -106,6 +108,12 @@ class UlschDemux:
         sch = np.zeros(plan.nof_sch_bits, np.int8)
         ack = np.zeros(c.nof_enc_harq_ack_bits if c.nof_harq_ack_bits else 0, np.int8)
         csi1 = np.zeros(c.nof_enc_csi_part1_bits if c.nof_csi_part1_bits else 0, np.int8)
+        if c.nof_csi_part2_bits and c.nof_csi_part1_bits:
+            csi2 = np.zeros(c.nof_enc_csi_part2_bits, np.int8)
+            _lib.check(self._lib.srs_amd_ulsch_demultiplex_csi2(self._h, plan._h, cw.ctypes.data, sch.ctypes.data,
+                                                                ack.ctypes.data, csi1.ctypes.data, csi2.ctypes.data),
+                       "ulsch_demultiplex_csi2")
+            return sch, ack, csi1, csi2
         _lib.check(self._lib.srs_amd_ulsch_demultiplex(self._h, plan._h, cw.ctypes.data, sch.ctypes.data,
                                                        ack.ctypes.data, csi1.ctypes.data), "ulsch_demultiplex")
         return sch, ack, csi1

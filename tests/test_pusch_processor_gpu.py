@@ -379,3 +379,80 @@ def test_pusch_processor_uci_vs_reference(case):
     if snr >= 20:
         assert want["tb_crc_ok"] and want["harq_ack_status"] in (0, 1) and want["csi_part1_status"] in (0, 1), name
         assert np.array_equal(want["harq_ack"], ack) and np.array_equal(want["csi_part1"], csi1), name
+
+
+# CSI part 2: its size comes from the decoded CSI part 1 through uci_part2_get_size; (name, pdu overrides,
+# HARQ-ACK bits, CSI part 1 bits, CSI part 2 size description, SNR dB).  Each case runs a batch of grids whose CSI
+# part 1 payloads select different CSI part 2 sizes (one of them 0: no CSI part 2 multiplexed).
+CSI2_CASES = [
+    ("csi2_qpsk", dict(modulation=2, target_code_rate=679.0), 4, 9, [([(0, 2)], [0, 5, 17, 40])], 20.0),
+    ("csi2_ack2_16qam", dict(modulation=4, target_code_rate=490.0, rnti=0x321, n_id=5), 2, 12,
+     [([(1, 1), (4, 2)], [3, 1, 2, 11, 30, 0, 64, 7])], 25.0),
+    ("csi2_two_entries_2layer", dict(modulation=4, target_code_rate=490.0, nof_tx_layers=2, nof_rx_ports=2,
+                                     dmrs_symbol_mask=(1 << 2) | (1 << 7) | (1 << 11)), 6, 20,
+     [([(0, 1)], [8, 0]), ([(2, 2)], [2, 0, 24, 100])], 28.0),
+    ("csi2_large_64qam", dict(bwp_size_rb=106, rb_count=106, modulation=6, target_code_rate=567.0, nof_rx_ports=2),
+     1, 40, [([(7, 1)], [150, 300])], 28.0),
+]
+
+
+@pytest.mark.parametrize("case", CSI2_CASES, ids=[c[0] for c in CSI2_CASES])
+def test_pusch_processor_csi_part2_vs_reference(case):
+    """CSI part 2 on PUSCH (pusch_processor_impl.cpp:73-103): the size each grid's decoded CSI part 1 selects, the
+    demultiplexer's CSI part 2 placement from the symbol where CSI part 1 ends, the CSI part 2 decoding and the
+    UL-SCH around it -- TB, CRC, LDPC statistics, every UCI payload and status identical to the compiled reference
+    processor, per grid of one batch."""
+    import torch
+
+    name, over, n_ack, n_csi1, part2, snr = case
+    pdu = dict(BASE, **over, nof_harq_ack=n_ack, nof_csi_part1=n_csi1, beta_offset_harq_ack=8.0,
+               beta_offset_csi_part1=6.25, beta_offset_csi_part2=5.0, alpha_scaling=1.0, csi_part2_size=part2)
+    nprb = pdu["bwp_size_rb"]
+    tbs = _tbs(pdu)
+    r = pdu["target_code_rate"] / 1024
+    pdu["base_graph"] = 2 if (tbs <= 292 or (tbs <= 3824 and r <= 0.67) or r <= 0.25) else 1
+    rng = np.random.default_rng(len(name) + 100)
+    L, P = pdu["nof_tx_layers"], pdu["nof_rx_ports"]
+    ch = (np.eye(L, P) + 0.2j * np.ones((L, P))).astype(np.complex64)
+    descr = amd.uci_part2_description(part2)
+    grids, wants, sent = [], [], []
+    for k in range(4):
+        tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+        ack = rng.integers(0, 2, n_ack).astype(np.uint8)
+        csi1 = rng.integers(0, 2, n_csi1).astype(np.uint8)
+        n2 = amd.uci_part2_get_size(csi1, descr)
+        assert n2 == pp.ref_uci_part2_get_size(csi1, part2)
+        csi2 = rng.integers(0, 2, n2).astype(np.uint8)
+        grid, _ = pp.ue_transmit(tb, pdu, 12 * nprb, channel=ch, snr_db=snr, seed=3 + k, uci=(ack, csi1, csi2))
+        grids.append(grid)
+        wants.append(pp.ref_pusch_process(grid, pdu, tbs // 8, iterations=6))
+        sent.append((tb, ack, csi1, csi2))
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=6), device=0)
+    plan = proc.plan(amd.make_pdu(**dict(pdu, tbs=tbs)), 12 * nprb)
+    g = torch.from_numpy(np.stack(grids).view(np.int32)).to("cuda:0")
+    n = len(grids)
+    max2 = sum(max(sizes) for _, sizes in part2)
+    d_ack = torch.zeros((n, max(n_ack, 1)), dtype=torch.uint8, device="cuda:0")
+    d_csi1 = torch.zeros((n, max(n_csi1, 1)), dtype=torch.uint8, device="cuda:0")
+    d_csi2 = torch.zeros((n, max(max2, 1)), dtype=torch.uint8, device="cuda:0")
+    out, res = proc.process_batch(g, plan, harq_ack=d_ack if n_ack else None, csi_part1=d_csi1, csi_part2=d_csi2)
+    torch.cuda.synchronize()
+    results = amd.pusch_processor.parse_results(res.cpu().numpy())
+    for k, ((want_tb, want), got) in enumerate(zip(wants, results)):
+        tag = "%s grid %d" % (name, k)
+        n2 = len(want["csi_part2"])
+        assert got.nof_csi_part2 == n2, (tag, got.nof_csi_part2, n2)
+        assert got.csi_part2_status == want["csi_part2_status"], (tag, got.csi_part2_status, want["csi_part2_status"])
+        assert got.csi_part1_status == want["csi_part1_status"], tag
+        assert got.harq_ack_status == want["harq_ack_status"], tag
+        assert bool(got.data.tb_crc_ok) == want["tb_crc_ok"], tag
+        assert np.array_equal(out[k].cpu().numpy(), want_tb), tag
+        assert got.data.ldpc_iterations_sum == want["iterations_sum"], (tag, got.data.ldpc_iterations_sum, want)
+        np.testing.assert_array_equal(d_csi1[k, :n_csi1].cpu().numpy(), want["csi_part1"], err_msg=tag)
+        np.testing.assert_array_equal(d_csi2[k, :n2].cpu().numpy(), want["csi_part2"], err_msg=tag)
+        if n_ack:
+            np.testing.assert_array_equal(d_ack[k, :n_ack].cpu().numpy(), want["harq_ack"], err_msg=tag)
+        tb, ack, csi1, csi2 = sent[k]
+        # at these SNRs the reference recovers what the UE sent
+        assert want["tb_crc_ok"] and np.array_equal(want["csi_part1"], csi1), tag
+        assert np.array_equal(want["csi_part2"], csi2), tag

@@ -80,3 +80,27 @@ def test_ulsch_information_rejects():
                         nof_layers=1)
     with pytest.raises(ValueError):  # DM-RS before the allocation
         amd.ulsch_information(c)
+
+
+@pytest.mark.skipif(oracle.REF is None, reason="oracle/_ref not built")
+def test_uci_part2_size_matches_reference():
+    """srs_amd_uci_part2_get_size against the compiled uci_part2_get_size over random descriptions (one or two
+    entries, zero- to four-bit indices from one or two CSI part 1 fields) and payloads."""
+    import srsran_project_amd as amd
+    from oracle import pusch_proc as pp
+
+    rng = np.random.default_rng(12)
+    for _ in range(300):
+        n1 = int(rng.integers(4, 40))
+        entries = []
+        for _e in range(int(rng.integers(1, 3))):
+            params, left = [], 4
+            for _q in range(int(rng.integers(1, 3))):
+                w = int(rng.integers(0, left + 1))
+                left -= w
+                params.append((int(rng.integers(0, n1 - w + 1)), w))
+            bits = sum(w for _, w in params)
+            entries.append((params, [int(v) for v in rng.integers(0, 300, 1 << bits)]))
+        part1 = rng.integers(0, 2, n1).astype(np.uint8)
+        got = amd.uci_part2_get_size(part1, amd.uci_part2_description(entries))
+        assert got == pp.ref_uci_part2_get_size(part1, entries), (entries, part1)
