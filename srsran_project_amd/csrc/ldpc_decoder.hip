@@ -37,6 +37,7 @@
 
 #include "ldpc_common.h"
 #include <cstdlib>
+#include <type_traits>
 #include <utility>
 
 namespace srs_amd {
@@ -1005,20 +1006,244 @@ __device__ __forceinline__ void hr_layers(lds_i8* lds, MSGS& c2v, uint32_t t, in
   }
 }
 
+// ============================================================================
+// Full-length BG1 / Z = 384 codeblocks (any layer count, e.g. the rate-1/3 codeblocks of configs[1]): the
+// high-rate layout above -- two check rows per lane in packed int16, three waves per codeblock, no argmin
+// index register -- with the check-to-variable messages of all 46 layers held COMPRESSED in registers.
+//
+// A min-sum message is a function of four values of its check row (ldpc_decoder_impl.cpp:290-310): the scaled
+// minima s1 <= s2, the edge index of the first minimum and the sign of each edge's message, c_e = +-(e == idx ?
+// s2 : s1).  Per row pair (rows t and t + 192, one per 16-bit half) the registers hold exactly that:
+//   word A: s2 (bits 0-6) | idx (bits 7-11) | signs of edges 0-3 (bits 12-15)
+//   word B: s2 - s1 (bits 0-6) | signs of edges 4-12 (bits 7-15)
+//   word C (the degree-19 rows only): signs of edges 13-18 (bits 0-5)
+// 96 VGPRs for all 46 layers, where int16 messages would take 316 and int8 pairs 158: the kernel runs at
+// three waves per SIMD, four codeblocks (12 waves, 4 x 26 KiB of soft bits) per CU with every SIMD equally
+// loaded.  Rebuilding an old message costs 7 packed instructions (index test, min-select, sign extract, sign
+// apply); the index of the first minimum comes out of pass 1 as the low bits of min(|v2c| << 5 | e).
+// Bit-exact with ldpc_decode_kernel (same per-edge arithmetic; identical outputs, iteration counts, final
+// soft bits).
+// ============================================================================
+
+typedef unsigned short pku16 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pk16 as_pk(uint32_t w)
+{
+  return __builtin_bit_cast(pk16, w);
+}
+__device__ __forceinline__ uint32_t as_u32(pk16 v)
+{
+  return __builtin_bit_cast(uint32_t, v);
+}
+// per 16-bit half: 0 if the half is zero, 1 otherwise -- one v_pk_min_u16 kept opaque: the compiler otherwise
+// turns min(x, 1) into a per-half compare and v_cndmask selects (no packed select exists)
+__device__ __forceinline__ pk16 pk_nonzero(uint32_t w)
+{
+  uint32_t r;
+  // op_sel_hi:[1,0]: the high half also reads the inline constant's low 16 bits (a splat 1)
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(r) : "v"(w));
+  return __builtin_bit_cast(pk16, r);
+}
+
+// compressed state words of BG1 layer l, and the offset of layer l's words
+constexpr int fr_words(int l)
+{
+  return bg_traits<1>::deg(l) > 13 ? 3 : 2;
+}
+constexpr int fr_off(int l)
+{
+  int s = 0;
+  for (int i = 0; i < l; ++i) {
+    s += fr_words(i);
+  }
+  return s;
+}
+constexpr int FR_STATE_WORDS = fr_off(bg_traits<1>::M);
+static_assert(FR_STATE_WORDS == 96, "BG1 compressed message state");
+// word and bit (of each 16-bit half) holding the sign of edge e of a row
+constexpr int fr_sign_word(int e)
+{
+  return e < 4 ? 0 : (e < 13 ? 1 : 2);
+}
+constexpr int fr_sign_bit(int e)
+{
+  return e < 4 ? 12 + e : (e < 13 ? e + 3 : e - 13);
+}
+
+// scale_mag of both halves in 16-bit arithmetic (minima are <= LLR_MAX; both forms equal scale_mag on 0..120):
+// ARITH_SIMD floor(m 52428 / 2^16) = max((205 m - 52) >> 8, 0), ARITH_GENERIC round(0.8 m) = (205 m + 102) >> 8
+template <int ARITH>
+__device__ __forceinline__ pk16 pk_scale16(pk16 m)
+{
+  if constexpr (ARITH == ARITH_GENERIC) {
+    return (m * pk_splat(205) + pk_splat(102)) >> 8;
+  } else {
+    return pk_max((m * pk_splat(205) - pk_splat(52)) >> 8, pk_splat(0));
+  }
+}
+
+// a * b + c in both halves as one v_pk_mad_u16 (the low 16 bits of the product are sign-agnostic); opaque, so
+// the compiler does not split it into a multiply and a subtract
+__device__ __forceinline__ pk16 pk_mad(pk16 a, pk16 b, pk16 c)
+{
+  uint32_t r;
+  asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(as_u32(a)), "v"(as_u32(b)), "v"(as_u32(c)));
+  return as_pk(r);
+}
+// a * 32 + E (E an inline constant), one v_pk_mad_u16
+template <int E>
+__device__ __forceinline__ pk16 pk_key(pk16 a)
+{
+  uint32_t r;
+  asm("v_pk_mad_u16 %0, %1, 32, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(as_u32(a)), "i"(E));
+  return as_pk(r);
+}
+
+#ifndef FR_SIGN_SHIFT
+#define FR_SIGN_SHIFT 1
+#endif
+#ifndef FR_KEEP_ADDR
+#define FR_KEEP_ADDR 19
+#endif
+
+struct fr_state {
+  uint32_t w[FR_STATE_WORDS];
+  __device__ __forceinline__ void zero()
+  {
+#pragma unroll
+    for (int i = 0; i < FR_STATE_WORDS; ++i) {
+      w[i] = 0;
+    }
+  }
+};
+
+// One layer (BG1 row L) for the row pair of lane t, messages rebuilt from / folded into the compressed state.
+template <int L, int ARITH, int... E>
+__device__ __forceinline__ void fr_layer(lds_i8* lds, fr_state& st, uint32_t t, std::integer_sequence<int, E...>)
+{
+  constexpr int  E0  = row_start<1>(L);
+  constexpr int  DEG = sizeof...(E);
+  constexpr int  O   = fr_off(L);
+  constexpr bool W3  = fr_words(L) == 3;
+  const uint32_t wold[3] = {st.w[O], st.w[O + 1], W3 ? st.w[O + 2] : 0u};
+  const pk16     s2o     = as_pk(wold[0] & 0x007f007fu);
+  const uint32_t imo     = wold[0] & 0x0f800f80u;
+  const pk16     dno     = pk_splat(0) - as_pk(wold[1] & 0x007f007fu); // s1 - s2 of the old messages
+  pk16           v[DEG];
+  pk16           min1[2], min2[2];
+  pk16           sgn = pk_splat(0);
+  // keys |v2c| << 5 | e; the initial key stands for the reference's LLR_MAX start value (no edge index)
+  min1[0] = min1[1] = min2[0] = min2[1] = pk_splat(LLR_MAX * 32 + 31);
+  // pass 1 (ldpc_decoder_impl.cpp:235 / :290): old message, v2c, check-node statistics
+  (
+      [&] {
+        if constexpr (E % HR_CHUNK1 == 0 && E > 0) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        constexpr int h = E & 1; // reduction chain
+        const pk16    s = pk16{static_cast<short>(lds[hr_addr<E0 + E, 0>(t)]),
+                            static_cast<short>(lds[hr_addr<E0 + E, HR_HALF>(t)])};
+        // old message: +-(e == idx ? s2 : s1)
+        const pk16 f   = pk_nonzero(imo ^ ((static_cast<uint32_t>(E) << 7) * 0x10001u));
+        const pk16 mag = pk_mad(f, dno, s2o);
+        const pk16 ng  = (as_pk(wold[fr_sign_word(E)]) << pk_splat(15 - fr_sign_bit(E))) >> 15;
+        const pk16 c   = (mag ^ ng) - ng;
+        const pk16 sat = pk_clamp(s, LLR_MAX);
+        // infinite soft bits (+-SOFT_INF) push |v2c| beyond 220 (see edge_pass1)
+        const pk16 x   = (s - sat) * pk_splat(INF_BOOST) + pk_clamp(s - c, LLR_MAX);
+        const pk16 key = pk_key<E>(__builtin_elementwise_abs(x));
+        min2[h]        = pk_max(min1[h], pk_min(key, min2[h])); // median(min1, key, min2)
+        min1[h]        = pk_min(min1[h], key);
+        sgn ^= x;
+        v[E] = x;
+      }(),
+      ...);
+  __builtin_amdgcn_sched_barrier(0);
+  const pk16     k1  = pk_min(min1[0], min1[1]);
+  const pk16     k2  = pk_min(pk_max(min1[0], min1[1]), pk_min(min2[0], min2[1]));
+  const pk16     s1  = pk_scale16<ARITH>(k1 >> 5);
+  const pk16     s2  = pk_scale16<ARITH>(k2 >> 5);
+  const pk16     d12 = s1 - s2;
+  const uint32_t idx = as_u32(k1) & 0x001f001fu;
+  uint32_t       acc[3] = {(idx << 7) | as_u32(s2), as_u32(s2 - s1), 0u};
+  if constexpr (DEG > FR_KEEP_ADDR) {
+    // rows of high degree recompute their scatter addresses instead of holding DEG of them live
+    asm volatile("" : "+v"(t));
+  }
+  // pass 2 (ldpc_decoder_impl.cpp:310, :270): new message, promotion sum, new state
+  (
+      [&] {
+        if constexpr (E % HR_CHUNK2 == 0 && E > 0) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const pk16 x   = v[E];
+        const pk16 f   = pk_nonzero(idx ^ (static_cast<uint32_t>(E) * 0x10001u)); // 0: this edge holds min1
+        const pk16 mag = f * d12 + s2;
+        const pk16 sx  = sgn ^ x;
+        const pk16 ng  = sx >> 15;
+        const pk16 c   = (mag ^ ng) - ng;
+        // promotion sum: |c + x| > LLR_MAX is +-SOFT_INF (see edge_pass2)
+        const pk16 out = pk_clamp(c + x, SOFT_INF);
+#if FR_SIGN_SHIFT
+        // sign bit into both halves of the state word: (sx >>> 15) << bit, one v_lshl_or_b32 with an inline shift
+        const uint32_t nb = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pku16, sx) >> 15);
+        acc[fr_sign_word(E)] |= nb << fr_sign_bit(E);
+#else
+        // sign mask of both halves into the state word: one v_and_or_b32 (mask constant in an SGPR)
+        acc[fr_sign_word(E)] |= as_u32(ng) & ((1u << fr_sign_bit(E)) * 0x10001u);
+#endif
+        lds[hr_addr<E0 + E, 0>(t)]       = static_cast<int8_t>(out.x);
+        lds[hr_addr<E0 + E, HR_HALF>(t)] = static_cast<int8_t>(out.y);
+      }(),
+      ...);
+  // pin the assembled words here: left alone the compiler sinks the sign-bit ORs past the layer's join and
+  // keeps (and spills) the separate bits until the next iteration reads the words
+  asm volatile("" : "+v"(acc[0]), "+v"(acc[1]));
+  st.w[O]     = acc[0];
+  st.w[O + 1] = acc[1];
+  if constexpr (W3) {
+    asm volatile("" : "+v"(acc[2]));
+    st.w[O + 2] = acc[2];
+  }
+}
+
+template <int L, int ARITH>
+__device__ __forceinline__ void fr_layers(lds_i8* lds, fr_state& st, uint32_t t, int nof_layers)
+{
+  if constexpr (L < bg_traits<1>::M) {
+    // laundered per layer: otherwise the 42 layer conditions are hoisted out of the iteration loop as 64-bit
+    // lane masks (84 SGPRs, spilled)
+    asm volatile("" : "+s"(nof_layers));
+    if (L < 4 || L < nof_layers) { // uniform; nof_layers >= 4
+      asm volatile("" : "+v"(t));
+      fr_layer<L, ARITH>(lds, st, t, std::make_integer_sequence<int, bg_traits<1>::deg(L)>{});
+      __syncthreads();
+    }
+    fr_layers<L + 1, ARITH>(lds, st, t, nof_layers);
+  }
+}
+
 // NP row pairs per lane: NP = 1 -> 192 threads (3 waves) per codeblock, NP = 3 -> one wave per codeblock
 // (no workgroup barriers, three independent pair streams per lane).
 #ifndef HR_WAVES
 #define HR_WAVES 4
 #endif
-template <int NP>
+#ifndef FR_WAVES
+#define FR_WAVES 3
+#endif
+template <int NP, int MAXL>
 constexpr int hr_waves_per_simd()
 {
-  return NP == 1 ? HR_WAVES : 2;
+  return MAXL == bg_traits<1>::M ? FR_WAVES : (NP == 1 ? HR_WAVES : 2);
 }
 
+// MAXL < 46: the high-rate kernel (int16 messages of the first MAXL layers in registers); MAXL == 46: the
+// full-length kernel (compressed messages of every layer).
 template <int ARITH, int MAXL, int NP>
-__global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_decode_hr_kernel(decode_args a)
+__global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>())) ldpc_decode_hr_kernel(decode_args a)
 {
+  constexpr bool FULL   = MAXL == bg_traits<1>::M;
+  static_assert(!FULL || NP == 1, "full-length codeblocks: one row pair per lane");
   constexpr int Z       = HR_Z;
   constexpr int K       = 22 * Z;
   constexpr int NODES   = 22 + MAXL;
@@ -1124,11 +1349,15 @@ __global__ void __launch_bounds__(HR_HALF / NP, hr_waves_per_simd<NP>()) ldpc_de
     const int nof_sig    = K - (a.fillers ? a.fillers[cb] : a.nof_filler_bits);
     int       result     = -1;
 
-    hr_msgs<NE> c2v;
+    std::conditional_t<FULL, fr_state, hr_msgs<NE>> c2v;
     c2v.zero();
 
     for (int it = 0; it < a.max_iterations; ++it) {
-      hr_layers<0, MAXL, ARITH, NP>(lds, c2v, t, nof_layers);
+      if constexpr (FULL) {
+        fr_layers<0, ARITH>(lds, c2v, t, nof_layers);
+      } else {
+        hr_layers<0, MAXL, ARITH, NP>(lds, c2v, t, nof_layers);
+      }
 
       if (a.crc_table) {
         // hard bits + CRC early stop (ldpc_decoder_impl.cpp:125), remainder up to a unit factor:
@@ -1262,6 +1491,18 @@ bool ldpc_decode_hr_eligible(const decode_args& args, const lifted_graph& g)
          ((reinterpret_cast<uintptr_t>(args.soft_out) | (args.soft_out ? 68u * HR_Z : 0u)) & 3u) == 0;
 }
 
+// BG1 Z = 384 codeblocks of any length through the packed full-length kernel (same launch conditions as the
+// high-rate kernel otherwise).  SRSRAN_AMD_LDPC_FULL=0 keeps them on ldpc_decode_kernel.
+static bool ldpc_decode_full_eligible(const decode_args& args, const lifted_graph& g)
+{
+  static const bool enabled = [] {
+    const char* e = std::getenv("SRSRAN_AMD_LDPC_FULL");
+    return e == nullptr || e[0] != '0';
+  }();
+  return enabled && g.bg == 1 && g.Z == HR_Z && args.llr_lens == nullptr && args.aligned4 != 0 &&
+         ((reinterpret_cast<uintptr_t>(args.soft_out) | (args.soft_out ? 68u * HR_Z : 0u)) & 3u) == 0;
+}
+
 size_t ldpc_decode_lds_bytes(const lifted_graph& g)
 {
   return g.bg == 1 ? lds_total_bytes<1>(g.Z) : lds_total_bytes<2>(g.Z);
@@ -1292,6 +1533,16 @@ hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, in
     } else {
       hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_SIMD, HR_MAXL, HR_NP>), dim3(grid), dim3(NT), lds, stream,
                          args);
+    }
+    return hipGetLastError();
+  }
+  if (ldpc_decode_full_eligible(args, g)) {
+    constexpr int    MAXL = bg_traits<1>::M;
+    constexpr size_t lds  = hr_lds_bytes<MAXL>();
+    if (arith == ARITH_GENERIC) {
+      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_GENERIC, MAXL, 1>), dim3(grid), dim3(HR_HALF), lds, stream, args);
+    } else {
+      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_SIMD, MAXL, 1>), dim3(grid), dim3(HR_HALF), lds, stream, args);
     }
     return hipGetLastError();
   }
