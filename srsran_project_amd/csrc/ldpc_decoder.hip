@@ -893,6 +893,55 @@ __device__ __forceinline__ pk16 pk_scale(pk16 m)
   return pk16{static_cast<short>(scale_mag<ARITH>(m.x)), static_cast<short>(scale_mag<ARITH>(m.y))};
 }
 
+typedef unsigned short pku16 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pk16 as_pk(uint32_t w)
+{
+  return __builtin_bit_cast(pk16, w);
+}
+__device__ __forceinline__ uint32_t as_u32(pk16 v)
+{
+  return __builtin_bit_cast(uint32_t, v);
+}
+// per 16-bit half: 0 if the half is zero, 1 otherwise -- one v_pk_min_u16 kept opaque: the compiler otherwise
+// turns min(x, 1) into a per-half compare and v_cndmask selects (no packed select exists)
+__device__ __forceinline__ pk16 pk_nonzero(uint32_t w)
+{
+  uint32_t r;
+  // op_sel_hi:[1,0]: the high half also reads the inline constant's low 16 bits (a splat 1)
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(r) : "v"(w));
+  return __builtin_bit_cast(pk16, r);
+}
+
+// scale_mag of both halves in 16-bit arithmetic (minima are <= LLR_MAX; both forms equal scale_mag on 0..120):
+// ARITH_SIMD floor(m 52428 / 2^16) = max((205 m - 52) >> 8, 0), ARITH_GENERIC round(0.8 m) = (205 m + 102) >> 8
+template <int ARITH>
+__device__ __forceinline__ pk16 pk_scale16(pk16 m)
+{
+  if constexpr (ARITH == ARITH_GENERIC) {
+    return (m * pk_splat(205) + pk_splat(102)) >> 8;
+  } else {
+    return pk_max((m * pk_splat(205) - pk_splat(52)) >> 8, pk_splat(0));
+  }
+}
+
+// a * b + c in both halves as one v_pk_mad_u16 (the low 16 bits of the product are sign-agnostic); opaque, so
+// the compiler does not split it into a multiply and a subtract
+__device__ __forceinline__ pk16 pk_mad(pk16 a, pk16 b, pk16 c)
+{
+  uint32_t r;
+  asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(as_u32(a)), "v"(as_u32(b)), "v"(as_u32(c)));
+  return as_pk(r);
+}
+// a * 32 + E (E an inline constant), one v_pk_mad_u16
+template <int E>
+__device__ __forceinline__ pk16 pk_key(pk16 a)
+{
+  uint32_t r;
+  asm("v_pk_mad_u16 %0, %1, 32, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(as_u32(a)), "i"(E));
+  return as_pk(r);
+}
+
 // Edges per scheduling group in the two passes of a layer (bounds the gathered values in flight).
 #ifndef HR_CHUNK1
 #define HR_CHUNK1 5
@@ -902,6 +951,11 @@ __device__ __forceinline__ pk16 pk_scale(pk16 m)
 #endif
 #ifndef HR_PIN_X
 #define HR_PIN_X 0
+#endif
+// argmin as the low bits of min(|v2c| << 5 | e) (as the full-length kernel below): pass 2 tests e == idx with two
+// instructions instead of recomputing |v2c| - min1 (four)
+#ifndef HR_KEYS
+#define HR_KEYS 0
 #endif
 
 // One layer (base-graph row L, global edges E0 .. E0 + DEG - 1) for the NP row pairs of lane t:
@@ -922,8 +976,9 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
   pk16          min1[2][NP], min2[2][NP], sgn[NP];
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    min1[0][k] = min1[1][k] = pk_splat(LLR_MAX);
-    min2[0][k] = min2[1][k] = pk_splat(LLR_MAX);
+    // HR_KEYS: minima of the keys |v2c| << 5 | e (the initial key stands for LLR_MAX with no edge index)
+    min1[0][k] = min1[1][k] = pk_splat(HR_KEYS ? LLR_MAX * 32 + 31 : LLR_MAX);
+    min2[0][k] = min2[1][k] = pk_splat(HR_KEYS ? LLR_MAX * 32 + 31 : LLR_MAX);
     sgn[k]                  = pk_splat(0);
   }
   // pass 1 (ldpc_decoder_impl.cpp:235 / :290): v2c and the check-node statistics
@@ -940,7 +995,11 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
           const pk16 sat = pk_clamp(s, LLR_MAX);
           // infinite soft bits (+-SOFT_INF) push |v2c| beyond 220 (see edge_pass1)
           const pk16 x = (s - sat) * pk_splat(INF_BOOST) + pk_clamp(s - c2v.template get<(E0 + E) * NP + k>(), LLR_MAX);
+#if HR_KEYS
+          const pk16 ax = pk_key<E>(__builtin_elementwise_abs(x));
+#else
           const pk16 ax = __builtin_elementwise_abs(x);
+#endif
           min2[h][k]    = pk_max(min1[h][k], pk_min(ax, min2[h][k])); // median(min1, |v|, min2)
           min1[h][k]    = pk_min(min1[h][k], ax);
           sgn[k] ^= x;
@@ -955,8 +1014,14 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
     // merge the two chains: min1 = min(a1, b1), min2 = min(max(a1, b1), min(a2, b2))
     m1[k]  = pk_min(min1[0][k], min1[1][k]);
     const pk16 mn2 = pk_min(pk_max(min1[0][k], min1[1][k]), pk_min(min2[0][k], min2[1][k]));
+#if HR_KEYS
+    s1[k]  = pk_scale16<ARITH>(m1[k] >> 5);
+    s2[k]  = pk_scale16<ARITH>(mn2 >> 5);
+    m1[k]  = as_pk(as_u32(m1[k]) & 0x001f001fu); // index of the first minimum
+#else
     s1[k]  = pk_scale<ARITH>(m1[k]);
     s2[k]  = pk_scale<ARITH>(mn2);
+#endif
     d12[k] = s1[k] - s2[k];
   }
   // pass 2 (ldpc_decoder_impl.cpp:310, :270): new message and promotion sum
@@ -972,7 +1037,11 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
           // opaque: otherwise |x| of pass 1 is kept live (19 more VGPRs) instead of being recomputed
           asm volatile("" : "+v"(x));
 #endif
+#if HR_KEYS
+          const pk16 f   = pk_nonzero(as_u32(m1[k]) ^ (static_cast<uint32_t>(E) * 0x10001u)); // 0: edge E holds min1
+#else
           const pk16 f   = pk_min(__builtin_elementwise_abs(x) - m1[k], pk_splat(1)); // 0: this edge holds min1
+#endif
           const pk16 mag = f * d12[k] + s2[k];
           const pk16 neg = (sgn[k] ^ x) >> 15;
           const pk16 c   = (mag ^ neg) - neg;
@@ -1025,26 +1094,6 @@ __device__ __forceinline__ void hr_layers(lds_i8* lds, MSGS& c2v, uint32_t t, in
 // soft bits).
 // ============================================================================
 
-typedef unsigned short pku16 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ pk16 as_pk(uint32_t w)
-{
-  return __builtin_bit_cast(pk16, w);
-}
-__device__ __forceinline__ uint32_t as_u32(pk16 v)
-{
-  return __builtin_bit_cast(uint32_t, v);
-}
-// per 16-bit half: 0 if the half is zero, 1 otherwise -- one v_pk_min_u16 kept opaque: the compiler otherwise
-// turns min(x, 1) into a per-half compare and v_cndmask selects (no packed select exists)
-__device__ __forceinline__ pk16 pk_nonzero(uint32_t w)
-{
-  uint32_t r;
-  // op_sel_hi:[1,0]: the high half also reads the inline constant's low 16 bits (a splat 1)
-  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(r) : "v"(w));
-  return __builtin_bit_cast(pk16, r);
-}
-
 // compressed state words of BG1 layer l, and the offset of layer l's words
 constexpr int fr_words(int l)
 {
@@ -1070,35 +1119,10 @@ constexpr int fr_sign_bit(int e)
   return e < 4 ? 12 + e : (e < 13 ? e + 3 : e - 13);
 }
 
-// scale_mag of both halves in 16-bit arithmetic (minima are <= LLR_MAX; both forms equal scale_mag on 0..120):
-// ARITH_SIMD floor(m 52428 / 2^16) = max((205 m - 52) >> 8, 0), ARITH_GENERIC round(0.8 m) = (205 m + 102) >> 8
-template <int ARITH>
-__device__ __forceinline__ pk16 pk_scale16(pk16 m)
-{
-  if constexpr (ARITH == ARITH_GENERIC) {
-    return (m * pk_splat(205) + pk_splat(102)) >> 8;
-  } else {
-    return pk_max((m * pk_splat(205) - pk_splat(52)) >> 8, pk_splat(0));
-  }
-}
-
-// a * b + c in both halves as one v_pk_mad_u16 (the low 16 bits of the product are sign-agnostic); opaque, so
-// the compiler does not split it into a multiply and a subtract
-__device__ __forceinline__ pk16 pk_mad(pk16 a, pk16 b, pk16 c)
-{
-  uint32_t r;
-  asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(as_u32(a)), "v"(as_u32(b)), "v"(as_u32(c)));
-  return as_pk(r);
-}
-// a * 32 + E (E an inline constant), one v_pk_mad_u16
-template <int E>
-__device__ __forceinline__ pk16 pk_key(pk16 a)
-{
-  uint32_t r;
-  asm("v_pk_mad_u16 %0, %1, 32, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(as_u32(a)), "i"(E));
-  return as_pk(r);
-}
-
+// v_pk_mad_u16 as opaque asm for the old-message magnitude and the argmin key (fewer instructions; 1 = on)
+#ifndef FR_ASM_MAD
+#define FR_ASM_MAD 1
+#endif
 #ifndef FR_SIGN_SHIFT
 #define FR_SIGN_SHIFT 1
 #endif
@@ -1145,13 +1169,21 @@ __device__ __forceinline__ void fr_layer(lds_i8* lds, fr_state& st, uint32_t t, 
                             static_cast<short>(lds[hr_addr<E0 + E, HR_HALF>(t)])};
         // old message: +-(e == idx ? s2 : s1)
         const pk16 f   = pk_nonzero(imo ^ ((static_cast<uint32_t>(E) << 7) * 0x10001u));
+#if FR_ASM_MAD
         const pk16 mag = pk_mad(f, dno, s2o);
+#else
+        const pk16 mag = f * dno + s2o;
+#endif
         const pk16 ng  = (as_pk(wold[fr_sign_word(E)]) << pk_splat(15 - fr_sign_bit(E))) >> 15;
         const pk16 c   = (mag ^ ng) - ng;
         const pk16 sat = pk_clamp(s, LLR_MAX);
         // infinite soft bits (+-SOFT_INF) push |v2c| beyond 220 (see edge_pass1)
         const pk16 x   = (s - sat) * pk_splat(INF_BOOST) + pk_clamp(s - c, LLR_MAX);
+#if FR_ASM_MAD
         const pk16 key = pk_key<E>(__builtin_elementwise_abs(x));
+#else
+        const pk16 key = __builtin_elementwise_abs(x) * pk_splat(32) + pk_splat(E);
+#endif
         min2[h]        = pk_max(min1[h], pk_min(key, min2[h])); // median(min1, key, min2)
         min1[h]        = pk_min(min1[h], key);
         sgn ^= x;
