@@ -1524,15 +1524,34 @@ bool ldpc_decode_hr_eligible(const decode_args& args, const lifted_graph& g)
 }
 
 // BG1 Z = 384 codeblocks of any length through the packed full-length kernel (same launch conditions as the
-// high-rate kernel otherwise).  SRSRAN_AMD_LDPC_FULL=0 keeps them on ldpc_decode_kernel.
+// high-rate kernel otherwise).  SRSRAN_AMD_LDPC_FULL (read per launch): 0 keeps them on ldpc_decode_kernel,
+// 1 takes the full-length kernel whatever the batch size (A/B timing, parity tests on small batches).
 static bool ldpc_decode_full_eligible(const decode_args& args, const lifted_graph& g)
 {
-  static const bool enabled = [] {
-    const char* e = std::getenv("SRSRAN_AMD_LDPC_FULL");
-    return e == nullptr || e[0] != '0';
+  const char* mode    = std::getenv("SRSRAN_AMD_LDPC_FULL");
+  const bool  enabled = mode == nullptr || mode[0] != '0';
+  const bool  forced  = mode != nullptr && mode[0] == '1';
+  if (!(enabled && g.bg == 1 && g.Z == HR_Z && args.llr_lens == nullptr && args.aligned4 != 0 &&
+        ((reinterpret_cast<uintptr_t>(args.soft_out) | (args.soft_out ? 68u * HR_Z : 0u)) & 3u) == 0)) {
+    return false;
+  }
+  if (forced) {
+    return true;
+  }
+  // Batch size: the full-length kernel keeps 4 codeblocks per CU in flight with 3 waves each, ldpc_decode_kernel
+  // 2 per CU with 8 waves each, and one of its codeblocks takes ~1.6x less time (configs[1]: 1.57 vs 1.26 M
+  // codeblocks/s at full occupancy).  A launch that fills only part of a round (e.g. a small slot bucket) is
+  // latency-bound, so take the full-length kernel only when it needs fewer codeblock-rounds in time.
+  static const uint32_t cus = [] {
+    int dev = 0, n = 0;
+    return (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+               ? static_cast<uint32_t>(n)
+               : 256u;
   }();
-  return enabled && g.bg == 1 && g.Z == HR_Z && args.llr_lens == nullptr && args.aligned4 != 0 &&
-         ((reinterpret_cast<uintptr_t>(args.soft_out) | (args.soft_out ? 68u * HR_Z : 0u)) & 3u) == 0;
+  const uint64_t rounds_general = (args.nof_cbs + 2ull * cus - 1) / (2ull * cus);
+  const uint64_t rounds_full    = (args.nof_cbs + 4ull * cus - 1) / (4ull * cus);
+  return 16 * rounds_full < 10 * rounds_general;
 }
 
 size_t ldpc_decode_lds_bytes(const lifted_graph& g)

@@ -38,7 +38,13 @@ def test_oracle_decoder_reproduces_golden():
 
 
 @pytest.mark.gpu
-def test_gpu_decoder_reproduces_golden():
+@pytest.mark.parametrize("full", ["auto", "1"])
+def test_gpu_decoder_reproduces_golden(full, monkeypatch):
+    # "1": BG1 Z=384 vectors (configs[1]) through the packed full-length kernel whatever the batch size
+    if full == "1":
+        monkeypatch.setenv("SRSRAN_AMD_LDPC_FULL", "1")
+    else:
+        monkeypatch.delenv("SRSRAN_AMD_LDPC_FULL", raising=False)
     import torch
 
     import srsran_project_amd as amd

@@ -26,6 +26,18 @@ def amd():
     return amd
 
 
+@pytest.fixture(autouse=True, params=["auto", "full"])
+def full_length_kernel(request, monkeypatch):
+    """Every case twice: the launch's own kernel choice (small batches of full-length BG1 Z=384 codeblocks go to
+    ldpc_decode_kernel) and SRSRAN_AMD_LDPC_FULL=1, which sends every BG1 Z=384 launch the high-rate kernel does
+    not take through the packed full-length kernel whatever the batch size."""
+    if request.param == "full":
+        monkeypatch.setenv("SRSRAN_AMD_LDPC_FULL", "1")
+    else:
+        monkeypatch.delenv("SRSRAN_AMD_LDPC_FULL", raising=False)
+    return request.param
+
+
 def _gpu_decode(amd, dec, llrs, bg, Z, iters, crc=None, filler=0, lens=None, want_soft=False):
     import torch
 
