@@ -212,6 +212,11 @@ def run_ldpc(args, dist, world, rank, dev):
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = ldpc_cpu_baseline(args, llrs[:512].cpu().numpy())
+    full_pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", "r03c_ldpc_full_pmc.json")
+    if os.path.exists(pmc_path):
+        row = json.load(open(pmc_path)).get("ldpc_decode_hr_kernel<0, 46, 1>", {})
+        full_pmc = {"hbm_bytes": row.get("hbm_mb", 0.0) * 1e6 or None, "valu_busy": row.get("valu_busy")}
     return {
         "metric": "LDPC decode codeblocks/s (BG1 Z=384, 8 min-sum iterations, full-length rate-1/3 codeblocks)",
         "value": value,
@@ -243,10 +248,15 @@ def run_ldpc(args, dist, world, rank, dev):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
-            "traffic": load_traffic("r01_ldpc_decode_traffic.json"),
-            "kernel": "ldpc_decode_kernel",
+            "traffic": full_pmc.get("hbm_bytes"),
+            "kernel": "ldpc_decode_hr_kernel<ARITH, 46, 1> (full-length BG1 Z=384 kernel)",
             "kernel_ms": kernel_ms,
             "algorithmic_bytes_per_launch": bytes_per_cb * args.batch,
+            "limiter": "valu",
+            "valu_busy_pmc": full_pmc.get("valu_busy"),
+            "note": "HBM-far by design (8 layered iterations over LDS-resident soft bits); the limiter is VALU issue: "
+                    "valu_busy_pmc = SQ_ACTIVE_INST_VALU x 4 / (1,024 SIMDs x kernel cycles) of this kernel on this "
+                    "workload, traffic = PMC FETCH + WRITE bytes per launch (profiles/r03c_ldpc_full_pmc.json)",
         },
         "cpu_baseline": cpu,
     }
