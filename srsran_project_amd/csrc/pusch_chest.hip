@@ -210,11 +210,17 @@ __device__ __forceinline__ uint32_t dmrs_words(const chest_args& a, uint32_t (*s
   return 12u * a.prb_lo - 32 * w_first;
 }
 
+// 1,024 threads (16 waves) per (grid, rx port), two pilots per thread: with 256 threads and seven pilots each the
+// 256-workgroup launch ran 4 waves per CU, every thread waiting out its load chains (PMC: 0.75 of wave time
+// waiting, VALU busy 0.09)
+constexpr int CFO_THREADS = 1024;
+constexpr int CFO_PPT     = CH_MAXPIL / CFO_THREADS;
+
 // One workgroup per (grid, rx port): EPRE over every received DM-RS RE and the CFO from the first two DM-RS
 // symbols over every layer of every CDM group (preprocess_pilots_and_estimate_cfo, :390-445), for the
 // slice workgroups of the port.
 template <bool MULTI>
-__global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a_in, chest_items items)
+__global__ __launch_bounds__(CFO_THREADS) void chest_cfo_kernel(chest_args a_in, chest_items items)
 {
   const chest_args& a = item_args<MULTI>(a_in, items);
   if (MULTI && blockIdx.x >= a.nof_ports) {
@@ -235,8 +241,8 @@ __global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a_in, 
   auto rxv = [&](int gg, int d, uint32_t m) { return from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + gg]); };
   float epre = 0;
 #pragma unroll
-  for (int k = 0; k < CS_PPT; ++k) {
-    const uint32_t m = tid + k * CS_THREADS;
+  for (int k = 0; k < CFO_PPT; ++k) {
+    const uint32_t m = tid + k * CFO_THREADS;
     if (m < npil) {
       // compile-time bounds (CDM groups of type 1, DM-RS symbols): every load of the thread is issued
       // before the first is used
@@ -256,8 +262,8 @@ __global__ __launch_bounds__(CS_THREADS) void chest_cfo_kernel(chest_args a_in, 
   float4 acc = make_float4(0, 0, 0, 0); // (re, im) of CDM group 0, then 1
   if (nds >= 2) {
 #pragma unroll
-    for (int k = 0; k < CS_PPT; ++k) {
-      const uint32_t m = tid + k * CS_THREADS;
+    for (int k = 0; k < CFO_PPT; ++k) {
+      const uint32_t m = tid + k * CFO_THREADS;
       if (m < npil) {
 #pragma unroll
         for (int vv = 0; vv < CH_MAXL; ++vv) {
@@ -549,9 +555,18 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
   const uint32_t      nsl  = a.L * a.nof_lse;
   const float*        crow = a.corr + static_cast<uint64_t>(gp) * nsl * N;
   for (uint32_t k = tid; k < N; k += ST_THREADS) {
+    // compile-time bound (every slice's load in flight at once), sum in slice order
+    float v[CH_MAXL * CH_MAXDMRS];
+#pragma unroll
+    for (uint32_t sl = 0; sl < CH_MAXL * CH_MAXDMRS; ++sl) {
+      v[sl] = sl < nsl ? crow[static_cast<uint64_t>(sl) * N + k] : 0.0f;
+    }
     float c = 0;
-    for (uint32_t sl = 0; sl < nsl; ++sl) {
-      c += crow[static_cast<uint64_t>(sl) * N + k];
+#pragma unroll
+    for (uint32_t sl = 0; sl < CH_MAXL * CH_MAXDMRS; ++sl) {
+      if (sl < nsl) {
+        c += v[sl];
+      }
     }
     corr[k] = c;
   }
@@ -568,17 +583,32 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
   const float2*   filt  = a.filt + static_cast<uint64_t>(gp) * a.L * a.nof_lse * npil;
   float           noise0 = 0, noise1 = 0;
   const float     sf     = a.beta / static_cast<float>(a.nof_lse);
+  const int nlse = static_cast<int>(a.nof_lse);
   for (uint32_t m = tid; m < npil; m += ST_THREADS) {
-    for (int g = 0; g < static_cast<int>(a.ncdm); ++g) {
+    // compile-time bounds on CDM groups, layers, LSE symbols and DM-RS symbols: every load of an iteration is
+    // issued before the first is used (the runtime-bounded loops waited one memory latency per load)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if (g >= static_cast<int>(a.ncdm)) {
+        continue;
+      }
       const int v0 = 2 * g, v1 = min(2 * g + 2, L);
       float2    sc0 = make_float2(0, 0), sc1 = make_float2(0, 0);
-      for (int v = v0; v < v1; ++v) {
+#pragma unroll
+      for (int vi = 0; vi < 2; ++vi) {
+        const int v = v0 + vi;
+        if (v >= v1) {
+          continue;
+        }
         const float2* fv = filt + static_cast<uint64_t>(v) * a.nof_lse * npil + m;
         float2        t  = cscale(fv[0], sf);
-        for (int s = 1; s < static_cast<int>(a.nof_lse); ++s) {
-          t = cadd(cscale(fv[static_cast<uint64_t>(s) * npil], sf), t);
+#pragma unroll
+        for (int s = 1; s < CH_MAXDMRS; ++s) {
+          if (s < nlse) {
+            t = cadd(cscale(fv[static_cast<uint64_t>(s) * npil], sf), t);
+          }
         }
-        if (v == v0) {
+        if (vi == 0) {
           sc0 = t;
         } else {
           sc1 = t;
@@ -587,7 +617,7 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
 #pragma unroll
       for (int d = 0; d < CH_MAXDMRS; ++d) {
         if (d >= nds) {
-          break;
+          continue;
         }
         float2 pred = cmul(sc0, pilot(a, seq, bit0, d, v0, m));
         if (rotate) {
@@ -757,7 +787,7 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   if (e != hipSuccess) {
     return e;
   }
-  hipLaunchKernelGGL(chest_cfo_kernel<false>, dim3(nb), dim3(CS_THREADS), 0, stream, a, chest_items{});
+  hipLaunchKernelGGL(chest_cfo_kernel<false>, dim3(nb), dim3(CFO_THREADS), 0, stream, a, chest_items{});
   e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
@@ -814,7 +844,7 @@ hipError_t launch_chest_items(const chest_items&                       items,
   hipLaunchKernelGGL(chest_seq_kernel<true>, dim3(1, 1, nof_items), dim3(CS_THREADS), 0, stream, none, items);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(chest_cfo_kernel<true>, dim3(max_ports, 1, nof_items), dim3(CS_THREADS), 0, stream, none,
+    hipLaunchKernelGGL(chest_cfo_kernel<true>, dim3(max_ports, 1, nof_items), dim3(CFO_THREADS), 0, stream, none,
                        items);
     e = hipGetLastError();
   }
