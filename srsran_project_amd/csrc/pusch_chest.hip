@@ -642,6 +642,52 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
   }
   const float4 tot = block_sum4(make_float4(noise0, noise1, 0, 0), red);
 
+  // Peak search of estimate_ta_correlation (time_alignment_estimator_dft_impl.cpp:248-310) over wave 0 instead
+  // of a serial scan by one thread: the first maximum (strict >) of corr[0, max_taps) and of
+  // corr[N - max_taps, N), each lane scanning a strided subset and the wave keeping the larger value or, on
+  // equal values, the smaller index.
+  int   i_d = 0, i_a = 0;
+  float v_d = 0.0f, v_a = 0.0f;
+  if (tid < 64) {
+    const int max_taps = a.ta_max_taps;
+    float     bd = -__builtin_inff(), ba = -__builtin_inff();
+    int       id = 0x7fffffff, ia = 0x7fffffff;
+    for (int i = static_cast<int>(tid); i < max_taps; i += 64) {
+      const float cd = corr[i];
+      const float ca = corr[N - max_taps + i];
+      if (i == 0 || cd > bd) {
+        bd = cd;
+        id = i;
+      }
+      if (i == 0 || ca > ba) {
+        ba = ca;
+        ia = i;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float obd = __shfl_xor(bd, o), oba = __shfl_xor(ba, o);
+      const int   oid = __shfl_xor(id, o), oia = __shfl_xor(ia, o);
+      if (obd > bd || (obd == bd && oid < id)) {
+        bd = obd;
+        id = oid;
+      }
+      if (oba > ba || (oba == ba && oia < ia)) {
+        ba = oba;
+        ia = oia;
+      }
+    }
+    i_d = id;
+    v_d = bd;
+    i_a = ia;
+    v_a = ba;
+    if (max_taps <= 0) { // empty ranges (never for a valid configuration): the scan's initial values
+      i_d = i_a = 0;
+      v_d = corr[0];
+      v_a = corr[min(N - max_taps, static_cast<uint32_t>(CH_TA_MAXN - 1))];
+    }
+  }
+
   if (tid == 0) {
     float nsum = 0;
     nsum += (isnormal(tot.x) ? tot.x : 0.0f);
@@ -654,19 +700,7 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
     }
     // estimate_ta_correlation (time_alignment_estimator_dft_impl.cpp:248-310).
     const int max_taps = a.ta_max_taps;
-    int       i_d = 0, i_a = 0;
-    float     v_d = corr[0], v_a = corr[N - max_taps];
-    for (int i = 1; i < max_taps; ++i) {
-      if (corr[i] > v_d) {
-        v_d = corr[i];
-        i_d = i;
-      }
-      if (corr[N - max_taps + i] > v_a) {
-        v_a = corr[N - max_taps + i];
-        i_a = i;
-      }
-    }
-    int idx = -(max_taps - i_a);
+    int       idx      = -(max_taps - i_a);
     if (v_d >= v_a) {
       idx = i_d;
     }
