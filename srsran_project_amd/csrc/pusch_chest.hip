@@ -317,8 +317,10 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
     return;
   }
   __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
+  // one pilot buffer: the FD filter's input, then (after a barrier) the smoothed pilots the interpolation
+  // reads -- a second 16.6 KiB buffer held the workgroup at 35.5 KiB of LDS, four per CU (4 waves per SIMD)
   __shared__ float2   enl_in[CH_MAXPIL + 2 * CH_MAXV];
-  __shared__ float2   enl_out[CH_MAXPIL + 2 * CH_MAXV];
+  float2* const       enl_out = enl_in;
   __shared__ float    red[4 * 16];
   __shared__ int      s_has_cfo;
   __shared__ float2   s_rot[CH_MAXDMRS];
@@ -453,6 +455,7 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
   }
 
   // RSRP share, store the smoothed pilots, stage them for the interpolation.
+  __syncthreads(); // every FIR read of enl_in is done before the smoothed pilots overwrite it
   float   rsrp = 0;
   float2* filt = a.filt + (static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice) * npil;
 #pragma unroll
