@@ -118,6 +118,8 @@ typedef struct srs_amd_pusch_processor_result {
   int32_t                      csi_part1_status; /* SRS_AMD_UCI_*; 0 without CSI part 1 */
   int32_t                      csi_part2_status; /* SRS_AMD_UCI_*; 0 without CSI part 2 */
   uint32_t                     nof_csi_part2;    /* CSI part 2 payload bits (from the decoded CSI part 1) */
+  float                        cfo_hz;           /* CFO of the best-SNR port (channel_estimation.h:273-276); NaN:
+                                                    none estimated (one DM-RS symbol or CFO compensation off) */
 } srs_amd_pusch_processor_result;
 
 typedef struct srs_amd_pusch_processor      srs_amd_pusch_processor;
@@ -159,6 +161,11 @@ typedef struct srs_amd_pusch_intermediates {
   /* CSI part 2 payloads: rows of csi_part2_stride bytes (at least the largest size the description allows) */
   uint8_t*                  d_csi_part2;
   uint32_t                  csi_part2_stride;
+  /* per-codeblock LDPC iteration counts [grid][C] (C = the plan's codeblocks, contiguous), in codeblock order as
+     pusch_decoder_impl fills cb_stats (pusch_decoder_impl.cpp:370-375, 414): the count of the decoding that passed
+     the codeblock CRC, or -1 when it failed (the reference's statistic is then nof_ldpc_iterations); codeblocks OK
+     from an earlier transmission report their soft-buffer flag value.  NULL: not returned. */
+  int32_t*                  d_cb_iterations;
 } srs_amd_pusch_intermediates;
 
 /* DEVICE, asynchronous: nof_grids received grids cbf16 [grid][port][14][nof_subc]
@@ -180,23 +187,49 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
 
 /* One PUSCH PDU of a slot (srs_amd_pusch_process_slot). */
 typedef struct srs_amd_pusch_slot_pdu {
-  const srs_amd_pusch_processor_plan* plan;      /* a plan of this processor */
-  uint32_t                            grid;      /* index of the received grid the PDU occupies in d_grids */
-  uint32_t                            reserved;  /* 0 */
-  uint64_t                            tb_offset; /* byte offset of its tbs / 8 transport-block bytes in d_tbs */
+  const srs_amd_pusch_processor_plan* plan;       /* a plan of this processor */
+  uint32_t                            grid;       /* index of the received grid the PDU occupies in d_grids */
+  uint32_t                            cb_offset;  /* index of its first codeblock in io->d_cb_iterations */
+  uint64_t                            tb_offset;  /* byte offset of its tbs / 8 transport-block bytes in d_tbs */
+  int8_t*                             d_soft;     /* DEVICE HARQ soft buffer (the plan's soft_buffer_bytes), kept by
+                                                     the caller between transmissions; NULL: new data, not kept */
+  uint64_t                            uci_offset; /* byte offset of its UCI payload row in io->d_uci: HARQ-ACK
+                                                     (nof_harq_ack) | CSI part 1 (nof_csi_part1) | CSI part 2 (the
+                                                     largest size its description allows), one bit per byte */
 } srs_amd_pusch_slot_pdu;
+
+/* Optional outputs of srs_amd_pusch_process_slot_ex (any member NULL: not returned). */
+typedef struct srs_amd_pusch_slot_io {
+  int32_t* d_cb_iterations; /* per-codeblock iteration counts (as srs_amd_pusch_intermediates), PDU i's C values from
+                               pdus[i].cb_offset */
+  uint8_t* d_uci;           /* UCI payload rows, PDU i's at pdus[i].uci_offset */
+} srs_amd_pusch_slot_io;
 
 /* DEVICE, asynchronous: every PUSCH PDU of a slot -- several UEs on disjoint PRBs of one received grid (or of
  * several grids), each with its own PRB range, layers, modulation, DM-RS symbols and scrambling, rnti / n_id
- * and code rate -- as ONE launch sequence: one channel-estimator sequence over all PDUs (per-PDU argument
- * blocks), one fused equalizer-demapper launch per (ports, layers, equalizer) kind, one slot decoder sequence
- * (srs_amd_pusch_decode_slot) and one result launch.  What uplink_processor_impl::process_pusch
+ * and code rate -- as ONE launch sequence.  What uplink_processor_impl::process_pusch
  * (uplink_processor_impl.cpp:270-326) does by calling pusch_processor_impl::process once per PDU.  Result of
  * pdus[i] in d_results[i], transport block at d_tbs + pdus[i].tb_offset; per PDU identical to
- * srs_amd_pusch_process_batch on that PDU's grid.  Scope: new transmissions (pdu.new_data = 1; HARQ
- * retransmissions go through srs_amd_pusch_process_batch with caller soft buffers), no transform precoding,
- * every plan covered by the fused estimator-equalizer (1, 2 or 4 receive ports, layers <= ports), plans
- * created for the same nof_subc. */
+ * srs_amd_pusch_process_batch on that PDU's grid.
+ * The new-data, UCI-free, CP-OFDM PDUs without a soft buffer (the bulk of a slot) run fused: one channel-estimator
+ * sequence over all of them (per-PDU argument blocks), one fused equalizer-demapper launch per (ports, layers,
+ * equalizer) kind, one slot decoder sequence (srs_amd_pusch_decode_slot) and one result launch.  Every other PDU
+ * -- HARQ retransmissions and new data kept in a soft buffer (d_soft), UCI on PUSCH (HARQ-ACK, CSI part 1, CSI
+ * part 2), transform precoding -- runs in the same call on the same stream through the batch chain of its plan
+ * (srs_amd_pusch_process_batch with one grid), before the fused group.  Plans created for the same nof_subc.
+ * A PDU with CSI part 2 makes the call synchronise the stream once (its size comes from the decoded CSI part 1). */
+int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
+                                  const srs_amd_pusch_slot_pdu*   pdus,
+                                  uint32_t                        nof_pdus,
+                                  const uint32_t*                 d_grids,
+                                  uint64_t                        grid_stride,
+                                  uint32_t                        nof_grids,
+                                  uint8_t*                        d_tbs,
+                                  srs_amd_pusch_processor_result* d_results,
+                                  const srs_amd_pusch_slot_io*    io,
+                                  void*                           stream);
+
+/* srs_amd_pusch_process_slot_ex without the optional outputs. */
 int srs_amd_pusch_process_slot(srs_amd_pusch_processor*        proc,
                                const srs_amd_pusch_slot_pdu*   pdus,
                                uint32_t                        nof_pdus,
@@ -206,6 +239,17 @@ int srs_amd_pusch_process_slot(srs_amd_pusch_processor*        proc,
                                uint8_t*                        d_tbs,
                                srs_amd_pusch_processor_result* d_results,
                                void*                           stream);
+
+/* Moves a plan to another slot (pdu_t::slot): the DM-RS sequences are the only per-slot quantity of a PDU
+ * configuration, so a caller keeps one plan per configuration across slots (plan creation uploads tables and
+ * synchronises; this does not).  Not while a call that uses the plan is being issued on another thread. */
+int srs_amd_pusch_processor_plan_set_slot(srs_amd_pusch_processor_plan* plan, uint32_t numerology,
+                                          uint32_t slot_index);
+
+/* The plan's transport block and segmentation: codeblocks C and the CSI part 2 payload row length
+ * (srs_amd_pusch_slot_pdu::uci_offset rows: nof_harq_ack + nof_csi_part1 + max_csi_part2 bytes). */
+int srs_amd_pusch_processor_plan_info(const srs_amd_pusch_processor_plan* plan, uint32_t* nof_codeblocks,
+                                      uint32_t* max_csi_part2, uint64_t* soft_buffer_bytes);
 
 /* HOST, synchronous: one grid [port][14][nof_subc]; tb gets tbs/8 bytes;
  * soft_buffer: HOST HARQ buffer of soft_buffer_bytes (or NULL for new data only). */

@@ -107,32 +107,36 @@ public:
 
   unsigned get_max_supported_buff_size() const override { return cfg.max_buffer_size; }
 
-  // The whole operation runs here (the GPU call is synchronous); a failure is reported by the dequeue.
+  // The whole operation runs here (the GPU call is synchronous).  A failed operation (encoding or rate-matching
+  // error, transport block size mismatch) never stalls the reference's driver, which calls dequeue_operation until
+  // it returns true (pdsch_encoder_hw_impl.cpp:150-160): the error is logged and the operation dequeues the
+  // configured codeword length as zeros.
   bool enqueue_operation(span<const uint8_t> data, span<const uint8_t> /*aux*/, unsigned cb_index) override
   {
     if (cb_index >= MAX_CBS) {
-      return false;
+      log_error("enqueue_operation", "codeblock index beyond the queue");
+      return true;
     }
     const hal::hw_pdsch_encoder_configuration& c = ops[cb_index];
-    ready[cb_index]                              = false;
+    ready[cb_index]                              = true;
     out[cb_index].clear();
     if (!c.cb_mode) {
       // TB mode: TB CRC, segmentation, CB CRCs, LDPC encoding and rate matching in one C-ABI call
       const srs_amd_sch_plan p = plan_of(c);
+      out[cb_index].assign(p.cw_length, 0);
       if (data.size() * 8 != p.tbs) {
         log_error("enqueue_operation", "transport block size differs from the configuration");
         return true;
       }
-      out[cb_index].resize(p.cw_length);
       if (srs_amd_pdsch_encode(tb_enc, out[cb_index].data(), data.data(), &p) != SRS_AMD_OK) {
         log_error("PDSCH encoding", srs_amd_last_error());
-        return true;
+        std::fill(out[cb_index].begin(), out[cb_index].end(), 0);
       }
-      ready[cb_index] = true;
       return true;
     }
     // CB mode: the codeblock's K - F message bits (CRCs attached by the reference's segmenter), then F filler
     // bits (zero) -- LDPC encoding of K bits and rate matching to E = rm_length bits
+    out[cb_index].assign(c.rm_length, 0);
     const unsigned K = message_length(c.base_graph_index, c.lifting_size);
     const unsigned N = (c.base_graph_index == ldpc_base_graph_type::BG1 ? 66 : 50) * c.lifting_size;
     const unsigned k = K - c.nof_filler_bits;
@@ -159,22 +163,27 @@ public:
       log_error("rate matching", srs_amd_last_error());
       return true;
     }
-    out[cb_index].resize(c.rm_length);
     for (unsigned i = 0; i != c.rm_length; ++i) {
       out[cb_index][i] = (packed[i >> 3] >> (7 - (i & 7))) & 1u;
     }
-    ready[cb_index] = true;
     return true;
   }
 
-  // data: the codeword (TB mode) or the rate-matched codeblock (CB mode), one bit per byte; aux: packed.
+  // data: the codeword (TB mode) or the rate-matched codeblock (CB mode), one bit per byte; aux: packed.  Returns
+  // false only for an operation that was never enqueued; a length mismatch is logged and dequeues zeros.
   bool dequeue_operation(span<uint8_t> data, span<uint8_t> aux, unsigned cb_index) override
   {
-    if (cb_index >= MAX_CBS || !ready[cb_index] || data.size() != out[cb_index].size()) {
-      if (cb_index < MAX_CBS && ready[cb_index]) {
-        log_error("dequeue_operation", "output length differs from the configured codeword");
-      }
+    if (cb_index >= MAX_CBS) { // refused at the enqueue (logged there): zeros
+      std::fill(data.begin(), data.end(), 0);
+      std::fill(aux.begin(), aux.end(), 0);
+      return true;
+    }
+    if (!ready[cb_index]) {
       return false;
+    }
+    if (data.size() != out[cb_index].size()) {
+      log_error("dequeue_operation", "output length differs from the configured codeword");
+      out[cb_index].assign(data.size(), 0);
     }
     std::memcpy(data.data(), out[cb_index].data(), data.size());
     std::fill(aux.begin(), aux.end(), 0);

@@ -242,8 +242,9 @@ public:
       fail("configure_operation", "too many codeblocks");
       return;
     }
-    cfg[cb_index] = config;
-    nof_cbs       = config.nof_segments;
+    cfg[cb_index]     = config;
+    abs_ids[cb_index] = config.absolute_cb_id;
+    nof_cbs           = config.nof_segments;
     bool fresh    = false;
     if (!failed && !harq->lookup(config.absolute_cb_id, cb_index, nof_cbs, config.new_data, tb_base, fresh)) {
       fail("HARQ", "no contiguous HARQ rows left for the transport block");
@@ -259,7 +260,7 @@ public:
   bool enqueue_operation(span<const int8_t> data, span<const int8_t> /*aux*/, unsigned cb_index) override
   {
     if (cb_index >= MAX_CBS) {
-      return false;
+      return true; // configure_operation marked the transport block failed: reported as CRC failures
     }
     if (flushed) {
       return false;
@@ -343,6 +344,15 @@ private:
     return rc == SRS_AMD_OK;
   }
 
+  // Returns the rows this transport block mapped fresh to the pool (their reset never ran).
+  void unmap_new_rows()
+  {
+    for (unsigned r : new_rows) {
+      harq->release(abs_ids[r]);
+    }
+    new_rows.clear();
+  }
+
   bool grow_staging(size_t n)
   {
     if (n <= staging_cap) {
@@ -376,6 +386,7 @@ private:
   {
     flushed = true;
     if (failed || !hip_ok(hipSetDevice(device), "hipSetDevice")) {
+      unmap_new_rows();
       return;
     }
     for (unsigned r = 0; r != nof_cbs; ++r) {
@@ -385,10 +396,16 @@ private:
     bool ok = hip_ok(hipMemcpyAsync(d_llrs, h_llrs, staged, hipMemcpyHostToDevice, stream), "H2D LLRs") &&
               hip_ok(hipMemcpyAsync(d_arrays, h_arrays, sizeof(uint32_t) * 2 * MAX_CBS, hipMemcpyHostToDevice, stream),
                      "H2D arrays");
-    // freshly mapped HARQ rows start as a cleared rx_buffer
+    // freshly mapped HARQ rows start as a cleared rx_buffer; rows whose reset was not issued are unmapped (a
+    // retransmission must not combine onto a previous occupant's soft bits)
+    bool cleared = ok;
     for (unsigned r : new_rows) {
-      ok = ok && hip_ok(hipMemsetAsync(harq->row(tb_base + r), 0, ROW, stream), "HARQ row reset");
+      cleared = cleared && hip_ok(hipMemsetAsync(harq->row(tb_base + r), 0, ROW, stream), "HARQ row reset");
     }
+    if (!cleared) {
+      unmap_new_rows();
+    }
+    ok = ok && cleared;
     for (unsigned a = 0; ok && a < nof_cbs;) {
       if (!enqueued[a]) {
         ++a;
@@ -438,6 +455,7 @@ private:
   srs_amd_ldpc_decoder*               dec    = nullptr;
   srs_amd_crc_calculator*             crc[4] = {};  // CRC24A, CRC24B, CRC16 (index 2), spare
   hal::hw_pusch_decoder_configuration cfg[MAX_CBS] = {};
+  unsigned                            abs_ids[MAX_CBS] = {};
   bool                                enqueued[MAX_CBS] = {};
   uint32_t                            offsets[MAX_CBS]  = {};
   uint32_t                            lengths[MAX_CBS]  = {};

@@ -5,7 +5,6 @@
 #include "srsran_amd/ldpc.h"
 
 #include <cstdio>
-#include <cstdlib>
 
 using namespace srsran;
 
@@ -14,17 +13,13 @@ namespace {
 class ldpc_decoder_hip : public ldpc_decoder
 {
 public:
-  ldpc_decoder_hip(int arith, bool force_decoding, int device)
-  {
-    if (srs_amd_ldpc_decoder_create(&dec, arith, force_decoding ? 1 : 0, device) != SRS_AMD_OK) {
-      std::fprintf(stderr, "ldpc_decoder_hip: %s\n", srs_amd_last_error());
-      std::abort();
-    }
-  }
+  explicit ldpc_decoder_hip(srs_amd_ldpc_decoder* dec_) : dec(dec_) {}
   ~ldpc_decoder_hip() override { srs_amd_ldpc_decoder_destroy(dec); }
 
   // ldpc_decoder_impl.cpp:55 semantics: trimmed input, CRC early stop, nullopt without a CRC pass (or always
-  // nullopt without a CRC calculator, as the reference returns after max_iterations).
+  // nullopt without a CRC calculator, as the reference returns after max_iterations).  A failed decode (an invalid
+  // configuration the reference would assert on, or a HIP runtime error) is logged and reported as "no CRC pass":
+  // the gNB keeps running and the codeblock counts as failed (HARQ retransmission).
   std::optional<unsigned> decode(bit_buffer&                      output,
                                  span<const log_likelihood_ratio> input,
                                  crc_calculator*                  crc,
@@ -38,8 +33,8 @@ public:
                                        reinterpret_cast<const int8_t*>(input.data()), input.size(),
                                        crc ? static_cast<int>(crc->get_generator_poly()) : SRS_AMD_NO_CRC, &c, &iters);
     if (rc != SRS_AMD_OK) {
-      std::fprintf(stderr, "ldpc_decoder_hip: %s\n", srs_amd_last_error());
-      std::abort(); // the reference asserts on the same invalid configurations
+      std::fprintf(stderr, "ldpc_decoder_hip: decode failed (reported as a CRC failure): %s\n", srs_amd_last_error());
+      return std::nullopt;
     }
     if (iters < 0) {
       return std::nullopt;
@@ -55,7 +50,17 @@ class ldpc_decoder_factory_hip : public ldpc_decoder_factory
 {
 public:
   ldpc_decoder_factory_hip(int arith_, bool force_, int device_) : arith(arith_), force(force_), device(device_) {}
-  std::unique_ptr<ldpc_decoder> create() override { return std::make_unique<ldpc_decoder_hip>(arith, force, device); }
+  // nullptr when the decoder cannot be created (no device, out of memory), as the reference's factories report a
+  // creation failure; the error is logged.
+  std::unique_ptr<ldpc_decoder> create() override
+  {
+    srs_amd_ldpc_decoder* dec = nullptr;
+    if (srs_amd_ldpc_decoder_create(&dec, arith, force ? 1 : 0, device) != SRS_AMD_OK) {
+      std::fprintf(stderr, "ldpc_decoder_hip: decoder creation failed: %s\n", srs_amd_last_error());
+      return nullptr;
+    }
+    return std::make_unique<ldpc_decoder_hip>(dec);
+  }
 
 private:
   int  arith;

@@ -92,6 +92,60 @@ int srs_ref_hw_pdsch_encode(int            device,
   return 0;
 }
 
+/* A failed PDSCH encoding operation must not stall the reference's driver, which calls dequeue_operation until it
+ * returns true (pdsch_encoder_hw_impl.cpp:150-160): the plug-in is handed a transport block whose size differs from
+ * its configuration (TB mode) and a codeblock shorter than K - F bits (CB mode).  Returns 0 when both dequeues
+ * return true on the first call with the configured length of zeros, a negative step number otherwise. */
+int srs_ref_hw_pdsch_enc_forced_failure(int device)
+{
+  for (int cb_mode = 0; cb_mode != 2; ++cb_mode) {
+    hip::pdsch_enc_accelerator_config acc;
+    acc.device   = device;
+    acc.cb_mode  = cb_mode != 0;
+    auto factory = hip::create_hip_pdsch_enc_acc_factory(acc);
+    auto enc     = factory->create();
+    hal::hw_pdsch_encoder_configuration c{};
+    c.nof_tb_bits        = 8 * 1000;
+    c.nof_tb_crc_bits    = 24;
+    c.base_graph_index   = ldpc_base_graph_type::BG1;
+    c.modulation         = modulation_scheme::QPSK;
+    c.nof_segments       = 1;
+    c.nof_short_segments = 0;
+    c.rv                 = 0;
+    c.cw_length_a        = 0;
+    c.cw_length_b        = 17000;
+    c.lifting_size       = 384;
+    c.Ncb                = 66 * 384;
+    c.Nref               = 66 * 384;
+    c.nof_segment_bits   = 8024;
+    c.nof_filler_bits    = 22 * 384 - 8024;
+    c.rm_length          = 17000;
+    c.cb_mode            = cb_mode != 0;
+    enc->reserve_queue();
+    enc->configure_operation(c, 0);
+    std::vector<uint8_t> tb(cb_mode ? 10 : 999, 0x5a); // TB one byte short / CB far shorter than K - F
+    if (!enc->enqueue_operation(tb, {}, 0)) {
+      return -1 - 10 * cb_mode;
+    }
+    std::vector<uint8_t> cw(17000, 1), packed((17000 + 7) / 8, 0xff);
+    if (!enc->dequeue_operation(cw, packed, 0)) {
+      return -2 - 10 * cb_mode;
+    }
+    for (uint8_t b : cw) {
+      if (b != 0) {
+        return -3 - 10 * cb_mode;
+      }
+    }
+    for (uint8_t b : packed) {
+      if (b != 0) {
+        return -4 - 10 * cb_mode;
+      }
+    }
+    enc->free_queue();
+  }
+  return 0;
+}
+
 /* ofdm_slot_modulator_impl / ofdm_slot_demodulator_impl of one port with the MI355X dft_processor (layouts as
  * srs_ref_ofdm_modulate_slot / srs_ref_ofdm_demodulate_slot); -1 when the adapter refuses the DFT size. */
 int srs_ref_hip_ofdm_modulate_slot(int             device,

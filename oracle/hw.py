@@ -34,6 +34,8 @@ def lib():
         f, d = ctypes.c_float, ctypes.c_double
         L.srs_ref_hw_pdsch_encode.restype = i
         L.srs_ref_hw_pdsch_encode.argtypes = [i, i, P, u] + [u] * 6 + [P]
+        L.srs_ref_hw_pdsch_enc_forced_failure.restype = i
+        L.srs_ref_hw_pdsch_enc_forced_failure.argtypes = [i]
         L.srs_ref_hip_ofdm_modulate_slot.restype = i
         L.srs_ref_hip_ofdm_modulate_slot.argtypes = [i, u, u, u, i, f, d, u, P, P]
         L.srs_ref_hip_ofdm_demodulate_slot.restype = i

@@ -87,6 +87,7 @@ from .pusch_processor import (  # noqa: F401
     PuschProcessorConfig,
     PuschSlot,
     PuschSlotPdu,
+    PuschSlotIo,
     PuschProcessorPlan,
     PuschProcessorResult,
     UciPart2SizeDescription,

@@ -237,6 +237,16 @@ struct pinned_stage {
     used = e == hipSuccess;
     return e;
   }
+  // Copies rows of `width` bytes (consecutive in the stage) to device rows dpitch bytes apart.
+  hipError_t upload_rows(void* d, size_t dpitch, size_t width, size_t rows, hipStream_t s)
+  {
+    hipError_t e = hipMemcpy2DAsync(d, dpitch, h, width, width, rows, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+      e = hipEventRecord(done, s);
+    }
+    used = e == hipSuccess;
+    return e;
+  }
 };
 
 inline size_t align_up(size_t n, size_t a)

@@ -22,6 +22,7 @@
 #include "ldpc_codec_internal.h"
 #include "ldpc_common.h"
 #include "rate_matching_common.h"
+#include "pusch_processor_args.h"
 #include "sch_args.h"
 #include <cstring>
 #include <algorithm>
@@ -260,6 +261,8 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
                        const int8_t*                       d_llrs,
                        uint8_t*                            d_tbs,
                        srs_amd_pusch_decoder_result*       d_results,
+                       const uint32_t*                     cb_offsets,
+                       int32_t*                            d_cb_iterations,
                        hipStream_t                         stream)
 {
   // Z = 384 rows: one uniform launch per (BG, CRC, bounded prefix) -- the compile-time Z = 384 kernels,
@@ -352,7 +355,7 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
       segOff.resize(p->nof_segments);
       (void)srs_amd_sch_plan_segments(p, segE.data(), segOff.data());
       tds[u] = tb_desc{ues[u].tb_offset, row,         p->nof_segments, p->cb_info_bits, p->tbs, p->nof_tb_crc_bits,
-                       p->zero_pad,       (p->segment_length + 7) / 8, 0};
+                       p->zero_pad,       (p->segment_length + 7) / 8, cb_offsets ? cb_offsets[u] : 0u};
       for (uint32_t r = 0; r < p->nof_segments; ++r, ++row) {
         row_E[row]   = segE[r];
         row_in[row]  = static_cast<uint32_t>(ues[u].llr_offset) + segOff[r];
@@ -516,7 +519,7 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   a.soft           = nullptr;
   a.tbs            = d_tbs;
   a.results        = d_results;
-  a.cb_iterations  = nullptr;
+  a.cb_iterations  = cb_offsets != nullptr ? d_cb_iterations : nullptr;
   a.crc24a_table   = crc_device_table(d->crc[1]);
   a.acc            = d->tb_acc.as<uint32_t>();
   a.msg_stride     = M;
@@ -663,24 +666,8 @@ int srs_amd_pusch_decode_slot(srs_amd_pusch_decoder*              dec,
                               srs_amd_pusch_decoder_result*       d_results,
                               void*                               stream)
 {
-  if (dec == nullptr || cfg == nullptr) {
-    return fail(SRS_AMD_EINVAL, "null argument");
-  }
-  if (cfg->nof_ldpc_iterations == 0) {
-    return fail(SRS_AMD_EINVAL, "The number of LDPC iterations must be positive.");
-  }
-  if (!cfg->new_data) {
-    return fail(SRS_AMD_EINVAL, "slot decoding serves new transmissions; HARQ retransmissions go through "
-                                "srs_amd_pusch_decode_batch with the caller's soft buffers");
-  }
-  if (nof_ues == 0) {
-    return SRS_AMD_OK;
-  }
-  if (ues == nullptr || d_llrs == nullptr || d_tbs == nullptr || d_results == nullptr) {
-    return fail(SRS_AMD_EINVAL, "null buffer");
-  }
-  std::lock_guard<std::mutex> lock(dec->mtx);
-  return decode_slot_locked(dec, cfg, ues, nof_ues, d_llrs, d_tbs, d_results, static_cast<hipStream_t>(stream));
+  return srs_amd::pusch_decode_slot_ex(dec, cfg, ues, nof_ues, d_llrs, d_tbs, d_results, nullptr, nullptr,
+                                      static_cast<hipStream_t>(stream));
 }
 
 int srs_amd_pusch_decode(srs_amd_pusch_decoder*              dec,
@@ -742,3 +729,38 @@ int srs_amd_pusch_decode(srs_amd_pusch_decoder*              dec,
 }
 
 } // extern "C"
+
+int srs_amd::pusch_decode_slot_ex(srs_amd_pusch_decoder*              dec,
+                                  const srs_amd_pusch_decoder_config* cfg,
+                                  const srs_amd_pusch_ue*             ues,
+                                  uint32_t                            nof_ues,
+                                  const int8_t*                       d_llrs,
+                                  uint8_t*                            d_tbs,
+                                  srs_amd_pusch_decoder_result*       d_results,
+                                  const uint32_t*                     cb_offsets,
+                                  int32_t*                            d_cb_iterations,
+                                  hipStream_t                         stream)
+{
+  if (dec == nullptr || cfg == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (cfg->nof_ldpc_iterations == 0) {
+    return fail(SRS_AMD_EINVAL, "The number of LDPC iterations must be positive.");
+  }
+  if ((cb_offsets == nullptr) != (d_cb_iterations == nullptr)) {
+    return fail(SRS_AMD_EINVAL, "per-codeblock iterations need both the offsets and the output buffer");
+  }
+  if (!cfg->new_data) {
+    return fail(SRS_AMD_EINVAL, "slot decoding serves new transmissions; HARQ retransmissions go through "
+                                "srs_amd_pusch_decode_batch with the caller's soft buffers");
+  }
+  if (nof_ues == 0) {
+    return SRS_AMD_OK;
+  }
+  if (ues == nullptr || d_llrs == nullptr || d_tbs == nullptr || d_results == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null buffer");
+  }
+  std::lock_guard<std::mutex> lock(dec->mtx);
+  return decode_slot_locked(dec, cfg, ues, nof_ues, d_llrs, d_tbs, d_results, cb_offsets, d_cb_iterations, stream);
+}
+

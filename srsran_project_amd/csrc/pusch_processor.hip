@@ -33,11 +33,12 @@ __global__ __launch_bounds__(64) void pusch_result_kernel(pusch_result_args a)
   r.epre_db          = 10.0f * log10f(epre / static_cast<float>(P));
   r.rsrp_db          = 10.0f * log10f(rsrp / static_cast<float>(P));
   r.time_alignment_s = st[best].time_alignment_s;
+  r.cfo_hz           = st[best].cfo_hz;
   r.harq_ack_status  = (a.uci_mask & 1u) ? a.uci_status[4 * g] : 0;
   r.csi_part1_status = (a.uci_mask & 2u) ? a.uci_status[4 * g + 1] : 0;
   r.csi_part2_status = (a.uci_mask & 4u) ? a.uci_status[4 * g + 2] : 0;
   r.nof_csi_part2    = (a.uci_mask & 4u) ? static_cast<uint32_t>(a.uci_status[4 * g + 3]) : 0u;
-  a.results[g]       = r;
+  a.results[a.result_ids != nullptr ? a.result_ids[g] : g] = r;
 }
 
 hipError_t launch_pusch_result(const pusch_result_args& a, hipStream_t stream)

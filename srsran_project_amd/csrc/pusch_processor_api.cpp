@@ -38,7 +38,8 @@ struct srs_amd_pusch_processor {
   hipStream_t                    stream = nullptr; // host-call stream
   device_buffer                  estimates, stats, llrs, dec_results, host_io, slot_ports;
   stream_order                   order;
-  pinned_stage                   stage; // slot form: per-PDU port counts
+  pinned_stage                   stage;  // slot form: per-PDU port counts and result indices
+  pinned_stage                   stage2; // CSI part 2 sizes of a batch
   std::mutex                     mtx;
   bool                           fuse = true; // SRSRAN_AMD_PUSCH_FUSED=0: always expand the estimates
   ~srs_amd_pusch_processor()
@@ -430,7 +431,11 @@ void srs_amd_pusch_processor_plan_destroy(srs_amd_pusch_processor_plan* plan)
   delete plan;
 }
 
-int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
+} // extern "C"
+
+namespace {
+
+int process_batch_locked(srs_amd_pusch_processor*            proc,
                                 const srs_amd_pusch_processor_plan* plan,
                                 const uint32_t*                     d_grids,
                                 uint64_t                            grid_stride,
@@ -470,8 +475,7 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
     return fail(SRS_AMD_EINVAL, "intermediate estimate or LLR stride too small");
   }
   auto           s          = static_cast<hipStream_t>(stream);
-  std::lock_guard<std::mutex> lock(proc->mtx);
-  hipError_t                  e = hipSetDevice(proc->device);
+  hipError_t     e          = hipSetDevice(proc->device);
   if (e == hipSuccess && own_est && !fused) {
     e = proc->estimates.ensure(nof_grids * est_stride * 4);
   }
@@ -508,12 +512,19 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   if (e == hipSuccess) {
     e = proc->order.begin(s);
   }
-  if (e == hipSuccess && uci) { // after begin: a previous call on another stream may still read the statuses
-    e = hipMemsetAsync(proc->uci_status.ptr, 0, static_cast<size_t>(nof_grids) * 4 * sizeof(int32_t), s);
-  }
   if (e != hipSuccess) {
     return hip_fail(e, "PUSCH processor scratch");
   }
+  // every return from here records the completion event the next call on another stream waits for
+  call_scope scope(proc->order, nullptr, s);
+  if (uci) { // after begin: a previous call on another stream may still read the statuses
+    e = hipMemsetAsync(proc->uci_status.ptr, 0, static_cast<size_t>(nof_grids) * 4 * sizeof(int32_t), s);
+    if (e != hipSuccess) {
+      return hip_fail(e, "PUSCH processor UCI status reset");
+    }
+  }
+  int32_t* const cb_iters = io != nullptr ? io->d_cb_iterations : nullptr;
+  const uint32_t C        = plan->sch.nof_segments;
   srs_amd_chest_port_stats* st   = (io && io->d_port_stats) ? io->d_port_stats : proc->stats.as<srs_amd_chest_port_stats>();
   uint32_t*                 est  = own_est ? proc->estimates.as<uint32_t>() : io->d_estimates;
   int8_t*                   llrs = own_llrs ? proc->llrs.as<int8_t>() : io->d_llrs;
@@ -589,9 +600,21 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
   if (rc == SRS_AMD_OK && !any2) {
     rc = srs_amd_pusch_decode_batch(proc->dec, &plan->sch, &plan->dec_cfg, d_tbs, tb_stride,
                                     proc->dec_results.as<srs_amd_pusch_decoder_result>(), llrs, llr_stride, d_soft,
-                                    nullptr, nof_grids, stream);
+                                    cb_iters, nof_grids, stream);
   }
-  // grid by grid when some CSI part 2 is present: each size has its own UL-SCH geometry
+  // grid by grid when some CSI part 2 is present: each size has its own UL-SCH geometry; the sizes are uploaded
+  // once (pinned staging) into the statuses' fourth column
+  if (rc == SRS_AMD_OK && any2) {
+    e = proc->stage2.acquire(sizeof(int32_t) * nof_grids);
+    if (e == hipSuccess) {
+      for (uint32_t g = 0; g < nof_grids; ++g) {
+        *proc->stage2.at<int32_t>(sizeof(int32_t) * g) = static_cast<int32_t>(n2[g]);
+      }
+      e = proc->stage2.upload_rows(proc->uci_status.as<int32_t>() + 3, 4 * sizeof(int32_t), sizeof(int32_t),
+                                   nof_grids, s);
+    }
+    rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "CSI part 2 size upload");
+  }
   for (uint32_t g = 0; g < nof_grids && rc == SRS_AMD_OK && any2; ++g) {
     const srs_amd_sch_plan* sch = &plan->sch;
     int8_t*                 row = llrs + static_cast<uint64_t>(g) * llr_stride;
@@ -620,20 +643,12 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
                                       pay_stride, proc->uci_status.as<int32_t>() + 4 * g + 2, 4 * sizeof(int32_t), 1,
                                       stream);
       }
-      if (rc == SRS_AMD_OK) {
-        const int32_t nb = static_cast<int32_t>(n2[g]);
-        e  = hipMemcpyAsync(proc->uci_status.as<int32_t>() + 4 * g + 3, &nb, sizeof(nb), hipMemcpyHostToDevice, s);
-        rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "CSI part 2 size upload");
-        if (rc == SRS_AMD_OK) {
-          e  = hipStreamSynchronize(s); // nb lives on this stack frame
-          rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "CSI part 2 size upload");
-        }
-      }
     }
     if (rc == SRS_AMD_OK) {
       rc = srs_amd_pusch_decode_batch(proc->dec, sch, &plan->dec_cfg, d_tbs + static_cast<uint64_t>(g) * tb_stride,
                                       tb_stride, proc->dec_results.as<srs_amd_pusch_decoder_result>() + g, row,
-                                      llr_stride, d_soft ? d_soft + g * plan->soft_bytes : nullptr, nullptr, 1,
+                                      llr_stride, d_soft ? d_soft + g * plan->soft_bytes : nullptr,
+                                      cb_iters != nullptr ? cb_iters + static_cast<size_t>(g) * C : nullptr, 1,
                                       stream);
     }
   }
@@ -650,22 +665,47 @@ int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
     a.uci_status = proc->uci_status.as<int32_t>();
     a.uci_mask   = (K_ack != 0 ? 1 : 0) | (K_csi1 != 0 ? 2 : 0) | (plan->csi2 ? 4 : 0);
   }
-  e             = launch_pusch_result(a, s);
-  if (e == hipSuccess) {
-    e = proc->order.end(s);
-  }
+  e                     = launch_pusch_result(a, s);
+  const hipError_t done = scope.close();
+  e                     = e != hipSuccess ? e : done;
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_result_kernel launch");
 }
 
-int srs_amd_pusch_process_slot(srs_amd_pusch_processor*        proc,
-                               const srs_amd_pusch_slot_pdu*   pdus,
-                               uint32_t                        nof_pdus,
-                               const uint32_t*                 d_grids,
-                               uint64_t                        grid_stride,
-                               uint32_t                        nof_grids,
-                               uint8_t*                        d_tbs,
-                               srs_amd_pusch_processor_result* d_results,
-                               void*                           stream)
+} // namespace
+
+extern "C" {
+
+int srs_amd_pusch_process_batch(srs_amd_pusch_processor*            proc,
+                                const srs_amd_pusch_processor_plan* plan,
+                                const uint32_t*                     d_grids,
+                                uint64_t                            grid_stride,
+                                uint32_t                            nof_grids,
+                                uint8_t*                            d_tbs,
+                                uint32_t                            tb_stride,
+                                srs_amd_pusch_processor_result*     d_results,
+                                int8_t*                             d_soft,
+                                const srs_amd_pusch_intermediates*  io,
+                                void*                               stream)
+{
+  if (proc == nullptr || plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  std::lock_guard<std::mutex> lock(proc->mtx);
+  return process_batch_locked(proc, plan, d_grids, grid_stride, nof_grids, d_tbs, tb_stride, d_results, d_soft, io,
+                              stream);
+}
+
+
+int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
+                                  const srs_amd_pusch_slot_pdu*   pdus,
+                                  uint32_t                        nof_pdus,
+                                  const uint32_t*                 d_grids,
+                                  uint64_t                        grid_stride,
+                                  uint32_t                        nof_grids,
+                                  uint8_t*                        d_tbs,
+                                  srs_amd_pusch_processor_result* d_results,
+                                  const srs_amd_pusch_slot_io*    io,
+                                  void*                           stream)
 {
   if (proc == nullptr || (nof_pdus != 0 && pdus == nullptr)) {
     return fail(SRS_AMD_EINVAL, "null argument");
@@ -678,49 +718,80 @@ int srs_amd_pusch_process_slot(srs_amd_pusch_processor*        proc,
   }
   constexpr uint32_t STATS_STRIDE = 4; // port measurements per PDU (at most four receive ports)
   const uint32_t     nof_subc     = pdus[0].plan != nullptr ? pdus[0].plan->nof_subc : 0;
-  std::vector<size_t> llr_off(nof_pdus);
-  size_t              llr_bytes = 0;
+  int32_t* const     cb_iters     = io != nullptr ? io->d_cb_iterations : nullptr;
+  uint8_t* const     d_uci        = io != nullptr ? io->d_uci : nullptr;
+  // the fused group (new data, no UCI, CP-OFDM, no soft buffer to keep) and the PDUs of the batch chain
+  std::vector<uint32_t> fused, others;
   for (uint32_t i = 0; i != nof_pdus; ++i) {
     const srs_amd_pusch_processor_plan* pl = pdus[i].plan;
     if (pl == nullptr) {
       return fail(SRS_AMD_EINVAL, "null plan");
     }
     const uint32_t P = pl->pdu.nof_rx_ports;
-    if (!pl->fusable || P > STATS_STRIDE) {
-      return fail(SRS_AMD_EINVAL, "PDU %u: the slot form needs the fused estimator-equalizer path", i);
-    }
-    if (!pl->dec_cfg.new_data) {
-      return fail(SRS_AMD_EINVAL, "PDU %u: HARQ retransmissions go through srs_amd_pusch_process_batch", i);
-    }
-    if (pl->uci) {
-      return fail(SRS_AMD_EINVAL, "PDU %u: UCI on PUSCH goes through srs_amd_pusch_process_batch", i);
-    }
     if (pl->nof_subc != nof_subc) {
       return fail(SRS_AMD_EINVAL, "PDU %u: plans of different grid sizes", i);
     }
     if (pdus[i].grid >= nof_grids || (nof_grids > 1 && grid_stride < 14ull * nof_subc * P)) {
       return fail(SRS_AMD_EINVAL, "PDU %u: grid index or grid stride out of range", i);
     }
-    llr_off[i] = llr_bytes;
-    llr_bytes += align_up(pl->sch.cw_length, 64);
+    if (!pl->dec_cfg.new_data && pdus[i].d_soft == nullptr) {
+      return fail(SRS_AMD_EINVAL, "PDU %u: a HARQ retransmission needs its soft buffer (d_soft)", i);
+    }
+    const bool f = proc->fuse && pl->fusable && P <= STATS_STRIDE && pl->dec_cfg.new_data && !pl->uci &&
+                   pl->pdu.transform_precoding == 0 && pdus[i].d_soft == nullptr;
+    (f ? fused : others).push_back(i);
   }
   auto                        s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(proc->mtx);
-  hipError_t                  e = hipSetDevice(proc->device);
+  // 1. PDUs outside the fused group: each through its plan's batch chain on this stream
+  for (uint32_t i : others) {
+    const srs_amd_pusch_processor_plan* pl = pdus[i].plan;
+    srs_amd_pusch_intermediates         x{};
+    x.d_cb_iterations = cb_iters != nullptr ? cb_iters + pdus[i].cb_offset : nullptr;
+    if (d_uci != nullptr && pl->uci) {
+      uint8_t* row       = d_uci + pdus[i].uci_offset;
+      x.d_harq_ack       = pl->pdu.nof_harq_ack != 0 ? row : nullptr;
+      x.harq_ack_stride  = std::max<uint32_t>(pl->pdu.nof_harq_ack, 1);
+      x.d_csi_part1      = pl->pdu.nof_csi_part1 != 0 ? row + pl->pdu.nof_harq_ack : nullptr;
+      x.csi_part1_stride = std::max<uint32_t>(pl->pdu.nof_csi_part1, 1);
+      x.d_csi_part2      = pl->csi2 ? row + pl->pdu.nof_harq_ack + pl->pdu.nof_csi_part1 : nullptr;
+      x.csi_part2_stride = std::max<uint32_t>(pl->max_csi2, 1);
+    }
+    const int rc = process_batch_locked(proc, pl, d_grids + pdus[i].grid * grid_stride, grid_stride, 1,
+                                        d_tbs + pdus[i].tb_offset, std::max<uint32_t>(pl->pdu.tbs / 8, 1),
+                                        d_results + i, pdus[i].d_soft, &x, stream);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+  }
+  const uint32_t n = static_cast<uint32_t>(fused.size());
+  if (n == 0) {
+    return SRS_AMD_OK;
+  }
+  // 2. the fused group
+  std::vector<size_t> llr_off(n);
+  size_t              llr_bytes = 0;
+  for (uint32_t k = 0; k != n; ++k) {
+    llr_off[k] = llr_bytes;
+    llr_bytes += align_up(pdus[fused[k]].plan->sch.cw_length, 64);
+  }
+  const bool       subset = n != nof_pdus; // results scattered to the fused PDUs' indices
+  const size_t     o_ids  = align_up(sizeof(uint32_t) * n, 16);
+  hipError_t       e      = hipSetDevice(proc->device);
   if (e == hipSuccess) {
-    e = proc->stats.ensure(static_cast<size_t>(nof_pdus) * STATS_STRIDE * sizeof(srs_amd_chest_port_stats));
+    e = proc->stats.ensure(static_cast<size_t>(n) * STATS_STRIDE * sizeof(srs_amd_chest_port_stats));
   }
   if (e == hipSuccess) {
     e = proc->llrs.ensure(std::max<size_t>(llr_bytes, 64));
   }
   if (e == hipSuccess) {
-    e = proc->dec_results.ensure(static_cast<size_t>(nof_pdus) * sizeof(srs_amd_pusch_decoder_result));
+    e = proc->dec_results.ensure(static_cast<size_t>(n) * sizeof(srs_amd_pusch_decoder_result));
   }
   if (e == hipSuccess) {
-    e = proc->slot_ports.ensure(sizeof(uint32_t) * nof_pdus);
+    e = proc->slot_ports.ensure(o_ids + sizeof(uint32_t) * n);
   }
   if (e == hipSuccess) {
-    e = proc->stage.acquire(sizeof(uint32_t) * nof_pdus);
+    e = proc->stage.acquire(o_ids + sizeof(uint32_t) * n);
   }
   if (e == hipSuccess) {
     e = proc->order.begin(s);
@@ -731,58 +802,110 @@ int srs_amd_pusch_process_slot(srs_amd_pusch_processor*        proc,
   call_scope scope(proc->order, nullptr, s);
   auto*      st   = proc->stats.as<srs_amd_chest_port_stats>();
   auto*      llrs = proc->llrs.as<int8_t>();
-  // 1. channel estimation of every PDU (one launch sequence)
-  std::vector<chest_slot_item> citems(nof_pdus);
-  for (uint32_t i = 0; i != nof_pdus; ++i) {
-    const srs_amd_pusch_processor_plan* pl = pdus[i].plan;
-    citems[i] = chest_slot_item{&pl->chest_cfg, d_grids + pdus[i].grid * grid_stride, pl->pdu.nof_rx_ports,
-                                st + static_cast<size_t>(i) * STATS_STRIDE};
+  // 2a. channel estimation of every fused PDU (one launch sequence)
+  std::vector<chest_slot_item> citems(n);
+  for (uint32_t k = 0; k != n; ++k) {
+    const srs_amd_pusch_slot_pdu& u = pdus[fused[k]];
+    citems[k] = chest_slot_item{&u.plan->chest_cfg, d_grids + u.grid * grid_stride, u.plan->pdu.nof_rx_ports,
+                                st + static_cast<size_t>(k) * STATS_STRIDE};
   }
-  std::vector<chest_args> views(nof_pdus);
-  int rc = chest_estimate_slot_unexpanded(proc->chest, citems.data(), nof_pdus, nof_subc, stream, views.data());
+  std::vector<chest_args> views(n);
+  int rc = chest_estimate_slot_unexpanded(proc->chest, citems.data(), n, nof_subc, stream, views.data());
   if (rc != SRS_AMD_OK) {
     return rc;
   }
-  // 2. equalization, demapping and descrambling into each PDU's codeword LLR row (one launch per kernel kind)
-  std::vector<demod_slot_item> ditems(nof_pdus);
-  for (uint32_t i = 0; i != nof_pdus; ++i) {
-    ditems[i] = demod_slot_item{pdus[i].plan->demod_plan, &views[i], citems[i].d_grid, citems[i].d_stats,
-                                llrs + llr_off[i]};
+  // 2b. equalization, demapping and descrambling into each PDU's codeword LLR row (one launch per kernel kind)
+  std::vector<demod_slot_item> ditems(n);
+  for (uint32_t k = 0; k != n; ++k) {
+    ditems[k] = demod_slot_item{pdus[fused[k]].plan->demod_plan, &views[k], citems[k].d_grid, citems[k].d_stats,
+                                llrs + llr_off[k]};
   }
-  rc = pusch_demodulate_slot_fused(proc->demod, ditems.data(), nof_pdus, stream);
+  rc = pusch_demodulate_slot_fused(proc->demod, ditems.data(), n, stream);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
-  // 3. UL-SCH decoding of every transport block of the slot (srs_amd_pusch_decode_slot)
-  std::vector<srs_amd_pusch_ue> ues(nof_pdus);
-  for (uint32_t i = 0; i != nof_pdus; ++i) {
-    ues[i] = srs_amd_pusch_ue{pdus[i].plan->sch, llr_off[i], pdus[i].tb_offset};
+  // 2c. UL-SCH decoding of every transport block of the group (srs_amd_pusch_decode_slot)
+  std::vector<srs_amd_pusch_ue> ues(n);
+  std::vector<uint32_t>         cb_off(n);
+  for (uint32_t k = 0; k != n; ++k) {
+    ues[k]    = srs_amd_pusch_ue{pdus[fused[k]].plan->sch, llr_off[k], pdus[fused[k]].tb_offset};
+    cb_off[k] = pdus[fused[k]].cb_offset;
   }
-  rc = srs_amd_pusch_decode_slot(proc->dec, &pdus[0].plan->dec_cfg, ues.data(), nof_pdus, llrs, d_tbs,
-                                 proc->dec_results.as<srs_amd_pusch_decoder_result>(), stream);
+  rc = pusch_decode_slot_ex(proc->dec, &pdus[fused[0]].plan->dec_cfg, ues.data(), n, llrs, d_tbs,
+                            proc->dec_results.as<srs_amd_pusch_decoder_result>(),
+                            cb_iters != nullptr ? cb_off.data() : nullptr, cb_iters, s);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
-  // 4. per-PDU results (decoder result + CSI from the PDU's own port measurements)
-  auto* h_ports = proc->stage.at<uint32_t>(0);
-  for (uint32_t i = 0; i != nof_pdus; ++i) {
-    h_ports[i] = pdus[i].plan->pdu.nof_rx_ports;
+  // 2d. per-PDU results (decoder result + CSI from the PDU's own port measurements)
+  for (uint32_t k = 0; k != n; ++k) {
+    *proc->stage.at<uint32_t>(sizeof(uint32_t) * k)         = pdus[fused[k]].plan->pdu.nof_rx_ports;
+    *proc->stage.at<uint32_t>(o_ids + sizeof(uint32_t) * k) = fused[k];
   }
-  e = proc->stage.upload(proc->slot_ports.ptr, sizeof(uint32_t) * nof_pdus, s);
+  e = proc->stage.upload(proc->slot_ports.ptr, o_ids + sizeof(uint32_t) * n, s);
   if (e == hipSuccess) {
     pusch_result_args a{};
     a.dec_results  = proc->dec_results.as<srs_amd_pusch_decoder_result>();
     a.stats        = st;
     a.results      = d_results;
-    a.nof_grids    = nof_pdus;
+    a.nof_grids    = n;
     a.nof_ports    = 0;
     a.port_counts  = proc->slot_ports.as<uint32_t>();
     a.stats_stride = STATS_STRIDE;
+    a.result_ids   = subset ? reinterpret_cast<const uint32_t*>(proc->slot_ports.as<uint8_t>() + o_ids) : nullptr;
     e              = launch_pusch_result(a, s);
   }
   const hipError_t done = scope.close();
   e                     = e != hipSuccess ? e : done;
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_result_kernel slot launch");
+}
+
+int srs_amd_pusch_process_slot(srs_amd_pusch_processor*        proc,
+                               const srs_amd_pusch_slot_pdu*   pdus,
+                               uint32_t                        nof_pdus,
+                               const uint32_t*                 d_grids,
+                               uint64_t                        grid_stride,
+                               uint32_t                        nof_grids,
+                               uint8_t*                        d_tbs,
+                               srs_amd_pusch_processor_result* d_results,
+                               void*                           stream)
+{
+  return srs_amd_pusch_process_slot_ex(proc, pdus, nof_pdus, d_grids, grid_stride, nof_grids, d_tbs, d_results,
+                                       nullptr, stream);
+}
+
+int srs_amd_pusch_processor_plan_set_slot(srs_amd_pusch_processor_plan* plan, uint32_t numerology,
+                                          uint32_t slot_index)
+{
+  if (plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null plan");
+  }
+  if (numerology > 4 || slot_index >= (10u << numerology)) {
+    return fail(SRS_AMD_EINVAL, "invalid slot %u of numerology %u", slot_index, numerology);
+  }
+  plan->pdu.numerology       = numerology;
+  plan->pdu.slot_index       = slot_index;
+  plan->chest_cfg.numerology = numerology;
+  plan->chest_cfg.slot_index = slot_index;
+  return SRS_AMD_OK;
+}
+
+int srs_amd_pusch_processor_plan_info(const srs_amd_pusch_processor_plan* plan, uint32_t* nof_codeblocks,
+                                      uint32_t* max_csi_part2, uint64_t* soft_buffer_bytes)
+{
+  if (plan == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null plan");
+  }
+  if (nof_codeblocks != nullptr) {
+    *nof_codeblocks = plan->sch.nof_segments;
+  }
+  if (max_csi_part2 != nullptr) {
+    *max_csi_part2 = plan->csi2 ? plan->max_csi2 : 0;
+  }
+  if (soft_buffer_bytes != nullptr) {
+    *soft_buffer_bytes = plan->soft_bytes;
+  }
+  return SRS_AMD_OK;
 }
 
 int srs_amd_pusch_process(srs_amd_pusch_processor*            proc,

@@ -23,8 +23,23 @@ struct pusch_result_args {
   // CSI part 2 payload bits
   const int32_t*                      uci_status   = nullptr;
   uint32_t                            uci_mask     = 0;
+  // slot form with PDUs outside the fused group: result g goes to results[result_ids[g]]
+  const uint32_t*                     result_ids   = nullptr;
 };
 
 hipError_t launch_pusch_result(const pusch_result_args& a, hipStream_t stream);
+
+// srs_amd_pusch_decode_slot (pusch_api.cpp) with per-codeblock iteration counts: UE u's C values at
+// d_cb_iterations + cb_offsets[u] (host array; both NULL: not returned).
+int pusch_decode_slot_ex(srs_amd_pusch_decoder*              dec,
+                         const srs_amd_pusch_decoder_config* cfg,
+                         const srs_amd_pusch_ue*             ues,
+                         uint32_t                            nof_ues,
+                         const int8_t*                       d_llrs,
+                         uint8_t*                            d_tbs,
+                         srs_amd_pusch_decoder_result*       d_results,
+                         const uint32_t*                     cb_offsets,
+                         int32_t*                            d_cb_iterations,
+                         hipStream_t                         stream);
 
 } // namespace srs_amd

@@ -361,7 +361,8 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
     s_fresh[r]          = prev ? 0 : 1;
     s_cb_ok[r]          = ok ? 1 : 0;
     if (a.cb_iterations) {
-      a.cb_iterations[cb] = ok ? static_cast<int32_t>(stat) : -1;
+      // slot form: the caller's per-codeblock index of the TB's first codeblock (tb_desc::pad)
+      a.cb_iterations[a.tds != nullptr ? a.tds[t].pad + r : cb] = ok ? static_cast<int32_t>(stat) : -1;
     }
     if (!prev && a.soft) {
       s_stat[r] = stat;

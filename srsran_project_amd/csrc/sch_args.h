@@ -50,7 +50,7 @@ struct tb_desc {
   uint32_t tb_crc_bits; // 16 / 24
   uint32_t zero_pad;
   uint32_t msg_bytes;   // ceil(K / 8)
-  uint32_t pad;
+  uint32_t pad;         // decode: index of the TB's first codeblock in assemble_args::cb_iterations
 };
 
 // PDSCH encoder of a heterogeneous batch: TB CRCs (CRC16 or CRC24A per TB, linear CRC over chunks XOR-ed

@@ -101,7 +101,7 @@ class PuschProcessorResult(ctypes.Structure):
     _fields_ = [("data", PuschDecoderResult), ("sinr_db", ctypes.c_float), ("epre_db", ctypes.c_float),
                 ("rsrp_db", ctypes.c_float), ("time_alignment_s", ctypes.c_float),
                 ("harq_ack_status", ctypes.c_int32), ("csi_part1_status", ctypes.c_int32),
-                ("csi_part2_status", ctypes.c_int32), ("nof_csi_part2", ctypes.c_uint32)]
+                ("csi_part2_status", ctypes.c_int32), ("nof_csi_part2", ctypes.c_uint32), ("cfo_hz", ctypes.c_float)]
 
 
 RESULT_BYTES = ctypes.sizeof(PuschProcessorResult)
@@ -114,14 +114,21 @@ class PuschIntermediates(ctypes.Structure):
                 ("d_llrs", ctypes.c_void_p), ("llr_stride", ctypes.c_uint32),
                 ("d_harq_ack", ctypes.c_void_p), ("harq_ack_stride", ctypes.c_uint32),
                 ("d_csi_part1", ctypes.c_void_p), ("csi_part1_stride", ctypes.c_uint32),
-                ("d_csi_part2", ctypes.c_void_p), ("csi_part2_stride", ctypes.c_uint32)]
+                ("d_csi_part2", ctypes.c_void_p), ("csi_part2_stride", ctypes.c_uint32),
+                ("d_cb_iterations", ctypes.c_void_p)]
 
 
 class PuschSlotPdu(ctypes.Structure):
     """``srs_amd_pusch_slot_pdu``: one PDU of srs_amd_pusch_process_slot."""
 
-    _fields_ = [("plan", ctypes.c_void_p), ("grid", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
-                ("tb_offset", ctypes.c_uint64)]
+    _fields_ = [("plan", ctypes.c_void_p), ("grid", ctypes.c_uint32), ("cb_offset", ctypes.c_uint32),
+                ("tb_offset", ctypes.c_uint64), ("d_soft", ctypes.c_void_p), ("uci_offset", ctypes.c_uint64)]
+
+
+class PuschSlotIo(ctypes.Structure):
+    """``srs_amd_pusch_slot_io``: optional outputs of srs_amd_pusch_process_slot_ex."""
+
+    _fields_ = [("d_cb_iterations", ctypes.c_void_p), ("d_uci", ctypes.c_void_p)]
 
 
 def make_pdu(**kw):
@@ -159,6 +166,10 @@ def _declare(lib):
         "srs_amd_pusch_process_batch": (c.c_int, [P, P, P, c.c_uint64, u, P, u, P, P, P, P]),
         "srs_amd_pusch_process": (c.c_int, [P, P, P, P, c.POINTER(PuschProcessorResult), P]),
         "srs_amd_pusch_process_slot": (c.c_int, [P, c.POINTER(PuschSlotPdu), u, P, c.c_uint64, u, P, P, P]),
+        "srs_amd_pusch_process_slot_ex": (c.c_int, [P, c.POINTER(PuschSlotPdu), u, P, c.c_uint64, u, P, P,
+                                                    c.POINTER(PuschSlotIo), P]),
+        "srs_amd_pusch_processor_plan_set_slot": (c.c_int, [P, u, u]),
+        "srs_amd_pusch_processor_plan_info": (c.c_int, [P, c.POINTER(u), c.POINTER(u), c.POINTER(c.c_uint64)]),
         "srs_amd_uci_part2_get_size": (c.c_int32, [P, u, c.POINTER(UciPart2SizeDescription)]),
     }
     for name, (res, args) in sigs.items():
@@ -194,6 +205,18 @@ class PuschProcessorPlan:
         self.nof_subc = nof_subc
         self.soft_bytes = sb.value
         self.tb_bytes = pdu.tbs // 8
+        nc, m2 = ctypes.c_uint32(), ctypes.c_uint32()
+        _lib.check(self._lib.srs_amd_pusch_processor_plan_info(h, ctypes.byref(nc), ctypes.byref(m2), None),
+                   "pusch_processor plan info")
+        self.nof_codeblocks = nc.value
+        self.max_csi_part2 = m2.value
+        self.uci_bytes = pdu.nof_harq_ack + pdu.nof_csi_part1 + self.max_csi_part2
+
+    def set_slot(self, numerology, slot_index):
+        """srs_amd_pusch_processor_plan_set_slot: the same configuration in another slot."""
+        _lib.check(self._lib.srs_amd_pusch_processor_plan_set_slot(self._h, numerology, slot_index),
+                   "pusch_processor plan set_slot")
+        self.pdu.numerology, self.pdu.slot_index = numerology, slot_index
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -280,10 +303,12 @@ class PuschProcessor:
             "pusch_process_batch")
         return tbs, results
 
-    def process_slot(self, grids, pdus, tbs=None, results=None, stream=None):
+    def process_slot(self, grids, pdus, tbs=None, results=None, stream=None, cb_iterations=None, uci=None):
         """Device: every PDU of a slot in one launch sequence (uplink_processor_impl::process_pusch per PDU).
-        grids int32 [n][P][14][nsubc]; pdus: a PuschSlot or a list of (plan, grid index). Returns (tbs uint8 flat,
-        tb offsets, results uint8 [len(pdus)][RESULT_BYTES])."""
+        grids int32 [n][P][14][nsubc]; pdus: a PuschSlot or a list of (plan, grid index[, soft buffer tensor]).
+        Optional outputs: cb_iterations int32 [slot.cb_total] (per-codeblock iteration counts, PDU u's from
+        slot.cb_offsets[u]), uci uint8 [slot.uci_total] (UCI payload rows at slot.uci_offsets[u]).  Returns (tbs
+        uint8 flat, tb offsets, results uint8 [len(pdus)][RESULT_BYTES])."""
         import torch
 
         slot = pdus if isinstance(pdus, PuschSlot) else PuschSlot(pdus)
@@ -294,27 +319,43 @@ class PuschProcessor:
             results = torch.zeros((slot.n, RESULT_BYTES), dtype=torch.uint8, device=dev)
         if stream is None:
             stream = torch.cuda.current_stream(dev)
-        _lib.check(self._lib.srs_amd_pusch_process_slot(
+        io = None
+        if cb_iterations is not None or uci is not None:
+            io = PuschSlotIo(None if cb_iterations is None else cb_iterations.data_ptr(),
+                             None if uci is None else uci.data_ptr())
+        _lib.check(self._lib.srs_amd_pusch_process_slot_ex(
             self._h, slot.arr, slot.n, grids.data_ptr(), grids.stride(0), grids.shape[0], tbs.data_ptr(),
-            results.data_ptr(), ctypes.c_void_p(stream.cuda_stream)), "pusch_process_slot")
+            results.data_ptr(), None if io is None else ctypes.byref(io), ctypes.c_void_p(stream.cuda_stream)),
+            "pusch_process_slot")
         return tbs, slot.offsets, results
 
 
 class PuschSlot:
     """The srs_amd_pusch_slot_pdu array of a slot, built once per slot configuration: pdus = list of
-    (plan, grid index); transport block u at byte offsets[u] (64-byte aligned) of a tb_total-byte buffer."""
+    (plan, grid index) or (plan, grid index, device soft buffer); transport block u at byte offsets[u] (64-byte
+    aligned) of a tb_total-byte buffer, its codeblock iteration counts at cb_offsets[u] of cb_total, its UCI payload
+    row at uci_offsets[u] of uci_total."""
 
     def __init__(self, pdus):
-        self.plans = [p for p, _ in pdus]  # keep the plans alive
+        self.plans = [p[0] for p in pdus]  # keep the plans alive
+        self.soft = [p[2] if len(p) > 2 else None for p in pdus]
         self.n = len(pdus)
-        self.offsets, total = [], 0
-        for plan, _ in pdus:
+        self.offsets, self.cb_offsets, self.uci_offsets = [], [], []
+        total = cbs = ucis = 0
+        for p in pdus:
+            plan = p[0]
             self.offsets.append(total)
+            self.cb_offsets.append(cbs)
+            self.uci_offsets.append(ucis)
             total += (plan.tb_bytes + 63) // 64 * 64
-        self.tb_total = total
+            cbs += plan.nof_codeblocks
+            ucis += plan.uci_bytes
+        self.tb_total, self.cb_total, self.uci_total = total, cbs, ucis
         self.arr = (PuschSlotPdu * max(self.n, 1))()
-        for i, ((plan, g), off) in enumerate(zip(pdus, self.offsets)):
-            self.arr[i] = PuschSlotPdu(plan._h.value, int(g), 0, off)
+        for i, p in enumerate(pdus):
+            soft = self.soft[i]
+            self.arr[i] = PuschSlotPdu(p[0]._h.value, int(p[1]), self.cb_offsets[i], self.offsets[i],
+                                       None if soft is None else soft.data_ptr(), self.uci_offsets[i])
 
 
 def parse_results(results):

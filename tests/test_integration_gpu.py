@@ -181,6 +181,14 @@ def test_hw_pdsch_enc_plugin_matches_pdsch_encoder_impl(hw, ci, cb_mode):
         assert np.array_equal(got, want), (SCH_CASES[ci], cb_mode, int((got != want).sum()))
 
 
+def test_hw_pdsch_enc_plugin_failure_does_not_stall(hw):
+    """a failed operation (TB-mode transport block one byte short of its configuration; CB-mode codeblock
+    shorter than K - F) is logged and dequeues the configured codeword length as zeros on the first call, so the
+    reference's driver loop (pdsch_encoder_hw_impl.cpp:150-160: dequeue until it returns true) moves on."""
+    ohw, _ = hw
+    assert ohw.lib().srs_ref_hw_pdsch_enc_forced_failure(0) == 0
+
+
 DFT_OFDM_CASES = [(1, 273, 4096, 1.0, 3.5e9), (0, 52, 1024, 0.5, 1.8e9), (1, 106, 1536, 0.7, 2.6e9)]
 
 

@@ -256,6 +256,67 @@ def test_pusch_slot_4ue_grid_vs_reference(eq):
         assert b.data.ldpc_iterations_sum == res[u].data.ldpc_iterations_sum, u
 
 
+def test_pusch_slot_mixed_pdus_vs_reference():
+    """one slot call over every PDU kind of a slot -- HARQ-ACK + CSI part 1 on PUSCH, DFT-s-OFDM, a
+    HARQ process kept in a device soft buffer (rv 0 new data, then rv 2 retransmission in the next slot) and two
+    plain PDUs of the fused group -- on one four-port grid, against the compiled pusch_processor_impl called once
+    per PDU on the same grid (the HARQ process with one reference rx_buffer across the two slots): TB bytes, CRC
+    flags, LDPC statistics (from the per-codeblock iteration output), CSI, UCI payloads and statuses."""
+    import torch
+
+    import oracle
+    from pusch_slot_cases import mixed_slot, NSUBC
+
+    iters = 6
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=iters), device=0)
+    ref_buf = soft = None
+    for slot_index, rv in ((3, 0), (4, 2)):
+        grid, pdus, sent = mixed_slot(slot_index, rv, seed=slot_index)
+        plans = [proc.plan(amd.make_pdu(**p), NSUBC) for p in pdus]
+        items = []
+        for p, pl in zip(pdus, plans):
+            if p["rnti"] == 0x5003:  # the HARQ process: its soft buffer lives across the slots
+                if soft is None:
+                    soft = torch.zeros(pl.soft_bytes, dtype=torch.int8, device="cuda:0")
+                    ref_buf = oracle.RefRxBuffer(pl.nof_codeblocks)
+                items.append((pl, 0, soft))
+            else:
+                items.append((pl, 0))
+        slot = amd.PuschSlot(items)
+        g = torch.from_numpy(grid.view(np.int32)[None]).to("cuda:0")
+        cbi = torch.full((slot.cb_total,), -7, dtype=torch.int32, device="cuda:0")
+        uci = torch.zeros(max(slot.uci_total, 1), dtype=torch.uint8, device="cuda:0")
+        out, offs, res = proc.process_slot(g, slot, cb_iterations=cbi, uci=uci)
+        torch.cuda.synchronize()
+        out, cbi, uci = out.cpu().numpy(), cbi.cpu().numpy(), uci.cpu().numpy()
+        res = amd.pusch_processor.parse_results(res.cpu().numpy())
+        for u, (pdu, pl) in enumerate(zip(pdus, plans)):
+            tag = "slot %d rnti %#x" % (slot_index, pdu["rnti"])
+            P = pdu["nof_rx_ports"]
+            kw = dict(rx_buffer=ref_buf) if pdu["rnti"] == 0x5003 else {}
+            want_tb, want = pp.ref_pusch_process(grid[:P], pdu, pl.tb_bytes, iterations=iters, **kw)
+            got_tb = out[offs[u]:offs[u] + pl.tb_bytes]
+            assert bool(res[u].data.tb_crc_ok) == want["tb_crc_ok"], tag
+            assert np.array_equal(got_tb, want_tb), tag
+            assert res[u].data.nof_codeblocks_total == want["nof_codeblocks_total"], tag
+            assert res[u].data.ldpc_iterations_sum == want["iterations_sum"], (tag, res[u].data, want)
+            c = cbi[slot.cb_offsets[u]:slot.cb_offsets[u] + pl.nof_codeblocks]
+            assert (c != -7).all(), tag
+            assert int(np.where(c >= 0, c, iters).sum()) == want["iterations_sum"], (tag, c)
+            _check_csi(res[u], want, tag)
+            if pdu.get("nof_harq_ack", 0):
+                row = uci[slot.uci_offsets[u]:slot.uci_offsets[u] + pl.uci_bytes]
+                n_ack, n_csi1 = pdu["nof_harq_ack"], pdu["nof_csi_part1"]
+                assert res[u].harq_ack_status == want["harq_ack_status"] == 1, tag
+                assert res[u].csi_part1_status == want["csi_part1_status"] == 1, tag
+                assert np.array_equal(row[:n_ack], want["harq_ack"]) and np.array_equal(row[:n_ack], sent[u][1][0])
+                assert np.array_equal(row[n_ack:n_ack + n_csi1], want["csi_part1"]), tag
+            if pdu["rnti"] == 0x5003:
+                assert want["tb_crc_ok"] == (rv == 2), tag  # rv 0 alone fails, the combined rv 2 decodes
+            else:
+                assert want["tb_crc_ok"] and np.array_equal(got_tb, sent[u][0]), tag
+
+
 def test_pusch_slot_rejects_unsupported():
     import torch
 
@@ -264,7 +325,7 @@ def test_pusch_slot_rejects_unsupported():
     g = torch.zeros((1, 1, 14, 12 * 51), dtype=torch.int32, device="cuda:0")
     retx = proc.plan(amd.make_pdu(**dict(pdu, new_data=0)), 12 * 51)
     with pytest.raises(ValueError):
-        proc.process_slot(g, [(retx, 0)])
+        proc.process_slot(g, [(retx, 0)])  # a retransmission without its soft buffer
     ok = proc.plan(amd.make_pdu(**pdu), 12 * 51)
     with pytest.raises(ValueError):
         proc.process_slot(g, [(ok, 1)])  # grid index out of range
