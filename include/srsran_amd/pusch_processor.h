@@ -203,6 +203,8 @@ typedef struct srs_amd_pusch_slot_io {
   int32_t* d_cb_iterations; /* per-codeblock iteration counts (as srs_amd_pusch_intermediates), PDU i's C values from
                                pdus[i].cb_offset */
   uint8_t* d_uci;           /* UCI payload rows, PDU i's at pdus[i].uci_offset */
+  srs_amd_chest_port_stats* d_port_stats; /* estimator measurements [pdu][4], PDU i's receive ports from 4 * i (the
+                                             per-port inputs of channel_estimate::get_channel_state_information) */
 } srs_amd_pusch_slot_io;
 
 /* DEVICE, asynchronous: every PUSCH PDU of a slot -- several UEs on disjoint PRBs of one received grid (or of

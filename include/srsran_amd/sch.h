@@ -148,6 +148,14 @@ void srs_amd_pusch_decoder_destroy(srs_amd_pusch_decoder* dec);
 /* Bytes of device soft buffer one transport block of this plan needs (HARQ rx_buffer). */
 uint64_t srs_amd_pusch_soft_buffer_size(const srs_amd_sch_plan* plan);
 
+/* Layout of the soft buffer: C rows of row_bytes, codeblock c at c * row_bytes holding its N = 66 Z (BG1) / 50 Z
+ * (BG2) rate-dematched LLRs (rx_buffer::get_codeblock_soft_bits, int8 log_likelihood_ratio) at 0, its decoded
+ * message (rx_buffer::get_codeblock_data_bits: K bits packed MSB first, as bit_buffer) at msg_offset and an int32
+ * flag at flag_offset: the LDPC iteration count of the decoding that passed the codeblock CRC, 0 while it has not
+ * (rx_buffer::get_codeblocks_crc).  A caller mirroring the reference's rx_buffer copies these three fields. */
+int srs_amd_pusch_soft_buffer_layout(const srs_amd_sch_plan* plan, uint32_t* row_bytes, uint32_t* nof_llrs,
+                                     uint32_t* msg_offset, uint32_t* flag_offset);
+
 /* LLRs per soft-buffer row the LDPC decoder scans after rate dematching this plan's codeblocks
  * (the rest of the row is provably zero): the whole row unless new data with k0 = 0 and no
  * circular wrap lands in a fresh buffer (fresh != 0) or covers the information bits of a

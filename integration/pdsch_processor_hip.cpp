@@ -1,0 +1,498 @@
+// pdsch_processor_hip.cpp -- srsran::pdsch_processor over the srsran_amd PDSCH slot C-ABI (see the header).
+#include "pdsch_processor_hip.h"
+#include "slot_collector.h"
+
+#include "srsran/phy/support/resource_grid_writer.h"
+#include "srsran/support/math/math_utils.h"
+#include "srsran_amd/pdsch_modulator.h"
+#include "srsran_amd/sch.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <list>
+#include <optional>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using namespace srsran;
+using namespace srsran::hip;
+
+namespace {
+
+constexpr unsigned NSYMB     = 14;          // OFDM symbols of a normal-CP slot
+constexpr unsigned MAX_PORTS = 4;           // transmit ports of one grid
+constexpr uint32_t SENTINEL  = 0xffffffffu; // bf16 NaN pair: never a PDSCH / DM-RS RE value
+
+void log_error(const char* what, const std::string& detail)
+{
+  std::fprintf(stderr, "pdsch_processor_hip: %s: %s\n", what, detail.c_str());
+}
+
+int32_t qm_code(modulation_scheme m)
+{
+  switch (m) {
+    case modulation_scheme::PI_2_BPSK:
+      return 0;
+    case modulation_scheme::BPSK:
+      return 1;
+    default:
+      return static_cast<int32_t>(get_bits_per_symbol(m));
+  }
+}
+
+// ldpc::compute_nof_codeblocks / compute_N_ref (ldpc.h:140-151, 225-228).
+uint32_t nof_codeblocks(uint32_t tbs, uint32_t bg)
+{
+  const uint32_t b = tbs + (tbs > 3824 ? 24u : 16u);
+  const uint32_t m = bg == 1 ? 8448u : 3840u;
+  return b <= m ? 1u : (b + (m - 24) - 1) / (m - 24);
+}
+
+uint32_t compute_N_ref(uint32_t tbs_lbrm_bytes, uint32_t C)
+{
+  const uint64_t n = static_cast<uint64_t>(tbs_lbrm_bytes) * 8 * 3 / (2 * C);
+  return static_cast<uint32_t>(std::min<uint64_t>(n, 384 * 66));
+}
+
+/// One queued process() call.
+struct pending_pdu {
+  resource_grid_writer*     grid     = nullptr;
+  pdsch_processor_notifier* notifier = nullptr;
+  std::optional<shared_transport_block> tb;
+  pdsch_processor::pdu_t    pdu;
+  srs_amd_pdsch_mod_config  mod{};
+  srs_amd_dmrs_pdsch_config dmrs{};
+  uint32_t                  numerology = 0;
+  std::string               error;
+};
+
+template <typename Mask>
+void set_mask_bytes(uint8_t* bytes, const Mask& m, unsigned n)
+{
+  for (unsigned i = 0; i != n && i < m.size(); ++i) {
+    if (m.test(i)) {
+      bytes[i / 8] |= static_cast<uint8_t>(1u << (i % 8));
+    }
+  }
+}
+
+// pdu_t -> the modulator / DM-RS configurations pdsch_processor_impl::modulate and pdsch_process_dmrs build
+// (pdsch_processor_impl.cpp:185-200, pdsch_processor_helpers.h:36-62); an empty string when supported.
+std::string convert(pending_pdu& p, unsigned nof_prb)
+{
+  const pdsch_processor::pdu_t& pdu = p.pdu;
+  if (pdu.cp != cyclic_prefix::NORMAL) {
+    return "extended cyclic prefix";
+  }
+  if (pdu.ptrs.has_value()) {
+    return "PT-RS";
+  }
+  if (pdu.codewords.size() != 1) {
+    return "two codewords";
+  }
+  const precoding_configuration& pc = pdu.precoding;
+  const unsigned                 L  = pc.get_nof_layers();
+  const unsigned                 P  = pc.get_nof_ports();
+  if (L == 0 || L > SRS_AMD_MAX_LAYERS || P == 0 || P > MAX_PORTS || P < L) {
+    return "layers / ports outside 1..4";
+  }
+  for (unsigned g = 1; g < pc.get_nof_prg(); ++g) {
+    if (!(pc.get_prg_coefficients(g) == pc.get_prg_coefficients(0))) {
+      return "precoding that differs between PRGs";
+    }
+  }
+  if (pdu.reserved.get_nof_entries() > SRS_AMD_MAX_RE_PATTERNS) {
+    return "more than eight reserved RE patterns";
+  }
+  if (pdu.start_symbol_index + pdu.nof_symbols > NSYMB || pdu.bwp_start_rb + pdu.bwp_size_rb > nof_prb) {
+    return "allocation outside the slot / grid";
+  }
+  const crb_bitmap crbs = pdu.freq_alloc.get_crb_mask(pdu.bwp_start_rb, pdu.bwp_size_rb);
+  if (crbs.none()) {
+    return "empty frequency allocation";
+  }
+  srs_amd_pdsch_mod_config& m = p.mod;
+  m                           = srs_amd_pdsch_mod_config{};
+  m.rnti                      = pdu.rnti;
+  m.n_id                      = pdu.n_id;
+  m.modulation                = qm_code(pdu.codewords[0].modulation);
+  m.bwp_start                 = pdu.bwp_start_rb;
+  m.bwp_size                  = pdu.bwp_size_rb;
+  set_mask_bytes(m.crb_mask, crbs, SRS_AMD_MAX_RB);
+  m.start_symbol = pdu.start_symbol_index;
+  m.nof_symbols  = pdu.nof_symbols;
+  for (unsigned l = 0; l != NSYMB && l < pdu.dmrs_symbol_mask.size(); ++l) {
+    m.dmrs_symbol_mask |= pdu.dmrs_symbol_mask.test(l) ? (1u << l) : 0u;
+  }
+  m.dmrs_type                   = pdu.dmrs == dmrs_type::TYPE1 ? 1u : 2u;
+  m.nof_cdm_groups_without_data = pdu.nof_cdm_groups_without_data;
+  m.scaling                     = convert_dB_to_amplitude(-pdu.ratio_pdsch_data_to_sss_dB);
+  m.nof_layers                  = L;
+  m.nof_ports                   = P;
+  for (unsigned l = 0; l != L; ++l) {
+    for (unsigned q = 0; q != P; ++q) {
+      const cf_t w       = pc.get_coefficient(l, q, 0);
+      m.weights[l][q][0] = w.real();
+      m.weights[l][q][1] = w.imag();
+    }
+  }
+  span<const re_pattern> res = pdu.reserved.get_re_patterns();
+  m.nof_reserved             = static_cast<uint32_t>(res.size());
+  for (size_t r = 0; r != res.size(); ++r) {
+    set_mask_bytes(m.reserved[r].crb_mask, res[r].crb_mask, SRS_AMD_MAX_RB);
+    for (unsigned k = 0; k != 12; ++k) {
+      m.reserved[r].re_mask |= res[r].re_mask.test(k) ? static_cast<uint16_t>(1u << k) : 0;
+    }
+    for (unsigned l = 0; l != NSYMB; ++l) {
+      m.reserved[r].symbols |= res[r].symbols.test(l) ? static_cast<uint16_t>(1u << l) : 0;
+    }
+  }
+  srs_amd_dmrs_pdsch_config& d = p.dmrs;
+  d                            = srs_amd_dmrs_pdsch_config{};
+  d.slot_index                 = pdu.slot.slot_index();
+  d.reference_point_k_rb       = pdu.ref_point == pdsch_processor::pdu_t::PRB0 ? pdu.bwp_start_rb : 0;
+  d.type                       = m.dmrs_type;
+  d.scrambling_id              = pdu.scrambling_id;
+  d.n_scid                     = pdu.n_scid ? 1 : 0;
+  d.amplitude                  = convert_dB_to_amplitude(-pdu.ratio_pdsch_dmrs_to_sss_dB);
+  d.symbols_mask               = m.dmrs_symbol_mask;
+  std::memcpy(d.crb_mask, m.crb_mask, sizeof(d.crb_mask));
+  d.nof_layers = L;
+  d.nof_ports  = P;
+  std::memcpy(d.weights, m.weights, sizeof(d.weights));
+  p.numerology = to_numerology_value(pdu.slot.scs());
+  return {};
+}
+
+class pdsch_engine
+{
+public:
+  explicit pdsch_engine(const pdsch_processor_hip_config& c) : cfg(c), nsubc(12 * c.nof_prb)
+  {
+    device = cfg.device;
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) {
+      throw std::runtime_error("pdsch_processor_hip: hipGetDevice");
+    }
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+      throw std::runtime_error("pdsch_processor_hip: device / stream");
+    }
+    if (srs_amd_pdsch_encoder_create(&enc, device) != SRS_AMD_OK ||
+        srs_amd_pdsch_modulator_create(&mod, device) != SRS_AMD_OK) {
+      const std::string e = srs_amd_last_error();
+      srs_amd_pdsch_encoder_destroy(enc);
+      (void)hipStreamDestroy(stream);
+      throw std::runtime_error("pdsch_processor_hip: encoder / modulator: " + e);
+    }
+    collector = std::make_unique<slot_collector<pending_pdu>>(
+        cfg.max_pdus_per_batch, cfg.max_wait_us, [this](std::vector<pending_pdu>& b) { return process(b); });
+  }
+
+  ~pdsch_engine()
+  {
+    collector.reset();
+    (void)hipSetDevice(device);
+    (void)hipStreamSynchronize(stream);
+    for (auto& kv : plans) {
+      srs_amd_pdsch_mod_plan_destroy(kv.second.plan);
+    }
+    srs_amd_pdsch_modulator_destroy(mod);
+    srs_amd_pdsch_encoder_destroy(enc);
+    (void)hipStreamDestroy(stream);
+  }
+
+  void enqueue(pending_pdu&& p)
+  {
+    const uint64_t key = (static_cast<uint64_t>(p.numerology) << 32) | p.pdu.slot.slot_index();
+    collector->enqueue(std::move(p), key);
+  }
+  void flush() { collector->flush(); }
+  void wait_idle() { collector->wait_idle(); }
+  pdsch_processor_factory_hip::statistics get_statistics() const
+  {
+    const auto                              c = collector->get_counters();
+    pdsch_processor_factory_hip::statistics s;
+    s.nof_pdus    = c.nof_pdus;
+    s.nof_batches = c.nof_batches;
+    s.nof_errors  = c.nof_errors;
+    return s;
+  }
+
+private:
+  struct plan_entry {
+    srs_amd_pdsch_mod_plan*          plan   = nullptr;
+    uint32_t                         nof_re = 0; // data REs per layer (pdsch_compute_nof_data_re)
+    std::list<std::string>::iterator lru;
+  };
+
+  plan_entry* plan_of(const srs_amd_pdsch_mod_config& m, std::string& error)
+  {
+    std::string key(reinterpret_cast<const char*>(&m), sizeof(m));
+    auto        it = plans.find(key);
+    if (it != plans.end()) {
+      lru.splice(lru.begin(), lru, it->second.lru);
+      return &it->second;
+    }
+    plan_entry e;
+    if (srs_amd_pdsch_mod_plan_create(mod, &m, nsubc, &e.plan, &e.nof_re) != SRS_AMD_OK) {
+      error = srs_amd_last_error();
+      return nullptr;
+    }
+    lru.push_front(key);
+    e.lru = lru.begin();
+    return &plans.emplace(key, e).first->second;
+  }
+
+  void evict_plans()
+  {
+    while (plans.size() > cfg.max_cached_plans && !lru.empty()) {
+      auto it = plans.find(lru.back());
+      srs_amd_pdsch_mod_plan_destroy(it->second.plan);
+      plans.erase(it);
+      lru.pop_back();
+    }
+  }
+
+  unsigned process(std::vector<pending_pdu>& batch)
+  {
+    const unsigned n      = static_cast<unsigned>(batch.size());
+    unsigned       errors = 0;
+    auto           done   = [](pending_pdu& p) { p.notifier->on_finish_processing(); };
+    if (hipSetDevice(device) != hipSuccess) {
+      for (auto& p : batch) {
+        done(p);
+      }
+      return n;
+    }
+    evict_plans();
+    // plans, segmentation, the writers' device grids
+    std::vector<plan_entry*>           pl(n, nullptr);
+    std::vector<srs_amd_pdsch_ue>      ues;
+    std::vector<srs_amd_pdsch_slot_pdu> sp;
+    std::vector<resource_grid_writer*> writers;
+    std::vector<unsigned>              live, grid_of(n, 0);
+    uint64_t                           tb_total = 0, cw_total = 0;
+    for (unsigned i = 0; i != n; ++i) {
+      pending_pdu& p = batch[i];
+      if (p.error.empty() && (p.grid->get_nof_subc() != nsubc || p.grid->get_nof_ports() < p.mod.nof_ports)) {
+        p.error = "resource grid dimensions differ from the processor's";
+      }
+      if (p.error.empty()) {
+        pl[i] = plan_of(p.mod, p.error);
+      }
+      srs_amd_pdsch_ue u{};
+      if (p.error.empty()) {
+        const uint32_t tbs = static_cast<uint32_t>(p.tb->get_buffer().size() * 8);
+        const uint32_t bg  = p.pdu.ldpc_base_graph == ldpc_base_graph_type::BG1 ? 1 : 2;
+        const uint32_t C   = nof_codeblocks(tbs, bg);
+        // pdsch_processor_impl::encode (pdsch_processor_impl.cpp:146-180)
+        if (srs_amd_sch_plan_compute(&u.plan, tbs, bg, p.pdu.codewords[0].rv,
+                                     get_bits_per_symbol(p.pdu.codewords[0].modulation),
+                                     compute_N_ref(static_cast<uint32_t>(p.pdu.tbs_lbrm.value()), C), p.mod.nof_layers,
+                                     pl[i]->nof_re * p.mod.nof_layers) != SRS_AMD_OK) {
+          p.error = srs_amd_last_error();
+        }
+      }
+      if (!p.error.empty()) {
+        log_error("PDU not processed", p.error);
+        done(p);
+        ++errors;
+        continue;
+      }
+      u.tb_offset = tb_total;
+      u.cw_offset = cw_total;
+      tb_total += (p.tb->get_buffer().size() + 63) / 64 * 64;
+      cw_total += (u.plan.cw_length + 511) / 512 * 64;
+      unsigned g = 0;
+      while (g != writers.size() && writers[g] != p.grid) {
+        ++g;
+      }
+      if (g == writers.size()) {
+        writers.push_back(p.grid);
+      }
+      grid_of[i] = g;
+      ues.push_back(u);
+      live.push_back(i);
+    }
+    if (live.empty()) {
+      return errors;
+    }
+    const size_t grid_words = static_cast<size_t>(MAX_PORTS) * NSYMB * nsubc;
+    if (!grids.ensure(writers.size() * grid_words * 4) || !tbs.ensure(std::max<uint64_t>(tb_total, 64)) ||
+        !cws.ensure(std::max<uint64_t>(cw_total, 64))) {
+      log_error("batch", "device / pinned buffer allocation");
+      for (unsigned i : live) {
+        done(batch[i]);
+      }
+      return n;
+    }
+    for (size_t k = 0; k != live.size(); ++k) {
+      const pending_pdu& p = batch[live[k]];
+      std::memcpy(tbs.h + ues[k].tb_offset, p.tb->get_buffer().data(), p.tb->get_buffer().size());
+      srs_amd_pdsch_slot_pdu s{};
+      s.plan      = pl[live[k]]->plan;
+      s.dmrs      = &p.dmrs;
+      s.grid      = grid_of[live[k]];
+      s.nof_bits  = ues[k].plan.cw_length;
+      s.cw_offset = ues[k].cw_offset;
+      sp.push_back(s);
+    }
+    hipError_t e = hipMemcpyAsync(tbs.d, tbs.h, tb_total, hipMemcpyHostToDevice, stream);
+    e            = e == hipSuccess ? hipMemsetAsync(grids.d, 0xff, writers.size() * grid_words * 4, stream) : e;
+    int rc = e == hipSuccess ? srs_amd_pdsch_encode_slot(enc, ues.data(), static_cast<uint32_t>(ues.size()), tbs.d,
+                                                         cws.d, stream)
+                             : SRS_AMD_EHIP;
+    if (rc == SRS_AMD_OK) {
+      rc = srs_amd_pdsch_modulate_slot(mod, sp.data(), static_cast<uint32_t>(sp.size()),
+                                       reinterpret_cast<uint32_t*>(grids.d), grid_words,
+                                       static_cast<uint32_t>(writers.size()), nsubc, cws.d, stream);
+    }
+    e = rc == SRS_AMD_OK ? hipMemcpyAsync(grids.h, grids.d, writers.size() * grid_words * 4, hipMemcpyDeviceToHost,
+                                          stream)
+                         : e;
+    e = (rc == SRS_AMD_OK && e == hipSuccess) ? hipStreamSynchronize(stream) : e;
+    if (rc != SRS_AMD_OK || e != hipSuccess) {
+      log_error("slot call", rc != SRS_AMD_OK ? std::string(srs_amd_last_error()) : hipGetErrorString(e));
+      (void)hipStreamSynchronize(stream);
+      for (unsigned i : live) {
+        done(batch[i]);
+      }
+      return n;
+    }
+    // the written REs into each writer (its other REs untouched); rows and subcarriers its PDUs span
+    for (size_t g = 0; g != writers.size(); ++g) {
+      unsigned ports = 0, l0 = NSYMB, l1 = 0, k0 = nsubc, k1 = 0;
+      for (unsigned i : live) {
+        if (grid_of[i] != g) {
+          continue;
+        }
+        const srs_amd_pdsch_mod_config& m = batch[i].mod;
+        ports                             = std::max(ports, m.nof_ports);
+        l0                                = std::min(l0, m.start_symbol);
+        l1                                = std::max(l1, m.start_symbol + m.nof_symbols);
+        for (unsigned r = 0; r != SRS_AMD_MAX_RB; ++r) {
+          if ((m.crb_mask[r / 8] >> (r % 8)) & 1u) {
+            k0 = std::min(k0, 12 * r);
+            k1 = std::max(k1, 12 * r + 12);
+          }
+        }
+      }
+      for (unsigned q = 0; q != ports; ++q) {
+        for (unsigned l = l0; l < l1; ++l) {
+          span<cbf16_t>   view = writers[g]->get_view(q, l);
+          const uint32_t* src  = reinterpret_cast<const uint32_t*>(grids.h) + ((g * MAX_PORTS + q) * NSYMB + l) * nsubc;
+          for (unsigned k = k0; k < k1 && k < view.size(); ++k) {
+            if (src[k] != SENTINEL) {
+              std::memcpy(&view[k], &src[k], sizeof(uint32_t));
+            }
+          }
+        }
+      }
+    }
+    for (unsigned i : live) {
+      done(batch[i]);
+    }
+    return errors;
+  }
+
+  pdsch_processor_hip_config                   cfg;
+  const unsigned                               nsubc;
+  int                                          device = 0;
+  hipStream_t                                  stream = nullptr;
+  srs_amd_pdsch_encoder*                       enc    = nullptr;
+  srs_amd_pdsch_modulator*                     mod    = nullptr;
+  std::unordered_map<std::string, plan_entry>  plans;
+  std::list<std::string>                       lru;
+  hip_mirrored_buffer                          grids, tbs, cws;
+  std::unique_ptr<slot_collector<pending_pdu>> collector; // last: stops before the state it uses goes
+};
+
+class pdsch_processor_hip : public pdsch_processor
+{
+public:
+  pdsch_processor_hip(std::shared_ptr<pdsch_engine> e, unsigned nof_prb_) : engine(std::move(e)), nof_prb(nof_prb_) {}
+
+  void process(resource_grid_writer&                                           grid,
+               pdsch_processor_notifier&                                       notifier,
+               static_vector<shared_transport_block, MAX_NOF_TRANSPORT_BLOCKS> data,
+               const pdu_t&                                                    pdu) override
+  {
+    pending_pdu p;
+    p.grid     = &grid;
+    p.notifier = &notifier;
+    p.pdu      = pdu;
+    if (data.empty()) {
+      p.error = "no transport block";
+    } else {
+      p.tb.emplace(data[0]);
+      p.error = convert(p, nof_prb);
+    }
+    engine->enqueue(std::move(p));
+  }
+
+private:
+  std::shared_ptr<pdsch_engine> engine;
+  unsigned                      nof_prb;
+};
+
+class pdsch_pdu_validator_hip : public pdsch_pdu_validator
+{
+public:
+  explicit pdsch_pdu_validator_hip(unsigned nof_prb_) : nof_prb(nof_prb_) {}
+  error_type<std::string> is_valid(const pdsch_processor::pdu_t& pdu) const override
+  {
+    pending_pdu p;
+    p.pdu               = pdu;
+    const std::string e = convert(p, nof_prb);
+    if (!e.empty()) {
+      return make_unexpected(e);
+    }
+    return default_success_t();
+  }
+
+private:
+  unsigned nof_prb;
+};
+
+class pdsch_processor_factory_hip_impl : public pdsch_processor_factory_hip
+{
+public:
+  explicit pdsch_processor_factory_hip_impl(const pdsch_processor_hip_config& c) :
+    cfg(c), engine(std::make_shared<pdsch_engine>(c))
+  {
+  }
+  std::unique_ptr<pdsch_processor> create() override { return std::make_unique<pdsch_processor_hip>(engine, cfg.nof_prb); }
+  // The reference wraps its processors in its logging decorator (factories.cpp:474); the MI355X processors log
+  // their errors themselves.
+  std::unique_ptr<pdsch_processor> create(srslog::basic_logger& /*logger*/, bool /*enable_logging_broadcast*/) override
+  {
+    return create();
+  }
+  std::unique_ptr<pdsch_pdu_validator> create_validator() override
+  {
+    return std::make_unique<pdsch_pdu_validator_hip>(cfg.nof_prb);
+  }
+  void       flush() override { engine->flush(); }
+  void       wait_idle() override { engine->wait_idle(); }
+  statistics get_statistics() const override { return engine->get_statistics(); }
+
+private:
+  pdsch_processor_hip_config    cfg;
+  std::shared_ptr<pdsch_engine> engine;
+};
+
+} // namespace
+
+std::shared_ptr<pdsch_processor_factory_hip>
+srsran::hip::create_pdsch_processor_factory_hip(const pdsch_processor_hip_config& cfg)
+{
+  try {
+    return std::make_shared<pdsch_processor_factory_hip_impl>(cfg);
+  } catch (const std::exception& e) {
+    log_error("factory", e.what());
+    return nullptr;
+  }
+}

@@ -1,0 +1,762 @@
+// pusch_processor_hip.cpp -- srsran::pusch_processor over the srsran_amd slot C-ABI (see the header).
+#include "pusch_processor_hip.h"
+#include "slot_collector.h"
+
+#include "srsran/adt/bit_buffer.h"
+#include "srsran/phy/support/resource_grid_reader.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_processor_result_notifier.h"
+#include "srsran/phy/upper/rx_buffer.h"
+#include "srsran/phy/upper/unique_rx_buffer.h"
+#include "srsran/ran/sch/modulation_scheme.h"
+#include "srsran_amd/pusch_processor.h"
+#include "srsran_amd/sch.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <list>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using namespace srsran;
+using namespace srsran::hip;
+
+namespace {
+
+constexpr unsigned MAX_PORTS_HIP = 4;   // receive ports per PDU (srs_amd_pusch_process_slot_ex port measurements)
+constexpr unsigned MAX_CB        = 512; // codeblocks of one transport block
+constexpr unsigned NSYMB         = 14;  // OFDM symbols of a normal-CP slot
+
+void log_error(const char* what, const std::string& detail)
+{
+  std::fprintf(stderr, "pusch_processor_hip: %s: %s\n", what, detail.c_str());
+}
+
+/// pusch_decoder_impl's cb_stats of one processor instance: the last LDPC count of each codeblock index.
+using cb_stat_array = std::array<unsigned, MAX_CB>;
+
+/// One queued process() call.
+struct pending_pdu {
+  span<uint8_t>                    data;
+  unique_rx_buffer                 rm_buffer;
+  pusch_processor_result_notifier* notifier = nullptr;
+  const resource_grid_reader*      grid     = nullptr;
+  pusch_processor::pdu_t           pdu;
+  srs_amd_pusch_pdu                c{};
+  std::vector<uint8_t>             rx_ports;
+  std::string                      error; // not supported: reported as a failed transmission
+  std::shared_ptr<cb_stat_array>   cb_stats;
+};
+
+// pdu_t -> srs_amd_pusch_pdu (the fields pusch_processor_impl.cpp:134-386 reads); an empty string when supported.
+std::string convert(const pusch_processor::pdu_t& pdu, size_t tb_bytes, srs_amd_pusch_pdu& c)
+{
+  c = srs_amd_pusch_pdu{};
+  if (!pdu.codeword.has_value()) {
+    return "PUSCH without a codeword (UCI only)";
+  }
+  if (pdu.cp != cyclic_prefix::NORMAL) {
+    return "extended cyclic prefix";
+  }
+  if (pdu.rx_ports.empty() || pdu.rx_ports.size() > MAX_PORTS_HIP || pdu.nof_tx_layers == 0 ||
+      pdu.nof_tx_layers > pdu.rx_ports.size()) {
+    return "receive ports / layers outside 1..4";
+  }
+  if (!pdu.freq_alloc.is_contiguous()) {
+    return "non-contiguous or interleaved frequency allocation";
+  }
+  const bool tp = std::holds_alternative<pusch_processor::dmrs_transform_precoding_configuration>(pdu.dmrs);
+  if (pdu.dc_position.has_value() && !tp) {
+    return "DC subcarrier zeroing (dc_position)";
+  }
+  c.numerology       = to_numerology_value(pdu.slot.scs());
+  c.slot_index       = pdu.slot.slot_index();
+  c.rnti             = pdu.rnti;
+  c.bwp_start_rb     = pdu.bwp_start_rb;
+  c.bwp_size_rb      = pdu.bwp_size_rb;
+  c.target_code_rate = pdu.mcs_descr.target_code_rate;
+  switch (pdu.mcs_descr.modulation) {
+    case modulation_scheme::PI_2_BPSK:
+      c.modulation = 0;
+      break;
+    case modulation_scheme::BPSK:
+      c.modulation = 1;
+      break;
+    default:
+      c.modulation = static_cast<int32_t>(get_bits_per_symbol(pdu.mcs_descr.modulation));
+  }
+  c.rv            = pdu.codeword->rv;
+  c.base_graph    = pdu.codeword->ldpc_base_graph == ldpc_base_graph_type::BG1 ? 1 : 2;
+  c.new_data      = pdu.codeword->new_data ? 1 : 0;
+  c.n_id          = pdu.n_id;
+  c.nof_tx_layers = pdu.nof_tx_layers;
+  c.nof_rx_ports  = static_cast<uint32_t>(pdu.rx_ports.size());
+  for (unsigned l = 0; l != NSYMB && l < pdu.dmrs_symbol_mask.size(); ++l) {
+    c.dmrs_symbol_mask |= pdu.dmrs_symbol_mask.test(l) ? (1u << l) : 0u;
+  }
+  if (tp) {
+    c.transform_precoding = 1;
+    c.n_rs_id             = std::get<pusch_processor::dmrs_transform_precoding_configuration>(pdu.dmrs).n_rs_id;
+    c.dmrs_type           = 1;
+    c.nof_cdm_groups_without_data = 2;
+  } else {
+    const auto& d                 = std::get<pusch_processor::dmrs_configuration>(pdu.dmrs);
+    c.dmrs_type                   = d.dmrs == dmrs_type::TYPE1 ? 1 : 2;
+    c.scrambling_id               = d.scrambling_id;
+    c.n_scid                      = d.n_scid ? 1 : 0;
+    c.nof_cdm_groups_without_data = d.nof_cdm_groups_without_data;
+  }
+  // the allocation's CRBs (pusch_processor_impl.cpp:166 get_crb_mask), contiguous: [rb_start, +rb_count) of the BWP
+  const crb_bitmap crbs = pdu.freq_alloc.get_crb_mask(pdu.bwp_start_rb, pdu.bwp_size_rb);
+  if (crbs.none() || static_cast<unsigned>(crbs.find_lowest()) < pdu.bwp_start_rb) {
+    return "empty frequency allocation";
+  }
+  c.rb_start           = static_cast<uint32_t>(crbs.find_lowest()) - pdu.bwp_start_rb;
+  c.rb_count           = static_cast<uint32_t>(crbs.count());
+  c.start_symbol_index = pdu.start_symbol_index;
+  c.nof_symbols        = pdu.nof_symbols;
+  c.tbs_lbrm_bytes     = static_cast<uint32_t>(pdu.tbs_lbrm.value());
+  c.tbs                = static_cast<uint32_t>(tb_bytes * 8);
+  c.nof_harq_ack          = pdu.uci.nof_harq_ack;
+  c.nof_csi_part1         = pdu.uci.nof_csi_part1;
+  c.alpha_scaling         = pdu.uci.alpha_scaling;
+  c.beta_offset_harq_ack  = pdu.uci.beta_offset_harq_ack;
+  c.beta_offset_csi_part1 = pdu.uci.beta_offset_csi_part1;
+  c.beta_offset_csi_part2 = pdu.uci.beta_offset_csi_part2;
+  const auto& entries     = pdu.uci.csi_part2_size.entries;
+  if (entries.size() > 2) {
+    return "more than two CSI part 2 size entries";
+  }
+  c.csi_part2_size.nof_entries = static_cast<uint32_t>(entries.size());
+  for (size_t e = 0; e != entries.size(); ++e) {
+    srs_amd_uci_part2_entry& en = c.csi_part2_size.entries[e];
+    if (entries[e].parameters.size() > 2 || entries[e].map.size() > 16) {
+      return "CSI part 2 size entry beyond two parameters / 16 map values";
+    }
+    en.nof_parameters = static_cast<uint32_t>(entries[e].parameters.size());
+    for (size_t q = 0; q != entries[e].parameters.size(); ++q) {
+      en.parameters[q].offset = entries[e].parameters[q].offset;
+      en.parameters[q].width  = entries[e].parameters[q].width;
+    }
+    en.map_size = static_cast<uint32_t>(entries[e].map.size());
+    for (size_t m = 0; m != entries[e].map.size(); ++m) {
+      en.map[m] = entries[e].map[m];
+    }
+  }
+  return {};
+}
+
+/// The slot collector and the MI355X processor shared by every pusch_processor of one factory.
+class slot_engine
+{
+public:
+  explicit slot_engine(const pusch_processor_hip_config& c) : cfg(c), nsubc(12 * c.nof_prb)
+  {
+    device = cfg.device;
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) {
+      throw std::runtime_error("pusch_processor_hip: hipGetDevice");
+    }
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+      throw std::runtime_error("pusch_processor_hip: device / stream");
+    }
+    srs_amd_pusch_processor_config pc{};
+    pc.dec_nof_iterations    = cfg.dec_nof_iterations;
+    pc.dec_enable_early_stop = cfg.dec_enable_early_stop ? 1 : 0;
+    pc.dec_force_decoding    = cfg.dec_force_decoding ? 1 : 0;
+    pc.equalizer        = cfg.equalizer == channel_equalizer_algorithm_type::mmse ? SRS_AMD_EQ_MMSE : SRS_AMD_EQ_ZF;
+    pc.fd_smoothing     = static_cast<int32_t>(cfg.fd_smoothing);
+    pc.td_interpolation = static_cast<int32_t>(cfg.td_interpolation);
+    pc.compensate_cfo   = cfg.compensate_cfo ? 1 : 0;
+    pc.ldpc_arith       = cfg.generic_ldpc ? SRS_AMD_ARITH_GENERIC : SRS_AMD_ARITH_SIMD;
+    if (srs_amd_pusch_processor_create(&proc, &pc, device) != SRS_AMD_OK) {
+      const std::string e = srs_amd_last_error();
+      (void)hipStreamDestroy(stream);
+      throw std::runtime_error("pusch_processor_hip: processor: " + e);
+    }
+    collector = std::make_unique<slot_collector<pending_pdu>>(
+        cfg.max_pdus_per_batch, cfg.max_wait_us, [this](std::vector<pending_pdu>& b) { return process(b); });
+  }
+
+  ~slot_engine()
+  {
+    collector.reset(); // processes what is pending, joins the collector thread
+    (void)hipSetDevice(device);
+    (void)hipStreamSynchronize(stream);
+    for (auto& kv : plans) {
+      srs_amd_pusch_processor_plan_destroy(kv.second.plan);
+    }
+    srs_amd_pusch_processor_destroy(proc);
+    (void)hipStreamDestroy(stream);
+  }
+
+  void enqueue(pending_pdu&& p)
+  {
+    const uint64_t key = (static_cast<uint64_t>(p.c.numerology) << 32) | p.c.slot_index;
+    collector->enqueue(std::move(p), key);
+  }
+
+  void flush() { collector->flush(); }
+
+  void wait_idle() { collector->wait_idle(); }
+
+  pusch_processor_factory_hip::statistics get_statistics() const
+  {
+    const auto                              c = collector->get_counters();
+    pusch_processor_factory_hip::statistics s;
+    s.nof_pdus            = c.nof_pdus;
+    s.nof_batches         = c.nof_batches;
+    s.nof_errors          = c.nof_errors;
+    s.nof_harq_redecodes  = stats_redecodes;
+    s.nof_retransmissions = stats_retx;
+    return s;
+  }
+
+private:
+  struct plan_entry {
+    srs_amd_pusch_processor_plan* plan = nullptr;
+    uint32_t                      nof_cbs = 0, max_csi2 = 0;
+    uint64_t                      soft_bytes = 0;
+    srs_amd_sch_plan              sch{};
+    std::list<std::string>::iterator lru;
+  };
+
+  // Plan of a PDU configuration (cached across slots, least recently used evicted between batches).
+  plan_entry* plan_of(const srs_amd_pusch_pdu& c, std::string& error)
+  {
+    srs_amd_pusch_pdu k = c;
+    k.numerology = k.slot_index = 0;
+    std::string key(reinterpret_cast<const char*>(&k), sizeof(k));
+    auto        it = plans.find(key);
+    if (it == plans.end()) {
+      plan_entry e;
+      if (srs_amd_pusch_processor_plan_create(proc, &c, nsubc, &e.plan, &e.sch, &e.soft_bytes) != SRS_AMD_OK) {
+        error = srs_amd_last_error();
+        return nullptr;
+      }
+      (void)srs_amd_pusch_processor_plan_info(e.plan, &e.nof_cbs, &e.max_csi2, nullptr);
+      lru.push_front(key);
+      e.lru = lru.begin();
+      it    = plans.emplace(key, e).first;
+    } else {
+      lru.splice(lru.begin(), lru, it->second.lru);
+    }
+    if (srs_amd_pusch_processor_plan_set_slot(it->second.plan, c.numerology, c.slot_index) != SRS_AMD_OK) {
+      error = srs_amd_last_error();
+      return nullptr;
+    }
+    return &it->second;
+  }
+
+  void evict_plans()
+  {
+    while (plans.size() > cfg.max_cached_plans && !lru.empty()) {
+      auto it = plans.find(lru.back());
+      srs_amd_pusch_processor_plan_destroy(it->second.plan);
+      plans.erase(it);
+      lru.pop_back();
+    }
+  }
+
+  // A transmission that could not be processed: the reference's "no dependencies" notification
+  // (pusch_processor_impl.cpp:140-157).
+  static void notify_failure(pending_pdu& p)
+  {
+    if (p.pdu.uci.nof_harq_ack != 0) {
+      pusch_processor_result_control uci;
+      uci.harq_ack.payload = uci_payload_type(p.pdu.uci.nof_harq_ack);
+      uci.harq_ack.status  = uci_status::invalid;
+      p.notifier->on_uci(uci);
+    }
+    if (p.rm_buffer.is_valid()) {
+      p.rm_buffer.unlock();
+    }
+    if (p.pdu.codeword.has_value()) {
+      p.notifier->on_sch({});
+    }
+  }
+
+  // Runs one batch; returns the number of PDUs reported as failed.
+  unsigned process(std::vector<pending_pdu>& batch)
+  {
+    const unsigned n      = static_cast<unsigned>(batch.size());
+    unsigned       errors = 0;
+    if (hipSetDevice(device) != hipSuccess) {
+      for (auto& p : batch) {
+        notify_failure(p);
+      }
+      return n;
+    }
+    evict_plans();
+    // plans, and the PDUs that go to the GPU
+    std::vector<plan_entry*> pl(n, nullptr);
+    std::vector<unsigned>    live;
+    for (unsigned i = 0; i != n; ++i) {
+      pending_pdu& p = batch[i];
+      if (p.error.empty()) {
+        pl[i] = plan_of(p.c, p.error);
+      }
+      if (p.error.empty() && !p.c.new_data && !p.rm_buffer.is_valid()) {
+        p.error = "retransmission without a valid rx_buffer";
+      }
+      if (p.error.empty() && p.rm_buffer.is_valid() && p.rm_buffer.get().get_nof_codeblocks() != pl[i]->nof_cbs) {
+        p.error = "rx_buffer codeblock count differs from the transport block's";
+      }
+      if (!p.error.empty()) {
+        log_error("PDU not processed", p.error);
+        notify_failure(p);
+        ++errors;
+        continue;
+      }
+      live.push_back(i);
+    }
+    if (live.empty()) {
+      return errors;
+    }
+    // receive grids: one device grid per (reader, port list); a PDU whose ports are a prefix of another PDU's list
+    // on the same reader shares that grid
+    std::unordered_map<const resource_grid_reader*, std::vector<uint8_t>> longest;
+    for (unsigned i : live) {
+      auto& l = longest[batch[i].grid];
+      if (batch[i].rx_ports.size() > l.size() &&
+          std::equal(l.begin(), l.end(), batch[i].rx_ports.begin())) {
+        l = batch[i].rx_ports;
+      }
+    }
+    struct grid_slot {
+      const resource_grid_reader* reader;
+      std::vector<uint8_t>        ports;
+    };
+    std::vector<grid_slot> grids;
+    std::vector<unsigned>  grid_of(n, 0);
+    for (unsigned i : live) {
+      const auto&           ports = batch[i].rx_ports;
+      const auto&           l     = longest[batch[i].grid];
+      std::vector<uint8_t>  want  = std::equal(ports.begin(), ports.end(), l.begin()) ? l : ports;
+      unsigned              g     = 0;
+      while (g != grids.size() && !(grids[g].reader == batch[i].grid && grids[g].ports == want)) {
+        ++g;
+      }
+      if (g == grids.size()) {
+        grids.push_back(grid_slot{batch[i].grid, want});
+      }
+      grid_of[i] = g;
+    }
+    const size_t grid_stride = static_cast<size_t>(MAX_PORTS_HIP) * NSYMB * nsubc; // uint32 words
+    // per-PDU offsets in the output / HARQ buffers
+    std::vector<uint64_t> tb_off(n), uci_off(n), soft_off(n);
+    std::vector<uint32_t> cb_off(n);
+    uint64_t              tb_total = 0, uci_total = 0, soft_total = 0;
+    uint32_t              cb_total = 0;
+    for (unsigned i : live) {
+      tb_off[i]  = tb_total;
+      uci_off[i] = uci_total;
+      cb_off[i]  = cb_total;
+      soft_off[i] = soft_total;
+      tb_total += (batch[i].data.size() + 63) / 64 * 64;
+      uci_total += batch[i].c.nof_harq_ack + batch[i].c.nof_csi_part1 + pl[i]->max_csi2;
+      cb_total += pl[i]->nof_cbs;
+      // soft buffers for retransmissions and for a second pass over failed new transmissions
+      if (batch[i].rm_buffer.is_valid()) {
+        soft_total += (pl[i]->soft_bytes + 255) / 256 * 256;
+      }
+    }
+    const bool ok = h_grids.ensure(grids.size() * grid_stride * 4) && tbs.ensure(std::max<uint64_t>(tb_total, 64)) &&
+                    results.ensure(sizeof(srs_amd_pusch_processor_result) * n) &&
+                    cbi.ensure(sizeof(int32_t) * std::max<uint32_t>(cb_total, 1)) &&
+                    uci.ensure(std::max<uint64_t>(uci_total, 64)) &&
+                    pstats.ensure(sizeof(srs_amd_chest_port_stats) * MAX_PORTS_HIP * n) &&
+                    soft.ensure(std::max<uint64_t>(soft_total, 256));
+    if (!ok) {
+      log_error("batch", "device / pinned buffer allocation");
+      for (unsigned i : live) {
+        notify_failure(batch[i]);
+      }
+      return n;
+    }
+    // grids from the readers (a view per port and OFDM symbol)
+    for (size_t g = 0; g != grids.size(); ++g) {
+      for (size_t j = 0; j != grids[g].ports.size(); ++j) {
+        for (unsigned l = 0; l != NSYMB; ++l) {
+          span<const cbf16_t> v   = grids[g].reader->get_view(grids[g].ports[j], l);
+          uint8_t*            dst = h_grids.h + ((g * MAX_PORTS_HIP + j) * NSYMB + l) * nsubc * 4;
+          if (v.size() >= nsubc) {
+            std::memcpy(dst, v.data(), nsubc * 4);
+          } else {
+            std::memset(dst, 0, nsubc * 4);
+          }
+        }
+      }
+    }
+    // retransmissions: the rx_buffer's state into the device soft buffer
+    std::vector<std::vector<char>> prev_ok(n);
+    for (unsigned i : live) {
+      if (!batch[i].c.new_data) {
+        upload_harq(batch[i], *pl[i], soft.h + soft_off[i], prev_ok[i]);
+        ++stats_retx;
+      }
+    }
+    // the slot call
+    std::vector<srs_amd_pusch_slot_pdu> sp;
+    for (unsigned i : live) {
+      srs_amd_pusch_slot_pdu u{};
+      u.plan       = pl[i]->plan;
+      u.grid       = grid_of[i];
+      u.cb_offset  = cb_off[i];
+      u.tb_offset  = tb_off[i];
+      u.d_soft     = batch[i].c.new_data ? nullptr : reinterpret_cast<int8_t*>(soft.d + soft_off[i]);
+      u.uci_offset = uci_off[i];
+      sp.push_back(u);
+    }
+    hipError_t e = hipMemcpyAsync(h_grids.d, h_grids.h, grids.size() * grid_stride * 4, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess && soft_total != 0) {
+      e = hipMemcpyAsync(soft.d, soft.h, soft_total, hipMemcpyHostToDevice, stream);
+    }
+    int rc = e == hipSuccess ? run_slot(sp, grids.size(), grid_stride) : SRS_AMD_EHIP;
+    e      = rc == SRS_AMD_OK ? download(n, tb_total, cb_total, uci_total, soft_total) : hipErrorUnknown;
+    if (rc != SRS_AMD_OK || e != hipSuccess) {
+      log_error("slot call", rc != SRS_AMD_OK ? std::string(srs_amd_last_error()) : hipGetErrorString(e));
+      (void)hipStreamSynchronize(stream);
+      for (unsigned i : live) {
+        notify_failure(batch[i]);
+      }
+      return n;
+    }
+    // new transmissions whose TB CRC failed and that keep HARQ state: decoded again with a soft buffer (the same
+    // decoding, now with its soft bits kept), then written to the rx_buffer
+    const auto*       res = reinterpret_cast<const srs_amd_pusch_processor_result*>(results.h);
+    std::vector<char> keep(live.size(), 0); // the rx_buffer takes the soft buffer's state after the call
+    std::vector<srs_amd_pusch_slot_pdu> again;
+    std::vector<unsigned>               again_ids;
+    for (size_t k = 0; k != live.size(); ++k) {
+      const unsigned i = live[k];
+      keep[k]          = !batch[i].c.new_data;
+      if (batch[i].c.new_data && batch[i].rm_buffer.is_valid() && !res[k].data.tb_crc_ok) {
+        srs_amd_pusch_slot_pdu u = sp[k];
+        u.d_soft                 = reinterpret_cast<int8_t*>(soft.d + soft_off[i]);
+        again.push_back(u);
+        again_ids.push_back(static_cast<unsigned>(k));
+      }
+    }
+    if (!again.empty()) {
+      stats_redecodes += again.size();
+      e = hipSuccess;
+      for (unsigned k : again_ids) {
+        const unsigned i = live[k];
+        e = e == hipSuccess ? hipMemsetAsync(soft.d + soft_off[i], 0, pl[i]->soft_bytes, stream) : e;
+      }
+      rc = e == hipSuccess ? run_slot(again, grids.size(), grid_stride, &again_ids) : SRS_AMD_EHIP;
+      for (unsigned k : again_ids) {
+        const unsigned i = live[k];
+        e = (rc == SRS_AMD_OK && e == hipSuccess)
+                ? hipMemcpyAsync(soft.h + soft_off[i], soft.d + soft_off[i], pl[i]->soft_bytes, hipMemcpyDeviceToHost,
+                                 stream)
+                : e;
+      }
+      e = e == hipSuccess ? hipStreamSynchronize(stream) : e;
+      if (rc != SRS_AMD_OK || e != hipSuccess) {
+        // the rx_buffers are left as they were (the transport blocks report their CRC failure either way)
+        log_error("HARQ soft-buffer pass", rc != SRS_AMD_OK ? std::string(srs_amd_last_error()) : hipGetErrorString(e));
+        (void)hipStreamSynchronize(stream);
+      } else {
+        for (unsigned k : again_ids) {
+          keep[k] = 1;
+        }
+      }
+    }
+    // results, HARQ state back into the rx_buffers, notifications
+    for (size_t k = 0; k != live.size(); ++k) {
+      const unsigned i = live[k];
+      pending_pdu&   p = batch[i];
+      if (keep[k]) {
+        store_harq(p, *pl[i], soft.h + soft_off[i]);
+      }
+      notify(p, *pl[i], res[k], reinterpret_cast<const int32_t*>(cbi.h) + cb_off[i], prev_ok[i],
+             tbs.h + tb_off[i], uci.h + uci_off[i],
+             reinterpret_cast<const srs_amd_chest_port_stats*>(pstats.h) + static_cast<size_t>(k) * MAX_PORTS_HIP);
+    }
+    return errors;
+  }
+
+  // srs_amd_pusch_process_slot_ex on the batch's device buffers; ids: the index of each PDU in the outputs (the
+  // second pass writes into the first pass's rows).
+  int run_slot(std::vector<srs_amd_pusch_slot_pdu>& sp, size_t nof_grids, size_t grid_stride,
+               const std::vector<unsigned>* ids = nullptr)
+  {
+    srs_amd_pusch_slot_io io{};
+    io.d_cb_iterations = reinterpret_cast<int32_t*>(cbi.d);
+    io.d_uci           = uci.d;
+    io.d_port_stats    = reinterpret_cast<srs_amd_chest_port_stats*>(pstats.d);
+    auto* d_res        = reinterpret_cast<srs_amd_pusch_processor_result*>(results.d);
+    if (ids == nullptr) {
+      return srs_amd_pusch_process_slot_ex(proc, sp.data(), static_cast<uint32_t>(sp.size()),
+                                           reinterpret_cast<const uint32_t*>(h_grids.d), grid_stride,
+                                           static_cast<uint32_t>(nof_grids), tbs.d, d_res, &io, stream);
+    }
+    // one PDU per call so that results / port measurements land in the first pass's rows
+    for (size_t j = 0; j != sp.size(); ++j) {
+      const unsigned        k = (*ids)[j];
+      srs_amd_pusch_slot_io x = io;
+      x.d_port_stats          = io.d_port_stats + static_cast<size_t>(k) * MAX_PORTS_HIP;
+      const int rc = srs_amd_pusch_process_slot_ex(proc, &sp[j], 1, reinterpret_cast<const uint32_t*>(h_grids.d),
+                                                   grid_stride, static_cast<uint32_t>(nof_grids), tbs.d, d_res + k,
+                                                   &x, stream);
+      if (rc != SRS_AMD_OK) {
+        return rc;
+      }
+    }
+    return SRS_AMD_OK;
+  }
+
+  hipError_t download(unsigned n, uint64_t tb_total, uint32_t cb_total, uint64_t uci_total, uint64_t soft_total)
+  {
+    hipError_t e = hipMemcpyAsync(tbs.h, tbs.d, tb_total, hipMemcpyDeviceToHost, stream);
+    auto       d2h = [&](hip_mirrored_buffer& m, size_t bytes) {
+      if (e == hipSuccess && bytes != 0) {
+        e = hipMemcpyAsync(m.h, m.d, bytes, hipMemcpyDeviceToHost, stream);
+      }
+    };
+    d2h(results, sizeof(srs_amd_pusch_processor_result) * n);
+    d2h(cbi, sizeof(int32_t) * cb_total);
+    d2h(uci, uci_total);
+    d2h(pstats, sizeof(srs_amd_chest_port_stats) * MAX_PORTS_HIP * n);
+    d2h(soft, soft_total);
+    return e == hipSuccess ? hipStreamSynchronize(stream) : e;
+  }
+
+  // rx_buffer -> device soft-buffer layout (srs_amd_pusch_soft_buffer_layout): soft bits, messages, CRC flags; the
+  // flag of a codeblock OK from an earlier transmission is non-zero (its statistic comes from cb_stats).
+  static void upload_harq(pending_pdu& p, const plan_entry& e, uint8_t* dst, std::vector<char>& prev)
+  {
+    uint32_t row = 0, nllr = 0, moff = 0, foff = 0;
+    (void)srs_amd_pusch_soft_buffer_layout(&e.sch, &row, &nllr, &moff, &foff);
+    rx_buffer&       rb   = p.rm_buffer.get();
+    span<const bool> crcs = rb.get_codeblocks_crc();
+    const unsigned   K    = e.sch.segment_length;
+    prev.assign(e.nof_cbs, 0);
+    std::memset(dst, 0, static_cast<size_t>(row) * e.nof_cbs);
+    for (unsigned cb = 0; cb != e.nof_cbs; ++cb) {
+      uint8_t*                   r  = dst + static_cast<size_t>(cb) * row;
+      span<log_likelihood_ratio> sb = rb.get_codeblock_soft_bits(cb, nllr);
+      std::memcpy(r, sb.data(), nllr);
+      bit_buffer msg = rb.get_codeblock_data_bits(cb, K);
+      std::memcpy(r + moff, msg.get_buffer().data(), (K + 7) / 8);
+      prev[cb]            = crcs[cb] ? 1 : 0;
+      const int32_t flag  = crcs[cb] ? std::max<int32_t>(1, static_cast<int32_t>((*p.cb_stats)[cb])) : 0;
+      std::memcpy(r + foff, &flag, sizeof(flag));
+    }
+  }
+
+  // device soft-buffer layout -> rx_buffer (after the call that decoded with it)
+  static void store_harq(pending_pdu& p, const plan_entry& e, const uint8_t* src)
+  {
+    uint32_t row = 0, nllr = 0, moff = 0, foff = 0;
+    (void)srs_amd_pusch_soft_buffer_layout(&e.sch, &row, &nllr, &moff, &foff);
+    rx_buffer&     rb   = p.rm_buffer.get();
+    span<bool>     crcs = rb.get_codeblocks_crc();
+    const unsigned K    = e.sch.segment_length;
+    for (unsigned cb = 0; cb != e.nof_cbs; ++cb) {
+      const uint8_t*             r  = src + static_cast<size_t>(cb) * row;
+      span<log_likelihood_ratio> sb = rb.get_codeblock_soft_bits(cb, nllr);
+      std::memcpy(sb.data(), r, nllr);
+      bit_buffer msg = rb.get_codeblock_data_bits(cb, K);
+      std::memcpy(msg.get_buffer().data(), r + moff, (K + 7) / 8);
+      int32_t flag = 0;
+      std::memcpy(&flag, r + foff, sizeof(flag));
+      crcs[cb] = flag != 0;
+    }
+  }
+
+  // pusch_processor_notifier_adaptor (pusch_processor_notifier_adaptor.h) + pusch_decoder_impl::join_and_notify
+  // (pusch_decoder_impl.cpp:404-457): transport block, rx_buffer release / unlock, on_uci, on_sch.
+  void notify(pending_pdu& p, const plan_entry& e, const srs_amd_pusch_processor_result& r, const int32_t* cb_it,
+              const std::vector<char>& prev, const uint8_t* tb, const uint8_t* uci_row,
+              const srs_amd_chest_port_stats* st)
+  {
+    // channel state information as channel_estimate::get_channel_state_information (channel_estimation.h:244-281)
+    channel_state_information csi(channel_state_information::sinr_type::channel_estimator);
+    const unsigned P        = static_cast<unsigned>(p.rx_ports.size());
+    float          epre_lin = 0.0F, best_snr = 0.0F, noise = 0.0F, rsrp = 0.0F;
+    unsigned       best     = 0;
+    std::array<float, MAX_PORTS_HIP> port_rsrp{};
+    for (unsigned q = 0; q != P; ++q) {
+      epre_lin += st[q].epre;
+      if (st[q].snr > best_snr) {
+        best_snr = st[q].snr;
+        best     = q;
+      }
+      port_rsrp[q] = st[q].rsrp;
+      noise += st[q].noise_var;
+      rsrp += st[q].rsrp;
+    }
+    csi.set_rsrp_lin(span<const float>(port_rsrp.data(), P));
+    csi.set_epre(10.0F * std::log10(epre_lin / static_cast<float>(P)));
+    csi.set_time_alignment(phy_time_unit::from_seconds(st[best].time_alignment_s));
+    csi.set_cfo(st[best].cfo_hz);
+    csi.set_sinr_dB(channel_state_information::sinr_type::channel_estimator,
+                    10.0F * std::log10(std::isnormal(noise) ? rsrp / noise : 0.0F));
+    // LDPC statistics in codeblock order (cb_stats semantics)
+    pusch_decoder_result dr;
+    dr.tb_crc_ok            = r.data.tb_crc_ok != 0;
+    dr.nof_codeblocks_total = e.nof_cbs;
+    dr.ldpc_decoder_stats.reset();
+    cb_stat_array& cs = *p.cb_stats;
+    for (unsigned cb = 0; cb != e.nof_cbs && cb < MAX_CB; ++cb) {
+      if (cb >= prev.size() || !prev[cb]) {
+        cs[cb] = cb_it[cb] >= 0 ? static_cast<unsigned>(cb_it[cb]) : cfg.dec_nof_iterations;
+      }
+      dr.ldpc_decoder_stats.update(cs[cb]);
+    }
+    std::memcpy(p.data.data(), tb, p.data.size());
+    if (p.rm_buffer.is_valid()) {
+      if (dr.tb_crc_ok) {
+        p.rm_buffer.release();
+      } else {
+        p.rm_buffer.unlock();
+      }
+    }
+    // UCI fields (pusch_processor_notifier_adaptor::check_and_notify_uci)
+    if (p.c.nof_harq_ack != 0 || p.c.nof_csi_part1 != 0) {
+      pusch_processor_result_control ctrl;
+      ctrl.csi      = csi;
+      auto field    = [](const uint8_t* bits, unsigned nbits, int32_t status, pusch_uci_field& f) {
+        f.payload = uci_payload_type(bits, bits + nbits);
+        f.status  = static_cast<uci_status>(status);
+      };
+      if (p.c.nof_harq_ack != 0) {
+        field(uci_row, p.c.nof_harq_ack, r.harq_ack_status, ctrl.harq_ack);
+      }
+      if (p.c.nof_csi_part1 != 0) {
+        field(uci_row + p.c.nof_harq_ack, p.c.nof_csi_part1, r.csi_part1_status, ctrl.csi_part1);
+      }
+      if (r.nof_csi_part2 != 0) {
+        field(uci_row + p.c.nof_harq_ack + p.c.nof_csi_part1, r.nof_csi_part2, r.csi_part2_status, ctrl.csi_part2);
+      }
+      p.notifier->on_uci(ctrl);
+    }
+    pusch_processor_result_data data;
+    data.data = dr;
+    data.csi  = csi;
+    p.notifier->on_sch(data);
+  }
+
+public:
+  std::atomic<uint64_t> stats_retx{0}, stats_redecodes{0};
+
+private:
+  pusch_processor_hip_config cfg;
+  const unsigned             nsubc;
+  int                        device = 0;
+  hipStream_t                stream = nullptr;
+  srs_amd_pusch_processor*   proc   = nullptr;
+  // collector-thread state
+  std::unordered_map<std::string, plan_entry> plans;
+  std::list<std::string>                      lru;
+  hip_mirrored_buffer                         h_grids, tbs, results, cbi, uci, pstats, soft;
+  // last: destroyed first, so the collector thread stops before the state it uses goes
+  std::unique_ptr<slot_collector<pending_pdu>> collector;
+};
+
+class pusch_processor_hip : public pusch_processor
+{
+public:
+  explicit pusch_processor_hip(std::shared_ptr<slot_engine> e) :
+    engine(std::move(e)), cb_stats(std::make_shared<cb_stat_array>())
+  {
+    cb_stats->fill(0);
+  }
+
+  void process(span<uint8_t>                    data,
+               unique_rx_buffer                 rm_buffer,
+               pusch_processor_result_notifier& notifier,
+               const resource_grid_reader&      grid,
+               const pdu_t&                     pdu) override
+  {
+    pending_pdu p;
+    p.data      = data;
+    p.rm_buffer = std::move(rm_buffer);
+    p.notifier  = &notifier;
+    p.grid      = &grid;
+    p.pdu       = pdu;
+    p.rx_ports.assign(pdu.rx_ports.begin(), pdu.rx_ports.end());
+    p.cb_stats = cb_stats;
+    p.error    = convert(pdu, data.size(), p.c);
+    engine->enqueue(std::move(p));
+  }
+
+private:
+  std::shared_ptr<slot_engine>   engine;
+  std::shared_ptr<cb_stat_array> cb_stats;
+};
+
+/// What the MI355X processor supports (the reference's pusch_processor_validator_impl checks, narrowed as
+/// convert() and srs_amd_pusch_processor_plan_create narrow them).
+class pusch_pdu_validator_hip : public pusch_pdu_validator
+{
+public:
+  explicit pusch_pdu_validator_hip(unsigned nof_prb_) : nof_prb(nof_prb_) {}
+  error_type<std::string> is_valid(const pusch_processor::pdu_t& pdu) const override
+  {
+    srs_amd_pusch_pdu c{};
+    std::string       e = convert(pdu, 1, c);
+    if (!e.empty()) {
+      return make_unexpected(e);
+    }
+    if (c.dmrs_type != 1) {
+      return make_unexpected(std::string("Only DM-RS Type 1 is currently supported."));
+    }
+    if (c.bwp_start_rb + c.bwp_size_rb > nof_prb || c.rb_start + c.rb_count > c.bwp_size_rb) {
+      return make_unexpected(std::string("Allocation outside the resource grid."));
+    }
+    if (c.start_symbol_index + c.nof_symbols > NSYMB) {
+      return make_unexpected(std::string("Time allocation outside the slot."));
+    }
+    return default_success_t();
+  }
+
+private:
+  unsigned nof_prb;
+};
+
+class pusch_processor_factory_hip_impl : public pusch_processor_factory_hip
+{
+public:
+  explicit pusch_processor_factory_hip_impl(const pusch_processor_hip_config& c) :
+    cfg(c), engine(std::make_shared<slot_engine>(c))
+  {
+  }
+  std::unique_ptr<pusch_processor> create() override { return std::make_unique<pusch_processor_hip>(engine); }
+  // The reference wraps its processors in its logging decorator (factories.cpp:393); the MI355X processors log
+  // their errors themselves.
+  std::unique_ptr<pusch_processor> create(srslog::basic_logger& /*logger*/) override { return create(); }
+  std::unique_ptr<pusch_pdu_validator> create_validator() override
+  {
+    return std::make_unique<pusch_pdu_validator_hip>(cfg.nof_prb);
+  }
+  void       flush() override { engine->flush(); }
+  void       wait_idle() override { engine->wait_idle(); }
+  statistics get_statistics() const override { return engine->get_statistics(); }
+
+private:
+  pusch_processor_hip_config   cfg;
+  std::shared_ptr<slot_engine> engine;
+};
+
+} // namespace
+
+std::shared_ptr<pusch_processor_factory_hip>
+srsran::hip::create_pusch_processor_factory_hip(const pusch_processor_hip_config& cfg)
+{
+  try {
+    return std::make_shared<pusch_processor_factory_hip_impl>(cfg);
+  } catch (const std::exception& e) {
+    log_error("factory", e.what());
+    return nullptr;
+  }
+}

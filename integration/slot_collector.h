@@ -1,0 +1,192 @@
+// slot_collector.h -- the batching policy shared by the MI355X channel-processor plug-ins (pusch_processor_hip,
+// pdsch_processor_hip): process() calls of the reference's upper PHY (one per PDU, from any thread) are queued,
+// and one collector thread hands the pending PDUs of a slot to the GPU as one batch when
+//   * flush() is called (the slot boundary),
+//   * a PDU of another slot arrives (the pending slot is complete),
+//   * max_batch PDUs are pending, or
+//   * the oldest pending PDU has waited max_wait_us (0: no timer).
+// The batch callback runs on the collector thread and calls each PDU's notifier.  wait_idle() blocks until every
+// PDU queued so far has been processed.  Destruction processes what is still pending, then joins the thread.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace srsran {
+namespace hip {
+
+template <typename Entry>
+class slot_collector
+{
+public:
+  /// process(batch) returns the number of PDUs it reported as failed.
+  using batch_function = std::function<unsigned(std::vector<Entry>&)>;
+
+  struct counters {
+    uint64_t nof_pdus = 0, nof_batches = 0, nof_errors = 0;
+  };
+
+  slot_collector(unsigned max_batch_, unsigned max_wait_us_, batch_function process_) :
+    max_batch(max_batch_ == 0 ? 1 : max_batch_), max_wait(max_wait_us_), process(std::move(process_))
+  {
+    worker = std::thread([this] { run(); });
+  }
+
+  ~slot_collector()
+  {
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      stop      = true;
+      flush_req = true;
+    }
+    cv.notify_all();
+    worker.join();
+  }
+
+  slot_collector(const slot_collector&)            = delete;
+  slot_collector& operator=(const slot_collector&) = delete;
+
+  /// Queues one PDU of slot `slot_key` (any value that differs between slots).
+  void enqueue(Entry&& e, uint64_t slot_key)
+  {
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      if (!queue.empty() && slot_key != queue_slot) {
+        cut = queue.size(); // the pending slot is complete
+      }
+      if (queue.empty() || cut == queue.size()) {
+        first_time = std::chrono::steady_clock::now();
+      }
+      queue_slot = slot_key;
+      queue.push_back(std::move(e));
+      ++in_flight;
+    }
+    cv.notify_all();
+  }
+
+  void flush()
+  {
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      flush_req = true;
+    }
+    cv.notify_all();
+  }
+
+  void wait_idle()
+  {
+    flush();
+    std::unique_lock<std::mutex> lock(mtx);
+    idle_cv.wait(lock, [this] { return in_flight == 0; });
+  }
+
+  counters get_counters() const
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    return stats;
+  }
+
+private:
+  void run()
+  {
+    std::unique_lock<std::mutex> lock(mtx);
+    while (true) {
+      const auto wait  = std::chrono::microseconds(max_wait);
+      auto       ready = [&] {
+        return !queue.empty() && (flush_req || stop || cut != 0 || queue.size() >= max_batch ||
+                                  (max_wait != 0 && std::chrono::steady_clock::now() - first_time >= wait));
+      };
+      if (queue.empty() && stop) {
+        break;
+      }
+      if (!ready()) {
+        if (max_wait != 0 && !queue.empty()) {
+          cv.wait_until(lock, first_time + wait);
+        } else {
+          cv.wait(lock);
+        }
+        continue;
+      }
+      // the complete slot (up to the cut), or everything pending, at most max_batch PDUs
+      const size_t       n = std::min<size_t>(cut != 0 ? cut : queue.size(), max_batch);
+      std::vector<Entry> batch;
+      batch.reserve(n);
+      for (size_t i = 0; i != n; ++i) {
+        batch.push_back(std::move(queue.front()));
+        queue.pop_front();
+      }
+      cut       = cut > n ? cut - n : 0;
+      flush_req = flush_req && !queue.empty();
+      if (!queue.empty()) {
+        first_time = std::chrono::steady_clock::now();
+      }
+      lock.unlock();
+      const unsigned errors = process(batch);
+      lock.lock();
+      stats.nof_pdus += batch.size();
+      stats.nof_batches += 1;
+      stats.nof_errors += errors;
+      in_flight -= batch.size();
+      if (in_flight == 0) {
+        idle_cv.notify_all();
+      }
+    }
+  }
+
+  const unsigned                        max_batch;
+  const unsigned                        max_wait;
+  batch_function                        process;
+  mutable std::mutex                    mtx;
+  std::condition_variable               cv, idle_cv;
+  std::deque<Entry>                     queue;
+  size_t                                cut        = 0; // queue[0, cut) is a complete slot
+  uint64_t                              queue_slot = 0;
+  std::chrono::steady_clock::time_point first_time;
+  bool                                  flush_req = false, stop = false;
+  size_t                                in_flight = 0;
+  counters                              stats;
+  std::thread                           worker;
+};
+
+/// Device buffer + pinned host mirror, grown on demand (contents not preserved).
+struct hip_mirrored_buffer {
+  uint8_t* d = nullptr;
+  uint8_t* h = nullptr;
+  size_t   n = 0;
+  hip_mirrored_buffer() = default;
+  hip_mirrored_buffer(const hip_mirrored_buffer&)            = delete;
+  hip_mirrored_buffer& operator=(const hip_mirrored_buffer&) = delete;
+  ~hip_mirrored_buffer()
+  {
+    (void)hipFree(d);
+    (void)hipHostFree(h);
+  }
+  bool ensure(size_t bytes)
+  {
+    if (bytes <= n) {
+      return true;
+    }
+    const size_t cap = std::max(bytes, n * 2);
+    (void)hipFree(d);
+    (void)hipHostFree(h);
+    d = h = nullptr;
+    n     = 0;
+    if (hipMalloc(&d, cap) != hipSuccess || hipHostMalloc(&h, cap, hipHostMallocDefault) != hipSuccess) {
+      return false;
+    }
+    n = cap;
+    return true;
+  }
+};
+
+} // namespace hip
+} // namespace srsran

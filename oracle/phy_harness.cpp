@@ -1,0 +1,343 @@
+// phy_harness.cpp -- TEST INFRASTRUCTURE: drives the MI355X channel-processor plug-ins of integration/
+// (libsrsran_amd_phy.so: pusch_processor_hip, pdsch_processor_hip) the way the reference's upper PHY does, so
+// tests/test_phy_plugins_gpu.py can compare them with the reference's own pusch_processor_impl /
+// pdsch_processor_impl (compiled from /root/reference into oracle/_ref/libsrsran_ref.so) on the same inputs:
+//   * received grids are the reference's resource_grid_reader_impl over a tensor (as ref_wrapper_pusch.cpp);
+//   * PUSCH PDUs arrive as the C-ABI's srs_amd_pusch_pdu (the Python tests' PuschPdu) and are turned into the
+//     reference's pusch_processor::pdu_t here, then handed to pusch_processor::process once per PDU -- what
+//     uplink_processor_impl::process_pusch does (uplink_processor_impl.cpp:270-326) -- with a result notifier per
+//     PDU and the reference's rx_buffer glue (ref_builders.h ref_rx_buffer) as HARQ buffer;
+//   * the slot boundary is the factory's flush(), completion its wait_idle().
+// Built by oracle/Makefile into oracle/_ref/libsrsran_ref_hw.so.  Never loaded by the product.
+#include "ref_builders.h"
+
+#include "../integration/pusch_processor_hip.h"
+#include "phy/support/resource_grid_reader_impl.h"
+#include "srsran/adt/tensor.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_processor_result_notifier.h"
+#include "srsran_amd/pusch_processor.h"
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+using namespace srsran;
+using namespace srs_ref;
+
+namespace {
+
+using grid_tensor =
+    dynamic_tensor<static_cast<unsigned>(resource_grid_dimensions::all), cbf16_t, resource_grid_dimensions>;
+
+/// A received slot grid: the reference's reader over a tensor [port][symbol][subcarrier].
+struct host_grid {
+  host_grid(const uint32_t* g, unsigned nports, unsigned nsubc) :
+    data({nsubc, MAX_NSYMB_PER_SLOT, nports}), reader(data, empty)
+  {
+    for (unsigned p = 0; p != nports; ++p) {
+      for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+        span<cbf16_t> row = data.get_view<static_cast<unsigned>(resource_grid_dimensions::symbol)>({l, p});
+        std::memcpy(row.data(), g + (p * MAX_NSYMB_PER_SLOT + l) * nsubc, nsubc * sizeof(cbf16_t));
+      }
+    }
+  }
+  grid_tensor               data;
+  std::atomic<unsigned>     empty{0};
+  resource_grid_reader_impl reader;
+};
+
+modulation_scheme scheme_of(int qm)
+{
+  switch (qm) {
+    case 0:
+      return modulation_scheme::PI_2_BPSK;
+    case 1:
+      return modulation_scheme::BPSK;
+    case 2:
+      return modulation_scheme::QPSK;
+    case 4:
+      return modulation_scheme::QAM16;
+    case 6:
+      return modulation_scheme::QAM64;
+    default:
+      return modulation_scheme::QAM256;
+  }
+}
+
+// srs_amd_pusch_pdu -> the reference's pdu_t (rx ports 0 .. nof_rx_ports - 1, type-1 allocation).
+pusch_processor::pdu_t to_pdu(const srs_amd_pusch_pdu& c)
+{
+  pusch_processor::pdu_t pdu = {};
+  pdu.slot                   = slot_point(c.numerology, c.slot_index);
+  pdu.rnti                   = static_cast<uint16_t>(c.rnti);
+  pdu.bwp_size_rb            = c.bwp_size_rb;
+  pdu.bwp_start_rb           = c.bwp_start_rb;
+  pdu.cp                     = cyclic_prefix::NORMAL;
+  pdu.mcs_descr              = sch_mcs_description{scheme_of(c.modulation), c.target_code_rate};
+  pdu.codeword.emplace(pusch_processor::codeword_description{
+      c.rv, c.base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2, c.new_data != 0});
+  pdu.uci.nof_harq_ack          = c.nof_harq_ack;
+  pdu.uci.nof_csi_part1         = c.nof_csi_part1;
+  pdu.uci.alpha_scaling         = c.alpha_scaling;
+  pdu.uci.beta_offset_harq_ack  = c.beta_offset_harq_ack;
+  pdu.uci.beta_offset_csi_part1 = c.beta_offset_csi_part1;
+  pdu.uci.beta_offset_csi_part2 = c.beta_offset_csi_part2;
+  for (unsigned e = 0; e != c.csi_part2_size.nof_entries; ++e) {
+    const srs_amd_uci_part2_entry&     x  = c.csi_part2_size.entries[e];
+    uci_part2_size_description::entry& en = pdu.uci.csi_part2_size.entries.emplace_back();
+    for (unsigned q = 0; q != x.nof_parameters; ++q) {
+      en.parameters.push_back(
+          uci_part2_size_description::parameter{x.parameters[q].offset, static_cast<uint8_t>(x.parameters[q].width)});
+    }
+    for (unsigned m = 0; m != x.map_size; ++m) {
+      en.map.push_back(x.map[m]);
+    }
+  }
+  pdu.n_id          = c.n_id;
+  pdu.nof_tx_layers = c.nof_tx_layers;
+  for (unsigned p = 0; p != c.nof_rx_ports; ++p) {
+    pdu.rx_ports.push_back(static_cast<uint8_t>(p));
+  }
+  pdu.dmrs_symbol_mask = symbol_slot_mask(MAX_NSYMB_PER_SLOT);
+  for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+    if ((c.dmrs_symbol_mask >> l) & 1u) {
+      pdu.dmrs_symbol_mask.set(l);
+    }
+  }
+  if (c.transform_precoding) {
+    pdu.dmrs = pusch_processor::dmrs_transform_precoding_configuration{.n_rs_id = c.n_rs_id};
+  } else {
+    pdu.dmrs = pusch_processor::dmrs_configuration{.dmrs          = c.dmrs_type == 2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1,
+                                                   .scrambling_id = c.scrambling_id,
+                                                   .n_scid        = c.n_scid != 0,
+                                                   .nof_cdm_groups_without_data = c.nof_cdm_groups_without_data};
+  }
+  pdu.freq_alloc         = rb_allocation::make_type1(c.rb_start, c.rb_count);
+  pdu.start_symbol_index = c.start_symbol_index;
+  pdu.nof_symbols        = c.nof_symbols;
+  pdu.tbs_lbrm           = c.tbs_lbrm_bytes ? units::bytes(c.tbs_lbrm_bytes) : tbs_lbrm_default;
+  return pdu;
+}
+
+/// The notifications of one process() call.
+class ticket : public pusch_processor_result_notifier
+{
+public:
+  void on_uci(const pusch_processor_result_control& u) override
+  {
+    uci = u;
+    ++nof_uci;
+  }
+  void on_sch(const pusch_processor_result_data& s) override
+  {
+    sch = s;
+    done.store(true, std::memory_order_release);
+  }
+  pusch_processor_result_control uci;
+  pusch_processor_result_data    sch;
+  unsigned                       nof_uci = 0;
+  std::atomic<bool>              done{false};
+};
+
+struct pusch_ctx {
+  std::shared_ptr<hip::pusch_processor_factory_hip> factory;
+  std::unique_ptr<pusch_processor>                  proc;
+  std::deque<ticket>                                tickets;
+  std::mutex                                        mtx;
+};
+
+void bits_out(const uci_payload_type& p, uint8_t* out)
+{
+  for (unsigned i = 0; i != p.size(); ++i) {
+    out[i] = p.test(i) ? 1 : 0;
+  }
+}
+
+} // namespace
+
+extern "C" {
+
+/* The MI355X PUSCH processor factory (pusch_processor_factory_hip) and one of its processors. eq: 0 ZF, 1 MMSE.
+ * max_wait_us: the collector's timer (0: only flush / slot change / batch size).  NULL on failure. */
+void* srs_ref_phy_pusch_create(int device, unsigned nof_prb, unsigned iterations, int eq, int generic,
+                               unsigned max_wait_us)
+{
+  hip::pusch_processor_hip_config cfg;
+  cfg.device             = device;
+  cfg.nof_prb            = nof_prb;
+  cfg.dec_nof_iterations = iterations;
+  cfg.equalizer = eq ? channel_equalizer_algorithm_type::mmse : channel_equalizer_algorithm_type::zf;
+  cfg.generic_ldpc = generic != 0;
+  cfg.max_wait_us  = max_wait_us;
+  auto f           = hip::create_pusch_processor_factory_hip(cfg);
+  if (!f) {
+    return nullptr;
+  }
+  auto* ctx    = new pusch_ctx;
+  ctx->factory = f;
+  ctx->proc    = f->create();
+  return ctx;
+}
+
+void srs_ref_phy_pusch_destroy(void* h)
+{
+  auto* ctx = static_cast<pusch_ctx*>(h);
+  ctx->factory->wait_idle();
+  delete ctx;
+}
+
+/* A second processor of the same factory (shares the collector): another cell of the node. */
+void* srs_ref_phy_pusch_sibling(void* h)
+{
+  auto* base   = static_cast<pusch_ctx*>(h);
+  auto* ctx    = new pusch_ctx;
+  ctx->factory = base->factory;
+  ctx->proc    = base->factory->create();
+  return ctx;
+}
+
+void* srs_ref_phy_grid_create(const uint32_t* grid, unsigned nports, unsigned nsubc)
+{
+  return new host_grid(grid, nports, nsubc);
+}
+
+void srs_ref_phy_grid_destroy(void* g)
+{
+  delete static_cast<host_grid*>(g);
+}
+
+/* pusch_processor::process of one PDU (asynchronous); rx_buffer: an srs_ref_rx_buffer_create handle or NULL (no
+ * HARQ buffer, as a failed reservation).  Returns the ticket of the call. */
+int srs_ref_phy_pusch_process(void* h, void* grid, const srs_amd_pusch_pdu* c, void* rx_buffer, uint8_t* tb,
+                              unsigned tb_bytes)
+{
+  auto*   ctx = static_cast<pusch_ctx*>(h);
+  ticket* t;
+  int     id;
+  {
+    std::lock_guard<std::mutex> lock(ctx->mtx);
+    id = static_cast<int>(ctx->tickets.size());
+    t  = &ctx->tickets.emplace_back();
+  }
+  unique_rx_buffer buf = rx_buffer ? unique_rx_buffer(*static_cast<ref_rx_buffer*>(rx_buffer)) : unique_rx_buffer();
+  ctx->proc->process(span<uint8_t>(tb, tb_bytes), std::move(buf), *t, static_cast<host_grid*>(grid)->reader,
+                     to_pdu(*c));
+  return id;
+}
+
+void srs_ref_phy_pusch_flush(void* h)
+{
+  static_cast<pusch_ctx*>(h)->factory->flush();
+}
+
+void srs_ref_phy_pusch_wait(void* h)
+{
+  static_cast<pusch_ctx*>(h)->factory->wait_idle();
+}
+
+/* Result of a ticket: 0 not notified yet, 1 done.  result[0..5] as srs_ref_pusch_process (tb_crc_ok, nof_codeblocks,
+ * LDPC observations, sum, min, max); csi[0..4] = SINR, EPRE, RSRP (dB), time alignment (s), CFO (Hz, NaN: none);
+ * uci[0..4] = on_uci calls, HARQ-ACK / CSI part 1 / CSI part 2 statuses, CSI part 2 bits; payloads one bit per
+ * byte into ack / csi1 / csi2 (NULL: not returned). */
+int srs_ref_phy_pusch_result(void* h, int id, double* result, double* csi, int* uci, uint8_t* ack, uint8_t* csi1,
+                             uint8_t* csi2)
+{
+  auto*   ctx = static_cast<pusch_ctx*>(h);
+  ticket* t;
+  {
+    std::lock_guard<std::mutex> lock(ctx->mtx);
+    if (id < 0 || static_cast<size_t>(id) >= ctx->tickets.size()) {
+      return -1;
+    }
+    t = &ctx->tickets[id];
+  }
+  if (!t->done.load(std::memory_order_acquire)) {
+    return 0;
+  }
+  const pusch_decoder_result& r  = t->sch.data;
+  const auto&                 st = r.ldpc_decoder_stats;
+  result[0]                      = r.tb_crc_ok ? 1 : 0;
+  result[1]                      = r.nof_codeblocks_total;
+  result[2]                      = st.get_nof_observations();
+  result[3]                      = st.get_mean() * st.get_nof_observations();
+  result[4]                      = st.get_min();
+  result[5]                      = st.get_max();
+  const channel_state_information& c = t->sch.csi;
+  csi[0]                             = c.get_sinr_dB().value_or(NAN);
+  csi[1]                             = c.get_epre_dB().value_or(NAN);
+  csi[2]                             = c.get_rsrp_dB().value_or(NAN);
+  csi[3]                             = c.get_time_alignment().has_value() ? c.get_time_alignment()->to_seconds() : NAN;
+  csi[4]                             = c.get_cfo_Hz().value_or(NAN);
+  uci[0]                             = static_cast<int>(t->nof_uci);
+  uci[1]                             = static_cast<int>(t->uci.harq_ack.status);
+  uci[2]                             = static_cast<int>(t->uci.csi_part1.status);
+  uci[3]                             = static_cast<int>(t->uci.csi_part2.status);
+  uci[4]                             = static_cast<int>(t->uci.csi_part2.payload.size());
+  if (ack != nullptr) {
+    bits_out(t->uci.harq_ack.payload, ack);
+  }
+  if (csi1 != nullptr) {
+    bits_out(t->uci.csi_part1.payload, csi1);
+  }
+  if (csi2 != nullptr) {
+    bits_out(t->uci.csi_part2.payload, csi2);
+  }
+  return 1;
+}
+
+/* Plug-in statistics: PDUs, batches, errors, HARQ re-decodes, retransmissions. */
+void srs_ref_phy_pusch_stats(void* h, uint64_t* out)
+{
+  const auto s = static_cast<pusch_ctx*>(h)->factory->get_statistics();
+  out[0]       = s.nof_pdus;
+  out[1]       = s.nof_batches;
+  out[2]       = s.nof_errors;
+  out[3]       = s.nof_harq_redecodes;
+  out[4]       = s.nof_retransmissions;
+}
+
+/* Throughput through the plug-in as the upper PHY drives it: every step, one PDU per cell grid (nof_cells grids,
+ * each with its own processor of the factory, i.e. one cell each), process() per PDU, flush() at the slot boundary,
+ * wait for every notification.  tbs:
+ * nof_cells rows of tb_bytes.  Returns seconds per step over `steps` timed steps after `warmup`; ok_out: TBs with
+ * CRC OK in the timed steps. */
+double srs_ref_phy_pusch_bench(void* h, void* const* grids, unsigned nof_cells, const srs_amd_pusch_pdu* c,
+                               unsigned warmup, unsigned steps, uint8_t* tbs, unsigned tb_bytes, unsigned* ok_out)
+{
+  auto*                                         ctx = static_cast<pusch_ctx*>(h);
+  std::vector<std::unique_ptr<pusch_processor>> procs;
+  for (unsigned i = 0; i != nof_cells; ++i) {
+    procs.push_back(ctx->factory->create());
+  }
+  std::vector<ticket>    tickets(nof_cells);
+  const srs_amd_pusch_pdu pc = *c; // the grids hold one slot's DM-RS: every step is that slot again
+  unsigned                ok = 0;
+  auto                   t0    = std::chrono::steady_clock::now();
+  for (unsigned s = 0; s != warmup + steps; ++s) {
+    if (s == warmup) {
+      t0 = std::chrono::steady_clock::now();
+    }
+    const pusch_processor::pdu_t pdu = to_pdu(pc);
+    for (unsigned i = 0; i != nof_cells; ++i) {
+      tickets[i].done.store(false);
+      procs[i]->process(span<uint8_t>(tbs + static_cast<size_t>(i) * tb_bytes, tb_bytes), unique_rx_buffer(),
+                        tickets[i], static_cast<host_grid*>(grids[i])->reader, pdu);
+    }
+    ctx->factory->flush();
+    ctx->factory->wait_idle();
+    if (s >= warmup) {
+      for (unsigned i = 0; i != nof_cells; ++i) {
+        ok += tickets[i].sch.data.tb_crc_ok ? 1 : 0;
+      }
+    }
+  }
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  *ok_out         = ok;
+  return steps ? dt / steps : 0.0;
+}
+
+} // extern "C"

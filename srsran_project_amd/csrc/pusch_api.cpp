@@ -604,6 +604,29 @@ void srs_amd_pusch_decoder_destroy(srs_amd_pusch_decoder* dec)
   delete dec;
 }
 
+int srs_amd_pusch_soft_buffer_layout(const srs_amd_sch_plan* plan, uint32_t* row_bytes, uint32_t* nof_llrs,
+                                     uint32_t* msg_offset, uint32_t* flag_offset)
+{
+  const int rc = check_plan(plan);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  const soft_row_layout l = layout_of(plan);
+  if (row_bytes != nullptr) {
+    *row_bytes = l.row_bytes;
+  }
+  if (nof_llrs != nullptr) {
+    *nof_llrs = l.soft_bytes;
+  }
+  if (msg_offset != nullptr) {
+    *msg_offset = l.msg_offset;
+  }
+  if (flag_offset != nullptr) {
+    *flag_offset = l.flag_offset;
+  }
+  return SRS_AMD_OK;
+}
+
 uint32_t srs_amd_pusch_decoder_llr_prefix(const srs_amd_sch_plan* plan, int new_data, int fresh)
 {
   if (plan == nullptr || plan->nof_segments == 0 || plan->lifting_size == 0) {

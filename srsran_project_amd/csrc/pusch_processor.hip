@@ -14,7 +14,8 @@ __global__ __launch_bounds__(64) void pusch_result_kernel(pusch_result_args a)
     return;
   }
   const uint32_t                  P  = a.port_counts != nullptr ? a.port_counts[g] : a.nof_ports;
-  const srs_amd_chest_port_stats* st = a.stats + static_cast<size_t>(g) * (a.stats_stride ? a.stats_stride : P);
+  const uint32_t                  sg = (a.stats_by_id && a.result_ids != nullptr) ? a.result_ids[g] : g;
+  const srs_amd_chest_port_stats* st = a.stats + static_cast<size_t>(sg) * (a.stats_stride ? a.stats_stride : P);
   float    noise = 0.0f, rsrp = 0.0f, epre = 0.0f, best_snr = 0.0f;
   uint32_t best  = 0;
   for (uint32_t p = 0; p < P; ++p) {

@@ -720,6 +720,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
   const uint32_t     nof_subc     = pdus[0].plan != nullptr ? pdus[0].plan->nof_subc : 0;
   int32_t* const     cb_iters     = io != nullptr ? io->d_cb_iterations : nullptr;
   uint8_t* const     d_uci        = io != nullptr ? io->d_uci : nullptr;
+  srs_amd_chest_port_stats* const out_stats = io != nullptr ? io->d_port_stats : nullptr;
   // the fused group (new data, no UCI, CP-OFDM, no soft buffer to keep) and the PDUs of the batch chain
   std::vector<uint32_t> fused, others;
   for (uint32_t i = 0; i != nof_pdus; ++i) {
@@ -748,6 +749,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     const srs_amd_pusch_processor_plan* pl = pdus[i].plan;
     srs_amd_pusch_intermediates         x{};
     x.d_cb_iterations = cb_iters != nullptr ? cb_iters + pdus[i].cb_offset : nullptr;
+    x.d_port_stats    = out_stats != nullptr ? out_stats + static_cast<size_t>(STATS_STRIDE) * i : nullptr;
     if (d_uci != nullptr && pl->uci) {
       uint8_t* row       = d_uci + pdus[i].uci_offset;
       x.d_harq_ack       = pl->pdu.nof_harq_ack != 0 ? row : nullptr;
@@ -800,14 +802,16 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     return hip_fail(e, "PUSCH processor slot scratch");
   }
   call_scope scope(proc->order, nullptr, s);
-  auto*      st   = proc->stats.as<srs_amd_chest_port_stats>();
+  // port measurements of fused PDU k at st + k * STATS_STRIDE, or straight in the caller's buffer at its PDU index
+  auto*      st   = out_stats != nullptr ? out_stats : proc->stats.as<srs_amd_chest_port_stats>();
   auto*      llrs = proc->llrs.as<int8_t>();
+  auto       stats_of = [&](uint32_t k) { return st + static_cast<size_t>(out_stats ? fused[k] : k) * STATS_STRIDE; };
   // 2a. channel estimation of every fused PDU (one launch sequence)
   std::vector<chest_slot_item> citems(n);
   for (uint32_t k = 0; k != n; ++k) {
     const srs_amd_pusch_slot_pdu& u = pdus[fused[k]];
     citems[k] = chest_slot_item{&u.plan->chest_cfg, d_grids + u.grid * grid_stride, u.plan->pdu.nof_rx_ports,
-                                st + static_cast<size_t>(k) * STATS_STRIDE};
+                                stats_of(k)};
   }
   std::vector<chest_args> views(n);
   int rc = chest_estimate_slot_unexpanded(proc->chest, citems.data(), n, nof_subc, stream, views.data());
@@ -852,6 +856,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     a.nof_ports    = 0;
     a.port_counts  = proc->slot_ports.as<uint32_t>();
     a.stats_stride = STATS_STRIDE;
+    a.stats_by_id  = out_stats != nullptr;
     a.result_ids   = subset ? reinterpret_cast<const uint32_t*>(proc->slot_ports.as<uint8_t>() + o_ids) : nullptr;
     e              = launch_pusch_result(a, s);
   }

@@ -25,6 +25,8 @@ struct pusch_result_args {
   uint32_t                            uci_mask     = 0;
   // slot form with PDUs outside the fused group: result g goes to results[result_ids[g]]
   const uint32_t*                     result_ids   = nullptr;
+  // the port measurements of result g are those of PDU result_ids[g] (caller's per-PDU buffer)
+  bool                                stats_by_id  = false;
 };
 
 hipError_t launch_pusch_result(const pusch_result_args& a, hipStream_t stream);

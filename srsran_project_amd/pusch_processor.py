@@ -128,7 +128,7 @@ class PuschSlotPdu(ctypes.Structure):
 class PuschSlotIo(ctypes.Structure):
     """``srs_amd_pusch_slot_io``: optional outputs of srs_amd_pusch_process_slot_ex."""
 
-    _fields_ = [("d_cb_iterations", ctypes.c_void_p), ("d_uci", ctypes.c_void_p)]
+    _fields_ = [("d_cb_iterations", ctypes.c_void_p), ("d_uci", ctypes.c_void_p), ("d_port_stats", ctypes.c_void_p)]
 
 
 def make_pdu(**kw):
@@ -303,11 +303,13 @@ class PuschProcessor:
             "pusch_process_batch")
         return tbs, results
 
-    def process_slot(self, grids, pdus, tbs=None, results=None, stream=None, cb_iterations=None, uci=None):
+    def process_slot(self, grids, pdus, tbs=None, results=None, stream=None, cb_iterations=None, uci=None,
+                     port_stats=None):
         """Device: every PDU of a slot in one launch sequence (uplink_processor_impl::process_pusch per PDU).
         grids int32 [n][P][14][nsubc]; pdus: a PuschSlot or a list of (plan, grid index[, soft buffer tensor]).
         Optional outputs: cb_iterations int32 [slot.cb_total] (per-codeblock iteration counts, PDU u's from
-        slot.cb_offsets[u]), uci uint8 [slot.uci_total] (UCI payload rows at slot.uci_offsets[u]).  Returns (tbs
+        slot.cb_offsets[u]), uci uint8 [slot.uci_total] (UCI payload rows at slot.uci_offsets[u]), port_stats float32
+        [len(pdus)][4][6] (estimator measurements per PDU and receive port).  Returns (tbs
         uint8 flat, tb offsets, results uint8 [len(pdus)][RESULT_BYTES])."""
         import torch
 
@@ -320,9 +322,10 @@ class PuschProcessor:
         if stream is None:
             stream = torch.cuda.current_stream(dev)
         io = None
-        if cb_iterations is not None or uci is not None:
+        if cb_iterations is not None or uci is not None or port_stats is not None:
             io = PuschSlotIo(None if cb_iterations is None else cb_iterations.data_ptr(),
-                             None if uci is None else uci.data_ptr())
+                             None if uci is None else uci.data_ptr(),
+                             None if port_stats is None else port_stats.data_ptr())
         _lib.check(self._lib.srs_amd_pusch_process_slot_ex(
             self._h, slot.arr, slot.n, grids.data_ptr(), grids.stride(0), grids.shape[0], tbs.data_ptr(),
             results.data_ptr(), None if io is None else ctypes.byref(io), ctypes.c_void_p(stream.cuda_stream)),

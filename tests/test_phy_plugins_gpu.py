@@ -1,0 +1,163 @@
+"""The channel-processor level of the boundary: the MI355X pusch_processor plug-in (integration/pusch_processor_hip,
+a pusch_processor_factory whose processors feed one slot collector that runs srs_amd_pusch_process_slot_ex) driven
+as the reference's upper PHY drives a pusch_processor -- one process() call per PDU on a shared received grid
+(uplink_processor_impl.cpp:270-326), results through pusch_processor_result_notifier, HARQ state in the reference's
+rx_buffer -- against the REFERENCE's own pusch_processor_impl (oracle/_ref) called once per PDU on the same grid.
+
+Bars: transport block bytes, TB CRC flags and LDPC iteration statistics (observations, sum, min, max) identical;
+CSI within the estimator tolerances (SINR / EPRE / RSRP 0.05 dB, time alignment 2 ns); UCI payloads and statuses
+identical, on_uci called exactly when the PDU carries UCI.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import srsran_project_amd as amd
+from oracle import pusch_proc as pp
+
+pytestmark = pytest.mark.gpu
+
+ITERS = 6
+
+
+@pytest.fixture(scope="module")
+def phy():
+    import torch
+
+    torch.cuda.init()
+    import oracle
+    from oracle import phy as ophy
+
+    return ophy, oracle
+
+
+def _check(got, want, tag):
+    assert got is not None, tag + ": not notified"
+    assert got["tb_crc_ok"] == want["tb_crc_ok"], tag
+    assert got["nof_codeblocks_total"] == want["nof_codeblocks_total"], tag
+    for k in ("nof_observations", "iterations_sum", "iterations_min", "iterations_max"):
+        assert got[k] == want[k], (tag, k, got[k], want[k])
+    for k in ("sinr_db", "epre_db", "rsrp_db"):
+        assert abs(got[k] - want[k]) <= 0.05, (tag, k, got[k], want[k])
+    assert abs(got["time_alignment_s"] - want["time_alignment_s"]) <= 2e-9, (tag, "ta")
+
+
+def _run_slot(ophy, oracle, plug, grid, pdus, bufs, ref_bufs):
+    """process() per PDU on one grid, flush, wait; returns [(got, got_tb, want, want_tb)]."""
+    g = ophy.Grid(grid)
+    tickets = []
+    for pdu in pdus:
+        key = pdu["rnti"]
+        if key not in bufs:
+            C = pp.nof_codeblocks(pdu["tbs"], pdu["base_graph"])
+            bufs[key], ref_bufs[key] = oracle.RefRxBuffer(C), oracle.RefRxBuffer(C)
+        tickets.append(plug.process(g, amd.make_pdu(**pdu), pdu["tbs"] // 8, rx_buffer=bufs[key]))
+    plug.flush()
+    plug.wait()
+    out = []
+    for pdu, (t, tb) in zip(pdus, tickets):
+        P = pdu["nof_rx_ports"]
+        want_tb, want = pp.ref_pusch_process(grid[:P], pdu, pdu["tbs"] // 8, iterations=ITERS,
+                                             rx_buffer=ref_bufs[pdu["rnti"]])
+        got = plug.result(t, pdu.get("nof_harq_ack", 0), pdu.get("nof_csi_part1", 0))
+        out.append((got, tb, want, want_tb))
+    return out
+
+
+def test_pusch_plugin_mixed_slots_vs_reference(phy):
+    """every PDU kind of a slot (UCI on PUSCH, DFT-s-OFDM, a HARQ process rv 0 -> rv 2, plain PDUs) on
+    one four-port grid, two consecutive slots, through pusch_processor::process of the plug-in, equal to the
+    reference's pusch_processor_impl on the same grid and PDUs (HARQ state kept in one rx_buffer per UE on each
+    side)."""
+    ophy, oracle = phy
+    from pusch_slot_cases import mixed_slot
+
+    plug = ophy.PuschProcessorPlugin(device=0, iterations=ITERS)
+    bufs, ref_bufs = {}, {}
+    for slot_index, rv in ((3, 0), (4, 2)):
+        grid, pdus, sent = mixed_slot(slot_index, rv, seed=slot_index)
+        for pdu, (tb_sent, uci_sent), (got, tb, want, want_tb) in zip(
+                pdus, sent, _run_slot(ophy, oracle, plug, grid, pdus, bufs, ref_bufs)):
+            tag = "slot %d rnti %#x" % (slot_index, pdu["rnti"])
+            _check(got, want, tag)
+            assert np.array_equal(tb, want_tb), tag
+            if pdu.get("nof_harq_ack", 0):
+                assert got["nof_uci"] == 1, tag
+                assert got["harq_ack_status"] == want["harq_ack_status"] == 1, tag
+                assert got["csi_part1_status"] == want["csi_part1_status"] == 1, tag
+                assert np.array_equal(got["harq_ack"], want["harq_ack"]), tag
+                assert np.array_equal(got["csi_part1"], want["csi_part1"]), tag
+            else:
+                assert got["nof_uci"] == 0, tag
+            if pdu["rnti"] == 0x5003:
+                assert want["tb_crc_ok"] == (rv == 2), tag
+            else:
+                assert want["tb_crc_ok"] and np.array_equal(tb, tb_sent), tag
+    s = plug.stats()
+    assert s["pdus"] == 10 and s["errors"] == 0, s
+    assert s["harq_redecodes"] == 1 and s["retransmissions"] == 1, s
+
+
+def test_pusch_plugin_two_cells_one_collector(phy):
+    """Two cells (two processors of one factory, two grids, different slots) queued before one flush: the collector
+    cuts the batch at the slot change and both cells' PDUs equal the reference."""
+    ophy, oracle = phy
+    from pusch_slot_cases import mixed_slot
+
+    plug = ophy.PuschProcessorPlugin(device=0, iterations=ITERS)
+    cell2 = ophy.PuschProcessorPlugin(sibling_of=plug)
+    grid_a, pdus_a, _ = mixed_slot(6, 0, seed=11, kinds=["uci", "plain", "plain2"])
+    grid_b, pdus_b, _ = mixed_slot(7, 0, seed=12, kinds=["tp", "plain", "plain2"])
+    ga, gb = ophy.Grid(grid_a), ophy.Grid(grid_b)
+    tickets = [(plug, plug.process(ga, amd.make_pdu(**p), p["tbs"] // 8), p, grid_a) for p in pdus_a]
+    tickets += [(cell2, cell2.process(gb, amd.make_pdu(**p), p["tbs"] // 8), p, grid_b) for p in pdus_b]
+    plug.flush()
+    plug.wait()
+    for proc, (t, tb), pdu, grid in tickets:
+        P = pdu["nof_rx_ports"]
+        want_tb, want = pp.ref_pusch_process(grid[:P], pdu, pdu["tbs"] // 8, iterations=ITERS)
+        tag = "slot %d rnti %#x" % (pdu["slot_index"], pdu["rnti"])
+        _check(proc.result(t, pdu.get("nof_harq_ack", 0), pdu.get("nof_csi_part1", 0)), want, tag)
+        assert np.array_equal(tb, want_tb), tag
+    s = plug.stats()
+    assert s["batches"] >= 2 and s["pdus"] == len(tickets), s
+
+
+def test_pusch_plugin_timer_flush(phy):
+    """Without flush() the collector's timer (max_wait_us) runs the pending PDUs: the notifier is called."""
+    ophy, oracle = phy
+    from pusch_slot_cases import mixed_slot
+
+    plug = ophy.PuschProcessorPlugin(device=0, iterations=ITERS, max_wait_us=500)
+    grid, pdus, sent = mixed_slot(2, 0, seed=21, kinds=["plain"])
+    g = ophy.Grid(grid)
+    t, tb = plug.process(g, amd.make_pdu(**pdus[0]), pdus[0]["tbs"] // 8)
+    deadline = time.time() + 30
+    got = None
+    while got is None and time.time() < deadline:
+        time.sleep(0.01)
+        got = plug.result(t)
+    assert got is not None and got["tb_crc_ok"] and np.array_equal(tb, sent[0][0])
+
+
+def test_pusch_plugin_unsupported_pdu_reports_failure(phy):
+    """A PDU the MI355X processor does not support (DM-RS type 2, which the reference's own validator also rejects)
+    is notified as a failed transmission -- HARQ-ACK invalid through on_uci, on_sch with the TB CRC KO -- instead of
+    stalling the upper PHY; the other PDUs of the slot are unaffected."""
+    ophy, oracle = phy
+    from pusch_slot_cases import mixed_slot
+
+    plug = ophy.PuschProcessorPlugin(device=0, iterations=ITERS)
+    grid, pdus, sent = mixed_slot(2, 0, seed=22, kinds=["uci", "plain"])
+    g = ophy.Grid(grid)
+    bad = dict(pdus[0], dmrs_type=2)
+    t_bad, _ = plug.process(g, amd.make_pdu(**bad), bad["tbs"] // 8)
+    t_ok, tb = plug.process(g, amd.make_pdu(**pdus[1]), pdus[1]["tbs"] // 8)
+    plug.flush()
+    plug.wait()
+    got = plug.result(t_bad, bad["nof_harq_ack"], bad["nof_csi_part1"])
+    assert got is not None and not got["tb_crc_ok"] and got["nof_uci"] == 1 and got["harq_ack_status"] == 2
+    got = plug.result(t_ok)
+    assert got["tb_crc_ok"] and np.array_equal(tb, sent[1][0])
+    assert plug.stats()["errors"] == 1
