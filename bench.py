@@ -88,6 +88,8 @@ def parse():
                    help="pipeline: PUSCH layers (4: MMSE 4x4, parity unpinned; 2: the reference-pinned ZF 2x4)")
     p.add_argument("--ingest", action="store_true",
                    help="pipeline, N > 1: rank 0 holds all cells' slot inputs; RCCL scatter / gather every step")
+    p.add_argument("--no-pinned", action="store_true",
+                   help="pipeline: skip the reference-pinned sibling line (PUSCH 2 layers x 4 rx, ZF)")
     p.add_argument("--no-latency", action="store_true",
                    help="pipeline: skip the 1 / 8 cell latency figures; sch_slot: skip the per-UE launch timing")
     p.add_argument("--ues-per-cell", type=int, default=8, help="sch_slot: UEs sharing each cell's 273 PRBs")

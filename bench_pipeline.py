@@ -407,6 +407,9 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = pipeline_cpu_baseline(args, pl)
+    pinned = None
+    if world == 1 and L > 2 and not getattr(args, "no_pinned", False):
+        pinned = pinned_sibling_line(args, dev, timed, dist, cpu)
     return {
         "metric": "PDSCH+PUSCH codeblocks/s @ 100 MHz 273-PRB %dx%d MIMO (PDSCH %d layers, PUSCH %d layers x %d rx)"
                   % (pl.dl_ports, pl.ul_ports, pl.dl_layers, L, pl.ul_ports),
@@ -423,8 +426,11 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         "data": "synthetic (random transport blocks; PUSCH from a UE transmission through a %dx4 channel + AWGN "
                 "%.0f dB)" % (L, pl.snr_db),
         "config": {
-            "workload": "configs[3]/headline: full PDSCH+PUSCH slot pipeline, 100 MHz numerology-1 273 PRB, "
-                        "256QAM R=948/1024",
+            "workload": "BASELINE metric (PDSCH+PUSCH codeblocks/s @ 100 MHz 273-PRB %dx%d MIMO): full PDSCH+PUSCH "
+                        "slot pipeline, 100 MHz numerology-1 273 PRB, 256QAM R=948/1024" % (pl.dl_ports, pl.ul_ports)
+                        if (pl.dl_ports, pl.ul_ports) == (4, 4) else
+                        "configs[3] (%dx%d MIMO): full PDSCH+PUSCH slot pipeline, 100 MHz numerology-1 273 PRB, "
+                        "256QAM R=948/1024" % (pl.dl_ports, pl.ul_ports),
             "cells_per_step_per_gpu": S,
             "pdsch": {"layers": pl.dl_layers, "ports": pl.dl_ports, "tbs": pl.tbs_dl, "codeblocks": cbs_dl},
             "pusch": {"layers": L, "rx_ports": pl.ul_ports, "tbs": pl.tbs_ul, "codeblocks": cbs_ul,
@@ -445,6 +451,7 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         "latency_ms": lat,
         "ingest_ms_per_step": ingest_ms,
         "low_snr": low,
+        "pinned_sibling": pinned,
         "roofline": {
             "bound": "hbm",
             "kernel": "ldpc_decode_hr_kernel (PUSCH codeblocks of one step, BG%d Z=%d, CRC24B early stop, <= %d it; "
@@ -461,7 +468,8 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
             "limiter": "valu",
             "valu": valu,
             "note": "bound/achieved/peak/frac: the decoder's HBM roofline (algorithmic bytes / measured kernel time / "
-                    "8 TB/s; PMC traffic = algorithmic bytes, no re-reads) -- far from HBM-bound.  Its limiter is VALU "
+                    "8 TB/s; traffic = PMC FETCH + WRITE bytes of the same launch, see DESIGN.md for its split against "
+                    "the algorithmic bytes) -- far from HBM-bound.  Its limiter is VALU "
                     "issue: valu.achieved_frac_of_peak_issue = modelled VALU issue cycles (PMC SQ_ACTIVE_INST_VALU "
                     "per codeblock and iteration, profiles/ldpc_valu_model.json) / (1,024 SIMDs x 2.4 GHz x kernel "
                     "time); the PMC-measured busy fraction of the same command is in profiles/r03_pmc_table.json",
@@ -492,6 +500,31 @@ def valu_bound(cbs, its_mean, kernel_ms):
     return {"achieved_frac_of_peak_issue": issue_s * 1e3 / kernel_ms, "issue_bound_ms": issue_s * 1e3,
             "kernel_ms": kernel_ms, "valu_issue_cycles": cycles, "basis": basis, "model": os.path.basename(path),
             "iterations_mean": its_mean}
+
+
+def pinned_sibling_line(args, dev, timed, dist, cpu):
+    """The reference-runnable form of the headline's 4x4-port slot: the same cells with the PUSCH at 2 layers x 4 rx
+    ports and the reference's ZF equalizer (every stage pinned to the compiled reference; the headline's 4-layer MMSE
+    solve has no open-reference counterpart).  Its CPU comparison is exactly the cpu_baseline of the main line, whose
+    reference chain runs this 2-layer PUSCH: the same work on both sides."""
+    import torch
+
+    pl = Pipeline(args.slots_pipeline, dev, snr_db=args.snr_db, ul_layers=2, dl_layers=DL_LAYERS, dl_ports=DL_PORTS,
+                  ul_ports=UL_PORTS)
+    stream = torch.cuda.current_stream(dev)
+    elapsed, _ = timed(args, dist, 1, dev, stream, lambda: pl.step(stream))
+    ok, its = pl.check()
+    cbs_cell = pl.plan_dl.nof_segments + pl.plan_ul.nof_segments
+    value = cbs_cell * pl.S * args.steps / elapsed
+    cpu_value = cpu.get("value") if isinstance(cpu, dict) else None
+    return {"metric": "PDSCH+PUSCH codeblocks/s @ 100 MHz 273-PRB 4x4 ports (PDSCH 4 layers, PUSCH 2 layers x 4 rx, "
+                      "reference ZF)",
+            "value": value, "unit": "codeblocks/s", "ms_per_step": elapsed / args.steps * 1e3,
+            "cells_per_step": pl.S, "codeblocks_per_cell": cbs_cell, "pusch_ldpc_iterations_mean": its,
+            "pusch_tb_ok_fraction": ok, "equalizer": pl.ul_equalizer, "parity": "every stage pinned to the compiled "
+            "reference (tests/test_pipeline_gpu.py::test_pipeline_vs_reference_chain)",
+            "cpu_baseline_same_work": cpu_value,
+            "speedup_vs_cpu_baseline": (value / cpu_value) if cpu_value else None}
 
 
 def low_snr_line(args, dev, timed, dist):

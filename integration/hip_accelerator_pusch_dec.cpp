@@ -437,12 +437,25 @@ private:
     // LDPC decoding with the codeblock CRC as early stop (pusch_codeblock_decoder.cpp:35-69)
     srs_amd_ldpc_decoder_config dc{bg, Z, c.nof_filler_bits, c.cb_crc_len, c.max_nof_ldpc_iterations};
     const unsigned              N = (bg == 1 ? 66 : 50) * Z;
+    // New data lands in freshly cleared rows: with k0 = 0 (rv 0) and no circular wrap only [0, E + F) and the
+    // systematic part can be non-zero, so the decoder scans that prefix (srs_amd_pusch_decoder_llr_prefix's rule,
+    // sch.h), which bounds its layer count and selects the high-rate kernel for high-rate codeblocks.
+    unsigned len = N;
+    if (c.new_data && c.rv == 0) {
+      unsigned end = 0;
+      for (unsigned r = first; r != first + n; ++r) {
+        end = std::max(end, cfg[r].cw_length + cfg[r].nof_filler_bits <= cfg[r].Ncb ? cfg[r].cw_length + cfg[r].nof_filler_bits
+                                                                                   : N);
+      }
+      end = std::max(end, (bg == 1 ? 20u : 8u) * Z);
+      len = std::min(N, std::max((bg == 1 ? 24u : 12u) * Z, (end + Z - 1) / Z * Z));
+    }
     return amd_ok(srs_amd_ldpc_rate_dematch_batch(dm, &md, c.new_data ? 1 : 0, d_llrs, d_arrays + first,
                                                   d_arrays + MAX_CBS + first, harq->row(tb_base + first), ROW, n,
                                                   stream),
                   "rate dematching") &&
            amd_ok(srs_amd_ldpc_decode_batch(dec, &dc, c.use_early_stop ? crc_poly(c.cb_crc_type) : SRS_AMD_NO_CRC,
-                                            harq->row(tb_base + first), ROW, nullptr, N,
+                                            harq->row(tb_base + first), ROW, nullptr, len,
                                             d_msgs + static_cast<size_t>(first) * MSG_ROW, MSG_ROW, d_iters + first,
                                             nullptr, n, stream),
                   "LDPC decoding");

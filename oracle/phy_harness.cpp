@@ -11,8 +11,23 @@
 // Built by oracle/Makefile into oracle/_ref/libsrsran_ref_hw.so.  Never loaded by the product.
 #include "ref_builders.h"
 
+#include "../integration/pdsch_processor_hip.h"
 #include "../integration/pusch_processor_hip.h"
+#include "phy/generic_functions/precoding/channel_precoder_avx2.h"
+#include "phy/generic_functions/precoding/channel_precoder_avx512.h"
+#include "phy/support/resource_grid_mapper_impl.h"
 #include "phy/support/resource_grid_reader_impl.h"
+#include "phy/support/resource_grid_writer_impl.h"
+#include "phy/upper/channel_coding/ldpc/ldpc_encoder_avx2.h"
+#include "phy/upper/channel_coding/ldpc/ldpc_rate_matcher_impl.h"
+#include "phy/upper/channel_coding/ldpc/ldpc_segmenter_tx_impl.h"
+#include "phy/upper/channel_modulation/modulation_mapper_lut_impl.h"
+#include "phy/upper/channel_processors/pdsch/pdsch_encoder_impl.h"
+#include "phy/upper/channel_processors/pdsch/pdsch_modulator_impl.h"
+#include "phy/upper/channel_processors/pdsch/pdsch_processor_impl.h"
+#include "phy/upper/signal_processors/pdsch/dmrs_pdsch_processor_impl.h"
+#include "phy/upper/signal_processors/ptrs/ptrs_pdsch_generator_impl.h"
+#include "srsran_amd/pdsch_modulator.h"
 #include "srsran/adt/tensor.h"
 #include "srsran/phy/upper/channel_processors/pusch/pusch_processor_result_notifier.h"
 #include "srsran_amd/pusch_processor.h"
@@ -149,6 +164,161 @@ struct pusch_ctx {
   std::deque<ticket>                                tickets;
   std::mutex                                        mtx;
 };
+
+// ---- PDSCH ----
+
+/// A flat pdsch_processor::pdu_t (test glue): type-0 allocation of the BWP's VRBs (non-interleaved), one codeword,
+/// wideband precoding, reserved RE patterns.
+struct srs_ref_pdsch_pdu {
+  uint32_t           numerology, slot_index, rnti, bwp_start_rb, bwp_size_rb;
+  int32_t            qm;
+  uint32_t           rv, n_id, ref_point; // ref_point: 0 CRB0, 1 PRB0
+  uint32_t           dmrs_symbol_mask, dmrs_type, scrambling_id, n_scid, nof_cdm_groups_without_data;
+  uint8_t            vrb_mask[SRS_AMD_CRB_MASK_BYTES];
+  uint8_t            pad;
+  uint32_t           start_symbol_index, nof_symbols, base_graph, tbs_lbrm_bytes;
+  float              ratio_pdsch_dmrs_to_sss_dB, ratio_pdsch_data_to_sss_dB;
+  uint32_t           nof_layers, nof_ports;
+  float              weights[4][4][2];
+  uint32_t           nof_reserved;
+  srs_amd_re_pattern reserved[SRS_AMD_MAX_RE_PATTERNS];
+};
+
+pdsch_processor::pdu_t to_pdsch_pdu(const srs_ref_pdsch_pdu& c)
+{
+  pdsch_processor::pdu_t pdu = {};
+  pdu.slot                   = slot_point(c.numerology, c.slot_index);
+  pdu.rnti                   = static_cast<uint16_t>(c.rnti);
+  pdu.bwp_size_rb            = c.bwp_size_rb;
+  pdu.bwp_start_rb           = c.bwp_start_rb;
+  pdu.cp                     = cyclic_prefix::NORMAL;
+  pdu.codewords.push_back(pdsch_processor::codeword_description{scheme_of(c.qm), c.rv});
+  pdu.n_id             = c.n_id;
+  pdu.ref_point        = c.ref_point ? pdsch_processor::pdu_t::PRB0 : pdsch_processor::pdu_t::CRB0;
+  pdu.dmrs_symbol_mask = symbol_slot_mask(MAX_NSYMB_PER_SLOT);
+  for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+    if ((c.dmrs_symbol_mask >> l) & 1u) {
+      pdu.dmrs_symbol_mask.set(l);
+    }
+  }
+  pdu.dmrs                        = c.dmrs_type == 2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
+  pdu.scrambling_id               = c.scrambling_id;
+  pdu.n_scid                      = c.n_scid != 0;
+  pdu.nof_cdm_groups_without_data = c.nof_cdm_groups_without_data;
+  vrb_bitmap vrbs(c.bwp_size_rb);
+  for (unsigned i = 0; i != c.bwp_size_rb; ++i) {
+    if ((c.vrb_mask[i / 8] >> (i % 8)) & 1u) {
+      vrbs.set(i);
+    }
+  }
+  pdu.freq_alloc         = rb_allocation::make_type0(vrbs);
+  pdu.start_symbol_index = c.start_symbol_index;
+  pdu.nof_symbols        = c.nof_symbols;
+  pdu.ldpc_base_graph    = c.base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
+  pdu.tbs_lbrm           = c.tbs_lbrm_bytes ? units::bytes(c.tbs_lbrm_bytes) : tbs_lbrm_default;
+  for (unsigned r = 0; r != c.nof_reserved; ++r) {
+    re_pattern pat;
+    pat.crb_mask = crb_bitmap(MAX_NOF_PRBS);
+    for (unsigned i = 0; i != MAX_NOF_PRBS; ++i) {
+      if ((c.reserved[r].crb_mask[i / 8] >> (i % 8)) & 1u) {
+        pat.crb_mask.set(i);
+      }
+    }
+    for (unsigned k = 0; k != NRE; ++k) {
+      if ((c.reserved[r].re_mask >> k) & 1u) {
+        pat.re_mask.set(k);
+      }
+    }
+    for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+      if ((c.reserved[r].symbols >> l) & 1u) {
+        pat.symbols.set(l);
+      }
+    }
+    pdu.reserved.merge(pat);
+  }
+  pdu.ratio_pdsch_dmrs_to_sss_dB = c.ratio_pdsch_dmrs_to_sss_dB;
+  pdu.ratio_pdsch_data_to_sss_dB = c.ratio_pdsch_data_to_sss_dB;
+  precoding_weight_matrix w(c.nof_layers, c.nof_ports);
+  for (unsigned l = 0; l != c.nof_layers; ++l) {
+    for (unsigned q = 0; q != c.nof_ports; ++q) {
+      w.set_coefficient(cf_t(c.weights[l][q][0], c.weights[l][q][1]), l, q);
+    }
+  }
+  pdu.precoding = precoding_configuration::make_wideband(w);
+  return pdu;
+}
+
+/// A slot grid written through the reference's resource_grid_writer_impl over a tensor [port][symbol][subcarrier].
+struct host_wgrid {
+  host_wgrid(const uint32_t* g, unsigned nports_, unsigned nsubc_) :
+    nports(nports_), nsubc(nsubc_), data({nsubc_, MAX_NSYMB_PER_SLOT, nports_}), writer(data, empty)
+  {
+    store(g);
+  }
+  void store(const uint32_t* g)
+  {
+    for (unsigned p = 0; p != nports; ++p) {
+      for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+        span<cbf16_t> row = data.get_view<static_cast<unsigned>(resource_grid_dimensions::symbol)>({l, p});
+        std::memcpy(row.data(), g + (p * MAX_NSYMB_PER_SLOT + l) * nsubc, nsubc * sizeof(cbf16_t));
+      }
+    }
+  }
+  void load(uint32_t* g)
+  {
+    for (unsigned p = 0; p != nports; ++p) {
+      for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+        span<cbf16_t> row = data.get_view<static_cast<unsigned>(resource_grid_dimensions::symbol)>({l, p});
+        std::memcpy(g + (p * MAX_NSYMB_PER_SLOT + l) * nsubc, row.data(), nsubc * sizeof(cbf16_t));
+      }
+    }
+  }
+  unsigned                  nports, nsubc;
+  grid_tensor               data;
+  std::atomic<unsigned>     empty{0};
+  resource_grid_writer_impl writer;
+};
+
+class pdsch_ticket : public pdsch_processor_notifier
+{
+public:
+  void              on_finish_processing() override { done.store(true, std::memory_order_release); }
+  std::atomic<bool> done{false};
+};
+
+struct pdsch_ctx {
+  std::shared_ptr<hip::pdsch_processor_factory_hip> factory;
+  std::unique_ptr<pdsch_processor>                  proc;
+  std::deque<pdsch_ticket>                          tickets;
+  std::deque<std::vector<uint8_t>>                  tbs; // the transport blocks' storage (shared_transport_block views)
+  std::mutex                                        mtx;
+};
+
+// The reference's pdsch_processor_impl with the "auto" components of this host (as ref_chain.cpp).
+std::unique_ptr<pdsch_processor_impl> make_ref_pdsch_processor()
+{
+  auto precoder = []() -> std::unique_ptr<channel_precoder> {
+    if (host_has_avx512_ldpc()) {
+      return std::make_unique<channel_precoder_avx512>();
+    }
+    return std::make_unique<channel_precoder_avx2>();
+  };
+  ldpc_segmenter_tx_impl::sch_crc crcs;
+  crcs.crc16  = make_crc(crc_generator_poly::CRC16, impl::automatic);
+  crcs.crc24A = make_crc(crc_generator_poly::CRC24A, impl::automatic);
+  crcs.crc24B = make_crc(crc_generator_poly::CRC24B, impl::automatic);
+  return std::make_unique<pdsch_processor_impl>(
+      std::make_unique<pdsch_encoder_impl>(std::make_unique<ldpc_segmenter_tx_impl>(crcs),
+                                           std::make_unique<ldpc_encoder_avx2>(),
+                                           std::make_unique<ldpc_rate_matcher_impl>()),
+      std::make_unique<pdsch_modulator_impl>(std::make_unique<modulation_mapper_lut_impl>(),
+                                             std::make_unique<pseudo_random_generator_impl>(),
+                                             std::make_unique<resource_grid_mapper_impl>(precoder())),
+      std::make_unique<dmrs_pdsch_processor_impl>(std::make_unique<pseudo_random_generator_impl>(),
+                                                  std::make_unique<resource_grid_mapper_impl>(precoder())),
+      std::make_unique<ptrs_pdsch_generator_generic_impl>(std::make_unique<pseudo_random_generator_impl>(),
+                                                          std::make_unique<resource_grid_mapper_impl>(precoder())));
+}
 
 void bits_out(const uci_payload_type& p, uint8_t* out)
 {
@@ -337,6 +507,132 @@ double srs_ref_phy_pusch_bench(void* h, void* const* grids, unsigned nof_cells, 
   }
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   *ok_out         = ok;
+  return steps ? dt / steps : 0.0;
+}
+
+/* ---- PDSCH: the reference's pdsch_processor_impl and the MI355X plug-in on writer-backed grids ---- */
+
+void* srs_ref_phy_wgrid_create(const uint32_t* grid, unsigned nports, unsigned nsubc)
+{
+  return new host_wgrid(grid, nports, nsubc);
+}
+
+void srs_ref_phy_wgrid_destroy(void* g)
+{
+  delete static_cast<host_wgrid*>(g);
+}
+
+/* The grid's contents, uint32 [ports][14][nsubc]. */
+void srs_ref_phy_wgrid_read(void* g, uint32_t* out)
+{
+  static_cast<host_wgrid*>(g)->load(out);
+}
+
+/* pdsch_processor_impl::process (pdsch_processor_impl.cpp:42-82) of one PDU into the grid. */
+int srs_ref_pdsch_process(void* g, const srs_ref_pdsch_pdu* c, const uint8_t* tb, unsigned tb_bytes)
+{
+  static thread_local std::unique_ptr<pdsch_processor_impl> proc = make_ref_pdsch_processor();
+  pdsch_ticket                                                 t;
+  static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
+  data.emplace_back(span<const uint8_t>(tb, tb_bytes));
+  proc->process(static_cast<host_wgrid*>(g)->writer, t, std::move(data), to_pdsch_pdu(*c));
+  return t.done ? 0 : -1;
+}
+
+void* srs_ref_phy_pdsch_create(int device, unsigned nof_prb, unsigned max_wait_us)
+{
+  hip::pdsch_processor_hip_config cfg;
+  cfg.device      = device;
+  cfg.nof_prb     = nof_prb;
+  cfg.max_wait_us = max_wait_us;
+  auto f          = hip::create_pdsch_processor_factory_hip(cfg);
+  if (!f) {
+    return nullptr;
+  }
+  auto* ctx    = new pdsch_ctx;
+  ctx->factory = f;
+  ctx->proc    = f->create();
+  return ctx;
+}
+
+void srs_ref_phy_pdsch_destroy(void* h)
+{
+  auto* ctx = static_cast<pdsch_ctx*>(h);
+  ctx->factory->wait_idle();
+  delete ctx;
+}
+
+/* pdsch_processor::process of the plug-in (asynchronous); the transport block is copied (the harness keeps it
+ * alive until the context goes).  Returns the ticket. */
+int srs_ref_phy_pdsch_process(void* h, void* g, const srs_ref_pdsch_pdu* c, const uint8_t* tb, unsigned tb_bytes)
+{
+  auto*                 ctx = static_cast<pdsch_ctx*>(h);
+  pdsch_ticket*         t;
+  std::vector<uint8_t>* b;
+  int                   id;
+  {
+    std::lock_guard<std::mutex> lock(ctx->mtx);
+    id = static_cast<int>(ctx->tickets.size());
+    t  = &ctx->tickets.emplace_back();
+    b  = &ctx->tbs.emplace_back(tb, tb + tb_bytes);
+  }
+  static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
+  data.emplace_back(span<const uint8_t>(b->data(), b->size()));
+  ctx->proc->process(static_cast<host_wgrid*>(g)->writer, *t, std::move(data), to_pdsch_pdu(*c));
+  return id;
+}
+
+void srs_ref_phy_pdsch_flush(void* h)
+{
+  static_cast<pdsch_ctx*>(h)->factory->flush();
+}
+
+void srs_ref_phy_pdsch_wait(void* h)
+{
+  static_cast<pdsch_ctx*>(h)->factory->wait_idle();
+}
+
+int srs_ref_phy_pdsch_done(void* h, int id)
+{
+  auto*                       ctx = static_cast<pdsch_ctx*>(h);
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  return (id >= 0 && static_cast<size_t>(id) < ctx->tickets.size() && ctx->tickets[id].done.load()) ? 1 : 0;
+}
+
+void srs_ref_phy_pdsch_stats(void* h, uint64_t* out)
+{
+  const auto s = static_cast<pdsch_ctx*>(h)->factory->get_statistics();
+  out[0]       = s.nof_pdus;
+  out[1]       = s.nof_batches;
+  out[2]       = s.nof_errors;
+}
+
+/* Throughput through the PDSCH plug-in: every step one PDU per cell grid (a processor per cell), process() per PDU,
+ * flush(), wait.  Returns seconds per step. */
+double srs_ref_phy_pdsch_bench(void* h, void* const* grids, unsigned nof_cells, const srs_ref_pdsch_pdu* c,
+                               const uint8_t* tb, unsigned tb_bytes, unsigned warmup, unsigned steps)
+{
+  auto*                                         ctx = static_cast<pdsch_ctx*>(h);
+  std::vector<std::unique_ptr<pdsch_processor>> procs;
+  for (unsigned i = 0; i != nof_cells; ++i) {
+    procs.push_back(ctx->factory->create());
+  }
+  std::vector<pdsch_ticket>    tickets(nof_cells);
+  const pdsch_processor::pdu_t pdu = to_pdsch_pdu(*c);
+  auto                         t0  = std::chrono::steady_clock::now();
+  for (unsigned s = 0; s != warmup + steps; ++s) {
+    if (s == warmup) {
+      t0 = std::chrono::steady_clock::now();
+    }
+    for (unsigned i = 0; i != nof_cells; ++i) {
+      static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
+      data.emplace_back(span<const uint8_t>(tb, tb_bytes));
+      procs[i]->process(static_cast<host_wgrid*>(grids[i])->writer, tickets[i], std::move(data), pdu);
+    }
+    ctx->factory->flush();
+    ctx->factory->wait_idle();
+  }
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return steps ? dt / steps : 0.0;
 }
 

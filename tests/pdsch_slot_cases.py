@@ -1,0 +1,57 @@
+"""PDSCH slots for the channel-processor plug-in tests: several PDSCH PDUs of one 273-PRB, four-port grid (own
+VRBs -- contiguous and type-0 sparse --, symbols, layers, modulation, wideband precoding, reserved REs, DM-RS type /
+CDM groups / scrambling, power offsets), each with a transport block sized by the TBS calculator.
+TEST INFRASTRUCTURE ONLY."""
+import numpy as np
+
+import srsran_project_amd as amd
+
+NPRB = 273
+NSUBC = 12 * NPRB
+
+# (qm, target rate, layers, vrbs, start, nof symbols, DM-RS mask, DM-RS type, CDM groups w/o data, reserved,
+#  data / DM-RS power offsets dB)
+PDUS = [
+    (2, 679.0, 1, (0, 60), 0, 14, (1 << 2) | (1 << 11), 1, 2, [], (0.0, 0.0)),
+    (6, 567.0, 2, (60, 140), 1, 13, (1 << 2) | (1 << 7) | (1 << 11), 1, 1, [((70, 90), 0b000100010001, 1 << 9)],
+     (-3.0, 3.0)),
+    (4, 490.0, 3, (140, 200), 2, 12, (1 << 3) | (1 << 4), 2, 2, [], (0.0, 4.77)),
+    (8, 797.0, 4, "sparse", 0, 14, 1 << 2, 1, 2, [], (1.5, 0.0)),
+]
+
+
+def reserved_masks(res):
+    out = []
+    for (c0, c1), re_mask, syms in res:
+        m = np.zeros(275, bool)
+        m[c0:c1] = True
+        out.append((m, re_mask, syms))
+    return out
+
+
+def slot(seed=5, slot_index=7, bwp=(0, NPRB), ref_point=0, pdus=PDUS):
+    """The PDU list [(PdschPdu, transport block)] and a random initial grid uint32 [4][14][NSUBC]."""
+    from oracle.phy import make_pdsch_pdu
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for i, (qm, rate, L, vrbs, start, ns, dmrs, dtype, ncdm, res, (pdata, pdmrs)) in enumerate(pdus):
+        if vrbs == "sparse":
+            vrbs = np.sort(rng.choice(np.arange(200, bwp[1]), min(50, bwp[1] - 200), replace=False))
+        else:
+            vrbs = np.arange(*vrbs)
+        nd = bin(dmrs).count("1")
+        ndmrs = (6 if dtype == 1 else 4) * nd * ncdm
+        tbs = amd.tbs_calculator_calculate(ns, ndmrs, 0, qm, rate, L, 0, len(vrbs))
+        r = rate / 1024
+        bg = 2 if (tbs <= 292 or (tbs <= 3824 and r <= 0.67) or r <= 0.25) else 1
+        W = ((rng.normal(size=(L, 4)) + 1j * rng.normal(size=(L, 4))) / np.sqrt(8)).astype(np.complex64)
+        pdu = make_pdsch_pdu(vrbs, W, reserved_masks(res), slot_index=slot_index, rnti=int(rng.integers(1, 65520)),
+                             bwp_start_rb=bwp[0], bwp_size_rb=bwp[1], qm=qm, n_id=int(rng.integers(0, 1024)),
+                             ref_point=ref_point, dmrs_symbol_mask=dmrs, dmrs_type=dtype,
+                             scrambling_id=int(rng.integers(0, 65536)), n_scid=i % 2,
+                             nof_cdm_groups_without_data=ncdm, start_symbol_index=start, nof_symbols=ns, base_graph=bg,
+                             ratio_pdsch_data_to_sss_dB=pdata, ratio_pdsch_dmrs_to_sss_dB=pdmrs)
+        out.append((pdu, rng.integers(0, 256, tbs // 8, dtype=np.uint8)))
+    grid0 = rng.integers(0, 1 << 32, (4, 14, NSUBC), dtype=np.uint64).astype(np.uint32)
+    return out, grid0
