@@ -111,7 +111,10 @@ int srs_amd_pdsch_modulate(srs_amd_pdsch_modulator*      mod,
                            uint32_t                      nof_bits);
 
 /* DEVICE, asynchronous: nof_cws codewords (rows of cw_stride bytes) into nof_cws
- * grids (grid_stride REs apart, ports nof_subc * 14 REs apart). */
+ * grids (grid_stride REs apart, ports nof_subc * 14 REs apart).  nof_bits >= nof_re x layers x Qm: a longer
+ * codeword maps its first nof_re x layers modulation symbols and the rest is dropped, as the reference's
+ * resource_grid_mapper consumes the symbol buffer only up to the allocation (pdsch_processor_impl sizes a DM-RS
+ * type-2 codeword with the type-2 pattern but maps it around the type-1 one, see pdsch_processor_hip.h). */
 int srs_amd_pdsch_modulate_batch(srs_amd_pdsch_modulator*      mod,
                                  const srs_amd_pdsch_mod_plan* plan,
                                  uint32_t*                     d_grids,
@@ -143,7 +146,7 @@ typedef struct srs_amd_pdsch_slot_pdu {
   const srs_amd_pdsch_mod_plan*    plan;      /* NULL: no data (DM-RS only) */
   const srs_amd_dmrs_pdsch_config* dmrs;      /* NULL: no DM-RS */
   uint32_t                         grid;      /* index of the grid in d_grids */
-  uint32_t                         nof_bits;  /* codeword length (nof_re x layers x Qm) */
+  uint32_t                         nof_bits;  /* codeword length (>= nof_re x layers x Qm, see _batch) */
   uint64_t                         cw_offset; /* byte offset of the packed codeword in d_codewords */
 } srs_amd_pdsch_slot_pdu;
 

@@ -128,7 +128,10 @@ std::string convert(pending_pdu& p, unsigned nof_prb)
   for (unsigned l = 0; l != NSYMB && l < pdu.dmrs_symbol_mask.size(); ++l) {
     m.dmrs_symbol_mask |= pdu.dmrs_symbol_mask.test(l) ? (1u << l) : 0u;
   }
-  m.dmrs_type                   = pdu.dmrs == dmrs_type::TYPE1 ? 1u : 2u;
+  // pdsch_processor_impl::modulate (pdsch_processor_impl.cpp:185-200) leaves pdsch_modulator::config_t::
+  // dmrs_config_type at its default, TYPE1: the data REs avoid the type-1 DM-RS pattern of the PDU's CDM groups
+  // whatever its DM-RS type (the DM-RS itself is mapped with the PDU's type afterwards)
+  m.dmrs_type                   = 1;
   m.nof_cdm_groups_without_data = pdu.nof_cdm_groups_without_data;
   m.scaling                     = convert_dB_to_amplitude(-pdu.ratio_pdsch_data_to_sss_dB);
   m.nof_layers                  = L;
@@ -155,7 +158,7 @@ std::string convert(pending_pdu& p, unsigned nof_prb)
   d                            = srs_amd_dmrs_pdsch_config{};
   d.slot_index                 = pdu.slot.slot_index();
   d.reference_point_k_rb       = pdu.ref_point == pdsch_processor::pdu_t::PRB0 ? pdu.bwp_start_rb : 0;
-  d.type                       = m.dmrs_type;
+  d.type                       = pdu.dmrs == dmrs_type::TYPE1 ? 1u : 2u;
   d.scrambling_id              = pdu.scrambling_id;
   d.n_scid                     = pdu.n_scid ? 1 : 0;
   d.amplitude                  = convert_dB_to_amplitude(-pdu.ratio_pdsch_dmrs_to_sss_dB);
@@ -166,6 +169,40 @@ std::string convert(pending_pdu& p, unsigned nof_prb)
   std::memcpy(d.weights, m.weights, sizeof(d.weights));
   p.numerology = to_numerology_value(pdu.slot.scs());
   return {};
+}
+
+// pdsch_compute_nof_data_re (pdsch_processor_helpers.h:97-140): the codeword's REs per layer -- the allocation minus
+// the reserved REs (counted without overlap) minus the DM-RS pattern of the PDU's own DM-RS type.
+uint32_t nof_data_re(const pending_pdu& p)
+{
+  const srs_amd_pdsch_mod_config& m    = p.mod;
+  const bool                      t2   = p.pdu.dmrs != dmrs_type::TYPE1;
+  const uint32_t                  ncdm = m.nof_cdm_groups_without_data;
+  uint32_t                        dmrs_re = 0;
+  for (uint32_t k = 0; k != 12; ++k) {
+    dmrs_re += (t2 ? (k % 6) < 2 * ncdm : (k % 2) < ncdm) ? 1 : 0;
+  }
+  uint32_t nof_prb = 0, reserved = 0;
+  for (uint32_t r = 0; r != SRS_AMD_MAX_RB; ++r) {
+    if (!((m.crb_mask[r / 8] >> (r % 8)) & 1u)) {
+      continue;
+    }
+    ++nof_prb;
+    for (uint32_t l = m.start_symbol; l != m.start_symbol + m.nof_symbols; ++l) {
+      uint16_t res = 0;
+      for (uint32_t q = 0; q != m.nof_reserved; ++q) {
+        const srs_amd_re_pattern& pat = m.reserved[q];
+        if (((pat.crb_mask[r / 8] >> (r % 8)) & 1u) && ((pat.symbols >> l) & 1u)) {
+          res |= pat.re_mask;
+        }
+      }
+      reserved += static_cast<uint32_t>(__builtin_popcount(res & 0xfffu));
+    }
+  }
+  const uint32_t nof_dmrs_symbols = static_cast<uint32_t>(__builtin_popcount(m.dmrs_symbol_mask & 0x3fffu));
+  const uint32_t grid_re          = nof_prb * 12 * m.nof_symbols;
+  const uint32_t grid_dmrs        = nof_prb * dmrs_re * nof_dmrs_symbols;
+  return grid_re > reserved + grid_dmrs ? grid_re - reserved - grid_dmrs : 0;
 }
 
 class pdsch_engine
@@ -289,10 +326,13 @@ private:
         const uint32_t bg  = p.pdu.ldpc_base_graph == ldpc_base_graph_type::BG1 ? 1 : 2;
         const uint32_t C   = nof_codeblocks(tbs, bg);
         // pdsch_processor_impl::encode (pdsch_processor_impl.cpp:146-180)
-        if (srs_amd_sch_plan_compute(&u.plan, tbs, bg, p.pdu.codewords[0].rv,
-                                     get_bits_per_symbol(p.pdu.codewords[0].modulation),
-                                     compute_N_ref(static_cast<uint32_t>(p.pdu.tbs_lbrm.value()), C), p.mod.nof_layers,
-                                     pl[i]->nof_re * p.mod.nof_layers) != SRS_AMD_OK) {
+        const uint32_t nre = nof_data_re(p);
+        if (nre < pl[i]->nof_re) {
+          p.error = "codeword shorter than the REs the modulator maps (the reference's mapper would overrun it)";
+        } else if (srs_amd_sch_plan_compute(&u.plan, tbs, bg, p.pdu.codewords[0].rv,
+                                            get_bits_per_symbol(p.pdu.codewords[0].modulation),
+                                            compute_N_ref(static_cast<uint32_t>(p.pdu.tbs_lbrm.value()), C),
+                                            p.mod.nof_layers, nre * p.mod.nof_layers) != SRS_AMD_OK) {
           p.error = srs_amd_last_error();
         }
       }

@@ -15,6 +15,11 @@
 // mapper being bit-exact with the GPU kernels -- are stored into each writer's grid through
 // resource_grid_writer::get_view, every other RE of the writer is left as it was; then on_finish_processing.
 //
+// Reproduced as the reference does it: pdsch_processor_impl sizes the codeword with the DM-RS pattern of the PDU's
+// DM-RS type (pdsch_compute_nof_data_re) but its modulator excludes the default type-1 pattern
+// (pdsch_processor_impl.cpp:185-200 leaves pdsch_modulator::config_t::dmrs_config_type unset), so a type-2 PDU's
+// data skips its DM-RS symbols entirely (two CDM groups) and the codeword's last symbols are not mapped.
+//
 // Not supported (logged; the PDU's REs are not written, on_finish_processing still called so the downlink processor
 // never stalls): PT-RS, more than four layers (two codewords), more than four ports, precoding that differs between
 // PRGs, more than eight reserved RE patterns, extended cyclic prefix.  Compiled against the reference's headers by

@@ -314,9 +314,9 @@ int srs_amd_pdsch_modulate_batch(srs_amd_pdsch_modulator*      mod,
   }
   const pdsch_map_args& pa  = plan->args;
   const uint32_t        bps = pa.qm < 2 ? 1u : static_cast<uint32_t>(pa.qm);
-  if (static_cast<uint64_t>(nof_bits) != static_cast<uint64_t>(plan->nof_re) * pa.nof_layers * bps) {
+  if (static_cast<uint64_t>(nof_bits) < static_cast<uint64_t>(plan->nof_re) * pa.nof_layers * bps) {
     return fail(SRS_AMD_EINVAL,
-                "The codeword length (i.e., %u bits) does not match the allocation (i.e., %u RE x %d layers x %u "
+                "The codeword length (i.e., %u bits) is shorter than the allocation (i.e., %u RE x %d layers x %u "
                 "bits).",
                 nof_bits, plan->nof_re, pa.nof_layers, bps);
   }
@@ -552,8 +552,10 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
       if (pa.nof_subc != nof_subc) {
         return fail(SRS_AMD_EINVAL, "PDU %u: plan for %u subcarriers, grid of %u.", i, pa.nof_subc, nof_subc);
       }
-      if (static_cast<uint64_t>(u.nof_bits) != static_cast<uint64_t>(u.plan->nof_re) * pa.nof_layers * bps) {
-        return fail(SRS_AMD_EINVAL, "PDU %u: the codeword length (i.e., %u bits) does not match the allocation.", i,
+      // a codeword longer than the allocation maps its first nof_re x layers symbols (as the reference's mapper,
+      // see pdsch_modulator.h); a shorter one cannot fill it
+      if (static_cast<uint64_t>(u.nof_bits) < static_cast<uint64_t>(u.plan->nof_re) * pa.nof_layers * bps) {
+        return fail(SRS_AMD_EINVAL, "PDU %u: the codeword length (i.e., %u bits) is shorter than the allocation.", i,
                     u.nof_bits);
       }
       if (nof_grids > 1 && grid_stride < static_cast<uint64_t>(pa.nof_ports) * pa.port_stride) {

@@ -215,3 +215,118 @@ def test_realistic_slot_equals_per_ue(decs, enc, early):
         tb1, res1 = decs["simd"].decode_batch(llrs[lo:lo + p.cw_length].view(1, -1), p, cfg)
         assert torch.equal(res[u], res1[0]), "UE %d: %s vs %s" % (u, res[u].tolist(), res1[0].tolist())
         assert torch.equal(d_tb[to:to + p.tbs // 8], tb1[0]), "UE %d TB" % u
+
+
+def _every_z_cases():
+    """One transport block per (base graph, lifting size, layers): C = 1 with the lifting size Z selected
+    (BG1: TBS + 24 just above 22 (Z_prev); BG2: TBS > 640 so K_b = 10), the PDSCH PDU shapes of the plug-in tests
+    (1-4 layers, QPSK..256QAM), codeword of about TBS / 0.6 bits."""
+    import srsran_project_amd as amd
+
+    out = []
+    zs = list(amd.LIFTING_SIZES)
+    for bg, kb, crc, lo in ((1, 22, 24, 0), (2, 10, 24, 656)):
+        for i, Z in enumerate(zs):
+            kmax = kb * Z - crc
+            kmin = kb * zs[i - 1] - crc + 1 if i else 8
+            tbs = (kmax // 8) * 8
+            if tbs < max(kmin, lo + 8) or tbs > (8424 if bg == 1 else 3816):
+                continue
+            lay, qm = 1 + i % 4, (2, 4, 6, 8)[(i // 4) % 4]
+            nre = -(-int(tbs / 0.6) // (lay * qm)) * lay
+            out.append((tbs, bg, qm, lay, nre, 0, 0))
+    # segmented: Z = 352, C = 6, 3 layers 16QAM (the pdsch_processor plug-in test's third PDU)
+    out.append((44040, 1, 4, 3, 23040, 0, 0))
+    return out
+
+
+@pytest.mark.parametrize("case", _every_z_cases())
+def test_encode_every_lifting_size(enc, case):
+    """Every lifting size of both base graphs (one transport block each, 1-4 layers) through the batch and slot
+    encoders, bit-exact with the reference's pdsch_encoder_impl (oracle.ref_pdsch_encode, the compiled reference)."""
+    import torch
+
+    import oracle
+    import srsran_project_amd as amd
+
+    tbs, bg, qm, lay, nre, rv, nref = case
+    p = amd.sch_plan(tbs, bg, rv, qm, nref, lay, nre)
+    op = osch.plan(tbs, bg, rv, qm, nref, lay, nre)
+    assert p.as_dict()["lifting_size"] == op["lifting_size"]
+    tb = tb_bytes(tbs, 77 + tbs)
+    want = oracle.ref_pdsch_encode(tb, op)
+    d_tb = torch.from_numpy(tb[None]).cuda()
+    got_b = enc.encode_batch(d_tb, p)
+    out = torch.zeros((p.cw_length + 7) // 8 + 8, dtype=torch.uint8, device="cuda")
+    enc.encode_slot(torch.from_numpy(tb).cuda(), [(p, 0, 0)], out=out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(np.unpackbits(got_b[0].cpu().numpy())[:p.cw_length], want, err_msg="batch")
+    np.testing.assert_array_equal(np.unpackbits(out.cpu().numpy())[:p.cw_length], want, err_msg="slot")
+
+
+def test_encode_slot_mixed_lifting_sizes_in_one_launch(enc):
+    """The transport blocks of one PDSCH slot with four different geometries -- Z = 288 (C = 2, 1 layer QPSK),
+    Z = 384 (C = 9, 2 layers 64QAM), Z = 352 (C = 6, 3 layers 16QAM), Z = 384 (C = 23, 4 layers 256QAM) -- encoded by
+    one srs_amd_pdsch_encode_slot call, each bit-exact with the reference's pdsch_encoder_impl."""
+    import torch
+
+    import oracle
+    import srsran_project_amd as amd
+
+    cases = [(11528, 1, 2, 1, 8640), (73776, 1, 6, 2, 2 * 10980), (44040, 1, 4, 3, 3 * 7680),
+             (192624, 1, 8, 4, 4 * 7800)]
+    ues, tbs_flat, tpos, cpos, want = [], [], 0, 0, []
+    for k, (tbs, bg, qm, lay, nch) in enumerate(cases):
+        p = amd.sch_plan(tbs, bg, 0, qm, 25344, lay, nch)
+        op = osch.plan(tbs, bg, 0, qm, 25344, lay, nch)
+        tb = tb_bytes(tbs, 900 + k)
+        want.append(oracle.ref_pdsch_encode(tb, op))
+        ues.append((p, tpos, cpos))
+        tbs_flat.append(np.concatenate([tb, np.zeros((-tb.size) % 64, np.uint8)]))
+        tpos += tbs_flat[-1].size
+        cpos += ((p.cw_length + 511) // 512) * 64
+    out = torch.zeros(cpos, dtype=torch.uint8, device="cuda")
+    enc.encode_slot(torch.from_numpy(np.concatenate(tbs_flat)).cuda(), ues, out=out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for k, ((p, _, co), w) in enumerate(zip(ues, want)):
+        bits = np.unpackbits(got[co:co + (p.cw_length + 7) // 8])[:p.cw_length]
+        assert np.array_equal(bits, w), (k, int((bits != w).sum()), int(np.flatnonzero(bits != w)[0]))
+
+
+@pytest.mark.parametrize("case", [(40, 2, 2, 34), (64, 2, 3, 54), (304, 8, 2, 64), (96, 4, 4, 20)])
+def test_small_z_codeblock_stages(enc, case):
+    """Small lifting sizes (C = 1) stage by stage: the single and batch LDPC encoders (whole codeblock), then the
+    single and batch rate matchers on the oracle's codeblock, against oracle/sch.py's restatement."""
+    import torch
+
+    import oracle
+    import srsran_project_amd as amd
+
+    tbs, qm, lay, nch = case
+    op = osch.plan(tbs, 1, 0, qm, 0, lay, nch)
+    Z, F, E, K = op["lifting_size"], op["nof_filler_bits"], op["cw_length"], op["segment_length"]
+    tb = np.unpackbits(tb_bytes(tbs, 77 + tbs))
+    c = oracle.crc_bits(osch._tb_crc_poly(op), tb)
+    L = op["nof_tb_crc_bits"]
+    msg = np.zeros(K, np.uint8)
+    msg[:tbs + L] = np.concatenate([tb, [(c >> (L - 1 - k)) & 1 for k in range(L)]])
+    want_cb = oracle.ldpc_encode(msg, 1, Z)
+    cfg = amd.LdpcEncoderConfiguration(base_graph=1, lifting_size=Z)
+    e1 = amd.LdpcEncoder()
+    got1 = e1.encode(msg, cfg)
+    d = np.flatnonzero(got1[:want_cb.size] != want_cb)
+    assert d.size == 0, "single encoder Z %d: %s" % (Z, d[:8].tolist())
+    gotb = e1.encode_batch(torch.from_numpy(np.packbits(msg)[None]).cuda(), cfg).cpu().numpy()
+    d = np.flatnonzero(np.unpackbits(gotb[0])[:want_cb.size] != want_cb)
+    assert d.size == 0, "batch encoder Z %d: %s" % (Z, d[:8].tolist())
+    want = osch.unpack_bits(oracle.rate_match(want_cb, 1, Z, 0, qm, E, 0, F), E)
+    meta = amd.CodeblockMetadata(base_graph=1, lifting_size=Z, rv=0, modulation_order=qm, Nref=0, nof_filler_bits=F)
+    rm = amd.LdpcRateMatcher()
+    got = np.unpackbits(rm.rate_match(E, want_cb, meta))[:E]
+    d = np.flatnonzero(got != want)
+    assert d.size == 0, "single rate matcher Z %d F %d E %d: %s" % (Z, F, E, d[:8].tolist())
+    got = np.unpackbits(rm.rate_match_batch(torch.from_numpy(np.packbits(want_cb)[None]).cuda(), [E], meta)
+                        .cpu().numpy())[:E]
+    d = np.flatnonzero(got != want)
+    assert d.size == 0, "batch rate matcher Z %d F %d E %d: %s" % (Z, F, E, d[:8].tolist())
