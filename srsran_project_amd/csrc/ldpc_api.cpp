@@ -306,6 +306,7 @@ void srs_amd::ldpc_mixed_row(void* row, uint32_t bg, uint32_t Z, int crc_poly)
   r.Z        = Z;
   r.edge_off = static_cast<uint32_t>(lifted_edges_offset(static_cast<int>(bg), static_cast<int>(Z)));
   r.crc_off  = crc_poly == SRS_AMD_NO_CRC ? NO_CRC_ROW : static_cast<uint32_t>(crc_poly) * MAX_CRC_BITS_LEN;
+  r.zmagic   = ldpc_z_magic(Z);
   std::memcpy(row, &r, sizeof(r));
 }
 

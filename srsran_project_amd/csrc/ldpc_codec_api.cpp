@@ -557,6 +557,11 @@ int srs_amd::rate_dematch_batch_ex(srs_amd_ldpc_rate_dematcher*      dm,
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ldpc_rate_dematch_kernel launch");
 }
 
+const uint32_t* srs_amd::ldpc_encoder_edges(const srs_amd_ldpc_encoder* enc)
+{
+  return enc != nullptr ? enc->edges : nullptr;
+}
+
 uint32_t srs_amd::ldpc_encode_mixed_row(void* row, uint32_t bg, uint32_t Z, uint32_t max_bits)
 {
   lifted_graph g{};

@@ -101,6 +101,9 @@ int ldpc_encode_mixed(srs_amd_ldpc_encoder* enc,
 uint32_t ldpc_encode_mixed_row(void* row, uint32_t bg, uint32_t Z, uint32_t max_bits);
 constexpr size_t LDPC_ENCODE_ROW_BYTES = 32;
 
+// Device table of every lifted graph's edges (ldpc_encode_mixed_row's edge_off indexes it).
+const uint32_t* ldpc_encoder_edges(const srs_amd_ldpc_encoder* enc);
+
 // Rate matching of codeblocks with per-codeblock geometry (srs_amd_pdsch_encode_slot): codeblock cb uses
 // geos[row_geo[cb]]; d_out_offsets are bit offsets into d_output.
 int rate_match_ragged(srs_amd_ldpc_rate_matcher* rm,

@@ -81,8 +81,15 @@ struct ldpc_row_desc {
   uint32_t Z;
   uint32_t edge_off;
   uint32_t crc_off;
-  uint32_t pad;
+  uint32_t zmagic; // ldpc_z_magic(Z): i / Z = umulhi(i, zmagic) for i < 2^16
 };
+
+// ceil-ish 2^32 / Z with umulhi(i, m) == i / Z for every i < 2^16 and valid lifting size Z.
+uint32_t ldpc_z_magic(uint32_t Z);
+
+// Waves per codeblock of the packed runtime-Z decoder kernel for (bg, Z) (Z a multiple of 4), 0 when that
+// kernel does not take it (SRSRAN_AMD_LDPC_PK=0 disables it).
+int ldpc_pk_waves(int bg, int Z);
 constexpr uint32_t NO_CRC_ROW = 0xffffffffu;
 constexpr int32_t LDPC_ITERS_SKIPPED = -2;
 

@@ -1505,6 +1505,456 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
   }
 }
 
+// ============================================================================
+// Packed decoder for every other lifted graph -- BG2, BG1 with Z < 384 and the mixed-Z launches of a slot --
+// when Z is a multiple of 4: the full-length kernel's layout with the lifting size known only at run time.
+//   * lane t owns check rows t and t + H (H = Z / 2) of every layer, one per 16-bit half; W = ceil(H / 64)
+//     waves per codeblock (W = 1 for Z <= 128: one wave and no barriers; W = 2 for Z <= 256; W = 3).  Lanes
+//     t >= H repeat lane t mod H, and odd rows past Z are rows mod Z: a repeated row computes the same
+//     values from the same soft bits and writes them to the same addresses;
+//   * soft bits in LDS at a compile-time stride of 128 W bytes per variable node, so the node offset of an
+//     edge is a literal in the ds instruction's immediate, and only (row + shift) mod Z is computed per row:
+//     two adds and a min on the lane index, the shift and shift - Z coming from the scalar unit;
+//   * the compressed messages of every layer in registers (fr_layer): BG1 96 VGPRs, BG2 84;
+//   * the LLR row, the CRC and the hard decision address the node-strided LDS through i / Z computed as
+//     umulhi(i, ceil(2^32 / Z)) (exact for i < 2^16).
+// Bit-exact with ldpc_decode_kernel (same per-edge arithmetic; identical outputs, iteration counts, soft bits).
+// ============================================================================
+
+template <int BG>
+constexpr int pk_words(int l)
+{
+  return bg_traits<BG>::deg(l) > 13 ? 3 : 2;
+}
+template <int BG>
+constexpr int pk_off(int l)
+{
+  int s = 0;
+  for (int i = 0; i < l; ++i) {
+    s += pk_words<BG>(i);
+  }
+  return s;
+}
+static_assert(pk_off<1>(46) == FR_STATE_WORDS && pk_off<2>(42) == 84, "compressed message state");
+
+template <int BG>
+struct pk_state {
+  uint32_t w[pk_off<BG>(bg_traits<BG>::M)];
+  __device__ __forceinline__ void zero()
+  {
+#pragma unroll
+    for (int i = 0; i < pk_off<BG>(bg_traits<BG>::M); ++i) {
+      w[i] = 0;
+    }
+  }
+};
+
+// base-graph variable node of edge E (compile time)
+template <int BG, int E>
+constexpr int bg_var()
+{
+  return BG == 1 ? tables::SRS_BG1_EDGES[E][1] : tables::SRS_BG2_EDGES[E][1];
+}
+
+// The lifted graph of one codeblock, wave-uniform.
+struct pk_geo {
+  const_u32_ptr edge; // lifted_graph::edge: var * Z | shift << 16
+  uint32_t      Z, H;
+};
+
+// Positions (row + shift) mod Z of rows t and t + H of edge EI within its variable node (t + H + shift < 2 Z).
+template <int EI>
+__device__ __forceinline__ void pk_rows(const pk_geo& g, uint32_t t, uint32_t& lo, uint32_t& hi)
+{
+  const uint32_t s  = g.edge[EI] >> 16;
+  uint32_t       sh = s + g.H;
+  sh                = sh >= g.Z ? sh - g.Z : sh;
+  lo                = __builtin_elementwise_min(t + s, t + (s - g.Z));
+  hi                = __builtin_elementwise_min(t + sh, t + (sh - g.Z));
+}
+
+// rows of degree <= PK_KEEP_ADDR keep their gather positions for the scatter; longer rows recompute them
+#ifndef PK_KEEP_ADDR
+#define PK_KEEP_ADDR 10
+#endif
+
+// One layer (row L of base graph BG) for the row pair of lane t (fr_layer with run-time positions).
+template <int BG, int L, int ARITH, int STRIDE, int... E>
+__device__ __forceinline__ void pk_layer(lds_i8* lds, pk_state<BG>& st, uint32_t t, const pk_geo& g,
+                                         std::integer_sequence<int, E...>)
+{
+  constexpr int  E0   = row_start<BG>(L);
+  constexpr int  DEG  = sizeof...(E);
+  constexpr int  O    = pk_off<BG>(L);
+  constexpr bool W3   = pk_words<BG>(L) == 3;
+  constexpr bool KEEP = DEG <= PK_KEEP_ADDR;
+  const uint32_t wold[3] = {st.w[O], st.w[O + 1], W3 ? st.w[O + 2] : 0u};
+  const pk16     s2o     = as_pk(wold[0] & 0x007f007fu);
+  const uint32_t imo     = wold[0] & 0x0f800f80u;
+  const pk16     dno     = pk_splat(0) - as_pk(wold[1] & 0x007f007fu); // s1 - s2 of the old messages
+  pk16           v[DEG];
+  uint32_t       plo[KEEP ? DEG : 1], phi[KEEP ? DEG : 1];
+  pk16           min1[2], min2[2];
+  pk16           sgn = pk_splat(0);
+  min1[0] = min1[1] = min2[0] = min2[1] = pk_splat(LLR_MAX * 32 + 31);
+  // pass 1 (ldpc_decoder_impl.cpp:235 / :290): old message, v2c, check-node statistics
+  (
+      [&] {
+        if constexpr (E % HR_CHUNK1 == 0 && E > 0) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        constexpr int      h    = E & 1; // reduction chain
+        constexpr uint32_t node = LDS_SOFT_OFFSET + bg_var<BG, E0 + E>() * STRIDE;
+        uint32_t           lo, hi;
+        pk_rows<E0 + E>(g, t, lo, hi);
+        if constexpr (KEEP) {
+          plo[E] = lo;
+          phi[E] = hi;
+        }
+        const pk16 s   = pk16{static_cast<short>(lds[lo + node]), static_cast<short>(lds[hi + node])};
+        const pk16 f   = pk_nonzero(imo ^ ((static_cast<uint32_t>(E) << 7) * 0x10001u));
+        const pk16 mag = pk_mad(f, dno, s2o);
+        const pk16 ng  = (as_pk(wold[fr_sign_word(E)]) << pk_splat(15 - fr_sign_bit(E))) >> 15;
+        const pk16 c   = (mag ^ ng) - ng;
+        const pk16 sat = pk_clamp(s, LLR_MAX);
+        const pk16 x   = (s - sat) * pk_splat(INF_BOOST) + pk_clamp(s - c, LLR_MAX);
+        const pk16 key = pk_key<E>(__builtin_elementwise_abs(x));
+        min2[h]        = pk_max(min1[h], pk_min(key, min2[h])); // median(min1, key, min2)
+        min1[h]        = pk_min(min1[h], key);
+        sgn ^= x;
+        v[E] = x;
+      }(),
+      ...);
+  __builtin_amdgcn_sched_barrier(0);
+  const pk16     k1     = pk_min(min1[0], min1[1]);
+  const pk16     k2     = pk_min(pk_max(min1[0], min1[1]), pk_min(min2[0], min2[1]));
+  const pk16     s1     = pk_scale16<ARITH>(k1 >> 5);
+  const pk16     s2     = pk_scale16<ARITH>(k2 >> 5);
+  const pk16     d12    = s1 - s2;
+  const uint32_t idx    = as_u32(k1) & 0x001f001fu;
+  uint32_t       acc[3] = {(idx << 7) | as_u32(s2), as_u32(s2 - s1), 0u};
+  if constexpr (!KEEP) {
+    asm volatile("" : "+v"(t));
+  }
+  // pass 2 (ldpc_decoder_impl.cpp:310, :270): new message, promotion sum, new state
+  (
+      [&] {
+        if constexpr (E % HR_CHUNK2 == 0 && E > 0) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        constexpr uint32_t node = LDS_SOFT_OFFSET + bg_var<BG, E0 + E>() * STRIDE;
+        const pk16         x    = v[E];
+        const pk16         f    = pk_nonzero(idx ^ (static_cast<uint32_t>(E) * 0x10001u)); // 0: edge E holds min1
+        const pk16         mag  = f * d12 + s2;
+        const pk16         sx   = sgn ^ x;
+        const pk16         ng   = sx >> 15;
+        const pk16         c    = (mag ^ ng) - ng;
+        const pk16         out  = pk_clamp(c + x, SOFT_INF);
+        const uint32_t     nb   = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pku16, sx) >> 15);
+        acc[fr_sign_word(E)] |= nb << fr_sign_bit(E);
+        uint32_t lo, hi;
+        if constexpr (KEEP) {
+          lo = plo[E];
+          hi = phi[E];
+        } else {
+          pk_rows<E0 + E>(g, t, lo, hi);
+        }
+        lds[lo + node] = static_cast<int8_t>(out.x);
+        lds[hi + node] = static_cast<int8_t>(out.y);
+      }(),
+      ...);
+  asm volatile("" : "+v"(acc[0]), "+v"(acc[1]));
+  st.w[O]     = acc[0];
+  st.w[O + 1] = acc[1];
+  if constexpr (W3) {
+    asm volatile("" : "+v"(acc[2]));
+    st.w[O + 2] = acc[2];
+  }
+}
+
+template <int BG, int L, int ARITH, int W>
+__device__ __forceinline__ void pk_layers(lds_i8* lds, pk_state<BG>& st, uint32_t t, pk_geo g, int nof_layers)
+{
+  if constexpr (L < bg_traits<BG>::M) {
+    asm volatile("" : "+s"(nof_layers));
+    if (L < 4 || L < nof_layers) { // uniform; nof_layers >= 4
+      // laundered per layer: the positions are iteration-invariant, hoisted they would spill
+      asm volatile("" : "+v"(t), "+s"(g.edge), "+s"(g.Z), "+s"(g.H));
+      pk_layer<BG, L, ARITH, 128 * W>(lds, st, t, g, std::make_integer_sequence<int, bg_traits<BG>::deg(L)>{});
+      if constexpr (W > 1) {
+        __syncthreads();
+      } else {
+        asm volatile("" ::: "memory"); // one wave: LDS accesses execute in issue order
+      }
+    }
+    pk_layers<BG, L + 1, ARITH, W>(lds, st, t, g, nof_layers);
+  }
+}
+
+#ifndef PK_WAVES_BG1
+#define PK_WAVES_BG1 3
+#endif
+#ifndef PK_WAVES_BG2
+#define PK_WAVES_BG2 3
+#endif
+
+__host__ __device__ constexpr int pk_lds_bytes(int bg, int w)
+{
+  return LDS_SOFT_OFFSET + (bg == 1 ? 68 : 52) * 128 * w;
+}
+
+template <int BG, int ARITH, int W>
+__global__ void __launch_bounds__(64 * W, (BG == 1 ? PK_WAVES_BG1 : PK_WAVES_BG2))
+    ldpc_decode_pk_kernel(decode_args a, uint32_t launch_z, uint32_t launch_magic)
+{
+  constexpr int      NT     = 64 * W;
+  constexpr uint32_t STRIDE = 128 * W;
+  constexpr int      KB     = bg_traits<BG>::K;
+  constexpr int      NF     = bg_traits<BG>::N_FULL;
+  lds_i32*           red    = (lds_i32*)(uintptr_t)LDS_RED_OFFSET;
+  lds_i8*            lds    = (lds_i8*)(uintptr_t)0;
+
+  for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
+    const bool      mixed = a.rows != nullptr;
+    const uint32_t  Z     = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].Z) : launch_z;
+    const uint32_t  magic = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].zmagic) : launch_magic;
+    const uint32_t  e_off = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].edge_off) : 0u;
+    const uint32_t  c_off = mixed ? __builtin_amdgcn_readfirstlane(a.rows[cb].crc_off) : 0u;
+    const uint32_t* crc_table = mixed ? (c_off == NO_CRC_ROW ? nullptr : a.crc_table + c_off) : a.crc_table;
+    if (a.skip_flags && *reinterpret_cast<const int32_t*>(a.skip_flags + static_cast<size_t>(cb) * a.skip_stride)) {
+      if (threadIdx.x == 0) {
+        a.nof_iters[cb] = LDPC_ITERS_SKIPPED; // uniform over the workgroup
+      }
+      continue;
+    }
+    const uint32_t gap = STRIDE - Z; // LDS bytes of a node row past its Z soft bits
+    // LDS byte of soft bit i (node i / Z, position i mod Z)
+    auto lds_at = [&](uint32_t i) { return LDS_SOFT_OFFSET + i + __umulhi(i, magic) * gap; };
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    const int8_t*  in     = a.llrs + static_cast<size_t>(cb) * a.llr_stride;
+    const uint32_t n_llrs = a.llr_lens ? a.llr_lens[cb] : a.llr_len;
+    uint8_t*       out    = a.out + static_cast<size_t>(cb) * a.out_stride;
+    const uint32_t KZ     = KB * Z;
+
+    if constexpr (W > 1) {
+      if (t == 0) {
+        red[0] = -1;
+        red[1] = red[2] = red[3] = red[4] = 0;
+      }
+      __syncthreads();
+    }
+    // ---- input scan (last non-zero LLR, ldpc_decoder_impl.cpp:86) fused with the soft-bit load (:160):
+    // LLR i is soft bit 2 Z + i; full nodes clamped to +-SOFT_CLAMP, the partial tail node to the soft-bit range,
+    // zeros past the input; nodes 0, 1 and the nodes past the input that a layer or the export reads zeroed.
+    int input_size;
+    {
+      const uint32_t in_nodes = __umulhi(n_llrs + Z - 1, magic); // nodes holding input
+      const uint32_t B4       = __umulhi(n_llrs, magic) * Z >> 2; // words of full (clamped) nodes
+      const uint32_t nw       = n_llrs >> 2;
+      const uint32_t wend     = in_nodes * Z >> 2;
+      const uint32_t tail     = n_llrs & 3;
+      const bool     al4      = a.aligned4 != 0;
+      const int32_t* in4      = reinterpret_cast<const int32_t*>(in);
+      int            last     = -1;
+      for (uint32_t w = t; w < wend; w += NT) {
+        uint32_t v = 0;
+        if (w < nw) {
+          if (al4) {
+            v = static_cast<uint32_t>(in4[w]);
+          } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              v |= static_cast<uint32_t>(static_cast<uint8_t>(in[4 * w + b])) << (8 * b);
+            }
+          }
+        } else if (w == nw) {
+          for (uint32_t b = 0; b < tail; ++b) {
+            v |= static_cast<uint32_t>(static_cast<uint8_t>(in[4 * w + b])) << (8 * b);
+          }
+        }
+        if (v != 0) {
+          last = static_cast<int>(4 * w + (31 - __builtin_clz(v)) / 8);
+        }
+        const int lim = w < B4 ? SOFT_CLAMP : SOFT_INF;
+        uint32_t  o   = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int x = static_cast<int8_t>(v >> (8 * b));
+          o |= (static_cast<uint32_t>(med3_i(x, -lim, lim)) & 0xffu) << (8 * b);
+        }
+        *reinterpret_cast<lds_u32*>(lds + lds_at(2 * Z + 4 * w)) = o;
+      }
+      // nodes 0 and 1 (punctured), then the nodes after the input up to the last one read
+      const uint32_t zend = a.soft_out ? NF : min(static_cast<uint32_t>(NF), max(2 + in_nodes, KB + 4u));
+      const uint32_t z0   = (2 + in_nodes) * Z >> 2;
+      const uint32_t nz   = (Z >> 1) + (zend > 2 + in_nodes ? (zend - 2 - in_nodes) * Z >> 2 : 0u);
+      for (uint32_t q = t; q < nz; q += NT) {
+        const uint32_t w = q < (Z >> 1) ? q : z0 + q - (Z >> 1);
+        *reinterpret_cast<lds_u32*>(lds + lds_at(4 * w)) = 0;
+      }
+      if constexpr (W == 1) {
+        input_size = __builtin_amdgcn_readfirstlane(wave_max(last) + 1);
+      } else {
+        if (last >= 0) {
+          __hip_atomic_fetch_max(&red[0], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        input_size = __builtin_amdgcn_readfirstlane(red[0] + 1);
+      }
+    }
+
+    if (input_size < static_cast<int>(KZ) && a.force_decoding) {
+      // ldpc_decoder_impl.cpp:92 (see ldpc_decode_kernel); K Z is a multiple of 8 here
+      for (uint32_t b = t; b < KZ / 8 && !crc_table; b += NT) {
+        out[b] = 0xff;
+      }
+      if (t == 0) {
+        a.nof_iters[cb] = -1;
+      }
+      if constexpr (W > 1) {
+        __syncthreads();
+      }
+      continue;
+    }
+    const uint32_t cb_len     = max(static_cast<uint32_t>(input_size) + 2 * Z, KZ + 4 * Z);
+    const int      nof_layers = static_cast<int>(__umulhi(cb_len + Z - 1, magic)) - KB;
+    const int      nof_sig    = static_cast<int>(KZ) - (a.fillers ? a.fillers[cb] : a.nof_filler_bits);
+    int            result     = -1;
+    const uint32_t H          = Z >> 1;
+    const pk_geo   geo{(const_u32_ptr)(a.edges + e_off), Z, H};
+    const uint32_t tr         = t < H ? t : t % H; // the row pair of this lane (lanes t >= H repeat one)
+
+    pk_state<BG> st;
+    st.zero();
+
+    for (int it = 0; it < a.max_iterations; ++it) {
+      pk_layers<BG, 0, ARITH, W>(lds, st, tr, geo, nof_layers);
+
+      if (crc_table) {
+        // hard bits + CRC early stop (ldpc_decoder_impl.cpp:125), remainder up to a unit factor (see the
+        // high-rate kernel): word q (soft bits 4q .. 4q+3, one node) reads remainders [KZ - 4 - 4q, KZ - 1 - 4q]
+        uint32_t tq = threadIdx.x;
+        asm volatile("" : "+v"(tq));
+        uint32_t crc = 0, zero = 0;
+        for (uint32_t q = tq; q < KZ / 4; q += NT) {
+          const uint32_t w4 = *reinterpret_cast<const lds_u32*>(lds + lds_at(4 * q));
+          const uint4    r  = *reinterpret_cast<const uint4*>(crc_table + (KZ - 4 - 4 * q));
+          zero |= (w4 - 0x01010101u) & ~w4 & 0x80808080u;
+          const uint32_t d     = ((w4 | 0x80808080u) - 0x01010101u) ^ (~w4 & 0x80808080u);
+          const uint32_t rr[4] = {r.w, r.z, r.y, r.x};
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            crc ^= rr[b] & static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(d), 8 * b + 7, 1));
+          }
+        }
+        // filler bits take no part in the CRC
+        for (uint32_t q = (static_cast<uint32_t>(nof_sig) >> 2) + tq; q < KZ / 4; q += NT) {
+          const uint32_t w4 = *reinterpret_cast<const lds_u32*>(lds + lds_at(4 * q));
+          const uint32_t d  = ((w4 | 0x80808080u) - 0x01010101u) ^ (~w4 & 0x80808080u);
+#pragma unroll
+          for (uint32_t b = 0; b < 4; ++b) {
+            if (4 * q + b >= static_cast<uint32_t>(nof_sig) && ((d >> (8 * b + 7)) & 1u)) {
+              crc ^= crc_table[KZ - 1 - (4 * q + b)];
+            }
+          }
+        }
+        if constexpr (W == 1) {
+          const uint32_t c_all = __builtin_amdgcn_readfirstlane(wave_xor(crc));
+          const uint32_t z_all = __builtin_amdgcn_readfirstlane(wave_or(zero));
+          if (z_all == 0 && c_all == 0) {
+            result = it + 1;
+            break;
+          }
+          continue;
+        } else {
+          lds_u32* acc = reinterpret_cast<lds_u32*>(&red[1 + 2 * (it & 1)]);
+          if (crc != 0) {
+            __hip_atomic_fetch_xor(&acc[0], crc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          if (zero != 0) {
+            __hip_atomic_fetch_or(&acc[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          __syncthreads();
+          const uint32_t c_all = __builtin_amdgcn_readfirstlane(acc[0]);
+          const uint32_t z_all = __builtin_amdgcn_readfirstlane(acc[1]);
+          if (tq == 0) {
+            lds_u32* nxt = reinterpret_cast<lds_u32*>(&red[1 + 2 * ((it + 1) & 1)]);
+            nxt[0]       = 0;
+            nxt[1]       = 0;
+          }
+          if (z_all == 0 && c_all == 0) {
+            result = it + 1;
+            break;
+          }
+        }
+      }
+    }
+
+    // ---- hard decision, packed MSB-first: one output byte (two soft-bit words of one node each) per task
+    uint32_t te = threadIdx.x;
+    asm volatile("" : "+v"(te));
+    for (uint32_t b = te; b < KZ / 8; b += NT) {
+      uint32_t o = 0;
+#pragma unroll
+      for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t w   = *reinterpret_cast<const lds_u32*>(lds + lds_at(8 * b + 4 * h));
+        const uint32_t d   = ((w | 0x80808080u) - 0x01010101u) ^ (~w & 0x80808080u);
+        const uint32_t nib = (((d & 0x80808080u) >> 7) * 0x08040201u) >> 24; // byte0 -> bit 3
+        o |= (nib & 0xfu) << (h ? 0 : 4);
+      }
+      out[b] = static_cast<uint8_t>(o);
+    }
+    if (a.soft_out) {
+      int32_t* so = reinterpret_cast<int32_t*>(a.soft_out + static_cast<size_t>(cb) * (NF * Z));
+      for (uint32_t q = te; q < NF * Z / 4; q += NT) {
+        so[q] = static_cast<int32_t>(soft_export4(*reinterpret_cast<const lds_u32*>(lds + lds_at(4 * q))));
+      }
+    }
+    if (te == 0) {
+      a.nof_iters[cb] = result;
+    }
+    if constexpr (W > 1) {
+      __syncthreads();
+    } else {
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
+// Waves per codeblock of the packed kernel for a lifting size, 0 when it does not take it.
+int ldpc_pk_waves(int bg, int Z)
+{
+  // read per call (A/B timing and the parity tests switch it per launch)
+  const char* mode    = std::getenv("SRSRAN_AMD_LDPC_PK");
+  const bool  enabled = mode == nullptr || mode[0] != '0';
+  if (!enabled || (bg != 1 && bg != 2) || Z < 4 || (Z & 3) != 0 || Z > MAX_LIFTING_SIZE) {
+    return 0;
+  }
+  return (Z / 2 + 63) / 64;
+}
+
+uint32_t ldpc_z_magic(uint32_t Z)
+{
+  return static_cast<uint32_t>((1ull << 32) / Z + 1);
+}
+
+template <int BG, int ARITH>
+static void launch_pk(const decode_args& args, int W, uint32_t Z, int grid, hipStream_t stream)
+{
+  const uint32_t magic = ldpc_z_magic(Z);
+  if (W == 1) {
+    hipLaunchKernelGGL((ldpc_decode_pk_kernel<BG, ARITH, 1>), dim3(grid), dim3(64), pk_lds_bytes(BG, 1), stream, args,
+                       Z, magic);
+  } else if (W == 2) {
+    hipLaunchKernelGGL((ldpc_decode_pk_kernel<BG, ARITH, 2>), dim3(grid), dim3(128), pk_lds_bytes(BG, 2), stream,
+                       args, Z, magic);
+  } else {
+    hipLaunchKernelGGL((ldpc_decode_pk_kernel<BG, ARITH, 3>), dim3(grid), dim3(192), pk_lds_bytes(BG, 3), stream,
+                       args, Z, magic);
+  }
+}
+
 constexpr int HR_MAXL = 4;
 #ifndef HR_NP_DEFAULT
 #define HR_NP_DEFAULT 1
@@ -1594,6 +2044,19 @@ hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, in
       hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_GENERIC, MAXL, 1>), dim3(grid), dim3(HR_HALF), lds, stream, args);
     } else {
       hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_SIMD, MAXL, 1>), dim3(grid), dim3(HR_HALF), lds, stream, args);
+    }
+    return hipGetLastError();
+  }
+  // every other graph with Z a multiple of 4: the packed runtime-Z kernel (BG1 Z = 384 keeps the compile-time
+  // kernels above and below)
+  const int pkw = ldpc_pk_waves(g.bg, g.Z);
+  if (pkw > 0 && !(g.bg == 1 && g.Z == HR_Z) && (reinterpret_cast<uintptr_t>(args.soft_out) & 3u) == 0) {
+    if (g.bg == 1) {
+      arith == ARITH_GENERIC ? launch_pk<1, ARITH_GENERIC>(args, pkw, g.Z, grid, stream)
+                             : launch_pk<1, ARITH_SIMD>(args, pkw, g.Z, grid, stream);
+    } else {
+      arith == ARITH_GENERIC ? launch_pk<2, ARITH_GENERIC>(args, pkw, g.Z, grid, stream)
+                             : launch_pk<2, ARITH_SIMD>(args, pkw, g.Z, grid, stream);
     }
     return hipGetLastError();
   }

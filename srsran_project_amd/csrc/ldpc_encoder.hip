@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ldpc_codec_args.h"
+#include "ldpc_encode_device.h"
 
 namespace srs_amd {
 
@@ -149,46 +150,10 @@ __global__ __launch_bounds__(MAX_LIFTING_SIZE) void ldpc_encode_kernel(encode_ar
   }
 }
 
-// ---- bit-sliced encoder (Z >= 32) -----------------------------------------------------------------
-// The codeword lives in LDS as ONE linear bit vector (bit i = lifted column i / Z, row i % Z, at word
-// i / 32, bit i % 32), so unpacking the MSB-first message and packing the output are word copies with a
-// bit reversal.  A lane computes 32 rows of a parity column at once: each edge is a 32-row window of the
-// variable column at the edge's cyclic shift (two LDS words and a funnel shift, a second pair where
-// the window wraps), XOR-ed into the row's accumulator.  One wave per codeblock: the four high-rate
-// rows of BG1 Z = 384 are 48 lane tasks.
+// ---- bit-sliced encoder (ldpc_encode_device.h) ----------------------------------------------------------
+// One wave per codeblock: the four high-rate rows of BG1 Z = 384 are 48 lane tasks.
 constexpr int ENC_BITS_THREADS = 64;
 constexpr uint32_t ENC_MSG_UNROLL = 5; // 1,056-byte BG1 Z = 384 message: 264 words, five per lane
-
-__device__ __forceinline__ uint32_t lds_bits32(const uint32_t* W, uint32_t off)
-{
-  const uint32_t w = off >> 5;
-  return __builtin_amdgcn_alignbit(W[w + 1], W[w], off & 31u);
-}
-
-// Rows x0 .. x0+31 of the column starting at bit cz, cyclically shifted by s: row x takes the column
-// bit (x + s) mod Z (x0 < Z, s < Z, Z >= 32; rows >= Z are don't-care).
-__device__ __forceinline__ uint32_t cyc32(const uint32_t* W, uint32_t cz, uint32_t Z, uint32_t x0, uint32_t s)
-{
-  uint32_t pos = x0 + s;
-  pos -= pos >= Z ? Z : 0u;
-  uint32_t v = lds_bits32(W, cz + pos);
-  if (pos + 32 > Z) {
-    const uint32_t n1 = Z - pos; // 1 .. 31
-    v = (v & ((1u << n1) - 1u)) | (lds_bits32(W, cz) << n1);
-  }
-  return v;
-}
-
-// ORs the low n bits of v into the (zeroed) bits off .. off+n-1.
-__device__ __forceinline__ void lds_or_bits(uint32_t* W, uint32_t off, uint32_t v, uint32_t n)
-{
-  v &= n < 32 ? (1u << n) - 1u : 0xffffffffu;
-  const uint32_t w = off >> 5, sh = off & 31u;
-  atomicOr(&W[w], v << sh);
-  if (sh != 0) {
-    atomicOr(&W[w + 1], v >> (32 - sh));
-  }
-}
 
 __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(encode_args a)
 {
@@ -214,8 +179,7 @@ __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(enco
     }
     const uint32_t kz  = K * Z;
     const uint32_t nq  = (Z + 31) / 32;
-    const uint32_t tot = (K + M_eff) * Z;
-    const uint32_t ncw = (tot + 31) / 32 + 2;
+    const uint32_t ncw = enc_bits_cw_words(K, M_eff, Z);
     uint32_t*      cw  = lw;            // [ncw] codeword bits
     uint32_t*      lam = lw + ncw;      // [4][nq] systematic part of the high-rate rows
     uint32_t*      ls  = lam + 4 * nq;  // [nq + 2] lambda sum as a column at bit 0
@@ -263,70 +227,8 @@ __global__ __launch_bounds__(ENC_BITS_THREADS) void ldpc_encode_bits_kernel(enco
     }
     __syncthreads();
 
-    // 2. Systematic part of the high-rate rows, 32 rows per task.
-    for (uint32_t task = j; task < 4 * nq; task += ENC_BITS_THREADS) {
-      const uint32_t r = task / nq, x0 = 32 * (task - r * nq);
-      uint32_t       acc = 0;
-      for (int e = a.row_start[r]; e < a.row_start[r + 1]; ++e) {
-        const uint32_t ed   = edges[e];
-        const uint32_t base = ed & 0xffffu;
-        if (base >= kz) {
-          break; // edges are sorted by column
-        }
-        acc ^= cyc32(cw, base, Z, x0, ed >> 16);
-      }
-      lam[task] = acc;
-    }
-    __syncthreads();
-    for (uint32_t q = j; q < nq; q += ENC_BITS_THREADS) {
-      const uint32_t n = min(32u, Z - 32 * q);
-      const uint32_t v = lam[q] ^ lam[nq + q] ^ lam[2 * nq + q] ^ lam[3 * nq + q];
-      ls[q]            = n < 32 ? v & ((1u << n) - 1u) : v;
-    }
-    __syncthreads();
-
-    // 3. p0 = P^-s (lambda sum): row x takes the sum's row (x - s) mod Z.
-    const uint32_t sh0 = (Z - static_cast<uint32_t>(p0_shift) % Z) % Z;
-    for (uint32_t q = j; q < nq; q += ENC_BITS_THREADS) {
-      lds_or_bits(cw, kz + 32 * q, cyc32(ls, 0, Z, 32 * q, sh0), min(32u, Z - 32 * q));
-    }
-    __syncthreads();
-
-    // 4. p1 .. p3 (double diagonal).
-    for (uint32_t q = j; q < nq; q += ENC_BITS_THREADS) {
-      const uint32_t x0 = 32 * q, n = min(32u, Z - x0);
-      auto           at = [&](int s) { return cyc32(cw, kz, Z, x0, static_cast<uint32_t>(s)); };
-      uint32_t       p1, p2, p3;
-      p1 = lam[q] ^ at(core_a[0]);
-      if (a.bg == 1) {
-        p2 = lam[nq + q] ^ at(core_a[1]) ^ p1;
-        p3 = lam[2 * nq + q] ^ p2;
-      } else {
-        p2 = lam[nq + q] ^ p1;
-        p3 = lam[2 * nq + q] ^ at(core_a[2]) ^ p2;
-      }
-      lds_or_bits(cw, kz + Z + x0, p1, n);
-      lds_or_bits(cw, kz + 2 * Z + x0, p2, n);
-      lds_or_bits(cw, kz + 3 * Z + x0, p3, n);
-    }
-    __syncthreads();
-
-    // 5. Extension rows: independent single-parity rows over columns < K + 4.
-    const uint32_t hz = kz + 4 * Z;
-    for (uint32_t task = j; task < (M_eff - 4) * nq; task += ENC_BITS_THREADS) {
-      const uint32_t rr = task / nq, r = 4 + rr, x0 = 32 * (task - rr * nq);
-      uint32_t       acc = 0;
-      for (int e = a.row_start[r]; e < a.row_start[r + 1]; ++e) {
-        const uint32_t ed   = edges[e];
-        const uint32_t base = ed & 0xffffu;
-        if (base >= hz) {
-          break;
-        }
-        acc ^= cyc32(cw, base, Z, x0, ed >> 16);
-      }
-      lds_or_bits(cw, (K + r) * Z + x0, acc, min(32u, Z - x0));
-    }
-    __syncthreads();
+    // 2-5. Parity (ldpc_encode_device.h).
+    encode_bits_parity<ENC_BITS_THREADS>(cw, lam, ls, edges, a.row_start, a.bg, K, Z, M_eff, p0_shift, core_a, j);
 
     // 6. Pack the shortened codeword (from bit 2Z), MSB-first.
     uint8_t*       out   = a.cws + static_cast<size_t>(cb) * a.cw_stride;
@@ -360,8 +262,7 @@ hipError_t launch_ldpc_encode(const encode_args& a, int grid, hipStream_t stream
 {
   // (mixed Z: a.Z / a.M_eff are the largest of the launch, for the LDS size)
   if (a.Z >= 32 || a.rows != nullptr) {
-    const size_t nq    = (a.Z + 31) / 32;
-    const size_t words = ((static_cast<size_t>(a.K) + a.M_eff) * a.Z + 31) / 32 + 2 + 4 * nq + nq + 2;
+    const size_t words = enc_bits_lds_words(a.K, a.M_eff, a.Z);
     hipLaunchKernelGGL(ldpc_encode_bits_kernel, dim3(grid), dim3(ENC_BITS_THREADS), words * 4, stream, a);
     return hipGetLastError();
   }

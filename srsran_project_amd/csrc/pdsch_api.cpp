@@ -1,11 +1,12 @@
 // pdsch_api.cpp -- C-ABI of the MI355X PDSCH encoder (include/srsran_amd/sch.h),
 // pdsch_encoder_impl::encode (lib/phy/upper/channel_processors/pdsch/pdsch_encoder_impl.cpp:28-80)
-// for a batch of transport blocks:
-//   1. TB CRC (CRC16 / CRC24A)            crc kernel over the TB rows
-//   2. segmentation                       segment_kernel (sch.hip)
-//   3. CB CRC24B attachment (C > 1)       crc kernel, in place
-//   4. LDPC encoding                      srs_amd_ldpc_encode_batch
-//   5. rate matching + concatenation      srs_amd_ldpc_rate_match_batch into the codeword rows
+// for a batch of transport blocks (srs_amd_pdsch_encode_batch) or a slot of heterogeneous ones
+// (srs_amd_pdsch_encode_slot), both through the fused two-launch chain of pdsch_encoder.hip:
+//   1. TB CRC (CRC16 / CRC24A) partials          pdsch_tb_crc_kernel
+//   2. segmentation, CB CRC24B, LDPC encoding,   pdsch_cb_kernel, one workgroup per codeblock
+//      rate matching + concatenation
+// SRSRAN_AMD_PDSCH_FUSED=0 (read per call) selects the previous five-stage chain instead (TB CRC, segmentation
+// + CB CRC, srs_amd_ldpc_encode_batch, srs_amd_ldpc_rate_match_batch), kept for A/B timing and cross-checks.
 #include "srsran_amd/crc.h"
 #include "srsran_amd/ldpc_encoder.h"
 #include "srsran_amd/ldpc_rate_matching.h"
@@ -16,10 +17,13 @@
 #include "api_common.h"
 #include "crc_internal.h"
 #include "device_buffer.h"
+#include "ldpc_codec_args.h"
+#include "ldpc_common.h"
 #include "ldpc_codec_internal.h"
 #include "rate_matching_common.h"
 #include "sch_args.h"
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -37,6 +41,8 @@ struct srs_amd_pdsch_encoder {
   srs_amd_ldpc_encoder*      enc    = nullptr;
   srs_amd_ldpc_rate_matcher* rm     = nullptr;
   device_buffer              tb_crcs, msgs, coded, rm_arrays, host_io, slot_desc;
+  device_buffer              batch_desc, tb_parts; // fused chain: uniform-batch descriptors, TB CRC partials
+  std::vector<uint8_t>       batch_key;            // the batch whose descriptors batch_desc holds
   geometry_cache             rm_geo; // last geometry written into rm_arrays
   stream_order               order; // scratch reuse across the callers' streams
   stream_fan                 fan;   // srs_amd_pdsch_encode_slot: concurrent LDPC encoder bucket launches
@@ -76,6 +82,258 @@ int check_plan(const srs_amd_sch_plan* p)
   return SRS_AMD_OK;
 }
 
+bool fused_enabled()
+{
+  const char* mode = std::getenv("SRSRAN_AMD_PDSCH_FUSED");
+  return mode == nullptr || mode[0] != '0';
+}
+
+// Host descriptors of one fused launch (pdsch_fused_args).
+struct fused_rows {
+  std::vector<tb_desc>      tds;
+  std::vector<uint32_t>     row_E, row_out, row_geo, row_tb;
+  std::vector<rm_geometry>  geos;
+  std::vector<enc_row_desc> enc;
+  uint32_t                  max_tb_bytes = 0;
+};
+
+struct fused_layout {
+  size_t o_E, o_out, o_geo, o_tb, o_G, o_TD, o_ER, total;
+  explicit fused_layout(const fused_rows& f)
+  {
+    const size_t R = f.row_E.size();
+    o_E            = 0;
+    o_out          = o_E + align_up(sizeof(uint32_t) * R, 16);
+    o_geo          = o_out + align_up(sizeof(uint32_t) * R, 16);
+    o_tb           = o_geo + align_up(sizeof(uint32_t) * R, 16);
+    o_G            = o_tb + align_up(sizeof(uint32_t) * R, 16);
+    o_TD           = o_G + align_up(sizeof(rm_geometry) * f.geos.size(), 16);
+    o_ER           = o_TD + align_up(sizeof(tb_desc) * f.tds.size(), 16);
+    total          = o_ER + sizeof(enc_row_desc) * R;
+  }
+};
+
+// Appends the codeblock rows of one transport block (plan p, TB bytes at tb_offset, codeword at bit cw_bit) with
+// rate-matching geometry index geo.
+void fused_add_tb(fused_rows& f, const srs_amd_sch_plan* p, uint64_t tb_offset, uint64_t cw_bit, uint32_t geo,
+                  const enc_row_desc& er, std::vector<uint32_t>& segE, std::vector<uint32_t>& segOff)
+{
+  const uint32_t row0 = static_cast<uint32_t>(f.row_E.size());
+  const uint32_t t    = static_cast<uint32_t>(f.tds.size());
+  f.tds.push_back(tb_desc{tb_offset, row0, p->nof_segments, p->cb_info_bits, p->tbs, p->nof_tb_crc_bits, p->zero_pad,
+                          (p->segment_length + 7) / 8, 0});
+  segE.resize(p->nof_segments);
+  segOff.resize(p->nof_segments);
+  (void)srs_amd_sch_plan_segments(p, segE.data(), segOff.data());
+  for (uint32_t r = 0; r < p->nof_segments; ++r) {
+    f.row_E.push_back(segE[r]);
+    f.row_out.push_back(static_cast<uint32_t>(cw_bit) + segOff[r]);
+    f.row_geo.push_back(geo);
+    f.row_tb.push_back(t);
+    f.enc.push_back(er);
+  }
+  f.max_tb_bytes = std::max(f.max_tb_bytes, p->tbs / 8);
+}
+
+// Encoder row descriptor of plan p: lifted graph and the circular-buffer window [0, k0 + E + F) the rate matcher
+// reads (ldpc_rate_matcher_impl.cpp:95-130), capped at Ncb.
+enc_row_desc fused_enc_row(const srs_amd_sch_plan* p, const rm_geometry& g)
+{
+  const uint64_t window = static_cast<uint64_t>(g.k0) + std::max(p->rm_length_long, p->rm_length_short) + g.F;
+  enc_row_desc   er{};
+  (void)ldpc_encode_mixed_row(&er, p->base_graph, p->lifting_size,
+                              window >= g.Ncb ? g.Ncb : static_cast<uint32_t>(window));
+  return er;
+}
+
+// Writes the descriptors to dd (device) from the pinned staging buffer when `upload`, then runs the two launches.
+int fused_launch_locked(srs_amd_pdsch_encoder* e,
+                        const fused_rows&      f,
+                        uint8_t*               dd,
+                        bool                   upload,
+                        const uint8_t*         d_tbs,
+                        uint8_t*               d_cw,
+                        hipStream_t            stream)
+{
+  static const auto row_starts = [] {
+    std::vector<int32_t> rs(2 * 47, 0);
+    for (int bg = 1; bg <= 2; ++bg) {
+      lifted_graph g{};
+      build_lifted_graph(g, bg, 2);
+      std::copy(g.row_start, g.row_start + g.M + 1, rs.begin() + 47 * (bg - 1));
+    }
+    return rs;
+  }();
+  const fused_layout L(f);
+  const uint32_t     U           = static_cast<uint32_t>(f.tds.size());
+  const uint32_t     R           = static_cast<uint32_t>(f.row_E.size());
+  const uint32_t     part_stride = std::max(1u, (f.max_tb_bytes + PE_TB_CHUNK - 1) / PE_TB_CHUNK);
+  hipError_t         he          = e->tb_parts.ensure(sizeof(uint32_t) * U * part_stride);
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH encoder TB CRC partials");
+  }
+  call_scope scope(e->order, nullptr, stream);
+  he = e->order.begin(stream);
+  if (he == hipSuccess && upload) {
+    // the pinned staging buffer is rewritten only once its previous upload completed
+    if (e->stage_used) {
+      he = hipEventSynchronize(e->stage_done);
+    }
+    if (he == hipSuccess && e->stage_done == nullptr) {
+      he = hipEventCreateWithFlags(&e->stage_done, hipEventDisableTiming);
+    }
+    if (he == hipSuccess && e->h_stage_size < L.total) {
+      (void)hipHostFree(e->h_stage);
+      e->h_stage      = nullptr;
+      e->h_stage_size = 0;
+      he              = hipHostMalloc(&e->h_stage, L.total, hipHostMallocDefault);
+      if (he == hipSuccess) {
+        e->h_stage_size = L.total;
+      }
+    }
+    if (he == hipSuccess) {
+      auto* h = static_cast<uint8_t*>(e->h_stage);
+      std::memcpy(h + L.o_E, f.row_E.data(), sizeof(uint32_t) * R);
+      std::memcpy(h + L.o_out, f.row_out.data(), sizeof(uint32_t) * R);
+      std::memcpy(h + L.o_geo, f.row_geo.data(), sizeof(uint32_t) * R);
+      std::memcpy(h + L.o_tb, f.row_tb.data(), sizeof(uint32_t) * R);
+      std::memcpy(h + L.o_G, f.geos.data(), sizeof(rm_geometry) * f.geos.size());
+      std::memcpy(h + L.o_TD, f.tds.data(), sizeof(tb_desc) * U);
+      std::memcpy(h + L.o_ER, f.enc.data(), sizeof(enc_row_desc) * R);
+      he = hipMemcpyAsync(dd, h, L.total, hipMemcpyHostToDevice, stream);
+    }
+    if (he == hipSuccess) {
+      he = hipEventRecord(e->stage_done, stream);
+      e->stage_used = he == hipSuccess;
+    }
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH encoder descriptors upload");
+  }
+  pdsch_fused_args a{};
+  a.tbs          = d_tbs;
+  a.tds          = reinterpret_cast<const tb_desc*>(dd + L.o_TD);
+  a.row_tb       = reinterpret_cast<const uint32_t*>(dd + L.o_tb);
+  a.row_E        = reinterpret_cast<const uint32_t*>(dd + L.o_E);
+  a.row_out      = reinterpret_cast<const uint32_t*>(dd + L.o_out);
+  a.row_geo      = reinterpret_cast<const uint32_t*>(dd + L.o_geo);
+  a.geos         = reinterpret_cast<const rm_geometry*>(dd + L.o_G);
+  a.enc_rows     = reinterpret_cast<const enc_row_desc*>(dd + L.o_ER);
+  a.edges        = ldpc_encoder_edges(e->enc);
+  a.tb_parts     = e->tb_parts.as<uint32_t>();
+  a.part_stride  = part_stride;
+  a.crc16_table  = crc_device_table(e->crc16);
+  a.crc24a_table = crc_device_table(e->crc24a);
+  a.crc24b_table = crc_device_table(e->crc24b);
+  a.crc16_poly   = crc_polynom(e->crc16);
+  a.crc24a_poly  = crc_polynom(e->crc24a);
+  a.crc24b_poly  = crc_polynom(e->crc24b);
+  a.cw           = d_cw;
+  a.nof_tbs      = U;
+  a.nof_cbs      = R;
+  a.max_tb_bytes = f.max_tb_bytes;
+  std::copy(row_starts.begin(), row_starts.begin() + 47, a.row_start[0]);
+  std::copy(row_starts.begin() + 47, row_starts.end(), a.row_start[1]);
+  he = launch_pdsch_fused(a, stream);
+  if (he == hipSuccess) {
+    he = scope.close();
+  }
+  return he == hipSuccess ? SRS_AMD_OK : hip_fail(he, "PDSCH fused encoder launch");
+}
+
+// srs_amd_pdsch_encode_batch through the fused chain: the descriptors of a uniform batch, uploaded again only
+// when the batch (plan, count, strides) changes.
+int encode_fused_batch_locked(srs_amd_pdsch_encoder* e,
+                              const srs_amd_sch_plan* p,
+                              uint8_t*                d_cw,
+                              uint32_t                cw_stride,
+                              const uint8_t*          d_tbs,
+                              uint32_t                tb_stride,
+                              uint32_t                nof_tbs,
+                              hipStream_t             stream)
+{
+  std::vector<uint8_t> key(sizeof(*p) + 3 * sizeof(uint32_t));
+  std::memcpy(key.data(), p, sizeof(*p));
+  const uint32_t k3[3] = {cw_stride, tb_stride, nof_tbs};
+  std::memcpy(key.data() + sizeof(*p), k3, sizeof(k3));
+  rm_geometry g{};
+  if (const char* msg = make_rm_geometry(g, p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                                         p->nof_filler_bits)) {
+    return fail(SRS_AMD_EINVAL, "%s", msg);
+  }
+  fused_rows f;
+  f.geos.push_back(g);
+  const enc_row_desc    er = fused_enc_row(p, g);
+  std::vector<uint32_t> segE, segOff;
+  for (uint32_t t = 0; t < nof_tbs; ++t) {
+    fused_add_tb(f, p, static_cast<uint64_t>(t) * tb_stride, static_cast<uint64_t>(t) * cw_stride * 8, 0, er, segE,
+                 segOff);
+  }
+  const bool upload = key != e->batch_key;
+  hipError_t he     = hipSetDevice(e->device);
+  if (he == hipSuccess && upload) {
+    he = e->batch_desc.ensure(fused_layout(f).total);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH encoder descriptors");
+  }
+  e->batch_key.clear();
+  int rc = fused_launch_locked(e, f, e->batch_desc.as<uint8_t>(), upload, d_tbs, d_cw, stream);
+  if (rc == SRS_AMD_OK) {
+    e->batch_key = std::move(key);
+  }
+  return rc;
+}
+
+// srs_amd_pdsch_encode_slot through the fused chain (every UE's plan, one launch pair).
+int encode_fused_slot_locked(srs_amd_pdsch_encoder*  e,
+                             const srs_amd_pdsch_ue* ues,
+                             uint32_t                U,
+                             const uint8_t*          d_tbs,
+                             uint8_t*                d_cw,
+                             hipStream_t             stream)
+{
+  fused_rows f;
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> geo_of;
+  std::vector<uint32_t> segE, segOff;
+  uint32_t              R = 0;
+  for (uint32_t u = 0; u < U; ++u) {
+    const srs_amd_sch_plan* p  = &ues[u].plan;
+    int                     rc = check_plan(p);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+    rm_geometry g{};
+    if (const char* msg = make_rm_geometry(g, p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                                           p->nof_filler_bits)) {
+      return fail(SRS_AMD_EINVAL, "UE %u: %s", u, msg);
+    }
+    if ((ues[u].cw_offset + (p->cw_length + 7) / 8) * 8 > 0xffffffffull) {
+      return fail(SRS_AMD_EINVAL, "UE %u: codeword span exceeds 2^32 bits", u);
+    }
+    R += p->nof_segments;
+    if (U > 65535 || R > 65535) {
+      return fail(SRS_AMD_EINVAL, "%u UEs / %u+ codeblocks exceed the 65535 of one slot batch", U, R);
+    }
+    const auto gkey = std::make_tuple(p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                                      p->nof_filler_bits, 0u);
+    auto       git  = geo_of.find(gkey);
+    if (git == geo_of.end()) {
+      git = geo_of.emplace(gkey, static_cast<uint32_t>(f.geos.size())).first;
+      f.geos.push_back(g);
+    }
+    fused_add_tb(f, p, ues[u].tb_offset, ues[u].cw_offset * 8, git->second, fused_enc_row(p, g), segE, segOff);
+  }
+  hipError_t he = hipSetDevice(e->device);
+  if (he == hipSuccess) {
+    he = e->slot_desc.ensure(fused_layout(f).total);
+  }
+  if (he != hipSuccess) {
+    return hip_fail(he, "PDSCH slot encoder descriptors");
+  }
+  return fused_launch_locked(e, f, e->slot_desc.as<uint8_t>(), true, d_tbs, d_cw, stream);
+}
+
 int encode_locked(srs_amd_pdsch_encoder* e,
                   const srs_amd_sch_plan* p,
                   uint8_t*                d_cw,
@@ -85,6 +343,9 @@ int encode_locked(srs_amd_pdsch_encoder* e,
                   uint32_t                nof_tbs,
                   hipStream_t             stream)
 {
+  if (fused_enabled()) {
+    return encode_fused_batch_locked(e, p, d_cw, cw_stride, d_tbs, tb_stride, nof_tbs, stream);
+  }
   const uint32_t C          = p->nof_segments;
   const uint32_t rows       = nof_tbs * C;
   const uint32_t K          = p->segment_length;
@@ -192,6 +453,9 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
                        uint8_t*                d_cw,
                        hipStream_t             stream)
 {
+  if (fused_enabled()) {
+    return encode_fused_slot_locked(e, ues, U, d_tbs, d_cw, stream);
+  }
   // Z < 32: one uniform launch per (BG, Z) (the byte-per-bit kernel); Z >= 32: one mixed-Z launch per BG
   // (the bit-sliced kernel reads each codeblock's Z, graph and encoded window from a row descriptor)
   struct bucket {

@@ -266,8 +266,8 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
                        hipStream_t                         stream)
 {
   // Z = 384 rows: one uniform launch per (BG, CRC, bounded prefix) -- the compile-time Z = 384 kernels,
-  // the high-rate one for bounded prefixes; Z < 384 rows: one mixed-Z launch per (BG, waves per
-  // codeblock), each row with its own Z, CRC, input length and filler bits.
+  // the high-rate one for bounded prefixes; Z < 384 rows: one mixed-Z launch per (BG, kernel class: the
+  // packed kernel's waves per codeblock), each row with its own Z, CRC, input length and filler bits.
   struct bucket {
     uint32_t              bg, Z; // Z: the lifting size (uniform) or the largest one (mixed)
     int                   poly;  // uniform buckets
@@ -299,7 +299,11 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     // rows whose non-zero prefix is bounded decode apart from full rows: the bucket's LLR length is its
     // longest prefix, and a bounded one selects the high-rate decoder kernel
     const bool mixed = p->lifting_size < 384;
-    const auto key   = mixed ? std::make_tuple(p->base_graph, (p->lifting_size + 63) / 64, -1, false)
+    // mixed launches: one per (BG, kernel class) -- the packed kernel's waves per codeblock, or (Z not a
+    // multiple of 4) the one-row-per-lane kernel's
+    const int  pkw   = ldpc_pk_waves(static_cast<int>(p->base_graph), static_cast<int>(p->lifting_size));
+    const auto key   = mixed ? std::make_tuple(p->base_graph, pkw > 0 ? static_cast<uint32_t>(pkw)
+                                                                     : 10u + (p->lifting_size + 63) / 64, -1, false)
                              : std::make_tuple(p->base_graph, p->lifting_size, crc_poly_of(p), prefix < lay.soft_bytes);
     auto       it    = bucket_of.find(key);
     if (it == bucket_of.end()) {

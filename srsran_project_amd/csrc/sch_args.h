@@ -10,6 +10,9 @@
 
 namespace srs_amd {
 
+struct rm_geometry;
+struct enc_row_desc;
+
 // ldpc_segmenter_tx_impl::read_codeblock (ldpc_segmenter_tx_impl.cpp:137-207) for
 // every (TB, segment) pair: data bits, TB CRC + zero pad in the last segment,
 // zeros where the CB CRC (attached afterwards) and the filler bits go.
@@ -72,6 +75,34 @@ struct tx_slot_args {
   uint32_t        max_msg_bytes;
 };
 hipError_t launch_tx_slot_segment(const tx_slot_args& a, hipStream_t stream);
+
+// Fused PDSCH encoder (pdsch_encoder.hip): launch 1 computes the TB CRC partials (one per PE_TB_CHUNK bytes of a
+// TB, moved to the TB end) and zeroes the codeword bytes two segments share; launch 2 builds, CRC-attaches,
+// LDPC-encodes and rate-matches one codeblock per workgroup, the codeblock never leaving LDS.
+struct pdsch_fused_args {
+  const uint8_t*                 tbs;      // TB bytes (tds[t].tb_offset)
+  const tb_desc*                 tds;      // per TB
+  const uint32_t*                row_tb;   // per codeblock: TB index
+  const uint32_t*                row_E;    // per codeblock: rate-matched length
+  const uint32_t*                row_out;  // per codeblock: first codeword bit (absolute)
+  const uint32_t*                row_geo;  // per codeblock: index into geos
+  const struct rm_geometry*      geos;
+  const struct enc_row_desc*     enc_rows; // per codeblock: lifted graph, encoded window
+  const uint32_t*                edges;    // every lifted graph (enc_row_desc::edge_off)
+  uint32_t*                      tb_parts; // [nof_tbs][part_stride] TB CRC partials
+  uint32_t                       part_stride;
+  const uint32_t*                crc16_table;
+  const uint32_t*                crc24a_table;
+  const uint32_t*                crc24b_table;
+  uint32_t                       crc16_poly, crc24a_poly, crc24b_poly;
+  uint8_t*                       cw;       // codewords
+  uint32_t                       nof_tbs;
+  uint32_t                       nof_cbs;
+  uint32_t                       max_tb_bytes;
+  int32_t                        row_start[2][47]; // check-row edge offsets of BG1 / BG2
+};
+constexpr uint32_t PE_TB_CHUNK = 8192; // TB bytes per partial of the TB CRC
+hipError_t launch_pdsch_fused(const pdsch_fused_args& a, hipStream_t stream);
 
 // pusch_decoder_impl.cpp:309-500 after the decoder: per-CB CRC status (kept in the
 // soft buffer across HARQ transmissions), statistics, codeblock concatenation

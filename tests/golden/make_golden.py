@@ -28,6 +28,12 @@ for bg in (1, 2):
 CASES += [("avx2", 1, 384, None, 8, -1, 0, 9.0), ("avx2", 1, 384, None, 8, 1, 0, 9.0),
           ("generic", 2, 384, None, 8, -1, 0, 9.0), ("avx2", 1, 64, 38, 5, 0, 64, 7.0),
           ("avx2", 2, 26, 20, 4, 3, 0, 6.0), ("avx2", 1, 13, 24, 1, -1, 0, 0.0)]
+# round 4: BG2 and Z < 384 through every class of the packed runtime-Z kernel (1, 2, 3 waves per codeblock),
+# shortened, with CRC early stop and filler bits
+CASES += [("avx2", 2, 52, None, 6, 3, 0, 7.5), ("generic", 2, 144, 30, 6, 1, 40, 7.0),
+          ("avx2", 2, 256, 20, 5, 0, 0, 6.5), ("avx2", 1, 120, None, 6, 1, 0, 8.0),
+          ("generic", 1, 224, 40, 6, 0, 96, 8.0), ("avx2", 1, 320, 30, 8, 1, 0, 7.0),
+          ("avx2", 1, 352, 26, 6, 1, 64, 6.0), ("generic", 2, 320, 14, 4, 3, 0, 5.0)]
 
 
 def main():

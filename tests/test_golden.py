@@ -38,13 +38,16 @@ def test_oracle_decoder_reproduces_golden():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("full", ["auto", "1"])
+@pytest.mark.parametrize("full", ["auto", "1", "nopk"])
 def test_gpu_decoder_reproduces_golden(full, monkeypatch):
-    # "1": BG1 Z=384 vectors (configs[1]) through the packed full-length kernel whatever the batch size
+    # "1": BG1 Z=384 vectors (configs[1]) through the packed full-length kernel whatever the batch size;
+    # "nopk": every other graph on the one-row-per-lane kernel instead of the packed runtime-Z kernel
+    monkeypatch.delenv("SRSRAN_AMD_LDPC_FULL", raising=False)
+    monkeypatch.delenv("SRSRAN_AMD_LDPC_PK", raising=False)
     if full == "1":
         monkeypatch.setenv("SRSRAN_AMD_LDPC_FULL", "1")
-    else:
-        monkeypatch.delenv("SRSRAN_AMD_LDPC_FULL", raising=False)
+    elif full == "nopk":
+        monkeypatch.setenv("SRSRAN_AMD_LDPC_PK", "0")
     import torch
 
     import srsran_project_amd as amd

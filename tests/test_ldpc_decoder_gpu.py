@@ -16,7 +16,9 @@ from tests.ldpc_cases import noisy_codeblocks
 
 pytestmark = pytest.mark.gpu
 
-ZS = [2, 3, 5, 7, 9, 11, 13, 15, 16, 36, 64, 104, 208, 240, 384]
+# every kernel class: Z not a multiple of 4 (one row per lane), the packed runtime-Z kernel with 1, 2 and 3 waves
+# per codeblock (Z <= 128, <= 256, > 256), BG1 Z = 384 (compile-time kernels)
+ZS = [2, 3, 4, 5, 7, 9, 11, 12, 13, 15, 16, 36, 44, 64, 104, 128, 144, 208, 240, 256, 288, 352, 384]
 
 
 @pytest.fixture(scope="module")
@@ -26,15 +28,19 @@ def amd():
     return amd
 
 
-@pytest.fixture(autouse=True, params=["auto", "full"])
+@pytest.fixture(autouse=True, params=["auto", "full", "nopk"])
 def full_length_kernel(request, monkeypatch):
-    """Every case twice: the launch's own kernel choice (small batches of full-length BG1 Z=384 codeblocks go to
-    ldpc_decode_kernel) and SRSRAN_AMD_LDPC_FULL=1, which sends every BG1 Z=384 launch the high-rate kernel does
-    not take through the packed full-length kernel whatever the batch size."""
+    """Every case three times: the launch's own kernel choice (small batches of full-length BG1 Z=384 codeblocks go
+    to ldpc_decode_kernel, other graphs with Z a multiple of 4 to the packed runtime-Z kernel),
+    SRSRAN_AMD_LDPC_FULL=1, which sends every BG1 Z=384 launch the high-rate kernel does not take through the packed
+    full-length kernel whatever the batch size, and SRSRAN_AMD_LDPC_PK=0, which keeps every other graph on the
+    one-row-per-lane ldpc_decode_kernel."""
+    monkeypatch.delenv("SRSRAN_AMD_LDPC_FULL", raising=False)
+    monkeypatch.delenv("SRSRAN_AMD_LDPC_PK", raising=False)
     if request.param == "full":
         monkeypatch.setenv("SRSRAN_AMD_LDPC_FULL", "1")
-    else:
-        monkeypatch.delenv("SRSRAN_AMD_LDPC_FULL", raising=False)
+    elif request.param == "nopk":
+        monkeypatch.setenv("SRSRAN_AMD_LDPC_PK", "0")
     return request.param
 
 
@@ -77,7 +83,7 @@ def test_parity_all_families(amd, bg, arith):
 def test_parity_shortened_lengths(amd, bg):
     # ldpc_enc_dec_test.cpp: create_range(min_cb_length, max_cb_length, 3).
     dec = amd.LdpcDecoder("simd")
-    for Z in (5, 52, 384):
+    for Z in (5, 52, 160, 320, 384):
         lo = (24 if bg == 1 else 12) * Z
         hi = oracle.BG_N_SHORT[bg] * Z
         step = (hi - lo) // 3
