@@ -10,6 +10,9 @@
  *   srs_amd_ofdm_modulator_get_slot_size / srs_amd_ofdm_modulate_slot
  *       ofdm_slot_modulator::get_slot_size / ::modulate(output, grid, port, slot_index)
  *       include/srsran/phy/lower/modulation/ofdm_modulator.h:98,108
+ *   srs_amd_ofdm_modulator_get_symbol_size / _set_center_frequency / srs_amd_ofdm_modulate_symbol
+ *       ofdm_symbol_modulator::get_symbol_size / ::set_center_frequency / ::modulate(output, grid, port, symbol)
+ *       include/srsran/phy/lower/modulation/ofdm_modulator.h:47-76
  *   srs_amd_ofdm_demodulator_* (same for ofdm_demodulator.h, nof_samples_window_offset honoured)
  *   srs_amd_dft_create / srs_amd_dft_run
  *       create_dft_processor_factory_generic()->create({size, dir}) / dft_processor::run()
@@ -74,6 +77,19 @@ int srs_amd_ofdm_modulate_batch(srs_amd_ofdm_modulator* mod,
                                 uint32_t                sample_stride,
                                 void*                   stream);
 
+/* Symbol granularity (ofdm_symbol_modulator, ofdm_modulator.h:47-76): symbol_index within the subframe,
+ * HOST buffers, synchronous.
+ *   get_symbol_size : cyclic prefix + DFT size samples (ofdm_symbol_modulator::get_symbol_size)
+ *   set_center_frequency : phase compensation of the following calls (ofdm_symbol_modulator::set_center_frequency;
+ *                          the slot forms use it too)
+ *   modulate_symbol : output get_symbol_size(symbol_index) complex floats; grid_symbol bw_rb * 12 cbf16 */
+uint32_t srs_amd_ofdm_modulator_get_symbol_size(const srs_amd_ofdm_modulator* mod, uint32_t symbol_index);
+int      srs_amd_ofdm_modulator_set_center_frequency(srs_amd_ofdm_modulator* mod, double center_freq_hz);
+int      srs_amd_ofdm_modulate_symbol(srs_amd_ofdm_modulator* mod,
+                                      float*                  output,
+                                      const uint16_t*         grid_symbol,
+                                      uint32_t                symbol_index);
+
 int      srs_amd_ofdm_demodulator_create(srs_amd_ofdm_demodulator** dem, const srs_amd_ofdm_config* cfg, int device);
 void     srs_amd_ofdm_demodulator_destroy(srs_amd_ofdm_demodulator* dem);
 uint32_t srs_amd_ofdm_demodulator_get_slot_size(const srs_amd_ofdm_demodulator* dem, uint32_t slot_index);
@@ -89,6 +105,15 @@ int      srs_amd_ofdm_demodulate_batch(srs_amd_ofdm_demodulator* dem,
                                        uint32_t                  nof_slots,
                                        uint16_t*                 d_grid,
                                        void*                     stream);
+
+/* ofdm_symbol_demodulator (ofdm_demodulator.h:44-73): as the modulator's symbol forms; grid_symbol receives the
+ * bw_rb * 12 cbf16 subcarriers of the symbol. */
+uint32_t srs_amd_ofdm_demodulator_get_symbol_size(const srs_amd_ofdm_demodulator* dem, uint32_t symbol_index);
+int      srs_amd_ofdm_demodulator_set_center_frequency(srs_amd_ofdm_demodulator* dem, double center_freq_hz);
+int      srs_amd_ofdm_demodulate_symbol(srs_amd_ofdm_demodulator* dem,
+                                        uint16_t*                 grid_symbol,
+                                        const float*              input,
+                                        uint32_t                  symbol_index);
 
 /* dft_processor: direction 0 = DIRECT (exp(-2*pi*i*n*k/N)), 1 = INVERSE; no normalisation. */
 int  srs_amd_dft_create(srs_amd_dft** dft, uint32_t size, int direction, int device);

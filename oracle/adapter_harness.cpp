@@ -4,6 +4,7 @@
 //   pdsch_encoder_hw_impl  (pdsch_encoder_hw_impl.cpp)  + hip_accelerator_pdsch_enc   vs pdsch_encoder_impl
 //   ofdm_slot_(de)modulator_impl (ofdm_(de)modulator_impl.cpp) + dft_processor_hip     vs the generic DFT
 //   pusch_demodulator_impl (pusch_demodulator_impl.cpp) + channel_equalizer_hip        vs channel_equalizer_generic
+//   ofdm_modulator_factory / ofdm_demodulator_factory plug-ins (ofdm_modulator_hip)      vs ofdm_slot_*_impl
 //   pusch_decoder_impl / pusch_codeblock_decoder (pusch_codeblock_decoder.cpp) + ldpc_decoder_hip
 //                                                                                        vs the AVX2 / generic decoders
 // Built by oracle/Makefile into oracle/_ref/libsrsran_ref_hw.so with hw_harness.cpp.  Never loaded by the product.
@@ -13,9 +14,11 @@
 #include "../integration/dft_processor_hip.h"
 #include "../integration/hip_accelerator_pdsch_enc.h"
 #include "../integration/ldpc_decoder_hip.h"
+#include "../integration/ofdm_modulator_hip.h"
 #include "phy/upper/channel_coding/crc_calculator_generic_impl.h"
 #include "phy/upper/channel_coding/ldpc/ldpc_segmenter_tx_impl.h"
 #include "phy/upper/channel_processors/pdsch/pdsch_encoder_hw_impl.h"
+#include <chrono>
 #include <map>
 #include <memory>
 
@@ -246,6 +249,135 @@ int srs_ref_hip_ldpc_pusch_decode(int           device,
   }
   return srs_ref::pusch_decode_on(*dec, rx_buffer, llrs, nof_llrs, tb, tb_bytes, bg, rv, qm, Nref, nof_layers,
                                   nof_iterations, force_decoding, use_early_stop, new_data, result);
+}
+
+} // extern "C"
+
+namespace {
+
+ofdm_modulator_configuration ofdm_mod_cfg(unsigned mu, unsigned bw_rb, unsigned dft_size, int ext, float scale,
+                                          double fc)
+{
+  ofdm_modulator_configuration c;
+  c.numerology     = mu;
+  c.bw_rb          = bw_rb;
+  c.dft_size       = dft_size;
+  c.cp             = ext ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL;
+  c.scale          = scale;
+  c.center_freq_Hz = fc;
+  return c;
+}
+
+ofdm_demodulator_configuration ofdm_dem_cfg(unsigned mu, unsigned bw_rb, unsigned dft_size, int ext, unsigned offset,
+                                            float scale, double fc)
+{
+  ofdm_demodulator_configuration c;
+  c.numerology                = mu;
+  c.bw_rb                     = bw_rb;
+  c.dft_size                  = dft_size;
+  c.cp                        = ext ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL;
+  c.nof_samples_window_offset = offset;
+  c.scale                     = scale;
+  c.center_freq_Hz            = fc;
+  return c;
+}
+
+} // namespace
+
+extern "C" {
+
+/* One port of one slot through the OFDM plug-ins of integration/ofdm_modulator_hip.h, created by their factories:
+ * mode 0 ofdm_slot_modulator, 1 ofdm_symbol_modulator (the slot's symbols one by one; fc2 != fc: after
+ * set_center_frequency(fc2)), 2 ofdm_slot_demodulator, 3 ofdm_symbol_demodulator.  Modulators read `grid` and
+ * write `samples`, demodulators the reverse.  -1 when a factory refuses the configuration. */
+int srs_ref_hw_ofdm_plugin(int             device,
+                           int             mode,
+                           unsigned        mu,
+                           unsigned        bw_rb,
+                           unsigned        dft_size,
+                           int             ext,
+                           unsigned        window_offset,
+                           float           scale,
+                           double          fc,
+                           double          fc2,
+                           unsigned        slot,
+                           uint16_t*       grid,
+                           float*          samples)
+{
+  const unsigned nsymb = ext ? 12 : 14;
+  const unsigned nsubc = bw_rb * NRE;
+  if (mode < 2) {
+    auto f = hip::create_ofdm_modulator_factory_hip(device);
+    auto c = ofdm_mod_cfg(mu, bw_rb, dft_size, ext, scale, fc);
+    if (mode == 0) {
+      auto m = f->create_ofdm_slot_modulator(c);
+      if (!m) {
+        return -1;
+      }
+      srs_ref::ofdm_run_slot_modulator(*m, nsymb, nsubc, slot, grid, samples);
+      return 0;
+    }
+    auto m = f->create_ofdm_symbol_modulator(c);
+    if (!m) {
+      return -1;
+    }
+    if (fc2 != fc) {
+      m->set_center_frequency(fc2);
+    }
+    srs_ref::ofdm_run_symbol_modulator(*m, nsymb, nsubc, slot, grid, samples);
+    return 0;
+  }
+  auto f = hip::create_ofdm_demodulator_factory_hip(device);
+  auto c = ofdm_dem_cfg(mu, bw_rb, dft_size, ext, window_offset, scale, fc);
+  if (mode == 2) {
+    auto d = f->create_ofdm_slot_demodulator(c);
+    if (!d) {
+      return -1;
+    }
+    srs_ref::ofdm_run_slot_demodulator(*d, nsymb, nsubc, slot, samples, grid);
+    return 0;
+  }
+  auto d = f->create_ofdm_symbol_demodulator(c);
+  if (!d) {
+    return -1;
+  }
+  if (fc2 != fc) {
+    d->set_center_frequency(fc2);
+  }
+  srs_ref::ofdm_run_symbol_demodulator(*d, nsymb, nsubc, slot, samples, grid);
+  return 0;
+}
+
+/* Throughput of slot (de)modulation of one port: `calls` slots through the plug-in (plugin = 1) or the reference's
+ * ofdm_slot_(de)modulator_impl over the generic DFT (plugin = 0, this thread), cycling over the slots of a
+ * subframe; returns the seconds taken (-1 on a refused configuration). */
+double srs_ref_hw_ofdm_bench(int device, int plugin, int demod, unsigned mu, unsigned bw_rb, unsigned dft_size,
+                             unsigned calls, const uint16_t* grid, float* samples, uint16_t* grid_out)
+{
+  const unsigned nsymb = 14, nsubc = bw_rb * NRE, nslots = 1u << mu;
+  std::unique_ptr<ofdm_slot_modulator>   mod;
+  std::unique_ptr<ofdm_slot_demodulator> dem;
+  if (demod) {
+    auto c = ofdm_dem_cfg(mu, bw_rb, dft_size, 0, 0, 1.0f, 3.5e9);
+    dem    = plugin ? hip::create_ofdm_demodulator_factory_hip(device)->create_ofdm_slot_demodulator(c)
+                    : srs_ref::make_ref_ofdm_slot_demodulator(c);
+  } else {
+    auto c = ofdm_mod_cfg(mu, bw_rb, dft_size, 0, 1.0f, 3.5e9);
+    mod    = plugin ? hip::create_ofdm_modulator_factory_hip(device)->create_ofdm_slot_modulator(c)
+                    : srs_ref::make_ref_ofdm_slot_modulator(c);
+  }
+  if (!mod && !dem) {
+    return -1;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned k = 0; k != calls; ++k) {
+    if (demod) {
+      srs_ref::ofdm_run_slot_demodulator(*dem, nsymb, nsubc, k % nslots, samples, grid_out);
+    } else {
+      srs_ref::ofdm_run_slot_modulator(*mod, nsymb, nsubc, k % nslots, grid, samples);
+    }
+  }
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 } // extern "C"

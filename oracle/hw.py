@@ -41,6 +41,10 @@ def lib():
         L.srs_ref_hip_ofdm_demodulate_slot.restype = i
         L.srs_ref_hip_ofdm_demodulate_slot.argtypes = [i, u, u, u, i, u, f, d, u, P, P]
         L.srs_ref_hip_pusch_demodulate.restype = i
+        L.srs_ref_hw_ofdm_plugin.restype = i
+        L.srs_ref_hw_ofdm_plugin.argtypes = [i, i, u, u, u, i, u, f, d, d, u, P, P]
+        L.srs_ref_hw_ofdm_bench.restype = d
+        L.srs_ref_hw_ofdm_bench.argtypes = [i, i, i, u, u, u, u, P, P, P]
         L.srs_ref_hip_pusch_demodulate.argtypes = [i, P, u, u, P, u, P, u, u, i, P, u, u, u, i, u, i, i, i, P, u, P]
         L.srs_ref_hip_ldpc_pusch_decode.restype = i
         L.srs_ref_hip_ldpc_pusch_decode.argtypes = [i, P, P, u, P, u] + [u] * 6 + [i] * 4 + [P]
@@ -125,6 +129,40 @@ def hip_ofdm_demodulate_slot(samples, slot, numerology, bw_rb, dft_size, scale, 
                                               _p(grid)):
         raise ValueError("the MI355X dft_processor refused size %d" % dft_size)
     return grid
+
+
+OFDM_PLUGIN_MODES = {"slot_mod": 0, "symbol_mod": 1, "slot_demod": 2, "symbol_demod": 3}
+
+
+def ofdm_plugin(mode, data, slot, numerology, bw_rb, dft_size, scale, fc, fc2=None, extended_cp=False,
+                window_offset=0, n=None, device=0):
+    """One port of one slot through the ofdm_modulator_factory / ofdm_demodulator_factory plug-ins of
+    integration/ofdm_modulator_hip.h ("slot_mod" / "symbol_mod": data = grid uint16 [nsymb][2 * 12 * bw_rb], returns
+    n complex samples; "slot_demod" / "symbol_demod": data = samples, returns the grid). fc2: the symbol forms call
+    set_center_frequency(fc2) first."""
+    ns = 12 if extended_cp else 14
+    fc2 = fc if fc2 is None else fc2
+    if OFDM_PLUGIN_MODES[mode] < 2:
+        grid = np.ascontiguousarray(data, dtype=np.uint16)
+        samples = np.zeros(n, np.complex64)
+    else:
+        samples = np.ascontiguousarray(data, dtype=np.complex64)
+        grid = np.zeros((ns, 2 * bw_rb * 12), np.uint16)
+    if lib().srs_ref_hw_ofdm_plugin(device, OFDM_PLUGIN_MODES[mode], numerology, bw_rb, dft_size, int(extended_cp),
+                                    window_offset, scale, fc, fc2, slot, _p(grid), _p(samples)):
+        raise ValueError("the OFDM plug-in factory refused the configuration")
+    return samples if OFDM_PLUGIN_MODES[mode] < 2 else grid
+
+
+def ofdm_bench(plugin, demod, numerology, bw_rb, dft_size, calls, device=0):
+    """Seconds for `calls` one-port slot (de)modulations through the plug-in (plugin=True) or the reference's
+    ofdm_slot_(de)modulator_impl over the generic DFT on this thread (plugin=False)."""
+    rng = np.random.default_rng(1)
+    grid = rng.integers(0, 1 << 16, (14, 2 * bw_rb * 12), dtype=np.uint16) & 0x3fff  # small finite bf16 values
+    samples = np.zeros(1 << 20, np.complex64)
+    gout = np.zeros_like(grid)
+    return lib().srs_ref_hw_ofdm_bench(device, int(plugin), int(demod), numerology, bw_rb, dft_size, calls, _p(grid),
+                                       _p(samples), _p(gout))
 
 
 def hip_pusch_demodulate(grid, estimates, noise_vars, rnti, n_id, qm, crbs, start_symbol, nof_symbols, dmrs_symb_mask,

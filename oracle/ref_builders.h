@@ -19,6 +19,8 @@
 #pragma once
 
 #include "phy/generic_functions/dft_processor_generic_impl.h"
+#include "srsran/phy/lower/modulation/ofdm_demodulator.h"
+#include "srsran/phy/lower/modulation/ofdm_modulator.h"
 #include "phy/generic_functions/transform_precoding/transform_precoder_dft_impl.h"
 #include "phy/support/interpolator/interpolator_linear_impl.h"
 #include "phy/support/time_alignment_estimator/time_alignment_estimator_dft_impl.h"
@@ -303,6 +305,19 @@ int ofdm_modulate_slot_with(std::unique_ptr<dft_processor> dft, unsigned numerol
 int ofdm_demodulate_slot_with(std::unique_ptr<dft_processor> dft, unsigned numerology, unsigned bw_rb,
                               unsigned dft_size, int extended_cp, unsigned window_offset, float scale, double fc,
                               unsigned slot, const float* in, uint16_t* grid);
+// One port of one slot through a given slot / symbol (de)modulator over a dense [symbol][subcarrier] cbf16 grid
+// (the plug-in factories of integration/ofdm_modulator_hip.h, or the reference's own classes).
+void ofdm_run_slot_modulator(ofdm_slot_modulator& mod, unsigned nsymb, unsigned nsubc, unsigned slot,
+                             const uint16_t* grid, float* out);
+void ofdm_run_symbol_modulator(ofdm_symbol_modulator& mod, unsigned nsymb, unsigned nsubc, unsigned slot,
+                               const uint16_t* grid, float* out);
+void ofdm_run_slot_demodulator(ofdm_slot_demodulator& dem, unsigned nsymb, unsigned nsubc, unsigned slot,
+                               const float* in, uint16_t* grid);
+void ofdm_run_symbol_demodulator(ofdm_symbol_demodulator& dem, unsigned nsymb, unsigned nsubc, unsigned slot,
+                                 const float* in, uint16_t* grid);
+// The reference's ofdm_slot_(de)modulator_impl over the generic DFT (the CPU baseline of the plug-in).
+std::unique_ptr<ofdm_slot_modulator>   make_ref_ofdm_slot_modulator(const ofdm_modulator_configuration& cfg);
+std::unique_ptr<ofdm_slot_demodulator> make_ref_ofdm_slot_demodulator(const ofdm_demodulator_configuration& cfg);
 int pusch_demodulate_with(std::unique_ptr<channel_equalizer> eq_impl, const uint32_t* grid, unsigned nof_rx_ports,
                           unsigned nsubc, const uint32_t* estimates, unsigned nof_layers, const float* noise_vars,
                           unsigned rnti, unsigned n_id, int qm, const uint8_t* crbs, unsigned start_symbol,

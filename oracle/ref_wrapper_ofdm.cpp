@@ -199,6 +199,55 @@ int srs_ref::ofdm_demodulate_slot_with(std::unique_ptr<dft_processor> dft,
   return 0;
 }
 
+void srs_ref::ofdm_run_slot_modulator(ofdm_slot_modulator& mod, unsigned nsymb, unsigned nsubc, unsigned slot,
+                                      const uint16_t* grid, float* out)
+{
+  dense_grid_reader rd(reinterpret_cast<const cbf16_t*>(grid), nsymb, nsubc);
+  mod.modulate(span<cf_t>(reinterpret_cast<cf_t*>(out), mod.get_slot_size(slot)), rd, 0, slot);
+}
+
+void srs_ref::ofdm_run_symbol_modulator(ofdm_symbol_modulator& mod, unsigned nsymb, unsigned nsubc, unsigned slot,
+                                        const uint16_t* grid, float* out)
+{
+  dense_grid_reader rd(reinterpret_cast<const cbf16_t*>(grid), nsymb, nsubc);
+  cf_t*             o = reinterpret_cast<cf_t*>(out);
+  for (unsigned l = 0; l != nsymb; ++l) {
+    const unsigned n = mod.get_symbol_size(nsymb * slot + l);
+    mod.modulate(span<cf_t>(o, n), rd, 0, nsymb * slot + l);
+    o += n;
+  }
+}
+
+void srs_ref::ofdm_run_slot_demodulator(ofdm_slot_demodulator& dem, unsigned nsymb, unsigned nsubc, unsigned slot,
+                                        const float* in, uint16_t* grid)
+{
+  dense_grid_writer wr(reinterpret_cast<cbf16_t*>(grid), nsymb, nsubc);
+  dem.demodulate(wr, span<const cf_t>(reinterpret_cast<const cf_t*>(in), dem.get_slot_size(slot)), 0, slot);
+}
+
+void srs_ref::ofdm_run_symbol_demodulator(ofdm_symbol_demodulator& dem, unsigned nsymb, unsigned nsubc, unsigned slot,
+                                          const float* in, uint16_t* grid)
+{
+  dense_grid_writer wr(reinterpret_cast<cbf16_t*>(grid), nsymb, nsubc);
+  const cf_t*       x = reinterpret_cast<const cf_t*>(in);
+  for (unsigned l = 0; l != nsymb; ++l) {
+    const unsigned n = dem.get_symbol_size(nsymb * slot + l);
+    dem.demodulate(wr, span<const cf_t>(x, n), 0, nsymb * slot + l);
+    x += n;
+  }
+}
+
+std::unique_ptr<ofdm_slot_modulator> srs_ref::make_ref_ofdm_slot_modulator(const ofdm_modulator_configuration& c)
+{
+  return make_modulator(c.numerology, c.bw_rb, c.dft_size, c.cp == cyclic_prefix::EXTENDED, c.scale, c.center_freq_Hz);
+}
+
+std::unique_ptr<ofdm_slot_demodulator> srs_ref::make_ref_ofdm_slot_demodulator(const ofdm_demodulator_configuration& c)
+{
+  return make_demodulator(c.numerology, c.bw_rb, c.dft_size, c.cp == cyclic_prefix::EXTENDED,
+                          c.nof_samples_window_offset, c.scale, c.center_freq_Hz);
+}
+
 extern "C" {
 
 // One dft_processor::run() of the reference generic DFT: in/out interleaved complex float.

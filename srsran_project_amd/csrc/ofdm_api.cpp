@@ -152,6 +152,7 @@ struct srs_amd_ofdm_engine {
   srs_amd_ofdm_config cfg{};
   ofdm_geometry       geo;
   ofdm_symbol_info*   d_symbols  = nullptr;
+  ofdm_symbol_info*   d_symbols0 = nullptr; // the same with every offset 0 (symbol forms)
   float*              d_twiddles = nullptr;
   float*              d_window   = nullptr;
   hipStream_t         stream     = nullptr;
@@ -166,6 +167,7 @@ struct srs_amd_ofdm_engine {
       (void)hipStreamDestroy(stream);
     }
     (void)hipFree(d_symbols);
+    (void)hipFree(d_symbols0);
     (void)hipFree(d_twiddles);
     (void)hipFree(d_window);
   }
@@ -185,6 +187,9 @@ struct srs_amd_ofdm_engine {
     cfg          = *c;
     hipError_t e = upload(&d_symbols, geo.symbols);
     if (e == hipSuccess) {
+      e = upload(&d_symbols0, symbols0());
+    }
+    if (e == hipSuccess) {
       e = upload(&d_twiddles, twiddle_table(geo.N));
     }
     if (e == hipSuccess && !tx && c->nof_samples_window_offset != 0) {
@@ -203,6 +208,93 @@ struct srs_amd_ofdm_engine {
       e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
     }
     return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "OFDM tables");
+  }
+
+  std::vector<ofdm_symbol_info> symbols0() const
+  {
+    std::vector<ofdm_symbol_info> s = geo.symbols;
+    for (ofdm_symbol_info& x : s) {
+      x.offset = 0;
+    }
+    return s;
+  }
+
+  // New phase compensation tables (same host arithmetic as the constructor), in stream order with the launches.
+  int set_center_frequency(double hz)
+  {
+    srs_amd_ofdm_config c = cfg;
+    c.center_freq_hz      = hz;
+    ofdm_geometry g;
+    int           rc = make_geometry(g, &c, is_tx);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+    std::lock_guard<std::mutex> lock(mtx);
+    hipError_t                  e = hipSetDevice(device);
+    if (e == hipSuccess) {
+      e = hipStreamSynchronize(stream); // no launch of this engine still reads the old tables
+    }
+    geo = g;
+    cfg = c;
+    if (e == hipSuccess) {
+      e = hipMemcpy(d_symbols, geo.symbols.data(), geo.symbols.size() * sizeof(ofdm_symbol_info), hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess) {
+      const std::vector<ofdm_symbol_info> s0 = symbols0();
+      e = hipMemcpy(d_symbols0, s0.data(), s0.size() * sizeof(ofdm_symbol_info), hipMemcpyHostToDevice);
+    }
+    return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "OFDM phase compensation tables");
+  }
+
+  // One symbol (index within the subframe) of one port: host buffers, synchronous.
+  int run_symbol(void* host_out, const void* host_in, uint32_t symbol_index)
+  {
+    const uint32_t nsym_sf = geo.nsymb * geo.slots_per_subframe;
+    if (symbol_index >= nsym_sf) {
+      return fail(SRS_AMD_EINVAL, "Symbol index %u exceeds the %u symbols of a subframe.", symbol_index, nsym_sf);
+    }
+    const ofdm_symbol_info& si     = geo.symbols[symbol_index];
+    const size_t            gbytes = static_cast<size_t>(geo.rg) * 4;
+    const size_t            sbytes = static_cast<size_t>(si.cp_len + geo.N) * 8;
+    std::lock_guard<std::mutex> lock(mtx);
+    hipError_t                  e = hipSetDevice(device);
+    if (e == hipSuccess) {
+      e = scratch.ensure(gbytes + sbytes);
+    }
+    auto* grid = static_cast<uint8_t*>(scratch.ptr);
+    auto* samp = grid + gbytes;
+    ofdm_args a{};
+    a.symbols            = d_symbols0 + symbol_index;
+    a.twiddles           = d_twiddles;
+    a.window             = d_window;
+    a.rg_size            = geo.rg;
+    a.nsymb              = 1;
+    a.nof_ports          = 1;
+    a.first_slot         = 0;
+    a.slots_per_subframe = 1;
+    a.nof_items          = 1;
+    a.sample_stride      = si.cp_len + geo.N;
+    a.window_offset      = is_tx ? 0 : cfg.nof_samples_window_offset;
+    a.in                 = is_tx ? static_cast<const void*>(grid) : static_cast<const void*>(samp);
+    a.out                = is_tx ? static_cast<void*>(samp) : static_cast<void*>(grid);
+    if (e == hipSuccess) {
+      e = hipMemcpyAsync(is_tx ? grid : samp, host_in, is_tx ? gbytes : sbytes, hipMemcpyHostToDevice, stream);
+    }
+    if (e == hipSuccess) {
+      e = is_tx ? launch_ofdm_modulate(a, geo.N, stream) : launch_ofdm_demodulate(a, geo.N, stream);
+    }
+    if (e == hipSuccess) {
+      e = hipMemcpyAsync(host_out, is_tx ? samp : grid, is_tx ? sbytes : gbytes, hipMemcpyDeviceToHost, stream);
+    }
+    if (e == hipSuccess) {
+      e = hipStreamSynchronize(stream);
+    }
+    return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, is_tx ? "ofdm modulate symbol" : "ofdm demodulate symbol");
+  }
+
+  uint32_t symbol_size(uint32_t symbol_index) const
+  {
+    return symbol_index < geo.symbols.size() ? geo.symbols[symbol_index].cp_len + geo.N : 0;
   }
 
   ofdm_args args(uint32_t nof_ports, uint32_t first_slot, uint32_t nof_slots, uint32_t stride) const
@@ -365,6 +457,54 @@ int srs_amd_ofdm_modulate_slot(srs_amd_ofdm_modulator* mod, float* output, const
     e = hipStreamSynchronize(mod->stream);
   }
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ofdm modulate");
+}
+
+uint32_t srs_amd_ofdm_modulator_get_symbol_size(const srs_amd_ofdm_modulator* mod, uint32_t symbol_index)
+{
+  return mod == nullptr ? 0 : mod->symbol_size(symbol_index);
+}
+
+int srs_amd_ofdm_modulator_set_center_frequency(srs_amd_ofdm_modulator* mod, double center_freq_hz)
+{
+  if (mod == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null modulator");
+  }
+  return mod->set_center_frequency(center_freq_hz);
+}
+
+int srs_amd_ofdm_modulate_symbol(srs_amd_ofdm_modulator* mod,
+                                 float*                  output,
+                                 const uint16_t*         grid_symbol,
+                                 uint32_t                symbol_index)
+{
+  if (mod == nullptr || output == nullptr || grid_symbol == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  return mod->run_symbol(output, grid_symbol, symbol_index);
+}
+
+uint32_t srs_amd_ofdm_demodulator_get_symbol_size(const srs_amd_ofdm_demodulator* dem, uint32_t symbol_index)
+{
+  return dem == nullptr ? 0 : dem->symbol_size(symbol_index);
+}
+
+int srs_amd_ofdm_demodulator_set_center_frequency(srs_amd_ofdm_demodulator* dem, double center_freq_hz)
+{
+  if (dem == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null demodulator");
+  }
+  return dem->set_center_frequency(center_freq_hz);
+}
+
+int srs_amd_ofdm_demodulate_symbol(srs_amd_ofdm_demodulator* dem,
+                                   uint16_t*                 grid_symbol,
+                                   const float*              input,
+                                   uint32_t                  symbol_index)
+{
+  if (dem == nullptr || grid_symbol == nullptr || input == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  return dem->run_symbol(grid_symbol, input, symbol_index);
 }
 
 int srs_amd_ofdm_demodulator_create(srs_amd_ofdm_demodulator** dem, const srs_amd_ofdm_config* cfg, int device)

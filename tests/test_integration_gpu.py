@@ -219,6 +219,69 @@ def test_dft_adapter_through_ofdm_modulator(hw, case):
         assert (gg == gw).mean() >= 0.99, (case, (gg == gw).mean())
 
 
+# (numerology, PRBs, DFT size, extended CP, window offset, scale, fc, fc after set_center_frequency)
+OFDM_PLUGIN_CASES = [(1, 273, 4096, False, 0, 1.0, 3.5e9, 3.6e9), (0, 52, 1024, False, 36, 0.5, 1.8e9, 1.8e9),
+                     (2, 66, 1024, True, 20, 0.8, 28e9, 27.5e9), (1, 106, 1536, False, 0, 0.7, 2.6e9, 2.6e9)]
+
+
+def _assert_grids_close(gg, gw, case):
+    a = (gg.view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+    b = (gw.view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+    tol = 2.0 ** -7 * np.maximum(np.abs(a), np.abs(b)) + 3e-5 * np.sqrt(np.mean(b ** 2))
+    assert (np.abs(a - b) <= tol).all(), case
+    assert (gg.view(np.uint32) == gw.view(np.uint32)).mean() >= 0.99, case
+
+
+@pytest.mark.parametrize("case", OFDM_PLUGIN_CASES)
+def test_ofdm_factory_plugins_vs_reference(hw, case):
+    """The ofdm_modulator_factory / ofdm_demodulator_factory plug-ins (integration/ofdm_modulator_hip.h: whole-slot
+    launches for ofdm_slot_*, one launch per symbol for ofdm_symbol_*, set_center_frequency on the symbol forms)
+    against the reference's ofdm_slot_(de)modulator_impl over the generic DFT built for the same center frequency:
+    samples within 2e-5 x RMS, grids within one bf16 ulp (+ 3e-5 x RMS near zero) and >= 99 % identical; an
+    extended-CP (12 symbols) and a window-offset case included."""
+    from oracle import ofdm as oofdm
+
+    ohw, _ = hw
+    mu, bw, N, ext, off, scale, fc, fc2 = case
+    ns = 12 if ext else 14
+    rng = np.random.default_rng(N + bw + off)
+    for slot in (0, (1 << mu) - 1):
+        g = oofdm.random_grid(rng, ns, bw * 12)
+        for mode, f in (("slot_mod", fc), ("symbol_mod", fc2)):
+            want = oracle.ref_ofdm_modulate_slot(g, slot, mu, bw, N, scale, f, extended_cp=ext)
+            got = ohw.ofdm_plugin(mode, g, slot, mu, bw, N, scale, fc, fc2=fc2, extended_cp=ext, n=want.size)
+            rms = float(np.sqrt(np.mean(np.abs(want) ** 2)))
+            assert np.max(np.abs(got - want)) <= 2e-5 * rms, (case, slot, mode, np.max(np.abs(got - want)) / rms)
+        rx = (want + (rng.normal(0, 0.05, want.size) + 1j * rng.normal(0, 0.05, want.size)) * rms).astype(np.complex64)
+        for mode, f in (("slot_demod", fc), ("symbol_demod", fc2)):
+            gw = oracle.ref_ofdm_demodulate_slot(rx, slot, mu, bw, N, scale, f, window_offset=off, extended_cp=ext)
+            gg = ohw.ofdm_plugin(mode, rx, slot, mu, bw, N, scale, fc, fc2=fc2, extended_cp=ext, window_offset=off)
+            _assert_grids_close(gg, gw, (case, slot, mode))
+
+
+def test_ofdm_factory_plugin_throughput(hw):
+    """Symbols/s of the slot plug-ins (synchronous per (port, slot) call, as the interface is) beside the reference's
+    ofdm_slot_(de)modulator_impl over the generic DFT on one host core, 100 MHz / 4096-point slots; written to
+    gpurun_out/ofdm_plugin_bench.json."""
+    import json
+    import os
+
+    ohw, _ = hw
+    out = {}
+    for demod in (False, True):
+        name = "demodulator" if demod else "modulator"
+        ohw.ofdm_bench(True, demod, 1, 273, 4096, 20)  # warm-up
+        t_gpu = ohw.ofdm_bench(True, demod, 1, 273, 4096, 400)
+        t_cpu = ohw.ofdm_bench(False, demod, 1, 273, 4096, 20)
+        assert t_gpu > 0 and t_cpu > 0
+        out[name] = {"plugin_symbols_per_s": 400 * 14 / t_gpu, "reference_1core_symbols_per_s": 20 * 14 / t_cpu,
+                     "plugin_us_per_slot": 1e6 * t_gpu / 400, "reference_us_per_slot": 1e6 * t_cpu / 20}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/ofdm_plugin_bench.json", "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(out)
+
+
 @pytest.mark.parametrize("ci", range(len(DEMOD_CASES)))
 def test_equalizer_adapter_through_pusch_demodulator(hw, ci):
     """pusch_demodulator_impl (pusch_demodulator_impl.cpp:203-445) built with the MI355X channel_equalizer instead of
