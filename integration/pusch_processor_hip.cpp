@@ -606,14 +606,21 @@ private:
     dr.tb_crc_ok            = r.data.tb_crc_ok != 0;
     dr.nof_codeblocks_total = e.nof_cbs;
     dr.ldpc_decoder_stats.reset();
-    cb_stat_array& cs = *p.cb_stats;
+    cb_stat_array& cs     = *p.cb_stats;
+    bool           all_ok = true; // every codeblock CRC passed (now or in an earlier transmission)
     for (unsigned cb = 0; cb != e.nof_cbs && cb < MAX_CB; ++cb) {
-      if (cb >= prev.size() || !prev[cb]) {
+      const bool earlier = cb < prev.size() && prev[cb];
+      if (!earlier) {
         cs[cb] = cb_it[cb] >= 0 ? static_cast<unsigned>(cb_it[cb]) : cfg.dec_nof_iterations;
       }
+      all_ok = all_ok && (earlier || cb_it[cb] >= 0);
       dr.ldpc_decoder_stats.update(cs[cb]);
     }
-    std::memcpy(p.data.data(), tb, p.data.size());
+    // the transport block is written only once every codeblock CRC passed (pusch_decoder_impl.cpp:409-440: the
+    // single codeblock's data, or the concatenation); otherwise the caller's buffer is left as it was
+    if (all_ok) {
+      std::memcpy(p.data.data(), tb, p.data.size());
+    }
     if (p.rm_buffer.is_valid()) {
       if (dr.tb_crc_ok) {
         p.rm_buffer.release();

@@ -155,7 +155,9 @@ __global__ __launch_bounds__(PE_THREADS) void pdsch_cb_kernel(pdsch_fused_args a
         tb_crc ^= a.tb_parts[static_cast<size_t>(t) * a.part_stride + i];
       }
     }
-    const uint8_t* tb = a.tbs + d.tb_offset;
+    // (a plan may count the TB CRC outside cb_info_bits, pdsch_encoder_hw_impl's single segment: bits up to the CRC)
+    const uint32_t seg_end = last ? n_data + d.tb_crc_bits : n_data;
+    const uint8_t* tb      = a.tbs + d.tb_offset;
     const uint32_t ob = r * cbi; // first TB bit of the segment
     __syncthreads(); // s_cw / lw of the previous codeblock are no longer read
     for (uint32_t q = j; q < (nmb + 3) / 4; q += PE_THREADS) {
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(PE_THREADS) void pdsch_cb_kernel(pdsch_fused_args a
             x |= tb[(p >> 3) + 1];
           }
           v = (x >> (8 - sh)) & 0xffu;
-        } else if (8 * jb < cbi) {
+        } else if (8 * jb < seg_end) {
 #pragma unroll
           for (uint32_t k = 0; k < 8; ++k) {
             const uint32_t p = 8 * jb + k;

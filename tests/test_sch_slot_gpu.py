@@ -317,7 +317,7 @@ def test_small_z_codeblock_stages(enc, case):
     got1 = e1.encode(msg, cfg)
     d = np.flatnonzero(got1[:want_cb.size] != want_cb)
     assert d.size == 0, "single encoder Z %d: %s" % (Z, d[:8].tolist())
-    gotb = e1.encode_batch(torch.from_numpy(np.packbits(msg)[None]).cuda(), cfg).cpu().numpy()
+    gotb = e1.encode_batch(torch.from_numpy(np.packbits(msg)).cuda().reshape(1, -1).contiguous(), cfg).cpu().numpy()
     d = np.flatnonzero(np.unpackbits(gotb[0])[:want_cb.size] != want_cb)
     assert d.size == 0, "batch encoder Z %d: %s" % (Z, d[:8].tolist())
     want = osch.unpack_bits(oracle.rate_match(want_cb, 1, Z, 0, qm, E, 0, F), E)
@@ -326,7 +326,7 @@ def test_small_z_codeblock_stages(enc, case):
     got = np.unpackbits(rm.rate_match(E, want_cb, meta))[:E]
     d = np.flatnonzero(got != want)
     assert d.size == 0, "single rate matcher Z %d F %d E %d: %s" % (Z, F, E, d[:8].tolist())
-    got = np.unpackbits(rm.rate_match_batch(torch.from_numpy(np.packbits(want_cb)[None]).cuda(), [E], meta)
+    got = np.unpackbits(rm.rate_match_batch(torch.from_numpy(np.packbits(want_cb)).cuda().reshape(1, -1).contiguous(), [E], meta)
                         .cpu().numpy())[:E]
     d = np.flatnonzero(got != want)
     assert d.size == 0, "batch rate matcher Z %d F %d E %d: %s" % (Z, F, E, d[:8].tolist())
