@@ -92,6 +92,8 @@ def parse():
                    help="pipeline: skip the reference-pinned sibling line (PUSCH 2 layers x 4 rx, ZF)")
     p.add_argument("--no-latency", action="store_true",
                    help="pipeline: skip the 1 / 8 cell latency figures; sch_slot: skip the per-UE launch timing")
+    p.add_argument("--graph", action="store_true",
+                   help="pipeline: replay each step as a HIP graph captured once (both streams, every launch)")
     p.add_argument("--ues-per-cell", type=int, default=8, help="sch_slot: UEs sharing each cell's 273 PRBs")
     return p.parse_args()
 

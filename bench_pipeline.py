@@ -24,6 +24,7 @@ data-path collective). With `--ingest`, rank 0 also holds the slot inputs of all
 cells and fans them out / gathers the decoded TBs over RCCL every step
 (srsran_project_amd/cell_fanout.py); that time is reported separately.
 """
+import sys
 import time
 
 import numpy as np
@@ -224,6 +225,31 @@ class Pipeline:
         self.ev_join.record(self.ul_stream)
         stream.wait_event(self.ev_join)
 
+    def graph(self, stream):
+        """The step (both chains, every C-ABI launch of both streams) captured once as a HIP graph on `stream` (a
+        non-default stream) after two warm-up steps, so scratch buffers are sized and the uniform-batch descriptors
+        cached: each replay is one graph launch instead of ~20 kernel launches.  Returns the replay callable (it
+        launches on `stream`), or None when the capture is refused (the step then runs eagerly)."""
+        t = self.torch
+        for _ in range(2):
+            self.step(stream)
+        t.cuda.synchronize(self.dev)
+        g = t.cuda.CUDAGraph()
+        try:
+            with t.cuda.graph(g, stream=stream):
+                self.step(stream)
+        except Exception as exc:  # noqa: BLE001 -- report and run eagerly
+            print("HIP graph capture refused: %s" % exc, file=sys.stderr)
+            t.cuda.synchronize(self.dev)
+            return None
+        t.cuda.synchronize(self.dev)
+        self._graph = g  # keep the graph (and its captured memory) alive
+
+        def replay():
+            with t.cuda.stream(stream):
+                g.replay()
+        return replay
+
     def results(self):
         import srsran_project_amd as amd
 
@@ -317,19 +343,22 @@ def chain_config(pl, choice="auto"):
                           ul_target_code_rate=RATE, choice={"generic": 0, "avx2": 1, "auto": 2}[choice])
 
 
-def latency_ms(dev, cells, steps=10, warmup=3, **shape):
-    """Wall time of one step (both chains of `cells` cells) measured step by step (synchronized each step)."""
+def latency_ms(dev, cells, steps=10, warmup=3, graph=False, **shape):
+    """Wall time of one step (both chains of `cells` cells) measured step by step (synchronized each step); graph:
+    each step a replay of the HIP graph captured once (Pipeline.graph)."""
     import torch
 
     pl = Pipeline(cells, dev, **shape)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev) if graph else torch.cuda.current_stream(dev)
+    run = pl.graph(stream) if graph else None
+    run = run or (lambda: pl.step(stream))
     for _ in range(warmup):
-        pl.step(stream)
+        run()
     torch.cuda.synchronize(dev)
     ts = []
     for _ in range(steps):
         t0 = time.perf_counter()
-        pl.step(stream)
+        run()
         torch.cuda.synchronize(dev)
         ts.append((time.perf_counter() - t0) * 1e3)
     return float(np.median(ts))
@@ -365,7 +394,12 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         el_compute, _ = timed(args, dist, world, dev, stream, lambda: pl.step(stream))
         ingest_ms = (elapsed - el_compute) / args.steps * 1e3
     else:
-        elapsed, step_ms = timed(args, dist, world, dev, stream, lambda: pl.step(stream))
+        run = None
+        if getattr(args, "graph", False) and dev.type == "cuda":
+            stream = torch.cuda.Stream(dev)
+            run = pl.graph(stream)
+        run = run or (lambda: pl.step(stream))
+        elapsed, step_ms = timed(args, dist, world, dev, stream, run)
     ok_frac, its_mean = pl.check()
     stages = pl.stage_ms(stream)
     cbs_dl, cbs_ul = pl.plan_dl.nof_segments, pl.plan_ul.nof_segments
@@ -398,7 +432,9 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         return None
     lat = None
     if world == 1 and not args.no_latency:
-        lat = {"1_cell": latency_ms(dev, 1, **shape_kw(args)), "8_cells": latency_ms(dev, 8, **shape_kw(args))}
+        lat = {"1_cell": latency_ms(dev, 1, **shape_kw(args)), "8_cells": latency_ms(dev, 8, **shape_kw(args)),
+               "1_cell_graph": latency_ms(dev, 1, graph=True, **shape_kw(args)),
+               "8_cells_graph": latency_ms(dev, 8, graph=True, **shape_kw(args))}
     low = None
     if args.low_snr_db is None:
         args.low_snr_db = LOW_SNR_DB.get((L, pl.ul_ports), -1.0)
@@ -449,6 +485,7 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         "stage_ms": stages,
         "stage_gbs": gbs,
         "latency_ms": lat,
+        "hip_graph": bool(getattr(args, "graph", False)),
         "ingest_ms_per_step": ingest_ms,
         "low_snr": low,
         "pinned_sibling": pinned,

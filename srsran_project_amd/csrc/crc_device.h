@@ -120,18 +120,68 @@ __device__ __forceinline__ uint32_t crc_chunk_contrib(const Fetch&    fetch,
 }
 
 // R(x) x^d mod g for a remainder R of degree < order: bit j moves to x^(j + d), reduced through the linear
-// table (table[k] = x^(k + order) mod g) when j + d >= order.
+// table (table[k] = x^(k + order) mod g) when j + d >= order.  Branch-free: the table words of every bit position
+// are loaded unconditionally (all in flight together, one memory latency) and masked by the bits of R.
 __device__ __forceinline__ uint32_t crc_move(uint32_t R, uint32_t d, uint32_t order, const uint32_t* table)
 {
   uint32_t out = 0;
 #pragma unroll
   for (uint32_t j = 0; j < CRC_MAX_ORDER; ++j) {
-    if (j < order && ((R >> j) & 1u)) {
-      const uint32_t k = j + d;
-      out ^= k < order ? (1u << k) : table[k - order];
-    }
+    const uint32_t k    = j + d;
+    const uint32_t word = k >= order ? table[k - order] : 0u;
+    const uint32_t v    = k < order ? (1u << (k & 31u)) : word;
+    out ^= (j < order) ? (v & (0u - ((R >> j) & 1u))) : 0u;
   }
   return out;
+}
+
+// The remainder M(x) mod g of the message bytes [b0, b1) alone (byte j = fetch(j), MSB first, every byte whole),
+// by the byte table T (crc_table8_init; order >= 8).
+template <typename Fetch>
+__device__ __forceinline__ uint32_t crc_chunk_rem(const Fetch& fetch, uint32_t b0, uint32_t b1, uint32_t order,
+                                                  const uint32_t* T)
+{
+  const uint32_t mask = (1u << order) - 1u;
+  const uint32_t sh   = order - 8;
+  uint32_t       r    = 0;
+  for (uint32_t b = b0; b < b1; b += CRC_FETCH_BATCH) {
+    uint32_t v[CRC_FETCH_BATCH];
+#pragma unroll
+    for (uint32_t k = 0; k < CRC_FETCH_BATCH; ++k) {
+      v[k] = b + k < b1 ? fetch(b + k) : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < CRC_FETCH_BATCH; ++k) {
+      if (b + k < b1) {
+        r = T[r >> sh] ^ ((r << 8) & mask) ^ v[k];
+      }
+    }
+  }
+  return r;
+}
+
+// a(x) c(x) mod g for a, c of degree < order (GF(2) multiplication, the reduction folded into the shifts of c);
+// polynom includes the x^order term (crc_params).
+__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t c, uint32_t order, uint32_t polynom)
+{
+  const uint32_t mask = (1u << order) - 1u;
+  const uint32_t top  = 1u << (order - 1);
+  uint32_t       r    = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < CRC_MAX_ORDER; ++i) {
+    if (i < order) {
+      r ^= c & (0u - ((a >> i) & 1u));
+      const uint32_t hi = c & top;
+      c                 = ((c << 1) & mask) ^ (hi ? (polynom & mask) : 0u);
+    }
+  }
+  return r;
+}
+
+// x^m mod g from the linear table (table[k] = x^(k + order) mod g).
+__device__ __forceinline__ uint32_t crc_xpow(uint32_t m, uint32_t order, const uint32_t* table)
+{
+  return m < order ? (1u << m) : table[m - order];
 }
 
 // XOR of v over the block (result to all threads). `partial`: __shared__, THREADS / 64 words.

@@ -1,10 +1,11 @@
 // pdsch_api.cpp -- C-ABI of the MI355X PDSCH encoder (include/srsran_amd/sch.h),
 // pdsch_encoder_impl::encode (lib/phy/upper/channel_processors/pdsch/pdsch_encoder_impl.cpp:28-80)
 // for a batch of transport blocks (srs_amd_pdsch_encode_batch) or a slot of heterogeneous ones
-// (srs_amd_pdsch_encode_slot), both through the fused two-launch chain of pdsch_encoder.hip:
-//   1. TB CRC (CRC16 / CRC24A) partials          pdsch_tb_crc_kernel
-//   2. segmentation, CB CRC24B, LDPC encoding,   pdsch_cb_kernel, one workgroup per codeblock
-//      rate matching + concatenation
+// (srs_amd_pdsch_encode_slot), both through the fused chain of pdsch_encoder.hip:
+//   1. TB CRC (CRC16 / CRC24A) partials           pdsch_tb_crc_kernel   } concurrently (two helper streams)
+//   2. segmentation, CB CRC24B, LDPC encoding,    pdsch_cb_kernel       } over every codeblock but the TBs' last
+//      rate matching + concatenation                                   }
+//   3. the TBs' last codeblocks (TB CRC attached) pdsch_cb_kernel
 // SRSRAN_AMD_PDSCH_FUSED=0 (read per call) selects the previous five-stage chain instead (TB CRC, segmentation
 // + CB CRC, srs_amd_ldpc_encode_batch, srs_amd_ldpc_rate_match_batch), kept for A/B timing and cross-checks.
 #include "srsran_amd/crc.h"
@@ -23,6 +24,7 @@
 #include "rate_matching_common.h"
 #include "sch_args.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -98,7 +100,7 @@ struct fused_rows {
 };
 
 struct fused_layout {
-  size_t o_E, o_out, o_geo, o_tb, o_G, o_TD, o_ER, total;
+  size_t o_E, o_out, o_geo, o_tb, o_G, o_TD, o_ER, o_LR, total;
   explicit fused_layout(const fused_rows& f)
   {
     const size_t R = f.row_E.size();
@@ -109,7 +111,8 @@ struct fused_layout {
     o_G            = o_tb + align_up(sizeof(uint32_t) * R, 16);
     o_TD           = o_G + align_up(sizeof(rm_geometry) * f.geos.size(), 16);
     o_ER           = o_TD + align_up(sizeof(tb_desc) * f.tds.size(), 16);
-    total          = o_ER + sizeof(enc_row_desc) * R;
+    o_LR           = o_ER + align_up(sizeof(enc_row_desc) * R, 16);
+    total          = o_LR + sizeof(uint32_t) * f.tds.size();
   }
 };
 
@@ -153,7 +156,8 @@ int fused_launch_locked(srs_amd_pdsch_encoder* e,
                         bool                   upload,
                         const uint8_t*         d_tbs,
                         uint8_t*               d_cw,
-                        hipStream_t            stream)
+                        hipStream_t            stream,
+                        bool                   overlap)
 {
   static const auto row_starts = [] {
     std::vector<int32_t> rs(2 * 47, 0);
@@ -165,14 +169,14 @@ int fused_launch_locked(srs_amd_pdsch_encoder* e,
     return rs;
   }();
   const fused_layout L(f);
-  const uint32_t     U           = static_cast<uint32_t>(f.tds.size());
-  const uint32_t     R           = static_cast<uint32_t>(f.row_E.size());
+  const uint32_t     U  = static_cast<uint32_t>(f.tds.size());
+  const uint32_t     R  = static_cast<uint32_t>(f.row_E.size());
   const uint32_t     part_stride = std::max(1u, (f.max_tb_bytes + PE_TB_CHUNK - 1) / PE_TB_CHUNK);
   hipError_t         he          = e->tb_parts.ensure(sizeof(uint32_t) * U * part_stride);
   if (he != hipSuccess) {
     return hip_fail(he, "PDSCH encoder TB CRC partials");
   }
-  call_scope scope(e->order, nullptr, stream);
+  call_scope scope(e->order, &e->fan, stream);
   he = e->order.begin(stream);
   if (he == hipSuccess && upload) {
     // the pinned staging buffer is rewritten only once its previous upload completed
@@ -200,6 +204,10 @@ int fused_launch_locked(srs_amd_pdsch_encoder* e,
       std::memcpy(h + L.o_G, f.geos.data(), sizeof(rm_geometry) * f.geos.size());
       std::memcpy(h + L.o_TD, f.tds.data(), sizeof(tb_desc) * U);
       std::memcpy(h + L.o_ER, f.enc.data(), sizeof(enc_row_desc) * R);
+      auto* lr = reinterpret_cast<uint32_t*>(h + L.o_LR);
+      for (uint32_t t = 0; t < U; ++t) {
+        lr[t] = f.tds[t].row0 + f.tds[t].nof_segments - 1;
+      }
       he = hipMemcpyAsync(dd, h, L.total, hipMemcpyHostToDevice, stream);
     }
     if (he == hipSuccess) {
@@ -219,9 +227,11 @@ int fused_launch_locked(srs_amd_pdsch_encoder* e,
   a.row_geo      = reinterpret_cast<const uint32_t*>(dd + L.o_geo);
   a.geos         = reinterpret_cast<const rm_geometry*>(dd + L.o_G);
   a.enc_rows     = reinterpret_cast<const enc_row_desc*>(dd + L.o_ER);
+  a.last_rows    = reinterpret_cast<const uint32_t*>(dd + L.o_LR);
   a.edges        = ldpc_encoder_edges(e->enc);
   a.tb_parts     = e->tb_parts.as<uint32_t>();
   a.part_stride  = part_stride;
+  a.max_tb_bytes = f.max_tb_bytes;
   a.crc16_table  = crc_device_table(e->crc16);
   a.crc24a_table = crc_device_table(e->crc24a);
   a.crc24b_table = crc_device_table(e->crc24b);
@@ -231,10 +241,23 @@ int fused_launch_locked(srs_amd_pdsch_encoder* e,
   a.cw           = d_cw;
   a.nof_tbs      = U;
   a.nof_cbs      = R;
-  a.max_tb_bytes = f.max_tb_bytes;
   std::copy(row_starts.begin(), row_starts.begin() + 47, a.row_start[0]);
   std::copy(row_starts.begin() + 47, row_starts.end(), a.row_start[1]);
-  he = launch_pdsch_fused(a, stream);
+  if (overlap) {
+    // TB CRC partials || codeblocks without a TB CRC, then the TBs' last codeblocks
+    he = e->fan.begin(stream, 2);
+    if (he == hipSuccess) {
+      he = launch_pdsch_fused(a, e->fan.stream(stream, 0), e->fan.stream(stream, 1), stream, 0);
+    }
+    if (he == hipSuccess) {
+      he = e->fan.end(stream);
+    }
+    if (he == hipSuccess) {
+      he = launch_pdsch_fused(a, stream, stream, stream, 1);
+    }
+  } else {
+    he = launch_pdsch_fused(a, stream, stream, stream, 2);
+  }
   if (he == hipSuccess) {
     he = scope.close();
   }
@@ -278,7 +301,9 @@ int encode_fused_batch_locked(srs_amd_pdsch_encoder* e,
     return hip_fail(he, "PDSCH encoder descriptors");
   }
   e->batch_key.clear();
-  int rc = fused_launch_locked(e, f, e->batch_desc.as<uint8_t>(), upload, d_tbs, d_cw, stream);
+  // a uniform batch of segmented TBs: the TB CRC runs beside the codeblocks that do not carry it
+  int rc = fused_launch_locked(e, f, e->batch_desc.as<uint8_t>(), upload, d_tbs, d_cw, stream,
+                               f.row_E.size() >= 4 * f.tds.size());
   if (rc == SRS_AMD_OK) {
     e->batch_key = std::move(key);
   }
@@ -331,7 +356,8 @@ int encode_fused_slot_locked(srs_amd_pdsch_encoder*  e,
   if (he != hipSuccess) {
     return hip_fail(he, "PDSCH slot encoder descriptors");
   }
-  return fused_launch_locked(e, f, e->slot_desc.as<uint8_t>(), true, d_tbs, d_cw, stream);
+  // heterogeneous slots (many single-codeblock TBs): one stream, TB CRC partials then every codeblock
+  return fused_launch_locked(e, f, e->slot_desc.as<uint8_t>(), true, d_tbs, d_cw, stream, false);
 }
 
 int encode_locked(srs_amd_pdsch_encoder* e,

@@ -76,9 +76,8 @@ struct tx_slot_args {
 };
 hipError_t launch_tx_slot_segment(const tx_slot_args& a, hipStream_t stream);
 
-// Fused PDSCH encoder (pdsch_encoder.hip): launch 1 computes the TB CRC partials (one per PE_TB_CHUNK bytes of a
-// TB, moved to the TB end) and zeroes the codeword bytes two segments share; launch 2 builds, CRC-attaches,
-// LDPC-encodes and rate-matches one codeblock per workgroup, the codeblock never leaving LDS.
+// Fused PDSCH encoder (pdsch_encoder.hip): TB CRC partials, then one workgroup per codeblock that builds,
+// CRC-attaches, LDPC-encodes and rate-matches its codeblock in LDS.
 struct pdsch_fused_args {
   const uint8_t*                 tbs;      // TB bytes (tds[t].tb_offset)
   const tb_desc*                 tds;      // per TB
@@ -89,8 +88,9 @@ struct pdsch_fused_args {
   const struct rm_geometry*      geos;
   const struct enc_row_desc*     enc_rows; // per codeblock: lifted graph, encoded window
   const uint32_t*                edges;    // every lifted graph (enc_row_desc::edge_off)
-  uint32_t*                      tb_parts; // [nof_tbs][part_stride] TB CRC partials
+  uint32_t*                      tb_parts; // [nof_tbs][part_stride] TB CRC partials (pdsch_tb_crc_kernel)
   uint32_t                       part_stride;
+  uint32_t                       max_tb_bytes;
   const uint32_t*                crc16_table;
   const uint32_t*                crc24a_table;
   const uint32_t*                crc24b_table;
@@ -98,11 +98,15 @@ struct pdsch_fused_args {
   uint8_t*                       cw;       // codewords
   uint32_t                       nof_tbs;
   uint32_t                       nof_cbs;
-  uint32_t                       max_tb_bytes;
+  const uint32_t*                last_rows; // [nof_tbs]: the row of each TB's last codeblock
+  uint32_t                       last_only; // set by launch_pdsch_fused
   int32_t                        row_start[2][47]; // check-row edge offsets of BG1 / BG2
 };
 constexpr uint32_t PE_TB_CHUNK = 8192; // TB bytes per partial of the TB CRC
-hipError_t launch_pdsch_fused(const pdsch_fused_args& a, hipStream_t stream);
+// phase 0: TB CRC partials on crc_stream, every codeblock but the TBs' last ones on cb_stream; phase 1 (after both):
+// the TBs' last codeblocks on stream; phase 2: the TB CRC partials, then every codeblock, on stream.
+hipError_t launch_pdsch_fused(const pdsch_fused_args& a, hipStream_t crc_stream, hipStream_t cb_stream,
+                              hipStream_t stream, int phase);
 
 // pusch_decoder_impl.cpp:309-500 after the decoder: per-CB CRC status (kept in the
 // soft buffer across HARQ transmissions), statistics, codeblock concatenation

@@ -21,6 +21,8 @@ step slot_nopk 200 env SRSRAN_AMD_LDPC_PK=0 python bench.py --workload sch_slot 
 step sp_pk 300 python bench.py --workload slot_pipeline --steps 10 --no-latency --no-cpu-baseline
 step sp_nopk 300 env SRSRAN_AMD_LDPC_PK=0 python bench.py --workload slot_pipeline --steps 10 --no-latency --no-cpu-baseline
 step one_cell 200 python bench.py --slots-pipeline 1 --steps 50 --no-cpu-baseline --no-pinned --no-latency --low-snr-db -1
+step one_cell_graph 200 python bench.py --graph --slots-pipeline 1 --steps 50 --no-cpu-baseline --no-pinned --no-latency --low-snr-db -1
+step bench_graph 200 python bench.py --graph --no-cpu-baseline --no-pinned --no-latency --low-snr-db -1
 step ldpc_cfg1 200 python bench.py --workload ldpc --no-cpu-baseline
 export TMPDIR=/tmp
 step prof_slot 300 rocprofv3 --kernel-trace --stats -d $O/prof_slot -o slot -- python bench.py --workload sch_slot --steps 10 --no-latency --no-cpu-baseline
