@@ -1269,6 +1269,15 @@ constexpr int hr_waves_per_simd()
   return MAXL == bg_traits<1>::M ? FR_WAVES : (NP == 1 ? HR_WAVES : 2);
 }
 
+// threadIdx.x rebuilt from the wave's first thread (wave-uniform) and the lane id: opaque (volatile), so it is
+// recomputed where it is asked for instead of being held in a VGPR (or hoisted) across the codeblock loop
+__device__ __forceinline__ uint32_t hr_thread(uint32_t wave_base)
+{
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return wave_base + l;
+}
+
 // MAXL < 46: the high-rate kernel (int16 messages of the first MAXL layers in registers); MAXL == 46: the
 // full-length kernel (compressed messages of every layer).
 template <int ARITH, int MAXL, int NP>
@@ -1287,14 +1296,18 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
   lds_i8*       soft    = lds + LDS_SOFT_OFFSET;
   lds_i32*      soft4   = reinterpret_cast<lds_i32*>(soft);
 
+  // The thread index is rebuilt per codeblock from the wave's first lane (an SGPR) and the lane id (v_mbcnt, opaque
+  // so that nothing derived from it is hoisted out of the codeblock loop): no VGPR holds threadIdx.x across the
+  // loop (held next to the message file, it was spilled -- scratch traffic of ~25 MB per headline launch).
+  const uint32_t wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u;
   for (uint32_t cb = blockIdx.x; cb < a.nof_cbs; cb += gridDim.x) {
+    uint32_t t = hr_thread(wave_base);
     if (a.skip_flags && *reinterpret_cast<const int32_t*>(a.skip_flags + static_cast<size_t>(cb) * a.skip_stride)) {
-      if (threadIdx.x == 0) {
+      if (t == 0) {
         a.nof_iters[cb] = LDPC_ITERS_SKIPPED; // uniform over the workgroup
       }
       continue;
     }
-    uint32_t t = threadIdx.x;
     asm volatile("" : "+v"(t));
     const int8_t* in     = a.llrs + static_cast<size_t>(cb) * a.llr_stride;
     const int     n_llrs = static_cast<int>(a.llr_len);
@@ -1365,10 +1378,11 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
 
     if (input_size < K && a.force_decoding) {
       // ldpc_decoder_impl.cpp:92 (see ldpc_decode_kernel)
-      for (int b = t; b < K / 8 && !a.crc_table; b += NT) {
+      const uint32_t tf = hr_thread(wave_base);
+      for (int b = tf; b < K / 8 && !a.crc_table; b += NT) {
         out[b] = 0xff;
       }
-      if (t == 0) {
+      if (tf == 0) {
         a.nof_iters[cb] = -1;
       }
       if constexpr (NT > 64) {
@@ -1378,7 +1392,8 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
     }
     const int cb_len     = max(input_size + 2 * Z, K + 4 * Z);
     const int nof_layers = (cb_len + Z - 1) / Z - 22;
-    const int nof_sig    = K - (a.fillers ? a.fillers[cb] : a.nof_filler_bits);
+    // wave-uniform (an SGPR, not a VGPR held across the iterations)
+    const int nof_sig    = __builtin_amdgcn_readfirstlane(K - (a.fillers ? a.fillers[cb] : a.nof_filler_bits));
     int       result     = -1;
 
     std::conditional_t<FULL, fr_state, hr_msgs<NE>> c2v;
@@ -1395,8 +1410,7 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
         // hard bits + CRC early stop (ldpc_decoder_impl.cpp:125), remainder up to a unit factor:
         // bit i contributes crc_table[K - 1 - i]; the word of soft bits 4q .. 4q+3 reads the
         // remainders [K - 4 - 4q, K - 1 - 4q] as one 16-byte load.
-        uint32_t tq = threadIdx.x;
-        asm volatile("" : "+v"(tq));
+        const uint32_t tq = hr_thread(wave_base);
         uint32_t crc = 0, zero = 0;
         // chunks of CRC_CHUNK words with a scheduling barrier in between: all eleven 16-byte remainder
         // loads in flight at once would need 44 VGPRs next to the message file
@@ -1465,27 +1479,32 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
     }
 
     // ---- hard decision, packed MSB-first: 4 output bytes per task
-    uint32_t te = threadIdx.x;
-    asm volatile("" : "+v"(te));
-    for (int task = te; task < K / 32; task += NT) {
-      uint32_t o = 0;
+    const uint32_t te = hr_thread(wave_base);
+    // 16 output bytes (128 soft bits) per task: one 16-byte store per lane when the row is 16-byte aligned
+    static_assert(K % 128 == 0, "whole 16-byte hard-decision tasks");
+    for (int task = te; task < K / 128; task += NT) {
+      uint32_t o[4];
 #pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        const uint32_t w = static_cast<uint32_t>(soft4[8 * task + h]);
-        // per-byte (x <= 0) = sign of x - 1 (SWAR subtract, no borrow between bytes)
-        const uint32_t d    = ((w | 0x80808080u) - 0x01010101u) ^ (~w & 0x80808080u);
-        const uint32_t nib  = (((d & 0x80808080u) >> 7) * 0x08040201u) >> 24; // byte0 -> bit 3
-        const int      byte = h >> 1;
-        o |= (nib & 0xfu) << (8 * byte + ((h & 1) ? 0 : 4));
+      for (int c = 0; c < 4; ++c) {
+        o[c] = 0;
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+          const uint32_t w = static_cast<uint32_t>(soft4[32 * task + 8 * c + h]);
+          // per-byte (x <= 0) = sign of x - 1 (SWAR subtract, no borrow between bytes)
+          const uint32_t d    = ((w | 0x80808080u) - 0x01010101u) ^ (~w & 0x80808080u);
+          const uint32_t nib  = (((d & 0x80808080u) >> 7) * 0x08040201u) >> 24; // byte0 -> bit 3
+          const int      byte = h >> 1;
+          o[c] |= (nib & 0xfu) << (8 * byte + ((h & 1) ? 0 : 4));
+        }
       }
-      uint8_t* ob = out + 4 * task;
-      if (((reinterpret_cast<uintptr_t>(ob)) & 3u) == 0) {
-        *reinterpret_cast<uint32_t*>(ob) = o;
+      uint8_t* ob = out + 16 * task;
+      if (((reinterpret_cast<uintptr_t>(ob)) & 15u) == 0) {
+        *reinterpret_cast<uint4*>(ob) = uint4{o[0], o[1], o[2], o[3]};
       } else {
-        ob[0] = static_cast<uint8_t>(o);
-        ob[1] = static_cast<uint8_t>(o >> 8);
-        ob[2] = static_cast<uint8_t>(o >> 16);
-        ob[3] = static_cast<uint8_t>(o >> 24);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+          ob[b] = static_cast<uint8_t>(o[b >> 2] >> (8 * (b & 3)));
+        }
       }
     }
     if (a.soft_out) {
