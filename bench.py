@@ -427,7 +427,7 @@ def main():
         from bench_pipeline import run_pipeline
 
         line = run_pipeline(args, dist, world, rank, dev, timed, HBM_PEAK_GBS,
-                            load_traffic("r03b_traffic.json", "ldpc_decode_hr_kernel"))
+                            load_traffic("r04_traffic.json", "ldpc_decode_hr_kernel"))
     elif args.workload == "sch_slot":
         from bench_slot import run_sch_slot
 

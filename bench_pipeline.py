@@ -505,8 +505,10 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
             "limiter": "valu",
             "valu": valu,
             "note": "bound/achieved/peak/frac: the decoder's HBM roofline (algorithmic bytes / measured kernel time / "
-                    "8 TB/s; traffic = PMC FETCH + WRITE bytes of the same launch, see DESIGN.md for its split against "
-                    "the algorithmic bytes) -- far from HBM-bound.  Its limiter is VALU "
+                    "8 TB/s; traffic = HBM bytes of the same launch from separate FETCH_SIZE / WRITE_SIZE passes, "
+                    "WRITE_SIZE halved by this box's calibration (profiles/r04_traffic.json, "
+                    "profiles/r04_hr_decoder_traffic.md): 1.02x the algorithmic bytes, no spill or re-read traffic) "
+                    "-- far from HBM-bound.  Its limiter is VALU "
                     "issue: valu.achieved_frac_of_peak_issue = modelled VALU issue cycles (PMC SQ_ACTIVE_INST_VALU "
                     "per codeblock and iteration, profiles/ldpc_valu_model.json) / (1,024 SIMDs x 2.4 GHz x kernel "
                     "time); the PMC-measured busy fraction of the same command is in profiles/r03_pmc_table.json",
