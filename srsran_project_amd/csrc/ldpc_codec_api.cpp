@@ -562,25 +562,57 @@ const uint32_t* srs_amd::ldpc_encoder_edges(const srs_amd_ldpc_encoder* enc)
   return enc != nullptr ? enc->edges : nullptr;
 }
 
+namespace {
+// The (BG, Z) part of an encoder row descriptor: building the lifted graph and its encoding parameters takes ~1 us,
+// which per UE was most of a 512-UE slot's host time (0.55 ms), so every pair is built once.
+struct mixed_row_base {
+  enc_row_desc r;
+  int32_t      M, K, N_short;
+};
+
+const mixed_row_base& mixed_row_of(uint32_t bg, uint32_t Z)
+{
+  static const std::vector<mixed_row_base> table = [] {
+    std::vector<mixed_row_base> t(2 * NOF_LIFTING_SIZES);
+    for (int b = 1; b <= 2; ++b) {
+      for (int z = 2; z <= MAX_LIFTING_SIZE; ++z) {
+        const int i = lifting_size_position(z);
+        if (i < 0) {
+          continue;
+        }
+        lifted_graph g{};
+        encode_args  a{};
+        build_lifted_graph(g, b, z);
+        (void)build_encode_params(a, g);
+        mixed_row_base& m = t[(b - 1) * NOF_LIFTING_SIZES + i];
+        m.r.Z             = static_cast<uint32_t>(z);
+        m.r.edge_off      = static_cast<uint32_t>(lifted_edges_offset(b, z));
+        m.r.p0_shift      = static_cast<uint32_t>(a.p0_shift);
+        for (int c = 0; c < 3; ++c) {
+          m.r.core_a[c] = static_cast<uint32_t>(a.core_a[c]);
+        }
+        m.M       = a.M;
+        m.K       = a.K;
+        m.N_short = g.N_short;
+      }
+    }
+    return t;
+  }();
+  return table[(bg - 1) * NOF_LIFTING_SIZES + static_cast<uint32_t>(lifting_size_position(static_cast<int>(Z)))];
+}
+} // namespace
+
 uint32_t srs_amd::ldpc_encode_mixed_row(void* row, uint32_t bg, uint32_t Z, uint32_t max_bits)
 {
-  lifted_graph g{};
-  encode_args  a{};
-  build_lifted_graph(g, static_cast<int>(bg), static_cast<int>(Z));
-  (void)build_encode_params(a, g);
+  // callers pass a validated plan's (bg, Z)
+  const mixed_row_base& m = mixed_row_of(bg, Z);
   // as ldpc_encode_batch_ex: rows whose parity columns hold shortened-codeword positions < max_bits
-  const uint32_t full_bits = static_cast<uint32_t>(g.N_short * g.Z);
+  const uint32_t full_bits = static_cast<uint32_t>(m.N_short) * Z;
   max_bits                 = std::min(max_bits, full_bits);
-  const int cols           = static_cast<int>((max_bits + Z - 1) / Z) + 2;
-  enc_row_desc r{};
-  r.Z         = Z;
-  r.edge_off  = static_cast<uint32_t>(lifted_edges_offset(static_cast<int>(bg), static_cast<int>(Z)));
-  r.M_eff     = static_cast<uint32_t>(std::max(4, std::min(a.M, cols - a.K)));
-  r.pack_bits = max_bits == full_bits ? full_bits : std::min(full_bits, (max_bits + 7) / 8 * 8);
-  r.p0_shift  = static_cast<uint32_t>(a.p0_shift);
-  for (int c = 0; c < 3; ++c) {
-    r.core_a[c] = static_cast<uint32_t>(a.core_a[c]);
-  }
+  const int    cols        = static_cast<int>((max_bits + Z - 1) / Z) + 2;
+  enc_row_desc r           = m.r;
+  r.M_eff                  = static_cast<uint32_t>(std::max(4, std::min(m.M, cols - m.K)));
+  r.pack_bits              = max_bits == full_bits ? full_bits : std::min(full_bits, (max_bits + 7) / 8 * 8);
   static_assert(sizeof(r) == LDPC_ENCODE_ROW_BYTES, "row descriptor size");
   std::memcpy(row, &r, sizeof(r));
   return r.M_eff;
