@@ -96,6 +96,15 @@ def ul_pdu(amd, layers, tbs, ports=UL_PORTS):
                         start_symbol_index=UL_START, nof_symbols=UL_NSYM, tbs=tbs)
 
 
+def chain_streams(torch, dev):
+    """The two streams of a step's PDSCH and PUSCH chains: two consecutive torch pool streams.  HIP maps streams
+    onto GPU_MAX_HW_QUEUES (4 on the box) hardware queues round-robin, so two streams created one after the other
+    never share a queue, while the caller's stream and a pool stream can -- and then the chains run one after the
+    other (tools/overlap_probe.py: 64-cell slot step 1.45 ms serialized, 1.23-1.26 ms overlapped; a high-priority
+    PUSCH stream measured 2.7 ms)."""
+    return torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+
 class Pipeline:
     def __init__(self, slots, dev, iters=LDPC_ITERS, snr_db=SNR_DB, ul_layers=UL_LAYERS, seed=0, ul_equalizer=None,
                  keep_estimates=False, dl_layers=DL_LAYERS, dl_ports=DL_PORTS, ul_ports=UL_PORTS):
@@ -110,6 +119,7 @@ class Pipeline:
         # the reference-pinned ZF for two layers, MMSE (parity unpinned) for four unless asked otherwise
         self.ul_equalizer = ul_equalizer or ("zf" if ul_layers <= 2 else UL_EQ)
         self.ul_stream = None
+        self._capturing = False
         d = dev.index
         all_crbs = list(range(NPRB))
         # ---- plans -------------------------------------------------------------------------
@@ -213,17 +223,25 @@ class Pipeline:
         per-TB kernels fill each other's idle CUs."""
         t = self.torch
         if self.ul_stream is None:
-            self.ul_stream = t.cuda.Stream(self.dev)
+            self.dl_stream, self.ul_stream = chain_streams(t, self.dev)
             self.ev_fork = t.cuda.Event()
-            self.ev_join = t.cuda.Event()
+            self.ev_join = [t.cuda.Event(), t.cuda.Event()]
+        # under HIP-graph capture the PDSCH chain stays on the capturing stream (a capture whose origin stream holds
+        # only the fork / join events crashed the capture); the replayed graph's placement is the runtime's
+        dl = stream if self._capturing else self.dl_stream
         self.ev_fork.record(stream)
+        if dl is not stream:
+            dl.wait_event(self.ev_fork)
         self.ul_stream.wait_event(self.ev_fork)
-        with t.cuda.stream(stream):
-            self.pdsch(stream)
+        with t.cuda.stream(dl):
+            self.pdsch(dl)
         with t.cuda.stream(self.ul_stream):
             self.pusch(self.ul_stream)
-        self.ev_join.record(self.ul_stream)
-        stream.wait_event(self.ev_join)
+        if dl is not stream:
+            self.ev_join[0].record(dl)
+            stream.wait_event(self.ev_join[0])
+        self.ev_join[1].record(self.ul_stream)
+        stream.wait_event(self.ev_join[1])
 
     def graph(self, stream):
         """The step (both chains, every C-ABI launch of both streams) captured once as a HIP graph on `stream` (a
@@ -235,6 +253,7 @@ class Pipeline:
             self.step(stream)
         t.cuda.synchronize(self.dev)
         g = t.cuda.CUDAGraph()
+        self._capturing = True
         try:
             with t.cuda.graph(g, stream=stream):
                 self.step(stream)
@@ -242,6 +261,8 @@ class Pipeline:
             print("HIP graph capture refused: %s" % exc, file=sys.stderr)
             t.cuda.synchronize(self.dev)
             return None
+        finally:
+            self._capturing = False
         t.cuda.synchronize(self.dev)
         self._graph = g  # keep the graph (and its captured memory) alive
 

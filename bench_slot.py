@@ -270,18 +270,23 @@ class SlotPipeline:
 
     def step(self, stream):
         """Both chains of every cell, concurrently on two HIP streams (fork / join on `stream`)."""
+        import bench_pipeline as bp
+
         t = self.torch
         if self.ul_stream is None:
-            self.ul_stream = t.cuda.Stream(self.dev)
-            self.ev_fork, self.ev_join = t.cuda.Event(), t.cuda.Event()
+            self.dl_stream, self.ul_stream = bp.chain_streams(t, self.dev)
+            self.ev_fork, self.ev_join = t.cuda.Event(), [t.cuda.Event(), t.cuda.Event()]
         self.ev_fork.record(stream)
+        self.dl_stream.wait_event(self.ev_fork)
         self.ul_stream.wait_event(self.ev_fork)
-        with t.cuda.stream(stream):
-            self.pdsch(stream)
+        with t.cuda.stream(self.dl_stream):
+            self.pdsch(self.dl_stream)
         with t.cuda.stream(self.ul_stream):
             self.pusch(self.ul_stream)
-        self.ev_join.record(self.ul_stream)
-        stream.wait_event(self.ev_join)
+        self.ev_join[0].record(self.dl_stream)
+        self.ev_join[1].record(self.ul_stream)
+        stream.wait_event(self.ev_join[0])
+        stream.wait_event(self.ev_join[1])
 
     def check(self):
         """Fraction of PUSCH TBs with CRC ok and equal to what the UE sent, mean LDPC iterations per codeblock."""
