@@ -232,7 +232,8 @@ int srs_amd::ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
                                   void*                              stream,
                                   const uint8_t*                     d_skip_flags,
                                   uint32_t                           skip_stride,
-                                  const int32_t*                     d_fillers)
+                                  const int32_t*                     d_fillers,
+                                  const ldpc_cw_rows*                cw)
 {
   if (d == nullptr) {
     return fail(SRS_AMD_EINVAL, "null decoder");
@@ -247,8 +248,13 @@ int srs_amd::ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
   if (nof_cbs == 0) {
     return SRS_AMD_OK;
   }
-  if (d_llrs == nullptr || d_output == nullptr || d_nof_iters == nullptr) {
+  if ((d_llrs == nullptr && cw == nullptr) || d_output == nullptr || d_nof_iters == nullptr ||
+      (cw != nullptr && (cw->llrs == nullptr || cw->offsets == nullptr || cw->lengths == nullptr))) {
     return fail(SRS_AMD_EINVAL, "null device buffer");
+  }
+  if (cw != nullptr && (d_llr_lens != nullptr || d_soft_out != nullptr || d_skip_flags != nullptr || cw->qm == 0 ||
+                        !ldpc_hr_takes(static_cast<int>(cfg->base_graph), static_cast<int>(cfg->lifting_size), llr_len))) {
+    return fail(SRS_AMD_EINVAL, "codeword-fed rows need the high-rate decoder's configuration");
   }
   if (out_stride < (K + 7) / 8) {
     return fail(SRS_AMD_EINVAL, "The output size %u is not equal to the message length %u.", out_stride * 8, K);
@@ -292,6 +298,16 @@ int srs_amd::ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
   a.skip_flags      = d_skip_flags;
   a.skip_stride     = skip_stride;
   a.fillers         = d_fillers;
+  if (cw != nullptr) {
+    a.llrs        = cw->llrs;
+    a.aligned4    = 1; // rows are built in LDS
+    a.cw_llrs     = cw->llrs;
+    a.cw_offsets  = cw->offsets;
+    a.cw_lengths  = cw->lengths;
+    a.cw_qm       = cw->qm;
+    a.cw_nof_info = cw->nof_info;
+    a.cw_filler   = cw->filler;
+  }
   const int grid    = static_cast<int>(nof_cbs < d->max_slots ? nof_cbs : d->max_slots);
   e = launch_ldpc_decode(a, g, d->arith, grid, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) {

@@ -43,6 +43,15 @@ int ldpc_encode_batch_ex(srs_amd_ldpc_encoder*              enc,
 // srs_amd_ldpc_decode_batch with an optional per-codeblock skip flag (int32 at d_skip_flags + cb *
 // skip_stride, non-zero: not decoded, nof_iters[cb] = -2): the PUSCH decoder's retransmissions of
 // codeblocks whose CRC passed in an earlier transmission (pusch_decoder_impl.cpp:330-345).
+// Codeblock rows built from the received codeword (decode_args::cw_llrs): the rate dematcher's new-data,
+// fresh-buffer, k0 = 0, no-wrap case fused into the high-rate decoder's load; d_llrs is then unused.
+struct ldpc_cw_rows {
+  const int8_t*   llrs;     // codeword LLRs
+  const uint32_t* offsets;  // [nof_cbs] byte offset of each codeblock's E LLRs
+  const uint32_t* lengths;  // [nof_cbs] E
+  uint32_t        qm, nof_info, filler;
+};
+
 int ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
                          const srs_amd_ldpc_decoder_config* cfg,
                          int                                crc_poly,
@@ -58,7 +67,8 @@ int ldpc_decode_batch_ex(srs_amd_ldpc_decoder*              d,
                          void*                              stream,
                          const uint8_t*                     d_skip_flags,
                          uint32_t                           skip_stride,
-                         const int32_t*                     d_fillers = nullptr);
+                         const int32_t*                     d_fillers = nullptr,
+                         const ldpc_cw_rows*                cw        = nullptr);
 
 // LDPC decoding of codeblocks of one base graph with per-codeblock lifting sizes (srs_amd_pusch_decode_slot):
 // row cb has lifting size row_z[cb] <= max_z < 384, input length llr_lens[cb], filler bits fillers[cb] and

@@ -74,6 +74,17 @@ struct decode_args {
   // optional per-codeblock graph (runtime-Z kernel only): codeblock cb has lifting size rows[cb].Z, its
   // edges at edges + rows[cb].edge_off and its CRC table at crc_table + rows[cb].crc_off (NO_CRC_ROW: none)
   const struct ldpc_row_desc* rows;
+  // optional (high-rate kernel only): the soft row of codeblock cb is built in LDS from its received codeword LLRs
+  // (cw_lengths[cb] = E of them at cw_llrs + cw_offsets[cb]) instead of read from llrs -- the PUSCH rate
+  // dematcher's new-data, fresh-buffer, k0 = 0, no-wrap case (ldpc_rate_dematch_kernel) fused into the load:
+  // position p < cw_nof_info takes deinterleaved LLR p, [cw_nof_info, + cw_filler) +infinity, then LLR p - filler
+  // up to E + filler, zeros after
+  const int8_t*   cw_llrs;
+  const uint32_t* cw_offsets;
+  const uint32_t* cw_lengths;
+  uint32_t        cw_qm;
+  uint32_t        cw_nof_info;
+  uint32_t        cw_filler;
 };
 
 // Per-codeblock graph of a mixed-lifting-size launch (srs_amd_pusch_decode_slot).
@@ -86,6 +97,10 @@ struct ldpc_row_desc {
 
 // ceil-ish 2^32 / Z with umulhi(i, m) == i / Z for every i < 2^16 and valid lifting size Z.
 uint32_t ldpc_z_magic(uint32_t Z);
+
+// The high-rate kernel takes (bg, Z) rows of llr_len LLRs (the launch conditions of ldpc_decode_hr_eligible that do
+// not depend on buffers): the PUSCH decoder then fuses its rate dematching into the decoder's load.
+bool ldpc_hr_takes(int bg, int Z, uint32_t llr_len);
 
 // Waves per codeblock of the packed runtime-Z decoder kernel for (bg, Z) (Z a multiple of 4), 0 when that
 // kernel does not take it (SRSRAN_AMD_LDPC_PK=0 disables it).

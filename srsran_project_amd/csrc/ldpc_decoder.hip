@@ -1324,7 +1324,81 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
       __syncthreads();
     }
     int input_size;
-    {
+    if (a.cw_llrs != nullptr) {
+      // ---- rate dematching fused into the load (decode_args::cw_llrs): the codeblock's E received LLRs are
+      // deinterleaved straight into the LDS row (symbol i, bit j -> deinterleaver index j Kq + i -> row position
+      // p, shifted past the filler block), then each word is completed (fillers +infinity, zeros from E + F),
+      // clamped and scanned exactly as a dematched row read from HBM (ldpc_rate_dematch_kernel's first pass).
+      const uint32_t E     = a.cw_lengths[cb];
+      const int8_t*  src   = a.cw_llrs + a.cw_offsets[cb];
+      const uint32_t Qm    = a.cw_qm;
+      const uint32_t Kq    = E / Qm;
+      const uint32_t ninfo = a.cw_nof_info;
+      const uint32_t F     = a.cw_filler;
+      lds_i8*        row   = soft + 2 * Z;
+      if (Qm == 8 && ((reinterpret_cast<uintptr_t>(src) & 7u) == 0)) {
+        for (uint32_t i = t; i < Kq; i += NT) {
+          const uint2 v = reinterpret_cast<const uint2*>(src)[i];
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t d = j * Kq + i;
+            row[d < ninfo ? d : d + F] = static_cast<int8_t>((j < 4 ? v.x : v.y) >> (8 * (j & 3u)));
+          }
+        }
+      } else {
+        for (uint32_t i = t; i < Kq; i += NT) {
+          for (uint32_t j = 0; j < Qm; ++j) {
+            const uint32_t d = j * Kq + i;
+            row[d < ninfo ? d : d + F] = src[i * Qm + j];
+          }
+        }
+      }
+      __syncthreads();
+      const int nw   = n_llrs >> 2; // n_llrs % 4 == 0 (ldpc_hr_takes)
+      const int B4   = (n_llrs / Z) * Z >> 2;
+      const int end  = static_cast<int>(E + F);
+      int       last = -1;
+#pragma unroll
+      for (int k = 0; k < (MAX_LLR / 4 + NT - 1) / NT; ++k) {
+        const int w = static_cast<int>(t) + k * NT;
+        uint32_t  v = 0;
+        if (w < nw) {
+          v = static_cast<uint32_t>(soft4[(2 * Z) / 4 + w]);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int      pb   = 4 * w + b;
+            const uint32_t mask = 0xffu << (8 * b);
+            v                   = pb >= end ? (v & ~mask) : v;
+            v = (pb >= static_cast<int>(ninfo) && pb < static_cast<int>(ninfo + F)) ? ((v & ~mask) | (0x7fu << (8 * b))) : v;
+          }
+        }
+        if (v != 0) {
+          last = 4 * w + (31 - __builtin_clz(v)) / 8;
+        }
+        const int lim = w < B4 ? SOFT_CLAMP : SOFT_INF;
+        uint32_t  o   = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int x = static_cast<int8_t>(v >> (8 * b));
+          o |= (static_cast<uint32_t>(med3_i(x, -lim, lim)) & 0xffu) << (8 * b);
+        }
+        if (w < (NODES - 2) * Z / 4) {
+          soft4[(2 * Z) / 4 + w] = static_cast<int32_t>(o);
+        }
+      }
+      for (int w = t; w < 2 * Z / 4; w += NT) {
+        soft4[w] = 0;
+      }
+      if constexpr (NT == 64) {
+        input_size = __builtin_amdgcn_readfirstlane(wave_max(last) + 1);
+      } else {
+        if (last >= 0) {
+          __hip_atomic_fetch_max(&red[0], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        input_size = __builtin_amdgcn_readfirstlane(red[0] + 1);
+      }
+    } else {
       const int      nw  = n_llrs >> 2;
       const int      B4  = (n_llrs / Z) * Z >> 2;
       const int32_t* in4 = reinterpret_cast<const int32_t*>(in);
@@ -1691,22 +1765,30 @@ __device__ __forceinline__ void pk_layer(lds_i8* lds, pk_state<BG>& st, uint32_t
   }
 }
 
+// own: the lane owns its row pair (threadIdx.x < H).  A repeating lane (t >= H, rows of lane t mod H) sits in another
+// wave than its owner when H is not a multiple of 64 (Z = 136..252 or 264..380 with Z / 2 mod 64 != 0): with no
+// barrier between a layer's gathers and scatters, the owner's wave can scatter a row's new soft bits before the
+// repeating wave gathers them, which then computes -- and scatters -- different values (BG2 Z = 288 soft bits
+// differed in 0.6 % of positions, intermittently).  Repeating lanes therefore skip the layers: they only fill the
+// workgroup for the CRC, hard-decision and export loops, which index words by threadIdx.x.
 template <int BG, int L, int ARITH, int W>
-__device__ __forceinline__ void pk_layers(lds_i8* lds, pk_state<BG>& st, uint32_t t, pk_geo g, int nof_layers)
+__device__ __forceinline__ void pk_layers(lds_i8* lds, pk_state<BG>& st, uint32_t t, pk_geo g, int nof_layers, bool own)
 {
   if constexpr (L < bg_traits<BG>::M) {
     asm volatile("" : "+s"(nof_layers));
     if (L < 4 || L < nof_layers) { // uniform; nof_layers >= 4
       // laundered per layer: the positions are iteration-invariant, hoisted they would spill
       asm volatile("" : "+v"(t), "+s"(g.edge), "+s"(g.Z), "+s"(g.H));
-      pk_layer<BG, L, ARITH, 128 * W>(lds, st, t, g, std::make_integer_sequence<int, bg_traits<BG>::deg(L)>{});
+      if (own) {
+        pk_layer<BG, L, ARITH, 128 * W>(lds, st, t, g, std::make_integer_sequence<int, bg_traits<BG>::deg(L)>{});
+      }
       if constexpr (W > 1) {
         __syncthreads();
       } else {
         asm volatile("" ::: "memory"); // one wave: LDS accesses execute in issue order
       }
     }
-    pk_layers<BG, L + 1, ARITH, W>(lds, st, t, g, nof_layers);
+    pk_layers<BG, L + 1, ARITH, W>(lds, st, t, g, nof_layers, own);
   }
 }
 
@@ -1848,7 +1930,7 @@ __global__ void __launch_bounds__(64 * W, (BG == 1 ? PK_WAVES_BG1 : PK_WAVES_BG2
     st.zero();
 
     for (int it = 0; it < a.max_iterations; ++it) {
-      pk_layers<BG, 0, ARITH, W>(lds, st, tr, geo, nof_layers);
+      pk_layers<BG, 0, ARITH, W>(lds, st, tr, geo, nof_layers, t < H);
 
       if (crc_table) {
         // hard bits + CRC early stop (ldpc_decoder_impl.cpp:125), remainder up to a unit factor (see the
@@ -2041,8 +2123,21 @@ static void launch_bg(const decode_args& args, const lifted_graph& g, int grid, 
   }
 }
 
+bool ldpc_hr_takes(int bg, int Z, uint32_t llr_len)
+{
+  static const bool enabled = [] {
+    const char* e = std::getenv("SRSRAN_AMD_LDPC_HR");
+    return e == nullptr || e[0] != '0';
+  }();
+  return enabled && bg == 1 && Z == HR_Z && llr_len <= static_cast<uint32_t>((20 + HR_MAXL) * HR_Z) &&
+         (llr_len & 3u) == 0;
+}
+
 hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, int arith, int grid, hipStream_t stream)
 {
+  if (args.cw_llrs != nullptr && !(ldpc_decode_hr_eligible(args, g) && ldpc_hr_takes(g.bg, g.Z, args.llr_len))) {
+    return hipErrorInvalidValue; // codeword-fed rows are the high-rate kernel's only
+  }
   if (ldpc_decode_hr_eligible(args, g)) {
     // The crc table of the high-rate kernel is indexed from K Z - 1 down, 16-byte aligned.
     constexpr size_t lds = hr_lds_bytes<HR_MAXL>();

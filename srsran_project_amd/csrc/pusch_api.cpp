@@ -110,6 +110,13 @@ uint32_t llr_prefix(const srs_amd_sch_plan* p, const soft_row_layout& lay, bool 
 }
 
 // CRC polynomial of the decoder's early stop and of the CB check (select_crc, pusch_decoder_impl.cpp:35-46).
+// SRSRAN_AMD_DEMATCH_FUSED=0 keeps the separate dematch launch (read per call: A/B timing, parity tests).
+bool dematch_fused_enabled()
+{
+  const char* e = std::getenv("SRSRAN_AMD_DEMATCH_FUSED");
+  return e == nullptr || e[0] != '0';
+}
+
 int crc_poly_of(const srs_amd_sch_plan* p)
 {
   return p->nof_segments > 1 ? 1 : (p->tbs > 3824 ? 0 : 3);
@@ -191,9 +198,27 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   // An internal (fresh) buffer is read back only by the LDPC decoder, over the provably non-zero prefix:
   // the dematcher writes just that prefix.
   const uint32_t prefix = llr_prefix(p, lay, cfg->new_data != 0, internal);
-  int rc = rate_dematch_batch_ex(d->dm, &md, cfg->new_data ? 1 : 0, d_llrs, d->arrays.as<uint32_t>() + rows,
-                                 d->arrays.as<uint32_t>(), d_soft, lay.row_bytes, rows, stream, internal,
-                                 internal ? prefix : 0);
+  // New data into an internal (fresh) buffer with k0 = 0 and no circular wrap, decoded by the high-rate kernel:
+  // the dematched row is [LLRs | +inf fillers | LLRs | zeros], which the decoder builds in LDS from the codeword
+  // itself (decode_args::cw_llrs) -- no dematch launch, no soft row written to and read back from HBM.
+  ldpc_cw_rows cw{};
+  bool         fuse = false;
+  if (internal && cfg->new_data && dematch_fused_enabled() && ldpc_hr_takes(static_cast<int>(p->base_graph),
+                                                                             static_cast<int>(p->lifting_size), prefix)) {
+    rm_geometry g{};
+    const uint32_t e_max = std::max(p->rm_length_long, p->nof_short_segments > 0 ? p->rm_length_short : 0u);
+    fuse = make_rm_geometry(g, p->base_graph, p->lifting_size, p->rv, p->modulation_order, p->Nref,
+                            p->nof_filler_bits) == nullptr &&
+           g.k0 == 0 && e_max <= g.L && e_max + g.F <= prefix;
+    cw = ldpc_cw_rows{d_llrs, d->arrays.as<uint32_t>() + rows, d->arrays.as<uint32_t>(), p->modulation_order,
+                      g.nof_info, g.F};
+  }
+  int rc = SRS_AMD_OK;
+  if (!fuse) {
+    rc = rate_dematch_batch_ex(d->dm, &md, cfg->new_data ? 1 : 0, d_llrs, d->arrays.as<uint32_t>() + rows,
+                               d->arrays.as<uint32_t>(), d_soft, lay.row_bytes, rows, stream, internal,
+                               internal ? prefix : 0);
+  }
   if (rc != SRS_AMD_OK) {
     return rc;
   }
@@ -213,7 +238,8 @@ int decode_locked(srs_amd_pusch_decoder*              d,
   rc = ldpc_decode_batch_ex(dec, &dc, cfg->use_early_stop ? crc_poly : SRS_AMD_NO_CRC, d_soft, lay.row_bytes, nullptr,
                             prefix, d->msgs.as<uint8_t>(), msg_stride,
                             d->iters.as<int32_t>(), nullptr, rows, stream,
-                            skip ? reinterpret_cast<const uint8_t*>(d_soft) + lay.flag_offset : nullptr, lay.row_bytes);
+                            skip ? reinterpret_cast<const uint8_t*>(d_soft) + lay.flag_offset : nullptr, lay.row_bytes,
+                            nullptr, fuse ? &cw : nullptr);
   if (rc != SRS_AMD_OK) {
     return rc;
   }

@@ -278,3 +278,14 @@ def test_high_rate_kernel_grid_stride_and_offsets(amd):
         for k in range(10):
             np.testing.assert_array_equal(out[16 * k + i], o)
             assert it[16 * k + i] == (-1 if r is None else r)
+
+
+@pytest.mark.parametrize("bg", [1, 2])
+def test_packed_kernel_repeating_lanes(amd, bg):
+    """Lifting sizes whose half Z / 2 is not a multiple of 64 with two or three waves per codeblock: the lanes past
+    Z / 2 repeat a row pair of another wave and must not scatter (a repeating wave that gathered after the owner's
+    scatter wrote different soft bits, intermittently).  48 noisy codeblocks per size, soft bits included."""
+    dec = amd.LdpcDecoder("simd")
+    for Z in (144, 160, 176, 208, 224, 240, 288, 320, 352):
+        msgs, llrs = noisy_codeblocks(bg, Z, 48, seed=Z * 13 + bg)
+        _check(amd, dec, "simd", llrs, bg, Z, iters=6)

@@ -186,3 +186,56 @@ def test_pipeline_slot_roundtrip(enc, decs):
     torch.cuda.synchronize()
     assert res[:, 0].all().item()
     assert torch.equal(d_tb, rows)
+
+
+# High-rate BG1 Z = 384 transport blocks whose new-data rows the high-rate decoder builds from the codeword itself
+# (rate dematching fused into its load, decode_args::cw_llrs): fillers of 56..416 bits, Qm 2..8, 1..4 layers,
+# short and long segments, the headline 4-layer 256QAM TB.  (tbs, Qm, layers, channel symbols)
+FUSED_DEMATCH_CASES = [
+    (160136, 2, 1, 87093),
+    (40024, 4, 1, 10887),
+    (72808, 6, 1, 13064),
+    (72808, 6, 2, 13064),
+    (160136, 8, 4, 21776),
+    (1179864, 8, 4, 156744),
+]
+
+
+@pytest.mark.parametrize("ci", range(len(FUSED_DEMATCH_CASES)))
+def test_pusch_decode_dematch_fused(decs, ci, monkeypatch):
+    """decode_batch with internal soft rows (new data, rv 0, no circular wrap, prefix 24 Z): the fused
+    dematch-in-decoder path against the oracle (pusch_decoder_impl restatement) and against the separate dematch
+    launch (SRSRAN_AMD_DEMATCH_FUSED=0): TBs, CRC verdicts, statistics and per-codeblock iterations bit-exact."""
+    import torch
+
+    import srsran_project_amd as amd
+
+    tbs, qm, lay, nre = FUSED_DEMATCH_CASES[ci]
+    p, op = _plan((tbs, 1, qm, lay, nre, 0, 0))
+    assert p.lifting_size == 384 and amd.decoder_llr_prefix(p, True, True) == 24 * 384
+    n = 2 if tbs > 500000 else 3
+    tb = [tb_bytes(p.tbs, 31 * ci + k) for k in range(n)]
+    # easy, near-threshold, undecodable
+    llrs = np.stack([noisy_llrs(osch.pdsch_encode(tb[k], op), 12, (2, 5, 12)[k], seed=ci * 10 + k) for k in range(n)])
+    C = p.nof_segments
+    cfg = amd.PuschDecoder.config(nof_ldpc_iterations=6)
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SRSRAN_AMD_DEMATCH_FUSED", mode)
+        cb_it = torch.zeros(n * C, dtype=torch.int32, device="cuda")
+        d_tb, res = decs["simd"].decode_batch(torch.from_numpy(llrs).cuda(), p, cfg, cb_iterations=cb_it)
+        torch.cuda.synchronize()
+        outs[mode] = (d_tb.cpu().numpy(), res.cpu().numpy(), cb_it.cpu().numpy().reshape(n, C))
+    for a, b in zip(outs["1"], outs["0"]):
+        np.testing.assert_array_equal(a, b)
+    d_tb, res, cb_it = outs["1"]
+    for k in range(n):
+        h = osch.HarqBuffer(op)
+        out = np.zeros(p.tbs // 8, np.uint8)
+        ok, iters, stats = osch.pusch_decode(llrs[k], op, h, out, 6, "simd")
+        msg = "case %d TB %d" % (ci, k)
+        assert bool(res[k, 0]) == ok, msg
+        assert (res[k, 2], res[k, 3], res[k, 4]) == (sum(stats), min(stats), max(stats)), msg
+        np.testing.assert_array_equal(cb_it[k], [-1 if i is None else i for i in iters], err_msg=msg)
+        np.testing.assert_array_equal(d_tb[k], out, err_msg=msg)
+    assert bool(res[0, 0]) and np.array_equal(d_tb[0], tb[0])
