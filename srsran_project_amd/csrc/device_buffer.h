@@ -1,6 +1,8 @@
 // device_buffer.h -- grow-only device scratch allocation used by the C-ABI objects.
 #pragma once
 
+#include <cstdlib>
+
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -98,13 +100,40 @@ struct stream_order {
 // Fans independent launches of one call out over up to FAN_STREAMS helper streams and joins them back into
 // the caller's stream (events only, no host synchronisation): the small per-bucket LDPC launches of a
 // heterogeneous slot run concurrently instead of one after the other on a mostly idle GPU.
+// Lanes of the fan: the helper streams, then (with_main) the caller's stream itself.  Configuration (read once):
+// SRSRAN_AMD_FAN_STREAMS helpers (0..4, default 1), SRSRAN_AMD_FAN_MAIN=0 keeps the caller's stream out of the
+// fan (default: it is a lane), SRSRAN_AMD_FAN_PRIORITY=1 helpers at the highest stream priority.  Measured on the
+// 64-cell sch_slot step (tools/gpu_r04_fan.sh, three processes each): one helper + the caller's stream 0.844-0.849
+// ms; four helpers 1.05-1.12 ms (the helpers' hardware queues are assigned per process and collide); no helper
+// 1.00 ms; high-priority helpers 1.39-1.65 ms.
 struct stream_fan {
   static constexpr int FAN_STREAMS = 4;
-  hipStream_t          s[FAN_STREAMS]    = {};
-  hipEvent_t           join[FAN_STREAMS] = {};
-  hipEvent_t           fork              = nullptr;
-  int                  n                 = 0;
-  stream_fan()                           = default;
+  struct config {
+    int  helpers;
+    bool with_main, high_priority;
+  };
+  static const config& cfg()
+  {
+    static const config c = [] {
+      auto env = [](const char* k, int dflt) {
+        const char* e = std::getenv(k);
+        return e != nullptr ? std::atoi(e) : dflt;
+      };
+      config r{};
+      const int h     = env("SRSRAN_AMD_FAN_STREAMS", 1);
+      r.helpers       = h < 0 ? 0 : (h > FAN_STREAMS ? FAN_STREAMS : h);
+      r.with_main     = env("SRSRAN_AMD_FAN_MAIN", 1) != 0;
+      r.high_priority = env("SRSRAN_AMD_FAN_PRIORITY", 0) != 0;
+      return r;
+    }();
+    return c;
+  }
+  hipStream_t s[FAN_STREAMS]    = {};
+  hipEvent_t  join[FAN_STREAMS] = {};
+  hipEvent_t  fork              = nullptr;
+  int         n                 = 0;     // helpers of the open fan
+  bool        main_lane         = false; // the caller's stream is lane n
+  stream_fan()                             = default;
   stream_fan(const stream_fan&)            = delete;
   stream_fan& operator=(const stream_fan&) = delete;
   ~stream_fan()
@@ -122,17 +151,27 @@ struct stream_fan {
       (void)hipEventDestroy(fork);
     }
   }
-  // The next `count` launches go to stream(i), i < count; count <= 1 keeps them on `main`.
+  // Lanes of the open fan (>= 1): launches i = 0 .. count-1 go to stream(main, i % width()).
+  int width() const { return n + (main_lane || n == 0 ? 1 : 0); }
   hipError_t begin(hipStream_t main, int count)
   {
-    n            = count > FAN_STREAMS ? FAN_STREAMS : (count > 1 ? count : 0);
-    hipError_t e = hipSuccess;
+    const config& c = cfg();
+    main_lane       = c.with_main;
+    const int want  = count - (main_lane ? 1 : 0); // helpers worth opening
+    n               = count <= 1 ? 0 : (want < c.helpers ? want : c.helpers);
+    n               = n < 0 ? 0 : n;
+    hipError_t e    = hipSuccess;
     if (n > 0 && fork == nullptr) {
       e = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
     }
     for (int i = 0; i < n && e == hipSuccess; ++i) {
       if (s[i] == nullptr) {
-        e = hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking);
+        int lo = 0, hi = 0;
+        if (c.high_priority && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+          e = hipStreamCreateWithPriority(&s[i], hipStreamNonBlocking, hi);
+        } else {
+          e = hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking);
+        }
         if (e == hipSuccess) {
           e = hipEventCreateWithFlags(&join[i], hipEventDisableTiming);
         }
@@ -146,8 +185,13 @@ struct stream_fan {
     }
     return e;
   }
-  hipStream_t stream(hipStream_t main, int i) const { return n > 0 ? s[i % n] : main; }
-  hipError_t  end(hipStream_t main)
+  hipStream_t stream(hipStream_t main, int i) const
+  {
+    const int w = width();
+    const int k = i % w;
+    return k < n ? s[k] : main;
+  }
+  hipError_t end(hipStream_t main)
   {
     hipError_t e = hipSuccess;
     for (int i = 0; i < n && e == hipSuccess; ++i) {

@@ -492,11 +492,12 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH slot decoder stream fan-out");
   }
-  uint64_t load[stream_fan::FAN_STREAMS] = {};
+  uint64_t  load[stream_fan::FAN_STREAMS + 1] = {};
+  const int width                             = d->fan.width();
   for (size_t bi : by_size) {
     const bucket& b  = buckets[bi];
     int           si = 0;
-    for (int k = 1; k < stream_fan::FAN_STREAMS; ++k) {
+    for (int k = 1; k < width; ++k) {
       si = load[k] < load[si] ? k : si;
     }
     load[si] += static_cast<uint64_t>(b.rows) * b.Z;
