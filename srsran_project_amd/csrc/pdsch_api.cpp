@@ -304,10 +304,8 @@ int encode_fused_batch_locked(srs_amd_pdsch_encoder* e,
   // a uniform batch of segmented TBs: with SRSRAN_AMD_PDSCH_OVERLAP=1 the TB CRC runs on a helper stream beside the
   // codeblocks that do not carry it.  Off by default: inside the pipeline (PDSCH and PUSCH chains concurrent) the
   // extra fork / join measured 0.864-0.877 ms per step against 0.851-0.863 ms without (tools/gpu_r04_fan2.sh).
-  static const bool overlap_on = [] {
-    const char* v = std::getenv("SRSRAN_AMD_PDSCH_OVERLAP");
-    return v != nullptr && v[0] == '1';
-  }();
+  const char* ov         = std::getenv("SRSRAN_AMD_PDSCH_OVERLAP"); // read per call (tests run both forms)
+  const bool  overlap_on = ov != nullptr && ov[0] == '1';
   int rc = fused_launch_locked(e, f, e->batch_desc.as<uint8_t>(), upload, d_tbs, d_cw, stream,
                                overlap_on && f.row_E.size() >= 4 * f.tds.size());
   if (rc == SRS_AMD_OK) {

@@ -33,9 +33,14 @@ def _plan(case):
     return amd.sch_plan(tbs, bg, rv, qm, nref, lay, nre), osch.plan(tbs, bg, rv, qm, nref, lay, nre)
 
 
+@pytest.mark.parametrize("overlap", ["0", "1"])
 @pytest.mark.parametrize("ci", range(len(SCH_CASES)))
-def test_pdsch_encode(enc, ci):
+def test_pdsch_encode(enc, ci, overlap, monkeypatch):
+    """Host and batch forms against the oracle; the batch with and without the TB-CRC overlap on a helper stream
+    (SRSRAN_AMD_PDSCH_OVERLAP)."""
     import torch
+
+    monkeypatch.setenv("SRSRAN_AMD_PDSCH_OVERLAP", overlap)
 
     p, op = _plan(SCH_CASES[ci])
     assert p.as_dict() == op
