@@ -532,7 +532,11 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
                     "-- far from HBM-bound.  Its limiter is VALU "
                     "issue: valu.achieved_frac_of_peak_issue = modelled VALU issue cycles (PMC SQ_ACTIVE_INST_VALU "
                     "per codeblock and iteration, profiles/ldpc_valu_model.json) / (1,024 SIMDs x 2.4 GHz x kernel "
-                    "time); the PMC-measured busy fraction of the same command is in profiles/r03_pmc_table.json",
+                    "time); the PMC-measured busy fraction of the same command is in profiles/r03_pmc_table.json.  "
+                    "kernel_ms is the decoder launched alone on its stream (HIP events); rocprofv3 over the same "
+                    "launches agrees (profiles/r04_hr_alone_kernel_stats.md), while inside the pipeline step the "
+                    "decoder shares the CUs with the concurrent PDSCH chain and averages longer "
+                    "(profiles/r04_bench_kernel_stats.md)",
         },
         "cpu_baseline": cpu,
     }
