@@ -1,6 +1,7 @@
 // device_buffer.h -- grow-only device scratch allocation used by the C-ABI objects.
 #pragma once
 
+#include <cstdio>
 #include <cstdlib>
 
 #include <hip/hip_runtime.h>
@@ -106,8 +107,12 @@ struct stream_order {
 // 64-cell sch_slot step (tools/gpu_r04_fan.sh, three processes each): one helper + the caller's stream 0.844-0.849
 // ms; four helpers 1.05-1.12 ms (the helpers' hardware queues are assigned per process and collide); no helper
 // 1.00 ms; high-priority helpers 1.39-1.65 ms.
+// true when kernels of streams a and b overlap (two spin kernels, host-synchronous; stream_probe.hip)
+hipError_t streams_run_concurrently(hipStream_t a, hipStream_t b, bool& concurrent);
+
 struct stream_fan {
   static constexpr int FAN_STREAMS = 4;
+  static constexpr int SPARES      = 6; // helpers found on the caller's queue, kept so the next one lands elsewhere
   struct config {
     int  helpers;
     bool with_main, high_priority;
@@ -133,6 +138,10 @@ struct stream_fan {
   hipEvent_t  fork              = nullptr;
   int         n                 = 0;     // helpers of the open fan
   bool        main_lane         = false; // the caller's stream is lane n
+  hipStream_t probed[FAN_STREAMS] = {};  // the caller's stream helper i was found concurrent with ...
+  bool        probe_done[FAN_STREAMS] = {}; // ... once probed (the caller's stream may be the null stream)
+  hipStream_t spare[SPARES]       = {};
+  int         nof_spares          = 0;
   stream_fan()                             = default;
   stream_fan(const stream_fan&)            = delete;
   stream_fan& operator=(const stream_fan&) = delete;
@@ -149,6 +158,47 @@ struct stream_fan {
     }
     if (fork) {
       (void)hipEventDestroy(fork);
+    }
+    for (int i = 0; i < nof_spares; ++i) {
+      (void)hipStreamDestroy(spare[i]);
+    }
+  }
+  // A helper that runs concurrently with `main`: probed once per (helper, caller stream) -- a helper found on the
+  // caller's hardware queue is kept aside (so the next stream created lands on another queue) and replaced, up to
+  // SPARES times.  Not while `main` is being captured into a graph (the probe synchronizes).
+  hipError_t ensure_concurrent(hipStream_t main, int i, bool high_priority)
+  {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if ((probe_done[i] && probed[i] == main) || hipStreamIsCapturing(main, &cs) != hipSuccess ||
+        cs != hipStreamCaptureStatusNone) {
+      return hipSuccess;
+    }
+    for (;;) {
+      bool       conc = true;
+      hipError_t e    = streams_run_concurrently(main, s[i], conc);
+      if (e != hipSuccess) {
+        return e;
+      }
+      if (std::getenv("SRSRAN_AMD_FAN_DEBUG") != nullptr) {
+        std::fprintf(stderr, "stream_fan: helper %d %s the caller's stream (%d set aside)\n", i,
+                     conc ? "runs beside" : "serializes with", nof_spares);
+      }
+      if (conc || nof_spares == SPARES) {
+        probed[i]     = main;
+        probe_done[i] = true;
+        return hipSuccess;
+      }
+      spare[nof_spares++] = s[i];
+      int lo = 0, hi = 0;
+      if (high_priority && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+        e = hipStreamCreateWithPriority(&s[i], hipStreamNonBlocking, hi);
+      } else {
+        e = hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking);
+      }
+      if (e != hipSuccess) {
+        s[i] = spare[--nof_spares];
+        return e;
+      }
     }
   }
   // Lanes of the open fan (>= 1): launches i = 0 .. count-1 go to stream(main, i % width()).
@@ -175,6 +225,9 @@ struct stream_fan {
         if (e == hipSuccess) {
           e = hipEventCreateWithFlags(&join[i], hipEventDisableTiming);
         }
+      }
+      if (e == hipSuccess && main_lane) {
+        e = ensure_concurrent(main, i, c.high_priority);
       }
     }
     if (n > 0 && e == hipSuccess) {

@@ -23,6 +23,7 @@ def main():
     if len(starts) < 2:
         print("anchor %r seen %d times" % (anchor, len(starts)))
         return
+    print("all step intervals (us):", " ".join("%.0f" % ((b - a) / 1e3) for a, b in zip(starts[:-1], starts[1:])))
     bounds = list(zip(starts[:-1], starts[1:]))[-nsteps:]
     for s0, s1 in bounds:
         ks = [r for r in rows if s0 <= r[0] < s1]
