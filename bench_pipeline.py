@@ -323,11 +323,13 @@ class Pipeline:
         return e0.elapsed_time(e1) / reps, nbytes, self.S * C, float(np.mean(np.where(it < 0, self.iters, it)))
 
     def stage_ms(self, stream, reps=3):
-        """Per-stage device time (HIP events on the launch stream), averaged over reps."""
+        """Per-stage device time (HIP events on the launch stream), averaged over reps after one untimed pass (the
+        objects last ran on the step's chain streams: the first call on `stream` carries their cross-stream
+        ordering wait and is not a stage time)."""
         t = self.torch
         names = ["pdsch_encode", "pdsch_modulate", "dmrs_pdsch", "ofdm_modulate", "ofdm_demodulate", "pusch_process"]
         acc = np.zeros(len(names))
-        for _ in range(reps):
+        for rep in range(reps + 1):
             ev = [t.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
             ev[0].record(stream)
             self.enc.encode_batch(self.tb_dl, self.plan_dl, out=self.cw_dl, stream=stream)
@@ -347,7 +349,8 @@ class Pipeline:
                                     port_stats=self.stats_ul, estimates=self.est_ul, llrs=self.llr_ul, stream=stream)
             ev[6].record(stream)
             t.cuda.synchronize(self.dev)
-            acc += np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(len(names))])
+            if rep > 0:
+                acc += np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(len(names))])
         return dict(zip(names, (acc / reps).tolist()))
 
 
