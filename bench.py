@@ -38,6 +38,7 @@ generic DFT for OFDM since FFTW is not in the image) on a bounded sample of the
 same workload, on the host cores of the same box, rank 0 only.
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -128,17 +129,27 @@ def timed(args, dist, world, dev, stream, step):
     if world > 1:
         dist.barrier()
     sync()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        if gpu:
-            starts[s].record(stream)
-        step()
-        if gpu:
-            ends[s].record(stream)
-    sync()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    # Python's cyclic garbage collector off while timing (as timeit does): a full collection of this process's
+    # heap takes ~7 ms and landed inside the timed steps of some runs (sch_slot: one 7 ms step in 20 -> 1.15 ms
+    # per step instead of 0.84, tools/gpu_r04_bimodal.sh); the GPU path itself allocates nothing per step
+    gc.collect()
+    gc_was_enabled = gc.isenabled()
+    gc.disable()
+    try:
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            if gpu:
+                starts[s].record(stream)
+            step()
+            if gpu:
+                ends[s].record(stream)
+        sync()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    finally:
+        if gc_was_enabled:
+            gc.enable()
     if gpu:
         event_ms = float(np.mean([starts[s].elapsed_time(ends[s]) for s in range(args.steps)]))
     else:

@@ -67,6 +67,19 @@ struct geometry_cache {
   void invalidate() { valid = false; }
 };
 
+// Host wait for an event by polling hipEventQuery: the staging buffers of the slot forms wait here once per call for
+// their previous upload, which has normally completed or is about to; hipEventSynchronize could fall back to an
+// interrupt-driven wait whose wake-up occasionally took ~7 ms (one such step in twenty, tools/gpu_r04_bimodal.sh).
+inline hipError_t event_wait_spin(hipEvent_t ev)
+{
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) {
+      return e;
+    }
+  }
+}
+
 // Orders the reuse of an object's device scratch across the caller's streams: a batch call on stream s
 // first waits for the previous call's completion event when that call ran on another stream, so two
 // calls on different streams never overwrite each other's in-flight scratch.
@@ -107,6 +120,10 @@ struct stream_order {
 // 64-cell sch_slot step (tools/gpu_r04_fan.sh, three processes each): one helper + the caller's stream 0.844-0.849
 // ms; four helpers 1.05-1.12 ms (the helpers' hardware queues are assigned per process and collide); no helper
 // 1.00 ms; high-priority helpers 1.39-1.65 ms.
+// n bytes from pinned host memory h (hipHostMalloc) to device memory d on stream s, by a copy kernel (not the SDMA
+// engine; stream_probe.hip)
+hipError_t upload_pinned(void* d, const void* h, size_t n, hipStream_t s);
+
 // true when kernels of streams a and b overlap (two spin kernels, host-synchronous; stream_probe.hip)
 hipError_t streams_run_concurrently(hipStream_t a, hipStream_t b, bool& concurrent);
 
@@ -305,7 +322,7 @@ struct pinned_stage {
   // Waits for the previous upload and grows the buffer to n bytes; the host pointer is then writable.
   hipError_t acquire(size_t n)
   {
-    hipError_t e = used ? hipEventSynchronize(done) : hipSuccess;
+    hipError_t e = used ? event_wait_spin(done) : hipSuccess;
     used         = false;
     if (e == hipSuccess && done == nullptr) {
       e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
@@ -327,7 +344,7 @@ struct pinned_stage {
   // Copies the first n bytes to device memory d on stream s.
   hipError_t upload(void* d, size_t n, hipStream_t s)
   {
-    hipError_t e = hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s);
+    hipError_t e = upload_pinned(d, h, n, s);
     if (e == hipSuccess) {
       e = hipEventRecord(done, s);
     }

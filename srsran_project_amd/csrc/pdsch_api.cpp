@@ -181,7 +181,7 @@ int fused_launch_locked(srs_amd_pdsch_encoder* e,
   if (he == hipSuccess && upload) {
     // the pinned staging buffer is rewritten only once its previous upload completed
     if (e->stage_used) {
-      he = hipEventSynchronize(e->stage_done);
+      he = event_wait_spin(e->stage_done);
     }
     if (he == hipSuccess && e->stage_done == nullptr) {
       he = hipEventCreateWithFlags(&e->stage_done, hipEventDisableTiming);
@@ -208,7 +208,7 @@ int fused_launch_locked(srs_amd_pdsch_encoder* e,
       for (uint32_t t = 0; t < U; ++t) {
         lr[t] = f.tds[t].row0 + f.tds[t].nof_segments - 1;
       }
-      he = hipMemcpyAsync(dd, h, L.total, hipMemcpyHostToDevice, stream);
+      he = upload_pinned(dd, h, L.total, stream);
     }
     if (he == hipSuccess) {
       he = hipEventRecord(e->stage_done, stream);
@@ -594,7 +594,7 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   hipError_t he = hipSetDevice(e->device);
   // the pinned staging buffer is rewritten only once its previous upload completed
   if (he == hipSuccess && e->stage_used) {
-    he = hipEventSynchronize(e->stage_done);
+    he = event_wait_spin(e->stage_done);
   }
   if (he == hipSuccess && e->stage_done == nullptr) {
     he = hipEventCreateWithFlags(&e->stage_done, hipEventDisableTiming);
@@ -635,7 +635,7 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   call_scope scope(e->order, &e->fan, stream);
   he = e->order.begin(stream);
   if (he == hipSuccess) {
-    he = hipMemcpyAsync(dd, h, total, hipMemcpyHostToDevice, stream);
+    he = upload_pinned(dd, h, total, stream);
   }
   if (he == hipSuccess) {
     he = hipEventRecord(e->stage_done, stream);

@@ -411,7 +411,7 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   hipError_t he = hipSetDevice(d->device);
   // the pinned staging buffer is rewritten only once its previous upload completed
   if (he == hipSuccess && d->stage_used) {
-    he = hipEventSynchronize(d->stage_done);
+    he = event_wait_spin(d->stage_done);
   }
   if (he == hipSuccess && d->stage_done == nullptr) {
     he = hipEventCreateWithFlags(&d->stage_done, hipEventDisableTiming);
@@ -460,7 +460,7 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   call_scope scope(d->order, &d->fan, stream);
   he = d->order.begin(stream);
   if (he == hipSuccess) {
-    he = hipMemcpyAsync(dd, h, total, hipMemcpyHostToDevice, stream);
+    he = upload_pinned(dd, h, total, stream);
   }
   if (he == hipSuccess) {
     he = hipEventRecord(d->stage_done, stream);

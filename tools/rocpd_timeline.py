@@ -24,7 +24,11 @@ def main():
         print("anchor %r seen %d times" % (anchor, len(starts)))
         return
     print("all step intervals (us):", " ".join("%.0f" % ((b - a) / 1e3) for a, b in zip(starts[:-1], starts[1:])))
-    bounds = list(zip(starts[:-1], starts[1:]))[-nsteps:]
+    bounds = list(zip(starts[:-1], starts[1:]))
+    if nsteps < 0:  # the slowest step after the first five (warm-up, setup)
+        bounds = [max(bounds[5:], key=lambda ab: ab[1] - ab[0])]
+    else:
+        bounds = bounds[-nsteps:]
     for s0, s1 in bounds:
         ks = [r for r in rows if s0 <= r[0] < s1]
         print("## step: %.1f us between anchors, %d kernels" % ((s1 - s0) / 1e3, len(ks)))
