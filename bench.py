@@ -126,16 +126,15 @@ def timed(args, dist, world, dev, stream, step):
     if gpu:
         starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
         ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    sync()
-    # Python's cyclic garbage collector off while timing (as timeit does): a full collection of this process's
-    # heap takes ~7 ms and landed inside the timed steps of some runs (sch_slot: one 7 ms step in 20 -> 1.15 ms
-    # per step instead of 0.84, tools/gpu_r04_bimodal.sh); the GPU path itself allocates nothing per step
+    # Python's cyclic garbage collector off while timing, as timeit does (collected before the barrier, so the ranks
+    # still start their clocks together): no collection pause inside the timed steps
     gc.collect()
     gc_was_enabled = gc.isenabled()
     gc.disable()
     try:
+        if world > 1:
+            dist.barrier()
+        sync()
         t0 = time.perf_counter()
         for s in range(args.steps):
             if gpu:
