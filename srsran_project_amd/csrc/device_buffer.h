@@ -32,6 +32,15 @@ struct device_buffer {
     }
     return e;
   }
+  // ensure(n), the bytes zeroed whenever the buffer is (re)allocated
+  hipError_t ensure_zeroed(size_t n)
+  {
+    if (n <= size) {
+      return hipSuccess;
+    }
+    hipError_t e = ensure(n);
+    return e == hipSuccess ? hipMemset(ptr, 0, size) : e;
+  }
   template <typename T>
   T* as() const
   {

@@ -171,7 +171,7 @@ int decode_locked(srs_amd_pusch_decoder*              d,
     he = d->arrays.ensure(sizeof(uint32_t) * 2 * rows);
   }
   if (he == hipSuccess) {
-    he = d->tb_acc.ensure(sizeof(uint32_t) * nof_tbs);
+    he = d->tb_acc.ensure_zeroed(sizeof(uint32_t) * nof_tbs);
   }
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH decoder scratch");
@@ -441,7 +441,7 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     he = d->checks.ensure(sizeof(uint32_t) * R);
   }
   if (he == hipSuccess) {
-    he = d->tb_acc.ensure(sizeof(uint32_t) * U);
+    he = d->tb_acc.ensure_zeroed(sizeof(uint32_t) * U);
   }
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH slot decoder scratch");

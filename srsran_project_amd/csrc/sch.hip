@@ -21,6 +21,8 @@
 // kernels they sit between (a few hundred KB per slot).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "crc_device.h"
 #include "sch_args.h"
 
@@ -324,15 +326,17 @@ __device__ __forceinline__ tb_view view_of(const assemble_args& a, uint32_t t)
           a.tbs_bits};
 }
 
-__global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
+// CB CRC status, LDPC statistics, HARQ flags, single-codeblock TBs and the result row of TB t (one workgroup).
+// zero_acc: clear the TB's CRC accumulator for asm_tb_kernel (launched after this kernel); the merged form
+// (asm_merged_kernel) relies on asm_final_kernel having cleared it after its previous use instead.
+__device__ __forceinline__ void assemble_tb(const assemble_args& a, uint32_t t, bool zero_acc)
 {
   __shared__ uint32_t s_ok, s_sum, s_min, s_max, s_tb_ok;
   __shared__ uint8_t  s_fresh[SCH_MAX_SEGMENTS]; // decoded in this call (not OK from a previous transmission)
   __shared__ uint8_t  s_cb_ok[SCH_MAX_SEGMENTS];
   __shared__ uint16_t s_stat[SCH_MAX_SEGMENTS]; // iterations of the freshly decoded codeblocks
-  const uint32_t      t = blockIdx.x;
   const tb_view       v = view_of(a, t);
-  if (threadIdx.x == 0 && a.acc != nullptr) {
+  if (zero_acc && threadIdx.x == 0 && a.acc != nullptr) {
     a.acc[t] = 0; // the TB CRC accumulator of asm_tb_kernel (launched after this kernel): no memset launch
   }
   const uint32_t      C = v.C;
@@ -414,6 +418,11 @@ __global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
   }
 }
 
+__global__ __launch_bounds__(ASM_THREADS) void assemble_kernel(assemble_args a)
+{
+  assemble_tb(a, blockIdx.x, true);
+}
+
 // Source of the concatenated codeblock messages of TB t (the soft-buffer copies when HARQ state is kept).
 __device__ __forceinline__ const uint8_t* asm_source(const assemble_args& a, const tb_view& v, uint32_t& stride)
 {
@@ -435,16 +444,41 @@ struct lds_fetch {
 // TB CRC24A contributions, one workgroup per TB_CHUNK bytes of a TB: the chunk is gathered with consecutive
 // threads on consecutive bytes (coalesced codeblock reads and TB writes) into LDS, then each thread folds
 // its TB_PER contiguous bytes into a CRC contribution.
-__global__ __launch_bounds__(ASM_THREADS) void asm_tb_kernel(assemble_args a)
+// Chunk `chunk` of TB t when every codeblock of the TB is OK (all_ok: from the assembly's result row, or computed
+// by the caller in the merged form).
+__device__ __forceinline__ void asm_tb_chunk(const assemble_args& a, uint32_t t, uint32_t chunk, bool use_results)
 {
   __shared__ uint32_t partial[ASM_THREADS / 64];
   __shared__ uint32_t T[256];
   __shared__ uint8_t  s_chunk[ASM_TB_CHUNK];
-  const uint32_t      t = blockIdx.y;
+  __shared__ uint32_t s_bad;
   const tb_view       v = view_of(a, t);
-  const uint32_t      c0 = blockIdx.x * ASM_TB_CHUNK;
-  if (v.C == 1 || c0 >= v.tbs_bits / 8 || a.results[t].nof_codeblocks_crc_ok != v.C) {
+  const uint32_t      c0 = chunk * ASM_TB_CHUNK;
+  if (v.C == 1 || c0 >= v.tbs_bits / 8) {
     return; // uniform over the workgroup
+  }
+  if (use_results) {
+    if (a.results[t].nof_codeblocks_crc_ok != v.C) {
+      return;
+    }
+  } else {
+    // no HARQ state (a.soft null): a codeblock is OK exactly when this call decoded it with a CRC pass, as
+    // assemble_tb counts it
+    if (threadIdx.x == 0) {
+      s_bad = 0;
+    }
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < v.C; r += ASM_THREADS) {
+      const uint32_t cb = v.row0 + r;
+      const bool     ok = a.crc_checks ? (a.crc_checks[cb] == 0) : (a.iters[cb] >= 0);
+      if (!ok) {
+        s_bad = 1;
+      }
+    }
+    __syncthreads();
+    if (s_bad != 0) {
+      return;
+    }
   }
   crc_table8_init<ASM_THREADS>(T, 24, CRC24A_POLY);
   uint32_t        stride;
@@ -482,6 +516,22 @@ __global__ __launch_bounds__(ASM_THREADS) void asm_tb_kernel(assemble_args a)
   }
 }
 
+__global__ __launch_bounds__(ASM_THREADS) void asm_tb_kernel(assemble_args a)
+{
+  asm_tb_chunk(a, blockIdx.y, blockIdx.x, true);
+}
+
+// No HARQ state (a.soft null): the assembly of TB blockIdx.y (last workgroup of its row) and its concatenation /
+// CRC chunks (the other workgroups) in one launch -- one launch and one dependency fewer on the PUSCH critical path.
+__global__ __launch_bounds__(ASM_THREADS) void asm_merged_kernel(assemble_args a)
+{
+  if (blockIdx.x == gridDim.x - 1) {
+    assemble_tb(a, blockIdx.y, false);
+  } else {
+    asm_tb_chunk(a, blockIdx.y, blockIdx.x, false);
+  }
+}
+
 // TB CRC verdict (pusch_decoder_impl.cpp:416-437): the checksum is the 24 bits after the TB data in the
 // last codeblock; a mismatch flags a false CB CRC positive and resets the kept CB flags.
 __global__ __launch_bounds__(64) void asm_final_kernel(assemble_args a, uint32_t nof_tbs)
@@ -505,6 +555,7 @@ __global__ __launch_bounds__(64) void asm_final_kernel(assemble_args a, uint32_t
   }
   const bool ok           = a.acc[t] == chk;
   a.results[t].tb_crc_ok  = ok ? 1 : 0;
+  a.acc[t]                = 0; // cleared for the next call (asm_merged_kernel does not clear it)
   if (!ok && a.soft) {
     for (uint32_t r = 0; r < C; ++r) {
       uint8_t* srow = a.soft + static_cast<size_t>(v.row0 + r) * a.lay.row_bytes;
@@ -582,13 +633,25 @@ hipError_t launch_assemble(const assemble_args& a, uint32_t nof_tbs, hipStream_t
     hipLaunchKernelGGL(asm_copy_kernel, dim3((ncb * nw + ASM_THREADS - 1) / ASM_THREADS), dim3(ASM_THREADS), 0,
                        stream, a, ncb, nw);
   }
+  const uint32_t nbytes = (a.tds != nullptr ? a.max_tb_bits : a.tbs_bits) / 8;
+  const char*    mv     = std::getenv("SRSRAN_AMD_ASM_MERGED"); // read per call: 0 keeps the three-launch form
+  if (a.soft == nullptr && !(a.tds == nullptr && a.nof_segments == 1) && !(mv != nullptr && mv[0] == '0')) {
+    // the accumulators start at zero (allocation) and asm_final_kernel clears each one it reads
+    hipLaunchKernelGGL(asm_merged_kernel, dim3((nbytes + ASM_TB_CHUNK - 1) / ASM_TB_CHUNK + 1, nof_tbs),
+                       dim3(ASM_THREADS), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      return e;
+    }
+    hipLaunchKernelGGL(asm_final_kernel, dim3((nof_tbs + 63) / 64), dim3(64), 0, stream, a, nof_tbs);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(assemble_kernel, dim3(nof_tbs), dim3(ASM_THREADS), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || (a.tds == nullptr && a.nof_segments == 1)) {
     return e;
   }
   // a.acc was zeroed by assemble_kernel
-  const uint32_t nbytes = (a.tds != nullptr ? a.max_tb_bits : a.tbs_bits) / 8;
   hipLaunchKernelGGL(asm_tb_kernel, dim3((nbytes + ASM_TB_CHUNK - 1) / ASM_TB_CHUNK, nof_tbs), dim3(ASM_THREADS), 0,
                      stream, a);
   e = hipGetLastError();
