@@ -22,14 +22,16 @@
  * Nref = compute_N_ref(tbs_lbrm, C) (ldpc.h:225), nof_ch_symbols from
  * get_ulsch_information without UCI (all data REs x layers), rb_mask of the
  * type-1 allocation relative to the BWP (:166).
- * Scope: PUSCH with a codeword and, optionally, HARQ-ACK and CSI part 1 multiplexed on it
+ * Scope: PUSCH with a codeword and, optionally, HARQ-ACK, CSI part 1 and CSI part 2 multiplexed on it
  * (ulsch_demux.h, uci_decoder.h: ulsch_demultiplex_impl + uci_decoder_impl as pusch_processor_impl.cpp:252-334
- * wires them; no CSI part 2, no UCI-only PUSCH),
- * DM-RS type 1 with the pseudo-random sequence, or transform precoding with the
- * low-PAPR DM-RS (pusch_processor_impl.cpp:172-196, validator :148-174), no DC-carrier
- * zeroing (pdu.dc_position unset). DM-RS type 2 is rejected as the reference's own
- * validator rejects it (pusch_processor_validator_impl.cpp:151-154); the reference
- * PUSCH has no intra-slot frequency hopping.
+ * wires them), or UCI only (no codeword, tbs = 0: pusch_processor_impl.cpp:305-324 -- estimator, demodulator,
+ * demultiplexer and UCI decoders, no UL-SCH decoding), DM-RS type 1 with the pseudo-random sequence, or transform
+ * precoding with the low-PAPR DM-RS (pusch_processor_impl.cpp:172-196, validator :148-174).  The DC subcarrier
+ * (pdu.dc_position) of a CP-OFDM PDU has its channel estimate zeroed on every receive port, layer and OFDM symbol of
+ * the allocation (pusch_processor_impl.cpp:235-249), so its REs equalize to zero symbols of infinite variance (zero
+ * LLRs); transform precoding leaves it untouched, as the reference.  DM-RS type 2 is rejected as the reference's own
+ * validator rejects it (pusch_processor_validator_impl.cpp:151-154); the reference PUSCH has no intra-slot frequency
+ * hopping.
  */
 #ifndef SRSRAN_AMD_PUSCH_PROCESSOR_H
 #define SRSRAN_AMD_PUSCH_PROCESSOR_H
@@ -101,6 +103,11 @@ typedef struct srs_amd_pusch_pdu {
      and the UL-SCH of each grid with the geometry of its CSI part 2 size. */
   float                              beta_offset_csi_part2;
   srs_amd_uci_part2_size_description csi_part2_size;
+  /* pdu_t::dc_position (pusch_processor.h:161): subcarrier index of the DC within the resource grid (the FAPI PDU's
+     tx_direct_current_location, lib/fapi_adaptor/phy/messages/pusch.cpp:150-152); has_dc_position = 0: unset.  A
+     position outside the grid changes nothing. */
+  uint32_t                           has_dc_position;
+  uint32_t                           dc_position;
 } srs_amd_pusch_pdu;
 
 /* Per-transport-block results: pusch_decoder_result (sch.h), the UCI statuses and the channel
@@ -196,6 +203,11 @@ typedef struct srs_amd_pusch_slot_pdu {
   uint64_t                            uci_offset; /* byte offset of its UCI payload row in io->d_uci: HARQ-ACK
                                                      (nof_harq_ack) | CSI part 1 (nof_csi_part1) | CSI part 2 (the
                                                      largest size its description allows), one bit per byte */
+  uint32_t                            has_slot;   /* 1: this PDU's slot is (numerology, slot_index) below, whatever
+                                                     slot the shared plan was created or last moved to (PDUs of
+                                                     different slots may share one plan within a call); 0: the plan's */
+  uint32_t                            numerology;
+  uint32_t                            slot_index;
 } srs_amd_pusch_slot_pdu;
 
 /* Optional outputs of srs_amd_pusch_process_slot_ex (any member NULL: not returned). */

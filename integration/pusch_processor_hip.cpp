@@ -59,8 +59,8 @@ struct pending_pdu {
 std::string convert(const pusch_processor::pdu_t& pdu, size_t tb_bytes, srs_amd_pusch_pdu& c)
 {
   c = srs_amd_pusch_pdu{};
-  if (!pdu.codeword.has_value()) {
-    return "PUSCH without a codeword (UCI only)";
+  if (!pdu.codeword.has_value() && (tb_bytes != 0 || (pdu.uci.nof_harq_ack == 0 && pdu.uci.nof_csi_part1 == 0))) {
+    return "PUSCH without a codeword must carry UCI and no transport block";
   }
   if (pdu.cp != cyclic_prefix::NORMAL) {
     return "extended cyclic prefix";
@@ -73,8 +73,10 @@ std::string convert(const pusch_processor::pdu_t& pdu, size_t tb_bytes, srs_amd_
     return "non-contiguous or interleaved frequency allocation";
   }
   const bool tp = std::holds_alternative<pusch_processor::dmrs_transform_precoding_configuration>(pdu.dmrs);
-  if (pdu.dc_position.has_value() && !tp) {
-    return "DC subcarrier zeroing (dc_position)";
+  // the DC subcarrier's estimate is zeroed for CP-OFDM by the processor (pusch_processor_impl.cpp:235-249)
+  if (pdu.dc_position.has_value()) {
+    c.has_dc_position = 1;
+    c.dc_position     = static_cast<uint32_t>(*pdu.dc_position);
   }
   c.numerology       = to_numerology_value(pdu.slot.scs());
   c.slot_index       = pdu.slot.slot_index();
@@ -92,9 +94,10 @@ std::string convert(const pusch_processor::pdu_t& pdu, size_t tb_bytes, srs_amd_
     default:
       c.modulation = static_cast<int32_t>(get_bits_per_symbol(pdu.mcs_descr.modulation));
   }
-  c.rv            = pdu.codeword->rv;
-  c.base_graph    = pdu.codeword->ldpc_base_graph == ldpc_base_graph_type::BG1 ? 1 : 2;
-  c.new_data      = pdu.codeword->new_data ? 1 : 0;
+  // UCI only (no codeword, tbs = 0): no UL-SCH to decode, nothing kept between transmissions
+  c.rv            = pdu.codeword.has_value() ? pdu.codeword->rv : 0;
+  c.base_graph    = pdu.codeword.has_value() && pdu.codeword->ldpc_base_graph == ldpc_base_graph_type::BG2 ? 2 : 1;
+  c.new_data      = pdu.codeword.has_value() && !pdu.codeword->new_data ? 0 : 1;
   c.n_id          = pdu.n_id;
   c.nof_tx_layers = pdu.nof_tx_layers;
   c.nof_rx_ports  = static_cast<uint32_t>(pdu.rx_ports.size());
@@ -247,10 +250,8 @@ private:
     } else {
       lru.splice(lru.begin(), lru, it->second.lru);
     }
-    if (srs_amd_pusch_processor_plan_set_slot(it->second.plan, c.numerology, c.slot_index) != SRS_AMD_OK) {
-      error = srs_amd_last_error();
-      return nullptr;
-    }
+    // the plan is shared by every slot of this configuration: each PDU carries its own slot in the slot call
+    // (srs_amd_pusch_slot_pdu::has_slot), so PDUs of two slots in one batch keep their own DM-RS sequences
     return &it->second;
   }
 
@@ -412,6 +413,9 @@ private:
       u.tb_offset  = tb_off[i];
       u.d_soft     = batch[i].c.new_data ? nullptr : reinterpret_cast<int8_t*>(soft.d + soft_off[i]);
       u.uci_offset = uci_off[i];
+      u.has_slot   = 1;
+      u.numerology = batch[i].c.numerology;
+      u.slot_index = batch[i].c.slot_index;
       sp.push_back(u);
     }
     hipError_t e = hipMemcpyAsync(h_grids.d, h_grids.h, grids.size() * grid_stride * 4, hipMemcpyHostToDevice, stream);
@@ -437,7 +441,7 @@ private:
     for (size_t k = 0; k != live.size(); ++k) {
       const unsigned i = live[k];
       keep[k]          = !batch[i].c.new_data;
-      if (batch[i].c.new_data && batch[i].rm_buffer.is_valid() && !res[k].data.tb_crc_ok) {
+      if (batch[i].c.new_data && batch[i].c.tbs != 0 && batch[i].rm_buffer.is_valid() && !res[k].data.tb_crc_ok) {
         srs_amd_pusch_slot_pdu u = sp[k];
         u.d_soft                 = reinterpret_cast<int8_t*>(soft.d + soft_off[i]);
         again.push_back(u);
@@ -646,6 +650,10 @@ private:
         field(uci_row + p.c.nof_harq_ack + p.c.nof_csi_part1, r.nof_csi_part2, r.csi_part2_status, ctrl.csi_part2);
       }
       p.notifier->on_uci(ctrl);
+    }
+    // UCI only: on_uci alone (pusch_processor_impl.cpp:305-324 sets up no decoder, so no on_sch)
+    if (!p.pdu.codeword.has_value()) {
+      return;
     }
     pusch_processor_result_data data;
     data.data = dr;

@@ -28,10 +28,13 @@
 // a TB CRC pass and unlocked otherwise.  The LDPC statistic of a codeblock OK from an earlier transmission is the
 // processor's last count for that codeblock index (pusch_decoder_impl's cb_stats semantics).
 //
+// UCI-only PDUs (no codeword) run estimator, demodulator, demultiplexer and UCI decoders and are notified through
+// on_uci alone, as pusch_processor_impl.cpp:305-324; dc_position zeroes the DC subcarrier's channel estimate of a
+// CP-OFDM PDU (pusch_processor_impl.cpp:235-249).  Each PDU carries its own slot into the slot call, so PDUs of
+// different slots that share a cached plan keep their own DM-RS sequences.
 // Not supported (the validator reports it): DM-RS type 2 and interleaved / non-contiguous allocations (as the
-// reference validator), more than four receive ports or layers, UCI-only PDUs (no codeword), dc_position set on a
-// CP-OFDM PDU (the reference zeroes that subcarrier's channel estimate).  Compiled against the reference's headers
-// by integration/Makefile.
+// reference validator), more than four receive ports or layers.  Compiled against the reference's headers by
+// integration/Makefile.
 #pragma once
 
 #include "srsran/phy/upper/channel_processors/pusch/factories.h"

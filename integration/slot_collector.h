@@ -5,6 +5,7 @@
 //   * a PDU of another slot arrives (the pending slot is complete),
 //   * max_batch PDUs are pending, or
 //   * the oldest pending PDU has waited max_wait_us (0: no timer).
+// A batch never spans a slot boundary: every slot change is remembered, and each batch ends at the first one.
 // The batch callback runs on the collector thread and calls each PDU's notifier.  wait_idle() blocks until every
 // PDU queued so far has been processed.  Destruction processes what is still pending, then joins the thread.
 #pragma once
@@ -60,14 +61,12 @@ public:
   {
     {
       std::lock_guard<std::mutex> lock(mtx);
-      if (!queue.empty() && slot_key != queue_slot) {
-        cut = queue.size(); // the pending slot is complete
+      const uint64_t seq = head_seq + queue.size();
+      if (!queue.empty() && slot_key != last_key) {
+        boundaries.push_back(seq); // the slot before seq is complete
       }
-      if (queue.empty() || cut == queue.size()) {
-        first_time = std::chrono::steady_clock::now();
-      }
-      queue_slot = slot_key;
-      queue.push_back(std::move(e));
+      last_key = slot_key;
+      queue.push_back(item{std::move(e), std::chrono::steady_clock::now()});
       ++in_flight;
     }
     cv.notify_all();
@@ -96,39 +95,46 @@ public:
   }
 
 private:
+  struct item {
+    Entry                                 e;
+    std::chrono::steady_clock::time_point t; // enqueue time
+  };
+
   void run()
   {
     std::unique_lock<std::mutex> lock(mtx);
     while (true) {
       const auto wait  = std::chrono::microseconds(max_wait);
       auto       ready = [&] {
-        return !queue.empty() && (flush_req || stop || cut != 0 || queue.size() >= max_batch ||
-                                  (max_wait != 0 && std::chrono::steady_clock::now() - first_time >= wait));
+        return !queue.empty() && (flush_req || stop || !boundaries.empty() || queue.size() >= max_batch ||
+                                  (max_wait != 0 && std::chrono::steady_clock::now() - queue.front().t >= wait));
       };
       if (queue.empty() && stop) {
         break;
       }
       if (!ready()) {
         if (max_wait != 0 && !queue.empty()) {
-          cv.wait_until(lock, first_time + wait);
+          cv.wait_until(lock, queue.front().t + wait); // the oldest pending PDU's deadline
         } else {
           cv.wait(lock);
         }
         continue;
       }
-      // the complete slot (up to the cut), or everything pending, at most max_batch PDUs
-      const size_t       n = std::min<size_t>(cut != 0 ? cut : queue.size(), max_batch);
+      // the oldest slot (up to its first boundary), or everything pending, at most max_batch PDUs: a batch never
+      // spans a slot boundary
+      const size_t       upto = boundaries.empty() ? queue.size() : static_cast<size_t>(boundaries.front() - head_seq);
+      const size_t       n    = std::min<size_t>(upto, max_batch);
       std::vector<Entry> batch;
       batch.reserve(n);
       for (size_t i = 0; i != n; ++i) {
-        batch.push_back(std::move(queue.front()));
+        batch.push_back(std::move(queue.front().e));
         queue.pop_front();
       }
-      cut       = cut > n ? cut - n : 0;
-      flush_req = flush_req && !queue.empty();
-      if (!queue.empty()) {
-        first_time = std::chrono::steady_clock::now();
+      head_seq += n;
+      while (!boundaries.empty() && boundaries.front() <= head_seq) {
+        boundaries.pop_front();
       }
+      flush_req = flush_req && !queue.empty();
       lock.unlock();
       const unsigned errors = process(batch);
       lock.lock();
@@ -147,10 +153,10 @@ private:
   batch_function                        process;
   mutable std::mutex                    mtx;
   std::condition_variable               cv, idle_cv;
-  std::deque<Entry>                     queue;
-  size_t                                cut        = 0; // queue[0, cut) is a complete slot
-  uint64_t                              queue_slot = 0;
-  std::chrono::steady_clock::time_point first_time;
+  std::deque<item>                      queue;
+  uint64_t                              head_seq = 0;   // sequence number of queue.front()
+  std::deque<uint64_t>                  boundaries;     // sequence numbers that start a new slot (ascending)
+  uint64_t                              last_key = 0;   // slot of the newest queued PDU
   bool                                  flush_req = false, stop = false;
   size_t                                in_flight = 0;
   counters                              stats;

@@ -34,8 +34,79 @@ def lib():
         L.srs_ref_phy_pusch_stats.argtypes = [P, P]
         L.srs_ref_phy_pusch_bench.restype = d
         L.srs_ref_phy_pusch_bench.argtypes = [P, P, u, P, u, u, P, u, P]
+        L.srs_ref_fapi_pusch_convert.restype = P
+        L.srs_ref_fapi_pusch_convert.argtypes = [P, P, P]
+        L.srs_ref_fapi_pusch_params.argtypes = [P, P]
+        L.srs_ref_fapi_pusch_free.argtypes = [P]
+        L.srs_ref_phy_pusch_process_fapi.restype = i
+        L.srs_ref_phy_pusch_process_fapi.argtypes = [P, P, P, P, P, u]
+        L.srs_ref_pusch_process_fapi.restype = i
+        L.srs_ref_pusch_process_fapi.argtypes = [P, P, u, u, P, P, u, P, P, P, P, P]
         _declared = True
     return L
+
+
+class FapiPusch(ctypes.Structure):
+    """srs_ref_fapi_pusch (phy_harness.cpp): a flat FAPI UL_TTI.request PUSCH PDU (fapi::ul_pusch_pdu subset)."""
+
+    _fields_ = [(n, ctypes.c_uint32) for n in ("rnti", "bwp_start", "bwp_size", "numerology", "sfn", "slot")] + \
+        [("qm", ctypes.c_int32)] + \
+        [(n, ctypes.c_uint32) for n in (
+            "target_code_rate", "transform_precoding", "nid_pusch", "num_layers", "ul_dmrs_symb_pos", "dmrs_type",
+            "scrambling_id", "dmrs_identity", "nscid", "num_dmrs_cdm_grps_no_data", "rb_start", "rb_size",
+            "start_symbol_index", "nr_of_symbols", "tx_direct_current_location", "has_data", "rv_index",
+            "harq_process_id", "new_data", "tb_size", "ldpc_base_graph", "tb_size_lbrm_bytes", "has_uci",
+            "harq_ack_bit_length", "csi_part1_bit_length", "alpha_scaling", "beta_offset_harq_ack",
+            "beta_offset_csi1", "beta_offset_csi2", "num_rx_ant")]
+
+
+class FapiPuschPdu:
+    """A FAPI PUSCH PDU converted by the reference's convert_pusch_fapi_to_phy into the PHY's pusch_pdu
+    (lib/fapi_adaptor/phy/messages/pusch.cpp).  dc_position: the converted pdu_t::dc_position (None: unset);
+    tb_bytes: the transport block size; params: target_code_rate, alpha, beta HARQ-ACK / CSI1 / CSI2 as floats."""
+
+    def __init__(self, **kw):
+        L = lib()
+        self.fapi = FapiPusch(**kw)
+        dc, tbb = ctypes.c_int(), ctypes.c_uint()
+        self.h = L.srs_ref_fapi_pusch_convert(ctypes.byref(self.fapi), ctypes.byref(dc), ctypes.byref(tbb))
+        self.dc_position = None if dc.value < 0 else dc.value
+        self.tb_bytes = tbb.value
+        out = np.zeros(5, np.float32)
+        L.srs_ref_fapi_pusch_params(self.h, out.ctypes.data)
+        self.params = dict(target_code_rate=float(out[0]), alpha_scaling=float(out[1]),
+                           beta_offset_harq_ack=float(out[2]), beta_offset_csi_part1=float(out[3]),
+                           beta_offset_csi_part2=float(out[4]))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().srs_ref_fapi_pusch_free(self.h)
+            self.h = None
+
+
+def ref_pusch_process_fapi(grid, fpdu, nof_prb=273, iterations=6, rx_buffer=None):
+    """The reference's pusch_processor_impl on a converted FAPI PDU: (tb, result dict as PuschProcessorPlugin.result)."""
+    tb = np.zeros(max(fpdu.tb_bytes, 1), np.uint8)
+    res, csi, uci = np.zeros(6, np.float64), np.zeros(5, np.float64), np.zeros(5, np.int32)
+    ack = np.zeros(max(fpdu.fapi.harq_ack_bit_length, 1), np.uint8)
+    c1 = np.zeros(max(fpdu.fapi.csi_part1_bit_length, 1), np.uint8)
+    r = lib().srs_ref_pusch_process_fapi(grid.h, fpdu.h, nof_prb, iterations, None if rx_buffer is None else
+                                        rx_buffer.h, tb.ctypes.data, fpdu.tb_bytes, res.ctypes.data, csi.ctypes.data,
+                                        uci.ctypes.data, ack.ctypes.data, c1.ctypes.data)
+    if r != 0:
+        raise RuntimeError("reference pusch_processor_impl did not notify")
+    return tb[:fpdu.tb_bytes], _result_dict(res, csi, uci, ack[:fpdu.fapi.harq_ack_bit_length],
+                                            c1[:fpdu.fapi.csi_part1_bit_length], np.zeros(0, np.uint8))
+
+
+def _result_dict(res, csi, uci, ack, c1, c2):
+    obs = int(res[2])  # an empty statistic (a failed or UCI-only transmission) has a NaN mean
+    return dict(tb_crc_ok=bool(res[0]), nof_codeblocks_total=int(res[1]), nof_observations=obs,
+                iterations_sum=int(round(res[3])) if obs else 0, iterations_min=int(res[4]) if obs else 0,
+                iterations_max=int(res[5]) if obs else 0,
+                sinr_db=csi[0], epre_db=csi[1], rsrp_db=csi[2], time_alignment_s=csi[3], cfo_hz=csi[4],
+                nof_uci=int(uci[0]), harq_ack_status=int(uci[1]), csi_part1_status=int(uci[2]),
+                csi_part2_status=int(uci[3]), harq_ack=ack, csi_part1=c1, csi_part2=c2)
 
 
 class Grid:
@@ -103,14 +174,15 @@ class PuschProcessorPlugin:
                                            ack.ctypes.data, c1.ctypes.data, c2.ctypes.data)
         if r <= 0:
             return None
-        obs = int(res[2])  # an empty statistic (a failed transmission) has a NaN mean
-        return dict(tb_crc_ok=bool(res[0]), nof_codeblocks_total=int(res[1]), nof_observations=obs,
-                    iterations_sum=int(round(res[3])) if obs else 0, iterations_min=int(res[4]) if obs else 0,
-                    iterations_max=int(res[5]) if obs else 0,
-                    sinr_db=csi[0], epre_db=csi[1], rsrp_db=csi[2], time_alignment_s=csi[3], cfo_hz=csi[4],
-                    nof_uci=int(uci[0]), harq_ack_status=int(uci[1]), csi_part1_status=int(uci[2]),
-                    csi_part2_status=int(uci[3]), harq_ack=ack[:nof_harq_ack], csi_part1=c1[:nof_csi_part1],
-                    csi_part2=c2[:int(uci[4])])
+        return _result_dict(res, csi, uci, ack[:nof_harq_ack], c1[:nof_csi_part1], c2[:int(uci[4])])
+
+    def process_fapi(self, grid, fpdu, rx_buffer=None):
+        """pusch_processor::process of a converted FAPI PDU (FapiPuschPdu): (ticket, transport-block buffer)."""
+        tb = np.zeros(max(fpdu.tb_bytes, 1), np.uint8)
+        self._keep.append((tb, fpdu, grid))
+        t = lib().srs_ref_phy_pusch_process_fapi(self.h, grid.h, fpdu.h, None if rx_buffer is None else rx_buffer.h,
+                                                 tb.ctypes.data, fpdu.tb_bytes)
+        return t, tb[:fpdu.tb_bytes]
 
     def stats(self):
         s = np.zeros(5, np.uint64)

@@ -29,6 +29,9 @@
 #include "phy/upper/signal_processors/ptrs/ptrs_pdsch_generator_impl.h"
 #include "srsran_amd/pdsch_modulator.h"
 #include "srsran/adt/tensor.h"
+#include "srsran/fapi/messages/ul_tti_request.h"
+#include "srsran/fapi_adaptor/phy/messages/pusch.h"
+#include "srsran/fapi_adaptor/uci_part2_correspondence_repository.h"
 #include "srsran/phy/upper/channel_processors/pusch/pusch_processor_result_notifier.h"
 #include "srsran_amd/pusch_processor.h"
 #include <atomic>
@@ -138,7 +141,7 @@ pusch_processor::pdu_t to_pdu(const srs_amd_pusch_pdu& c)
   return pdu;
 }
 
-/// The notifications of one process() call.
+/// The notifications of one process() call (a UCI-only PDU completes with on_uci: expect_sch = false).
 class ticket : public pusch_processor_result_notifier
 {
 public:
@@ -146,6 +149,9 @@ public:
   {
     uci = u;
     ++nof_uci;
+    if (!expect_sch) {
+      done.store(true, std::memory_order_release);
+    }
   }
   void on_sch(const pusch_processor_result_data& s) override
   {
@@ -154,8 +160,29 @@ public:
   }
   pusch_processor_result_control uci;
   pusch_processor_result_data    sch;
-  unsigned                       nof_uci = 0;
+  unsigned                       nof_uci    = 0;
+  bool                           expect_sch = true;
   std::atomic<bool>              done{false};
+};
+
+/// A flat FAPI UL_TTI.request PUSCH PDU (SCF-222 v4.0 3.4.3.2, fapi::ul_pusch_pdu): the fields the reference's
+/// MAC -> FAPI translator fills for a type-1 PUSCH (test glue; converted by the reference's own
+/// convert_pusch_fapi_to_phy, lib/fapi_adaptor/phy/messages/pusch.cpp).
+struct srs_ref_fapi_pusch {
+  uint32_t rnti, bwp_start, bwp_size, numerology, sfn, slot;
+  int32_t  qm;               /* modulation order code (0 pi/2-BPSK, 2, 4, 6, 8) */
+  uint32_t target_code_rate; /* R x 1024 x 10 */
+  uint32_t transform_precoding, nid_pusch, num_layers, ul_dmrs_symb_pos, dmrs_type, scrambling_id, dmrs_identity;
+  uint32_t nscid, num_dmrs_cdm_grps_no_data, rb_start, rb_size, start_symbol_index, nr_of_symbols;
+  uint32_t tx_direct_current_location; /* >= 3300: not set */
+  uint32_t has_data, rv_index, harq_process_id, new_data, tb_size, ldpc_base_graph, tb_size_lbrm_bytes;
+  uint32_t has_uci, harq_ack_bit_length, csi_part1_bit_length, alpha_scaling, beta_offset_harq_ack, beta_offset_csi1,
+      beta_offset_csi2;
+  uint32_t num_rx_ant;
+};
+
+struct fapi_pusch_handle {
+  uplink_pdu_slot_repository::pusch_pdu pdu;
 };
 
 struct pusch_ctx {
@@ -436,7 +463,7 @@ int srs_ref_phy_pusch_result(void* h, int id, double* result, double* csi, int* 
   result[3]                      = st.get_mean() * st.get_nof_observations();
   result[4]                      = st.get_min();
   result[5]                      = st.get_max();
-  const channel_state_information& c = t->sch.csi;
+  const channel_state_information& c = t->expect_sch ? t->sch.csi : t->uci.csi;
   csi[0]                             = c.get_sinr_dB().value_or(NAN);
   csi[1]                             = c.get_epre_dB().value_or(NAN);
   csi[2]                             = c.get_rsrp_dB().value_or(NAN);
@@ -457,6 +484,145 @@ int srs_ref_phy_pusch_result(void* h, int id, double* result, double* csi, int* 
     bits_out(t->uci.csi_part2.payload, csi2);
   }
   return 1;
+}
+
+/* fapi::ul_pusch_pdu from the flat description, converted to the PHY's PUSCH PDU by the reference's
+ * convert_pusch_fapi_to_phy (what the FAPI adaptor does for every UL_TTI.request PUSCH PDU).  Returns a handle (free
+ * with srs_ref_fapi_pusch_free); dc_out: the converted pdu_t::dc_position (-1: unset); tb_bytes_out: tb_size. */
+void* srs_ref_fapi_pusch_convert(const srs_ref_fapi_pusch* f, int* dc_out, unsigned* tb_bytes_out)
+{
+  fapi::ul_pusch_pdu fp = {};
+  fp.pdu_bitmap.set(fapi::ul_pusch_pdu::PUSCH_DATA_BIT, f->has_data != 0);
+  fp.pdu_bitmap.set(fapi::ul_pusch_pdu::PUSCH_UCI_BIT, f->has_uci != 0);
+  fp.pdu_bitmap.set(fapi::ul_pusch_pdu::DFTS_OFDM_BIT, f->transform_precoding != 0);
+  fp.rnti                      = to_rnti(f->rnti);
+  fp.bwp_size                  = static_cast<uint16_t>(f->bwp_size);
+  fp.bwp_start                 = static_cast<uint16_t>(f->bwp_start);
+  fp.scs                       = to_subcarrier_spacing(f->numerology);
+  fp.cp                        = cyclic_prefix::NORMAL;
+  fp.target_code_rate          = static_cast<uint16_t>(f->target_code_rate);
+  fp.qam_mod_order             = scheme_of(f->qm);
+  fp.transform_precoding       = f->transform_precoding != 0;
+  fp.nid_pusch                 = static_cast<uint16_t>(f->nid_pusch);
+  fp.num_layers                = static_cast<uint8_t>(f->num_layers);
+  fp.ul_dmrs_symb_pos          = static_cast<uint16_t>(f->ul_dmrs_symb_pos);
+  fp.dmrs_type                 = f->dmrs_type == 2 ? fapi::dmrs_cfg_type::type_2 : fapi::dmrs_cfg_type::type_1;
+  fp.pusch_dmrs_scrambling_id  = static_cast<uint16_t>(f->scrambling_id);
+  fp.pusch_dmrs_identity       = static_cast<uint16_t>(f->dmrs_identity);
+  fp.nscid                     = static_cast<uint8_t>(f->nscid);
+  fp.num_dmrs_cdm_grps_no_data = static_cast<uint8_t>(f->num_dmrs_cdm_grps_no_data);
+  fp.resource_alloc            = fapi::resource_allocation_type::type_1;
+  fp.rb_start                  = static_cast<uint16_t>(f->rb_start);
+  fp.rb_size                   = static_cast<uint16_t>(f->rb_size);
+  fp.tx_direct_current_location = static_cast<uint16_t>(f->tx_direct_current_location);
+  fp.start_symbol_index        = static_cast<uint8_t>(f->start_symbol_index);
+  fp.nr_of_symbols             = static_cast<uint8_t>(f->nr_of_symbols);
+  fp.pusch_data.rv_index        = static_cast<uint8_t>(f->rv_index);
+  fp.pusch_data.harq_process_id = static_cast<uint8_t>(f->harq_process_id);
+  fp.pusch_data.new_data        = f->new_data != 0;
+  fp.pusch_data.tb_size         = units::bytes(f->tb_size);
+  fp.pusch_maintenance_v3.ldpc_base_graph =
+      f->ldpc_base_graph == 2 ? ldpc_base_graph_type::BG2 : ldpc_base_graph_type::BG1;
+  fp.pusch_maintenance_v3.tb_size_lbrm_bytes = units::bytes(f->tb_size_lbrm_bytes);
+  fp.pusch_uci.harq_ack_bit_length  = static_cast<uint16_t>(f->harq_ack_bit_length);
+  fp.pusch_uci.csi_part1_bit_length = static_cast<uint16_t>(f->csi_part1_bit_length);
+  fp.pusch_uci.flags_csi_part2      = 0;
+  fp.pusch_uci.alpha_scaling        = static_cast<alpha_scaling_opt>(f->alpha_scaling);
+  fp.pusch_uci.beta_offset_harq_ack = static_cast<uint8_t>(f->beta_offset_harq_ack);
+  fp.pusch_uci.beta_offset_csi1     = static_cast<uint8_t>(f->beta_offset_csi1);
+  fp.pusch_uci.beta_offset_csi2     = static_cast<uint8_t>(f->beta_offset_csi2);
+  std::vector<static_vector<uint16_t, uci_part2_size_description::max_size_table>> part2(1);
+  fapi_adaptor::uci_part2_correspondence_repository repo(std::move(part2));
+  auto* h = new fapi_pusch_handle;
+  fapi_adaptor::convert_pusch_fapi_to_phy(h->pdu, fp, static_cast<uint16_t>(f->sfn), static_cast<uint16_t>(f->slot),
+                                          static_cast<uint16_t>(f->num_rx_ant), repo);
+  if (!fp.pdu_bitmap.test(fapi::ul_pusch_pdu::PUSCH_DATA_BIT)) {
+    h->pdu.tb_size = units::bytes(0);
+  }
+  *dc_out       = h->pdu.pdu.dc_position.has_value() ? static_cast<int>(*h->pdu.pdu.dc_position) : -1;
+  *tb_bytes_out = static_cast<unsigned>(h->pdu.tb_size.value());
+  return h;
+}
+
+/* The converted PDU's floating-point fields: out[0..4] = mcs_descr.target_code_rate (R x 1024), uci.alpha_scaling,
+ * uci.beta_offset_harq_ack, uci.beta_offset_csi_part1, uci.beta_offset_csi_part2. */
+void srs_ref_fapi_pusch_params(void* h, float* out)
+{
+  const auto& pdu = static_cast<fapi_pusch_handle*>(h)->pdu.pdu;
+  out[0]          = pdu.mcs_descr.target_code_rate;
+  out[1]          = pdu.uci.alpha_scaling;
+  out[2]          = pdu.uci.beta_offset_harq_ack;
+  out[3]          = pdu.uci.beta_offset_csi_part1;
+  out[4]          = pdu.uci.beta_offset_csi_part2;
+}
+
+void srs_ref_fapi_pusch_free(void* h)
+{
+  delete static_cast<fapi_pusch_handle*>(h);
+}
+
+/* pusch_processor::process of the plug-in with a converted FAPI PDU (asynchronous).  Returns the ticket. */
+int srs_ref_phy_pusch_process_fapi(void* h, void* grid, void* fapi_pdu, void* rx_buffer, uint8_t* tb,
+                                   unsigned tb_bytes)
+{
+  auto*       ctx = static_cast<pusch_ctx*>(h);
+  const auto& pdu = static_cast<fapi_pusch_handle*>(fapi_pdu)->pdu.pdu;
+  ticket*     t;
+  int         id;
+  {
+    std::lock_guard<std::mutex> lock(ctx->mtx);
+    id            = static_cast<int>(ctx->tickets.size());
+    t             = &ctx->tickets.emplace_back();
+    t->expect_sch = pdu.codeword.has_value();
+  }
+  unique_rx_buffer buf = rx_buffer ? unique_rx_buffer(*static_cast<ref_rx_buffer*>(rx_buffer)) : unique_rx_buffer();
+  ctx->proc->process(span<uint8_t>(tb, tb_bytes), std::move(buf), *t, static_cast<host_grid*>(grid)->reader, pdu);
+  return id;
+}
+
+/* The REFERENCE's pusch_processor_impl (the "auto" decoder, ZF, filter FD smoothing, interpolate TD, CFO
+ * compensation, as srs_ref_pusch_process) on the same converted FAPI PDU and grid.  Outputs as
+ * srs_ref_phy_pusch_result (uci[0..4]); returns 0 when notified (on_sch, or on_uci for a UCI-only PDU), -1 otherwise. */
+int srs_ref_pusch_process_fapi(void* grid, void* fapi_pdu, unsigned nof_prb, unsigned iterations, void* rx_buffer,
+                               uint8_t* tb, unsigned tb_bytes, double* result, double* csi, int* uci, uint8_t* ack,
+                               uint8_t* csi1)
+{
+  const auto& pdu    = static_cast<fapi_pusch_handle*>(fapi_pdu)->pdu.pdu;
+  auto        bundle = make_pusch_processor(impl::automatic, nof_prb, static_cast<unsigned>(pdu.rx_ports.size()), 4,
+                                            iterations, 0, 2, 0, true);
+  ticket      t;
+  t.expect_sch         = pdu.codeword.has_value();
+  unique_rx_buffer buf = rx_buffer ? unique_rx_buffer(*static_cast<ref_rx_buffer*>(rx_buffer)) : unique_rx_buffer();
+  bundle->proc->process(span<uint8_t>(tb, tb_bytes), std::move(buf), t, static_cast<host_grid*>(grid)->reader, pdu);
+  if (!t.done.load()) {
+    return -1;
+  }
+  const pusch_decoder_result& r  = t.sch.data;
+  const auto&                 st = r.ldpc_decoder_stats;
+  result[0]                      = r.tb_crc_ok ? 1 : 0;
+  result[1]                      = r.nof_codeblocks_total;
+  result[2]                      = st.get_nof_observations();
+  result[3]                      = st.get_mean() * st.get_nof_observations();
+  result[4]                      = st.get_min();
+  result[5]                      = st.get_max();
+  const channel_state_information& c = t.expect_sch ? t.sch.csi : t.uci.csi;
+  csi[0]                             = c.get_sinr_dB().value_or(NAN);
+  csi[1]                             = c.get_epre_dB().value_or(NAN);
+  csi[2]                             = c.get_rsrp_dB().value_or(NAN);
+  csi[3]                             = c.get_time_alignment().has_value() ? c.get_time_alignment()->to_seconds() : NAN;
+  csi[4]                             = c.get_cfo_Hz().value_or(NAN);
+  uci[0]                             = static_cast<int>(t.nof_uci);
+  uci[1]                             = static_cast<int>(t.uci.harq_ack.status);
+  uci[2]                             = static_cast<int>(t.uci.csi_part1.status);
+  uci[3]                             = static_cast<int>(t.uci.csi_part2.status);
+  uci[4]                             = static_cast<int>(t.uci.csi_part2.payload.size());
+  if (ack != nullptr) {
+    bits_out(t.uci.harq_ack.payload, ack);
+  }
+  if (csi1 != nullptr) {
+    bits_out(t.uci.csi_part1.payload, csi1);
+  }
+  return 0;
 }
 
 /* Plug-in statistics: PDUs, batches, errors, HARQ re-decodes, retransmissions. */

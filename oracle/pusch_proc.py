@@ -59,15 +59,23 @@ def describe(choice="auto"):
 
 def ref_pusch_process(grid, pdu, tb_bytes, iterations=2, choice="auto", rx_buffer=None):
     """grid uint32 [P][14][nsubc]; pdu: dict with the PuschPdu fields (transform_precoding / n_rs_id: the
-    dmrs_transform_precoding_configuration). Returns (tb, result dict)."""
+    dmrs_transform_precoding_configuration; dc_position: pdu_t::dc_position; tbs = 0 / tb_bytes = 0: a PDU without
+    codeword, UCI only). Returns (tb, result dict)."""
     if REF is None:
         raise RuntimeError("oracle/_ref not built")
     g = np.ascontiguousarray(grid, np.uint32)
     P, _, nsubc = g.shape
     tp = bool(pdu.get("transform_precoding", 0))
-    C = nof_codeblocks(tb_bytes * 8, pdu["base_graph"])
+    uci_only = tb_bytes == 0
+    C = 1 if uci_only else nof_codeblocks(tb_bytes * 8, pdu["base_graph"])
     buf = rx_buffer or RefRxBuffer(C)
-    tb = np.zeros(tb_bytes, np.uint8)
+    dc = pdu.get("dc_position")
+    if dc is not None or uci_only:
+        f = REF.srs_ref_pusch_set_options
+        f.restype = None
+        f.argtypes = [_c.c_int, _c.c_int]
+        f(-1 if dc is None else int(dc), int(uci_only))
+    tb = np.zeros(max(tb_bytes, 1), np.uint8)
     res = np.zeros(6, np.float64)
     csi = np.zeros(4, np.float64)
     ack = np.zeros(max(1, pdu.get("nof_harq_ack", 0)), np.uint8)
@@ -97,9 +105,11 @@ def ref_pusch_process(grid, pdu, tb_bytes, iterations=2, choice="auto", rx_buffe
     g.restype = _c.c_int
     g.argtypes = [_c.c_void_p, _c.c_uint, _c.c_void_p]
     n2 = g(_ptr(csi2), csi2.size, _ptr(st2))
+    tb = tb[:tb_bytes]
     return tb, dict(csi_part2=csi2[:n2].copy(), csi_part2_status=int(st2[0]),
                     tb_crc_ok=bool(res[0]), nof_codeblocks_total=int(res[1]), nof_observations=int(res[2]),
-                    iterations_sum=int(round(res[3])), iterations_min=int(res[4]), iterations_max=int(res[5]),
+                    iterations_sum=int(round(res[3])) if res[2] else 0, iterations_min=int(res[4]) if res[2] else 0,
+                    iterations_max=int(res[5]) if res[2] else 0,
                     sinr_db=csi[0], epre_db=csi[1], rsrp_db=csi[2], time_alignment_s=csi[3],
                     harq_ack=ack[:pdu.get("nof_harq_ack", 0)], csi_part1=csi1[:pdu.get("nof_csi_part1", 0)],
                     harq_ack_status=int(ust[0]), csi_part1_status=int(ust[1]))
@@ -129,10 +139,13 @@ def ue_transmit(tb, pdu, nsubc, channel=None, snr_db=None, seed=0, nof_rx_ports=
     if uci is not None:
         info = ref_ulsch_information(pdu, tbs, len(uci[2]) if len(uci) > 2 else 0)
         nch = info["nof_ul_sch_bits"] // pdu["modulation"]
-    p = osch.plan(tbs, pdu["base_graph"], pdu["rv"], pdu["modulation"], nref(tbs, pdu["base_graph"],
-                                                                            pdu.get("tbs_lbrm_bytes", 0)),
-                  L, nch)
-    cw = ref_pdsch_encode(np.asarray(tb, np.uint8), p)
+    if tbs == 0:  # UCI only: the codeword is the multiplexed UCI alone
+        p, cw = None, np.zeros(0, np.uint8)
+    else:
+        p = osch.plan(tbs, pdu["base_graph"], pdu["rv"], pdu["modulation"], nref(tbs, pdu["base_graph"],
+                                                                                pdu.get("tbs_lbrm_bytes", 0)),
+                      L, nch)
+        cw = ref_pdsch_encode(np.asarray(tb, np.uint8), p)
     if uci is not None:
         cw = ue_multiplex_uci(cw, pdu, info, nre * L * pdu["modulation"], uci[0], uci[1],
                               uci[2] if len(uci) > 2 else ())

@@ -119,6 +119,7 @@ public:
   void on_uci(const pusch_processor_result_control& uci) override
   {
     ++nof_uci;
+    uci_csi         = uci.csi;
     harq_ack_status = static_cast<int>(uci.harq_ack.status);
     csi1_status     = static_cast<int>(uci.csi_part1.status);
     csi2_status     = static_cast<int>(uci.csi_part2.status);
@@ -141,6 +142,7 @@ public:
     done   = true;
   }
   pusch_processor_result_data result;
+  channel_state_information   uci_csi;
   bool                        done    = false;
   unsigned                    nof_uci = 0;
   int                         harq_ack_status = 0, csi1_status = 0, csi2_status = 0;
@@ -242,8 +244,17 @@ std::vector<uint16_t> g_part2_descr;
 float                 g_part2_beta = 5.0F;
 std::vector<uint8_t>  g_part2_out;
 int                   g_part2_status = 0;
+// pdu_t::dc_position (-1: unset) and a PDU without codeword (UCI only) for the next srs_ref_pusch_process call
+int g_dc_position = -1;
+int g_no_codeword = 0;
 
 extern "C" {
+
+void srs_ref_pusch_set_options(int dc_position, int no_codeword)
+{
+  g_dc_position = dc_position;
+  g_no_codeword = no_codeword;
+}
 
 void srs_ref_pusch_set_csi_part2(const uint16_t* descr, unsigned nof_words, float beta)
 {
@@ -403,15 +414,24 @@ int srs_ref_pusch_process(const uint32_t* grid,
   pdu.start_symbol_index = start_symbol;
   pdu.nof_symbols        = nof_symbols;
   pdu.tbs_lbrm           = tbs_lbrm_bytes ? units::bytes(tbs_lbrm_bytes) : tbs_lbrm_default;
+  if (g_dc_position >= 0) {
+    pdu.dc_position = static_cast<unsigned>(g_dc_position);
+  }
+  const bool uci_only = g_no_codeword != 0;
+  if (uci_only) {
+    pdu.codeword.reset();
+  }
+  g_dc_position = -1;
+  g_no_codeword = 0;
 
   result_notifier  notifier;
-  unique_rx_buffer buf(*static_cast<ref_rx_buffer*>(rx_buffer));
-  bundle->proc->process(span<uint8_t>(tb, tb_bytes), std::move(buf), notifier, reader, pdu);
+  unique_rx_buffer buf = uci_only ? unique_rx_buffer() : unique_rx_buffer(*static_cast<ref_rx_buffer*>(rx_buffer));
+  bundle->proc->process(span<uint8_t>(tb, uci_only ? 0 : tb_bytes), std::move(buf), notifier, reader, pdu);
   g_part2_descr.clear();
   g_part2_beta   = 5.0F;
   g_part2_out    = notifier.csi2;
   g_part2_status = notifier.csi2_status;
-  if (!notifier.done) {
+  if (!(uci_only ? notifier.nof_uci != 0 : notifier.done)) {
     return -1;
   }
   if (uci_status_out != nullptr) {
@@ -433,7 +453,7 @@ int srs_ref_pusch_process(const uint32_t* grid,
   result[4]                      = st.get_min();
   result[5]                      = st.get_max();
   if (csi != nullptr) {
-    const channel_state_information& c = notifier.result.csi;
+    const channel_state_information& c = uci_only ? notifier.uci_csi : notifier.result.csi;
     csi[0]                             = c.get_sinr_dB().value_or(NAN);
     csi[1]                             = c.get_epre_dB().value_or(NAN);
     csi[2]                             = c.get_rsrp_dB().value_or(NAN);

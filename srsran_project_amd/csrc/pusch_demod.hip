@@ -193,6 +193,7 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
   const uint32_t* grid  = a.grids + gi * a.grid_stride + l * a.nof_subc + sc;
   const uint32_t* est   = a.estimates + gi * a.est_stride + l * a.nof_subc + sc;
   const uint32_t  plane = 14 * a.nof_subc;
+  const bool      dc    = sc == a.dc_subc; // the processor's zeroed DC estimate
 
   eq::cplx y[P], h[P * L];
 #pragma unroll
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256) void pusch_equalize_kernel(pusch_eq_args a)
     y[p] = eq::from_cbf16(grid[static_cast<uint64_t>(p) * plane]);
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-      h[p * L + l] = eq::from_cbf16(est[static_cast<uint64_t>(p * L + l) * plane]);
+      h[p * L + l] = eq::from_cbf16(dc ? 0u : est[static_cast<uint64_t>(p * L + l) * plane]);
     }
   }
   equalize_write<P, L, MMSE>(a, lt, gi, j, l, y, h);
@@ -265,13 +266,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void p
   const uint32_t  plane = 14 * a.nof_subc;
   const int       i0    = chdev::lse_index(c, l);
   const bool      two   = c.td != SRS_AMD_CHEST_TD_AVERAGE && c.td_interp[l];
+  const bool      dc    = sc == a.dc_subc; // the processor's zeroed DC estimate (pusch_processor_impl.cpp:235-249)
   // channel coefficient of port p, layer v
   auto coef = [&](int p, int v) {
     const float2*  fr = c.freq + (((static_cast<uint64_t>(gi) * P + p) * L + v) * c.nof_lse + i0) * c.nof_re + kk;
     const float2   x0 = fr[0];
     const float2   x1 = two ? fr[c.nof_re] : x0;
     const uint32_t u  = chdev::expand_pair(c, x0, x1, l, s_rot[p] != 0, s_ph[p]);
-    return eq::from_cbf16(u);
+    return eq::from_cbf16(dc ? 0u : u);
   };
   if constexpr (L >= 3 || (L == 2 && MMSE)) {
     // the normal equations built port by port as the coefficients are rebuilt (few live registers)
@@ -312,7 +314,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void p
   }
 }
 
+// One thread per (grid, estimate plane, OFDM symbol of the allocation): the DC subcarrier's estimate set to zero.
+__global__ __launch_bounds__(256) void pusch_dc_zero_kernel(uint32_t* est, uint64_t est_stride, uint32_t nof_planes,
+                                                            uint32_t nof_subc, uint32_t first_symbol,
+                                                            uint32_t nof_symbols, uint32_t dc, uint32_t total)
+{
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) {
+    return;
+  }
+  const uint32_t l  = first_symbol + t % nof_symbols;
+  const uint32_t pl = (t / nof_symbols) % nof_planes;
+  const uint32_t g  = t / (nof_symbols * nof_planes);
+  est[g * est_stride + (static_cast<uint64_t>(pl) * 14 + l) * nof_subc + dc] = 0u;
+}
+
 } // namespace
+
+hipError_t launch_pusch_dc_zero(uint32_t* estimates, uint64_t est_stride, uint32_t nof_planes, uint32_t nof_subc,
+                                uint32_t first_symbol, uint32_t nof_symbols, uint32_t dc_subc, uint32_t nof_grids,
+                                hipStream_t stream)
+{
+  const uint32_t total = nof_grids * nof_planes * nof_symbols;
+  if (total == 0 || dc_subc >= nof_subc || first_symbol + nof_symbols > 14) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(pusch_dc_zero_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, estimates, est_stride,
+                     nof_planes, nof_subc, first_symbol, nof_symbols, dc_subc, total);
+  return hipGetLastError();
+}
 
 hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers, bool mmse,
                                  uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_grids, hipStream_t stream)

@@ -206,6 +206,13 @@ static int demodulate_impl(srs_amd_pusch_demodulator*      dem,
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH demodulator completion event");
 }
 
+void srs_amd::pusch_demod_plan_set_dc(::srs_amd_pusch_demod_plan* plan, uint32_t dc_subc)
+{
+  if (plan != nullptr) {
+    plan->args.dc_subc = (plan->tp_subc == 0 && dc_subc < plan->args.nof_subc) ? dc_subc : ~0u;
+  }
+}
+
 int srs_amd::pusch_demodulate_batch_fused(::srs_amd_pusch_demodulator*      dem,
                                           const ::srs_amd_pusch_demod_plan* plan,
                                           const uint32_t*                   d_grids,
@@ -469,6 +476,7 @@ int srs_amd_pusch_demod_plan_create(srs_amd_pusch_demodulator*        dem,
   a.nof_re         = count;
   a.first_symbol   = cfg->start_symbol;
   a.first_subc     = lo * 12;
+  a.dc_subc        = ~0u;
   hipError_t e     = hipSetDevice(dem->device);
   if (e == hipSuccess) {
     e = hipMalloc(&p->d_table, table.size() * sizeof(uint32_t));

@@ -40,7 +40,19 @@ struct pusch_eq_args {
   uint64_t                        eq_stride;
   uint32_t                        tiles_x;   // fused equalizer: 256-subcarrier tiles per grid
   uint32_t                        nof_tiles; // tiles_x x grids
+  // DC subcarrier whose channel coefficients are taken as zero (pusch_processor_impl.cpp:235-249); ~0u: none
+  uint32_t                        dc_subc;
 };
+
+// The processor's DC zeroing (pusch_processor_impl.cpp:235-249) for a demodulator plan: every equalizer form then
+// reads zero channel coefficients at grid subcarrier dc_subc (~0u: none).  Plans with transform precoding ignore it.
+void pusch_demod_plan_set_dc(::srs_amd_pusch_demod_plan* plan, uint32_t dc_subc);
+
+// Zeroes subcarrier dc_subc of the expanded estimates [grid][P x L][14][nof_subc] (est_stride uint32 per grid) in
+// OFDM symbols [first_symbol, first_symbol + nof_symbols): the reference's ch_estimate after the DC step.
+hipError_t launch_pusch_dc_zero(uint32_t* estimates, uint64_t est_stride, uint32_t nof_planes, uint32_t nof_subc,
+                                uint32_t first_symbol, uint32_t nof_symbols, uint32_t dc_subc, uint32_t nof_grids,
+                                hipStream_t stream);
 
 
 hipError_t launch_pusch_equalize(const pusch_eq_args& a, uint32_t nof_ports, uint32_t nof_layers, bool mmse,

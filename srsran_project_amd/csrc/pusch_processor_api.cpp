@@ -67,6 +67,9 @@ struct srs_amd_pusch_processor_plan {
   srs_amd_pusch_decoder_config dec_cfg{};
   uint64_t                     soft_bytes = 0;
   bool                         fusable    = false; // the fused estimator-equalizer path covers this PDU
+  bool                         has_sch    = true;  // a codeword (tbs != 0); UCI-only PUSCH otherwise
+  uint32_t                     dc_subc    = ~0u;   // DC subcarrier zeroed in the estimates (CP-OFDM only)
+  uint32_t                     dummy_sch_bits = 0; // UCI only: the demultiplexer's discarded UL-SCH stream length
   // UCI on PUSCH: multiplexing geometry (get_ulsch_information), demultiplexer plan, codeword bits
   bool                         uci        = false;
   srs_amd_ulsch_info           info{};
@@ -151,14 +154,15 @@ int plan_part2(srs_amd_pusch_processor*                                    proc,
     return rc;
   }
   const uint32_t qm_bits = pl->pdu.modulation < 2 ? 1u : static_cast<uint32_t>(pl->pdu.modulation);
-  if (total != pl->cw_bits || sch_bits != g.info.nof_ul_sch_bits) {
+  if (total != pl->cw_bits || (pl->has_sch && sch_bits != g.info.nof_ul_sch_bits)) {
     srs_amd_ulsch_demux_plan_destroy(g.demux);
     return fail(SRS_AMD_EINVAL, "CSI part 2 multiplexing geometry mismatch (%u / %u UL-SCH bits).", sch_bits,
                 g.info.nof_ul_sch_bits);
   }
-  rc = srs_amd_sch_plan_compute(&g.sch, pl->pdu.tbs, pl->pdu.base_graph, pl->pdu.rv,
-                                static_cast<uint32_t>(pl->pdu.modulation), pl->nref, pl->pdu.nof_tx_layers,
-                                sch_bits / qm_bits);
+  rc = !pl->has_sch ? SRS_AMD_OK
+                    : srs_amd_sch_plan_compute(&g.sch, pl->pdu.tbs, pl->pdu.base_graph, pl->pdu.rv,
+                                               static_cast<uint32_t>(pl->pdu.modulation), pl->nref,
+                                               pl->pdu.nof_tx_layers, sch_bits / qm_bits);
   if (rc != SRS_AMD_OK) {
     srs_amd_ulsch_demux_plan_destroy(g.demux);
     return rc;
@@ -264,15 +268,22 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
   if (pdu->bwp_start_rb + pdu->bwp_size_rb > nof_subc / 12) {
     return fail(SRS_AMD_EINVAL, "The BWP exceeds the resource grid.");
   }
-  if (pdu->tbs == 0 || pdu->tbs % 8 != 0) {
+  // no codeword (tbs = 0): UCI only (pusch_processor_impl.cpp:305-324), which needs some UCI to carry
+  const bool has_sch = pdu->tbs != 0;
+  if (pdu->tbs % 8 != 0 || (!has_sch && pdu->nof_harq_ack == 0 && pdu->nof_csi_part1 == 0)) {
     return fail(SRS_AMD_EINVAL, "Invalid transport block size (i.e., %u).", pdu->tbs);
   }
-  if (pdu->base_graph != 1 && pdu->base_graph != 2) {
+  if (has_sch && pdu->base_graph != 1 && pdu->base_graph != 2) {
     return fail(SRS_AMD_EINVAL, "Invalid base graph.");
   }
   auto* pl     = new srs_amd_pusch_processor_plan();
   pl->pdu      = *pdu;
   pl->nof_subc = nof_subc;
+  pl->has_sch  = has_sch;
+  // DC subcarrier (pusch_processor_impl.cpp:235-249): zeroed in the estimates of CP-OFDM PDUs inside the grid
+  if (!tp && pdu->has_dc_position && pdu->dc_position < nof_subc) {
+    pl->dc_subc = pdu->dc_position;
+  }
   // DM-RS estimator configuration (pusch_processor_impl.cpp:184-200)
   const uint32_t crb0       = pdu->bwp_start_rb + pdu->rb_start;
   srs_amd_pusch_chest_config& c = pl->chest_cfg;
@@ -322,12 +333,17 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
     delete pl;
     return rc;
   }
+  pusch_demod_plan_set_dc(pl->demod_plan, pl->dc_subc);
   // UCI multiplexing (pusch_processor_impl.cpp:252-299): the geometry of get_ulsch_information, the
   // demultiplexer's placement; the UL-SCH then gets nof_ul_sch_bits of the codeword's bits
   const uint32_t qm_bits  = pdu->modulation < 2 ? 1u : static_cast<uint32_t>(pdu->modulation);
   pl->cw_bits             = pl->nof_re * pdu->nof_tx_layers * qm_bits;
   uint32_t       sch_bits = pl->cw_bits;
   pl->uci                 = pdu->nof_harq_ack != 0 || pdu->nof_csi_part1 != 0;
+  // the allocation overlaps the DC (pusch_processor_impl.cpp:262-286 contains_dc: nof_dc_overlap_bits of the
+  // multiplexing geometry, informational)
+  const uint32_t dc_prb   = pdu->has_dc_position ? pdu->dc_position / 12 : ~0u;
+  const int32_t  with_dc  = dc_prb >= crb0 && dc_prb < crb0 + pdu->rb_count ? 1 : 0;
   pl->csi2                = pdu->nof_csi_part1 != 0 && pdu->csi_part2_size.nof_entries != 0;
   if (pdu->csi_part2_size.nof_entries > 2) {
     delete pl;
@@ -370,6 +386,7 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
     uc.nof_cdm_groups_without_data = ncdm;
     uc.nof_layers                  = pdu->nof_tx_layers;
     uc.beta_offset_csi_part2       = pdu->beta_offset_csi_part2;
+    uc.contains_dc                 = with_dc;
     rc                             = srs_amd_ulsch_information(&uc, &pl->info);
     pl->ucfg                       = uc;
     srs_amd_ulsch_demux_config dx{};
@@ -392,7 +409,7 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
     if (rc == SRS_AMD_OK) {
       rc = srs_amd_ulsch_demux_plan_create(proc->demux, &dx, &pl->demux_plan, &total, &sch_bits);
     }
-    if (rc == SRS_AMD_OK && (total != pl->cw_bits || sch_bits != pl->info.nof_ul_sch_bits)) {
+    if (rc == SRS_AMD_OK && (total != pl->cw_bits || (has_sch && sch_bits != pl->info.nof_ul_sch_bits))) {
       rc = fail(SRS_AMD_EINVAL, "UCI multiplexing geometry mismatch (%u / %u codeword bits, %u / %u UL-SCH bits).",
                 total, pl->cw_bits, sch_bits, pl->info.nof_ul_sch_bits);
     }
@@ -402,11 +419,18 @@ int srs_amd_pusch_processor_plan_create(srs_amd_pusch_processor*       proc,
     }
   }
   // decoder configuration (pusch_processor_impl.cpp:322-347): the UL-SCH's share of the codeword
-  const uint32_t C       = nof_codeblocks(pdu->tbs, pdu->base_graph);
-  const uint32_t tbs_lbrm = pdu->tbs_lbrm_bytes ? pdu->tbs_lbrm_bytes : 159749u; // tbs_lbrm_default
-  pl->nref = compute_N_ref(tbs_lbrm, C);
-  rc = srs_amd_sch_plan_compute(&pl->sch, pdu->tbs, pdu->base_graph, pdu->rv, static_cast<uint32_t>(pdu->modulation),
-                                pl->nref, pdu->nof_tx_layers, sch_bits / qm_bits);
+  if (has_sch) {
+    const uint32_t C        = nof_codeblocks(pdu->tbs, pdu->base_graph);
+    const uint32_t tbs_lbrm = pdu->tbs_lbrm_bytes ? pdu->tbs_lbrm_bytes : 159749u; // tbs_lbrm_default
+    pl->nref                = compute_N_ref(tbs_lbrm, C);
+    rc = srs_amd_sch_plan_compute(&pl->sch, pdu->tbs, pdu->base_graph, pdu->rv,
+                                  static_cast<uint32_t>(pdu->modulation), pl->nref, pdu->nof_tx_layers,
+                                  sch_bits / qm_bits);
+  } else {
+    // UCI only: REs the UCI leaves free go to the demultiplexer's UL-SCH stream, which nothing decodes (the
+    // reference's decoder_buffer_dummy, pusch_processor_impl.cpp:300-305): a discarded row of that length
+    pl->dummy_sch_bits = sch_bits;
+  }
   if (rc != SRS_AMD_OK) {
     delete pl;
     return rc;
@@ -435,17 +459,19 @@ void srs_amd_pusch_processor_plan_destroy(srs_amd_pusch_processor_plan* plan)
 
 namespace {
 
+// chest: the estimator configuration to run (the plan's, or a copy in another slot); nullptr: the plan's.
 int process_batch_locked(srs_amd_pusch_processor*            proc,
-                                const srs_amd_pusch_processor_plan* plan,
-                                const uint32_t*                     d_grids,
-                                uint64_t                            grid_stride,
-                                uint32_t                            nof_grids,
-                                uint8_t*                            d_tbs,
-                                uint32_t                            tb_stride,
-                                srs_amd_pusch_processor_result*     d_results,
-                                int8_t*                             d_soft,
-                                const srs_amd_pusch_intermediates*  io,
-                                void*                               stream)
+                         const srs_amd_pusch_processor_plan* plan,
+                         const uint32_t*                     d_grids,
+                         uint64_t                            grid_stride,
+                         uint32_t                            nof_grids,
+                         uint8_t*                            d_tbs,
+                         uint32_t                            tb_stride,
+                         srs_amd_pusch_processor_result*     d_results,
+                         int8_t*                             d_soft,
+                         const srs_amd_pusch_intermediates*  io,
+                         void*                               stream,
+                         const srs_amd_pusch_chest_config*   chest = nullptr)
 {
   if (proc == nullptr || plan == nullptr) {
     return fail(SRS_AMD_EINVAL, "null argument");
@@ -453,7 +479,7 @@ int process_batch_locked(srs_amd_pusch_processor*            proc,
   if (nof_grids == 0) {
     return SRS_AMD_OK;
   }
-  if (d_grids == nullptr || d_tbs == nullptr || d_results == nullptr) {
+  if (d_grids == nullptr || (d_tbs == nullptr && plan->has_sch) || d_results == nullptr) {
     return fail(SRS_AMD_EINVAL, "null device buffer");
   }
   const uint32_t P     = plan->pdu.nof_rx_ports;
@@ -462,7 +488,8 @@ int process_batch_locked(srs_amd_pusch_processor*            proc,
   if (nof_grids > 1 && (grid_stride < P * plane || tb_stride < plan->pdu.tbs / 8)) {
     return fail(SRS_AMD_EINVAL, "grid or transport block stride too small");
   }
-  const uint32_t G            = plan->sch.cw_length;
+  const srs_amd_pusch_chest_config* cc = chest != nullptr ? chest : &plan->chest_cfg;
+  const uint32_t G            = plan->has_sch ? plan->sch.cw_length : plan->dummy_sch_bits;
   const bool     uci          = plan->uci;
   const bool     own_est      = io == nullptr || io->d_estimates == nullptr;
   // Without a caller estimate buffer the equalizer rebuilds each RE's estimate from the estimator's
@@ -534,15 +561,22 @@ int process_batch_locked(srs_amd_pusch_processor*            proc,
   int rc;
   if (fused) {
     chest_args view;
-    rc = chest_estimate_batch_unexpanded(proc->chest, &plan->chest_cfg, d_grids, grid_stride, P, plan->nof_subc,
-                                         nof_grids, st, stream, &view);
+    rc = chest_estimate_batch_unexpanded(proc->chest, cc, d_grids, grid_stride, P, plan->nof_subc, nof_grids, st,
+                                         stream, &view);
     if (rc == SRS_AMD_OK) {
       rc = pusch_demodulate_batch_fused(proc->demod, plan->demod_plan, d_grids, grid_stride, view, st, dem_rows,
                                         dem_stride, nof_grids, stream);
     }
   } else {
-    rc = srs_amd_pusch_chest_estimate_batch(proc->chest, &plan->chest_cfg, d_grids, grid_stride, P, plan->nof_subc,
-                                            nof_grids, est, est_stride, st, stream);
+    rc = srs_amd_pusch_chest_estimate_batch(proc->chest, cc, d_grids, grid_stride, P, plan->nof_subc, nof_grids, est,
+                                            est_stride, st, stream);
+    // the DC step of pusch_processor_impl.cpp:235-249 on the caller's estimates (the equalizer reads the DC
+    // subcarrier as zero in any case)
+    if (rc == SRS_AMD_OK && !own_est && plan->dc_subc != ~0u) {
+      e  = launch_pusch_dc_zero(est, est_stride, P * L, plan->nof_subc, plan->pdu.start_symbol_index,
+                                plan->pdu.nof_symbols, plan->dc_subc, nof_grids, s);
+      rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_dc_zero_kernel launch");
+    }
     if (rc == SRS_AMD_OK) {
       rc = srs_amd_pusch_demodulate_batch(proc->demod, plan->demod_plan, d_grids, grid_stride, est, est_stride, st,
                                           dem_rows, dem_stride, nof_grids, stream);
@@ -571,11 +605,12 @@ int process_batch_locked(srs_amd_pusch_processor*            proc,
   }
   // CSI part 2 sizes from the decoded CSI part 1 (one readback), grids without CSI part 2 keep the plan's geometry
   std::vector<uint32_t> n2(nof_grids, 0);
+  std::vector<int32_t>  st1; // statuses [grid][4] read back with CSI part 1
   if (rc == SRS_AMD_OK && plan->csi2) {
     const bool     out1 = io != nullptr && io->d_csi_part1 != nullptr;
     const uint8_t* p1   = out1 ? io->d_csi_part1 : proc->uci_payload.as<uint8_t>() + K_ack;
     const uint64_t p1s  = out1 ? io->csi_part1_stride : pay_stride;
-    std::vector<int32_t> st1(static_cast<size_t>(nof_grids) * 4);
+    st1.assign(static_cast<size_t>(nof_grids) * 4, 0);
     std::vector<uint8_t> part1(static_cast<size_t>(nof_grids) * K_csi1);
     e = hipMemcpyAsync(st1.data(), proc->uci_status.ptr, st1.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) {
@@ -597,21 +632,30 @@ int process_batch_locked(srs_amd_pusch_processor*            proc,
     }
   }
   const bool any2 = std::any_of(n2.begin(), n2.end(), [](uint32_t v) { return v != 0; });
-  if (rc == SRS_AMD_OK && !any2) {
+  // UCI only: no UL-SCH decoding (pusch_processor_impl.cpp:305: has_sch_data), an empty decoder result
+  if (rc == SRS_AMD_OK && !plan->has_sch) {
+    e  = hipMemsetAsync(proc->dec_results.ptr, 0, sizeof(srs_amd_pusch_decoder_result) * nof_grids, s);
+    rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH processor UCI-only result");
+  }
+  if (rc == SRS_AMD_OK && !any2 && plan->has_sch) {
     rc = srs_amd_pusch_decode_batch(proc->dec, &plan->sch, &plan->dec_cfg, d_tbs, tb_stride,
                                     proc->dec_results.as<srs_amd_pusch_decoder_result>(), llrs, llr_stride, d_soft,
                                     cb_iters, nof_grids, stream);
   }
-  // grid by grid when some CSI part 2 is present: each size has its own UL-SCH geometry; the sizes are uploaded
-  // once (pinned staging) into the statuses' fourth column
+  // grid by grid when some CSI part 2 is present: each size has its own UL-SCH geometry; the sizes go into the
+  // statuses' fourth column: the statuses read back above (HARQ-ACK, CSI part 1) with the sizes, uploaded whole
+  // by the copy kernel (upload_pinned: no small SDMA transfer)
   if (rc == SRS_AMD_OK && any2) {
-    e = proc->stage2.acquire(sizeof(int32_t) * nof_grids);
+    e = proc->stage2.acquire(4 * sizeof(int32_t) * nof_grids);
     if (e == hipSuccess) {
       for (uint32_t g = 0; g < nof_grids; ++g) {
-        *proc->stage2.at<int32_t>(sizeof(int32_t) * g) = static_cast<int32_t>(n2[g]);
+        int32_t* row = proc->stage2.at<int32_t>(4 * sizeof(int32_t) * g);
+        for (uint32_t k = 0; k < 4; ++k) {
+          row[k] = st1[4 * g + k];
+        }
+        row[3] = static_cast<int32_t>(n2[g]);
       }
-      e = proc->stage2.upload_rows(proc->uci_status.as<int32_t>() + 3, 4 * sizeof(int32_t), sizeof(int32_t),
-                                   nof_grids, s);
+      e = proc->stage2.upload(proc->uci_status.ptr, 4 * sizeof(int32_t) * nof_grids, s);
     }
     rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "CSI part 2 size upload");
   }
@@ -644,7 +688,7 @@ int process_batch_locked(srs_amd_pusch_processor*            proc,
                                       stream);
       }
     }
-    if (rc == SRS_AMD_OK) {
+    if (rc == SRS_AMD_OK && plan->has_sch) {
       rc = srs_amd_pusch_decode_batch(proc->dec, sch, &plan->dec_cfg, d_tbs + static_cast<uint64_t>(g) * tb_stride,
                                       tb_stride, proc->dec_results.as<srs_amd_pusch_decoder_result>() + g, row,
                                       llr_stride, d_soft ? d_soft + g * plan->soft_bytes : nullptr,
@@ -735,12 +779,26 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     if (pdus[i].grid >= nof_grids || (nof_grids > 1 && grid_stride < 14ull * nof_subc * P)) {
       return fail(SRS_AMD_EINVAL, "PDU %u: grid index or grid stride out of range", i);
     }
-    if (!pl->dec_cfg.new_data && pdus[i].d_soft == nullptr) {
+    if (pl->has_sch && !pl->dec_cfg.new_data && pdus[i].d_soft == nullptr) {
       return fail(SRS_AMD_EINVAL, "PDU %u: a HARQ retransmission needs its soft buffer (d_soft)", i);
+    }
+    if (pdus[i].has_slot && (pdus[i].numerology > 4 || pdus[i].slot_index >= (10u << pdus[i].numerology))) {
+      return fail(SRS_AMD_EINVAL, "PDU %u: invalid slot %u of numerology %u", i, pdus[i].slot_index,
+                  pdus[i].numerology);
     }
     const bool f = proc->fuse && pl->fusable && P <= STATS_STRIDE && pl->dec_cfg.new_data && !pl->uci &&
                    pl->pdu.transform_precoding == 0 && pdus[i].d_soft == nullptr;
     (f ? fused : others).push_back(i);
+  }
+  // each PDU's estimator configuration: its plan's, moved to the PDU's own slot when it carries one (the DM-RS
+  // sequences are the only per-slot quantity; PDUs of several slots may share a plan within one call)
+  std::vector<srs_amd_pusch_chest_config> ccfg(nof_pdus);
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    ccfg[i] = pdus[i].plan->chest_cfg;
+    if (pdus[i].has_slot) {
+      ccfg[i].numerology = pdus[i].numerology;
+      ccfg[i].slot_index = pdus[i].slot_index;
+    }
   }
   auto                        s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(proc->mtx);
@@ -761,7 +819,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     }
     const int rc = process_batch_locked(proc, pl, d_grids + pdus[i].grid * grid_stride, grid_stride, 1,
                                         d_tbs + pdus[i].tb_offset, std::max<uint32_t>(pl->pdu.tbs / 8, 1),
-                                        d_results + i, pdus[i].d_soft, &x, stream);
+                                        d_results + i, pdus[i].d_soft, &x, stream, &ccfg[i]);
     if (rc != SRS_AMD_OK) {
       return rc;
     }
@@ -810,7 +868,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
   std::vector<chest_slot_item> citems(n);
   for (uint32_t k = 0; k != n; ++k) {
     const srs_amd_pusch_slot_pdu& u = pdus[fused[k]];
-    citems[k] = chest_slot_item{&u.plan->chest_cfg, d_grids + u.grid * grid_stride, u.plan->pdu.nof_rx_ports,
+    citems[k] = chest_slot_item{&ccfg[fused[k]], d_grids + u.grid * grid_stride, u.plan->pdu.nof_rx_ports,
                                 stats_of(k)};
   }
   std::vector<chest_args> views(n);

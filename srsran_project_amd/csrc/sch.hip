@@ -542,6 +542,11 @@ __global__ __launch_bounds__(64) void asm_final_kernel(assemble_args a, uint32_t
   }
   const tb_view  v = view_of(a, t);
   const uint32_t C = v.C;
+  // the accumulator is read and cleared on every path (the merged form relies on zero accumulators at its start)
+  const uint32_t acc = a.acc != nullptr ? a.acc[t] : 0u;
+  if (a.acc != nullptr) {
+    a.acc[t] = 0;
+  }
   if (C == 1 || a.results[t].nof_codeblocks_crc_ok != C) {
     return;
   }
@@ -553,9 +558,8 @@ __global__ __launch_bounds__(64) void asm_final_kernel(assemble_args a, uint32_t
   for (uint32_t k = 0; k < 24; ++k) {
     chk = (chk << 1) | bit_at(m, off + k);
   }
-  const bool ok           = a.acc[t] == chk;
+  const bool ok           = acc == chk;
   a.results[t].tb_crc_ok  = ok ? 1 : 0;
-  a.acc[t]                = 0; // cleared for the next call (asm_merged_kernel does not clear it)
   if (!ok && a.soft) {
     for (uint32_t r = 0; r < C; ++r) {
       uint8_t* srow = a.soft + static_cast<size_t>(v.row0 + r) * a.lay.row_bytes;

@@ -18,12 +18,19 @@ namespace srs_amd {
 
 namespace {
 
-// one wave that waits `ticks` of the constant-rate wall clock (s_memrealtime); no memory traffic
-__global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks)
+// one wave that waits `ticks` of the constant-rate wall clock (s_memrealtime) and stamps its start and end into
+// stamp[0..1] (vector stores by lane 0)
+__global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks, uint64_t* stamp)
 {
   const uint64_t t0 = wall_clock64();
-  while (wall_clock64() - t0 < ticks) {
+  uint64_t       t1 = t0;
+  while (t1 - t0 < ticks) {
     __builtin_amdgcn_s_sleep(8);
+    t1 = wall_clock64();
+  }
+  if (threadIdx.x == 0) {
+    stamp[0] = t0;
+    stamp[1] = t1;
   }
 }
 
@@ -63,8 +70,11 @@ hipError_t upload_pinned(void* d, const void* h, size_t n, hipStream_t s)
 
 hipError_t streams_run_concurrently(hipStream_t a, hipStream_t b, bool& concurrent)
 {
+  // Two spin kernels, one per stream, b's released by an event recorded on a just before a's spin: they overlap in
+  // time exactly when the streams run concurrently.  The overlap is read from the kernels' own wall-clock stamps,
+  // so neither the cross-queue event latency (~10-50 us) nor other work on the device enters the verdict.
   concurrent         = true;
-  constexpr float MS = 0.1f; // each spin: long against a cross-queue event wait (~10-50 us)
+  constexpr float MS = 0.2f;
   int             device = 0, khz = 0;
   hipError_t      e      = hipGetDevice(&device);
   if (e == hipSuccess) {
@@ -73,49 +83,41 @@ hipError_t streams_run_concurrently(hipStream_t a, hipStream_t b, bool& concurre
   if (e != hipSuccess || khz <= 0) {
     return e;
   }
-  hipEvent_t ev[4] = {};
-  for (int i = 0; i < 4 && e == hipSuccess; ++i) {
-    e = hipEventCreate(&ev[i]);
+  uint64_t*  d_stamp = nullptr;
+  hipEvent_t ev      = nullptr;
+  e                  = hipMalloc(&d_stamp, 4 * sizeof(uint64_t));
+  if (e == hipSuccess) {
+    e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   }
   const uint64_t ticks = static_cast<uint64_t>(MS * static_cast<float>(khz));
   if (e == hipSuccess) {
-    e = hipEventRecord(ev[0], a); // b starts after a's earlier work, together with a's spin
+    e = hipEventRecord(ev, a); // b starts after a's earlier work, together with a's spin
   }
   if (e == hipSuccess) {
-    e = hipStreamWaitEvent(b, ev[0], 0);
+    e = hipStreamWaitEvent(b, ev, 0);
   }
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, a, ticks);
-    hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, b, ticks);
+    hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, a, ticks, d_stamp);
+    hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, b, ticks, d_stamp + 2);
     e = hipGetLastError();
   }
   if (e == hipSuccess) {
-    e = hipEventRecord(ev[1], a);
+    e = hipStreamSynchronize(a);
   }
   if (e == hipSuccess) {
-    e = hipEventRecord(ev[2], b);
+    e = hipStreamSynchronize(b);
+  }
+  uint64_t h[4] = {};
+  if (e == hipSuccess) {
+    e = hipMemcpy(h, d_stamp, sizeof(h), hipMemcpyDeviceToHost);
   }
   if (e == hipSuccess) {
-    e = hipEventSynchronize(ev[1]);
+    concurrent = h[2] < h[1] && h[0] < h[3]; // the two spins' [start, end) intervals intersect
   }
-  if (e == hipSuccess) {
-    e = hipEventSynchronize(ev[2]);
+  if (ev != nullptr) {
+    (void)hipEventDestroy(ev);
   }
-  float ta = 0.f, tb = 0.f;
-  if (e == hipSuccess) {
-    e = hipEventElapsedTime(&ta, ev[0], ev[1]);
-  }
-  if (e == hipSuccess) {
-    e = hipEventElapsedTime(&tb, ev[0], ev[2]);
-  }
-  if (e == hipSuccess) {
-    concurrent = (ta > tb ? ta : tb) < 1.5f * MS;
-  }
-  for (hipEvent_t x : ev) {
-    if (x != nullptr) {
-      (void)hipEventDestroy(x);
-    }
-  }
+  (void)hipFree(d_stamp);
   return e;
 }
 

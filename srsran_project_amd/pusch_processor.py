@@ -92,7 +92,8 @@ class PuschPdu(ctypes.Structure):
                                         "transform_precoding", "n_rs_id", "nof_harq_ack", "nof_csi_part1")] + \
         [("alpha_scaling", ctypes.c_float), ("beta_offset_harq_ack", ctypes.c_float),
          ("beta_offset_csi_part1", ctypes.c_float), ("beta_offset_csi_part2", ctypes.c_float),
-         ("csi_part2_size", UciPart2SizeDescription)]
+         ("csi_part2_size", UciPart2SizeDescription), ("has_dc_position", ctypes.c_uint32),
+         ("dc_position", ctypes.c_uint32)]
 
 
 class PuschProcessorResult(ctypes.Structure):
@@ -122,7 +123,8 @@ class PuschSlotPdu(ctypes.Structure):
     """``srs_amd_pusch_slot_pdu``: one PDU of srs_amd_pusch_process_slot."""
 
     _fields_ = [("plan", ctypes.c_void_p), ("grid", ctypes.c_uint32), ("cb_offset", ctypes.c_uint32),
-                ("tb_offset", ctypes.c_uint64), ("d_soft", ctypes.c_void_p), ("uci_offset", ctypes.c_uint64)]
+                ("tb_offset", ctypes.c_uint64), ("d_soft", ctypes.c_void_p), ("uci_offset", ctypes.c_uint64),
+                ("has_slot", ctypes.c_uint32), ("numerology", ctypes.c_uint32), ("slot_index", ctypes.c_uint32)]
 
 
 class PuschSlotIo(ctypes.Structure):
@@ -139,8 +141,11 @@ def make_pdu(**kw):
              nof_cdm_groups_without_data=2, rb_start=0, rb_count=None, start_symbol_index=0, nof_symbols=14,
              tbs_lbrm_bytes=0, tbs=0, transform_precoding=0, n_rs_id=0, nof_harq_ack=0, nof_csi_part1=0,
              alpha_scaling=1.0, beta_offset_harq_ack=5.0, beta_offset_csi_part1=5.0, beta_offset_csi_part2=5.0,
-             csi_part2_size=None)
+             csi_part2_size=None, dc_position=None)
     d.update(kw)
+    dc = d.pop("dc_position")
+    if dc is not None:  # pdu_t::dc_position (unset: None)
+        d["has_dc_position"], d["dc_position"] = 1, int(dc)
     if d["rb_count"] is None:
         d["rb_count"] = d["bwp_size_rb"] - d["rb_start"]
     p = PuschPdu()
@@ -339,7 +344,8 @@ class PuschSlot:
     aligned) of a tb_total-byte buffer, its codeblock iteration counts at cb_offsets[u] of cb_total, its UCI payload
     row at uci_offsets[u] of uci_total."""
 
-    def __init__(self, pdus):
+    def __init__(self, pdus, slots=None):
+        """slots: optional per-PDU (numerology, slot_index) (srs_amd_pusch_slot_pdu has_slot), None: the plans'."""
         self.plans = [p[0] for p in pdus]  # keep the plans alive
         self.soft = [p[2] if len(p) > 2 else None for p in pdus]
         self.n = len(pdus)
@@ -359,6 +365,9 @@ class PuschSlot:
             soft = self.soft[i]
             self.arr[i] = PuschSlotPdu(p[0]._h.value, int(p[1]), self.cb_offsets[i], self.offsets[i],
                                        None if soft is None else soft.data_ptr(), self.uci_offsets[i])
+            if slots is not None and slots[i] is not None:
+                self.arr[i].has_slot = 1
+                self.arr[i].numerology, self.arr[i].slot_index = slots[i]
 
 
 def parse_results(results):

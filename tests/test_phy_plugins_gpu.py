@@ -286,3 +286,136 @@ def test_plugin_throughput_64_cells(phy):
     with open("gpurun_out/plugin_bench.json", "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
+
+
+# ---- PDUs as the reference's FAPI adaptor produces them ----
+
+FAPI_DC = 1638  # tx_direct_current_location: subcarrier 12 x 273 / 2 (scheduler default initial_ul_dc_offset = center)
+
+
+def _fapi_ues():
+    """(kind, FAPI fields) of one slot's PUSCH PDUs on a 273-PRB, four-antenna cell: every PDU carries the cell's
+    tx_direct_current_location as the MAC -> FAPI translator sets it."""
+    common = dict(bwp_start=0, bwp_size=273, numerology=1, sfn=0, num_layers=1, ul_dmrs_symb_pos=(1 << 2) | (1 << 11),
+                  dmrs_type=1, nscid=0, num_dmrs_cdm_grps_no_data=2, start_symbol_index=0, nr_of_symbols=14,
+                  tx_direct_current_location=FAPI_DC, has_data=1, rv_index=0, new_data=1, ldpc_base_graph=1,
+                  tb_size_lbrm_bytes=159749, alpha_scaling=3, beta_offset_harq_ack=7, beta_offset_csi1=13,
+                  beta_offset_csi2=13, num_rx_ant=4)
+    return [
+        ("dc_data", dict(common, rnti=0x4601, nid_pusch=21, scrambling_id=210, qm=4, target_code_rate=4900,
+                         rb_start=110, rb_size=50, harq_process_id=1)),
+        ("uci_data", dict(common, rnti=0x4602, nid_pusch=22, scrambling_id=220, qm=4, target_code_rate=4900,
+                          rb_start=0, rb_size=60, harq_process_id=2, has_uci=1, harq_ack_bit_length=3,
+                          csi_part1_bit_length=12)),
+        ("uci_only", dict(common, rnti=0x4603, nid_pusch=23, scrambling_id=230, qm=2, target_code_rate=1200,
+                          rb_start=200, rb_size=10, has_data=0, has_uci=1, harq_ack_bit_length=5,
+                          csi_part1_bit_length=12)),
+        ("tp_dc", dict(common, rnti=0x4604, nid_pusch=24, qm=4, target_code_rate=4340, transform_precoding=1,
+                       dmrs_identity=99, rb_start=125, rb_size=25, harq_process_id=3)),
+        ("two_layer", dict(common, rnti=0x4605, nid_pusch=25, scrambling_id=250, nscid=1, qm=6,
+                           target_code_rate=5670, num_layers=2, rb_start=160, rb_size=40, harq_process_id=4,
+                           ul_dmrs_symb_pos=(1 << 2) | (1 << 7) | (1 << 11))),
+    ]
+
+
+def _fapi_slot(ophy, slot, seed, kinds=None):
+    """The slot's FAPI PDUs converted by convert_pusch_fapi_to_phy, the received grid (each UE from the reference's
+    transmit classes, summed, AWGN) and what each UE sent."""
+    from pusch_slot_cases import NSUBC, _bf16, _chan, _cplx, tbs_of
+    from oracle.pusch_proc import ue_transmit, ue_transmit_tp
+
+    rng = np.random.default_rng(seed)
+    z = np.zeros((4, 14, NSUBC), np.complex128)
+    out = []
+    for u, (kind, f) in enumerate(_fapi_ues()):
+        if kinds is not None and kind not in kinds:
+            continue
+        pdu = dict(numerology=1, slot_index=slot, rnti=f["rnti"], bwp_start_rb=0, bwp_size_rb=273, modulation=f["qm"],
+                   target_code_rate=f["target_code_rate"] / 10.0, rv=0, new_data=1, n_id=f["nid_pusch"],
+                   nof_tx_layers=f["num_layers"], nof_rx_ports=4, dmrs_symbol_mask=f["ul_dmrs_symb_pos"], dmrs_type=1,
+                   scrambling_id=f.get("scrambling_id", 0), n_scid=f["nscid"], nof_cdm_groups_without_data=2,
+                   rb_start=f["rb_start"], rb_count=f["rb_size"], start_symbol_index=0, nof_symbols=14,
+                   transform_precoding=f.get("transform_precoding", 0), n_rs_id=f.get("dmrs_identity", 0))
+        tbs = tbs_of(pdu) if f["has_data"] else 0
+        bg = 1 if tbs > 3824 or not tbs else 2
+        f = dict(f, slot=slot, tb_size=tbs // 8, ldpc_base_graph=bg)
+        fp = ophy.FapiPuschPdu(**f)
+        assert fp.dc_position == FAPI_DC, kind  # the adaptor forwards the DC location to the PHY
+        pdu.update(fp.params, base_graph=bg, tbs=tbs, nof_harq_ack=f.get("harq_ack_bit_length", 0),
+                   nof_csi_part1=f.get("csi_part1_bit_length", 0))
+        tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+        uci = None
+        if f.get("has_uci"):
+            uci = (rng.integers(0, 2, pdu["nof_harq_ack"]).astype(np.uint8),
+                   rng.integers(0, 2, pdu["nof_csi_part1"]).astype(np.uint8))
+        if pdu["transform_precoding"]:
+            g, _ = ue_transmit_tp(tb, pdu, NSUBC, channel=np.array([0.8, 0.3j, -0.5, 0.6 + 0.2j]))
+        else:
+            g, _ = ue_transmit(tb, pdu, NSUBC, channel=_chan(pdu["nof_tx_layers"], 4, 60 + u), uci=uci)
+        zu = _cplx(g)
+        z += zu / np.sqrt(float(np.mean(np.abs(zu[np.abs(zu) > 0]) ** 2)))
+        out.append((kind, fp, tb, uci))
+    sigma2 = 10 ** (-26.0 / 10)
+    z += np.sqrt(sigma2 / 2) * (rng.normal(size=z.shape) + 1j * rng.normal(size=z.shape))
+    return _bf16(z), out
+
+
+def test_pusch_plugin_fapi_pdus_dc_uci_only_vs_reference(phy):
+    """PUSCH PDUs produced by the reference's own FAPI -> PHY conversion (convert_pusch_fapi_to_phy,
+    lib/fapi_adaptor/phy/messages/pusch.cpp, compiled into the oracle) from FAPI PDUs carrying
+    tx_direct_current_location = 1638 -- a data PDU whose allocation contains the DC, a data + UCI PDU, a UCI-only PDU
+    (no data bit), a DFT-s-OFDM PDU over the DC, a two-layer PDU -- through the plug-in's pusch_processor::process,
+    equal to the reference's pusch_processor_impl on the same converted PDUs and grid: TB, CRC, LDPC statistics, UCI
+    payloads / statuses (on_uci alone for the UCI-only PDU), CSI."""
+    ophy, oracle = phy
+    plug = ophy.PuschProcessorPlugin(device=0, iterations=ITERS)
+    for slot in (3, 4):
+        grid, ues = _fapi_slot(ophy, slot, seed=slot)
+        g = ophy.Grid(grid)
+        tickets = [plug.process_fapi(g, fp) for _, fp, _, _ in ues]
+        plug.flush()
+        plug.wait()
+        for (kind, fp, tb_sent, uci), (t, tb) in zip(ues, tickets):
+            tag = "slot %d %s" % (slot, kind)
+            want_tb, want = ophy.ref_pusch_process_fapi(g, fp, iterations=ITERS)
+            got = plug.result(t, fp.fapi.harq_ack_bit_length, fp.fapi.csi_part1_bit_length)
+            assert got is not None, tag + ": not notified"
+            assert got["nof_uci"] == want["nof_uci"] == (1 if uci is not None else 0), tag
+            if fp.tb_bytes:
+                _check(got, want, tag)
+                assert np.array_equal(tb, want_tb), tag
+                assert want["tb_crc_ok"] and np.array_equal(want_tb, tb_sent), tag
+            else:
+                for k in ("sinr_db", "epre_db", "rsrp_db"):
+                    assert abs(got[k] - want[k]) <= 0.05, (tag, k, got[k], want[k])
+            if uci is not None:
+                assert got["harq_ack_status"] == want["harq_ack_status"] == 1, tag
+                assert got["csi_part1_status"] == want["csi_part1_status"] == 1, tag
+                assert np.array_equal(got["harq_ack"], want["harq_ack"]) and np.array_equal(want["harq_ack"], uci[0])
+                assert np.array_equal(got["csi_part1"], want["csi_part1"]) and np.array_equal(want["csi_part1"], uci[1])
+    s = plug.stats()
+    assert s["errors"] == 0 and s["pdus"] == 10, s
+
+
+def test_pusch_plugin_three_slots_one_config(phy):
+    """ADVICE r4 (high/medium): three slots of one UE with an identical PDU configuration (one cached plan) queued
+    before a single flush: the collector cuts a batch at every slot change, each PDU carries its own slot, and every
+    transport block equals the reference."""
+    ophy, oracle = phy
+    from pusch_slot_cases import mixed_slot
+
+    plug = ophy.PuschProcessorPlugin(device=0, iterations=ITERS)
+    runs = []
+    for sl in (6, 7, 8):
+        grid, pdus, sent = mixed_slot(sl, 0, seed=40, kinds=["plain"])
+        g = ophy.Grid(grid)
+        runs.append((grid, pdus[0], sent[0][0], g, plug.process(g, amd.make_pdu(**pdus[0]), pdus[0]["tbs"] // 8)))
+    plug.flush()
+    plug.wait()
+    for grid, pdu, tb_sent, g, (t, tb) in runs:
+        want_tb, want = pp.ref_pusch_process(grid[:pdu["nof_rx_ports"]], pdu, pdu["tbs"] // 8, iterations=ITERS)
+        got = plug.result(t)
+        _check(got, want, "slot %d" % pdu["slot_index"])
+        assert got["tb_crc_ok"] and np.array_equal(tb, tb_sent) and np.array_equal(tb, want_tb)
+    s = plug.stats()
+    assert s["batches"] == 3 and s["pdus"] == 3, s

@@ -517,3 +517,225 @@ def test_pusch_processor_csi_part2_vs_reference(case):
         # at these SNRs the reference recovers what the UE sent
         assert want["tb_crc_ok"] and np.array_equal(want["csi_part1"], csi1), tag
         assert np.array_equal(want["csi_part2"], csi2), tag
+
+
+# DC subcarrier (pdu_t::dc_position): pusch_processor_impl.cpp:235-249 zeroes the DC subcarrier's channel estimate of
+# a CP-OFDM PDU on every port, layer and OFDM symbol, so its REs equalize to zero symbols of infinite variance (zero
+# LLRs); transform precoding leaves it.  DC at subcarrier 1638 = 12 x 273 / 2, where the reference's scheduler default
+# (initial_ul_dc_offset = center) puts it.  (name, pdu overrides, SNR dB)
+DC = 1638
+DC_CASES = [
+    ("dc_16qam_4rx", dict(bwp_size_rb=273, rb_start=100, rb_count=80, modulation=4, target_code_rate=490.0,
+                          nof_rx_ports=4, rnti=0x4711, n_id=3), 25.0),
+    ("dc_2layer_zf_64qam", dict(bwp_size_rb=273, rb_start=130, rb_count=12, modulation=6, target_code_rate=567.0,
+                                nof_tx_layers=2, nof_rx_ports=2, dmrs_symbol_mask=(1 << 2) | (1 << 7) | (1 << 11)),
+     30.0),
+    ("dc_cdm1_bwp", dict(bwp_start_rb=100, bwp_size_rb=150, rb_start=30, rb_count=20, nof_cdm_groups_without_data=1,
+                         dmrs_symbol_mask=1 << 3, start_symbol_index=1, nof_symbols=12, nof_rx_ports=2), 22.0),
+    ("dc_outside_allocation", dict(bwp_size_rb=273, rb_start=0, rb_count=60, nof_rx_ports=2), 22.0),
+]
+
+
+def _dc_re_positions(pdu, nsubc):
+    """Codeword RE indices (data-RE order) of the DC subcarrier."""
+    from oracle.pusch_demod import data_re_mask
+
+    crb0 = pdu["bwp_start_rb"] + pdu["rb_start"]
+    mask = data_re_mask(nsubc, list(range(crb0, crb0 + pdu["rb_count"])), pdu["start_symbol_index"],
+                        pdu["nof_symbols"], pdu["dmrs_symbol_mask"], False, pdu["nof_cdm_groups_without_data"])
+    idx = np.cumsum(mask.reshape(-1)).reshape(mask.shape) - 1
+    return [int(idx[l, DC]) for l in range(14) if mask[l, DC]]
+
+
+@pytest.mark.parametrize("case", DC_CASES, ids=[c[0] for c in DC_CASES])
+def test_pusch_processor_dc_position_vs_reference(case):
+    """dc_position -- TB, CRC, LDPC statistics and CSI identical to the compiled pusch_processor_impl
+    with the same dc_position, through the estimator-fused path and through the expanded-estimate path (whose caller
+    estimates then hold zeros at the DC, as the reference's ch_estimate does); the DC REs' LLRs are zero and every
+    other LLR equals the run without dc_position."""
+    import torch
+
+    name, over, snr = case
+    pdu = dict(BASE, **over)
+    nprb = 273
+    nsubc = 12 * nprb
+    tbs = _tbs(pdu)
+    r = pdu["target_code_rate"] / 1024
+    pdu["base_graph"] = 2 if (tbs <= 292 or (tbs <= 3824 and r <= 0.67) or r <= 0.25) else 1
+    rng = np.random.default_rng(len(name) + 7)
+    tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+    L, P = pdu["nof_tx_layers"], pdu["nof_rx_ports"]
+    ch = (np.eye(L, P) + 0.15j * np.ones((L, P))).astype(np.complex64)
+    grid, splan = pp.ue_transmit(tb, pdu, nsubc, channel=ch, snr_db=snr, seed=4)
+    want_tb, want = pp.ref_pusch_process(grid, dict(pdu, dc_position=DC), tbs // 8, iterations=6)
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=6), device=0)
+    plan = proc.plan(amd.make_pdu(**dict(pdu, tbs=tbs, dc_position=DC)), nsubc)
+    plan_nodc = proc.plan(amd.make_pdu(**dict(pdu, tbs=tbs)), nsubc)
+    g = torch.from_numpy(grid.view(np.int32)[None]).to("cuda:0")
+    G = plan.sch.cw_length
+    llrs = torch.zeros((1, (G + 63) // 64 * 64), dtype=torch.int8, device="cuda:0")
+    llrs0 = torch.zeros_like(llrs)
+    est = torch.zeros((1, P * L * 14 * nsubc), dtype=torch.int32, device="cuda:0")
+    out_f, res_f = proc.process_batch(g, plan, llrs=llrs)
+    out_e, res_e = proc.process_batch(g, plan, estimates=est)
+    _, _ = proc.process_batch(g, plan_nodc, llrs=llrs0)
+    torch.cuda.synchronize()
+    for tag, out, res in (("fused", out_f, res_f), ("expanded", out_e, res_e)):
+        got = amd.pusch_processor.parse_results(res.cpu().numpy())[0]
+        assert bool(got.data.tb_crc_ok) == want["tb_crc_ok"], (name, tag)
+        assert np.array_equal(out[0].cpu().numpy(), want_tb), (name, tag)
+        assert got.data.ldpc_iterations_sum == want["iterations_sum"], (name, tag, got.data.ldpc_iterations_sum, want)
+        assert got.data.ldpc_iterations_max == want["iterations_max"], (name, tag)
+        _check_csi(got, want, name + " " + tag)
+    assert want["tb_crc_ok"] and np.array_equal(want_tb, tb), name
+    # LLRs: zero at the DC REs (every layer and bit), equal elsewhere
+    qm = pdu["modulation"]
+    a, b = llrs[0, :G].cpu().numpy(), llrs0[0, :G].cpu().numpy()
+    pos = _dc_re_positions(pdu, nsubc)
+    dc_bits = np.zeros(G, bool)
+    for j in pos:
+        dc_bits[j * L * qm:(j + 1) * L * qm] = True
+    assert (a[dc_bits] == 0).all(), name
+    np.testing.assert_array_equal(a[~dc_bits], b[~dc_bits], err_msg=name)
+    if pos:
+        assert (b[dc_bits] != 0).any(), name  # the DC step changed something
+    # the caller's estimates hold zeros at the DC subcarrier inside the allocation's symbols
+    e = est[0].cpu().numpy().reshape(P * L, 14, nsubc)
+    crb0 = pdu["bwp_start_rb"] + pdu["rb_start"]
+    inside = crb0 * 12 <= DC < (crb0 + pdu["rb_count"]) * 12
+    sy = slice(pdu["start_symbol_index"], pdu["start_symbol_index"] + pdu["nof_symbols"])
+    if inside:
+        assert (e[:, sy, DC] == 0).all() and (e[:, sy, DC + 1] != 0).all(), name
+    else:
+        assert not pos, name
+
+
+def test_pusch_processor_dc_transform_precoding_untouched():
+    """dc_position on a DFT-s-OFDM PDU changes nothing (pusch_processor_impl.cpp:235: only CP-OFDM), as the
+    reference."""
+    import torch
+
+    pdu = dict(BASE, bwp_size_rb=273, rb_start=120, rb_count=25, modulation=4, target_code_rate=434.0,
+               transform_precoding=1, n_rs_id=55, nof_rx_ports=2)
+    tbs = pp_tbs_tp(pdu)
+    pdu["base_graph"] = 2 if (tbs <= 292 or (tbs <= 3824 and 434.0 / 1024 <= 0.67)) else 1
+    tb = np.random.default_rng(9).integers(0, 256, tbs // 8, dtype=np.uint8)
+    grid, _ = pp.ue_transmit_tp(tb, pdu, 12 * 273, channel=np.array([0.8, 0.4j]), snr_db=25.0, seed=1)
+    want_tb, want = pp.ref_pusch_process(grid, dict(pdu, dc_position=DC), tbs // 8, iterations=6)
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=6), device=0)
+    plan = proc.plan(amd.make_pdu(**dict(pdu, tbs=tbs, dc_position=DC)), 12 * 273)
+    g = torch.from_numpy(grid.view(np.int32)[None]).to("cuda:0")
+    out, res = proc.process_batch(g, plan)
+    torch.cuda.synchronize()
+    got = amd.pusch_processor.parse_results(res.cpu().numpy())[0]
+    assert bool(got.data.tb_crc_ok) == want["tb_crc_ok"] and want["tb_crc_ok"]
+    assert np.array_equal(out[0].cpu().numpy(), want_tb)
+    assert got.data.ldpc_iterations_sum == want["iterations_sum"]
+
+
+def pp_tbs_tp(pdu):
+    nd = bin(pdu["dmrs_symbol_mask"]).count("1")
+    return amd.tbs_calculator_calculate(pdu["nof_symbols"], 12 * nd, 0, pdu["modulation"], pdu["target_code_rate"],
+                                        1, 0, pdu["rb_count"])
+
+
+# UCI-only PUSCH (no codeword): pusch_processor_impl.cpp:305-324 -- estimator, demodulator, demultiplexer into the
+# UCI decoders, no UL-SCH.  (name, pdu overrides, HARQ-ACK bits, CSI part 1 bits, SNR dB)
+UCI_ONLY_CASES = [
+    ("uci_only_ack5_csi12_16qam", dict(modulation=4, target_code_rate=490.0, nof_rx_ports=2), 5, 12, 20.0),
+    ("uci_only_ack1_csi20_qpsk", dict(modulation=2, target_code_rate=679.0, rb_count=10), 1, 20, 15.0),
+    ("uci_only_ack2_qpsk", dict(modulation=2, target_code_rate=120.0, rb_count=4), 2, 0, 10.0),
+    ("uci_only_csi60_2layer_dc", dict(bwp_size_rb=273, rb_start=130, rb_count=12, modulation=4,
+                                      target_code_rate=378.0, nof_tx_layers=2, nof_rx_ports=2, dc_position=DC), 0, 60,
+     25.0),
+]
+
+
+@pytest.mark.parametrize("case", UCI_ONLY_CASES, ids=[c[0] for c in UCI_ONLY_CASES])
+def test_pusch_processor_uci_only_vs_reference(case):
+    """a PUSCH PDU without codeword (tbs = 0) -- HARQ-ACK / CSI part 1 payloads and statuses and the
+    CSI identical to the compiled pusch_processor_impl processing the same PDU without codeword; the result carries no
+    transport block (TB CRC KO, no codeblocks).  Through the batch chain and the slot form next to a data PDU."""
+    import torch
+
+    name, over, n_ack, n_csi1, snr = case
+    pdu = dict(BASE, **over, nof_harq_ack=n_ack, nof_csi_part1=n_csi1, beta_offset_harq_ack=8.0,
+               beta_offset_csi_part1=6.25, alpha_scaling=1.0)
+    nprb = pdu["bwp_size_rb"]
+    nsubc = 12 * nprb
+    rng = np.random.default_rng(len(name) + 50)
+    ack = rng.integers(0, 2, n_ack).astype(np.uint8)
+    csi1 = rng.integers(0, 2, n_csi1).astype(np.uint8)
+    L, P = pdu["nof_tx_layers"], pdu["nof_rx_ports"]
+    ch = (np.eye(L, P) + 0.2j * np.ones((L, P))).astype(np.complex64)
+    tx = {k: v for k, v in pdu.items() if k != "dc_position"}
+    grid, _ = pp.ue_transmit(np.zeros(0, np.uint8), tx, nsubc, channel=ch, snr_db=snr, seed=6, uci=(ack, csi1))
+    _, want = pp.ref_pusch_process(grid, pdu, 0, iterations=6)
+    assert want["nof_codeblocks_total"] == 0 and not want["tb_crc_ok"]
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=6), device=0)
+    plan = proc.plan(amd.make_pdu(**dict(pdu, tbs=0)), nsubc)
+    assert plan.nof_codeblocks == 0 and plan.tb_bytes == 0
+    g = torch.from_numpy(grid.view(np.int32)[None]).to("cuda:0")
+    d_ack = torch.zeros((1, max(n_ack, 1)), dtype=torch.uint8, device="cuda:0")
+    d_csi = torch.zeros((1, max(n_csi1, 1)), dtype=torch.uint8, device="cuda:0")
+    _, res = proc.process_batch(g, plan, harq_ack=d_ack if n_ack else None, csi_part1=d_csi if n_csi1 else None)
+    # the slot form: the UCI-only PDU next to a data PDU on its own grid
+    dpdu = dict(BASE, bwp_size_rb=nprb, rb_start=0, rb_count=4, rnti=0x77, slot_index=pdu["slot_index"])
+    dtbs = _tbs(dpdu)
+    dpdu["base_graph"] = 2
+    dtb = rng.integers(0, 256, dtbs // 8, dtype=np.uint8)
+    dgrid, _ = pp.ue_transmit(dtb, dpdu, nsubc, snr_db=25.0, seed=8, nof_rx_ports=P)
+    dplan = proc.plan(amd.make_pdu(**dict(dpdu, tbs=dtbs, nof_rx_ports=P)), nsubc)
+    grids = torch.from_numpy(np.stack([grid, dgrid]).view(np.int32)).to("cuda:0")
+    slot = amd.PuschSlot([(plan, 0), (dplan, 1)])
+    uci = torch.zeros(max(slot.uci_total, 1), dtype=torch.uint8, device="cuda:0")
+    tbs_s, offs, res_s = proc.process_slot(grids, slot, uci=uci)
+    torch.cuda.synchronize()
+    for tag, got, a_bits, c_bits in (
+            ("batch", amd.pusch_processor.parse_results(res.cpu().numpy())[0], d_ack[0, :n_ack].cpu().numpy(),
+             d_csi[0, :n_csi1].cpu().numpy()),
+            ("slot", amd.pusch_processor.parse_results(res_s.cpu().numpy())[0],
+             uci[:n_ack].cpu().numpy(), uci[n_ack:n_ack + n_csi1].cpu().numpy())):
+        assert not got.data.tb_crc_ok and got.data.nof_codeblocks_total == 0, (name, tag)
+        assert got.harq_ack_status == want["harq_ack_status"], (name, tag, got.harq_ack_status, want)
+        assert got.csi_part1_status == want["csi_part1_status"], (name, tag, got.csi_part1_status, want)
+        np.testing.assert_array_equal(a_bits, want["harq_ack"], err_msg=name + tag)
+        np.testing.assert_array_equal(c_bits, want["csi_part1"], err_msg=name + tag)
+        _check_csi(got, want, name + " " + tag)
+    # the reference recovers what the UE sent; the data PDU of the slot decodes
+    assert np.array_equal(want["harq_ack"], ack) and np.array_equal(want["csi_part1"], csi1), name
+    got_d = amd.pusch_processor.parse_results(res_s.cpu().numpy())[1]
+    assert got_d.data.tb_crc_ok and np.array_equal(tbs_s[offs[1]:offs[1] + dtbs // 8].cpu().numpy(), dtb)
+
+
+def test_pusch_slot_per_pdu_slot_shared_plan():
+    """PDUs of three slots that share one plan in one slot call each use their own slot's DM-RS
+    (srs_amd_pusch_slot_pdu::has_slot): every transport block decodes, equal to the reference per slot."""
+    import torch
+
+    pdu = dict(BASE, bwp_size_rb=52, rb_count=52, nof_rx_ports=2, modulation=4, target_code_rate=490.0)
+    tbs = _tbs(pdu)
+    pdu["base_graph"] = 1 if tbs > 3824 else 2
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=6), device=0)
+    plan = proc.plan(amd.make_pdu(**dict(pdu, tbs=tbs)), 12 * 52)  # created for slot 0
+    grids, tbs_sent, wants, slots = [], [], [], [5, 6, 9]
+    for k, sl in enumerate(slots):
+        p = dict(pdu, slot_index=sl)
+        tb = np.random.default_rng(sl).integers(0, 256, tbs // 8, dtype=np.uint8)
+        grid, _ = pp.ue_transmit(tb, p, 12 * 52, snr_db=25.0, seed=sl)
+        grids.append(grid)
+        tbs_sent.append(tb)
+        wants.append(pp.ref_pusch_process(grid, p, tbs // 8, iterations=6))
+    g = torch.from_numpy(np.stack(grids).view(np.int32)).to("cuda:0")
+    # the fused route (new data, no soft buffer), then the batch-chain route (HARQ soft buffers kept)
+    soft = [torch.zeros(plan.soft_bytes, dtype=torch.int8, device="cuda:0") for _ in range(3)]
+    for route, pdus in (("fused", [(plan, k) for k in range(3)]), ("chain", [(plan, k, soft[k]) for k in range(3)])):
+        slot = amd.PuschSlot(pdus, slots=[(1, sl) for sl in slots])
+        out, offs, res = proc.process_slot(g, slot)
+        torch.cuda.synchronize()
+        for k, got in enumerate(amd.pusch_processor.parse_results(res.cpu().numpy())):
+            want_tb, want = wants[k]
+            assert got.data.tb_crc_ok and want["tb_crc_ok"], (route, k)
+            assert np.array_equal(out[offs[k]:offs[k] + tbs // 8].cpu().numpy(), tbs_sent[k]), (route, k)
+            assert got.data.ldpc_iterations_sum == want["iterations_sum"], (route, k)
+            _check_csi(got, want, "%s slot %d" % (route, slots[k]))
