@@ -89,6 +89,8 @@ def parse():
                    help="pipeline: PUSCH layers (4: MMSE 4x4, parity unpinned; 2: the reference-pinned ZF 2x4)")
     p.add_argument("--ingest", action="store_true",
                    help="pipeline, N > 1: rank 0 holds all cells' slot inputs; RCCL scatter / gather every step")
+    p.add_argument("--alone-probe", action="store_true",
+                   help="pipeline: also time the LDPC decoder alone on pre-dematched rows (an extra launch form)")
     p.add_argument("--no-pinned", action="store_true",
                    help="pipeline: skip the reference-pinned sibling line (PUSCH 2 layers x 4 rx, ZF)")
     p.add_argument("--no-latency", action="store_true",
@@ -112,13 +114,17 @@ def load_traffic(name, kernel=None):
     return None
 
 
-def timed(args, dist, world, dev, stream, step):
+def timed(args, dist, world, dev, stream, step, probes=None):
     """Warmup, then K steps bracketed by barrier + synchronize; per-step HIP
     events on the launch stream.  Returns (elapsed_s max over ranks, mean event ms).
-    On a CPU device (the gloo tests of the multi-rank path) the events are skipped."""
+    On a CPU device (the gloo tests of the multi-rank path) the events are skipped.
+    probes: optional dict {probe id: None} of live kernel probes (srsran_project_amd.profiling) armed over exactly
+    the K timed steps; filled with (launches, mean ms, min ms, max ms) of each kernel family's launches in them."""
     import torch
 
     gpu = dev.type == "cuda"
+    if probes and gpu:
+        from srsran_project_amd import profiling
     sync = (lambda: torch.cuda.synchronize(dev)) if gpu else (lambda: None)
     for _ in range(args.warmup):
         step()
@@ -135,6 +141,9 @@ def timed(args, dist, world, dev, stream, step):
         if world > 1:
             dist.barrier()
         sync()
+        if probes and gpu:
+            for p in probes:
+                profiling.arm(p, 64 * args.steps)
         t0 = time.perf_counter()
         for s in range(args.steps):
             if gpu:
@@ -149,6 +158,9 @@ def timed(args, dist, world, dev, stream, step):
     finally:
         if gc_was_enabled:
             gc.enable()
+    if probes and gpu:
+        for p in probes:
+            probes[p] = profiling.read(p)
     if gpu:
         event_ms = float(np.mean([starts[s].elapsed_time(ends[s]) for s in range(args.steps)]))
     else:
@@ -437,7 +449,7 @@ def main():
         from bench_pipeline import run_pipeline
 
         line = run_pipeline(args, dist, world, rank, dev, timed, HBM_PEAK_GBS,
-                            load_traffic("r04_traffic.json", "ldpc_decode_hr_kernel"))
+                            load_traffic("r05_traffic.json", "ldpc_decode_hr_kernel"))
     elif args.workload == "sch_slot":
         from bench_slot import run_sch_slot
 

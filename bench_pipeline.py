@@ -423,14 +423,41 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
             stream = torch.cuda.Stream(dev)
             run = pl.graph(stream)
         run = run or (lambda: pl.step(stream))
-        elapsed, step_ms = timed(args, dist, world, dev, stream, run)
+        probes = None
+        if dev.type == "cuda":
+            from srsran_project_amd import profiling as prof
+
+            probes = {prof.PROBE_LDPC_HR: None, prof.PROBE_EQUALIZER: None, prof.PROBE_OFDM_DEMOD: None,
+                      prof.PROBE_OFDM_MOD: None}
+        elapsed, step_ms = timed(args, dist, world, dev, stream, run, probes=probes)
     ok_frac, its_mean = pl.check()
     stages = pl.stage_ms(stream)
     cbs_dl, cbs_ul = pl.plan_dl.nof_segments, pl.plan_ul.nof_segments
     cbs = (cbs_dl + cbs_ul) * S * args.steps * world
     bits = (pl.tbs_dl + pl.tbs_ul) * S * args.steps * world
     value = cbs / elapsed
-    dec_ms, dec_bytes, dec_cbs, dec_its = pl.ldpc_decoder_ms(stream)
+    # the dominant kernel as the timed steps launched it (fused rate dematching: it reads each codeblock's E received
+    # LLRs of the codeword, writes its message and iteration count), timed live by the probe on its own stream
+    dec_cbs = pl.plan_ul.nof_segments * S
+    dec_its = its_mean
+    dec_bytes = S * (pl.plan_ul.cw_length + pl.plan_ul.nof_segments *
+                     ((__import__("srsran_project_amd").message_length(pl.plan_ul.base_graph, pl.plan_ul.lifting_size)
+                       + 7) // 8 + 4))
+    in_step = {}
+    if probes:
+        from srsran_project_amd import profiling as prof
+
+        for k, v in probes.items():
+            if v is not None and v[0]:
+                in_step[prof.NAMES[k]] = {"launches": v[0], "mean_ms": v[1], "min_ms": v[2], "max_ms": v[3]}
+    hr = probes.get(__import__("srsran_project_amd").profiling.PROBE_LDPC_HR) if probes else None
+    dec_ms = hr[1] if hr and hr[0] else None
+    alone = None
+    if getattr(args, "alone_probe", False) or dec_ms is None:
+        a_ms, a_bytes, _, _ = pl.ldpc_decoder_ms(stream)
+        alone = {"kernel_ms": a_ms, "algorithmic_bytes": a_bytes,
+                 "note": "the decoder alone on pre-dematched soft-buffer rows (a different input form)"}
+        dec_ms = dec_ms or a_ms
     # algorithmic HBM bytes of each stage per step (inputs read once, outputs written once)
     samp_dl = S * pl.dl_ports * pl.ofdm_mod.get_slot_size(SLOT) * 8
     samp_ul = S * pl.ul_ports * pl.ofdm_dem.get_slot_size(SLOT) * 8
@@ -513,56 +540,69 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         "ingest_ms_per_step": ingest_ms,
         "low_snr": low,
         "pinned_sibling": pinned,
+        "kernel_ms_in_step": in_step,
         "roofline": {
             "bound": "hbm",
-            "kernel": "ldpc_decode_hr_kernel (PUSCH codeblocks of one step, BG%d Z=%d, CRC24B early stop, <= %d it; "
-                      "the decoder reads the %d-LLR non-zero prefix of each soft-buffer row)"
-                      % (pl.plan_ul.base_graph, pl.plan_ul.lifting_size, pl.iters,
-                         __import__("srsran_project_amd").decoder_llr_prefix(pl.plan_ul)),
+            "kernel": "ldpc_decode_hr_kernel<0,4,1> as the timed steps launch it (PUSCH codeblocks of one step, BG%d "
+                      "Z=%d, CRC24B early stop, <= %d it, rate dematching fused into its load: it reads each "
+                      "codeblock's E received LLRs from the codeword row)"
+                      % (pl.plan_ul.base_graph, pl.plan_ul.lifting_size, pl.iters),
             "achieved": dec_bytes / (dec_ms * 1e-3) / 1e9,
             "peak": hbm_peak,
             "unit": "GB/s",
             "frac": dec_bytes / (dec_ms * 1e-3) / 1e9 / hbm_peak,
             "traffic": traffic,
             "kernel_ms": dec_ms,
+            "kernel_ms_source": "live probe: HIP events around every launch of the kernel on its own stream over the "
+                                "timed steps (srs_amd_probe_*, include/srsran_amd/profiling.h)" if hr and hr[0]
+                                else "alone on pre-dematched rows (no live probe)",
             "algorithmic_bytes_per_launch": dec_bytes,
+            "alone": alone,
             "limiter": "valu",
             "valu": valu,
-            "note": "bound/achieved/peak/frac: the decoder's HBM roofline (algorithmic bytes / measured kernel time / "
-                    "8 TB/s; traffic = HBM bytes of the same launch from separate FETCH_SIZE / WRITE_SIZE passes, "
-                    "WRITE_SIZE halved by this box's calibration (profiles/r04_traffic.json, "
-                    "profiles/r04_hr_decoder_traffic.md): 1.02x the algorithmic bytes, no spill or re-read traffic) "
-                    "-- far from HBM-bound.  Its limiter is VALU "
-                    "issue: valu.achieved_frac_of_peak_issue = modelled VALU issue cycles (PMC SQ_ACTIVE_INST_VALU "
-                    "per codeblock and iteration, profiles/ldpc_valu_model.json) / (1,024 SIMDs x 2.4 GHz x kernel "
-                    "time); the PMC-measured busy fraction of the same command is in profiles/r03_pmc_table.json.  "
-                    "kernel_ms is the decoder launched alone on its stream (HIP events); rocprofv3 over the same "
-                    "launches agrees (profiles/r04_hr_alone_kernel_stats.md), while inside the pipeline step the "
-                    "decoder shares the CUs with the concurrent PDSCH chain and averages longer "
-                    "(profiles/r04_bench_kernel_stats.md)",
+            "note": "bound/achieved/peak/frac: the decoder's HBM roofline (algorithmic bytes = the codeword's LLR bytes "
+                    "+ 1,060 B of message and iteration count per codeblock, / the live in-step launch time, / 8 TB/s); "
+                    "traffic = HBM bytes per launch of the same in-step kernel from separate FETCH_SIZE / WRITE_SIZE "
+                    "passes over this command, each counter scaled by its calibration in the kernel's own access "
+                    "forms (profiles/r05_traffic.json, tools/traffic_calib.hip).  Its limiter is VALU issue "
+                    "(valu: r05 PMC of the same launch, profiles/r05_ldpc_valu_model.json).",
         },
         "cpu_baseline": cpu,
     }
 
 
 def valu_bound(cbs, its_mean, kernel_ms):
-    """VALU-issue roofline of ldpc_decode_hr_kernel from the committed PMC model (profiles/ldpc_valu_model.json,
-    tools/pmc_valu_model.py: SQ_ACTIVE_INST_VALU issue cycles per codeblock, fixed + per iteration) scaled to this
-    launch's codeblocks and measured mean iterations: issue bound = cycles / (1,024 SIMDs x 2.4 GHz), frac = issue
-    bound / measured kernel time (1.0 = every SIMD issues VALU work every cycle of the kernel)."""
+    """VALU-issue roofline of ldpc_decode_hr_kernel.  r05: the PMC of the in-step launch itself
+    (profiles/r05_ldpc_valu_model.json, tools/pmc_valu_r05.py over the bench command's rocprofv3 --pmc passes):
+    SQ_INSTS_VALU wave-instructions per codeblock at the measured mean iterations, issued at the guide's 2 cycles per
+    wave64 VALU instruction (MI355X_MICROARCH.md wave scheduling) on 1,024 SIMDs at 2.4 GHz -> issue bound; frac =
+    issue bound / live kernel time.  The measured SQ_ACTIVE_INST_VALU busy fraction of the same launches is reported
+    beside it.  Without the r05 model: the r03 model (profiles/ldpc_valu_model.json), labelled as such."""
     import json
     import os
 
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "ldpc_valu_model.json")
+    prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+    path = os.path.join(prof, "r05_ldpc_valu_model.json")
+    if os.path.exists(path):
+        m = json.load(open(path))
+        insts = cbs * m["valu_insts_per_cb"] * (its_mean / m["iterations_mean"]) if m.get("scale_by_iterations") \
+            else cbs * m["valu_insts_per_cb"]
+        cycles = insts * m.get("cycles_per_valu_insn", 2.0)
+        issue_s = cycles / (1024 * 2.4e9)
+        return {"achieved_frac_of_peak_issue": issue_s * 1e3 / kernel_ms, "issue_bound_ms": issue_s * 1e3,
+                "kernel_ms": kernel_ms, "valu_insts": insts, "cycles_per_valu_insn": m.get("cycles_per_valu_insn", 2.0),
+                "valu_busy_pmc": m.get("valu_busy"), "basis": "SQ_INSTS_VALU of the in-step launch (r05 PMC)",
+                "model": os.path.basename(path), "iterations_mean": its_mean}
+    path = os.path.join(prof, "ldpc_valu_model.json")
     if not os.path.exists(path):
         return None
     m = json.load(open(path))
     if "valu_cycles_per_cb_fixed" in m:
         cycles = cbs * (m["valu_cycles_per_cb_fixed"] + m["valu_cycles_per_cb_iteration"] * its_mean)
-        basis = "SQ_ACTIVE_INST_VALU issue cycles"
+        basis = "SQ_ACTIVE_INST_VALU issue cycles (r03 model, before the r04 kernel changes)"
     else:  # older model: instruction counts at 2 cycles per wave64 VALU instruction
         cycles = 2 * cbs * (m["valu_per_cb_fixed"] + m["valu_per_cb_iteration"] * its_mean)
-        basis = "SQ_INSTS_VALU x 2 cycles"
+        basis = "SQ_INSTS_VALU x 2 cycles (r03 model)"
     issue_s = cycles / (1024 * 2.4e9)
     return {"achieved_frac_of_peak_issue": issue_s * 1e3 / kernel_ms, "issue_bound_ms": issue_s * 1e3,
             "kernel_ms": kernel_ms, "valu_issue_cycles": cycles, "basis": basis, "model": os.path.basename(path),

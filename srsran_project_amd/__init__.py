@@ -118,3 +118,4 @@ from .transform_precoding import TransformPrecoder, is_nof_prbs_valid as transfo
 from .ulsch_info import UlschConfig, UlschInfo, ulsch_information  # noqa: F401,E402
 from .ulsch_demux import UlschDemux, UlschDemuxConfig, UlschDemuxPlan  # noqa: F401,E402
 from .uci_decoder import UCI_INVALID, UCI_UNKNOWN, UCI_VALID, UciDecoder  # noqa: F401,E402
+from . import profiling  # noqa: F401,E402

@@ -33,6 +33,8 @@
 //   * CRC early stop: the CRC is linear over GF(2), so each lane XORs the
 //     precomputed remainders x^(n-1-i+L) mod g of its set hard bits and the
 //     workgroup XOR-reduces -- one pass over LDS instead of a serial bit loop.
+#include "kernel_probe.h"
+#include "srsran_amd/profiling.h"
 #include <hip/hip_runtime.h>
 
 #include "ldpc_common.h"
@@ -2142,6 +2144,7 @@ hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, in
     // The crc table of the high-rate kernel is indexed from K Z - 1 down, 16-byte aligned.
     constexpr size_t lds = hr_lds_bytes<HR_MAXL>();
     constexpr int    NT  = HR_HALF / HR_NP;
+    const probe_scope probe(SRS_AMD_PROBE_LDPC_HR, stream); // live in-step timing (profiling.h)
     if (arith == ARITH_GENERIC) {
       hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_GENERIC, HR_MAXL, HR_NP>), dim3(grid), dim3(NT), lds, stream,
                          args);
@@ -2154,6 +2157,7 @@ hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, in
   if (ldpc_decode_full_eligible(args, g)) {
     constexpr int    MAXL = bg_traits<1>::M;
     constexpr size_t lds  = hr_lds_bytes<MAXL>();
+    const probe_scope probe(SRS_AMD_PROBE_LDPC_FULL, stream);
     if (arith == ARITH_GENERIC) {
       hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_GENERIC, MAXL, 1>), dim3(grid), dim3(HR_HALF), lds, stream, args);
     } else {

@@ -21,6 +21,8 @@
 
 #include "dft_engine.h"
 #include "ofdm_args.h"
+#include "kernel_probe.h"
+#include "srsran_amd/profiling.h"
 
 namespace srs_amd {
 
@@ -186,6 +188,7 @@ hipError_t launch_ofdm_modulate(const ofdm_args& a, uint32_t N, hipStream_t stre
   if (blocks > MAX_GRID_X) {
     return hipErrorInvalidValue;
   }
+  const probe_scope probe(SRS_AMD_PROBE_OFDM_MOD, stream);
 #define SRS_CASE(NN)                                                                                                   \
   if (N == NN) {                                                                                                       \
     hipLaunchKernelGGL(ofdm_modulate_kernel<NN>, dim3(blocks), dim3(dft::plan<NN>::T), 0, stream, a);                \
@@ -205,6 +208,7 @@ hipError_t launch_ofdm_demodulate(const ofdm_args& a, uint32_t N, hipStream_t st
   if (blocks > MAX_GRID_X) {
     return hipErrorInvalidValue;
   }
+  const probe_scope probe(SRS_AMD_PROBE_OFDM_DEMOD, stream);
 #define SRS_CASE(NN)                                                                                                   \
   if (N == NN) {                                                                                                       \
     hipLaunchKernelGGL(ofdm_demodulate_kernel<NN>, dim3(blocks), dim3(dft::plan<NN>::T), 0, stream, a);              \

@@ -21,6 +21,8 @@
 #include "demap_device.h"
 #include "equalizer_device.h"
 #include "pusch_demod_args.h"
+#include "kernel_probe.h"
+#include "srsran_amd/profiling.h"
 
 namespace srs_amd {
 namespace {
@@ -395,6 +397,7 @@ hipError_t launch_pusch_equalize_fused(const pusch_eq_args& a, const chest_args&
   ax.tiles_x       = (span_subc + 255) / 256;
   ax.nof_tiles     = ax.tiles_x * nof_grids;
   const dim3 grid(pusch_equalize_fused_blocks(c.nof_symbols, ax.nof_tiles));
+  const probe_scope probe(SRS_AMD_PROBE_EQUALIZER, stream);
 #define SRS_EQF_CASE(PP, LL, MM)                                                                                      \
   if (nof_ports == PP && nof_layers == LL && mmse == MM) {                                                            \
     hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM, false>), grid, dim3(256), 0, stream, eq_item{ax, c},   \
@@ -424,6 +427,7 @@ hipError_t launch_pusch_equalize_fused_items(const eq_items& items, uint32_t cou
   }
   const dim3    grid(max_blocks, count);
   const eq_item none{};
+  const probe_scope probe(SRS_AMD_PROBE_EQUALIZER, stream);
 #define SRS_EQF_CASE(PP, LL, MM)                                                                                      \
   if (nof_ports == PP && nof_layers == LL && mmse == MM) {                                                            \
     hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM, true>), grid, dim3(256), 0, stream, none, items);     \
