@@ -89,6 +89,8 @@ def parse():
                    help="pipeline: PUSCH layers (4: MMSE 4x4, parity unpinned; 2: the reference-pinned ZF 2x4)")
     p.add_argument("--ingest", action="store_true",
                    help="pipeline, N > 1: rank 0 holds all cells' slot inputs; RCCL scatter / gather every step")
+    p.add_argument("--no-probe", action="store_true",
+                   help="pipeline: no live kernel probes in the timed steps (roofline from the alone decoder)")
     p.add_argument("--alone-probe", action="store_true",
                    help="pipeline: also time the LDPC decoder alone on pre-dematched rows (an extra launch form)")
     p.add_argument("--no-pinned", action="store_true",

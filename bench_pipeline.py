@@ -424,7 +424,7 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
             run = pl.graph(stream)
         run = run or (lambda: pl.step(stream))
         probes = None
-        if dev.type == "cuda":
+        if dev.type == "cuda" and not getattr(args, "no_probe", False):
             from srsran_project_amd import profiling as prof
 
             probes = {prof.PROBE_LDPC_HR: None, prof.PROBE_EQUALIZER: None, prof.PROBE_OFDM_DEMOD: None,

@@ -399,7 +399,7 @@ def ue_multiplex_uci(sch_cw, pdu, info, nof_cw_bits, ack_bits, csi1_bits, csi2_b
     pos = np.arange(bpre)
     # UL-SCH REs (the zero LLRs of the demultiplexer's SCH stream are the REs an ACK of <= 2 bits punctures)
     sch_src = src[0].reshape(-1, bpre)[:, 0]
-    for j, r in enumerate(sch_src):
+    for j, r in enumerate(sch_src if len(sch_cw) else ()):  # UCI only: REs no UCI uses carry nothing (zero bits)
         if r >= 0:
             out[r * bpre + pos] = sch_cw[j * bpre + pos]
     # CSI part 2 first: where a 1/2-bit HARQ-ACK shares a reserved RE with it, the HARQ-ACK is what is sent

@@ -641,11 +641,13 @@ def pp_tbs_tp(pdu):
 
 # UCI-only PUSCH (no codeword): pusch_processor_impl.cpp:305-324 -- estimator, demodulator, demultiplexer into the
 # UCI decoders, no UL-SCH.  (name, pdu overrides, HARQ-ACK bits, CSI part 1 bits, SNR dB)
+# (without UL-SCH, CSI part 1 takes every RE the HARQ-ACK leaves, TS 38.212 6.3.2.4.1.2: allocations small enough for
+# one polar codeword of E <= 8192 bits, as a scheduler grants them)
 UCI_ONLY_CASES = [
-    ("uci_only_ack5_csi12_16qam", dict(modulation=4, target_code_rate=490.0, nof_rx_ports=2), 5, 12, 20.0),
+    ("uci_only_ack5_csi12_16qam", dict(modulation=4, target_code_rate=490.0, nof_rx_ports=2, rb_count=8), 5, 12, 20.0),
     ("uci_only_ack1_csi20_qpsk", dict(modulation=2, target_code_rate=679.0, rb_count=10), 1, 20, 15.0),
     ("uci_only_ack2_qpsk", dict(modulation=2, target_code_rate=120.0, rb_count=4), 2, 0, 10.0),
-    ("uci_only_csi60_2layer_dc", dict(bwp_size_rb=273, rb_start=130, rb_count=12, modulation=4,
+    ("uci_only_csi60_2layer_dc", dict(bwp_size_rb=273, rb_start=134, rb_count=6, modulation=4,
                                       target_code_rate=378.0, nof_tx_layers=2, nof_rx_ports=2, dc_position=DC), 0, 60,
      25.0),
 ]

@@ -24,9 +24,11 @@ KERNEL = "ldpc_decode_hr_kernel"
 
 
 def counter(agg, prefix, name):
-    for k, c in agg.items():
-        if k.startswith(prefix) and name in c:
-            return mean(c[name]), len(c[name]), k
+    """The kernel named exactly `prefix`, else the first whose name starts with it (template arguments)."""
+    keys = [k for k in agg if k == prefix] or [k for k in agg if k.startswith(prefix + "<") or k.startswith(prefix)]
+    for k in keys:
+        if name in agg[k]:
+            return mean(agg[k][name]), len(agg[k][name]), k
     return None, 0, None
 
 
