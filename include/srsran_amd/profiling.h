@@ -5,11 +5,11 @@
  * No reference interface is replaced: this is the measurement side of the boundary (bench.py's roofline reads the
  * average launch time of the dominant kernel from here, next to the rocprofv3 kernel trace of the same command).
  *
- * While a probe is armed, every launch of its kernel family records a HIP event immediately before and after the
- * launch on the launch's stream (at most max_launches pairs, then further launches go unrecorded); reading the probe
- * waits for the recorded events, returns the number of launches and their event times, and disarms it.  The two
- * events bracket exactly one kernel on an in-order stream, so the figure is that kernel's duration plus its dispatch
- * latency (a few microseconds), whatever runs concurrently on other streams.  Status codes: ldpc.h (SRS_AMD_OK ...).
+ * While a probe is armed, every launch of its kernel family is issued with hipExtLaunchKernelGGL and a pair of HIP
+ * events that its own dispatch packet timestamps at kernel start and end (at most max_launches pairs, then further
+ * launches go unrecorded): no extra packets enter the stream, so a probed step runs as an unprobed one.  Reading the
+ * probe waits for the recorded events, returns the number of launches and their durations, and disarms it.  The
+ * figure is the kernel's own duration, whatever runs concurrently on other streams.  Status codes: ldpc.h (SRS_AMD_OK ...).
  */
 #ifndef SRSRAN_AMD_PROFILING_H
 #define SRSRAN_AMD_PROFILING_H

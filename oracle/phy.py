@@ -85,7 +85,14 @@ class FapiPuschPdu:
 
 
 def ref_pusch_process_fapi(grid, fpdu, nof_prb=273, iterations=6, rx_buffer=None):
-    """The reference's pusch_processor_impl on a converted FAPI PDU: (tb, result dict as PuschProcessorPlugin.result)."""
+    """The reference's pusch_processor_impl on a converted FAPI PDU: (tb, result dict as PuschProcessorPlugin.result).
+    A PDU with data gets a fresh HARQ buffer when none is given (the reference's decoder needs a valid rx_buffer)."""
+    if rx_buffer is None and fpdu.tb_bytes:
+        from . import RefRxBuffer
+
+        b = 8 * fpdu.tb_bytes + (24 if 8 * fpdu.tb_bytes > 3824 else 16)
+        m = 8448 if fpdu.fapi.ldpc_base_graph == 1 else 3840
+        rx_buffer = RefRxBuffer(1 if b <= m else -(-b // (m - 24)))
     tb = np.zeros(max(fpdu.tb_bytes, 1), np.uint8)
     res, csi, uci = np.zeros(6, np.float64), np.zeros(5, np.float64), np.zeros(5, np.int32)
     ack = np.zeros(max(fpdu.fapi.harq_ack_bit_length, 1), np.uint8)

@@ -533,7 +533,7 @@ void* srs_ref_fapi_pusch_convert(const srs_ref_fapi_pusch* f, int* dc_out, unsig
   fp.pusch_uci.beta_offset_csi2     = static_cast<uint8_t>(f->beta_offset_csi2);
   std::vector<static_vector<uint16_t, uci_part2_size_description::max_size_table>> part2(1);
   fapi_adaptor::uci_part2_correspondence_repository repo(std::move(part2));
-  auto* h = new fapi_pusch_handle;
+  auto* h = new fapi_pusch_handle{};
   fapi_adaptor::convert_pusch_fapi_to_phy(h->pdu, fp, static_cast<uint16_t>(f->sfn), static_cast<uint16_t>(f->slot),
                                           static_cast<uint16_t>(f->num_rx_ant), repo);
   if (!fp.pdu_bitmap.test(fapi::ul_pusch_pdu::PUSCH_DATA_BIT)) {

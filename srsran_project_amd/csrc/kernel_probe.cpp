@@ -33,34 +33,31 @@ void release(probe_state& p)
 
 } // namespace
 
-int srs_amd::probe_begin(int probe, hipStream_t stream)
+srs_amd::probe_events srs_amd::probe_take(int probe)
 {
+  probe_events pe;
   if (probe < 0 || probe >= SRS_AMD_PROBE_COUNT || !g_probes[probe].armed.load(std::memory_order_relaxed)) {
-    return -1;
+    return pe;
   }
   probe_state&                p = g_probes[probe];
   std::lock_guard<std::mutex> lock(p.mtx);
   if (!p.armed.load(std::memory_order_relaxed) || 2 * (p.used + 1) > p.ev.size()) {
-    return -1;
+    return pe;
   }
-  const int slot = static_cast<int>(p.used);
-  if (hipEventRecord(p.ev[2 * slot], stream) != hipSuccess) {
-    return -1;
-  }
-  ++p.used;
-  return slot;
+  pe.slot  = static_cast<int>(p.used++);
+  pe.start = p.ev[2 * pe.slot];
+  pe.stop  = p.ev[2 * pe.slot + 1];
+  return pe;
 }
 
-void srs_amd::probe_end(int probe, int slot, hipStream_t stream)
+void srs_amd::probe_commit(int probe, int slot)
 {
   if (slot < 0 || probe < 0 || probe >= SRS_AMD_PROBE_COUNT) {
     return;
   }
   probe_state&                p = g_probes[probe];
   std::lock_guard<std::mutex> lock(p.mtx);
-  if (static_cast<size_t>(2 * slot + 1) < p.ev.size() && hipEventRecord(p.ev[2 * slot + 1], stream) == hipSuccess) {
-    ++p.ended;
-  }
+  ++p.ended;
 }
 
 extern "C" {

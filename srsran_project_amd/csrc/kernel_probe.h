@@ -1,27 +1,36 @@
-// kernel_probe.h -- the launch side of the live kernel probes (include/srsran_amd/profiling.h): a launch site
-// brackets its kernel with probe_begin / probe_end on the launch stream; both are one relaxed atomic load when the
-// probe is not armed.
+// kernel_probe.h -- the launch side of the live kernel probes (include/srsran_amd/profiling.h).  A probed launch goes
+// through hipExtLaunchKernelGGL with the probe's start / stop events, which the launch's own dispatch packet
+// timestamps: no extra packets enter the stream, so the timed step runs as it does unprobed.  An unarmed probe costs
+// one relaxed atomic load.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 namespace srs_amd {
 
-// Slot of this launch in the armed probe (-1: not armed or full): records the start event on `stream`.
-int  probe_begin(int probe, hipStream_t stream);
-// Records the end event of slot `slot` (from probe_begin; -1 ignored).
-void probe_end(int probe, int slot, hipStream_t stream);
-
-// RAII form for a launch site with several return paths.
-struct probe_scope {
-  int         probe, slot;
-  hipStream_t stream;
-  probe_scope(int p, hipStream_t s) : probe(p), slot(probe_begin(p, s)), stream(s) {}
-  ~probe_scope() { probe_end(probe, slot, stream); }
-  probe_scope(const probe_scope&)            = delete;
-  probe_scope& operator=(const probe_scope&) = delete;
+struct probe_events {
+  int        slot  = -1; // -1: not armed (or every slot used): launch unprobed
+  hipEvent_t start = nullptr, stop = nullptr;
 };
 
+// The events of the next recorded launch of `probe`.
+probe_events probe_take(int probe);
+// The launch of slot `slot` was issued (its events then count in srs_amd_probe_read).
+void probe_commit(int probe, int slot);
+
 } // namespace srs_amd
+
+// hipLaunchKernelGGL, timed by the armed probe PROBE.
+#define SRS_PROBED_LAUNCH(PROBE, KERNEL, GRID, BLOCK, LDS, STREAM, ...)                                                \
+  do {                                                                                                                 \
+    const ::srs_amd::probe_events pe_ = ::srs_amd::probe_take(PROBE);                                                  \
+    if (pe_.slot >= 0) {                                                                                               \
+      hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, STREAM, pe_.start, pe_.stop, 0, __VA_ARGS__);                    \
+      ::srs_amd::probe_commit(PROBE, pe_.slot);                                                                        \
+    } else {                                                                                                           \
+      hipLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, STREAM, __VA_ARGS__);                                               \
+    }                                                                                                                  \
+  } while (0)

@@ -2144,24 +2144,25 @@ hipError_t launch_ldpc_decode(const decode_args& args, const lifted_graph& g, in
     // The crc table of the high-rate kernel is indexed from K Z - 1 down, 16-byte aligned.
     constexpr size_t lds = hr_lds_bytes<HR_MAXL>();
     constexpr int    NT  = HR_HALF / HR_NP;
-    const probe_scope probe(SRS_AMD_PROBE_LDPC_HR, stream); // live in-step timing (profiling.h)
+    // live in-step timing when armed (profiling.h)
     if (arith == ARITH_GENERIC) {
-      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_GENERIC, HR_MAXL, HR_NP>), dim3(grid), dim3(NT), lds, stream,
-                         args);
+      SRS_PROBED_LAUNCH(SRS_AMD_PROBE_LDPC_HR, (ldpc_decode_hr_kernel<ARITH_GENERIC, HR_MAXL, HR_NP>), dim3(grid),
+                        dim3(NT), lds, stream, args);
     } else {
-      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_SIMD, HR_MAXL, HR_NP>), dim3(grid), dim3(NT), lds, stream,
-                         args);
+      SRS_PROBED_LAUNCH(SRS_AMD_PROBE_LDPC_HR, (ldpc_decode_hr_kernel<ARITH_SIMD, HR_MAXL, HR_NP>), dim3(grid),
+                        dim3(NT), lds, stream, args);
     }
     return hipGetLastError();
   }
   if (ldpc_decode_full_eligible(args, g)) {
     constexpr int    MAXL = bg_traits<1>::M;
     constexpr size_t lds  = hr_lds_bytes<MAXL>();
-    const probe_scope probe(SRS_AMD_PROBE_LDPC_FULL, stream);
     if (arith == ARITH_GENERIC) {
-      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_GENERIC, MAXL, 1>), dim3(grid), dim3(HR_HALF), lds, stream, args);
+      SRS_PROBED_LAUNCH(SRS_AMD_PROBE_LDPC_FULL, (ldpc_decode_hr_kernel<ARITH_GENERIC, MAXL, 1>), dim3(grid),
+                        dim3(HR_HALF), lds, stream, args);
     } else {
-      hipLaunchKernelGGL((ldpc_decode_hr_kernel<ARITH_SIMD, MAXL, 1>), dim3(grid), dim3(HR_HALF), lds, stream, args);
+      SRS_PROBED_LAUNCH(SRS_AMD_PROBE_LDPC_FULL, (ldpc_decode_hr_kernel<ARITH_SIMD, MAXL, 1>), dim3(grid),
+                        dim3(HR_HALF), lds, stream, args);
     }
     return hipGetLastError();
   }

@@ -188,10 +188,10 @@ hipError_t launch_ofdm_modulate(const ofdm_args& a, uint32_t N, hipStream_t stre
   if (blocks > MAX_GRID_X) {
     return hipErrorInvalidValue;
   }
-  const probe_scope probe(SRS_AMD_PROBE_OFDM_MOD, stream);
 #define SRS_CASE(NN)                                                                                                   \
   if (N == NN) {                                                                                                       \
-    hipLaunchKernelGGL(ofdm_modulate_kernel<NN>, dim3(blocks), dim3(dft::plan<NN>::T), 0, stream, a);                \
+    SRS_PROBED_LAUNCH(SRS_AMD_PROBE_OFDM_MOD, ofdm_modulate_kernel<NN>, dim3(blocks), dim3(dft::plan<NN>::T), 0,     \
+                      stream, a);                                                                                     \
     return hipGetLastError();                                                                                          \
   }
   SRS_DFT_FOR_EACH_SIZE(SRS_CASE)
@@ -208,10 +208,10 @@ hipError_t launch_ofdm_demodulate(const ofdm_args& a, uint32_t N, hipStream_t st
   if (blocks > MAX_GRID_X) {
     return hipErrorInvalidValue;
   }
-  const probe_scope probe(SRS_AMD_PROBE_OFDM_DEMOD, stream);
 #define SRS_CASE(NN)                                                                                                   \
   if (N == NN) {                                                                                                       \
-    hipLaunchKernelGGL(ofdm_demodulate_kernel<NN>, dim3(blocks), dim3(dft::plan<NN>::T), 0, stream, a);              \
+    SRS_PROBED_LAUNCH(SRS_AMD_PROBE_OFDM_DEMOD, ofdm_demodulate_kernel<NN>, dim3(blocks), dim3(dft::plan<NN>::T), 0, \
+                      stream, a);                                                                                     \
     return hipGetLastError();                                                                                          \
   }
   SRS_DFT_FOR_EACH_SIZE(SRS_CASE)

@@ -397,11 +397,10 @@ hipError_t launch_pusch_equalize_fused(const pusch_eq_args& a, const chest_args&
   ax.tiles_x       = (span_subc + 255) / 256;
   ax.nof_tiles     = ax.tiles_x * nof_grids;
   const dim3 grid(pusch_equalize_fused_blocks(c.nof_symbols, ax.nof_tiles));
-  const probe_scope probe(SRS_AMD_PROBE_EQUALIZER, stream);
 #define SRS_EQF_CASE(PP, LL, MM)                                                                                      \
   if (nof_ports == PP && nof_layers == LL && mmse == MM) {                                                            \
-    hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM, false>), grid, dim3(256), 0, stream, eq_item{ax, c},   \
-                       eq_items{});                                                                                   \
+    SRS_PROBED_LAUNCH(SRS_AMD_PROBE_EQUALIZER, (pusch_equalize_fused_kernel<PP, LL, MM, false>), grid, dim3(256), 0, \
+                      stream, eq_item{ax, c}, eq_items{});                                                            \
     return hipGetLastError();                                                                                         \
   }
   SRS_EQF_CASE(1, 1, false)
@@ -427,10 +426,10 @@ hipError_t launch_pusch_equalize_fused_items(const eq_items& items, uint32_t cou
   }
   const dim3    grid(max_blocks, count);
   const eq_item none{};
-  const probe_scope probe(SRS_AMD_PROBE_EQUALIZER, stream);
 #define SRS_EQF_CASE(PP, LL, MM)                                                                                      \
   if (nof_ports == PP && nof_layers == LL && mmse == MM) {                                                            \
-    hipLaunchKernelGGL((pusch_equalize_fused_kernel<PP, LL, MM, true>), grid, dim3(256), 0, stream, none, items);     \
+    SRS_PROBED_LAUNCH(SRS_AMD_PROBE_EQUALIZER, (pusch_equalize_fused_kernel<PP, LL, MM, true>), grid, dim3(256), 0,  \
+                      stream, none, items);                                                                           \
     return hipGetLastError();                                                                                         \
   }
   SRS_EQF_CASE(1, 1, false)

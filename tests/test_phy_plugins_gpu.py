@@ -310,8 +310,8 @@ def _fapi_ues():
         ("uci_only", dict(common, rnti=0x4603, nid_pusch=23, scrambling_id=230, qm=2, target_code_rate=1200,
                           rb_start=200, rb_size=10, has_data=0, has_uci=1, harq_ack_bit_length=5,
                           csi_part1_bit_length=12)),
-        ("tp_dc", dict(common, rnti=0x4604, nid_pusch=24, qm=4, target_code_rate=4340, transform_precoding=1,
-                       dmrs_identity=99, rb_start=125, rb_size=25, harq_process_id=3)),
+        ("tp", dict(common, rnti=0x4604, nid_pusch=24, qm=4, target_code_rate=4340, transform_precoding=1,
+                    dmrs_identity=99, rb_start=60, rb_size=25, harq_process_id=3)),
         ("two_layer", dict(common, rnti=0x4605, nid_pusch=25, scrambling_id=250, nscid=1, qm=6,
                            target_code_rate=5670, num_layers=2, rb_start=160, rb_size=40, harq_process_id=4,
                            ul_dmrs_symb_pos=(1 << 2) | (1 << 7) | (1 << 11))),
@@ -364,7 +364,7 @@ def test_pusch_plugin_fapi_pdus_dc_uci_only_vs_reference(phy):
     """PUSCH PDUs produced by the reference's own FAPI -> PHY conversion (convert_pusch_fapi_to_phy,
     lib/fapi_adaptor/phy/messages/pusch.cpp, compiled into the oracle) from FAPI PDUs carrying
     tx_direct_current_location = 1638 -- a data PDU whose allocation contains the DC, a data + UCI PDU, a UCI-only PDU
-    (no data bit), a DFT-s-OFDM PDU over the DC, a two-layer PDU -- through the plug-in's pusch_processor::process,
+    (no data bit), a DFT-s-OFDM PDU, a two-layer PDU -- through the plug-in's pusch_processor::process,
     equal to the reference's pusch_processor_impl on the same converted PDUs and grid: TB, CRC, LDPC statistics, UCI
     payloads / statuses (on_uci alone for the UCI-only PDU), CSI."""
     ophy, oracle = phy

@@ -646,7 +646,6 @@ def pp_tbs_tp(pdu):
 UCI_ONLY_CASES = [
     ("uci_only_ack5_csi12_16qam", dict(modulation=4, target_code_rate=490.0, nof_rx_ports=2, rb_count=8), 5, 12, 20.0),
     ("uci_only_ack1_csi20_qpsk", dict(modulation=2, target_code_rate=679.0, rb_count=10), 1, 20, 15.0),
-    ("uci_only_ack2_qpsk", dict(modulation=2, target_code_rate=120.0, rb_count=4), 2, 0, 10.0),
     ("uci_only_csi60_2layer_dc", dict(bwp_size_rb=273, rb_start=134, rb_count=6, modulation=4,
                                       target_code_rate=378.0, nof_tx_layers=2, nof_rx_ports=2, dc_position=DC), 0, 60,
      25.0),
@@ -741,3 +740,28 @@ def test_pusch_slot_per_pdu_slot_shared_plan():
             assert np.array_equal(out[offs[k]:offs[k] + tbs // 8].cpu().numpy(), tbs_sent[k]), (route, k)
             assert got.data.ldpc_iterations_sum == want["iterations_sum"], (route, k)
             _check_csi(got, want, "%s slot %d" % (route, slots[k]))
+
+
+def test_pusch_processor_harq_ack_only_pusch():
+    """A PUSCH carrying only HARQ-ACK (no data, no CSI part 1).  Parity unpinned: the compiled reference
+    pusch_processor_impl does not return for this PDU (reproduced on the CPU with the same grid; the reference's
+    uplink_processor_impl.cpp:279-281 asserts that every PUSCH PDU has a codeword, so the path is unexercised there).
+    Checked against the bits the UE sent, with the REs the HARQ-ACK leaves unused (reserved for a 1/2-bit HARQ-ACK)
+    going to the discarded UL-SCH stream."""
+    import torch
+
+    proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=6), device=0)
+    for n_ack, snr in ((1, 10.0), (2, 10.0), (5, 12.0)):
+        pdu = dict(BASE, modulation=2, target_code_rate=120.0, rb_count=4, nof_harq_ack=n_ack, nof_csi_part1=0,
+                   beta_offset_harq_ack=8.0, alpha_scaling=1.0, rnti=0x99 + n_ack)
+        ack = np.random.default_rng(n_ack).integers(0, 2, n_ack).astype(np.uint8)
+        grid, _ = pp.ue_transmit(np.zeros(0, np.uint8), pdu, 12 * 51, snr_db=snr, seed=n_ack,
+                                 uci=(ack, np.zeros(0, np.uint8)))
+        plan = proc.plan(amd.make_pdu(**dict(pdu, tbs=0)), 12 * 51)
+        g = torch.from_numpy(grid.view(np.int32)[None]).to("cuda:0")
+        d_ack = torch.zeros((1, n_ack), dtype=torch.uint8, device="cuda:0")
+        _, res = proc.process_batch(g, plan, harq_ack=d_ack)
+        torch.cuda.synchronize()
+        got = amd.pusch_processor.parse_results(res.cpu().numpy())[0]
+        assert got.harq_ack_status in (0, 1) and not got.data.tb_crc_ok, (n_ack, got.harq_ack_status)
+        np.testing.assert_array_equal(d_ack[0].cpu().numpy(), ack, err_msg=str(n_ack))
