@@ -423,13 +423,18 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
             stream = torch.cuda.Stream(dev)
             run = pl.graph(stream)
         run = run or (lambda: pl.step(stream))
+        elapsed, step_ms = timed(args, dist, world, dev, stream, run)
+        # the same K steps again with the live kernel probes armed: each probed launch carries timestamped events in
+        # its dispatch packet, which costs the step ~4 % (measured, profiles/r05_probe_overhead.json), so the
+        # headline value comes from the unprobed pass above and the kernel times from this one
         probes = None
         if dev.type == "cuda" and not getattr(args, "no_probe", False):
             from srsran_project_amd import profiling as prof
 
             probes = {prof.PROBE_LDPC_HR: None, prof.PROBE_EQUALIZER: None, prof.PROBE_OFDM_DEMOD: None,
                       prof.PROBE_OFDM_MOD: None}
-        elapsed, step_ms = timed(args, dist, world, dev, stream, run, probes=probes)
+            el_probed, _ = timed(args, dist, world, dev, stream, run, probes=probes)
+            probes["probed_ms_per_step"] = el_probed / args.steps * 1e3
     ok_frac, its_mean = pl.check()
     stages = pl.stage_ms(stream)
     cbs_dl, cbs_ul = pl.plan_dl.nof_segments, pl.plan_ul.nof_segments
@@ -448,7 +453,7 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         from srsran_project_amd import profiling as prof
 
         for k, v in probes.items():
-            if v is not None and v[0]:
+            if isinstance(k, int) and v is not None and v[0]:
                 in_step[prof.NAMES[k]] = {"launches": v[0], "mean_ms": v[1], "min_ms": v[2], "max_ms": v[3]}
     hr = probes.get(__import__("srsran_project_amd").profiling.PROBE_LDPC_HR) if probes else None
     dec_ms = hr[1] if hr and hr[0] else None
@@ -541,6 +546,7 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
         "low_snr": low,
         "pinned_sibling": pinned,
         "kernel_ms_in_step": in_step,
+        "probed_ms_per_step": probes.get("probed_ms_per_step") if probes else None,
         "roofline": {
             "bound": "hbm",
             "kernel": "ldpc_decode_hr_kernel<0,4,1> as the timed steps launch it (PUSCH codeblocks of one step, BG%d "
