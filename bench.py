@@ -144,7 +144,7 @@ def timed(args, dist, world, dev, stream, step, probes=None):
             dist.barrier()
         sync()
         if probes and gpu:
-            for p in probes:
+            for p in [q for q in probes if isinstance(q, int)]:
                 profiling.arm(p, 64 * args.steps)
         t0 = time.perf_counter()
         for s in range(args.steps):
@@ -161,7 +161,7 @@ def timed(args, dist, world, dev, stream, step, probes=None):
         if gc_was_enabled:
             gc.enable()
     if probes and gpu:
-        for p in probes:
+        for p in [q for q in probes if isinstance(q, int)]:
             probes[p] = profiling.read(p)
     if gpu:
         event_ms = float(np.mean([starts[s].elapsed_time(ends[s]) for s in range(args.steps)]))
