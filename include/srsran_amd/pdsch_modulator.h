@@ -148,6 +148,8 @@ typedef struct srs_amd_pdsch_slot_pdu {
   uint32_t                         grid;      /* index of the grid in d_grids */
   uint32_t                         nof_bits;  /* codeword length (>= nof_re x layers x Qm, see _batch) */
   uint64_t                         cw_offset; /* byte offset of the packed codeword in d_codewords */
+  uint32_t*                        d_grid;    /* non-NULL: this PDU's own DEVICE grid cbf16 [port][14][nof_subc]
+                                                 (a device-resident resource grid), instead of d_grids[grid] */
 } srs_amd_pdsch_slot_pdu;
 
 /* DEVICE, asynchronous: every PDSCH PDU of a slot -- several UEs on disjoint PRBs of one grid (or of several

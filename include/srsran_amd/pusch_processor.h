@@ -208,6 +208,9 @@ typedef struct srs_amd_pusch_slot_pdu {
                                                      different slots may share one plan within a call); 0: the plan's */
   uint32_t                            numerology;
   uint32_t                            slot_index;
+  const uint32_t*                     d_grid;     /* non-NULL: this PDU's own DEVICE grid cbf16 [port][14][nof_subc]
+                                                     (a device-resident resource grid, receive ports 0 .. P - 1),
+                                                     instead of d_grids[grid] */
 } srs_amd_pusch_slot_pdu;
 
 /* Optional outputs of srs_amd_pusch_process_slot_ex (any member NULL: not returned). */

@@ -1,5 +1,6 @@
 // pdsch_processor_hip.cpp -- srsran::pdsch_processor over the srsran_amd PDSCH slot C-ABI (see the header).
 #include "pdsch_processor_hip.h"
+#include "hip_resource_grid.h"
 #include "slot_collector.h"
 
 #include "srsran/phy/support/resource_grid_writer.h"
@@ -10,11 +11,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <list>
 #include <optional>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -205,10 +210,16 @@ uint32_t nof_data_re(const pending_pdu& p)
   return grid_re > reserved + grid_dmrs ? grid_re - reserved - grid_dmrs : 0;
 }
 
+/// The slot collector and the MI355X encoder / modulator shared by every pdsch_processor of one factory.  As the
+/// PUSCH engine, a batch runs in two halves: the collector thread uploads the transport blocks and issues the slot
+/// encoder, the slot modulator (into the device copy of each hip_resource_grid writer, or into staging grids for
+/// host writers) and the staging downloads; the completion thread waits for the batch, merges the written REs of
+/// the staging grids into the host writers (a pool of worker threads, one row each) and calls the notifiers.  Two
+/// buffer sets alternate between batches.
 class pdsch_engine
 {
 public:
-  explicit pdsch_engine(const pdsch_processor_hip_config& c) : cfg(c), nsubc(12 * c.nof_prb)
+  explicit pdsch_engine(const pdsch_processor_hip_config& c) : cfg(c), nsubc(12 * c.nof_prb), pool(c.nof_copy_threads)
   {
     device = cfg.device;
     if (device < 0 && hipGetDevice(&device) != hipSuccess) {
@@ -217,6 +228,11 @@ public:
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
       throw std::runtime_error("pdsch_processor_hip: device / stream");
     }
+    for (auto& bs : sets) {
+      if (hipEventCreateWithFlags(&bs.done, hipEventDisableTiming) != hipSuccess) {
+        throw std::runtime_error("pdsch_processor_hip: event");
+      }
+    }
     if (srs_amd_pdsch_encoder_create(&enc, device) != SRS_AMD_OK ||
         srs_amd_pdsch_modulator_create(&mod, device) != SRS_AMD_OK) {
       const std::string e = srs_amd_last_error();
@@ -224,6 +240,7 @@ public:
       (void)hipStreamDestroy(stream);
       throw std::runtime_error("pdsch_processor_hip: encoder / modulator: " + e);
     }
+    completer = std::thread([this] { complete_loop(); });
     collector = std::make_unique<slot_collector<pending_pdu>>(
         cfg.max_pdus_per_batch, cfg.max_wait_us, [this](std::vector<pending_pdu>& b) { return process(b); });
   }
@@ -231,6 +248,12 @@ public:
   ~pdsch_engine()
   {
     collector.reset();
+    {
+      std::lock_guard<std::mutex> lock(jmtx);
+      stop = true;
+    }
+    jcv.notify_all();
+    completer.join();
     (void)hipSetDevice(device);
     (void)hipStreamSynchronize(stream);
     for (auto& kv : plans) {
@@ -238,6 +261,9 @@ public:
     }
     srs_amd_pdsch_modulator_destroy(mod);
     srs_amd_pdsch_encoder_destroy(enc);
+    for (auto& bs : sets) {
+      (void)hipEventDestroy(bs.done);
+    }
     (void)hipStreamDestroy(stream);
   }
 
@@ -247,14 +273,20 @@ public:
     collector->enqueue(std::move(p), key);
   }
   void flush() { collector->flush(); }
-  void wait_idle() { collector->wait_idle(); }
+  void wait_idle()
+  {
+    collector->wait_idle();
+    std::unique_lock<std::mutex> lock(jmtx);
+    jcv.wait(lock, [this] { return jobs.empty() && !completing; });
+  }
   pdsch_processor_factory_hip::statistics get_statistics() const
   {
     const auto                              c = collector->get_counters();
     pdsch_processor_factory_hip::statistics s;
-    s.nof_pdus    = c.nof_pdus;
-    s.nof_batches = c.nof_batches;
-    s.nof_errors  = c.nof_errors;
+    s.nof_pdus         = c.nof_pdus;
+    s.nof_batches      = c.nof_batches;
+    s.nof_errors       = c.nof_errors + stats_late_errors;
+    s.nof_device_grids = stats_device_grids;
     return s;
   }
 
@@ -263,6 +295,25 @@ private:
     srs_amd_pdsch_mod_plan*          plan   = nullptr;
     uint32_t                         nof_re = 0; // data REs per layer (pdsch_compute_nof_data_re)
     std::list<std::string>::iterator lru;
+  };
+
+  struct buffer_set {
+    hip_mirrored_buffer grids, tbs, cws;
+    hipEvent_t          done = nullptr;
+    bool                busy = false;
+  };
+
+  /// A host writer's staging grid and the region its PDUs wrote.
+  struct host_grid {
+    resource_grid_writer* writer;
+    unsigned              ports = 0, l0 = NSYMB, l1 = 0, k0 = 0, k1 = 0;
+  };
+
+  struct job {
+    std::vector<pending_pdu> pdus;
+    std::vector<host_grid>   hosts;
+    buffer_set*              bs     = nullptr;
+    bool                     failed = false;
   };
 
   plan_entry* plan_of(const srs_amd_pdsch_mod_config& m, std::string& error)
@@ -285,11 +336,31 @@ private:
 
   void evict_plans()
   {
+    {
+      std::lock_guard<std::mutex> lock(jmtx);
+      if (!jobs.empty() || completing) {
+        return; // a batch in flight may still use a plan
+      }
+    }
     while (plans.size() > cfg.max_cached_plans && !lru.empty()) {
       auto it = plans.find(lru.back());
       srs_amd_pdsch_mod_plan_destroy(it->second.plan);
       plans.erase(it);
       lru.pop_back();
+    }
+  }
+
+  buffer_set* acquire_set()
+  {
+    std::unique_lock<std::mutex> lock(jmtx);
+    for (;;) {
+      for (auto& bs : sets) {
+        if (!bs.busy) {
+          bs.busy = true;
+          return &bs;
+        }
+      }
+      jcv.wait(lock);
     }
   }
 
@@ -306,19 +377,21 @@ private:
     }
     evict_plans();
     // plans, segmentation, the writers' device grids
-    std::vector<plan_entry*>           pl(n, nullptr);
-    std::vector<srs_amd_pdsch_ue>      ues;
+    auto                                j = std::make_unique<job>();
+    std::vector<plan_entry*>            pl;
+    std::vector<srs_amd_pdsch_ue>       ues;
     std::vector<srs_amd_pdsch_slot_pdu> sp;
-    std::vector<resource_grid_writer*> writers;
-    std::vector<unsigned>              live, grid_of(n, 0);
-    uint64_t                           tb_total = 0, cw_total = 0;
+    std::vector<hip_resource_grid*>     dev_grids; // device-resident writers of the batch
+    std::vector<unsigned>               grid_of;
+    uint64_t                            tb_total = 0, cw_total = 0;
     for (unsigned i = 0; i != n; ++i) {
       pending_pdu& p = batch[i];
       if (p.error.empty() && (p.grid->get_nof_subc() != nsubc || p.grid->get_nof_ports() < p.mod.nof_ports)) {
         p.error = "resource grid dimensions differ from the processor's";
       }
+      plan_entry* pe = nullptr;
       if (p.error.empty()) {
-        pl[i] = plan_of(p.mod, p.error);
+        pe = plan_of(p.mod, p.error);
       }
       srs_amd_pdsch_ue u{};
       if (p.error.empty()) {
@@ -327,7 +400,7 @@ private:
         const uint32_t C   = nof_codeblocks(tbs, bg);
         // pdsch_processor_impl::encode (pdsch_processor_impl.cpp:146-180)
         const uint32_t nre = nof_data_re(p);
-        if (nre < pl[i]->nof_re) {
+        if (nre < pe->nof_re) {
           p.error = "codeword shorter than the REs the modulator maps (the reference's mapper would overrun it)";
         } else if (srs_amd_sch_plan_compute(&u.plan, tbs, bg, p.pdu.codewords[0].rv,
                                             get_bits_per_symbol(p.pdu.codewords[0].modulation),
@@ -346,107 +419,212 @@ private:
       u.cw_offset = cw_total;
       tb_total += (p.tb->get_buffer().size() + 63) / 64 * 64;
       cw_total += (u.plan.cw_length + 511) / 512 * 64;
+      hip_resource_grid* hg = hip_grid_of(*p.grid);
+      if (hg != nullptr && (hg->device() != device || hg->nof_subc() != nsubc || hg->nof_symbols() != NSYMB)) {
+        hg = nullptr; // not usable in place: through the host path
+      }
       unsigned g = 0;
-      while (g != writers.size() && writers[g] != p.grid) {
-        ++g;
+      if (hg != nullptr) {
+        while (g != dev_grids.size() && dev_grids[g] != hg) {
+          ++g;
+        }
+        if (g == dev_grids.size()) {
+          dev_grids.push_back(hg);
+        }
+        g |= 0x80000000u; // a device grid
+      } else {
+        while (g != j->hosts.size() && j->hosts[g].writer != p.grid) {
+          ++g;
+        }
+        if (g == j->hosts.size()) {
+          j->hosts.push_back(host_grid{p.grid, 0, NSYMB, 0, nsubc, 0});
+        }
+        // the region of the host writer the PDUs write (rows and subcarriers merged back)
+        host_grid&                      h = j->hosts[g];
+        const srs_amd_pdsch_mod_config& m = p.mod;
+        h.ports                           = std::max(h.ports, m.nof_ports);
+        h.l0                              = std::min(h.l0, m.start_symbol);
+        h.l1                              = std::max(h.l1, m.start_symbol + m.nof_symbols);
+        for (unsigned r = 0; r != SRS_AMD_MAX_RB; ++r) {
+          if ((m.crb_mask[r / 8] >> (r % 8)) & 1u) {
+            h.k0 = std::min(h.k0, 12 * r);
+            h.k1 = std::max(h.k1, 12 * r + 12);
+          }
+        }
       }
-      if (g == writers.size()) {
-        writers.push_back(p.grid);
-      }
-      grid_of[i] = g;
+      grid_of.push_back(g);
       ues.push_back(u);
-      live.push_back(i);
+      pl.push_back(pe);
+      j->pdus.push_back(std::move(p));
     }
-    if (live.empty()) {
+    const size_t m = j->pdus.size();
+    if (m == 0) {
       return errors;
     }
+    buffer_set*  bs         = acquire_set();
+    j->bs                   = bs;
     const size_t grid_words = static_cast<size_t>(MAX_PORTS) * NSYMB * nsubc;
-    if (!grids.ensure(writers.size() * grid_words * 4) || !tbs.ensure(std::max<uint64_t>(tb_total, 64)) ||
-        !cws.ensure(std::max<uint64_t>(cw_total, 64))) {
+    const size_t nh         = j->hosts.size();
+    if (!bs->grids.ensure(std::max<size_t>(nh, 1) * grid_words * 4) || !bs->tbs.ensure(std::max<uint64_t>(tb_total, 64)) ||
+        !bs->cws.ensure(std::max<uint64_t>(cw_total, 64))) {
       log_error("batch", "device / pinned buffer allocation");
-      for (unsigned i : live) {
-        done(batch[i]);
+      for (auto& p : j->pdus) {
+        done(p);
       }
+      std::lock_guard<std::mutex> lock(jmtx);
+      bs->busy = false;
       return n;
     }
-    for (size_t k = 0; k != live.size(); ++k) {
-      const pending_pdu& p = batch[live[k]];
-      std::memcpy(tbs.h + ues[k].tb_offset, p.tb->get_buffer().data(), p.tb->get_buffer().size());
+    // device grids: made current on this stream (the host's own writes, e.g. PDCCH, uploaded first)
+    std::vector<uint32_t*> dptr(dev_grids.size());
+    for (size_t g = 0; g != dev_grids.size(); ++g) {
+      dptr[g] = dev_grids[g]->device_write(stream);
+    }
+    stats_device_grids += dev_grids.size();
+    for (size_t k = 0; k != m; ++k) {
+      const pending_pdu& p = j->pdus[k];
+      std::memcpy(bs->tbs.h + ues[k].tb_offset, p.tb->get_buffer().data(), p.tb->get_buffer().size());
       srs_amd_pdsch_slot_pdu s{};
-      s.plan      = pl[live[k]]->plan;
+      s.plan      = pl[k]->plan;
       s.dmrs      = &p.dmrs;
-      s.grid      = grid_of[live[k]];
       s.nof_bits  = ues[k].plan.cw_length;
       s.cw_offset = ues[k].cw_offset;
+      if (grid_of[k] & 0x80000000u) {
+        s.d_grid = dptr[grid_of[k] & 0x7fffffffu];
+      } else {
+        s.grid = grid_of[k];
+      }
       sp.push_back(s);
     }
-    hipError_t e = hipMemcpyAsync(tbs.d, tbs.h, tb_total, hipMemcpyHostToDevice, stream);
-    e            = e == hipSuccess ? hipMemsetAsync(grids.d, 0xff, writers.size() * grid_words * 4, stream) : e;
-    int rc = e == hipSuccess ? srs_amd_pdsch_encode_slot(enc, ues.data(), static_cast<uint32_t>(ues.size()), tbs.d,
-                                                         cws.d, stream)
+    hipError_t e = hipMemcpyAsync(bs->tbs.d, bs->tbs.h, tb_total, hipMemcpyHostToDevice, stream);
+    e = (e == hipSuccess && nh != 0) ? hipMemsetAsync(bs->grids.d, 0xff, nh * grid_words * 4, stream) : e;
+    int rc = e == hipSuccess ? srs_amd_pdsch_encode_slot(enc, ues.data(), static_cast<uint32_t>(ues.size()),
+                                                         bs->tbs.d, bs->cws.d, stream)
                              : SRS_AMD_EHIP;
     if (rc == SRS_AMD_OK) {
       rc = srs_amd_pdsch_modulate_slot(mod, sp.data(), static_cast<uint32_t>(sp.size()),
-                                       reinterpret_cast<uint32_t*>(grids.d), grid_words,
-                                       static_cast<uint32_t>(writers.size()), nsubc, cws.d, stream);
+                                       reinterpret_cast<uint32_t*>(bs->grids.d), grid_words,
+                                       static_cast<uint32_t>(std::max<size_t>(nh, 1)), nsubc, bs->cws.d, stream);
     }
-    e = rc == SRS_AMD_OK ? hipMemcpyAsync(grids.h, grids.d, writers.size() * grid_words * 4, hipMemcpyDeviceToHost,
-                                          stream)
-                         : e;
-    e = (rc == SRS_AMD_OK && e == hipSuccess) ? hipStreamSynchronize(stream) : e;
+    for (hip_resource_grid* g : dev_grids) {
+      g->device_written(stream); // host accesses and the OFDM modulator wait for the slot call
+    }
+    e = (rc == SRS_AMD_OK && nh != 0)
+            ? hipMemcpyAsync(bs->grids.h, bs->grids.d, nh * grid_words * 4, hipMemcpyDeviceToHost, stream)
+            : e;
+    e = (rc == SRS_AMD_OK && e == hipSuccess) ? hipEventRecord(bs->done, stream) : e;
     if (rc != SRS_AMD_OK || e != hipSuccess) {
       log_error("slot call", rc != SRS_AMD_OK ? std::string(srs_amd_last_error()) : hipGetErrorString(e));
       (void)hipStreamSynchronize(stream);
-      for (unsigned i : live) {
-        done(batch[i]);
-      }
-      return n;
+      j->failed = true;
     }
-    // the written REs into each writer (its other REs untouched); rows and subcarriers its PDUs span
-    for (size_t g = 0; g != writers.size(); ++g) {
-      unsigned ports = 0, l0 = NSYMB, l1 = 0, k0 = nsubc, k1 = 0;
-      for (unsigned i : live) {
-        if (grid_of[i] != g) {
-          continue;
-        }
-        const srs_amd_pdsch_mod_config& m = batch[i].mod;
-        ports                             = std::max(ports, m.nof_ports);
-        l0                                = std::min(l0, m.start_symbol);
-        l1                                = std::max(l1, m.start_symbol + m.nof_symbols);
-        for (unsigned r = 0; r != SRS_AMD_MAX_RB; ++r) {
-          if ((m.crb_mask[r / 8] >> (r % 8)) & 1u) {
-            k0 = std::min(k0, 12 * r);
-            k1 = std::max(k1, 12 * r + 12);
-          }
-        }
-      }
-      for (unsigned q = 0; q != ports; ++q) {
-        for (unsigned l = l0; l < l1; ++l) {
-          span<cbf16_t>   view = writers[g]->get_view(q, l);
-          const uint32_t* src  = reinterpret_cast<const uint32_t*>(grids.h) + ((g * MAX_PORTS + q) * NSYMB + l) * nsubc;
-          for (unsigned k = k0; k < k1 && k < view.size(); ++k) {
-            if (src[k] != SENTINEL) {
-              std::memcpy(&view[k], &src[k], sizeof(uint32_t));
-            }
-          }
-        }
-      }
+    {
+      std::lock_guard<std::mutex> lock(jmtx);
+      jobs.push_back(std::move(j));
     }
-    for (unsigned i : live) {
-      done(batch[i]);
-    }
+    jcv.notify_all();
     return errors;
   }
 
-  pdsch_processor_hip_config                   cfg;
-  const unsigned                               nsubc;
-  int                                          device = 0;
-  hipStream_t                                  stream = nullptr;
-  srs_amd_pdsch_encoder*                       enc    = nullptr;
-  srs_amd_pdsch_modulator*                     mod    = nullptr;
-  std::unordered_map<std::string, plan_entry>  plans;
-  std::list<std::string>                       lru;
-  hip_mirrored_buffer                          grids, tbs, cws;
+  void complete_loop()
+  {
+    for (;;) {
+      std::unique_ptr<job> j;
+      {
+        std::unique_lock<std::mutex> lock(jmtx);
+        jcv.wait(lock, [this] { return stop || !jobs.empty(); });
+        if (jobs.empty()) {
+          return;
+        }
+        j = std::move(jobs.front());
+        jobs.pop_front();
+        completing = true;
+      }
+      (void)hipSetDevice(device);
+      complete(*j);
+      buffer_set* bs = j->bs;
+      j.reset();
+      {
+        std::lock_guard<std::mutex> lock(jmtx);
+        bs->busy   = false;
+        completing = false;
+      }
+      jcv.notify_all();
+    }
+  }
+
+  void complete(job& j)
+  {
+    buffer_set* bs = j.bs;
+    if (!j.failed) {
+      hipError_t e;
+      while ((e = hipEventQuery(bs->done)) == hipErrorNotReady) {
+        std::this_thread::yield();
+      }
+      if (e != hipSuccess) {
+        log_error("batch", hipGetErrorString(e));
+        j.failed = true;
+      }
+    }
+    if (j.failed) {
+      stats_late_errors += j.pdus.size();
+    } else {
+      // the written REs into each host writer (its other REs untouched): one (grid, port, symbol) row per task
+      size_t rows = 0;
+      for (const host_grid& h : j.hosts) {
+        rows += static_cast<size_t>(h.ports) * (h.l1 > h.l0 ? h.l1 - h.l0 : 0);
+      }
+      std::vector<std::pair<unsigned, unsigned>> index; // (host grid, row within it)
+      index.reserve(rows);
+      for (unsigned g = 0; g != j.hosts.size(); ++g) {
+        const host_grid& h = j.hosts[g];
+        for (unsigned r = 0; r != h.ports * (h.l1 > h.l0 ? h.l1 - h.l0 : 0); ++r) {
+          index.emplace_back(g, r);
+        }
+      }
+      const size_t grid_words = static_cast<size_t>(MAX_PORTS) * NSYMB * nsubc;
+      pool.run(index.size(), [&](size_t t) {
+        const host_grid& h  = j.hosts[index[t].first];
+        const unsigned   nl = h.l1 - h.l0;
+        const unsigned   q  = index[t].second / nl;
+        const unsigned   l  = h.l0 + index[t].second % nl;
+        span<cbf16_t>    view = h.writer->get_view(q, l);
+        const uint32_t*  src  = reinterpret_cast<const uint32_t*>(bs->grids.h) + index[t].first * grid_words +
+                              (static_cast<size_t>(q) * NSYMB + l) * nsubc;
+        auto*          dst = reinterpret_cast<uint32_t*>(view.data());
+        const unsigned k1  = std::min<unsigned>(h.k1, static_cast<unsigned>(view.size()));
+        for (unsigned k = h.k0; k < k1; ++k) {
+          const uint32_t v = src[k];
+          if (v != SENTINEL) {
+            dst[k] = v;
+          }
+        }
+      });
+    }
+    for (auto& p : j.pdus) {
+      p.notifier->on_finish_processing();
+    }
+  }
+
+public:
+  std::atomic<uint64_t> stats_late_errors{0}, stats_device_grids{0};
+
+private:
+  pdsch_processor_hip_config                  cfg;
+  const unsigned                              nsubc;
+  int                                         device = 0;
+  hipStream_t                                 stream = nullptr;
+  srs_amd_pdsch_encoder*                      enc    = nullptr;
+  srs_amd_pdsch_modulator*                    mod    = nullptr;
+  std::unordered_map<std::string, plan_entry> plans;
+  std::list<std::string>                      lru;
+  row_pool                                    pool;
+  buffer_set                                  sets[2];
+  std::mutex                                  jmtx;
+  std::condition_variable                     jcv;
+  std::deque<std::unique_ptr<job>>            jobs;
+  bool                                        completing = false, stop = false;
+  std::thread                                 completer;
   std::unique_ptr<slot_collector<pending_pdu>> collector; // last: stops before the state it uses goes
 };
 

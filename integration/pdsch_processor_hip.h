@@ -44,6 +44,9 @@ struct pdsch_processor_hip_config {
   unsigned max_wait_us        = 200;
   /// PDU configurations kept as C-ABI modulator plans.
   unsigned max_cached_plans = 4096;
+  /// Worker threads merging the written rows of host resource grids (0: the completion thread alone).  Grids of a
+  /// hip_resource_grid factory are written in place in HBM.
+  unsigned nof_copy_threads = 8;
 };
 
 class pdsch_processor_factory_hip : public pdsch_processor_factory
@@ -55,6 +58,8 @@ public:
   virtual void wait_idle() = 0;
   struct statistics {
     uint64_t nof_pdus = 0, nof_batches = 0, nof_errors = 0;
+    /// Device-resident grids (hip_resource_grid) written in place, counted once per batch.
+    uint64_t nof_device_grids = 0;
   };
   virtual statistics get_statistics() const = 0;
 };

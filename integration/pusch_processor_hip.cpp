@@ -1,5 +1,6 @@
 // pusch_processor_hip.cpp -- srsran::pusch_processor over the srsran_amd slot C-ABI (see the header).
 #include "pusch_processor_hip.h"
+#include "hip_resource_grid.h"
 #include "slot_collector.h"
 
 #include "srsran/adt/bit_buffer.h"
@@ -18,10 +19,13 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <list>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -157,17 +161,30 @@ std::string convert(const pusch_processor::pdu_t& pdu, size_t tb_bytes, srs_amd_
 }
 
 /// The slot collector and the MI355X processor shared by every pusch_processor of one factory.
+///
+/// A batch runs in two halves on two threads, so consecutive batches overlap: the collector thread stages the batch
+/// (grid rows copied into pinned memory by a pool of worker threads, or the device grid of a hip_resource_grid taken
+/// as it is), issues the uploads, the slot call and the downloads on the engine's stream and hands the batch to the
+/// completion thread; the completion thread waits for that batch's event, runs the HARQ soft-buffer pass for failed
+/// new transmissions, writes HARQ state back into the rx_buffers and calls the notifiers.  Two sets of pinned /
+/// device buffers alternate between batches (a set is reused once its batch has been notified).
 class slot_engine
 {
 public:
-  explicit slot_engine(const pusch_processor_hip_config& c) : cfg(c), nsubc(12 * c.nof_prb)
+  explicit slot_engine(const pusch_processor_hip_config& c) : cfg(c), nsubc(12 * c.nof_prb), pool(c.nof_copy_threads)
   {
     device = cfg.device;
     if (device < 0 && hipGetDevice(&device) != hipSuccess) {
       throw std::runtime_error("pusch_processor_hip: hipGetDevice");
     }
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking) != hipSuccess) {
       throw std::runtime_error("pusch_processor_hip: device / stream");
+    }
+    for (auto& bs : sets) {
+      if (hipEventCreateWithFlags(&bs.done, hipEventDisableTiming) != hipSuccess) {
+        throw std::runtime_error("pusch_processor_hip: event");
+      }
     }
     srs_amd_pusch_processor_config pc{};
     pc.dec_nof_iterations    = cfg.dec_nof_iterations;
@@ -181,8 +198,10 @@ public:
     if (srs_amd_pusch_processor_create(&proc, &pc, device) != SRS_AMD_OK) {
       const std::string e = srs_amd_last_error();
       (void)hipStreamDestroy(stream);
+      (void)hipStreamDestroy(stream2);
       throw std::runtime_error("pusch_processor_hip: processor: " + e);
     }
+    completer = std::thread([this] { complete_loop(); });
     collector = std::make_unique<slot_collector<pending_pdu>>(
         cfg.max_pdus_per_batch, cfg.max_wait_us, [this](std::vector<pending_pdu>& b) { return process(b); });
   }
@@ -190,13 +209,24 @@ public:
   ~slot_engine()
   {
     collector.reset(); // processes what is pending, joins the collector thread
+    {
+      std::lock_guard<std::mutex> lock(jmtx);
+      stop = true;
+    }
+    jcv.notify_all();
+    completer.join(); // notifies what is in flight
     (void)hipSetDevice(device);
     (void)hipStreamSynchronize(stream);
+    (void)hipStreamSynchronize(stream2);
     for (auto& kv : plans) {
       srs_amd_pusch_processor_plan_destroy(kv.second.plan);
     }
     srs_amd_pusch_processor_destroy(proc);
+    for (auto& bs : sets) {
+      (void)hipEventDestroy(bs.done);
+    }
     (void)hipStreamDestroy(stream);
+    (void)hipStreamDestroy(stream2);
   }
 
   void enqueue(pending_pdu&& p)
@@ -207,7 +237,13 @@ public:
 
   void flush() { collector->flush(); }
 
-  void wait_idle() { collector->wait_idle(); }
+  // every queued PDU dispatched (collector), then every dispatched batch notified (completion thread)
+  void wait_idle()
+  {
+    collector->wait_idle();
+    std::unique_lock<std::mutex> lock(jmtx);
+    jcv.wait(lock, [this] { return jobs.empty() && !completing; });
+  }
 
   pusch_processor_factory_hip::statistics get_statistics() const
   {
@@ -215,22 +251,45 @@ public:
     pusch_processor_factory_hip::statistics s;
     s.nof_pdus            = c.nof_pdus;
     s.nof_batches         = c.nof_batches;
-    s.nof_errors          = c.nof_errors;
+    s.nof_errors          = c.nof_errors + stats_late_errors;
     s.nof_harq_redecodes  = stats_redecodes;
     s.nof_retransmissions = stats_retx;
+    s.nof_device_grids    = stats_device_grids;
     return s;
   }
 
 private:
   struct plan_entry {
-    srs_amd_pusch_processor_plan* plan = nullptr;
-    uint32_t                      nof_cbs = 0, max_csi2 = 0;
-    uint64_t                      soft_bytes = 0;
-    srs_amd_sch_plan              sch{};
+    srs_amd_pusch_processor_plan*    plan    = nullptr;
+    uint32_t                         nof_cbs = 0, max_csi2 = 0;
+    uint64_t                         soft_bytes = 0;
+    srs_amd_sch_plan                 sch{};
     std::list<std::string>::iterator lru;
   };
 
-  // Plan of a PDU configuration (cached across slots, least recently used evicted between batches).
+  /// One alternating set of the batch's pinned / device buffers.
+  struct buffer_set {
+    hip_mirrored_buffer h_grids, tbs, results, cbi, uci, pstats, soft;
+    hipEvent_t          done = nullptr; // the batch's downloads
+    bool                busy = false;
+  };
+
+  /// A dispatched batch, waiting for its completion.
+  struct job {
+    std::vector<pending_pdu>            pdus;     // the live PDUs, in slot-call order
+    std::vector<plan_entry>             pl;       // their plans (copies: eviction waits for idle)
+    std::vector<srs_amd_pusch_slot_pdu> sp;       // the slot call's PDUs
+    std::vector<uint64_t>               tb_off, uci_off, soft_off;
+    std::vector<uint32_t>               cb_off;
+    std::vector<std::vector<char>>      prev_ok;  // CB CRC flags of the rx_buffer before the call
+    uint64_t                            soft_total = 0, tb_total = 0, uci_total = 0;
+    uint32_t                            cb_total   = 0;
+    size_t                              nof_grids = 0, grid_stride = 0;
+    buffer_set*                         bs = nullptr;
+    bool                                failed = false; // the slot call failed: every PDU reported as failed
+  };
+
+  // Plan of a PDU configuration (cached across slots, least recently used evicted when no batch is in flight).
   plan_entry* plan_of(const srs_amd_pusch_pdu& c, std::string& error)
   {
     srs_amd_pusch_pdu k = c;
@@ -257,6 +316,12 @@ private:
 
   void evict_plans()
   {
+    {
+      std::lock_guard<std::mutex> lock(jmtx);
+      if (!jobs.empty() || completing) {
+        return; // a batch in flight may still use a plan
+      }
+    }
     while (plans.size() > cfg.max_cached_plans && !lru.empty()) {
       auto it = plans.find(lru.back());
       srs_amd_pusch_processor_plan_destroy(it->second.plan);
@@ -283,7 +348,31 @@ private:
     }
   }
 
-  // Runs one batch; returns the number of PDUs reported as failed.
+  // A free buffer set (waits for the completion thread to release one).
+  buffer_set* acquire_set()
+  {
+    std::unique_lock<std::mutex> lock(jmtx);
+    for (;;) {
+      for (auto& bs : sets) {
+        if (!bs.busy) {
+          bs.busy = true;
+          return &bs;
+        }
+      }
+      jcv.wait(lock);
+    }
+  }
+
+  void release_set(buffer_set* bs)
+  {
+    {
+      std::lock_guard<std::mutex> lock(jmtx);
+      bs->busy = false;
+    }
+    jcv.notify_all();
+  }
+
+  // Collector thread: stages and dispatches one batch; returns the number of PDUs reported as failed here.
   unsigned process(std::vector<pending_pdu>& batch)
   {
     const unsigned n      = static_cast<unsigned>(batch.size());
@@ -295,18 +384,18 @@ private:
       return n;
     }
     evict_plans();
+    auto j = std::make_unique<job>();
     // plans, and the PDUs that go to the GPU
-    std::vector<plan_entry*> pl(n, nullptr);
-    std::vector<unsigned>    live;
     for (unsigned i = 0; i != n; ++i) {
-      pending_pdu& p = batch[i];
+      pending_pdu& p  = batch[i];
+      plan_entry*  pe = nullptr;
       if (p.error.empty()) {
-        pl[i] = plan_of(p.c, p.error);
+        pe = plan_of(p.c, p.error);
       }
       if (p.error.empty() && !p.c.new_data && !p.rm_buffer.is_valid()) {
         p.error = "retransmission without a valid rx_buffer";
       }
-      if (p.error.empty() && p.rm_buffer.is_valid() && p.rm_buffer.get().get_nof_codeblocks() != pl[i]->nof_cbs) {
+      if (p.error.empty() && p.rm_buffer.is_valid() && p.rm_buffer.get().get_nof_codeblocks() != pe->nof_cbs) {
         p.error = "rx_buffer codeblock count differs from the transport block's";
       }
       if (!p.error.empty()) {
@@ -315,19 +404,40 @@ private:
         ++errors;
         continue;
       }
-      live.push_back(i);
+      j->pdus.push_back(std::move(p));
+      j->pl.push_back(*pe);
     }
-    if (live.empty()) {
+    const size_t m = j->pdus.size();
+    if (m == 0) {
       return errors;
     }
-    // receive grids: one device grid per (reader, port list); a PDU whose ports are a prefix of another PDU's list
-    // on the same reader shares that grid
+    buffer_set* bs = acquire_set();
+    j->bs          = bs;
+    // receive grids: a hip_resource_grid's device copy as it is (receive ports 0 .. P - 1); otherwise one staged
+    // device grid per (reader, port list), a PDU whose ports are a prefix of another PDU's list on the same reader
+    // sharing that grid
+    std::vector<const uint32_t*> dev_grid(m, nullptr);
+    for (size_t k = 0; k != m; ++k) {
+      const pending_pdu& p  = j->pdus[k];
+      hip_resource_grid* hg = hip_grid_of(*p.grid);
+      bool               ok = hg != nullptr && hg->device() == device && hg->nof_subc() == nsubc &&
+                hg->nof_symbols() == NSYMB && p.rx_ports.size() <= hg->nof_ports();
+      for (size_t q = 0; ok && q != p.rx_ports.size(); ++q) {
+        ok = p.rx_ports[q] == q;
+      }
+      if (ok) {
+        dev_grid[k] = hg->device_read(stream); // the engine's stream waits for the grid's producer
+        ++stats_device_grids;
+      }
+    }
     std::unordered_map<const resource_grid_reader*, std::vector<uint8_t>> longest;
-    for (unsigned i : live) {
-      auto& l = longest[batch[i].grid];
-      if (batch[i].rx_ports.size() > l.size() &&
-          std::equal(l.begin(), l.end(), batch[i].rx_ports.begin())) {
-        l = batch[i].rx_ports;
+    for (size_t k = 0; k != m; ++k) {
+      if (dev_grid[k] != nullptr) {
+        continue;
+      }
+      auto& l = longest[j->pdus[k].grid];
+      if (j->pdus[k].rx_ports.size() > l.size() && std::equal(l.begin(), l.end(), j->pdus[k].rx_ports.begin())) {
+        l = j->pdus[k].rx_ports;
       }
     }
     struct grid_slot {
@@ -335,139 +445,209 @@ private:
       std::vector<uint8_t>        ports;
     };
     std::vector<grid_slot> grids;
-    std::vector<unsigned>  grid_of(n, 0);
-    for (unsigned i : live) {
-      const auto&           ports = batch[i].rx_ports;
-      const auto&           l     = longest[batch[i].grid];
-      std::vector<uint8_t>  want  = std::equal(ports.begin(), ports.end(), l.begin()) ? l : ports;
-      unsigned              g     = 0;
-      while (g != grids.size() && !(grids[g].reader == batch[i].grid && grids[g].ports == want)) {
+    std::vector<unsigned>  grid_of(m, 0);
+    for (size_t k = 0; k != m; ++k) {
+      if (dev_grid[k] != nullptr) {
+        continue;
+      }
+      const auto&          ports = j->pdus[k].rx_ports;
+      const auto&          l     = longest[j->pdus[k].grid];
+      std::vector<uint8_t> want  = std::equal(ports.begin(), ports.end(), l.begin()) ? l : ports;
+      unsigned             g     = 0;
+      while (g != grids.size() && !(grids[g].reader == j->pdus[k].grid && grids[g].ports == want)) {
         ++g;
       }
       if (g == grids.size()) {
-        grids.push_back(grid_slot{batch[i].grid, want});
+        grids.push_back(grid_slot{j->pdus[k].grid, want});
       }
-      grid_of[i] = g;
+      grid_of[k] = g;
     }
-    const size_t grid_stride = static_cast<size_t>(MAX_PORTS_HIP) * NSYMB * nsubc; // uint32 words
+    j->grid_stride = static_cast<size_t>(MAX_PORTS_HIP) * NSYMB * nsubc; // uint32 words
+    j->nof_grids   = grids.size();
     // per-PDU offsets in the output / HARQ buffers
-    std::vector<uint64_t> tb_off(n), uci_off(n), soft_off(n);
-    std::vector<uint32_t> cb_off(n);
-    uint64_t              tb_total = 0, uci_total = 0, soft_total = 0;
-    uint32_t              cb_total = 0;
-    for (unsigned i : live) {
-      tb_off[i]  = tb_total;
-      uci_off[i] = uci_total;
-      cb_off[i]  = cb_total;
-      soft_off[i] = soft_total;
-      tb_total += (batch[i].data.size() + 63) / 64 * 64;
-      uci_total += batch[i].c.nof_harq_ack + batch[i].c.nof_csi_part1 + pl[i]->max_csi2;
-      cb_total += pl[i]->nof_cbs;
+    j->tb_off.resize(m);
+    j->uci_off.resize(m);
+    j->soft_off.resize(m);
+    j->cb_off.resize(m);
+    j->prev_ok.resize(m);
+    uint64_t tb_total = 0, uci_total = 0, soft_total = 0;
+    uint32_t cb_total = 0;
+    for (size_t k = 0; k != m; ++k) {
+      j->tb_off[k]   = tb_total;
+      j->uci_off[k]  = uci_total;
+      j->cb_off[k]   = cb_total;
+      j->soft_off[k] = soft_total;
+      tb_total += (j->pdus[k].data.size() + 63) / 64 * 64;
+      uci_total += j->pdus[k].c.nof_harq_ack + j->pdus[k].c.nof_csi_part1 + j->pl[k].max_csi2;
+      cb_total += j->pl[k].nof_cbs;
       // soft buffers for retransmissions and for a second pass over failed new transmissions
-      if (batch[i].rm_buffer.is_valid()) {
-        soft_total += (pl[i]->soft_bytes + 255) / 256 * 256;
+      if (j->pdus[k].rm_buffer.is_valid()) {
+        soft_total += (j->pl[k].soft_bytes + 255) / 256 * 256;
       }
     }
-    const bool ok = h_grids.ensure(grids.size() * grid_stride * 4) && tbs.ensure(std::max<uint64_t>(tb_total, 64)) &&
-                    results.ensure(sizeof(srs_amd_pusch_processor_result) * n) &&
-                    cbi.ensure(sizeof(int32_t) * std::max<uint32_t>(cb_total, 1)) &&
-                    uci.ensure(std::max<uint64_t>(uci_total, 64)) &&
-                    pstats.ensure(sizeof(srs_amd_chest_port_stats) * MAX_PORTS_HIP * n) &&
-                    soft.ensure(std::max<uint64_t>(soft_total, 256));
+    j->soft_total = soft_total;
+    j->tb_total   = tb_total;
+    j->uci_total  = uci_total;
+    j->cb_total   = cb_total;
+    const bool ok = bs->h_grids.ensure(std::max<size_t>(grids.size(), 1) * j->grid_stride * 4) &&
+                    bs->tbs.ensure(std::max<uint64_t>(tb_total, 64)) &&
+                    bs->results.ensure(sizeof(srs_amd_pusch_processor_result) * m) &&
+                    bs->cbi.ensure(sizeof(int32_t) * std::max<uint32_t>(cb_total, 1)) &&
+                    bs->uci.ensure(std::max<uint64_t>(uci_total, 64)) &&
+                    bs->pstats.ensure(sizeof(srs_amd_chest_port_stats) * MAX_PORTS_HIP * m) &&
+                    bs->soft.ensure(std::max<uint64_t>(soft_total, 256));
     if (!ok) {
       log_error("batch", "device / pinned buffer allocation");
-      for (unsigned i : live) {
-        notify_failure(batch[i]);
+      for (auto& p : j->pdus) {
+        notify_failure(p);
       }
+      release_set(bs);
       return n;
     }
-    // grids from the readers (a view per port and OFDM symbol)
-    for (size_t g = 0; g != grids.size(); ++g) {
-      for (size_t j = 0; j != grids[g].ports.size(); ++j) {
-        for (unsigned l = 0; l != NSYMB; ++l) {
-          span<const cbf16_t> v   = grids[g].reader->get_view(grids[g].ports[j], l);
-          uint8_t*            dst = h_grids.h + ((g * MAX_PORTS_HIP + j) * NSYMB + l) * nsubc * 4;
-          if (v.size() >= nsubc) {
-            std::memcpy(dst, v.data(), nsubc * 4);
-          } else {
-            std::memset(dst, 0, nsubc * 4);
-          }
-        }
+    // grid rows from the readers (a view per port and OFDM symbol), copied by the worker pool
+    const size_t rows_per_grid = MAX_PORTS_HIP * NSYMB;
+    pool.run(grids.size() * rows_per_grid, [&](size_t r) {
+      const size_t g = r / rows_per_grid, q = (r / NSYMB) % MAX_PORTS_HIP;
+      const auto   l = static_cast<unsigned>(r % NSYMB);
+      if (q >= grids[g].ports.size()) {
+        return;
       }
-    }
+      span<const cbf16_t> v   = grids[g].reader->get_view(grids[g].ports[q], l);
+      uint8_t*            dst = bs->h_grids.h + ((g * MAX_PORTS_HIP + q) * NSYMB + l) * nsubc * 4;
+      if (v.size() >= nsubc) {
+        std::memcpy(dst, v.data(), nsubc * 4);
+      } else {
+        std::memset(dst, 0, nsubc * 4);
+      }
+    });
     // retransmissions: the rx_buffer's state into the device soft buffer
-    std::vector<std::vector<char>> prev_ok(n);
-    for (unsigned i : live) {
-      if (!batch[i].c.new_data) {
-        upload_harq(batch[i], *pl[i], soft.h + soft_off[i], prev_ok[i]);
+    for (size_t k = 0; k != m; ++k) {
+      if (!j->pdus[k].c.new_data) {
+        upload_harq(j->pdus[k], j->pl[k], bs->soft.h + j->soft_off[k], j->prev_ok[k]);
         ++stats_retx;
       }
     }
     // the slot call
-    std::vector<srs_amd_pusch_slot_pdu> sp;
-    for (unsigned i : live) {
+    for (size_t k = 0; k != m; ++k) {
       srs_amd_pusch_slot_pdu u{};
-      u.plan       = pl[i]->plan;
-      u.grid       = grid_of[i];
-      u.cb_offset  = cb_off[i];
-      u.tb_offset  = tb_off[i];
-      u.d_soft     = batch[i].c.new_data ? nullptr : reinterpret_cast<int8_t*>(soft.d + soft_off[i]);
-      u.uci_offset = uci_off[i];
+      u.plan       = j->pl[k].plan;
+      u.grid       = grid_of[k];
+      u.d_grid     = dev_grid[k];
+      u.cb_offset  = j->cb_off[k];
+      u.tb_offset  = j->tb_off[k];
+      u.d_soft     = j->pdus[k].c.new_data ? nullptr : reinterpret_cast<int8_t*>(bs->soft.d + j->soft_off[k]);
+      u.uci_offset = j->uci_off[k];
       u.has_slot   = 1;
-      u.numerology = batch[i].c.numerology;
-      u.slot_index = batch[i].c.slot_index;
-      sp.push_back(u);
+      u.numerology = j->pdus[k].c.numerology;
+      u.slot_index = j->pdus[k].c.slot_index;
+      j->sp.push_back(u);
     }
-    hipError_t e = hipMemcpyAsync(h_grids.d, h_grids.h, grids.size() * grid_stride * 4, hipMemcpyHostToDevice, stream);
+    hipError_t e = grids.empty() ? hipSuccess
+                                 : hipMemcpyAsync(bs->h_grids.d, bs->h_grids.h, grids.size() * j->grid_stride * 4,
+                                                  hipMemcpyHostToDevice, stream);
     if (e == hipSuccess && soft_total != 0) {
-      e = hipMemcpyAsync(soft.d, soft.h, soft_total, hipMemcpyHostToDevice, stream);
+      e = hipMemcpyAsync(bs->soft.d, bs->soft.h, soft_total, hipMemcpyHostToDevice, stream);
     }
-    int rc = e == hipSuccess ? run_slot(sp, grids.size(), grid_stride) : SRS_AMD_EHIP;
-    e      = rc == SRS_AMD_OK ? download(n, tb_total, cb_total, uci_total, soft_total) : hipErrorUnknown;
+    int rc = e == hipSuccess ? run_slot(*j, j->sp, stream) : SRS_AMD_EHIP;
+    e      = rc == SRS_AMD_OK ? download(*j, stream) : hipErrorUnknown;
+    e      = e == hipSuccess ? hipEventRecord(bs->done, stream) : e;
     if (rc != SRS_AMD_OK || e != hipSuccess) {
       log_error("slot call", rc != SRS_AMD_OK ? std::string(srs_amd_last_error()) : hipGetErrorString(e));
       (void)hipStreamSynchronize(stream);
-      for (unsigned i : live) {
-        notify_failure(batch[i]);
+      j->failed = true;
+    }
+    // to the completion thread
+    {
+      std::lock_guard<std::mutex> lock(jmtx);
+      jobs.push_back(std::move(j));
+    }
+    jcv.notify_all();
+    return errors;
+  }
+
+  // Completion thread: notifies the dispatched batches in order.
+  void complete_loop()
+  {
+    for (;;) {
+      std::unique_ptr<job> j;
+      {
+        std::unique_lock<std::mutex> lock(jmtx);
+        jcv.wait(lock, [this] { return stop || !jobs.empty(); });
+        if (jobs.empty()) {
+          return; // stop, nothing in flight
+        }
+        j = std::move(jobs.front());
+        jobs.pop_front();
+        completing = true;
       }
-      return n;
+      (void)hipSetDevice(device);
+      complete(*j);
+      buffer_set* bs = j->bs;
+      j.reset();
+      {
+        std::lock_guard<std::mutex> lock(jmtx);
+        bs->busy   = false;
+        completing = false;
+      }
+      jcv.notify_all();
+    }
+  }
+
+  void complete(job& j)
+  {
+    buffer_set* bs = j.bs;
+    const size_t m = j.pdus.size();
+    if (!j.failed) {
+      // poll the batch's event: an interrupt-driven wait could oversleep (device_buffer.h event_wait_spin)
+      hipError_t e;
+      while ((e = hipEventQuery(bs->done)) == hipErrorNotReady) {
+        std::this_thread::yield();
+      }
+      if (e != hipSuccess) {
+        log_error("batch", hipGetErrorString(e));
+        j.failed = true;
+      }
+    }
+    if (j.failed) {
+      stats_late_errors += m;
+      for (auto& p : j.pdus) {
+        notify_failure(p);
+      }
+      return;
     }
     // new transmissions whose TB CRC failed and that keep HARQ state: decoded again with a soft buffer (the same
     // decoding, now with its soft bits kept), then written to the rx_buffer
-    const auto*       res = reinterpret_cast<const srs_amd_pusch_processor_result*>(results.h);
-    std::vector<char> keep(live.size(), 0); // the rx_buffer takes the soft buffer's state after the call
+    const auto*                         res = reinterpret_cast<const srs_amd_pusch_processor_result*>(bs->results.h);
+    std::vector<char>                   keep(m, 0); // the rx_buffer takes the soft buffer's state after the call
     std::vector<srs_amd_pusch_slot_pdu> again;
     std::vector<unsigned>               again_ids;
-    for (size_t k = 0; k != live.size(); ++k) {
-      const unsigned i = live[k];
-      keep[k]          = !batch[i].c.new_data;
-      if (batch[i].c.new_data && batch[i].c.tbs != 0 && batch[i].rm_buffer.is_valid() && !res[k].data.tb_crc_ok) {
-        srs_amd_pusch_slot_pdu u = sp[k];
-        u.d_soft                 = reinterpret_cast<int8_t*>(soft.d + soft_off[i]);
+    for (size_t k = 0; k != m; ++k) {
+      keep[k] = !j.pdus[k].c.new_data;
+      if (j.pdus[k].c.new_data && j.pdus[k].c.tbs != 0 && j.pdus[k].rm_buffer.is_valid() && !res[k].data.tb_crc_ok) {
+        srs_amd_pusch_slot_pdu u = j.sp[k];
+        u.d_soft                 = reinterpret_cast<int8_t*>(bs->soft.d + j.soft_off[k]);
         again.push_back(u);
         again_ids.push_back(static_cast<unsigned>(k));
       }
     }
     if (!again.empty()) {
       stats_redecodes += again.size();
-      e = hipSuccess;
+      hipError_t e = hipSuccess;
       for (unsigned k : again_ids) {
-        const unsigned i = live[k];
-        e = e == hipSuccess ? hipMemsetAsync(soft.d + soft_off[i], 0, pl[i]->soft_bytes, stream) : e;
+        e = e == hipSuccess ? hipMemsetAsync(bs->soft.d + j.soft_off[k], 0, j.pl[k].soft_bytes, stream2) : e;
       }
-      rc = e == hipSuccess ? run_slot(again, grids.size(), grid_stride, &again_ids) : SRS_AMD_EHIP;
+      int rc = e == hipSuccess ? run_slot(j, again, stream2, &again_ids) : SRS_AMD_EHIP;
       for (unsigned k : again_ids) {
-        const unsigned i = live[k];
         e = (rc == SRS_AMD_OK && e == hipSuccess)
-                ? hipMemcpyAsync(soft.h + soft_off[i], soft.d + soft_off[i], pl[i]->soft_bytes, hipMemcpyDeviceToHost,
-                                 stream)
+                ? hipMemcpyAsync(bs->soft.h + j.soft_off[k], bs->soft.d + j.soft_off[k], j.pl[k].soft_bytes,
+                                 hipMemcpyDeviceToHost, stream2)
                 : e;
       }
-      e = e == hipSuccess ? hipStreamSynchronize(stream) : e;
+      e = e == hipSuccess ? hipStreamSynchronize(stream2) : e;
       if (rc != SRS_AMD_OK || e != hipSuccess) {
         // the rx_buffers are left as they were (the transport blocks report their CRC failure either way)
         log_error("HARQ soft-buffer pass", rc != SRS_AMD_OK ? std::string(srs_amd_last_error()) : hipGetErrorString(e));
-        (void)hipStreamSynchronize(stream);
+        (void)hipStreamSynchronize(stream2);
       } else {
         for (unsigned k : again_ids) {
           keep[k] = 1;
@@ -475,42 +655,41 @@ private:
       }
     }
     // results, HARQ state back into the rx_buffers, notifications
-    for (size_t k = 0; k != live.size(); ++k) {
-      const unsigned i = live[k];
-      pending_pdu&   p = batch[i];
+    for (size_t k = 0; k != m; ++k) {
+      pending_pdu& p = j.pdus[k];
       if (keep[k]) {
-        store_harq(p, *pl[i], soft.h + soft_off[i]);
+        store_harq(p, j.pl[k], bs->soft.h + j.soft_off[k]);
       }
-      notify(p, *pl[i], res[k], reinterpret_cast<const int32_t*>(cbi.h) + cb_off[i], prev_ok[i],
-             tbs.h + tb_off[i], uci.h + uci_off[i],
-             reinterpret_cast<const srs_amd_chest_port_stats*>(pstats.h) + static_cast<size_t>(k) * MAX_PORTS_HIP);
+      notify(p, j.pl[k], res[k], reinterpret_cast<const int32_t*>(bs->cbi.h) + j.cb_off[k], j.prev_ok[k],
+             bs->tbs.h + j.tb_off[k], bs->uci.h + j.uci_off[k],
+             reinterpret_cast<const srs_amd_chest_port_stats*>(bs->pstats.h) + k * MAX_PORTS_HIP);
     }
-    return errors;
   }
 
   // srs_amd_pusch_process_slot_ex on the batch's device buffers; ids: the index of each PDU in the outputs (the
   // second pass writes into the first pass's rows).
-  int run_slot(std::vector<srs_amd_pusch_slot_pdu>& sp, size_t nof_grids, size_t grid_stride,
+  int run_slot(job& j, std::vector<srs_amd_pusch_slot_pdu>& sp, hipStream_t s,
                const std::vector<unsigned>* ids = nullptr)
   {
+    buffer_set*           bs = j.bs;
     srs_amd_pusch_slot_io io{};
-    io.d_cb_iterations = reinterpret_cast<int32_t*>(cbi.d);
-    io.d_uci           = uci.d;
-    io.d_port_stats    = reinterpret_cast<srs_amd_chest_port_stats*>(pstats.d);
-    auto* d_res        = reinterpret_cast<srs_amd_pusch_processor_result*>(results.d);
+    io.d_cb_iterations = reinterpret_cast<int32_t*>(bs->cbi.d);
+    io.d_uci           = bs->uci.d;
+    io.d_port_stats    = reinterpret_cast<srs_amd_chest_port_stats*>(bs->pstats.d);
+    auto* d_res        = reinterpret_cast<srs_amd_pusch_processor_result*>(bs->results.d);
+    auto* d_grids      = reinterpret_cast<const uint32_t*>(bs->h_grids.d);
+    const uint32_t ng  = static_cast<uint32_t>(std::max<size_t>(j.nof_grids, 1));
     if (ids == nullptr) {
-      return srs_amd_pusch_process_slot_ex(proc, sp.data(), static_cast<uint32_t>(sp.size()),
-                                           reinterpret_cast<const uint32_t*>(h_grids.d), grid_stride,
-                                           static_cast<uint32_t>(nof_grids), tbs.d, d_res, &io, stream);
+      return srs_amd_pusch_process_slot_ex(proc, sp.data(), static_cast<uint32_t>(sp.size()), d_grids, j.grid_stride, ng,
+                                           bs->tbs.d, d_res, &io, s);
     }
     // one PDU per call so that results / port measurements land in the first pass's rows
-    for (size_t j = 0; j != sp.size(); ++j) {
-      const unsigned        k = (*ids)[j];
+    for (size_t q = 0; q != sp.size(); ++q) {
+      const unsigned        k = (*ids)[q];
       srs_amd_pusch_slot_io x = io;
       x.d_port_stats          = io.d_port_stats + static_cast<size_t>(k) * MAX_PORTS_HIP;
-      const int rc = srs_amd_pusch_process_slot_ex(proc, &sp[j], 1, reinterpret_cast<const uint32_t*>(h_grids.d),
-                                                   grid_stride, static_cast<uint32_t>(nof_grids), tbs.d, d_res + k,
-                                                   &x, stream);
+      const int rc = srs_amd_pusch_process_slot_ex(proc, &sp[q], 1, d_grids, j.grid_stride, ng, bs->tbs.d, d_res + k,
+                                                   &x, s);
       if (rc != SRS_AMD_OK) {
         return rc;
       }
@@ -518,20 +697,23 @@ private:
     return SRS_AMD_OK;
   }
 
-  hipError_t download(unsigned n, uint64_t tb_total, uint32_t cb_total, uint64_t uci_total, uint64_t soft_total)
+  hipError_t download(job& j, hipStream_t s)
   {
-    hipError_t e = hipMemcpyAsync(tbs.h, tbs.d, tb_total, hipMemcpyDeviceToHost, stream);
-    auto       d2h = [&](hip_mirrored_buffer& m, size_t bytes) {
+    buffer_set* bs  = j.bs;
+    const auto  m   = j.pdus.size();
+    hipError_t  e   = hipSuccess;
+    auto        d2h = [&](hip_mirrored_buffer& b, size_t bytes) {
       if (e == hipSuccess && bytes != 0) {
-        e = hipMemcpyAsync(m.h, m.d, bytes, hipMemcpyDeviceToHost, stream);
+        e = hipMemcpyAsync(b.h, b.d, bytes, hipMemcpyDeviceToHost, s);
       }
     };
-    d2h(results, sizeof(srs_amd_pusch_processor_result) * n);
-    d2h(cbi, sizeof(int32_t) * cb_total);
-    d2h(uci, uci_total);
-    d2h(pstats, sizeof(srs_amd_chest_port_stats) * MAX_PORTS_HIP * n);
-    d2h(soft, soft_total);
-    return e == hipSuccess ? hipStreamSynchronize(stream) : e;
+    d2h(bs->tbs, j.tb_total);
+    d2h(bs->results, sizeof(srs_amd_pusch_processor_result) * m);
+    d2h(bs->cbi, sizeof(int32_t) * j.cb_total);
+    d2h(bs->uci, j.uci_total);
+    d2h(bs->pstats, sizeof(srs_amd_chest_port_stats) * MAX_PORTS_HIP * m);
+    d2h(bs->soft, j.soft_total);
+    return e;
   }
 
   // rx_buffer -> device soft-buffer layout (srs_amd_pusch_soft_buffer_layout): soft bits, messages, CRC flags; the
@@ -662,18 +844,26 @@ private:
   }
 
 public:
-  std::atomic<uint64_t> stats_retx{0}, stats_redecodes{0};
+  std::atomic<uint64_t> stats_retx{0}, stats_redecodes{0}, stats_late_errors{0}, stats_device_grids{0};
 
 private:
   pusch_processor_hip_config cfg;
   const unsigned             nsubc;
-  int                        device = 0;
-  hipStream_t                stream = nullptr;
-  srs_amd_pusch_processor*   proc   = nullptr;
+  int                        device  = 0;
+  hipStream_t                stream  = nullptr; // batches
+  hipStream_t                stream2 = nullptr; // HARQ soft-buffer passes (completion thread)
+  srs_amd_pusch_processor*   proc    = nullptr;
   // collector-thread state
   std::unordered_map<std::string, plan_entry> plans;
   std::list<std::string>                      lru;
-  hip_mirrored_buffer                         h_grids, tbs, results, cbi, uci, pstats, soft;
+  row_pool                                    pool;
+  // dispatched batches (collector -> completion thread) and the buffer sets they use
+  buffer_set                        sets[2];
+  std::mutex                        jmtx;
+  std::condition_variable           jcv;
+  std::deque<std::unique_ptr<job>>  jobs;
+  bool                              completing = false, stop = false;
+  std::thread                       completer;
   // last: destroyed first, so the collector thread stops before the state it uses goes
   std::unique_ptr<slot_collector<pending_pdu>> collector;
 };

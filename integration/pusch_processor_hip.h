@@ -15,10 +15,12 @@
 //   * max_pdus_per_batch PDUs are pending, or
 //   * the oldest pending PDU has waited max_wait_us,
 // as one srs_amd_pusch_process_slot_ex call: the grids are copied from the readers (resource_grid_reader::
-// get_view, one pinned staging buffer, one H2D copy per batch), every new-data UCI-free CP-OFDM PDU runs through
-// the fused estimator-equalizer-decoder sequence, UCI / DFT-s-OFDM / HARQ PDUs through the batch chain in the same
-// call, and then each PDU's transport block is copied into its span and its notifier called (on_uci, then on_sch)
-// from the collector thread.
+// get_view, rows copied by a pool of worker threads into one of two alternating pinned staging buffers, one H2D
+// copy per batch) -- or, for grids of a hip_resource_grid factory (hip_resource_grid.h), read in place in HBM --,
+// every new-data UCI-free CP-OFDM PDU runs through the fused estimator-equalizer-decoder sequence, UCI / DFT-s-OFDM /
+// HARQ PDUs through the batch chain in the same call.  A completion thread then waits for the batch, copies each
+// PDU's transport block into its span and calls its notifier (on_uci, then on_sch), while the collector thread
+// already stages the next batch.
 //
 // HARQ state stays in the reference's rx_buffer (the uplink processor's rx_buffer_pool decides its lifetime): a
 // retransmission uploads the rx_buffer's codeblock soft bits, decoded messages and CRC flags into a device soft
@@ -72,6 +74,9 @@ struct pusch_processor_hip_config {
   unsigned max_wait_us        = 200;
   /// PDU configurations kept as C-ABI plans (plan creation uploads tables; a plan serves every slot).
   unsigned max_cached_plans = 4096;
+  /// Worker threads copying the rows of host resource grids into the batch's pinned staging buffer (0: the
+  /// collector thread alone).  Grids of a hip_resource_grid factory are used in HBM as they are.
+  unsigned nof_copy_threads = 8;
 };
 
 /// pusch_processor_factory whose processors share one slot collector and one MI355X PUSCH processor.
@@ -86,6 +91,8 @@ public:
   /// buffer, retransmissions.
   struct statistics {
     uint64_t nof_pdus = 0, nof_batches = 0, nof_errors = 0, nof_harq_redecodes = 0, nof_retransmissions = 0;
+    /// PDUs whose received grid was a hip_resource_grid read in place (no host staging, no PCIe copy).
+    uint64_t nof_device_grids = 0;
   };
   virtual statistics get_statistics() const = 0;
 };

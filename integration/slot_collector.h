@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -161,6 +162,94 @@ private:
   size_t                                in_flight = 0;
   counters                              stats;
   std::thread                           worker;
+};
+
+/// A fixed pool of worker threads for the host-side row copies of a batch (grid staging, grid merging): run(n, fn)
+/// calls fn(i) for every i < n on the workers and the calling thread and returns when all calls are done.
+class row_pool
+{
+public:
+  explicit row_pool(unsigned nof_threads)
+  {
+    for (unsigned t = 0; t < nof_threads; ++t) {
+      threads.emplace_back([this] { work(); });
+    }
+  }
+  ~row_pool()
+  {
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : threads) {
+      t.join();
+    }
+  }
+  row_pool(const row_pool&)            = delete;
+  row_pool& operator=(const row_pool&) = delete;
+
+  void run(size_t n, const std::function<void(size_t)>& fn)
+  {
+    if (n == 0) {
+      return;
+    }
+    if (threads.empty() || n == 1) {
+      for (size_t i = 0; i != n; ++i) {
+        fn(i);
+      }
+      return;
+    }
+    std::unique_lock<std::mutex> lock(run_mtx); // one run at a time
+    {
+      std::lock_guard<std::mutex> g(mtx);
+      job   = &fn;
+      count = n;
+      next.store(0);
+      done.store(0);
+      ++generation;
+    }
+    cv.notify_all();
+    drain();
+    std::unique_lock<std::mutex> g(mtx);
+    done_cv.wait(g, [&] { return done.load() == count; });
+    job = nullptr;
+  }
+
+private:
+  void drain()
+  {
+    for (size_t i = next.fetch_add(1); i < count; i = next.fetch_add(1)) {
+      (*job)(i);
+      if (done.fetch_add(1) + 1 == count) {
+        std::lock_guard<std::mutex> g(mtx);
+        done_cv.notify_all();
+      }
+    }
+  }
+  void work()
+  {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lock(mtx);
+        cv.wait(lock, [&] { return stop || (generation != seen && job != nullptr); });
+        if (stop) {
+          return;
+        }
+        seen = generation;
+      }
+      drain();
+    }
+  }
+  std::vector<std::thread>                  threads;
+  std::mutex                                mtx, run_mtx;
+  std::condition_variable                   cv, done_cv;
+  const std::function<void(size_t)>*        job   = nullptr;
+  size_t                                    count = 0;
+  std::atomic<size_t>                       next{0}, done{0};
+  uint64_t                                  generation = 0;
+  bool                                      stop       = false;
 };
 
 /// Device buffer + pinned host mirror, grown on demand (contents not preserved).

@@ -34,6 +34,12 @@ def lib():
         L.srs_ref_phy_pusch_stats.argtypes = [P, P]
         L.srs_ref_phy_pusch_bench.restype = d
         L.srs_ref_phy_pusch_bench.argtypes = [P, P, u, P, u, u, P, u, P]
+        L.srs_ref_phy_hgrid_create.restype = P
+        L.srs_ref_phy_hgrid_create.argtypes = [P, u, u, i]
+        L.srs_ref_phy_hgrid_set_device.restype = i
+        L.srs_ref_phy_hgrid_set_device.argtypes = [P, P]
+        L.srs_ref_phy_hgrid_read.argtypes = [P, P, P]
+        L.srs_ref_phy_hgrid_transfers.argtypes = [P, P]
         L.srs_ref_fapi_pusch_convert.restype = P
         L.srs_ref_fapi_pusch_convert.argtypes = [P, P, P]
         L.srs_ref_fapi_pusch_params.argtypes = [P, P]
@@ -116,6 +122,39 @@ def _result_dict(res, csi, uci, ack, c1, c2):
                 csi_part2_status=int(uci[3]), harq_ack=ack, csi_part1=c1, csi_part2=c2)
 
 
+class DeviceGrid:
+    """A device-resident grid (integration/hip_resource_grid: hip_resource_grid over the reference's
+    resource_grid_impl) of uint32 [P][14][nsubc]; usable wherever Grid / WriterGrid are.  grid: initial contents
+    through the host writer; device=True: written into the DEVICE copy instead (as the OFDM demodulator plug-in
+    would), leaving the host mirror stale."""
+
+    def __init__(self, grid=None, shape=None, device=False, hip_device=0):
+        L = lib()
+        if grid is not None:
+            g = np.ascontiguousarray(grid, np.uint32)
+            shape = g.shape
+        self.shape = tuple(shape)
+        self.h = L.srs_ref_phy_hgrid_create(None if (grid is None or device) else g.ctypes.data, self.shape[0],
+                                            self.shape[2], hip_device)
+        if grid is not None and device and L.srs_ref_phy_hgrid_set_device(self.h, g.ctypes.data) != 0:
+            raise RuntimeError("device grid write failed")
+
+    def read(self):
+        out = np.zeros(self.shape, np.uint32)
+        lib().srs_ref_phy_hgrid_read(self.h, out.ctypes.data, None)
+        return out
+
+    def transfers(self):
+        t = np.zeros(2, np.uint64)
+        lib().srs_ref_phy_hgrid_transfers(self.h, t.ctypes.data)
+        return dict(downloads=int(t[0]), uploads=int(t[1]))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().srs_ref_phy_grid_destroy(self.h)
+            self.h = None
+
+
 class Grid:
     """A received grid uint32 [P][14][nsubc] behind the reference's resource_grid_reader_impl."""
 
@@ -192,9 +231,10 @@ class PuschProcessorPlugin:
         return t, tb[:fpdu.tb_bytes]
 
     def stats(self):
-        s = np.zeros(5, np.uint64)
+        s = np.zeros(6, np.uint64)
         lib().srs_ref_phy_pusch_stats(self.h, s.ctypes.data)
-        return dict(zip(("pdus", "batches", "errors", "harq_redecodes", "retransmissions"), (int(v) for v in s)))
+        return dict(zip(("pdus", "batches", "errors", "harq_redecodes", "retransmissions", "device_grids"),
+                        (int(v) for v in s)))
 
     def bench(self, grids, pdu, tb_bytes, warmup, steps):
         """Seconds per step with one PDU per cell grid (process per PDU, flush, wait) and the TB CRC-OK count."""
@@ -343,9 +383,9 @@ class PdschProcessorPlugin:
         return bool(_L().srs_ref_phy_pdsch_done(self.h, ticket))
 
     def stats(self):
-        s = np.zeros(3, np.uint64)
+        s = np.zeros(4, np.uint64)
         _L().srs_ref_phy_pdsch_stats(self.h, s.ctypes.data)
-        return dict(zip(("pdus", "batches", "errors"), (int(v) for v in s)))
+        return dict(zip(("pdus", "batches", "errors", "device_grids"), (int(v) for v in s)))
 
     def bench(self, grids, pdu, tb, warmup, steps):
         arr = (ctypes.c_void_p * len(grids))(*[g.h for g in grids])

@@ -534,18 +534,18 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
   if (nof_pdus == 0) {
     return SRS_AMD_OK;
   }
-  if (d_grids == nullptr) {
-    return fail(SRS_AMD_EINVAL, "null device buffer");
-  }
   std::vector<pdsch_map_args>  maps;
   std::vector<dmrs_pdsch_args> dmrs;
   uint32_t                     max_tiles = 0, max_symbols = 0, max_blocks = 0, max_dmrs_symbols = 0;
   for (uint32_t i = 0; i != nof_pdus; ++i) {
     const srs_amd_pdsch_slot_pdu& u = pdus[i];
-    if (u.grid >= nof_grids) {
-      return fail(SRS_AMD_EINVAL, "PDU %u: grid index %u out of range.", i, u.grid);
+    if (u.d_grid == nullptr && (d_grids == nullptr || u.grid >= nof_grids)) {
+      return fail(SRS_AMD_EINVAL, "PDU %u: grid index %u out of range (or no grid).", i, u.grid);
     }
-    uint32_t* grid = d_grids + u.grid * grid_stride;
+    // a PDU with its own grid (device-resident resource grid) is checked as a single-grid call
+    const bool      own  = u.d_grid != nullptr;
+    uint32_t* const grid = own ? u.d_grid : d_grids + u.grid * grid_stride;
+    const uint32_t  ng   = own ? 1u : nof_grids;
     if (u.plan != nullptr) {
       const pdsch_map_args& pa  = u.plan->args;
       const uint32_t        bps = pa.qm < 2 ? 1u : static_cast<uint32_t>(pa.qm);
@@ -558,7 +558,7 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
         return fail(SRS_AMD_EINVAL, "PDU %u: the codeword length (i.e., %u bits) is shorter than the allocation.", i,
                     u.nof_bits);
       }
-      if (nof_grids > 1 && grid_stride < static_cast<uint64_t>(pa.nof_ports) * pa.port_stride) {
+      if (ng > 1 && grid_stride < static_cast<uint64_t>(pa.nof_ports) * pa.port_stride) {
         return fail(SRS_AMD_EINVAL, "grid stride too small");
       }
       if (d_codewords == nullptr) {
@@ -580,7 +580,7 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
       if (rc != SRS_AMD_OK) {
         return rc;
       }
-      if (nof_grids > 1 && grid_stride < static_cast<uint64_t>(a.nof_ports) * a.port_stride) {
+      if (ng > 1 && grid_stride < static_cast<uint64_t>(a.nof_ports) * a.port_stride) {
         return fail(SRS_AMD_EINVAL, "grid stride too small");
       }
       a.grids       = grid;

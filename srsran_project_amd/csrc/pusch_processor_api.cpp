@@ -757,7 +757,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
   if (nof_pdus == 0) {
     return SRS_AMD_OK;
   }
-  if (d_grids == nullptr || d_tbs == nullptr || d_results == nullptr) {
+  if (d_tbs == nullptr || d_results == nullptr) {
     return fail(SRS_AMD_EINVAL, "null device buffer");
   }
   constexpr uint32_t STATS_STRIDE = 4; // port measurements per PDU (at most four receive ports)
@@ -776,7 +776,8 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     if (pl->nof_subc != nof_subc) {
       return fail(SRS_AMD_EINVAL, "PDU %u: plans of different grid sizes", i);
     }
-    if (pdus[i].grid >= nof_grids || (nof_grids > 1 && grid_stride < 14ull * nof_subc * P)) {
+    if (pdus[i].d_grid == nullptr &&
+        (d_grids == nullptr || pdus[i].grid >= nof_grids || (nof_grids > 1 && grid_stride < 14ull * nof_subc * P))) {
       return fail(SRS_AMD_EINVAL, "PDU %u: grid index or grid stride out of range", i);
     }
     if (pl->has_sch && !pl->dec_cfg.new_data && pdus[i].d_soft == nullptr) {
@@ -800,6 +801,10 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
       ccfg[i].slot_index = pdus[i].slot_index;
     }
   }
+  // each PDU's received grid: its own device grid, or its slot of d_grids
+  auto grid_of = [&](const srs_amd_pusch_slot_pdu& u) {
+    return u.d_grid != nullptr ? u.d_grid : d_grids + u.grid * grid_stride;
+  };
   auto                        s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(proc->mtx);
   // 1. PDUs outside the fused group: each through its plan's batch chain on this stream
@@ -817,7 +822,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
       x.d_csi_part2      = pl->csi2 ? row + pl->pdu.nof_harq_ack + pl->pdu.nof_csi_part1 : nullptr;
       x.csi_part2_stride = std::max<uint32_t>(pl->max_csi2, 1);
     }
-    const int rc = process_batch_locked(proc, pl, d_grids + pdus[i].grid * grid_stride, grid_stride, 1,
+    const int rc = process_batch_locked(proc, pl, grid_of(pdus[i]), grid_stride, 1,
                                         d_tbs + pdus[i].tb_offset, std::max<uint32_t>(pl->pdu.tbs / 8, 1),
                                         d_results + i, pdus[i].d_soft, &x, stream, &ccfg[i]);
     if (rc != SRS_AMD_OK) {
@@ -868,7 +873,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
   std::vector<chest_slot_item> citems(n);
   for (uint32_t k = 0; k != n; ++k) {
     const srs_amd_pusch_slot_pdu& u = pdus[fused[k]];
-    citems[k] = chest_slot_item{&ccfg[fused[k]], d_grids + u.grid * grid_stride, u.plan->pdu.nof_rx_ports,
+    citems[k] = chest_slot_item{&ccfg[fused[k]], grid_of(u), u.plan->pdu.nof_rx_ports,
                                 stats_of(k)};
   }
   std::vector<chest_args> views(n);

@@ -238,54 +238,93 @@ def test_pdsch_plugin_two_slots_two_cells(phy):
 
 def test_plugin_throughput_64_cells(phy):
     """Codeblocks/s THROUGH the plug-ins at the headline shape (64 cells of 100 MHz / 273 PRB, PUSCH 4 layers x 4
-    rx MMSE 256QAM, PDSCH 4 layers x 4 ports 256QAM): per step, one process() per cell on the cell's host
-    resource grid (the reference's reader / writer), flush() at the slot boundary, wait for every notification --
-    host grids in and out, so the figure includes the grid copies over PCIe.  Written to
-    gpurun_out/plugin_bench.json next to the headline (which keeps grids resident in HBM)."""
+    rx MMSE 256QAM, PDSCH 4 layers x 4 ports 256QAM): per step, one process() per cell on the cell's resource grid,
+    flush() at the slot boundary, wait for every notification.  Two grid kinds:
+      host    the reference's reader / writer over host memory: grids staged over PCIe each step (row copies by the
+              plug-ins' worker threads, two alternating buffer sets, completion on a separate thread);
+      device  hip_resource_grid (integration/hip_resource_grid.h): the grids live in HBM (as the OFDM plug-ins produce
+              / consume them) and the plug-ins work on them in place.
+    Each kind is timed PUSCH alone, PDSCH alone, and both at once (two host threads, as the uplink and downlink
+    processors run).  Written to gpurun_out/plugin_bench.json.  Floors: the device-grid PDSCH + PUSCH figure at least
+    8 M codeblocks/s (VERDICT r4 #3), and the host-grid one at least 2x round 4's 1.85 M."""
     import json
     import os
+    import threading
 
     import torch
 
     import bench_pipeline as bp
 
     ophy, oracle = phy
-    cells, warmup, steps = 64, 2, 8
+    cells, warmup, steps = 64, 2, 10
     dev = torch.device("cuda:0")
     pl = bp.Pipeline(1, dev)
     pl.step(torch.cuda.current_stream(dev))
     torch.cuda.synchronize()
     grid = pl.grid_ul[0].cpu().numpy().view(np.uint32)
     tb_ul = pl.tb_ul[0].cpu().numpy()
-    # PUSCH
-    grids = [ophy.Grid(grid) for _ in range(cells)]
-    plug = ophy.PuschProcessorPlugin(device=0, iterations=bp.LDPC_ITERS, mmse=True)
-    dt_ul, ok, tbs = plug.bench(grids, pl.pdu_ul, pl.tbs_ul // 8, warmup, steps)
-    assert ok == cells * steps and all(np.array_equal(t, tb_ul) for t in tbs)
-    # PDSCH
+    tb_dl = pl.tb_dl[0].cpu().numpy()
     from oracle.phy import make_pdsch_pdu
 
-    pdu = make_pdsch_pdu(range(bp.NPRB), bp.dl_weights(), slot_index=bp.SLOT, rnti=bp.RNTI, qm=bp.QM, n_id=bp.N_ID,
-                         dmrs_symbol_mask=bp.DMRS_MASK, scrambling_id=bp.N_ID, nof_cdm_groups_without_data=bp.NCDM,
-                         start_symbol_index=bp.DL_START, nof_symbols=bp.DL_NSYM,
-                         base_graph=bp.base_graph(pl.tbs_dl, bp.RATE / 1024), ratio_pdsch_dmrs_to_sss_dB=-3.0)
-    wgrids = [ophy.WriterGrid(np.zeros((bp.DL_PORTS, 14, bp.NSUBC), np.uint32)) for _ in range(cells)]
-    dplug = ophy.PdschProcessorPlugin(device=0)
-    tb_dl = pl.tb_dl[0].cpu().numpy()
-    dt_dl = dplug.bench(wgrids, pdu, tb_dl, warmup, steps)
-    # the plug-in's grid equals the Python-driven pipeline's PDSCH grid of the same transport block
-    np.testing.assert_array_equal(wgrids[0].read(), pl.grid_dl[0].cpu().numpy().view(np.uint32))
+    pdu_dl = make_pdsch_pdu(range(bp.NPRB), bp.dl_weights(), slot_index=bp.SLOT, rnti=bp.RNTI, qm=bp.QM, n_id=bp.N_ID,
+                            dmrs_symbol_mask=bp.DMRS_MASK, scrambling_id=bp.N_ID, nof_cdm_groups_without_data=bp.NCDM,
+                            start_symbol_index=bp.DL_START, nof_symbols=bp.DL_NSYM,
+                            base_graph=bp.base_graph(pl.tbs_dl, bp.RATE / 1024), ratio_pdsch_dmrs_to_sss_dB=-3.0)
     c_ul, c_dl = pl.plan_ul.nof_segments, pl.plan_dl.nof_segments
-    res = dict(cells=cells, steps=steps, pusch_ms_per_step=dt_ul * 1e3, pdsch_ms_per_step=dt_dl * 1e3,
-               pusch_codeblocks_per_s=cells * c_ul / dt_ul, pdsch_codeblocks_per_s=cells * c_dl / dt_dl,
-               pdsch_pusch_codeblocks_per_s_serial=cells * (c_ul + c_dl) / (dt_ul + dt_dl),
-               pusch_stats=plug.stats(), pdsch_stats=dplug.stats(),
-               note="host resource grids through the reference's reader / writer, one process() per cell, flush, "
-                    "wait; PUSCH and PDSCH timed one after the other")
+    want_dl = pl.grid_dl[0].cpu().numpy().view(np.uint32)
+    zeros = np.zeros((bp.DL_PORTS, 14, bp.NSUBC), np.uint32)
+    plug = ophy.PuschProcessorPlugin(device=0, iterations=bp.LDPC_ITERS, mmse=True)
+    dplug = ophy.PdschProcessorPlugin(device=0)
+    res = dict(cells=cells, steps=steps)
+    for kind in ("host", "device"):
+        if kind == "host":
+            ul = [ophy.Grid(grid) for _ in range(cells)]
+            dl = [ophy.WriterGrid(zeros) for _ in range(cells)]
+        else:
+            ul = [ophy.DeviceGrid(grid, device=True) for _ in range(cells)]
+            dl = [ophy.DeviceGrid(zeros) for _ in range(cells)]
+        out = {}
+
+        def run_ul():
+            out["ul"] = plug.bench(ul, pl.pdu_ul, pl.tbs_ul // 8, warmup, steps)
+
+        def run_dl():
+            out["dl"] = dplug.bench(dl, pdu_dl, tb_dl, warmup, steps)
+
+        run_ul()
+        run_dl()
+        dt_ul, ok, tbs = out["ul"]
+        dt_dl = out["dl"]
+        assert ok == cells * steps and all(np.array_equal(t, tb_ul) for t in tbs), kind
+        # the plug-in's grid equals the Python-driven pipeline's PDSCH grid of the same transport block
+        np.testing.assert_array_equal(dl[0].read(), want_dl, err_msg=kind)
+        # both at once: the uplink and downlink processors on two threads (ctypes releases the GIL)
+        th = [threading.Thread(target=run_ul), threading.Thread(target=run_dl)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        wall = time.perf_counter() - t0
+        both_steps = wall / (warmup + steps)  # both benches run warmup + steps steps
+        res[kind] = dict(pusch_ms_per_step=dt_ul * 1e3, pdsch_ms_per_step=dt_dl * 1e3,
+                         pusch_codeblocks_per_s=cells * c_ul / dt_ul, pdsch_codeblocks_per_s=cells * c_dl / dt_dl,
+                         concurrent_ms_per_step=both_steps * 1e3,
+                         pdsch_pusch_codeblocks_per_s=cells * (c_ul + c_dl) / both_steps)
+        if kind == "device":
+            res[kind]["ul_grid_transfers"] = ul[0].transfers()
+            res[kind]["dl_grid_transfers"] = dl[1].transfers()
+    res["pusch_stats"], res["pdsch_stats"] = plug.stats(), dplug.stats()
+    res["note"] = ("one process() per cell, flush, wait; concurrent = the PUSCH and PDSCH benches on two host threads "
+                   "at once, codeblocks of both over the wall time per step")
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/plugin_bench.json", "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
+    # device-resident grids: no grid crosses PCIe in the timed steps
+    assert res["device"]["ul_grid_transfers"]["downloads"] == 0 and res["device"]["dl_grid_transfers"]["downloads"] <= 1
+    assert res["device"]["pdsch_pusch_codeblocks_per_s"] >= 8e6, res["device"]
+    assert res["host"]["pdsch_pusch_codeblocks_per_s"] >= 3.7e6, res["host"]
 
 
 # ---- PDUs as the reference's FAPI adaptor produces them (VERDICT r4 #1) ----
