@@ -119,3 +119,5 @@ from .ulsch_info import UlschConfig, UlschInfo, ulsch_information  # noqa: F401,
 from .ulsch_demux import UlschDemux, UlschDemuxConfig, UlschDemuxPlan  # noqa: F401,E402
 from .uci_decoder import UCI_INVALID, UCI_UNKNOWN, UCI_VALID, UciDecoder  # noqa: F401,E402
 from . import profiling  # noqa: F401,E402
+from . import pdcch  # noqa: F401,E402
+from .pdcch import CceToRegMapping, PdcchPdu, PdcchProcessor  # noqa: F401,E402
