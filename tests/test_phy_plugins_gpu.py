@@ -458,3 +458,65 @@ def test_pusch_plugin_three_slots_one_config(phy):
         assert got["tb_crc_ok"] and np.array_equal(tb, tb_sent) and np.array_equal(tb, want_tb)
     s = plug.stats()
     assert s["batches"] == 3 and s["pdus"] == 3, s
+
+
+def _pdcch_grid(seed, ports, nsubc):
+    g = np.random.default_rng(seed).integers(0, 2**32, (ports, 14, nsubc), dtype=np.uint64)
+    return g.astype(np.uint32)
+
+
+def test_pdcch_plugin_vs_reference(phy):
+    """pdcch_processor_factory_hip's processors, driven through the reference's pdcch_processor
+    interface, write exactly the grid pdcch_processor_impl writes -- on a host writer grid (the REs of the DCI's CRBs
+    stored through get_view) and on a device-resident hip_resource_grid (written in place, read back once by the host
+    reader) -- for every case PDU, and for five DCIs of two CORESETs on one grid."""
+    from oracle import pdcch as op
+    from tests.pdcch_cases import cases, slot_pdus
+
+    ophy, _ = phy
+    plug = ophy.PdcchProcessorPlugin(device=0)
+    for i, (name, pdu) in enumerate(cases()):
+        c = pdu.coreset
+        nsubc = 12 * min(c.bwp_start_rb + c.bwp_size_rb + 2, 275)
+        g0 = _pdcch_grid(i, pdu.dci.nof_ports + 1, nsubc)
+        want = op.ref_process(g0.copy(), [pdu])
+        wg = ophy.WriterGrid(g0)
+        plug.process(wg, [pdu])
+        assert np.array_equal(wg.read(), want), (name, "host grid")
+        dg = ophy.DeviceGrid(g0)
+        plug.process(dg, [pdu])
+        assert np.array_equal(dg.read(), want), (name, "device grid")
+        assert dg.transfers() == dict(downloads=1, uploads=1), name
+        assert plug.validate(pdu) is None, name
+    nsubc = 12 * 106
+    pdus = [p for p in slot_pdus(1, nsubc)]
+    g0 = _pdcch_grid(99, 2, nsubc)
+    want = op.ref_process(g0.copy(), pdus)
+    dg = ophy.DeviceGrid(g0, device=True)
+    plug.process(dg, pdus)
+    assert np.array_equal(dg.read(), want), "five DCIs, device grid"
+    wg = ophy.WriterGrid(g0)
+    plug.process(wg, pdus)
+    assert np.array_equal(wg.read(), want), "five DCIs, host grid"
+    s = plug.stats()
+    n = len(cases())
+    assert s == dict(pdus=2 * n + 2 * len(pdus), errors=0, device_grids=n + len(pdus)), s
+
+
+def test_pdcch_plugin_validator_and_unsupported(phy):
+    """The plug-in factory's validator rejects what pdcch_processor_validator_impl rejects (same messages); an invalid
+    PDU handed to process anyway is logged and counted, and leaves the grid untouched."""
+    from srsran_project_amd.pdcch import make_pdu
+    from tests.pdcch_cases import INVALID
+
+    ophy, _ = phy
+    plug = ophy.PdcchProcessorPlugin(device=0)
+    for name, kw, text in INVALID:
+        pdu = make_pdu(np.ones(20, np.uint8), **kw)
+        msg = plug.validate(pdu)
+        assert msg is not None and text in msg, (name, msg)
+    g0 = _pdcch_grid(3, 1, 12 * 52)
+    wg = ophy.WriterGrid(g0)
+    plug.process(wg, [make_pdu(np.ones(20, np.uint8), aggregation_level=3)])
+    assert np.array_equal(wg.read(), g0)
+    assert plug.stats()["errors"] == 1
