@@ -11,6 +11,10 @@
  *   dmrs_pdsch_processor::map(resource_grid_writer&, const config_t&)
  *       include/srsran/phy/upper/signal_processors/pdsch/dmrs_pdsch_processor.h:65
  *       (impl lib/phy/upper/signal_processors/pdsch/dmrs_pdsch_processor_impl.cpp:126-234)
+ *   ptrs_pdsch_generator::generate(resource_grid_writer&, const configuration&)
+ *       include/srsran/phy/upper/signal_processors/ptrs/ptrs_pdsch_generator.h
+ *       (impl lib/phy/upper/signal_processors/ptrs/ptrs_pdsch_generator_impl.cpp:30-130, the pattern of
+ *        lib/ran/ptrs/ptrs_pattern.cpp:54-110), as the third launch of the slot form
  *
  * Resource grids are complex bf16 (real in the low 16 bits of each 32-bit RE)
  * [port][symbol (14)][subcarrier], the reference's resource_grid_impl storage.
@@ -101,6 +105,35 @@ int  srs_amd_pdsch_mod_plan_create(srs_amd_pdsch_modulator*        mod,
                                    uint32_t*                       nof_re);
 void srs_amd_pdsch_mod_plan_destroy(srs_amd_pdsch_mod_plan* plan);
 
+/* PDSCH PT-RS (ptrs_pdsch_generator::configuration, ptrs_pdsch_generator.h; pdsch_process_ptrs,
+ * pdsch_processor_helpers.h:78-118, builds it from the PDU).  Contiguous allocations (get_ptrs_pattern). */
+typedef struct srs_amd_ptrs_pdsch_config {
+  uint32_t     slot_index;           /* slot_point::slot_index() */
+  uint32_t     rnti;
+  uint32_t     dmrs_type;            /* 1 or 2 */
+  uint32_t     reference_point_k_rb;
+  uint32_t     scrambling_id;
+  uint32_t     n_scid;
+  float        amplitude;            /* convert_dB_to_amplitude(PT-RS to data ratio - data to SSS ratio) */
+  uint32_t     dmrs_symbols_mask;
+  uint8_t      crb_mask[SRS_AMD_CRB_MASK_BYTES]; /* the PDSCH CRBs (contiguous) */
+  uint8_t      reserved0;
+  uint32_t     start_symbol;         /* time allocation */
+  uint32_t     nof_symbols;
+  uint32_t     freq_density;         /* K_PT-RS: 2 or 4 */
+  uint32_t     time_density;         /* L_PT-RS: 1, 2 or 4 */
+  uint32_t     re_offset;            /* ptrs_re_offset: 0 .. 3 */
+  uint32_t     nof_ports;            /* transmit ports, 1 .. 4 */
+  uint32_t     nof_prg;              /* precoding PRGs, >= 1 */
+  uint32_t     prg_size;             /* PRBs per PRG */
+  const float* weights;              /* HOST [nof_prg][nof_ports] (re, im): the layer-0 weights (TS 38.214 5.1.6.3) */
+} srs_amd_ptrs_pdsch_config;
+
+/* The PT-RS REs as an RE pattern (get_ptrs_pattern, ptrs_pattern.cpp:54-110, with one port), validating cfg.  The
+ * reference's PDSCH processor maps data over them and then the PT-RS (pdsch_processor_hip.h explains why its
+ * codeword does not exclude them either). */
+int srs_amd_ptrs_pdsch_reserved(const srs_amd_ptrs_pdsch_config* cfg, srs_amd_re_pattern* pattern);
+
 /* HOST, synchronous: grid [grid_ports][14][nof_subc] cbf16 (as uint32) updated in
  * place; codeword packed MSB first (bit_buffer), nof_bits bits. */
 int srs_amd_pdsch_modulate(srs_amd_pdsch_modulator*      mod,
@@ -111,10 +144,13 @@ int srs_amd_pdsch_modulate(srs_amd_pdsch_modulator*      mod,
                            uint32_t                      nof_bits);
 
 /* DEVICE, asynchronous: nof_cws codewords (rows of cw_stride bytes) into nof_cws
- * grids (grid_stride REs apart, ports nof_subc * 14 REs apart).  nof_bits >= nof_re x layers x Qm: a longer
- * codeword maps its first nof_re x layers modulation symbols and the rest is dropped, as the reference's
- * resource_grid_mapper consumes the symbol buffer only up to the allocation (pdsch_processor_impl sizes a DM-RS
- * type-2 codeword with the type-2 pattern but maps it around the type-1 one, see pdsch_processor_hip.h). */
+ * grids (grid_stride REs apart, ports nof_subc * 14 REs apart).  A codeword of other than nof_re x layers x Qm
+ * bits maps as the reference's resource_grid_mapper consumes its symbol buffer: a longer one maps its first
+ * nof_re x layers modulation symbols and the rest is dropped (pdsch_processor_impl sizes a DM-RS type-2 codeword
+ * with the type-2 pattern but maps it around the type-1 one, see pdsch_processor_hip.h); a shorter one fills the
+ * first nof_bits / (layers x Qm) REs of the allocation in mapping order and leaves the others untouched, the mapper
+ * stopping when its buffer runs empty (resource_grid_mapper_impl.cpp:453-456 -- a PT-RS PDU's codeword, sized
+ * without the PT-RS REs). */
 int srs_amd_pdsch_modulate_batch(srs_amd_pdsch_modulator*      mod,
                                  const srs_amd_pdsch_mod_plan* plan,
                                  uint32_t*                     d_grids,
@@ -150,6 +186,7 @@ typedef struct srs_amd_pdsch_slot_pdu {
   uint64_t                         cw_offset; /* byte offset of the packed codeword in d_codewords */
   uint32_t*                        d_grid;    /* non-NULL: this PDU's own DEVICE grid cbf16 [port][14][nof_subc]
                                                  (a device-resident resource grid), instead of d_grids[grid] */
+  const srs_amd_ptrs_pdsch_config* ptrs;      /* NULL: no PT-RS; else mapped after the data and before the DM-RS */
 } srs_amd_pdsch_slot_pdu;
 
 /* DEVICE, asynchronous: every PDSCH PDU of a slot -- several UEs on disjoint PRBs of one grid (or of several

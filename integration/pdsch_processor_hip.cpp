@@ -73,6 +73,10 @@ struct pending_pdu {
   srs_amd_dmrs_pdsch_config dmrs{};
   uint32_t                  numerology = 0;
   std::string               error;
+  // PT-RS (pdsch_process_ptrs, pdsch_processor_helpers.h:78-118): its configuration and layer-0 weights per PRG
+  bool                      has_ptrs = false;
+  srs_amd_ptrs_pdsch_config ptrs{};
+  std::vector<float>        ptrs_w;
 };
 
 template <typename Mask>
@@ -93,9 +97,6 @@ std::string convert(pending_pdu& p, unsigned nof_prb)
   if (pdu.cp != cyclic_prefix::NORMAL) {
     return "extended cyclic prefix";
   }
-  if (pdu.ptrs.has_value()) {
-    return "PT-RS";
-  }
   if (pdu.codewords.size() != 1) {
     return "two codewords";
   }
@@ -105,6 +106,10 @@ std::string convert(pending_pdu& p, unsigned nof_prb)
   if (L == 0 || L > SRS_AMD_MAX_LAYERS || P == 0 || P > MAX_PORTS || P < L) {
     return "layers / ports outside 1..4";
   }
+  // precoding that differs between PRGs: the reference's data mapper would take the first PRG's weights for every
+  // PRB (resource_grid_mapper_impl.cpp:322-323), but its DM-RS processor writes PRG >= 1 weights into a one-PRG
+  // configuration (dmrs_pdsch_processor_impl.cpp:150-160: an assertion, or an out-of-bounds write without asserts),
+  // so there is no reference output to reproduce
   for (unsigned g = 1; g < pc.get_nof_prg(); ++g) {
     if (!(pc.get_prg_coefficients(g) == pc.get_prg_coefficients(0))) {
       return "precoding that differs between PRGs";
@@ -173,6 +178,42 @@ std::string convert(pending_pdu& p, unsigned nof_prb)
   d.nof_ports  = P;
   std::memcpy(d.weights, m.weights, sizeof(d.weights));
   p.numerology = to_numerology_value(pdu.slot.scs());
+  p.has_ptrs   = pdu.ptrs.has_value();
+  if (p.has_ptrs) {
+    const pdsch_processor::ptrs_configuration& t = *pdu.ptrs;
+    srs_amd_ptrs_pdsch_config&                 c = p.ptrs;
+    c                                            = srs_amd_ptrs_pdsch_config{};
+    c.slot_index                                 = d.slot_index;
+    c.rnti                                       = pdu.rnti;
+    c.dmrs_type                                  = d.type;
+    c.reference_point_k_rb                       = d.reference_point_k_rb;
+    c.scrambling_id                              = pdu.scrambling_id;
+    c.n_scid                                     = d.n_scid;
+    c.amplitude         = convert_dB_to_amplitude(t.ratio_ptrs_to_pdsch_data_dB - pdu.ratio_pdsch_data_to_sss_dB);
+    c.dmrs_symbols_mask = m.dmrs_symbol_mask;
+    std::memcpy(c.crb_mask, m.crb_mask, sizeof(c.crb_mask));
+    c.start_symbol = pdu.start_symbol_index;
+    c.nof_symbols  = pdu.nof_symbols;
+    c.freq_density = to_value(t.freq_density);
+    c.time_density = to_value(t.time_density);
+    c.re_offset    = to_value(t.re_offset);
+    c.nof_ports    = P;
+    c.nof_prg      = pc.get_nof_prg();
+    c.prg_size     = pc.get_prg_size();
+    p.ptrs_w.resize(2 * c.nof_prg * P);
+    for (unsigned g = 0; g != c.nof_prg; ++g) {
+      for (unsigned q = 0; q != P; ++q) {
+        const cf_t w                   = pc.get_coefficient(0, q, g);
+        p.ptrs_w[2 * (g * P + q)]     = w.real();
+        p.ptrs_w[2 * (g * P + q) + 1] = w.imag();
+      }
+    }
+    c.weights = p.ptrs_w.data();
+    srs_amd_re_pattern pattern; // validates the PT-RS configuration (the pattern itself reserves nothing, see .h)
+    if (srs_amd_ptrs_pdsch_reserved(&c, &pattern) != SRS_AMD_OK) {
+      return srs_amd_last_error();
+    }
+  }
   return {};
 }
 
@@ -487,6 +528,11 @@ private:
       srs_amd_pdsch_slot_pdu s{};
       s.plan      = pl[k]->plan;
       s.dmrs      = &p.dmrs;
+      if (p.has_ptrs) {
+        pending_pdu& q    = j->pdus[k];
+        q.ptrs.weights    = q.ptrs_w.data();
+        s.ptrs            = &q.ptrs;
+      }
       s.nof_bits  = ues[k].plan.cw_length;
       s.cw_offset = ues[k].cw_offset;
       if (grid_of[k] & 0x80000000u) {

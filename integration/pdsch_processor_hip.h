@@ -20,10 +20,19 @@
 // (pdsch_processor_impl.cpp:185-200 leaves pdsch_modulator::config_t::dmrs_config_type unset), so a type-2 PDU's
 // data skips its DM-RS symbols entirely (two CDM groups) and the codeword's last symbols are not mapped.
 //
+// PT-RS (pdsch_processor_impl.cpp:82-84, ptrs_pdsch_generator_impl.cpp) as the reference does it: the data mapper
+// does not skip the PT-RS REs (the modulator gets only the PDU's reserved list, pdsch_processor_impl.cpp:148) and the
+// codeword covers them too -- pdsch_compute_nof_data_re (pdsch_processor_helpers.h:146-175) builds the PT-RS pattern
+// it merges into the reserved list on a default re_pattern, whose CRB bitmap has size 0, so its set() calls land
+// outside the bitmap and the pattern counts no RE -- then the PT-RS overwrites the data at its REs.
+// The PT-RS kernel precodes per PRG (srs_amd_ptrs_pdsch_config).
+//
 // Not supported (logged; the PDU's REs are not written, on_finish_processing still called so the downlink processor
-// never stalls): PT-RS, more than four layers (two codewords), more than four ports, precoding that differs between
-// PRGs, more than eight reserved RE patterns, extended cyclic prefix.  Compiled against the reference's headers by
-// integration/Makefile.
+// never stalls): more than four layers (two codewords), more than four ports, more than eight reserved RE patterns,
+// extended cyclic prefix, and precoding that differs between PRGs -- the reference's DM-RS processor writes the
+// weights of PRG >= 1 into a one-PRG configuration (dmrs_pdsch_processor_impl.cpp:150-160), an assertion with
+// asserts on and an out-of-bounds write without (tests/test_oracle_vs_ref.py shows it crash), so it has no output to
+// reproduce.  Compiled against the reference's headers by integration/Makefile.
 #pragma once
 
 #include "srsran/phy/upper/channel_processors/pdsch/factories.h"

@@ -259,11 +259,16 @@ class PdschPdu(ctypes.Structure):
         [(n, ctypes.c_uint32) for n in ("start_symbol_index", "nof_symbols", "base_graph", "tbs_lbrm_bytes")] + \
         [("ratio_pdsch_dmrs_to_sss_dB", ctypes.c_float), ("ratio_pdsch_data_to_sss_dB", ctypes.c_float),
          ("nof_layers", ctypes.c_uint32), ("nof_ports", ctypes.c_uint32), ("weights", ctypes.c_float * 32),
-         ("nof_reserved", ctypes.c_uint32), ("reserved", RePattern * 8)]
+         ("nof_reserved", ctypes.c_uint32), ("reserved", RePattern * 8)] + \
+        [(n, ctypes.c_uint32) for n in ("has_ptrs", "ptrs_freq_density", "ptrs_time_density", "ptrs_re_offset")] + \
+        [("ratio_ptrs_to_pdsch_data_dB", ctypes.c_float), ("nof_prg", ctypes.c_uint32), ("prg_size", ctypes.c_uint32),
+         ("prg_weights", ctypes.c_float * (7 * 32))]
 
 
-def make_pdsch_pdu(vrbs, weights, reserved=(), **kw):
-    """vrbs: the BWP-relative VRB indices; weights complex [L][P]; reserved: [(crb bool mask, re_mask, symbols)]."""
+def make_pdsch_pdu(vrbs, weights, reserved=(), ptrs=None, prg=None, **kw):
+    """vrbs: the BWP-relative VRB indices; weights complex [L][P] (PRG 0); reserved: [(crb bool mask, re_mask,
+    symbols)]; ptrs: (frequency density, time density, RE offset, PT-RS to data ratio dB); prg: (PRG size in PRBs,
+    [weights complex [L][P] of PRG 1, 2, ..])."""
     p = PdschPdu()
     d = dict(numerology=1, slot_index=0, rnti=1, bwp_start_rb=0, bwp_size_rb=273, qm=2, rv=0, n_id=0, ref_point=0,
              dmrs_symbol_mask=(1 << 2) | (1 << 11), dmrs_type=1, scrambling_id=0, n_scid=0,
@@ -280,6 +285,19 @@ def make_pdsch_pdu(vrbs, weights, reserved=(), **kw):
         for q in range(W.shape[1]):
             p.weights[(l * 4 + q) * 2] = float(W[l, q].real)
             p.weights[(l * 4 + q) * 2 + 1] = float(W[l, q].imag)
+    if ptrs is not None:
+        p.has_ptrs = 1
+        p.ptrs_freq_density, p.ptrs_time_density, p.ptrs_re_offset = (int(v) for v in ptrs[:3])
+        p.ratio_ptrs_to_pdsch_data_dB = float(ptrs[3])
+    if prg is not None:
+        p.prg_size, extra = int(prg[0]), prg[1]
+        p.nof_prg = 1 + len(extra)
+        for g, Wg in enumerate(extra):
+            Wg = np.asarray(Wg, np.complex64)
+            for l in range(Wg.shape[0]):
+                for q in range(Wg.shape[1]):
+                    p.prg_weights[((g * 4 + l) * 4 + q) * 2] = float(Wg[l, q].real)
+                    p.prg_weights[((g * 4 + l) * 4 + q) * 2 + 1] = float(Wg[l, q].imag)
     p.nof_reserved = len(reserved)
     for r, (cm, rm, sm) in enumerate(reserved):
         cm = np.asarray(cm, bool)

@@ -224,6 +224,11 @@ struct srs_ref_pdsch_pdu {
   float              weights[4][4][2];
   uint32_t           nof_reserved;
   srs_amd_re_pattern reserved[SRS_AMD_MAX_RE_PATTERNS];
+  // PT-RS (has_ptrs != 0) and per-PRG precoding (nof_prg > 1: PRG g >= 1 from prg_weights[g - 1])
+  uint32_t           has_ptrs, ptrs_freq_density, ptrs_time_density, ptrs_re_offset;
+  float              ratio_ptrs_to_pdsch_data_dB;
+  uint32_t           nof_prg, prg_size;
+  float              prg_weights[7][4][4][2];
 };
 
 pdsch_processor::pdu_t to_pdsch_pdu(const srs_ref_pdsch_pdu& c)
@@ -286,7 +291,25 @@ pdsch_processor::pdu_t to_pdsch_pdu(const srs_ref_pdsch_pdu& c)
       w.set_coefficient(cf_t(c.weights[l][q][0], c.weights[l][q][1]), l, q);
     }
   }
-  pdu.precoding = precoding_configuration::make_wideband(w);
+  if (c.nof_prg > 1) {
+    pdu.precoding = precoding_configuration(c.nof_layers, c.nof_ports, c.nof_prg, c.prg_size);
+    for (unsigned g = 0; g != c.nof_prg; ++g) {
+      for (unsigned l = 0; l != c.nof_layers; ++l) {
+        for (unsigned q = 0; q != c.nof_ports; ++q) {
+          const float* v = g == 0 ? c.weights[l][q] : c.prg_weights[g - 1][l][q];
+          pdu.precoding.set_coefficient(cf_t(v[0], v[1]), l, q, g);
+        }
+      }
+    }
+  } else {
+    pdu.precoding = precoding_configuration::make_wideband(w);
+  }
+  if (c.has_ptrs) {
+    pdu.ptrs = pdsch_processor::ptrs_configuration{static_cast<ptrs_frequency_density>(c.ptrs_freq_density),
+                                                   static_cast<ptrs_time_density>(c.ptrs_time_density),
+                                                   static_cast<ptrs_re_offset>(c.ptrs_re_offset),
+                                                   c.ratio_ptrs_to_pdsch_data_dB};
+  }
   return pdu;
 }
 

@@ -148,6 +148,9 @@ __global__ __launch_bounds__(PDSCH_THREADS) void pdsch_map_kernel(pdsch_map_args
     return;
   }
   const uint32_t j = (e >> 12) + __builtin_popcount(e & ((1u << bit) - 1u));
+  if ((j + 1) * bits_per_re > a.nof_bits) {
+    return; // past a shorter codeword: the reference's mapper stops when its symbol buffer runs empty
+  }
 
   const int bps = a.qm < 2 ? 1 : a.qm;
   float2    x[4];
@@ -320,6 +323,38 @@ hipError_t launch_dmrs_pdsch_items(const dmrs_pdsch_args* items, uint32_t count,
   }
   hipLaunchKernelGGL(dmrs_pdsch_kernel<true>, dim3(max_crb_blocks, max_symbols, count), dim3(DMRS_THREADS), 0,
                      stream, dmrs_pdsch_args{}, items, 1u);
+  return hipGetLastError();
+}
+
+// PT-RS (ptrs_pdsch_generator_impl.cpp:30-130): one thread per (PT-RS PRB, symbol).  The reference generates the
+// DM-RS-like sequence of the first DM-RS symbol from the pattern's first PRB and picks every rb_stride-th PRB's
+// re_offset / 2-th element; the same values go on every PT-RS symbol, precoded per PRG (the generic mapper path,
+// resource_grid_mapper_impl.cpp:258-286, PRG = CRB / prg_size).
+__global__ __launch_bounds__(64) void ptrs_pdsch_kernel(const ptrs_pdsch_args* items)
+{
+  const ptrs_pdsch_args& a = items[blockIdx.z];
+  const uint32_t         i = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t         l = blockIdx.y;
+  if (i >= a.nof_prb || ((a.symbol_mask >> l) & 1u) == 0) {
+    return;
+  }
+  const uint32_t b    = a.bit0 + i * a.bit_step; // even: both bits in one word
+  const uint32_t bits = gold_word(a.jump, a.c_init, 32 * (b / 32)) >> (b % 32);
+  const float2   x    = make_float2((bits & 1u) ? -a.amplitude : a.amplitude, (bits & 2u) ? -a.amplitude : a.amplitude);
+  const uint32_t crb  = a.rb_begin + i * a.rb_stride;
+  const float*   w    = a.w + 2 * (crb / a.prg_size) * a.nof_ports;
+  uint32_t*      re   = a.grid + static_cast<uint64_t>(l) * a.nof_subc + crb * PDSCH_NRE + a.k;
+  for (uint32_t p = 0; p < a.nof_ports; ++p) {
+    re[static_cast<uint64_t>(p) * a.port_stride] = pack_cbf16(cmul_simd(x, w[2 * p], w[2 * p + 1]));
+  }
+}
+
+hipError_t launch_ptrs_pdsch_items(const ptrs_pdsch_args* items, uint32_t count, uint32_t max_prb, hipStream_t stream)
+{
+  if (count == 0 || max_prb == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(ptrs_pdsch_kernel, dim3((max_prb + 63) / 64, PDSCH_NSYMB, count), dim3(64), 0, stream, items);
   return hipGetLastError();
 }
 

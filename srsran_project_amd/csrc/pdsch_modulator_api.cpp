@@ -314,11 +314,9 @@ int srs_amd_pdsch_modulate_batch(srs_amd_pdsch_modulator*      mod,
   }
   const pdsch_map_args& pa  = plan->args;
   const uint32_t        bps = pa.qm < 2 ? 1u : static_cast<uint32_t>(pa.qm);
-  if (static_cast<uint64_t>(nof_bits) < static_cast<uint64_t>(plan->nof_re) * pa.nof_layers * bps) {
-    return fail(SRS_AMD_EINVAL,
-                "The codeword length (i.e., %u bits) is shorter than the allocation (i.e., %u RE x %d layers x %u "
-                "bits).",
-                nof_bits, plan->nof_re, pa.nof_layers, bps);
+  if (nof_bits == 0 || nof_bits % (pa.nof_layers * bps) != 0) {
+    return fail(SRS_AMD_EINVAL, "The codeword length (i.e., %u bits) is not a whole number of REs (%d layers x %u bits).",
+                nof_bits, pa.nof_layers, bps);
   }
   if (nof_cws == 0) {
     return SRS_AMD_OK;
@@ -390,6 +388,118 @@ int srs_amd_pdsch_modulate(srs_amd_pdsch_modulator*      mod,
 }
 
 } // extern "C"
+
+// get_ptrs_pattern (lib/ran/ptrs/ptrs_pattern.cpp:54-110) for the PT-RS of cfg: PRBs rb_begin, rb_begin + stride, ..
+// < rb_end, subcarrier k of the RB (the first port's k_re_ref, TS 38.211 Table 7.4.1.2.2-1), symbols of symbol_mask.
+struct ptrs_layout {
+  uint32_t rb_begin = 0, rb_end = 0, stride = 1, k = 0, symbol_mask = 0, mask_begin = 0;
+};
+
+static int ptrs_pattern(const srs_amd_ptrs_pdsch_config* c, ptrs_layout& o)
+{
+  if (c->dmrs_type != 1 && c->dmrs_type != 2) {
+    return fail(SRS_AMD_EINVAL, "Invalid DM-RS type %u.", c->dmrs_type);
+  }
+  if (c->freq_density != 2 && c->freq_density != 4) {
+    return fail(SRS_AMD_EINVAL, "Invalid PT-RS frequency density %u.", c->freq_density);
+  }
+  if (c->time_density != 1 && c->time_density != 2 && c->time_density != 4) {
+    return fail(SRS_AMD_EINVAL, "Invalid PT-RS time density %u.", c->time_density);
+  }
+  if (c->re_offset > 3 || c->start_symbol + c->nof_symbols > PDSCH_NSYMB || c->nof_symbols == 0) {
+    return fail(SRS_AMD_EINVAL, "Invalid PT-RS RE offset or time allocation.");
+  }
+  int lo = -1, hi = -1, n = 0;
+  for (uint32_t r = 0; r != SRS_AMD_MAX_RB; ++r) {
+    if (crb_bit(c->crb_mask, r)) {
+      lo = lo < 0 ? static_cast<int>(r) : lo;
+      hi = static_cast<int>(r);
+      ++n;
+    }
+  }
+  if (lo < 0 || hi - lo + 1 != n) {
+    return fail(SRS_AMD_EINVAL, "Only contiguous allocations are supported.");
+  }
+  static const uint8_t k_type1[4] = {0, 2, 6, 8};
+  static const uint8_t k_type2[4] = {0, 1, 6, 7};
+  const uint32_t       K          = c->freq_density;
+  const uint32_t       L          = c->time_density;
+  uint32_t             k_rb_ref   = (c->rnti & 0xffffu) % K;
+  if (n % K != 0) {
+    k_rb_ref = (c->rnti & 0xffffu) % (n % K);
+  }
+  o.mask_begin  = static_cast<uint32_t>(lo);
+  o.rb_begin    = k_rb_ref + static_cast<uint32_t>(lo);
+  o.rb_end      = static_cast<uint32_t>(lo + n);
+  o.stride      = K;
+  o.k           = c->dmrs_type == 1 ? k_type1[c->re_offset] : k_type2[c->re_offset];
+  o.symbol_mask = 0;
+  const int stop = static_cast<int>(c->start_symbol + c->nof_symbols);
+  int       i = 0, l_ref = static_cast<int>(c->start_symbol);
+  while (l_ref + i * static_cast<int>(L) < stop) {
+    const int startpos = std::max(l_ref + (i - 1) * static_cast<int>(L) + 1, l_ref);
+    const int endpos   = l_ref + i * static_cast<int>(L);
+    int       dmrs_pos = -1;
+    for (int l = endpos; l >= startpos; --l) {
+      if ((c->dmrs_symbols_mask >> l) & 1u) {
+        dmrs_pos = l;
+        break;
+      }
+    }
+    if (dmrs_pos >= 0) {
+      i     = 1;
+      l_ref = dmrs_pos;
+      continue;
+    }
+    o.symbol_mask |= 1u << (l_ref + i * static_cast<int>(L));
+    ++i;
+  }
+  return SRS_AMD_OK;
+}
+
+// The PT-RS argument block of cfg (ptrs_pdsch_generator_impl.cpp:30-130); weights_offset: where cfg's weights will
+// be in the device weight array (floats).
+static int make_ptrs_args(const srs_amd_pdsch_modulator* mod, const srs_amd_ptrs_pdsch_config* c, uint32_t nof_subc,
+                          ptrs_pdsch_args& a)
+{
+  ptrs_layout o;
+  int         rc = ptrs_pattern(c, o);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  if (c->nof_ports == 0 || c->nof_ports > SRS_AMD_MAX_TX_PORTS || c->nof_prg == 0 || c->prg_size == 0 ||
+      c->weights == nullptr) {
+    return fail(SRS_AMD_EINVAL, "Invalid PT-RS precoding (%u ports, %u PRGs of %u PRBs).", c->nof_ports, c->nof_prg,
+                c->prg_size);
+  }
+  if (o.rb_end > nof_subc / 12 || o.mask_begin < c->reference_point_k_rb) {
+    return fail(SRS_AMD_EINVAL, "PT-RS CRBs outside the grid or below the reference point.");
+  }
+  const uint32_t nd = c->dmrs_type == 1 ? 6 : 4;
+  a                 = ptrs_pdsch_args{};
+  a.jump            = mod->d_jump;
+  a.port_stride     = PDSCH_NSYMB * nof_subc;
+  a.nof_subc        = nof_subc;
+  a.rb_begin        = o.rb_begin;
+  a.rb_stride       = o.stride;
+  a.nof_prb         = o.rb_end > o.rb_begin ? (o.rb_end - o.rb_begin + o.stride - 1) / o.stride : 0;
+  if (a.nof_prb != 0 && (o.rb_begin + (a.nof_prb - 1) * o.stride) / c->prg_size >= c->nof_prg) {
+    return fail(SRS_AMD_EINVAL, "PT-RS CRBs beyond the precoding PRGs.");
+  }
+  a.k           = o.k;
+  a.symbol_mask = o.symbol_mask;
+  // ptrs_pdsch_generator_impl.cpp: l_0 = the first DM-RS symbol; unsigned arithmetic modulo 2^32 then % 2^31
+  const uint32_t l0    = c->dmrs_symbols_mask != 0 ? static_cast<uint32_t>(__builtin_ctz(c->dmrs_symbols_mask)) : 0u;
+  const uint32_t nid   = c->scrambling_id;
+  const uint32_t nscid = c->n_scid ? 1u : 0u;
+  a.c_init   = ((PDSCH_NSYMB * c->slot_index + l0 + 1) * (2 * nid + 1) * (1u << 17) + (2 * nid + nscid)) % (1u << 31);
+  a.bit0     = 2 * ((o.rb_begin - c->reference_point_k_rb) * nd + o.k / 2);
+  a.bit_step = 2 * nd * o.stride;
+  a.amplitude = static_cast<float>(M_SQRT1_2 * c->amplitude);
+  a.nof_ports = c->nof_ports;
+  a.prg_size  = c->prg_size;
+  return SRS_AMD_OK;
+}
 
 // The DM-RS argument block of cfg (dmrs_pdsch_processor_impl.cpp:40-90) for grids of nof_subc subcarriers.
 static int make_dmrs_args(const srs_amd_pdsch_modulator* mod, const srs_amd_dmrs_pdsch_config* cfg, uint32_t nof_subc,
@@ -536,7 +646,10 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
   }
   std::vector<pdsch_map_args>  maps;
   std::vector<dmrs_pdsch_args> dmrs;
-  uint32_t                     max_tiles = 0, max_symbols = 0, max_blocks = 0, max_dmrs_symbols = 0;
+  std::vector<ptrs_pdsch_args> ptrs;
+  std::vector<float>           ptrs_w;    // every PT-RS PDU's [prg][port] weights
+  std::vector<size_t>          ptrs_woff; // offset of each PT-RS PDU's weights in ptrs_w
+  uint32_t                     max_tiles = 0, max_symbols = 0, max_blocks = 0, max_dmrs_symbols = 0, max_ptrs = 0;
   for (uint32_t i = 0; i != nof_pdus; ++i) {
     const srs_amd_pdsch_slot_pdu& u = pdus[i];
     if (u.d_grid == nullptr && (d_grids == nullptr || u.grid >= nof_grids)) {
@@ -552,10 +665,10 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
       if (pa.nof_subc != nof_subc) {
         return fail(SRS_AMD_EINVAL, "PDU %u: plan for %u subcarriers, grid of %u.", i, pa.nof_subc, nof_subc);
       }
-      // a codeword longer than the allocation maps its first nof_re x layers symbols (as the reference's mapper,
-      // see pdsch_modulator.h); a shorter one cannot fill it
-      if (static_cast<uint64_t>(u.nof_bits) < static_cast<uint64_t>(u.plan->nof_re) * pa.nof_layers * bps) {
-        return fail(SRS_AMD_EINVAL, "PDU %u: the codeword length (i.e., %u bits) is shorter than the allocation.", i,
+      // a codeword longer than the allocation maps its first nof_re x layers symbols, a shorter one its first
+      // nof_bits / (layers x Qm) REs (as the reference's mapper, see pdsch_modulator.h)
+      if (u.nof_bits == 0 || u.nof_bits % (pa.nof_layers * bps) != 0) {
+        return fail(SRS_AMD_EINVAL, "PDU %u: the codeword length (i.e., %u bits) is not a whole number of REs.", i,
                     u.nof_bits);
       }
       if (ng > 1 && grid_stride < static_cast<uint64_t>(pa.nof_ports) * pa.port_stride) {
@@ -591,9 +704,28 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
         max_dmrs_symbols = std::max(max_dmrs_symbols, a.nof_dmrs_symbols);
       }
     }
+    if (u.ptrs != nullptr) {
+      ptrs_pdsch_args a;
+      int             rc = make_ptrs_args(mod, u.ptrs, nof_subc, a);
+      if (rc != SRS_AMD_OK) {
+        return rc;
+      }
+      if (ng > 1 && grid_stride < static_cast<uint64_t>(a.nof_ports) * a.port_stride) {
+        return fail(SRS_AMD_EINVAL, "grid stride too small");
+      }
+      a.grid = grid;
+      if (a.nof_prb != 0 && a.symbol_mask != 0) {
+        ptrs_woff.push_back(ptrs_w.size());
+        ptrs_w.insert(ptrs_w.end(), u.ptrs->weights, u.ptrs->weights + 2 * u.ptrs->nof_prg * u.ptrs->nof_ports);
+        ptrs.push_back(a);
+        max_ptrs = std::max(max_ptrs, a.nof_prb);
+      }
+    }
   }
   const size_t o_dmrs = align_up(sizeof(pdsch_map_args) * maps.size(), 256);
-  const size_t total  = o_dmrs + sizeof(dmrs_pdsch_args) * dmrs.size();
+  const size_t o_ptrs = align_up(o_dmrs + sizeof(dmrs_pdsch_args) * dmrs.size(), 256);
+  const size_t o_w    = align_up(o_ptrs + sizeof(ptrs_pdsch_args) * ptrs.size(), 256);
+  const size_t total  = ptrs.empty() ? o_dmrs + sizeof(dmrs_pdsch_args) * dmrs.size() : o_w + sizeof(float) * ptrs_w.size();
   if (total == 0) {
     return SRS_AMD_OK;
   }
@@ -616,10 +748,22 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
   std::memcpy(mod->stage.at<pdsch_map_args>(0), maps.data(), sizeof(pdsch_map_args) * maps.size());
   std::memcpy(mod->stage.at<dmrs_pdsch_args>(o_dmrs), dmrs.data(), sizeof(dmrs_pdsch_args) * dmrs.size());
   auto* d = mod->slot_items.as<uint8_t>();
+  for (size_t q = 0; q != ptrs.size(); ++q) {
+    ptrs[q].w = reinterpret_cast<const float*>(d + o_w) + ptrs_woff[q];
+  }
+  if (!ptrs.empty()) {
+    std::memcpy(mod->stage.at<ptrs_pdsch_args>(o_ptrs), ptrs.data(), sizeof(ptrs_pdsch_args) * ptrs.size());
+    std::memcpy(mod->stage.at<float>(o_w), ptrs_w.data(), sizeof(float) * ptrs_w.size());
+  }
   e       = mod->stage.upload(d, total, s);
   if (e == hipSuccess) {
     e = launch_pdsch_map_items(reinterpret_cast<const pdsch_map_args*>(d), static_cast<uint32_t>(maps.size()),
                                max_tiles, max_symbols, s);
+  }
+  if (e == hipSuccess) {
+    // pdsch_processor_impl.cpp:80-88: the PT-RS after the data (over the data mapped at its REs), then the DM-RS
+    e = launch_ptrs_pdsch_items(reinterpret_cast<const ptrs_pdsch_args*>(d + o_ptrs),
+                                static_cast<uint32_t>(ptrs.size()), max_ptrs, s);
   }
   if (e == hipSuccess) {
     e = launch_dmrs_pdsch_items(reinterpret_cast<const dmrs_pdsch_args*>(d + o_dmrs),
@@ -628,6 +772,25 @@ int srs_amd_pdsch_modulate_slot(srs_amd_pdsch_modulator*      mod,
   const hipError_t done = scope.close();
   e                     = e != hipSuccess ? e : done;
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PDSCH modulator slot launch");
+}
+
+int srs_amd_ptrs_pdsch_reserved(const srs_amd_ptrs_pdsch_config* cfg, srs_amd_re_pattern* pattern)
+{
+  if (cfg == nullptr || pattern == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  ptrs_layout o;
+  int         rc = ptrs_pattern(cfg, o);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  *pattern = srs_amd_re_pattern{};
+  for (uint32_t r = o.rb_begin; r < o.rb_end; r += o.stride) {
+    pattern->crb_mask[r / 8] |= static_cast<uint8_t>(1u << (r % 8));
+  }
+  pattern->re_mask = static_cast<uint16_t>(1u << o.k);
+  pattern->symbols = static_cast<uint16_t>(o.symbol_mask);
+  return SRS_AMD_OK;
 }
 
 } // extern "C"

@@ -55,6 +55,30 @@ struct dmrs_pdsch_args {
   uint16_t        crbs[PDSCH_MAX_RB];
 };
 
+// PT-RS of one PDU (ptrs_pdsch_generator_impl.cpp:30-130): PT-RS PRB i (CRB rb_begin + i rb_stride) carries, on
+// every symbol of symbol_mask, sequence bits bit0 + i bit_step and the next one, at M_SQRT1_2 x amplitude, precoded
+// with the layer-0 weights of the CRB's PRG.
+struct ptrs_pdsch_args {
+  uint32_t*       grid;        // cbf16 [port][14][nof_subc]
+  const uint32_t* jump;        // Gold-sequence jump matrices
+  const float*    w;           // [nof_prg][nof_ports] (re, im), device
+  uint32_t        port_stride; // 14 x nof_subc
+  uint32_t        nof_subc;
+  uint32_t        c_init;
+  uint32_t        bit0;
+  uint32_t        bit_step;
+  uint32_t        rb_begin;
+  uint32_t        rb_stride;
+  uint32_t        nof_prb;     // PT-RS PRBs
+  uint32_t        k;           // subcarrier within the RB
+  uint32_t        symbol_mask;
+  float           amplitude;
+  uint32_t        nof_ports;
+  uint32_t        prg_size;
+};
+
+hipError_t launch_ptrs_pdsch_items(const ptrs_pdsch_args* items, uint32_t count, uint32_t max_prb, hipStream_t stream);
+
 hipError_t launch_pdsch_map(const pdsch_map_args& a, uint32_t nof_symbols, uint32_t span_subc, uint32_t nof_cws,
                             hipStream_t stream);
 hipError_t launch_dmrs_pdsch(const dmrs_pdsch_args& a, uint32_t nof_grids, hipStream_t stream);

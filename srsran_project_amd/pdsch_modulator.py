@@ -157,7 +157,8 @@ class PdschSlotPdu(ctypes.Structure):
     """``srs_amd_pdsch_slot_pdu``: one PDU of srs_amd_pdsch_modulate_slot."""
 
     _fields_ = [("plan", ctypes.c_void_p), ("dmrs", ctypes.c_void_p), ("grid", ctypes.c_uint32),
-                ("nof_bits", ctypes.c_uint32), ("cw_offset", ctypes.c_uint64), ("d_grid", ctypes.c_void_p)]
+                ("nof_bits", ctypes.c_uint32), ("cw_offset", ctypes.c_uint64), ("d_grid", ctypes.c_void_p),
+                ("ptrs", ctypes.c_void_p)]
 
 
 def _declare(lib):

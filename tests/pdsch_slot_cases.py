@@ -20,6 +20,21 @@ PDUS = [
 ]
 
 
+# PT-RS (frequency density, time density, RE offset, PT-RS to data ratio dB) variants, and per-PRG precoding (PRG
+# size, number of PRGs): (qm, target rate, layers, vrbs, start, symbols, DM-RS mask, type, CDM groups, reserved,
+# powers, ptrs, prg).  Per-PRG precoding is not in PTRS_PDUS: the reference's PDSCH DM-RS processor cannot run it
+# (tests/test_oracle_vs_ref.py::test_reference_pdsch_multi_prg_precoding_is_out_of_bounds).
+PTRS_PDUS = [
+    (4, 490.0, 1, (0, 50), 0, 14, (1 << 2) | (1 << 11), 1, 2, [], (0.0, 0.0), (2, 1, 0, 0.0), None),
+    (6, 567.0, 2, (60, 140), 1, 13, 1 << 2, 1, 1, [((70, 90), 0b000100010001, 1 << 9)], (-3.0, 3.0),
+     (4, 2, 1, 3.0), None),
+    (2, 379.0, 1, (150, 175), 3, 11, 1 << 3, 2, 2, [], (1.0, 0.0), (4, 4, 2, 4.77), None),
+    (2, 120.0, 1, (240, 243), 2, 12, (1 << 2) | (1 << 8), 1, 2, [], (0.0, 0.0), (2, 1, 3, -2.0), None),
+    (8, 797.0, 3, (200, 230), 0, 14, (1 << 2) | (1 << 9), 1, 2, [], (0.0, 0.0), (2, 2, 2, 6.0), None),
+]
+MULTI_PRG_PDU = (8, 797.0, 3, (200, 230), 0, 14, (1 << 2) | (1 << 9), 1, 2, [], (0.0, 0.0), None, (64, 4))
+
+
 def reserved_masks(res):
     out = []
     for (c0, c1), re_mask, syms in res:
@@ -35,7 +50,9 @@ def slot(seed=5, slot_index=7, bwp=(0, NPRB), ref_point=0, pdus=PDUS):
 
     rng = np.random.default_rng(seed)
     out = []
-    for i, (qm, rate, L, vrbs, start, ns, dmrs, dtype, ncdm, res, (pdata, pdmrs)) in enumerate(pdus):
+    for i, case in enumerate(pdus):
+        qm, rate, L, vrbs, start, ns, dmrs, dtype, ncdm, res, (pdata, pdmrs) = case[:11]
+        ptrs, prg = (case[11], case[12]) if len(case) > 11 else (None, None)
         if vrbs == "sparse":
             vrbs = np.sort(rng.choice(np.arange(200, bwp[1]), min(50, bwp[1] - 200), replace=False))
         else:
@@ -46,7 +63,12 @@ def slot(seed=5, slot_index=7, bwp=(0, NPRB), ref_point=0, pdus=PDUS):
         r = rate / 1024
         bg = 2 if (tbs <= 292 or (tbs <= 3824 and r <= 0.67) or r <= 0.25) else 1
         W = ((rng.normal(size=(L, 4)) + 1j * rng.normal(size=(L, 4))) / np.sqrt(8)).astype(np.complex64)
-        pdu = make_pdsch_pdu(vrbs, W, reserved_masks(res), slot_index=slot_index, rnti=int(rng.integers(1, 65520)),
+        if prg is not None:
+            extra = [((rng.normal(size=(L, 4)) + 1j * rng.normal(size=(L, 4))) / np.sqrt(8)).astype(np.complex64)
+                     for _ in range(prg[1] - 1)]
+            prg = (prg[0], extra)
+        pdu = make_pdsch_pdu(vrbs, W, reserved_masks(res), ptrs=ptrs, prg=prg, slot_index=slot_index,
+                             rnti=int(rng.integers(1, 65520)),
                              bwp_start_rb=bwp[0], bwp_size_rb=bwp[1], qm=qm, n_id=int(rng.integers(0, 1024)),
                              ref_point=ref_point, dmrs_symbol_mask=dmrs, dmrs_type=dtype,
                              scrambling_id=int(rng.integers(0, 65536)), n_scid=i % 2,

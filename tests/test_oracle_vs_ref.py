@@ -465,3 +465,31 @@ def test_pdcch_invalid_pdus_rejected_like_reference():
             op.ref_process(np.zeros((1, 14, 12 * 52), np.uint32), [pdu])
         with pytest.raises(ValueError, match=text):
             rb_mask(pdu)
+
+
+@pytest.mark.skipif(oracle.REF is None, reason="oracle/_ref not built")
+def test_reference_pdsch_multi_prg_precoding_is_out_of_bounds():
+    """Why the PDSCH plug-in rejects precoding that differs between PRGs (integration/pdsch_processor_hip.h): the
+    reference's pdsch_processor_impl, run on such a PDU, dies in its DM-RS processor (dmrs_pdsch_processor_impl.cpp:
+    150-160 writes the weights of PRG >= 1 into a one-PRG precoding_configuration), while the same PDU with one PRG
+    runs.  Each run in its own process (CPU only: the harness's PDSCH path does not touch the GPU)."""
+    import os
+    import subprocess
+    import sys
+    import textwrap
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent("""
+        import sys
+        sys.path[:0] = [%r, %r]
+        from pdsch_slot_cases import MULTI_PRG_PDU, slot
+        from oracle import phy as ophy
+        case = MULTI_PRG_PDU if sys.argv[1] == "multi" else MULTI_PRG_PDU[:12] + (None,)
+        (pdu, tb), = slot(seed=3, pdus=[case])[0]
+        ophy.ref_pdsch_process(ophy.WriterGrid(slot(seed=3, pdus=[case])[1]), pdu, tb)
+        print("done")
+    """ % (root, os.path.join(root, "tests")))
+    one = subprocess.run([sys.executable, "-c", code, "one"], capture_output=True, text=True, timeout=300)
+    assert one.returncode == 0 and "done" in one.stdout, one.stderr[-2000:]
+    multi = subprocess.run([sys.executable, "-c", code, "multi"], capture_output=True, text=True, timeout=300)
+    assert multi.returncode != 0 and "done" not in multi.stdout, (multi.returncode, multi.stdout)

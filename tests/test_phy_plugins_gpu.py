@@ -210,6 +210,32 @@ def test_pdsch_plugin_slot_vs_reference(phy, bwp, ref_point):
                     "sentinel): %s" % (int((g != w).sum()), report))
 
 
+@pytest.mark.parametrize("device_grid", [False, True], ids=["host_grid", "device_grid"])
+def test_pdsch_plugin_ptrs_and_prg_precoding_vs_reference(phy, device_grid):
+    """PDSCH PDUs with PT-RS (frequency density 2 / 4, time density 1 / 2 / 4, every RE offset, power
+    ratios, DM-RS type 1 and 2) and with precoding that differs between PRGs (2 to 7 PRGs), one grid, one flush: the
+    grid is bit-identical to pdsch_processor_impl's -- the data filling the allocation over the PT-RS REs and
+    stopping when the codeword (sized without them) runs out, the PT-RS overwriting its REs, data and DM-RS on the
+    first PRG's weights, the PT-RS per PRG."""
+    from pdsch_slot_cases import PTRS_PDUS, slot
+
+    ophy, oracle = phy
+    pdus, grid0 = slot(seed=17, slot_index=5, pdus=PTRS_PDUS)
+    want = ophy.WriterGrid(grid0)
+    for pdu, tb in pdus:
+        ophy.ref_pdsch_process(want, pdu, tb)
+    plug = ophy.PdschProcessorPlugin(device=0)
+    got = ophy.DeviceGrid(grid0) if device_grid else ophy.WriterGrid(grid0)
+    tickets = [plug.process(got, pdu, tb) for pdu, tb in pdus]
+    plug.flush()
+    plug.wait()
+    assert all(plug.done(t) for t in tickets)
+    assert plug.stats()["errors"] == 0
+    w, g = want.read(), got.read()
+    diff = np.argwhere(g != w)
+    assert diff.size == 0, ("REs differ", len(diff), diff[:8].tolist())
+
+
 def test_pdsch_plugin_two_slots_two_cells(phy):
     """Two cells (two writers) over two slots through one factory: each slot's PDUs land in their own writers,
     bit-identical to the reference, and the collector cuts between the slots."""
