@@ -100,6 +100,8 @@ def parse():
     p.add_argument("--graph", action="store_true",
                    help="pipeline: replay each step as a HIP graph captured once (both streams, every launch)")
     p.add_argument("--ues-per-cell", type=int, default=8, help="sch_slot: UEs sharing each cell's 273 PRBs")
+    p.add_argument("--mixed", action="store_true",
+                   help="slot_pipeline: ~20%% UCI-on-PUSCH, ~10%% HARQ retransmission, ~3%% DFT-s-OFDM PDUs")
     return p.parse_args()
 
 

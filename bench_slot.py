@@ -129,6 +129,7 @@ def run_sch_slot(args, dist, world, rank, dev, timed):
             "parallelism": "cells sharded over ranks" if world > 1 else "single GPU",
         },
         "step_event_ms": step_ms,
+        "pusch_pdu_kinds": {k: pl.kinds.count(k) for k in sorted(set(pl.kinds))},
         "pusch_tb_ok_fraction": ok,
         "pusch_tbs_equal_sent": tb_equal,
         "per_ue_launches": per_ue,
@@ -146,7 +147,7 @@ class SlotPipeline:
     fixed channel + AWGN, symbols 0-13; the UE transmissions are synthesised before the timed region (the PDSCH
     modulator as the UE transmitter, per-UE channel as its precoder) and every run checks the decoded TBs."""
 
-    def __init__(self, cells, ues_per_cell, dev, seed=0, iters=6, snr_db=35.0, ul_max_layers=2):
+    def __init__(self, cells, ues_per_cell, dev, seed=0, iters=6, snr_db=35.0, ul_max_layers=2, mixed=False):
         import torch
 
         import bench_pipeline as bp
@@ -164,6 +165,8 @@ class SlotPipeline:
             amd.OfdmDemodulatorConfiguration(bp.MU, NOF_PRB, bp.NFFT, 0, 1.0, 3.5e9, 0), device=d)
         nsubc = 12 * NOF_PRB
         dl, ul, ue_tx = [], [], []   # (sch plan, mod plan, dmrs, cell) / (processor plan, cell) / UE TX
+        self.kinds = []              # UL PDU kinds (mixed: "uci", "harq", "tp" or "data")
+        self.tp_ues = []             # DFT-s-OFDM UEs: (cell, first PRB, end PRB, channel [port], n_rs_id)
         for c in range(cells):
             n_id = int(rng.integers(0, 1008))
             for side in ("dl", "ul"):
@@ -189,25 +192,51 @@ class SlotPipeline:
                                                  symbols_mask=bp.DMRS_MASK, crbs=crbs, precoding=w)
                         dl.append((sp, mp, dm, c))
                     else:
-                        layers = int(rng.integers(1, ul_max_layers + 1))
+                        j = len(ul)
+                        kind = "data"
+                        if mixed:
+                            # ~20 % HARQ-ACK + CSI part 1 on the UL-SCH, ~10 % retransmissions (new_data = 0,
+                            # combined into a soft buffer; rv 0, decodable alone from the cleared buffer), ~3 %
+                            # DFT-s-OFDM
+                            kind = ("tp" if j % 32 == 17 else "uci" if j % 5 == 1 else "harq" if j % 10 == 3
+                                    else "data")
+                        layers = 1 if kind in ("tp", "uci") else int(rng.integers(1, ul_max_layers + 1))
+                        if kind == "tp":
+                            n = hi - lo
+                            while not amd.transform_precoding_nof_prbs_valid(n):
+                                n -= 1
+                            hi = lo + n
+                            crbs = list(range(lo, hi))
+                        extra = {}
+                        if kind == "uci":
+                            extra = dict(nof_harq_ack=4, nof_csi_part1=20, beta_offset_harq_ack=8.0,
+                                         beta_offset_csi_part1=6.25, alpha_scaling=1.0)
+                        if kind == "tp":
+                            extra = dict(transform_precoding=1, n_rs_id=n_id)
+                        rv, new_data = (0, 0) if kind == "harq" else (0, 1)
                         tbs = amd.tbs_calculator_calculate(14, 24, 0, qm, r, layers, 0, hi - lo)
                         pdu = amd.make_pdu(numerology=bp.MU, slot_index=bp.SLOT, rnti=rnti, bwp_start_rb=0,
-                                           bwp_size_rb=NOF_PRB, modulation=qm, target_code_rate=r, rv=0,
-                                           base_graph=base_graph(tbs, r / 1024), new_data=1, n_id=n_id,
+                                           bwp_size_rb=NOF_PRB, modulation=qm, target_code_rate=r, rv=rv,
+                                           base_graph=base_graph(tbs, r / 1024), new_data=new_data, n_id=n_id,
                                            nof_tx_layers=layers, nof_rx_ports=4, dmrs_symbol_mask=bp.DMRS_MASK,
                                            scrambling_id=n_id, n_scid=0, nof_cdm_groups_without_data=2, rb_start=lo,
-                                           rb_count=hi - lo, start_symbol_index=0, nof_symbols=14, tbs=tbs)
+                                           rb_count=hi - lo, start_symbol_index=0, nof_symbols=14, tbs=tbs, **extra)
+                        self.kinds.append(kind)
                         pp = self.proc.plan(pdu, nsubc)
                         h = bp.ul_channel(layers, 4)
                         mp = self.mod.plan(amd.PdschModulatorConfig(
                             rnti=rnti, bwp_start=0, bwp_size=NOF_PRB, modulation=qm, crbs=crbs, start_symbol=0,
                             nof_symbols=14, dmrs_symb_pos=bp.DMRS_MASK, dmrs_type=1, nof_cdm_groups_without_data=2,
                             n_id=n_id, precoding=h), nsubc)
-                        assert mp.nof_bits == pp.sch.cw_length
+                        assert kind == "uci" or mp.nof_bits == pp.sch.cw_length
                         dm = amd.DmrsPdschConfig(slot_index=bp.SLOT, reference_point_k_rb=0, type=1,
                                                  scrambling_id=n_id, n_scid=False, amplitude=bp.DMRS_AMP,
                                                  symbols_mask=bp.DMRS_MASK, crbs=crbs, precoding=h)
                         ul.append((pp, c))
+                        if kind == "tp":
+                            self.tp_ues.append((c, lo, hi, h[0], n_id))
+                        # the UE transmits the codeword of the PDU's own rv (UCI not multiplexed: those PDUs'
+                        # TBs fail, see check(); DFT-s-OFDM UEs are DFT-spread below)
                         ue_tx.append((pp.sch, mp, dm, c))
         self.dl, self.ul = dl, ul
         g = torch.Generator(device=dev)
@@ -236,6 +265,8 @@ class SlotPipeline:
         grid = torch.zeros((cells, 4, 14, nsubc), dtype=torch.int32, device=dev)
         self.mod.modulate_slot(grid, amd.PdschSlot([(mp, dm, c, co) for (sp, mp, dm, c), (_, _, co)
                                                     in zip(ue_tx, ul_ues)]), codewords=cw_ul)
+        for c, lo, hi, h, n_rs_id in self.tp_ues:
+            self._transform_precode(amd, bp, grid, c, lo, hi, h, n_rs_id)
         samp = self.ofdm_mod.modulate_batch(grid.view(torch.int16).view(cells, 4, 14, 2 * nsubc), bp.SLOT)
         p = float(torch.mean(torch.abs(samp) ** 2).item())
         sigma = np.sqrt(p / 10 ** (snr_db / 10) / 2)
@@ -243,12 +274,46 @@ class SlotPipeline:
                               torch.randn(samp.shape, device=dev, generator=g)) * sigma
         self.samp_ul = (samp + noise.to(torch.complex64)).contiguous()
         self.ul_tb_off = [to for _, to, _ in ul_ues]
-        self.ul_slot = amd.PuschSlot(ul)
+        # retransmissions: one soft buffer each, cleared at the start of every step (the state a failed first
+        # transmission leaves is modelled as empty; clearing keeps every step's decoding work the same)
+        soft_sizes = [amd.soft_buffer_size(pp.sch) if k == "harq" else 0 for (pp, _), k in zip(ul, self.kinds)]
+        self.soft_all = torch.zeros(max(sum((n + 255) // 256 * 256 for n in soft_sizes), 1), dtype=torch.int8,
+                                    device=dev)
+        items, off = [], 0
+        for (pp, c), n in zip(ul, soft_sizes):
+            if n:
+                items.append((pp, c, self.soft_all[off:off + n]))
+                off += (n + 255) // 256 * 256
+            else:
+                items.append((pp, c))
+        self.ul_slot = amd.PuschSlot(items)
+        self.uci = torch.zeros(max(self.ul_slot.uci_total, 1), dtype=torch.uint8, device=dev)
         self.grid_ul = torch.zeros((cells, 4, 14, nsubc), dtype=torch.int32, device=dev)
         self.tb_rx = torch.zeros(max(self.ul_slot.tb_total, 1), dtype=torch.uint8, device=dev)
         self.res_ul = torch.zeros((len(ul), amd.pusch_processor.RESULT_BYTES), dtype=torch.uint8, device=dev)
         self.ul_stream = None
         torch.cuda.synchronize(dev)
+
+    def _transform_precode(self, amd, bp, grid, c, lo, hi, h, n_rs_id):
+        """A DFT-s-OFDM UE's transmission (untimed setup): the data symbols the PDSCH modulator mapped (scrambled,
+        modulated, times the channel h[port]) DFT-spread over the allocation per OFDM symbol (TS 38.211 6.3.1.4,
+        unit-energy DFT; one layer, so the per-port channel factor commutes with the DFT), and the DM-RS replaced by
+        the low-PAPR sequence of n_rs_id on the even subcarriers (TS 38.211 6.4.1.1.1.2, no hopping, one layer)."""
+        torch = self.torch
+        k0, k1 = 12 * lo, 12 * hi
+        g = grid[c].view(torch.int16).view(4, 14, 2 * grid.shape[-1])
+        x = g[:, :, 2 * k0:2 * k1].contiguous().view(torch.bfloat16).float().view(4, 14, k1 - k0, 2)
+        z = torch.view_as_complex(x.contiguous())
+        seq = torch.from_numpy(amd.low_papr_sequence((k1 - k0) // 2, n_rs_id % 30)).to(z.device)
+        for l in range(14):
+            if (bp.DMRS_MASK >> l) & 1:
+                z[:, l, :] = 0
+                for p in range(4):
+                    z[p, l, 0::2] = seq * np.complex64(bp.DMRS_AMP * h[p])
+            else:
+                z[:, l, :] = torch.fft.fft(z[:, l, :], norm="ortho")
+        y = torch.view_as_real(z).to(torch.bfloat16).contiguous().view(torch.int16).view(4, 14, 2 * (k1 - k0))
+        g[:, :, 2 * k0:2 * k1] = y
 
     def pdsch(self, stream):
         import bench_pipeline as bp
@@ -266,7 +331,10 @@ class SlotPipeline:
         self.ofdm_dem.demodulate_batch(self.samp_ul, bp.SLOT,
                                        grid=self.grid_ul.view(t.int16).view(self.S, 4, 14, 2 * 12 * NOF_PRB),
                                        stream=stream)
-        self.proc.process_slot(self.grid_ul, self.ul_slot, tbs=self.tb_rx, results=self.res_ul, stream=stream)
+        if any(k == "harq" for k in self.kinds):
+            self.soft_all.zero_()
+        self.proc.process_slot(self.grid_ul, self.ul_slot, tbs=self.tb_rx, results=self.res_ul, stream=stream,
+                               uci=self.uci if self.ul_slot.uci_total else None)
 
     def step(self, stream):
         """Both chains of every cell, concurrently on two HIP streams (fork / join on `stream`)."""
@@ -295,7 +363,9 @@ class SlotPipeline:
         res = amd.pusch_processor.parse_results(self.res_ul.cpu().numpy())
         rx, tx = self.tb_rx.cpu().numpy(), self.tb_ul.cpu().numpy()
         ok = []
-        for (pp, _), r, off, toff in zip(self.ul, res, self.ul_slot.offsets, self.ul_tb_off):
+        for (pp, _), r, off, toff, k in zip(self.ul, res, self.ul_slot.offsets, self.ul_tb_off, self.kinds):
+            if k == "uci":
+                continue  # transmitted without UCI multiplexing: not decodable by construction
             n = pp.tb_bytes
             ok.append(bool(r.data.tb_crc_ok) and np.array_equal(rx[off:off + n], tx[toff:toff + n]))
         its = sum(r.data.ldpc_iterations_sum for r in res) / max(1, sum(r.data.nof_codeblocks_total for r in res))
@@ -309,7 +379,8 @@ def run_slot_pipeline(args, dist, world, rank, dev, timed):
     import torch
 
     cells = args.slots_pipeline
-    pl = SlotPipeline(cells, args.ues_per_cell, dev, seed=rank, iters=args.iters, snr_db=args.snr_db)
+    pl = SlotPipeline(cells, args.ues_per_cell, dev, seed=rank, iters=args.iters, snr_db=args.snr_db,
+                      mixed=args.mixed)
     stream = torch.cuda.current_stream(dev)
     elapsed, step_ms = timed(args, dist, world, dev, stream, lambda: pl.step(stream))
     torch.cuda.synchronize(dev)
@@ -339,6 +410,7 @@ def run_slot_pipeline(args, dist, world, rank, dev, timed):
             "parallelism": "cells sharded over ranks" if world > 1 else "single GPU",
         },
         "step_event_ms": step_ms,
+        "pusch_pdu_kinds": {k: pl.kinds.count(k) for k in sorted(set(pl.kinds))},
         "pusch_tb_ok_fraction": ok,
         "pusch_mean_ldpc_iterations": its,
     }

@@ -708,7 +708,8 @@ int srs_amd::rate_dematch_ragged(srs_amd_ldpc_rate_dematcher* dm,
                                  int8_t*                      d_soft,
                                  uint32_t                     soft_stride,
                                  uint32_t                     nof_cbs,
-                                 void*                        stream)
+                                 void*                        stream,
+                                 const uint8_t*               d_row_flags)
 {
   if (dm == nullptr) {
     return fail(SRS_AMD_EINVAL, "null rate dematcher");
@@ -733,6 +734,7 @@ int srs_amd::rate_dematch_ragged(srs_amd_ldpc_rate_dematcher* dm,
   a.row_geo       = d_row_geo;
   a.geos          = static_cast<const rm_geometry*>(d_geos);
   a.geo_write_end = d_geo_write_end;
+  a.row_flags     = d_row_flags;
   std::lock_guard<std::mutex> lock(dm->mtx);
   hipError_t                  e = hipSetDevice(dm->device);
   if (e == hipSuccess) {

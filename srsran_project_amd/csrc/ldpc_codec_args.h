@@ -57,6 +57,8 @@ struct dematch_args {
   const uint32_t*    row_geo;
   const rm_geometry* geos;
   const uint32_t*    geo_write_end;
+  // optional per-codeblock flags (replace new_data / fresh): bit 0 new data, bit 1 fresh (PUSCH slot form with HARQ)
+  const uint8_t*     row_flags;
 };
 
 struct rate_match_args {

@@ -129,7 +129,8 @@ int rate_match_ragged(srs_amd_ldpc_rate_matcher* rm,
 
 // Rate dematching of codeblocks with per-codeblock geometry (srs_amd_pusch_decode_slot): codeblock cb
 // uses geos[row_geo[cb]] and writes soft-buffer bytes [0, geo_write_end[row_geo[cb]]) of its row
-// (new data into fresh internal buffers, whose old contents are taken as zero).
+// (new data into fresh internal buffers, whose old contents are taken as zero; with d_row_flags, codeblock cb's
+// new-data / fresh flags: bit 0 / bit 1 of d_row_flags[cb]).
 int rate_dematch_ragged(srs_amd_ldpc_rate_dematcher* dm,
                         const int8_t*                d_input,
                         const uint32_t*              d_in_offsets,
@@ -140,6 +141,7 @@ int rate_dematch_ragged(srs_amd_ldpc_rate_dematcher* dm,
                         int8_t*                      d_soft,
                         uint32_t                     soft_stride,
                         uint32_t                     nof_cbs,
-                        void*                        stream);
+                        void*                        stream,
+                        const uint8_t*               d_row_flags = nullptr);
 
 } // namespace srs_amd

@@ -79,6 +79,9 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
     const uint32_t    gi        = RAGGED ? a.row_geo[cb] : 0u;
     const rm_geometry g         = RAGGED ? a.geos[gi] : a.g;
     const uint32_t    write_end = RAGGED ? a.geo_write_end[gi] : a.write_end;
+    const uint32_t flags    = RAGGED && a.row_flags != nullptr ? a.row_flags[cb] : 0u;
+    const int32_t  new_data = RAGGED && a.row_flags != nullptr ? static_cast<int32_t>(flags & 1u) : a.new_data;
+    const int32_t  fresh    = RAGGED && a.row_flags != nullptr ? static_cast<int32_t>((flags >> 1) & 1u) : a.fresh;
     const uint32_t E   = a.rm_lengths[cb];
     const int8_t*  in  = a.in + a.in_offsets[cb];
     int8_t*        buf = a.soft + static_cast<size_t>(cb) * a.soft_stride;
@@ -186,13 +189,13 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
     auto llr_in = [&](uint32_t t, uint32_t i, uint32_t j) -> int { return staged ? s_in[t] : in[i * g.Qm + j]; };
 
     // First loop pass of the reference (copy mode), see the file header.
-    const bool     first_pass = a.new_data && E > 0;
+    const bool     first_pass = new_data && E > 0;
     const uint32_t L1         = g.L - g.rank0;
     const uint32_t ncopy      = first_pass ? min(E, L1) : 0u;
     const bool     k0_in_info = g.k0 < g.nof_info;
     const uint32_t zero_end   = first_pass ? (k0_in_info ? g.k0 : g.nof_info) : 0u;
     uint32_t       zero_from  = g.N; // final tail zeroing
-    if (a.new_data) {
+    if (new_data) {
       uint32_t tmp;
       if (E == 0) {
         tmp = g.k0;
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(DEMATCH_THREADS) void ldpc_rate_dematch_kernel(dema
     // With new data, k0 = 0 and no limited-buffer rate matching, the first pass covers [0, E + F) (the
     // walk skips to nof_sys when the input ends in the information part) and the tail zeroing starts
     // where it stopped: once E >= nof_info nothing of the old contents survives.
-    const bool read_old = !a.fresh && !(a.new_data && E >= g.nof_info && g.k0 == 0 && g.Ncb == g.N);
+    const bool read_old = !fresh && !(new_data && E >= g.nof_info && g.k0 == 0 && g.Ncb == g.N);
     const bool vec      = (reinterpret_cast<uintptr_t>(buf) & 3u) == 0 && (g.N & 15u) == 0;
     const bool vec16    = (reinterpret_cast<uintptr_t>(buf) & 15u) == 0; // PUSCH soft rows are 64-byte aligned
     auto       store16  = [&](uint32_t* o, uint4 v) {

@@ -143,17 +143,22 @@ __global__ __launch_bounds__(64 * WAVES) void polar_encode_kernel(polar_args a)
   }
 }
 
-__global__ __launch_bounds__(64 * WAVES) void polar_decode_kernel(polar_args a)
+// MULTI: one argument block (one codeword, its own code) per wave: items[blockIdx.x * WAVES + wave], nof items
+template <bool MULTI>
+__global__ __launch_bounds__(64 * WAVES) void polar_decode_kernel(polar_args own, const polar_args* items,
+                                                                   uint32_t nof)
 {
   __shared__ int8_t  llr_all[WAVES][2048]; // stage s at offset 2^s - 1
   __shared__ uint8_t est_all[WAVES][1024];
   __shared__ uint8_t msg_all[WAVES][1024];
   const int          wave = threadIdx.x >> 6;
   const int          lane = threadIdx.x & 63;
-  const uint32_t     cw   = blockIdx.x * WAVES + wave;
-  if (cw >= a.nof) {
+  const uint32_t     w    = blockIdx.x * WAVES + wave;
+  if (w >= (MULTI ? nof : own.nof)) {
     return;
   }
+  const polar_args& a  = MULTI ? items[w] : own;
+  const uint32_t    cw = MULTI ? 0u : w;
   int8_t*       llr = llr_all[wave];
   uint8_t*      est = est_all[wave];
   uint8_t*      dec = msg_all[wave];
@@ -242,7 +247,18 @@ hipError_t launch_polar_decode(const polar_args& a, hipStream_t stream)
   if (a.nof == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(polar_decode_kernel, dim3((a.nof + WAVES - 1) / WAVES), dim3(64 * WAVES), 0, stream, a);
+  hipLaunchKernelGGL(polar_decode_kernel<false>, dim3((a.nof + WAVES - 1) / WAVES), dim3(64 * WAVES), 0, stream, a,
+                     nullptr, 0u);
+  return hipGetLastError();
+}
+
+hipError_t launch_polar_decode_items(const polar_args* items, uint32_t n, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(polar_decode_kernel<true>, dim3((n + WAVES - 1) / WAVES), dim3(64 * WAVES), 0, stream,
+                     polar_args{}, items, n);
   return hipGetLastError();
 }
 

@@ -34,6 +34,11 @@ struct srs_amd_polar_code {
   }
 };
 
+const polar_args& srs_amd::polar_code_base(const ::srs_amd_polar_code* code)
+{
+  return code->base;
+}
+
 namespace {
 
 template <class T>

@@ -8,6 +8,8 @@
 
 #include "polar_code.h"
 
+struct srs_amd_polar_code;
+
 namespace srs_amd {
 
 struct polar_args {
@@ -30,5 +32,9 @@ struct polar_args {
 
 hipError_t launch_polar_encode(const polar_args& a, hipStream_t stream);
 hipError_t launch_polar_decode(const polar_args& a, hipStream_t stream);
+// The code's argument block (tables, sizes) to which a launch adds its buffers.
+const polar_args& polar_code_base(const ::srs_amd_polar_code* code);
+// Slot form: one argument block per codeword (device array, nof = 1 each), each with its own code.
+hipError_t launch_polar_decode_items(const polar_args* items, uint32_t n, hipStream_t stream);
 
 } // namespace srs_amd

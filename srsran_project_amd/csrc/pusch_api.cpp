@@ -41,6 +41,7 @@ struct srs_amd_pusch_decoder {
   srs_amd_ldpc_rate_dematcher* dm     = nullptr;
   srs_amd_ldpc_decoder*        dec[2] = {nullptr, nullptr}; // force_decoding 0 / 1
   device_buffer                soft, msgs, iters, checks, arrays, results, host_io, tb_acc, slot_desc;
+  device_buffer                harq_prev; // slot form: the CRC flags of HARQ codeblocks before this transmission
   geometry_cache               rm_geo; // last geometry written into arrays (rm_arrays_kernel)
   stream_order                 order; // scratch reuse across the callers' streams
   stream_fan                   fan;   // srs_amd_pusch_decode_slot: concurrent LDPC bucket launches
@@ -289,8 +290,15 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
                        srs_amd_pusch_decoder_result*       d_results,
                        const uint32_t*                     cb_offsets,
                        int32_t*                            d_cb_iterations,
-                       hipStream_t                         stream)
+                       hipStream_t                         stream,
+                       const slot_harq*                    harq)
 {
+  // HARQ UEs (a caller soft buffer): their codeblocks decode in internal rows like the others, the soft bits
+  // gathered from / scattered to the caller's rows around the rate dematcher / decoder (harq_* kernels), full-length
+  // rows (the whole soft buffer is state), the rate dematcher combining into the gathered bits (per-row flags)
+  auto harq_of = [&](uint32_t u) -> const slot_harq* {
+    return harq != nullptr && harq[u].soft != nullptr ? &harq[u] : nullptr;
+  };
   // Z = 384 rows: one uniform launch per (BG, CRC, bounded prefix) -- the compile-time Z = 384 kernels,
   // the high-rate one for bounded prefixes; Z < 384 rows: one mixed-Z launch per (BG, kernel class: the
   // packed kernel's waves per codeblock), each row with its own Z, CRC, input length and filler bits.
@@ -320,7 +328,8 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
       return fail(SRS_AMD_EINVAL, "UE %u: LLR span exceeds 2^32 bytes", u);
     }
     const soft_row_layout lay    = layout_of(p);
-    const uint32_t        prefix = llr_prefix(p, lay, true, true);
+    const slot_harq*      h      = harq_of(u);
+    const uint32_t        prefix = h != nullptr ? lay.soft_bytes : llr_prefix(p, lay, true, true);
     ue_prefix[u]                = prefix;
     // rows whose non-zero prefix is bounded decode apart from full rows: the bucket's LLR length is its
     // longest prefix, and a bounded one selects the high-rate decoder kernel
@@ -360,6 +369,10 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   std::map<std::tuple<size_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> geo_of;
   std::vector<tb_desc>                                                               tds(U);
   std::vector<uint32_t>                                                              segE, segOff;
+  std::vector<uint8_t>                                                               row_flags(R, 3); // new, fresh
+  std::vector<harq_row_desc>                                                         hrows;
+  std::vector<harq_tb_desc>                                                          htbs;
+  uint32_t                                                                           max_soft = 0;
   uint32_t                                                                           row = 0;
   for (size_t bi = 0; bi < buckets.size(); ++bi) {
     bucket& b = buckets[bi];
@@ -386,6 +399,19 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
       (void)srs_amd_sch_plan_segments(p, segE.data(), segOff.data());
       tds[u] = tb_desc{ues[u].tb_offset, row,         p->nof_segments, p->cb_info_bits, p->tbs, p->nof_tb_crc_bits,
                        p->zero_pad,       (p->segment_length + 7) / 8, cb_offsets ? cb_offsets[u] : 0u};
+      const slot_harq* h = harq_of(u);
+      if (h != nullptr) {
+        const soft_row_layout lay = layout_of(p);
+        htbs.push_back(harq_tb_desc{reinterpret_cast<uint8_t*>(h->soft), u, p->nof_segments, lay.row_bytes,
+                                    lay.flag_offset});
+        max_soft = std::max(max_soft, lay.soft_bytes);
+        for (uint32_t r = 0; r < p->nof_segments; ++r) {
+          hrows.push_back(harq_row_desc{reinterpret_cast<uint8_t*>(h->soft) + static_cast<size_t>(r) * lay.row_bytes,
+                                        row + r, lay.soft_bytes, lay.msg_offset, lay.flag_offset - lay.msg_offset,
+                                        lay.flag_offset, h->new_data ? 1u : 0u});
+          row_flags[row + r] = h->new_data ? 3 : 0;
+        }
+      }
       for (uint32_t r = 0; r < p->nof_segments; ++r, ++row) {
         row_E[row]   = segE[r];
         row_in[row]  = static_cast<uint32_t>(ues[u].llr_offset) + segOff[r];
@@ -406,7 +432,10 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   const size_t o_TD  = o_GE + align_up(sizeof(uint32_t) * geos.size(), 16);
   const size_t o_LEN = o_TD + align_up(sizeof(tb_desc) * U, 16);
   const size_t o_RD  = o_LEN + align_up(sizeof(uint32_t) * R, 16);
-  const size_t total = o_RD + sizeof(ldpc_row_desc) * R;
+  const size_t o_RF  = o_RD + align_up(sizeof(ldpc_row_desc) * R, 16);
+  const size_t o_HR  = o_RF + align_up(R, 16);
+  const size_t o_HT  = o_HR + align_up(sizeof(harq_row_desc) * hrows.size(), 16);
+  const size_t total = hrows.empty() ? o_RF : o_HT + sizeof(harq_tb_desc) * htbs.size();
 
   hipError_t he = hipSetDevice(d->device);
   // the pinned staging buffer is rewritten only once its previous upload completed
@@ -443,6 +472,9 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   if (he == hipSuccess) {
     he = d->tb_acc.ensure_zeroed(sizeof(uint32_t) * U);
   }
+  if (he == hipSuccess && !hrows.empty()) {
+    he = d->harq_prev.ensure(sizeof(int32_t) * hrows.size());
+  }
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH slot decoder scratch");
   }
@@ -456,6 +488,11 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   std::memcpy(h + o_TD, tds.data(), sizeof(tb_desc) * U);
   std::memcpy(h + o_LEN, row_len.data(), sizeof(uint32_t) * R);
   std::memcpy(h + o_RD, row_desc.data(), sizeof(ldpc_row_desc) * R);
+  if (!hrows.empty()) {
+    std::memcpy(h + o_RF, row_flags.data(), R);
+    std::memcpy(h + o_HR, hrows.data(), sizeof(harq_row_desc) * hrows.size());
+    std::memcpy(h + o_HT, htbs.data(), sizeof(harq_tb_desc) * htbs.size());
+  }
   auto*      dd = d->slot_desc.as<uint8_t>();
   call_scope scope(d->order, &d->fan, stream);
   he = d->order.begin(stream);
@@ -469,11 +506,30 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     return hip_fail(he, "PUSCH slot descriptors upload");
   }
   d->stage_used = true;
-  // 1. Rate dematching of every codeblock of the slot, one launch.
-  int8_t* soft = d->soft.as<int8_t>();
-  int     rc   = rate_dematch_ragged(d->dm, d_llrs, reinterpret_cast<const uint32_t*>(dd + o_in),
-                                     reinterpret_cast<const uint32_t*>(dd + o_E), reinterpret_cast<const uint32_t*>(dd + o_geo),
-                                     dd + o_G, reinterpret_cast<const uint32_t*>(dd + o_GE), soft, S, R, stream);
+  // 1. Rate dematching of every codeblock of the slot, one launch (HARQ rows combining into their gathered bits).
+  int8_t*   soft = d->soft.as<int8_t>();
+  harq_args ha{};
+  ha.rows     = reinterpret_cast<const harq_row_desc*>(dd + o_HR);
+  ha.nof_rows = static_cast<uint32_t>(hrows.size());
+  ha.tbs      = reinterpret_cast<const harq_tb_desc*>(dd + o_HT);
+  ha.nof_tbs  = static_cast<uint32_t>(htbs.size());
+  ha.internal = soft;
+  ha.S        = S;
+  ha.msgs     = d->msgs.as<uint8_t>();
+  ha.M        = M;
+  ha.iters    = d->iters.as<int32_t>();
+  ha.prev     = d->harq_prev.as<int32_t>();
+  ha.results  = d_results;
+  if (ha.nof_rows != 0) {
+    he = launch_harq_gather(ha, max_soft, stream);
+    if (he != hipSuccess) {
+      return hip_fail(he, "harq_gather_kernel launch");
+    }
+  }
+  int rc = rate_dematch_ragged(d->dm, d_llrs, reinterpret_cast<const uint32_t*>(dd + o_in),
+                               reinterpret_cast<const uint32_t*>(dd + o_E), reinterpret_cast<const uint32_t*>(dd + o_geo),
+                               dd + o_G, reinterpret_cast<const uint32_t*>(dd + o_GE), soft, S, R, stream,
+                               hrows.empty() ? nullptr : dd + o_RF);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
@@ -542,6 +598,13 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
       }
     }
   }
+  // HARQ rows: soft bits back to the caller, earlier messages / fresh flags (before the assembly reads msgs / iters)
+  if (ha.nof_rows != 0) {
+    he = launch_harq_scatter(ha, max_soft, stream);
+    if (he != hipSuccess) {
+      return hip_fail(he, "harq_scatter_kernel launch");
+    }
+  }
   // 3. Concatenation and TB CRC, per-TB descriptors.
   assemble_args a{};
   a.msgs           = d->msgs.as<uint8_t>();
@@ -559,6 +622,9 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   a.tds            = reinterpret_cast<const tb_desc*>(dd + o_TD);
   a.max_tb_bits    = max_tb_bits;
   he               = launch_assemble(a, U, stream);
+  if (he == hipSuccess) {
+    he = launch_harq_final(ha, stream);
+  }
   if (he == hipSuccess) {
     he = scope.close();
   }
@@ -793,7 +859,8 @@ int srs_amd::pusch_decode_slot_ex(srs_amd_pusch_decoder*              dec,
                                   srs_amd_pusch_decoder_result*       d_results,
                                   const uint32_t*                     cb_offsets,
                                   int32_t*                            d_cb_iterations,
-                                  hipStream_t                         stream)
+                                  hipStream_t                         stream,
+                                  const slot_harq*                    harq)
 {
   if (dec == nullptr || cfg == nullptr) {
     return fail(SRS_AMD_EINVAL, "null argument");
@@ -804,9 +871,12 @@ int srs_amd::pusch_decode_slot_ex(srs_amd_pusch_decoder*              dec,
   if ((cb_offsets == nullptr) != (d_cb_iterations == nullptr)) {
     return fail(SRS_AMD_EINVAL, "per-codeblock iterations need both the offsets and the output buffer");
   }
-  if (!cfg->new_data) {
+  if (harq == nullptr && !cfg->new_data) {
     return fail(SRS_AMD_EINVAL, "slot decoding serves new transmissions; HARQ retransmissions go through "
                                 "srs_amd_pusch_decode_batch with the caller's soft buffers");
+  }
+  if (harq != nullptr && !cfg->use_early_stop) {
+    return fail(SRS_AMD_EINVAL, "slot decoding with HARQ state needs the early-stop decoder");
   }
   if (nof_ues == 0) {
     return SRS_AMD_OK;
@@ -815,6 +885,7 @@ int srs_amd::pusch_decode_slot_ex(srs_amd_pusch_decoder*              dec,
     return fail(SRS_AMD_EINVAL, "null buffer");
   }
   std::lock_guard<std::mutex> lock(dec->mtx);
-  return decode_slot_locked(dec, cfg, ues, nof_ues, d_llrs, d_tbs, d_results, cb_offsets, d_cb_iterations, stream);
+  return decode_slot_locked(dec, cfg, ues, nof_ues, d_llrs, d_tbs, d_results, cb_offsets, d_cb_iterations, stream,
+                            harq);
 }
 

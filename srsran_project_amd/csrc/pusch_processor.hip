@@ -35,10 +35,11 @@ __global__ __launch_bounds__(64) void pusch_result_kernel(pusch_result_args a)
   r.rsrp_db          = 10.0f * log10f(rsrp / static_cast<float>(P));
   r.time_alignment_s = st[best].time_alignment_s;
   r.cfo_hz           = st[best].cfo_hz;
-  r.harq_ack_status  = (a.uci_mask & 1u) ? a.uci_status[4 * g] : 0;
-  r.csi_part1_status = (a.uci_mask & 2u) ? a.uci_status[4 * g + 1] : 0;
-  r.csi_part2_status = (a.uci_mask & 4u) ? a.uci_status[4 * g + 2] : 0;
-  r.nof_csi_part2    = (a.uci_mask & 4u) ? static_cast<uint32_t>(a.uci_status[4 * g + 3]) : 0u;
+  const uint32_t mask = a.uci_masks != nullptr ? a.uci_masks[g] : a.uci_mask;
+  r.harq_ack_status  = (mask & 1u) ? a.uci_status[4 * g] : 0;
+  r.csi_part1_status = (mask & 2u) ? a.uci_status[4 * g + 1] : 0;
+  r.csi_part2_status = (mask & 4u) ? a.uci_status[4 * g + 2] : 0;
+  r.nof_csi_part2    = (mask & 4u) ? static_cast<uint32_t>(a.uci_status[4 * g + 3]) : 0u;
   a.results[a.result_ids != nullptr ? a.result_ids[g] : g] = r;
 }
 

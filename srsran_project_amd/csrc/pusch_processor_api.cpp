@@ -13,6 +13,8 @@
 
 #include "api_common.h"
 #include "device_buffer.h"
+#include "uci_args.h"
+#include "ulsch_demux_args.h"
 #include "pusch_chest_args.h"
 #include "pusch_demod_args.h"
 #include "pusch_processor_args.h"
@@ -40,6 +42,9 @@ struct srs_amd_pusch_processor {
   stream_order                   order;
   pinned_stage                   stage;  // slot form: per-PDU port counts and result indices
   pinned_stage                   stage2; // CSI part 2 sizes of a batch
+  pinned_stage                   stage3; // slot form: UCI descriptors (demultiplexer, decoders, field masks)
+  device_buffer                  uci_items, uci_cbs;
+  size_t                         uci_masks_offset = 0; // of the fused group's per-PDU UCI field masks in uci_items
   std::mutex                     mtx;
   bool                           fuse = true; // SRSRAN_AMD_PUSCH_FUSED=0: always expand the estimates
   ~srs_amd_pusch_processor()
@@ -460,6 +465,95 @@ void srs_amd_pusch_processor_plan_destroy(srs_amd_pusch_processor_plan* plan)
 namespace {
 
 // chest: the estimator configuration to run (the plan's, or a copy in another slot); nullptr: the plan's.
+// The UCI PDUs (index ucis[j] of the fused group) of a slot call: one demultiplexer launch over every codeword, the
+// HARQ-ACK / CSI part 1 messages through the slot-form UCI decoder (uci_slot_build), statuses into uci_status[k][4]
+// (zeroed first) and payloads into the caller's UCI rows (d_uci + uci_offset) or scratch; the per-PDU field masks
+// of the result kernel (every fused PDU k) after the descriptors in uci_items.
+int fused_uci(srs_amd_pusch_processor* proc, const srs_amd_pusch_slot_pdu* pdus, const std::vector<uint32_t>& fused,
+              const std::vector<uint32_t>& ucis, const std::vector<size_t>& cw_off, const std::vector<size_t>& uci_off,
+              const std::vector<size_t>& pay_off, int8_t* llrs, const std::vector<size_t>& llr_off, uint8_t* d_uci,
+              hipStream_t s)
+{
+  const uint32_t n  = static_cast<uint32_t>(fused.size());
+  int8_t*        cw = proc->cw_llrs.as<int8_t>();
+  int8_t*        ur = proc->uci_llrs.as<int8_t>();
+  int32_t*       st = proc->uci_status.as<int32_t>();
+  std::vector<demux_args>       dx;
+  std::vector<uci_slot_message> msgs;
+  std::vector<uint32_t>         masks(n, 0);
+  uint32_t                      max_re = 0;
+  for (uint32_t k : ucis) {
+    const srs_amd_pusch_slot_pdu&       u    = pdus[fused[k]];
+    const srs_amd_pusch_processor_plan* pl   = u.plan;
+    const uint32_t                      ka   = pl->pdu.nof_harq_ack, kc = pl->pdu.nof_csi_part1;
+    const uint32_t                      ea   = pl->info.nof_harq_ack_bits, ec = pl->info.nof_csi_part1_bits;
+    int8_t*                             rows = ur + uci_off[k];
+    uint8_t* pay = d_uci != nullptr ? d_uci + u.uci_offset : proc->uci_payload.as<uint8_t>() + pay_off[k];
+    dx.push_back(make_demux_args(pl->demux_plan, cw + cw_off[k], llrs + llr_off[k], rows, rows + ea));
+    max_re = std::max(max_re, dx.back().nof_re);
+    if (ka != 0) {
+      msgs.push_back(uci_slot_message{rows, ea, ka, pl->pdu.modulation, pay, st + 4 * k});
+    }
+    if (kc != 0) {
+      msgs.push_back(uci_slot_message{rows + ea, ec, kc, pl->pdu.modulation, pay + ka, st + 4 * k + 1});
+    }
+    masks[k] = (ka != 0 ? 1u : 0u) | (kc != 0 ? 2u : 0u);
+  }
+  uci_slot_plan up;
+  int           rc = uci_slot_build(proc->uci, msgs.data(), static_cast<uint32_t>(msgs.size()), nullptr, up);
+  hipError_t    e  = hipSuccess;
+  if (rc == SRS_AMD_OK && up.cb_bytes != 0) {
+    e = proc->uci_cbs.ensure(up.cb_bytes);
+  }
+  if (rc == SRS_AMD_OK && e == hipSuccess) {
+    rc = uci_slot_build(proc->uci, msgs.data(), static_cast<uint32_t>(msgs.size()), proc->uci_cbs.as<uint8_t>(), up);
+  }
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  const size_t o_sh  = align_up(sizeof(demux_args) * dx.size(), 64);
+  const size_t o_po  = o_sh + align_up(sizeof(uci_short_args) * up.shorts.size(), 64);
+  const size_t o_fi  = o_po + align_up(sizeof(polar_args) * up.polars.size(), 64);
+  const size_t o_mk  = o_fi + align_up(sizeof(uci_polar_args) * up.finishes.size(), 64);
+  const size_t total = o_mk + sizeof(uint32_t) * n;
+  if (e == hipSuccess) {
+    e = proc->uci_items.ensure(total);
+  }
+  if (e == hipSuccess) {
+    e = proc->stage3.acquire(total);
+  }
+  if (e == hipSuccess) {
+    e = hipMemsetAsync(st, 0, sizeof(int32_t) * 4 * n, s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH slot UCI scratch");
+  }
+  std::memcpy(proc->stage3.at<uint8_t>(0), dx.data(), sizeof(demux_args) * dx.size());
+  std::memcpy(proc->stage3.at<uint8_t>(o_sh), up.shorts.data(), sizeof(uci_short_args) * up.shorts.size());
+  std::memcpy(proc->stage3.at<uint8_t>(o_po), up.polars.data(), sizeof(polar_args) * up.polars.size());
+  std::memcpy(proc->stage3.at<uint8_t>(o_fi), up.finishes.data(), sizeof(uci_polar_args) * up.finishes.size());
+  std::memcpy(proc->stage3.at<uint8_t>(o_mk), masks.data(), sizeof(uint32_t) * n);
+  proc->uci_masks_offset = o_mk;
+  auto* d = proc->uci_items.as<uint8_t>();
+  e       = proc->stage3.upload(d, total, s);
+  if (e == hipSuccess) {
+    e = launch_ulsch_demux_items(reinterpret_cast<const demux_args*>(d), static_cast<uint32_t>(dx.size()), max_re, s);
+  }
+  if (e == hipSuccess) {
+    e = launch_uci_short_items(reinterpret_cast<const uci_short_args*>(d + o_sh),
+                               static_cast<uint32_t>(up.shorts.size()), s);
+  }
+  if (e == hipSuccess) {
+    e = launch_polar_decode_items(reinterpret_cast<const polar_args*>(d + o_po),
+                                  static_cast<uint32_t>(up.polars.size()), s);
+  }
+  if (e == hipSuccess) {
+    e = launch_uci_polar_finish_items(reinterpret_cast<const uci_polar_args*>(d + o_fi),
+                                      static_cast<uint32_t>(up.finishes.size()), s);
+  }
+  return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH slot UCI launches");
+}
+
 int process_batch_locked(srs_amd_pusch_processor*            proc,
                          const srs_amd_pusch_processor_plan* plan,
                          const uint32_t*                     d_grids,
@@ -787,8 +881,13 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
       return fail(SRS_AMD_EINVAL, "PDU %u: invalid slot %u of numerology %u", i, pdus[i].slot_index,
                   pdus[i].numerology);
     }
-    const bool f = proc->fuse && pl->fusable && P <= STATS_STRIDE && pl->dec_cfg.new_data && !pl->uci &&
-                   pl->pdu.transform_precoding == 0 && pdus[i].d_soft == nullptr;
+    // HARQ-ACK / CSI part 1 on the UL-SCH join the group (slot-form demultiplexer and UCI decoders); CSI part 2
+    // (its sizes come from the decoded CSI part 1) and UCI-only PDUs take the batch chain
+    // HARQ processes with a soft buffer (new data or retransmission) join it too (the slot decoder's HARQ rows,
+    // early-stop decoding)
+    const bool f = proc->fuse && pl->fusable && P <= STATS_STRIDE && pl->has_sch && !pl->csi2 &&
+                   pl->pdu.transform_precoding == 0 &&
+                   (pdus[i].d_soft == nullptr ? pl->dec_cfg.new_data != 0 : pl->dec_cfg.use_early_stop != 0);
     (f ? fused : others).push_back(i);
   }
   // each PDU's estimator configuration: its plan's, moved to the PDU's own slot when it carries one (the DM-RS
@@ -842,7 +941,38 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
   }
   const bool       subset = n != nof_pdus; // results scattered to the fused PDUs' indices
   const size_t     o_ids  = align_up(sizeof(uint32_t) * n, 16);
+  // UCI PDUs of the group: the demodulator's codeword rows, the demultiplexed HARQ-ACK / CSI part 1 rows, payload
+  // rows (the caller's d_uci, or scratch) and statuses [k][4]
+  std::vector<uint32_t> ucis;
+  std::vector<size_t>   cw_off(n), uci_off(n), pay_off(n);
+  size_t                cw_bytes = 0, uci_bytes = 0, pay_bytes = 0;
+  for (uint32_t k = 0; k != n; ++k) {
+    const srs_amd_pusch_processor_plan* pl = pdus[fused[k]].plan;
+    if (!pl->uci) {
+      continue;
+    }
+    ucis.push_back(k);
+    cw_off[k]  = cw_bytes;
+    uci_off[k] = uci_bytes;
+    pay_off[k] = pay_bytes;
+    cw_bytes += align_up(pl->cw_bits, 64);
+    uci_bytes += align_up(pl->info.nof_harq_ack_bits + pl->info.nof_csi_part1_bits, 64);
+    pay_bytes += align_up(pl->pdu.nof_harq_ack + pl->pdu.nof_csi_part1, 64);
+  }
+  const uint32_t nu = static_cast<uint32_t>(ucis.size());
   hipError_t       e      = hipSetDevice(proc->device);
+  if (e == hipSuccess && nu != 0) {
+    e = proc->cw_llrs.ensure(cw_bytes);
+  }
+  if (e == hipSuccess && nu != 0) {
+    e = proc->uci_llrs.ensure(uci_bytes);
+  }
+  if (e == hipSuccess && nu != 0) {
+    e = proc->uci_payload.ensure(pay_bytes);
+  }
+  if (e == hipSuccess && nu != 0) {
+    e = proc->uci_status.ensure(static_cast<size_t>(n) * 4 * sizeof(int32_t));
+  }
   if (e == hipSuccess) {
     e = proc->stats.ensure(static_cast<size_t>(n) * STATS_STRIDE * sizeof(srs_amd_chest_port_stats));
   }
@@ -882,25 +1012,42 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     return rc;
   }
   // 2b. equalization, demapping and descrambling into each PDU's codeword LLR row (one launch per kernel kind)
+  // (a UCI PDU's whole codeword goes to its codeword row, for the demultiplexer)
   std::vector<demod_slot_item> ditems(n);
+  int8_t* const                cw_rows = proc->cw_llrs.as<int8_t>();
   for (uint32_t k = 0; k != n; ++k) {
-    ditems[k] = demod_slot_item{pdus[fused[k]].plan->demod_plan, &views[k], citems[k].d_grid, citems[k].d_stats,
-                                llrs + llr_off[k]};
+    const srs_amd_pusch_processor_plan* pl = pdus[fused[k]].plan;
+    ditems[k] = demod_slot_item{pl->demod_plan, &views[k], citems[k].d_grid, citems[k].d_stats,
+                                pl->uci ? cw_rows + cw_off[k] : llrs + llr_off[k]};
   }
   rc = pusch_demodulate_slot_fused(proc->demod, ditems.data(), n, stream);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
+  // 2b'. UCI PDUs: the demultiplexer of every codeword (UL-SCH LLRs into the PDU's decoder row) in one launch, then
+  //      the HARQ-ACK and CSI part 1 decoders of every PDU (one short-block, one polar and one CRC launch)
+  if (nu != 0) {
+    rc = fused_uci(proc, pdus, fused, ucis, cw_off, uci_off, pay_off, llrs, llr_off, d_uci, s);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+  }
   // 2c. UL-SCH decoding of every transport block of the group (srs_amd_pusch_decode_slot)
   std::vector<srs_amd_pusch_ue> ues(n);
   std::vector<uint32_t>         cb_off(n);
+  std::vector<slot_harq>        harq(n);
+  bool                          any_harq = false;
   for (uint32_t k = 0; k != n; ++k) {
-    ues[k]    = srs_amd_pusch_ue{pdus[fused[k]].plan->sch, llr_off[k], pdus[fused[k]].tb_offset};
-    cb_off[k] = pdus[fused[k]].cb_offset;
+    const srs_amd_pusch_slot_pdu& u = pdus[fused[k]];
+    ues[k]    = srs_amd_pusch_ue{u.plan->sch, llr_off[k], u.tb_offset};
+    cb_off[k] = u.cb_offset;
+    harq[k]   = slot_harq{u.d_soft, u.plan->dec_cfg.new_data};
+    any_harq |= u.d_soft != nullptr;
   }
   rc = pusch_decode_slot_ex(proc->dec, &pdus[fused[0]].plan->dec_cfg, ues.data(), n, llrs, d_tbs,
                             proc->dec_results.as<srs_amd_pusch_decoder_result>(),
-                            cb_iters != nullptr ? cb_off.data() : nullptr, cb_iters, s);
+                            cb_iters != nullptr ? cb_off.data() : nullptr, cb_iters, s,
+                            any_harq ? harq.data() : nullptr);
   if (rc != SRS_AMD_OK) {
     return rc;
   }
@@ -921,6 +1068,10 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     a.stats_stride = STATS_STRIDE;
     a.stats_by_id  = out_stats != nullptr;
     a.result_ids   = subset ? reinterpret_cast<const uint32_t*>(proc->slot_ports.as<uint8_t>() + o_ids) : nullptr;
+    if (nu != 0) { // the field masks follow the UCI descriptors (fused_uci)
+      a.uci_status = proc->uci_status.as<int32_t>();
+      a.uci_masks  = reinterpret_cast<const uint32_t*>(proc->uci_items.as<uint8_t>() + proc->uci_masks_offset);
+    }
     e              = launch_pusch_result(a, s);
   }
   const hipError_t done = scope.close();

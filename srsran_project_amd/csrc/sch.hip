@@ -570,6 +570,124 @@ __global__ __launch_bounds__(64) void asm_final_kernel(assemble_args a, uint32_t
 
 } // namespace
 
+// ---- HARQ state of the slot decoder (sch_args.h harq_args) ----------------------------------------------------------
+constexpr uint32_t HARQ_THREADS = 256;
+
+// Copies n bytes (4-byte words when both ends allow it) with the workgroup's threads, chunk blockIdx.x.
+__device__ __forceinline__ void harq_copy(uint8_t* dst, const uint8_t* src, uint32_t n)
+{
+  const uint32_t chunk = HARQ_THREADS * 16;
+  const uint32_t b0    = blockIdx.x * chunk;
+  const uint32_t b1    = min(n, b0 + chunk);
+  if (b0 >= b1) {
+    return;
+  }
+  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 3u) == 0) {
+    const uint32_t w1 = b1 / 4;
+    for (uint32_t w = b0 / 4 + threadIdx.x; w < w1; w += HARQ_THREADS) {
+      reinterpret_cast<uint32_t*>(dst)[w] = reinterpret_cast<const uint32_t*>(src)[w];
+    }
+    for (uint32_t j = max(b0, w1 * 4) + threadIdx.x; j < b1; j += HARQ_THREADS) {
+      dst[j] = src[j];
+    }
+    return;
+  }
+  for (uint32_t j = b0 + threadIdx.x; j < b1; j += HARQ_THREADS) {
+    dst[j] = src[j];
+  }
+}
+
+__global__ __launch_bounds__(HARQ_THREADS) void harq_gather_kernel(harq_args a)
+{
+  const harq_row_desc d = a.rows[blockIdx.y];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // new data: every CRC flag starts cleared (pusch_decoder_impl.cpp:133-135)
+    a.prev[blockIdx.y] = d.new_data ? 0 : *reinterpret_cast<const int32_t*>(d.soft_row + d.flag_offset);
+  }
+  if (!d.new_data) { // combining reads the earlier transmissions' soft bits
+    harq_copy(reinterpret_cast<uint8_t*>(a.internal) + static_cast<size_t>(d.row) * a.S, d.soft_row, d.soft_bytes);
+  }
+}
+
+__global__ __launch_bounds__(HARQ_THREADS) void harq_scatter_kernel(harq_args a)
+{
+  const harq_row_desc d = a.rows[blockIdx.y];
+  harq_copy(d.soft_row, reinterpret_cast<const uint8_t*>(a.internal) + static_cast<size_t>(d.row) * a.S, d.soft_bytes);
+  if (blockIdx.x != 0) {
+    return;
+  }
+  const int32_t prev = a.prev[blockIdx.y];
+  uint8_t*      m    = a.msgs + static_cast<size_t>(d.row) * a.M;
+  uint8_t*      sm   = d.soft_row + d.msg_offset;
+  if (prev != 0) {
+    // OK from an earlier transmission: its stored message and iteration count (:333-345, cb_stats not updated)
+    for (uint32_t j = threadIdx.x; j < d.msg_bytes; j += HARQ_THREADS) {
+      m[j] = sm[j];
+    }
+    if (threadIdx.x == 0) {
+      a.iters[d.row] = prev;
+    }
+    return;
+  }
+  const int32_t it = a.iters[d.row];
+  if (it >= 0) { // decoded now: the message and the flag (its iteration count) kept for later transmissions
+    for (uint32_t j = threadIdx.x; j < d.msg_bytes; j += HARQ_THREADS) {
+      sm[j] = m[j];
+    }
+  }
+  if (threadIdx.x == 0) {
+    *reinterpret_cast<int32_t*>(d.soft_row + d.flag_offset) = it >= 0 ? it : 0;
+  }
+}
+
+__global__ __launch_bounds__(64) void harq_final_kernel(harq_args a)
+{
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= a.nof_tbs) {
+    return;
+  }
+  const harq_tb_desc                  d = a.tbs[t];
+  const srs_amd_pusch_decoder_result& r = a.results[d.result];
+  // every codeblock passed but not the TB CRC: reset_codeblocks_crc (pusch_decoder_impl.cpp:425-437)
+  if (d.C > 1 && r.nof_codeblocks_crc_ok == d.C && !r.tb_crc_ok) {
+    for (uint32_t c = 0; c < d.C; ++c) {
+      *reinterpret_cast<int32_t*>(d.soft + static_cast<size_t>(c) * d.row_bytes + d.flag_offset) = 0;
+    }
+  }
+}
+
+hipError_t launch_harq_gather(const harq_args& a, uint32_t max_soft_bytes, hipStream_t stream)
+{
+  if (a.nof_rows == 0) {
+    return hipSuccess;
+  }
+  const uint32_t gx = max_soft_bytes > HARQ_THREADS * 16 ? (max_soft_bytes + HARQ_THREADS * 16 - 1) / (HARQ_THREADS * 16)
+                                                         : 1u;
+  hipLaunchKernelGGL(harq_gather_kernel, dim3(gx, a.nof_rows), dim3(HARQ_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_harq_scatter(const harq_args& a, uint32_t max_soft_bytes, hipStream_t stream)
+{
+  if (a.nof_rows == 0) {
+    return hipSuccess;
+  }
+  const uint32_t gx = max_soft_bytes > HARQ_THREADS * 16 ? (max_soft_bytes + HARQ_THREADS * 16 - 1) / (HARQ_THREADS * 16)
+                                                         : 1u;
+  hipLaunchKernelGGL(harq_scatter_kernel, dim3(gx, a.nof_rows), dim3(HARQ_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_harq_final(const harq_args& a, hipStream_t stream)
+{
+  if (a.nof_tbs == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(harq_final_kernel, dim3((a.nof_tbs + 63) / 64), dim3(64), 0, stream, a);
+  return hipGetLastError();
+}
+
+
 __global__ __launch_bounds__(256) void rm_arrays_kernel(uint32_t* arrays, uint32_t rows, uint32_t C, uint32_t S,
                                                        uint32_t e_short, uint32_t e_long, uint32_t tb_units)
 {

@@ -135,6 +135,47 @@ struct assemble_args {
   uint32_t                      max_tb_bits;
 };
 
+// HARQ state of the PUSCH slot decoder (pusch_api.cpp decode_slot_locked): the codeblocks of transport blocks with a
+// caller soft buffer are decoded in the slot's internal rows; their soft bits are gathered from the caller's rows
+// before the rate dematcher combines into them and scattered back after decoding, with the message / CRC-flag
+// bookkeeping of pusch_decoder_impl.cpp:320-375 and 416-437 (what the assemble kernels do for a uniform batch).
+struct harq_row_desc {
+  uint8_t* soft_row;    // the caller's soft-buffer row: soft LLRs | message bytes | int32 flag (soft_row_layout)
+  uint32_t row;         // the decoder row
+  uint32_t soft_bytes;  // soft LLR bytes
+  uint32_t msg_offset;
+  uint32_t msg_bytes;
+  uint32_t flag_offset;
+  uint32_t new_data;
+};
+struct harq_tb_desc {
+  uint8_t* soft;        // the caller's soft buffer (C rows)
+  uint32_t result;      // index of the TB's decoder result
+  uint32_t C;
+  uint32_t row_bytes;
+  uint32_t flag_offset;
+};
+struct harq_args {
+  const harq_row_desc*          rows;
+  uint32_t                      nof_rows;
+  const harq_tb_desc*           tbs;
+  uint32_t                      nof_tbs;
+  int8_t*                       internal; // decoder soft rows, stride S
+  uint32_t                      S;
+  uint8_t*                      msgs;     // decoder message rows, stride M
+  uint32_t                      M;
+  int32_t*                      iters;    // decoder iterations per row (-1: CRC failed)
+  int32_t*                      prev;     // [nof_rows]: the codeblock's flag before this transmission
+  srs_amd_pusch_decoder_result* results;
+};
+// Before the rate dematcher: soft bits of the retransmitted rows into the decoder rows, the previous flags.
+hipError_t launch_harq_gather(const harq_args& a, uint32_t max_soft_bytes, hipStream_t stream);
+// After the LDPC decoder, before the assembly: soft bits back, messages / iterations of codeblocks OK from an
+// earlier transmission into the decoder rows, the fresh messages and flags into the caller's rows.
+hipError_t launch_harq_scatter(const harq_args& a, uint32_t max_soft_bytes, hipStream_t stream);
+// After the assembly: a TB whose codeblocks all passed but whose TB CRC failed clears its CRC flags.
+hipError_t launch_harq_final(const harq_args& a, hipStream_t stream);
+
 hipError_t launch_segment(const segment_args& a, hipStream_t stream);
 // true when launch_segment also attaches the codeblock CRCs (segment_crc_kernel)
 bool       segment_attaches_crc(const segment_args& a);

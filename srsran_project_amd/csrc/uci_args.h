@@ -5,6 +5,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
+
+#include "polar_args.h"
+
+struct srs_amd_uci_decoder;
 
 namespace srs_amd {
 
@@ -37,5 +42,29 @@ struct uci_polar_args {
 
 hipError_t launch_uci_short(const uci_short_args& a, uint32_t nof, hipStream_t stream);
 hipError_t launch_uci_polar_finish(const uci_polar_args& a, uint32_t nof, hipStream_t stream);
+// One UCI message of a slot (HARQ-ACK, CSI part 1 ... of one PUSCH PDU): its E LLRs, K payload bits and status.
+struct uci_slot_message {
+  const int8_t* llrs;
+  uint32_t      E, K;
+  int32_t       modulation;
+  uint8_t*      msg;
+  int32_t*      status;
+};
+// The descriptors of a slot's UCI decoding (uci_decoder_impl.cpp:47-111 per message): the 1-11 bit messages for the
+// short-block kernel, every polar codeblock (its own code) for the polar decoder, the polar messages' CRC / filler
+// step; cb_bytes: the decoded-codeblock scratch the polar rows take at d_cbs.
+struct uci_slot_plan {
+  std::vector<uci_short_args> shorts;
+  std::vector<polar_args>     polars;
+  std::vector<uci_polar_args> finishes;
+  size_t                      cb_bytes = 0;
+};
+// Builds the plan (d_cbs may be null to size the scratch first).  Codes are created and cached by the decoder.
+int uci_slot_build(::srs_amd_uci_decoder* dec, const uci_slot_message* msgs, uint32_t n, uint8_t* d_cbs,
+                   uci_slot_plan& out);
+
+// Slot forms: one argument block per message (device arrays), each with its own E / K / Qm.
+hipError_t launch_uci_short_items(const uci_short_args* items, uint32_t n, hipStream_t stream);
+hipError_t launch_uci_polar_finish_items(const uci_polar_args* items, uint32_t n, hipStream_t stream);
 
 } // namespace srs_amd

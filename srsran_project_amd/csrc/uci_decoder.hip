@@ -34,10 +34,13 @@ __device__ __forceinline__ int wave_sum(int v)
   return v;
 }
 
-__global__ __launch_bounds__(64) void uci_short_kernel(uci_short_args a)
+// MULTI: one argument block per message (items[blockIdx.x], row 0), the slot form of the PUSCH processor
+template <bool MULTI>
+__global__ __launch_bounds__(64) void uci_short_kernel(uci_short_args own, const uci_short_args* items)
 {
+  const uci_short_args& a = MULTI ? items[blockIdx.x] : own;
   __shared__ int tmp[32];
-  const uint32_t row  = blockIdx.x;
+  const uint32_t row  = MULTI ? 0u : blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const int8_t*  in   = a.llrs + row * a.llr_stride;
   uint8_t*       msg  = a.msgs + row * a.msg_stride;
@@ -181,12 +184,16 @@ __device__ bool crc_ok(const uint8_t* bits, uint32_t n, uint32_t L)
   return crc == 0;
 }
 
-__global__ __launch_bounds__(64) void uci_polar_finish_kernel(uci_polar_args a, uint32_t nof)
+template <bool MULTI>
+__global__ __launch_bounds__(64) void uci_polar_finish_kernel(uci_polar_args own, const uci_polar_args* items,
+                                                              uint32_t nof)
 {
-  const uint32_t row = blockIdx.x * 64 + threadIdx.x;
-  if (row >= nof) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= nof) {
     return;
   }
+  const uci_polar_args& a   = MULTI ? items[i] : own;
+  const uint32_t        row = MULTI ? 0u : i;
   const uint8_t* cb0 = a.cbs + static_cast<uint64_t>(row) * a.C * a.cb_stride;
   uint8_t*       msg = a.msgs + row * a.msg_stride;
   int32_t* st = reinterpret_cast<int32_t*>(reinterpret_cast<uint8_t*>(a.status) + row * a.status_stride);
@@ -215,7 +222,7 @@ hipError_t launch_uci_short(const uci_short_args& a, uint32_t nof, hipStream_t s
   if (nof == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(uci_short_kernel, dim3(nof), dim3(64), 0, stream, a);
+  hipLaunchKernelGGL(uci_short_kernel<false>, dim3(nof), dim3(64), 0, stream, a, nullptr);
   return hipGetLastError();
 }
 
@@ -224,7 +231,26 @@ hipError_t launch_uci_polar_finish(const uci_polar_args& a, uint32_t nof, hipStr
   if (nof == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(uci_polar_finish_kernel, dim3((nof + 63) / 64), dim3(64), 0, stream, a, nof);
+  hipLaunchKernelGGL(uci_polar_finish_kernel<false>, dim3((nof + 63) / 64), dim3(64), 0, stream, a, nullptr, nof);
+  return hipGetLastError();
+}
+
+hipError_t launch_uci_short_items(const uci_short_args* items, uint32_t n, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(uci_short_kernel<true>, dim3(n), dim3(64), 0, stream, uci_short_args{}, items);
+  return hipGetLastError();
+}
+
+hipError_t launch_uci_polar_finish_items(const uci_polar_args* items, uint32_t n, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(uci_polar_finish_kernel<true>, dim3((n + 63) / 64), dim3(64), 0, stream, uci_polar_args{},
+                     items, n);
   return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #include "api_common.h"
 #include "device_buffer.h"
 #include "uci_args.h"
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -63,6 +64,51 @@ uint32_t nof_codeblocks(uint32_t A, uint32_t E) // get_nof_uci_codeblocks (uci_i
 }
 
 } // namespace
+
+int srs_amd::uci_slot_build(srs_amd_uci_decoder* dec, const uci_slot_message* msgs, uint32_t n, uint8_t* d_cbs,
+                            uci_slot_plan& out)
+{
+  out = uci_slot_plan{};
+  std::lock_guard<std::mutex> lock(dec->mtx);
+  for (uint32_t i = 0; i != n; ++i) {
+    const uci_slot_message& m  = msgs[i];
+    const uint32_t          qm = m.modulation < 2 ? 1u : static_cast<uint32_t>(m.modulation);
+    if (m.K == 0 || m.K > 1706) {
+      return fail(SRS_AMD_EINVAL, "Invalid UCI payload size %u.", m.K);
+    }
+    if (m.K <= 11) {
+      out.shorts.push_back(uci_short_args{m.llrs, 0, m.msg, 0, m.status, 0, m.E, m.K, qm});
+      continue;
+    }
+    // polar codeblocks (uci_decoder_impl.cpp:47-76), as srs_amd_uci_decode_batch
+    const uint32_t C  = nof_codeblocks(m.K, m.E);
+    const uint32_t L  = crc_size(m.K);
+    const uint32_t A0 = m.K / C, E0 = m.E / C, F0 = m.K % C;
+    const uint32_t A1 = (m.K + C - 1) / C, E1 = m.E / C;
+    const uint32_t K0 = A0 + L + F0, K1 = A1 + L;
+    if (E0 == 0) {
+      return fail(SRS_AMD_EINVAL, "UCI codeword of %u bits too short.", m.E);
+    }
+    const uint64_t cb_stride = (std::max(K0, K1) + 63) / 64 * 64;
+    uint8_t*       cbs       = d_cbs + out.cb_bytes;
+    for (uint32_t r = 0; r != C; ++r) {
+      srs_amd_polar_code* c = dec->code(r == 0 ? K0 : K1, r == 0 ? E0 : E1);
+      if (c == nullptr) {
+        return SRS_AMD_EINVAL; // the polar code reported why
+      }
+      polar_args a = polar_code_base(c);
+      a.llrs       = m.llrs + r * E0;
+      a.msgs_out   = cbs + r * cb_stride;
+      a.llr_stride = r == 0 ? E0 : E1;
+      a.msg_stride = static_cast<uint32_t>(cb_stride);
+      a.nof        = 1;
+      out.polars.push_back(a);
+    }
+    out.finishes.push_back(uci_polar_args{cbs, cb_stride, m.msg, 0, m.status, 0, C, A0, F0, A1, L});
+    out.cb_bytes += C * cb_stride;
+  }
+  return SRS_AMD_OK;
+}
 
 extern "C" {
 

@@ -18,10 +18,13 @@ __device__ __forceinline__ uint32_t scr_bit(const uint32_t* scr, uint32_t n)
   return (scr[n >> 5] >> (n & 31)) & 1u;
 }
 
-__global__ __launch_bounds__(DMX_THREADS) void ulsch_demux_kernel(demux_args a)
+// MULTI: one argument block per codeword (items[blockIdx.y], row 0), the slot form of the PUSCH processor
+template <bool MULTI>
+__global__ __launch_bounds__(DMX_THREADS) void ulsch_demux_kernel(demux_args own, const demux_args* items)
 {
-  const uint32_t re  = blockIdx.x * DMX_THREADS + threadIdx.x;
-  const uint64_t row = blockIdx.y;
+  const demux_args& a   = MULTI ? items[blockIdx.y] : own;
+  const uint32_t    re  = blockIdx.x * DMX_THREADS + threadIdx.x;
+  const uint64_t    row = MULTI ? 0u : blockIdx.y;
   if (re >= a.nof_re) {
     return;
   }
@@ -79,8 +82,18 @@ hipError_t launch_ulsch_demux(const demux_args& a, uint32_t nof_cws, hipStream_t
   if (a.nof_re == 0 || nof_cws == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(ulsch_demux_kernel, dim3((a.nof_re + DMX_THREADS - 1) / DMX_THREADS, nof_cws),
-                     dim3(DMX_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(ulsch_demux_kernel<false>, dim3((a.nof_re + DMX_THREADS - 1) / DMX_THREADS, nof_cws),
+                     dim3(DMX_THREADS), 0, stream, a, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_ulsch_demux_items(const demux_args* items, uint32_t n, uint32_t max_re, hipStream_t stream)
+{
+  if (n == 0 || max_re == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(ulsch_demux_kernel<true>, dim3((max_re + DMX_THREADS - 1) / DMX_THREADS, n), dim3(DMX_THREADS),
+                     0, stream, demux_args{}, items);
   return hipGetLastError();
 }
 

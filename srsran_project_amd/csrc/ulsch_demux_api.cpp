@@ -458,3 +458,22 @@ int srs_amd_ulsch_demultiplex_csi2(srs_amd_ulsch_demux*            demux,
 }
 
 } // extern "C"
+
+demux_args srs_amd::make_demux_args(const srs_amd_ulsch_demux_plan* plan, const int8_t* cws, int8_t* sch, int8_t* ack,
+                                    int8_t* csi1)
+{
+  demux_args a{};
+  a.cws     = cws;
+  a.sch     = sch;
+  a.ack     = ack;
+  a.csi1    = csi1;
+  a.sch_map = plan->d_maps;
+  a.uci_map = plan->d_maps + plan->pl.nof_re;
+  a.scr     = plan->d_scr;
+  a.nof_re  = plan->pl.nof_re;
+  a.qm      = bits_per_symbol(plan->cfg.modulation);
+  a.bpre    = a.qm * plan->cfg.nof_layers;
+  a.ack_ph  = plan->cfg.nof_harq_ack_bits <= 2 ? plan->cfg.nof_harq_ack_bits : 0u;
+  a.csi1_ph = plan->cfg.nof_csi_part1_bits <= 2 ? plan->cfg.nof_csi_part1_bits : 0u;
+  return a;
+}

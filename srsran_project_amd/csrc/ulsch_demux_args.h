@@ -49,5 +49,10 @@ struct demux_placement {
 int build_demux_placement(const srs_amd_ulsch_demux_config& cfg, demux_placement& out);
 
 hipError_t launch_ulsch_demux(const demux_args& a, uint32_t nof_cws, hipStream_t stream);
+// Slot form: one argument block per codeword (device array), each with its own plan; max_re: the largest nof_re.
+hipError_t launch_ulsch_demux_items(const demux_args* items, uint32_t n, uint32_t max_re, hipStream_t stream);
+// The argument block of one codeword of `plan` (no CSI part 2): codeword LLRs cws, outputs sch / ack / csi1.
+demux_args make_demux_args(const srs_amd_ulsch_demux_plan* plan, const int8_t* cws, int8_t* sch, int8_t* ack,
+                           int8_t* csi1);
 
 } // namespace srs_amd
