@@ -167,6 +167,7 @@ class SlotPipeline:
         dl, ul, ue_tx = [], [], []   # (sch plan, mod plan, dmrs, cell) / (processor plan, cell) / UE TX
         self.kinds = []              # UL PDU kinds (mixed: "uci", "harq", "tp" or "data")
         self.tp_ues = []             # DFT-s-OFDM UEs: (cell, first PRB, end PRB, channel [port], n_rs_id)
+        self.ul_pdus = []            # the UL PDUs (UCI UEs multiplex their UCI REs at the transmitter)
         for c in range(cells):
             n_id = int(rng.integers(0, 1008))
             for side in ("dl", "ul"):
@@ -222,6 +223,7 @@ class SlotPipeline:
                                            scrambling_id=n_id, n_scid=0, nof_cdm_groups_without_data=2, rb_start=lo,
                                            rb_count=hi - lo, start_symbol_index=0, nof_symbols=14, tbs=tbs, **extra)
                         self.kinds.append(kind)
+                        self.ul_pdus.append(pdu)
                         pp = self.proc.plan(pdu, nsubc)
                         h = bp.ul_channel(layers, 4)
                         mp = self.mod.plan(amd.PdschModulatorConfig(
@@ -235,8 +237,8 @@ class SlotPipeline:
                         ul.append((pp, c))
                         if kind == "tp":
                             self.tp_ues.append((c, lo, hi, h[0], n_id))
-                        # the UE transmits the codeword of the PDU's own rv (UCI not multiplexed: those PDUs'
-                        # TBs fail, see check(); DFT-s-OFDM UEs are DFT-spread below)
+                        # the UE transmits the codeword of the PDU's own rv (UCI UEs multiplexed and DFT-s-OFDM
+                        # UEs DFT-spread below)
                         ue_tx.append((pp.sch, mp, dm, c))
         self.dl, self.ul = dl, ul
         g = torch.Generator(device=dev)
@@ -262,9 +264,25 @@ class SlotPipeline:
         self.tb_ul = torch.randint(0, 256, (tpos,), device=dev, dtype=torch.uint8, generator=g)
         cw_ul = torch.zeros(cpos, dtype=torch.uint8, device=dev)
         self.enc.encode_slot(self.tb_ul, ul_ues, out=cw_ul)
+        # the UEs' transmitted codewords: the UL-SCH codeword, or for a UCI UE the whole multiplexed codeword (its
+        # UL-SCH bits at the REs the receiver's demultiplexer takes them from, random bits on the UCI REs)
+        cw_host = cw_ul.cpu().numpy()
+        tx_parts, tx_off, pos = [], [], 0
+        for j, ((sp, mp, dm, c), (_, _, co)) in enumerate(zip(ue_tx, ul_ues)):
+            if self.kinds[j] == "uci":
+                sch = np.unpackbits(cw_host[co:co + (sp.cw_length + 7) // 8])[:sp.cw_length]
+                part = np.packbits(self._multiplex(amd, self.ul_pdus[j], sch, mp.nof_bits, rng))
+            else:
+                part = cw_host[co:co + (sp.cw_length + 7) // 8]
+            tx_off.append(pos)
+            tx_parts.append(part)
+            pos += (part.size + 63) // 64 * 64
+        cw_tx = np.zeros(max(pos, 1), np.uint8)
+        for off, part in zip(tx_off, tx_parts):
+            cw_tx[off:off + part.size] = part
         grid = torch.zeros((cells, 4, 14, nsubc), dtype=torch.int32, device=dev)
-        self.mod.modulate_slot(grid, amd.PdschSlot([(mp, dm, c, co) for (sp, mp, dm, c), (_, _, co)
-                                                    in zip(ue_tx, ul_ues)]), codewords=cw_ul)
+        self.mod.modulate_slot(grid, amd.PdschSlot([(mp, dm, c, off) for (sp, mp, dm, c), off in zip(ue_tx, tx_off)]),
+                               codewords=torch.from_numpy(cw_tx).to(dev))
         for c, lo, hi, h, n_rs_id in self.tp_ues:
             self._transform_precode(amd, bp, grid, c, lo, hi, h, n_rs_id)
         samp = self.ofdm_mod.modulate_batch(grid.view(torch.int16).view(cells, 4, 14, 2 * nsubc), bp.SLOT)
@@ -293,6 +311,38 @@ class SlotPipeline:
         self.res_ul = torch.zeros((len(ul), amd.pusch_processor.RESULT_BYTES), dtype=torch.uint8, device=dev)
         self.ul_stream = None
         torch.cuda.synchronize(dev)
+
+    def _multiplex(self, amd, pdu, sch_bits, nof_bits, rng):
+        """UE-side UL-SCH / UCI multiplexing for the timing bench (untimed setup): the UL-SCH codeword placed where
+        the MI355X demultiplexer (srs_amd_ulsch_demultiplex, this library's own) reads it -- found by passing
+        RE-index-coded LLRs through it, seven bits per pass -- and random bits on the HARQ-ACK / CSI part 1 REs (the
+        bench checks the transport blocks, not the UCI payloads)."""
+        qm, L = pdu.modulation, pdu.nof_tx_layers
+        bpre = qm * L
+        nre = nof_bits // bpre
+        info = amd.ulsch_information(amd.UlschConfig(
+            tbs=pdu.tbs, modulation=qm, target_code_rate=pdu.target_code_rate, nof_harq_ack_bits=pdu.nof_harq_ack,
+            nof_csi_part1_bits=pdu.nof_csi_part1, alpha_scaling=pdu.alpha_scaling,
+            beta_offset_harq_ack=pdu.beta_offset_harq_ack, beta_offset_csi_part1=pdu.beta_offset_csi_part1,
+            nof_rb=pdu.rb_count, start_symbol_index=pdu.start_symbol_index, nof_symbols=pdu.nof_symbols,
+            dmrs_type=pdu.dmrs_type, dmrs_symbol_mask=pdu.dmrs_symbol_mask,
+            nof_cdm_groups_without_data=pdu.nof_cdm_groups_without_data, nof_layers=L))
+        if not hasattr(self, "_demux"):
+            self._demux = amd.UlschDemux(device=self.dev.index)
+        plan = self._demux.plan(amd.UlschDemuxConfig(
+            qm, L, pdu.rb_count, pdu.start_symbol_index, pdu.nof_symbols, info["nof_harq_ack_rvd"], pdu.dmrs_type,
+            pdu.dmrs_symbol_mask, pdu.nof_cdm_groups_without_data, pdu.nof_harq_ack, info["nof_harq_ack_bits"],
+            pdu.nof_csi_part1, info["nof_csi_part1_bits"], (pdu.rnti << 15) + pdu.n_id))
+        assert plan.nof_codeword_bits == nof_bits and plan.nof_sch_bits == sch_bits.size
+        re_of = np.zeros(sch_bits.size // bpre, np.int64)
+        for k in range(3):
+            code = (((np.arange(nre) >> (7 * k)) & 0x7F) + 1).astype(np.int8)
+            out = self._demux.demultiplex(np.repeat(code, bpre), plan)[0]
+            re_of += (np.abs(out[::bpre].astype(np.int64)) - 1) << (7 * k)  # 128 wraps to -128 in int8
+        cw = rng.integers(0, 2, nof_bits).astype(np.uint8)
+        idx = (re_of[:, None] * bpre + np.arange(bpre)).ravel()
+        cw[idx] = sch_bits
+        return cw
 
     def _transform_precode(self, amd, bp, grid, c, lo, hi, h, n_rs_id):
         """A DFT-s-OFDM UE's transmission (untimed setup): the data symbols the PDSCH modulator mapped (scrambled,
@@ -363,9 +413,7 @@ class SlotPipeline:
         res = amd.pusch_processor.parse_results(self.res_ul.cpu().numpy())
         rx, tx = self.tb_rx.cpu().numpy(), self.tb_ul.cpu().numpy()
         ok = []
-        for (pp, _), r, off, toff, k in zip(self.ul, res, self.ul_slot.offsets, self.ul_tb_off, self.kinds):
-            if k == "uci":
-                continue  # transmitted without UCI multiplexing: not decodable by construction
+        for (pp, _), r, off, toff in zip(self.ul, res, self.ul_slot.offsets, self.ul_tb_off):
             n = pp.tb_bytes
             ok.append(bool(r.data.tb_crc_ok) and np.array_equal(rx[off:off + n], tx[toff:toff + n]))
         its = sum(r.data.ldpc_iterations_sum for r in res) / max(1, sum(r.data.nof_codeblocks_total for r in res))

@@ -76,13 +76,21 @@ __global__ __launch_bounds__(256) void demodulate_kernel(demodulate_args a)
 // state jumped once on the scalar unit) and writes the descrambled LLRs 8 bytes at a time.
 constexpr uint32_t DD_SYMS = 1024;
 
-__global__ __launch_bounds__(256) void demap_descramble_kernel(demodulate_args a, demap_descramble_args d)
+// MULTI: one argument pair per PDU (items[blockIdx.y], grid 0), the PUSCH processor's slot form
+template <bool MULTI>
+__global__ __launch_bounds__(256) void demap_descramble_kernel(demodulate_args own_a, demap_descramble_args own_d,
+                                                               const demap_item* items)
 {
+  const demodulate_args&       a = MULTI ? items[blockIdx.y].a : own_a;
+  const demap_descramble_args& d = MULTI ? items[blockIdx.y].d : own_d;
+  if (MULTI && blockIdx.x * DD_SYMS >= d.grid_symbols) {
+    return;
+  }
   __shared__ int8_t   s_llr[DD_SYMS * 8];
   __shared__ uint32_t words[DD_SYMS * 8 / 32];
   __shared__ float    lt[4 * 2 * 16];
   stage_interval_tables(a, lt);
-  const uint32_t      g   = blockIdx.y;
+  const uint32_t      g   = MULTI ? 0u : blockIdx.y;
   const uint32_t      bpp = a.qm < 1 ? 1u : static_cast<uint32_t>(a.qm); // LLRs per symbol
   const uint32_t      s0  = blockIdx.x * DD_SYMS;                        // first symbol (within the grid)
   const uint32_t      n0  = s0 * bpp;                                    // first LLR of the workgroup
@@ -224,8 +232,18 @@ hipError_t launch_demap_descramble(const demodulate_args& a, const demap_descram
   if (d.grid_symbols == 0 || nof_grids == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(demap_descramble_kernel, dim3((d.grid_symbols + DD_SYMS - 1) / DD_SYMS, nof_grids), dim3(256), 0,
-                     stream, a, d);
+  hipLaunchKernelGGL(demap_descramble_kernel<false>, dim3((d.grid_symbols + DD_SYMS - 1) / DD_SYMS, nof_grids),
+                     dim3(256), 0, stream, a, d, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_demap_descramble_items(const demap_item* items, uint32_t n, uint32_t max_symbols, hipStream_t stream)
+{
+  if (n == 0 || max_symbols == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(demap_descramble_kernel<true>, dim3((max_symbols + DD_SYMS - 1) / DD_SYMS, n), dim3(256), 0,
+                     stream, demodulate_args{}, demap_descramble_args{}, items);
   return hipGetLastError();
 }
 

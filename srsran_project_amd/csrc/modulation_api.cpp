@@ -571,6 +571,28 @@ uint32_t srs_amd::demap_symbol_bounds(int qm, const uint32_t* sym_counts, uint32
   return s0;
 }
 
+int srs_amd::make_demap_item(srs_amd_modulator* mod, int qm, int8_t* d_llrs, const float* d_symbols,
+                             const float* d_noise_vars, uint32_t grid_symbols, const uint32_t* sym_counts,
+                             const uint32_t* d_jump, uint32_t c_init, demap_item& out)
+{
+  int rc = check(mod, qm);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  out              = demap_item{};
+  out.a            = demodulate_args_for(mod, qm, grid_symbols);
+  out.a.symbols    = d_symbols;
+  out.a.noise_vars = d_noise_vars;
+  out.d.llrs         = d_llrs;
+  out.d.jump         = d_jump;
+  out.d.grid_symbols = grid_symbols;
+  out.d.c_init       = c_init;
+  if (demap_symbol_bounds(qm, sym_counts, out.d.sym_lo, out.d.simd_hi) != grid_symbols) {
+    return fail(SRS_AMD_EINVAL, "per-symbol counts do not add up to the grid symbols (%u)", grid_symbols);
+  }
+  return SRS_AMD_OK;
+}
+
 int srs_amd::demap_descramble_batch(srs_amd_modulator* mod, int qm, int8_t* d_llrs, uint64_t llr_stride,
                                     const float* d_symbols, const float* d_noise_vars, uint32_t grid_symbols,
                                     const uint32_t* sym_counts, uint32_t nof_grids, const uint32_t* d_jump,

@@ -66,6 +66,13 @@ struct demap_descramble_args {
 };
 hipError_t launch_demap_descramble(const demodulate_args& a, const demap_descramble_args& d, uint32_t nof_grids,
                                    hipStream_t stream);
+// Slot form: one argument pair per PDU (device array, one grid each), max_symbols: the largest grid_symbols.
+struct demap_item {
+  demodulate_args       a;
+  demap_descramble_args d;
+};
+hipError_t launch_demap_descramble_items(const demap_item* items, uint32_t n, uint32_t max_symbols,
+                                         hipStream_t stream);
 // Gold-sequence words 0 .. nof_words of c_init into out (c(32 w + b) at bit b of word w).
 hipError_t launch_gold_words(const uint32_t* jump, uint32_t c_init, uint32_t* out, uint32_t nof_words,
                              hipStream_t stream);
@@ -88,6 +95,10 @@ uint32_t demap_symbol_bounds(int qm, const uint32_t* sym_counts, uint32_t* sym_l
 int demap_descramble_batch(srs_amd_modulator* mod, int qm, int8_t* d_llrs, uint64_t llr_stride, const float* d_symbols,
                            const float* d_noise_vars, uint32_t grid_symbols, const uint32_t* sym_counts,
                            uint32_t nof_grids, const uint32_t* d_jump, uint32_t c_init, void* stream);
+// The argument pair demap_descramble_batch launches for one grid (the slot form's item).
+int make_demap_item(srs_amd_modulator* mod, int qm, int8_t* d_llrs, const float* d_symbols, const float* d_noise_vars,
+                    uint32_t grid_symbols, const uint32_t* sym_counts, const uint32_t* d_jump, uint32_t c_init,
+                    demap_item& out);
 hipError_t launch_scramble_bits(const prbs_args& a, hipStream_t stream);
 hipError_t launch_descramble_llrs(const prbs_args& a, hipStream_t stream);
 

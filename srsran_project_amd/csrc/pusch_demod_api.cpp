@@ -9,6 +9,7 @@
 // descrambling, three launches on the caller's stream.
 #include "srsran_amd/pusch_demodulator.h"
 #include "srsran_amd/transform_precoding.h"
+#include "transform_precoding_args.h"
 
 #include <hip/hip_runtime.h>
 
@@ -255,9 +256,6 @@ int srs_amd::pusch_demodulate_slot_fused(::srs_amd_pusch_demodulator* dem,
       return fail(SRS_AMD_EINVAL, "null device buffer");
     }
     const chest_args& c = *it.chest_view;
-    if (pl->tp_subc != 0) {
-      return fail(SRS_AMD_EINVAL, "transform precoding is not supported by the slot form");
-    }
     if (c.nof_ports != pl->nof_ports || c.L != pl->nof_layers || c.nsubc != pl->args.nof_subc ||
         c.first_symbol != pl->args.first_symbol || c.nof_symbols != pl->nof_symbols ||
         pl->args.first_subc < 12 * c.prb_lo || pl->args.first_subc + pl->span_subc > 12 * c.prb_lo + c.nof_re ||
@@ -275,6 +273,16 @@ int srs_amd::pusch_demodulate_slot_fused(::srs_amd_pusch_demodulator* dem,
     a.tiles_x       = (pl->span_subc + 255) / 256;
     a.nof_tiles     = a.tiles_x;
     pairs[i]        = eq_item{a, c};
+  }
+  // transform precoding (one layer): the equalizer writes its symbols and noise variances to scratch, then per PDU
+  // the deprecoder and the demapper (pusch_demodulator_impl.cpp:344-351, as demodulate_impl)
+  std::vector<size_t> tp_off(nof_items, 0);
+  size_t              tp_res = 0;
+  for (uint32_t i = 0; i != nof_items; ++i) {
+    if (items[i].plan->tp_subc != 0) {
+      tp_off[i] = tp_res;
+      tp_res += items[i].plan->args.nof_re;
+    }
   }
   for (uint32_t i = 0; i != nof_items; ++i) {
     const auto* pl = items[i].plan;
@@ -304,12 +312,29 @@ int srs_amd::pusch_demodulate_slot_fused(::srs_amd_pusch_demodulator* dem,
     return SRS_AMD_OK;
   }
   const size_t o_ids = align_up(sizeof(eq_item) * nof_items, 256);
-  const size_t total = o_ids + sizeof(uint32_t) * order.size();
+  const size_t n_tp  = std::count_if(items, items + nof_items, [](const demod_slot_item& it) {
+    return it.plan->tp_subc != 0 && it.plan->args.nof_re != 0;
+  });
+  const size_t o_tp  = align_up(o_ids + sizeof(uint32_t) * order.size(), 256);
+  const size_t o_dm  = align_up(o_tp + sizeof(tp_args) * n_tp, 256);
+  const size_t total = n_tp == 0 ? o_ids + sizeof(uint32_t) * order.size() : o_dm + sizeof(demap_item) * n_tp;
   auto         s     = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lock(dem->mtx);
   hipError_t                  e = hipSetDevice(dem->device);
   if (e == hipSuccess) {
     e = dem->slot_items.ensure(total);
+  }
+  if (e == hipSuccess && tp_res != 0) {
+    e = dem->scratch.ensure(tp_res * (sizeof(float2) + sizeof(float)));
+  }
+  float2* const eq_out = dem->scratch.as<float2>();
+  float* const  nv_out = reinterpret_cast<float*>(eq_out + tp_res);
+  for (uint32_t i = 0; i != nof_items && e == hipSuccess; ++i) {
+    if (items[i].plan->tp_subc != 0) {
+      pairs[i].a.eq_out    = eq_out + tp_off[i];
+      pairs[i].a.nv_out    = nv_out + tp_off[i];
+      pairs[i].a.eq_stride = items[i].plan->args.nof_re;
+    }
   }
   if (e == hipSuccess) {
     e = dem->stage.acquire(total);
@@ -323,6 +348,34 @@ int srs_amd::pusch_demodulate_slot_fused(::srs_amd_pusch_demodulator* dem,
   call_scope scope(dem->order, nullptr, s);
   std::memcpy(dem->stage.at<eq_item>(0), pairs.data(), sizeof(eq_item) * nof_items);
   std::memcpy(dem->stage.at<uint32_t>(o_ids), order.data(), sizeof(uint32_t) * order.size());
+  // transform-precoded PDUs: deprecoder rows and demapper of each (one launch each for all of them)
+  uint32_t tp_rows = 0, tp_syms = 0;
+  size_t   tp_lds  = 0;
+  for (uint32_t i = 0, k = 0; i != nof_items; ++i) {
+    const auto* pl = items[i].plan;
+    if (pl->tp_subc == 0 || pl->args.nof_re == 0) {
+      continue;
+    }
+    float2*  y   = eq_out + tp_off[i];
+    float*   v   = nv_out + tp_off[i];
+    size_t   lds = 0;
+    tp_args  ta;
+    int      rc  = make_tp_args(y, pl->tp_subc, v, pl->tp_subc, pl->tp_subc, pl->args.nof_re / pl->tp_subc, ta, lds);
+    demap_item di;
+    if (rc == SRS_AMD_OK) {
+      rc = make_demap_item(dem->demapper, pl->qm, items[i].d_llrs, reinterpret_cast<const float*>(y), v,
+                           pl->args.nof_re, pl->sym_counts, dem->d_jump, pl->c_init, di);
+    }
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+    std::memcpy(dem->stage.at<tp_args>(o_tp + sizeof(tp_args) * k), &ta, sizeof(ta));
+    std::memcpy(dem->stage.at<demap_item>(o_dm + sizeof(demap_item) * k), &di, sizeof(di));
+    tp_rows = std::max(tp_rows, ta.nof_rows);
+    tp_syms = std::max(tp_syms, pl->args.nof_re);
+    tp_lds  = std::max(tp_lds, lds);
+    ++k;
+  }
   auto* d = dem->slot_items.as<uint8_t>();
   e       = dem->stage.upload(d, total, s);
   for (const group& g : groups) {
@@ -331,6 +384,14 @@ int srs_amd::pusch_demodulate_slot_fused(::srs_amd_pusch_demodulator* dem,
     }
     const eq_items m{reinterpret_cast<const eq_item*>(d), reinterpret_cast<const uint32_t*>(d + o_ids) + g.first};
     e = launch_pusch_equalize_fused_items(m, g.count, g.P, g.L, g.mmse, g.max_blocks, s);
+  }
+  if (e == hipSuccess && n_tp != 0) {
+    e = launch_transform_deprecode_items(reinterpret_cast<const tp_args*>(d + o_tp), static_cast<uint32_t>(n_tp),
+                                         tp_rows, tp_lds, s);
+  }
+  if (e == hipSuccess && n_tp != 0) {
+    e = launch_demap_descramble_items(reinterpret_cast<const demap_item*>(d + o_dm), static_cast<uint32_t>(n_tp),
+                                      tp_syms, s);
   }
   const hipError_t done = scope.close();
   e                     = e != hipSuccess ? e : done;

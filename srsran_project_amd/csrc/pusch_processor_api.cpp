@@ -44,6 +44,7 @@ struct srs_amd_pusch_processor {
   pinned_stage                   stage2; // CSI part 2 sizes of a batch
   pinned_stage                   stage3; // slot form: UCI descriptors (demultiplexer, decoders, field masks)
   device_buffer                  uci_items, uci_cbs;
+  stream_fan                     fan; // slot form: the UCI decoders beside the UL-SCH decoder
   size_t                         uci_masks_offset = 0; // of the fused group's per-PDU UCI field masks in uci_items
   std::mutex                     mtx;
   bool                           fuse = true; // SRSRAN_AMD_PUSCH_FUSED=0: always expand the estimates
@@ -539,17 +540,23 @@ int fused_uci(srs_amd_pusch_processor* proc, const srs_amd_pusch_slot_pdu* pdus,
   if (e == hipSuccess) {
     e = launch_ulsch_demux_items(reinterpret_cast<const demux_args*>(d), static_cast<uint32_t>(dx.size()), max_re, s);
   }
+  // the UCI decoders depend only on the demultiplexer: on a helper stream beside the UL-SCH decoder (joined by the
+  // caller before the result kernel)
+  if (e == hipSuccess) {
+    e = proc->fan.begin(s, 2);
+  }
+  const hipStream_t hs = proc->fan.stream(s, 0);
   if (e == hipSuccess) {
     e = launch_uci_short_items(reinterpret_cast<const uci_short_args*>(d + o_sh),
-                               static_cast<uint32_t>(up.shorts.size()), s);
+                               static_cast<uint32_t>(up.shorts.size()), hs);
   }
   if (e == hipSuccess) {
     e = launch_polar_decode_items(reinterpret_cast<const polar_args*>(d + o_po),
-                                  static_cast<uint32_t>(up.polars.size()), s);
+                                  static_cast<uint32_t>(up.polars.size()), hs);
   }
   if (e == hipSuccess) {
     e = launch_uci_polar_finish_items(reinterpret_cast<const uci_polar_args*>(d + o_fi),
-                                      static_cast<uint32_t>(up.finishes.size()), s);
+                                      static_cast<uint32_t>(up.finishes.size()), hs);
   }
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH slot UCI launches");
 }
@@ -881,12 +888,12 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
       return fail(SRS_AMD_EINVAL, "PDU %u: invalid slot %u of numerology %u", i, pdus[i].slot_index,
                   pdus[i].numerology);
     }
-    // HARQ-ACK / CSI part 1 on the UL-SCH join the group (slot-form demultiplexer and UCI decoders); CSI part 2
+    // HARQ-ACK / CSI part 1 on the UL-SCH and DFT-s-OFDM PDUs join the group (slot-form demultiplexer and UCI
+    // decoders; the equalizer's symbols through the transform deprecoder); CSI part 2
     // (its sizes come from the decoded CSI part 1) and UCI-only PDUs take the batch chain
     // HARQ processes with a soft buffer (new data or retransmission) join it too (the slot decoder's HARQ rows,
     // early-stop decoding)
     const bool f = proc->fuse && pl->fusable && P <= STATS_STRIDE && pl->has_sch && !pl->csi2 &&
-                   pl->pdu.transform_precoding == 0 &&
                    (pdus[i].d_soft == nullptr ? pl->dec_cfg.new_data != 0 : pl->dec_cfg.use_early_stop != 0);
     (f ? fused : others).push_back(i);
   }
@@ -994,7 +1001,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
   if (e != hipSuccess) {
     return hip_fail(e, "PUSCH processor slot scratch");
   }
-  call_scope scope(proc->order, nullptr, s);
+  call_scope scope(proc->order, &proc->fan, s);
   // port measurements of fused PDU k at st + k * STATS_STRIDE, or straight in the caller's buffer at its PDU index
   auto*      st   = out_stats != nullptr ? out_stats : proc->stats.as<srs_amd_chest_port_stats>();
   auto*      llrs = proc->llrs.as<int8_t>();
@@ -1050,6 +1057,11 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
                             any_harq ? harq.data() : nullptr);
   if (rc != SRS_AMD_OK) {
     return rc;
+  }
+  // the UCI decoders' helper stream rejoins (statuses read by the result kernel)
+  e = proc->fan.end(s);
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUSCH slot UCI stream join");
   }
   // 2d. per-PDU results (decoder result + CSI from the PDU's own port measurements)
   for (uint32_t k = 0; k != n; ++k) {

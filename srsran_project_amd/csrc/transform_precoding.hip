@@ -36,8 +36,11 @@ __device__ __forceinline__ bool valid_nv(float v)
 
 } // namespace
 
-__global__ __launch_bounds__(TP_THREADS) void transform_deprecode_kernel(tp_args a)
+// MULTI: one argument block per PDU (items[blockIdx.y], its own M), the PUSCH processor's slot form
+template <bool MULTI>
+__global__ __launch_bounds__(TP_THREADS) void transform_deprecode_kernel(tp_args own, const tp_args* items)
 {
+  const tp_args& a = MULTI ? items[blockIdx.y] : own;
   extern __shared__ float2 lds[];
   const uint32_t M = a.M, M1 = a.M1, M2 = a.M2;
   float2*        x  = lds;     // [M] input symbol
@@ -129,7 +132,19 @@ hipError_t launch_transform_deprecode(const tp_args& a, hipStream_t stream)
   }
   const uint32_t grid = a.nof_rows < 65535u ? a.nof_rows : 65535u;
   const size_t   lds  = (2 * a.M + a.M1 + a.M2) * sizeof(float2); // <= 53 KiB (M <= 3300)
-  hipLaunchKernelGGL(transform_deprecode_kernel, dim3(grid), dim3(TP_THREADS), lds, stream, a);
+  hipLaunchKernelGGL(transform_deprecode_kernel<false>, dim3(grid), dim3(TP_THREADS), lds, stream, a, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_transform_deprecode_items(const tp_args* items, uint32_t n, uint32_t max_rows, size_t lds_bytes,
+                                            hipStream_t stream)
+{
+  if (n == 0 || max_rows == 0) {
+    return hipSuccess;
+  }
+  const uint32_t grid = max_rows < 65535u ? max_rows : 65535u;
+  hipLaunchKernelGGL(transform_deprecode_kernel<true>, dim3(grid, n), dim3(TP_THREADS), lds_bytes, stream, tp_args{},
+                     items);
   return hipGetLastError();
 }
 

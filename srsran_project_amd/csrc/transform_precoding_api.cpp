@@ -195,3 +195,24 @@ int srs_amd_transform_deprecode_noise(srs_amd_transform_precoder* tp, float* out
 }
 
 } // extern "C"
+
+int srs_amd::make_tp_args(float2* symbols, uint64_t sym_stride, float* noise, uint64_t nv_stride, uint32_t nof_subc,
+                          uint32_t nof_rows, tp_args& a, size_t& lds)
+{
+  int rc = check_size(nof_subc);
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  a            = tp_args{};
+  a.symbols    = symbols;
+  a.sym_stride = sym_stride;
+  a.noise      = noise;
+  a.nv_stride  = nv_stride;
+  a.M          = nof_subc;
+  a.M1         = factor_of(nof_subc);
+  a.M2         = nof_subc / a.M1;
+  a.nof_rows   = nof_rows;
+  a.scale      = 1.0f / std::sqrt(static_cast<float>(nof_subc)); // transform_precoder_dft_impl.cpp:45
+  lds          = (2 * a.M + a.M1 + a.M2) * sizeof(float2);
+  return SRS_AMD_OK;
+}

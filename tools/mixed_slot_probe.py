@@ -41,9 +41,9 @@ def timed(label, slot, reps=5):
 
 soft = {i: pl.ul_slot.soft[i] for i in range(len(pl.ul))}
 full = [(pp, c, soft[i]) if soft[i] is not None else (pp, c) for i, (pp, c) in enumerate(pl.ul)]
-if only is None:
+if only in (None, "all"):
     timed("all", amd.PuschSlot(full))
-for kind in ("data", "uci", "harq", "tp") if only is None else (only,):
+for kind in ("data", "uci", "harq", "tp") if only is None else (() if only == "all" else (only,)):
     sub = [x for x, k in zip(full, pl.kinds) if k == kind]
     if sub:
         timed(kind, amd.PuschSlot(sub))
