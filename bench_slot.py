@@ -130,6 +130,7 @@ def run_sch_slot(args, dist, world, rank, dev, timed):
         },
         "step_event_ms": step_ms,
         "pusch_pdu_kinds": {k: pl.kinds.count(k) for k in sorted(set(pl.kinds))},
+        "pusch_tb_ok_fraction_by_kind": pl.ok_by_kind,
         "pusch_tb_ok_fraction": ok,
         "pusch_tbs_equal_sent": tb_equal,
         "per_ue_launches": per_ue,
@@ -413,9 +414,12 @@ class SlotPipeline:
         res = amd.pusch_processor.parse_results(self.res_ul.cpu().numpy())
         rx, tx = self.tb_rx.cpu().numpy(), self.tb_ul.cpu().numpy()
         ok = []
-        for (pp, _), r, off, toff in zip(self.ul, res, self.ul_slot.offsets, self.ul_tb_off):
+        self.ok_by_kind = {}
+        for (pp, _), r, off, toff, k in zip(self.ul, res, self.ul_slot.offsets, self.ul_tb_off, self.kinds):
             n = pp.tb_bytes
             ok.append(bool(r.data.tb_crc_ok) and np.array_equal(rx[off:off + n], tx[toff:toff + n]))
+            self.ok_by_kind.setdefault(k, []).append(ok[-1])
+        self.ok_by_kind = {k: float(np.mean(v)) for k, v in self.ok_by_kind.items()}
         its = sum(r.data.ldpc_iterations_sum for r in res) / max(1, sum(r.data.nof_codeblocks_total for r in res))
         return float(np.mean(ok)), float(its)
 
@@ -459,6 +463,7 @@ def run_slot_pipeline(args, dist, world, rank, dev, timed):
         },
         "step_event_ms": step_ms,
         "pusch_pdu_kinds": {k: pl.kinds.count(k) for k in sorted(set(pl.kinds))},
+        "pusch_tb_ok_fraction_by_kind": pl.ok_by_kind,
         "pusch_tb_ok_fraction": ok,
         "pusch_mean_ldpc_iterations": its,
     }
