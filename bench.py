@@ -87,6 +87,9 @@ def parse():
                         "(configs[3]: PDSCH 2 layers x 2 ports, PUSCH 2 layers x 2 rx, reference-pinned ZF)")
     p.add_argument("--ul-layers", type=int, default=4, choices=[1, 2, 3, 4],
                    help="pipeline: PUSCH layers (4: MMSE 4x4, parity unpinned; 2: the reference-pinned ZF 2x4)")
+    p.add_argument("--chest-td", default="average", choices=["average", "interpolate"],
+                   help="pipeline: PUSCH DM-RS estimator time-domain strategy (average: the reference app's default, "
+                        "du_low_config.h:68)")
     p.add_argument("--ingest", action="store_true",
                    help="pipeline, N > 1: rank 0 holds all cells' slot inputs; RCCL scatter / gather every step")
     p.add_argument("--no-probe", action="store_true",

@@ -13,7 +13,8 @@ Per slot (= one cell; `--slots-pipeline` cells per step and rank, all resident i
          baseband -> OFDM demodulator -> pusch_processor (the C-ABI PUSCH processor:
          DM-RS estimator -> demodulator -> UL-SCH decoder with CRC early stop), configured as
          the reference pusch_processor_impl (DM-RS scaling from the CDM groups, Nref from
-         tbs_lbrm_default, ZF, filter / interpolate / CFO compensation).
+         tbs_lbrm_default, ZF, filter FD smoothing, average TD strategy (the reference app's default), CFO
+         compensation).
 The PUSCH input is a UE transmission synthesised before the timed region through a
 fixed UL_LAYERS x 4 MIMO channel plus AWGN; every run checks the decoded TBs against
 what the UE sent. A step processes every slot of the batch through both chains;
@@ -24,6 +25,7 @@ data-path collective). With `--ingest`, rank 0 also holds the slot inputs of all
 cells and fans them out / gathers the decoded TBs over RCCL every step
 (srsran_project_amd/cell_fanout.py); that time is reported separately.
 """
+import os
 import sys
 import time
 
@@ -39,6 +41,10 @@ DL_START, DL_NSYM = 1, 13
 UL_START, UL_NSYM = 0, 14
 RNTI, N_ID, SLOT = 0x4601, 500, 0
 SNR_DB = 35.0
+# DM-RS estimator time-domain strategy: average over the DM-RS symbols, the reference application's default
+# (du_low_config.h:68 pusch_channel_estimator_td_strategy = "average" -> upper_phy_factories.cpp:596-600);
+# --chest-td interpolate selects the per-symbol estimates with linear interpolation in time
+UL_TD = {"interpolate": 0, "average": 1}
 # near the decoding threshold (tools/snr_sweep.py, mean LDPC iterations ~4): per PUSCH layer count
 LOW_SNR_DB = {(2, 4): 23.8, (4, 4): 32.0}  # (PUSCH layers, rx ports)
 LDPC_ITERS = 6
@@ -64,7 +70,8 @@ def shape_kw(args):
     dl_l, dl_p, ul_l, ul_p = MIMO[getattr(args, "mimo", "4x4")]
     if getattr(args, "mimo", "4x4") == "4x4":
         ul_l = args.ul_layers
-    return dict(dl_layers=dl_l, dl_ports=dl_p, ul_layers=ul_l, ul_ports=ul_p)
+    return dict(dl_layers=dl_l, dl_ports=dl_p, ul_layers=ul_l, ul_ports=ul_p,
+                ul_td=getattr(args, "chest_td", "average"))
 
 
 def dl_weights(layers=DL_LAYERS, ports=DL_PORTS):
@@ -107,7 +114,7 @@ def chain_streams(torch, dev):
 
 class Pipeline:
     def __init__(self, slots, dev, iters=LDPC_ITERS, snr_db=SNR_DB, ul_layers=UL_LAYERS, seed=0, ul_equalizer=None,
-                 keep_estimates=False, dl_layers=DL_LAYERS, dl_ports=DL_PORTS, ul_ports=UL_PORTS):
+                 keep_estimates=False, dl_layers=DL_LAYERS, dl_ports=DL_PORTS, ul_ports=UL_PORTS, ul_td="average"):
         import torch
 
         import srsran_project_amd as amd
@@ -118,6 +125,7 @@ class Pipeline:
         assert dl_layers <= dl_ports and ul_layers <= ul_ports
         # the reference-pinned ZF for two layers, MMSE (parity unpinned) for four unless asked otherwise
         self.ul_equalizer = ul_equalizer or ("zf" if ul_layers <= 2 else UL_EQ)
+        self.ul_td = UL_TD[ul_td]
         self.ul_stream = None
         self._capturing = False
         d = dev.index
@@ -145,7 +153,7 @@ class Pipeline:
         self.ofdm_dem = amd.OfdmSlotDemodulator(
             amd.OfdmDemodulatorConfiguration(MU, NPRB, NFFT, 0, 1.0, 3.5e9, 0), device=d)
         self.proc = amd.PuschProcessor(amd.PuschProcessorConfig(
-            dec_nof_iterations=iters, dec_enable_early_stop=True, fd_smoothing=2, td_interpolation=0,
+            dec_nof_iterations=iters, dec_enable_early_stop=True, fd_smoothing=2, td_interpolation=self.ul_td,
             compensate_cfo=True, equalizer=int(getattr(amd.ChannelEqualizerAlgorithmType, self.ul_equalizer))),
             device=d)
         self.pdu_ul = ul_pdu(amd, ul_layers, self.tbs_ul, ul_ports)
@@ -228,7 +236,8 @@ class Pipeline:
             self.ev_join = [t.cuda.Event(), t.cuda.Event()]
         # under HIP-graph capture the PDSCH chain stays on the capturing stream (a capture whose origin stream holds
         # only the fork / join events crashed the capture); the replayed graph's placement is the runtime's
-        dl = stream if self._capturing else self.dl_stream
+        # (SRSRAN_AMD_GRAPH_FORK=1 captures the forked form anyway: the probe that records the capture's HIP error)
+        dl = stream if self._capturing and os.environ.get("SRSRAN_AMD_GRAPH_FORK") != "1" else self.dl_stream
         self.ev_fork.record(stream)
         if dl is not stream:
             dl.wait_event(self.ev_fork)
@@ -364,7 +373,8 @@ def chain_config(pl, choice="auto"):
                           dl_bg=pl.plan_dl.base_graph, dl_weights=dl_weights(pl.dl_layers, pl.dl_ports),
                           dl_dmrs_amplitude=DMRS_AMP, ul_layers=pl.ul_layers, ul_ports=pl.ul_ports, ul_start=UL_START, ul_nsym=UL_NSYM,
                           ul_tbs=pl.tbs_ul, ul_bg=pl.plan_ul.base_graph, ul_iterations=pl.iters,
-                          ul_target_code_rate=RATE, choice={"generic": 0, "avx2": 1, "auto": 2}[choice])
+                          ul_target_code_rate=RATE, choice={"generic": 0, "avx2": 1, "auto": 2}[choice],
+                          ul_td=pl.ul_td)
 
 
 def latency_ms(dev, cells, steps=10, warmup=3, graph=False, **shape):
@@ -530,7 +540,8 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
                       "equalizer_parity": "pinned (reference ZF)" if (L <= 2 and pl.ul_equalizer == "zf") or L == 1
                       else "unpinned: the open reference asserts for this topology; fp64 solve within stated "
                            "tolerance (tests/test_equalizer_mimo_gpu.py)",
-                      "ldpc_max_iterations": pl.iters, "early_stop": True},
+                      "ldpc_max_iterations": pl.iters, "early_stop": True,
+                      "chest_td": {0: "interpolate", 1: "average"}[pl.ul_td]},
             "parallelism": ("cells sharded over ranks" + (", slot ingest scatter/gather over RCCL"
                                                            if ingest_ms is not None else "")) if world > 1
             else "single GPU",

@@ -19,7 +19,7 @@ class RefChainConfig(_c.Structure):
         [("dl_weights", _c.c_float * 32), ("dl_dmrs_amplitude", _c.c_float)] + \
         [(n, _c.c_uint32) for n in ("ul_layers", "ul_ports", "ul_start", "ul_nsym", "ul_tbs", "ul_bg",
                                     "ul_iterations")] + \
-        [("ul_target_code_rate", _c.c_float), ("choice", _c.c_int32)]
+        [("ul_target_code_rate", _c.c_float), ("choice", _c.c_int32), ("ul_td", _c.c_int32)]
 
 
 if REF is not None and hasattr(REF, "srs_ref_chain_run"):

@@ -60,6 +60,7 @@ struct srs_ref_chain_config {
   uint32_t ul_layers, ul_ports, ul_start, ul_nsym, ul_tbs, ul_bg, ul_iterations;
   float    ul_target_code_rate;
   int32_t  choice; // 0 generic, 1 avx2, 2 auto
+  int32_t  ul_td;  // estimator time-domain strategy: 0 interpolate, 1 average (the reference app's default)
 };
 
 } // extern "C"
@@ -185,7 +186,7 @@ struct chain {
           dft_processor::configuration{c.dft_size, dft_processor::direction::DIRECT});
       ofdm_dem = std::make_unique<ofdm_slot_demodulator_impl>(cfg, std::make_unique<ofdm_symbol_demodulator_impl>(common, cfg));
     }
-    pusch = make_pusch_processor(choice, c.nof_prb, c.ul_ports, c.ul_layers, c.ul_iterations, 0, 2, 0, true);
+    pusch = make_pusch_processor(choice, c.nof_prb, c.ul_ports, c.ul_layers, c.ul_iterations, 0, 2, c.ul_td, true);
     dl_samples.resize(ofdm_mod->get_slot_size(c.slot));
     tb_out.resize(c.ul_tbs / 8);
     // PDSCH encoder configuration (bench_pipeline.py: 273 PRB, the DL data REs)

@@ -27,6 +27,8 @@
 // of any radix-R float FFT, O(eps * log N) of the RMS (tests state the bound).
 #pragma once
 
+#include <type_traits>
+
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -225,6 +227,17 @@ __device__ __forceinline__ void twiddle_powers(cf w1, cf* w)
   }
 }
 
+// First-pass input held in registers: thread t's samples t + T r, r < K (plans whose first pass has N / R = T
+// butterflies, one per thread); passed as the engine's Load.
+template <int K>
+struct reg_input {
+  cf v[K];
+};
+template <class L>
+struct is_reg_input : std::false_type {};
+template <int K>
+struct is_reg_input<reg_input<K>> : std::true_type {};
+
 // Runs the passes Rs... over one N-point vector with T threads.
 //   load(i)       -> cf  : input sample i (first pass only)
 //   store(i, v)          : output sample i (last pass only)
@@ -241,7 +254,8 @@ struct stockham {
     return N / R / T;
   }
 
-  template <int Ns, int R, int... Rest, class Load, class Store>
+  // G: the workgroup may hold more than T threads; threads T.. only take part in the barriers
+  template <bool G, int Ns, int R, int... Rest, class Load, class Store>
   __device__ __forceinline__ static void pass(cf* lds, const cf* tw, Load& load, Store& store, const cf* wbase)
   {
     constexpr int  NB    = N / R;           // butterflies in this pass
@@ -249,7 +263,8 @@ struct stockham {
     constexpr bool FIRST = Ns == 1;
     constexpr bool LAST  = sizeof...(Rest) == 0;
     static_assert(NB % T == 0, "butterflies must divide evenly over the threads");
-    const int tid = threadIdx.x;
+    const int  tid = threadIdx.x;
+    const bool act = !G || tid < T;
 
     // prefetch the next pass's twiddle bases
     constexpr int R2   = LAST ? 1 : first_of<Rest..., 1>::value;
@@ -260,7 +275,7 @@ struct stockham {
 #pragma unroll
       for (int b = 0; b < PER2; ++b) {
         const int j2 = tid + b * T;
-        wnext[b]     = tw[(j2 % Ns2) * (N / (Ns2 * R2))];
+        wnext[b]     = act ? tw[(j2 % Ns2) * (N / (Ns2 * R2))] : cf{1, 0};
       }
     }
 
@@ -270,7 +285,14 @@ struct stockham {
       const int j = tid + b * T;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        v[b][r] = FIRST ? load(j + r * NB) : lds[pad(j + r * NB)];
+        if constexpr (FIRST && is_reg_input<Load>::value) {
+          static_assert(PER == 1, "register input needs one first-pass butterfly per thread");
+          v[b][r] = load.v[r];
+        } else if constexpr (FIRST) {
+          v[b][r] = act ? load(j + r * NB) : cf{0, 0};
+        } else {
+          v[b][r] = act ? lds[pad(j + r * NB)] : cf{0, 0};
+        }
       }
     }
 #pragma unroll
@@ -295,7 +317,9 @@ struct stockham {
         const int j = tid + b * T; // j < Ns here
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          store(j + r * Ns, v[b][r]);
+          if (act) {
+            store(j + r * Ns, v[b][r]);
+          }
         }
       }
     } else {
@@ -309,18 +333,26 @@ struct stockham {
         const int base = (j / Ns) * Ns * R + k;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          lds[pad(base + r * Ns)] = v[b][r];
+          if (act) {
+            lds[pad(base + r * Ns)] = v[b][r];
+          }
         }
       }
       __syncthreads();
-      pass<Ns * R, Rest...>(lds, tw, load, store, wnext);
+      pass<G, Ns * R, Rest...>(lds, tw, load, store, wnext);
     }
   }
 
   template <class Load, class Store>
   __device__ __forceinline__ static void run(cf* lds, const cf* tw, Load& load, Store& store)
   {
-    pass<1, Rs...>(lds, tw, load, store, nullptr);
+    pass<false, 1, Rs...>(lds, tw, load, store, nullptr);
+  }
+  // the same transform in a workgroup of more than T threads (all of them reach this call)
+  template <class Load, class Store>
+  __device__ __forceinline__ static void run_guarded(cf* lds, const cf* tw, Load& load, Store& store)
+  {
+    pass<true, 1, Rs...>(lds, tw, load, store, nullptr);
   }
 };
 

@@ -19,8 +19,14 @@ constexpr int PRBS_NJUMP = 24; // jumps by 2^k, k < 24 (sequences up to 2^24 - 1
 constexpr int PRBS_RADIX_DIGITS = 6;                        // 4-bit digits of a jump (24 bits)
 constexpr int PRBS_RADIX_OFF    = 2 * PRBS_NJUMP * 31;      // start of the radix-16 matrices
 
+// Nibble tables of the binary matrices A^(2^k), k = PRBS_NIB_K0 .. PRBS_NIB_K0 + PRBS_NIB_NK - 1: entry [q][v] =
+// M x (v << 4 q), so a product is eight table reads and seven XORs (gf2_apply_nib) instead of 31 masked XORs.
+constexpr int PRBS_NIB_K0  = 5;
+constexpr int PRBS_NIB_NK  = 7;
+constexpr int PRBS_NIB_OFF = PRBS_RADIX_OFF + 2 * PRBS_RADIX_DIGITS * 16 * 31;
+
 // [2][PRBS_NJUMP][31] jump matrices A^(2^k) (columns), x1 then x2, followed by the radix-16 matrices
-// [2][PRBS_RADIX_DIGITS][16][31] A^(d 16^k) (d = 0 unused).
+// [2][PRBS_RADIX_DIGITS][16][31] A^(d 16^k) (d = 0 unused) and the nibble tables [2][PRBS_NIB_NK][8][16].
 std::vector<uint32_t> gold_jump_tables();
 
 // state' = M * state over GF(2), M given by its 31 columns.
@@ -106,6 +112,42 @@ __device__ __forceinline__ void gold_state_wave(const uint32_t* jump, uint32_t c
 {
   gold_state(jump, __builtin_amdgcn_readfirstlane(c_init), __builtin_amdgcn_readfirstlane(n_wave), x1, x2);
   gold_advance16(jump, off, x1, x2);
+}
+
+// state' = A^(2^k) x state (k in [PRBS_NIB_K0, PRBS_NIB_K0 + PRBS_NIB_NK)) by its nibble table.
+__device__ __forceinline__ uint32_t gf2_apply_nib(const uint32_t* jump, int which, int k, uint32_t state)
+{
+  const uint32_t* t = jump + PRBS_NIB_OFF + ((which * PRBS_NIB_NK + (k - PRBS_NIB_K0)) * 8) * 16;
+  uint32_t        r = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    r ^= t[q * 16 + ((state >> (4 * q)) & 15u)];
+  }
+  return r;
+}
+
+// States whose next output is c(n_wave + 32 lane), n_wave the same for every lane of the wave: the jump to n_wave on
+// the scalar unit, then the lane's offset by doubling rounds over bits 0..5 of lane with the nibble tables of
+// A^(32 2^k) (eight reads of one 64-byte row per product, the same matrix in every lane).
+__device__ __forceinline__ void gold_state_lanes(const uint32_t* jump, uint32_t c_init, uint32_t n_wave, uint32_t lane,
+                                                 uint32_t& x1, uint32_t& x2)
+{
+  gold_state(jump, __builtin_amdgcn_readfirstlane(c_init), __builtin_amdgcn_readfirstlane(n_wave), x1, x2);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint32_t y1 = gf2_apply_nib(jump, 0, 5 + k, x1);
+    const uint32_t y2 = gf2_apply_nib(jump, 1, 5 + k, x2);
+    const bool     b  = ((lane >> k) & 1u) != 0;
+    x1                = b ? y1 : x1;
+    x2                = b ? y2 : x2;
+  }
+}
+
+// States advanced by 2^k positions (k in [PRBS_NIB_K0, PRBS_NIB_K0 + PRBS_NIB_NK), the same k in every lane).
+__device__ __forceinline__ void gold_advance_pow2(const uint32_t* jump, int k, uint32_t& x1, uint32_t& x2)
+{
+  x1 = gf2_apply_nib(jump, 0, k, x1);
+  x2 = gf2_apply_nib(jump, 1, k, x2);
 }
 
 } // namespace srs_amd

@@ -121,7 +121,7 @@ uint32_t gf2_apply_host(const uint32_t* cols, uint32_t s)
 
 std::vector<uint32_t> srs_amd::gold_jump_tables()
 {
-  std::vector<uint32_t> t(PRBS_RADIX_OFF + 2 * PRBS_RADIX_DIGITS * 16 * 31, 0u);
+  std::vector<uint32_t> t(PRBS_NIB_OFF + 2 * PRBS_NIB_NK * 8 * 16, 0u);
   for (int which = 0; which < 2; ++which) {
     uint32_t* m0 = t.data() + (which * PRBS_NJUMP) * 31;
     for (int j = 0; j < 31; ++j) {
@@ -144,6 +144,16 @@ std::vector<uint32_t> srs_amd::gold_jump_tables()
       for (int d = 2; d < 16; ++d) {
         for (int j = 0; j < 31; ++j) {
           row[d * 31 + j] = gf2_apply_host(row + (d - 1) * 31, base[j]);
+        }
+      }
+    }
+    // nibble tables of A^(2^k): [q][v] = A^(2^k) (v << 4 q) (the state has 31 bits: nibble 7 holds bits 28..30)
+    for (int k = 0; k < PRBS_NIB_NK; ++k) {
+      const uint32_t* m   = t.data() + (which * PRBS_NJUMP + PRBS_NIB_K0 + k) * 31;
+      uint32_t*       tab = t.data() + PRBS_NIB_OFF + ((which * PRBS_NIB_NK + k) * 8) * 16;
+      for (int q = 0; q < 8; ++q) {
+        for (uint32_t v = 0; v < 16; ++v) {
+          tab[q * 16 + v] = gf2_apply_host(m, (v << (4 * q)) & 0x7fffffffu);
         }
       }
     }

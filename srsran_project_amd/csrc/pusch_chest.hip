@@ -1,25 +1,26 @@
 // pusch_chest.hip -- MI355X PUSCH DM-RS channel estimator (dmrs_pusch_estimator_impl
 // + port_channel_estimator_average_impl, DM-RS type 1, one hop).
 //
-// Six launches per batch of grids (the last only when the per-RE estimates are wanted):
-//   chest_seq_kernel     one workgroup: the DM-RS Gold words of the batch (jump-ahead) for the kernels below.
-//   chest_cfo_kernel     one workgroup per (grid, rx port): EPRE and the CFO from the first two DM-RS symbols.
-//   chest_slice_kernel   one 256-thread workgroup per (grid, rx port, slice = layer x LSE symbol), so the
-//                        slices of a port run concurrently. DM-RS Gold words into LDS (jump-ahead);
+// Two launches per batch of grids (a third when the per-RE estimates are wanted):
+//   chest_pilot_kernel   one 256-thread workgroup per (grid, rx port, slice = layer x LSE symbol), so the
+//                        slices of a port run concurrently: the DM-RS Gold words into LDS (jump-ahead, one wave
+//                        per DM-RS symbol); the port's CFO from the first two DM-RS symbols over every layer of
+//                        every CDM group (computed by each slice of the port, the same value in each);
 //                        LSE (rx * conj(pilot)), CFO compensation and time accumulation, CDM
 //                        pair averaging (lane shuffle), scaling, FD smoothing in LDS (mean, or virtual
 //                        pilots + raised-cosine FIR), the slice's RSRP share, linear interpolation to
-//                        every RE of the allocation (port_channel_estimator_average_impl.cpp:130-506).
-//   chest_ta_kernel<N>   one workgroup per (grid, port, slice): the N-point IDFT of the slice's smoothed
-//                        pilots with the fused Stockham engine, |.|^2 into the slice's correlation row
-//                        (time_alignment_estimator_dft_impl.cpp:122-200).
-//   chest_stats_kernel   one workgroup per (grid, port): noise energy per CDM group, the correlations
+//                        every RE of the allocation (port_channel_estimator_average_impl.cpp:130-506), and
+//                        the slice's time-alignment IDFT of its smoothed pilots (fused Stockham engine,
+//                        |.|^2 into the slice's correlation row, time_alignment_estimator_dft_impl.cpp:122-200).
+//   chest_stats_kernel   one workgroup per (grid, port): EPRE and the noise energy per CDM group from the
+//                        smoothed pilots of every slice (estimate_noise, :594-690), the correlations
 //                        summed, peak search and quadratic refinement (:248-310), and the per-port
 //                        measurements (noise variance, EPRE, RSRP, SNR, CFO).
 //   chest_expand_kernel  one thread per (subcarrier, port, layer), every symbol: the time-domain strategy
 //                        (average or interpolation between DM-RS symbols), bf16
 //                        rounding and the CFO phase of the symbol -- the only
 //                        HBM-heavy step (4 bytes per RE x layer x port written).
+// (r04 ran the Gold words, the CFO, the slices and the IDFTs as four launches: 87 us of a 64-cell step.)
 // Complex products follow the reference's AVX2+FMA srsran_simd_cf_prod
 // (re = fma(a.re, b.re, -a.im b.im), im = fma(a.re, b.im, a.im b.re)); sums
 // are reassociated by the reductions (float tolerance).
@@ -185,20 +186,39 @@ __device__ __forceinline__ uint32_t dmrs_nof_words(const chest_args& a, uint32_t
   return (bit_first + 2 * a.npil + 31) / 32 - w_first;
 }
 
-// One workgroup: the DM-RS Gold words of the batch (jump-ahead, one word per thread) into a.dmrs_seq.
-template <bool MULTI>
-__global__ __launch_bounds__(CS_THREADS) void chest_seq_kernel(chest_args a_in, chest_items items)
+// The DM-RS words of the item into LDS, one wave per DM-RS symbol: the wave jumps to the allocation's first word
+// once (uniform c_init and position), each lane then to its own words w = lane and lane + 64 (gold_state_lanes;
+// nwords <= 106).  Workgroup (0, 0) of the item also keeps them in a.dmrs_seq for the
+// statistics kernel.  Returns the bit offset of the first allocated pilot in word 0.
+__device__ __forceinline__ uint32_t dmrs_words_gen(const chest_args& a, uint32_t (*seq)[CH_SEQWORDS])
 {
-  const chest_args& a = item_args<MULTI>(a_in, items);
   uint32_t       w_first;
   const uint32_t nwords = dmrs_nof_words(a, w_first);
-  for (uint32_t i = threadIdx.x; i < nwords * a.nds; i += CS_THREADS) {
-    const uint32_t d = i / nwords, w = i % nwords;
-    a.dmrs_seq[d * CH_SEQWORDS + w] = gold_word(a.jump, a.c_init[d], 32 * (w_first + w));
+  const uint32_t d      = threadIdx.x / 64;
+  const uint32_t lane   = threadIdx.x % 64;
+  const bool     keep   = blockIdx.x == 0 && blockIdx.y == 0;
+  if (d < a.nds) {
+    uint32_t x1, x2;
+    gold_state_lanes(a.jump, a.c_init[d], 32 * w_first, lane, x1, x2);
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+      const uint32_t w = lane + 64 * h;
+      if (w < nwords) {
+        const uint32_t word = gold_emit32(x1, x2);
+        seq[d][w]           = word;
+        if (keep) {
+          a.dmrs_seq[d * CH_SEQWORDS + w] = word;
+        }
+      }
+      if (h == 0) {
+        gold_advance_pow2(a.jump, 11, x1, x2); // + 64 words
+      }
+    }
   }
+  return 12u * a.prb_lo - 32 * w_first;
 }
 
-// The batch's DM-RS words into LDS; returns the bit offset of the first allocated pilot in word 0.
+// The item's DM-RS words from a.dmrs_seq into LDS (statistics kernel).
 __device__ __forceinline__ uint32_t dmrs_words(const chest_args& a, uint32_t (*seq)[CH_SEQWORDS])
 {
   uint32_t       w_first;
@@ -210,120 +230,79 @@ __device__ __forceinline__ uint32_t dmrs_words(const chest_args& a, uint32_t (*s
   return 12u * a.prb_lo - 32 * w_first;
 }
 
-// 1,024 threads (16 waves) per (grid, rx port), two pilots per thread: with 256 threads and seven pilots each the
-// 256-workgroup launch ran 4 waves per CU, every thread waiting out its load chains (PMC: 0.75 of wave time
-// waiting, VALU busy 0.09)
-constexpr int CFO_THREADS = 1024;
-constexpr int CFO_PPT     = CH_MAXPIL / CFO_THREADS;
-
-// One workgroup per (grid, rx port): EPRE over every received DM-RS RE and the CFO from the first two DM-RS
-// symbols over every layer of every CDM group (preprocess_pilots_and_estimate_cfo, :390-445), for the
-// slice workgroups of the port.
-template <bool MULTI>
-__global__ __launch_bounds__(CFO_THREADS) void chest_cfo_kernel(chest_args a_in, chest_items items)
+// Time alignment of one slice: the N-point IDFT of its smoothed pilots with the fused Stockham engine and |.|^2
+// into the slice's correlation row (time_alignment_estimator_dft_impl.cpp:122-200).
+// N <= 512 (npil <= 412): plan<N> on the workgroup's first plan<N>::T threads, input from the pilots in LDS,
+// work area in the unused upper half of the pilot buffer.
+template <int N>
+__device__ __forceinline__ void slice_ta_small(const chest_args& a, const float2* pil, dft::cf* lds, float* corr)
 {
-  const chest_args& a = item_args<MULTI>(a_in, items);
-  if (MULTI && blockIdx.x >= a.nof_ports) {
-    return; // slot form: the launch covers the largest item
-  }
-  __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
-  __shared__ float    red[4 * 16];
-  const uint32_t      gp   = blockIdx.x;
-  const uint32_t      grid = gp / a.nof_ports;
-  const uint32_t      port = gp % a.nof_ports;
-  const uint32_t      tid  = threadIdx.x;
+  using dft::cf;
+  const int npil = static_cast<int>(a.npil);
+  auto      load = [&](int i) -> cf {
+    if (i < npil) {
+      const float2 v = pil[i];
+      return cf{v.x, v.y};
+    }
+    return cf{0, 0};
+  };
+  auto store = [&](int k, cf v) { corr[k] = v.x * v.x + v.y * v.y; };
+  static_assert(dft::plan<N>::T <= CS_THREADS, "IDFT plan wider than the slice workgroup");
+  dft::plan<N>::template engine<+1>::run_guarded(lds, reinterpret_cast<const cf*>(a.ta_tw), load, store);
+}
+// N = 1024 / 2048: 256-thread plans whose first pass takes the thread's own pilots m = tid + 256 r straight from
+// its registers x[r] (N / R_first = 256), work area the whole pilot buffer (after a barrier).
+using ta_plan_1024 = dft::stockham<1024, CS_THREADS, +1, 4, 4, 4, 4, 4>;
+using ta_plan_2048 = dft::stockham<2048, CS_THREADS, +1, 8, 8, 8, 4>;
+template <class Plan, int R>
+__device__ __forceinline__ void slice_ta_regs(const chest_args& a, const float2 (&x)[CS_PPT], dft::cf* lds,
+                                              float* corr)
+{
+  using dft::cf;
+  static_assert(R <= CS_PPT, "first radix beyond the thread's pilots");
   const uint32_t      npil = a.npil;
-  const int           nds  = static_cast<int>(a.nds);
-  const int           L    = static_cast<int>(a.L);
-  const uint32_t      bit0 = dmrs_words(a, seq);
-  const uint32_t*     gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc +
-                          12 * a.prb_lo;
-  auto rxv = [&](int gg, int d, uint32_t m) { return from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + gg]); };
-  float epre = 0;
+  dft::reg_input<R> load;
 #pragma unroll
-  for (int k = 0; k < CFO_PPT; ++k) {
-    const uint32_t m = tid + k * CFO_THREADS;
-    if (m < npil) {
-      // compile-time bounds (CDM groups of type 1, DM-RS symbols): every load of the thread is issued
-      // before the first is used
-#pragma unroll
-      for (int gg = 0; gg < 2; ++gg) {
-#pragma unroll
-        for (int d = 0; d < CH_MAXDMRS; ++d) {
-          if (gg < static_cast<int>(a.ncdm) && d < nds) {
-            const float2 u = rxv(gg, d, m);
-            epre           = __builtin_fmaf(u.x, u.x, __builtin_fmaf(u.y, u.y, epre));
-          }
-        }
-      }
-    }
+  for (int r = 0; r < R; ++r) {
+    load.v[r] = threadIdx.x + r * CS_THREADS < npil ? cf{x[r].x, x[r].y} : cf{0, 0};
   }
-  __syncthreads(); // seq ready
-  float4 acc = make_float4(0, 0, 0, 0); // (re, im) of CDM group 0, then 1
-  if (nds >= 2) {
-#pragma unroll
-    for (int k = 0; k < CFO_PPT; ++k) {
-      const uint32_t m = tid + k * CFO_THREADS;
-      if (m < npil) {
-#pragma unroll
-        for (int vv = 0; vv < CH_MAXL; ++vv) {
-          if (vv >= L) {
-            break;
-          }
-          const int    gg = vv / 2;
-          const float2 p0 = cmulc(rxv(gg, 0, m), pilot(a, seq, bit0, 0, vv, m));
-          const float2 p1 = cmulc(rxv(gg, 1, m), pilot(a, seq, bit0, 1, vv, m));
-          const float2 t  = cmulc(p1, p0);
-          if (gg == 0) {
-            acc.x += t.x;
-            acc.y += t.y;
-          } else {
-            acc.z += t.x;
-            acc.w += t.y;
-          }
-        }
-      }
-    }
-    acc = block_sum4(acc, red);
-  }
-  const float4 te = block_sum4(make_float4(epre, 0, 0, 0), red);
-  if (tid == 0) {
-    float* out = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
-    float  cfo = 0;
-    if (nds >= 2) {
-      const float de = a.epoch[a.dmrs_sym[1]] - a.epoch[a.dmrs_sym[0]];
-      cfo            = atan2f(acc.y, acc.x) / TWOPI_F / de;
-      if (a.ncdm > 1) {
-        cfo += atan2f(acc.w, acc.z) / TWOPI_F / de;
-      }
-      cfo /= static_cast<float>(a.ncdm);
-    }
-    out[0] = te.x;
-    out[3] = nds >= 2 ? 1.0f : 0.0f;
-    out[4] = cfo;
-  }
+  auto store = [&](int k, cf v) { corr[k] = v.x * v.x + v.y * v.y; };
+  Plan::run(lds, reinterpret_cast<const cf*>(a.ta_tw), load, store);
 }
 
+// Pilot buffer of the slice kernel: the FD filter's input, then the smoothed pilots, then the IDFT's work area.
+constexpr int CH_ENL = dft::lds_complex<2048>() > CH_MAXPIL + 2 * CH_MAXV ? dft::lds_complex<2048>()
+                                                                          : CH_MAXPIL + 2 * CH_MAXV;
+static_assert(1024 + dft::lds_complex<512>() <= CH_ENL, "small IDFT work area exceeds the pilot buffer");
+
 // One workgroup per (grid, rx port, slice = layer x LSE symbol): every slice of a port is estimated
-// concurrently, with the port's CFO from chest_cfo_kernel.  Per slice: LSE
-// (rx * conj(pilot)), CFO compensation and time accumulation, CDM pair averaging (lane shuffle), scaling, FD
-// smoothing in LDS (mean, or virtual pilots + raised-cosine FIR), the slice's RSRP share, linear
-// interpolation to every RE of the allocation (port_channel_estimator_average_impl.cpp:130-506).
+// concurrently.  The port's CFO from the first two DM-RS symbols over every layer of every CDM group
+// (preprocess_pilots_and_estimate_cfo, :390-445) is computed by each slice workgroup of the port (the same
+// operations in the same order, so the same value; slice 0 keeps it in acc for the statistics, expansion and
+// equalizer kernels).  Per slice: LSE (rx * conj(pilot)), CFO compensation and time accumulation, CDM pair
+// averaging (lane shuffle), scaling, FD smoothing in LDS (mean, or virtual pilots + raised-cosine FIR), the
+// slice's RSRP share, linear interpolation to every RE of the allocation
+// (port_channel_estimator_average_impl.cpp:130-506), the slice's time-alignment IDFT.
+// occupancy target of the pilot kernel (waves per SIMD; registers 512 / waves), a build-time tuning knob
+#ifndef SRS_AMD_CHEST_WAVES_PER_EU
+#define SRS_AMD_CHEST_WAVES_PER_EU 5
+#endif
 template <bool MULTI>
-__global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in, chest_items items)
+__global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(SRS_AMD_CHEST_WAVES_PER_EU))) void
+chest_pilot_kernel(chest_args a_in, chest_items items)
 {
   const chest_args& a = item_args<MULTI>(a_in, items);
   if (MULTI && (blockIdx.x >= a.nof_ports || blockIdx.y >= a.L * a.nof_lse)) {
     return;
   }
   __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
-  // one pilot buffer: the FD filter's input, then (after a barrier) the smoothed pilots the interpolation
-  // reads -- a second 16.6 KiB buffer held the workgroup at 35.5 KiB of LDS, four per CU (4 waves per SIMD)
-  __shared__ float2   enl_in[CH_MAXPIL + 2 * CH_MAXV];
+  // one pilot buffer: the FD filter's input, then (after a barrier) the smoothed pilots the interpolation and
+  // the IDFT read
+  __shared__ float2   enl_in[CH_ENL];
   float2* const       enl_out = enl_in;
   __shared__ float    red[4 * 16];
-  __shared__ int      s_has_cfo;
   __shared__ float2   s_rot[CH_MAXDMRS];
+  __shared__ int      s_has_cfo;
 
   const uint32_t gp    = blockIdx.x; // grid * nof_ports + port
   const uint32_t slice = blockIdx.y; // layer * nof_lse + LSE symbol
@@ -337,21 +316,96 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
   const int      s     = static_cast<int>(slice % a.nof_lse);
   const int      g     = v / 2;
 
-  const uint32_t  bit0  = dmrs_words(a, seq);
   const uint32_t* gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc +
                           12 * a.prb_lo;
   // received pilot m of CDM group gg in DM-RS symbol d (subcarrier 12 prb_lo + 2m + gg)
   auto rxv = [&](int gg, int d, uint32_t m) { return from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + gg]); };
-
-  if (tid < static_cast<uint32_t>(nds)) { // the port's CFO phases (chest_cfo_kernel)
-    const float* acc = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
-    s_rot[tid]       = (acc[3] != 0.0f && a.compensate_cfo) ? polar1(-TWOPI_F * a.epoch[a.dmrs_sym[tid]] * acc[4])
-                                                            : make_float2(1, 0);
-    if (tid == 0) {
-      s_has_cfo = acc[3] != 0.0f ? 1 : 0;
+  // The thread's pilots of both CDM groups in the first two DM-RS symbols, loaded before the Gold words are
+  // generated (their latency hides behind it); the CFO and the slice's LSE of those symbols read them here.
+  uint32_t r01[CS_PPT][2][2];
+#pragma unroll
+  for (int k = 0; k < CS_PPT; ++k) {
+    const uint32_t m = tid + k * CS_THREADS;
+#pragma unroll
+    for (int gg = 0; gg < 2; ++gg) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        r01[k][gg][d] = (m < npil && gg < static_cast<int>(a.ncdm) && d < nds)
+                            ? gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + gg]
+                            : 0u;
+      }
     }
   }
-  __syncthreads(); // seq, rotations ready
+  // pilot k of group gg (runtime) in DM-RS symbol d (runtime): the registers above for d < 2
+  auto rxk = [&](int k, int gg, int d, uint32_t m) {
+    if (d >= 2) {
+      return rxv(gg, d, m);
+    }
+    const uint32_t u0 = gg == 0 ? r01[k][0][0] : r01[k][1][0];
+    const uint32_t u1 = gg == 0 ? r01[k][0][1] : r01[k][1][1];
+    return from_cbf16(d == 0 ? u0 : u1);
+  };
+  const uint32_t bit0 = dmrs_words_gen(a, seq);
+  __syncthreads(); // seq ready
+
+  // The port's CFO: sum over the layers v of (rx_1 conj(p_1,v)) conj(rx_0 conj(p_0,v)).  The two layers of a CDM
+  // group differ in their pilots by w_f = -1 on odd indices in both symbols, which cancels in the product: the
+  // term of layer 2 gg is added once per layer of the group (as a loop over the layers adds it).
+  if (nds >= 2) {
+    float4 acc = make_float4(0, 0, 0, 0); // (re, im) of CDM group 0, then 1
+#pragma unroll
+    for (int k = 0; k < CS_PPT; ++k) {
+      const uint32_t m = tid + k * CS_THREADS;
+      if (m < npil) {
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int nl = min(2, L - 2 * gg); // layers of the group
+          if (nl <= 0) {
+            continue;
+          }
+          const float2 p0 = cmulc(from_cbf16(r01[k][gg][0]), pilot(a, seq, bit0, 0, 2 * gg, m));
+          const float2 p1 = cmulc(from_cbf16(r01[k][gg][1]), pilot(a, seq, bit0, 1, 2 * gg, m));
+          const float2 t  = cmulc(p1, p0);
+          for (int r = 0; r < nl; ++r) {
+            if (gg == 0) {
+              acc.x += t.x;
+              acc.y += t.y;
+            } else {
+              acc.z += t.x;
+              acc.w += t.y;
+            }
+          }
+        }
+      }
+    }
+    acc = block_sum4(acc, red);
+    if (tid == 0) {
+      const float de  = a.epoch[a.dmrs_sym[1]] - a.epoch[a.dmrs_sym[0]];
+      float       cfo = atan2f(acc.y, acc.x) / TWOPI_F / de;
+      if (a.ncdm > 1) {
+        cfo += atan2f(acc.w, acc.z) / TWOPI_F / de;
+      }
+      cfo /= static_cast<float>(a.ncdm);
+      for (int d = 0; d < nds; ++d) {
+        s_rot[d] = a.compensate_cfo ? polar1(-TWOPI_F * a.epoch[a.dmrs_sym[d]] * cfo) : make_float2(1, 0);
+      }
+      s_has_cfo = 1;
+      if (slice == 0) {
+        float* out = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
+        out[3]     = 1.0f;
+        out[4]     = cfo;
+      }
+    }
+  } else if (tid == 0) {
+    s_rot[0]  = make_float2(1, 0);
+    s_has_cfo = 0;
+    if (slice == 0) {
+      float* out = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
+      out[3]     = 0.0f;
+      out[4]     = 0.0f;
+    }
+  }
+  __syncthreads(); // rotations ready
   const bool  has_cfo  = s_has_cfo != 0;
   const bool  rotate   = has_cfo && a.compensate_cfo;
   const float total    = a.td == SRS_AMD_CHEST_TD_AVERAGE ? (1.0f / a.beta) / static_cast<float>(nds) : 1.0f / a.beta;
@@ -366,7 +420,7 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
     float2         y = make_float2(0, 0);
     if (m < npil) {
       if (a.td == SRS_AMD_CHEST_TD_AVERAGE) {
-        y = cmulc(rxv(g, 0, m), pilot(a, seq, bit0, 0, v, m));
+        y = cmulc(rxk(k, g, 0, m), pilot(a, seq, bit0, 0, v, m));
         if (rotate) {
           y = cmul(y, s_rot[0]);
         }
@@ -375,14 +429,14 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
           if (d >= nds) {
             break;
           }
-          float2 t = cmulc(rxv(g, d, m), pilot(a, seq, bit0, d, v, m));
+          float2 t = cmulc(rxk(k, g, d, m), pilot(a, seq, bit0, d, v, m));
           if (rotate) {
             t = cmul(t, s_rot[d]);
           }
           y = cadd(y, t);
         }
       } else {
-        y = cmulc(rxv(g, s, m), pilot(a, seq, bit0, s, v, m));
+        y = cmulc(rxk(k, g, s, m), pilot(a, seq, bit0, s, v, m));
         if (rotate) {
           y = cmul(y, s_rot[s]);
         }
@@ -495,43 +549,30 @@ __global__ __launch_bounds__(CS_THREADS) void chest_slice_kernel(chest_args a_in
       }
     }
   }
+  // the slice's time-alignment correlation row (every thread takes part in the engine's barriers)
+  float*   corr = a.corr + (static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice) * a.ta_n;
+  auto*    work = reinterpret_cast<dft::cf*>(enl_in);
+  switch (a.ta_n) {
+    case 128: slice_ta_small<128>(a, enl_out, work + 1024, corr); break;
+    case 256: slice_ta_small<256>(a, enl_out, work + 1024, corr); break;
+    case 512: slice_ta_small<512>(a, enl_out, work + 1024, corr); break;
+    case 1024:
+      __syncthreads(); // the interpolation's reads of the pilot buffer are done
+      slice_ta_regs<ta_plan_1024, 4>(a, x, work, corr);
+      break;
+    default: // 2048 (the host admits N <= 2048)
+      __syncthreads();
+      slice_ta_regs<ta_plan_2048, 8>(a, x, work, corr);
+      break;
+  }
   const float4 tot = block_sum4(make_float4(rsrp, 0, 0, 0), red);
   if (tid == 0) {
     a.acc[static_cast<uint64_t>(gp) * CH_ACC + CH_ACC_RSRP + slice] = tot.x;
   }
 }
 
-// Time alignment, one workgroup per (grid, port, slice): the N-point IDFT of the slice's smoothed pilots
-// with the fused Stockham engine and |.|^2 into the slice's correlation row
-// (time_alignment_estimator_dft_impl.cpp:122-200).
-template <int N, bool MULTI>
-__global__ __launch_bounds__(dft::plan<N>::T) void chest_ta_kernel(chest_args a_in, chest_items items)
-{
-  const chest_args& a = item_args<MULTI>(a_in, items);
-  if (MULTI && (blockIdx.x >= a.nof_ports || blockIdx.y >= a.L * a.nof_lse)) {
-    return;
-  }
-  using dft::cf;
-  __shared__ cf  lds[dft::lds_complex<N>()];
-  const uint32_t gp     = blockIdx.x;
-  const uint32_t slice  = blockIdx.y;
-  const uint32_t npil   = a.npil;
-  const uint64_t row    = static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice;
-  const float2*  in     = a.filt + row * npil;
-  float*         corr   = a.corr + row * N;
-  auto           load   = [&](int i) -> cf {
-    if (i < static_cast<int>(npil)) {
-      const float2 v = in[i];
-      return cf{v.x, v.y};
-    }
-    return cf{0, 0};
-  };
-  auto store = [&](int k, cf v) { corr[k] = v.x * v.x + v.y * v.y; };
-  dft::plan<N>::template engine<+1>::run(lds, reinterpret_cast<const cf*>(a.ta_tw), load, store);
-}
-
-// Per-port measurements, one workgroup per (grid, port): the noise energy per CDM group from the smoothed
-// pilots of every slice (estimate_noise, :594-690), the slices' correlations summed in slice order (the
+// Per-port measurements, one workgroup per (grid, port): EPRE over every received DM-RS RE, the noise energy per
+// CDM group from the smoothed pilots of every slice (estimate_noise, :594-690), the slices' correlations summed in slice order (the
 // reference accumulates them symbol-major; the sum is order-free up to rounding), the peak search and
 // quadratic refinement (time_alignment_estimator_dft_impl.cpp:248-310) and noise variance, EPRE, RSRP,
 // SNR and CFO (do_compute tail, port_channel_estimator_average_impl.cpp:160-199).
@@ -584,7 +625,7 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
   const uint32_t* gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc +
                           12 * a.prb_lo;
   const float2*   filt  = a.filt + static_cast<uint64_t>(gp) * a.L * a.nof_lse * npil;
-  float           noise0 = 0, noise1 = 0;
+  float           noise0 = 0, noise1 = 0, epre = 0;
   const float     sf     = a.beta / static_cast<float>(a.nof_lse);
   const int nlse = static_cast<int>(a.nof_lse);
   for (uint32_t m = tid; m < npil; m += ST_THREADS) {
@@ -633,8 +674,10 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
           }
           pred = cadd(pred, po);
         }
-        const float2 n = csub(from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + g]), pred);
-        const float  e = __builtin_fmaf(n.x, n.x, n.y * n.y);
+        const float2 rx = from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + g]);
+        epre            = __builtin_fmaf(rx.x, rx.x, __builtin_fmaf(rx.y, rx.y, epre));
+        const float2 n  = csub(rx, pred);
+        const float  e  = __builtin_fmaf(n.x, n.x, n.y * n.y);
         if (g == 0) {
           noise0 += e;
         } else {
@@ -643,7 +686,7 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
       }
     }
   }
-  const float4 tot = block_sum4(make_float4(noise0, noise1, 0, 0), red);
+  const float4 tot = block_sum4(make_float4(noise0, noise1, epre, 0), red);
 
   // Peak search of estimate_ta_correlation (time_alignment_estimator_dft_impl.cpp:248-310) over wave 0 instead
   // of a serial scan by one thread: the first maximum (strict >) of corr[0, max_taps) and of
@@ -736,7 +779,7 @@ __global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in
     // do_compute tail (port_channel_estimator_average_impl.cpp:160-199).
     const float npilt  = static_cast<float>(npil * a.nds);
     const float rsrp   = rsrp_sum / (npilt * static_cast<float>(a.L));
-    const float epre   = acc[0] / npilt;
+    const float epre   = tot.z / npilt;
     float       nvar   = nsum / (npilt * static_cast<float>(a.ncdm) - 1.0f);
     nvar               = fmaxf(rsrp / 1e10f, nvar);
     const float datarp = rsrp * static_cast<float>(a.L) / a.beta / a.beta;
@@ -819,38 +862,12 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   if (nb == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(chest_seq_kernel<false>, dim3(1), dim3(CS_THREADS), 0, stream, a, chest_items{});
+  if (a.ta_n > 2048) { // the pilot kernel's largest IDFT (4096 npil / (275 x 12), npil <= 1650)
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(chest_pilot_kernel<false>, dim3(nb, a.L * a.nof_lse), dim3(CS_THREADS), 0, stream, a,
+                     chest_items{});
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    return e;
-  }
-  hipLaunchKernelGGL(chest_cfo_kernel<false>, dim3(nb), dim3(CFO_THREADS), 0, stream, a, chest_items{});
-  e = hipGetLastError();
-  if (e != hipSuccess) {
-    return e;
-  }
-  const dim3 slices(nb, a.L * a.nof_lse);
-  hipLaunchKernelGGL(chest_slice_kernel<false>, slices, dim3(CS_THREADS), 0, stream, a, chest_items{});
-  e = hipGetLastError();
-  if (e != hipSuccess) {
-    return e;
-  }
-  switch (a.ta_n) {
-#define SRS_TA_CASE(NN)                                                                                               \
-  case NN:                                                                                                            \
-    hipLaunchKernelGGL((chest_ta_kernel<NN, false>), slices, dim3(dft::plan<NN>::T), 0, stream, a, chest_items{});                           \
-    break;
-    SRS_TA_CASE(128)
-    SRS_TA_CASE(256)
-    SRS_TA_CASE(512)
-    SRS_TA_CASE(1024)
-    SRS_TA_CASE(2048)
-    SRS_TA_CASE(4096)
-#undef SRS_TA_CASE
-    default:
-      return hipErrorInvalidValue;
-  }
-  e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
   }
@@ -867,50 +884,16 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   return hipGetLastError();
 }
 
-hipError_t launch_chest_items(const chest_items&                       items,
-                              uint32_t                                 nof_items,
-                              uint32_t                                 max_ports,
-                              uint32_t                                 max_slices,
-                              const std::vector<chest_ta_group>&       ta_groups,
-                              hipStream_t                              stream)
+hipError_t launch_chest_items(const chest_items& items, uint32_t nof_items, uint32_t max_ports, uint32_t max_slices,
+                              hipStream_t stream)
 {
   if (nof_items == 0) {
     return hipSuccess;
   }
   const chest_args none{};
-  hipLaunchKernelGGL(chest_seq_kernel<true>, dim3(1, 1, nof_items), dim3(CS_THREADS), 0, stream, none, items);
+  hipLaunchKernelGGL(chest_pilot_kernel<true>, dim3(max_ports, max_slices, nof_items), dim3(CS_THREADS), 0, stream,
+                     none, items);
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(chest_cfo_kernel<true>, dim3(max_ports, 1, nof_items), dim3(CFO_THREADS), 0, stream, none,
-                       items);
-    e = hipGetLastError();
-  }
-  const dim3 slices(max_ports, max_slices, nof_items);
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(chest_slice_kernel<true>, slices, dim3(CS_THREADS), 0, stream, none, items);
-    e = hipGetLastError();
-  }
-  // time alignment: one launch per IDFT size, over the items of that size (ids)
-  for (const chest_ta_group& g : ta_groups) {
-    if (e != hipSuccess) {
-      break;
-    }
-    const chest_items sub{items.items, g.ids};
-    const dim3        gs(max_ports, max_slices, g.count);
-    switch (g.n) {
-#define SRS_TA_CASE(NN)                                                                                                 case NN:                                                                                                                hipLaunchKernelGGL((chest_ta_kernel<NN, true>), gs, dim3(dft::plan<NN>::T), 0, stream, none, sub);                   break;
-      SRS_TA_CASE(128)
-      SRS_TA_CASE(256)
-      SRS_TA_CASE(512)
-      SRS_TA_CASE(1024)
-      SRS_TA_CASE(2048)
-      SRS_TA_CASE(4096)
-#undef SRS_TA_CASE
-      default:
-        return hipErrorInvalidValue;
-    }
-    e = hipGetLastError();
-  }
   if (e == hipSuccess) {
     hipLaunchKernelGGL(chest_stats_kernel<true>, dim3(max_ports, 1, nof_items), dim3(ST_THREADS), 0, stream, none,
                        items);

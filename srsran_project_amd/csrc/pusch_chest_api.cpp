@@ -280,6 +280,9 @@ int make_args(chest_args& a, const srs_amd_pusch_chest_config* cfg, uint32_t nof
   uint32_t req = a.npil * TA_MAX_N / (275 * 12);
   uint32_t N   = 1u << log2_ceil(std::max(req, 1u));
   N            = std::max<uint32_t>(TA_MIN_N, N);
+  if (N > 2048) { // the fused pilot kernel's largest IDFT (npil <= 6 x 275)
+    return fail(SRS_AMD_EINVAL, "Time-alignment IDFT of %u points exceeds 2048.", N);
+  }
   a.ta_n       = N;
   a.ta_fs      = static_cast<double>(N) * scs_k * 1000 * 2;
   const double half_cp_s = static_cast<double>((144u * 64u) >> (mu + 1)) * T_C;
@@ -472,20 +475,12 @@ int srs_amd::chest_estimate_slot_unexpanded(::srs_amd_pusch_chest* chest,
     max_ports  = std::max(max_ports, views[i].nof_ports);
     max_slices = std::max(max_slices, views[i].L * views[i].nof_lse);
   }
-  // TA groups: item ids per IDFT size, after the argument blocks
-  std::vector<uint32_t> sizes;
-  for (uint32_t i = 0; i != nof_items; ++i) {
-    if (std::find(sizes.begin(), sizes.end(), views[i].ta_n) == sizes.end()) {
-      sizes.push_back(views[i].ta_n);
-    }
-  }
   const size_t o_args = total;
-  const size_t o_ids  = o_args + align_up(sizeof(chest_args) * nof_items, 256);
-  const size_t stage  = o_ids - o_args + sizeof(uint32_t) * nof_items;
+  const size_t stage  = sizeof(chest_args) * nof_items;
   std::lock_guard<std::mutex> lock(chest->mtx);
   hipError_t                  e = hipSetDevice(chest->device);
   if (e == hipSuccess) {
-    e = chest->scratch.ensure(o_ids + sizeof(uint32_t) * nof_items);
+    e = chest->scratch.ensure(o_args + stage);
   }
   if (e == hipSuccess) {
     e = chest->stage.acquire(stage);
@@ -493,21 +488,7 @@ int srs_amd::chest_estimate_slot_unexpanded(::srs_amd_pusch_chest* chest,
   if (e != hipSuccess) {
     return hip_fail(e, "PUSCH channel estimator slot scratch");
   }
-  auto*                       base = chest->scratch.as<uint8_t>();
-  auto*                       ids  = reinterpret_cast<uint32_t*>(base + o_ids);
-  std::vector<chest_ta_group> groups;
-  uint32_t*                   h_ids = chest->stage.at<uint32_t>(o_ids - o_args);
-  uint32_t                    n_ids = 0;
-  for (uint32_t n : sizes) {
-    chest_ta_group g{n, 0, ids + n_ids};
-    for (uint32_t i = 0; i != nof_items; ++i) {
-      if (views[i].ta_n == n) {
-        h_ids[n_ids++] = i;
-        ++g.count;
-      }
-    }
-    groups.push_back(g);
-  }
+  auto* base = chest->scratch.as<uint8_t>();
   for (uint32_t i = 0; i != nof_items; ++i) {
     chest_args& a = views[i];
     uint8_t*    b = base + offset[i];
@@ -545,7 +526,7 @@ int srs_amd::chest_estimate_slot_unexpanded(::srs_amd_pusch_chest* chest,
   e = chest->stage.upload(base + o_args, stage, s);
   if (e == hipSuccess) {
     const chest_items all{reinterpret_cast<const chest_args*>(base + o_args), nullptr};
-    e = launch_chest_items(all, nof_items, max_ports, max_slices, groups, s);
+    e = launch_chest_items(all, nof_items, max_ports, max_slices, s);
   }
   const hipError_t done = scope.close();
   e                     = e != hipSuccess ? e : done;

@@ -5,7 +5,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <vector>
 
 #include "srsran_amd/pusch_chest.h"
 
@@ -78,8 +77,7 @@ struct chest_args {
 
 // Slot form (several PDUs of one grid, srs_amd_pusch_process_slot): one argument block per work item (one PDU on
 // one grid, nof_ports of its own, grids / scratch / stats pointers of its own) in device memory; the kernels of a
-// launch take item ids[blockIdx.z] (ids == nullptr: item blockIdx.z), so launches grouped by a template parameter
-// (the time-alignment IDFT size) cover a subset of the items.
+// launch take item ids[blockIdx.z] (ids == nullptr: item blockIdx.z).
 struct chest_items {
   const chest_args* items = nullptr;
   const uint32_t*   ids   = nullptr;
@@ -98,21 +96,10 @@ __device__ __forceinline__ const chest_args& item_args(const chest_args& a, cons
   }
 }
 
-// Items sharing one time-alignment IDFT size (ids: device array of count item indices).
-struct chest_ta_group {
-  uint32_t        n;
-  uint32_t        count;
-  const uint32_t* ids;
-};
-
-// The slot form's pilot, time-alignment and statistics kernels over nof_items items (no expansion: the fused
-// equalizer consumes freq / acc).  max_ports / max_slices: the largest nof_ports / L x nof_lse of the items.
-hipError_t launch_chest_items(const chest_items&                 items,
-                              uint32_t                           nof_items,
-                              uint32_t                           max_ports,
-                              uint32_t                           max_slices,
-                              const std::vector<chest_ta_group>& ta_groups,
-                              hipStream_t                        stream);
+// The slot form's pilot and statistics kernels over nof_items items (no expansion: the fused equalizer consumes
+// freq / acc).  max_ports / max_slices: the largest nof_ports / L x nof_lse of the items.
+hipError_t launch_chest_items(const chest_items& items, uint32_t nof_items, uint32_t max_ports, uint32_t max_slices,
+                              hipStream_t stream);
 
 // expand = false: pilot and time-alignment kernels only -- the per-subcarrier estimates (freq) and the
 // per-port accumulators (acc) stay in the estimator's scratch for a consumer that rebuilds each RE's

@@ -73,8 +73,12 @@ def test_pdsch_modulate_rejects_wrong_length(mod):
     plan = mod.plan(_config(kw), grid0.shape[2])
     g = _as_u32(grid0)
     cw = np.packbits(bits)
+    # not a whole number of REs (QPSK, one layer: an odd bit count): rejected, as the reference's assertion
+    rc = mod._lib.srs_amd_pdsch_modulate(mod._h, plan._h, g.ctypes.data, 1, cw.ctypes.data, plan.nof_bits - 1)
+    assert rc == -1  # SRS_AMD_EINVAL
+    # a whole number of REs shorter than the allocation: accepted, its first REs mapped (the reference's mapper)
     rc = mod._lib.srs_amd_pdsch_modulate(mod._h, plan._h, g.ctypes.data, 1, cw.ctypes.data, plan.nof_bits - 2)
-    assert rc == -1  # SRS_AMD_EINVAL, as the reference's assertion
+    assert rc == 0
 
 
 def _dmrs_config(kw):

@@ -101,7 +101,7 @@ def test_pipeline_vs_reference_chain(case):
         # UL channel estimates on the GPU's grid
         est = pl.est_ul[c].cpu().numpy().view(np.uint32)
         est_ref, st_ref = och.ref_pusch_chest(gul, bp.SLOT, False, pl.ul_layers, bp.N_ID, 0, bp.DMRS_AMP, bp.DMRS_MASK,
-                                              0, bp.NPRB, bp.UL_START, bp.UL_NSYM, fd=2, td=0, compensate_cfo=True,
+                                              0, bp.NPRB, bp.UL_START, bp.UL_NSYM, fd=2, td=pl.ul_td, compensate_cfo=True,
                                               numerology=bp.MU)
         assert_estimates_close(est, est_ref, "cell %d estimates" % c)
         st = pl.stats_ul[c].cpu().numpy()
@@ -143,7 +143,7 @@ def test_pipeline_four_layer_pusch():
             assert same.mean() >= 0.99, (c, p, same.mean())
         est = pl.est_ul[c].cpu().numpy().view(np.uint32)
         est_ref, st_ref = och.ref_pusch_chest(gul, bp.SLOT, False, 4, bp.N_ID, 0, bp.DMRS_AMP, bp.DMRS_MASK, 0,
-                                              bp.NPRB, bp.UL_START, bp.UL_NSYM, fd=2, td=0, compensate_cfo=True,
+                                              bp.NPRB, bp.UL_START, bp.UL_NSYM, fd=2, td=pl.ul_td, compensate_cfo=True,
                                               numerology=bp.MU)
         assert_estimates_close(est, est_ref, "cell %d estimates" % c)
         st = pl.stats_ul[c].cpu().numpy()
