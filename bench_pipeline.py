@@ -334,12 +334,19 @@ class Pipeline:
     def stage_ms(self, stream, reps=3):
         """Per-stage device time (HIP events on the launch stream), averaged over reps after one untimed pass (the
         objects last ran on the step's chain streams: the first call on `stream` carries their cross-stream
-        ordering wait and is not a stage time)."""
+        ordering wait and is not a stage time).  A spin kernel (~1 ms) queued ahead of the stages lets the host
+        enqueue every stage's launches before the GPU reaches them, so an event pair brackets device time only:
+        right after a synchronize the GPU would otherwise wait for the host's launch calls inside the first
+        stage (the PDSCH encoder measured 0.15-0.18 ms that way, 0.09 ms back to back)."""
         t = self.torch
         names = ["pdsch_encode", "pdsch_modulate", "dmrs_pdsch", "ofdm_modulate", "ofdm_demodulate", "pusch_process"]
         acc = np.zeros(len(names))
+        spin = getattr(t.cuda, "_sleep", None)
         for rep in range(reps + 1):
             ev = [t.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
+            if spin is not None:
+                with t.cuda.stream(stream):
+                    spin(2_000_000)
             ev[0].record(stream)
             self.enc.encode_batch(self.tb_dl, self.plan_dl, out=self.cw_dl, stream=stream)
             ev[1].record(stream)

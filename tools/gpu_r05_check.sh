@@ -28,4 +28,11 @@ rc=$?; echo "trace rc=$rc" >> "$out/steps.log"; ok $rc
 timeout -k 10 300 python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --graph --slots-pipeline 1 \
   > "$out/one_cell_graph.json" 2> "$out/one_cell_graph.err"
 rc=$?; echo "one-cell rc=$rc" >> "$out/steps.log"; ok $rc
+
+# the graph-capture probe: the PDSCH chain forked onto its own stream inside the capture (SRSRAN_AMD_GRAPH_FORK=1)
+if [ -n "$GRAPH_FORK_PROBE" ]; then
+  SRSRAN_AMD_GRAPH_FORK=1 timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --graph \
+    --slots-pipeline 1 > "$out/graph_fork.json" 2> "$out/graph_fork.err"
+  echo "graph fork probe rc=$?" >> "$out/steps.log"
+fi
 echo done >> "$out/steps.log"
