@@ -121,3 +121,5 @@ from .uci_decoder import UCI_INVALID, UCI_UNKNOWN, UCI_VALID, UciDecoder  # noqa
 from . import profiling  # noqa: F401,E402
 from . import pdcch  # noqa: F401,E402
 from .pdcch import CceToRegMapping, PdcchPdu, PdcchProcessor  # noqa: F401,E402
+from . import ssb  # noqa: F401,E402
+from .ssb import SsbPatternCase, SsbPdu, SsbProcessor  # noqa: F401,E402

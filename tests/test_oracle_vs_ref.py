@@ -493,3 +493,32 @@ def test_reference_pdsch_multi_prg_precoding_is_out_of_bounds():
     assert one.returncode == 0 and "done" in one.stdout, one.stderr[-2000:]
     multi = subprocess.run([sys.executable, "-c", code, "multi"], capture_output=True, text=True, timeout=300)
     assert multi.returncode != 0 and "done" not in multi.stdout, (multi.returncode, multi.stdout)
+
+
+# ---- SS/PBCH block -------------------------------------------------------------------------------------------------
+from tests import ssb_cases  # noqa: E402
+
+
+@pytest.mark.parametrize("case", ssb_cases.CASES, ids=[c[0] for c in ssb_cases.CASES])
+def test_ssb_restatement_matches_reference(case):
+    """oracle/ssb.py (numpy) equals the compiled ssb_processor_impl bit for bit, and the C-ABI's block position equals
+    ssb_get_l_first / ssb_get_k_first."""
+    import srsran_project_amd as amd
+    from oracle import ssb as oss
+
+    p = ssb_cases.pdu(case, seed=3)
+    g0 = ssb_cases.grid0(seed=4)
+    want = oss.ref_process(g0.copy(), [p])
+    got = oss.process(g0.copy(), p)
+    assert np.array_equal(got, want), "%d REs differ" % int((got != want).sum())
+    assert amd.ssb.position(p) == oss.ref_position(p)
+
+
+def test_ssb_invalid_pdus_rejected():
+    """PDUs the reference asserts on (wrong slot, non-integer subcarrier, FR2 SCS / k_SSB limits, SSB index beyond
+    the pattern) are rejected by the C-ABI's host checks (no GPU call)."""
+    import srsran_project_amd as amd
+
+    for c in ssb_cases.INVALID:
+        with pytest.raises(ValueError):
+            amd.ssb.position(ssb_cases.pdu(c))
