@@ -20,6 +20,8 @@
 
 #include <stdint.h>
 
+#include "srsran_amd/ldpc.h" /* SRS_AMD_OK, SRS_AMD_EINVAL, srs_amd_last_error */
+
 #ifdef __cplusplus
 extern "C" {
 #endif

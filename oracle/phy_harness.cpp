@@ -13,6 +13,7 @@
 
 #include "../integration/hip_resource_grid.h"
 #include "../integration/pdcch_processor_hip.h"
+#include "../integration/ssb_processor_hip.h"
 #include "../integration/pdsch_processor_hip.h"
 #include "../integration/pusch_processor_hip.h"
 #include "phy/generic_functions/precoding/channel_precoder_avx2.h"
@@ -31,6 +32,7 @@
 #include "phy/upper/signal_processors/pdsch/dmrs_pdsch_processor_impl.h"
 #include "phy/upper/signal_processors/ptrs/ptrs_pdsch_generator_impl.h"
 #include "ref_pdcch_pdu.h"
+#include "ref_ssb_pdu.h"
 #include "srsran_amd/pdsch_modulator.h"
 #include "srsran/adt/tensor.h"
 #include "srsran/fapi/messages/ul_tti_request.h"
@@ -972,6 +974,68 @@ int srs_ref_phy_pdcch_validate(void* h, const srs_amd_pdcch_pdu* pdu, char* msg,
 void srs_ref_phy_pdcch_stats(void* h, uint64_t* out)
 {
   const auto s = static_cast<pdcch_ctx*>(h)->factory->get_statistics();
+  out[0]       = s.nof_pdus;
+  out[1]       = s.nof_errors;
+  out[2]       = s.nof_device_grids;
+}
+
+} // extern "C"
+
+/* ---- SSB: the MI355X plug-in (integration/ssb_processor_hip) driven through the reference interface ---- */
+
+namespace {
+struct ssb_ctx {
+  std::shared_ptr<hip::ssb_processor_factory_hip> factory;
+  std::unique_ptr<ssb_processor>                  proc;
+  std::unique_ptr<ssb_pdu_validator>              validator;
+};
+} // namespace
+
+extern "C" {
+
+void* srs_ref_phy_ssb_create(int device)
+{
+  hip::ssb_processor_hip_config cfg;
+  cfg.device   = device;
+  auto ctx     = std::make_unique<ssb_ctx>();
+  ctx->factory = hip::create_ssb_processor_factory_hip(cfg);
+  if (!ctx->factory) {
+    return nullptr;
+  }
+  ctx->proc      = ctx->factory->create();
+  ctx->validator = ctx->factory->create_validator();
+  return ctx.release();
+}
+
+void srs_ref_phy_ssb_destroy(void* h)
+{
+  delete static_cast<ssb_ctx*>(h);
+}
+
+/* ssb_processor::process of each PDU, in order, into grid g (a host writer grid or a device-resident grid). */
+void srs_ref_phy_ssb_process(void* h, void* g, const srs_amd_ssb_pdu* pdus, unsigned n)
+{
+  auto* ctx = static_cast<ssb_ctx*>(h);
+  for (unsigned i = 0; i != n; ++i) {
+    ctx->proc->process(static_cast<any_grid*>(g)->wr(), srs_ref::ssb_pdu_from_amd(pdus[i]));
+  }
+}
+
+/* The plug-in factory's validator: 1 valid, 0 invalid (msg filled). */
+int srs_ref_phy_ssb_validate(void* h, const srs_amd_ssb_pdu* pdu, char* msg, unsigned msg_size)
+{
+  error_type<std::string> r = static_cast<ssb_ctx*>(h)->validator->is_valid(srs_ref::ssb_pdu_from_amd(*pdu));
+  if (r.has_value()) {
+    return 1;
+  }
+  std::snprintf(msg, msg_size, "%s", r.error().c_str());
+  return 0;
+}
+
+/* [0] PDUs, [1] errors, [2] device-resident grids. */
+void srs_ref_phy_ssb_stats(void* h, uint64_t* out)
+{
+  const auto s = static_cast<ssb_ctx*>(h)->factory->get_statistics();
   out[0]       = s.nof_pdus;
   out[1]       = s.nof_errors;
   out[2]       = s.nof_device_grids;

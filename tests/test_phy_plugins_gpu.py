@@ -546,3 +546,36 @@ def test_pdcch_plugin_validator_and_unsupported(phy):
     plug.process(wg, [make_pdu(np.ones(20, np.uint8), aggregation_level=3)])
     assert np.array_equal(wg.read(), g0)
     assert plug.stats()["errors"] == 1
+
+
+def test_ssb_plugin_vs_reference(phy):
+    """ssb_processor_factory_hip's processors, driven through the reference's ssb_processor interface, write exactly
+    the grid ssb_processor_impl writes -- on a host writer grid (the block's PSS / SSS / PBCH / DM-RS REs stored
+    through get_view) and on a device-resident hip_resource_grid -- for every case of tests/ssb_cases.py; PDUs the
+    reference asserts on are refused by the validator, logged and counted, the grid untouched."""
+    from oracle import ssb as oss
+    from tests import ssb_cases
+
+    ophy, _ = phy
+    plug = ophy.SsbProcessorPlugin(device=0)
+    for i, case in enumerate(ssb_cases.CASES):
+        pdu = ssb_cases.pdu(case, seed=40 + i)
+        g0 = ssb_cases.grid0(seed=50 + i)
+        want = oss.ref_process(g0.copy(), [pdu])
+        wg = ophy.WriterGrid(g0)
+        plug.process(wg, [pdu])
+        assert np.array_equal(wg.read(), want), (case[0], "host grid")
+        dg = ophy.DeviceGrid(g0)
+        plug.process(dg, [pdu])
+        assert np.array_equal(dg.read(), want), (case[0], "device grid")
+        assert plug.validate(pdu) is None, case[0]
+    n = len(ssb_cases.CASES)
+    assert plug.stats() == dict(pdus=2 * n, errors=0, device_grids=n), plug.stats()
+    g0 = ssb_cases.grid0(seed=3)
+    for case in ssb_cases.INVALID:
+        pdu = ssb_cases.pdu(case)
+        assert plug.validate(pdu) is not None, case[0]
+        wg = ophy.WriterGrid(g0)
+        plug.process(wg, [pdu])
+        assert np.array_equal(wg.read(), g0), case[0]
+    assert plug.stats()["errors"] == len(ssb_cases.INVALID)
