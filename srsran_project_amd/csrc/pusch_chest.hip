@@ -177,6 +177,14 @@ __device__ void virtual_pilots_wave(float2* out, const float2* in, int n, bool i
   }
 }
 
+// Allocations of at most CH_SMALL_NPIL pilots per DM-RS symbol (68 PRBs: time-alignment IDFTs of <= 512 points)
+// take the narrow workgroups of the pilot and statistics kernels.
+constexpr uint32_t CH_SMALL_NPIL = 412;
+__device__ __host__ __forceinline__ bool chest_small(const chest_args& a)
+{
+  return a.npil <= CH_SMALL_NPIL;
+}
+
 // Words of the DM-RS Gold sequences (bits 2 x 6 x prb_lo .. of every DM-RS symbol), shared by every grid
 // and port of the batch.
 __device__ __forceinline__ uint32_t dmrs_nof_words(const chest_args& a, uint32_t& w_first)
@@ -194,10 +202,9 @@ __device__ __forceinline__ uint32_t dmrs_words_gen(const chest_args& a, uint32_t
 {
   uint32_t       w_first;
   const uint32_t nwords = dmrs_nof_words(a, w_first);
-  const uint32_t d      = threadIdx.x / 64;
   const uint32_t lane   = threadIdx.x % 64;
   const bool     keep   = blockIdx.x == 0 && blockIdx.y == 0;
-  if (d < a.nds) {
+  for (uint32_t d = threadIdx.x / 64; d < a.nds; d += blockDim.x / 64) {
     uint32_t x1, x2;
     gold_state_lanes(a.jump, a.c_init[d], 32 * w_first, lane, x1, x2);
 #pragma unroll
@@ -283,22 +290,26 @@ static_assert(1024 + dft::lds_complex<512>() <= CH_ENL, "small IDFT work area ex
 // averaging (lane shuffle), scaling, FD smoothing in LDS (mean, or virtual pilots + raised-cosine FIR), the
 // slice's RSRP share, linear interpolation to every RE of the allocation
 // (port_channel_estimator_average_impl.cpp:130-506), the slice's time-alignment IDFT.
-// occupancy target of the pilot kernel (waves per SIMD; registers 512 / waves), a build-time tuning knob
-#ifndef SRS_AMD_CHEST_WAVES_PER_EU
-#define SRS_AMD_CHEST_WAVES_PER_EU 5
-#endif
-template <bool MULTI>
-__global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(SRS_AMD_CHEST_WAVES_PER_EU))) void
+//
+// T = 256 threads (eight pilots each, up to 2,048), or T = 64 for allocations of at most CH_SMALL_NPIL pilots (68
+// PRBs): one wave per slice, so the small PDUs of a multi-UE slot -- most of its workgroups -- do not hold three idle
+// waves through every barrier (the slot form launches both widths, each workgroup leaving at once when its item
+// belongs to the other).
+template <bool MULTI, int T>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T == 256 && !MULTI ? 5 : 4))) void
 chest_pilot_kernel(chest_args a_in, chest_items items)
 {
   const chest_args& a = item_args<MULTI>(a_in, items);
-  if (MULTI && (blockIdx.x >= a.nof_ports || blockIdx.y >= a.L * a.nof_lse)) {
+  if (MULTI && (blockIdx.x >= a.nof_ports || blockIdx.y >= a.L * a.nof_lse || chest_small(a) != (T == 64))) {
     return;
   }
+  constexpr int CS_THREADS = T;
+  // pilot buffer: the FD filter's input, then (after a barrier) the smoothed pilots the interpolation and the IDFT
+  // read, then the IDFT's work area (from WORK_OFF for N <= 512)
+  constexpr int ENL      = T == 64 ? CH_SMALL_NPIL + 2 * CH_MAXV + dft::lds_complex<512>() : CH_ENL;
+  constexpr int WORK_OFF = T == 64 ? CH_SMALL_NPIL + 2 * CH_MAXV : 1024;
   __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
-  // one pilot buffer: the FD filter's input, then (after a barrier) the smoothed pilots the interpolation and
-  // the IDFT read
-  __shared__ float2   enl_in[CH_ENL];
+  __shared__ float2   enl_in[ENL];
   float2* const       enl_out = enl_in;
   __shared__ float    red[4 * 16];
   __shared__ float2   s_rot[CH_MAXDMRS];
@@ -480,7 +491,10 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
       }
     }
     __syncthreads();
-    if (tid < 64) {
+    if (T == 64) { // one wave: both ends in turn
+      virtual_pilots_wave(enl_in + CH_MAXV - nv, enl_in + CH_MAXV, nv, true);
+      virtual_pilots_wave(enl_in + CH_MAXV + npil, enl_in + CH_MAXV + npil - nv, nv, false);
+    } else if (tid < 64) {
       virtual_pilots_wave(enl_in + CH_MAXV - nv, enl_in + CH_MAXV, nv, true);
     } else if (tid < 128) {
       virtual_pilots_wave(enl_in + CH_MAXV + npil, enl_in + CH_MAXV + npil - nv, nv, false);
@@ -553,16 +567,18 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
   float*   corr = a.corr + (static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice) * a.ta_n;
   auto*    work = reinterpret_cast<dft::cf*>(enl_in);
   switch (a.ta_n) {
-    case 128: slice_ta_small<128>(a, enl_out, work + 1024, corr); break;
-    case 256: slice_ta_small<256>(a, enl_out, work + 1024, corr); break;
-    case 512: slice_ta_small<512>(a, enl_out, work + 1024, corr); break;
-    case 1024:
-      __syncthreads(); // the interpolation's reads of the pilot buffer are done
-      slice_ta_regs<ta_plan_1024, 4>(a, x, work, corr);
-      break;
-    default: // 2048 (the host admits N <= 2048)
-      __syncthreads();
-      slice_ta_regs<ta_plan_2048, 8>(a, x, work, corr);
+    case 128: slice_ta_small<128>(a, enl_out, work + WORK_OFF, corr); break;
+    case 256: slice_ta_small<256>(a, enl_out, work + WORK_OFF, corr); break;
+    case 512: slice_ta_small<512>(a, enl_out, work + WORK_OFF, corr); break;
+    default:
+      if constexpr (T == 256) {
+        __syncthreads(); // the interpolation's reads of the pilot buffer are done
+        if (a.ta_n == 1024) {
+          slice_ta_regs<ta_plan_1024, 4>(a, x, work, corr);
+        } else { // 2048 (the host admits N <= 2048)
+          slice_ta_regs<ta_plan_2048, 8>(a, x, work, corr);
+        }
+      }
       break;
   }
   const float4 tot = block_sum4(make_float4(rsrp, 0, 0, 0), red);
@@ -576,13 +592,15 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
 // reference accumulates them symbol-major; the sum is order-free up to rounding), the peak search and
 // quadratic refinement (time_alignment_estimator_dft_impl.cpp:248-310) and noise variance, EPRE, RSRP,
 // SNR and CFO (do_compute tail, port_channel_estimator_average_impl.cpp:160-199).
-template <bool MULTI>
-__global__ __launch_bounds__(ST_THREADS) void chest_stats_kernel(chest_args a_in, chest_items items)
+// ST = 1,024 threads, or 256 for allocations of at most CH_SMALL_NPIL pilots (as the pilot kernel's widths).
+template <bool MULTI, int ST>
+__global__ __launch_bounds__(ST) void chest_stats_kernel(chest_args a_in, chest_items items)
 {
   const chest_args& a = item_args<MULTI>(a_in, items);
-  if (MULTI && blockIdx.x >= a.nof_ports) {
+  if (MULTI && (blockIdx.x >= a.nof_ports || chest_small(a) != (ST == 256))) {
     return;
   }
+  constexpr int ST_THREADS = ST;
   __shared__ uint32_t seq[CH_MAXDMRS][CH_SEQWORDS];
   __shared__ float    corr[CH_TA_MAXN];
   __shared__ float    red[4 * 16];
@@ -865,13 +883,21 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
   if (a.ta_n > 2048) { // the pilot kernel's largest IDFT (4096 npil / (275 x 12), npil <= 1650)
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(chest_pilot_kernel<false>, dim3(nb, a.L * a.nof_lse), dim3(CS_THREADS), 0, stream, a,
-                     chest_items{});
+  const dim3 slices(nb, a.L * a.nof_lse);
+  if (chest_small(a)) {
+    hipLaunchKernelGGL((chest_pilot_kernel<false, 64>), slices, dim3(64), 0, stream, a, chest_items{});
+  } else {
+    hipLaunchKernelGGL((chest_pilot_kernel<false, 256>), slices, dim3(256), 0, stream, a, chest_items{});
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
   }
-  hipLaunchKernelGGL(chest_stats_kernel<false>, dim3(nb), dim3(ST_THREADS), 0, stream, a, chest_items{});
+  if (chest_small(a)) {
+    hipLaunchKernelGGL((chest_stats_kernel<false, 256>), dim3(nb), dim3(256), 0, stream, a, chest_items{});
+  } else {
+    hipLaunchKernelGGL((chest_stats_kernel<false, 1024>), dim3(nb), dim3(1024), 0, stream, a, chest_items{});
+  }
   e = hipGetLastError();
   if (e != hipSuccess) {
     return e;
@@ -885,17 +911,30 @@ hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t str
 }
 
 hipError_t launch_chest_items(const chest_items& items, uint32_t nof_items, uint32_t max_ports, uint32_t max_slices,
-                              hipStream_t stream)
+                              uint32_t nof_small, hipStream_t stream)
 {
   if (nof_items == 0) {
     return hipSuccess;
   }
   const chest_args none{};
-  hipLaunchKernelGGL(chest_pilot_kernel<true>, dim3(max_ports, max_slices, nof_items), dim3(CS_THREADS), 0, stream,
-                     none, items);
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(chest_stats_kernel<true>, dim3(max_ports, 1, nof_items), dim3(ST_THREADS), 0, stream, none,
+  const dim3       slices(max_ports, max_slices, nof_items);
+  hipError_t       e = hipSuccess;
+  // each launch covers every item; the workgroups of the other width's items leave at once
+  if (nof_small != 0) {
+    hipLaunchKernelGGL((chest_pilot_kernel<true, 64>), slices, dim3(64), 0, stream, none, items);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && nof_small != nof_items) {
+    hipLaunchKernelGGL((chest_pilot_kernel<true, 256>), slices, dim3(256), 0, stream, none, items);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && nof_small != 0) {
+    hipLaunchKernelGGL((chest_stats_kernel<true, 256>), dim3(max_ports, 1, nof_items), dim3(256), 0, stream, none,
+                       items);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && nof_small != nof_items) {
+    hipLaunchKernelGGL((chest_stats_kernel<true, 1024>), dim3(max_ports, 1, nof_items), dim3(1024), 0, stream, none,
                        items);
     e = hipGetLastError();
   }

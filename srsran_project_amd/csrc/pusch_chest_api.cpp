@@ -526,7 +526,11 @@ int srs_amd::chest_estimate_slot_unexpanded(::srs_amd_pusch_chest* chest,
   e = chest->stage.upload(base + o_args, stage, s);
   if (e == hipSuccess) {
     const chest_items all{reinterpret_cast<const chest_args*>(base + o_args), nullptr};
-    e = launch_chest_items(all, nof_items, max_ports, max_slices, s);
+    uint32_t nof_small = 0;
+    for (uint32_t i = 0; i != nof_items; ++i) {
+      nof_small += views[i].npil <= 412 ? 1u : 0u;
+    }
+    e = launch_chest_items(all, nof_items, max_ports, max_slices, nof_small, s);
   }
   const hipError_t done = scope.close();
   e                     = e != hipSuccess ? e : done;

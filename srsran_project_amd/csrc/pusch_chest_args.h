@@ -13,7 +13,6 @@ namespace srs_amd {
 constexpr int CH_MAXPIL   = 2048;           // pilots per DM-RS symbol (type 1: 6 x 275 = 1650)
 constexpr int CS_THREADS  = 256;            // slice and stats kernel workgroups
 constexpr int CS_PPT      = CH_MAXPIL / CS_THREADS;
-constexpr int ST_THREADS  = 1024;           // per-port statistics kernel workgroup
 constexpr int CH_TA_MAXN  = 4096;           // largest time-alignment IDFT
 constexpr int CH_MAXV     = 12;             // MAX_V_PILOTS
 constexpr int CH_MAXDMRS  = 4;              // DM-RS symbols per slot
@@ -99,7 +98,8 @@ __device__ __forceinline__ const chest_args& item_args(const chest_args& a, cons
 // The slot form's pilot and statistics kernels over nof_items items (no expansion: the fused equalizer consumes
 // freq / acc).  max_ports / max_slices: the largest nof_ports / L x nof_lse of the items.
 hipError_t launch_chest_items(const chest_items& items, uint32_t nof_items, uint32_t max_ports, uint32_t max_slices,
-                              hipStream_t stream);
+                              uint32_t nof_small, hipStream_t stream);
+// nof_small: items of at most 412 pilots per DM-RS symbol (the narrow workgroups, pusch_chest.hip chest_small).
 
 // expand = false: pilot and time-alignment kernels only -- the per-subcarrier estimates (freq) and the
 // per-port accumulators (acc) stay in the estimator's scratch for a consumer that rebuilds each RE's
