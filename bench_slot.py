@@ -129,8 +129,6 @@ def run_sch_slot(args, dist, world, rank, dev, timed):
             "parallelism": "cells sharded over ranks" if world > 1 else "single GPU",
         },
         "step_event_ms": step_ms,
-        "pusch_pdu_kinds": {k: pl.kinds.count(k) for k in sorted(set(pl.kinds))},
-        "pusch_tb_ok_fraction_by_kind": pl.ok_by_kind,
         "pusch_tb_ok_fraction": ok,
         "pusch_tbs_equal_sent": tb_equal,
         "per_ue_launches": per_ue,
