@@ -1,0 +1,134 @@
+"""Host-side mirror of srsRAN's PUCCH Format 0 detector over the MI355X C-ABI (include/srsran_amd/pucch.h).
+
+Reference interface: pucch_detector::detect(const resource_grid_reader&, const format0_configuration&)
+(include/srsran/phy/upper/channel_processors/pucch/pucch_detector.h:44-77, impl pucch_detector_format0.cpp:124-246),
+the Format 0 branch of pucch_processor::process.  Grids are cbf16 [port][14][nof_subc]: numpy uint32 for the host
+form, torch int32 [n][port][14][nof_subc] on the device for the slot form.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+UCI_STATUS_VALID = 1
+UCI_STATUS_INVALID = 2
+
+
+class PucchF0Pdu(ctypes.Structure):
+    _fields_ = [("numerology", ctypes.c_uint32), ("slot_index", ctypes.c_uint32), ("starting_prb", ctypes.c_uint32),
+                ("second_hop_prb", ctypes.c_int32), ("start_symbol_index", ctypes.c_uint32),
+                ("nof_symbols", ctypes.c_uint32), ("initial_cyclic_shift", ctypes.c_uint32),
+                ("n_id", ctypes.c_uint32), ("nof_harq_ack", ctypes.c_uint32), ("sr_opportunity", ctypes.c_uint32),
+                ("nof_ports", ctypes.c_uint32), ("ports", ctypes.c_uint8 * 4), ("grid", ctypes.c_uint32),
+                ("d_grid", ctypes.c_void_p)]
+
+
+class PucchF0Result(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_uint32), ("nof_sr", ctypes.c_uint32), ("nof_harq_ack", ctypes.c_uint32),
+                ("sr", ctypes.c_uint8), ("harq_ack", ctypes.c_uint8 * 2), ("reserved", ctypes.c_uint8),
+                ("detection_metric", ctypes.c_float), ("sinr_dB", ctypes.c_float), ("rsrp_dB", ctypes.c_float),
+                ("epre_dB", ctypes.c_float)]
+
+
+RESULT_DTYPE = np.dtype([("status", "<u4"), ("nof_sr", "<u4"), ("nof_harq_ack", "<u4"), ("sr", "u1"),
+                         ("harq_ack", "u1", (2,)), ("reserved", "u1"), ("detection_metric", "<f4"),
+                         ("sinr_dB", "<f4"), ("rsrp_dB", "<f4"), ("epre_dB", "<f4")])
+assert RESULT_DTYPE.itemsize == ctypes.sizeof(PucchF0Result)
+
+
+def make_f0_pdu(*, numerology=0, slot_index=0, starting_prb=0, second_hop_prb=None, start_symbol_index=12,
+                nof_symbols=2, initial_cyclic_shift=0, n_id=0, nof_harq_ack=1, sr_opportunity=False, ports=(0,),
+                grid=0):
+    """pucch_detector::format0_configuration."""
+    p = PucchF0Pdu()
+    p.numerology, p.slot_index, p.starting_prb = int(numerology), int(slot_index), int(starting_prb)
+    p.second_hop_prb = -1 if second_hop_prb is None else int(second_hop_prb)
+    p.start_symbol_index, p.nof_symbols = int(start_symbol_index), int(nof_symbols)
+    p.initial_cyclic_shift, p.n_id = int(initial_cyclic_shift), int(n_id)
+    p.nof_harq_ack, p.sr_opportunity = int(nof_harq_ack), int(bool(sr_opportunity))
+    if not 1 <= len(ports) <= 4:
+        raise ValueError("1 to 4 ports")
+    p.nof_ports = len(ports)
+    for i, q in enumerate(ports):
+        p.ports[i] = int(q)
+    p.grid = int(grid)
+    return p
+
+
+def _declare(lib):
+    c = ctypes
+    P = c.c_void_p
+    sigs = {
+        "srs_amd_pucch_processor_create": (c.c_int, [c.POINTER(P), c.c_int]),
+        "srs_amd_pucch_processor_destroy": (None, [P]),
+        "srs_amd_pucch_f0_detect_slot": (c.c_int, [P, P, c.c_uint32, P, c.c_uint64, c.c_uint32, c.c_uint32,
+                                                   c.c_uint32, P, P]),
+        "srs_amd_pucch_f0_detect": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P]),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+_declared = False
+
+
+def _L():
+    global _declared
+    lib = _lib.lib()
+    if not _declared:
+        _declare(lib)
+        _declared = True
+    return lib
+
+
+class PucchProcessor:
+    """PUCCH Format 0 detection on the MI355X (one per device; thread-safe)."""
+
+    def __init__(self, device=0):
+        self._lib = _L()
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.srs_amd_pucch_processor_create(ctypes.byref(h), int(device)), "pucch_processor create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.srs_amd_pucch_processor_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def detect_f0(self, grid, pdu):
+        """pucch_detector::detect of one Format 0 PDU on a host grid (numpy uint32 [ports][14][nof_subc])."""
+        if grid.dtype != np.uint32 or grid.ndim != 3 or grid.shape[1] != 14 or not grid.flags.c_contiguous:
+            raise ValueError("grid must be a C-contiguous uint32 array [ports][14][nof_subc]")
+        r = PucchF0Result()
+        _lib.check(self._lib.srs_amd_pucch_f0_detect(self._h, ctypes.byref(pdu), grid.ctypes.data, grid.shape[0],
+                                                     grid.shape[2], ctypes.byref(r)), "pucch f0 detect")
+        return r
+
+    def detect_f0_slot(self, grids, pdus, stream=None):
+        """Every Format 0 PDU of a slot on device grids (torch int32 [n][ports][14][nof_subc]); returns a torch
+        uint8 tensor of nof_pdus RESULT_DTYPE records (asynchronous on stream)."""
+        import torch
+
+        arr = (PucchF0Pdu * len(pdus))(*pdus)
+        out = torch.zeros((len(pdus), RESULT_DTYPE.itemsize), dtype=torch.uint8, device=grids.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(grids.device)
+        _lib.check(self._lib.srs_amd_pucch_f0_detect_slot(
+            self._h, arr, len(pdus), grids.data_ptr(), grids.stride(0), grids.shape[0], grids.shape[1],
+            grids.shape[-1], out.data_ptr(), ctypes.c_void_p(stream.cuda_stream)), "pucch f0 detect_slot")
+        return out
+
+
+def parse_results(raw):
+    """uint8 [n][record] (numpy) -> RESULT_DTYPE records."""
+    return np.ascontiguousarray(raw).view(RESULT_DTYPE).reshape(-1)

@@ -1,0 +1,37 @@
+"""PUCCH Format 0 PDUs with transmitted cyclic shifts (or noise only): 1-2 symbols, frequency hopping, 0-2 HARQ-ACK
+bits with and without an SR opportunity, 1-4 ports, slots across numerologies, SNRs from well above to below the
+detection threshold.  TEST INFRASTRUCTURE ONLY."""
+import numpy as np
+
+import srsran_project_amd as amd
+
+NSUBC = 12 * 52
+
+
+def cases(n=24, seed=0):
+    """[(pdu, grid uint32 [4][14][NSUBC], transmitted table index or None)]"""
+    from oracle import pucch as op
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        nh = int(rng.integers(0, 3))
+        sr = bool(rng.integers(0, 2)) or nh == 0
+        nsym = int(rng.integers(1, 3))
+        hop = int(rng.integers(0, 52)) if (nsym == 2 and rng.integers(0, 2)) else None
+        nports = int(rng.integers(1, 5))
+        mu = int(rng.integers(0, 3))
+        pdu = amd.pucch.make_f0_pdu(numerology=mu, slot_index=int(rng.integers(0, 10 << mu)),
+                                    starting_prb=int(rng.integers(0, 52)), second_hop_prb=hop,
+                                    start_symbol_index=int(rng.integers(0, 15 - nsym)), nof_symbols=nsym,
+                                    initial_cyclic_shift=int(rng.integers(0, 12)), n_id=int(rng.integers(0, 1024)),
+                                    nof_harq_ack=nh, sr_opportunity=sr,
+                                    ports=tuple(int(x) for x in rng.permutation(4)[:nports]))
+        table = op.TABLES[(nh, sr)]
+        sent = None if i % 6 == 5 else int(rng.integers(0, len(table)))
+        grid = rng.integers(0, 1 << 32, (4, 14, NSUBC), dtype=np.uint64).astype(np.uint32)
+        gains = (rng.normal(size=nports) + 1j * rng.normal(size=nports)) / np.sqrt(2)
+        noise = [0.01, 0.1, 1.0, 3.0][i % 4]
+        op.transmit(grid, pdu, None if sent is None else table[sent][0], gains, noise, rng)
+        out.append((pdu, grid, sent))
+    return out

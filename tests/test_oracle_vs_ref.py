@@ -522,3 +522,22 @@ def test_ssb_invalid_pdus_rejected():
     for c in ssb_cases.INVALID:
         with pytest.raises(ValueError):
             amd.ssb.position(ssb_cases.pdu(c))
+
+
+# ---- PUCCH Format 0 ------------------------------------------------------------------------------------------------
+def test_pucch_f0_restatement_matches_reference():
+    """oracle/pucch.py gives the compiled pucch_detector_format0's message bits and status on every case, and its
+    metric / CSI within float tolerance (the restated cyclic shift is a double-precision exponential, the reference's
+    a float table: 1e-3 relative / 0.01 dB)."""
+    from oracle import pucch as op
+    from tests.pucch_cases import cases
+
+    for i, (pdu, grid, sent) in enumerate(cases()):
+        st, sr, harq, metric, sinr, rsrp, epre = op.detect(grid, pdu)
+        r = op.ref_detect(grid, pdu)
+        assert r.status == st, (i, r.status, st, metric)
+        assert list(r.harq_ack)[:r.nof_harq_ack] == list(harq), i
+        assert ([r.sr] if r.nof_sr else []) == list(sr), i
+        np.testing.assert_allclose(r.detection_metric, metric, rtol=1e-3, err_msg=str(i))
+        for a, b in ((r.sinr_dB, sinr), (r.rsrp_dB, rsrp), (r.epre_dB, epre)):
+            assert abs(a - b) <= 0.01, (i, a, b)
