@@ -1,8 +1,16 @@
 /*
- * srsran_amd/pucch.h -- C-ABI of the MI355X PUCCH Format 0 detector: for every PDU of a slot, the 12 received REs of
- * each OFDM symbol and receive port correlated with the low-PAPR sequence of every cyclic shift the UCI payload allows
- * (TS 38.213 9.2.3 / 9.2.5 tables), the detection metric (correlation over the residual energy), the best shift's
- * HARQ-ACK / SR bits, validity against the reference's threshold table, and the SINR / RSRP / EPRE measurements.
+ * srsran_amd/pucch.h -- C-ABI of the MI355X PUCCH Format 0 and Format 1 detectors.
+ *
+ * Format 0: for every PDU of a slot, the 12 received REs of each OFDM symbol and receive port correlated with the
+ * low-PAPR sequence of every cyclic shift the UCI payload allows (TS 38.213 9.2.3 / 9.2.5 tables), the detection
+ * metric (correlation over the residual energy), the best shift's HARQ-ACK / SR bits, validity against the
+ * reference's threshold table, and the SINR / RSRP / EPRE measurements.
+ *
+ * Format 1: for every batch of a slot (the PUCCHs multiplexed on one PRB / symbol allocation by initial cyclic shift
+ * and time-domain OCC), per hop the received REs matched to the base sequence and despread by a 12-point DFT, per OCC
+ * in use the OCC combination of data and DM-RS symbols, the per-shift channel estimates (shifts 10 dB below the
+ * strongest dropped), the noise from the DM-RS minus its reconstruction, and per multiplexed PUCCH the BPSK / QPSK
+ * symbol, the detection metric against the reference's threshold and the CSI.
  *
  * Replaces (reference interface):
  *   pucch_detector::detect(const resource_grid_reader&, const format0_configuration&)
@@ -11,7 +19,12 @@
  *        include/srsran/phy/upper/pucch_helper.h get_alpha_index, group sequence u = n_id mod 30 without hopping,
  *        low-PAPR sequences of low_papr_sequence_collection_impl.cpp)
  *   the Format 0 branch of pucch_processor::process (pucch_processor_impl.cpp).
- * The slot form detects every PDU of many cells' grids in one launch.  Grids are cbf16 [port][14][nof_subc].
+ *   pucch_detector::detect(const resource_grid_reader&, const format1_configuration&, const pucch_format1_map<unsigned>&)
+ *       pucch_detector.h:86-118, 155-160 (impl pucch_detector_format1.cpp:156-663, OCCs of
+ *       include/srsran/phy/upper/pucch_orthogonal_sequence.h), and
+ *   pucch_processor::process(const resource_grid_reader&, const format1_batch_configuration&)
+ *       pucch_processor_impl.cpp:74-138.
+ * The slot forms detect every PDU / batch of many cells' grids in one launch.  Grids are cbf16 [port][14][nof_subc].
  * Message bits and status equal the reference's; the CSI values are float measurements (tests/test_pucch_gpu.py
  * states the tolerance).
  */
@@ -47,19 +60,46 @@ typedef struct srs_amd_pucch_f0_pdu {
 #define SRS_AMD_UCI_STATUS_VALID 1 /* uci_status (uci_status.h): unknown 0, valid 1, invalid 2 */
 #define SRS_AMD_UCI_STATUS_INVALID 2
 
-/* The detector's pucch_uci_message and channel_state_information. */
-typedef struct srs_amd_pucch_f0_result {
+/* The detector's pucch_uci_message and channel_state_information (both formats). */
+typedef struct srs_amd_pucch_result {
   uint32_t status;           /* SRS_AMD_UCI_STATUS_* */
   uint32_t nof_sr;           /* 0 / 1 */
   uint32_t nof_harq_ack;
   uint8_t  sr;               /* SR bit */
   uint8_t  harq_ack[2];
   uint8_t  reserved;
-  float    detection_metric; /* the best shift's metric (linear) */
-  float    sinr_dB;          /* convert_power_to_dB(metric) */
+  float    detection_metric; /* F0: the best shift's metric (linear); F1: the metric over the threshold */
+  float    sinr_dB;          /* F0: convert_power_to_dB(metric); F1: RSRP over the noise variance */
   float    rsrp_dB;
   float    epre_dB;
-} srs_amd_pucch_f0_result;
+} srs_amd_pucch_result;
+typedef srs_amd_pucch_result srs_amd_pucch_f0_result;
+
+/* One multiplexed Format 1 PUCCH of a batch (an entry of format1_batch_configuration / pucch_format1_map<unsigned>). */
+typedef struct srs_amd_pucch_f1_entry {
+  uint8_t initial_cyclic_shift; /* 0 .. 11 */
+  uint8_t time_domain_occ;      /* 0 .. 6, below nof_symbols / 2 (/ 4 with frequency hopping) */
+  uint8_t nof_harq_ack;         /* 0 (SR only) .. 2 */
+  uint8_t reserved;
+} srs_amd_pucch_f1_entry;
+
+/* pucch_detector::format1_configuration with the batch's entries.  The reference detector reads grid ports 0 ..
+ * nof_ports - 1 of the reader it is given (pucch_detector_format1.cpp:568-583); here the PDU's ports[] name them. */
+typedef struct srs_amd_pucch_f1_batch {
+  uint32_t numerology;
+  uint32_t slot_index;
+  uint32_t starting_prb;
+  int32_t  second_hop_prb;        /* -1: no frequency hopping */
+  uint32_t start_symbol_index;    /* 0 .. 10 */
+  uint32_t nof_symbols;           /* 4 .. 14 */
+  uint32_t n_id;
+  uint32_t nof_ports;             /* 1, 2 or 4 */
+  uint8_t  ports[4];
+  uint32_t nof_entries;           /* 1 .. 84, no two with the same (shift, OCC) */
+  const srs_amd_pucch_f1_entry* entries;
+  uint32_t grid;                  /* index of the grid in d_grids */
+  const uint32_t* d_grid;         /* non-NULL: this batch's own DEVICE grid instead of d_grids[grid] */
+} srs_amd_pucch_f1_batch;
 
 typedef struct srs_amd_pucch_processor srs_amd_pucch_processor;
 
@@ -85,6 +125,27 @@ int srs_amd_pucch_f0_detect(srs_amd_pucch_processor*    proc,
                             uint32_t                    nof_ports,
                             uint32_t                    nof_subc,
                             srs_amd_pucch_f0_result*    result);
+
+/* DEVICE, asynchronous: every Format 1 batch of a slot detected; the result of entry e of batch b goes to
+ * d_results[nof_entries(0) + ... + nof_entries(b - 1) + e]. */
+int srs_amd_pucch_f1_detect_slot(srs_amd_pucch_processor*      proc,
+                                 const srs_amd_pucch_f1_batch* batches,
+                                 uint32_t                      nof_batches,
+                                 const uint32_t*               d_grids,
+                                 uint64_t                      grid_stride,
+                                 uint32_t                      nof_grids,
+                                 uint32_t                      nof_grid_ports,
+                                 uint32_t                      nof_subc,
+                                 srs_amd_pucch_result*         d_results,
+                                 void*                         stream);
+
+/* HOST, synchronous: one batch on a host grid [nof_ports][14][nof_subc], results[batch->nof_entries]. */
+int srs_amd_pucch_f1_detect(srs_amd_pucch_processor*      proc,
+                            const srs_amd_pucch_f1_batch* batch,
+                            const uint32_t*               grid,
+                            uint32_t                      nof_ports,
+                            uint32_t                      nof_subc,
+                            srs_amd_pucch_result*         results);
 
 #ifdef __cplusplus
 }

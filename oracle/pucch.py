@@ -120,3 +120,166 @@ def ref_detect(grid, pdu):
     r = PucchF0Result()
     _ref().srs_ref_pucch_f0_detect(g.ctypes.data, g.shape[0], g.shape[2], ctypes.addressof(pdu), ctypes.byref(r))
     return r
+
+
+# ---- Format 1 ------------------------------------------------------------------------------------------------------
+# TS 38.211 Table 6.3.2.4.1-2 (include/srsran/phy/upper/pucch_orthogonal_sequence.h:104-126)
+OCC_PHI = [
+    [[0]],
+    [[0, 0], [0, 1]],
+    [[0, 0, 0], [0, 1, 2], [0, 2, 1]],
+    [[0, 0, 0, 0], [0, 2, 0, 2], [0, 0, 2, 2], [0, 2, 2, 0]],
+    [[0, 0, 0, 0, 0], [0, 1, 2, 3, 4], [0, 2, 4, 1, 3], [0, 3, 1, 4, 2], [0, 4, 3, 2, 1]],
+    [[0] * 6, [0, 1, 2, 3, 4, 5], [0, 2, 4, 0, 2, 4], [0, 3, 0, 3, 0, 3], [0, 4, 2, 0, 4, 2], [0, 5, 4, 3, 2, 1]],
+    [[(i * m) % 7 for m in range(7)] for i in range(7)],
+]
+F1_THRESHOLD = {1: 0.9, 2: 3.0, 4: 4.45, 8: 6.95}  # pucch_detector_format1.cpp:194-212
+
+
+def occ(n, i):
+    return np.exp(2j * np.pi * np.array(OCC_PHI[n - 1][i], np.float64) / n).astype(np.complex64)
+
+
+def f1_hops(b):
+    """[(first allocated symbol r0, symbols, PRB)] of each hop (pucch_detector_format1.cpp:524-546)."""
+    if b.second_hop_prb < 0:
+        return [(0, b.nof_symbols, b.starting_prb)]
+    h = b.nof_symbols // 2
+    return [(0, h, b.starting_prb), (h, b.nof_symbols - h, b.second_hop_prb)]
+
+
+def _f1_base_seq(b, r):
+    """The base (m0 = m_cs = 0) sequence of allocated symbol r."""
+    from .chest import ref_low_papr
+
+    base = ref_low_papr(12, b.n_id % 30).astype(np.complex64)
+    c = prbs(b.n_id, 8 * (14 * b.slot_index + b.start_symbol_index + r) + 8)[8 * (14 * b.slot_index +
+                                                                                  b.start_symbol_index + r):]
+    a = int(sum(int(x) << m for m, x in enumerate(c[:8]))) % 12
+    return (base * np.exp(2j * np.pi * ((a * np.arange(12)) % 12) / 12)).astype(np.complex64), a
+
+
+def _row(grid, port, l, prb):
+    u = grid[port, l, 12 * prb:12 * prb + 12].astype(np.uint32)
+    return ((u << 16).view(np.float32) + 1j * (u & 0xFFFF0000).view(np.float32)).astype(np.complex64)
+
+
+def _detect_symbol(nb, x):
+    s = np.float32(np.sqrt(0.5))
+    if nb == 1:
+        m = s * x.real - s * x.imag
+        return (abs(m), [0]) if m > 0 else (abs(m), [1])
+    m1, m2 = s * x.real - s * x.imag, s * x.real + s * x.imag
+    m, bits = m1, [0, 0]
+    if abs(m2) > abs(m1):
+        m, bits = m2, [0, 1]
+    if m < 0:
+        m, bits = -m, [1 - bits[0], 1 - bits[1]]
+    return m, bits
+
+
+def detect_f1(grid, b, entries):
+    """pucch_detector_format1::detect (pucch_detector_format1.cpp:156-284) of a batch whose ports are grid ports
+    b.ports[:nof_ports]; entries = [(shift, occ, nof_harq_ack)] -> [(status, harq bits, metric / threshold, sinr_dB,
+    rsrp_dB, epre_dB)] in the same order."""
+    ports = [b.ports[i] for i in range(b.nof_ports)]
+    P = len(ports)
+    occs = sorted({o for _, o, _ in entries})
+    hop_metrics, epre, n_epre, noise, n_noise = [], 0.0, 0, 0.0, []
+    for r0, nh, prb in f1_hops(b):
+        dm, da = [], []  # LSE rows [port][12] of DM-RS (even allocated symbols) and data symbols
+        for r in range(r0, r0 + nh):
+            seq, _ = _f1_base_seq(b, r)
+            rows = np.stack([_row(grid, p, b.start_symbol_index + r, prb) for p in ports])
+            epre += float(np.sum(np.abs(rows) ** 2))
+            (dm if r % 2 == 0 else da).append(rows * np.conj(seq))
+        dm, da = np.array(dm, np.complex64), np.array(da, np.complex64)  # [sym][port][12]
+        nm, nd = len(dm), len(da)
+        Xm, Xd = np.fft.fft(dm, axis=-1).astype(np.complex64), np.fft.fft(da, axis=-1).astype(np.complex64)
+        recon = np.zeros_like(dm)
+        metrics = {}
+        for o in occs:
+            ds = np.einsum("spk,s->pk", Xd, np.conj(occ(nd, o)) / np.sqrt(nd)).astype(np.complex64)
+            ms = np.einsum("spk,s->pk", Xm, np.conj(occ(nm, o)) / np.sqrt(nm)).astype(np.complex64)
+            nrm = 1 / (12 * (nd + nm))
+            main = (np.sum(np.abs(ds) ** 2, 0) + np.sum(np.abs(ms) ** 2, 0)) * nrm
+            cross = np.sum(ms * np.conj(ds), 0) * nrm
+            ch = ms / (np.sqrt(nm) * 12)
+            rs = np.sum(np.abs(ch) ** 2, 0)
+            ch = np.where(rs > rs.max() / 10, ch, 0)
+            metrics[o] = (main, cross, rs / P)
+            v = np.fft.ifft(ch, axis=-1) * 12  # unnormalised IDFT
+            recon += (occ(nm, o)[:, None, None] * v[None]).astype(np.complex64)
+        hop_metrics.append(metrics)
+        n_epre += 12 * nh * P
+        noise += float(np.sum(np.abs(dm - recon) ** 2))
+        n_noise.append(12 * nm * P)
+    epre /= n_epre
+    noise /= sum(n_noise)
+    th = F1_THRESHOLD[P * len(hop_metrics)]
+    out = []
+    for ics, o, nh in entries:
+        main = sum(m[o][0][ics] for m in hop_metrics)
+        cross = sum(m[o][1][ics] for m in hop_metrics)
+        if len(hop_metrics) == 2:
+            rsrp = (hop_metrics[0][o][2][ics] * n_noise[0] + hop_metrics[1][o][2][ics] * n_noise[1]) / sum(n_noise)
+        else:
+            rsrp = hop_metrics[0][o][2][ics]
+        sinr = rsrp / noise if np.isfinite(noise) and noise > 0 else 0.0
+        det, bits = _detect_symbol(max(nh, 1), cross)
+        metric = (main + 2 * det) / noise
+        ok = metric > th and (nh != 0 or bits[0] == 0)
+        db = lambda x: 10 * np.log10(x) if x > 0 else -np.inf  # noqa: E731
+        out.append((1 if ok else 2, bits[:nh], metric / th, db(sinr), db(rsrp), db(epre)))
+    return out
+
+
+def transmit_f1(grid, b, pucchs, noise, rng):
+    """Writes the Format 1 PUCCHs [(shift, occ, bits, per-port gains)] of batch b (TS 38.211 6.3.2.4 / 6.4.1.3.1:
+    BPSK / QPSK symbol d spread by the shifted low-PAPR sequence and the OCC on data symbols, the shifted sequence and
+    the OCC on DM-RS symbols) plus complex Gaussian noise of variance noise onto its REs (uint32 cbf16, in place)."""
+    from .pdsch_mod import to_bf16
+
+    ports = [b.ports[i] for i in range(b.nof_ports)]
+    for r0, nh, prb in f1_hops(b):
+        nm = (r0 + nh + 1) // 2 - (r0 + 1) // 2
+        nd = nh - nm
+        for r in range(r0, r0 + nh):
+            base, a = _f1_base_seq(b, r)
+            is_dmrs = r % 2 == 0
+            m = (r + 1) // 2 - (r0 + 1) // 2 if is_dmrs else r // 2 - r0 // 2
+            y = np.zeros((len(ports), 12), np.complex64)
+            for ics, o, bits, gains in pucchs:
+                seq = base * np.exp(2j * np.pi * ((ics * np.arange(12)) % 12) / 12)
+                if is_dmrs:
+                    z = occ(nm, o)[m] * seq
+                else:
+                    bb = list(bits) if bits else [0]
+                    d = ((1 - 2 * bb[0]) * (1 + 1j) / np.sqrt(2) if len(bb) == 1 else
+                         ((1 - 2 * bb[0]) + 1j * (1 - 2 * bb[1])) / np.sqrt(2))
+                    z = occ(nd, o)[m] * d * seq
+                y += np.asarray(gains, np.complex64)[:, None] * z[None, :]
+            y += np.sqrt(noise / 2) * (rng.normal(size=y.shape) + 1j * rng.normal(size=y.shape))
+            y = y.astype(np.complex64)
+            for i, p in enumerate(ports):
+                grid[p, b.start_symbol_index + r, 12 * prb:12 * prb + 12] = (
+                    to_bf16(y[i].real).astype(np.uint32) | (to_bf16(y[i].imag).astype(np.uint32) << 16))
+    return grid
+
+
+def ref_detect_f1(grid, b):
+    """The compiled pucch_detector_format1::detect of batch b -> [srsran_project_amd.pucch.PucchResult] (entry
+    order).  The reference reads grid ports 0 .. nof_ports - 1, so the batch's ports are gathered into a dense grid
+    first."""
+    import ctypes
+
+    from srsran_project_amd.pucch import PucchResult
+
+    ref = _ref()
+    ref.srs_ref_pucch_f1_detect.restype = None
+    ref.srs_ref_pucch_f1_detect.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p,
+                                            ctypes.c_void_p]
+    g = np.ascontiguousarray(grid[[b.ports[i] for i in range(b.nof_ports)]], np.uint32)
+    out = (PucchResult * b.nof_entries)()
+    ref.srs_ref_pucch_f1_detect(g.ctypes.data, g.shape[0], g.shape[2], ctypes.addressof(b), out)
+    return list(out)

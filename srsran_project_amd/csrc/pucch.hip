@@ -1,11 +1,21 @@
-// pucch.hip -- MI355X PUCCH Format 0 detector (include/srsran_amd/pucch.h), after pucch_detector_format0.cpp:124-246.
+// pucch.hip -- MI355X PUCCH Format 0 and Format 1 detectors (include/srsran_amd/pucch.h).
 //
+// Format 0, after pucch_detector_format0.cpp:124-246.
 // One 64-thread workgroup per PDU: the received REs of every symbol and port into LDS (12 per symbol and port, the
 // second hop's PRB for symbol 1), the EPRE, then one thread per candidate cyclic shift: per symbol and port the
 // average power, the correlation with the shift's low-PAPR sequence (sum of rx conj(seq)), |corr|^2 / 12 into the
 // correlation sum and 12 power - |corr|^2 / 12 into the noise sum, the metric corr / max(noise, 1e-6); thread 0
 // keeps the first largest metric in table order, compares it with the threshold and writes the message and the
 // SINR / RSRP / EPRE in dB.
+//
+// Format 1, after pucch_detector_format1.cpp:156-663.  One 64-thread workgroup (one wave) per batch of multiplexed
+// PUCCHs.  Per hop: the received REs times the conjugated base sequence (cyclic shift n_cs of the symbol) into LDS,
+// split into DM-RS (even allocated symbols) and data rows, and their EPRE; a 12-point DFT of every row (bin k = the
+// initial cyclic shift k); then for every time-domain OCC in use, thread (port, shift) combines the rows with the
+// conjugated OCC, threads 0..11 form the main / cross contributions and the channel estimate of their shift, and
+// thread (port, RE) rebuilds the DM-RS with the shifts within 10 dB of the strongest (12-point IDFT times the OCC),
+// accumulated in registers over the OCCs; the noise is the energy of DM-RS minus reconstruction.  Last, thread e
+// decides entry e: the BPSK / QPSK symbol that maximises the cross term, the metric against the threshold, the CSI.
 #include <hip/hip_runtime.h>
 
 #include "pucch_args.h"
@@ -100,7 +110,269 @@ __global__ __launch_bounds__(64) void pucch_f0_kernel(const pucch_f0_desc* desc,
   }
 }
 
+// TS 38.211 Table 6.3.2.4.1-2 phases phi(m) of the Format 1 OCCs (pucch_orthogonal_sequence.h), [length - 1][i][m].
+__constant__ uint8_t F1_PHI[7][7][7] = {
+    {{0}},
+    {{0, 0}, {0, 1}},
+    {{0, 0, 0}, {0, 1, 2}, {0, 2, 1}},
+    {{0, 0, 0, 0}, {0, 2, 0, 2}, {0, 0, 2, 2}, {0, 2, 2, 0}},
+    {{0, 0, 0, 0, 0}, {0, 1, 2, 3, 4}, {0, 2, 4, 1, 3}, {0, 3, 1, 4, 2}, {0, 4, 3, 2, 1}},
+    {{0, 0, 0, 0, 0, 0}, {0, 1, 2, 3, 4, 5}, {0, 2, 4, 0, 2, 4}, {0, 3, 0, 3, 0, 3}, {0, 4, 2, 0, 4, 2},
+     {0, 5, 4, 3, 2, 1}},
+    {{0, 0, 0, 0, 0, 0, 0}, {0, 1, 2, 3, 4, 5, 6}, {0, 2, 4, 6, 1, 3, 5}, {0, 3, 6, 2, 5, 1, 4}, {0, 4, 1, 5, 2, 6, 3},
+     {0, 5, 3, 1, 6, 4, 2}, {0, 6, 5, 4, 3, 2, 1}}};
+
+constexpr float F1_TWOPI = 6.283185307179586f;
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b)
+{
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+__device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) // a conj(b)
+{
+  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+
+__device__ __forceinline__ float norm2(float2 a)
+{
+  return a.x * a.x + a.y * a.y;
+}
+
+__device__ __forceinline__ float wave_sum(float v)
+{
+  for (int o = 32; o != 0; o >>= 1) {
+    v += __shfl_xor(v, o);
+  }
+  return v;
+}
+
+// OCC value w_i(m) of length n: e^(j 2 pi phi / n)
+__device__ __forceinline__ float2 occ_w(uint32_t n, uint32_t i, uint32_t m)
+{
+  float sn, cs;
+  sincosf(F1_TWOPI * static_cast<float>(F1_PHI[n - 1][i][m]) / static_cast<float>(n), &sn, &cs);
+  return make_float2(cs, sn);
+}
+
+// detect_symbol (pucch_detector_format1.cpp:108-154): BPSK (nb = 1) or QPSK symbol maximising Re(d x), its bits.
+__device__ __forceinline__ float f1_detect_symbol(uint32_t nb, float2 x, uint8_t* bits)
+{
+  constexpr float s = 0.70710678118654752f;
+  if (nb == 1) {
+    float m = s * x.x - s * x.y;
+    bits[0] = 0;
+    if (!(m > 0.0f)) {
+      m       = -m;
+      bits[0] = 1;
+    }
+    return m;
+  }
+  const float m1 = s * x.x - s * x.y, m2 = s * x.x + s * x.y;
+  float       m  = m1;
+  bits[0] = bits[1] = 0;
+  if (fabsf(m2) > fabsf(m1)) {
+    m       = m2;
+    bits[1] = 1;
+  }
+  if (m < 0.0f) {
+    m       = -m;
+    bits[0] = 1 - bits[0];
+    bits[1] = 1 - bits[1];
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(64) void pucch_f1_kernel(const pucch_f1_desc*          desc,
+                                                      const srs_amd_pucch_f1_entry* entries,
+                                                      srs_amd_pucch_result*         results)
+{
+  const pucch_f1_desc& d = desc[blockIdx.x];
+  const uint32_t       t = threadIdx.x;
+  const uint32_t       P = d.nof_ports;
+  __shared__ float2    tw[12];
+  __shared__ float2    Ld[7][4][12], Lm[7][4][12], Xd[7][4][12], Xm[7][4][12];
+  __shared__ float2    s_d[4][12], s_m[4][12], s_ch[4][12];
+  __shared__ float     s_r[12];
+  __shared__ float     h_main[2][7][12], h_rsrp[2][7][12];
+  __shared__ float2    h_cross[2][7][12];
+  if (t < 12) {
+    float sn, cs;
+    sincosf(F1_TWOPI * static_cast<float>(t) / 12.0f, &sn, &cs);
+    tw[t] = make_float2(cs, sn);
+  }
+  float    epre = 0.0f, noise = 0.0f;
+  uint32_t n_epre = 0, n_noise0 = 0, n_noise1 = 0;
+  for (uint32_t h = 0; h != d.nof_hops; ++h) {
+    const uint32_t r0 = h == 0 ? 0 : d.nsym / 2;
+    const uint32_t nh = d.nof_hops == 1 ? d.nsym : (h == 0 ? d.nsym / 2 : d.nsym - d.nsym / 2);
+    const uint32_t nm = (r0 + nh + 1) / 2 - (r0 + 1) / 2; // DM-RS: even allocated symbols
+    const uint32_t nd = nh - nm;
+    const uint32_t nre = nh * P * 12;
+    __syncthreads();
+    float e_acc = 0.0f;
+    for (uint32_t i = t; i < nre; i += 64) {
+      const uint32_t sh = i / (P * 12), p = (i / 12) % P, n = i % 12, r = r0 + sh;
+      const float2   x  = from_cbf16(d.grid[static_cast<uint64_t>(d.ports[p]) * d.port_stride +
+                                           static_cast<uint64_t>(d.l0 + r) * d.nof_subc + d.subc0[h] + n]);
+      e_acc += norm2(x);
+      const float2 v = cmul_conj(x, cmul(d.base[n], tw[(d.alpha[r] * n) % 12]));
+      if ((r & 1u) == 0) {
+        Lm[(r + 1) / 2 - (r0 + 1) / 2][p][n] = v;
+      } else {
+        Ld[r / 2 - r0 / 2][p][n] = v;
+      }
+    }
+    epre += wave_sum(e_acc);
+    n_epre += nre;
+    __syncthreads();
+    for (uint32_t i = t; i < nre; i += 64) { // direct DFT of every row
+      const uint32_t q = i / (P * 12), p = (i / 12) % P, k = i % 12;
+      const float2*  in  = q < nm ? Lm[q][p] : Ld[q - nm][p];
+      float2         acc = make_float2(0.0f, 0.0f);
+      for (uint32_t n = 0; n != 12; ++n) {
+        const float2 v = cmul_conj(in[n], tw[(k * n) % 12]);
+        acc.x += v.x;
+        acc.y += v.y;
+      }
+      (q < nm ? Xm[q][p] : Xd[q - nm][p])[k] = acc;
+    }
+    __syncthreads();
+    float2 recon[7];
+#pragma unroll
+    for (uint32_t s = 0; s != 7; ++s) {
+      recon[s] = make_float2(0.0f, 0.0f);
+    }
+    const float nrm_d = 1.0f / sqrtf(static_cast<float>(nd)), nrm_m = 1.0f / sqrtf(static_cast<float>(nm));
+    for (uint32_t occi = 0; occi < nd; ++occi) {
+      if (((d.occ_mask >> occi) & 1u) == 0) {
+        continue;
+      }
+      if (t < P * 12) { // OCC combination of (port, shift)
+        const uint32_t p = t / 12, k = t % 12;
+        float2         a = make_float2(0.0f, 0.0f), b = make_float2(0.0f, 0.0f);
+        for (uint32_t s = 0; s != nd; ++s) {
+          const float2 w = occ_w(nd, occi, s);
+          const float2 v = cmul(Xd[s][p][k], make_float2(w.x * nrm_d, -w.y * nrm_d));
+          a.x += v.x;
+          a.y += v.y;
+        }
+        for (uint32_t s = 0; s != nm; ++s) {
+          const float2 w = occ_w(nm, occi, s);
+          const float2 v = cmul(Xm[s][p][k], make_float2(w.x * nrm_m, -w.y * nrm_m));
+          b.x += v.x;
+          b.y += v.y;
+        }
+        s_d[p][k] = a;
+        s_m[p][k] = b;
+      }
+      __syncthreads();
+      if (t < 12) { // contributions and channel estimate of shift t
+        float        main = 0.0f, r = 0.0f;
+        float2       cross = make_float2(0.0f, 0.0f);
+        const float  cn    = 1.0f / (sqrtf(static_cast<float>(nm)) * 12.0f);
+        for (uint32_t p = 0; p != P; ++p) {
+          const float2 a = s_d[p][t], b = s_m[p][t];
+          main += norm2(a) + norm2(b);
+          const float2 c = cmul_conj(b, a);
+          cross.x += c.x;
+          cross.y += c.y;
+          const float2 ch = make_float2(b.x * cn, b.y * cn);
+          s_ch[p][t]      = ch;
+          r += norm2(ch);
+        }
+        const float nrm        = 1.0f / static_cast<float>(12 * (nd + nm));
+        h_main[h][occi][t]  = main * nrm;
+        h_cross[h][occi][t] = make_float2(cross.x * nrm, cross.y * nrm);
+        h_rsrp[h][occi][t]  = r / static_cast<float>(P);
+        s_r[t]              = r;
+      }
+      __syncthreads();
+      if (t < P * 12) { // rebuild the DM-RS of (port, RE) from the shifts within 10 dB of the strongest
+        const uint32_t p = t / 12, n = t % 12;
+        float          mx = s_r[0];
+        for (uint32_t k = 1; k != 12; ++k) {
+          mx = fmaxf(mx, s_r[k]);
+        }
+        const float th = mx / 10.0f;
+        float2      v  = make_float2(0.0f, 0.0f);
+        for (uint32_t k = 0; k != 12; ++k) {
+          if (s_r[k] > th) {
+            const float2 c = cmul(s_ch[p][k], tw[(k * n) % 12]);
+            v.x += c.x;
+            v.y += c.y;
+          }
+        }
+#pragma unroll
+        for (uint32_t s = 0; s != 7; ++s) {
+          if (s < nm) {
+            const float2 c = cmul(v, occ_w(nm, occi, s));
+            recon[s].x += c.x;
+            recon[s].y += c.y;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    float n_acc = 0.0f;
+    if (t < P * 12) {
+      const uint32_t p = t / 12, n = t % 12;
+#pragma unroll
+      for (uint32_t s = 0; s != 7; ++s) {
+        if (s < nm) {
+          const float2 x = Lm[s][p][n];
+          n_acc += norm2(make_float2(x.x - recon[s].x, x.y - recon[s].y));
+        }
+      }
+    }
+    noise += wave_sum(n_acc);
+    (h == 0 ? n_noise0 : n_noise1) = nm * P * 12;
+  }
+  epre /= static_cast<float>(n_epre);
+  noise /= static_cast<float>(n_noise0 + n_noise1);
+  const bool noise_normal = isfinite(noise) && noise >= 1.17549435e-38f;
+  for (uint32_t e = t; e < d.nof_entries; e += 64) {
+    const srs_amd_pucch_f1_entry en = entries[d.entry0 + e];
+    const uint32_t               o = en.time_domain_occ, k = en.initial_cyclic_shift;
+    float                        main  = h_main[0][o][k];
+    float2                       cross = h_cross[0][o][k];
+    float                        rsrp  = h_rsrp[0][o][k];
+    if (d.nof_hops == 2) {
+      main += h_main[1][o][k];
+      cross.x += h_cross[1][o][k].x;
+      cross.y += h_cross[1][o][k].y;
+      rsrp = (rsrp * static_cast<float>(n_noise0) + h_rsrp[1][o][k] * static_cast<float>(n_noise1)) /
+             static_cast<float>(n_noise0 + n_noise1);
+    }
+    const float sinr = noise_normal ? rsrp / noise : 0.0f;
+    uint8_t     bits[2];
+    const float det    = f1_detect_symbol(en.nof_harq_ack == 0 ? 1 : en.nof_harq_ack, cross, bits);
+    const float metric = (main + 2.0f * det) / noise;
+    const bool  ok     = metric > d.threshold;
+    srs_amd_pucch_result r{};
+    r.status = ok && (en.nof_harq_ack != 0 || bits[0] == 0) ? SRS_AMD_UCI_STATUS_VALID : SRS_AMD_UCI_STATUS_INVALID;
+    r.nof_harq_ack = en.nof_harq_ack;
+    r.harq_ack[0]  = en.nof_harq_ack > 0 ? bits[0] : 0;
+    r.harq_ack[1]  = en.nof_harq_ack > 1 ? bits[1] : 0;
+    r.detection_metric      = metric / d.threshold;
+    r.sinr_dB               = to_dB(sinr);
+    r.rsrp_dB               = to_dB(rsrp);
+    r.epre_dB               = to_dB(epre);
+    results[d.entry0 + e]   = r;
+  }
+}
+
 } // namespace
+
+hipError_t launch_pucch_f1(const pucch_f1_desc* d_desc, uint32_t nof, const srs_amd_pucch_f1_entry* d_entries,
+                           srs_amd_pucch_result* d_results, hipStream_t stream)
+{
+  if (nof == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(pucch_f1_kernel, dim3(nof), dim3(64), 0, stream, d_desc, d_entries, d_results);
+  return hipGetLastError();
+}
 
 hipError_t launch_pucch_f0(const pucch_f0_desc* d_desc, uint32_t nof, srs_amd_pucch_f0_result* d_results,
                            hipStream_t stream)

@@ -6,6 +6,11 @@
 // alpha = (m0 + m_cs + n_cs) mod 12, n_cs = sum_m 2^m c(8 (14 n_slot + l) + m) of the Gold sequence of n_id
 // (pucch_helper::get_alpha_index), and its low-PAPR sequence (srs_amd_low_papr_sequence x e^(j 2 pi alpha n / 12));
 // device side: pucch_f0_kernel.
+//
+// Format 1 (pucch_detector_format1.cpp:156-663 behind pucch_processor_impl.cpp:74-138): per batch, the checks of
+// validate_config (:57-98) and of the processor's PDU validator, the threshold by ports x hops (:194-212), the base
+// cyclic shift n_cs of every allocated symbol (get_alpha_index with m0 = m_cs = 0, :562), the base sequence of group
+// n_id mod 30 and the set of OCC indices in use; device side: pucch_f1_kernel.
 #include "srsran_amd/pucch.h"
 #include "srsran_amd/low_papr.h"
 
@@ -192,6 +197,84 @@ int make_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f0_pdu& p
   return SRS_AMD_OK;
 }
 
+int make_f1_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f1_batch& b, const uint32_t* d_grids,
+                 uint64_t grid_stride, uint32_t nof_grids, uint32_t nof_grid_ports, uint32_t nof_subc, uint32_t entry0,
+                 pucch_f1_desc& d)
+{
+  if (b.start_symbol_index > 10 || b.nof_symbols < 4 || b.nof_symbols > 14 ||
+      b.start_symbol_index + b.nof_symbols > NSYMB) {
+    return fail(SRS_AMD_EINVAL, "Invalid Format 1 symbols (start %u, %u symbols).", b.start_symbol_index,
+                b.nof_symbols);
+  }
+  if (b.numerology > 4 || b.slot_index >= (10u << b.numerology) || b.n_id > 1023) {
+    return fail(SRS_AMD_EINVAL, "Invalid Format 1 batch (slot %u, numerology %u, n_id %u).", b.slot_index,
+                b.numerology, b.n_id);
+  }
+  const uint32_t hops = b.second_hop_prb >= 0 ? 2u : 1u;
+  const uint32_t contributions = b.nof_ports * hops;
+  if (b.nof_ports == 0 || b.nof_ports > 4 ||
+      (contributions != 1 && contributions != 2 && contributions != 4 && contributions != 8)) {
+    return fail(SRS_AMD_EINVAL, "The PUCCH detector does not support %u ports.", b.nof_ports);
+  }
+  if (b.nof_entries == 0 || b.nof_entries > PUCCH_F1_MAX_ENTRIES || b.entries == nullptr) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of multiplexed PUCCH (i.e., %u).", b.nof_entries);
+  }
+  if (b.d_grid == nullptr && (d_grids == nullptr || b.grid >= nof_grids)) {
+    return fail(SRS_AMD_EINVAL, "grid index %u out of range (or no grid).", b.grid);
+  }
+  d             = pucch_f1_desc{};
+  d.grid        = b.d_grid != nullptr ? b.d_grid : d_grids + b.grid * grid_stride;
+  d.port_stride = NSYMB * nof_subc;
+  d.nof_subc    = nof_subc;
+  d.l0          = b.start_symbol_index;
+  d.nsym        = b.nof_symbols;
+  d.nof_hops    = hops;
+  for (uint32_t h = 0; h != hops; ++h) {
+    const uint32_t prb = h == 0 ? b.starting_prb : static_cast<uint32_t>(b.second_hop_prb);
+    if (prb > 274 || 12 * (prb + 1) > nof_subc) {
+      return fail(SRS_AMD_EINVAL, "PRB %u outside the grid.", prb);
+    }
+    d.subc0[h] = 12 * prb;
+  }
+  d.nof_ports = b.nof_ports;
+  for (uint32_t i = 0; i != b.nof_ports; ++i) {
+    if (b.ports[i] >= nof_grid_ports) {
+      return fail(SRS_AMD_EINVAL, "port %u outside the grid's %u ports.", b.ports[i], nof_grid_ports);
+    }
+    d.ports[i] = b.ports[i];
+  }
+  const uint32_t occ_ratio = hops == 2 ? 4u : 2u;
+  uint32_t       used[7]   = {};
+  for (uint32_t e = 0; e != b.nof_entries; ++e) {
+    const srs_amd_pucch_f1_entry& en = b.entries[e];
+    if (en.initial_cyclic_shift > 11 || en.time_domain_occ > 6 || en.time_domain_occ >= b.nof_symbols / occ_ratio ||
+        en.nof_harq_ack > 2) {
+      return fail(SRS_AMD_EINVAL, "Invalid multiplexed PUCCH (shift %u, OCC %u, %u HARQ-ACK bits, %u symbols).",
+                  en.initial_cyclic_shift, en.time_domain_occ, en.nof_harq_ack, b.nof_symbols);
+    }
+    if ((used[en.time_domain_occ] >> en.initial_cyclic_shift) & 1u) {
+      return fail(SRS_AMD_EINVAL, "Two PUCCH with shift %u and OCC %u.", en.initial_cyclic_shift, en.time_domain_occ);
+    }
+    used[en.time_domain_occ] |= 1u << en.initial_cyclic_shift;
+    d.occ_mask |= 1u << en.time_domain_occ;
+  }
+  d.nof_entries = b.nof_entries;
+  d.entry0      = entry0;
+  d.threshold   = contributions == 1 ? 0.9f : contributions == 2 ? 3.0f : contributions == 4 ? 4.45f : 6.95f;
+  for (uint32_t r = 0; r != b.nof_symbols; ++r) {
+    d.alpha[r] = static_cast<uint8_t>(
+        gold_byte(proc->jump, b.n_id, 8 * (NSYMB * b.slot_index + b.start_symbol_index + r)) % 12);
+  }
+  float base[24];
+  if (srs_amd_low_papr_sequence(base, 12, b.n_id % 30, 0) != SRS_AMD_OK) {
+    return SRS_AMD_EINVAL;
+  }
+  for (uint32_t k = 0; k != 12; ++k) {
+    d.base[k] = make_float2(base[2 * k], base[2 * k + 1]);
+  }
+  return SRS_AMD_OK;
+}
+
 } // namespace
 
 extern "C" {
@@ -308,6 +391,115 @@ int srs_amd_pucch_f0_detect(srs_amd_pucch_processor*    proc,
                                         proc->host_res.as<srs_amd_pucch_f0_result>(), proc->stream);
   if (rc == SRS_AMD_OK) {
     e  = hipMemcpyAsync(result, proc->host_res.ptr, sizeof(*result), hipMemcpyDeviceToHost, proc->stream);
+    e  = e == hipSuccess ? hipStreamSynchronize(proc->stream) : e;
+    rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUCCH result download");
+  } else {
+    (void)hipStreamSynchronize(proc->stream);
+  }
+  return rc;
+}
+
+int srs_amd_pucch_f1_detect_slot(srs_amd_pucch_processor*      proc,
+                                 const srs_amd_pucch_f1_batch* batches,
+                                 uint32_t                      nof_batches,
+                                 const uint32_t*               d_grids,
+                                 uint64_t                      grid_stride,
+                                 uint32_t                      nof_grids,
+                                 uint32_t                      nof_grid_ports,
+                                 uint32_t                      nof_subc,
+                                 srs_amd_pucch_result*         d_results,
+                                 void*                         stream)
+{
+  if (proc == nullptr || (nof_batches != 0 && (batches == nullptr || d_results == nullptr))) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_batches == 0) {
+    return SRS_AMD_OK;
+  }
+  if (nof_subc == 0 || nof_subc % 12 != 0) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of grid subcarriers (i.e., %u).", nof_subc);
+  }
+  std::lock_guard<std::mutex>         lock(proc->mtx);
+  std::vector<pucch_f1_desc>          desc(nof_batches);
+  std::vector<srs_amd_pucch_f1_entry> ent;
+  for (uint32_t i = 0; i != nof_batches; ++i) {
+    const int rc = make_f1_desc(proc, batches[i], d_grids, grid_stride, nof_grids, nof_grid_ports, nof_subc,
+                                static_cast<uint32_t>(ent.size()), desc[i]);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+    ent.insert(ent.end(), batches[i].entries, batches[i].entries + batches[i].nof_entries);
+  }
+  const size_t dbytes = sizeof(pucch_f1_desc) * nof_batches;
+  const size_t ebytes = sizeof(srs_amd_pucch_f1_entry) * ent.size();
+  const size_t eoff   = (dbytes + 255) & ~size_t(255);
+  const size_t bytes  = eoff + ebytes;
+  auto         s      = static_cast<hipStream_t>(stream);
+  hipError_t   e      = hipSetDevice(proc->device);
+  if (e == hipSuccess) {
+    e = proc->buf.ensure(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->stage.acquire(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->order.begin(s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUCCH processor scratch");
+  }
+  call_scope scope(proc->order, nullptr, s);
+  std::memcpy(proc->stage.at<uint8_t>(0), desc.data(), dbytes);
+  std::memcpy(proc->stage.at<uint8_t>(eoff), ent.data(), ebytes);
+  e = proc->stage.upload(proc->buf.ptr, bytes, s);
+  if (e == hipSuccess) {
+    e = launch_pucch_f1(proc->buf.as<pucch_f1_desc>(),
+                        nof_batches,
+                        reinterpret_cast<const srs_amd_pucch_f1_entry*>(proc->buf.as<uint8_t>() + eoff),
+                        d_results,
+                        s);
+  }
+  const int        rc   = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pucch_f1_kernel launch");
+  const hipError_t done = scope.close();
+  return rc != SRS_AMD_OK ? rc : (done == hipSuccess ? SRS_AMD_OK : hip_fail(done, "PUCCH completion event"));
+}
+
+int srs_amd_pucch_f1_detect(srs_amd_pucch_processor*      proc,
+                            const srs_amd_pucch_f1_batch* batch,
+                            const uint32_t*               grid,
+                            uint32_t                      nof_ports,
+                            uint32_t                      nof_subc,
+                            srs_amd_pucch_result*         results)
+{
+  if (proc == nullptr || batch == nullptr || grid == nullptr || results == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (batch->nof_entries == 0 || batch->nof_entries > PUCCH_F1_MAX_ENTRIES) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of multiplexed PUCCH (i.e., %u).", batch->nof_entries);
+  }
+  const size_t                bytes = sizeof(uint32_t) * nof_ports * NSYMB * nof_subc;
+  const size_t                rbytes = sizeof(srs_amd_pucch_result) * batch->nof_entries;
+  std::lock_guard<std::mutex> host_lock(proc->host_mtx);
+  hipError_t                  e = hipSetDevice(proc->device);
+  if (e == hipSuccess) {
+    e = proc->host_grid.ensure(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->host_res.ensure(rbytes);
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(proc->host_grid.ptr, grid, bytes, hipMemcpyHostToDevice, proc->stream);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUCCH grid upload");
+  }
+  srs_amd_pucch_f1_batch b = *batch;
+  b.grid                   = 0;
+  b.d_grid                 = nullptr;
+  int rc = srs_amd_pucch_f1_detect_slot(proc, &b, 1, proc->host_grid.as<uint32_t>(), 0, 1, nof_ports, nof_subc,
+                                        proc->host_res.as<srs_amd_pucch_result>(), proc->stream);
+  if (rc == SRS_AMD_OK) {
+    e  = hipMemcpyAsync(results, proc->host_res.ptr, rbytes, hipMemcpyDeviceToHost, proc->stream);
     e  = e == hipSuccess ? hipStreamSynchronize(proc->stream) : e;
     rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUCCH result download");
   } else {

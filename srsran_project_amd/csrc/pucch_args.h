@@ -1,5 +1,5 @@
-// pucch_args.h -- per-PDU descriptor of the PUCCH Format 0 detector kernel (pucch.hip), built by the C-ABI
-// (pucch_api.cpp).
+// pucch_args.h -- per-PDU / per-batch descriptors of the PUCCH Format 0 and Format 1 detector kernels (pucch.hip),
+// built by the C-ABI (pucch_api.cpp).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -31,5 +31,28 @@ struct pucch_f0_desc {
 // Detection of every PDU (one 64-thread workgroup per PDU), results into d_results.
 hipError_t launch_pucch_f0(const pucch_f0_desc* d_desc, uint32_t nof, srs_amd_pucch_f0_result* d_results,
                            hipStream_t stream);
+
+constexpr uint32_t PUCCH_F1_MAX_ENTRIES = 84; // 12 initial cyclic shifts x 7 time-domain OCCs
+
+struct pucch_f1_desc {
+  const uint32_t* grid;        // cbf16 [port][14][nof_subc]
+  uint32_t        port_stride; // 14 x nof_subc
+  uint32_t        nof_subc;
+  uint32_t        l0, nsym;    // allocation: first symbol and 4 .. 14 symbols
+  uint32_t        nof_hops;    // 1, or 2 with frequency hopping
+  uint32_t        subc0[2];    // first subcarrier of each hop
+  uint32_t        nof_ports;
+  uint32_t        ports[4];
+  uint32_t        occ_mask;    // time-domain OCC indices in use
+  uint32_t        nof_entries;
+  uint32_t        entry0;      // first entry / result of the batch
+  float           threshold;   // by ports x hops (pucch_detector_format1.cpp:194-212)
+  uint8_t         alpha[14];   // base cyclic shift n_cs of each allocated symbol (m0 = m_cs = 0)
+  float2          base[12];    // low-PAPR base sequence of group n_id mod 30
+};
+
+// Detection of every batch (one 64-thread workgroup per batch); entries[] of all batches, results alike.
+hipError_t launch_pucch_f1(const pucch_f1_desc* d_desc, uint32_t nof, const srs_amd_pucch_f1_entry* d_entries,
+                           srs_amd_pucch_result* d_results, hipStream_t stream);
 
 } // namespace srs_amd

@@ -1,8 +1,10 @@
-"""Host-side mirror of srsRAN's PUCCH Format 0 detector over the MI355X C-ABI (include/srsran_amd/pucch.h).
+"""Host-side mirror of srsRAN's PUCCH Format 0 / Format 1 detectors over the MI355X C-ABI (include/srsran_amd/pucch.h).
 
-Reference interface: pucch_detector::detect(const resource_grid_reader&, const format0_configuration&)
+Reference interfaces: pucch_detector::detect(const resource_grid_reader&, const format0_configuration&)
 (include/srsran/phy/upper/channel_processors/pucch/pucch_detector.h:44-77, impl pucch_detector_format0.cpp:124-246),
-the Format 0 branch of pucch_processor::process.  Grids are cbf16 [port][14][nof_subc]: numpy uint32 for the host
+the Format 0 branch of pucch_processor::process; pucch_detector::detect(grid, format1_configuration,
+pucch_format1_map<unsigned>) (pucch_detector.h:86-118, 155-160, impl pucch_detector_format1.cpp:156-663) behind
+pucch_processor::process(grid, format1_batch_configuration) (pucch_processor_impl.cpp:74-138).  Grids are cbf16 [port][14][nof_subc]: numpy uint32 for the host
 form, torch int32 [n][port][14][nof_subc] on the device for the slot form.
 """
 import ctypes
@@ -24,17 +26,33 @@ class PucchF0Pdu(ctypes.Structure):
                 ("d_grid", ctypes.c_void_p)]
 
 
-class PucchF0Result(ctypes.Structure):
+class PucchResult(ctypes.Structure):
     _fields_ = [("status", ctypes.c_uint32), ("nof_sr", ctypes.c_uint32), ("nof_harq_ack", ctypes.c_uint32),
                 ("sr", ctypes.c_uint8), ("harq_ack", ctypes.c_uint8 * 2), ("reserved", ctypes.c_uint8),
                 ("detection_metric", ctypes.c_float), ("sinr_dB", ctypes.c_float), ("rsrp_dB", ctypes.c_float),
                 ("epre_dB", ctypes.c_float)]
 
 
+PucchF0Result = PucchResult
+
+
+class PucchF1Entry(ctypes.Structure):
+    _fields_ = [("initial_cyclic_shift", ctypes.c_uint8), ("time_domain_occ", ctypes.c_uint8),
+                ("nof_harq_ack", ctypes.c_uint8), ("reserved", ctypes.c_uint8)]
+
+
+class PucchF1Batch(ctypes.Structure):
+    _fields_ = [("numerology", ctypes.c_uint32), ("slot_index", ctypes.c_uint32), ("starting_prb", ctypes.c_uint32),
+                ("second_hop_prb", ctypes.c_int32), ("start_symbol_index", ctypes.c_uint32),
+                ("nof_symbols", ctypes.c_uint32), ("n_id", ctypes.c_uint32), ("nof_ports", ctypes.c_uint32),
+                ("ports", ctypes.c_uint8 * 4), ("nof_entries", ctypes.c_uint32), ("entries", ctypes.c_void_p),
+                ("grid", ctypes.c_uint32), ("d_grid", ctypes.c_void_p)]
+
+
 RESULT_DTYPE = np.dtype([("status", "<u4"), ("nof_sr", "<u4"), ("nof_harq_ack", "<u4"), ("sr", "u1"),
                          ("harq_ack", "u1", (2,)), ("reserved", "u1"), ("detection_metric", "<f4"),
                          ("sinr_dB", "<f4"), ("rsrp_dB", "<f4"), ("epre_dB", "<f4")])
-assert RESULT_DTYPE.itemsize == ctypes.sizeof(PucchF0Result)
+assert RESULT_DTYPE.itemsize == ctypes.sizeof(PucchResult)
 
 
 def make_f0_pdu(*, numerology=0, slot_index=0, starting_prb=0, second_hop_prb=None, start_symbol_index=12,
@@ -56,6 +74,29 @@ def make_f0_pdu(*, numerology=0, slot_index=0, starting_prb=0, second_hop_prb=No
     return p
 
 
+def make_f1_batch(entries, *, numerology=0, slot_index=0, starting_prb=0, second_hop_prb=None,
+                  start_symbol_index=0, nof_symbols=14, n_id=0, ports=(0,), grid=0):
+    """pucch_processor::format1_batch_configuration: the common allocation and entries = [(initial cyclic shift,
+    time-domain OCC, nof_harq_ack)].  The entry array is kept alive by the returned batch (attribute _entries)."""
+    b = PucchF1Batch()
+    b.numerology, b.slot_index, b.starting_prb = int(numerology), int(slot_index), int(starting_prb)
+    b.second_hop_prb = -1 if second_hop_prb is None else int(second_hop_prb)
+    b.start_symbol_index, b.nof_symbols, b.n_id = int(start_symbol_index), int(nof_symbols), int(n_id)
+    if not 1 <= len(ports) <= 4:
+        raise ValueError("1 to 4 ports")
+    b.nof_ports = len(ports)
+    for i, q in enumerate(ports):
+        b.ports[i] = int(q)
+    arr = (PucchF1Entry * max(len(entries), 1))()
+    for i, (ics, occ, nh) in enumerate(entries):
+        arr[i].initial_cyclic_shift, arr[i].time_domain_occ, arr[i].nof_harq_ack = int(ics), int(occ), int(nh)
+    b.nof_entries = len(entries)
+    b.entries = ctypes.addressof(arr)
+    b._entries = arr
+    b.grid = int(grid)
+    return b
+
+
 def _declare(lib):
     c = ctypes
     P = c.c_void_p
@@ -65,6 +106,9 @@ def _declare(lib):
         "srs_amd_pucch_f0_detect_slot": (c.c_int, [P, P, c.c_uint32, P, c.c_uint64, c.c_uint32, c.c_uint32,
                                                    c.c_uint32, P, P]),
         "srs_amd_pucch_f0_detect": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P]),
+        "srs_amd_pucch_f1_detect_slot": (c.c_int, [P, P, c.c_uint32, P, c.c_uint64, c.c_uint32, c.c_uint32,
+                                                   c.c_uint32, P, P]),
+        "srs_amd_pucch_f1_detect": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -109,7 +153,7 @@ class PucchProcessor:
         """pucch_detector::detect of one Format 0 PDU on a host grid (numpy uint32 [ports][14][nof_subc])."""
         if grid.dtype != np.uint32 or grid.ndim != 3 or grid.shape[1] != 14 or not grid.flags.c_contiguous:
             raise ValueError("grid must be a C-contiguous uint32 array [ports][14][nof_subc]")
-        r = PucchF0Result()
+        r = PucchResult()
         _lib.check(self._lib.srs_amd_pucch_f0_detect(self._h, ctypes.byref(pdu), grid.ctypes.data, grid.shape[0],
                                                      grid.shape[2], ctypes.byref(r)), "pucch f0 detect")
         return r
@@ -127,6 +171,31 @@ class PucchProcessor:
             self._h, arr, len(pdus), grids.data_ptr(), grids.stride(0), grids.shape[0], grids.shape[1],
             grids.shape[-1], out.data_ptr(), ctypes.c_void_p(stream.cuda_stream)), "pucch f0 detect_slot")
         return out
+
+    def detect_f1(self, grid, batch):
+        """pucch_processor::process of one Format 1 batch on a host grid (numpy uint32 [ports][14][nof_subc]);
+        returns one PucchResult per entry, in entry order."""
+        if grid.dtype != np.uint32 or grid.ndim != 3 or grid.shape[1] != 14 or not grid.flags.c_contiguous:
+            raise ValueError("grid must be a C-contiguous uint32 array [ports][14][nof_subc]")
+        out = (PucchResult * max(batch.nof_entries, 1))()
+        _lib.check(self._lib.srs_amd_pucch_f1_detect(self._h, ctypes.byref(batch), grid.ctypes.data, grid.shape[0],
+                                                     grid.shape[2], out), "pucch f1 detect")
+        return list(out)[:batch.nof_entries]
+
+    def detect_f1_slot(self, grids, batches, stream=None):
+        """Every Format 1 batch of a slot on device grids (torch int32 [n][ports][14][nof_subc]); returns a torch
+        uint8 tensor of RESULT_DTYPE records, the entries of all batches in order (asynchronous on stream)."""
+        import torch
+
+        arr = (PucchF1Batch * len(batches))(*batches)
+        total = sum(b.nof_entries for b in batches)
+        out = torch.zeros((max(total, 1), RESULT_DTYPE.itemsize), dtype=torch.uint8, device=grids.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(grids.device)
+        _lib.check(self._lib.srs_amd_pucch_f1_detect_slot(
+            self._h, arr, len(batches), grids.data_ptr(), grids.stride(0), grids.shape[0], grids.shape[1],
+            grids.shape[-1], out.data_ptr(), ctypes.c_void_p(stream.cuda_stream)), "pucch f1 detect_slot")
+        return out[:total]
 
 
 def parse_results(raw):

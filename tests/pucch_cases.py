@@ -35,3 +35,43 @@ def cases(n=24, seed=0):
         op.transmit(grid, pdu, None if sent is None else table[sent][0], gains, noise, rng)
         out.append((pdu, grid, sent))
     return out
+
+
+def f1_cases(n=16, seed=0):
+    """[(batch, grid uint32 [4][14][NSUBC], {(shift, occ): transmitted bits})]: 4-14 symbols from symbols 0-10, with
+    and without frequency hopping, 1 / 2 / 4 ports, 1-6 multiplexed PUCCHs of 0-2 HARQ-ACK bits of which some are
+    silent (DTX), noise variance 0.01-3 against unit-power channel taps."""
+    from oracle import pucch as op
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        hop = bool(rng.integers(0, 2))
+        nports = [1, 2, 4][int(rng.integers(0, 3))]
+        start = int(rng.integers(0, 11))
+        nsym = int(rng.integers(4, 15 - start))
+        mu = int(rng.integers(0, 3))
+        nocc = nsym // (4 if hop else 2)
+        k = int(rng.integers(1, 7))
+        coords = set()
+        while len(coords) < k:
+            coords.add((int(rng.integers(0, 12)), int(rng.integers(0, nocc))))
+        entries = [(ics, o, int(rng.integers(0, 3))) for ics, o in sorted(coords, key=lambda c: rng.random())]
+        b = amd.pucch.make_f1_batch(entries, numerology=mu, slot_index=int(rng.integers(0, 10 << mu)),
+                                    starting_prb=int(rng.integers(0, 52)),
+                                    second_hop_prb=int(rng.integers(0, 52)) if hop else None,
+                                    start_symbol_index=start, nof_symbols=nsym, n_id=int(rng.integers(0, 1024)),
+                                    ports=tuple(int(x) for x in rng.permutation(4)[:nports]))
+        sent = {}
+        pucchs = []
+        for ics, o, nh in entries:
+            if rng.random() < 0.2:
+                continue  # DTX
+            bits = [int(x) for x in rng.integers(0, 2, nh)]
+            sent[(ics, o)] = bits
+            gains = (rng.normal(size=nports) + 1j * rng.normal(size=nports)) / np.sqrt(2)
+            pucchs.append((ics, o, bits, gains))
+        grid = rng.integers(0, 1 << 32, (4, 14, NSUBC), dtype=np.uint64).astype(np.uint32)
+        op.transmit_f1(grid, b, pucchs, [0.01, 0.1, 1.0, 3.0][i % 4], rng)
+        out.append((b, grid, sent))
+    return out

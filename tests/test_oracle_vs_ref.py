@@ -541,3 +541,21 @@ def test_pucch_f0_restatement_matches_reference():
         np.testing.assert_allclose(r.detection_metric, metric, rtol=1e-3, err_msg=str(i))
         for a, b in ((r.sinr_dB, sinr), (r.rsrp_dB, rsrp), (r.epre_dB, epre)):
             assert abs(a - b) <= 0.01, (i, a, b)
+
+
+def test_pucch_f1_restatement_matches_reference():
+    """oracle/pucch.py detect_f1 gives the compiled pucch_detector_format1's status and HARQ-ACK bits for every
+    multiplexed PUCCH of every batch, and its normalised metric / CSI within 1e-3 relative / 0.01 dB."""
+    from oracle import pucch as op
+    from tests.pucch_cases import f1_cases
+
+    for i, (b, grid, sent) in enumerate(f1_cases()):
+        ref = op.ref_detect_f1(grid, b)
+        mine = op.detect_f1(grid, b, [(e.initial_cyclic_shift, e.time_domain_occ, e.nof_harq_ack)
+                                      for e in b._entries[:b.nof_entries]])
+        for j, (r, (st, bits, metric, sinr, rsrp, epre)) in enumerate(zip(ref, mine)):
+            assert r.status == st, (i, j, r.status, st, metric)
+            assert list(r.harq_ack)[:r.nof_harq_ack] == bits, (i, j)
+            np.testing.assert_allclose(r.detection_metric, metric, rtol=1e-3, err_msg=str((i, j)))
+            for a, c in ((r.sinr_dB, sinr), (r.rsrp_dB, rsrp), (r.epre_dB, epre)):
+                assert abs(a - c) <= 0.01, (i, j, a, c)
