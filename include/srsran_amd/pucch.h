@@ -12,6 +12,11 @@
  * strongest dropped), the noise from the DM-RS minus its reconstruction, and per multiplexed PUCCH the BPSK / QPSK
  * symbol, the detection metric against the reference's threshold and the CSI.
  *
+ * Format 2: for every PDU of a slot, the DM-RS channel estimate of every receive port (port_channel_estimator_average
+ * with the frequency-domain filter, time-domain averaging and CFO compensation, per hop), ZF equalization of the data
+ * REs over the ports, QPSK soft demapping, descrambling, and the UCI decoder (short block or polar) -- payload bits,
+ * status and the CSI (SINR, RSRP, EPRE, time alignment, CFO).
+ *
  * Replaces (reference interface):
  *   pucch_detector::detect(const resource_grid_reader&, const format0_configuration&)
  *       include/srsran/phy/upper/channel_processors/pucch/pucch_detector.h:44-77 (format0_configuration)
@@ -24,6 +29,12 @@
  *       include/srsran/phy/upper/pucch_orthogonal_sequence.h), and
  *   pucch_processor::process(const resource_grid_reader&, const format1_batch_configuration&)
  *       pucch_processor_impl.cpp:74-138.
+ *   pucch_processor::process(const resource_grid_reader&, const format2_configuration&)
+ *       pucch_processor_impl.cpp:140-220 (dmrs_pucch_estimator_format2.cpp, port_channel_estimator_average_impl.cpp
+ *       with filter / average / CFO compensation as signal_processors/pucch/factories.cpp:52-56 builds it,
+ *       pucch_demodulator_format2.cpp with the ZF equalizer of upper_phy_factories.cpp:676-677,
+ *       uci_decoder_impl.cpp).  The reference's demodulator reads grid ports 0 .. n-1 while its estimator reads
+ *       ports[]; here both read ports[] (identical when ports[] = 0 .. n-1).
  * The slot forms detect every PDU / batch of many cells' grids in one launch.  Grids are cbf16 [port][14][nof_subc].
  * Message bits and status equal the reference's; the CSI values are float measurements (tests/test_pucch_gpu.py
  * states the tolerance).
@@ -125,6 +136,79 @@ int srs_amd_pucch_f0_detect(srs_amd_pucch_processor*    proc,
                             uint32_t                    nof_ports,
                             uint32_t                    nof_subc,
                             srs_amd_pucch_f0_result*    result);
+
+/* pucch_processor::format2_configuration (pucch_processor.h:223-275). */
+typedef struct srs_amd_pucch_f2_pdu {
+  uint32_t numerology;
+  uint32_t slot_index;
+  uint32_t bwp_start_rb;
+  uint32_t bwp_size_rb;
+  uint32_t starting_prb;        /* within the BWP */
+  int32_t  second_hop_prb;      /* within the BWP; -1: no frequency hopping */
+  uint32_t nof_prb;             /* 1 .. 16 */
+  uint32_t start_symbol_index;
+  uint32_t nof_symbols;         /* 1 or 2 */
+  uint32_t rnti;
+  uint32_t n_id;                /* data scrambling identity */
+  uint32_t n_id_0;              /* DM-RS scrambling identity */
+  uint32_t nof_harq_ack;
+  uint32_t nof_sr;
+  uint32_t nof_csi_part1;
+  uint32_t nof_csi_part2;       /* must be 0, as the reference's validator requires */
+  uint32_t nof_ports;           /* 1 .. 4 */
+  uint8_t  ports[4];
+  uint32_t grid;                /* index of the grid in d_grids */
+  const uint32_t* d_grid;       /* non-NULL: this PDU's own DEVICE grid instead of d_grids[grid] */
+} srs_amd_pucch_f2_pdu;
+
+/* pucch_processor_result of Formats 2 / 3 / 4: the UCI status and the CSI; the payload bits (HARQ-ACK, SR, CSI part 1,
+ * CSI part 2, one per byte) go to a separate row. */
+typedef struct srs_amd_pucch_uci_result {
+  uint32_t status;              /* SRS_AMD_UCI_STATUS_* */
+  uint32_t nof_harq_ack;
+  uint32_t nof_sr;
+  uint32_t nof_csi_part1;
+  uint32_t nof_csi_part2;
+  float    sinr_dB;
+  float    rsrp_dB;
+  float    epre_dB;
+  float    time_alignment_s;    /* phy_time_unit of the best-SNR port, in seconds */
+  float    cfo_Hz;              /* NaN: not measured */
+} srs_amd_pucch_uci_result;
+
+/* DEVICE, asynchronous: every Format 2 PDU of a slot; result i to d_results[i], its payload bits to
+ * d_payloads + i * payload_stride. */
+int srs_amd_pucch_f2_process_slot(srs_amd_pucch_processor*    proc,
+                                  const srs_amd_pucch_f2_pdu* pdus,
+                                  uint32_t                    nof_pdus,
+                                  const uint32_t*             d_grids,
+                                  uint64_t                    grid_stride,
+                                  uint32_t                    nof_grids,
+                                  uint32_t                    nof_grid_ports,
+                                  uint32_t                    nof_subc,
+                                  srs_amd_pucch_uci_result*   d_results,
+                                  uint8_t*                    d_payloads,
+                                  uint64_t                    payload_stride,
+                                  void*                       stream);
+
+/* HOST, synchronous: one PDU on a host grid [nof_ports][14][nof_subc]; payload[nof bits]. */
+int srs_amd_pucch_f2_process(srs_amd_pucch_processor*    proc,
+                             const srs_amd_pucch_f2_pdu* pdu,
+                             const uint32_t*             grid,
+                             uint32_t                    nof_ports,
+                             uint32_t                    nof_subc,
+                             srs_amd_pucch_uci_result*   result,
+                             uint8_t*                    payload);
+
+/* HOST, synchronous: the estimator and demodulator of one Format 2 PDU -- pucch_demodulator::demodulate
+ * (pucch_demodulator.h, impl pucch_demodulator_format2.cpp:92-160) after dmrs_pucch_estimator::estimate --
+ * llrs[16 nof_prb nof_symbols], descrambled. */
+int srs_amd_pucch_f2_demodulate(srs_amd_pucch_processor*    proc,
+                                const srs_amd_pucch_f2_pdu* pdu,
+                                const uint32_t*             grid,
+                                uint32_t                    nof_ports,
+                                uint32_t                    nof_subc,
+                                int8_t*                     llrs);
 
 /* DEVICE, asynchronous: every Format 1 batch of a slot detected; the result of entry e of batch b goes to
  * d_results[nof_entries(0) + ... + nof_entries(b - 1) + e]. */

@@ -1,0 +1,487 @@
+// pucch_processor_hip.cpp -- see pucch_processor_hip.h.
+#include "pucch_processor_hip.h"
+#include "hip_resource_grid.h"
+
+#include "srsran/phy/support/resource_grid_reader.h"
+#include "srsran_amd/pucch.h"
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+using namespace srsran;
+using namespace srsran::hip;
+
+namespace {
+
+constexpr unsigned NSYMB = 14;
+
+void log_error(const char* what, const std::string& detail)
+{
+  std::fprintf(stderr, "pucch_processor_hip: %s: %s\n", what, detail.c_str());
+}
+
+uint32_t numerology_of(slot_point slot)
+{
+  return to_numerology_value(slot.scs());
+}
+
+srs_amd_pucch_f0_pdu convert(const pucch_processor::format0_configuration& c)
+{
+  srs_amd_pucch_f0_pdu p{};
+  p.numerology           = numerology_of(c.slot);
+  p.slot_index           = c.slot.slot_index();
+  p.starting_prb         = c.bwp_start_rb + c.starting_prb;
+  p.second_hop_prb       = c.second_hop_prb.has_value() ? static_cast<int32_t>(c.bwp_start_rb + *c.second_hop_prb) : -1;
+  p.start_symbol_index   = c.start_symbol_index;
+  p.nof_symbols          = c.nof_symbols;
+  p.initial_cyclic_shift = c.initial_cyclic_shift;
+  p.n_id                 = c.n_id;
+  p.nof_harq_ack         = c.nof_harq_ack;
+  p.sr_opportunity       = c.sr_opportunity ? 1 : 0;
+  p.nof_ports            = static_cast<uint32_t>(c.ports.size());
+  for (unsigned i = 0; i != c.ports.size() && i != 4; ++i) {
+    p.ports[i] = c.ports[i];
+  }
+  return p;
+}
+
+srs_amd_pucch_f2_pdu convert(const pucch_processor::format2_configuration& c)
+{
+  srs_amd_pucch_f2_pdu p{};
+  p.numerology         = numerology_of(c.slot);
+  p.slot_index         = c.slot.slot_index();
+  p.bwp_start_rb       = c.bwp_start_rb;
+  p.bwp_size_rb        = c.bwp_size_rb;
+  p.starting_prb       = c.starting_prb;
+  p.second_hop_prb     = c.second_hop_prb.has_value() ? static_cast<int32_t>(*c.second_hop_prb) : -1;
+  p.nof_prb            = c.nof_prb;
+  p.start_symbol_index = c.start_symbol_index;
+  p.nof_symbols        = c.nof_symbols;
+  p.rnti               = c.rnti;
+  p.n_id               = c.n_id;
+  p.n_id_0             = c.n_id_0;
+  p.nof_harq_ack       = c.nof_harq_ack;
+  p.nof_sr             = c.nof_sr;
+  p.nof_csi_part1      = c.nof_csi_part1;
+  p.nof_csi_part2      = c.nof_csi_part2;
+  p.nof_ports          = static_cast<uint32_t>(c.ports.size());
+  for (unsigned i = 0; i != c.ports.size() && i != 4; ++i) {
+    p.ports[i] = c.ports[i];
+  }
+  return p;
+}
+
+struct shared_state {
+  srs_amd_pucch_processor*   proc   = nullptr;
+  int                        device = 0;
+  pucch_processor_hip_config cfg;
+  std::atomic<uint64_t>      nof_pdus{0}, nof_errors{0}, nof_device{0};
+  ~shared_state() { srs_amd_pucch_processor_destroy(proc); }
+};
+
+class pucch_processor_hip : public pucch_processor
+{
+public:
+  explicit pucch_processor_hip(std::shared_ptr<shared_state> s) : st(std::move(s))
+  {
+    (void)hipSetDevice(st->device);
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&d_res, RES_BYTES) != hipSuccess || hipHostMalloc(&h_res, RES_BYTES, hipHostMallocDefault) != hipSuccess) {
+      throw std::runtime_error("pucch_processor_hip: stream / result buffers");
+    }
+  }
+  ~pucch_processor_hip() override
+  {
+    (void)hipSetDevice(st->device);
+    (void)hipStreamSynchronize(stream);
+    (void)hipStreamDestroy(stream);
+    (void)hipFree(scratch);
+    (void)hipHostFree(stage);
+    (void)hipFree(d_res);
+    (void)hipHostFree(h_res);
+  }
+
+  pucch_processor_result process(const resource_grid_reader& grid, const format0_configuration& config) override
+  {
+    ++st->nof_pdus;
+    pucch_processor_result result;
+    result.message = pucch_uci_message({.nof_sr = config.sr_opportunity ? 1U : 0U,
+                                        .nof_harq_ack = config.nof_harq_ack, .nof_csi_part1 = 0, .nof_csi_part2 = 0});
+    result.message.set_status(uci_status::invalid);
+    srs_amd_pucch_f0_pdu p = convert(config);
+    unsigned             nof_ports = 0, nsubc = 0;
+    const uint32_t*      g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
+    auto*                r = static_cast<srs_amd_pucch_f0_result*>(h_res);
+    if (g == nullptr || !run([&] {
+          p.d_grid = g;
+          return srs_amd_pucch_f0_detect_slot(st->proc, &p, 1, nullptr, 0, 0, nof_ports, nsubc,
+                                              static_cast<srs_amd_pucch_f0_result*>(d_res), stream);
+        }, sizeof(srs_amd_pucch_f0_result))) {
+      return result;
+    }
+    result.message = pucch_uci_message({.nof_sr = r->nof_sr, .nof_harq_ack = r->nof_harq_ack, .nof_csi_part1 = 0,
+                                        .nof_csi_part2 = 0});
+    if (r->nof_sr != 0) {
+      result.message.get_sr_bits()[0] = r->sr;
+    }
+    for (unsigned i = 0; i != r->nof_harq_ack && i != 2; ++i) {
+      result.message.get_harq_ack_bits()[i] = r->harq_ack[i];
+    }
+    result.message.set_status(static_cast<uci_status>(r->status));
+    result.csi = channel_state_information(channel_state_information::sinr_type::post_equalization);
+    result.csi.set_sinr_dB(channel_state_information::sinr_type::post_equalization, r->sinr_dB);
+    result.csi.set_rsrp_dB(r->rsrp_dB);
+    result.csi.set_epre(r->epre_dB);
+    return result;
+  }
+
+  pucch_format1_map<pucch_processor_result> process(const resource_grid_reader&        grid,
+                                                    const format1_batch_configuration& batch) override
+  {
+    const format1_common_configuration& c = batch.common_config;
+    pucch_format1_map<pucch_processor_result> out;
+    std::vector<srs_amd_pucch_f1_entry>       entries;
+    for (const auto& e : batch.entries) {
+      entries.push_back({static_cast<uint8_t>(e.initial_cyclic_shift), static_cast<uint8_t>(e.time_domain_occ),
+                         static_cast<uint8_t>(e.value.nof_harq_ack), 0});
+      pucch_processor_result r;
+      r.message = pucch_uci_message({.nof_sr = 0, .nof_harq_ack = e.value.nof_harq_ack, .nof_csi_part1 = 0,
+                                     .nof_csi_part2 = 0});
+      r.message.set_status(uci_status::invalid);
+      out.insert(e.initial_cyclic_shift, e.time_domain_occ, r);
+    }
+    st->nof_pdus += entries.size();
+    // the reference's Format 1 detector reads every port of the grid, 0 .. nof_ports - 1
+    // (pucch_detector_format1.cpp:529, 568-583)
+    srs_amd_pucch_f1_batch b{};
+    b.numerology         = numerology_of(c.slot);
+    b.slot_index         = c.slot.slot_index();
+    b.starting_prb       = c.bwp_start_rb + c.starting_prb;
+    b.second_hop_prb     = c.second_hop_prb.has_value() ? static_cast<int32_t>(c.bwp_start_rb + *c.second_hop_prb) : -1;
+    b.start_symbol_index = c.start_symbol_index;
+    b.nof_symbols        = c.nof_symbols;
+    b.n_id               = c.n_id;
+    b.nof_ports          = std::min<unsigned>(grid.get_nof_ports(), 4);
+    for (unsigned i = 0; i != b.nof_ports; ++i) {
+      b.ports[i] = static_cast<uint8_t>(i);
+    }
+    b.nof_entries = static_cast<uint32_t>(entries.size());
+    b.entries     = entries.data();
+    if (entries.size() * sizeof(srs_amd_pucch_result) > RES_BYTES) {
+      ++st->nof_errors;
+      log_error("batch not processed", "too many entries");
+      return out;
+    }
+    unsigned        nof_ports = 0, nsubc = 0;
+    const uint32_t* g = grid_for(grid, b.ports, b.nof_ports, b.start_symbol_index, b.nof_symbols, nof_ports, nsubc);
+    if (g == nullptr || !run([&] {
+          b.d_grid = g;
+          return srs_amd_pucch_f1_detect_slot(st->proc, &b, 1, nullptr, 0, 0, nof_ports, nsubc,
+                                              static_cast<srs_amd_pucch_result*>(d_res), stream);
+        }, entries.size() * sizeof(srs_amd_pucch_result))) {
+      return out;
+    }
+    const auto* r = static_cast<const srs_amd_pucch_result*>(h_res);
+    for (unsigned k = 0; k != entries.size(); ++k) {
+      pucch_processor_result& res = out.get(entries[k].initial_cyclic_shift, entries[k].time_domain_occ);
+      for (unsigned i = 0; i != r[k].nof_harq_ack && i != 2; ++i) {
+        res.message.get_harq_ack_bits()[i] = r[k].harq_ack[i];
+      }
+      res.message.set_status(static_cast<uci_status>(r[k].status));
+      res.csi = channel_state_information();
+      res.csi.set_epre(r[k].epre_dB);
+      res.csi.set_rsrp_dB(r[k].rsrp_dB);
+      res.csi.set_sinr_dB(channel_state_information::sinr_type::channel_estimator, r[k].sinr_dB);
+      res.csi.reset_time_alignment();
+      res.detection_metric = r[k].detection_metric;
+    }
+    return out;
+  }
+
+  pucch_processor_result process(const resource_grid_reader& grid, const format2_configuration& config) override
+  {
+    ++st->nof_pdus;
+    pucch_processor_result result;
+    result.message = pucch_uci_message({.nof_sr = config.nof_sr, .nof_harq_ack = config.nof_harq_ack,
+                                        .nof_csi_part1 = config.nof_csi_part1, .nof_csi_part2 = config.nof_csi_part2});
+    result.message.set_status(uci_status::invalid);
+    srs_amd_pucch_f2_pdu p = convert(config);
+    const unsigned       K = config.nof_sr + config.nof_harq_ack + config.nof_csi_part1 + config.nof_csi_part2;
+    unsigned             nof_ports = 0, nsubc = 0;
+    const uint32_t*      g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
+    auto*                d_pay = static_cast<uint8_t*>(d_res) + PAYLOAD_OFF;
+    if (g == nullptr || K > 1706 || !run([&] {
+          p.d_grid = g;
+          return srs_amd_pucch_f2_process_slot(st->proc, &p, 1, nullptr, 0, 0, nof_ports, nsubc,
+                                               static_cast<srs_amd_pucch_uci_result*>(d_res), d_pay, 1706, stream);
+        }, PAYLOAD_OFF + K)) {
+      return result;
+    }
+    const auto* r = static_cast<const srs_amd_pucch_uci_result*>(h_res);
+    std::memcpy(result.message.get_full_payload().data(), static_cast<const uint8_t*>(h_res) + PAYLOAD_OFF, K);
+    result.message.set_status(static_cast<uci_status>(r->status));
+    result.csi = channel_state_information();
+    result.csi.set_epre(r->epre_dB);
+    result.csi.set_rsrp_dB(r->rsrp_dB);
+    result.csi.set_sinr_dB(channel_state_information::sinr_type::channel_estimator, r->sinr_dB);
+    result.csi.set_time_alignment(phy_time_unit::from_seconds(r->time_alignment_s));
+    if (!std::isnan(r->cfo_Hz)) {
+      result.csi.set_cfo(r->cfo_Hz);
+    }
+    return result;
+  }
+
+  pucch_processor_result process(const resource_grid_reader&, const format3_configuration& config) override
+  {
+    return unsupported("Format 3", config.nof_sr, config.nof_harq_ack, config.nof_csi_part1, config.nof_csi_part2);
+  }
+
+  pucch_processor_result process(const resource_grid_reader&, const format4_configuration& config) override
+  {
+    return unsupported("Format 4", config.nof_sr, config.nof_harq_ack, config.nof_csi_part1, config.nof_csi_part2);
+  }
+
+private:
+  static constexpr size_t RES_BYTES   = 4096;
+  static constexpr size_t PAYLOAD_OFF = 256;
+
+  pucch_processor_result unsupported(const char* what, unsigned sr, unsigned harq, unsigned csi1, unsigned csi2)
+  {
+    ++st->nof_pdus;
+    ++st->nof_errors;
+    log_error(what, "not supported by the hip PUCCH processor");
+    pucch_processor_result result;
+    result.message = pucch_uci_message({.nof_sr = sr, .nof_harq_ack = harq, .nof_csi_part1 = csi1,
+                                        .nof_csi_part2 = csi2});
+    result.message.set_status(uci_status::invalid);
+    return result;
+  }
+
+  // Launch through `call`, bring `bytes` of the result buffer back, wait.  false (logged) on any error.
+  template <typename F>
+  bool run(F&& call, size_t bytes)
+  {
+    int        rc = call();
+    hipError_t e  = hipSuccess;
+    if (rc == SRS_AMD_OK) {
+      e = hipMemcpyAsync(h_res, d_res, bytes, hipMemcpyDeviceToHost, stream);
+      e = e == hipSuccess ? hipStreamSynchronize(stream) : e;
+    } else {
+      (void)hipStreamSynchronize(stream);
+    }
+    if (rc != SRS_AMD_OK || e != hipSuccess) {
+      ++st->nof_errors;
+      log_error("PDU not processed", rc != SRS_AMD_OK ? std::string(srs_amd_last_error()) : hipGetErrorString(e));
+      return false;
+    }
+    return true;
+  }
+
+  // The grid on the device: a hip_resource_grid's own copy, or the PDU's symbols of its ports copied into a scratch
+  // grid of the same dimensions.
+  const uint32_t* grid_for(const resource_grid_reader& grid, const uint8_t* ports, unsigned nports, unsigned l0,
+                           unsigned nsym, unsigned& nof_ports, unsigned& nsubc)
+  {
+    (void)hipSetDevice(st->device);
+    nof_ports = grid.get_nof_ports();
+    nsubc     = grid.get_nof_subc();
+    if (hip_resource_grid* h = hip_grid_of(grid)) {
+      ++st->nof_device;
+      return h->device_read(stream);
+    }
+    if (l0 + nsym > NSYMB) {
+      return nullptr; // the C-ABI call reports the PDU
+    }
+    const size_t plane = static_cast<size_t>(NSYMB) * nsubc;
+    if (!reserve(nof_ports * plane * sizeof(uint32_t), nports * nsym * nsubc * sizeof(uint32_t))) {
+      ++st->nof_errors;
+      log_error("PDU not processed", "device / pinned buffer allocation");
+      return nullptr;
+    }
+    size_t row = 0;
+    for (unsigned i = 0; i != nports; ++i) {
+      if (ports[i] >= nof_ports) {
+        continue; // the C-ABI call reports the port
+      }
+      for (unsigned l = l0; l != l0 + nsym; ++l, ++row) {
+        span<const cbf16_t> v   = grid.get_view(ports[i], l);
+        uint32_t*           dst = stage + row * nsubc;
+        std::memcpy(dst, v.data(), nsubc * sizeof(uint32_t));
+        if (hipMemcpyAsync(scratch + ports[i] * plane + static_cast<size_t>(l) * nsubc, dst, nsubc * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, stream) != hipSuccess) {
+          return nullptr;
+        }
+      }
+    }
+    return scratch;
+  }
+
+  bool reserve(size_t dev_bytes, size_t host_bytes)
+  {
+    if (dev_bytes > dev_capacity) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipFree(scratch);
+      scratch      = nullptr;
+      dev_capacity = 0;
+      if (hipMalloc(&scratch, dev_bytes) != hipSuccess) {
+        return false;
+      }
+      dev_capacity = dev_bytes;
+    }
+    if (host_bytes > host_capacity) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipHostFree(stage);
+      stage         = nullptr;
+      host_capacity = 0;
+      if (hipHostMalloc(&stage, host_bytes, hipHostMallocDefault) != hipSuccess) {
+        return false;
+      }
+      host_capacity = host_bytes;
+    }
+    return true;
+  }
+
+  std::shared_ptr<shared_state> st;
+  hipStream_t                   stream        = nullptr;
+  uint32_t*                     scratch       = nullptr;
+  uint32_t*                     stage         = nullptr;
+  size_t                        dev_capacity  = 0;
+  size_t                        host_capacity = 0;
+  void*                         d_res         = nullptr;
+  void*                         h_res         = nullptr;
+};
+
+// pucch_pdu_validator_impl (pucch_processor_impl.cpp:399-760) for the formats the plug-in builds; Formats 3 / 4 are
+// reported as unsupported.
+class pucch_pdu_validator_hip : public pucch_pdu_validator
+{
+public:
+  explicit pucch_pdu_validator_hip(const pucch_processor_hip_config& c) : cfg(c) {}
+
+  error_type<std::string> is_valid(const pucch_processor::format0_configuration& c) const override
+  {
+    if (c.bwp_start_rb + c.bwp_size_rb > cfg.max_nof_prb || c.starting_prb >= c.bwp_size_rb ||
+        (c.second_hop_prb.has_value() && *c.second_hop_prb >= c.bwp_size_rb)) {
+      return make_unexpected(std::string("PRB allocation outside the BWP or the grid"));
+    }
+    if (c.nof_symbols < 1 || c.nof_symbols > 2 || c.start_symbol_index + c.nof_symbols > NSYMB) {
+      return make_unexpected(std::string("invalid Format 0 symbols"));
+    }
+    if (c.initial_cyclic_shift > 11 || c.n_id > 1023 || c.nof_harq_ack > 2 ||
+        (c.nof_harq_ack == 0 && !c.sr_opportunity)) {
+      return make_unexpected(std::string("invalid Format 0 PDU"));
+    }
+    return ports_ok(c.ports);
+  }
+  error_type<std::string> is_valid(const pucch_processor::format1_configuration& c) const override
+  {
+    const unsigned ratio = c.second_hop_prb.has_value() ? 4 : 2;
+    if (c.bwp_start_rb + c.bwp_size_rb > cfg.max_nof_prb || c.starting_prb >= c.bwp_size_rb ||
+        (c.second_hop_prb.has_value() && *c.second_hop_prb >= c.bwp_size_rb)) {
+      return make_unexpected(std::string("PRB allocation outside the BWP or the grid"));
+    }
+    if (c.start_symbol_index > 10 || c.nof_symbols < 4 || c.start_symbol_index + c.nof_symbols > NSYMB ||
+        c.initial_cyclic_shift > 11 || c.time_domain_occ >= c.nof_symbols / ratio || c.nof_harq_ack > 2 ||
+        c.n_id > 1023) {
+      return make_unexpected(std::string("invalid Format 1 PDU"));
+    }
+    return ports_ok(c.ports);
+  }
+  error_type<std::string> is_valid(const pucch_processor::format2_configuration& c) const override
+  {
+    const unsigned K = c.nof_harq_ack + c.nof_sr + c.nof_csi_part1 + c.nof_csi_part2;
+    const unsigned E = 16 * c.nof_prb * c.nof_symbols;
+    const unsigned A = K <= 11 ? 0 : (K <= 19 ? 6 : 11);
+    if (c.bwp_start_rb + c.bwp_size_rb > cfg.max_nof_prb || c.starting_prb + c.nof_prb > c.bwp_size_rb ||
+        c.nof_prb == 0 || c.nof_prb > 16) {
+      return make_unexpected(std::string("PRB allocation outside the BWP or the grid"));
+    }
+    if (c.nof_symbols < 1 || c.nof_symbols > 2 || c.start_symbol_index + c.nof_symbols > NSYMB ||
+        (c.second_hop_prb.has_value() && c.nof_symbols != 2)) {
+      return make_unexpected(std::string("invalid Format 2 symbols"));
+    }
+    if (c.nof_csi_part2 != 0) {
+      return make_unexpected(std::string("CSI Part 2 is not currently supported."));
+    }
+    if (K < 3 || K > 1706 || static_cast<float>(K + A) / static_cast<float>(E) > 0.8F) {
+      return make_unexpected(std::string("invalid Format 2 payload size or code rate"));
+    }
+    return ports_ok(c.ports);
+  }
+  error_type<std::string> is_valid(const pucch_processor::format3_configuration&) const override
+  {
+    return make_unexpected(std::string("PUCCH Format 3 is not supported by the hip PUCCH processor"));
+  }
+  error_type<std::string> is_valid(const pucch_processor::format4_configuration&) const override
+  {
+    return make_unexpected(std::string("PUCCH Format 4 is not supported by the hip PUCCH processor"));
+  }
+
+private:
+  error_type<std::string> ports_ok(const static_vector<uint8_t, MAX_PORTS>& ports) const
+  {
+    if (ports.empty() || ports.size() > cfg.max_nof_ports || ports.size() > 4) {
+      return make_unexpected(std::string("invalid number of receive ports"));
+    }
+    return default_success_t();
+  }
+  pucch_processor_hip_config cfg;
+};
+
+class pucch_processor_factory_hip_impl : public pucch_processor_factory_hip
+{
+public:
+  explicit pucch_processor_factory_hip_impl(std::shared_ptr<shared_state> s) : st(std::move(s)) {}
+
+  std::unique_ptr<pucch_processor> create() override
+  {
+    try {
+      return std::make_unique<pucch_processor_hip>(st);
+    } catch (const std::exception& e) {
+      log_error("create", e.what());
+      return nullptr;
+    }
+  }
+  std::unique_ptr<pucch_pdu_validator> create_validator() override
+  {
+    return std::make_unique<pucch_pdu_validator_hip>(st->cfg);
+  }
+  statistics get_statistics() const override
+  {
+    statistics s;
+    s.nof_pdus         = st->nof_pdus;
+    s.nof_errors       = st->nof_errors;
+    s.nof_device_grids = st->nof_device;
+    return s;
+  }
+
+private:
+  std::shared_ptr<shared_state> st;
+};
+
+} // namespace
+
+std::shared_ptr<pucch_processor_factory_hip>
+srsran::hip::create_pucch_processor_factory_hip(const pucch_processor_hip_config& cfg)
+{
+  auto st = std::make_shared<shared_state>();
+  st->cfg = cfg;
+  int dev = cfg.device;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) {
+    log_error("create", "no HIP device");
+    return nullptr;
+  }
+  st->device = dev;
+  if (srs_amd_pucch_processor_create(&st->proc, dev) != SRS_AMD_OK) {
+    log_error("create", srs_amd_last_error());
+    return nullptr;
+  }
+  return std::make_shared<pucch_processor_factory_hip_impl>(std::move(st));
+}

@@ -502,3 +502,66 @@ class SsbProcessorPlugin:
         s = np.zeros(3, np.uint64)
         lib().srs_ref_phy_ssb_stats(self.h, s.ctypes.data)
         return dict(zip(("pdus", "errors", "device_grids"), (int(v) for v in s)))
+
+
+class PucchProcessorPlugin:
+    """pucch_processor_factory_hip + one of its pucch_processors and its validator (integration/pucch_processor_hip),
+    driven through the reference's pucch_processor interface."""
+
+    def __init__(self, device=0):
+        L = lib()
+        P, u, i = ctypes.c_void_p, ctypes.c_uint, ctypes.c_int
+        L.srs_ref_phy_pucch_create.restype = P
+        L.srs_ref_phy_pucch_create.argtypes = [i]
+        L.srs_ref_phy_pucch_destroy.argtypes = [P]
+        L.srs_ref_phy_pucch_f0.argtypes = [P, P, P, u, P]
+        L.srs_ref_phy_pucch_f1.argtypes = [P, P, P, u, P]
+        L.srs_ref_phy_pucch_f2.argtypes = [P, P, P, P, P]
+        L.srs_ref_phy_pucch_f2_validate.restype = i
+        L.srs_ref_phy_pucch_f2_validate.argtypes = [P, P, ctypes.c_char_p, u]
+        L.srs_ref_phy_pucch_stats.argtypes = [P, P]
+        self.h = L.srs_ref_phy_pucch_create(device)
+        if not self.h:
+            raise RuntimeError("pucch_processor_factory_hip creation failed")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().srs_ref_phy_pucch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def f0(self, grid, pdu, grid_prb):
+        from srsran_project_amd.pucch import PucchResult
+
+        r = PucchResult()
+        lib().srs_ref_phy_pucch_f0(self.h, grid.h, ctypes.byref(pdu), grid_prb, ctypes.byref(r))
+        return r
+
+    def f1(self, grid, batch, grid_prb):
+        from srsran_project_amd.pucch import PucchResult
+
+        out = (PucchResult * batch.nof_entries)()
+        lib().srs_ref_phy_pucch_f1(self.h, grid.h, ctypes.byref(batch), grid_prb, out)
+        return list(out)
+
+    def f2(self, grid, pdu):
+        from srsran_project_amd.pucch import PucchUciResult, payload_bits
+
+        r = PucchUciResult()
+        pay = np.zeros(max(payload_bits(pdu), 1), np.uint8)
+        lib().srs_ref_phy_pucch_f2(self.h, grid.h, ctypes.byref(pdu), ctypes.byref(r), pay.ctypes.data)
+        return r, pay[:payload_bits(pdu)]
+
+    def validate_f2(self, pdu):
+        msg = ctypes.create_string_buffer(512)
+        return None if lib().srs_ref_phy_pucch_f2_validate(self.h, ctypes.byref(pdu), msg, 512) else msg.value.decode()
+
+    def stats(self):
+        out = (ctypes.c_uint64 * 3)()
+        lib().srs_ref_phy_pucch_stats(self.h, out)
+        return dict(pdus=out[0], errors=out[1], device_grids=out[2])

@@ -14,6 +14,8 @@
 #include "../integration/hip_resource_grid.h"
 #include "../integration/pdcch_processor_hip.h"
 #include "../integration/ssb_processor_hip.h"
+#include "../integration/pucch_processor_hip.h"
+#include "srsran_amd/pucch.h"
 #include "../integration/pdsch_processor_hip.h"
 #include "../integration/pusch_processor_hip.h"
 #include "phy/generic_functions/precoding/channel_precoder_avx2.h"
@@ -1036,6 +1038,190 @@ int srs_ref_phy_ssb_validate(void* h, const srs_amd_ssb_pdu* pdu, char* msg, uns
 void srs_ref_phy_ssb_stats(void* h, uint64_t* out)
 {
   const auto s = static_cast<ssb_ctx*>(h)->factory->get_statistics();
+  out[0]       = s.nof_pdus;
+  out[1]       = s.nof_errors;
+  out[2]       = s.nof_device_grids;
+}
+
+/* ---- PUCCH: the MI355X plug-in (integration/pucch_processor_hip) driven through the reference interface ---- */
+struct pucch_ctx {
+  std::shared_ptr<hip::pucch_processor_factory_hip> factory;
+  std::unique_ptr<pucch_processor>                  proc;
+  std::unique_ptr<pucch_pdu_validator>              validator;
+};
+
+void* srs_ref_phy_pucch_create(int device)
+{
+  hip::pucch_processor_hip_config cfg;
+  cfg.device   = device;
+  auto ctx     = std::make_unique<pucch_ctx>();
+  ctx->factory = hip::create_pucch_processor_factory_hip(cfg);
+  if (!ctx->factory) {
+    return nullptr;
+  }
+  ctx->proc      = ctx->factory->create();
+  ctx->validator = ctx->factory->create_validator();
+  return ctx->proc ? ctx.release() : nullptr;
+}
+
+void srs_ref_phy_pucch_destroy(void* h)
+{
+  delete static_cast<pucch_ctx*>(h);
+}
+
+static void csi_out(const channel_state_information& csi, float* sinr, float* rsrp, float* epre)
+{
+  *sinr = csi.get_sinr_dB().value_or(NAN);
+  *rsrp = csi.get_rsrp_dB().value_or(NAN);
+  *epre = csi.get_epre_dB().value_or(NAN);
+}
+
+/* pucch_processor::process(format0_configuration) of a C-ABI Format 0 PDU (BWP from PRB 0 over the grid). */
+void srs_ref_phy_pucch_f0(void* h, void* g, const srs_amd_pucch_f0_pdu* p, unsigned grid_prb,
+                          srs_amd_pucch_result* out)
+{
+  pucch_processor::format0_configuration c;
+  c.slot         = slot_point(p->numerology, p->slot_index);
+  c.cp           = cyclic_prefix::NORMAL;
+  c.bwp_size_rb  = grid_prb;
+  c.bwp_start_rb = 0;
+  c.starting_prb = p->starting_prb;
+  if (p->second_hop_prb >= 0) {
+    c.second_hop_prb = static_cast<unsigned>(p->second_hop_prb);
+  }
+  c.start_symbol_index   = p->start_symbol_index;
+  c.nof_symbols          = p->nof_symbols;
+  c.initial_cyclic_shift = p->initial_cyclic_shift;
+  c.n_id                 = p->n_id;
+  c.nof_harq_ack         = p->nof_harq_ack;
+  c.sr_opportunity       = p->sr_opportunity != 0;
+  for (unsigned i = 0; i != p->nof_ports; ++i) {
+    c.ports.push_back(p->ports[i]);
+  }
+  const pucch_processor_result r = static_cast<pucch_ctx*>(h)->proc->process(static_cast<any_grid*>(g)->rd(), c);
+  std::memset(out, 0, sizeof(*out));
+  out->status       = static_cast<uint32_t>(r.message.get_status());
+  out->nof_sr       = r.message.get_sr_bits().size();
+  out->nof_harq_ack = r.message.get_harq_ack_bits().size();
+  if (out->nof_sr != 0) {
+    out->sr = r.message.get_sr_bits()[0];
+  }
+  for (unsigned i = 0; i != out->nof_harq_ack && i != 2; ++i) {
+    out->harq_ack[i] = r.message.get_harq_ack_bits()[i];
+  }
+  csi_out(r.csi, &out->sinr_dB, &out->rsrp_dB, &out->epre_dB);
+  out->detection_metric = std::pow(10.0F, out->sinr_dB / 10.0F);
+}
+
+/* pucch_processor::process(format1_batch_configuration) of a C-ABI batch (BWP from PRB 0 over the grid); out[e] for
+ * entry e. */
+void srs_ref_phy_pucch_f1(void* h, void* g, const srs_amd_pucch_f1_batch* b, unsigned grid_prb,
+                          srs_amd_pucch_result* out)
+{
+  pucch_processor::format1_batch_configuration c;
+  c.common_config.slot         = slot_point(b->numerology, b->slot_index);
+  c.common_config.bwp_size_rb  = grid_prb;
+  c.common_config.bwp_start_rb = 0;
+  c.common_config.cp           = cyclic_prefix::NORMAL;
+  c.common_config.starting_prb = b->starting_prb;
+  if (b->second_hop_prb >= 0) {
+    c.common_config.second_hop_prb = static_cast<unsigned>(b->second_hop_prb);
+  }
+  c.common_config.n_id = b->n_id;
+  for (unsigned i = 0; i != b->nof_ports; ++i) {
+    c.common_config.ports.push_back(b->ports[i]);
+  }
+  c.common_config.nof_symbols        = b->nof_symbols;
+  c.common_config.start_symbol_index = b->start_symbol_index;
+  for (unsigned e = 0; e != b->nof_entries; ++e) {
+    c.entries.insert(b->entries[e].initial_cyclic_shift,
+                     b->entries[e].time_domain_occ,
+                     {.context = std::nullopt, .nof_harq_ack = b->entries[e].nof_harq_ack});
+  }
+  const auto res = static_cast<pucch_ctx*>(h)->proc->process(static_cast<any_grid*>(g)->rd(), c);
+  for (unsigned e = 0; e != b->nof_entries; ++e) {
+    const pucch_processor_result& r = res.get(b->entries[e].initial_cyclic_shift, b->entries[e].time_domain_occ);
+    std::memset(&out[e], 0, sizeof(out[e]));
+    out[e].status       = static_cast<uint32_t>(r.message.get_status());
+    out[e].nof_harq_ack = r.message.get_harq_ack_bits().size();
+    for (unsigned i = 0; i != out[e].nof_harq_ack && i != 2; ++i) {
+      out[e].harq_ack[i] = r.message.get_harq_ack_bits()[i];
+    }
+    csi_out(r.csi, &out[e].sinr_dB, &out[e].rsrp_dB, &out[e].epre_dB);
+    out[e].detection_metric = r.detection_metric.value_or(NAN);
+  }
+}
+
+/* pucch_processor::process(format2_configuration) of a C-ABI Format 2 PDU; payload[nof bits]. */
+void srs_ref_phy_pucch_f2(void* h, void* g, const srs_amd_pucch_f2_pdu* p, srs_amd_pucch_uci_result* out,
+                          uint8_t* payload)
+{
+  pucch_processor::format2_configuration c;
+  c.slot         = slot_point(p->numerology, p->slot_index);
+  c.bwp_size_rb  = p->bwp_size_rb;
+  c.bwp_start_rb = p->bwp_start_rb;
+  c.cp           = cyclic_prefix::NORMAL;
+  c.starting_prb = p->starting_prb;
+  if (p->second_hop_prb >= 0) {
+    c.second_hop_prb = static_cast<unsigned>(p->second_hop_prb);
+  }
+  c.nof_prb            = p->nof_prb;
+  c.start_symbol_index = p->start_symbol_index;
+  c.nof_symbols        = p->nof_symbols;
+  c.rnti               = static_cast<uint16_t>(p->rnti);
+  c.n_id               = p->n_id;
+  c.n_id_0             = p->n_id_0;
+  c.nof_harq_ack       = p->nof_harq_ack;
+  c.nof_sr             = p->nof_sr;
+  c.nof_csi_part1      = p->nof_csi_part1;
+  c.nof_csi_part2      = p->nof_csi_part2;
+  for (unsigned i = 0; i != p->nof_ports; ++i) {
+    c.ports.push_back(p->ports[i]);
+  }
+  const pucch_processor_result r = static_cast<pucch_ctx*>(h)->proc->process(static_cast<any_grid*>(g)->rd(), c);
+  std::memset(out, 0, sizeof(*out));
+  out->status        = static_cast<uint32_t>(r.message.get_status());
+  out->nof_harq_ack  = r.message.get_harq_ack_bits().size();
+  out->nof_sr        = r.message.get_sr_bits().size();
+  out->nof_csi_part1 = r.message.get_csi_part1_bits().size();
+  out->nof_csi_part2 = r.message.get_csi_part2_bits().size();
+  const auto full    = r.message.get_full_payload();
+  std::memcpy(payload, full.data(), full.size());
+  csi_out(r.csi, &out->sinr_dB, &out->rsrp_dB, &out->epre_dB);
+  out->time_alignment_s = r.csi.get_time_alignment().has_value() ? r.csi.get_time_alignment()->to_seconds() : NAN;
+  out->cfo_Hz           = r.csi.get_cfo_Hz().value_or(NAN);
+}
+
+/* The plug-in factory's validator on a Format 2 PDU: 1 valid, 0 invalid (msg filled). */
+int srs_ref_phy_pucch_f2_validate(void* h, const srs_amd_pucch_f2_pdu* p, char* msg, unsigned msg_size)
+{
+  pucch_processor::format2_configuration c;
+  c.slot         = slot_point(p->numerology, p->slot_index);
+  c.bwp_size_rb  = p->bwp_size_rb;
+  c.bwp_start_rb = p->bwp_start_rb;
+  c.starting_prb = p->starting_prb;
+  c.nof_prb      = p->nof_prb;
+  c.start_symbol_index = p->start_symbol_index;
+  c.nof_symbols        = p->nof_symbols;
+  c.nof_harq_ack       = p->nof_harq_ack;
+  c.nof_sr             = p->nof_sr;
+  c.nof_csi_part1      = p->nof_csi_part1;
+  c.nof_csi_part2      = p->nof_csi_part2;
+  for (unsigned i = 0; i != p->nof_ports; ++i) {
+    c.ports.push_back(p->ports[i]);
+  }
+  error_type<std::string> r = static_cast<pucch_ctx*>(h)->validator->is_valid(c);
+  if (r.has_value()) {
+    return 1;
+  }
+  std::snprintf(msg, msg_size, "%s", r.error().c_str());
+  return 0;
+}
+
+/* [0] PDUs, [1] errors, [2] device-resident grids. */
+void srs_ref_phy_pucch_stats(void* h, uint64_t* out)
+{
+  const auto s = static_cast<pucch_ctx*>(h)->factory->get_statistics();
   out[0]       = s.nof_pdus;
   out[1]       = s.nof_errors;
   out[2]       = s.nof_device_grids;

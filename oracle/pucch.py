@@ -283,3 +283,80 @@ def ref_detect_f1(grid, b):
     out = (PucchResult * b.nof_entries)()
     ref.srs_ref_pucch_f1_detect(g.ctypes.data, g.shape[0], g.shape[2], ctypes.addressof(b), out)
     return list(out)
+
+
+# ---- Format 2 ------------------------------------------------------------------------------------------------------
+def f2_data_res(nof_prb):
+    """PRB-relative subcarriers of the data REs of an allocation: every RE but 1, 4, 7, 10 of each PRB."""
+    return np.array([12 * b + k for b in range(nof_prb) for k in range(12) if k % 3 != 1])
+
+
+def f2_pilots(pdu, s):
+    """The DM-RS of allocated symbol s (dmrs_pucch_estimator_format2.cpp:34-56), complex64 [4 nof_prb]."""
+    l = pdu.start_symbol_index + s
+    prb = pdu.bwp_start_rb + (pdu.second_hop_prb if (s > 0 and pdu.second_hop_prb >= 0) else pdu.starting_prb)
+    c_init = ((14 * pdu.slot_index + l + 1) * (2 * pdu.n_id_0 + 1) * (1 << 17) + 2 * pdu.n_id_0) % (1 << 31)
+    n = 4 * pdu.nof_prb
+    c = prbs(c_init, 8 * prb + 2 * n)[8 * prb:]
+    a = np.float32(np.sqrt(0.5))
+    return (np.where(c[0::2] != 0, -a, a) + 1j * np.where(c[1::2] != 0, -a, a)).astype(np.complex64)
+
+
+def transmit_f2(grid, pdu, payload, gains, noise, rng):
+    """Writes a Format 2 transmission of payload (TS 38.212 6.3.1 UCI encoding, TS 38.211 6.3.2.5 scrambling with
+    c_init = rnti 2^15 + n_id, QPSK, data REs symbol by symbol; DM-RS on REs 1, 4, 7, 10) through per-port channel
+    gains plus complex Gaussian noise of variance noise onto its REs of grid (uint32 cbf16, in place)."""
+    from .pdsch_mod import to_bf16
+    from .pusch_proc import uci_encode
+
+    E = 16 * pdu.nof_prb * pdu.nof_symbols
+    bits = uci_encode(np.asarray(payload, np.uint8), E, 2) ^ prbs(pdu.rnti * (1 << 15) + pdu.n_id, E)
+    qpsk = (((1 - 2 * bits[0::2].astype(np.float32)) + 1j * (1 - 2 * bits[1::2].astype(np.float32))) /
+            np.sqrt(2)).astype(np.complex64)
+    nd = 8 * pdu.nof_prb
+    res = f2_data_res(pdu.nof_prb)
+    ports = [pdu.ports[i] for i in range(pdu.nof_ports)]
+    for s in range(pdu.nof_symbols):
+        l = pdu.start_symbol_index + s
+        prb = pdu.bwp_start_rb + (pdu.second_hop_prb if (s > 0 and pdu.second_hop_prb >= 0) else pdu.starting_prb)
+        x = np.zeros(12 * pdu.nof_prb, np.complex64)
+        x[res] = qpsk[s * nd:(s + 1) * nd]
+        x[1::3] = f2_pilots(pdu, s)
+        for i, p in enumerate(ports):
+            y = x * np.complex64(gains[i]) + np.sqrt(noise / 2) * (rng.normal(size=x.size) + 1j * rng.normal(size=x.size))
+            y = y.astype(np.complex64)
+            grid[p, l, 12 * prb:12 * prb + x.size] = (to_bf16(y.real).astype(np.uint32) |
+                                                      (to_bf16(y.imag).astype(np.uint32) << 16))
+    return grid
+
+
+def ref_process_f2(grid, pdu):
+    """The compiled pucch_processor_impl::process(format2_configuration) -> (PucchUciResult, payload bits)."""
+    import ctypes
+
+    from srsran_project_amd.pucch import PucchUciResult, payload_bits
+
+    ref = _ref()
+    ref.srs_ref_pucch_f2_process.restype = None
+    ref.srs_ref_pucch_f2_process.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+    g = np.ascontiguousarray(grid, np.uint32)
+    r = PucchUciResult()
+    pay = np.zeros(max(payload_bits(pdu), 1), np.uint8)
+    ref.srs_ref_pucch_f2_process(g.ctypes.data, g.shape[0], g.shape[2], ctypes.addressof(pdu), ctypes.byref(r),
+                                 pay.ctypes.data)
+    return r, pay[:payload_bits(pdu)]
+
+
+def ref_demodulate_f2(grid, pdu):
+    """The compiled dmrs_pucch_estimator_format2 + pucch_demodulator_format2 -> int8 LLRs [16 nof_prb nof_symbols]."""
+    import ctypes
+
+    ref = _ref()
+    ref.srs_ref_pucch_f2_demodulate.restype = None
+    ref.srs_ref_pucch_f2_demodulate.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p,
+                                                ctypes.c_void_p]
+    g = np.ascontiguousarray(grid, np.uint32)
+    llr = np.zeros(16 * pdu.nof_prb * pdu.nof_symbols, np.int8)
+    ref.srs_ref_pucch_f2_demodulate(g.ctypes.data, g.shape[0], g.shape[2], ctypes.addressof(pdu), llr.ctypes.data)
+    return llr

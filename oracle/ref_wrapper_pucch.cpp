@@ -13,7 +13,17 @@
 // (include/srsran_amd/pucch.h), the result as its srs_amd_pucch_result; the grid as a dense complex-bf16 array
 // [port][14][subcarrier].
 #include "phy/support/resource_grid_reader_impl.h"
+#include "ref_builders.h"
 #include "phy/generic_functions/dft_processor_generic_impl.h"
+#include "phy/upper/channel_processors/pucch/pucch_demodulator_format2.h"
+#include "phy/upper/channel_processors/pucch/pucch_demodulator_format3.h"
+#include "phy/upper/channel_processors/pucch/pucch_demodulator_format4.h"
+#include "phy/upper/channel_processors/pucch/pucch_demodulator_impl.h"
+#include "phy/upper/channel_processors/pucch/pucch_detector_impl.h"
+#include "phy/upper/channel_processors/pucch/pucch_processor_impl.h"
+#include "phy/upper/signal_processors/pucch/dmrs_pucch_estimator_format2.h"
+#include "phy/upper/signal_processors/pucch/dmrs_pucch_estimator_formats3_4.h"
+#include "phy/upper/signal_processors/pucch/dmrs_pucch_estimator_impl.h"
 #include "phy/upper/channel_processors/pucch/pucch_detector_format0.h"
 #include "phy/upper/channel_processors/pucch/pucch_detector_format1.h"
 #include "phy/upper/sequence_generators/low_papr_sequence_collection_impl.h"
@@ -57,6 +67,61 @@ std::unique_ptr<pucch_detector_format1> make_detector_f1()
       std::make_unique<dft_processor_generic_impl>(dft_processor::configuration{NRE, dft_processor::direction::DIRECT}),
       std::make_unique<dft_processor_generic_impl>(
           dft_processor::configuration{NRE, dft_processor::direction::INVERSE}));
+}
+
+// pucch_processor_impl as the reference's PUCCH factories assemble it: DM-RS estimators with the FD filter, TD
+// averaging and CFO compensation (Format 2) / none (Formats 3, 4) (signal_processors/pucch/factories.cpp:52-64),
+// ZF equalizers (upper_phy_factories.cpp:676-677), the UCI decoder.
+std::unique_ptr<pucch_processor> make_processor(unsigned nof_prb, unsigned nof_ports)
+{
+  using namespace srs_ref;
+  auto est = std::make_unique<dmrs_pucch_estimator_impl>(
+      std::make_unique<dmrs_pucch_estimator_format2>(std::make_unique<pseudo_random_generator_impl>(),
+                                                     make_port_estimator(2, 1, true)),
+      std::make_unique<dmrs_pucch_estimator_formats3_4>(std::make_unique<pseudo_random_generator_impl>(),
+                                                        std::make_unique<low_papr_sequence_generator_impl>(),
+                                                        make_port_estimator(2, 1, false)));
+  auto det   = std::make_unique<pucch_detector_impl>(make_detector(), make_detector_f1());
+  auto eq    = [] { return std::make_unique<channel_equalizer_generic_impl>(channel_equalizer_algorithm_type::zf); };
+  auto demod = std::make_unique<pucch_demodulator_impl>(
+      std::make_unique<pucch_demodulator_format2>(
+          eq(), std::make_unique<demodulation_mapper_impl>(), std::make_unique<pseudo_random_generator_impl>()),
+      std::make_unique<pucch_demodulator_format3>(eq(),
+                                                  std::make_unique<demodulation_mapper_impl>(),
+                                                  std::make_unique<pseudo_random_generator_impl>(),
+                                                  make_transform_precoder(16)),
+      std::make_unique<pucch_demodulator_format4>(eq(),
+                                                  std::make_unique<demodulation_mapper_impl>(),
+                                                  std::make_unique<pseudo_random_generator_impl>(),
+                                                  make_transform_precoder(16)));
+  channel_estimate::channel_estimate_dimensions dims;
+  dims.nof_prb       = nof_prb;
+  dims.nof_symbols   = MAX_NSYMB_PER_SLOT;
+  dims.nof_rx_ports  = nof_ports;
+  dims.nof_tx_layers = 1;
+  return std::make_unique<pucch_processor_impl>(std::make_unique<pucch_pdu_validator_impl>(dims),
+                                                std::move(est),
+                                                std::move(det),
+                                                std::move(demod),
+                                                make_uci_decoder(),
+                                                dims);
+}
+
+void fill_uci_result(const pucch_processor_result& r, srs_amd_pucch_uci_result* out, uint8_t* payload)
+{
+  std::memset(out, 0, sizeof(*out));
+  out->status        = static_cast<uint32_t>(r.message.get_status());
+  out->nof_harq_ack  = r.message.get_harq_ack_bits().size();
+  out->nof_sr        = r.message.get_sr_bits().size();
+  out->nof_csi_part1 = r.message.get_csi_part1_bits().size();
+  out->nof_csi_part2 = r.message.get_csi_part2_bits().size();
+  const auto full    = r.message.get_full_payload();
+  std::memcpy(payload, full.data(), full.size());
+  out->sinr_dB          = r.csi.get_sinr_dB().value_or(NAN);
+  out->rsrp_dB          = r.csi.get_rsrp_dB().value_or(NAN);
+  out->epre_dB          = r.csi.get_epre_dB().value_or(NAN);
+  out->time_alignment_s = r.csi.get_time_alignment().has_value() ? r.csi.get_time_alignment()->to_seconds() : NAN;
+  out->cfo_Hz           = r.csi.get_cfo_Hz().value_or(NAN);
 }
 
 void fill_grid(grid_tensor& data, const uint32_t* grid, unsigned nof_grid_ports, unsigned nsubc)
@@ -164,6 +229,98 @@ void srs_ref_pucch_f1_detect(const uint32_t* grid, unsigned nof_grid_ports, unsi
     out[e].rsrp_dB          = r.csi.get_rsrp_dB().value_or(NAN);
     out[e].epre_dB          = r.csi.get_epre_dB().value_or(NAN);
   }
+}
+
+// dmrs_pucch_estimator::estimate + pucch_demodulator::demodulate of one Format 2 PDU (as pucch_processor_impl.cpp:
+// 158-201 calls them): llrs[16 nof_prb nof_symbols].
+void srs_ref_pucch_f2_demodulate(const uint32_t* grid, unsigned nof_grid_ports, unsigned nsubc,
+                                 const srs_amd_pucch_f2_pdu* p, int8_t* llrs)
+{
+  grid_tensor data({nsubc, MAX_NSYMB_PER_SLOT, nof_grid_ports});
+  fill_grid(data, grid, nof_grid_ports, nsubc);
+  std::atomic<unsigned>     empty{0};
+  resource_grid_reader_impl reader(data, empty);
+  using namespace srs_ref;
+  dmrs_pucch_estimator_format2 est(std::make_unique<pseudo_random_generator_impl>(), make_port_estimator(2, 1, true));
+  pucch_demodulator_format2    dem(std::make_unique<channel_equalizer_generic_impl>(channel_equalizer_algorithm_type::zf),
+                                std::make_unique<demodulation_mapper_impl>(),
+                                std::make_unique<pseudo_random_generator_impl>());
+  const unsigned prb0 = p->bwp_start_rb + p->starting_prb;
+  std::optional<unsigned> hop;
+  if (p->second_hop_prb >= 0) {
+    hop = p->bwp_start_rb + static_cast<unsigned>(p->second_hop_prb);
+  }
+  dmrs_pucch_estimator::format2_configuration ec;
+  ec.slot               = slot_point(p->numerology, p->slot_index);
+  ec.cp                 = cyclic_prefix::NORMAL;
+  ec.group_hopping      = pucch_group_hopping::NEITHER;
+  ec.start_symbol_index = p->start_symbol_index;
+  ec.nof_symbols        = p->nof_symbols;
+  ec.starting_prb       = prb0;
+  ec.second_hop_prb     = hop;
+  ec.nof_prb            = p->nof_prb;
+  ec.n_id_0             = p->n_id_0;
+  for (unsigned i = 0; i != p->nof_ports; ++i) {
+    ec.ports.push_back(p->ports[i]);
+  }
+  channel_estimate::channel_estimate_dimensions dims;
+  dims.nof_prb       = nsubc / NRE;
+  dims.nof_symbols   = MAX_NSYMB_PER_SLOT;
+  dims.nof_rx_ports  = p->nof_ports;
+  dims.nof_tx_layers = 1;
+  channel_estimate ce(dims);
+  est.estimate(ce, reader, ec);
+  pucch_demodulator::format2_configuration dc;
+  for (unsigned i = 0; i != p->nof_ports; ++i) {
+    dc.rx_ports.push_back(p->ports[i]);
+  }
+  dc.first_prb          = prb0;
+  dc.second_hop_prb     = hop;
+  dc.nof_prb            = p->nof_prb;
+  dc.start_symbol_index = p->start_symbol_index;
+  dc.nof_symbols        = p->nof_symbols;
+  dc.rnti               = static_cast<uint16_t>(p->rnti);
+  dc.n_id               = p->n_id;
+  dem.demodulate(span<log_likelihood_ratio>(reinterpret_cast<log_likelihood_ratio*>(llrs),
+                                            16 * p->nof_prb * p->nof_symbols),
+                 reader,
+                 ce,
+                 dc);
+}
+
+// pucch_processor_impl::process of one Format 2 PDU on grid [nof_grid_ports][14][nsubc].
+void srs_ref_pucch_f2_process(const uint32_t* grid, unsigned nof_grid_ports, unsigned nsubc,
+                              const srs_amd_pucch_f2_pdu* p, srs_amd_pucch_uci_result* out, uint8_t* payload)
+{
+  grid_tensor data({nsubc, MAX_NSYMB_PER_SLOT, nof_grid_ports});
+  fill_grid(data, grid, nof_grid_ports, nsubc);
+  std::atomic<unsigned>     empty{0};
+  resource_grid_reader_impl reader(data, empty);
+
+  pucch_processor::format2_configuration cfg;
+  cfg.slot         = slot_point(p->numerology, p->slot_index);
+  cfg.bwp_size_rb  = p->bwp_size_rb;
+  cfg.bwp_start_rb = p->bwp_start_rb;
+  cfg.cp           = cyclic_prefix::NORMAL;
+  cfg.starting_prb = p->starting_prb;
+  if (p->second_hop_prb >= 0) {
+    cfg.second_hop_prb = static_cast<unsigned>(p->second_hop_prb);
+  }
+  cfg.nof_prb            = p->nof_prb;
+  cfg.start_symbol_index = p->start_symbol_index;
+  cfg.nof_symbols        = p->nof_symbols;
+  cfg.rnti               = static_cast<uint16_t>(p->rnti);
+  cfg.n_id               = p->n_id;
+  cfg.n_id_0             = p->n_id_0;
+  cfg.nof_harq_ack       = p->nof_harq_ack;
+  cfg.nof_sr             = p->nof_sr;
+  cfg.nof_csi_part1      = p->nof_csi_part1;
+  cfg.nof_csi_part2      = p->nof_csi_part2;
+  for (unsigned i = 0; i != p->nof_ports; ++i) {
+    cfg.ports.push_back(p->ports[i]);
+  }
+  auto proc = make_processor(nsubc / NRE, nof_grid_ports);
+  fill_uci_result(proc->process(reader, cfg), out, payload);
 }
 
 } // extern "C"

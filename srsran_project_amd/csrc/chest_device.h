@@ -1,7 +1,8 @@
 // chest_device.h -- device helpers of the PUSCH DM-RS channel estimator shared by its expansion kernel
 // (pusch_chest.hip chest_expand_kernel) and the PUSCH demodulator's fused equalizer (pusch_demod.hip),
 // which rebuilds each RE's estimate from the estimator's per-subcarrier values with the SAME operations
-// instead of reading an expanded estimate tensor from HBM.
+// instead of reading an expanded estimate tensor from HBM; the virtual pilots of the FD filter are shared with
+// the PUCCH Format 2 estimator (pucch.hip).
 // Complex products follow the reference's AVX2+FMA srsran_simd_cf_prod
 // (re = fma(a.re, b.re, -a.im b.im), im = fma(a.re, b.im, a.im b.re)).
 #pragma once
@@ -95,6 +96,75 @@ __device__ __forceinline__ uint32_t expand_value(const chest_args& a, const floa
   };
   const int i0 = lse_index(a, l);
   return expand_pair(a, lse(i0), lse(i0 + 1), l, rot, ph);
+}
+
+// compute_v_pilots (port_channel_estimator_helpers.cpp:334-378) over one wave: lane i < n <= 12 computes the
+// modulus / argument of value i and output value i; the short serial parts (phase unwrapping, the four
+// sums) run redundantly in every lane on the shuffled values, in the reference's order.  One lane running
+// the whole function was a chain of 3 n transcendental functions on the slice kernel's critical path.
+__device__ inline void virtual_pilots_wave(float2* out, const float2* in, int n, bool is_start)
+{
+#pragma clang fp contract(off)
+  const int lane = static_cast<int>(threadIdx.x & 63u);
+  float     av = 0, gv = 0;
+  if (lane < n) {
+    av = sqrtf(in[lane].x * in[lane].x + in[lane].y * in[lane].y);
+    gv = atan2f(in[lane].y, in[lane].x);
+  }
+  float absv[CH_MAXV], argv[CH_MAXV];
+#pragma unroll
+  for (int i = 0; i < CH_MAXV; ++i) {
+    absv[i] = __shfl(av, i);
+    argv[i] = __shfl(gv, i);
+  }
+  // unwrap_list (unwrap.cpp:42-62)
+  const float width = 3.14159265358979323846f;
+  float       k     = 0;
+#pragma unroll
+  for (int i = 0; i < CH_MAXV - 1; ++i) {
+    if (i < n - 1) {
+      const float old_a = argv[i], next_a = argv[i + 1];
+      argv[i] += 2.0f * k * width;
+      const float jump = next_a - old_a;
+      if (fabsf(jump) > width) {
+        k = k - copysignf(1.0f, jump);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < CH_MAXV; ++i) {
+    if (i == n - 1) {
+      argv[i] += 2.0f * k * width;
+    }
+  }
+  const float mean_x    = static_cast<float>(n * (n - 1)) / 2.0f / n;
+  const float norm_x_sq = static_cast<float>((n - 1) * n * (2 * n - 1)) / 6.0f;
+  float       sa = 0, sg = 0, ma = 0, mg = 0;
+#pragma unroll
+  for (int i = 0; i < CH_MAXV; ++i) {
+    if (i < n) {
+      ma += absv[i];
+      mg += argv[i];
+      sa += absv[i] * static_cast<float>(i);
+      sg += argv[i] * static_cast<float>(i);
+    }
+  }
+  ma /= n;
+  mg /= n;
+  sa -= mean_x * ma * n;
+  sa /= (norm_x_sq - n * mean_x * mean_x);
+  sg -= mean_x * mg * n;
+  sg /= (norm_x_sq - n * mean_x * mean_x);
+  const float ia  = ma - sa * mean_x;
+  const float ig  = mg - sg * mean_x;
+  const int   off = is_start ? -n : n;
+  if (lane < n) {
+    const int   iv  = lane + off;
+    const float rho = sa * iv + ia;
+    const float ph  = sg * iv + ig + ((rho > 0) ? 0.0f : 3.14159265358979323846f);
+    const float r   = fabsf(rho);
+    out[lane]       = make_float2(r * cosf(ph), r * sinf(ph));
+  }
 }
 
 } // namespace chdev

@@ -16,8 +16,21 @@
 // thread (port, RE) rebuilds the DM-RS with the shifts within 10 dB of the strongest (12-point IDFT times the OCC),
 // accumulated in registers over the OCCs; the noise is the energy of DM-RS minus reconstruction.  Last, thread e
 // decides entry e: the BPSK / QPSK symbol that maximises the cross term, the metric against the threshold, the CSI.
+//
+// Format 2, after pucch_processor_impl.cpp:140-220.  One 256-thread workgroup per PDU; wave w estimates the channel
+// of receive port w (port_channel_estimator_average_impl.cpp:122-409 with the PUCCH Format 2 DM-RS on REs 1, 4, 7, 10
+// of every PRB, per hop): lane k holds pilot k -- the LSE, the CFO between two DM-RS symbols of a hop and its
+// compensation, the FD filter with virtual pilots (chest_device.h), the RSRP, the linear interpolation to the data
+// REs rounded to cbf16 as the reference's estimate grid stores them, the noise from the pilots minus their
+// reconstruction, and the time alignment from the IDFT correlation (time_alignment_estimator_dft_impl.cpp, stride 3).
+// Then thread i equalizes data RE i over the ports (ZF, equalizer_device.h), demaps it (QPSK, demap_device.h: the
+// reference's 16-symbol AVX2 blocks and scalar tail) and descrambles its two LLRs; thread 0 writes the CSI.  The UCI
+// decoder (uci_decoder.hip) then decodes the LLR rows, grouped by payload and codeword size.
 #include <hip/hip_runtime.h>
 
+#include "chest_device.h"
+#include "demap_device.h"
+#include "equalizer_device.h"
 #include "pucch_args.h"
 
 namespace srs_amd {
@@ -362,7 +375,337 @@ __global__ __launch_bounds__(64) void pucch_f1_kernel(const pucch_f1_desc*      
   }
 }
 
+// ---- Format 2 -------------------------------------------------------------------------------------------------------
+constexpr double F2_T_C = 1.0 / (480000.0 * 4096.0);
+
+__device__ __forceinline__ float2 f2_pilot(const uint32_t* bits, uint32_t k) // QPSK at M_SQRT1_2
+{
+  constexpr float A  = 0.70710678118654752440f;
+  const uint32_t  c0 = (bits[(2 * k) >> 5] >> ((2 * k) & 31)) & 1u, c1 = (bits[(2 * k + 1) >> 5] >> ((2 * k + 1) & 31)) & 1u;
+  return make_float2(c0 ? -A : A, c1 ? -A : A);
+}
+
+__device__ __forceinline__ float2 wave_sum2(float2 v)
+{
+  return make_float2(wave_sum(v.x), wave_sum(v.y));
+}
+
+// The PRB-relative subcarrier of data RE q (0 .. 7) of a PRB: every RE but 1, 4, 7, 10.
+__device__ __forceinline__ uint32_t f2_data_re(uint32_t q)
+{
+  return q + (q + 1) / 2;
+}
+
+__global__ __launch_bounds__(256) void pucch_f2_kernel(const pucch_f2_desc* desc)
+{
+#pragma clang fp contract(off)
+  using chdev::cmul;
+  const pucch_f2_desc& d    = desc[blockIdx.x];
+  const uint32_t       t    = threadIdx.x;
+  const uint32_t       w    = t / 64, lane = t % 64;
+  const uint32_t       P    = d.nof_ports;
+  const uint32_t       np   = 4 * d.nof_prb; // pilots per DM-RS symbol
+  const uint32_t       nd8  = 8 * d.nof_prb; // data REs per symbol
+  const bool           live = w < P;
+  const uint32_t       port = live ? d.ports[w] : d.ports[0];
+  __shared__ float2    s_enl[4][CH_MAXV + 64 + CH_MAXV];
+  __shared__ float2    s_est[4][2][8 * PUCCH_F2_MAX_PRB];
+  __shared__ float     s_corr[4][PUCCH_MAX_TA_N];
+  __shared__ float     s_st[4][8]; // epre, rsrp, noise, snr, ta, cfo, cfo valid
+  const uint32_t*      g = d.grid + static_cast<uint64_t>(port) * d.port_stride;
+
+  float epre = 0.0f, rsrp = 0.0f, noise = 0.0f, ta = 0.0f, cfo = 0.0f;
+  bool  has_cfo = false;
+  const uint32_t nhops = d.hop ? 2u : 1u;
+  for (uint32_t h = 0; h != nhops; ++h) {
+    const uint32_t s0 = d.hop ? h : 0u;      // first allocated symbol of the hop
+    const uint32_t nd = d.hop ? 1u : d.nsym; // DM-RS symbols of the hop
+    const uint32_t prb = d.prb[s0];
+    float2 rx0 = make_float2(0.0f, 0.0f), rx1 = rx0, p0 = rx0, p1 = rx0;
+    if (lane < np) {
+      const uint32_t re = 12 * (prb + lane / 4) + 1 + 3 * (lane % 4);
+      rx0               = chdev::from_cbf16(g[static_cast<uint64_t>(d.l0 + s0) * d.nof_subc + re]);
+      p0                = f2_pilot(d.pil[s0], lane);
+      if (nd == 2) {
+        rx1 = chdev::from_cbf16(g[static_cast<uint64_t>(d.l0 + 1) * d.nof_subc + re]);
+        p1  = f2_pilot(d.pil[1], lane);
+      }
+    }
+    epre += wave_sum(norm2(rx0) + norm2(rx1));
+    float2 lse = cmul_conj(rx0, p0);
+    bool   cfo_hop = false;
+    float  cfo_h   = 0.0f;
+    if (nd == 2) {
+      float2       prod1 = cmul_conj(rx1, p1);
+      const float2 z     = wave_sum2(cmul_conj(prod1, lse));
+      cfo_h              = atan2f(z.y, z.x) / F1_TWOPI / (d.epoch[1] - d.epoch[0]);
+      cfo_hop            = true;
+      cfo                = has_cfo ? (cfo + cfo_h) / 2.0f : cfo_h;
+      has_cfo            = true;
+      lse                = cmul(lse, chdev::polar1(-F1_TWOPI * d.epoch[0] * cfo_h));
+      prod1              = cmul(prod1, chdev::polar1(-F1_TWOPI * d.epoch[1] * cfo_h));
+      lse.x += prod1.x;
+      lse.y += prod1.y;
+    }
+    const float total = (1.0f / 1.0f) / static_cast<float>(nd);
+    lse               = make_float2(lse.x * total, lse.y * total);
+    // FD smoothing: virtual pilots at both ends, then the FIR (port_channel_estimator_helpers.cpp:205-246)
+    float2* enl = s_enl[w];
+    for (uint32_t i = lane; i < CH_MAXV + 64 + CH_MAXV; i += 64) {
+      enl[i] = make_float2(0.0f, 0.0f);
+    }
+    __syncthreads();
+    if (lane < np) {
+      enl[CH_MAXV + lane] = lse;
+    }
+    __syncthreads();
+    const int nv = d.nof_v;
+    chdev::virtual_pilots_wave(enl + CH_MAXV - nv, enl + CH_MAXV, nv, true);
+    chdev::virtual_pilots_wave(enl + CH_MAXV + np, enl + CH_MAXV + np - nv, nv, false);
+    __syncthreads();
+    float2    f    = make_float2(0.0f, 0.0f);
+    const int half = d.nof_taps / 2;
+    if (lane < np) {
+      for (int j = 0; j < d.nof_taps; ++j) {
+        const int i = static_cast<int>(lane) + j - half;
+        if (i >= -nv && i < static_cast<int>(np) + nv) {
+          const float2 in = enl[CH_MAXV + i];
+          const float  c  = d.rc[d.nof_taps - 1 - j];
+          f.x             = f.x + in.x * c;
+          f.y             = f.y + in.y * c;
+        }
+      }
+    }
+    __syncthreads();
+    rsrp += wave_sum(norm2(f)) * (1.0f * 1.0f * static_cast<float>(nd) / 1.0f);
+    enl[lane] = f; // the smoothed pilots, for the interpolation and the IDFT
+    __syncthreads();
+    // linear interpolation to the data REs (offset 1, stride 3), rounded to cbf16
+    for (uint32_t j = lane; j < nd8; j += 64) {
+      const uint32_t r = 12 * (j / 8) + f2_data_re(j % 8);
+      float2         v;
+      if (r <= 1) {
+        v = enl[0];
+      } else {
+        const uint32_t i = (r - 1) / 3, rem = (r - 1) % 3;
+        if (i >= np - 1) {
+          v = enl[np - 1];
+        } else {
+          const float  wgt = static_cast<float>(rem) / 3.0f;
+          const float2 a = enl[i], b = enl[i + 1];
+          v = make_float2(a.x + (b.x - a.x) * wgt, a.y + (b.y - a.y) * wgt);
+        }
+      }
+      v = chdev::from_cbf16(chdev::to_cbf16(v));
+      for (uint32_t s = s0; s != s0 + (d.hop ? 1u : d.nsym); ++s) {
+        s_est[w][s][j] = v;
+      }
+    }
+    // noise: received pilots minus the smoothed estimate times the pilots (estimate_noise, :704-803)
+    float n_acc = 0.0f;
+    if (lane < np) {
+      for (uint32_t k = 0; k != nd; ++k) {
+        float2 pred = cmul(f, k == 0 ? p0 : p1);
+        if (cfo_hop) {
+          pred = cmul(pred, chdev::polar1(F1_TWOPI * d.epoch[k] * cfo_h));
+        }
+        const float2 rx = k == 0 ? rx0 : rx1;
+        n_acc += norm2(make_float2(rx.x - pred.x, rx.y - pred.y));
+      }
+    }
+    const float energy = wave_sum(n_acc);
+    noise += (isfinite(energy) && energy >= 1.17549435e-38f) ? energy : 0.0f;
+    // time alignment: |IDFT|^2 of the smoothed pilots (stride 3)
+    for (uint32_t tt = lane; tt < d.ta_n; tt += 64) {
+      float2 c = make_float2(0.0f, 0.0f);
+      for (uint32_t k = 0; k != np; ++k) {
+        const float2 e = chdev::polar1(F1_TWOPI * static_cast<float>((k * tt) % d.ta_n) / static_cast<float>(d.ta_n));
+        const float2 x = cmul(enl[k], e);
+        c.x += x.x;
+        c.y += x.y;
+      }
+      s_corr[w][tt] = norm2(c);
+    }
+    __syncthreads();
+    if (lane == 0) {
+      const float*   corr = s_corr[w];
+      const int      N = static_cast<int>(d.ta_n), M = d.ta_max_taps;
+      int            i_d = 0, i_a = 0;
+      float          v_d = corr[0], v_a = corr[N - M];
+      for (int i = 1; i < M; ++i) {
+        if (corr[i] > v_d) {
+          v_d = corr[i];
+          i_d = i;
+        }
+        if (corr[N - M + i] > v_a) {
+          v_a = corr[N - M + i];
+          i_a = i;
+        }
+      }
+      const int idx  = v_d >= v_a ? i_d : -(M - i_a);
+      double    frac = 0.0;
+      if (d.ta_frac) {
+        float pk[5];
+        const int taps = M > 2 ? 5 : 3;
+        for (int i = 0; i < taps; ++i) {
+          pk[i] = corr[static_cast<uint32_t>(idx + i + N - taps / 2) % static_cast<uint32_t>(N)];
+        }
+        float r;
+        if (taps == 5) {
+          const float num = -0.4f * pk[0] + -0.2f * pk[1] + 0.0f * pk[2] + 0.2f * pk[3] + 0.4f * pk[4];
+          const float den = 0.571429f * pk[0] + -0.285714f * pk[1] + -0.571429f * pk[2] + -0.285714f * pk[3] +
+                            0.571429f * pk[4];
+          r = -1.0f * num / den;
+        } else {
+          const float num = -0.5f * pk[0] + 0.0f * pk[1] + 0.5f * pk[2];
+          const float den = 0.5f * pk[0] + -1.0f * pk[1] + 0.5f * pk[2];
+          r = -0.5f * num / den;
+        }
+        frac = (isnan(r) || isinf(r) || fabsf(r) > 1.0f) ? 0.0 : static_cast<double>(r);
+      }
+      ta += static_cast<float>((static_cast<double>(idx) + frac) / d.ta_fs);
+    }
+    __syncthreads();
+  }
+  if (d.hop) {
+    ta /= 2.0f;
+  }
+  const float npil_all = static_cast<float>(np * d.nsym);
+  rsrp /= npil_all * 1.0f;
+  epre /= npil_all;
+  noise /= static_cast<float>(np * d.nsym * 1 - 1);
+  noise = fmaxf(rsrp / 1e10f, noise);
+  const float snr = (isfinite(noise) && noise >= 1.17549435e-38f) ? rsrp * 1.0f / 1.0f / 1.0f / noise : 0.0f;
+  // CFO rotation of the cbf16 estimates (port_channel_estimator_average_impl.cpp:184-194)
+  if (has_cfo) {
+    for (uint32_t j = lane; j < nd8; j += 64) {
+      for (uint32_t s = 0; s != d.nsym; ++s) {
+        s_est[w][s][j] = chdev::from_cbf16(chdev::to_cbf16(cmul(s_est[w][s][j], chdev::polar1(F1_TWOPI * d.epoch[s] * cfo))));
+      }
+    }
+  }
+  if (lane == 0) {
+    s_st[w][0] = epre;
+    s_st[w][1] = rsrp;
+    s_st[w][2] = noise;
+    s_st[w][3] = snr;
+    s_st[w][4] = ta;
+    s_st[w][5] = cfo;
+    s_st[w][6] = has_cfo ? 1.0f : 0.0f;
+  }
+  __syncthreads();
+  // ZF equalization over the ports, QPSK demapping, descrambling
+  if (t < d.n_re) {
+    const uint32_t s = t / nd8, j = t % nd8;
+    const uint32_t re = 12 * (d.prb[s] + j / 8) + f2_data_re(j % 8);
+    eq::cplx       y[4], hh[4];
+    float          nvp[4];
+    uint32_t       valid = 0;
+#pragma unroll
+    for (uint32_t p = 0; p < 4; ++p) {
+      y[p] = hh[p] = {0.0f, 0.0f};
+      nvp[p]       = 0.0f;
+      if (p < P) {
+        y[p]             = eq::from_cbf16(d.grid[static_cast<uint64_t>(d.ports[p]) * d.port_stride +
+                                          static_cast<uint64_t>(d.l0 + s) * d.nof_subc + re]);
+        const float2 e   = s_est[p][s][j];
+        hh[p]            = {e.x, e.y};
+        nvp[p]           = s_st[p][2];
+        const bool ok_nv = nvp[p] > 0.0f && nvp[p] < __builtin_inff();
+        valid |= ok_nv ? (1u << p) : 0u;
+      }
+    }
+    eq::cplx x;
+    float    nvx;
+    eq::equalize_1xn<4>(y, hh, nvp, valid, 1.0f, x, nvx);
+    const bool  simd = t < (d.n_re / 16) * 16;
+    const float GAIN = 2.0f * 1.41421356237309504880f;
+    const float xs[2] = {x.x, x.y};
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c) {
+      int v = simd ? demap::q_simd((GAIN * xs[c]) * demap::safe_rcp(nvx), 24.0f)
+                   : (nvx > 0.0f ? demap::q_scalar(GAIN * xs[c] / nvx, 24.0f) : 0);
+      const uint32_t b = 2 * t + c;
+      if ((d.scr[b >> 5] >> (b & 31)) & 1u) {
+        v = -v;
+      }
+      d.llr[b] = static_cast<int8_t>(v);
+    }
+  }
+  if (t == 0) { // channel_estimate::get_channel_state_information (channel_estimation.h:244-281)
+    float    epre_lin = 0.0f, best_snr = 0.0f, rsrp_tot = 0.0f, nv_tot = 0.0f, rsrp_all = 0.0f;
+    uint32_t best = 0, nvalid = 0;
+    for (uint32_t p = 0; p != P; ++p) {
+      epre_lin += s_st[p][0];
+      if (s_st[p][3] > best_snr) {
+        best_snr = s_st[p][3];
+        best     = p;
+      }
+      const float r = s_st[p][1];
+      if (isfinite(r) && fabsf(r) >= 1.17549435e-38f) {
+        rsrp_tot += r;
+        ++nvalid;
+      }
+      nv_tot += s_st[p][2];
+      rsrp_all += s_st[p][1];
+    }
+    epre_lin /= static_cast<float>(P);
+    const float rsrp_lin = nvalid != 0 ? rsrp_tot / static_cast<float>(nvalid) : 0.0f;
+    const float sinr     = (isfinite(nv_tot) && nv_tot >= 1.17549435e-38f) ? rsrp_all / nv_tot : 0.0f;
+    // phy_time_unit::from_seconds: tenths of T_C truncated, rounded half up
+    const double  tc   = static_cast<double>(s_st[best][4]) / F2_T_C;
+    const int64_t tc10 = static_cast<int64_t>(tc * 10.0);
+    const int64_t unit = tc10 / 10 + (tc10 % 10) / 5;
+    srs_amd_pucch_uci_result* r = d.result;
+    r->nof_harq_ack     = d.counts[0];
+    r->nof_sr           = d.counts[1];
+    r->nof_csi_part1    = d.counts[2];
+    r->nof_csi_part2    = d.counts[3];
+    r->sinr_dB          = to_dB(sinr);
+    r->rsrp_dB          = to_dB(rsrp_lin);
+    r->epre_dB          = to_dB(epre_lin);
+    r->time_alignment_s = static_cast<float>(static_cast<double>(unit) * F2_T_C);
+    r->cfo_Hz           = s_st[best][6] != 0.0f ? s_st[best][5] * d.scs_hz : __builtin_nanf("");
+  }
+}
+
+__global__ __launch_bounds__(256) void pucch_uci_finish_kernel(const int32_t* status, const uint8_t* messages,
+                                                               uint32_t msg_stride, const uint32_t* perm,
+                                                               const uint32_t* nbits, srs_amd_pucch_uci_result* results,
+                                                               uint8_t* payloads, uint64_t payload_stride)
+{
+  const uint32_t j = blockIdx.x, dst = perm[j];
+  if (threadIdx.x == 0) {
+    results[dst].status = static_cast<uint32_t>(status[j]);
+  }
+  for (uint32_t i = threadIdx.x; i < nbits[j]; i += 256) {
+    payloads[dst * payload_stride + i] = messages[static_cast<uint64_t>(j) * msg_stride + i];
+  }
+}
+
 } // namespace
+
+hipError_t launch_pucch_f2(const pucch_f2_desc* d_desc, uint32_t nof, hipStream_t stream)
+{
+  if (nof == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(pucch_f2_kernel, dim3(nof), dim3(256), 0, stream, d_desc);
+  return hipGetLastError();
+}
+
+hipError_t launch_pucch_uci_finish(const int32_t* status, const uint8_t* messages, uint32_t msg_stride,
+                                   const uint32_t* perm, const uint32_t* nbits, uint32_t nof,
+                                   srs_amd_pucch_uci_result* results, uint8_t* payloads, uint64_t payload_stride,
+                                   hipStream_t stream)
+{
+  if (nof == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(pucch_uci_finish_kernel, dim3(nof), dim3(256), 0, stream, status, messages, msg_stride, perm,
+                     nbits, results, payloads, payload_stride);
+  return hipGetLastError();
+}
 
 hipError_t launch_pucch_f1(const pucch_f1_desc* d_desc, uint32_t nof, const srs_amd_pucch_f1_entry* d_entries,
                            srs_amd_pucch_result* d_results, hipStream_t stream)

@@ -13,6 +13,7 @@
 // n_id mod 30 and the set of OCC indices in use; device side: pucch_f1_kernel.
 #include "srsran_amd/pucch.h"
 #include "srsran_amd/low_papr.h"
+#include "srsran_amd/uci_decoder.h"
 
 #include <hip/hip_runtime.h>
 
@@ -20,9 +21,11 @@
 #include "device_buffer.h"
 #include "gold_sequence.h"
 #include "pucch_args.h"
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <numeric>
 #include <vector>
 
 using namespace srs_amd;
@@ -30,7 +33,8 @@ using namespace srs_amd;
 struct srs_amd_pucch_processor {
   int                   device = 0;
   std::vector<uint32_t> jump; // host copy of gold_jump_tables()
-  device_buffer         buf, host_grid, host_res;
+  device_buffer         buf, host_grid, host_res, work, host_payload;
+  srs_amd_uci_decoder*  uci = nullptr;     // Formats 2 / 3 / 4
   pinned_stage          stage;
   stream_order          order;
   hipStream_t           stream = nullptr; // host calls
@@ -42,6 +46,9 @@ struct srs_amd_pucch_processor {
     if (stream) {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
+    }
+    if (uci != nullptr) {
+      srs_amd_uci_decoder_destroy(uci);
     }
   }
 };
@@ -113,6 +120,181 @@ uint32_t gold_byte(const std::vector<uint32_t>& jump, uint32_t c_init, uint32_t 
     x2                = (x2 >> 1) | (n2 << 30);
   }
   return out;
+}
+
+// Gold-sequence bits c(n0 .. n0 + nbits - 1) of c_init into out (bit i of word i / 32).
+void gold_bits(const std::vector<uint32_t>& jump, uint32_t c_init, uint32_t n0, uint32_t nbits, uint32_t* out)
+{
+  uint32_t       x1 = 1u, x2 = c_init & 0x7fffffffu;
+  const uint32_t steps = n0 + 1600u;
+  for (int k = 0; k < PRBS_NJUMP; ++k) {
+    if ((steps >> k) & 1u) {
+      x1 = gf2_apply_h(jump.data() + (0 * PRBS_NJUMP + k) * 31, x1);
+      x2 = gf2_apply_h(jump.data() + (1 * PRBS_NJUMP + k) * 31, x2);
+    }
+  }
+  std::memset(out, 0, sizeof(uint32_t) * ((nbits + 31) / 32));
+  for (uint32_t m = 0; m != nbits; ++m) {
+    out[m / 32] |= ((x1 ^ x2) & 1u) << (m % 32);
+    const uint32_t n1 = ((x1 >> 3) ^ x1) & 1u;
+    const uint32_t n2 = ((x2 >> 3) ^ (x2 >> 2) ^ (x2 >> 1) ^ x2) & 1u;
+    x1                = (x1 >> 1) | (n1 << 30);
+    x2                = (x2 >> 1) | (n2 << 30);
+  }
+}
+
+constexpr double T_C = 1.0 / (480000.0 * 4096.0);
+
+// initialize_symbol_start_epochs (port_channel_estimator_average_impl.cpp:543-554), normal cyclic prefix.
+void symbol_epochs(uint32_t mu, float* epoch)
+{
+  const unsigned scs_k = 15u << mu;
+  auto           cp_s  = [mu](unsigned i) {
+    unsigned k = 144u >> mu;
+    if (i == 0 || i == 7u * (1u << mu)) {
+      k += 16;
+    }
+    return static_cast<double>(k * 64) * T_C;
+  };
+  epoch[0] = static_cast<float>(cp_s(0) * scs_k * 1000);
+  for (unsigned i = 1; i < NSYMB; ++i) {
+    epoch[i] = static_cast<float>(epoch[i - 1] + cp_s(i) * scs_k * 1000 + 1.0F);
+  }
+}
+
+const float RC_FILTER[31] = {-0.0641253, -0.0660711, -0.0611526, -0.0485918, -0.0281126, 0.0000000, 0.0348830,
+                             0.0751249,  0.1188406,  0.1637874,  0.2075139,  0.2475302,  0.2814857, 0.3073415,
+                             0.3235207,  0.3290274,  0.3235207,  0.3073415,  0.2814857,  0.2475302, 0.2075139,
+                             0.1637874,  0.1188406,  0.0751249,  0.0348830,  0.0000000,  -0.0281126, -0.0485918,
+                             -0.0611526, -0.0660711, -0.0641253};
+
+// filter_type(nof_rb, stride) (port_channel_estimator_helpers.cpp:84-111) and the virtual pilots per side.
+void fd_filter(uint32_t nof_rb, uint32_t stride, uint32_t npil, float* rc, int32_t& nof_taps, int32_t& nof_v)
+{
+  const unsigned nrb       = std::min(nof_rb, 3u);
+  const unsigned nof_coefs = nrb * 10 + 1;
+  unsigned       n_out     = nof_coefs / 2 / stride;
+  const unsigned n_first   = 31 / 2 - n_out * stride;
+  n_out                    = 2 * n_out + 1;
+  float total              = 0;
+  for (unsigned i = 0; i < n_out; ++i) {
+    rc[i] = RC_FILTER[n_first + stride * i];
+    total += rc[i];
+  }
+  const float inv = 1 / total;
+  for (unsigned i = 0; i < n_out; ++i) {
+    rc[i] *= inv;
+  }
+  nof_taps = static_cast<int32_t>(n_out);
+  nof_v    = nof_rb == 1 ? static_cast<int32_t>(npil) : std::min<int32_t>(12, nof_taps / 2);
+}
+
+// time_alignment_estimator_dft_impl::get_idft / estimate_ta_correlation constants for npil pilots of a stride.
+void ta_setup(uint32_t npil, uint32_t stride, uint32_t mu, uint32_t& n, int32_t& max_taps, int32_t& frac, double& fs)
+{
+  constexpr uint32_t MAX_N = 4096, MIN_N = 128;
+  const uint32_t     req   = npil * MAX_N / (275 * 12);
+  uint32_t           N     = 1;
+  while (N < req) {
+    N <<= 1;
+  }
+  N                     = std::max(MIN_N, N);
+  n                     = N;
+  fs                    = static_cast<double>(N) * (15u << mu) * 1000 * stride;
+  const double half_cp  = static_cast<double>((144u * 64u) >> (mu + 1)) * T_C;
+  max_taps              = static_cast<int32_t>(std::floor(half_cp * fs));
+  frac                  = N != MAX_N ? 1 : 0;
+}
+
+// UCI CRC bits (uci_info.h:40-77).
+uint32_t uci_crc_bits(uint32_t A, uint32_t E)
+{
+  const uint32_t C = ((A >= 360 && E >= 1088) || A >= 1013) ? 2u : 1u;
+  const uint32_t L = A <= 11 ? 0u : (A <= 19 ? 6u : 11u);
+  return C * L;
+}
+
+int make_f2_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f2_pdu& p, const uint32_t* d_grids,
+                 uint64_t grid_stride, uint32_t nof_grids, uint32_t nof_grid_ports, uint32_t nof_subc,
+                 pucch_f2_desc& d)
+{
+  const uint32_t grid_prb = nof_subc / 12;
+  if (p.bwp_start_rb + p.bwp_size_rb > grid_prb) {
+    return fail(SRS_AMD_EINVAL, "BWP allocation goes up to PRB %u, exceeding the configured maximum grid RB size, i.e., %u.",
+                p.bwp_start_rb + p.bwp_size_rb, grid_prb);
+  }
+  if (p.nof_prb == 0 || p.nof_prb > PUCCH_F2_MAX_PRB || p.starting_prb + p.nof_prb > p.bwp_size_rb) {
+    return fail(SRS_AMD_EINVAL, "PRB allocation within the BWP goes up to PRB %u, exceeding BWP size, i.e., %u.",
+                p.starting_prb + p.nof_prb, p.bwp_size_rb);
+  }
+  if (p.nof_symbols == 0 || p.nof_symbols > 2 || p.start_symbol_index + p.nof_symbols > NSYMB) {
+    return fail(SRS_AMD_EINVAL, "Invalid Format 2 symbols (start %u, %u symbols).", p.start_symbol_index,
+                p.nof_symbols);
+  }
+  if (p.second_hop_prb >= 0 && (p.nof_symbols != 2 ||
+                                (p.bwp_start_rb + static_cast<uint32_t>(p.second_hop_prb) + p.nof_prb) > grid_prb)) {
+    return fail(SRS_AMD_EINVAL, "Frequency hopping requires 2 OFDM symbols inside the grid.");
+  }
+  if (p.nof_ports == 0 || p.nof_ports > 4) {
+    return fail(SRS_AMD_EINVAL, "The number of receive ports, i.e. %u, is not 1 to 4.", p.nof_ports);
+  }
+  if (p.nof_csi_part2 != 0) {
+    return fail(SRS_AMD_EINVAL, "CSI Part 2 is not currently supported.");
+  }
+  if (p.numerology > 4 || p.slot_index >= (10u << p.numerology) || p.n_id > 1023 || p.rnti > 65535 ||
+      p.n_id_0 > 65535) {
+    return fail(SRS_AMD_EINVAL, "Invalid Format 2 PDU (slot %u, numerology %u, RNTI %u, n_id %u, n_id_0 %u).",
+                p.slot_index, p.numerology, p.rnti, p.n_id, p.n_id_0);
+  }
+  const uint32_t K = p.nof_harq_ack + p.nof_sr + p.nof_csi_part1 + p.nof_csi_part2;
+  const uint32_t E = 16 * p.nof_prb * p.nof_symbols;
+  if (K < 3 || K > 1706) {
+    return fail(SRS_AMD_EINVAL, "UCI Payload length, i.e., %u is not supported. Payload length must be 3 to 1706 bits.",
+                K);
+  }
+  if (static_cast<float>(K + uci_crc_bits(K, E)) / static_cast<float>(E) > 0.80F) {
+    return fail(SRS_AMD_EINVAL, "The effective code rate exceeds the maximum allowed 0.8.");
+  }
+  if (p.d_grid == nullptr && (d_grids == nullptr || p.grid >= nof_grids)) {
+    return fail(SRS_AMD_EINVAL, "grid index %u out of range (or no grid).", p.grid);
+  }
+  d             = pucch_f2_desc{};
+  d.grid        = p.d_grid != nullptr ? p.d_grid : d_grids + p.grid * grid_stride;
+  d.port_stride = NSYMB * nof_subc;
+  d.nof_subc    = nof_subc;
+  d.l0          = p.start_symbol_index;
+  d.nsym        = p.nof_symbols;
+  d.hop         = p.second_hop_prb >= 0 ? 1u : 0u;
+  d.nof_prb     = p.nof_prb;
+  d.prb[0]      = p.bwp_start_rb + p.starting_prb;
+  d.prb[1]      = d.hop ? p.bwp_start_rb + static_cast<uint32_t>(p.second_hop_prb) : d.prb[0];
+  d.nof_ports   = p.nof_ports;
+  for (uint32_t i = 0; i != p.nof_ports; ++i) {
+    if (p.ports[i] >= nof_grid_ports) {
+      return fail(SRS_AMD_EINVAL, "port %u outside the grid's %u ports.", p.ports[i], nof_grid_ports);
+    }
+    d.ports[i] = p.ports[i];
+  }
+  float epoch[NSYMB];
+  symbol_epochs(p.numerology, epoch);
+  const uint32_t np = 4 * p.nof_prb;
+  for (uint32_t s = 0; s != p.nof_symbols; ++s) {
+    const uint32_t l      = p.start_symbol_index + s;
+    d.epoch[s]            = epoch[l];
+    const uint64_t c_init = ((static_cast<uint64_t>(NSYMB) * p.slot_index + l + 1) * (2ull * p.n_id_0 + 1) *
+                                 (1ull << 17) + 2ull * p.n_id_0) % (1ull << 31);
+    gold_bits(proc->jump, static_cast<uint32_t>(c_init), d.prb[s] * 4 * 2, 2 * np, d.pil[s]);
+  }
+  d.scs_hz = static_cast<float>((15u << p.numerology) * 1000);
+  fd_filter(p.nof_prb, 3, np, d.rc, d.nof_taps, d.nof_v);
+  ta_setup(np, 3, p.numerology, d.ta_n, d.ta_max_taps, d.ta_frac, d.ta_fs);
+  gold_bits(proc->jump, p.rnti * (1u << 15) + p.n_id, 0, E, d.scr);
+  d.n_re   = 8 * p.nof_prb * p.nof_symbols;
+  d.counts[0] = p.nof_harq_ack;
+  d.counts[1] = p.nof_sr;
+  d.counts[2] = p.nof_csi_part1;
+  d.counts[3] = p.nof_csi_part2;
+  return SRS_AMD_OK;
 }
 
 int make_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f0_pdu& p, const uint32_t* d_grids,
@@ -296,6 +478,11 @@ int srs_amd_pucch_processor_create(srs_amd_pucch_processor** proc, int device)
     delete p;
     return hip_fail(hipErrorUnknown, "PUCCH processor stream");
   }
+  rc = srs_amd_uci_decoder_create(&p->uci, device);
+  if (rc != SRS_AMD_OK) {
+    delete p;
+    return rc;
+  }
   *proc = p;
   return SRS_AMD_OK;
 }
@@ -391,6 +578,243 @@ int srs_amd_pucch_f0_detect(srs_amd_pucch_processor*    proc,
                                         proc->host_res.as<srs_amd_pucch_f0_result>(), proc->stream);
   if (rc == SRS_AMD_OK) {
     e  = hipMemcpyAsync(result, proc->host_res.ptr, sizeof(*result), hipMemcpyDeviceToHost, proc->stream);
+    e  = e == hipSuccess ? hipStreamSynchronize(proc->stream) : e;
+    rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUCCH result download");
+  } else {
+    (void)hipStreamSynchronize(proc->stream);
+  }
+  return rc;
+}
+
+} // extern "C"
+
+namespace {
+
+// The Format 2 slot form; decode = false stops after the LLRs (rows of PUCCH_F2_MAX_E in proc->work, decoder order).
+int f2_slot(srs_amd_pucch_processor*    proc,
+            const srs_amd_pucch_f2_pdu* pdus,
+            uint32_t                    nof_pdus,
+            const uint32_t*             d_grids,
+            uint64_t                    grid_stride,
+            uint32_t                    nof_grids,
+            uint32_t                    nof_grid_ports,
+            uint32_t                    nof_subc,
+            srs_amd_pucch_uci_result*   d_results,
+            uint8_t*                    d_payloads,
+            uint64_t                    payload_stride,
+            void*                       stream,
+            bool                        decode)
+{
+  if (proc == nullptr || (nof_pdus != 0 && (pdus == nullptr || d_results == nullptr || d_payloads == nullptr))) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_pdus == 0) {
+    return SRS_AMD_OK;
+  }
+  if (nof_subc == 0 || nof_subc % 12 != 0) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of grid subcarriers (i.e., %u).", nof_subc);
+  }
+  std::lock_guard<std::mutex> lock(proc->mtx);
+  std::vector<pucch_f2_desc>  desc(nof_pdus);
+  std::vector<uint32_t>       K(nof_pdus), E(nof_pdus);
+  uint32_t                    max_k = 0;
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    const srs_amd_pucch_f2_pdu& p = pdus[i];
+    if (p.nof_harq_ack + p.nof_sr + p.nof_csi_part1 + p.nof_csi_part2 > payload_stride) {
+      return fail(SRS_AMD_EINVAL, "payload_stride %llu below the PDU's %u payload bits.",
+                  static_cast<unsigned long long>(payload_stride),
+                  p.nof_harq_ack + p.nof_sr + p.nof_csi_part1 + p.nof_csi_part2);
+    }
+  }
+  // decoder order: PDUs grouped by (payload, codeword) size, one UCI decoder launch per group
+  std::vector<uint32_t> perm(nof_pdus);
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    const srs_amd_pucch_f2_pdu& p = pdus[i];
+    K[i]  = p.nof_harq_ack + p.nof_sr + p.nof_csi_part1 + p.nof_csi_part2;
+    E[i]  = 16 * p.nof_prb * p.nof_symbols;
+    max_k = std::max(max_k, K[i]);
+  }
+  std::iota(perm.begin(), perm.end(), 0u);
+  std::stable_sort(perm.begin(), perm.end(),
+                   [&](uint32_t a, uint32_t b) { return K[a] != K[b] ? K[a] < K[b] : E[a] < E[b]; });
+  const uint32_t msg_stride = (std::max(max_k, 1u) + 63) / 64 * 64;
+  const size_t   llr_bytes  = static_cast<size_t>(nof_pdus) * PUCCH_F2_MAX_E;
+  const size_t   msg_bytes  = static_cast<size_t>(nof_pdus) * msg_stride;
+  const size_t   st_bytes   = static_cast<size_t>(nof_pdus) * sizeof(int32_t);
+  auto           s          = static_cast<hipStream_t>(stream);
+  hipError_t     e          = hipSetDevice(proc->device);
+  if (e == hipSuccess) {
+    e = proc->work.ensure(llr_bytes + msg_bytes + st_bytes);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUCCH processor scratch");
+  }
+  int8_t*  d_llr = proc->work.as<int8_t>();
+  uint8_t* d_msg = proc->work.as<uint8_t>() + llr_bytes;
+  int32_t* d_st  = reinterpret_cast<int32_t*>(proc->work.as<uint8_t>() + llr_bytes + msg_bytes);
+  std::vector<uint32_t> nbits(nof_pdus);
+  for (uint32_t j = 0; j != nof_pdus; ++j) {
+    const uint32_t i = perm[j];
+    const int rc = make_f2_desc(proc, pdus[i], d_grids, grid_stride, nof_grids, nof_grid_ports, nof_subc, desc[j]);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+    desc[j].llr    = d_llr + static_cast<size_t>(j) * PUCCH_F2_MAX_E;
+    desc[j].result = d_results + i;
+    nbits[j]       = K[i];
+  }
+  const size_t dbytes = sizeof(pucch_f2_desc) * nof_pdus;
+  const size_t ioff   = (dbytes + 255) & ~size_t(255);
+  const size_t ibytes = sizeof(uint32_t) * nof_pdus;
+  const size_t bytes  = ioff + 2 * ibytes;
+  if (e == hipSuccess) {
+    e = proc->buf.ensure(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->stage.acquire(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->order.begin(s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUCCH processor scratch");
+  }
+  call_scope scope(proc->order, nullptr, s);
+  std::memcpy(proc->stage.at<uint8_t>(0), desc.data(), dbytes);
+  std::memcpy(proc->stage.at<uint8_t>(ioff), perm.data(), ibytes);
+  std::memcpy(proc->stage.at<uint8_t>(ioff + ibytes), nbits.data(), ibytes);
+  e = proc->stage.upload(proc->buf.ptr, bytes, s);
+  if (e == hipSuccess) {
+    e = launch_pucch_f2(proc->buf.as<pucch_f2_desc>(), nof_pdus, s);
+  }
+  int rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pucch_f2_kernel launch");
+  for (uint32_t j0 = 0; decode && rc == SRS_AMD_OK && j0 != nof_pdus;) {
+    uint32_t j1 = j0 + 1;
+    while (j1 != nof_pdus && K[perm[j1]] == K[perm[j0]] && E[perm[j1]] == E[perm[j0]]) {
+      ++j1;
+    }
+    rc = srs_amd_uci_decode_batch(proc->uci, d_llr + static_cast<size_t>(j0) * PUCCH_F2_MAX_E, PUCCH_F2_MAX_E,
+                                  E[perm[j0]], K[perm[j0]], 2, d_msg + static_cast<size_t>(j0) * msg_stride,
+                                  msg_stride, d_st + j0, sizeof(int32_t), j1 - j0, s);
+    j0 = j1;
+  }
+  if (decode && rc == SRS_AMD_OK) {
+    const uint32_t* d_perm = reinterpret_cast<const uint32_t*>(proc->buf.as<uint8_t>() + ioff);
+    e  = launch_pucch_uci_finish(d_st, d_msg, msg_stride, d_perm, d_perm + nof_pdus, nof_pdus, d_results, d_payloads,
+                                 payload_stride, s);
+    rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pucch_uci_finish_kernel launch");
+  }
+  const hipError_t done = scope.close();
+  return rc != SRS_AMD_OK ? rc : (done == hipSuccess ? SRS_AMD_OK : hip_fail(done, "PUCCH completion event"));
+}
+
+} // namespace
+
+extern "C" {
+
+int srs_amd_pucch_f2_process_slot(srs_amd_pucch_processor*    proc,
+                                  const srs_amd_pucch_f2_pdu* pdus,
+                                  uint32_t                    nof_pdus,
+                                  const uint32_t*             d_grids,
+                                  uint64_t                    grid_stride,
+                                  uint32_t                    nof_grids,
+                                  uint32_t                    nof_grid_ports,
+                                  uint32_t                    nof_subc,
+                                  srs_amd_pucch_uci_result*   d_results,
+                                  uint8_t*                    d_payloads,
+                                  uint64_t                    payload_stride,
+                                  void*                       stream)
+{
+  return f2_slot(proc, pdus, nof_pdus, d_grids, grid_stride, nof_grids, nof_grid_ports, nof_subc, d_results,
+                 d_payloads, payload_stride, stream, true);
+}
+
+int srs_amd_pucch_f2_demodulate(srs_amd_pucch_processor*    proc,
+                                const srs_amd_pucch_f2_pdu* pdu,
+                                const uint32_t*             grid,
+                                uint32_t                    nof_ports,
+                                uint32_t                    nof_subc,
+                                int8_t*                     llrs)
+{
+  if (proc == nullptr || pdu == nullptr || grid == nullptr || llrs == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  const uint32_t              E     = 16 * pdu->nof_prb * pdu->nof_symbols;
+  const size_t                bytes = sizeof(uint32_t) * nof_ports * NSYMB * nof_subc;
+  std::lock_guard<std::mutex> host_lock(proc->host_mtx);
+  hipError_t                  e = hipSetDevice(proc->device);
+  if (e == hipSuccess) {
+    e = proc->host_grid.ensure(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->host_res.ensure(sizeof(srs_amd_pucch_uci_result));
+  }
+  if (e == hipSuccess) {
+    e = proc->host_payload.ensure(1706);
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(proc->host_grid.ptr, grid, bytes, hipMemcpyHostToDevice, proc->stream);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUCCH grid upload");
+  }
+  srs_amd_pucch_f2_pdu p = *pdu;
+  p.grid                 = 0;
+  p.d_grid               = nullptr;
+  int rc = f2_slot(proc, &p, 1, proc->host_grid.as<uint32_t>(), 0, 1, nof_ports, nof_subc,
+                   proc->host_res.as<srs_amd_pucch_uci_result>(), proc->host_payload.as<uint8_t>(), 1706,
+                   proc->stream, false);
+  if (rc == SRS_AMD_OK) {
+    e  = hipMemcpyAsync(llrs, proc->work.ptr, E, hipMemcpyDeviceToHost, proc->stream);
+    e  = e == hipSuccess ? hipStreamSynchronize(proc->stream) : e;
+    rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUCCH LLR download");
+  } else {
+    (void)hipStreamSynchronize(proc->stream);
+  }
+  return rc;
+}
+
+int srs_amd_pucch_f2_process(srs_amd_pucch_processor*    proc,
+                             const srs_amd_pucch_f2_pdu* pdu,
+                             const uint32_t*             grid,
+                             uint32_t                    nof_ports,
+                             uint32_t                    nof_subc,
+                             srs_amd_pucch_uci_result*   result,
+                             uint8_t*                    payload)
+{
+  if (proc == nullptr || pdu == nullptr || grid == nullptr || result == nullptr || payload == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  const uint32_t              K     = pdu->nof_harq_ack + pdu->nof_sr + pdu->nof_csi_part1 + pdu->nof_csi_part2;
+  const size_t                bytes = sizeof(uint32_t) * nof_ports * NSYMB * nof_subc;
+  std::lock_guard<std::mutex> host_lock(proc->host_mtx);
+  hipError_t                  e = hipSetDevice(proc->device);
+  if (e == hipSuccess) {
+    e = proc->host_grid.ensure(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->host_res.ensure(sizeof(srs_amd_pucch_uci_result));
+  }
+  if (e == hipSuccess) {
+    e = proc->host_payload.ensure(std::max(K, 1u));
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(proc->host_grid.ptr, grid, bytes, hipMemcpyHostToDevice, proc->stream);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUCCH grid upload");
+  }
+  srs_amd_pucch_f2_pdu p = *pdu;
+  p.grid                 = 0;
+  p.d_grid               = nullptr;
+  int rc = srs_amd_pucch_f2_process_slot(proc, &p, 1, proc->host_grid.as<uint32_t>(), 0, 1, nof_ports, nof_subc,
+                                         proc->host_res.as<srs_amd_pucch_uci_result>(),
+                                         proc->host_payload.as<uint8_t>(), std::max(K, 1u), proc->stream);
+  if (rc == SRS_AMD_OK) {
+    e = hipMemcpyAsync(result, proc->host_res.ptr, sizeof(*result), hipMemcpyDeviceToHost, proc->stream);
+    if (e == hipSuccess && K != 0) {
+      e = hipMemcpyAsync(payload, proc->host_payload.ptr, K, hipMemcpyDeviceToHost, proc->stream);
+    }
     e  = e == hipSuccess ? hipStreamSynchronize(proc->stream) : e;
     rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUCCH result download");
   } else {

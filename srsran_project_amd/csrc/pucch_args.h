@@ -55,4 +55,45 @@ struct pucch_f1_desc {
 hipError_t launch_pucch_f1(const pucch_f1_desc* d_desc, uint32_t nof, const srs_amd_pucch_f1_entry* d_entries,
                            srs_amd_pucch_result* d_results, hipStream_t stream);
 
+constexpr uint32_t PUCCH_F2_MAX_PRB = 16;
+constexpr uint32_t PUCCH_F2_MAX_RE  = 8 * PUCCH_F2_MAX_PRB * 2; // data REs of 16 PRBs over 2 symbols
+constexpr uint32_t PUCCH_F2_MAX_E   = 2 * PUCCH_F2_MAX_RE;      // QPSK LLRs
+constexpr uint32_t PUCCH_MAX_TA_N   = 256;                      // largest time-alignment IDFT of a PUCCH estimate
+
+struct pucch_f2_desc {
+  const uint32_t*           grid;        // cbf16 [port][14][nof_subc]
+  uint32_t                  port_stride; // 14 x nof_subc
+  uint32_t                  nof_subc;
+  uint32_t                  l0, nsym;    // allocation: first symbol, 1 or 2 symbols
+  uint32_t                  hop;         // frequency hopping (two hops of one symbol)
+  uint32_t                  nof_prb;
+  uint32_t                  prb[2];      // first PRB of allocated symbols 0 / 1 (absolute)
+  uint32_t                  nof_ports;
+  uint32_t                  ports[4];
+  float                     epoch[2];    // start epochs of allocated symbols 0 / 1 (symbol units)
+  float                     scs_hz;
+  int32_t                   nof_taps;    // FD filter (filter_type(min(nof_prb, 3), 3))
+  int32_t                   nof_v;       // virtual pilots per side
+  float                     rc[11];
+  uint32_t                  ta_n;        // time-alignment IDFT size
+  int32_t                   ta_max_taps;
+  int32_t                   ta_frac;     // fractional-delay refinement (ta_n below the largest IDFT)
+  double                    ta_fs;       // sampling rate of the IDFT (x stride 3)
+  uint32_t                  pil[2][4];   // DM-RS QPSK bits of allocated symbols 0 / 1 (2 per pilot)
+  uint32_t                  scr[PUCCH_F2_MAX_E / 32]; // data scrambling sequence c(0 .. E - 1)
+  uint32_t                  n_re;        // data REs, 8 nof_prb nsym
+  uint32_t                  counts[4];   // HARQ-ACK, SR, CSI part 1, CSI part 2 bits
+  int8_t*                   llr;         // the PDU's LLR row
+  srs_amd_pucch_uci_result* result;      // its result record (CSI fields)
+};
+
+// Estimation, equalization, demapping and descrambling of every Format 2 PDU (one 256-thread workgroup each).
+hipError_t launch_pucch_f2(const pucch_f2_desc* d_desc, uint32_t nof, hipStream_t stream);
+
+// Status and payload bits of row j (decoder order) to result / payload row perm[j] (user order).
+hipError_t launch_pucch_uci_finish(const int32_t* status, const uint8_t* messages, uint32_t msg_stride,
+                                   const uint32_t* perm, const uint32_t* nbits, uint32_t nof,
+                                   srs_amd_pucch_uci_result* results, uint8_t* payloads, uint64_t payload_stride,
+                                   hipStream_t stream);
+
 } // namespace srs_amd

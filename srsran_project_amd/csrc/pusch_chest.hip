@@ -42,6 +42,7 @@ using chdev::from_cbf16;
 using chdev::polar1;
 using chdev::to_cbf16;
 using chdev::TWOPI_F;
+using chdev::virtual_pilots_wave;
 constexpr float AMP = 0.70710678118654752440f; // M_SQRT1_2 as float
 
 __device__ __forceinline__ float2 cmulc(float2 a, float2 b) // a * conj(b)
@@ -107,74 +108,6 @@ __device__ __forceinline__ float2 pilot(const chest_args& a, const uint32_t (*se
     p = make_float2(-p.x, -p.y);
   }
   return p;
-}
-
-// compute_v_pilots (port_channel_estimator_helpers.cpp:334-378) over one wave: lane i < n <= 12 computes the
-// modulus / argument of value i and output value i; the short serial parts (phase unwrapping, the four
-// sums) run redundantly in every lane on the shuffled values, in the reference's order.  One lane running
-// the whole function was a chain of 3 n transcendental functions on the slice kernel's critical path.
-__device__ void virtual_pilots_wave(float2* out, const float2* in, int n, bool is_start)
-{
-  const int lane = static_cast<int>(threadIdx.x & 63u);
-  float     av = 0, gv = 0;
-  if (lane < n) {
-    av = sqrtf(in[lane].x * in[lane].x + in[lane].y * in[lane].y);
-    gv = atan2f(in[lane].y, in[lane].x);
-  }
-  float absv[CH_MAXV], argv[CH_MAXV];
-#pragma unroll
-  for (int i = 0; i < CH_MAXV; ++i) {
-    absv[i] = __shfl(av, i);
-    argv[i] = __shfl(gv, i);
-  }
-  // unwrap_list (unwrap.cpp:42-62)
-  const float width = 3.14159265358979323846f;
-  float       k     = 0;
-#pragma unroll
-  for (int i = 0; i < CH_MAXV - 1; ++i) {
-    if (i < n - 1) {
-      const float old_a = argv[i], next_a = argv[i + 1];
-      argv[i] += 2.0f * k * width;
-      const float jump = next_a - old_a;
-      if (fabsf(jump) > width) {
-        k = k - copysignf(1.0f, jump);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < CH_MAXV; ++i) {
-    if (i == n - 1) {
-      argv[i] += 2.0f * k * width;
-    }
-  }
-  const float mean_x    = static_cast<float>(n * (n - 1)) / 2.0f / n;
-  const float norm_x_sq = static_cast<float>((n - 1) * n * (2 * n - 1)) / 6.0f;
-  float       sa = 0, sg = 0, ma = 0, mg = 0;
-#pragma unroll
-  for (int i = 0; i < CH_MAXV; ++i) {
-    if (i < n) {
-      ma += absv[i];
-      mg += argv[i];
-      sa += absv[i] * static_cast<float>(i);
-      sg += argv[i] * static_cast<float>(i);
-    }
-  }
-  ma /= n;
-  mg /= n;
-  sa -= mean_x * ma * n;
-  sa /= (norm_x_sq - n * mean_x * mean_x);
-  sg -= mean_x * mg * n;
-  sg /= (norm_x_sq - n * mean_x * mean_x);
-  const float ia  = ma - sa * mean_x;
-  const float ig  = mg - sg * mean_x;
-  const int   off = is_start ? -n : n;
-  if (lane < n) {
-    const int   iv  = lane + off;
-    const float rho = sa * iv + ia;
-    const float ph  = sg * iv + ig + ((rho > 0) ? 0.0f : 3.14159265358979323846f);
-    const float r   = fabsf(rho);
-    out[lane]       = make_float2(r * cosf(ph), r * sinf(ph));
-  }
 }
 
 // Allocations of at most CH_SMALL_NPIL pilots per DM-RS symbol (68 PRBs: time-alignment IDFTs of <= 512 points)

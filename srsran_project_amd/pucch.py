@@ -49,6 +49,49 @@ class PucchF1Batch(ctypes.Structure):
                 ("grid", ctypes.c_uint32), ("d_grid", ctypes.c_void_p)]
 
 
+class PucchF2Pdu(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("numerology", "slot_index", "bwp_start_rb", "bwp_size_rb",
+                                                "starting_prb")] + [("second_hop_prb", ctypes.c_int32)] + \
+               [(n, ctypes.c_uint32) for n in ("nof_prb", "start_symbol_index", "nof_symbols", "rnti", "n_id", "n_id_0",
+                                                "nof_harq_ack", "nof_sr", "nof_csi_part1", "nof_csi_part2",
+                                                "nof_ports")] + \
+               [("ports", ctypes.c_uint8 * 4), ("grid", ctypes.c_uint32), ("d_grid", ctypes.c_void_p)]
+
+
+class PucchUciResult(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("status", "nof_harq_ack", "nof_sr", "nof_csi_part1", "nof_csi_part2")] + \
+               [(n, ctypes.c_float) for n in ("sinr_dB", "rsrp_dB", "epre_dB", "time_alignment_s", "cfo_Hz")]
+
+
+UCI_RESULT_DTYPE = np.dtype([(n, "<u4") for n in ("status", "nof_harq_ack", "nof_sr", "nof_csi_part1",
+                                                  "nof_csi_part2")] +
+                            [(n, "<f4") for n in ("sinr_dB", "rsrp_dB", "epre_dB", "time_alignment_s", "cfo_Hz")])
+assert UCI_RESULT_DTYPE.itemsize == ctypes.sizeof(PucchUciResult)
+
+
+def make_f2_pdu(*, numerology=0, slot_index=0, bwp_start_rb=0, bwp_size_rb=52, starting_prb=0, second_hop_prb=None,
+                nof_prb=1, start_symbol_index=12, nof_symbols=2, rnti=0x4601, n_id=0, n_id_0=0, nof_harq_ack=0,
+                nof_sr=0, nof_csi_part1=0, nof_csi_part2=0, ports=(0,), grid=0):
+    """pucch_processor::format2_configuration."""
+    p = PucchF2Pdu()
+    for k, v in dict(numerology=numerology, slot_index=slot_index, bwp_start_rb=bwp_start_rb, bwp_size_rb=bwp_size_rb,
+                     starting_prb=starting_prb, nof_prb=nof_prb, start_symbol_index=start_symbol_index,
+                     nof_symbols=nof_symbols, rnti=rnti, n_id=n_id, n_id_0=n_id_0, nof_harq_ack=nof_harq_ack,
+                     nof_sr=nof_sr, nof_csi_part1=nof_csi_part1, nof_csi_part2=nof_csi_part2, grid=grid).items():
+        setattr(p, k, int(v))
+    p.second_hop_prb = -1 if second_hop_prb is None else int(second_hop_prb)
+    if not 1 <= len(ports) <= 4:
+        raise ValueError("1 to 4 ports")
+    p.nof_ports = len(ports)
+    for i, q in enumerate(ports):
+        p.ports[i] = int(q)
+    return p
+
+
+def payload_bits(pdu):
+    return pdu.nof_harq_ack + pdu.nof_sr + pdu.nof_csi_part1 + pdu.nof_csi_part2
+
+
 RESULT_DTYPE = np.dtype([("status", "<u4"), ("nof_sr", "<u4"), ("nof_harq_ack", "<u4"), ("sr", "u1"),
                          ("harq_ack", "u1", (2,)), ("reserved", "u1"), ("detection_metric", "<f4"),
                          ("sinr_dB", "<f4"), ("rsrp_dB", "<f4"), ("epre_dB", "<f4")])
@@ -109,6 +152,10 @@ def _declare(lib):
         "srs_amd_pucch_f1_detect_slot": (c.c_int, [P, P, c.c_uint32, P, c.c_uint64, c.c_uint32, c.c_uint32,
                                                    c.c_uint32, P, P]),
         "srs_amd_pucch_f1_detect": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P]),
+        "srs_amd_pucch_f2_process_slot": (c.c_int, [P, P, c.c_uint32, P, c.c_uint64, c.c_uint32, c.c_uint32,
+                                                    c.c_uint32, P, P, c.c_uint64, P]),
+        "srs_amd_pucch_f2_process": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P, P]),
+        "srs_amd_pucch_f2_demodulate": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -196,6 +243,47 @@ class PucchProcessor:
             self._h, arr, len(batches), grids.data_ptr(), grids.stride(0), grids.shape[0], grids.shape[1],
             grids.shape[-1], out.data_ptr(), ctypes.c_void_p(stream.cuda_stream)), "pucch f1 detect_slot")
         return out[:total]
+
+    def process_f2(self, grid, pdu):
+        """pucch_processor::process of one Format 2 PDU on a host grid -> (PucchUciResult, payload bits uint8)."""
+        if grid.dtype != np.uint32 or grid.ndim != 3 or grid.shape[1] != 14 or not grid.flags.c_contiguous:
+            raise ValueError("grid must be a C-contiguous uint32 array [ports][14][nof_subc]")
+        r = PucchUciResult()
+        payload = np.zeros(max(payload_bits(pdu), 1), np.uint8)
+        _lib.check(self._lib.srs_amd_pucch_f2_process(self._h, ctypes.byref(pdu), grid.ctypes.data, grid.shape[0],
+                                                      grid.shape[2], ctypes.byref(r), payload.ctypes.data),
+                   "pucch f2 process")
+        return r, payload[:payload_bits(pdu)]
+
+    def demodulate_f2(self, grid, pdu):
+        """Estimator + pucch_demodulator of one Format 2 PDU on a host grid -> int8 LLRs [16 nof_prb nof_symbols]."""
+        if grid.dtype != np.uint32 or grid.ndim != 3 or grid.shape[1] != 14 or not grid.flags.c_contiguous:
+            raise ValueError("grid must be a C-contiguous uint32 array [ports][14][nof_subc]")
+        llr = np.zeros(16 * pdu.nof_prb * pdu.nof_symbols, np.int8)
+        _lib.check(self._lib.srs_amd_pucch_f2_demodulate(self._h, ctypes.byref(pdu), grid.ctypes.data, grid.shape[0],
+                                                         grid.shape[2], llr.ctypes.data), "pucch f2 demodulate")
+        return llr
+
+    def process_f2_slot(self, grids, pdus, payload_stride=1706, stream=None):
+        """Every Format 2 PDU of a slot on device grids (torch int32 [n][ports][14][nof_subc]) -> (torch uint8
+        [n][UCI_RESULT_DTYPE record], torch uint8 [n][payload_stride] payload rows), asynchronous on stream."""
+        import torch
+
+        arr = (PucchF2Pdu * len(pdus))(*pdus)
+        res = torch.zeros((max(len(pdus), 1), UCI_RESULT_DTYPE.itemsize), dtype=torch.uint8, device=grids.device)
+        pay = torch.zeros((max(len(pdus), 1), payload_stride), dtype=torch.uint8, device=grids.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(grids.device)
+        _lib.check(self._lib.srs_amd_pucch_f2_process_slot(
+            self._h, arr, len(pdus), grids.data_ptr(), grids.stride(0), grids.shape[0], grids.shape[1],
+            grids.shape[-1], res.data_ptr(), pay.data_ptr(), payload_stride, ctypes.c_void_p(stream.cuda_stream)),
+            "pucch f2 process_slot")
+        return res[:len(pdus)], pay[:len(pdus)]
+
+
+def parse_uci_results(raw):
+    """uint8 [n][record] (numpy) -> UCI_RESULT_DTYPE records."""
+    return np.ascontiguousarray(raw).view(UCI_RESULT_DTYPE).reshape(-1)
 
 
 def parse_results(raw):

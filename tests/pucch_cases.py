@@ -75,3 +75,41 @@ def f1_cases(n=16, seed=0):
         op.transmit_f1(grid, b, pucchs, [0.01, 0.1, 1.0, 3.0][i % 4], rng)
         out.append((b, grid, sent))
     return out
+
+
+def f2_cases(n=16, seed=0):
+    """[(pdu, grid uint32 [4][14][NSUBC], payload bits)]: 1-16 PRBs, 1-2 symbols, hopping, 1-4 ports (0 .. n-1: the
+    reference's demodulator reads grid ports 0 .. n-1), 3-11 bit (Reed-Muller) and 12+ bit (polar) payloads within the
+    0.8 code rate, SNRs from clean to failing."""
+    from oracle import pucch as op
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        nprb = int(rng.integers(1, 17))
+        nsym = int(rng.integers(1, 3))
+        hop = nsym == 2 and i % 3 == 0
+        nports = int(rng.integers(1, 5))
+        mu = int(rng.integers(0, 3))
+        E = 16 * nprb * nsym
+        kmax = max(3, min(int(0.8 * E) - 11, 300))
+        K = int(rng.integers(3, 12)) if (i % 2 == 0 or kmax < 12) else int(rng.integers(12, kmax + 1))
+        while K > 11 and (K + (6 if K < 20 else 11)) > 0.8 * E:
+            K -= 1
+        if K > 11 and K + (6 if K < 20 else 11) > 0.8 * E or (K <= 11 and K > 0.8 * E):
+            K = 3
+        nh = int(rng.integers(0, K + 1))
+        nsr = int(rng.integers(0, min(4, K - nh) + 1))
+        pdu = amd.pucch.make_f2_pdu(numerology=mu, slot_index=int(rng.integers(0, 10 << mu)), bwp_start_rb=2,
+                                    bwp_size_rb=48, starting_prb=int(rng.integers(0, 48 - nprb + 1)),
+                                    second_hop_prb=int(rng.integers(0, 48 - nprb + 1)) if hop else None,
+                                    nof_prb=nprb, start_symbol_index=int(rng.integers(0, 15 - nsym)),
+                                    nof_symbols=nsym, rnti=int(rng.integers(1, 65536)), n_id=int(rng.integers(0, 1024)),
+                                    n_id_0=int(rng.integers(0, 65536)), nof_harq_ack=nh, nof_sr=nsr,
+                                    nof_csi_part1=K - nh - nsr, ports=tuple(range(nports)))
+        payload = rng.integers(0, 2, K).astype(np.uint8)
+        grid = rng.integers(0, 1 << 32, (4, 14, NSUBC), dtype=np.uint64).astype(np.uint32)
+        gains = (rng.normal(size=nports) + 1j * rng.normal(size=nports)) / np.sqrt(2)
+        op.transmit_f2(grid, pdu, payload, gains, [0.001, 0.03, 0.3, 3.0][i % 4], rng)
+        out.append((pdu, grid, payload))
+    return out

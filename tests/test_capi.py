@@ -157,7 +157,7 @@ def test_integration_plugins_built_against_reference_headers():
 
 
 def test_channel_processor_plugins_take_only_reference_interface_symbols():
-    """integration/_build/libsrsran_amd_phy.so -- the pusch / pdsch / pdcch / ssb processor plug-ins -- exports its factory
+    """integration/_build/libsrsran_amd_phy.so -- the pusch / pdsch / pdcch / ssb / pucch processor plug-ins -- exports its factory
     entry points and leaves undefined only the vtables / typeinfo of the reference's factory interfaces (their key
     function, create(srslog::basic_logger&), lives in the srsRAN library the plug-in is linked into) and
     rb_allocation::get_crb_mask; with the
@@ -174,12 +174,16 @@ def test_channel_processor_plugins_take_only_reference_interface_symbols():
     assert "srsran::hip::create_pdsch_processor_factory_hip(srsran::hip::pdsch_processor_hip_config const&)" in out
     assert "srsran::hip::create_pdcch_processor_factory_hip(srsran::hip::pdcch_processor_hip_config const&)" in out
     assert "srsran::hip::create_ssb_processor_factory_hip(srsran::hip::ssb_processor_hip_config const&)" in out
+    assert "srsran::hip::create_pucch_processor_factory_hip(srsran::hip::pucch_processor_hip_config const&)" in out
     undef = subprocess.run(["nm", "-D", "-C", "-u", path], capture_output=True, text=True, check=True).stdout
     ref_syms = sorted({l.split(" U ")[-1].strip() for l in undef.splitlines() if "srsran::" in l or "srslog::" in l})
     allowed = {"vtable for srsran::pusch_processor_factory", "typeinfo for srsran::pusch_processor_factory",
                "vtable for srsran::pdsch_processor_factory", "typeinfo for srsran::pdsch_processor_factory",
                "vtable for srsran::pdcch_processor_factory", "typeinfo for srsran::pdcch_processor_factory",
                "vtable for srsran::ssb_processor_factory", "typeinfo for srsran::ssb_processor_factory",
+               "vtable for srsran::pucch_processor_factory", "typeinfo for srsran::pucch_processor_factory",
+               "srsran::pucch_processor_factory::create(srslog::detail::logger_impl<srslog::basic_logger_channels, "
+               "srslog::basic_levels>&)",
                "srsran::rb_allocation::get_crb_mask(unsigned int, unsigned int) const"}
     assert set(ref_syms) <= allowed, ref_syms
     ctypes.CDLL(ref, mode=ctypes.RTLD_GLOBAL)

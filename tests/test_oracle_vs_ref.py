@@ -559,3 +559,19 @@ def test_pucch_f1_restatement_matches_reference():
             np.testing.assert_allclose(r.detection_metric, metric, rtol=1e-3, err_msg=str((i, j)))
             for a, c in ((r.sinr_dB, sinr), (r.rsrp_dB, rsrp), (r.epre_dB, epre)):
                 assert abs(a - c) <= 0.01, (i, j, a, c)
+
+
+def test_pucch_f2_transmitter_decoded_by_reference():
+    """tests/pucch_cases.py's Format 2 transmitter (UCI encoding, scrambling, DM-RS) is the reference receiver's
+    convention: at the highest SNR of the cases the compiled pucch_processor_impl returns the payload, valid."""
+    from oracle import pucch as op
+    from tests.pucch_cases import f2_cases
+
+    n = 0
+    for i, (pdu, grid, payload) in enumerate(f2_cases(n=12, seed=5)):
+        if i % 4 != 0:
+            continue
+        r, pay = op.ref_process_f2(grid, pdu)
+        assert r.status == 1 and np.array_equal(pay, payload), i
+        n += 1
+    assert n == 3

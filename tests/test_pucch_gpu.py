@@ -159,3 +159,95 @@ def test_pucch_f1_invalid_batch_fails_loudly(proc):
     for entries, kw in bad:
         with pytest.raises(ValueError):
             proc.detect_f1(g, amd.pucch.make_f1_batch(entries, **kw))
+
+
+# ---- Format 2 ------------------------------------------------------------------------------------------------------
+F2_TA_TOL = 2.5 / (480e3 * 4096)  # two T_C units: the correlation peak's fractional refinement in float
+
+
+def _check_uci(i, got, pay, want, want_pay):
+    assert got["status"] == want.status, (i, got["status"], want.status, want.sinr_dB)
+    for k in ("nof_harq_ack", "nof_sr", "nof_csi_part1", "nof_csi_part2"):
+        assert got[k] == getattr(want, k), (i, k)
+    assert np.array_equal(np.asarray(pay), np.asarray(want_pay)), i
+    for k in ("sinr_dB", "rsrp_dB", "epre_dB"):
+        assert abs(float(got[k]) - getattr(want, k)) <= 0.02, (i, k, got[k], getattr(want, k))
+    assert abs(float(got["time_alignment_s"]) - want.time_alignment_s) <= F2_TA_TOL, (i, got["time_alignment_s"],
+                                                                                      want.time_alignment_s)
+    if np.isnan(want.cfo_Hz):
+        assert np.isnan(got["cfo_Hz"]), i
+    else:
+        assert abs(float(got["cfo_Hz"]) - want.cfo_Hz) <= 1e-3 * max(1.0, abs(want.cfo_Hz)), (i, got["cfo_Hz"],
+                                                                                               want.cfo_Hz)
+
+
+def _uci_rec(r):
+    import srsran_project_amd as amd
+
+    return np.frombuffer(bytes(r), amd.pucch.UCI_RESULT_DTYPE)[0]
+
+
+def test_pucch_f2_llrs_vs_reference(proc):
+    """The descrambled LLRs of the estimator + demodulator against the compiled dmrs_pucch_estimator_format2 +
+    pucch_demodulator_format2: every LLR within one quantisation step, at least 99 % identical."""
+    from oracle import pucch as op
+    from tests.pucch_cases import f2_cases
+
+    for i, (pdu, grid, payload) in enumerate(f2_cases(n=24, seed=1)):
+        want = op.ref_demodulate_f2(grid, pdu).astype(np.int32)
+        got = proc.demodulate_f2(grid, pdu).astype(np.int32)
+        diff = np.abs(got - want)
+        bad = np.nonzero(diff > 1)[0]
+        assert bad.size == 0, (i, pdu.nof_prb, pdu.nof_symbols, pdu.second_hop_prb, bad[:8], got[bad[:8]],
+                               want[bad[:8]], int(np.sum(np.sign(got) != np.sign(want))))
+        assert np.mean(diff == 0) >= 0.99, (i, float(np.mean(diff == 0)))
+
+
+def test_pucch_f2_host_form_vs_reference(proc):
+    """Payload bits and status equal to the compiled pucch_processor_impl; CSI within 0.02 dB / two T_C / 1e-3."""
+    from oracle import pucch as op
+    from tests.pucch_cases import f2_cases
+
+    n_valid = 0
+    for i, (pdu, grid, payload) in enumerate(f2_cases(n=24, seed=1)):
+        want, want_pay = op.ref_process_f2(grid, pdu)
+        got, pay = proc.process_f2(grid, pdu)
+        _check_uci(i, _uci_rec(got), pay, want, want_pay)
+        n_valid += want.status == 1
+    assert 0 < n_valid < 24
+
+
+def test_pucch_f2_slot_form_one_call(proc):
+    """Many PDUs of mixed payload / codeword sizes (several UCI decoder groups) over their own grids in one call."""
+    import torch
+
+    import srsran_project_amd as amd
+    from oracle import pucch as op
+    from tests.pucch_cases import f2_cases
+
+    cs = f2_cases(n=20, seed=2)
+    for i, (pdu, _, _) in enumerate(cs):
+        pdu.grid = i
+    g = np.stack([c[1] for c in cs])
+    d = torch.from_numpy(g.view(np.int32).copy()).to("cuda:0")
+    res, pay = proc.process_f2_slot(d, [c[0] for c in cs])
+    torch.cuda.synchronize()
+    got = amd.pucch.parse_uci_results(res.cpu().numpy())
+    pay = pay.cpu().numpy()
+    for i, (pdu, grid, _) in enumerate(cs):
+        want, want_pay = op.ref_process_f2(grid, pdu)
+        _check_uci(i, got[i], pay[i, :amd.pucch.payload_bits(pdu)], want, want_pay)
+
+
+def test_pucch_f2_invalid_pdu_fails_loudly(proc):
+    import srsran_project_amd as amd
+
+    g = np.zeros((4, 14, 624), np.uint32)
+    ok = dict(nof_prb=2, nof_harq_ack=4)
+    bad = [dict(nof_prb=17, nof_harq_ack=4), dict(nof_prb=0, nof_harq_ack=4), dict(ok, nof_symbols=3),
+           dict(ok, start_symbol_index=13), dict(ok, nof_symbols=1, second_hop_prb=5), dict(ok, nof_harq_ack=2),
+           dict(ok, nof_csi_part2=4), dict(nof_prb=1, nof_symbols=1, nof_harq_ack=20), dict(ok, starting_prb=51),
+           dict(ok, bwp_start_rb=10, bwp_size_rb=48), dict(ok, ports=(4,)), dict(ok, n_id=1024)]
+    for kw in bad:
+        with pytest.raises(ValueError):
+            proc.process_f2(g, amd.pucch.make_f2_pdu(**kw))
