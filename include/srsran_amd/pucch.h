@@ -17,6 +17,11 @@
  * REs over the ports, QPSK soft demapping, descrambling, and the UCI decoder (short block or polar) -- payload bits,
  * status and the CSI (SINR, RSRP, EPRE, time alignment, CFO).
  *
+ * Formats 3 and 4 (DFT-s-OFDM): per port the estimate from the low-PAPR DM-RS symbols (filter, averaging, CFO
+ * measured but not compensated), per data symbol ZF equalization and transform deprecoding (IDFT of 12 nof_prb points,
+ * mean noise), Format 4's inverse block-wise spreading (OCC of length 2 / 4), QPSK or pi/2-BPSK demapping,
+ * descrambling, and the UCI decoder.
+ *
  * Replaces (reference interface):
  *   pucch_detector::detect(const resource_grid_reader&, const format0_configuration&)
  *       include/srsran/phy/upper/channel_processors/pucch/pucch_detector.h:44-77 (format0_configuration)
@@ -199,6 +204,68 @@ int srs_amd_pucch_f2_process(srs_amd_pucch_processor*    proc,
                              uint32_t                    nof_subc,
                              srs_amd_pucch_uci_result*   result,
                              uint8_t*                    payload);
+
+/* pucch_processor::format3_configuration / format4_configuration (pucch_processor.h:277-394). */
+typedef struct srs_amd_pucch_f34_pdu {
+  uint32_t format;              /* 3 or 4 */
+  uint32_t numerology;
+  uint32_t slot_index;
+  uint32_t bwp_start_rb;
+  uint32_t bwp_size_rb;
+  uint32_t starting_prb;        /* within the BWP */
+  int32_t  second_hop_prb;      /* within the BWP; -1: no frequency hopping */
+  uint32_t nof_prb;             /* Format 3: 1 .. 16 with 2^a 3^b 5^c PRBs; Format 4: 1 */
+  uint32_t start_symbol_index;
+  uint32_t nof_symbols;         /* 4 .. 14 */
+  uint32_t rnti;
+  uint32_t n_id_hopping;        /* DM-RS sequence group / cyclic-shift hopping identity */
+  uint32_t n_id_scrambling;     /* data scrambling identity */
+  uint32_t nof_harq_ack;
+  uint32_t nof_sr;
+  uint32_t nof_csi_part1;
+  uint32_t nof_csi_part2;       /* must be 0 */
+  uint32_t additional_dmrs;     /* 0 / 1 */
+  uint32_t pi2_bpsk;            /* 0: QPSK, 1: pi/2-BPSK */
+  uint32_t occ_index;           /* Format 4 */
+  uint32_t occ_length;          /* Format 4: 2 or 4 */
+  uint32_t nof_ports;           /* 1 .. 4 */
+  uint8_t  ports[4];
+  uint32_t grid;
+  const uint32_t* d_grid;
+} srs_amd_pucch_f34_pdu;
+
+/* DEVICE, asynchronous: every Format 3 / 4 PDU of a slot; result i to d_results[i], its payload bits to
+ * d_payloads + i * payload_stride. */
+int srs_amd_pucch_f34_process_slot(srs_amd_pucch_processor*     proc,
+                                   const srs_amd_pucch_f34_pdu* pdus,
+                                   uint32_t                     nof_pdus,
+                                   const uint32_t*              d_grids,
+                                   uint64_t                     grid_stride,
+                                   uint32_t                     nof_grids,
+                                   uint32_t                     nof_grid_ports,
+                                   uint32_t                     nof_subc,
+                                   srs_amd_pucch_uci_result*    d_results,
+                                   uint8_t*                     d_payloads,
+                                   uint64_t                     payload_stride,
+                                   void*                        stream);
+
+/* HOST, synchronous: one Format 3 / 4 PDU; payload[nof bits]. */
+int srs_amd_pucch_f34_process(srs_amd_pucch_processor*     proc,
+                              const srs_amd_pucch_f34_pdu* pdu,
+                              const uint32_t*              grid,
+                              uint32_t                     nof_ports,
+                              uint32_t                     nof_subc,
+                              srs_amd_pucch_uci_result*    result,
+                              uint8_t*                     payload);
+
+/* HOST, synchronous: estimator + pucch_demodulator (format3 / format4, pucch_demodulator_format3.cpp /
+ * pucch_demodulator_format4.cpp) of one PDU -- the descrambled LLRs. */
+int srs_amd_pucch_f34_demodulate(srs_amd_pucch_processor*     proc,
+                                 const srs_amd_pucch_f34_pdu* pdu,
+                                 const uint32_t*              grid,
+                                 uint32_t                     nof_ports,
+                                 uint32_t                     nof_subc,
+                                 int8_t*                      llrs);
 
 /* HOST, synchronous: the estimator and demodulator of one Format 2 PDU -- pucch_demodulator::demodulate
  * (pucch_demodulator.h, impl pucch_demodulator_format2.cpp:92-160) after dmrs_pucch_estimator::estimate --

@@ -78,6 +78,38 @@ srs_amd_pucch_f2_pdu convert(const pucch_processor::format2_configuration& c)
   return p;
 }
 
+template <typename C>
+srs_amd_pucch_f34_pdu convert34(const C& c, uint32_t format, uint32_t nof_prb, uint32_t occ_index, uint32_t occ_length)
+{
+  srs_amd_pucch_f34_pdu p{};
+  p.format             = format;
+  p.numerology         = numerology_of(c.slot);
+  p.slot_index         = c.slot.slot_index();
+  p.bwp_start_rb       = c.bwp_start_rb;
+  p.bwp_size_rb        = c.bwp_size_rb;
+  p.starting_prb       = c.starting_prb;
+  p.second_hop_prb     = c.second_hop_prb.has_value() ? static_cast<int32_t>(*c.second_hop_prb) : -1;
+  p.nof_prb            = nof_prb;
+  p.start_symbol_index = c.start_symbol_index;
+  p.nof_symbols        = c.nof_symbols;
+  p.rnti               = c.rnti;
+  p.n_id_hopping       = c.n_id_hopping;
+  p.n_id_scrambling    = c.n_id_scrambling;
+  p.nof_harq_ack       = c.nof_harq_ack;
+  p.nof_sr             = c.nof_sr;
+  p.nof_csi_part1      = c.nof_csi_part1;
+  p.nof_csi_part2      = c.nof_csi_part2;
+  p.additional_dmrs    = c.additional_dmrs ? 1 : 0;
+  p.pi2_bpsk           = c.pi2_bpsk ? 1 : 0;
+  p.occ_index          = occ_index;
+  p.occ_length         = occ_length;
+  p.nof_ports          = static_cast<uint32_t>(c.ports.size());
+  for (unsigned i = 0; i != c.ports.size() && i != 4; ++i) {
+    p.ports[i] = c.ports[i];
+  }
+  return p;
+}
+
 struct shared_state {
   srs_amd_pucch_processor*   proc   = nullptr;
   int                        device = 0;
@@ -224,6 +256,52 @@ public:
         }, PAYLOAD_OFF + K)) {
       return result;
     }
+    fill_uci(result, K);
+    return result;
+  }
+
+  pucch_processor_result process(const resource_grid_reader& grid, const format3_configuration& config) override
+  {
+    return process34(grid, convert34(config, 3, config.nof_prb, 0, 1), config.nof_sr, config.nof_harq_ack,
+                     config.nof_csi_part1, config.nof_csi_part2);
+  }
+
+  pucch_processor_result process(const resource_grid_reader& grid, const format4_configuration& config) override
+  {
+    return process34(grid, convert34(config, 4, 1, config.occ_index, config.occ_length), config.nof_sr,
+                     config.nof_harq_ack, config.nof_csi_part1, config.nof_csi_part2);
+  }
+
+private:
+  static constexpr size_t RES_BYTES   = 4096;
+  static constexpr size_t PAYLOAD_OFF = 256;
+
+  // Formats 3 / 4: the PDU's symbols through srs_amd_pucch_f34_process_slot, the message and CSI back.
+  pucch_processor_result process34(const resource_grid_reader& grid, srs_amd_pucch_f34_pdu p, unsigned sr,
+                                   unsigned harq, unsigned csi1, unsigned csi2)
+  {
+    ++st->nof_pdus;
+    pucch_processor_result result;
+    result.message = pucch_uci_message({.nof_sr = sr, .nof_harq_ack = harq, .nof_csi_part1 = csi1,
+                                        .nof_csi_part2 = csi2});
+    result.message.set_status(uci_status::invalid);
+    const unsigned  K         = sr + harq + csi1 + csi2;
+    unsigned        nof_ports = 0, nsubc = 0;
+    const uint32_t* g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
+    auto*           d_pay = static_cast<uint8_t*>(d_res) + PAYLOAD_OFF;
+    if (g == nullptr || K > 1706 || !run([&] {
+          p.d_grid = g;
+          return srs_amd_pucch_f34_process_slot(st->proc, &p, 1, nullptr, 0, 0, nof_ports, nsubc,
+                                                static_cast<srs_amd_pucch_uci_result*>(d_res), d_pay, 1706, stream);
+        }, PAYLOAD_OFF + K)) {
+      return result;
+    }
+    fill_uci(result, K);
+    return result;
+  }
+
+  void fill_uci(pucch_processor_result& result, unsigned K) const
+  {
     const auto* r = static_cast<const srs_amd_pucch_uci_result*>(h_res);
     std::memcpy(result.message.get_full_payload().data(), static_cast<const uint8_t*>(h_res) + PAYLOAD_OFF, K);
     result.message.set_status(static_cast<uci_status>(r->status));
@@ -235,33 +313,6 @@ public:
     if (!std::isnan(r->cfo_Hz)) {
       result.csi.set_cfo(r->cfo_Hz);
     }
-    return result;
-  }
-
-  pucch_processor_result process(const resource_grid_reader&, const format3_configuration& config) override
-  {
-    return unsupported("Format 3", config.nof_sr, config.nof_harq_ack, config.nof_csi_part1, config.nof_csi_part2);
-  }
-
-  pucch_processor_result process(const resource_grid_reader&, const format4_configuration& config) override
-  {
-    return unsupported("Format 4", config.nof_sr, config.nof_harq_ack, config.nof_csi_part1, config.nof_csi_part2);
-  }
-
-private:
-  static constexpr size_t RES_BYTES   = 4096;
-  static constexpr size_t PAYLOAD_OFF = 256;
-
-  pucch_processor_result unsupported(const char* what, unsigned sr, unsigned harq, unsigned csi1, unsigned csi2)
-  {
-    ++st->nof_pdus;
-    ++st->nof_errors;
-    log_error(what, "not supported by the hip PUCCH processor");
-    pucch_processor_result result;
-    result.message = pucch_uci_message({.nof_sr = sr, .nof_harq_ack = harq, .nof_csi_part1 = csi1,
-                                        .nof_csi_part2 = csi2});
-    result.message.set_status(uci_status::invalid);
-    return result;
   }
 
   // Launch through `call`, bring `bytes` of the result buffer back, wait.  false (logged) on any error.
@@ -415,16 +466,64 @@ public:
     }
     return ports_ok(c.ports);
   }
-  error_type<std::string> is_valid(const pucch_processor::format3_configuration&) const override
+  error_type<std::string> is_valid(const pucch_processor::format3_configuration& c) const override
   {
-    return make_unexpected(std::string("PUCCH Format 3 is not supported by the hip PUCCH processor"));
+    return f34_ok(c, c.nof_prb, false, 1);
   }
-  error_type<std::string> is_valid(const pucch_processor::format4_configuration&) const override
+  error_type<std::string> is_valid(const pucch_processor::format4_configuration& c) const override
   {
-    return make_unexpected(std::string("PUCCH Format 4 is not supported by the hip PUCCH processor"));
+    if (c.occ_length != 2 && c.occ_length != 4) {
+      return make_unexpected(std::string("Invalid OCC length value. Valid values are 2 and 4."));
+    }
+    return f34_ok(c, 1, true, c.occ_length);
   }
 
 private:
+  // pucch_pdu_validator_impl format3 / format4 checks (pucch_processor_impl.cpp), plus the transform-precoding PRB
+  // sizes and the symbol range the reference asserts on.
+  template <typename C>
+  error_type<std::string> f34_ok(const C& c, unsigned nprb, bool f4, unsigned occ) const
+  {
+    static const unsigned masks[2][15] = {{0, 0, 0, 0, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2},
+                                          {0, 0, 0, 0, 2, 2, 2, 2, 2, 2, 4, 4, 4, 4, 4}};
+    if (c.bwp_start_rb + c.bwp_size_rb > cfg.max_nof_prb || c.starting_prb + nprb > c.bwp_size_rb) {
+      return make_unexpected(std::string("PRB allocation outside the BWP or the grid"));
+    }
+    unsigned n = nprb;
+    for (unsigned f : {2U, 3U, 5U}) {
+      while (n != 0 && n % f == 0) {
+        n /= f;
+      }
+    }
+    if (nprb == 0 || nprb > 16 || n != 1) {
+      return make_unexpected(std::string("Number of PRBs is outside the allowed range for PUCCH Format 3"));
+    }
+    if (c.nof_symbols < 4 || c.nof_symbols > 14 || c.start_symbol_index + c.nof_symbols > NSYMB) {
+      return make_unexpected(std::string("invalid Format 3 / 4 symbols"));
+    }
+    if (c.nof_csi_part2 != 0) {
+      return make_unexpected(std::string("CSI Part 2 is not currently supported."));
+    }
+    unsigned nd = masks[c.additional_dmrs ? 1 : 0][c.nof_symbols];
+    if (c.nof_symbols == 4 && c.second_hop_prb.has_value()) {
+      nd = 2;
+    }
+    const unsigned K     = c.nof_harq_ack + c.nof_sr + c.nof_csi_part1 + c.nof_csi_part2;
+    const unsigned qb    = c.pi2_bpsk ? 1 : 2;
+    const unsigned nds   = c.nof_symbols - nd;
+    const unsigned e_tot = f4 ? 12 * nds * qb / occ : 12 * nprb * nds * qb;
+    const unsigned chan  = 12 * (f4 ? 1 : nprb) * nds * qb;
+    const unsigned ncb   = ((K >= 360 && e_tot >= 1088) || K >= 1013) ? 2 : 1;
+    const unsigned L     = K <= 11 ? 0 : (K <= 19 ? 6 : 11);
+    if (static_cast<float>(K + ncb * L) / static_cast<float>(chan) > 0.8F) {
+      return make_unexpected(std::string("The effective code rate exceeds the maximum allowed 0.8"));
+    }
+    if (K < 3 || K > 1706) {
+      return make_unexpected(std::string("UCI Payload length is outside the supported range"));
+    }
+    return ports_ok(c.ports);
+  }
+
   error_type<std::string> ports_ok(const static_vector<uint8_t, MAX_PORTS>& ports) const
   {
     if (ports.empty() || ports.size() > cfg.max_nof_ports || ports.size() > 4) {

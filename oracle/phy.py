@@ -517,6 +517,7 @@ class PucchProcessorPlugin:
         L.srs_ref_phy_pucch_f0.argtypes = [P, P, P, u, P]
         L.srs_ref_phy_pucch_f1.argtypes = [P, P, P, u, P]
         L.srs_ref_phy_pucch_f2.argtypes = [P, P, P, P, P]
+        L.srs_ref_phy_pucch_f34.argtypes = [P, P, P, P, P]
         L.srs_ref_phy_pucch_f2_validate.restype = i
         L.srs_ref_phy_pucch_f2_validate.argtypes = [P, P, ctypes.c_char_p, u]
         L.srs_ref_phy_pucch_stats.argtypes = [P, P]
@@ -555,6 +556,14 @@ class PucchProcessorPlugin:
         r = PucchUciResult()
         pay = np.zeros(max(payload_bits(pdu), 1), np.uint8)
         lib().srs_ref_phy_pucch_f2(self.h, grid.h, ctypes.byref(pdu), ctypes.byref(r), pay.ctypes.data)
+        return r, pay[:payload_bits(pdu)]
+
+    def f34(self, grid, pdu):
+        from srsran_project_amd.pucch import PucchUciResult, payload_bits
+
+        r = PucchUciResult()
+        pay = np.zeros(max(payload_bits(pdu), 1), np.uint8)
+        lib().srs_ref_phy_pucch_f34(self.h, grid.h, ctypes.byref(pdu), ctypes.byref(r), pay.ctypes.data)
         return r, pay[:payload_bits(pdu)]
 
     def validate_f2(self, pdu):

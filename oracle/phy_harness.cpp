@@ -1192,6 +1192,61 @@ void srs_ref_phy_pucch_f2(void* h, void* g, const srs_amd_pucch_f2_pdu* p, srs_a
   out->cfo_Hz           = r.csi.get_cfo_Hz().value_or(NAN);
 }
 
+/* pucch_processor::process(format3 / format4_configuration) of a C-ABI Format 3 / 4 PDU; payload[nof bits]. */
+void srs_ref_phy_pucch_f34(void* h, void* g, const srs_amd_pucch_f34_pdu* p, srs_amd_pucch_uci_result* out,
+                           uint8_t* payload)
+{
+  auto fill = [p](auto& c) {
+    c.slot = slot_point(p->numerology, p->slot_index);
+    c.cp   = cyclic_prefix::NORMAL;
+    for (unsigned i = 0; i != p->nof_ports; ++i) {
+      c.ports.push_back(p->ports[i]);
+    }
+    c.bwp_size_rb  = p->bwp_size_rb;
+    c.bwp_start_rb = p->bwp_start_rb;
+    c.starting_prb = p->starting_prb;
+    if (p->second_hop_prb >= 0) {
+      c.second_hop_prb = static_cast<unsigned>(p->second_hop_prb);
+    }
+    c.start_symbol_index = p->start_symbol_index;
+    c.nof_symbols        = p->nof_symbols;
+    c.rnti               = static_cast<uint16_t>(p->rnti);
+    c.n_id_hopping       = p->n_id_hopping;
+    c.n_id_scrambling    = p->n_id_scrambling;
+    c.nof_harq_ack       = p->nof_harq_ack;
+    c.nof_sr             = p->nof_sr;
+    c.nof_csi_part1      = p->nof_csi_part1;
+    c.nof_csi_part2      = p->nof_csi_part2;
+    c.additional_dmrs    = p->additional_dmrs != 0;
+    c.pi2_bpsk           = p->pi2_bpsk != 0;
+  };
+  auto*                  ctx = static_cast<pucch_ctx*>(h);
+  pucch_processor_result r;
+  if (p->format == 4) {
+    pucch_processor::format4_configuration c;
+    fill(c);
+    c.occ_index  = p->occ_index;
+    c.occ_length = p->occ_length;
+    r            = ctx->proc->process(static_cast<any_grid*>(g)->rd(), c);
+  } else {
+    pucch_processor::format3_configuration c;
+    fill(c);
+    c.nof_prb = p->nof_prb;
+    r         = ctx->proc->process(static_cast<any_grid*>(g)->rd(), c);
+  }
+  std::memset(out, 0, sizeof(*out));
+  out->status        = static_cast<uint32_t>(r.message.get_status());
+  out->nof_harq_ack  = r.message.get_harq_ack_bits().size();
+  out->nof_sr        = r.message.get_sr_bits().size();
+  out->nof_csi_part1 = r.message.get_csi_part1_bits().size();
+  out->nof_csi_part2 = r.message.get_csi_part2_bits().size();
+  const auto full    = r.message.get_full_payload();
+  std::memcpy(payload, full.data(), full.size());
+  csi_out(r.csi, &out->sinr_dB, &out->rsrp_dB, &out->epre_dB);
+  out->time_alignment_s = r.csi.get_time_alignment().has_value() ? r.csi.get_time_alignment()->to_seconds() : NAN;
+  out->cfo_Hz           = r.csi.get_cfo_Hz().value_or(NAN);
+}
+
 /* The plug-in factory's validator on a Format 2 PDU: 1 valid, 0 invalid (msg filled). */
 int srs_ref_phy_pucch_f2_validate(void* h, const srs_amd_pucch_f2_pdu* p, char* msg, unsigned msg_size)
 {

@@ -360,3 +360,101 @@ def ref_demodulate_f2(grid, pdu):
     llr = np.zeros(16 * pdu.nof_prb * pdu.nof_symbols, np.int8)
     ref.srs_ref_pucch_f2_demodulate(g.ctypes.data, g.shape[0], g.shape[2], ctypes.addressof(pdu), llr.ctypes.data)
     return llr
+
+
+# ---- Formats 3 / 4 -------------------------------------------------------------------------------------------------
+F4_OCC = {2: [[1] * 12, [1] * 6 + [-1] * 6],
+          4: [[1] * 12, [1] * 3 + [-1j] * 3 + [-1] * 3 + [1j] * 3, [1] * 3 + [-1] * 3 + [1] * 3 + [-1] * 3,
+              [1] * 3 + [1j] * 3 + [-1] * 3 + [-1j] * 3]}  # pucch_orthogonal_sequence.h:162-172
+
+
+def f34_pilots(pdu, r):
+    """The DM-RS of allocated symbol r (dmrs_pucch_estimator_formats3_4.cpp:30-55): the low-PAPR sequence of group
+    n_id mod 30 with cyclic shift (m0 + n_cs) mod 12, m0 = 0, 6, 3, 9 for Format 4's OCC index."""
+    from .chest import ref_low_papr
+
+    M = 12 * (1 if pdu.format == 4 else pdu.nof_prb)
+    base = ref_low_papr(M, pdu.n_id_hopping % 30).astype(np.complex64)
+    m0 = [0, 6, 3, 9][pdu.occ_index] if pdu.format == 4 else 0
+    n = 8 * (14 * pdu.slot_index + pdu.start_symbol_index + r)
+    c = prbs(pdu.n_id_hopping, n + 8)[n:]
+    a = (m0 + int(sum(int(x) << m for m, x in enumerate(c[:8])))) % 12
+    return (base * np.exp(2j * np.pi * ((a * np.arange(M)) % 12) / 12)).astype(np.complex64)
+
+
+def transmit_f34(grid, pdu, payload, gains, noise, rng):
+    """Writes a Format 3 / 4 transmission of payload (UCI encoding, scrambling with c_init = rnti 2^15 + n_id, QPSK or
+    pi/2-BPSK, Format 4's block-wise spreading, transform precoding, the DM-RS symbols) through per-port gains plus
+    complex Gaussian noise of variance noise onto its REs of grid (uint32 cbf16, in place)."""
+    from srsran_project_amd.pucch import f34_dmrs_mask, f34_nof_llrs
+
+    from .pdsch_mod import to_bf16
+    from .pusch_proc import uci_encode
+
+    hop = pdu.second_hop_prb >= 0
+    mask = f34_dmrs_mask(pdu.nof_symbols, hop, pdu.additional_dmrs)
+    E = f34_nof_llrs(pdu)
+    bits = (uci_encode(np.asarray(payload, np.uint8), E, 0 if pdu.pi2_bpsk else 2) ^
+            prbs(pdu.rnti * (1 << 15) + pdu.n_id_scrambling, E)).astype(np.float32)
+    if pdu.pi2_bpsk:
+        i = np.arange(E)
+        sym = (np.exp(1j * np.pi * (i % 2) / 2) * ((1 - 2 * bits) + 1j * (1 - 2 * bits)) / np.sqrt(2))
+    else:
+        sym = ((1 - 2 * bits[0::2]) + 1j * (1 - 2 * bits[1::2])) / np.sqrt(2)
+    M = 12 * (1 if pdu.format == 4 else pdu.nof_prb)
+    ports = [pdu.ports[k] for k in range(pdu.nof_ports)]
+    q = 0
+    for r in range(pdu.nof_symbols):
+        prb = pdu.bwp_start_rb + (pdu.second_hop_prb if (hop and r >= pdu.nof_symbols // 2) else pdu.starting_prb)
+        if r in mask:
+            x = f34_pilots(pdu, r)
+        else:
+            if pdu.format == 4:
+                mod = 12 // pdu.occ_length
+                w = np.asarray(F4_OCC[pdu.occ_length][pdu.occ_index])
+                y = np.array([sym[q * mod + k % mod] for k in range(12)]) * w
+            else:
+                y = sym[q * M:(q + 1) * M]
+            x = (np.fft.fft(y) / np.sqrt(M)).astype(np.complex64)
+            q += 1
+        for k, p in enumerate(ports):
+            v = x * np.complex64(gains[k]) + np.sqrt(noise / 2) * (rng.normal(size=M) + 1j * rng.normal(size=M))
+            v = v.astype(np.complex64)
+            grid[p, pdu.start_symbol_index + r, 12 * prb:12 * prb + M] = (to_bf16(v.real).astype(np.uint32) |
+                                                                           (to_bf16(v.imag).astype(np.uint32) << 16))
+    return grid
+
+
+def ref_process_f34(grid, pdu):
+    """The compiled pucch_processor_impl::process(format3 / format4_configuration) -> (PucchUciResult, payload)."""
+    import ctypes
+
+    from srsran_project_amd.pucch import PucchUciResult, payload_bits
+
+    ref = _ref()
+    ref.srs_ref_pucch_f34_process.restype = None
+    ref.srs_ref_pucch_f34_process.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]
+    g = np.ascontiguousarray(grid, np.uint32)
+    r = PucchUciResult()
+    pay = np.zeros(max(payload_bits(pdu), 1), np.uint8)
+    ref.srs_ref_pucch_f34_process(g.ctypes.data, g.shape[0], g.shape[2], ctypes.addressof(pdu), ctypes.byref(r),
+                                  pay.ctypes.data)
+    return r, pay[:payload_bits(pdu)]
+
+
+def ref_demodulate_f34(grid, pdu):
+    """The compiled dmrs_pucch_estimator_formats3_4 + pucch_demodulator_format3 / 4 -> int8 LLRs."""
+    import ctypes
+
+    from srsran_project_amd.pucch import f34_nof_llrs
+
+    ref = _ref()
+    ref.srs_ref_pucch_f34_demodulate.restype = None
+    ref.srs_ref_pucch_f34_demodulate.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_uint]
+    g = np.ascontiguousarray(grid, np.uint32)
+    llr = np.zeros(f34_nof_llrs(pdu), np.int8)
+    ref.srs_ref_pucch_f34_demodulate(g.ctypes.data, g.shape[0], g.shape[2], ctypes.addressof(pdu), llr.ctypes.data,
+                                     llr.size)
+    return llr

@@ -288,6 +288,171 @@ void srs_ref_pucch_f2_demodulate(const uint32_t* grid, unsigned nof_grid_ports, 
                  dc);
 }
 
+static void fill_f34(const srs_amd_pucch_f34_pdu* p, pucch_processor::format3_configuration& c)
+{
+  c.slot         = slot_point(p->numerology, p->slot_index);
+  c.cp           = cyclic_prefix::NORMAL;
+  for (unsigned i = 0; i != p->nof_ports; ++i) {
+    c.ports.push_back(p->ports[i]);
+  }
+  c.bwp_size_rb  = p->bwp_size_rb;
+  c.bwp_start_rb = p->bwp_start_rb;
+  c.starting_prb = p->starting_prb;
+  if (p->second_hop_prb >= 0) {
+    c.second_hop_prb = static_cast<unsigned>(p->second_hop_prb);
+  }
+  c.nof_prb            = p->nof_prb;
+  c.start_symbol_index = p->start_symbol_index;
+  c.nof_symbols        = p->nof_symbols;
+  c.rnti               = static_cast<uint16_t>(p->rnti);
+  c.n_id_hopping       = p->n_id_hopping;
+  c.n_id_scrambling    = p->n_id_scrambling;
+  c.nof_harq_ack       = p->nof_harq_ack;
+  c.nof_sr             = p->nof_sr;
+  c.nof_csi_part1      = p->nof_csi_part1;
+  c.nof_csi_part2      = p->nof_csi_part2;
+  c.additional_dmrs    = p->additional_dmrs != 0;
+  c.pi2_bpsk           = p->pi2_bpsk != 0;
+}
+
+static pucch_processor::format4_configuration to_f4(const srs_amd_pucch_f34_pdu* p)
+{
+  pucch_processor::format3_configuration c3;
+  fill_f34(p, c3);
+  pucch_processor::format4_configuration c;
+  c.slot               = c3.slot;
+  c.cp                 = c3.cp;
+  c.ports              = c3.ports;
+  c.bwp_size_rb        = c3.bwp_size_rb;
+  c.bwp_start_rb       = c3.bwp_start_rb;
+  c.starting_prb       = c3.starting_prb;
+  c.second_hop_prb     = c3.second_hop_prb;
+  c.start_symbol_index = c3.start_symbol_index;
+  c.nof_symbols        = c3.nof_symbols;
+  c.rnti               = c3.rnti;
+  c.n_id_hopping       = c3.n_id_hopping;
+  c.n_id_scrambling    = c3.n_id_scrambling;
+  c.nof_harq_ack       = c3.nof_harq_ack;
+  c.nof_sr             = c3.nof_sr;
+  c.nof_csi_part1      = c3.nof_csi_part1;
+  c.nof_csi_part2      = c3.nof_csi_part2;
+  c.additional_dmrs    = c3.additional_dmrs;
+  c.pi2_bpsk           = c3.pi2_bpsk;
+  c.occ_index          = p->occ_index;
+  c.occ_length         = p->occ_length;
+  return c;
+}
+
+// pucch_processor_impl::process of one Format 3 / 4 PDU on grid [nof_grid_ports][14][nsubc].
+void srs_ref_pucch_f34_process(const uint32_t* grid, unsigned nof_grid_ports, unsigned nsubc,
+                               const srs_amd_pucch_f34_pdu* p, srs_amd_pucch_uci_result* out, uint8_t* payload)
+{
+  grid_tensor data({nsubc, MAX_NSYMB_PER_SLOT, nof_grid_ports});
+  fill_grid(data, grid, nof_grid_ports, nsubc);
+  std::atomic<unsigned>     empty{0};
+  resource_grid_reader_impl reader(data, empty);
+  auto                      proc = make_processor(nsubc / NRE, nof_grid_ports);
+  if (p->format == 4) {
+    fill_uci_result(proc->process(reader, to_f4(p)), out, payload);
+  } else {
+    pucch_processor::format3_configuration c;
+    fill_f34(p, c);
+    fill_uci_result(proc->process(reader, c), out, payload);
+  }
+}
+
+// dmrs_pucch_estimator::estimate + pucch_demodulator::demodulate of one Format 3 / 4 PDU (as
+// pucch_processor_impl.cpp:240-289 / 328-378 call them): the descrambled LLRs.
+void srs_ref_pucch_f34_demodulate(const uint32_t* grid, unsigned nof_grid_ports, unsigned nsubc,
+                                  const srs_amd_pucch_f34_pdu* p, int8_t* llrs, unsigned nof_llrs)
+{
+  grid_tensor data({nsubc, MAX_NSYMB_PER_SLOT, nof_grid_ports});
+  fill_grid(data, grid, nof_grid_ports, nsubc);
+  std::atomic<unsigned>     empty{0};
+  resource_grid_reader_impl reader(data, empty);
+  using namespace srs_ref;
+  dmrs_pucch_estimator_formats3_4 est(std::make_unique<pseudo_random_generator_impl>(),
+                                      std::make_unique<low_papr_sequence_generator_impl>(),
+                                      make_port_estimator(2, 1, false));
+  auto eq = [] { return std::make_unique<channel_equalizer_generic_impl>(channel_equalizer_algorithm_type::zf); };
+  channel_estimate::channel_estimate_dimensions dims;
+  dims.nof_prb       = nsubc / NRE;
+  dims.nof_symbols   = MAX_NSYMB_PER_SLOT;
+  dims.nof_rx_ports  = p->nof_ports;
+  dims.nof_tx_layers = 1;
+  channel_estimate ce(dims);
+  const unsigned   prb0 = p->bwp_start_rb + p->starting_prb;
+  std::optional<unsigned> hop;
+  if (p->second_hop_prb >= 0) {
+    hop = p->bwp_start_rb + static_cast<unsigned>(p->second_hop_prb);
+  }
+  static_vector<uint8_t, MAX_PORTS> ports;
+  for (unsigned i = 0; i != p->nof_ports; ++i) {
+    ports.push_back(p->ports[i]);
+  }
+  span<log_likelihood_ratio> out(reinterpret_cast<log_likelihood_ratio*>(llrs), nof_llrs);
+  if (p->format == 4) {
+    dmrs_pucch_estimator::format4_configuration ec;
+    ec.slot               = slot_point(p->numerology, p->slot_index);
+    ec.cp                 = cyclic_prefix::NORMAL;
+    ec.group_hopping      = pucch_group_hopping::NEITHER;
+    ec.start_symbol_index = p->start_symbol_index;
+    ec.nof_symbols        = p->nof_symbols;
+    ec.starting_prb       = prb0;
+    ec.second_hop_prb     = hop;
+    ec.n_id               = p->n_id_hopping;
+    ec.ports.assign(ports.begin(), ports.end());
+    ec.additional_dmrs = p->additional_dmrs != 0;
+    ec.occ_index       = p->occ_index;
+    est.estimate(ce, reader, ec);
+    pucch_demodulator_format4 dem(
+        eq(), std::make_unique<demodulation_mapper_impl>(), std::make_unique<pseudo_random_generator_impl>(),
+        make_transform_precoder(16));
+    pucch_demodulator::format4_configuration dc;
+    dc.rx_ports           = ports;
+    dc.first_prb          = prb0;
+    dc.second_hop_prb     = hop;
+    dc.start_symbol_index = p->start_symbol_index;
+    dc.nof_symbols        = p->nof_symbols;
+    dc.rnti               = static_cast<uint16_t>(p->rnti);
+    dc.n_id               = p->n_id_scrambling;
+    dc.additional_dmrs    = p->additional_dmrs != 0;
+    dc.pi2_bpsk           = p->pi2_bpsk != 0;
+    dc.occ_index          = p->occ_index;
+    dc.occ_length         = p->occ_length;
+    dem.demodulate(out, reader, ce, dc);
+    return;
+  }
+  dmrs_pucch_estimator::format3_configuration ec;
+  ec.slot               = slot_point(p->numerology, p->slot_index);
+  ec.cp                 = cyclic_prefix::NORMAL;
+  ec.group_hopping      = pucch_group_hopping::NEITHER;
+  ec.start_symbol_index = p->start_symbol_index;
+  ec.nof_symbols        = p->nof_symbols;
+  ec.starting_prb       = prb0;
+  ec.second_hop_prb     = hop;
+  ec.nof_prb            = p->nof_prb;
+  ec.n_id               = p->n_id_hopping;
+  ec.ports.assign(ports.begin(), ports.end());
+  ec.additional_dmrs = p->additional_dmrs != 0;
+  est.estimate(ce, reader, ec);
+  pucch_demodulator_format3 dem(
+      eq(), std::make_unique<demodulation_mapper_impl>(), std::make_unique<pseudo_random_generator_impl>(),
+      make_transform_precoder(16));
+  pucch_demodulator::format3_configuration dc;
+  dc.rx_ports           = ports;
+  dc.first_prb          = prb0;
+  dc.second_hop_prb     = hop;
+  dc.nof_prb            = p->nof_prb;
+  dc.start_symbol_index = p->start_symbol_index;
+  dc.nof_symbols        = p->nof_symbols;
+  dc.rnti               = static_cast<uint16_t>(p->rnti);
+  dc.n_id               = p->n_id_scrambling;
+  dc.additional_dmrs    = p->additional_dmrs != 0;
+  dc.pi2_bpsk           = p->pi2_bpsk != 0;
+  dem.demodulate(out, reader, ce, dc);
+}
+
 // pucch_processor_impl::process of one Format 2 PDU on grid [nof_grid_ports][14][nsubc].
 void srs_ref_pucch_f2_process(const uint32_t* grid, unsigned nof_grid_ports, unsigned nsubc,
                               const srs_amd_pucch_f2_pdu* p, srs_amd_pucch_uci_result* out, uint8_t* payload)

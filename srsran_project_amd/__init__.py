@@ -124,4 +124,4 @@ from .pdcch import CceToRegMapping, PdcchPdu, PdcchProcessor  # noqa: F401,E402
 from . import ssb  # noqa: F401,E402
 from .ssb import SsbPatternCase, SsbPdu, SsbProcessor  # noqa: F401,E402
 from . import pucch  # noqa: F401,E402
-from .pucch import PucchF0Pdu, PucchF1Batch, PucchF2Pdu, PucchProcessor  # noqa: F401,E402
+from .pucch import PucchF0Pdu, PucchF1Batch, PucchF2Pdu, PucchF34Pdu, PucchProcessor  # noqa: F401,E402

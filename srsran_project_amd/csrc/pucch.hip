@@ -669,6 +669,373 @@ __global__ __launch_bounds__(256) void pucch_f2_kernel(const pucch_f2_desc* desc
   }
 }
 
+// ---- Formats 3 / 4 ----------------------------------------------------------------------------------------------
+// After pucch_processor_impl.cpp:222-397: dmrs_pucch_estimator_formats3_4.cpp (all 12 REs of a PRB carry DM-RS on the
+// DM-RS symbols of get_pucch_formats3_4_dmrs_symbol_mask; the port estimator with the FD filter, TD averaging, the
+// CFO measured between the first two DM-RS symbols of a hop and not compensated), pucch_formats3_4_helpers.h
+// pucch_3_4_extract_and_equalize (ZF per data symbol, transform deprecoding, mean noise), Format 4's
+// inverse_blockwise_spreading (pucch_demodulator_format4.cpp:113-130), the soft demapper and the descrambler.
+__global__ __launch_bounds__(256) void pucch_f34_kernel(const pucch_f34_desc* desc)
+{
+#pragma clang fp contract(off)
+  using chdev::cmul;
+  const pucch_f34_desc& d    = desc[blockIdx.x];
+  const uint32_t        t    = threadIdx.x;
+  const uint32_t        w    = t / 64, lane = t % 64;
+  const uint32_t        P    = d.nof_ports;
+  const uint32_t        M    = d.M;
+  const bool            live = w < P;
+  const uint32_t        port = live ? d.ports[w] : d.ports[0];
+  __shared__ float2     s_enl[4][CH_MAXV + PUCCH_F3_MAX_M + CH_MAXV];
+  __shared__ float2     s_est[4][2][PUCCH_F3_MAX_M];
+  __shared__ float      s_corr[4][PUCCH_MAX_TA_N];
+  __shared__ float2     s_tw[PUCCH_MAX_TA_N];
+  __shared__ float2     s_twm[PUCCH_F3_MAX_M];
+  __shared__ float      s_st[4][8];
+  __shared__ float2     s_x[PUCCH_F3_MAX_DATA * PUCCH_F3_MAX_M];
+  __shared__ float      s_nv[PUCCH_F3_MAX_DATA * PUCCH_F3_MAX_M];
+  __shared__ float2     s_y[PUCCH_F3_MAX_DATA * PUCCH_F3_MAX_M];
+  __shared__ float      s_mean[PUCCH_F3_MAX_DATA];
+  for (uint32_t i = t; i < d.ta_n; i += 256) {
+    s_tw[i] = chdev::polar1(F1_TWOPI * static_cast<float>(i) / static_cast<float>(d.ta_n));
+  }
+  for (uint32_t i = t; i < M; i += 256) {
+    s_twm[i] = chdev::polar1(F1_TWOPI * static_cast<float>(i) / static_cast<float>(M));
+  }
+  const uint32_t* g = d.grid + static_cast<uint64_t>(port) * d.port_stride;
+  float           epre = 0.0f, rsrp = 0.0f, noise = 0.0f, ta = 0.0f, cfo = 0.0f;
+  bool            has_cfo = false;
+  const uint32_t  nhops   = d.hop_sym < d.nsym ? 2u : 1u;
+  uint32_t        dmrs_before = 0, nd_total = 0;
+  for (uint32_t h = 0; h != nhops; ++h) {
+    const uint32_t r0 = h == 0 ? 0u : d.hop_sym, r1 = (nhops == 2 && h == 0) ? d.hop_sym : d.nsym;
+    uint32_t       rs[4], nd = 0;
+    for (uint32_t r = r0; r != r1; ++r) {
+      if (((d.dmrs_mask >> r) & 1u) && nd < 4) {
+        rs[nd++] = r;
+      }
+    }
+    const uint32_t subc = d.subc0[h];
+    float2         lse[3];
+    float          e_acc = 0.0f;
+    float2         z     = make_float2(0.0f, 0.0f);
+#pragma unroll
+    for (uint32_t m = 0; m < 3; ++m) {
+      lse[m]           = make_float2(0.0f, 0.0f);
+      const uint32_t k = lane + 64 * m;
+      if (k < M) {
+        float2 p0 = make_float2(0.0f, 0.0f);
+        for (uint32_t q = 0; q != nd; ++q) {
+          const float2 rx = chdev::from_cbf16(g[static_cast<uint64_t>(d.l0 + rs[q]) * d.nof_subc + subc + k]);
+          e_acc += norm2(rx);
+          const float2 prod = cmul_conj(rx, d.pil[(dmrs_before + q) * M + k]);
+          if (q == 0) {
+            p0 = prod;
+          } else if (q == 1) {
+            const float2 c = cmul_conj(prod, p0);
+            z.x += c.x;
+            z.y += c.y;
+          }
+          lse[m].x += prod.x;
+          lse[m].y += prod.y;
+        }
+      }
+    }
+    epre += wave_sum(e_acc);
+    if (nd >= 2) {
+      const float2 zs    = wave_sum2(z);
+      const float  cfo_h = atan2f(zs.y, zs.x) / F1_TWOPI / (d.epoch[rs[1]] - d.epoch[rs[0]]);
+      cfo                = has_cfo ? (cfo + cfo_h) / 2.0f : cfo_h;
+      has_cfo            = true;
+    }
+    const float total = (1.0f / 1.0f) / static_cast<float>(nd);
+    float2*     enl   = s_enl[w];
+    for (uint32_t i = lane; i < CH_MAXV + PUCCH_F3_MAX_M + CH_MAXV; i += 64) {
+      enl[i] = make_float2(0.0f, 0.0f);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t m = 0; m < 3; ++m) {
+      const uint32_t k = lane + 64 * m;
+      if (k < M) {
+        enl[CH_MAXV + k] = make_float2(lse[m].x * total, lse[m].y * total);
+      }
+    }
+    __syncthreads();
+    const int nv = d.nof_v;
+    chdev::virtual_pilots_wave(enl + CH_MAXV - nv, enl + CH_MAXV, nv, true);
+    chdev::virtual_pilots_wave(enl + CH_MAXV + M, enl + CH_MAXV + M - nv, nv, false);
+    __syncthreads();
+    float2    f[3];
+    float     p_acc = 0.0f;
+    const int half  = d.nof_taps / 2;
+#pragma unroll
+    for (uint32_t m = 0; m < 3; ++m) {
+      f[m]        = make_float2(0.0f, 0.0f);
+      const int k = static_cast<int>(lane + 64 * m);
+      if (k < static_cast<int>(M)) {
+        for (int j = 0; j < d.nof_taps; ++j) {
+          const int i = k + j - half;
+          if (i >= -nv && i < static_cast<int>(M) + nv) {
+            const float2 in = enl[CH_MAXV + i];
+            const float  c  = d.rc[d.nof_taps - 1 - j];
+            f[m].x          = f[m].x + in.x * c;
+            f[m].y          = f[m].y + in.y * c;
+          }
+        }
+        p_acc += norm2(f[m]);
+      }
+    }
+    __syncthreads();
+    rsrp += wave_sum(p_acc) * (1.0f * 1.0f * static_cast<float>(nd) / 1.0f);
+    float n_acc = 0.0f;
+#pragma unroll
+    for (uint32_t m = 0; m < 3; ++m) {
+      const uint32_t k = lane + 64 * m;
+      if (k < M) {
+        enl[k]         = f[m];
+        s_est[w][h][k] = chdev::from_cbf16(chdev::to_cbf16(f[m]));
+        for (uint32_t q = 0; q != nd; ++q) {
+          const float2 rx   = chdev::from_cbf16(g[static_cast<uint64_t>(d.l0 + rs[q]) * d.nof_subc + subc + k]);
+          const float2 pred = cmul(f[m], d.pil[(dmrs_before + q) * M + k]);
+          n_acc += norm2(make_float2(rx.x - pred.x, rx.y - pred.y));
+        }
+      }
+    }
+    const float energy = wave_sum(n_acc);
+    noise += (isfinite(energy) && energy >= 1.17549435e-38f) ? energy : 0.0f;
+    __syncthreads();
+    // time alignment: |IDFT|^2 of the smoothed pilots (stride 1)
+    for (uint32_t tt = lane; tt < d.ta_n; tt += 64) {
+      float2 c = make_float2(0.0f, 0.0f);
+      for (uint32_t k = 0; k != M; ++k) {
+        const float2 x = cmul(enl[k], s_tw[(k * tt) % d.ta_n]);
+        c.x += x.x;
+        c.y += x.y;
+      }
+      s_corr[w][tt] = norm2(c);
+    }
+    __syncthreads();
+    if (lane == 0) {
+      const float* corr = s_corr[w];
+      const int    N = static_cast<int>(d.ta_n), Mx = d.ta_max_taps;
+      int          i_d = 0, i_a = 0;
+      float        v_d = corr[0], v_a = corr[N - Mx];
+      for (int i = 1; i < Mx; ++i) {
+        if (corr[i] > v_d) {
+          v_d = corr[i];
+          i_d = i;
+        }
+        if (corr[N - Mx + i] > v_a) {
+          v_a = corr[N - Mx + i];
+          i_a = i;
+        }
+      }
+      const int idx  = v_d >= v_a ? i_d : -(Mx - i_a);
+      double    frac = 0.0;
+      if (d.ta_frac) {
+        float     pk[5];
+        const int taps = Mx > 2 ? 5 : 3;
+        for (int i = 0; i < taps; ++i) {
+          pk[i] = corr[static_cast<uint32_t>(idx + i + N - taps / 2) % static_cast<uint32_t>(N)];
+        }
+        float r;
+        if (taps == 5) {
+          const float num = -0.4f * pk[0] + -0.2f * pk[1] + 0.0f * pk[2] + 0.2f * pk[3] + 0.4f * pk[4];
+          const float den = 0.571429f * pk[0] + -0.285714f * pk[1] + -0.571429f * pk[2] + -0.285714f * pk[3] +
+                            0.571429f * pk[4];
+          r = -1.0f * num / den;
+        } else {
+          const float num = -0.5f * pk[0] + 0.0f * pk[1] + 0.5f * pk[2];
+          const float den = 0.5f * pk[0] + -1.0f * pk[1] + 0.5f * pk[2];
+          r = -0.5f * num / den;
+        }
+        frac = (isnan(r) || isinf(r) || fabsf(r) > 1.0f) ? 0.0 : static_cast<double>(r);
+      }
+      ta += static_cast<float>((static_cast<double>(idx) + frac) / d.ta_fs);
+    }
+    __syncthreads();
+    dmrs_before += nd;
+    nd_total += nd;
+  }
+  if (nhops == 2) {
+    ta /= 2.0f;
+  }
+  const float npil_all = static_cast<float>(M * nd_total);
+  rsrp /= npil_all * 1.0f;
+  epre /= npil_all;
+  noise /= static_cast<float>(M * nd_total * 1 - 1);
+  noise = fmaxf(rsrp / 1e10f, noise);
+  const float snr = (isfinite(noise) && noise >= 1.17549435e-38f) ? rsrp * 1.0f / 1.0f / 1.0f / noise : 0.0f;
+  if (lane == 0) {
+    s_st[w][0] = epre;
+    s_st[w][1] = rsrp;
+    s_st[w][2] = noise;
+    s_st[w][3] = snr;
+    s_st[w][4] = ta;
+    s_st[w][5] = cfo;
+    s_st[w][6] = has_cfo ? 1.0f : 0.0f;
+  }
+  __syncthreads();
+  // ZF equalization of every data RE
+  const uint32_t nds = d.nsym - __popc(d.dmrs_mask);
+  for (uint32_t i = t; i < nds * M; i += 256) {
+    const uint32_t q = i / M, n = i % M;
+    uint32_t       r = 0;
+    for (uint32_t c = 0, s = 0; s != d.nsym; ++s) {
+      if (!((d.dmrs_mask >> s) & 1u)) {
+        if (c == q) {
+          r = s;
+        }
+        ++c;
+      }
+    }
+    const uint32_t h = r >= d.hop_sym ? 1u : 0u;
+    eq::cplx       y[4], hh[4];
+    float          nvp[4];
+    uint32_t       valid = 0;
+#pragma unroll
+    for (uint32_t p = 0; p < 4; ++p) {
+      y[p] = hh[p] = {0.0f, 0.0f};
+      nvp[p]       = 0.0f;
+      if (p < P) {
+        y[p]           = eq::from_cbf16(d.grid[static_cast<uint64_t>(d.ports[p]) * d.port_stride +
+                                          static_cast<uint64_t>(d.l0 + r) * d.nof_subc + d.subc0[h] + n]);
+        const float2 e = s_est[p][h][n];
+        hh[p]          = {e.x, e.y};
+        nvp[p]         = s_st[p][2];
+        valid |= (nvp[p] > 0.0f && nvp[p] < __builtin_inff()) ? (1u << p) : 0u;
+      }
+    }
+    eq::cplx x;
+    float    nvx;
+    eq::equalize_1xn<4>(y, hh, nvp, valid, 1.0f, x, nvx);
+    s_x[i]  = make_float2(x.x, x.y);
+    s_nv[i] = nvx;
+  }
+  __syncthreads();
+  // transform deprecoding: IDFT of M points / sqrt(M) per data symbol; the mean of the valid noise variances
+  const float scaling = 1.0f / sqrtf(static_cast<float>(M));
+  for (uint32_t i = t; i < nds * M; i += 256) {
+    const uint32_t q = i / M, m = i % M;
+    float2         c = make_float2(0.0f, 0.0f);
+    for (uint32_t n = 0; n != M; ++n) {
+      const float2 x = cmul(s_x[q * M + n], s_twm[(n * m) % M]);
+      c.x += x.x;
+      c.y += x.y;
+    }
+    s_y[i] = make_float2(c.x * scaling, c.y * scaling);
+  }
+  if (t < nds) {
+    float    acc = 0.0f;
+    uint32_t cnt = 0;
+    for (uint32_t n = 0; n != M; ++n) {
+      const float v = s_nv[t * M + n];
+      if (v > 0.0f && !isnan(v) && !isinf(v)) {
+        acc += v;
+        ++cnt;
+      }
+    }
+    s_mean[t] = cnt != 0 ? acc / static_cast<float>(cnt) : acc;
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < nds * M; i += 256) {
+    const float v = s_nv[i];
+    s_nv[i]       = (v > 0.0f && !isnan(v) && !isinf(v)) ? s_mean[i / M] : v;
+  }
+  __syncthreads();
+  // Format 4: inverse block-wise spreading into s_x (symbols) and s_nv (noise)
+  if (d.occ_len > 1) {
+    const uint32_t mod = 12 / d.occ_len;
+    for (uint32_t o = t; o < d.n_sym; o += 256) {
+      const uint32_t l = o / mod, k0 = o % mod;
+      float2         acc = make_float2(0.0f, 0.0f);
+      float          nva = 0.0f;
+      for (uint32_t k = k0; k < 12; k += mod) {
+        const float2 x = cmul_conj(s_y[l * 12 + k], d.occ_w[k]);
+        acc.x += x.x;
+        acc.y += x.y;
+        nva += s_nv[l * 12 + k];
+      }
+      const float sc = 1.0f / static_cast<float>(d.occ_len);
+      s_x[o]         = make_float2(acc.x * sc, acc.y * sc);
+      s_y[PUCCH_F3_MAX_DATA * PUCCH_F3_MAX_M - 1 - o] = make_float2(nva, 0.0f);
+    }
+    __syncthreads();
+    for (uint32_t o = t; o < d.n_sym; o += 256) {
+      s_nv[o] = s_y[PUCCH_F3_MAX_DATA * PUCCH_F3_MAX_M - 1 - o].x;
+      s_y[o]  = s_x[o];
+    }
+    __syncthreads();
+  }
+  // soft demapping and descrambling
+  const float GAIN = 2.0f * 1.41421356237309504880f;
+  for (uint32_t i = t; i < d.n_sym; i += 256) {
+    const float2 x  = s_y[i];
+    const float  nv = s_nv[i];
+    if (d.qm == 2) {
+      const bool  simd  = i < (d.n_sym / 16) * 16;
+      const float xs[2] = {x.x, x.y};
+#pragma unroll
+      for (uint32_t c = 0; c < 2; ++c) {
+        int v = simd ? demap::q_simd((GAIN * xs[c]) * demap::safe_rcp(nv), 24.0f)
+                     : (nv > 0.0f ? demap::q_scalar(GAIN * xs[c] / nv, 24.0f) : 0);
+        const uint32_t b = 2 * i + c;
+        if ((d.scr[b >> 5] >> (b & 31)) & 1u) {
+          v = -v;
+        }
+        d.llr[b] = static_cast<int8_t>(v);
+      }
+    } else {
+      float re = x.x, im = x.y;
+      if (i & 1u) {
+        const float tmp = re;
+        re              = im;
+        im              = -tmp;
+      }
+      int v = nv > 0.0f ? demap::q_scalar(2.0f * 1.41421356237309504880f * (re + im) / nv, 24.0f) : 0;
+      if ((d.scr[i >> 5] >> (i & 31)) & 1u) {
+        v = -v;
+      }
+      d.llr[i] = static_cast<int8_t>(v);
+    }
+  }
+  if (t == 0) {
+    float    epre_lin = 0.0f, best_snr = 0.0f, rsrp_tot = 0.0f, nv_tot = 0.0f, rsrp_all = 0.0f;
+    uint32_t best = 0, nvalid = 0;
+    for (uint32_t p = 0; p != P; ++p) {
+      epre_lin += s_st[p][0];
+      if (s_st[p][3] > best_snr) {
+        best_snr = s_st[p][3];
+        best     = p;
+      }
+      const float r = s_st[p][1];
+      if (isfinite(r) && fabsf(r) >= 1.17549435e-38f) {
+        rsrp_tot += r;
+        ++nvalid;
+      }
+      nv_tot += s_st[p][2];
+      rsrp_all += s_st[p][1];
+    }
+    epre_lin /= static_cast<float>(P);
+    const float   rsrp_lin = nvalid != 0 ? rsrp_tot / static_cast<float>(nvalid) : 0.0f;
+    const float   sinr     = (isfinite(nv_tot) && nv_tot >= 1.17549435e-38f) ? rsrp_all / nv_tot : 0.0f;
+    const double  tc       = static_cast<double>(s_st[best][4]) / F2_T_C;
+    const int64_t tc10     = static_cast<int64_t>(tc * 10.0);
+    const int64_t unit     = tc10 / 10 + (tc10 % 10) / 5;
+    srs_amd_pucch_uci_result* r = d.result;
+    r->nof_harq_ack     = d.counts[0];
+    r->nof_sr           = d.counts[1];
+    r->nof_csi_part1    = d.counts[2];
+    r->nof_csi_part2    = d.counts[3];
+    r->sinr_dB          = to_dB(sinr);
+    r->rsrp_dB          = to_dB(rsrp_lin);
+    r->epre_dB          = to_dB(epre_lin);
+    r->time_alignment_s = static_cast<float>(static_cast<double>(unit) * F2_T_C);
+    r->cfo_Hz           = s_st[best][6] != 0.0f ? s_st[best][5] * d.scs_hz : __builtin_nanf("");
+  }
+}
+
 __global__ __launch_bounds__(256) void pucch_uci_finish_kernel(const int32_t* status, const uint8_t* messages,
                                                                uint32_t msg_stride, const uint32_t* perm,
                                                                const uint32_t* nbits, srs_amd_pucch_uci_result* results,
@@ -691,6 +1058,15 @@ hipError_t launch_pucch_f2(const pucch_f2_desc* d_desc, uint32_t nof, hipStream_
     return hipSuccess;
   }
   hipLaunchKernelGGL(pucch_f2_kernel, dim3(nof), dim3(256), 0, stream, d_desc);
+  return hipGetLastError();
+}
+
+hipError_t launch_pucch_f34(const pucch_f34_desc* d_desc, uint32_t nof, hipStream_t stream)
+{
+  if (nof == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(pucch_f34_kernel, dim3(nof), dim3(256), 0, stream, d_desc);
   return hipGetLastError();
 }
 

@@ -297,6 +297,318 @@ int make_f2_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f2_pdu
   return SRS_AMD_OK;
 }
 
+// get_pucch_formats3_4_dmrs_symbol_mask (pucch_formats3_4_helpers.h): DM-RS symbols of a Format 3 / 4 allocation.
+uint32_t f34_dmrs_mask(uint32_t nsym, bool hop, bool add)
+{
+  switch (nsym) {
+    case 4:
+      return hop ? 0b101u : 0b10u;
+    case 5:
+      return 0b1001u;
+    case 6:
+    case 7:
+      return 0b10010u;
+    case 8:
+      return 0b100010u;
+    case 9:
+      return 0b1000010u;
+    case 10:
+      return add ? ((1u << 1) | (1u << 3) | (1u << 6) | (1u << 8)) : ((1u << 2) | (1u << 7));
+    case 11:
+      return add ? ((1u << 1) | (1u << 3) | (1u << 6) | (1u << 9)) : ((1u << 2) | (1u << 7));
+    case 12:
+      return add ? ((1u << 1) | (1u << 4) | (1u << 7) | (1u << 10)) : ((1u << 2) | (1u << 8));
+    case 13:
+      return add ? ((1u << 1) | (1u << 4) | (1u << 7) | (1u << 11)) : ((1u << 2) | (1u << 9));
+    case 14:
+      return add ? ((1u << 1) | (1u << 5) | (1u << 8) | (1u << 12)) : ((1u << 3) | (1u << 10));
+    default:
+      return 0;
+  }
+}
+
+bool tp_prb_valid(uint32_t n) // transform_precoding::is_nof_prbs_valid: 2^a 3^b 5^c
+{
+  if (n == 0) {
+    return false;
+  }
+  for (uint32_t f : {2u, 3u, 5u}) {
+    while (n % f == 0) {
+      n /= f;
+    }
+  }
+  return n == 1;
+}
+
+// Formats 3 / 4: the descriptor plus the PDU's DM-RS (pil: nof DM-RS x M values) and scrambling words (scr).
+int make_f34_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f34_pdu& p, const uint32_t* d_grids,
+                  uint64_t grid_stride, uint32_t nof_grids, uint32_t nof_grid_ports, uint32_t nof_subc,
+                  pucch_f34_desc& d, std::vector<float2>& pil, std::vector<uint32_t>& scr, uint32_t& E, uint32_t& K)
+{
+  const bool     f4       = p.format == 4;
+  const uint32_t grid_prb = nof_subc / 12;
+  if (p.format != 3 && p.format != 4) {
+    return fail(SRS_AMD_EINVAL, "PUCCH format %u is not 3 or 4.", p.format);
+  }
+  const uint32_t nprb = f4 ? 1u : p.nof_prb;
+  if (p.bwp_start_rb + p.bwp_size_rb > grid_prb) {
+    return fail(SRS_AMD_EINVAL, "BWP allocation goes up to PRB %u, exceeding the configured maximum grid RB size, i.e., %u.",
+                p.bwp_start_rb + p.bwp_size_rb, grid_prb);
+  }
+  if (nprb == 0 || nprb > 16 || !tp_prb_valid(nprb) || p.starting_prb + nprb > p.bwp_size_rb) {
+    return fail(SRS_AMD_EINVAL, "Invalid PUCCH Format %u PRB allocation (%u PRBs from PRB %u of a %u-PRB BWP).",
+                p.format, nprb, p.starting_prb, p.bwp_size_rb);
+  }
+  if (p.nof_symbols < 4 || p.nof_symbols > 14 || p.start_symbol_index + p.nof_symbols > NSYMB) {
+    return fail(SRS_AMD_EINVAL, "Invalid Format %u symbols (start %u, %u symbols).", p.format, p.start_symbol_index,
+                p.nof_symbols);
+  }
+  const bool hop = p.second_hop_prb >= 0;
+  if (hop && p.bwp_start_rb + static_cast<uint32_t>(p.second_hop_prb) + nprb > grid_prb) {
+    return fail(SRS_AMD_EINVAL, "Second hop PRB allocation outside the grid.");
+  }
+  if (p.nof_ports == 0 || p.nof_ports > 4) {
+    return fail(SRS_AMD_EINVAL, "The number of receive ports, i.e. %u, is not 1 to 4.", p.nof_ports);
+  }
+  if (p.nof_csi_part2 != 0) {
+    return fail(SRS_AMD_EINVAL, "CSI Part 2 is not currently supported.");
+  }
+  if (f4 && ((p.occ_length != 2 && p.occ_length != 4) || p.occ_index >= p.occ_length)) {
+    return fail(SRS_AMD_EINVAL, "Invalid OCC length value (i.e., %u) or index (i.e., %u).", p.occ_length,
+                p.occ_index);
+  }
+  if (p.numerology > 4 || p.slot_index >= (10u << p.numerology) || p.n_id_hopping > 1023 ||
+      p.n_id_scrambling > 1023 || p.rnti > 65535) {
+    return fail(SRS_AMD_EINVAL, "Invalid Format %u PDU (slot %u, numerology %u, RNTI %u, n_id %u / %u).", p.format,
+                p.slot_index, p.numerology, p.rnti, p.n_id_hopping, p.n_id_scrambling);
+  }
+  const uint32_t mask = f34_dmrs_mask(p.nof_symbols, hop, p.additional_dmrs != 0);
+  const uint32_t nd   = static_cast<uint32_t>(__builtin_popcount(mask));
+  const uint32_t nds  = p.nof_symbols - nd;
+  const uint32_t qb   = p.pi2_bpsk ? 1u : 2u;
+  const uint32_t M    = 12 * nprb;
+  const uint32_t occ  = f4 ? p.occ_length : 1u;
+  K                   = p.nof_harq_ack + p.nof_sr + p.nof_csi_part1 + p.nof_csi_part2;
+  E                   = nds * M * qb / occ;
+  // pucch_format3_code_rate / pucch_format4_code_rate (pucch_info.h:80-120)
+  const uint32_t e_tot = f4 ? 12 * nds * qb / occ : M * nds * qb;
+  const uint32_t chan  = f4 ? 12 * nds * qb : M * nds * qb;
+  if (K < 3 || K > 1706) {
+    return fail(SRS_AMD_EINVAL, "UCI Payload length (i.e., %u) is outside the supported range (i.e., [3, 1706]).", K);
+  }
+  if (static_cast<float>(K + uci_crc_bits(K, e_tot)) / static_cast<float>(chan) > 0.80F) {
+    return fail(SRS_AMD_EINVAL, "The effective code rate exceeds the maximum allowed 0.8.");
+  }
+  if (p.d_grid == nullptr && (d_grids == nullptr || p.grid >= nof_grids)) {
+    return fail(SRS_AMD_EINVAL, "grid index %u out of range (or no grid).", p.grid);
+  }
+  d             = pucch_f34_desc{};
+  d.grid        = p.d_grid != nullptr ? p.d_grid : d_grids + p.grid * grid_stride;
+  d.port_stride = NSYMB * nof_subc;
+  d.nof_subc    = nof_subc;
+  d.l0          = p.start_symbol_index;
+  d.nsym        = p.nof_symbols;
+  d.M           = M;
+  d.dmrs_mask   = mask;
+  d.hop_sym     = hop ? p.nof_symbols / 2 : p.nof_symbols;
+  d.subc0[0]    = 12 * (p.bwp_start_rb + p.starting_prb);
+  d.subc0[1]    = hop ? 12 * (p.bwp_start_rb + static_cast<uint32_t>(p.second_hop_prb)) : d.subc0[0];
+  d.nof_ports   = p.nof_ports;
+  for (uint32_t i = 0; i != p.nof_ports; ++i) {
+    if (p.ports[i] >= nof_grid_ports) {
+      return fail(SRS_AMD_EINVAL, "port %u outside the grid's %u ports.", p.ports[i], nof_grid_ports);
+    }
+    d.ports[i] = p.ports[i];
+  }
+  float epoch[NSYMB];
+  symbol_epochs(p.numerology, epoch);
+  for (uint32_t r = 0; r != p.nof_symbols; ++r) {
+    d.epoch[r] = epoch[p.start_symbol_index + r];
+  }
+  d.scs_hz = static_cast<float>((15u << p.numerology) * 1000);
+  fd_filter(nprb, 1, M, d.rc, d.nof_taps, d.nof_v);
+  ta_setup(M, 1, p.numerology, d.ta_n, d.ta_max_taps, d.ta_frac, d.ta_fs);
+  // DM-RS: the low-PAPR sequence of group n_id mod 30 (v = 0), cyclic shift (m0 + n_cs) mod 12 per DM-RS symbol with
+  // m0 = 0, 6, 3, 9 for OCC index 0 .. 3 (dmrs_pucch_estimator_formats3_4.cpp:30-55)
+  std::vector<float> base(2 * M);
+  if (srs_amd_low_papr_sequence(base.data(), M, p.n_id_hopping % 30, 0) != SRS_AMD_OK) {
+    return SRS_AMD_EINVAL;
+  }
+  static const uint32_t m0_of[4] = {0, 6, 3, 9};
+  const uint32_t        m0       = f4 ? m0_of[p.occ_index & 3] : 0u;
+  for (uint32_t r = 0; r != p.nof_symbols; ++r) {
+    if (!((mask >> r) & 1u)) {
+      continue;
+    }
+    const uint32_t n_cs  = gold_byte(proc->jump, p.n_id_hopping, 8 * (NSYMB * p.slot_index + p.start_symbol_index + r));
+    const uint32_t alpha = (m0 + n_cs) % 12;
+    for (uint32_t k = 0; k != M; ++k) {
+      const double ph = 2.0 * M_PI * static_cast<double>((alpha * k) % 12) / 12.0;
+      const float  cr = static_cast<float>(std::cos(ph)), ci = static_cast<float>(std::sin(ph));
+      const float  br = base[2 * k], bi = base[2 * k + 1];
+      pil.push_back(make_float2(br * cr - bi * ci, br * ci + bi * cr));
+    }
+  }
+  d.qm      = p.pi2_bpsk ? 0u : 2u;
+  d.occ_len = occ;
+  if (f4) {
+    // pucch_orthogonal_sequence_format4 (pucch_orthogonal_sequence.h:162-172)
+    static const float2 W2[2][12] = {{{1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0},
+                                      {1, 0}, {1, 0}},
+                                     {{1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {-1, 0}, {-1, 0}, {-1, 0},
+                                      {-1, 0}, {-1, 0}, {-1, 0}}};
+    static const float2 W4[4][12] = {
+        {{1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}, {1, 0}},
+        {{1, 0}, {1, 0}, {1, 0}, {0, -1}, {0, -1}, {0, -1}, {-1, 0}, {-1, 0}, {-1, 0}, {0, 1}, {0, 1}, {0, 1}},
+        {{1, 0}, {1, 0}, {1, 0}, {-1, 0}, {-1, 0}, {-1, 0}, {1, 0}, {1, 0}, {1, 0}, {-1, 0}, {-1, 0}, {-1, 0}},
+        {{1, 0}, {1, 0}, {1, 0}, {0, 1}, {0, 1}, {0, 1}, {-1, 0}, {-1, 0}, {-1, 0}, {0, -1}, {0, -1}, {0, -1}}};
+    for (uint32_t k = 0; k != 12; ++k) {
+      d.occ_w[k] = occ == 2 ? W2[p.occ_index][k] : W4[p.occ_index][k];
+    }
+  }
+  d.n_sym = nds * M / occ;
+  scr.assign((E + 31) / 32, 0u);
+  gold_bits(proc->jump, p.rnti * (1u << 15) + p.n_id_scrambling, 0, E, scr.data());
+  d.counts[0] = p.nof_harq_ack;
+  d.counts[1] = p.nof_sr;
+  d.counts[2] = p.nof_csi_part1;
+  d.counts[3] = p.nof_csi_part2;
+  return SRS_AMD_OK;
+}
+
+// The Format 3 / 4 slot form; decode = false stops after the LLRs (rows of PUCCH_F3_MAX_E in proc->work).
+int f34_slot(srs_amd_pucch_processor*     proc,
+             const srs_amd_pucch_f34_pdu* pdus,
+             uint32_t                     nof_pdus,
+             const uint32_t*              d_grids,
+             uint64_t                     grid_stride,
+             uint32_t                     nof_grids,
+             uint32_t                     nof_grid_ports,
+             uint32_t                     nof_subc,
+             srs_amd_pucch_uci_result*    d_results,
+             uint8_t*                     d_payloads,
+             uint64_t                     payload_stride,
+             void*                        stream,
+             bool                         decode)
+{
+  if (proc == nullptr || (nof_pdus != 0 && (pdus == nullptr || d_results == nullptr || d_payloads == nullptr))) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (nof_pdus == 0) {
+    return SRS_AMD_OK;
+  }
+  if (nof_subc == 0 || nof_subc % 12 != 0) {
+    return fail(SRS_AMD_EINVAL, "Invalid number of grid subcarriers (i.e., %u).", nof_subc);
+  }
+  std::lock_guard<std::mutex>        lock(proc->mtx);
+  std::vector<pucch_f34_desc>        desc(nof_pdus);
+  std::vector<std::vector<float2>>   pil(nof_pdus);
+  std::vector<std::vector<uint32_t>> scr(nof_pdus);
+  std::vector<uint32_t>              K(nof_pdus), E(nof_pdus), Q(nof_pdus);
+  uint32_t                           max_k = 0;
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    const int rc = make_f34_desc(proc, pdus[i], d_grids, grid_stride, nof_grids, nof_grid_ports, nof_subc, desc[i],
+                                 pil[i], scr[i], E[i], K[i]);
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
+    if (K[i] > payload_stride) {
+      return fail(SRS_AMD_EINVAL, "payload_stride %llu below the PDU's %u payload bits.",
+                  static_cast<unsigned long long>(payload_stride), K[i]);
+    }
+    Q[i]  = pdus[i].pi2_bpsk ? 0u : 2u;
+    max_k = std::max(max_k, K[i]);
+  }
+  std::vector<uint32_t> perm(nof_pdus);
+  std::iota(perm.begin(), perm.end(), 0u);
+  std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+    return K[a] != K[b] ? K[a] < K[b] : (E[a] != E[b] ? E[a] < E[b] : Q[a] < Q[b]);
+  });
+  const uint32_t msg_stride = (std::max(max_k, 1u) + 63) / 64 * 64;
+  const size_t   llr_bytes  = static_cast<size_t>(nof_pdus) * PUCCH_F3_MAX_E;
+  const size_t   msg_bytes  = static_cast<size_t>(nof_pdus) * msg_stride;
+  const size_t   st_bytes   = static_cast<size_t>(nof_pdus) * sizeof(int32_t);
+  auto           s          = static_cast<hipStream_t>(stream);
+  hipError_t     e          = hipSetDevice(proc->device);
+  if (e == hipSuccess) {
+    e = proc->work.ensure(llr_bytes + msg_bytes + st_bytes);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUCCH processor scratch");
+  }
+  int8_t*  d_llr = proc->work.as<int8_t>();
+  uint8_t* d_msg = proc->work.as<uint8_t>() + llr_bytes;
+  int32_t* d_st  = reinterpret_cast<int32_t*>(proc->work.as<uint8_t>() + llr_bytes + msg_bytes);
+  // stage layout: descriptors (decoder order), perm, nbits, then every PDU's DM-RS and scrambling words
+  const size_t dbytes = sizeof(pucch_f34_desc) * nof_pdus;
+  const size_t ioff   = (dbytes + 255) & ~size_t(255);
+  const size_t ibytes = sizeof(uint32_t) * nof_pdus;
+  size_t       off    = (ioff + 2 * ibytes + 255) & ~size_t(255);
+  std::vector<size_t> pil_off(nof_pdus), scr_off(nof_pdus);
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    pil_off[i] = off;
+    off        = (off + pil[i].size() * sizeof(float2) + 15) & ~size_t(15);
+    scr_off[i] = off;
+    off        = (off + scr[i].size() * sizeof(uint32_t) + 15) & ~size_t(15);
+  }
+  const size_t bytes = off;
+  if (e == hipSuccess) {
+    e = proc->buf.ensure(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->stage.acquire(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->order.begin(s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUCCH processor scratch");
+  }
+  std::vector<pucch_f34_desc> ordered(nof_pdus);
+  std::vector<uint32_t>       nbits(nof_pdus);
+  for (uint32_t j = 0; j != nof_pdus; ++j) {
+    const uint32_t i = perm[j];
+    ordered[j]       = desc[i];
+    ordered[j].pil    = reinterpret_cast<const float2*>(proc->buf.as<uint8_t>() + pil_off[i]);
+    ordered[j].scr    = reinterpret_cast<const uint32_t*>(proc->buf.as<uint8_t>() + scr_off[i]);
+    ordered[j].llr    = d_llr + static_cast<size_t>(j) * PUCCH_F3_MAX_E;
+    ordered[j].result = d_results + i;
+    nbits[j]          = K[i];
+  }
+  call_scope scope(proc->order, nullptr, s);
+  std::memcpy(proc->stage.at<uint8_t>(0), ordered.data(), dbytes);
+  std::memcpy(proc->stage.at<uint8_t>(ioff), perm.data(), ibytes);
+  std::memcpy(proc->stage.at<uint8_t>(ioff + ibytes), nbits.data(), ibytes);
+  for (uint32_t i = 0; i != nof_pdus; ++i) {
+    std::memcpy(proc->stage.at<uint8_t>(pil_off[i]), pil[i].data(), pil[i].size() * sizeof(float2));
+    std::memcpy(proc->stage.at<uint8_t>(scr_off[i]), scr[i].data(), scr[i].size() * sizeof(uint32_t));
+  }
+  e = proc->stage.upload(proc->buf.ptr, bytes, s);
+  if (e == hipSuccess) {
+    e = launch_pucch_f34(proc->buf.as<pucch_f34_desc>(), nof_pdus, s);
+  }
+  int rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pucch_f34_kernel launch");
+  for (uint32_t j0 = 0; decode && rc == SRS_AMD_OK && j0 != nof_pdus;) {
+    const uint32_t i0 = perm[j0];
+    uint32_t       j1 = j0 + 1;
+    while (j1 != nof_pdus && K[perm[j1]] == K[i0] && E[perm[j1]] == E[i0] && Q[perm[j1]] == Q[i0]) {
+      ++j1;
+    }
+    rc = srs_amd_uci_decode_batch(proc->uci, d_llr + static_cast<size_t>(j0) * PUCCH_F3_MAX_E, PUCCH_F3_MAX_E, E[i0],
+                                  K[i0], static_cast<int32_t>(Q[i0]), d_msg + static_cast<size_t>(j0) * msg_stride,
+                                  msg_stride, d_st + j0, sizeof(int32_t), j1 - j0, s);
+    j0 = j1;
+  }
+  if (decode && rc == SRS_AMD_OK) {
+    const uint32_t* d_perm = reinterpret_cast<const uint32_t*>(proc->buf.as<uint8_t>() + ioff);
+    e  = launch_pucch_uci_finish(d_st, d_msg, msg_stride, d_perm, d_perm + nof_pdus, nof_pdus, d_results, d_payloads,
+                                 payload_stride, s);
+    rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pucch_uci_finish_kernel launch");
+  }
+  const hipError_t done = scope.close();
+  return rc != SRS_AMD_OK ? rc : (done == hipSuccess ? SRS_AMD_OK : hip_fail(done, "PUCCH completion event"));
+}
+
 int make_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f0_pdu& p, const uint32_t* d_grids,
               uint64_t grid_stride, uint32_t nof_grids, uint32_t nof_grid_ports, uint32_t nof_subc, pucch_f0_desc& d)
 {
@@ -821,6 +1133,108 @@ int srs_amd_pucch_f2_process(srs_amd_pucch_processor*    proc,
     (void)hipStreamSynchronize(proc->stream);
   }
   return rc;
+}
+
+int srs_amd_pucch_f34_process_slot(srs_amd_pucch_processor*     proc,
+                                   const srs_amd_pucch_f34_pdu* pdus,
+                                   uint32_t                     nof_pdus,
+                                   const uint32_t*              d_grids,
+                                   uint64_t                     grid_stride,
+                                   uint32_t                     nof_grids,
+                                   uint32_t                     nof_grid_ports,
+                                   uint32_t                     nof_subc,
+                                   srs_amd_pucch_uci_result*    d_results,
+                                   uint8_t*                     d_payloads,
+                                   uint64_t                     payload_stride,
+                                   void*                        stream)
+{
+  return f34_slot(proc, pdus, nof_pdus, d_grids, grid_stride, nof_grids, nof_grid_ports, nof_subc, d_results,
+                  d_payloads, payload_stride, stream, true);
+}
+
+namespace {
+
+// Host forms of Formats 3 / 4: the grid up, one PDU, the result and payload (or the LLRs) down.
+int f34_host(srs_amd_pucch_processor* proc, const srs_amd_pucch_f34_pdu* pdu, const uint32_t* grid,
+             uint32_t nof_ports, uint32_t nof_subc, srs_amd_pucch_uci_result* result, uint8_t* payload, int8_t* llrs)
+{
+  if (proc == nullptr || pdu == nullptr || grid == nullptr || (llrs == nullptr && (result == nullptr || payload == nullptr))) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  const uint32_t              K     = pdu->nof_harq_ack + pdu->nof_sr + pdu->nof_csi_part1 + pdu->nof_csi_part2;
+  const size_t                bytes = sizeof(uint32_t) * nof_ports * NSYMB * nof_subc;
+  std::lock_guard<std::mutex> host_lock(proc->host_mtx);
+  hipError_t                  e = hipSetDevice(proc->device);
+  if (e == hipSuccess) {
+    e = proc->host_grid.ensure(bytes);
+  }
+  if (e == hipSuccess) {
+    e = proc->host_res.ensure(sizeof(srs_amd_pucch_uci_result));
+  }
+  if (e == hipSuccess) {
+    e = proc->host_payload.ensure(1706);
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(proc->host_grid.ptr, grid, bytes, hipMemcpyHostToDevice, proc->stream);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "PUCCH grid upload");
+  }
+  srs_amd_pucch_f34_pdu p = *pdu;
+  p.grid                  = 0;
+  p.d_grid                = nullptr;
+  int rc = f34_slot(proc, &p, 1, proc->host_grid.as<uint32_t>(), 0, 1, nof_ports, nof_subc,
+                    proc->host_res.as<srs_amd_pucch_uci_result>(), proc->host_payload.as<uint8_t>(), 1706,
+                    proc->stream, llrs == nullptr);
+  if (rc == SRS_AMD_OK) {
+    if (llrs != nullptr) {
+      const bool     f4  = p.format == 4;
+      const uint32_t nd  = static_cast<uint32_t>(__builtin_popcount(f34_dmrs_mask(p.nof_symbols, p.second_hop_prb >= 0,
+                                                                                  p.additional_dmrs != 0)));
+      const uint32_t E   = (p.nof_symbols - nd) * 12 * (f4 ? 1u : p.nof_prb) * (p.pi2_bpsk ? 1u : 2u) /
+                         (f4 ? p.occ_length : 1u);
+      e = hipMemcpyAsync(llrs, proc->work.ptr, E, hipMemcpyDeviceToHost, proc->stream);
+    } else {
+      e = hipMemcpyAsync(result, proc->host_res.ptr, sizeof(*result), hipMemcpyDeviceToHost, proc->stream);
+      if (e == hipSuccess && K != 0) {
+        e = hipMemcpyAsync(payload, proc->host_payload.ptr, K, hipMemcpyDeviceToHost, proc->stream);
+      }
+    }
+    e  = e == hipSuccess ? hipStreamSynchronize(proc->stream) : e;
+    rc = e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUCCH result download");
+  } else {
+    (void)hipStreamSynchronize(proc->stream);
+  }
+  return rc;
+}
+
+} // namespace
+
+int srs_amd_pucch_f34_process(srs_amd_pucch_processor*     proc,
+                              const srs_amd_pucch_f34_pdu* pdu,
+                              const uint32_t*              grid,
+                              uint32_t                     nof_ports,
+                              uint32_t                     nof_subc,
+                              srs_amd_pucch_uci_result*    result,
+                              uint8_t*                     payload)
+{
+  if (result == nullptr || payload == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  return f34_host(proc, pdu, grid, nof_ports, nof_subc, result, payload, nullptr);
+}
+
+int srs_amd_pucch_f34_demodulate(srs_amd_pucch_processor*     proc,
+                                 const srs_amd_pucch_f34_pdu* pdu,
+                                 const uint32_t*              grid,
+                                 uint32_t                     nof_ports,
+                                 uint32_t                     nof_subc,
+                                 int8_t*                      llrs)
+{
+  if (llrs == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  return f34_host(proc, pdu, grid, nof_ports, nof_subc, nullptr, nullptr, llrs);
 }
 
 int srs_amd_pucch_f1_detect_slot(srs_amd_pucch_processor*      proc,

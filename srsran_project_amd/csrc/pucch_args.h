@@ -96,4 +96,41 @@ hipError_t launch_pucch_uci_finish(const int32_t* status, const uint8_t* message
                                    srs_amd_pucch_uci_result* results, uint8_t* payloads, uint64_t payload_stride,
                                    hipStream_t stream);
 
+constexpr uint32_t PUCCH_F3_MAX_M    = 12 * 16;                   // subcarriers of a Format 3 allocation
+constexpr uint32_t PUCCH_F3_MAX_DATA = 12;                        // data symbols (14 minus two DM-RS symbols)
+constexpr uint32_t PUCCH_F3_MAX_E    = 2 * PUCCH_F3_MAX_M * PUCCH_F3_MAX_DATA;
+
+struct pucch_f34_desc {
+  const uint32_t*           grid;        // cbf16 [port][14][nof_subc]
+  uint32_t                  port_stride;
+  uint32_t                  nof_subc;
+  uint32_t                  l0, nsym;
+  uint32_t                  M;           // subcarriers (12 nof_prb)
+  uint32_t                  dmrs_mask;   // allocated symbols carrying DM-RS
+  uint32_t                  hop_sym;     // first allocated symbol of the second hop (nsym: no hopping)
+  uint32_t                  subc0[2];    // first subcarrier of each hop
+  uint32_t                  nof_ports;
+  uint32_t                  ports[4];
+  float                     epoch[14];   // start epochs of the allocated symbols
+  float                     scs_hz;
+  int32_t                   nof_taps, nof_v;
+  float                     rc[31];
+  uint32_t                  ta_n;
+  int32_t                   ta_max_taps;
+  int32_t                   ta_frac;
+  double                    ta_fs;
+  uint32_t                  qm;          // 0: pi/2-BPSK, 2: QPSK
+  uint32_t                  occ_len;     // Format 4 spreading factor (1: Format 3)
+  float2                    occ_w[12];   // Format 4 OCC w_n(k)
+  uint32_t                  n_sym;       // modulation symbols after deprecoding / despreading
+  uint32_t                  counts[4];
+  const float2*             pil;         // DM-RS of each DM-RS symbol [nof DM-RS][M] (device)
+  const uint32_t*           scr;         // scrambling sequence words (device)
+  int8_t*                   llr;
+  srs_amd_pucch_uci_result* result;
+};
+
+// Estimation, equalization, deprecoding, despreading, demapping and descrambling of every Format 3 / 4 PDU.
+hipError_t launch_pucch_f34(const pucch_f34_desc* d_desc, uint32_t nof, hipStream_t stream);
+
 } // namespace srs_amd

@@ -88,6 +88,54 @@ def make_f2_pdu(*, numerology=0, slot_index=0, bwp_start_rb=0, bwp_size_rb=52, s
     return p
 
 
+class PucchF34Pdu(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("format", "numerology", "slot_index", "bwp_start_rb", "bwp_size_rb",
+                                                "starting_prb")] + [("second_hop_prb", ctypes.c_int32)] + \
+               [(n, ctypes.c_uint32) for n in ("nof_prb", "start_symbol_index", "nof_symbols", "rnti", "n_id_hopping",
+                                                "n_id_scrambling", "nof_harq_ack", "nof_sr", "nof_csi_part1",
+                                                "nof_csi_part2", "additional_dmrs", "pi2_bpsk", "occ_index",
+                                                "occ_length", "nof_ports")] + \
+               [("ports", ctypes.c_uint8 * 4), ("grid", ctypes.c_uint32), ("d_grid", ctypes.c_void_p)]
+
+
+def make_f34_pdu(*, format=3, numerology=0, slot_index=0, bwp_start_rb=0, bwp_size_rb=52, starting_prb=0,
+                 second_hop_prb=None, nof_prb=1, start_symbol_index=0, nof_symbols=14, rnti=0x4601, n_id_hopping=0,
+                 n_id_scrambling=0, nof_harq_ack=0, nof_sr=0, nof_csi_part1=0, nof_csi_part2=0, additional_dmrs=False,
+                 pi2_bpsk=False, occ_index=0, occ_length=2, ports=(0,), grid=0):
+    """pucch_processor::format3_configuration (format=3) / format4_configuration (format=4)."""
+    p = PucchF34Pdu()
+    for k, v in dict(format=format, numerology=numerology, slot_index=slot_index, bwp_start_rb=bwp_start_rb,
+                     bwp_size_rb=bwp_size_rb, starting_prb=starting_prb, nof_prb=1 if format == 4 else nof_prb,
+                     start_symbol_index=start_symbol_index, nof_symbols=nof_symbols, rnti=rnti,
+                     n_id_hopping=n_id_hopping, n_id_scrambling=n_id_scrambling, nof_harq_ack=nof_harq_ack,
+                     nof_sr=nof_sr, nof_csi_part1=nof_csi_part1, nof_csi_part2=nof_csi_part2,
+                     additional_dmrs=bool(additional_dmrs), pi2_bpsk=bool(pi2_bpsk), occ_index=occ_index,
+                     occ_length=occ_length, grid=grid).items():
+        setattr(p, k, int(v))
+    p.second_hop_prb = -1 if second_hop_prb is None else int(second_hop_prb)
+    if not 1 <= len(ports) <= 4:
+        raise ValueError("1 to 4 ports")
+    p.nof_ports = len(ports)
+    for i, q in enumerate(ports):
+        p.ports[i] = int(q)
+    return p
+
+
+def f34_dmrs_mask(nof_symbols, hop, additional):
+    """get_pucch_formats3_4_dmrs_symbol_mask (pucch_formats3_4_helpers.h): allocated symbols carrying DM-RS."""
+    t = {4: [0, 2] if hop else [1], 5: [0, 3], 6: [1, 4], 7: [1, 4], 8: [1, 5], 9: [1, 6],
+         10: [1, 3, 6, 8] if additional else [2, 7], 11: [1, 3, 6, 9] if additional else [2, 7],
+         12: [1, 4, 7, 10] if additional else [2, 8], 13: [1, 4, 7, 11] if additional else [2, 9],
+         14: [1, 5, 8, 12] if additional else [3, 10]}
+    return t[nof_symbols]
+
+
+def f34_nof_llrs(pdu):
+    nd = len(f34_dmrs_mask(pdu.nof_symbols, pdu.second_hop_prb >= 0, pdu.additional_dmrs))
+    M = 12 * (1 if pdu.format == 4 else pdu.nof_prb)
+    return (pdu.nof_symbols - nd) * M * (1 if pdu.pi2_bpsk else 2) // (pdu.occ_length if pdu.format == 4 else 1)
+
+
 def payload_bits(pdu):
     return pdu.nof_harq_ack + pdu.nof_sr + pdu.nof_csi_part1 + pdu.nof_csi_part2
 
@@ -156,6 +204,10 @@ def _declare(lib):
                                                     c.c_uint32, P, P, c.c_uint64, P]),
         "srs_amd_pucch_f2_process": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P, P]),
         "srs_amd_pucch_f2_demodulate": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P]),
+        "srs_amd_pucch_f34_process_slot": (c.c_int, [P, P, c.c_uint32, P, c.c_uint64, c.c_uint32, c.c_uint32,
+                                                     c.c_uint32, P, P, c.c_uint64, P]),
+        "srs_amd_pucch_f34_process": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P, P]),
+        "srs_amd_pucch_f34_demodulate": (c.c_int, [P, P, P, c.c_uint32, c.c_uint32, P]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -263,6 +315,40 @@ class PucchProcessor:
         _lib.check(self._lib.srs_amd_pucch_f2_demodulate(self._h, ctypes.byref(pdu), grid.ctypes.data, grid.shape[0],
                                                          grid.shape[2], llr.ctypes.data), "pucch f2 demodulate")
         return llr
+
+    def process_f34(self, grid, pdu):
+        """pucch_processor::process of one Format 3 / 4 PDU on a host grid -> (PucchUciResult, payload bits)."""
+        if grid.dtype != np.uint32 or grid.ndim != 3 or grid.shape[1] != 14 or not grid.flags.c_contiguous:
+            raise ValueError("grid must be a C-contiguous uint32 array [ports][14][nof_subc]")
+        r = PucchUciResult()
+        payload = np.zeros(max(payload_bits(pdu), 1), np.uint8)
+        _lib.check(self._lib.srs_amd_pucch_f34_process(self._h, ctypes.byref(pdu), grid.ctypes.data, grid.shape[0],
+                                                       grid.shape[2], ctypes.byref(r), payload.ctypes.data),
+                   "pucch f34 process")
+        return r, payload[:payload_bits(pdu)]
+
+    def demodulate_f34(self, grid, pdu):
+        """Estimator + pucch_demodulator of one Format 3 / 4 PDU on a host grid -> int8 LLRs."""
+        llr = np.zeros(f34_nof_llrs(pdu), np.int8)
+        _lib.check(self._lib.srs_amd_pucch_f34_demodulate(self._h, ctypes.byref(pdu), grid.ctypes.data,
+                                                          grid.shape[0], grid.shape[2], llr.ctypes.data),
+                   "pucch f34 demodulate")
+        return llr
+
+    def process_f34_slot(self, grids, pdus, payload_stride=1706, stream=None):
+        """Every Format 3 / 4 PDU of a slot on device grids -> (torch uint8 result records, payload rows)."""
+        import torch
+
+        arr = (PucchF34Pdu * len(pdus))(*pdus)
+        res = torch.zeros((max(len(pdus), 1), UCI_RESULT_DTYPE.itemsize), dtype=torch.uint8, device=grids.device)
+        pay = torch.zeros((max(len(pdus), 1), payload_stride), dtype=torch.uint8, device=grids.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(grids.device)
+        _lib.check(self._lib.srs_amd_pucch_f34_process_slot(
+            self._h, arr, len(pdus), grids.data_ptr(), grids.stride(0), grids.shape[0], grids.shape[1],
+            grids.shape[-1], res.data_ptr(), pay.data_ptr(), payload_stride, ctypes.c_void_p(stream.cuda_stream)),
+            "pucch f34 process_slot")
+        return res[:len(pdus)], pay[:len(pdus)]
 
     def process_f2_slot(self, grids, pdus, payload_stride=1706, stream=None):
         """Every Format 2 PDU of a slot on device grids (torch int32 [n][ports][14][nof_subc]) -> (torch uint8

@@ -113,3 +113,49 @@ def f2_cases(n=16, seed=0):
         op.transmit_f2(grid, pdu, payload, gains, [0.001, 0.03, 0.3, 3.0][i % 4], rng)
         out.append((pdu, grid, payload))
     return out
+
+
+F3_PRBS = [1, 2, 3, 4, 5, 6, 8, 9, 10, 12, 15, 16]
+
+
+def f34_cases(n=16, seed=0, fmt=None):
+    """[(pdu, grid uint32 [4][14][NSUBC], payload bits)]: Formats 3 (1-16 PRBs of the transform-precoding sizes) and 4
+    (OCC 2 / 4), 4-14 symbols, hopping, additional DM-RS, QPSK and pi/2-BPSK, 1-4 ports in any order, Reed-Muller and
+    polar payloads within the 0.8 code rate, SNRs from clean to failing."""
+    from oracle import pucch as op
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        f = fmt if fmt is not None else (3 if i % 3 else 4)
+        nprb = F3_PRBS[int(rng.integers(0, len(F3_PRBS)))] if f == 3 else 1
+        nsym = int(rng.integers(4, 15))
+        hop = bool(rng.integers(0, 2))
+        add = bool(rng.integers(0, 2))
+        pi2 = bool(rng.integers(0, 2))
+        occ = [2, 4][int(rng.integers(0, 2))]
+        nports = int(rng.integers(1, 5))
+        mu = int(rng.integers(0, 3))
+        kw = dict(format=f, numerology=mu, slot_index=int(rng.integers(0, 10 << mu)), bwp_start_rb=1, bwp_size_rb=50,
+                  starting_prb=int(rng.integers(0, 50 - nprb + 1)),
+                  second_hop_prb=int(rng.integers(0, 50 - nprb + 1)) if hop else None, nof_prb=nprb,
+                  start_symbol_index=int(rng.integers(0, 15 - nsym)), nof_symbols=nsym,
+                  rnti=int(rng.integers(1, 65536)), n_id_hopping=int(rng.integers(0, 1024)),
+                  n_id_scrambling=int(rng.integers(0, 1024)), additional_dmrs=add, pi2_bpsk=pi2,
+                  occ_index=int(rng.integers(0, occ)), occ_length=occ,
+                  ports=tuple(int(x) for x in rng.permutation(4)[:nports]))
+        probe = amd.pucch.make_f34_pdu(nof_harq_ack=3, **kw)
+        E = amd.pucch.f34_nof_llrs(probe)
+        chan = E  # the codeword E (the validator's Format 4 rate counts 12 REs per symbol whatever the OCC)
+        K = int(rng.integers(3, 12)) if i % 2 == 0 else int(rng.integers(12, max(13, min(int(0.8 * chan) - 11, 200))))
+        while K > 3 and (K + (0 if K <= 11 else (6 if K < 20 else 11))) > 0.8 * chan:
+            K -= 1
+        nh = int(rng.integers(0, K + 1))
+        nsr = int(rng.integers(0, min(4, K - nh) + 1))
+        pdu = amd.pucch.make_f34_pdu(nof_harq_ack=nh, nof_sr=nsr, nof_csi_part1=K - nh - nsr, **kw)
+        payload = rng.integers(0, 2, K).astype(np.uint8)
+        grid = rng.integers(0, 1 << 32, (4, 14, NSUBC), dtype=np.uint64).astype(np.uint32)
+        gains = (rng.normal(size=nports) + 1j * rng.normal(size=nports)) / np.sqrt(2)
+        op.transmit_f34(grid, pdu, payload, gains, [0.001, 0.03, 0.3, 3.0][i % 4], rng)
+        out.append((pdu, grid, payload))
+    return out

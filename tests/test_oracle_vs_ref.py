@@ -575,3 +575,20 @@ def test_pucch_f2_transmitter_decoded_by_reference():
         assert r.status == 1 and np.array_equal(pay, payload), i
         n += 1
     assert n == 3
+
+
+def test_pucch_f34_transmitter_decoded_by_reference():
+    """tests/pucch_cases.py's Format 3 / 4 transmitter (UCI encoding, scrambling, pi/2-BPSK / QPSK, OCC spreading,
+    transform precoding, low-PAPR DM-RS) is the reference receiver's convention: at the highest SNR of the cases the
+    compiled pucch_processor_impl returns the payload, valid."""
+    from oracle import pucch as op
+    from tests.pucch_cases import f34_cases
+
+    n = 0
+    for i, (pdu, grid, payload) in enumerate(f34_cases(n=24, seed=5)):
+        if i % 4 != 0:
+            continue
+        r, pay = op.ref_process_f34(grid, pdu)
+        assert r.status == 1 and np.array_equal(pay, payload), (i, pdu.format, pdu.nof_prb, pdu.pi2_bpsk, r.status)
+        n += 1
+    assert n == 6
