@@ -21,6 +21,9 @@ float baseband and back (ofdm_slot_modulator / ofdm_slot_demodulator).
 `--workload sch_slot` (heterogeneous slots, not a BASELINE.json config): one step PDSCH-encodes and
 PUSCH-decodes the transport blocks of `--slots-pipeline` cells x `--ues-per-cell` UEs with different PRB
 shares, MCS and layer counts through the slot-level entry points -- see bench_slot.py.
+`--workload pucch`: every PUCCH (Formats 0-4) of a slot of --slots-pipeline cells through the slot forms of
+include/srsran_amd/pucch.h, UCI messages/s, with the reference pucch_processor_impl as the CPU baseline
+(bench_pucch.py).
 `--workload slot_pipeline`: the full PDSCH + PUSCH chains of such multi-UE cells (slot encoder, slot modulator
 + DM-RS, OFDM; OFDM, slot PUSCH processor) -- bench_slot.SlotPipeline.
 
@@ -67,7 +70,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="pipeline", choices=["pipeline", "ldpc", "ofdm", "sch_slot",
-                                                                       "slot_pipeline"])
+                                                                       "slot_pipeline", "pucch"])
     p.add_argument("--batch", type=int, default=4096, help="ldpc: codeblocks per rank per step")
     p.add_argument("--slots", type=int, default=160, help="ofdm: slots per rank per step (x 4 ports)")
     p.add_argument("--slots-pipeline", type=int, default=64,
@@ -465,6 +468,10 @@ def main():
         from bench_slot import run_slot_pipeline
 
         line = run_slot_pipeline(args, dist, world, rank, dev, timed)
+    elif args.workload == "pucch":
+        from bench_pucch import run_pucch
+
+        line = run_pucch(args, dist, world, rank, dev, timed)
     else:
         run = run_ldpc if args.workload == "ldpc" else run_ofdm
         line = run(args, dist, world, rank, dev)

@@ -33,6 +33,8 @@
 #include "srsran/ran/cyclic_prefix.h"
 #include "srsran_amd/pucch.h"
 #include <atomic>
+#include <chrono>
+#include <vector>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -451,6 +453,121 @@ void srs_ref_pucch_f34_demodulate(const uint32_t* grid, unsigned nof_grid_ports,
   dc.additional_dmrs    = p->additional_dmrs != 0;
   dc.pi2_bpsk           = p->pi2_bpsk != 0;
   dem.demodulate(out, reader, ce, dc);
+}
+
+// CPU baseline of bench.py --workload pucch: one pucch_processor_impl (built once) processes every PDU of the lists
+// on grid [nof_grid_ports][14][nsubc], reps times, on the calling thread; returns the seconds taken.  Format 0 / 1
+// PDUs carry absolute PRBs (BWP from PRB 0).
+double srs_ref_pucch_time(const uint32_t* grid, unsigned nof_grid_ports, unsigned nsubc,
+                          const srs_amd_pucch_f0_pdu* f0, unsigned n0, const srs_amd_pucch_f1_batch* f1, unsigned n1,
+                          const srs_amd_pucch_f2_pdu* f2, unsigned n2, const srs_amd_pucch_f34_pdu* f34, unsigned n34,
+                          unsigned reps)
+{
+  grid_tensor data({nsubc, MAX_NSYMB_PER_SLOT, nof_grid_ports});
+  fill_grid(data, grid, nof_grid_ports, nsubc);
+  std::atomic<unsigned>     empty{0};
+  resource_grid_reader_impl reader(data, empty);
+  auto                      proc = make_processor(nsubc / NRE, nof_grid_ports);
+  std::vector<pucch_processor::format0_configuration>       c0(n0);
+  std::vector<pucch_processor::format1_batch_configuration> c1(n1);
+  std::vector<pucch_processor::format2_configuration>       c2(n2);
+  std::vector<pucch_processor::format3_configuration>       c3;
+  std::vector<pucch_processor::format4_configuration>       c4;
+  for (unsigned i = 0; i != n0; ++i) {
+    const srs_amd_pucch_f0_pdu& p = f0[i];
+    auto&                       c = c0[i];
+    c.slot                        = slot_point(p.numerology, p.slot_index);
+    c.cp                          = cyclic_prefix::NORMAL;
+    c.bwp_size_rb                 = nsubc / NRE;
+    c.bwp_start_rb                = 0;
+    c.starting_prb                = p.starting_prb;
+    if (p.second_hop_prb >= 0) {
+      c.second_hop_prb = static_cast<unsigned>(p.second_hop_prb);
+    }
+    c.start_symbol_index   = p.start_symbol_index;
+    c.nof_symbols          = p.nof_symbols;
+    c.initial_cyclic_shift = p.initial_cyclic_shift;
+    c.n_id                 = p.n_id;
+    c.nof_harq_ack         = p.nof_harq_ack;
+    c.sr_opportunity       = p.sr_opportunity != 0;
+    for (unsigned k = 0; k != p.nof_ports; ++k) {
+      c.ports.push_back(p.ports[k]);
+    }
+  }
+  for (unsigned i = 0; i != n1; ++i) {
+    const srs_amd_pucch_f1_batch& b = f1[i];
+    auto&                         c = c1[i].common_config;
+    c.slot                          = slot_point(b.numerology, b.slot_index);
+    c.bwp_size_rb                   = nsubc / NRE;
+    c.bwp_start_rb                  = 0;
+    c.cp                            = cyclic_prefix::NORMAL;
+    c.starting_prb                  = b.starting_prb;
+    if (b.second_hop_prb >= 0) {
+      c.second_hop_prb = static_cast<unsigned>(b.second_hop_prb);
+    }
+    c.n_id = b.n_id;
+    for (unsigned k = 0; k != b.nof_ports; ++k) {
+      c.ports.push_back(b.ports[k]);
+    }
+    c.nof_symbols        = b.nof_symbols;
+    c.start_symbol_index = b.start_symbol_index;
+    for (unsigned e = 0; e != b.nof_entries; ++e) {
+      c1[i].entries.insert(b.entries[e].initial_cyclic_shift, b.entries[e].time_domain_occ,
+                           {.context = std::nullopt, .nof_harq_ack = b.entries[e].nof_harq_ack});
+    }
+  }
+  for (unsigned i = 0; i != n2; ++i) {
+    const srs_amd_pucch_f2_pdu& p = f2[i];
+    auto&                       c = c2[i];
+    c.slot                        = slot_point(p.numerology, p.slot_index);
+    c.bwp_size_rb                 = p.bwp_size_rb;
+    c.bwp_start_rb                = p.bwp_start_rb;
+    c.cp                          = cyclic_prefix::NORMAL;
+    c.starting_prb                = p.starting_prb;
+    if (p.second_hop_prb >= 0) {
+      c.second_hop_prb = static_cast<unsigned>(p.second_hop_prb);
+    }
+    c.nof_prb            = p.nof_prb;
+    c.start_symbol_index = p.start_symbol_index;
+    c.nof_symbols        = p.nof_symbols;
+    c.rnti               = static_cast<uint16_t>(p.rnti);
+    c.n_id               = p.n_id;
+    c.n_id_0             = p.n_id_0;
+    c.nof_harq_ack       = p.nof_harq_ack;
+    c.nof_sr             = p.nof_sr;
+    c.nof_csi_part1      = p.nof_csi_part1;
+    c.nof_csi_part2      = p.nof_csi_part2;
+    for (unsigned k = 0; k != p.nof_ports; ++k) {
+      c.ports.push_back(p.ports[k]);
+    }
+  }
+  for (unsigned i = 0; i != n34; ++i) {
+    if (f34[i].format == 4) {
+      c4.push_back(to_f4(&f34[i]));
+    } else {
+      c3.emplace_back();
+      fill_f34(&f34[i], c3.back());
+    }
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned r = 0; r != reps; ++r) {
+    for (const auto& c : c0) {
+      (void)proc->process(reader, c);
+    }
+    for (const auto& c : c1) {
+      (void)proc->process(reader, c);
+    }
+    for (const auto& c : c2) {
+      (void)proc->process(reader, c);
+    }
+    for (const auto& c : c3) {
+      (void)proc->process(reader, c);
+    }
+    for (const auto& c : c4) {
+      (void)proc->process(reader, c);
+    }
+  }
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // pucch_processor_impl::process of one Format 2 PDU on grid [nof_grid_ports][14][nsubc].

@@ -89,6 +89,20 @@ float threshold(uint32_t nof_ports, uint32_t nof_symbols, uint32_t nof_seq)
   return -1.0f;
 }
 
+// e^(j 2 pi m / 12), m = 0 .. 11 (cos / sin in double, rounded to float), for the cyclic shifts.
+const float2* twelfth_roots()
+{
+  static const std::vector<float2> t = [] {
+    std::vector<float2> v(12);
+    for (uint32_t m = 0; m != 12; ++m) {
+      const double ph = 2.0 * M_PI * static_cast<double>(m) / 12.0;
+      v[m]            = make_float2(static_cast<float>(std::cos(ph)), static_cast<float>(std::sin(ph)));
+    }
+    return v;
+  }();
+  return t.data();
+}
+
 uint32_t gf2_apply_h(const uint32_t* cols, uint32_t s)
 {
   uint32_t r = 0;
@@ -442,11 +456,11 @@ int make_f34_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f34_p
     }
     const uint32_t n_cs  = gold_byte(proc->jump, p.n_id_hopping, 8 * (NSYMB * p.slot_index + p.start_symbol_index + r));
     const uint32_t alpha = (m0 + n_cs) % 12;
+    const float2* ph = twelfth_roots();
     for (uint32_t k = 0; k != M; ++k) {
-      const double ph = 2.0 * M_PI * static_cast<double>((alpha * k) % 12) / 12.0;
-      const float  cr = static_cast<float>(std::cos(ph)), ci = static_cast<float>(std::sin(ph));
+      const float2 e = ph[(alpha * k) % 12];
       const float  br = base[2 * k], bi = base[2 * k + 1];
-      pil.push_back(make_float2(br * cr - bi * ci, br * ci + bi * cr));
+      pil.push_back(make_float2(br * e.x - bi * e.y, br * e.y + bi * e.x));
     }
   }
   d.qm      = p.pi2_bpsk ? 0u : 2u;
@@ -673,18 +687,21 @@ int make_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f0_pdu& p
   if (srs_amd_low_papr_sequence(base, 12, p.n_id % 30, 0) != SRS_AMD_OK) {
     return SRS_AMD_EINVAL;
   }
+  uint32_t n_cs[2] = {0, 0}; // the Gold-sequence shift of each symbol, common to every candidate
+  for (uint32_t l = 0; l != p.nof_symbols; ++l) {
+    n_cs[l] = gold_byte(proc->jump, p.n_id, 8 * (NSYMB * p.slot_index + p.start_symbol_index + l));
+  }
+  const float2* ph = twelfth_roots();
   for (uint32_t c = 0; c != n; ++c) {
     d.msg[c][0] = tab[c].sr;
     d.msg[c][1] = tab[c].h0;
     d.msg[c][2] = tab[c].h1;
     for (uint32_t l = 0; l != p.nof_symbols; ++l) {
-      const uint32_t n_cs  = gold_byte(proc->jump, p.n_id, 8 * (NSYMB * p.slot_index + p.start_symbol_index + l));
-      const uint32_t alpha = (p.initial_cyclic_shift + tab[c].m_cs + n_cs) % 12;
+      const uint32_t alpha = (p.initial_cyclic_shift + tab[c].m_cs + n_cs[l]) % 12;
       for (uint32_t k = 0; k != 12; ++k) {
-        const double ph = 2.0 * M_PI * static_cast<double>((alpha * k) % 12) / 12.0;
-        const float  cr = static_cast<float>(std::cos(ph)), ci = static_cast<float>(std::sin(ph));
+        const float2 e = ph[(alpha * k) % 12];
         const float  br = base[2 * k], bi = base[2 * k + 1];
-        d.seq[c][l][k] = make_float2(br * cr - bi * ci, br * ci + bi * cr);
+        d.seq[c][l][k] = make_float2(br * e.x - bi * e.y, br * e.y + bi * e.x);
       }
     }
   }
