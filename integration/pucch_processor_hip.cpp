@@ -356,19 +356,21 @@ private:
       log_error("PDU not processed", "device / pinned buffer allocation");
       return nullptr;
     }
+    // the PDU's symbols of each port: staged contiguously, one copy per port
     size_t row = 0;
     for (unsigned i = 0; i != nports; ++i) {
       if (ports[i] >= nof_ports) {
         continue; // the C-ABI call reports the port
       }
+      uint32_t* dst = stage + row * nsubc;
       for (unsigned l = l0; l != l0 + nsym; ++l, ++row) {
-        span<const cbf16_t> v   = grid.get_view(ports[i], l);
-        uint32_t*           dst = stage + row * nsubc;
-        std::memcpy(dst, v.data(), nsubc * sizeof(uint32_t));
-        if (hipMemcpyAsync(scratch + ports[i] * plane + static_cast<size_t>(l) * nsubc, dst, nsubc * sizeof(uint32_t),
-                           hipMemcpyHostToDevice, stream) != hipSuccess) {
-          return nullptr;
-        }
+        span<const cbf16_t> v = grid.get_view(ports[i], l);
+        std::memcpy(stage + row * nsubc, v.data(), nsubc * sizeof(uint32_t));
+      }
+      if (hipMemcpyAsync(scratch + ports[i] * plane + static_cast<size_t>(l0) * nsubc, dst,
+                         static_cast<size_t>(nsym) * nsubc * sizeof(uint32_t), hipMemcpyHostToDevice,
+                         stream) != hipSuccess) {
+        return nullptr;
       }
     }
     return scratch;

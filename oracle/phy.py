@@ -518,6 +518,8 @@ class PucchProcessorPlugin:
         L.srs_ref_phy_pucch_f1.argtypes = [P, P, P, u, P]
         L.srs_ref_phy_pucch_f2.argtypes = [P, P, P, P, P]
         L.srs_ref_phy_pucch_f34.argtypes = [P, P, P, P, P]
+        L.srs_ref_phy_pucch_latency.restype = ctypes.c_double
+        L.srs_ref_phy_pucch_latency.argtypes = [P, P, P, P, u, u]
         L.srs_ref_phy_pucch_f2_validate.restype = i
         L.srs_ref_phy_pucch_f2_validate.argtypes = [P, P, ctypes.c_char_p, u]
         L.srs_ref_phy_pucch_stats.argtypes = [P, P]
@@ -565,6 +567,12 @@ class PucchProcessorPlugin:
         pay = np.zeros(max(payload_bits(pdu), 1), np.uint8)
         lib().srs_ref_phy_pucch_f34(self.h, grid.h, ctypes.byref(pdu), ctypes.byref(r), pay.ctypes.data)
         return r, pay[:payload_bits(pdu)]
+
+    def latency_us(self, grid, pdu0=None, pdu2=None, grid_prb=0, reps=200):
+        """Mean microseconds per pucch_processor::process call (Format 0 or Format 2 PDU)."""
+        t = lib().srs_ref_phy_pucch_latency(self.h, grid.h, None if pdu0 is None else ctypes.byref(pdu0),
+                                            None if pdu2 is None else ctypes.byref(pdu2), grid_prb, reps)
+        return t * 1e6 / reps
 
     def validate_f2(self, pdu):
         msg = ctypes.create_string_buffer(512)

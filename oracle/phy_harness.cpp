@@ -1247,6 +1247,25 @@ void srs_ref_phy_pucch_f34(void* h, void* g, const srs_amd_pucch_f34_pdu* p, srs
   out->cfo_Hz           = r.csi.get_cfo_Hz().value_or(NAN);
 }
 
+/* Seconds for reps calls of pucch_processor::process on one Format 0 PDU / Format 2 PDU (grid g), for the plug-in's
+ * per-call latency (the reference interface returns each result synchronously). */
+double srs_ref_phy_pucch_latency(void* h, void* g, const srs_amd_pucch_f0_pdu* p0, const srs_amd_pucch_f2_pdu* p2,
+                                 unsigned grid_prb, unsigned reps)
+{
+  srs_amd_pucch_result     r0;
+  srs_amd_pucch_uci_result r2;
+  uint8_t                  pay[1706];
+  const auto               t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 0; i != reps; ++i) {
+    if (p0 != nullptr) {
+      srs_ref_phy_pucch_f0(h, g, p0, grid_prb, &r0);
+    } else {
+      srs_ref_phy_pucch_f2(h, g, p2, &r2, pay);
+    }
+  }
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 /* The plug-in factory's validator on a Format 2 PDU: 1 valid, 0 invalid (msg filled). */
 int srs_ref_phy_pucch_f2_validate(void* h, const srs_amd_pucch_f2_pdu* p, char* msg, unsigned msg_size)
 {

@@ -13,12 +13,15 @@ identical, on_uci called exactly when the PDU carries UCI.
 PDSCH: the plug-in (pdsch_processor::process per PDU on one resource_grid_writer) against the reference's
 pdsch_processor_impl on the same PDUs and initial grid: the grids bit-identical.
 """
+import os
 import time
 
 import numpy as np
 import pytest
 
 import srsran_project_amd as amd
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 from oracle import pusch_proc as pp
 
 pytestmark = pytest.mark.gpu
@@ -642,3 +645,28 @@ def test_pucch_plugin_vs_reference(phy):
 
     assert plug.validate_f2(amd.pucch.make_f2_pdu(nof_prb=2, nof_harq_ack=4, nof_csi_part2=3)) is not None
     assert plug.validate_f2(amd.pucch.make_f2_pdu(nof_prb=1, nof_symbols=1, nof_harq_ack=40)) is not None
+
+
+def test_pucch_plugin_latency(phy):
+    """Per-call latency of the synchronous pucch_processor::process through the plug-in (host reader grid and
+    device-resident grid; Format 0 and Format 2), written to gpurun_out/pucch_plugin_latency.json; a floor that only
+    catches a regression to per-row copies or extra synchronisations."""
+    import json
+
+    from tests import pucch_cases as pc
+
+    ophy, _ = phy
+    plug = ophy.PucchProcessorPlugin(device=0)
+    pdu0, grid0, _ = pc.cases(n=1, seed=21)[0]
+    pdu2, grid2, _ = pc.f2_cases(n=1, seed=22)[0]
+    nprb = pc.NSUBC // 12
+    out = {}
+    for name, g0, g2 in (("host_grid", ophy.Grid(grid0), ophy.Grid(grid2)),
+                         ("device_grid", ophy.DeviceGrid(grid0), ophy.DeviceGrid(grid2))):
+        plug.latency_us(g0, pdu0=pdu0, grid_prb=nprb, reps=20)
+        out[name] = dict(f0_us=round(plug.latency_us(g0, pdu0=pdu0, grid_prb=nprb), 1),
+                         f2_us=round(plug.latency_us(g2, pdu2=pdu2), 1))
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "pucch_plugin_latency.json"), "w") as f:
+        json.dump(out, f)
+    assert out["device_grid"]["f0_us"] < 1000 and out["host_grid"]["f2_us"] < 2000, out
