@@ -317,3 +317,54 @@ def test_pucch_f34_invalid_pdu_fails_loudly(proc):
     for kw in bad:
         with pytest.raises(ValueError):
             proc.process_f34(g, amd.pucch.make_f34_pdu(**kw))
+
+
+def test_pucch_every_format_sharing_one_grid(proc):
+    """Several PDUs of every format on disjoint PRBs of ONE grid, each format's slot form called once on it: every
+    result equals the compiled reference's for the same grid (the kernels read only their PDU's REs)."""
+    import torch
+
+    import srsran_project_amd as amd
+    from oracle import pucch as op
+    from tests import pucch_cases as pc
+
+    rng = np.random.default_rng(31)
+    grid = rng.integers(0, 1 << 32, (4, 14, pc.NSUBC), dtype=np.uint64).astype(np.uint32)
+    f0 = [amd.pucch.make_f0_pdu(numerology=1, slot_index=5, starting_prb=k, start_symbol_index=12, nof_symbols=2,
+                                initial_cyclic_shift=k, n_id=40 + k, nof_harq_ack=1 + k % 2, sr_opportunity=k % 3 == 0,
+                                ports=(0, 1)) for k in range(3)]
+    for k, p in enumerate(f0):
+        op.transmit(grid, p, op.TABLES[(p.nof_harq_ack, bool(p.sr_opportunity))][k % 2][0], [0.8, -0.5j], 0.05, rng)
+    f2 = [amd.pucch.make_f2_pdu(numerology=1, slot_index=5, bwp_size_rb=52, starting_prb=4 + 3 * k, nof_prb=3,
+                                start_symbol_index=12, nof_symbols=2, rnti=100 + k, n_id=7 + k, n_id_0=9 + k,
+                                nof_harq_ack=2, nof_csi_part1=10 + 8 * k, ports=(0, 1)) for k in range(3)]
+    pay2 = [rng.integers(0, 2, amd.pucch.payload_bits(p)).astype(np.uint8) for p in f2]
+    for p, y in zip(f2, pay2):
+        op.transmit_f2(grid, p, y, [0.9, 0.4 + 0.3j], 0.02, rng)
+    f34 = [amd.pucch.make_f34_pdu(format=3, numerology=1, slot_index=5, bwp_size_rb=52, starting_prb=20 + 4 * k,
+                                  nof_prb=4, start_symbol_index=0, nof_symbols=12, rnti=200 + k, n_id_hopping=3 + k,
+                                  n_id_scrambling=5 + k, nof_harq_ack=3, nof_csi_part1=20 * (k + 1), ports=(0, 1))
+           for k in range(2)]
+    f34.append(amd.pucch.make_f34_pdu(format=4, numerology=1, slot_index=5, bwp_size_rb=52, starting_prb=30,
+                                      start_symbol_index=0, nof_symbols=12, rnti=300, n_id_hopping=8,
+                                      n_id_scrambling=9, nof_harq_ack=4, occ_index=1, occ_length=2, ports=(0, 1)))
+    pay34 = [rng.integers(0, 2, amd.pucch.payload_bits(p)).astype(np.uint8) for p in f34]
+    for p, y in zip(f34, pay34):
+        op.transmit_f34(grid, p, y, [0.7j, 0.6], 0.02, rng)
+    d = torch.from_numpy(grid[None].view(np.int32).copy()).to("cuda:0")
+    r0 = amd.pucch.parse_results(proc.detect_f0_slot(d, f0).cpu().numpy())
+    res2, p2 = proc.process_f2_slot(d, f2)
+    res34, p34 = proc.process_f34_slot(d, f34)
+    torch.cuda.synchronize()
+    r2, p2 = amd.pucch.parse_uci_results(res2.cpu().numpy()), p2.cpu().numpy()
+    r34, p34 = amd.pucch.parse_uci_results(res34.cpu().numpy()), p34.cpu().numpy()
+    for k, p in enumerate(f0):
+        _check(k, r0[k], op.ref_detect(grid, p))
+    for k, p in enumerate(f2):
+        want, want_pay = op.ref_process_f2(grid, p)
+        _check_uci(k, r2[k], p2[k, :amd.pucch.payload_bits(p)], want, want_pay)
+        assert want.status == 1 and np.array_equal(want_pay, pay2[k]), k
+    for k, p in enumerate(f34):
+        want, want_pay = op.ref_process_f34(grid, p)
+        _check_uci(k, r34[k], p34[k, :amd.pucch.payload_bits(p)], want, want_pay)
+        assert want.status == 1 and np.array_equal(want_pay, pay34[k]), k
