@@ -51,7 +51,17 @@ __global__ __launch_bounds__(64) void pucch_f0_kernel(const pucch_f0_desc* desc,
   const pucch_f0_desc& d = desc[blockIdx.x];
   __shared__ float2    re[2][4][12];
   __shared__ float     s_metric[PUCCH_F0_MAX_CAND], s_corr[PUCCH_F0_MAX_CAND];
+  __shared__ float2    s_seq[PUCCH_F0_MAX_CAND][2][12];
   const uint32_t       t = threadIdx.x;
+  // the candidates' sequences: base times e^(j 2 pi alpha k / 12) (the twelfth roots from double precision)
+  for (uint32_t i = t; i < d.nof_cand * d.nsym * 12; i += 64) {
+    const uint32_t c = i / (d.nsym * 12), l = (i / 12) % d.nsym, k = i % 12;
+    double         sn, cs;
+    sincospi(static_cast<double>((d.alpha[c][l] * k) % 12) / 6.0, &sn, &cs);
+    const float2 e = make_float2(static_cast<float>(cs), static_cast<float>(sn));
+    const float2 b = d.base[k];
+    s_seq[c][l][k] = make_float2(b.x * e.x - b.y * e.y, b.x * e.y + b.y * e.x);
+  }
   for (uint32_t i = t; i < d.nsym * d.nof_ports * 12; i += 64) {
     const uint32_t l = i / (d.nof_ports * 12), p = (i / 12) % d.nof_ports, k = i % 12;
     re[l][p][k] = from_cbf16(d.grid[static_cast<uint64_t>(d.ports[p]) * d.port_stride +
@@ -72,7 +82,7 @@ __global__ __launch_bounds__(64) void pucch_f0_kernel(const pucch_f0_desc* desc,
       for (uint32_t p = 0; p != d.nof_ports; ++p) {
         float2 c = make_float2(0.0f, 0.0f);
         for (uint32_t k = 0; k != 12; ++k) { // rx conj(seq)
-          const float2 x = re[l][p][k], y = d.seq[t][l][k];
+          const float2 x = re[l][p][k], y = s_seq[t][l][k];
           c.x += x.x * y.x + x.y * y.y;
           c.y += x.y * y.x - x.x * y.y;
         }

@@ -147,13 +147,21 @@ void gold_bits(const std::vector<uint32_t>& jump, uint32_t c_init, uint32_t n0, 
       x2 = gf2_apply_h(jump.data() + (1 * PRBS_NJUMP + k) * 31, x2);
     }
   }
-  std::memset(out, 0, sizeof(uint32_t) * ((nbits + 31) / 32));
-  for (uint32_t m = 0; m != nbits; ++m) {
-    out[m / 32] |= ((x1 ^ x2) & 1u) << (m % 32);
-    const uint32_t n1 = ((x1 >> 3) ^ x1) & 1u;
-    const uint32_t n2 = ((x2 >> 3) ^ (x2 >> 2) ^ (x2 >> 1) ^ x2) & 1u;
-    x1                = (x1 >> 1) | (n1 << 30);
-    x2                = (x2 >> 1) | (n2 << 30);
+  // 32 outputs per step, word-parallel (the host twin of gold_sequence.h gold_next32): bit b of word w = c(n0 + 32 w + b)
+  const uint32_t nwords = (nbits + 31) / 32;
+  for (uint32_t w = 0; w != nwords; ++w) {
+    uint64_t a = x1;
+    a |= static_cast<uint64_t>(((a >> 3) ^ a) & 0x0fffffffu) << 31;
+    a |= static_cast<uint64_t>(((a >> 31) ^ (a >> 28)) & 0xfu) << 59;
+    uint64_t b = x2;
+    b |= static_cast<uint64_t>(((b >> 3) ^ (b >> 2) ^ (b >> 1) ^ b) & 0x0fffffffu) << 31;
+    b |= static_cast<uint64_t>(((b >> 31) ^ (b >> 30) ^ (b >> 29) ^ (b >> 28)) & 0xfu) << 59;
+    x1     = static_cast<uint32_t>(a >> 32) & 0x7fffffffu;
+    x2     = static_cast<uint32_t>(b >> 32) & 0x7fffffffu;
+    out[w] = static_cast<uint32_t>(a ^ b);
+  }
+  if (nbits % 32 != 0) {
+    out[nwords - 1] &= (1u << (nbits % 32)) - 1u;
   }
 }
 
@@ -691,18 +699,15 @@ int make_desc(const srs_amd_pucch_processor* proc, const srs_amd_pucch_f0_pdu& p
   for (uint32_t l = 0; l != p.nof_symbols; ++l) {
     n_cs[l] = gold_byte(proc->jump, p.n_id, 8 * (NSYMB * p.slot_index + p.start_symbol_index + l));
   }
-  const float2* ph = twelfth_roots();
+  for (uint32_t k = 0; k != 12; ++k) {
+    d.base[k] = make_float2(base[2 * k], base[2 * k + 1]);
+  }
   for (uint32_t c = 0; c != n; ++c) {
     d.msg[c][0] = tab[c].sr;
     d.msg[c][1] = tab[c].h0;
     d.msg[c][2] = tab[c].h1;
     for (uint32_t l = 0; l != p.nof_symbols; ++l) {
-      const uint32_t alpha = (p.initial_cyclic_shift + tab[c].m_cs + n_cs[l]) % 12;
-      for (uint32_t k = 0; k != 12; ++k) {
-        const float2 e = ph[(alpha * k) % 12];
-        const float  br = base[2 * k], bi = base[2 * k + 1];
-        d.seq[c][l][k] = make_float2(br * e.x - bi * e.y, br * e.y + bi * e.x);
-      }
+      d.alpha[c][l] = static_cast<uint8_t>((p.initial_cyclic_shift + tab[c].m_cs + n_cs[l]) % 12);
     }
   }
   return SRS_AMD_OK;

@@ -25,7 +25,8 @@ struct pucch_f0_desc {
   uint32_t        nof_sr_default;   // of the default (invalid) message: the SR opportunity
   float           threshold;   // pick_threshold(ports, symbols, candidates)
   uint8_t         msg[PUCCH_F0_MAX_CAND][3]; // SR, HARQ-ACK 0, HARQ-ACK 1 of each candidate (table order)
-  float2          seq[PUCCH_F0_MAX_CAND][2][12]; // the low-PAPR sequence of each candidate and symbol
+  uint8_t         alpha[PUCCH_F0_MAX_CAND][2]; // cyclic shift (m0 + m_cs + n_cs) mod 12 of each candidate and symbol
+  float2          base[12];    // low-PAPR base sequence of group n_id mod 30
 };
 
 // Detection of every PDU (one 64-thread workgroup per PDU), results into d_results.
