@@ -186,9 +186,13 @@ __global__ __launch_bounds__(64 * WAVES) void polar_decode_kernel(polar_args own
   }
   wave_sync();
 
-  // ---- SSC program
+  // ---- SSC program (the next operation's word is loaded one step ahead, behind the current step's LDS work)
+  uint32_t next = a.prog_len != 0 ? a.program[0] : 0u;
   for (uint32_t o = 0; o < a.prog_len; ++o) {
-    const uint32_t op   = a.program[o];
+    const uint32_t op = next;
+    if (o + 1 < a.prog_len) {
+      next = a.program[o + 1];
+    }
     const int      type = op & 3;
     const int      s    = (op >> 2) & 63;
     const int      p    = op >> 8;
