@@ -458,3 +458,100 @@ def ref_demodulate_f34(grid, pdu):
     ref.srs_ref_pucch_f34_demodulate(g.ctypes.data, g.shape[0], g.shape[2], ctypes.addressof(pdu), llr.ctypes.data,
                                      llr.size)
     return llr
+
+
+def _bf16c(x):
+    """complex64 rounded to complex bf16 (and back), as the reference's estimate grid stores it."""
+    from .pdsch_mod import to_bf16
+
+    x = np.asarray(x, np.complex64)
+    r = (to_bf16(x.real).astype(np.uint32) << 16).view(np.float32)
+    i = (to_bf16(x.imag).astype(np.uint32) << 16).view(np.float32)
+    return (r + 1j * i).astype(np.complex64)
+
+
+def demodulate_f2(grid, pdu):
+    """Numpy restatement of dmrs_pucch_estimator_format2 (dmrs_pucch_estimator_format2.cpp:87-130 over
+    port_channel_estimator_average_impl.cpp:122-409 with the FD filter, TD averaging and CFO compensation: the LSE,
+    the CFO between the two DM-RS symbols of a hop and its compensation, the filter with virtual pilots, the linear
+    interpolation from REs 1, 4, 7, 10, the bf16 estimate grid, the noise from the pilots minus their reconstruction)
+    and pucch_demodulator_format2 (pucch_demodulator_format2.cpp:92-160: ZF, QPSK soft demapping, descrambling with
+    c_init = rnti 2^15 + n_id) -> int8 LLRs.  The time alignment (CSI only) is not restated."""
+    from . import demodulate
+    from .chest import fd_smoothing, interpolate, symbol_start_epochs
+    from .equalizer import equalize
+
+    nprb, nsym = pdu.nof_prb, pdu.nof_symbols
+    hop = pdu.second_hop_prb >= 0
+    epochs = symbol_start_epochs(pdu.numerology)
+    npil = 4 * nprb
+    prbs_of = [pdu.bwp_start_rb + (pdu.second_hop_prb if (hop and s > 0) else pdu.starting_prb) for s in range(nsym)]
+    pilot_re = np.array([12 * (i // 4) + 1 + 3 * (i % 4) for i in range(npil)])
+    data_re = f2_data_res(nprb)
+    ports = [pdu.ports[k] for k in range(pdu.nof_ports)]
+
+    def row(p, s):
+        u = grid[p, pdu.start_symbol_index + s, 12 * prbs_of[s]:12 * prbs_of[s] + 12 * nprb].astype(np.uint32)
+        return ((u << 16).view(np.float32) + 1j * (u & 0xFFFF0000).view(np.float32)).astype(np.complex64)
+
+    est, nvar = {}, []
+    for p in ports:
+        rsrp, noise, cfo = np.float32(0), np.float32(0), None
+        hops = [[0], [1]] if hop else [list(range(nsym))]
+        e_p = {}
+        for syms in hops:
+            rx = [row(p, s)[pilot_re] for s in syms]
+            pil = [f2_pilots(pdu, s) for s in syms]
+            lse = (rx[0] * np.conj(pil[0])).astype(np.complex64)
+            cfo_h = None
+            if len(syms) == 2:
+                prod1 = (rx[1] * np.conj(pil[1])).astype(np.complex64)
+                z = np.sum(prod1.astype(np.complex128) * np.conj(lse.astype(np.complex128)))
+                e0, e1 = float(epochs[pdu.start_symbol_index]), float(epochs[pdu.start_symbol_index + 1])
+                cfo_h = np.float32(np.angle(z) / (2 * np.pi) / (e1 - e0))
+                cfo = cfo_h
+                lse = (lse * np.exp(-2j * np.pi * e0 * float(cfo_h)) + prod1 * np.exp(-2j * np.pi * e1 * float(cfo_h)))
+                lse = lse.astype(np.complex64)
+            lse = (lse / np.float32(len(syms))).astype(np.complex64)
+            f = fd_smoothing(lse, nprb, 3, 2)
+            rsrp = np.float32(rsrp + np.float32(np.sum(np.abs(f.astype(np.complex128)) ** 2)) * np.float32(len(syms)))
+            freq = _bf16c(interpolate(f, 12 * nprb, 1, 3))
+            for s in syms:
+                e_p[s] = freq
+            energy = 0.0
+            for k, s in enumerate(syms):
+                pred = f.astype(np.complex128) * pil[k]
+                if cfo_h is not None:
+                    pred = pred * np.exp(2j * np.pi * float(epochs[pdu.start_symbol_index + s]) * float(cfo_h))
+                energy += float(np.sum(np.abs(rx[k] - pred) ** 2))
+            noise = np.float32(noise + (np.float32(energy) if np.isfinite(energy) and energy > 0 else 0))
+        rsrp = np.float32(rsrp / np.float32(npil * nsym))
+        noise = np.float32(noise / np.float32(npil * nsym - 1))
+        noise = max(np.float32(rsrp / np.float32(1e10)), noise)
+        if cfo is not None:
+            for s in range(nsym):
+                e_p[s] = _bf16c(e_p[s] * np.exp(2j * np.pi * float(epochs[pdu.start_symbol_index + s]) * float(cfo)))
+        est[p] = e_p
+        nvar.append(noise)
+    eq_all, nv_all = [], []
+    for s in range(nsym):
+        y = np.stack([grid[p, pdu.start_symbol_index + s, 12 * prbs_of[s]:12 * prbs_of[s] + 12 * nprb][data_re]
+                      for p in ports]).astype(np.uint32)
+        h = np.stack([est[p][s][data_re] for p in ports])
+        hu = (np.asarray(_to_u32(h), np.uint32))
+        eq, nv = equalize(y.view(np.uint16), hu[None].view(np.uint16), np.array(nvar, np.float32), 1.0, 1)
+        eq_all.append(eq[:, 0])
+        nv_all.append(nv[:, 0])
+    eq = np.concatenate(eq_all).astype(np.complex64)
+    nv = np.concatenate(nv_all).astype(np.float32)
+    llr = demodulate(eq, nv, 2)
+    E = llr.size
+    c = prbs(pdu.rnti * (1 << 15) + pdu.n_id, E)
+    return np.where(c != 0, -llr.astype(np.int16), llr.astype(np.int16)).astype(np.int8)
+
+
+def _to_u32(x):
+    from .pdsch_mod import to_bf16
+
+    x = np.asarray(x, np.complex64)
+    return to_bf16(x.real).astype(np.uint32) | (to_bf16(x.imag).astype(np.uint32) << 16)

@@ -592,3 +592,18 @@ def test_pucch_f34_transmitter_decoded_by_reference():
         assert r.status == 1 and np.array_equal(pay, payload), (i, pdu.format, pdu.nof_prb, pdu.pi2_bpsk, r.status)
         n += 1
     assert n == 6
+
+
+def test_pucch_f2_restatement_llrs_match_reference():
+    """oracle/pucch.py demodulate_f2 (estimator + demodulator restated in numpy) against the compiled
+    dmrs_pucch_estimator_format2 + pucch_demodulator_format2: every LLR within one quantisation step, >= 98 % equal
+    (the restatement accumulates in float64 where the reference sums in float)."""
+    from oracle import pucch as op
+    from tests.pucch_cases import f2_cases
+
+    for i, (pdu, grid, _) in enumerate(f2_cases(n=12, seed=1)):
+        want = op.ref_demodulate_f2(grid, pdu).astype(np.int32)
+        got = op.demodulate_f2(grid, pdu).astype(np.int32)
+        diff = np.abs(got - want)
+        assert diff.max() <= 1, (i, int(diff.max()), int(np.argmax(diff)))
+        assert np.mean(diff == 0) >= 0.98, (i, float(np.mean(diff == 0)))
