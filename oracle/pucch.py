@@ -555,3 +555,84 @@ def _to_u32(x):
 
     x = np.asarray(x, np.complex64)
     return to_bf16(x.real).astype(np.uint32) | (to_bf16(x.imag).astype(np.uint32) << 16)
+
+
+def demodulate_f34(grid, pdu):
+    """Numpy restatement of dmrs_pucch_estimator_formats3_4 (all 12 REs of a PRB on the DM-RS symbols, the port
+    estimator with the FD filter and TD averaging, the CFO not compensated) and pucch_demodulator_format3 / 4
+    (pucch_formats3_4_helpers.h pucch_3_4_extract_and_equalize: ZF per data symbol, transform deprecoding with the
+    mean noise; Format 4's inverse_blockwise_spreading, pucch_demodulator_format4.cpp:113-130; soft demapping,
+    descrambling with c_init = rnti 2^15 + n_id) -> int8 LLRs."""
+    from srsran_project_amd.pucch import f34_dmrs_mask, f34_nof_llrs
+
+    from . import demodulate
+    from .chest import fd_smoothing
+    from .equalizer import equalize
+
+    f4 = pdu.format == 4
+    nprb = 1 if f4 else pdu.nof_prb
+    M, nsym = 12 * nprb, pdu.nof_symbols
+    hop = pdu.second_hop_prb >= 0
+    mask = f34_dmrs_mask(nsym, hop, pdu.additional_dmrs)
+    hop_sym = nsym // 2 if hop else nsym
+    prbs_of = [pdu.bwp_start_rb + (pdu.second_hop_prb if (hop and s >= hop_sym) else pdu.starting_prb)
+               for s in range(nsym)]
+    ports = [pdu.ports[k] for k in range(pdu.nof_ports)]
+
+    def row(p, s):
+        u = grid[p, pdu.start_symbol_index + s, 12 * prbs_of[s]:12 * prbs_of[s] + M].astype(np.uint32)
+        return ((u << 16).view(np.float32) + 1j * (u & 0xFFFF0000).view(np.float32)).astype(np.complex64)
+
+    hops = [list(range(hop_sym)), list(range(hop_sym, nsym))] if hop else [list(range(nsym))]
+    est, nvar = {}, []
+    for p in ports:
+        rsrp, noise, e_p = np.float32(0), np.float32(0), {}
+        for hs in hops:
+            syms = [s for s in hs if s in mask]
+            rx = [row(p, s) for s in syms]
+            pil = [f34_pilots(pdu, s) for s in syms]
+            lse = np.zeros(M, np.complex64)
+            for k in range(len(syms)):
+                lse = (lse + rx[k] * np.conj(pil[k])).astype(np.complex64)
+            lse = (lse / np.float32(len(syms))).astype(np.complex64)
+            f = fd_smoothing(lse, nprb, 1, 2)
+            rsrp = np.float32(rsrp + np.float32(np.sum(np.abs(f.astype(np.complex128)) ** 2)) * np.float32(len(syms)))
+            for s in hs:
+                e_p[s] = _bf16c(f)
+            energy = sum(float(np.sum(np.abs(rx[k] - f.astype(np.complex128) * pil[k]) ** 2)) for k in range(len(syms)))
+            noise = np.float32(noise + (np.float32(energy) if np.isfinite(energy) and energy > 0 else 0))
+        nd = len(mask)
+        rsrp = np.float32(rsrp / np.float32(M * nd))
+        noise = np.float32(noise / np.float32(M * nd - 1))
+        est[p] = e_p
+        nvar.append(max(np.float32(rsrp / np.float32(1e10)), noise))
+    xs, nvs = [], []
+    for s in range(nsym):
+        if s in mask:
+            continue
+        y = np.stack([grid[p, pdu.start_symbol_index + s, 12 * prbs_of[s]:12 * prbs_of[s] + M] for p in ports])
+        hu = np.stack([_to_u32(est[p][s]) for p in ports]).astype(np.uint32)
+        eq, nv = equalize(y.astype(np.uint32).view(np.uint16), hu[None].view(np.uint16), np.array(nvar, np.float32),
+                          1.0, 1)
+        x = np.fft.ifft(eq[:, 0].astype(np.complex64)) * M / np.float32(np.sqrt(M))
+        v = nv[:, 0].astype(np.float32)
+        ok = (v > 0) & np.isfinite(v)
+        v = np.where(ok, np.float32(np.sum(v[ok]) / max(int(np.sum(ok)), 1)) if ok.any() else v, v)
+        xs.append(x.astype(np.complex64))
+        nvs.append(v.astype(np.float32))
+    x, nv = np.concatenate(xs), np.concatenate(nvs)
+    if f4:
+        mod = 12 // pdu.occ_length
+        w = np.asarray(F4_OCC[pdu.occ_length][pdu.occ_index], np.complex64)
+        L = x.size // 12
+        orig = np.zeros(L * mod, np.complex64)
+        onv = np.zeros(L * mod, np.float32)
+        for k in range(12):
+            for l in range(L):
+                orig[l * mod + k % mod] += x[l * 12 + k] / w[k]
+                onv[l * mod + k % mod] += nv[l * 12 + k]
+        x, nv = (orig / np.float32(pdu.occ_length)).astype(np.complex64), onv
+    llr = demodulate(x, nv, 0 if pdu.pi2_bpsk else 2)
+    assert llr.size == f34_nof_llrs(pdu)
+    c = prbs(pdu.rnti * (1 << 15) + pdu.n_id_scrambling, llr.size)
+    return np.where(c != 0, -llr.astype(np.int16), llr.astype(np.int16)).astype(np.int8)

@@ -607,3 +607,17 @@ def test_pucch_f2_restatement_llrs_match_reference():
         diff = np.abs(got - want)
         assert diff.max() <= 1, (i, int(diff.max()), int(np.argmax(diff)))
         assert np.mean(diff == 0) >= 0.98, (i, float(np.mean(diff == 0)))
+
+
+def test_pucch_f34_restatement_llrs_match_reference():
+    """oracle/pucch.py demodulate_f34 against the compiled dmrs_pucch_estimator_formats3_4 +
+    pucch_demodulator_format3 / 4: every LLR within one quantisation step, >= 98 % equal."""
+    from oracle import pucch as op
+    from tests.pucch_cases import f34_cases
+
+    for i, (pdu, grid, _) in enumerate(f34_cases(n=12, seed=1)):
+        want = op.ref_demodulate_f34(grid, pdu).astype(np.int32)
+        got = op.demodulate_f34(grid, pdu).astype(np.int32)
+        diff = np.abs(got - want)
+        assert diff.max() <= 1, (i, pdu.format, pdu.pi2_bpsk, int(diff.max()), int(np.argmax(diff)))
+        assert np.mean(diff == 0) >= 0.98, (i, float(np.mean(diff == 0)))
