@@ -1132,20 +1132,23 @@ constexpr int fr_sign_bit(int e)
 #define FR_KEEP_ADDR 19
 #endif
 
-struct fr_state {
-  uint32_t w[FR_STATE_WORDS];
+// compressed message state of the first NW / (2 or 3) layers (all 46: fr_state)
+template <int NW>
+struct fr_state_n {
+  uint32_t w[NW];
   __device__ __forceinline__ void zero()
   {
 #pragma unroll
-    for (int i = 0; i < FR_STATE_WORDS; ++i) {
+    for (int i = 0; i < NW; ++i) {
       w[i] = 0;
     }
   }
 };
+using fr_state = fr_state_n<FR_STATE_WORDS>;
 
 // One layer (BG1 row L) for the row pair of lane t, messages rebuilt from / folded into the compressed state.
-template <int L, int ARITH, int... E>
-__device__ __forceinline__ void fr_layer(lds_i8* lds, fr_state& st, uint32_t t, std::integer_sequence<int, E...>)
+template <int L, int ARITH, typename ST, int... E>
+__device__ __forceinline__ void fr_layer(lds_i8* lds, ST& st, uint32_t t, std::integer_sequence<int, E...>)
 {
   constexpr int  E0  = row_start<1>(L);
   constexpr int  DEG = sizeof...(E);
@@ -1241,10 +1244,10 @@ __device__ __forceinline__ void fr_layer(lds_i8* lds, fr_state& st, uint32_t t, 
   }
 }
 
-template <int L, int ARITH>
-__device__ __forceinline__ void fr_layers(lds_i8* lds, fr_state& st, uint32_t t, int nof_layers)
+template <int L, int ARITH, int MAXL, typename ST>
+__device__ __forceinline__ void fr_layers(lds_i8* lds, ST& st, uint32_t t, int nof_layers)
 {
-  if constexpr (L < bg_traits<1>::M) {
+  if constexpr (L < MAXL) {
     // laundered per layer: otherwise the 42 layer conditions are hoisted out of the iteration loop as 64-bit
     // lane masks (84 SGPRs, spilled)
     asm volatile("" : "+s"(nof_layers));
@@ -1253,7 +1256,7 @@ __device__ __forceinline__ void fr_layers(lds_i8* lds, fr_state& st, uint32_t t,
       fr_layer<L, ARITH>(lds, st, t, std::make_integer_sequence<int, bg_traits<1>::deg(L)>{});
       __syncthreads();
     }
-    fr_layers<L + 1, ARITH>(lds, st, t, nof_layers);
+    fr_layers<L + 1, ARITH, MAXL>(lds, st, t, nof_layers);
   }
 }
 
@@ -1265,10 +1268,22 @@ __device__ __forceinline__ void fr_layers(lds_i8* lds, fr_state& st, uint32_t t,
 #ifndef FR_WAVES
 #define FR_WAVES 3
 #endif
+// HR_CMP: the high-rate kernel holds its MAXL layers' messages compressed (fr_layer) instead of as int16 pairs
+#ifndef HR_CMP
+#define HR_CMP 0
+#endif
+// HR_OLD_LOAD: the codeword-fed load deinterleaves raw bytes and clamps / completes / scans the row in a second pass
+// (r05 form, kept for A/B)
+#ifndef HR_OLD_LOAD
+#define HR_OLD_LOAD 0
+#endif
+#ifndef HR_CMP_WAVES
+#define HR_CMP_WAVES 8
+#endif
 template <int NP, int MAXL>
 constexpr int hr_waves_per_simd()
 {
-  return MAXL == bg_traits<1>::M ? FR_WAVES : (NP == 1 ? HR_WAVES : 2);
+  return MAXL == bg_traits<1>::M ? FR_WAVES : (NP == 1 ? (HR_CMP ? HR_CMP_WAVES : HR_WAVES) : 2);
 }
 
 // threadIdx.x rebuilt from the wave's first thread (wave-uniform) and the lane id: opaque (volatile), so it is
@@ -1286,6 +1301,7 @@ template <int ARITH, int MAXL, int NP>
 __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>())) ldpc_decode_hr_kernel(decode_args a)
 {
   constexpr bool FULL   = MAXL == bg_traits<1>::M;
+  constexpr bool CMP    = FULL || (HR_CMP && NP == 1); // compressed message state
   static_assert(!FULL || NP == 1, "full-length codeblocks: one row pair per lane");
   constexpr int Z       = HR_Z;
   constexpr int K       = 22 * Z;
@@ -1338,6 +1354,95 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
       const uint32_t ninfo = a.cw_nof_info;
       const uint32_t F     = a.cw_filler;
       lds_i8*        row   = soft + 2 * Z;
+      if (Qm == 8 && ((reinterpret_cast<uintptr_t>(src) & 7u) == 0) && n_llrs % Z == 0 && !HR_OLD_LOAD) {
+        // Whole nodes only (the fused launches' prefix is whole nodes): every byte of the row is a full-node soft
+        // bit, clamped to +-SOFT_CLAMP as it is stored, so the row needs no second pass.  Fillers (+infinity)
+        // are stored as +SOFT_CLAMP and the bytes from E + F on as zeros (disjoint from the deinterleaved bytes,
+        // so one barrier covers all three).  Clamp of a byte pair: offset binary (b ^ 0x80), each byte into the
+        // low byte of a 16-bit half by one v_perm_b32, v_pk_max_u16 / v_pk_min_u16 against 128 -+ SOFT_CLAMP,
+        // back by ^ 0x80; the two halves go out with ds_write_b8 / ds_write_b8_d16_hi.
+        const uint32_t lane = t & 63u;
+        for (uint32_t i = t; i < Kq; i += NT) {
+          const uint2    v  = reinterpret_cast<const uint2*>(src)[i];
+          const uint32_t ox = v.x ^ 0x80808080u, oy = v.y ^ 0x80808080u;
+          uint32_t       q[4];
+          // [b0 | b1], [b2 | b3] of x, then of y: selector bytes 0-3 pick S1 (= the second operand), 12 gives 0x00
+          q[0] = __builtin_amdgcn_perm(0u, ox, 0x0c010c00u);
+          q[1] = __builtin_amdgcn_perm(0u, ox, 0x0c030c02u);
+          q[2] = __builtin_amdgcn_perm(0u, oy, 0x0c010c00u);
+          q[3] = __builtin_amdgcn_perm(0u, oy, 0x0c030c02u);
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const pku16 u = __builtin_elementwise_min(
+                __builtin_elementwise_max(__builtin_bit_cast(pku16, q[h]), pku16{128 - SOFT_CLAMP, 128 - SOFT_CLAMP}),
+                pku16{128 + SOFT_CLAMP, 128 + SOFT_CLAMP});
+            q[h] = __builtin_bit_cast(uint32_t, u) ^ 0x00800080u;
+          }
+          // the wave's first symbol index (uniform): the row position of bit j is d = j Kq + i, moved past the
+          // filler block when d >= ninfo -- uniform for the whole wave except in at most one (wave, j)
+          const uint32_t iw = __builtin_amdgcn_readfirstlane(i - lane);
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t lo = j * Kq + iw;
+            uint32_t       p  = j * Kq + i;
+            if (lo >= ninfo) {
+              p += F;
+            } else if (lo + 63 >= ninfo) {
+              p = p < ninfo ? p : p + F;
+            }
+            const uint32_t w = q[j >> 1];
+            if ((j & 1u) == 0) {
+              row[p] = static_cast<int8_t>(w);
+            } else {
+              row[p] = static_cast<int8_t>(w >> 16);
+            }
+          }
+        }
+        for (uint32_t p = ninfo + t; p < ninfo + F; p += NT) {
+          row[p] = static_cast<int8_t>(SOFT_CLAMP);
+        }
+        {
+          // zeros from E + F to the end of the row: the bytes up to the next word boundary, then words
+          constexpr uint32_t ROW = (NODES - 2) * Z;
+          const uint32_t     e0  = E + F;
+          const uint32_t     w0  = (e0 + 3u) & ~3u;
+          if (t < w0 - e0) {
+            row[e0 + t] = 0;
+          }
+          lds_i32* row4 = soft4 + (2 * Z) / 4;
+          for (uint32_t w = w0 / 4 + t; w < ROW / 4; w += NT) {
+            row4[w] = 0;
+          }
+        }
+        for (int w = t; w < 2 * Z / 4; w += NT) {
+          soft4[w] = 0;
+        }
+        __syncthreads();
+        if (FULL || a.force_decoding) {
+          // last non-zero soft bit (only the layer count of a full-length row and force_decoding read it; a clamp
+          // keeps zero and non-zero bytes apart, fillers are non-zero)
+          const int nw   = n_llrs >> 2;
+          int       last = -1;
+          for (int w = static_cast<int>(t); w < nw; w += NT) {
+            const uint32_t v = static_cast<uint32_t>(soft4[(2 * Z) / 4 + w]);
+            if (v != 0) {
+              last = 4 * w + (31 - __builtin_clz(v)) / 8;
+            }
+          }
+          if constexpr (NT == 64) {
+            input_size = __builtin_amdgcn_readfirstlane(wave_max(last) + 1);
+          } else {
+            if (last >= 0) {
+              __hip_atomic_fetch_max(&red[0], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            __syncthreads();
+            input_size = __builtin_amdgcn_readfirstlane(red[0] + 1);
+          }
+        } else {
+          // MAXL layers whatever the last non-zero position (<= (NODES - 2) Z): cb_len below gives MAXL
+          input_size = n_llrs;
+        }
+      } else {
       if (Qm == 8 && ((reinterpret_cast<uintptr_t>(src) & 7u) == 0)) {
         for (uint32_t i = t; i < Kq; i += NT) {
           const uint2 v = reinterpret_cast<const uint2*>(src)[i];
@@ -1399,6 +1504,7 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
         }
         __syncthreads();
         input_size = __builtin_amdgcn_readfirstlane(red[0] + 1);
+      }
       }
     } else {
       const int      nw  = n_llrs >> 2;
@@ -1472,12 +1578,12 @@ __global__ void __launch_bounds__(HR_HALF / NP, (hr_waves_per_simd<NP, MAXL>()))
     const int nof_sig    = __builtin_amdgcn_readfirstlane(K - (a.fillers ? a.fillers[cb] : a.nof_filler_bits));
     int       result     = -1;
 
-    std::conditional_t<FULL, fr_state, hr_msgs<NE>> c2v;
+    std::conditional_t<CMP, fr_state_n<fr_off(MAXL)>, hr_msgs<NE>> c2v;
     c2v.zero();
 
     for (int it = 0; it < a.max_iterations; ++it) {
-      if constexpr (FULL) {
-        fr_layers<0, ARITH>(lds, c2v, t, nof_layers);
+      if constexpr (CMP) {
+        fr_layers<0, ARITH, MAXL>(lds, c2v, t, nof_layers);
       } else {
         hr_layers<0, MAXL, ARITH, NP>(lds, c2v, t, nof_layers);
       }
