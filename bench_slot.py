@@ -167,6 +167,7 @@ class SlotPipeline:
         self.kinds = []              # UL PDU kinds (mixed: "uci", "harq", "tp" or "data")
         self.tp_ues = []             # DFT-s-OFDM UEs: (cell, first PRB, end PRB, channel [port], n_rs_id)
         self.ul_pdus = []            # the UL PDUs (UCI UEs multiplex their UCI REs at the transmitter)
+        self.uci_sent = {}           # CSI part 1 / CSI part 2 payloads of the "csi2" / "ucionly" UEs, by UL PDU index
         for c in range(cells):
             n_id = int(rng.integers(0, 1008))
             for side in ("dl", "ul"):
@@ -195,12 +196,17 @@ class SlotPipeline:
                         j = len(ul)
                         kind = "data"
                         if mixed:
-                            # ~20 % HARQ-ACK + CSI part 1 on the UL-SCH, ~10 % retransmissions (new_data = 0,
-                            # combined into a soft buffer; rv 0, decodable alone from the cleared buffer), ~3 %
-                            # DFT-s-OFDM
-                            kind = ("tp" if j % 32 == 17 else "uci" if j % 5 == 1 else "harq" if j % 10 == 3
-                                    else "data")
-                        layers = 1 if kind in ("tp", "uci") else int(rng.integers(1, ul_max_layers + 1))
+                            # ~20 % HARQ-ACK + CSI part 1 on the UL-SCH, ~6 % CSI part 1 + CSI part 2 (its size from
+                            # the CSI part 1 payload) on the UL-SCH, ~3 % UCI-only PUSCH (CSI part 1 + CSI part 2, no
+                            # codeword), ~10 % retransmissions (new_data = 0, combined into a soft buffer; rv 0,
+                            # decodable alone from the cleared buffer), ~3 % DFT-s-OFDM
+                            kind = ("tp" if j % 32 == 17 else "ucionly" if j % 32 == 9 else "csi2" if j % 16 == 7
+                                    else "uci" if j % 5 == 1 else "harq" if j % 10 == 3 else "data")
+                        layers = 1 if kind in ("tp", "uci", "csi2", "ucionly") else int(rng.integers(1, ul_max_layers + 1))
+                        if kind == "ucionly":
+                            # one polar codeword per UCI field: a narrow allocation (E <= 8192)
+                            hi = lo + min(hi - lo, 6)
+                            crbs = list(range(lo, hi))
                         if kind == "tp":
                             n = hi - lo
                             while not amd.transform_precoding_nof_prbs_valid(n):
@@ -213,8 +219,14 @@ class SlotPipeline:
                                          beta_offset_csi_part1=6.25, alpha_scaling=1.0)
                         if kind == "tp":
                             extra = dict(transform_precoding=1, n_rs_id=n_id)
+                        if kind in ("csi2", "ucionly"):
+                            # (UCI-only PUSCH carries no CSI part 2: the reference sizes CSI part 1 of a UCI-only PDU
+                            # for "no CSI part 2" before CSI part 2 is known, ulsch_info.cpp:96-123)
+                            extra = dict(nof_csi_part1=CSI1_BITS, beta_offset_csi_part1=6.25, alpha_scaling=1.0)
+                            if kind == "csi2":
+                                extra.update(beta_offset_csi_part2=5.0, csi_part2_size=PART2)
                         rv, new_data = (0, 0) if kind == "harq" else (0, 1)
-                        tbs = amd.tbs_calculator_calculate(14, 24, 0, qm, r, layers, 0, hi - lo)
+                        tbs = 0 if kind == "ucionly" else amd.tbs_calculator_calculate(14, 24, 0, qm, r, layers, 0, hi - lo)
                         pdu = amd.make_pdu(numerology=bp.MU, slot_index=bp.SLOT, rnti=rnti, bwp_start_rb=0,
                                            bwp_size_rb=NOF_PRB, modulation=qm, target_code_rate=r, rv=rv,
                                            base_graph=base_graph(tbs, r / 1024), new_data=new_data, n_id=n_id,
@@ -229,7 +241,7 @@ class SlotPipeline:
                             rnti=rnti, bwp_start=0, bwp_size=NOF_PRB, modulation=qm, crbs=crbs, start_symbol=0,
                             nof_symbols=14, dmrs_symb_pos=bp.DMRS_MASK, dmrs_type=1, nof_cdm_groups_without_data=2,
                             n_id=n_id, precoding=h), nsubc)
-                        assert kind == "uci" or mp.nof_bits == pp.sch.cw_length
+                        assert kind in ("uci", "csi2", "ucionly") or mp.nof_bits == pp.sch.cw_length
                         dm = amd.DmrsPdschConfig(slot_index=bp.SLOT, reference_point_k_rb=0, type=1,
                                                  scrambling_id=n_id, n_scid=False, amplitude=bp.DMRS_AMP,
                                                  symbols_mask=bp.DMRS_MASK, crbs=crbs, precoding=h)
@@ -237,8 +249,17 @@ class SlotPipeline:
                         if kind == "tp":
                             self.tp_ues.append((c, lo, hi, h[0], n_id))
                         # the UE transmits the codeword of the PDU's own rv (UCI UEs multiplexed and DFT-s-OFDM
-                        # UEs DFT-spread below)
-                        ue_tx.append((pp.sch, mp, dm, c))
+                        # UEs DFT-spread below); a CSI part 2 UE rate-matches its UL-SCH to the REs its CSI part 2
+                        # leaves (the size its CSI part 1 payload selects)
+                        sp_tx = pp.sch
+                        if kind in ("csi2", "ucionly"):
+                            csi1 = rng.integers(0, 2, CSI1_BITS).astype(np.uint8)
+                            n2 = amd.uci_part2_get_size(csi1, pdu.csi_part2_size) if kind == "csi2" else 0
+                            self.uci_sent[j] = (csi1, rng.integers(0, 2, n2).astype(np.uint8))
+                            if kind == "csi2" and n2:
+                                g = self._ulsch_info(amd, pdu, n2)["nof_ul_sch_bits"]
+                                sp_tx = amd.sch_plan(tbs, pdu.base_graph, 0, qm, pp.sch.Nref, layers, g // qm)
+                        ue_tx.append((sp_tx, mp, dm, c))
         self.dl, self.ul = dl, ul
         g = torch.Generator(device=dev)
         g.manual_seed(4242 + d + 7919 * seed)
@@ -260,17 +281,19 @@ class SlotPipeline:
             ul_ues.append((sp, tpos, cpos))
             tpos += sp.tbs // 8
             cpos += (sp.cw_length + 7) // 8 + 64
-        self.tb_ul = torch.randint(0, 256, (tpos,), device=dev, dtype=torch.uint8, generator=g)
+        self.tb_ul = torch.randint(0, 256, (max(tpos, 1),), device=dev, dtype=torch.uint8, generator=g)
         cw_ul = torch.zeros(cpos, dtype=torch.uint8, device=dev)
-        self.enc.encode_slot(self.tb_ul, ul_ues, out=cw_ul)
+        self.enc.encode_slot(self.tb_ul, [u for u, k in zip(ul_ues, self.kinds) if k != "ucionly"], out=cw_ul)
         # the UEs' transmitted codewords: the UL-SCH codeword, or for a UCI UE the whole multiplexed codeword (its
-        # UL-SCH bits at the REs the receiver's demultiplexer takes them from, random bits on the UCI REs)
+        # UL-SCH bits at the REs the receiver's demultiplexer takes them from; random bits on the HARQ-ACK / CSI part 1
+        # REs of "uci" UEs, the encoded CSI part 1 / CSI part 2 of "csi2" / "ucionly" UEs)
         cw_host = cw_ul.cpu().numpy()
         tx_parts, tx_off, pos = [], [], 0
         for j, ((sp, mp, dm, c), (_, _, co)) in enumerate(zip(ue_tx, ul_ues)):
-            if self.kinds[j] == "uci":
-                sch = np.unpackbits(cw_host[co:co + (sp.cw_length + 7) // 8])[:sp.cw_length]
-                part = np.packbits(self._multiplex(amd, self.ul_pdus[j], sch, mp.nof_bits, rng))
+            if self.kinds[j] in ("uci", "csi2", "ucionly"):
+                sch = (np.unpackbits(cw_host[co:co + (sp.cw_length + 7) // 8])[:sp.cw_length]
+                       if self.kinds[j] != "ucionly" else np.zeros(0, np.uint8))
+                part = np.packbits(self._multiplex(amd, self.ul_pdus[j], sch, mp.nof_bits, rng, j))
             else:
                 part = cw_host[co:co + (sp.cw_length + 7) // 8]
             tx_off.append(pos)
@@ -311,36 +334,60 @@ class SlotPipeline:
         self.ul_stream = None
         torch.cuda.synchronize(dev)
 
-    def _multiplex(self, amd, pdu, sch_bits, nof_bits, rng):
-        """UE-side UL-SCH / UCI multiplexing for the timing bench (untimed setup): the UL-SCH codeword placed where
-        the MI355X demultiplexer (srs_amd_ulsch_demultiplex, this library's own) reads it -- found by passing
-        RE-index-coded LLRs through it, seven bits per pass -- and random bits on the HARQ-ACK / CSI part 1 REs (the
-        bench checks the transport blocks, not the UCI payloads)."""
+    @staticmethod
+    def _ulsch_info(amd, pdu, n2):
+        """get_ulsch_information of a UL PDU with n2 CSI part 2 bits."""
+        return amd.ulsch_information(amd.UlschConfig(
+            tbs=pdu.tbs, modulation=pdu.modulation, target_code_rate=pdu.target_code_rate,
+            nof_harq_ack_bits=pdu.nof_harq_ack, nof_csi_part1_bits=pdu.nof_csi_part1, nof_csi_part2_bits=n2,
+            alpha_scaling=pdu.alpha_scaling, beta_offset_harq_ack=pdu.beta_offset_harq_ack,
+            beta_offset_csi_part1=pdu.beta_offset_csi_part1, beta_offset_csi_part2=pdu.beta_offset_csi_part2,
+            nof_rb=pdu.rb_count, start_symbol_index=pdu.start_symbol_index, nof_symbols=pdu.nof_symbols,
+            dmrs_type=pdu.dmrs_type, dmrs_symbol_mask=pdu.dmrs_symbol_mask,
+            nof_cdm_groups_without_data=pdu.nof_cdm_groups_without_data, nof_layers=pdu.nof_tx_layers))
+
+    def _multiplex(self, amd, pdu, sch_bits, nof_bits, rng, j):
+        """UE-side UL-SCH / UCI multiplexing for the timing bench (untimed setup): every stream placed where the
+        MI355X demultiplexer (srs_amd_ulsch_demultiplex, this library's own) reads it -- found by passing
+        RE-index-coded LLRs through it, seven bits per pass.  HARQ-ACK / CSI part 1 of "uci" UEs are random bits (the
+        bench checks their transport blocks); "csi2" / "ucionly" UEs send an encoded CSI part 1 (polar, CRC11) whose
+        first bits select the CSI part 2 size, and that CSI part 2 encoded the same way (TS 38.212 6.3.2.4), checked
+        by check() -- so the receiver's device-side CSI part 2 sizing is exercised with real sizes."""
         qm, L = pdu.modulation, pdu.nof_tx_layers
         bpre = qm * L
         nre = nof_bits // bpre
-        info = amd.ulsch_information(amd.UlschConfig(
-            tbs=pdu.tbs, modulation=qm, target_code_rate=pdu.target_code_rate, nof_harq_ack_bits=pdu.nof_harq_ack,
-            nof_csi_part1_bits=pdu.nof_csi_part1, alpha_scaling=pdu.alpha_scaling,
-            beta_offset_harq_ack=pdu.beta_offset_harq_ack, beta_offset_csi_part1=pdu.beta_offset_csi_part1,
-            nof_rb=pdu.rb_count, start_symbol_index=pdu.start_symbol_index, nof_symbols=pdu.nof_symbols,
-            dmrs_type=pdu.dmrs_type, dmrs_symbol_mask=pdu.dmrs_symbol_mask,
-            nof_cdm_groups_without_data=pdu.nof_cdm_groups_without_data, nof_layers=L))
+        csi1, csi2 = self.uci_sent.get(j, (None, None))
+        n2 = csi2.size if csi2 is not None else 0
+        info = self._ulsch_info(amd, pdu, n2)
         if not hasattr(self, "_demux"):
             self._demux = amd.UlschDemux(device=self.dev.index)
         plan = self._demux.plan(amd.UlschDemuxConfig(
             qm, L, pdu.rb_count, pdu.start_symbol_index, pdu.nof_symbols, info["nof_harq_ack_rvd"], pdu.dmrs_type,
             pdu.dmrs_symbol_mask, pdu.nof_cdm_groups_without_data, pdu.nof_harq_ack, info["nof_harq_ack_bits"],
-            pdu.nof_csi_part1, info["nof_csi_part1_bits"], (pdu.rnti << 15) + pdu.n_id))
-        assert plan.nof_codeword_bits == nof_bits and plan.nof_sch_bits == sch_bits.size
-        re_of = np.zeros(sch_bits.size // bpre, np.int64)
+            pdu.nof_csi_part1, info["nof_csi_part1_bits"], (pdu.rnti << 15) + pdu.n_id, n2,
+            info["nof_csi_part2_bits"] if n2 else 0))
+        if pdu.tbs == 0:  # UCI only: the REs the UCI leaves carry nothing the receiver decodes
+            sch_bits = rng.integers(0, 2, plan.nof_sch_bits).astype(np.uint8)
+        assert plan.nof_codeword_bits == nof_bits and plan.nof_sch_bits == sch_bits.size, (
+            j, self.kinds[j], n2, plan.nof_codeword_bits, nof_bits, plan.nof_sch_bits, sch_bits.size)
+        streams = None
         for k in range(3):
             code = (((np.arange(nre) >> (7 * k)) & 0x7F) + 1).astype(np.int8)
-            out = self._demux.demultiplex(np.repeat(code, bpre), plan)[0]
-            re_of += (np.abs(out[::bpre].astype(np.int64)) - 1) << (7 * k)  # 128 wraps to -128 in int8
+            out = self._demux.demultiplex(np.repeat(code, bpre), plan)
+            if streams is None:
+                streams = [np.zeros(o.size // bpre, np.int64) for o in out]
+            for s, o in zip(streams, out):
+                s += (np.abs(o[::bpre].astype(np.int64)) - 1) << (7 * k)  # 128 wraps to -128 in int8
         cw = rng.integers(0, 2, nof_bits).astype(np.uint8)
-        idx = (re_of[:, None] * bpre + np.arange(bpre)).ravel()
-        cw[idx] = sch_bits
+
+        def place(re_of, bits):
+            cw[(re_of[:, None] * bpre + np.arange(bpre)).ravel()] = bits
+
+        place(streams[0], sch_bits)
+        if csi1 is not None:
+            place(streams[2], _uci_encode(amd, csi1, info["nof_csi_part1_bits"], self.dev.index))
+            if n2:
+                place(streams[3], _uci_encode(amd, csi2, info["nof_csi_part2_bits"], self.dev.index))
         return cw
 
     def _transform_precode(self, amd, bp, grid, c, lo, hi, h, n_rs_id):
@@ -413,9 +460,20 @@ class SlotPipeline:
         rx, tx = self.tb_rx.cpu().numpy(), self.tb_ul.cpu().numpy()
         ok = []
         self.ok_by_kind = {}
-        for (pp, _), r, off, toff, k in zip(self.ul, res, self.ul_slot.offsets, self.ul_tb_off, self.kinds):
+        uci = self.uci.cpu().numpy()
+        for j, ((pp, _), r, off, toff, k) in enumerate(zip(self.ul, res, self.ul_slot.offsets, self.ul_tb_off,
+                                                           self.kinds)):
             n = pp.tb_bytes
-            ok.append(bool(r.data.tb_crc_ok) and np.array_equal(rx[off:off + n], tx[toff:toff + n]))
+            good = k == "ucionly" or (bool(r.data.tb_crc_ok) and np.array_equal(rx[off:off + n], tx[toff:toff + n]))
+            if j in self.uci_sent:
+                # CSI part 1 and the CSI part 2 of the size it selected, as the UE sent them
+                csi1, csi2 = self.uci_sent[j]
+                row = uci[self.ul_slot.uci_offsets[j]:]
+                n1 = csi1.size
+                good = (good and r.csi_part1_status == 1 and np.array_equal(row[:n1], csi1)
+                        and r.nof_csi_part2 == csi2.size and (csi2.size == 0 or (
+                            r.csi_part2_status == 1 and np.array_equal(row[n1:n1 + csi2.size], csi2))))
+            ok.append(good)
             self.ok_by_kind.setdefault(k, []).append(ok[-1])
         self.ok_by_kind = {k: float(np.mean(v)) for k, v in self.ok_by_kind.items()}
         its = sum(r.data.ldpc_iterations_sum for r in res) / max(1, sum(r.data.nof_codeblocks_total for r in res))
@@ -423,6 +481,38 @@ class SlotPipeline:
 
     def codeblocks(self):
         return (sum(sp.nof_segments for sp, _, _, _ in self.dl), sum(pp.sch.nof_segments for pp, _ in self.ul))
+
+
+# CSI part 1 / CSI part 2 of the mixed slot's "csi2" and "ucionly" UEs: 20 CSI part 1 bits (polar, CRC11) whose
+# first two bits select a CSI part 2 of 0, 20, 24 or 40 bits (uci_part2_size_description, one entry)
+CSI1_BITS = 20
+PART2 = [([(0, 2)], [0, 20, 24, 40])]
+
+
+def _uci_crc(bits, L):
+    """TS 38.212 5.1 CRC6 (D^6 + D^5 + 1) / CRC11 (D^11 + D^10 + D^9 + D^5 + 1) parity bits of a UCI payload."""
+    poly = {6: 0x21, 11: 0x621}[L]
+    reg = 0
+    for b in bits:
+        fb = ((reg >> (L - 1)) & 1) ^ int(b)
+        reg = (reg << 1) & ((1 << L) - 1)
+        reg ^= poly if fb else 0
+    return np.array([(reg >> (L - 1 - i)) & 1 for i in range(L)], np.uint8)
+
+
+_POLAR = {}
+
+
+def _uci_encode(amd, payload, E, device):
+    """UCI on PUSCH for 12 <= A < 360 payload bits: CRC, polar code (nMax 10, channel interleaver), rate matching to
+    E bits (TS 38.212 6.3.2.4 / 5.3.1; the decoder side is uci_decoder_impl)."""
+    A = payload.size
+    L = 6 if A < 20 else 11
+    assert 12 <= A < 360
+    key = (A + L, E, device)
+    if key not in _POLAR:
+        _POLAR[key] = amd.PolarCode(A + L, E, 10, amd.PolarCodeIbil.present, device=device)
+    return _POLAR[key].encode(np.concatenate([payload, _uci_crc(payload, L)]))
 
 
 def run_slot_pipeline(args, dist, world, rank, dev, timed):

@@ -159,6 +159,9 @@ __global__ __launch_bounds__(64 * WAVES) void polar_decode_kernel(polar_args own
   }
   const polar_args& a  = MULTI ? items[w] : own;
   const uint32_t    cw = MULTI ? 0u : w;
+  if (MULTI && a.pred != nullptr && *a.pred != a.pred_val) {
+    return; // one wave per item: nothing else of the workgroup waits for it
+  }
   int8_t*       llr = llr_all[wave];
   uint8_t*      est = est_all[wave];
   uint8_t*      dec = msg_all[wave];

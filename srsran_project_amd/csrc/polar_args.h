@@ -28,6 +28,9 @@ struct polar_args {
   const uint16_t* rx_e2f;  // [E]
   const uint16_t* blk;     // [N]
   const uint32_t* program; // [prog_len]
+  // slot form (launch_polar_decode_items): decoded only when *pred == pred_val (pred null: always)
+  const int32_t*  pred     = nullptr;
+  int32_t         pred_val = 0;
 };
 
 hipError_t launch_polar_encode(const polar_args& a, hipStream_t stream);

@@ -291,7 +291,9 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
                        const uint32_t*                     cb_offsets,
                        int32_t*                            d_cb_iterations,
                        hipStream_t                         stream,
-                       const slot_harq*                    harq)
+                       const slot_harq*                    harq,
+                       const slot_ue_patch*                patches,
+                       uint32_t                            nof_patches)
 {
   // HARQ UEs (a caller soft buffer): their codeblocks decode in internal rows like the others, the soft bits
   // gathered from / scattered to the caller's rows around the rate dematcher / decoder (harq_* kernels), full-length
@@ -435,7 +437,13 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   const size_t o_RF  = o_RD + align_up(sizeof(ldpc_row_desc) * R, 16);
   const size_t o_HR  = o_RF + align_up(R, 16);
   const size_t o_HT  = o_HR + align_up(sizeof(harq_row_desc) * hrows.size(), 16);
-  const size_t total = hrows.empty() ? o_RF : o_HT + sizeof(harq_tb_desc) * htbs.size();
+  const size_t o_PT  = align_up(hrows.empty() ? o_RF : o_HT + sizeof(harq_tb_desc) * htbs.size(), 16);
+  const size_t total = o_PT + sizeof(slot_row_patch) * nof_patches;
+  for (uint32_t q = 0; q < nof_patches; ++q) {
+    if (patches[q].ue >= U || patches[q].sel == nullptr || patches[q].cand_E == nullptr || patches[q].cand_off == nullptr) {
+      return fail(SRS_AMD_EINVAL, "slot decoder: invalid row patch %u", q);
+    }
+  }
 
   hipError_t he = hipSetDevice(d->device);
   // the pinned staging buffer is rewritten only once its previous upload completed
@@ -493,7 +501,19 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     std::memcpy(h + o_HR, hrows.data(), sizeof(harq_row_desc) * hrows.size());
     std::memcpy(h + o_HT, htbs.data(), sizeof(harq_tb_desc) * htbs.size());
   }
-  auto*      dd = d->slot_desc.as<uint8_t>();
+  auto* dd = d->slot_desc.as<uint8_t>();
+  for (uint32_t q = 0; q < nof_patches; ++q) {
+    const uint32_t u = patches[q].ue;
+    slot_row_patch rp{};
+    rp.row_E      = reinterpret_cast<uint32_t*>(dd + o_E) + tds[u].row0;
+    rp.row_in     = reinterpret_cast<uint32_t*>(dd + o_in) + tds[u].row0;
+    rp.sel        = patches[q].sel;
+    rp.cand_E     = patches[q].cand_E;
+    rp.cand_off   = patches[q].cand_off;
+    rp.llr_offset = static_cast<uint32_t>(ues[u].llr_offset);
+    rp.C          = ues[u].plan.nof_segments;
+    std::memcpy(h + o_PT + sizeof(slot_row_patch) * q, &rp, sizeof(rp));
+  }
   call_scope scope(d->order, &d->fan, stream);
   he = d->order.begin(stream);
   if (he == hipSuccess) {
@@ -506,6 +526,13 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
     return hip_fail(he, "PUSCH slot descriptors upload");
   }
   d->stage_used = true;
+  // 0. UEs whose UL-SCH geometry was selected on the device (CSI part 2): their rows' lengths / offsets
+  if (nof_patches != 0) {
+    he = launch_slot_row_patch(reinterpret_cast<const slot_row_patch*>(dd + o_PT), nof_patches, stream);
+    if (he != hipSuccess) {
+      return hip_fail(he, "slot_row_patch_kernel launch");
+    }
+  }
   // 1. Rate dematching of every codeblock of the slot, one launch (HARQ rows combining into their gathered bits).
   int8_t*   soft = d->soft.as<int8_t>();
   harq_args ha{};
@@ -860,7 +887,9 @@ int srs_amd::pusch_decode_slot_ex(srs_amd_pusch_decoder*              dec,
                                   const uint32_t*                     cb_offsets,
                                   int32_t*                            d_cb_iterations,
                                   hipStream_t                         stream,
-                                  const slot_harq*                    harq)
+                                  const slot_harq*                    harq,
+                                  const slot_ue_patch*                patches,
+                                  uint32_t                            nof_patches)
 {
   if (dec == nullptr || cfg == nullptr) {
     return fail(SRS_AMD_EINVAL, "null argument");
@@ -886,6 +915,6 @@ int srs_amd::pusch_decode_slot_ex(srs_amd_pusch_decoder*              dec,
   }
   std::lock_guard<std::mutex> lock(dec->mtx);
   return decode_slot_locked(dec, cfg, ues, nof_ues, d_llrs, d_tbs, d_results, cb_offsets, d_cb_iterations, stream,
-                            harq);
+                            harq, patches, nof_patches);
 }
 

@@ -43,6 +43,46 @@ __global__ __launch_bounds__(64) void pusch_result_kernel(pusch_result_args a)
   a.results[a.result_ids != nullptr ? a.result_ids[g] : g] = r;
 }
 
+__global__ __launch_bounds__(64) void csi2_select_kernel(const csi2_select_args* items, uint32_t n)
+{
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) {
+    return;
+  }
+  const csi2_select_args& a  = items[i];
+  int32_t                 n2 = 0;
+  if (*a.status1 == SRS_AMD_UCI_VALID) { // on_csi_part1 is notified with a valid CSI part 1 only
+    for (uint32_t e = 0; e < a.descr.nof_entries && e < 2; ++e) {
+      const srs_amd_uci_part2_entry& en    = a.descr.entries[e];
+      uint32_t                       index = 0;
+      for (uint32_t q = 0; q < en.nof_parameters && q < 2; ++q) {
+        // the field's first bit is its most significant (uci_part2_size_calculator.cpp extract_parameter)
+        uint32_t value = 0;
+        for (uint32_t b = 0; b < en.parameters[q].width; ++b) {
+          value = (value << 1) | (a.part1[en.parameters[q].offset + b] & 1u);
+        }
+        index = (index << en.parameters[q].width) | value;
+      }
+      n2 += index < en.map_size && index < 16 ? en.map[index] : 0;
+    }
+  }
+  int32_t s = -1;
+  for (uint32_t c = 0; c < a.nof_cand && n2 != 0; ++c) {
+    s = a.cand[c] == n2 ? static_cast<int32_t>(c) : s;
+  }
+  *a.nof_part2 = s >= 0 ? n2 : 0;
+  *a.sel       = s;
+}
+
+hipError_t launch_csi2_select(const csi2_select_args* items, uint32_t n, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(csi2_select_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, items, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_pusch_result(const pusch_result_args& a, hipStream_t stream)
 {
   if (a.nof_grids == 0) {

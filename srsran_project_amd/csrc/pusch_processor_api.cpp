@@ -44,6 +44,7 @@ struct srs_amd_pusch_processor {
   pinned_stage                   stage2; // CSI part 2 sizes of a batch
   pinned_stage                   stage3; // slot form: UCI descriptors (demultiplexer, decoders, field masks)
   device_buffer                  uci_items, uci_cbs;
+  device_buffer                  csi2_sel; // slot form: CSI part 2 size candidate selected per fused PDU
   stream_fan                     fan; // slot form: the UCI decoders beside the UL-SCH decoder
   size_t                         uci_masks_offset = 0; // of the fused group's per-PDU UCI field masks in uci_items
   std::mutex                     mtx;
@@ -95,6 +96,19 @@ struct srs_amd_pusch_processor_plan {
   };
   mutable std::map<uint32_t, part2_geometry> part2;
   mutable std::mutex                         part2_mtx;
+  // every CSI part 2 size the description can produce (the fused slot group selects among them on the device),
+  // built on first use: sizes, geometries, the largest encoded length, and the device table
+  // [NC] int32 sizes | [NC][C] rate-matching lengths | [NC][C] LLR offsets (srs_amd_sch_plan_segments)
+  struct csi2_candidates {
+    std::vector<uint32_t>              n2;
+    std::vector<const part2_geometry*> geo;
+    uint32_t                           max_e2 = 0;
+    device_buffer                      d;
+    bool                               ready = false;
+    int                                rc    = SRS_AMD_OK; // a size without a geometry (cached)
+  };
+  mutable csi2_candidates cand;
+  mutable std::mutex      cand_mtx;
   ~srs_amd_pusch_processor_plan()
   {
     srs_amd_pusch_demod_plan_destroy(demod_plan);
@@ -174,6 +188,67 @@ int plan_part2(srs_amd_pusch_processor*                                    proc,
     return rc;
   }
   *out = &pl->part2.emplace(n2, g).first->second;
+  return SRS_AMD_OK;
+}
+
+// The CSI part 2 candidates of `pl` (every size its description maps some CSI part 1 value to), with their
+// geometries and device table; built once per plan (one synchronous upload).
+int plan_csi2_candidates(srs_amd_pusch_processor* proc, const srs_amd_pusch_processor_plan* pl,
+                         const srs_amd_pusch_processor_plan::csi2_candidates** out)
+{
+  std::lock_guard<std::mutex> lock(pl->cand_mtx);
+  auto&                       c = pl->cand;
+  if (c.ready && c.rc != SRS_AMD_OK) {
+    return c.rc;
+  }
+  if (!c.ready) {
+    const srs_amd_uci_part2_size_description& d  = pl->pdu.csi_part2_size;
+    const uint32_t                            m0 = d.nof_entries > 0 ? d.entries[0].map_size : 1u;
+    const uint32_t                            m1 = d.nof_entries > 1 ? d.entries[1].map_size : 1u;
+    std::vector<uint32_t>                     sizes;
+    for (uint32_t i0 = 0; i0 < m0 && i0 < 16; ++i0) {
+      for (uint32_t i1 = 0; i1 < m1 && i1 < 16; ++i1) {
+        const uint32_t n = (d.nof_entries > 0 ? d.entries[0].map[i0] : 0u) + (d.nof_entries > 1 ? d.entries[1].map[i1] : 0u);
+        if (n != 0 && std::find(sizes.begin(), sizes.end(), n) == sizes.end()) {
+          sizes.push_back(n);
+        }
+      }
+    }
+    std::sort(sizes.begin(), sizes.end());
+    c.n2.clear();
+    c.geo.clear();
+    c.max_e2 = 0;
+    for (uint32_t n : sizes) {
+      const srs_amd_pusch_processor_plan::part2_geometry* g = nullptr;
+      int rc = plan_part2(proc, pl, n, &g);
+      if (rc != SRS_AMD_OK) {
+        c.ready = true;
+        c.rc    = rc;
+        return rc;
+      }
+      c.n2.push_back(n);
+      c.geo.push_back(g);
+      c.max_e2 = std::max(c.max_e2, g->info.nof_csi_part2_bits);
+    }
+    const size_t          NC = c.n2.size();
+    const uint32_t        C  = pl->has_sch ? pl->sch.nof_segments : 0u;
+    std::vector<uint32_t> tab(NC + 2 * NC * C);
+    for (size_t k = 0; k < NC; ++k) {
+      tab[k] = c.n2[k];
+      if (C != 0) {
+        (void)srs_amd_sch_plan_segments(&c.geo[k]->sch, tab.data() + NC + k * C, tab.data() + NC + NC * C + k * C);
+      }
+    }
+    hipError_t e = c.d.ensure(std::max<size_t>(tab.size(), 1) * sizeof(uint32_t));
+    if (e == hipSuccess && !tab.empty()) {
+      e = hipMemcpy(c.d.ptr, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+      return hip_fail(e, "CSI part 2 candidate table");
+    }
+    c.ready = true;
+  }
+  *out = &c;
   return SRS_AMD_OK;
 }
 
@@ -465,24 +540,32 @@ void srs_amd_pusch_processor_plan_destroy(srs_amd_pusch_processor_plan* plan)
 
 namespace {
 
-// chest: the estimator configuration to run (the plan's, or a copy in another slot); nullptr: the plan's.
 // The UCI PDUs (index ucis[j] of the fused group) of a slot call: one demultiplexer launch over every codeword, the
 // HARQ-ACK / CSI part 1 messages through the slot-form UCI decoder (uci_slot_build), statuses into uci_status[k][4]
 // (zeroed first) and payloads into the caller's UCI rows (d_uci + uci_offset) or scratch; the per-PDU field masks
 // of the result kernel (every fused PDU k) after the descriptors in uci_items.
+// CSI part 2 PDUs (cands[k] non-null): after their CSI part 1 is decoded, csi2_select_kernel picks the size on the
+// device (sel[k], the fourth status column); a second demultiplexer launch with one block per (PDU, candidate size)
+// and one UCI decoder set per (PDU, candidate size) run only for the selected candidate (device predicates), so the
+// UL-SCH rows and the CSI part 2 message take that size's geometry with no host round trip
+// (pusch_processor_impl.cpp:56-103 does the same from on_csi_part1).  Without CSI part 2 the UCI decoders run on a
+// helper stream beside the UL-SCH decoder; with it they run on the call's stream, before the decoder.
 int fused_uci(srs_amd_pusch_processor* proc, const srs_amd_pusch_slot_pdu* pdus, const std::vector<uint32_t>& fused,
               const std::vector<uint32_t>& ucis, const std::vector<size_t>& cw_off, const std::vector<size_t>& uci_off,
-              const std::vector<size_t>& pay_off, int8_t* llrs, const std::vector<size_t>& llr_off, uint8_t* d_uci,
-              hipStream_t s)
+              const std::vector<size_t>& c2_off, const std::vector<size_t>& pay_off,
+              const std::vector<const srs_amd_pusch_processor_plan::csi2_candidates*>& cands, int8_t* llrs,
+              const std::vector<size_t>& llr_off, uint8_t* d_uci, hipStream_t s)
 {
   const uint32_t n  = static_cast<uint32_t>(fused.size());
   int8_t*        cw = proc->cw_llrs.as<int8_t>();
   int8_t*        ur = proc->uci_llrs.as<int8_t>();
   int32_t*       st = proc->uci_status.as<int32_t>();
-  std::vector<demux_args>       dx;
-  std::vector<uci_slot_message> msgs;
+  int32_t*       sel = proc->csi2_sel.as<int32_t>();
+  std::vector<demux_args>       dx, dx2;
+  std::vector<uci_slot_message> msgs, msgs2;
+  std::vector<csi2_select_args> sels;
   std::vector<uint32_t>         masks(n, 0);
-  uint32_t                      max_re = 0;
+  uint32_t                      max_re = 0, max_re2 = 0;
   for (uint32_t k : ucis) {
     const srs_amd_pusch_slot_pdu&       u    = pdus[fused[k]];
     const srs_amd_pusch_processor_plan* pl   = u.plan;
@@ -499,24 +582,73 @@ int fused_uci(srs_amd_pusch_processor* proc, const srs_amd_pusch_slot_pdu* pdus,
       msgs.push_back(uci_slot_message{rows + ea, ec, kc, pl->pdu.modulation, pay + ka, st + 4 * k + 1});
     }
     masks[k] = (ka != 0 ? 1u : 0u) | (kc != 0 ? 2u : 0u);
+    const auto* c = cands[k];
+    if (c == nullptr) {
+      continue;
+    }
+    masks[k] |= 4u;
+    csi2_select_args sa{};
+    sa.part1     = pay + ka;
+    sa.status1   = st + 4 * k + 1;
+    sa.nof_part2 = st + 4 * k + 3;
+    sa.sel       = sel + k;
+    sa.cand      = c->d.as<int32_t>();
+    sa.nof_cand  = static_cast<uint32_t>(c->n2.size());
+    sa.nof_part1 = kc;
+    sa.descr     = pl->pdu.csi_part2_size;
+    sels.push_back(sa);
+    int8_t* c2 = ur + c2_off[k];
+    for (size_t q = 0; q < c->n2.size(); ++q) {
+      const auto* g = c->geo[q];
+      demux_args  d = make_demux_args_csi2(g->demux, cw + cw_off[k], llrs + llr_off[k], rows, rows + ea, c2);
+      d.sel         = sel + k;
+      d.sel_val     = static_cast<int32_t>(q);
+      dx2.push_back(d);
+      max_re2 = std::max(max_re2, d.nof_re);
+      uci_slot_message m{c2, g->info.nof_csi_part2_bits, c->n2[q], pl->pdu.modulation, pay + ka + kc, st + 4 * k + 2};
+      m.pred     = sel + k;
+      m.pred_val = static_cast<int32_t>(q);
+      msgs2.push_back(m);
+    }
   }
-  uci_slot_plan up;
+  uci_slot_plan up, up2;
   int           rc = uci_slot_build(proc->uci, msgs.data(), static_cast<uint32_t>(msgs.size()), nullptr, up);
-  hipError_t    e  = hipSuccess;
-  if (rc == SRS_AMD_OK && up.cb_bytes != 0) {
-    e = proc->uci_cbs.ensure(up.cb_bytes);
+  if (rc == SRS_AMD_OK) {
+    rc = uci_slot_build(proc->uci, msgs2.data(), static_cast<uint32_t>(msgs2.size()), nullptr, up2);
+  }
+  hipError_t e = hipSuccess;
+  if (rc == SRS_AMD_OK && up.cb_bytes + up2.cb_bytes != 0) {
+    e = proc->uci_cbs.ensure(up.cb_bytes + up2.cb_bytes);
   }
   if (rc == SRS_AMD_OK && e == hipSuccess) {
     rc = uci_slot_build(proc->uci, msgs.data(), static_cast<uint32_t>(msgs.size()), proc->uci_cbs.as<uint8_t>(), up);
   }
+  if (rc == SRS_AMD_OK && e == hipSuccess) {
+    rc = uci_slot_build(proc->uci, msgs2.data(), static_cast<uint32_t>(msgs2.size()),
+                        proc->uci_cbs.as<uint8_t>() + up.cb_bytes, up2);
+  }
   if (rc != SRS_AMD_OK) {
     return rc;
   }
-  const size_t o_sh  = align_up(sizeof(demux_args) * dx.size(), 64);
-  const size_t o_po  = o_sh + align_up(sizeof(uci_short_args) * up.shorts.size(), 64);
-  const size_t o_fi  = o_po + align_up(sizeof(polar_args) * up.polars.size(), 64);
-  const size_t o_mk  = o_fi + align_up(sizeof(uci_polar_args) * up.finishes.size(), 64);
-  const size_t total = o_mk + sizeof(uint32_t) * n;
+  // staging layout: pass-1 demux | shorts | polars | finishes | field masks | CSI part 2 selections | pass-2 demux |
+  // CSI part 2 shorts | polars | finishes
+  size_t     off = 0;
+  const auto put = [&](size_t bytes) {
+    const size_t o = off;
+    off            = align_up(off + bytes, 64);
+    return o;
+  };
+  const size_t o_dx  = put(sizeof(demux_args) * dx.size());
+  const size_t o_sh  = put(sizeof(uci_short_args) * up.shorts.size());
+  const size_t o_po  = put(sizeof(polar_args) * up.polars.size());
+  const size_t o_fi  = put(sizeof(uci_polar_args) * up.finishes.size());
+  const size_t o_mk  = put(sizeof(uint32_t) * n);
+  const size_t o_se  = put(sizeof(csi2_select_args) * sels.size());
+  const size_t o_dx2 = put(sizeof(demux_args) * dx2.size());
+  const size_t o_sh2 = put(sizeof(uci_short_args) * up2.shorts.size());
+  const size_t o_po2 = put(sizeof(polar_args) * up2.polars.size());
+  const size_t o_fi2 = put(sizeof(uci_polar_args) * up2.finishes.size());
+  const size_t total = off;
   if (e == hipSuccess) {
     e = proc->uci_items.ensure(total);
   }
@@ -529,23 +661,35 @@ int fused_uci(srs_amd_pusch_processor* proc, const srs_amd_pusch_slot_pdu* pdus,
   if (e != hipSuccess) {
     return hip_fail(e, "PUSCH slot UCI scratch");
   }
-  std::memcpy(proc->stage3.at<uint8_t>(0), dx.data(), sizeof(demux_args) * dx.size());
-  std::memcpy(proc->stage3.at<uint8_t>(o_sh), up.shorts.data(), sizeof(uci_short_args) * up.shorts.size());
-  std::memcpy(proc->stage3.at<uint8_t>(o_po), up.polars.data(), sizeof(polar_args) * up.polars.size());
-  std::memcpy(proc->stage3.at<uint8_t>(o_fi), up.finishes.data(), sizeof(uci_polar_args) * up.finishes.size());
-  std::memcpy(proc->stage3.at<uint8_t>(o_mk), masks.data(), sizeof(uint32_t) * n);
+  auto copy = [&](size_t o, const void* src, size_t bytes) {
+    if (bytes != 0) {
+      std::memcpy(proc->stage3.at<uint8_t>(o), src, bytes);
+    }
+  };
+  copy(o_dx, dx.data(), sizeof(demux_args) * dx.size());
+  copy(o_sh, up.shorts.data(), sizeof(uci_short_args) * up.shorts.size());
+  copy(o_po, up.polars.data(), sizeof(polar_args) * up.polars.size());
+  copy(o_fi, up.finishes.data(), sizeof(uci_polar_args) * up.finishes.size());
+  copy(o_mk, masks.data(), sizeof(uint32_t) * n);
+  copy(o_se, sels.data(), sizeof(csi2_select_args) * sels.size());
+  copy(o_dx2, dx2.data(), sizeof(demux_args) * dx2.size());
+  copy(o_sh2, up2.shorts.data(), sizeof(uci_short_args) * up2.shorts.size());
+  copy(o_po2, up2.polars.data(), sizeof(polar_args) * up2.polars.size());
+  copy(o_fi2, up2.finishes.data(), sizeof(uci_polar_args) * up2.finishes.size());
   proc->uci_masks_offset = o_mk;
   auto* d = proc->uci_items.as<uint8_t>();
   e       = proc->stage3.upload(d, total, s);
   if (e == hipSuccess) {
-    e = launch_ulsch_demux_items(reinterpret_cast<const demux_args*>(d), static_cast<uint32_t>(dx.size()), max_re, s);
+    e = launch_ulsch_demux_items(reinterpret_cast<const demux_args*>(d + o_dx), static_cast<uint32_t>(dx.size()),
+                                 max_re, s);
   }
   // the UCI decoders depend only on the demultiplexer: on a helper stream beside the UL-SCH decoder (joined by the
-  // caller before the result kernel)
-  if (e == hipSuccess) {
+  // caller before the result kernel) -- unless CSI part 2 sizes the UL-SCH geometry, then on this stream
+  const bool serial = !sels.empty();
+  if (e == hipSuccess && !serial) {
     e = proc->fan.begin(s, 2);
   }
-  const hipStream_t hs = proc->fan.stream(s, 0);
+  const hipStream_t hs = serial ? s : proc->fan.stream(s, 0);
   if (e == hipSuccess) {
     e = launch_uci_short_items(reinterpret_cast<const uci_short_args*>(d + o_sh),
                                static_cast<uint32_t>(up.shorts.size()), hs);
@@ -558,9 +702,31 @@ int fused_uci(srs_amd_pusch_processor* proc, const srs_amd_pusch_slot_pdu* pdus,
     e = launch_uci_polar_finish_items(reinterpret_cast<const uci_polar_args*>(d + o_fi),
                                       static_cast<uint32_t>(up.finishes.size()), hs);
   }
+  if (serial) {
+    if (e == hipSuccess) {
+      e = launch_csi2_select(reinterpret_cast<const csi2_select_args*>(d + o_se), static_cast<uint32_t>(sels.size()), s);
+    }
+    if (e == hipSuccess) {
+      e = launch_ulsch_demux_items(reinterpret_cast<const demux_args*>(d + o_dx2), static_cast<uint32_t>(dx2.size()),
+                                   max_re2, s);
+    }
+    if (e == hipSuccess) {
+      e = launch_uci_short_items(reinterpret_cast<const uci_short_args*>(d + o_sh2),
+                                 static_cast<uint32_t>(up2.shorts.size()), s);
+    }
+    if (e == hipSuccess) {
+      e = launch_polar_decode_items(reinterpret_cast<const polar_args*>(d + o_po2),
+                                    static_cast<uint32_t>(up2.polars.size()), s);
+    }
+    if (e == hipSuccess) {
+      e = launch_uci_polar_finish_items(reinterpret_cast<const uci_polar_args*>(d + o_fi2),
+                                        static_cast<uint32_t>(up2.finishes.size()), s);
+    }
+  }
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH slot UCI launches");
 }
 
+// chest: the estimator configuration to run (the plan's, or a copy in another slot); nullptr: the plan's.
 int process_batch_locked(srs_amd_pusch_processor*            proc,
                          const srs_amd_pusch_processor_plan* plan,
                          const uint32_t*                     d_grids,
@@ -888,14 +1054,27 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
       return fail(SRS_AMD_EINVAL, "PDU %u: invalid slot %u of numerology %u", i, pdus[i].slot_index,
                   pdus[i].numerology);
     }
-    // HARQ-ACK / CSI part 1 on the UL-SCH and DFT-s-OFDM PDUs join the group (slot-form demultiplexer and UCI
-    // decoders; the equalizer's symbols through the transform deprecoder); CSI part 2
-    // (its sizes come from the decoded CSI part 1) and UCI-only PDUs take the batch chain
-    // HARQ processes with a soft buffer (new data or retransmission) join it too (the slot decoder's HARQ rows,
-    // early-stop decoding)
-    const bool f = proc->fuse && pl->fusable && P <= STATS_STRIDE && pl->has_sch && !pl->csi2 &&
-                   (pdus[i].d_soft == nullptr ? pl->dec_cfg.new_data != 0 : pl->dec_cfg.use_early_stop != 0);
+    // HARQ-ACK / CSI part 1 / CSI part 2 on the UL-SCH, UCI-only and DFT-s-OFDM PDUs join the group (slot-form
+    // demultiplexer and UCI decoders, CSI part 2 sized on the device; the equalizer's symbols through the transform
+    // deprecoder); HARQ processes with a soft buffer (new data or retransmission) join it too (the slot decoder's
+    // HARQ rows, early-stop decoding)
+    bool f = proc->fuse && pl->fusable && P <= STATS_STRIDE &&
+             (!pl->has_sch || (pdus[i].d_soft == nullptr ? pl->dec_cfg.new_data != 0 : pl->dec_cfg.use_early_stop != 0));
+    if (f && pl->csi2) {
+      // every CSI part 2 size of the description must have a geometry (a UCI-only PDU with CSI part 2 has none: its
+      // CSI part 1 takes every RE, ulsch_info.cpp:96-123); otherwise the PDU keeps the batch chain, which fails
+      // only when a decoded CSI part 1 selects such a size
+      const srs_amd_pusch_processor_plan::csi2_candidates* c = nullptr;
+      f = plan_csi2_candidates(proc, pl, &c) == SRS_AMD_OK;
+    }
     (f ? fused : others).push_back(i);
+  }
+  // PDUs with a codeword first: the slot decoder's UEs are then the first nsch PDUs of the group (results are
+  // scattered back to the PDU indices by the result kernel)
+  std::stable_partition(fused.begin(), fused.end(), [&](uint32_t i) { return pdus[i].plan->has_sch; });
+  uint32_t nsch = 0;
+  for (uint32_t i : fused) {
+    nsch += pdus[i].plan->has_sch ? 1u : 0u;
   }
   // each PDU's estimator configuration: its plan's, moved to the PDU's own slot when it carries one (the DM-RS
   // sequences are the only per-slot quantity; PDUs of several slots may share a plan within one call)
@@ -940,23 +1119,32 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     return SRS_AMD_OK;
   }
   // 2. the fused group
+  // UL-SCH LLR rows (a UCI-only PDU's row takes the demultiplexer's discarded UL-SCH stream)
   std::vector<size_t> llr_off(n);
   size_t              llr_bytes = 0;
   for (uint32_t k = 0; k != n; ++k) {
-    llr_off[k] = llr_bytes;
-    llr_bytes += align_up(pdus[fused[k]].plan->sch.cw_length, 64);
+    const srs_amd_pusch_processor_plan* pl = pdus[fused[k]].plan;
+    llr_off[k]                             = llr_bytes;
+    llr_bytes += align_up(std::max<uint32_t>(pl->has_sch ? pl->sch.cw_length : pl->dummy_sch_bits, 1), 64);
   }
-  const bool       subset = n != nof_pdus; // results scattered to the fused PDUs' indices
   const size_t     o_ids  = align_up(sizeof(uint32_t) * n, 16);
-  // UCI PDUs of the group: the demodulator's codeword rows, the demultiplexed HARQ-ACK / CSI part 1 rows, payload
-  // rows (the caller's d_uci, or scratch) and statuses [k][4]
+  // UCI PDUs of the group: the demodulator's codeword rows, the demultiplexed HARQ-ACK / CSI part 1 (/ CSI part 2)
+  // rows, payload rows (the caller's d_uci, or scratch) and statuses [k][4]
   std::vector<uint32_t> ucis;
-  std::vector<size_t>   cw_off(n), uci_off(n), pay_off(n);
+  std::vector<size_t>   cw_off(n), uci_off(n), c2_off(n), pay_off(n);
+  std::vector<const srs_amd_pusch_processor_plan::csi2_candidates*> cands(n, nullptr);
   size_t                cw_bytes = 0, uci_bytes = 0, pay_bytes = 0;
   for (uint32_t k = 0; k != n; ++k) {
     const srs_amd_pusch_processor_plan* pl = pdus[fused[k]].plan;
     if (!pl->uci) {
       continue;
+    }
+    if (pl->csi2) {
+      const int rc = plan_csi2_candidates(proc, pl, &cands[k]);
+      if (rc != SRS_AMD_OK) {
+        return rc;
+      }
+      cands[k] = cands[k]->n2.empty() ? nullptr : cands[k];
     }
     ucis.push_back(k);
     cw_off[k]  = cw_bytes;
@@ -964,10 +1152,17 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     pay_off[k] = pay_bytes;
     cw_bytes += align_up(pl->cw_bits, 64);
     uci_bytes += align_up(pl->info.nof_harq_ack_bits + pl->info.nof_csi_part1_bits, 64);
-    pay_bytes += align_up(pl->pdu.nof_harq_ack + pl->pdu.nof_csi_part1, 64);
+    if (cands[k] != nullptr) {
+      c2_off[k] = uci_bytes;
+      uci_bytes += align_up(cands[k]->max_e2, 64);
+    }
+    pay_bytes += align_up(pl->pdu.nof_harq_ack + pl->pdu.nof_csi_part1 + pl->max_csi2, 64);
   }
   const uint32_t nu = static_cast<uint32_t>(ucis.size());
   hipError_t       e      = hipSetDevice(proc->device);
+  if (e == hipSuccess && nu != 0) {
+    e = proc->csi2_sel.ensure(sizeof(int32_t) * n);
+  }
   if (e == hipSuccess && nu != 0) {
     e = proc->cw_llrs.ensure(cw_bytes);
   }
@@ -1034,29 +1229,46 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
   // 2b'. UCI PDUs: the demultiplexer of every codeword (UL-SCH LLRs into the PDU's decoder row) in one launch, then
   //      the HARQ-ACK and CSI part 1 decoders of every PDU (one short-block, one polar and one CRC launch)
   if (nu != 0) {
-    rc = fused_uci(proc, pdus, fused, ucis, cw_off, uci_off, pay_off, llrs, llr_off, d_uci, s);
+    rc = fused_uci(proc, pdus, fused, ucis, cw_off, uci_off, c2_off, pay_off, cands, llrs, llr_off, d_uci, s);
     if (rc != SRS_AMD_OK) {
       return rc;
     }
   }
-  // 2c. UL-SCH decoding of every transport block of the group (srs_amd_pusch_decode_slot)
-  std::vector<srs_amd_pusch_ue> ues(n);
-  std::vector<uint32_t>         cb_off(n);
-  std::vector<slot_harq>        harq(n);
+  // 2c. UL-SCH decoding of every transport block of the group (srs_amd_pusch_decode_slot): the first nsch PDUs; a
+  //     UCI-only PDU's decoder result is empty (pusch_processor_impl.cpp:305); a CSI part 2 PDU's rows take the
+  //     geometry of the size selected in 2b' (row patches)
+  std::vector<srs_amd_pusch_ue> ues(nsch);
+  std::vector<uint32_t>         cb_off(nsch);
+  std::vector<slot_harq>        harq(nsch);
+  std::vector<slot_ue_patch>    patches;
   bool                          any_harq = false;
-  for (uint32_t k = 0; k != n; ++k) {
+  for (uint32_t k = 0; k != nsch; ++k) {
     const srs_amd_pusch_slot_pdu& u = pdus[fused[k]];
     ues[k]    = srs_amd_pusch_ue{u.plan->sch, llr_off[k], u.tb_offset};
     cb_off[k] = u.cb_offset;
     harq[k]   = slot_harq{u.d_soft, u.plan->dec_cfg.new_data};
     any_harq |= u.d_soft != nullptr;
+    if (cands[k] != nullptr) {
+      const uint32_t NC = static_cast<uint32_t>(cands[k]->n2.size()), C = u.plan->sch.nof_segments;
+      const auto*    t  = cands[k]->d.as<uint32_t>();
+      patches.push_back(slot_ue_patch{k, proc->csi2_sel.as<int32_t>() + k, t + NC, t + NC + NC * C});
+    }
   }
-  rc = pusch_decode_slot_ex(proc->dec, &pdus[fused[0]].plan->dec_cfg, ues.data(), n, llrs, d_tbs,
-                            proc->dec_results.as<srs_amd_pusch_decoder_result>(),
-                            cb_iters != nullptr ? cb_off.data() : nullptr, cb_iters, s,
-                            any_harq ? harq.data() : nullptr);
-  if (rc != SRS_AMD_OK) {
-    return rc;
+  if (nsch < n) {
+    e = hipMemsetAsync(proc->dec_results.as<srs_amd_pusch_decoder_result>() + nsch, 0,
+                       sizeof(srs_amd_pusch_decoder_result) * (n - nsch), s);
+    if (e != hipSuccess) {
+      return hip_fail(e, "PUSCH slot UCI-only results");
+    }
+  }
+  if (nsch != 0) {
+    rc = pusch_decode_slot_ex(proc->dec, &pdus[fused[0]].plan->dec_cfg, ues.data(), nsch, llrs, d_tbs,
+                              proc->dec_results.as<srs_amd_pusch_decoder_result>(),
+                              cb_iters != nullptr ? cb_off.data() : nullptr, cb_iters, s,
+                              any_harq ? harq.data() : nullptr, patches.data(), static_cast<uint32_t>(patches.size()));
+    if (rc != SRS_AMD_OK) {
+      return rc;
+    }
   }
   // the UCI decoders' helper stream rejoins (statuses read by the result kernel)
   e = proc->fan.end(s);
@@ -1079,7 +1291,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     a.port_counts  = proc->slot_ports.as<uint32_t>();
     a.stats_stride = STATS_STRIDE;
     a.stats_by_id  = out_stats != nullptr;
-    a.result_ids   = subset ? reinterpret_cast<const uint32_t*>(proc->slot_ports.as<uint8_t>() + o_ids) : nullptr;
+    a.result_ids   = reinterpret_cast<const uint32_t*>(proc->slot_ports.as<uint8_t>() + o_ids);
     if (nu != 0) { // the field masks follow the UCI descriptors (fused_uci)
       a.uci_status = proc->uci_status.as<int32_t>();
       a.uci_masks  = reinterpret_cast<const uint32_t*>(proc->uci_items.as<uint8_t>() + proc->uci_masks_offset);

@@ -678,6 +678,28 @@ hipError_t launch_harq_scatter(const harq_args& a, uint32_t max_soft_bytes, hipS
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(64) void slot_row_patch_kernel(const slot_row_patch* items)
+{
+  const slot_row_patch& p = items[blockIdx.x];
+  const int32_t         s = *p.sel;
+  if (s < 0) {
+    return;
+  }
+  for (uint32_t r = threadIdx.x; r < p.C; r += 64) {
+    p.row_E[r]  = p.cand_E[static_cast<size_t>(s) * p.C + r];
+    p.row_in[r] = p.llr_offset + p.cand_off[static_cast<size_t>(s) * p.C + r];
+  }
+}
+
+hipError_t launch_slot_row_patch(const slot_row_patch* items, uint32_t n, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(slot_row_patch_kernel, dim3(n), dim3(64), 0, stream, items);
+  return hipGetLastError();
+}
+
 hipError_t launch_harq_final(const harq_args& a, hipStream_t stream)
 {
   if (a.nof_tbs == 0) {

@@ -176,6 +176,19 @@ hipError_t launch_harq_scatter(const harq_args& a, uint32_t max_soft_bytes, hipS
 // After the assembly: a TB whose codeblocks all passed but whose TB CRC failed clears its CRC flags.
 hipError_t launch_harq_final(const harq_args& a, hipStream_t stream);
 
+// Slot decoder rows of a UE whose UL-SCH geometry is selected on the device (pusch_processor_args.h slot_ue_patch):
+// rows row_E[0 .. C) / row_in[0 .. C) of the uploaded descriptors take candidate *sel's lengths and offsets.
+struct slot_row_patch {
+  uint32_t*       row_E;
+  uint32_t*       row_in;
+  const int32_t*  sel;
+  const uint32_t* cand_E;   // [nof_cand][C]
+  const uint32_t* cand_off; // [nof_cand][C], relative to the UE's LLR row
+  uint32_t        llr_offset;
+  uint32_t        C;
+};
+hipError_t launch_slot_row_patch(const slot_row_patch* items, uint32_t n, hipStream_t stream);
+
 hipError_t launch_segment(const segment_args& a, hipStream_t stream);
 // true when launch_segment also attaches the codeblock CRCs (segment_crc_kernel)
 bool       segment_attaches_crc(const segment_args& a);

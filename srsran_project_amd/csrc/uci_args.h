@@ -23,6 +23,9 @@ struct uci_short_args {
   uint32_t      E;
   uint32_t      K;             // 1 .. 11
   uint32_t      qm;            // bits per modulation symbol
+  // slot form: decoded only when *pred == pred_val (pred null: always), see uci_slot_message
+  const int32_t* pred     = nullptr;
+  int32_t        pred_val = 0;
 };
 
 // Polar codeblocks already decoded (deallocated message bits, one per byte, rows of cb_stride): CRC check,
@@ -38,6 +41,8 @@ struct uci_polar_args {
   uint32_t       A0, F0;   // payload bits / filler bits of codeblock 0
   uint32_t       A1;       // payload bits of codeblock 1
   uint32_t       L;        // CRC bits (6 or 11)
+  const int32_t* pred     = nullptr; // slot form: as uci_short_args
+  int32_t        pred_val = 0;
 };
 
 hipError_t launch_uci_short(const uci_short_args& a, uint32_t nof, hipStream_t stream);
@@ -49,6 +54,10 @@ struct uci_slot_message {
   int32_t       modulation;
   uint8_t*      msg;
   int32_t*      status;
+  // decoded only when *pred == pred_val on the device (pred null: always): the CSI part 2 messages of a PDU, one per
+  // size its CSI part 1 may select, share the PDU's LLR row, payload and status and run only for the selected size
+  const int32_t* pred     = nullptr;
+  int32_t        pred_val = 0;
 };
 // The descriptors of a slot's UCI decoding (uci_decoder_impl.cpp:47-111 per message): the 1-11 bit messages for the
 // short-block kernel, every polar codeblock (its own code) for the polar decoder, the polar messages' CRC / filler

@@ -40,6 +40,9 @@ __global__ __launch_bounds__(64) void uci_short_kernel(uci_short_args own, const
 {
   const uci_short_args& a = MULTI ? items[blockIdx.x] : own;
   __shared__ int tmp[32];
+  if (MULTI && a.pred != nullptr && *a.pred != a.pred_val) {
+    return;
+  }
   const uint32_t row  = MULTI ? 0u : blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const int8_t*  in   = a.llrs + row * a.llr_stride;
@@ -194,6 +197,9 @@ __global__ __launch_bounds__(64) void uci_polar_finish_kernel(uci_polar_args own
   }
   const uci_polar_args& a   = MULTI ? items[i] : own;
   const uint32_t        row = MULTI ? 0u : i;
+  if (MULTI && a.pred != nullptr && *a.pred != a.pred_val) {
+    return;
+  }
   const uint8_t* cb0 = a.cbs + static_cast<uint64_t>(row) * a.C * a.cb_stride;
   uint8_t*       msg = a.msgs + row * a.msg_stride;
   int32_t* st = reinterpret_cast<int32_t*>(reinterpret_cast<uint8_t*>(a.status) + row * a.status_stride);

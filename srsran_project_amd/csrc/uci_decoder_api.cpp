@@ -77,7 +77,7 @@ int srs_amd::uci_slot_build(srs_amd_uci_decoder* dec, const uci_slot_message* ms
       return fail(SRS_AMD_EINVAL, "Invalid UCI payload size %u.", m.K);
     }
     if (m.K <= 11) {
-      out.shorts.push_back(uci_short_args{m.llrs, 0, m.msg, 0, m.status, 0, m.E, m.K, qm});
+      out.shorts.push_back(uci_short_args{m.llrs, 0, m.msg, 0, m.status, 0, m.E, m.K, qm, m.pred, m.pred_val});
       continue;
     }
     // polar codeblocks (uci_decoder_impl.cpp:47-76), as srs_amd_uci_decode_batch
@@ -102,9 +102,11 @@ int srs_amd::uci_slot_build(srs_amd_uci_decoder* dec, const uci_slot_message* ms
       a.llr_stride = r == 0 ? E0 : E1;
       a.msg_stride = static_cast<uint32_t>(cb_stride);
       a.nof        = 1;
+      a.pred       = m.pred;
+      a.pred_val   = m.pred_val;
       out.polars.push_back(a);
     }
-    out.finishes.push_back(uci_polar_args{cbs, cb_stride, m.msg, 0, m.status, 0, C, A0, F0, A1, L});
+    out.finishes.push_back(uci_polar_args{cbs, cb_stride, m.msg, 0, m.status, 0, C, A0, F0, A1, L, m.pred, m.pred_val});
     out.cb_bytes += C * cb_stride;
   }
   return SRS_AMD_OK;

@@ -25,7 +25,7 @@ __global__ __launch_bounds__(DMX_THREADS) void ulsch_demux_kernel(demux_args own
   const demux_args& a   = MULTI ? items[blockIdx.y] : own;
   const uint32_t    re  = blockIdx.x * DMX_THREADS + threadIdx.x;
   const uint64_t    row = MULTI ? 0u : blockIdx.y;
-  if (re >= a.nof_re) {
+  if (re >= a.nof_re || (MULTI && a.sel != nullptr && *a.sel != a.sel_val)) {
     return;
   }
   const uint32_t s = a.sch_map[re];

@@ -477,3 +477,13 @@ demux_args srs_amd::make_demux_args(const srs_amd_ulsch_demux_plan* plan, const 
   a.csi1_ph = plan->cfg.nof_csi_part1_bits <= 2 ? plan->cfg.nof_csi_part1_bits : 0u;
   return a;
 }
+
+demux_args srs_amd::make_demux_args_csi2(const srs_amd_ulsch_demux_plan* plan, const int8_t* cws, int8_t* sch,
+                                         int8_t* ack, int8_t* csi1, int8_t* csi2)
+{
+  demux_args a = make_demux_args(plan, cws, sch, ack, csi1);
+  a.csi2_map   = plan->pl.nof_csi2_re != 0 ? plan->d_maps + 2 * plan->pl.nof_re : nullptr;
+  a.csi2       = csi2;
+  a.csi2_ph    = plan->cfg.nof_csi_part2_bits <= 2 ? plan->cfg.nof_csi_part2_bits : 0u;
+  return a;
+}

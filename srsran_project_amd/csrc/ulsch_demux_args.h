@@ -39,6 +39,10 @@ struct demux_args {
   uint32_t        ack_ph;  // HARQ-ACK payload bits when 1 or 2 (placeholders), else 0
   uint32_t        csi1_ph; // CSI part 1 payload bits when 1 or 2, else 0
   uint32_t        csi2_ph; // CSI part 2 payload bits when 1 or 2, else 0
+  // slot form: the block runs only when *sel == sel_val (one block per CSI part 2 size candidate of a PDU, the size
+  // selected on the device from the decoded CSI part 1); sel null: always
+  const int32_t*  sel     = nullptr;
+  int32_t         sel_val = 0;
 };
 
 // Host placement (ulsch_demultiplex_impl.cpp:285-444) of every data RE of the codeword, in demodulator order.
@@ -54,5 +58,8 @@ hipError_t launch_ulsch_demux_items(const demux_args* items, uint32_t n, uint32_
 // The argument block of one codeword of `plan` (no CSI part 2): codeword LLRs cws, outputs sch / ack / csi1.
 demux_args make_demux_args(const srs_amd_ulsch_demux_plan* plan, const int8_t* cws, int8_t* sch, int8_t* ack,
                            int8_t* csi1);
+// The same with the plan's CSI part 2 placement (a plan created with nof_csi_part2_bits != 0) into csi2.
+demux_args make_demux_args_csi2(const srs_amd_ulsch_demux_plan* plan, const int8_t* cws, int8_t* sch, int8_t* ack,
+                                int8_t* csi1, int8_t* csi2);
 
 } // namespace srs_amd

@@ -8,6 +8,14 @@ every kind the reference's pusch_processor_impl::process serves in one slot (upl
   plain   64QAM, 2 layers, 4 rx ports (the fused slot path)
   plain2  QPSK, 1 layer, 4 rx ports, its own DM-RS symbols (the fused slot path)
 
+and, on request (kinds=...; they take the PRBs of tp / harq, so a slot holds them instead of those):
+
+  csi2    HARQ-ACK (2 bits) + CSI part 1 (12 bits) + CSI part 2 sized by CSI part 1 (two fields, 8 sizes) on the
+          UL-SCH, 16QAM, 25 PRB
+  ucionly no codeword (tbs = 0): HARQ-ACK (1 bit) + CSI part 1 (20 bits), QPSK (no CSI part 2: the reference sizes a
+          UCI-only PDU's CSI part 1 for "no CSI part 2" before the part 2 size is known, ulsch_info.cpp:96-123, so the
+          two cannot share a PDU consistently)
+
 Each UE's transmission comes from the reference's own transmit classes (oracle.pusch_proc.ue_transmit /
 ue_transmit_tp); the grid is their sum plus AWGN (the strong UEs at SNR_DB, the HARQ UE scaled to HARQ_SNR_DB).
 TEST INFRASTRUCTURE ONLY.
@@ -42,6 +50,17 @@ UES = [
     ("plain2", dict(rnti=0x5005, n_id=11, scrambling_id=110, rb_start=230, rb_count=43, modulation=2,
                     target_code_rate=679.0, nof_cdm_groups_without_data=1, dmrs_symbol_mask=1 << 3,
                     start_symbol_index=1, nof_symbols=12)),
+]
+
+
+PART2_CSI2 = [([(1, 1), (4, 2)], [3, 1, 2, 11, 30, 0, 64, 7])]
+UES_EXTRA = [
+    ("csi2", dict(rnti=0x5006, n_id=12, scrambling_id=120, rb_start=60, rb_count=25, modulation=4,
+                  target_code_rate=490.0, nof_harq_ack=2, nof_csi_part1=12, beta_offset_harq_ack=8.0,
+                  beta_offset_csi_part1=6.25, beta_offset_csi_part2=5.0, alpha_scaling=1.0, csi_part2_size=PART2_CSI2)),
+    ("ucionly", dict(rnti=0x5007, n_id=13, scrambling_id=130, rb_start=90, rb_count=10, modulation=2,
+                     target_code_rate=679.0, nof_harq_ack=1, nof_csi_part1=20, beta_offset_harq_ack=8.0,
+                     beta_offset_csi_part1=6.25, alpha_scaling=1.0)),
 ]
 
 
@@ -84,21 +103,24 @@ def mixed_slot(slot_index, harq_rv, seed, kinds=None):
     pdus, sent = [], []
     strong = None
     parts = []
-    for u, (kind, over) in enumerate(UES):
+    for u, (kind, over) in enumerate(UES + UES_EXTRA):
         if kind not in kinds:
             continue
         pdu = dict(BASE, **over, slot_index=slot_index)
         if kind == "harq":
             pdu.update(rv=harq_rv, new_data=int(harq_rv == 0))
-        tbs = tbs_of(pdu)
+        tbs = 0 if kind == "ucionly" else tbs_of(pdu)
         pdu["tbs"] = tbs
         pdu["base_graph"] = base_graph_of(tbs, pdu["target_code_rate"])
         tb_rng = np.random.default_rng(77 if kind == "harq" else 31 * seed + u)
         tb = tb_rng.integers(0, 256, tbs // 8, dtype=np.uint8)
         uci = None
-        if kind == "uci":
+        if kind in ("uci", "csi2", "ucionly"):
             uci = (rng.integers(0, 2, pdu["nof_harq_ack"]).astype(np.uint8),
                    rng.integers(0, 2, pdu["nof_csi_part1"]).astype(np.uint8))
+            if "csi_part2_size" in pdu:
+                n2 = amd.uci_part2_get_size(uci[1], amd.uci_part2_description(pdu["csi_part2_size"]))
+                uci = uci + (rng.integers(0, 2, n2).astype(np.uint8),)
         P = pdu["nof_rx_ports"]
         if kind == "tp":
             g, _ = pp.ue_transmit_tp(tb, pdu, NSUBC, channel=np.array([0.8, 0.3j, -0.5, 0.6 + 0.2j]))
@@ -122,6 +144,10 @@ def mixed_slot(slot_index, harq_rv, seed, kinds=None):
 
 
 def kind_of(pdu):
+    if pdu.get("tbs", 1) == 0:
+        return "ucionly"
+    if "csi_part2_size" in pdu:
+        return "csi2"
     if pdu.get("nof_harq_ack", 0) or pdu.get("nof_csi_part1", 0):
         return "uci"
     if pdu.get("transform_precoding", 0):

@@ -317,6 +317,77 @@ def test_pusch_slot_mixed_pdus_vs_reference():
                 assert want["tb_crc_ok"] and np.array_equal(got_tb, sent[u][0]), tag
 
 
+@pytest.mark.parametrize("slot_index", [3, 4, 6])
+def test_pusch_slot_csi_part2_uci_only_fused_vs_reference(slot_index, monkeypatch):
+    """PDUs with CSI part 2 (sized by their decoded CSI part 1) and UCI-only PDUs (no codeword,
+    HARQ-ACK + CSI part 1) in the FUSED slot group -- CSI part 2 size selected on the device, the
+    demultiplexer / UCI decoder / UL-SCH row geometry of the selected size, no host readback -- next to a HARQ-ACK +
+    CSI part 1 PDU and two plain PDUs on one four-port grid, against the compiled pusch_processor_impl called once per
+    PDU (pusch_processor_impl.cpp:56-103, :305-324): TB bytes, CRC flags, LDPC statistics, CSI, every UCI payload,
+    status and CSI part 2 size; and every output identical to the per-PDU batch chains (SRSRAN_AMD_PUSCH_FUSED=0).
+    The three slots' CSI part 1 payloads select different CSI part 2 sizes."""
+    import torch
+
+    from pusch_slot_cases import mixed_slot, kind_of, NSUBC
+
+    iters = 6
+    kinds = ["uci", "csi2", "ucionly", "plain", "plain2"]
+    grid, pdus, sent = mixed_slot(slot_index, 0, seed=slot_index, kinds=kinds)
+    assert sorted(kind_of(p) for p in pdus) == sorted(["uci", "csi2", "ucionly", "plain", "plain"])
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SRSRAN_AMD_PUSCH_FUSED", mode)
+        proc = amd.PuschProcessor(amd.PuschProcessorConfig(dec_nof_iterations=iters), device=0)
+        plans = [proc.plan(amd.make_pdu(**p), NSUBC) for p in pdus]
+        slot = amd.PuschSlot([(pl, 0) for pl in plans])
+        g = torch.from_numpy(grid.view(np.int32)[None]).to("cuda:0")
+        cbi = torch.full((max(slot.cb_total, 1),), -7, dtype=torch.int32, device="cuda:0")
+        uci = torch.zeros(max(slot.uci_total, 1), dtype=torch.uint8, device="cuda:0")
+        out, offs, res = proc.process_slot(g, slot, cb_iterations=cbi, uci=uci)
+        torch.cuda.synchronize()
+        outs[mode] = (out.cpu().numpy(), offs, res.cpu().numpy(), cbi.cpu().numpy(), uci.cpu().numpy(), slot, plans)
+    for a, b in zip(outs["1"][:5], outs["0"][:5]):
+        if isinstance(a, np.ndarray):
+            np.testing.assert_array_equal(a, b)
+        else:
+            assert list(a) == list(b)
+    out, offs, res, cbi, uci, slot, plans = outs["1"]
+    res = amd.pusch_processor.parse_results(res)
+    seen_sizes = []
+    for u, (pdu, pl) in enumerate(zip(pdus, plans)):
+        kind = kind_of(pdu)
+        tag = "slot %d %s" % (slot_index, kind)
+        P = pdu["nof_rx_ports"]
+        want_tb, want = pp.ref_pusch_process(grid[:P], pdu, pl.tb_bytes, iterations=iters)
+        got = res[u]
+        assert bool(got.data.tb_crc_ok) == want["tb_crc_ok"], tag
+        assert got.data.nof_codeblocks_total == want["nof_codeblocks_total"], tag
+        if kind != "ucionly":
+            assert np.array_equal(out[offs[u]:offs[u] + pl.tb_bytes], want_tb), tag
+            assert got.data.ldpc_iterations_sum == want["iterations_sum"], (tag, got.data, want)
+            c = cbi[slot.cb_offsets[u]:slot.cb_offsets[u] + pl.nof_codeblocks]
+            assert int(np.where(c >= 0, c, iters).sum()) == want["iterations_sum"], (tag, c)
+            assert want["tb_crc_ok"] and np.array_equal(want_tb, sent[u][0]), tag
+        _check_csi(got, want, tag)
+        if kind in ("uci", "csi2", "ucionly"):
+            row = uci[slot.uci_offsets[u]:slot.uci_offsets[u] + pl.uci_bytes]
+            n_ack, n_csi1 = pdu["nof_harq_ack"], pdu["nof_csi_part1"]
+            assert got.harq_ack_status == want["harq_ack_status"], tag
+            assert got.csi_part1_status == want["csi_part1_status"], tag
+            np.testing.assert_array_equal(row[:n_ack], want["harq_ack"], err_msg=tag)
+            np.testing.assert_array_equal(row[n_ack:n_ack + n_csi1], want["csi_part1"], err_msg=tag)
+            np.testing.assert_array_equal(want["harq_ack"], sent[u][1][0], err_msg=tag)
+            np.testing.assert_array_equal(want["csi_part1"], sent[u][1][1], err_msg=tag)
+            if kind == "csi2":
+                n2 = len(want["csi_part2"])
+                assert got.nof_csi_part2 == n2 == len(sent[u][1][2]), (tag, got.nof_csi_part2, n2)
+                assert got.csi_part2_status == want["csi_part2_status"], tag
+                np.testing.assert_array_equal(row[n_ack + n_csi1:n_ack + n_csi1 + n2], want["csi_part2"], err_msg=tag)
+                np.testing.assert_array_equal(want["csi_part2"], sent[u][1][2], err_msg=tag)
+                seen_sizes.append(n2)
+    assert len(seen_sizes) == 1
+
+
 def test_pusch_slot_rejects_unsupported():
     import torch
 
