@@ -98,9 +98,11 @@ typedef struct srs_amd_pusch_pdu {
   float    beta_offset_harq_ack;
   float    beta_offset_csi_part1;
   /* CSI part 2 (uci_description::csi_part2_size, beta_offset_csi_part2): its size comes from the decoded CSI part 1
-     (uci_part2_get_size, pusch_processor_impl.cpp:73-103); no entries: none.  srs_amd_pusch_process_batch then
-     decodes CSI part 1 first, reads it back (one host synchronisation) and demultiplexes and decodes CSI part 2
-     and the UL-SCH of each grid with the geometry of its CSI part 2 size. */
+     (uci_part2_get_size, pusch_processor_impl.cpp:73-103); no entries: none.  The processor decodes CSI part 1
+     first, selects each grid's CSI part 2 size on the device (among every size the description can produce; no host
+     synchronisation) and demultiplexes and decodes CSI part 2 and the UL-SCH of each grid with the geometry of that
+     size.  (A UCI-only PDU with CSI part 2 has no consistent geometry in the reference -- its CSI part 1 is sized for
+     "no CSI part 2", ulsch_info.cpp:96-123 -- and keeps a host readback that fails if a part 2 size is selected.) */
   float                              beta_offset_csi_part2;
   srs_amd_uci_part2_size_description csi_part2_size;
   /* pdu_t::dc_position (pusch_processor.h:161): subcarrier index of the DC within the resource grid (the FAPI PDU's
@@ -211,6 +213,11 @@ typedef struct srs_amd_pusch_slot_pdu {
   const uint32_t*                     d_grid;     /* non-NULL: this PDU's own DEVICE grid cbf16 [port][14][nof_subc]
                                                      (a device-resident resource grid, receive ports 0 .. P - 1),
                                                      instead of d_grids[grid] */
+  uint32_t                            soft_on_failure; /* new data with d_soft: 1 = its soft LLRs are written to
+                                                     d_soft only when the decoding leaves the transport block failed
+                                                     (the state a retransmission combines with, as an rx_buffer the
+                                                     reference would unlock rather than release); messages and CRC
+                                                     flags always.  0: every soft LLR written */
 } srs_amd_pusch_slot_pdu;
 
 /* Optional outputs of srs_amd_pusch_process_slot_ex (any member NULL: not returned). */
@@ -228,13 +235,14 @@ typedef struct srs_amd_pusch_slot_io {
  * (uplink_processor_impl.cpp:270-326) does by calling pusch_processor_impl::process once per PDU.  Result of
  * pdus[i] in d_results[i], transport block at d_tbs + pdus[i].tb_offset; per PDU identical to
  * srs_amd_pusch_process_batch on that PDU's grid.
- * The new-data, UCI-free, CP-OFDM PDUs without a soft buffer (the bulk of a slot) run fused: one channel-estimator
- * sequence over all of them (per-PDU argument blocks), one fused equalizer-demapper launch per (ports, layers,
- * equalizer) kind, one slot decoder sequence (srs_amd_pusch_decode_slot) and one result launch.  Every other PDU
- * -- HARQ retransmissions and new data kept in a soft buffer (d_soft), UCI on PUSCH (HARQ-ACK, CSI part 1, CSI
- * part 2), transform precoding -- runs in the same call on the same stream through the batch chain of its plan
- * (srs_amd_pusch_process_batch with one grid), before the fused group.  Plans created for the same nof_subc.
- * A PDU with CSI part 2 makes the call synchronise the stream once (its size comes from the decoded CSI part 1). */
+ * Every PDU whose equalizer kind the fused estimator-equalizer covers runs fused -- data, HARQ processes with a
+ * soft buffer (d_soft; early-stop decoding), UCI on PUSCH (HARQ-ACK, CSI part 1, CSI part 2 sized on the device from
+ * the decoded CSI part 1), UCI-only PDUs (tbs = 0), transform precoding: one channel-estimator sequence over all of
+ * them (per-PDU argument blocks), one fused equalizer-demapper launch per (ports, layers, equalizer) kind, one
+ * demultiplexer launch and one UCI decoder set over the UCI PDUs, one slot decoder sequence
+ * (srs_amd_pusch_decode_slot) and one result launch.  Other PDUs run in the same call on the same stream through the
+ * batch chain of their plan (srs_amd_pusch_process_batch with one grid), before the fused group.  Plans created for
+ * the same nof_subc.  No host synchronisation. */
 int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
                                   const srs_amd_pusch_slot_pdu*   pdus,
                                   uint32_t                        nof_pdus,

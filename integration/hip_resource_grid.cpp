@@ -1,6 +1,10 @@
 // hip_resource_grid.cpp -- device-resident srsran::resource_grid (see the header).
 #include "hip_resource_grid.h"
 
+#include "srsran_amd/grid.h"
+#include "srsran_amd/ldpc.h"
+
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -34,13 +38,15 @@ hip_resource_grid::hip_resource_grid(std::unique_ptr<resource_grid> host_, int d
     check(hipGetDevice(&dev), "hipGetDevice");
   }
   check(hipSetDevice(dev), "hipSetDevice");
-  check(hipMalloc(&d, sizeof(uint32_t) * ports * symbols * subc), "hipMalloc");
+  const size_t n = static_cast<size_t>(ports) * symbols * subc;
+  check(hipMalloc(&d, sizeof(uint32_t) * n), "hipMalloc");
   check(hipStreamCreateWithFlags(&own, hipStreamNonBlocking), "stream");
   check(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");
-  // the host mirror starts as the reference grid does (all zero): so does the device copy
-  check(hipMemsetAsync(d, 0, sizeof(uint32_t) * ports * symbols * subc, own), "hipMemsetAsync");
+  check(hipEventCreateWithFlags(&joiner, hipEventDisableTiming), "event");
+  // the host mirror starts as the reference grid does (all zero): so do the device copy and the agreed state
+  base.assign(n, 0u);
+  check(hipMemsetAsync(d, 0, sizeof(uint32_t) * n, own), "hipMemsetAsync");
   check(hipEventRecord(ready, own), "hipEventRecord");
-  producer = true;
 }
 
 hip_resource_grid::~hip_resource_grid()
@@ -53,104 +59,158 @@ hip_resource_grid::~hip_resource_grid()
     (void)hipEventSynchronize(ready);
     (void)hipEventDestroy(ready);
   }
+  if (joiner != nullptr) {
+    (void)hipEventDestroy(joiner);
+  }
   if (own != nullptr) {
     (void)hipStreamDestroy(own);
   }
   (void)hipFree(d);
+  (void)hipFree(d_delta);
+  (void)hipFree(d_rows);
 }
 
 void hip_resource_grid::set_all_zero()
 {
-  std::lock_guard<std::mutex> lock(mtx);
+  std::unique_lock<std::mutex> lock(mtx);
+  cv.wait(lock, [this] { return pending == 0; });
   host->set_all_zero();
+  std::fill(base.begin(), base.end(), 0u);
   check(hipSetDevice(dev), "hipSetDevice");
-  if (producer) {
-    check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
-  }
+  check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
   check(hipMemsetAsync(d, 0, sizeof(uint32_t) * ports * symbols * subc, own), "hipMemsetAsync");
   check(hipEventRecord(ready, own), "hipEventRecord");
-  producer     = true;
-  host_valid   = true;
-  device_valid = true;
+  host_dirty   = false;
+  view_open    = false; // the slot boundary: writes through earlier views are over
+  device_dirty = false;
 }
 
-void hip_resource_grid::host_access(bool write) const
+void hip_resource_grid::host_access(std::unique_lock<std::mutex>& lock, bool write) const
 {
-  // (the caller holds mtx)
-  if (!host_valid) {
+  // every device writer has published its completion (device_written)
+  cv.wait(lock, [this] { return pending == 0; });
+  if (device_dirty) {
+    // the device's changes since the last agreement: host ^= device ^ base, base = device
     auto* self = const_cast<hip_resource_grid*>(this);
     check(hipSetDevice(dev), "hipSetDevice");
     check(hipEventSynchronize(ready), "hipEventSynchronize");
-    // one row per (port, symbol): the host grid's writer views (which also mark the ports non-empty)
+    std::vector<uint32_t> now(base.size());
+    check(hipMemcpy(now.data(), d, sizeof(uint32_t) * now.size(), hipMemcpyDeviceToHost), "download");
     resource_grid_writer& w = self->host->get_writer();
     for (unsigned p = 0; p != ports; ++p) {
       for (unsigned l = 0; l != symbols; ++l) {
-        span<cbf16_t> v = w.get_view(p, l);
-        check(hipMemcpy(v.data(), d + (static_cast<size_t>(p) * symbols + l) * subc, sizeof(uint32_t) * subc,
-                        hipMemcpyDeviceToHost),
-              "download");
+        const size_t    o  = (static_cast<size_t>(p) * symbols + l) * subc;
+        const uint32_t* dv = now.data() + o;
+        uint32_t*       bv = base.data() + o;
+        if (std::memcmp(dv, bv, sizeof(uint32_t) * subc) == 0) {
+          continue;
+        }
+        // (the host grid's writer view also marks the port non-empty)
+        span<cbf16_t> v  = w.get_view(p, l);
+        auto*         hv = reinterpret_cast<uint32_t*>(v.data());
+        for (unsigned k = 0; k != subc; ++k) {
+          hv[k] ^= dv[k] ^ bv[k];
+          bv[k] = dv[k];
+        }
       }
     }
-    host_valid = true;
+    device_dirty = false;
     ++downloads;
   }
   if (write) {
-    device_valid = false;
+    host_dirty = true;
   }
 }
 
-void hip_resource_grid::device_access(hipStream_t stream, bool write)
+void hip_resource_grid::device_access(std::unique_lock<std::mutex>& lock, hipStream_t stream, bool write)
 {
-  // (the caller holds mtx)
   check(hipSetDevice(dev), "hipSetDevice");
-  if (!device_valid) {
-    if (producer) {
-      check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
-    }
+  if (!write) {
+    // readers see every producer (a writer does not need the others: disjoint REs)
+    cv.wait(lock, [this] { return pending == 0; });
+  }
+  if (host_dirty) {
+    // the host's changes since the last agreement: delta = host ^ base per changed row, applied on the device where
+    // non-zero (srs_amd_grid_merge_rows); base = host
+    const size_t          rows = static_cast<size_t>(ports) * symbols;
+    std::vector<uint32_t> delta, ids;
     const resource_grid_reader& r = host->get_reader();
     for (unsigned p = 0; p != ports; ++p) {
       for (unsigned l = 0; l != symbols; ++l) {
-        span<const cbf16_t> v = r.get_view(p, l);
-        check(hipMemcpyAsync(d + (static_cast<size_t>(p) * symbols + l) * subc, v.data(), sizeof(uint32_t) * subc,
-                             hipMemcpyHostToDevice, own),
-              "upload");
+        const size_t        o  = (static_cast<size_t>(p) * symbols + l) * subc;
+        span<const cbf16_t> v  = r.get_view(p, l);
+        const auto*         hv = reinterpret_cast<const uint32_t*>(v.data());
+        uint32_t*           bv = base.data() + o;
+        if (std::memcmp(hv, bv, sizeof(uint32_t) * subc) == 0) {
+          continue;
+        }
+        const size_t q = delta.size();
+        delta.resize(q + subc);
+        for (unsigned k = 0; k != subc; ++k) {
+          const uint32_t x = hv[k]; // read once: a writer may still be writing through its view
+          delta[q + k]     = x ^ bv[k];
+          bv[k]            = x;
+        }
+        ids.push_back(static_cast<uint32_t>(p * symbols + l));
       }
     }
-    check(hipEventRecord(ready, own), "hipEventRecord");
-    check(hipStreamSynchronize(own), "upload"); // pageable host memory: the copies are done when this returns
-    producer     = true;
-    device_valid = true;
-    ++uploads;
+    if (!ids.empty()) {
+      if (d_delta == nullptr) {
+        check(hipMalloc(&d_delta, sizeof(uint32_t) * rows * subc), "hipMalloc");
+        check(hipMalloc(&d_rows, sizeof(uint32_t) * rows), "hipMalloc");
+      }
+      check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
+      check(hipMemcpyAsync(d_delta, delta.data(), sizeof(uint32_t) * delta.size(), hipMemcpyHostToDevice, own), "upload");
+      check(hipMemcpyAsync(d_rows, ids.data(), sizeof(uint32_t) * ids.size(), hipMemcpyHostToDevice, own), "upload");
+      if (srs_amd_grid_merge_rows(d, d_delta, d_rows, static_cast<uint32_t>(ids.size()), subc, own) != SRS_AMD_OK) {
+        throw std::runtime_error(std::string("hip_resource_grid: merge: ") + srs_amd_last_error());
+      }
+      check(hipEventRecord(ready, own), "hipEventRecord");
+      check(hipStreamSynchronize(own), "upload"); // pageable host memory: the copies are done when this returns
+      ++uploads;
+    }
+    // a writable view still out: later writes are merged by the next device access -- until a device READER finds
+    // nothing new (a reader consumes the finished slot: the reference's host writers are done by then)
+    if (!write && ids.empty()) {
+      view_open = false;
+    }
+    host_dirty = view_open;
   }
-  if (producer) {
-    check(hipStreamWaitEvent(stream, ready, 0), "hipStreamWaitEvent");
-  }
+  check(hipStreamWaitEvent(stream, ready, 0), "hipStreamWaitEvent");
   if (write) {
-    host_valid = false;
+    device_dirty = true;
   }
 }
 
 const uint32_t* hip_resource_grid::device_read(hipStream_t stream)
 {
-  std::lock_guard<std::mutex> lock(mtx);
-  device_access(stream, false);
+  std::unique_lock<std::mutex> lock(mtx);
+  device_access(lock, stream, false);
   return d;
 }
 
 uint32_t* hip_resource_grid::device_write(hipStream_t stream)
 {
-  std::lock_guard<std::mutex> lock(mtx);
-  device_access(stream, true);
+  std::unique_lock<std::mutex> lock(mtx);
+  device_access(lock, stream, true);
+  ++pending;
   return d;
 }
 
 void hip_resource_grid::device_written(hipStream_t stream)
 {
-  std::lock_guard<std::mutex> lock(mtx);
-  check(hipSetDevice(dev), "hipSetDevice");
-  check(hipEventRecord(ready, stream), "hipEventRecord");
-  producer   = true;
-  host_valid = false;
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    check(hipSetDevice(dev), "hipSetDevice");
+    // ready := (every earlier producer) and (this writer): own waits for both, then records ready
+    check(hipEventRecord(joiner, stream), "hipEventRecord");
+    check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
+    check(hipStreamWaitEvent(own, joiner, 0), "hipStreamWaitEvent");
+    check(hipEventRecord(ready, own), "hipEventRecord");
+    device_dirty = true;
+    pending      = pending > 0 ? pending - 1 : 0;
+  }
+  cv.notify_all();
 }
 
 // ---- reader ----
@@ -170,43 +230,44 @@ unsigned hip_grid_reader::get_nof_symbols() const
 bool hip_grid_reader::is_empty(unsigned port) const
 {
   std::lock_guard<std::mutex> lock(grid.mtx);
-  return grid.host_valid && grid.host->get_reader().is_empty(port); // written on the device: not empty
+  // written on the device (or being written): not empty
+  return grid.pending == 0 && !grid.device_dirty && grid.host->get_reader().is_empty(port);
 }
 bool hip_grid_reader::is_empty() const
 {
   std::lock_guard<std::mutex> lock(grid.mtx);
-  return grid.host_valid && grid.host->get_reader().is_empty();
+  return grid.pending == 0 && !grid.device_dirty && grid.host->get_reader().is_empty();
 }
 span<cf_t> hip_grid_reader::get(span<cf_t> symbols, unsigned port, unsigned l, unsigned k_init,
                                 const bounded_bitset<MAX_RB * NRE>& mask) const
 {
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(false);
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, false);
   return grid.host->get_reader().get(symbols, port, l, k_init, mask);
 }
 span<cbf16_t> hip_grid_reader::get(span<cbf16_t> symbols, unsigned port, unsigned l, unsigned k_init,
                                    const bounded_bitset<MAX_RB * NRE>& mask) const
 {
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(false);
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, false);
   return grid.host->get_reader().get(symbols, port, l, k_init, mask);
 }
 void hip_grid_reader::get(span<cf_t> symbols, unsigned port, unsigned l, unsigned k_init, unsigned stride) const
 {
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(false);
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, false);
   grid.host->get_reader().get(symbols, port, l, k_init, stride);
 }
 void hip_grid_reader::get(span<cbf16_t> symbols, unsigned port, unsigned l, unsigned k_init) const
 {
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(false);
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, false);
   grid.host->get_reader().get(symbols, port, l, k_init);
 }
 span<const cbf16_t> hip_grid_reader::get_view(unsigned port, unsigned l) const
 {
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(false);
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, false);
   return grid.host->get_reader().get_view(port, l);
 }
 
@@ -227,34 +288,36 @@ unsigned hip_grid_writer::get_nof_symbols() const
 span<const cf_t> hip_grid_writer::put(unsigned port, unsigned l, unsigned k_init,
                                       const bounded_bitset<NRE * MAX_RB>& mask, span<const cf_t> symbols)
 {
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(true);
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, true);
   return grid.host->get_writer().put(port, l, k_init, mask, symbols);
 }
 span<const cbf16_t> hip_grid_writer::put(unsigned port, unsigned l, unsigned k_init,
                                          const bounded_bitset<NRE * MAX_RB>& mask, span<const cbf16_t> symbols)
 {
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(true);
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, true);
   return grid.host->get_writer().put(port, l, k_init, mask, symbols);
 }
 void hip_grid_writer::put(unsigned port, unsigned l, unsigned k_init, span<const cf_t> symbols)
 {
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(true);
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, true);
   grid.host->get_writer().put(port, l, k_init, symbols);
 }
 void hip_grid_writer::put(unsigned port, unsigned l, unsigned k_init, unsigned stride, span<const cbf16_t> symbols)
 {
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(true);
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, true);
   grid.host->get_writer().put(port, l, k_init, stride, symbols);
 }
 span<cbf16_t> hip_grid_writer::get_view(unsigned port, unsigned l)
 {
-  // the caller writes through the view after this returns: the device copy is stale from here on
-  std::lock_guard<std::mutex> lock(grid.mtx);
-  grid.host_access(true);
+  // the caller writes through the view after this returns (the reference's mapper and PRS generator do): the host
+  // side stays dirty until the slot boundary, so writes made after a device access are merged by the next one
+  std::unique_lock<std::mutex> lock(grid.mtx);
+  grid.host_access(lock, true);
+  grid.mark_view_open();
   return grid.host->get_writer().get_view(port, l);
 }
 

@@ -9,11 +9,20 @@
 // the OFDM modulator plug-in the same way.  Every other component keeps the reference interfaces: the first host
 // access after a device write downloads the grid (once), the first device access after a host write uploads it.
 //
-// Coherence: two validity flags (host, device) and the completion event of the last device producer.  A reader or
-// writer call makes the host copy valid first; a writer call then marks the device copy stale.  device_read /
-// device_write make the device copy valid on the caller's stream (waiting for the last producer there);
-// device_write also marks the host copy stale, and device_written records the producer's completion event.
-// Calls are serialised per grid by a mutex, so the reference's concurrent channel processors may share a grid.
+// Coherence (r06): a three-way merge against the state both copies last agreed on (`base`, a host array).  Host
+// writers (the reference's channel processors through put / get_view) change the host mirror, device writers (the
+// plug-ins' kernels) the device copy, concurrently and on disjoint REs as the downlink processor's executors do
+// (downlink_processor_multi_executor_impl.cpp).  Before a device access the host's changes go up as the XOR of each
+// changed row with `base`, applied on the device only where non-zero (srs_amd_grid_merge_rows), so REs the device
+// wrote meanwhile stay; before a host access the device's changes come down the same way (host ^= device ^ base), so
+// REs the host wrote meanwhile stay.  A writable view handed out by get_view keeps the host side dirty until the slot
+// boundary (set_all_zero) or until a device reader finds no host change left (readers consume the finished slot):
+// writes through it after an upload are merged by the next device access.  Every device
+// writer is tracked: device_write / device_written bracket it (a pending count host accesses and device readers wait
+// for), and each device_written joins its stream into the `ready` event (the own stream waits for the old `ready` and
+// the writer's event, then records `ready` again), so readers wait for every producer, not only the last.  Calls are
+// serialised per grid by a mutex.  An RE written on both sides between two merges keeps neither value exactly (XOR):
+// the reference's processors never write the same RE twice in a slot.
 #pragma once
 
 #include "srsran/phy/support/resource_grid.h"
@@ -23,9 +32,11 @@
 
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdint>
 #include <memory>
 #include <mutex>
+#include <vector>
 
 namespace srsran {
 namespace hip {
@@ -109,20 +120,28 @@ public:
 private:
   friend class hip_grid_reader;
   friend class hip_grid_writer;
-  // the host mirror valid (download when the device copy is newer); write: the device copy then becomes stale
-  void host_access(bool write) const;
-  // the device copy valid on `stream` (upload when the host mirror is newer)
-  void device_access(hipStream_t stream, bool write);
+  // the host mirror current (the device's changes merged in); write: the host side becomes dirty.  lock: mtx, held
+  void host_access(std::unique_lock<std::mutex>& lock, bool write) const;
+  // the device copy current on `stream` (the host's changes merged in; readers also wait for pending writers)
+  void device_access(std::unique_lock<std::mutex>& lock, hipStream_t stream, bool write);
+  // a writable view is out (get_view): the host side stays dirty until the slot boundary
+  void mark_view_open() const { view_open = true; }
 
   std::unique_ptr<resource_grid> host;
   unsigned                       ports = 0, symbols = 0, subc = 0;
   int                            dev   = 0;
   uint32_t*                      d     = nullptr;
-  hipEvent_t                     ready = nullptr; // the last device producer's completion
-  hipStream_t                    own   = nullptr; // transfers
-  mutable std::mutex             mtx;
-  mutable bool                   host_valid = true, device_valid = true, producer = false;
-  mutable uint64_t               downloads = 0, uploads = 0;
+  hipEvent_t                     ready  = nullptr; // every device producer's completion (joined on `own`)
+  hipEvent_t                     joiner = nullptr; // a writer's completion, joined into `ready`
+  hipStream_t                    own    = nullptr; // transfers, merges, joins
+  mutable std::mutex              mtx;
+  mutable std::condition_variable cv;              // pending reaches 0
+  mutable std::vector<uint32_t>   base;            // the state host and device copies last agreed on
+  mutable bool                    host_dirty = false, view_open = false, device_dirty = false;
+  mutable int                     pending    = 0;  // device writers between device_write and device_written
+  mutable uint32_t*               d_delta    = nullptr; // merge staging: changed rows' XOR deltas, their row indices
+  mutable uint32_t*               d_rows     = nullptr;
+  mutable uint64_t                downloads = 0, uploads = 0;
   hip_grid_reader                reader;
   hip_grid_writer                writer;
 };

@@ -336,6 +336,7 @@ private:
     srs_amd_pdsch_mod_plan*          plan   = nullptr;
     uint32_t                         nof_re = 0; // data REs per layer (pdsch_compute_nof_data_re)
     std::list<std::string>::iterator lru;
+    uint64_t                         last_seq = 0; // the last batch that used the plan (eviction: completed_seq)
   };
 
   struct buffer_set {
@@ -351,6 +352,7 @@ private:
   };
 
   struct job {
+    uint64_t                 seq = 0; // dispatch sequence number (plan eviction)
     std::vector<pending_pdu> pdus;
     std::vector<host_grid>   hosts;
     buffer_set*              bs     = nullptr;
@@ -363,6 +365,7 @@ private:
     auto        it = plans.find(key);
     if (it != plans.end()) {
       lru.splice(lru.begin(), lru, it->second.lru);
+      it->second.last_seq = cur_seq;
       return &it->second;
     }
     plan_entry e;
@@ -371,25 +374,28 @@ private:
       return nullptr;
     }
     lru.push_front(key);
-    e.lru = lru.begin();
+    e.lru      = lru.begin();
+    e.last_seq = cur_seq;
     return &plans.emplace(key, e).first->second;
   }
 
+  // Least recently used plans beyond the cache size, once no dispatched batch can still use them: a plan last used
+  // by batch n is free when batch n has completed (batches complete in dispatch order).  (the r05 form
+  // evicted only when nothing was in flight, which never happens under back-to-back slots.)
   void evict_plans()
   {
-    {
-      std::lock_guard<std::mutex> lock(jmtx);
-      if (!jobs.empty() || completing) {
-        return; // a batch in flight may still use a plan
-      }
-    }
+    const uint64_t done = completed_seq.load();
     while (plans.size() > cfg.max_cached_plans && !lru.empty()) {
       auto it = plans.find(lru.back());
+      if (it->second.last_seq > done) {
+        break; // the least recently used plan may still be in flight, and so may every more recent one
+      }
       srs_amd_pdsch_mod_plan_destroy(it->second.plan);
       plans.erase(it);
       lru.pop_back();
     }
   }
+
 
   buffer_set* acquire_set()
   {
@@ -417,8 +423,10 @@ private:
       return n;
     }
     evict_plans();
+    cur_seq = ++dispatch_seq;
     // plans, segmentation, the writers' device grids
     auto                                j = std::make_unique<job>();
+    j->seq                                = cur_seq;
     std::vector<plan_entry*>            pl;
     std::vector<srs_amd_pdsch_ue>       ues;
     std::vector<srs_amd_pdsch_slot_pdu> sp;
@@ -588,6 +596,7 @@ private:
       }
       (void)hipSetDevice(device);
       complete(*j);
+      completed_seq.store(j->seq); // batches complete in dispatch order
       buffer_set* bs = j->bs;
       j.reset();
       {
@@ -670,6 +679,8 @@ private:
   std::condition_variable                     jcv;
   std::deque<std::unique_ptr<job>>            jobs;
   bool                                        completing = false, stop = false;
+  uint64_t                          dispatch_seq = 0, cur_seq = 0; // collector thread: batches dispatched / this one
+  std::atomic<uint64_t>             completed_seq{0};              // the last batch the completion thread finished
   std::thread                                 completer;
   std::unique_ptr<slot_collector<pending_pdu>> collector; // last: stops before the state it uses goes
 };

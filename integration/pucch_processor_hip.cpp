@@ -147,6 +147,9 @@ public:
     result.message = pucch_uci_message({.nof_sr = config.sr_opportunity ? 1U : 0U,
                                         .nof_harq_ack = config.nof_harq_ack, .nof_csi_part1 = 0, .nof_csi_part2 = 0});
     result.message.set_status(uci_status::invalid);
+    if (!normal_cp(config.cp)) {
+      return result;
+    }
     srs_amd_pucch_f0_pdu p = convert(config);
     unsigned             nof_ports = 0, nsubc = 0;
     const uint32_t*      g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
@@ -190,6 +193,9 @@ public:
       out.insert(e.initial_cyclic_shift, e.time_domain_occ, r);
     }
     st->nof_pdus += entries.size();
+    if (!normal_cp(c.cp)) {
+      return out;
+    }
     // the reference's Format 1 detector reads every port of the grid, 0 .. nof_ports - 1
     // (pucch_detector_format1.cpp:529, 568-583)
     srs_amd_pucch_f1_batch b{};
@@ -244,6 +250,9 @@ public:
     result.message = pucch_uci_message({.nof_sr = config.nof_sr, .nof_harq_ack = config.nof_harq_ack,
                                         .nof_csi_part1 = config.nof_csi_part1, .nof_csi_part2 = config.nof_csi_part2});
     result.message.set_status(uci_status::invalid);
+    if (!normal_cp(config.cp)) {
+      return result;
+    }
     srs_amd_pucch_f2_pdu p = convert(config);
     const unsigned       K = config.nof_sr + config.nof_harq_ack + config.nof_csi_part1 + config.nof_csi_part2;
     unsigned             nof_ports = 0, nsubc = 0;
@@ -263,13 +272,13 @@ public:
   pucch_processor_result process(const resource_grid_reader& grid, const format3_configuration& config) override
   {
     return process34(grid, convert34(config, 3, config.nof_prb, 0, 1), config.nof_sr, config.nof_harq_ack,
-                     config.nof_csi_part1, config.nof_csi_part2);
+                     config.nof_csi_part1, config.nof_csi_part2, config.cp);
   }
 
   pucch_processor_result process(const resource_grid_reader& grid, const format4_configuration& config) override
   {
     return process34(grid, convert34(config, 4, 1, config.occ_index, config.occ_length), config.nof_sr,
-                     config.nof_harq_ack, config.nof_csi_part1, config.nof_csi_part2);
+                     config.nof_harq_ack, config.nof_csi_part1, config.nof_csi_part2, config.cp);
   }
 
 private:
@@ -277,14 +286,29 @@ private:
   static constexpr size_t PAYLOAD_OFF = 256;
 
   // Formats 3 / 4: the PDU's symbols through srs_amd_pucch_f34_process_slot, the message and CSI back.
+  // Extended cyclic prefix: the plug-in's kernels are built for 14 symbols per slot; such a PDU is reported as not
+  // processed (invalid status) and counted as an error, as the validator rejects it
+  bool normal_cp(cyclic_prefix cp)
+  {
+    if (cp == cyclic_prefix::NORMAL) {
+      return true;
+    }
+    ++st->nof_errors;
+    log_error("PDU not processed", "extended cyclic prefix");
+    return false;
+  }
+
   pucch_processor_result process34(const resource_grid_reader& grid, srs_amd_pucch_f34_pdu p, unsigned sr,
-                                   unsigned harq, unsigned csi1, unsigned csi2)
+                                   unsigned harq, unsigned csi1, unsigned csi2, cyclic_prefix cp)
   {
     ++st->nof_pdus;
     pucch_processor_result result;
     result.message = pucch_uci_message({.nof_sr = sr, .nof_harq_ack = harq, .nof_csi_part1 = csi1,
                                         .nof_csi_part2 = csi2});
     result.message.set_status(uci_status::invalid);
+    if (!normal_cp(cp)) {
+      return result;
+    }
     const unsigned  K         = sr + harq + csi1 + csi2;
     unsigned        nof_ports = 0, nsubc = 0;
     const uint32_t* g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
@@ -411,8 +435,9 @@ private:
   void*                         h_res         = nullptr;
 };
 
-// pucch_pdu_validator_impl (pucch_processor_impl.cpp:399-760) for the formats the plug-in builds; Formats 3 / 4 are
-// reported as unsupported.
+// pucch_pdu_validator_impl (pucch_processor_impl.cpp:399-760) for every format the plug-in builds (0-4), normal cyclic
+// prefix only (the reference also accepts extended: the plug-in reports it unsupported, as the PUSCH / PDSCH / PDCCH
+// plug-ins do).
 class pucch_pdu_validator_hip : public pucch_pdu_validator
 {
 public:
@@ -420,6 +445,9 @@ public:
 
   error_type<std::string> is_valid(const pucch_processor::format0_configuration& c) const override
   {
+    if (c.cp != cyclic_prefix::NORMAL) {
+      return make_unexpected(std::string("extended cyclic prefix"));
+    }
     if (c.bwp_start_rb + c.bwp_size_rb > cfg.max_nof_prb || c.starting_prb >= c.bwp_size_rb ||
         (c.second_hop_prb.has_value() && *c.second_hop_prb >= c.bwp_size_rb)) {
       return make_unexpected(std::string("PRB allocation outside the BWP or the grid"));
@@ -435,6 +463,9 @@ public:
   }
   error_type<std::string> is_valid(const pucch_processor::format1_configuration& c) const override
   {
+    if (c.cp != cyclic_prefix::NORMAL) {
+      return make_unexpected(std::string("extended cyclic prefix"));
+    }
     const unsigned ratio = c.second_hop_prb.has_value() ? 4 : 2;
     if (c.bwp_start_rb + c.bwp_size_rb > cfg.max_nof_prb || c.starting_prb >= c.bwp_size_rb ||
         (c.second_hop_prb.has_value() && *c.second_hop_prb >= c.bwp_size_rb)) {
@@ -449,6 +480,9 @@ public:
   }
   error_type<std::string> is_valid(const pucch_processor::format2_configuration& c) const override
   {
+    if (c.cp != cyclic_prefix::NORMAL) {
+      return make_unexpected(std::string("extended cyclic prefix"));
+    }
     const unsigned K = c.nof_harq_ack + c.nof_sr + c.nof_csi_part1 + c.nof_csi_part2;
     const unsigned E = 16 * c.nof_prb * c.nof_symbols;
     const unsigned A = K <= 11 ? 0 : (K <= 19 ? 6 : 11);
@@ -486,6 +520,9 @@ private:
   template <typename C>
   error_type<std::string> f34_ok(const C& c, unsigned nprb, bool f4, unsigned occ) const
   {
+    if (c.cp != cyclic_prefix::NORMAL) {
+      return make_unexpected(std::string("extended cyclic prefix"));
+    }
     static const unsigned masks[2][15] = {{0, 0, 0, 0, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2},
                                           {0, 0, 0, 0, 2, 2, 2, 2, 2, 2, 4, 4, 4, 4, 4}};
     if (c.bwp_start_rb + c.bwp_size_rb > cfg.max_nof_prb || c.starting_prb + nprb > c.bwp_size_rb) {

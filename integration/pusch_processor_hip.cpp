@@ -252,7 +252,8 @@ public:
     s.nof_pdus            = c.nof_pdus;
     s.nof_batches         = c.nof_batches;
     s.nof_errors          = c.nof_errors + stats_late_errors;
-    s.nof_harq_redecodes  = stats_redecodes;
+    s.nof_harq_redecodes  = 0; // one decoding per PDU: a failed new transmission's soft buffer is downloaded
+    s.nof_harq_soft_downloads = stats_soft_downloads;
     s.nof_retransmissions = stats_retx;
     s.nof_device_grids    = stats_device_grids;
     return s;
@@ -265,6 +266,7 @@ private:
     uint64_t                         soft_bytes = 0;
     srs_amd_sch_plan                 sch{};
     std::list<std::string>::iterator lru;
+    uint64_t                         last_seq = 0; // the last batch that used the plan (eviction: completed_seq)
   };
 
   /// One alternating set of the batch's pinned / device buffers.
@@ -276,6 +278,7 @@ private:
 
   /// A dispatched batch, waiting for its completion.
   struct job {
+    uint64_t                            seq = 0;  // dispatch sequence number (plan eviction)
     std::vector<pending_pdu>            pdus;     // the live PDUs, in slot-call order
     std::vector<plan_entry>             pl;       // their plans (copies: eviction waits for idle)
     std::vector<srs_amd_pusch_slot_pdu> sp;       // the slot call's PDUs
@@ -311,24 +314,27 @@ private:
     }
     // the plan is shared by every slot of this configuration: each PDU carries its own slot in the slot call
     // (srs_amd_pusch_slot_pdu::has_slot), so PDUs of two slots in one batch keep their own DM-RS sequences
+    it->second.last_seq = cur_seq;
     return &it->second;
   }
 
+  // Least recently used plans beyond the cache size, once no dispatched batch can still use them: a plan last used
+  // by batch n is free when batch n has completed (batches complete in dispatch order).  (the r05 form
+  // evicted only when nothing was in flight, which never happens under back-to-back slots.)
   void evict_plans()
   {
-    {
-      std::lock_guard<std::mutex> lock(jmtx);
-      if (!jobs.empty() || completing) {
-        return; // a batch in flight may still use a plan
-      }
-    }
+    const uint64_t done = completed_seq.load();
     while (plans.size() > cfg.max_cached_plans && !lru.empty()) {
       auto it = plans.find(lru.back());
+      if (it->second.last_seq > done) {
+        break; // the least recently used plan may still be in flight, and so may every more recent one
+      }
       srs_amd_pusch_processor_plan_destroy(it->second.plan);
       plans.erase(it);
       lru.pop_back();
     }
   }
+
 
   // A transmission that could not be processed: the reference's "no dependencies" notification
   // (pusch_processor_impl.cpp:140-157).
@@ -384,7 +390,9 @@ private:
       return n;
     }
     evict_plans();
+    cur_seq = ++dispatch_seq;
     auto j = std::make_unique<job>();
+    j->seq = cur_seq;
     // plans, and the PDUs that go to the GPU
     for (unsigned i = 0; i != n; ++i) {
       pending_pdu& p  = batch[i];
@@ -535,7 +543,12 @@ private:
       u.d_grid     = dev_grid[k];
       u.cb_offset  = j->cb_off[k];
       u.tb_offset  = j->tb_off[k];
-      u.d_soft     = j->pdus[k].c.new_data ? nullptr : reinterpret_cast<int8_t*>(bs->soft.d + j->soft_off[k]);
+      // a PDU with an rx_buffer decodes into its device soft buffer: a retransmission combines with it, a new
+      // transmission keeps its soft LLRs only when its TB fails (soft_on_failure), as the reference's single decode
+      // leaves them in the rx_buffer it then unlocks (pusch_decoder_impl.cpp:324-360)
+      u.d_soft          = j->pdus[k].rm_buffer.is_valid() ? reinterpret_cast<int8_t*>(bs->soft.d + j->soft_off[k])
+                                                          : nullptr;
+      u.soft_on_failure = j->pdus[k].c.new_data ? 1u : 0u;
       u.uci_offset = j->uci_off[k];
       u.has_slot   = 1;
       u.numerology = j->pdus[k].c.numerology;
@@ -545,8 +558,12 @@ private:
     hipError_t e = grids.empty() ? hipSuccess
                                  : hipMemcpyAsync(bs->h_grids.d, bs->h_grids.h, grids.size() * j->grid_stride * 4,
                                                   hipMemcpyHostToDevice, stream);
-    if (e == hipSuccess && soft_total != 0) {
-      e = hipMemcpyAsync(bs->soft.d, bs->soft.h, soft_total, hipMemcpyHostToDevice, stream);
+    // retransmissions' soft buffers up (new transmissions start from a cleared buffer on the device)
+    for (size_t k = 0; k != m && e == hipSuccess; ++k) {
+      if (!j->pdus[k].c.new_data) {
+        e = hipMemcpyAsync(bs->soft.d + j->soft_off[k], bs->soft.h + j->soft_off[k], j->pl[k].soft_bytes,
+                           hipMemcpyHostToDevice, stream);
+      }
     }
     int rc = e == hipSuccess ? run_slot(*j, j->sp, stream) : SRS_AMD_EHIP;
     e      = rc == SRS_AMD_OK ? download(*j, stream) : hipErrorUnknown;
@@ -582,6 +599,7 @@ private:
       }
       (void)hipSetDevice(device);
       complete(*j);
+      completed_seq.store(j->seq); // batches complete in dispatch order
       buffer_set* bs = j->bs;
       j.reset();
       {
@@ -615,41 +633,33 @@ private:
       }
       return;
     }
-    // new transmissions whose TB CRC failed and that keep HARQ state: decoded again with a soft buffer (the same
-    // decoding, now with its soft bits kept), then written to the rx_buffer
-    const auto*                         res = reinterpret_cast<const srs_amd_pusch_processor_result*>(bs->results.h);
-    std::vector<char>                   keep(m, 0); // the rx_buffer takes the soft buffer's state after the call
-    std::vector<srs_amd_pusch_slot_pdu> again;
-    std::vector<unsigned>               again_ids;
+    // new transmissions whose TB CRC failed and that keep HARQ state: the first (and only) decoding left their soft
+    // LLRs, messages and CRC flags in the device soft buffer -- downloaded now (failed TBs only), then written to the
+    // rx_buffer
+    const auto*           res = reinterpret_cast<const srs_amd_pusch_processor_result*>(bs->results.h);
+    std::vector<char>     keep(m, 0); // the rx_buffer takes the soft buffer's state after the call
+    std::vector<unsigned> failed;
     for (size_t k = 0; k != m; ++k) {
       keep[k] = !j.pdus[k].c.new_data;
       if (j.pdus[k].c.new_data && j.pdus[k].c.tbs != 0 && j.pdus[k].rm_buffer.is_valid() && !res[k].data.tb_crc_ok) {
-        srs_amd_pusch_slot_pdu u = j.sp[k];
-        u.d_soft                 = reinterpret_cast<int8_t*>(bs->soft.d + j.soft_off[k]);
-        again.push_back(u);
-        again_ids.push_back(static_cast<unsigned>(k));
+        failed.push_back(static_cast<unsigned>(k));
       }
     }
-    if (!again.empty()) {
-      stats_redecodes += again.size();
+    if (!failed.empty()) {
+      stats_soft_downloads += failed.size();
       hipError_t e = hipSuccess;
-      for (unsigned k : again_ids) {
-        e = e == hipSuccess ? hipMemsetAsync(bs->soft.d + j.soft_off[k], 0, j.pl[k].soft_bytes, stream2) : e;
-      }
-      int rc = e == hipSuccess ? run_slot(j, again, stream2, &again_ids) : SRS_AMD_EHIP;
-      for (unsigned k : again_ids) {
-        e = (rc == SRS_AMD_OK && e == hipSuccess)
-                ? hipMemcpyAsync(bs->soft.h + j.soft_off[k], bs->soft.d + j.soft_off[k], j.pl[k].soft_bytes,
-                                 hipMemcpyDeviceToHost, stream2)
-                : e;
+      for (unsigned k : failed) {
+        e = e == hipSuccess ? hipMemcpyAsync(bs->soft.h + j.soft_off[k], bs->soft.d + j.soft_off[k], j.pl[k].soft_bytes,
+                                             hipMemcpyDeviceToHost, stream2)
+                            : e;
       }
       e = e == hipSuccess ? hipStreamSynchronize(stream2) : e;
-      if (rc != SRS_AMD_OK || e != hipSuccess) {
+      if (e != hipSuccess) {
         // the rx_buffers are left as they were (the transport blocks report their CRC failure either way)
-        log_error("HARQ soft-buffer pass", rc != SRS_AMD_OK ? std::string(srs_amd_last_error()) : hipGetErrorString(e));
+        log_error("HARQ soft-buffer download", hipGetErrorString(e));
         (void)hipStreamSynchronize(stream2);
       } else {
-        for (unsigned k : again_ids) {
+        for (unsigned k : failed) {
           keep[k] = 1;
         }
       }
@@ -712,7 +722,14 @@ private:
     d2h(bs->cbi, sizeof(int32_t) * j.cb_total);
     d2h(bs->uci, j.uci_total);
     d2h(bs->pstats, sizeof(srs_amd_chest_port_stats) * MAX_PORTS_HIP * m);
-    d2h(bs->soft, j.soft_total);
+    // retransmissions' soft buffers (their state goes back to the rx_buffer whatever the outcome); new transmissions'
+    // only if their TB fails (complete())
+    for (size_t k = 0; k != m && e == hipSuccess; ++k) {
+      if (!j.pdus[k].c.new_data) {
+        e = hipMemcpyAsync(bs->soft.h + j.soft_off[k], bs->soft.d + j.soft_off[k], j.pl[k].soft_bytes,
+                           hipMemcpyDeviceToHost, s);
+      }
+    }
     return e;
   }
 
@@ -844,7 +861,7 @@ private:
   }
 
 public:
-  std::atomic<uint64_t> stats_retx{0}, stats_redecodes{0}, stats_late_errors{0}, stats_device_grids{0};
+  std::atomic<uint64_t> stats_retx{0}, stats_soft_downloads{0}, stats_late_errors{0}, stats_device_grids{0};
 
 private:
   pusch_processor_hip_config cfg;
@@ -863,6 +880,8 @@ private:
   std::condition_variable           jcv;
   std::deque<std::unique_ptr<job>>  jobs;
   bool                              completing = false, stop = false;
+  uint64_t                          dispatch_seq = 0, cur_seq = 0; // collector thread: batches dispatched / this one
+  std::atomic<uint64_t>             completed_seq{0};              // the last batch the completion thread finished
   std::thread                       completer;
   // last: destroyed first, so the collector thread stops before the state it uses goes
   std::unique_ptr<slot_collector<pending_pdu>> collector;

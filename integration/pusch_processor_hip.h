@@ -87,10 +87,12 @@ public:
   virtual void flush() = 0;
   /// Blocks until no PDU is pending or being processed (every notifier of the PDUs queued so far was called).
   virtual void wait_idle() = 0;
-  /// Counters: PDUs processed, batches run, failed (error-reported) PDUs, new-data TBs decoded again with a soft
-  /// buffer, retransmissions.
+  /// Counters: PDUs processed, batches run, failed (error-reported) PDUs, new-data TBs decoded again (always 0 since
+  /// r06: one decoding keeps the soft state), retransmissions, failed new-data TBs whose device soft buffer went to
+  /// their rx_buffer.
   struct statistics {
     uint64_t nof_pdus = 0, nof_batches = 0, nof_errors = 0, nof_harq_redecodes = 0, nof_retransmissions = 0;
+    uint64_t nof_harq_soft_downloads = 0;
     /// PDUs whose received grid was a hip_resource_grid read in place (no host staging, no PCIe copy).
     uint64_t nof_device_grids = 0;
   };

@@ -211,8 +211,10 @@ public:
     }
     cv.notify_all();
     drain();
+    // every item done AND every worker out of drain(): a worker still inside could otherwise fetch an index of the
+    // next run (after its reset of `next`) and count it against the wrong run
     std::unique_lock<std::mutex> g(mtx);
-    done_cv.wait(g, [&] { return done.load() == count; });
+    done_cv.wait(g, [&] { return done.load() == count && active == 0; });
     job = nullptr;
   }
 
@@ -238,8 +240,14 @@ private:
           return;
         }
         seen = generation;
+        ++active; // under the lock that run() resets the counters with: this worker drains this run only
       }
       drain();
+      {
+        std::lock_guard<std::mutex> lock(mtx);
+        --active;
+      }
+      done_cv.notify_all();
     }
   }
   std::vector<std::thread>                  threads;
@@ -249,6 +257,7 @@ private:
   size_t                                    count = 0;
   std::atomic<size_t>                       next{0}, done{0};
   uint64_t                                  generation = 0;
+  unsigned                                  active     = 0; // workers inside drain()
   bool                                      stop       = false;
 };
 

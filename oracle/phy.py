@@ -231,10 +231,10 @@ class PuschProcessorPlugin:
         return t, tb[:fpdu.tb_bytes]
 
     def stats(self):
-        s = np.zeros(6, np.uint64)
+        s = np.zeros(7, np.uint64)
         lib().srs_ref_phy_pusch_stats(self.h, s.ctypes.data)
-        return dict(zip(("pdus", "batches", "errors", "harq_redecodes", "retransmissions", "device_grids"),
-                        (int(v) for v in s)))
+        return dict(zip(("pdus", "batches", "errors", "harq_redecodes", "retransmissions", "device_grids",
+                         "harq_soft_downloads"), (int(v) for v in s)))
 
     def bench(self, grids, pdu, tb_bytes, warmup, steps):
         """Seconds per step with one PDU per cell grid (process per PDU, flush, wait) and the TB CRC-OK count."""

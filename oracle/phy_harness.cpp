@@ -42,6 +42,7 @@
 #include "srsran/fapi_adaptor/uci_part2_correspondence_repository.h"
 #include "srsran/phy/upper/channel_processors/pusch/pusch_processor_result_notifier.h"
 #include "srsran_amd/pusch_processor.h"
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <stdexcept>
@@ -680,7 +681,7 @@ int srs_ref_pusch_process_fapi(void* grid, void* fapi_pdu, unsigned nof_prb, uns
   return 0;
 }
 
-/* Plug-in statistics: PDUs, batches, errors, HARQ re-decodes, retransmissions. */
+/* Plug-in statistics: PDUs, batches, errors, HARQ re-decodes, retransmissions, device grids, soft-buffer downloads. */
 void srs_ref_phy_pusch_stats(void* h, uint64_t* out)
 {
   const auto s = static_cast<pusch_ctx*>(h)->factory->get_statistics();
@@ -690,6 +691,7 @@ void srs_ref_phy_pusch_stats(void* h, uint64_t* out)
   out[3]       = s.nof_harq_redecodes;
   out[4]       = s.nof_retransmissions;
   out[5]       = s.nof_device_grids;
+  out[6]       = s.nof_harq_soft_downloads;
 }
 
 /* Throughput through the plug-in as the upper PHY drives it: every step, one PDU per cell grid (nof_cells grids,
@@ -749,7 +751,9 @@ void srs_ref_phy_wgrid_destroy(void* g)
 void* srs_ref_phy_hgrid_create(const uint32_t* grid, unsigned nports, unsigned nsubc, int device)
 {
   auto* g = new dev_grid(nports, nsubc, device);
-  if (grid != nullptr) {
+  // (an all-zero grid is what the new grid holds already: no host write, so the grid has no writable view out)
+  const size_t n = static_cast<size_t>(nports) * MAX_NSYMB_PER_SLOT * nsubc;
+  if (grid != nullptr && std::any_of(grid, grid + n, [](uint32_t v) { return v != 0; })) {
     resource_grid_writer& w = g->grid.get_writer();
     for (unsigned p = 0; p != nports; ++p) {
       for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {

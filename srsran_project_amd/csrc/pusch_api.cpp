@@ -404,13 +404,14 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
       const slot_harq* h = harq_of(u);
       if (h != nullptr) {
         const soft_row_layout lay = layout_of(p);
+        const uint32_t lazy = h->lazy && h->new_data ? 1u : 0u;
         htbs.push_back(harq_tb_desc{reinterpret_cast<uint8_t*>(h->soft), u, p->nof_segments, lay.row_bytes,
-                                    lay.flag_offset});
+                                    lay.flag_offset, lazy, row, lay.soft_bytes});
         max_soft = std::max(max_soft, lay.soft_bytes);
         for (uint32_t r = 0; r < p->nof_segments; ++r) {
           hrows.push_back(harq_row_desc{reinterpret_cast<uint8_t*>(h->soft) + static_cast<size_t>(r) * lay.row_bytes,
                                         row + r, lay.soft_bytes, lay.msg_offset, lay.flag_offset - lay.msg_offset,
-                                        lay.flag_offset, h->new_data ? 1u : 0u});
+                                        lay.flag_offset, h->new_data ? 1u : 0u, lazy, row, p->nof_segments});
           row_flags[row + r] = h->new_data ? 3 : 0;
         }
       }

@@ -726,6 +726,134 @@ int fused_uci(srs_amd_pusch_processor* proc, const srs_amd_pusch_slot_pdu* pdus,
   return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH slot UCI launches");
 }
 
+// CSI part 2 of a batch of grids of one plan on the device, after its CSI part 1 decoding (statuses [g][4] in
+// uci_status): the size selection per grid, the second demultiplexer pass and the CSI part 2 decoders per (grid,
+// candidate size) under device predicates, and the UL-SCH of every grid through the slot decoder with per-grid row
+// patches to the selected size's geometry (pusch_processor_impl.cpp:56-103, as the fused slot group does).
+int csi2_batch_device(srs_amd_pusch_processor* proc, const srs_amd_pusch_processor_plan* plan,
+                      const srs_amd_pusch_processor_plan::csi2_candidates* cand, uint32_t nof_grids,
+                      const int8_t* dem_rows, uint64_t cw_stride, int8_t* llrs, uint64_t llr_stride, int8_t* uci_rows,
+                      uint64_t uci_stride, uint64_t ack_e, uint64_t csi2_stride, const uint8_t* part1,
+                      uint64_t part1_stride, uint8_t* part2, uint64_t part2_stride, uint8_t* d_tbs, uint32_t tb_stride,
+                      int8_t* d_soft, int32_t* cb_iters, hipStream_t s)
+{
+  int32_t*       st  = proc->uci_status.as<int32_t>();
+  hipError_t     e   = proc->csi2_sel.ensure(sizeof(int32_t) * nof_grids);
+  if (e != hipSuccess) {
+    return hip_fail(e, "CSI part 2 selection scratch");
+  }
+  int32_t*                      sel = proc->csi2_sel.as<int32_t>();
+  const size_t                  NC  = cand->n2.size();
+  std::vector<csi2_select_args> sels(nof_grids);
+  std::vector<demux_args>       dx;
+  std::vector<uci_slot_message> msgs;
+  uint32_t                      max_re = 0;
+  int8_t* const                 c2_base = uci_rows + static_cast<uint64_t>(nof_grids) * uci_stride;
+  for (uint32_t g = 0; g < nof_grids; ++g) {
+    csi2_select_args& a = sels[g];
+    a.part1     = part1 + g * part1_stride;
+    a.status1   = st + 4 * g + 1;
+    a.nof_part2 = st + 4 * g + 3;
+    a.sel       = sel + g;
+    a.cand      = cand->d.as<int32_t>();
+    a.nof_cand  = static_cast<uint32_t>(NC);
+    a.nof_part1 = plan->pdu.nof_csi_part1;
+    a.descr     = plan->pdu.csi_part2_size;
+    int8_t* u1  = uci_rows + g * uci_stride;
+    int8_t* c2  = c2_base + g * csi2_stride;
+    for (size_t q = 0; q < NC; ++q) {
+      const auto* geo = cand->geo[q];
+      demux_args  d   = make_demux_args_csi2(geo->demux, dem_rows + g * cw_stride, llrs + g * llr_stride, u1,
+                                             u1 + ack_e, c2);
+      d.sel           = sel + g;
+      d.sel_val       = static_cast<int32_t>(q);
+      dx.push_back(d);
+      max_re = std::max(max_re, d.nof_re);
+      uci_slot_message m{c2, geo->info.nof_csi_part2_bits, cand->n2[q], plan->pdu.modulation, part2 + g * part2_stride,
+                         st + 4 * g + 2};
+      m.pred     = sel + g;
+      m.pred_val = static_cast<int32_t>(q);
+      msgs.push_back(m);
+    }
+  }
+  uci_slot_plan up;
+  int           rc = uci_slot_build(proc->uci, msgs.data(), static_cast<uint32_t>(msgs.size()), nullptr, up);
+  if (rc == SRS_AMD_OK && up.cb_bytes != 0) {
+    e = proc->uci_cbs.ensure(up.cb_bytes);
+  }
+  if (rc == SRS_AMD_OK && e == hipSuccess) {
+    rc = uci_slot_build(proc->uci, msgs.data(), static_cast<uint32_t>(msgs.size()), proc->uci_cbs.as<uint8_t>(), up);
+  }
+  if (rc != SRS_AMD_OK) {
+    return rc;
+  }
+  const size_t o_se  = 0;
+  const size_t o_dx  = align_up(sizeof(csi2_select_args) * sels.size(), 64);
+  const size_t o_sh  = o_dx + align_up(sizeof(demux_args) * dx.size(), 64);
+  const size_t o_po  = o_sh + align_up(sizeof(uci_short_args) * up.shorts.size(), 64);
+  const size_t o_fi  = o_po + align_up(sizeof(polar_args) * up.polars.size(), 64);
+  const size_t total = o_fi + sizeof(uci_polar_args) * up.finishes.size();
+  if (e == hipSuccess) {
+    e = proc->uci_items.ensure(total);
+  }
+  if (e == hipSuccess) {
+    e = proc->stage3.acquire(total);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "CSI part 2 descriptors");
+  }
+  std::memcpy(proc->stage3.at<uint8_t>(o_se), sels.data(), sizeof(csi2_select_args) * sels.size());
+  std::memcpy(proc->stage3.at<uint8_t>(o_dx), dx.data(), sizeof(demux_args) * dx.size());
+  std::memcpy(proc->stage3.at<uint8_t>(o_sh), up.shorts.data(), sizeof(uci_short_args) * up.shorts.size());
+  std::memcpy(proc->stage3.at<uint8_t>(o_po), up.polars.data(), sizeof(polar_args) * up.polars.size());
+  std::memcpy(proc->stage3.at<uint8_t>(o_fi), up.finishes.data(), sizeof(uci_polar_args) * up.finishes.size());
+  auto* d = proc->uci_items.as<uint8_t>();
+  e       = proc->stage3.upload(d, total, s);
+  if (e == hipSuccess) {
+    e = launch_csi2_select(reinterpret_cast<const csi2_select_args*>(d + o_se), nof_grids, s);
+  }
+  if (e == hipSuccess) {
+    e = launch_ulsch_demux_items(reinterpret_cast<const demux_args*>(d + o_dx), static_cast<uint32_t>(dx.size()),
+                                 max_re, s);
+  }
+  if (e == hipSuccess) {
+    e = launch_uci_short_items(reinterpret_cast<const uci_short_args*>(d + o_sh),
+                               static_cast<uint32_t>(up.shorts.size()), s);
+  }
+  if (e == hipSuccess) {
+    e = launch_polar_decode_items(reinterpret_cast<const polar_args*>(d + o_po), static_cast<uint32_t>(up.polars.size()),
+                                  s);
+  }
+  if (e == hipSuccess) {
+    e = launch_uci_polar_finish_items(reinterpret_cast<const uci_polar_args*>(d + o_fi),
+                                      static_cast<uint32_t>(up.finishes.size()), s);
+  }
+  if (e != hipSuccess) {
+    return hip_fail(e, "CSI part 2 launches");
+  }
+  auto* dres = proc->dec_results.as<srs_amd_pusch_decoder_result>();
+  if (!plan->has_sch) {
+    e = hipMemsetAsync(dres, 0, sizeof(srs_amd_pusch_decoder_result) * nof_grids, s);
+    return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "PUSCH processor UCI-only result");
+  }
+  // the UL-SCH of every grid: one slot-decoder UE per grid, rows patched to the selected size's geometry
+  const uint32_t                NCu = static_cast<uint32_t>(NC), C = plan->sch.nof_segments;
+  const auto*                   t   = cand->d.as<uint32_t>();
+  std::vector<srs_amd_pusch_ue> ues(nof_grids);
+  std::vector<uint32_t>         cb_off(nof_grids);
+  std::vector<slot_harq>        harq(nof_grids);
+  std::vector<slot_ue_patch>    patches(nof_grids);
+  for (uint32_t g = 0; g < nof_grids; ++g) {
+    ues[g]     = srs_amd_pusch_ue{plan->sch, g * llr_stride, static_cast<uint64_t>(g) * tb_stride};
+    cb_off[g]  = g * C;
+    harq[g]    = slot_harq{d_soft != nullptr ? d_soft + g * plan->soft_bytes : nullptr, plan->dec_cfg.new_data};
+    patches[g] = slot_ue_patch{g, sel + g, t + NCu, t + NCu + NCu * C};
+  }
+  return pusch_decode_slot_ex(proc->dec, &plan->dec_cfg, ues.data(), nof_grids, llrs, d_tbs, dres,
+                              cb_iters != nullptr ? cb_off.data() : nullptr, cb_iters, s,
+                              d_soft != nullptr ? harq.data() : nullptr, patches.data(), nof_grids);
+}
+
 // chest: the estimator configuration to run (the plan's, or a copy in another slot); nullptr: the plan's.
 int process_batch_locked(srs_amd_pusch_processor*            proc,
                          const srs_amd_pusch_processor_plan* plan,
@@ -870,7 +998,43 @@ int process_batch_locked(srs_amd_pusch_processor*            proc,
                                   out ? io->csi_part1_stride : pay_stride, proc->uci_status.as<int32_t>() + 1,
                                   4 * sizeof(int32_t), nof_grids, stream);
   }
-  // CSI part 2 sizes from the decoded CSI part 1 (one readback), grids without CSI part 2 keep the plan's geometry
+  // CSI part 2 sized on the device (csi2_batch_device: no host round trip) whenever the plan's candidate sizes all
+  // have a geometry and the UL-SCH can go through the slot decoder; otherwise the sizes come from one readback of the
+  // decoded CSI part 1 below.  Grids without CSI part 2 keep the plan's geometry.
+  if (rc == SRS_AMD_OK && plan->csi2) {
+    const srs_amd_pusch_processor_plan::csi2_candidates* cand = nullptr;
+    const bool dev2 = (!plan->has_sch || d_soft == nullptr || plan->dec_cfg.use_early_stop) &&
+                      (plan->has_sch || d_soft == nullptr) && plan_csi2_candidates(proc, plan, &cand) == SRS_AMD_OK &&
+                      !cand->n2.empty() && (plan->dec_cfg.new_data || d_soft != nullptr);
+    if (dev2) {
+      const bool     out1 = io != nullptr && io->d_csi_part1 != nullptr;
+      const uint8_t* p1   = out1 ? io->d_csi_part1 : proc->uci_payload.as<uint8_t>() + K_ack;
+      const uint64_t p1s  = out1 ? io->csi_part1_stride : pay_stride;
+      const bool     out2 = io != nullptr && io->d_csi_part2 != nullptr;
+      if (out2 && io->csi_part2_stride < plan->max_csi2) {
+        return fail(SRS_AMD_EINVAL, "CSI part 2 payload stride too small (%u bits)", plan->max_csi2);
+      }
+      rc = csi2_batch_device(proc, plan, cand, nof_grids, dem_rows, cw_stride, llrs, llr_stride, uci_rows, uci_stride,
+                             ack_e, csi2_stride, p1, p1s,
+                             out2 ? io->d_csi_part2 : proc->uci_payload.as<uint8_t>() + K_ack + K_csi1,
+                             out2 ? io->csi_part2_stride : pay_stride, d_tbs, tb_stride, d_soft, cb_iters, s);
+      if (rc != SRS_AMD_OK) {
+        return rc;
+      }
+      pusch_result_args a{};
+      a.dec_results = proc->dec_results.as<srs_amd_pusch_decoder_result>();
+      a.stats       = st;
+      a.results     = d_results;
+      a.nof_grids   = nof_grids;
+      a.nof_ports   = P;
+      a.uci_status  = proc->uci_status.as<int32_t>();
+      a.uci_mask    = (K_ack != 0 ? 1 : 0) | (K_csi1 != 0 ? 2 : 0) | 4;
+      e                     = launch_pusch_result(a, s);
+      const hipError_t done = scope.close();
+      e                     = e != hipSuccess ? e : done;
+      return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "pusch_result_kernel launch");
+    }
+  }
   std::vector<uint32_t> n2(nof_grids, 0);
   std::vector<int32_t>  st1; // statuses [grid][4] read back with CSI part 1
   if (rc == SRS_AMD_OK && plan->csi2) {
@@ -1246,7 +1410,7 @@ int srs_amd_pusch_process_slot_ex(srs_amd_pusch_processor*        proc,
     const srs_amd_pusch_slot_pdu& u = pdus[fused[k]];
     ues[k]    = srs_amd_pusch_ue{u.plan->sch, llr_off[k], u.tb_offset};
     cb_off[k] = u.cb_offset;
-    harq[k]   = slot_harq{u.d_soft, u.plan->dec_cfg.new_data};
+    harq[k]   = slot_harq{u.d_soft, u.plan->dec_cfg.new_data, u.soft_on_failure != 0 ? 1 : 0};
     any_harq |= u.d_soft != nullptr;
     if (cands[k] != nullptr) {
       const uint32_t NC = static_cast<uint32_t>(cands[k]->n2.size()), C = u.plan->sch.nof_segments;

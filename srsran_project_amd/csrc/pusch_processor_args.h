@@ -56,6 +56,7 @@ hipError_t launch_csi2_select(const csi2_select_args* items, uint32_t n, hipStre
 struct slot_harq {
   int8_t* soft;
   int     new_data;
+  int     lazy = 0; // new data: soft LLRs kept only when the decoding leaves the TB failed (harq_row_desc::lazy)
 };
 
 // srs_amd_pusch_decode_slot (pusch_api.cpp) with per-codeblock iteration counts: UE u's C values at

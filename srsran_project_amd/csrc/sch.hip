@@ -611,8 +611,20 @@ __global__ __launch_bounds__(HARQ_THREADS) void harq_gather_kernel(harq_args a)
 
 __global__ __launch_bounds__(HARQ_THREADS) void harq_scatter_kernel(harq_args a)
 {
-  const harq_row_desc d = a.rows[blockIdx.y];
-  harq_copy(d.soft_row, reinterpret_cast<const uint8_t*>(a.internal) + static_cast<size_t>(d.row) * a.S, d.soft_bytes);
+  const harq_row_desc d    = a.rows[blockIdx.y];
+  bool                keep = true;
+  if (d.lazy) {
+    // new data kept only for a retransmission: the soft LLRs matter only if some codeblock of the TB failed
+    int fail = 0;
+    for (uint32_t c = threadIdx.x; c < d.tb_C; c += HARQ_THREADS) {
+      fail |= a.iters[d.tb_row0 + c] < 0 ? 1 : 0;
+    }
+    keep = __syncthreads_or(fail) != 0;
+  }
+  if (keep) {
+    harq_copy(d.soft_row, reinterpret_cast<const uint8_t*>(a.internal) + static_cast<size_t>(d.row) * a.S,
+              d.soft_bytes);
+  }
   if (blockIdx.x != 0) {
     return;
   }
@@ -640,18 +652,25 @@ __global__ __launch_bounds__(HARQ_THREADS) void harq_scatter_kernel(harq_args a)
   }
 }
 
-__global__ __launch_bounds__(64) void harq_final_kernel(harq_args a)
+// one workgroup per TB
+__global__ __launch_bounds__(HARQ_THREADS) void harq_final_kernel(harq_args a)
 {
-  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= a.nof_tbs) {
-    return;
-  }
-  const harq_tb_desc                  d = a.tbs[t];
+  const harq_tb_desc                  d = a.tbs[blockIdx.x];
   const srs_amd_pusch_decoder_result& r = a.results[d.result];
   // every codeblock passed but not the TB CRC: reset_codeblocks_crc (pusch_decoder_impl.cpp:425-437)
   if (d.C > 1 && r.nof_codeblocks_crc_ok == d.C && !r.tb_crc_ok) {
-    for (uint32_t c = 0; c < d.C; ++c) {
+    for (uint32_t c = threadIdx.x; c < d.C; c += HARQ_THREADS) {
       *reinterpret_cast<int32_t*>(d.soft + static_cast<size_t>(c) * d.row_bytes + d.flag_offset) = 0;
+    }
+    if (d.lazy) {
+      // the scatter skipped the soft LLRs (no codeblock failed): the retransmission combines with them
+      for (uint32_t c = 0; c < d.C; ++c) {
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(a.internal) + static_cast<size_t>(d.row0 + c) * a.S;
+        uint8_t*       dst = d.soft + static_cast<size_t>(c) * d.row_bytes;
+        for (uint32_t j = threadIdx.x; j < d.soft_bytes; j += HARQ_THREADS) {
+          dst[j] = src[j];
+        }
+      }
     }
   }
 }
@@ -705,7 +724,7 @@ hipError_t launch_harq_final(const harq_args& a, hipStream_t stream)
   if (a.nof_tbs == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(harq_final_kernel, dim3((a.nof_tbs + 63) / 64), dim3(64), 0, stream, a);
+  hipLaunchKernelGGL(harq_final_kernel, dim3(a.nof_tbs), dim3(HARQ_THREADS), 0, stream, a);
   return hipGetLastError();
 }
 

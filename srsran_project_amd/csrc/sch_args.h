@@ -147,6 +147,12 @@ struct harq_row_desc {
   uint32_t msg_bytes;
   uint32_t flag_offset;
   uint32_t new_data;
+  // lazy (new data only): the soft LLRs are copied back only when some codeblock of the TB (decoder rows
+  // tb_row0 .. tb_row0 + tb_C - 1) failed its CRC -- the state a retransmission combines with; the message and flag
+  // are written always
+  uint32_t lazy;
+  uint32_t tb_row0;
+  uint32_t tb_C;
 };
 struct harq_tb_desc {
   uint8_t* soft;        // the caller's soft buffer (C rows)
@@ -154,6 +160,9 @@ struct harq_tb_desc {
   uint32_t C;
   uint32_t row_bytes;
   uint32_t flag_offset;
+  uint32_t lazy;        // as harq_row_desc::lazy: a TB whose codeblocks all passed but whose TB CRC failed then copies
+  uint32_t row0;        // its soft LLRs back here (decoder rows row0 .., soft_bytes each)
+  uint32_t soft_bytes;
 };
 struct harq_args {
   const harq_row_desc*          rows;

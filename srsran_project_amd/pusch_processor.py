@@ -125,7 +125,7 @@ class PuschSlotPdu(ctypes.Structure):
     _fields_ = [("plan", ctypes.c_void_p), ("grid", ctypes.c_uint32), ("cb_offset", ctypes.c_uint32),
                 ("tb_offset", ctypes.c_uint64), ("d_soft", ctypes.c_void_p), ("uci_offset", ctypes.c_uint64),
                 ("has_slot", ctypes.c_uint32), ("numerology", ctypes.c_uint32), ("slot_index", ctypes.c_uint32),
-                ("d_grid", ctypes.c_void_p)]
+                ("d_grid", ctypes.c_void_p), ("soft_on_failure", ctypes.c_uint32)]
 
 
 class PuschSlotIo(ctypes.Structure):
