@@ -115,6 +115,38 @@ int      srs_amd_ofdm_demodulate_symbol(srs_amd_ofdm_demodulator* dem,
                                         const float*              input,
                                         uint32_t                  symbol_index);
 
+/* Symbol granularity, ASYNCHRONOUS on `stream`: the same transforms with both buffers device-accessible (device
+ * memory, or pinned host memory the kernel reads / writes over the bus): no copy, no synchronisation.  What the
+ * reference-side OFDM plug-ins run per ofdm_symbol_(de)modulator call on a device-resident resource grid
+ * (integration/ofdm_modulator_hip.cpp), the grid row being (port, symbol % nsymb) of the device copy. */
+int srs_amd_ofdm_modulate_symbol_async(srs_amd_ofdm_modulator* mod,
+                                       float*                  output,
+                                       const uint16_t*         grid_symbol,
+                                       uint32_t                symbol_index,
+                                       void*                   stream);
+int srs_amd_ofdm_demodulate_symbol_async(srs_amd_ofdm_demodulator* dem,
+                                         uint16_t*                 grid_symbol,
+                                         const float*              input,
+                                         uint32_t                  symbol_index,
+                                         void*                     stream);
+/* Many staged symbols in one launch, ASYNCHRONOUS on `stream` (the deferred form of the symbol demodulator plug-in:
+ * each ofdm_symbol_demodulator::demodulate call copies its samples into pinned staging, the symbols of a slot go in
+ * one launch).  items [count][2] = {symbol index within the subframe, offset of the symbol's grid row in cbf16
+ * pairs from `grid`}; samples [count][sample_stride] complex floats, symbol i's get_symbol_size(items[2i]) samples
+ * (cyclic prefix first) at the start of its row; sample_stride >= the longest symbol.  items and samples
+ * device-accessible (pinned host memory is).  An item with an out-of-range symbol index is skipped.
+ * d_scratch: NULL -- the kernel reads items and samples where they are (over the bus when pinned); else items and
+ * samples are pinned host memory, first copied into d_scratch (device memory of count * (8 * sample_stride + 8)
+ * bytes) by a copy kernel (wide reads, many in flight), and the transform reads HBM. */
+int srs_amd_ofdm_demodulate_symbols_async(srs_amd_ofdm_demodulator* dem,
+                                          uint16_t*                 grid,
+                                          const uint32_t*           items,
+                                          const float*              samples,
+                                          uint32_t                  sample_stride,
+                                          uint32_t                  count,
+                                          void*                     d_scratch,
+                                          void*                     stream);
+
 /* dft_processor: direction 0 = DIRECT (exp(-2*pi*i*n*k/N)), 1 = INVERSE; no normalisation. */
 int  srs_amd_dft_create(srs_amd_dft** dft, uint32_t size, int direction, int device);
 void srs_amd_dft_destroy(srs_amd_dft* dft);

@@ -5,6 +5,7 @@
 #include "srsran_amd/ldpc.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -26,6 +27,8 @@ void check(hipError_t e, const char* what)
 hip_resource_grid::hip_resource_grid(std::unique_ptr<resource_grid> host_, int device_) :
   host(std::move(host_)), reader(*this), writer(*this)
 {
+  static std::atomic<uint64_t> next_uid{1};
+  uid = next_uid.fetch_add(1);
   if (!host) {
     throw std::runtime_error("hip_resource_grid: no host grid");
   }
@@ -51,6 +54,13 @@ hip_resource_grid::hip_resource_grid(std::unique_ptr<resource_grid> host_, int d
 
 hip_resource_grid::~hip_resource_grid()
 {
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    for (hip_grid_deferred_writer* w : deferred) {
+      w->detach(*this);
+    }
+    deferred.clear();
+  }
   (void)hipSetDevice(dev);
   if (own != nullptr) {
     (void)hipStreamSynchronize(own);
@@ -74,6 +84,8 @@ void hip_resource_grid::set_all_zero()
 {
   std::unique_lock<std::mutex> lock(mtx);
   cv.wait(lock, [this] { return pending == 0; });
+  run_deferred(nullptr); // (ordered before the zeroing, as the reference's writes before set_all_zero are)
+  ++ver;
   host->set_all_zero();
   std::fill(base.begin(), base.end(), 0u);
   check(hipSetDevice(dev), "hipSetDevice");
@@ -87,8 +99,9 @@ void hip_resource_grid::set_all_zero()
 
 void hip_resource_grid::host_access(std::unique_lock<std::mutex>& lock, bool write) const
 {
-  // every device writer has published its completion (device_written)
+  // every device writer has published its completion (device_written); staged writes issued
   cv.wait(lock, [this] { return pending == 0; });
+  run_deferred(nullptr);
   if (device_dirty) {
     // the device's changes since the last agreement: host ^= device ^ base, base = device
     auto* self = const_cast<hip_resource_grid*>(this);
@@ -119,6 +132,7 @@ void hip_resource_grid::host_access(std::unique_lock<std::mutex>& lock, bool wri
   }
   if (write) {
     host_dirty = true;
+    ++ver;
   }
 }
 
@@ -126,8 +140,9 @@ void hip_resource_grid::device_access(std::unique_lock<std::mutex>& lock, hipStr
 {
   check(hipSetDevice(dev), "hipSetDevice");
   if (!write) {
-    // readers see every producer (a writer does not need the others: disjoint REs)
+    // readers see every producer (a writer does not need the others: disjoint REs), staged writes included
     cv.wait(lock, [this] { return pending == 0; });
+    run_deferred(nullptr);
   }
   if (host_dirty) {
     // the host's changes since the last agreement: delta = host ^ base per changed row, applied on the device where
@@ -179,14 +194,62 @@ void hip_resource_grid::device_access(std::unique_lock<std::mutex>& lock, hipStr
   check(hipStreamWaitEvent(stream, ready, 0), "hipStreamWaitEvent");
   if (write) {
     device_dirty = true;
+    ++ver;
   }
 }
 
-const uint32_t* hip_resource_grid::device_read(hipStream_t stream)
+const uint32_t* hip_resource_grid::device_read(hipStream_t stream, uint64_t* version)
 {
   std::unique_lock<std::mutex> lock(mtx);
   device_access(lock, stream, false);
+  if (version != nullptr) {
+    *version = ver;
+  }
   return d;
+}
+
+void hip_resource_grid::run_deferred(hip_grid_deferred_writer* only) const
+{
+  for (auto it = deferred.begin(); it != deferred.end();) {
+    hip_grid_deferred_writer* w = *it;
+    if (only != nullptr && w != only) {
+      ++it;
+      continue;
+    }
+    it                = deferred.erase(it);
+    hipStream_t     s = w->stream();
+    check(hipSetDevice(dev), "hipSetDevice");
+    check(hipStreamWaitEvent(s, ready, 0), "hipStreamWaitEvent");
+    w->issue(*const_cast<hip_resource_grid*>(this), d);
+    // ready := (every earlier producer) and (this writer), as device_written
+    check(hipEventRecord(joiner, s), "hipEventRecord");
+    check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
+    check(hipStreamWaitEvent(own, joiner, 0), "hipStreamWaitEvent");
+    check(hipEventRecord(ready, own), "hipEventRecord");
+    device_dirty = true;
+  }
+}
+
+void hip_resource_grid::defer(hip_grid_deferred_writer& w)
+{
+  std::lock_guard<std::mutex> lock(mtx);
+  if (std::find(deferred.begin(), deferred.end(), &w) == deferred.end()) {
+    deferred.push_back(&w);
+  }
+  device_dirty = true;
+  ++ver;
+}
+
+void hip_resource_grid::issue_deferred(hip_grid_deferred_writer& w)
+{
+  std::lock_guard<std::mutex> lock(mtx);
+  run_deferred(&w);
+}
+
+bool hip_resource_grid::unchanged_since(uint64_t version) const
+{
+  std::lock_guard<std::mutex> lock(mtx);
+  return version == ver && !host_dirty && pending == 0 && deferred.empty();
 }
 
 uint32_t* hip_resource_grid::device_write(hipStream_t stream)
@@ -209,6 +272,7 @@ void hip_resource_grid::device_written(hipStream_t stream)
     check(hipEventRecord(ready, own), "hipEventRecord");
     device_dirty = true;
     pending      = pending > 0 ? pending - 1 : 0;
+    ++ver;
   }
   cv.notify_all();
 }

@@ -3,11 +3,18 @@
 // srsran_amd C-ABI grids), next to a host mirror -- any resource_grid the reference's own factory builds
 // (support_factories.h create_resource_grid_factory) -- that the reader / writer interfaces serve.
 //
-// Plug-ins that understand it (pusch_processor_hip, pdsch_processor_hip, the OFDM plug-ins) reach the device copy
-// through hip_grid_reader / hip_grid_writer and run on it directly: the uplink grid the OFDM demodulator plug-in
-// writes is read by the PUSCH plug-in without crossing PCIe, and the downlink grid the PDSCH plug-in writes goes to
-// the OFDM modulator plug-in the same way.  Every other component keeps the reference interfaces: the first host
-// access after a device write downloads the grid (once), the first device access after a host write uploads it.
+// Plug-ins that understand it (pusch_processor_hip, pdsch_processor_hip, pdcch / ssb / pucch, the OFDM plug-ins of
+// ofdm_modulator_hip) reach the device copy through hip_grid_reader / hip_grid_writer and run on it directly: the
+// uplink grid the OFDM demodulator plug-in writes is read by the PUSCH plug-in without crossing PCIe, and the downlink
+// grid the PDSCH plug-in writes is read in place by the OFDM modulator plug-in (whose samples then go to the host, as
+// its interface returns them).  Every other component keeps the reference interfaces: the first host access after a
+// device write downloads the grid (once), the first device access after a host write uploads it.
+//
+// Deferred writers (r06): a device producer may stage its writes on the host and register with defer(); they are
+// issued (hip_grid_deferred_writer::issue, one launch for everything staged) before the next access of either copy,
+// at set_all_zero, or when the producer asks (issue_deferred).  The OFDM symbol demodulator plug-in works this way:
+// a demodulate() call per port and symbol (puxch_processor_impl.cpp:73-82) costs a host copy of its samples, the
+// slot's symbols go to the device in one launch when the PUSCH plug-in (or anything else) reads the grid.
 //
 // Coherence (r06): a three-way merge against the state both copies last agreed on (`base`, a host array).  Host
 // writers (the reference's channel processors through put / get_view) change the host mirror, device writers (the
@@ -42,6 +49,20 @@ namespace srsran {
 namespace hip {
 
 class hip_resource_grid;
+
+/// A device producer whose writes are staged on the host and issued lazily (see the header comment).
+class hip_grid_deferred_writer
+{
+public:
+  virtual ~hip_grid_deferred_writer() = default;
+  /// Issues every staged write for `grid` into its device copy `d`, kernels on stream() (which already waits for the
+  /// grid's earlier producers).  Called with the grid locked.
+  virtual void issue(hip_resource_grid& grid, uint32_t* d) = 0;
+  /// The stream issue() launches on.
+  virtual hipStream_t stream() const = 0;
+  /// The grid is being destroyed: forget it, dropping what is staged for it.  Called with the grid locked.
+  virtual void detach(hip_resource_grid& grid) = 0;
+};
 
 /// Reader of a hip_resource_grid: the reference interface over the host mirror (downloaded on demand).
 class hip_grid_reader : public resource_grid_reader
@@ -105,13 +126,25 @@ public:
   unsigned nof_symbols() const { return symbols; }
   unsigned nof_subc() const { return subc; }
   int      device() const { return dev; }
+  /// Unique over the process's grids (an address can be reused by a later grid; an identity cannot).
+  uint64_t identity() const { return uid; }
 
-  /// Device copy, current, for kernels on `stream` that read it (stream waits for the last device producer).
-  const uint32_t* device_read(hipStream_t stream);
+  /// Device copy, current, for kernels on `stream` that read it (stream waits for every device producer);
+  /// version (optional): the content version read (see unchanged_since).
+  const uint32_t* device_read(hipStream_t stream, uint64_t* version = nullptr);
   /// Device copy, current, for kernels on `stream` that write it; the host mirror becomes stale.
   uint32_t* device_write(hipStream_t stream);
   /// The kernels that wrote the device copy were issued on `stream`: host accesses and other streams wait for them.
   void device_written(hipStream_t stream);
+
+  /// `w` has writes staged for this grid: issued before the next access of either copy, at set_all_zero, or by
+  /// issue_deferred(w).
+  void defer(hip_grid_deferred_writer& w);
+  /// Issues w's staged writes now (nothing when w is not registered).
+  void issue_deferred(hip_grid_deferred_writer& w);
+  /// Nothing was written (host or device, issued or staged, or through a writable view still out) since
+  /// device_read returned `version`: a reader may reuse what it computed from that read.
+  bool unchanged_since(uint64_t version) const;
 
   /// Transfers (for tests and statistics): host <- device downloads, device <- host uploads.
   uint64_t nof_downloads() const { return downloads; }
@@ -126,10 +159,13 @@ private:
   void device_access(std::unique_lock<std::mutex>& lock, hipStream_t stream, bool write);
   // a writable view is out (get_view): the host side stays dirty until the slot boundary
   void mark_view_open() const { view_open = true; }
+  // issues the registered deferred writers' staged writes (only: that one writer), lock held
+  void run_deferred(hip_grid_deferred_writer* only) const;
 
   std::unique_ptr<resource_grid> host;
   unsigned                       ports = 0, symbols = 0, subc = 0;
   int                            dev   = 0;
+  uint64_t                       uid   = 0;
   uint32_t*                      d     = nullptr;
   hipEvent_t                     ready  = nullptr; // every device producer's completion (joined on `own`)
   hipEvent_t                     joiner = nullptr; // a writer's completion, joined into `ready`
@@ -142,6 +178,8 @@ private:
   mutable uint32_t*               d_delta    = nullptr; // merge staging: changed rows' XOR deltas, their row indices
   mutable uint32_t*               d_rows     = nullptr;
   mutable uint64_t                downloads = 0, uploads = 0;
+  mutable uint64_t                ver       = 0; // content version: bumped by every write access
+  mutable std::vector<hip_grid_deferred_writer*> deferred;
   hip_grid_reader                reader;
   hip_grid_writer                writer;
 };

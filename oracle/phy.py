@@ -48,6 +48,14 @@ def lib():
         L.srs_ref_phy_pusch_process_fapi.argtypes = [P, P, P, P, P, u]
         L.srs_ref_pusch_process_fapi.restype = i
         L.srs_ref_pusch_process_fapi.argtypes = [P, P, u, u, P, P, u, P, P, P, P, P]
+        L.srs_ref_phy_ofdm_demodulate.restype = i
+        L.srs_ref_phy_ofdm_demodulate.argtypes = [P, i, i, u, u, u, d, ctypes.c_float, u, u, P]
+        L.srs_ref_phy_ofdm_symbol_bench.restype = d
+        L.srs_ref_phy_ofdm_symbol_bench.argtypes = [i, i, i, u, u, u, u, u, u, P, P, P]
+        L.srs_ref_phy_ofdm_modulate_twice.restype = i
+        L.srs_ref_phy_ofdm_modulate_twice.argtypes = [P, i, u, u, u, d, ctypes.c_float, u, u, P, i, P, P]
+        L.srs_ref_phy_ofdm_modulate.restype = i
+        L.srs_ref_phy_ofdm_modulate.argtypes = [P, i, i, u, u, u, d, ctypes.c_float, u, u, P]
         _declared = True
     return L
 
@@ -244,6 +252,57 @@ class PuschProcessorPlugin:
         dt = lib().srs_ref_phy_pusch_bench(self.h, arr, len(grids), ctypes.byref(pdu), warmup, steps,
                                            tbs.ctypes.data, tb_bytes, ctypes.byref(ok))
         return dt, ok.value, tbs.reshape(len(grids), tb_bytes)
+
+
+# ---- OFDM demodulator plug-ins on a device-resident grid ----
+
+def ofdm_demodulate(grid, samples, slot, numerology, bw_rb, dft_size, fc, scale=1.0, form=1, device=0):
+    """The uplink lower-PHY step (puxch_processor_impl.cpp:73-82) through the MI355X OFDM demodulator plug-in:
+    samples complex64 [P][slot size] of slot `slot` of the subframe demodulated into grid (DeviceGrid: written in
+    place on the device) port by port, symbol by symbol (form 1, ofdm_symbol_demodulator) or slot by slot (form 0)."""
+    x = np.ascontiguousarray(samples, np.complex64)
+    if lib().srs_ref_phy_ofdm_demodulate(grid.h, device, form, numerology, bw_rb, dft_size, fc, scale, slot, x.shape[0],
+                                         x.ctypes.data) != 0:
+        raise RuntimeError("OFDM demodulator plug-in refused the configuration")
+
+
+def ofdm_modulate(grid, nports, slot, numerology, bw_rb, dft_size, fc, scale, n, form=1, device=0):
+    """The downlink lower-PHY step through the MI355X OFDM modulator plug-in: every port of slot `slot` of grid
+    (DeviceGrid: read in place on the device) modulated symbol by symbol (form 1) or slot by slot (form 0); returns
+    complex64 [nports][n] (n: the slot size)."""
+    y = np.zeros((nports, n), np.complex64)
+    if lib().srs_ref_phy_ofdm_modulate(grid.h, device, form, numerology, bw_rb, dft_size, fc, scale, slot, nports,
+                                       y.ctypes.data) != 0:
+        raise RuntimeError("OFDM modulator plug-in refused the configuration")
+    return y
+
+
+def ofdm_modulate_twice(grid, nports, slot, numerology, bw_rb, dft_size, fc, scale, n, nxt, next_on_host, device=0):
+    """srs_ref_phy_ofdm_modulate_twice: one symbol modulator plug-in over `grid`, then over `nxt` (uint32 [P][14][nsubc]
+    written on the device or through the host writer); returns the two complex64 [nports][n] outputs."""
+    y0, y1 = np.zeros((nports, n), np.complex64), np.zeros((nports, n), np.complex64)
+    g = np.ascontiguousarray(nxt, np.uint32)
+    if lib().srs_ref_phy_ofdm_modulate_twice(grid.h, device, numerology, bw_rb, dft_size, fc, scale, slot, nports,
+                                             g.ctypes.data, int(next_on_host), y0.ctypes.data, y1.ctypes.data) != 0:
+        raise RuntimeError("OFDM modulator plug-in refused the configuration")
+    return y0, y1
+
+
+def ofdm_symbol_bench(plugin, threads, numerology, bw_rb, dft_size, samples, slots, modulate=False, grid=None,
+                      device=0):
+    """Symbol-form demodulation (modulate=True: modulation of `grid` uint32 [P][14][nsubc]) from `threads` sector
+    threads (srs_ref_phy_ofdm_symbol_bench): plugin 1 the MI355X plug-in on device-resident grids, 0 the reference's
+    ofdm_symbol_(de)modulator_impl.  samples complex64 [P][slot size] (slot 0).  Returns (seconds, mean host us per
+    call, grid transfers)."""
+    x = np.ascontiguousarray(samples, np.complex64)
+    g = None if grid is None else np.ascontiguousarray(grid, np.uint32)
+    out = np.zeros(2, np.float64)
+    dt = lib().srs_ref_phy_ofdm_symbol_bench(device, plugin, int(modulate), threads, numerology, bw_rb, dft_size,
+                                             x.shape[0], slots, x.ctypes.data, None if g is None else g.ctypes.data,
+                                             out.ctypes.data)
+    if dt < 0:
+        raise RuntimeError("OFDM symbol bench failed")
+    return dt, float(out[0]), int(out[1])
 
 
 # ---- PDSCH ----

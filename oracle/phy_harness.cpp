@@ -1306,3 +1306,320 @@ void srs_ref_phy_pucch_stats(void* h, uint64_t* out)
 }
 
 } // extern "C"
+
+/* ---- OFDM: the demodulator plug-ins writing a device-resident grid, as the lower PHY drives them ---- */
+
+#include "../integration/ofdm_modulator_hip.h"
+#include <thread>
+
+namespace {
+
+ofdm_demodulator_configuration ul_dem_cfg(unsigned mu, unsigned bw_rb, unsigned dft_size, double fc, float scale = 1.0f)
+{
+  ofdm_demodulator_configuration c;
+  c.numerology                = mu;
+  c.bw_rb                     = bw_rb;
+  c.dft_size                  = dft_size;
+  c.cp                        = cyclic_prefix::NORMAL;
+  c.nof_samples_window_offset = 0;
+  c.scale                     = scale;
+  c.center_freq_Hz            = fc;
+  return c;
+}
+
+// Sample offsets of the symbols of slot `slot` within the slot (per port), and the slot size.
+std::vector<unsigned> symbol_offsets(const ofdm_symbol_demodulator& d, unsigned slot, unsigned& slot_size)
+{
+  std::vector<unsigned> off(MAX_NSYMB_PER_SLOT);
+  slot_size = 0;
+  for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+    off[l] = slot_size;
+    slot_size += d.get_symbol_size(MAX_NSYMB_PER_SLOT * slot + l);
+  }
+  return off;
+}
+
+ofdm_modulator_configuration dl_mod_cfg(unsigned mu, unsigned bw_rb, unsigned dft_size, double fc, float scale)
+{
+  ofdm_modulator_configuration c;
+  c.numerology     = mu;
+  c.bw_rb          = bw_rb;
+  c.dft_size       = dft_size;
+  c.cp             = cyclic_prefix::NORMAL;
+  c.scale          = scale;
+  c.center_freq_Hz = fc;
+  return c;
+}
+
+} // namespace
+
+extern "C" {
+
+/* The downlink step pdxch_processor_impl runs per OFDM symbol: every port of every symbol of slot `slot` (of the
+ * subframe) of `grid` modulated through the MI355X OFDM modulator plug-in (form 1 ofdm_symbol_modulator, symbol by
+ * symbol and port by port; form 0 ofdm_slot_modulator, port by port) into out [port][slot size] complex floats.
+ * 0 on success, -1 when the factory refuses the configuration. */
+int srs_ref_phy_ofdm_modulate(void* grid, int device, int form, unsigned mu, unsigned bw_rb, unsigned dft_size,
+                              double fc, float scale, unsigned slot, unsigned nports, float* out)
+{
+  auto                        f = hip::create_ofdm_modulator_factory_hip(device);
+  const auto                  c = dl_mod_cfg(mu, bw_rb, dft_size, fc, scale);
+  const resource_grid_reader& r = static_cast<any_grid*>(grid)->rd();
+  cf_t*                       y = reinterpret_cast<cf_t*>(out);
+  if (form == 0) {
+    auto m = f->create_ofdm_slot_modulator(c);
+    if (!m) {
+      return -1;
+    }
+    const unsigned n = m->get_slot_size(slot);
+    for (unsigned p = 0; p != nports; ++p) {
+      m->modulate(span<cf_t>(y + static_cast<size_t>(p) * n, n), r, p, slot);
+    }
+    return 0;
+  }
+  auto m = f->create_ofdm_symbol_modulator(c);
+  if (!m) {
+    return -1;
+  }
+  unsigned n = 0;
+  for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+    n += m->get_symbol_size(MAX_NSYMB_PER_SLOT * slot + l);
+  }
+  for (unsigned l = 0, off = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+    const unsigned sz = m->get_symbol_size(MAX_NSYMB_PER_SLOT * slot + l);
+    for (unsigned p = 0; p != nports; ++p) {
+      m->modulate(span<cf_t>(y + static_cast<size_t>(p) * n + off, sz), r, p, MAX_NSYMB_PER_SLOT * slot + l);
+    }
+    off += sz;
+  }
+  return 0;
+}
+
+/* One ofdm_symbol_modulator plug-in over two contents of the same grid: slot `slot` modulated (every port, symbol by
+ * symbol) into out0, then the grid rewritten with `next` -- on the device (next_on_host = 0, as a device producer) or
+ * through the host writer's put (1, as a reference processor) -- and modulated again by the SAME modulator into
+ * out1.  Checks that the plug-in's per-slot sample cache follows the grid's content.  0 on success. */
+int srs_ref_phy_ofdm_modulate_twice(void* grid, int device, unsigned mu, unsigned bw_rb, unsigned dft_size, double fc,
+                                    float scale, unsigned slot, unsigned nports, const uint32_t* next,
+                                    int next_on_host, float* out0, float* out1)
+{
+  auto m = hip::create_ofdm_modulator_factory_hip(device)->create_ofdm_symbol_modulator(
+      dl_mod_cfg(mu, bw_rb, dft_size, fc, scale));
+  auto* g = dynamic_cast<dev_grid*>(static_cast<any_grid*>(grid));
+  if (!m || g == nullptr) {
+    return -1;
+  }
+  unsigned n = 0;
+  for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+    n += m->get_symbol_size(MAX_NSYMB_PER_SLOT * slot + l);
+  }
+  auto run = [&](float* out) {
+    cf_t* y = reinterpret_cast<cf_t*>(out);
+    for (unsigned l = 0, off = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+      const unsigned sz = m->get_symbol_size(MAX_NSYMB_PER_SLOT * slot + l);
+      for (unsigned p = 0; p != nports; ++p) {
+        m->modulate(span<cf_t>(y + static_cast<size_t>(p) * n + off, sz), g->grid.get_reader(), p,
+                    MAX_NSYMB_PER_SLOT * slot + l);
+      }
+      off += sz;
+    }
+  };
+  run(out0);
+  if (next_on_host) {
+    resource_grid_writer& w     = g->grid.get_writer();
+    const unsigned        nsubc = g->grid.nof_subc();
+    for (unsigned p = 0; p != nports; ++p) {
+      for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+        const auto* src = reinterpret_cast<const cbf16_t*>(next + (p * MAX_NSYMB_PER_SLOT + l) * nsubc);
+        w.put(p, l, 0, 1, span<const cbf16_t>(src, nsubc));
+      }
+    }
+  } else if (srs_ref_phy_hgrid_set_device(grid, next) != 0) {
+    return -1;
+  }
+  run(out1);
+  return 0;
+}
+
+/* The uplink step puxch_processor_impl runs per OFDM symbol (puxch_processor_impl.cpp:73-82): every port of every
+ * symbol of slot `slot` (of the subframe) demodulated into `grid` through the MI355X OFDM demodulator plug-in, form 1
+ * the ofdm_symbol_demodulator (symbol by symbol, port by port), form 0 the ofdm_slot_demodulator (port by port).
+ * samples: [port][slot size] complex floats.  A device-resident grid (srs_ref_phy_hgrid_create) is written in place on
+ * the device.  0 on success, -1 when the factory refuses the configuration. */
+int srs_ref_phy_ofdm_demodulate(void* grid, int device, int form, unsigned mu, unsigned bw_rb, unsigned dft_size,
+                                double fc, float scale, unsigned slot, unsigned nports, const float* samples)
+{
+  auto                  f = hip::create_ofdm_demodulator_factory_hip(device);
+  const auto            c = ul_dem_cfg(mu, bw_rb, dft_size, fc, scale);
+  resource_grid_writer& w = static_cast<any_grid*>(grid)->wr();
+  const cf_t*           x = reinterpret_cast<const cf_t*>(samples);
+  if (form == 0) {
+    auto d = f->create_ofdm_slot_demodulator(c);
+    if (!d) {
+      return -1;
+    }
+    const unsigned n = d->get_slot_size(slot);
+    for (unsigned p = 0; p != nports; ++p) {
+      d->demodulate(w, span<const cf_t>(x + static_cast<size_t>(p) * n, n), p, slot);
+    }
+    return 0;
+  }
+  auto d = f->create_ofdm_symbol_demodulator(c);
+  if (!d) {
+    return -1;
+  }
+  unsigned                    n   = 0;
+  const std::vector<unsigned> off = symbol_offsets(*d, slot, n);
+  for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+    const unsigned sz = d->get_symbol_size(MAX_NSYMB_PER_SLOT * slot + l);
+    for (unsigned p = 0; p != nports; ++p) {
+      d->demodulate(w, span<const cf_t>(x + static_cast<size_t>(p) * n + off[l], sz), p, MAX_NSYMB_PER_SLOT * slot + l);
+    }
+  }
+  return 0;
+}
+
+/* Symbol-form OFDM demodulation throughput as the lower PHY drives it: `threads` sectors, each with its own
+ * ofdm_symbol_demodulator and its own slot grid, demodulating `slots` slots of `nports` ports symbol by symbol (slot
+ * 0 of the subframe each time; samples: [port][slot size]).  plugin 1: the MI355X plug-in into a device-resident grid
+ * (hip_resource_grid), each sector's grid then read on the device as the PUSCH plug-in reads it (device_read + stream
+ * synchronise: the timed region ends when every kernel has completed); plugin 0: the reference's
+ * ofdm_symbol_demodulator_impl over the generic DFT into a resource_grid_impl.  modulate = 1: the downlink twin,
+ * ofdm_symbol_modulator per port and symbol (pdxch_processor_impl) of the finished grid grid0 [port][14][nsubc] --
+ * on the device for the plug-in, rewritten on the device between slots as the PDSCH plug-in writes it (a new
+ * content version every slot), on the host for the reference.  Returns the wall seconds from the start barrier to
+ * the last sector done (-1: configuration refused); out[0] = mean host time per call (us), out[1] = grid transfers
+ * (downloads + uploads, all sectors). */
+double srs_ref_phy_ofdm_symbol_bench(int device, int plugin, int modulate, unsigned threads, unsigned mu,
+                                     unsigned bw_rb, unsigned dft_size, unsigned nports, unsigned slots,
+                                     const float* samples, const uint32_t* grid0, double* out)
+{
+  const unsigned nsubc = bw_rb * NRE;
+  const auto     c     = ul_dem_cfg(mu, bw_rb, dft_size, 3.5e9);
+  const auto     cm    = dl_mod_cfg(mu, bw_rb, dft_size, 3.5e9, 1.0f / 64);
+  auto           f     = plugin && !modulate ? hip::create_ofdm_demodulator_factory_hip(device) : nullptr;
+  auto           fm    = plugin && modulate ? hip::create_ofdm_modulator_factory_hip(device) : nullptr;
+  std::vector<std::unique_ptr<ofdm_symbol_demodulator>> dems;
+  std::vector<std::unique_ptr<ofdm_symbol_modulator>>   mods;
+  std::vector<std::unique_ptr<dev_grid>>                dgrids;
+  std::vector<std::unique_ptr<resource_grid_impl>>      hgrids;
+  for (unsigned t = 0; t != threads; ++t) {
+    if (modulate) {
+      mods.push_back(plugin ? fm->create_ofdm_symbol_modulator(cm) : srs_ref::make_ref_ofdm_symbol_modulator(cm));
+      if (!mods.back()) {
+        return -1;
+      }
+    } else {
+      dems.push_back(plugin ? f->create_ofdm_symbol_demodulator(c) : srs_ref::make_ref_ofdm_symbol_demodulator(c));
+      if (!dems.back()) {
+        return -1;
+      }
+    }
+    if (plugin) {
+      dgrids.push_back(std::make_unique<dev_grid>(nports, nsubc, device));
+    } else {
+      hgrids.push_back(std::make_unique<resource_grid_impl>(nports, MAX_NSYMB_PER_SLOT, nsubc));
+    }
+    if (modulate) {
+      // the finished downlink grid: on the device for the plug-in (as the PDSCH plug-in leaves it), on the host for
+      // the reference
+      if (plugin) {
+        if (srs_ref_phy_hgrid_set_device(static_cast<any_grid*>(dgrids.back().get()), grid0) != 0) {
+          return -1;
+        }
+      } else {
+        resource_grid_writer& w = hgrids.back()->get_writer();
+        for (unsigned p = 0; p != nports; ++p) {
+          for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+            std::memcpy(static_cast<void*>(w.get_view(p, l).data()), grid0 + (p * MAX_NSYMB_PER_SLOT + l) * nsubc,
+                        nsubc * sizeof(uint32_t));
+          }
+        }
+      }
+    }
+  }
+  unsigned              n = 0;
+  std::vector<unsigned> off(MAX_NSYMB_PER_SLOT), sz(MAX_NSYMB_PER_SLOT);
+  for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+    sz[l]  = modulate ? mods[0]->get_symbol_size(l) : dems[0]->get_symbol_size(l);
+    off[l] = n;
+    n += sz[l];
+  }
+  const cf_t*                 x   = reinterpret_cast<const cf_t*>(samples);
+  std::atomic<unsigned>       arrived{0};
+  std::vector<double>         busy(threads, 0.0);
+  std::vector<int>            fail(threads, 0);
+  auto                        worker = [&](unsigned t) {
+    (void)hipSetDevice(device < 0 ? 0 : device);
+    resource_grid_writer&       w = plugin ? dgrids[t]->grid.get_writer() : hgrids[t]->get_writer();
+    const resource_grid_reader& r = plugin ? dgrids[t]->grid.get_reader() : hgrids[t]->get_reader();
+    std::vector<cf_t>           y(n);
+    hipStream_t                 producer = nullptr; // the PDSCH plug-in's stand-in (modulator runs)
+    if (plugin && modulate && hipStreamCreateWithFlags(&producer, hipStreamNonBlocking) != hipSuccess) {
+      fail[t] = 1;
+    }
+    arrived.fetch_add(1);
+    while (arrived.load() != threads + 1) {
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned s = 0; s != slots; ++s) {
+      for (unsigned l = 0; l != MAX_NSYMB_PER_SLOT; ++l) {
+        for (unsigned p = 0; p != nports; ++p) {
+          if (modulate) {
+            mods[t]->modulate(span<cf_t>(y.data() + off[l], sz[l]), r, p, l);
+          } else {
+            dems[t]->demodulate(w, span<const cf_t>(x + static_cast<size_t>(p) * n + off[l], sz[l]), p, l);
+          }
+        }
+      }
+      if (modulate && plugin && producer != nullptr) {
+        // the next slot's grid, written on the device as the PDSCH plug-in writes it: a new content version, so
+        // the modulator launches again (no cached slot reused across slots)
+        (void)dgrids[t]->grid.device_write(producer);
+        dgrids[t]->grid.device_written(producer);
+      }
+    }
+    if (producer != nullptr) {
+      (void)hipStreamSynchronize(producer);
+      (void)hipStreamDestroy(producer);
+    }
+    busy[t] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (plugin && !modulate) {
+      hipStream_t st = nullptr;
+      fail[t]        = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess;
+      if (!fail[t]) {
+        (void)dgrids[t]->grid.device_read(st);
+        fail[t] = hipStreamSynchronize(st) != hipSuccess;
+        (void)hipStreamDestroy(st);
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (unsigned t = 0; t != threads; ++t) {
+    pool.emplace_back(worker, t);
+  }
+  while (arrived.load() != threads) {
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  arrived.fetch_add(1);
+  for (auto& th : pool) {
+    th.join();
+  }
+  const double dt    = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  double       calls = static_cast<double>(threads) * slots * MAX_NSYMB_PER_SLOT * nports, host = 0;
+  uint64_t     xfer  = 0;
+  for (unsigned t = 0; t != threads; ++t) {
+    host += busy[t];
+    if (plugin) {
+      xfer += dgrids[t]->grid.nof_downloads() + dgrids[t]->grid.nof_uploads();
+    }
+    if (fail[t]) {
+      return -1;
+    }
+  }
+  out[0] = calls > 0 ? host / calls * 1e6 : 0;
+  out[1] = static_cast<double>(xfer);
+  return dt;
+}
+
+} // extern "C"

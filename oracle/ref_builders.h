@@ -318,6 +318,11 @@ void ofdm_run_symbol_demodulator(ofdm_symbol_demodulator& dem, unsigned nsymb, u
 // The reference's ofdm_slot_(de)modulator_impl over the generic DFT (the CPU baseline of the plug-in).
 std::unique_ptr<ofdm_slot_modulator>   make_ref_ofdm_slot_modulator(const ofdm_modulator_configuration& cfg);
 std::unique_ptr<ofdm_slot_demodulator> make_ref_ofdm_slot_demodulator(const ofdm_demodulator_configuration& cfg);
+// The reference's ofdm_symbol_demodulator_impl over the generic DFT (what puxch_processor_impl calls per port and
+// symbol, puxch_processor_impl.cpp:73-82).
+std::unique_ptr<ofdm_symbol_demodulator> make_ref_ofdm_symbol_demodulator(const ofdm_demodulator_configuration& cfg);
+// The reference's ofdm_symbol_modulator_impl over the generic DFT (pdxch_processor_impl's modulator).
+std::unique_ptr<ofdm_symbol_modulator> make_ref_ofdm_symbol_modulator(const ofdm_modulator_configuration& cfg);
 int pusch_demodulate_with(std::unique_ptr<channel_equalizer> eq_impl, const uint32_t* grid, unsigned nof_rx_ports,
                           unsigned nsubc, const uint32_t* estimates, unsigned nof_layers, const float* noise_vars,
                           unsigned rnti, unsigned n_id, int qm, const uint8_t* crbs, unsigned start_symbol,

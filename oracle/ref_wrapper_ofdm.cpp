@@ -248,6 +248,23 @@ std::unique_ptr<ofdm_slot_demodulator> srs_ref::make_ref_ofdm_slot_demodulator(c
                           c.nof_samples_window_offset, c.scale, c.center_freq_Hz);
 }
 
+std::unique_ptr<ofdm_symbol_demodulator>
+srs_ref::make_ref_ofdm_symbol_demodulator(const ofdm_demodulator_configuration& c)
+{
+  ofdm_demodulator_common_configuration common;
+  common.dft = std::make_unique<dft_processor_generic_impl>(
+      dft_processor::configuration{c.dft_size, dft_processor::direction::DIRECT});
+  return std::make_unique<ofdm_symbol_demodulator_impl>(common, c);
+}
+
+std::unique_ptr<ofdm_symbol_modulator> srs_ref::make_ref_ofdm_symbol_modulator(const ofdm_modulator_configuration& c)
+{
+  ofdm_modulator_common_configuration common;
+  common.dft = std::make_unique<dft_processor_generic_impl>(
+      dft_processor::configuration{c.dft_size, dft_processor::direction::INVERSE});
+  return std::make_unique<ofdm_symbol_modulator_impl>(common, c);
+}
+
 extern "C" {
 
 // One dft_processor::run() of the reference generic DFT: in/out interleaved complex float.

@@ -129,13 +129,29 @@ template <int N>
 __global__ __launch_bounds__(dft::plan<N>::T) void ofdm_demodulate_kernel(ofdm_args a)
 {
   __shared__ cf lds[dft::lds_complex<N>()];
-  const uint32_t sym  = blockIdx.x % a.nsymb;
-  const uint32_t item = blockIdx.x / a.nsymb;
-  const uint32_t slot = (a.first_slot + item / a.nof_ports) % a.slots_per_subframe;
-  const ofdm_symbol_info si = a.symbols[slot * a.nsymb + sym];
-  const cf* in = static_cast<const cf*>(a.in) + static_cast<size_t>(item) * a.sample_stride + si.offset + si.cp_len -
-                 a.window_offset;
-  uint32_t*       grid = static_cast<uint32_t*>(a.out) + (static_cast<size_t>(item) * a.nsymb + sym) * a.rg_size;
+  const cf*        in;
+  uint32_t*        grid;
+  ofdm_symbol_info si;
+  if (a.items != nullptr) {
+    // a staged symbol: its own symbol index and grid row (workgroup-uniform)
+    const uint32_t s   = a.items[2 * blockIdx.x];
+    const uint32_t row = a.items[2 * blockIdx.x + 1];
+    if (s >= a.nof_symbol_infos) {
+      return;
+    }
+    si   = a.symbols[s];
+    in   = static_cast<const cf*>(a.in) + static_cast<size_t>(blockIdx.x) * a.sample_stride + si.cp_len -
+           a.window_offset;
+    grid = static_cast<uint32_t*>(a.out) + row;
+  } else {
+    const uint32_t sym  = blockIdx.x % a.nsymb;
+    const uint32_t item = blockIdx.x / a.nsymb;
+    const uint32_t slot = (a.first_slot + item / a.nof_ports) % a.slots_per_subframe;
+    si   = a.symbols[slot * a.nsymb + sym];
+    in   = static_cast<const cf*>(a.in) + static_cast<size_t>(item) * a.sample_stride + si.offset + si.cp_len -
+           a.window_offset;
+    grid = static_cast<uint32_t*>(a.out) + (static_cast<size_t>(item) * a.nsymb + sym) * a.rg_size;
+  }
   const int       half = static_cast<int>(a.rg_size / 2);
   const cf        coef = {si.coef_re, si.coef_im};
   const cf*       win  = reinterpret_cast<const cf*>(a.window);

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include "api_common.h"
+#include "device_buffer.h"
 #include "ofdm_args.h"
 #include <cmath>
 #include <complex>
@@ -292,6 +293,69 @@ struct srs_amd_ofdm_engine {
     return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, is_tx ? "ofdm modulate symbol" : "ofdm demodulate symbol");
   }
 
+  // one symbol between device-accessible buffers on `s` (no copies, no scratch: no lock needed)
+  int run_symbol_async(void* out, const void* in, uint32_t symbol_index, hipStream_t s) const
+  {
+    const uint32_t nsym_sf = geo.nsymb * geo.slots_per_subframe;
+    if (symbol_index >= nsym_sf) {
+      return fail(SRS_AMD_EINVAL, "Symbol index %u exceeds the %u symbols of a subframe.", symbol_index, nsym_sf);
+    }
+    const ofdm_symbol_info& si = geo.symbols[symbol_index];
+    ofdm_args               a{};
+    a.symbols            = d_symbols0 + symbol_index;
+    a.twiddles           = d_twiddles;
+    a.window             = d_window;
+    a.rg_size            = geo.rg;
+    a.nsymb              = 1;
+    a.nof_ports          = 1;
+    a.first_slot         = 0;
+    a.slots_per_subframe = 1;
+    a.nof_items          = 1;
+    a.sample_stride      = si.cp_len + geo.N;
+    a.window_offset      = is_tx ? 0 : cfg.nof_samples_window_offset;
+    a.in                 = in;
+    a.out                = out;
+    hipError_t e         = hipSetDevice(device);
+    if (e == hipSuccess) {
+      e = is_tx ? launch_ofdm_modulate(a, geo.N, s) : launch_ofdm_demodulate(a, geo.N, s);
+    }
+    return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, is_tx ? "ofdm modulate symbol" : "ofdm demodulate symbol");
+  }
+
+  // staged symbols (demodulator): items [count][2] and samples [count][stride], device-accessible, on `s`
+  int run_symbols_async(uint16_t* grid, const uint32_t* items, const float* samples, uint32_t stride, uint32_t count,
+                        hipStream_t s) const
+  {
+    const uint32_t nsym_sf = geo.nsymb * geo.slots_per_subframe;
+    uint32_t       max_sz  = 0;
+    for (uint32_t i = 0; i != nsym_sf; ++i) {
+      max_sz = std::max(max_sz, geo.symbols[i].cp_len + geo.N);
+    }
+    if (stride < max_sz) {
+      return fail(SRS_AMD_EINVAL, "Sample stride %u below the longest symbol (%u samples).", stride, max_sz);
+    }
+    ofdm_args a{};
+    a.symbols            = d_symbols0;
+    a.twiddles           = d_twiddles;
+    a.window             = d_window;
+    a.rg_size            = geo.rg;
+    a.nsymb              = 1;
+    a.nof_ports          = 1;
+    a.slots_per_subframe = 1;
+    a.nof_items          = count;
+    a.sample_stride      = stride;
+    a.window_offset      = cfg.nof_samples_window_offset;
+    a.in                 = samples;
+    a.out                = grid;
+    a.items              = items;
+    a.nof_symbol_infos   = nsym_sf;
+    hipError_t e         = hipSetDevice(device);
+    if (e == hipSuccess) {
+      e = launch_ofdm_demodulate(a, geo.N, s);
+    }
+    return e == hipSuccess ? SRS_AMD_OK : hip_fail(e, "ofdm demodulate symbols");
+  }
+
   uint32_t symbol_size(uint32_t symbol_index) const
   {
     return symbol_index < geo.symbols.size() ? geo.symbols[symbol_index].cp_len + geo.N : 0;
@@ -505,6 +569,56 @@ int srs_amd_ofdm_demodulate_symbol(srs_amd_ofdm_demodulator* dem,
     return fail(SRS_AMD_EINVAL, "null argument");
   }
   return dem->run_symbol(grid_symbol, input, symbol_index);
+}
+
+int srs_amd_ofdm_modulate_symbol_async(srs_amd_ofdm_modulator* mod, float* output, const uint16_t* grid_symbol,
+                                       uint32_t symbol_index, void* stream)
+{
+  if (mod == nullptr || output == nullptr || grid_symbol == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  return mod->run_symbol_async(output, grid_symbol, symbol_index, static_cast<hipStream_t>(stream));
+}
+
+int srs_amd_ofdm_demodulate_symbol_async(srs_amd_ofdm_demodulator* dem, uint16_t* grid_symbol, const float* input,
+                                         uint32_t symbol_index, void* stream)
+{
+  if (dem == nullptr || grid_symbol == nullptr || input == nullptr) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  return dem->run_symbol_async(grid_symbol, input, symbol_index, static_cast<hipStream_t>(stream));
+}
+
+int srs_amd_ofdm_demodulate_symbols_async(srs_amd_ofdm_demodulator* dem, uint16_t* grid, const uint32_t* items,
+                                          const float* samples, uint32_t sample_stride, uint32_t count,
+                                          void* d_scratch, void* stream)
+{
+  if (dem == nullptr || (count != 0 && (grid == nullptr || items == nullptr || samples == nullptr))) {
+    return fail(SRS_AMD_EINVAL, "null argument");
+  }
+  if (count == 0) {
+    return SRS_AMD_OK;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (d_scratch != nullptr) {
+    // pinned staging -> HBM by copy kernels (srs_amd::upload_pinned), then the transform from HBM
+    const size_t sample_bytes = sizeof(float) * 2 * static_cast<size_t>(count) * sample_stride;
+    auto*        d_samples    = static_cast<float*>(d_scratch);
+    auto*        d_items      = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_scratch) + sample_bytes);
+    hipError_t   e            = hipSetDevice(dem->device);
+    if (e == hipSuccess) {
+      e = srs_amd::upload_pinned(d_samples, samples, sample_bytes, s);
+    }
+    if (e == hipSuccess) {
+      e = srs_amd::upload_pinned(d_items, items, sizeof(uint32_t) * 2 * count, s);
+    }
+    if (e != hipSuccess) {
+      return hip_fail(e, "ofdm staged symbols upload");
+    }
+    samples = d_samples;
+    items   = d_items;
+  }
+  return dem->run_symbols_async(grid, items, samples, sample_stride, count, s);
 }
 
 int srs_amd_ofdm_demodulator_create(srs_amd_ofdm_demodulator** dem, const srs_amd_ofdm_config* cfg, int device)

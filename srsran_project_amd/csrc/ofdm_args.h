@@ -30,6 +30,11 @@ struct ofdm_args {
   uint32_t                nof_items; // slots * ports
   uint32_t                sample_stride; // complex samples per (slot, port) row
   uint32_t                window_offset; // demod: nof_samples_window_offset
+  // demod, staged symbols (nsymb = 1, one workgroup per item): item i = {symbol index within the subframe (into
+  // `symbols`, entries with offset 0), first cbf16 of its grid row in `out`}, its samples (CP first) at
+  // in + i * sample_stride; items with a symbol index >= nof_symbol_infos are skipped.  nullptr: the regular layout.
+  const uint32_t*         items;
+  uint32_t                nof_symbol_infos;
 };
 
 struct dft_args {

@@ -386,7 +386,16 @@ def _fapi_ues():
         ("two_layer", dict(common, rnti=0x4605, nid_pusch=25, scrambling_id=250, nscid=1, qm=6,
                            target_code_rate=5670, num_layers=2, rb_start=160, rb_size=40, harq_process_id=4,
                            ul_dmrs_symb_pos=(1 << 2) | (1 << 7) | (1 << 11))),
+        # DFT-s-OFDM over the DC (PRB 136 holds subcarrier 1638): contains_dc changes the geometry
+        # (pusch_processor_impl.cpp:262-286, ulsch_info.cpp:353-357); it takes dc_data's place in even slots
+        ("tp_dc", dict(common, rnti=0x4606, nid_pusch=26, qm=4, target_code_rate=4340, transform_precoding=1,
+                       dmrs_identity=77, rb_start=125, rb_size=25, harq_process_id=5)),
     ]
+
+
+def _default_kinds(slot):
+    """dc_data and tp_dc both hold the DC PRB: odd slots carry dc_data, even slots tp_dc."""
+    return [k for k, _ in _fapi_ues() if k != ("tp_dc" if slot % 2 else "dc_data")]
 
 
 def _fapi_slot(ophy, slot, seed, kinds=None):
@@ -398,8 +407,9 @@ def _fapi_slot(ophy, slot, seed, kinds=None):
     rng = np.random.default_rng(seed)
     z = np.zeros((4, 14, NSUBC), np.complex128)
     out = []
+    kinds = _default_kinds(slot) if kinds is None else kinds
     for u, (kind, f) in enumerate(_fapi_ues()):
-        if kinds is not None and kind not in kinds:
+        if kind not in kinds:
             continue
         pdu = dict(numerology=1, slot_index=slot, rnti=f["rnti"], bwp_start_rb=0, bwp_size_rb=273, modulation=f["qm"],
                    target_code_rate=f["target_code_rate"] / 10.0, rv=0, new_data=1, n_id=f["nid_pusch"],
@@ -432,10 +442,11 @@ def _fapi_slot(ophy, slot, seed, kinds=None):
 
 
 def test_pusch_plugin_fapi_pdus_dc_uci_only_vs_reference(phy):
-    """PUSCH PDUs produced by the reference's own FAPI -> PHY conversion (convert_pusch_fapi_to_phy,
-    lib/fapi_adaptor/phy/messages/pusch.cpp, compiled into the oracle) from FAPI PDUs carrying
-    tx_direct_current_location = 1638 -- a data PDU whose allocation contains the DC, a data + UCI PDU, a UCI-only PDU
-    (no data bit), a DFT-s-OFDM PDU, a two-layer PDU -- through the plug-in's pusch_processor::process,
+    """PUSCH PDUs produced by the reference's own FAPI -> PHY conversion
+    (convert_pusch_fapi_to_phy, lib/fapi_adaptor/phy/messages/pusch.cpp, compiled into the oracle) from FAPI PDUs
+    carrying tx_direct_current_location = 1638 -- a data PDU whose allocation contains the DC (slot 3), a DFT-s-OFDM PDU
+    whose allocation contains the DC (slot 4), a data + UCI PDU, a UCI-only PDU (no data bit), a DFT-s-OFDM PDU off the
+    DC, a two-layer PDU -- through the plug-in's pusch_processor::process,
     equal to the reference's pusch_processor_impl on the same converted PDUs and grid: TB, CRC, LDPC statistics, UCI
     payloads / statuses (on_uci alone for the UCI-only PDU), CSI."""
     ophy, oracle = phy
@@ -733,3 +744,127 @@ def test_pucch_plugin_latency(phy):
     with open(os.path.join(ROOT, "gpurun_out", "pucch_plugin_latency.json"), "w") as f:
         json.dump(out, f)
     assert out["device_grid"]["f0_us"] < 1000 and out["host_grid"]["f2_us"] < 2000, out
+
+
+# ---- the OFDM demodulator plug-in feeding the PUSCH plug-in on the device ----
+
+def _time_domain(oracle, grid, slot, fc):
+    """Each port of the slot through the reference's OFDM modulator (CPU), 100 MHz, 4096-point DFT, scale 1/64."""
+    u16 = np.ascontiguousarray(grid).view(np.uint16).reshape(grid.shape[0], 14, -1)
+    return np.stack([oracle.ref_ofdm_modulate_slot(u16[p], slot % 2, 1, 273, 4096, 1 / 64, fc)
+                     for p in range(grid.shape[0])])
+
+
+@pytest.mark.parametrize("form", [1, 0], ids=["symbol_form", "slot_form"])
+def test_ofdm_demodulator_plugin_feeds_pusch_plugin_on_device(phy, form):
+    """The uplink chain through the reference interfaces with the grid resident in HBM: the OFDM demodulator plug-in
+    (ofdm_symbol_demodulator called per port and symbol as puxch_processor_impl.cpp:73-82 does; or the slot form)
+    writes a hip_resource_grid's device copy in place, the PUSCH plug-in reads it there.  Bars: zero grid transfers
+    (no download, no upload) up to the PUSCH results; the demodulated grid within one bf16 ulp of the reference's
+    ofdm_slot_demodulator_impl on the same samples; the PUSCH plug-in equal to the reference's pusch_processor_impl on
+    that grid (TB, CRC, LDPC statistics, UCI, CSI); end to end, the transport blocks and UCI the UEs sent, as the
+    reference's chain (its demodulator, then pusch_processor_impl) also returns."""
+    from pusch_slot_cases import NSUBC
+
+    ophy, oracle = phy
+    slot, fc = 3, 3.5e9
+    grid, ues = _fapi_slot(ophy, slot, seed=17, kinds=["dc_data", "uci_data", "tp", "two_layer"])
+    x = _time_domain(oracle, grid, slot, fc)
+    dg = ophy.DeviceGrid(shape=(4, 14, NSUBC))
+    ophy.ofdm_demodulate(dg, x, slot % 2, 1, 273, 4096, fc, scale=1 / 64, form=form)
+    plug = ophy.PuschProcessorPlugin(device=0, iterations=ITERS)
+    tickets = [plug.process_fapi(dg, fp) for _, fp, _, _ in ues]
+    plug.flush()
+    plug.wait()
+    assert dg.transfers() == dict(downloads=0, uploads=0)
+    assert plug.stats()["device_grids"] >= 1 and plug.stats()["errors"] == 0
+    got_grid = dg.read()  # (the first host access: one download)
+    want_grid = np.stack([oracle.ref_ofdm_demodulate_slot(x[p], slot % 2, 1, 273, 4096, 1 / 64, fc)
+                          for p in range(4)]).view(np.uint32)
+    a = (got_grid.view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+    b = (want_grid.view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+    tol = 2.0 ** -7 * np.maximum(np.abs(a), np.abs(b)) + 3e-5 * np.sqrt(np.mean(b ** 2))
+    assert (np.abs(a - b) <= tol).all() and (got_grid == want_grid).mean() >= 0.99
+    same, ref_chain = ophy.Grid(got_grid), ophy.Grid(want_grid)
+    for (kind, fp, tb_sent, uci), (t, tb) in zip(ues, tickets):
+        got = plug.result(t, fp.fapi.harq_ack_bit_length, fp.fapi.csi_part1_bit_length)
+        want_tb, want = ophy.ref_pusch_process_fapi(same, fp, iterations=ITERS)
+        _check(got, want, kind)
+        assert np.array_equal(tb, want_tb) and got["tb_crc_ok"] and np.array_equal(tb, tb_sent), kind
+        chain_tb, chain = ophy.ref_pusch_process_fapi(ref_chain, fp, iterations=ITERS)
+        assert chain["tb_crc_ok"] and np.array_equal(chain_tb, tb), kind
+        if uci is not None:
+            assert np.array_equal(got["harq_ack"], uci[0]) and np.array_equal(got["csi_part1"], uci[1]), kind
+            assert np.array_equal(chain["harq_ack"], uci[0]) and np.array_equal(chain["csi_part1"], uci[1]), kind
+
+
+def _random_grid(seed, ports=4):
+    from oracle import ofdm as oofdm
+    from pusch_slot_cases import NSUBC
+
+    rng = np.random.default_rng(seed)
+    return np.stack([oofdm.random_grid(rng, 14, NSUBC) for _ in range(ports)]).view(np.uint32)
+
+
+@pytest.mark.parametrize("form", [1, 0], ids=["symbol_form", "slot_form"])
+def test_ofdm_modulator_plugin_reads_device_grid(phy, form):
+    """The downlink end of the chain: a grid written on the device (as the PDSCH plug-in leaves it) modulated by the
+    OFDM modulator plug-in in place -- every port of the slot in one launch at the first call, later calls served from
+    that launch -- with zero grid transfers; samples within 2e-5 x RMS of the reference's ofdm_slot_modulator_impl on
+    the same grid.  The symbol form again on the same grid rewritten on the device and through the host writer: the
+    plug-in's per-slot samples follow the grid's content (no stale slot)."""
+    ophy, oracle = phy
+    slot, fc = 1, 3.5e9
+    g0, g1 = _random_grid(21), _random_grid(22)
+
+    def want(g):
+        u16 = g.view(np.uint16).reshape(4, 14, -1)
+        return np.stack([oracle.ref_ofdm_modulate_slot(u16[p], slot, 1, 273, 4096, 1 / 64, fc) for p in range(4)])
+
+    w0, w1 = want(g0), want(g1)
+    rms = float(np.sqrt(np.mean(np.abs(w0) ** 2)))
+    dg = ophy.DeviceGrid(g0, device=True)
+    got = ophy.ofdm_modulate(dg, 4, slot, 1, 273, 4096, fc, 1 / 64, w0.shape[1], form=form)
+    assert dg.transfers() == dict(downloads=0, uploads=0)
+    assert np.max(np.abs(got - w0)) <= 2e-5 * rms
+    if form == 1:
+        for on_host in (False, True):
+            dg = ophy.DeviceGrid(g0, device=True)
+            y0, y1 = ophy.ofdm_modulate_twice(dg, 4, slot, 1, 273, 4096, fc, 1 / 64, w0.shape[1], g1, on_host)
+            assert np.max(np.abs(y0 - w0)) <= 2e-5 * rms, on_host
+            assert np.max(np.abs(y1 - w1)) <= 2e-5 * rms, on_host
+            # (a host write after device writes merges the device's changes into the host mirror first: one download)
+            assert dg.transfers()["downloads"] == int(on_host), on_host
+
+
+def test_ofdm_symbol_plugin_rate(phy):
+    """Symbol-form OFDM as the lower PHY drives it (one ofdm_symbol_(de)modulator per sector, one call per port and
+    symbol): 16 sector threads through the plug-ins on device-resident grids -- the demodulator staging its symbols
+    and launching a slot at a time (the timed region ends when every kernel has completed), the modulator launching
+    every port of a slot at its first call on a grid rewritten on the device every slot -- beside 16 threads of the
+    reference's ofdm_symbol_(de)modulator_impl (generic DFT), 100 MHz / 4096-point / 4 ports; also one sector alone
+    (host time per call).  Zero grid transfers.  Written to gpurun_out/ofdm_symbol_plugin_rate.json."""
+    import json
+
+    ophy, oracle = phy
+    rng = np.random.default_rng(5)
+    x = (rng.normal(size=(4, 61440)) + 1j * rng.normal(size=(4, 61440))).astype(np.complex64) * 0.1
+    g = _random_grid(23)
+    out = {}
+    for kind, modulate in (("demodulator", False), ("modulator", True)):
+        ophy.ofdm_symbol_bench(1, 1, 1, 273, 4096, x, 2, modulate=modulate, grid=g)  # warm-up (code objects, pinned)
+        res = {}
+        for name, plugin, threads, slots in (("plugin_1_sector", 1, 1, 200), ("plugin_16_sectors", 1, 16, 100),
+                                             ("reference_16_threads", 0, 16, 4)):
+            dt, us_call, xfer = ophy.ofdm_symbol_bench(plugin, threads, 1, 273, 4096, x, slots, modulate=modulate,
+                                                       grid=g)
+            assert xfer == 0
+            res[name] = dict(symbols_per_s=threads * slots * 14 * 4 / dt, host_us_per_call=us_call,
+                             slot_us_per_sector=1e6 * dt / slots, threads=threads)
+        res["plugin_vs_reference_16"] = res["plugin_16_sectors"]["symbols_per_s"] / res["reference_16_threads"][
+            "symbols_per_s"]
+        out[kind] = res
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/ofdm_symbol_plugin_rate.json", "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(out)
