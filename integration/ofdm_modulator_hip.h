@@ -11,10 +11,24 @@
 //   the demodulator twins (ofdm_demodulator.h:44-100): srs_amd_ofdm_demodulate_slot / _symbol, every subcarrier of
 //       the demodulated symbols stored through resource_grid_writer::get_view (the reference's symbol demodulator
 //       writes the whole symbol with resource_grid_writer::put).
-// Grid rows are read with resource_grid_reader::get_view into pinned staging (an empty port gives zeros, as
-// ofdm_symbol_modulator_impl::modulate); every call is synchronous, as the interface is.  Errors are logged and give
-// zeros; nothing aborts.  create_* returns nullptr for a configuration the MI355X kernels do not take (DFT sizes of
-// include/srsran_amd/ofdm.h).  Compiled against the reference's headers by integration/Makefile.
+// On a reference grid, rows are read with resource_grid_reader::get_view into pinned staging (an empty port gives
+// zeros, as ofdm_symbol_modulator_impl::modulate) and written back through resource_grid_writer::get_view; every call
+// is synchronous.
+//
+// On a device-resident grid (hip_resource_grid.h) the grid never crosses PCIe (r06):
+//   demodulators: each call copies its samples into pinned staging with the symbol index and grid row, and registers
+//       with the grid as a deferred writer; the staged symbols are demodulated into the device copy in ONE launch
+//       (srs_amd_ofdm_demodulate_symbols_async) when the grid is next accessed -- the PUSCH plug-in's read -- or when
+//       64 are staged.  A call makes no HIP call and never waits for the device (1.2-1.7 us per 4096-point symbol on
+//       one host thread, profiles/r06_ofdm_symbol_plugin_rate_*.json); the kernel reads the pinned samples over the
+//       bus (SRS_AMD_OFDM_STAGING=dma / copy-kernel: DMA or a copy kernel into HBM first, measured slower).
+//   modulators: the first call for a slot modulates every port of that slot in place in one launch
+//       (srs_amd_ofdm_modulate_batch on the device copy, samples DMA-copied to pinned memory); the later calls of the
+//       slot copy their share while the grid is unchanged (hip_resource_grid::unchanged_since): the lower PHY calls
+//       per port and symbol on a finished grid.  The samples leave the device because the interface returns them.
+// Errors are logged and give zeros; nothing aborts.  create_* returns nullptr for a configuration the MI355X kernels
+// do not take (DFT sizes of include/srsran_amd/ofdm.h).  Compiled against the reference's headers by
+// integration/Makefile, into libsrsran_amd_phy.so with hip_resource_grid.
 #pragma once
 
 #include "srsran/phy/lower/modulation/modulation_factories.h"
