@@ -7,8 +7,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <tuple>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -110,12 +117,272 @@ srs_amd_pucch_f34_pdu convert34(const C& c, uint32_t format, uint32_t nof_prb, u
   return p;
 }
 
+// One process() call on a device-resident grid, waiting in the rendezvous (below) for its batch.
+struct pucch_call {
+  enum kind_t { F0, F1, F2, F34 } kind = F0;
+  hip_resource_grid*                  grid = nullptr;
+  unsigned                            nof_ports = 0, nsubc = 0;
+  srs_amd_pucch_f0_pdu                f0{};
+  srs_amd_pucch_f1_batch              f1{};
+  std::vector<srs_amd_pucch_f1_entry> entries;
+  srs_amd_pucch_f2_pdu                f2{};
+  srs_amd_pucch_f34_pdu               f34{};
+  unsigned                            K = 0; // payload bits (Formats 2-4)
+  // filled by the batch's leader
+  bool                              ok = false, done = false;
+  bool                              lead = false; // this caller leads the next batch
+  std::condition_variable           cv;           // done, or lead handed over
+  srs_amd_pucch_f0_result           r0{};
+  std::vector<srs_amd_pucch_result> r1;
+  srs_amd_pucch_uci_result          ruci{};
+  std::vector<uint8_t>              payload;
+};
+
+// Rendezvous of the synchronous pucch_processor::process calls of every processor of the factory.
+// uplink_processor_impl hands all PUCCH PDUs of a slot's end symbol to the PUCCH executor at once
+// (uplink_processor_impl.cpp:199-229, one task per PDU): the calls that arrive while a batch is in flight on the GPU
+// (or within `window_us` of the first) go together in the next one -- one slot-form launch per format, one result
+// download, one synchronisation -- and each caller returns with its own result.  The first waiting caller leads the
+// batch (no thread of its own); the others sleep until it is done.
+class pucch_rendezvous
+{
+public:
+  pucch_rendezvous(srs_amd_pucch_processor* p, int dev, unsigned window) : proc(p), device(dev), window_us(window)
+  {
+    (void)hipSetDevice(device);
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+      throw std::runtime_error("pucch_processor_hip: rendezvous stream");
+    }
+  }
+  ~pucch_rendezvous()
+  {
+    (void)hipSetDevice(device);
+    (void)hipStreamSynchronize(stream);
+    (void)hipStreamDestroy(stream);
+    (void)hipFree(d_buf);
+    (void)hipHostFree(h_buf);
+  }
+
+  // returns when c's batch is done (c.ok: processed).  Each waiting caller sleeps on its own condition variable: the
+  // leader wakes exactly the callers of its batch and hands the lead to the oldest caller still pending.
+  void submit(pucch_call& c)
+  {
+    std::unique_lock<std::mutex> lock(mtx);
+    pending.push_back(&c);
+    if (!leading) {
+      leading = true;
+      c.lead  = true;
+    }
+    while (!c.done) {
+      if (!c.lead) {
+        c.cv.wait(lock);
+        continue;
+      }
+      c.lead = false;
+      if (window_us != 0) {
+        lock.unlock();
+        std::this_thread::sleep_for(std::chrono::microseconds(window_us));
+        lock.lock();
+      }
+      std::vector<pucch_call*> batch;
+      batch.swap(pending);
+      lock.unlock();
+      run(batch);
+      lock.lock();
+      ++nof_batches;
+      for (pucch_call* b : batch) {
+        b->done = true;
+        if (b != &c) {
+          b->cv.notify_one();
+        }
+      }
+      if (pending.empty()) {
+        leading = false;
+      } else {
+        pending.front()->lead = true;
+        pending.front()->cv.notify_one();
+      }
+    }
+  }
+
+  std::atomic<uint64_t> nof_batches{0};
+  // time spent by the leaders: reading the grids and launching (host), then waiting for the batch's results
+  std::atomic<uint64_t> host_ns{0}, wait_ns{0};
+
+private:
+  // (kind, grid ports, grid subcarriers): calls that go in one slot-form launch
+  using group_key = std::tuple<int, unsigned, unsigned>;
+
+  bool reserve(size_t bytes)
+  {
+    if (bytes <= capacity) {
+      return true;
+    }
+    (void)hipFree(d_buf);
+    (void)hipHostFree(h_buf);
+    d_buf    = nullptr;
+    h_buf    = nullptr;
+    capacity = 0;
+    if (hipMalloc(&d_buf, bytes) != hipSuccess || hipHostMalloc(&h_buf, bytes, hipHostMallocDefault) != hipSuccess) {
+      return false;
+    }
+    capacity = bytes;
+    return true;
+  }
+
+  void run(std::vector<pucch_call*>& batch)
+  {
+    const auto t_start = std::chrono::steady_clock::now();
+    (void)hipSetDevice(device);
+    std::map<group_key, std::vector<pucch_call*>> groups;
+    for (pucch_call* c : batch) {
+      groups[{static_cast<int>(c->kind), c->nof_ports, c->nsubc}].push_back(c);
+    }
+    // result area: per group, the results then (Formats 2-4) the payload rows
+    constexpr size_t PAY = 1706;
+    size_t           bytes = 0;
+    std::vector<size_t> off;
+    for (auto& [key, calls] : groups) {
+      off.push_back(bytes);
+      size_t n = 0;
+      switch (std::get<0>(key)) {
+        case pucch_call::F0:
+          n = calls.size() * sizeof(srs_amd_pucch_f0_result);
+          break;
+        case pucch_call::F1:
+          for (pucch_call* c : calls) {
+            n += c->entries.size() * sizeof(srs_amd_pucch_result);
+          }
+          break;
+        default:
+          n = calls.size() * (sizeof(srs_amd_pucch_uci_result) + PAY);
+      }
+      bytes += (n + 255) & ~size_t(255);
+    }
+    if (!reserve(bytes)) {
+      return; // (ok stays false: logged by the callers)
+    }
+    // every distinct grid read once on the rendezvous stream (it waits for the grid's producers)
+    std::map<hip_resource_grid*, const uint32_t*> dev_of;
+    for (pucch_call* c : batch) {
+      if (dev_of.count(c->grid) == 0) {
+        dev_of[c->grid] = c->grid->device_read(stream);
+      }
+    }
+    bool   ok = true;
+    size_t gi = 0;
+    for (auto& [key, calls] : groups) {
+      uint8_t*       d     = static_cast<uint8_t*>(d_buf) + off[gi++];
+      const unsigned ports = std::get<1>(key), nsubc = std::get<2>(key);
+      const unsigned n     = static_cast<unsigned>(calls.size());
+      int            rc    = SRS_AMD_OK;
+      switch (std::get<0>(key)) {
+        case pucch_call::F0: {
+          std::vector<srs_amd_pucch_f0_pdu> pdus;
+          for (pucch_call* c : calls) {
+            pdus.push_back(c->f0);
+            pdus.back().d_grid = dev_of[c->grid];
+          }
+          rc = srs_amd_pucch_f0_detect_slot(proc, pdus.data(), n, nullptr, 0, 0, ports, nsubc,
+                                            reinterpret_cast<srs_amd_pucch_f0_result*>(d), stream);
+          break;
+        }
+        case pucch_call::F1: {
+          std::vector<srs_amd_pucch_f1_batch> bs;
+          for (pucch_call* c : calls) {
+            bs.push_back(c->f1);
+            bs.back().d_grid  = dev_of[c->grid];
+            bs.back().entries = c->entries.data();
+          }
+          rc = srs_amd_pucch_f1_detect_slot(proc, bs.data(), n, nullptr, 0, 0, ports, nsubc,
+                                            reinterpret_cast<srs_amd_pucch_result*>(d), stream);
+          break;
+        }
+        case pucch_call::F2: {
+          std::vector<srs_amd_pucch_f2_pdu> pdus;
+          for (pucch_call* c : calls) {
+            pdus.push_back(c->f2);
+            pdus.back().d_grid = dev_of[c->grid];
+          }
+          rc = srs_amd_pucch_f2_process_slot(proc, pdus.data(), n, nullptr, 0, 0, ports, nsubc,
+                                             reinterpret_cast<srs_amd_pucch_uci_result*>(d),
+                                             d + n * sizeof(srs_amd_pucch_uci_result), PAY, stream);
+          break;
+        }
+        default: {
+          std::vector<srs_amd_pucch_f34_pdu> pdus;
+          for (pucch_call* c : calls) {
+            pdus.push_back(c->f34);
+            pdus.back().d_grid = dev_of[c->grid];
+          }
+          rc = srs_amd_pucch_f34_process_slot(proc, pdus.data(), n, nullptr, 0, 0, ports, nsubc,
+                                              reinterpret_cast<srs_amd_pucch_uci_result*>(d),
+                                              d + n * sizeof(srs_amd_pucch_uci_result), PAY, stream);
+        }
+      }
+      if (rc != SRS_AMD_OK) {
+        log_error("batch not processed", srs_amd_last_error());
+        ok = false;
+      }
+    }
+    ok             = ok && hipMemcpyAsync(h_buf, d_buf, bytes, hipMemcpyDeviceToHost, stream) == hipSuccess;
+    const auto t_l = std::chrono::steady_clock::now();
+    ok             = hipStreamSynchronize(stream) == hipSuccess && ok;
+    const auto t_w = std::chrono::steady_clock::now();
+    host_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t_l - t_start).count();
+    wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t_w - t_l).count();
+    if (!ok) {
+      return;
+    }
+    gi = 0;
+    for (auto& [key, calls] : groups) {
+      const uint8_t* h = static_cast<const uint8_t*>(h_buf) + off[gi++];
+      const size_t   n = calls.size();
+      size_t         e = 0;
+      for (size_t i = 0; i != n; ++i) {
+        pucch_call& c = *calls[i];
+        switch (c.kind) {
+          case pucch_call::F0:
+            std::memcpy(&c.r0, h + i * sizeof(srs_amd_pucch_f0_result), sizeof(c.r0));
+            break;
+          case pucch_call::F1:
+            c.r1.resize(c.entries.size());
+            std::memcpy(c.r1.data(), h + e * sizeof(srs_amd_pucch_result), c.r1.size() * sizeof(srs_amd_pucch_result));
+            e += c.entries.size();
+            break;
+          default:
+            std::memcpy(&c.ruci, h + i * sizeof(srs_amd_pucch_uci_result), sizeof(c.ruci));
+            c.payload.assign(h + n * sizeof(srs_amd_pucch_uci_result) + i * PAY,
+                             h + n * sizeof(srs_amd_pucch_uci_result) + i * PAY + c.K);
+        }
+        c.ok = true;
+      }
+    }
+  }
+
+  srs_amd_pucch_processor* proc;
+  int                      device;
+  unsigned                 window_us;
+  hipStream_t              stream   = nullptr;
+  void*                    d_buf    = nullptr;
+  void*                    h_buf    = nullptr;
+  size_t                   capacity = 0;
+  std::mutex               mtx;
+  std::vector<pucch_call*> pending;
+  bool                     leading = false;
+};
+
 struct shared_state {
-  srs_amd_pucch_processor*   proc   = nullptr;
-  int                        device = 0;
-  pucch_processor_hip_config cfg;
-  std::atomic<uint64_t>      nof_pdus{0}, nof_errors{0}, nof_device{0};
-  ~shared_state() { srs_amd_pucch_processor_destroy(proc); }
+  srs_amd_pucch_processor*          proc   = nullptr;
+  int                               device = 0;
+  pucch_processor_hip_config        cfg;
+  std::atomic<uint64_t>             nof_pdus{0}, nof_errors{0}, nof_device{0};
+  std::unique_ptr<pucch_rendezvous> rdv;
+  ~shared_state()
+  {
+    rdv.reset();
+    srs_amd_pucch_processor_destroy(proc);
+  }
 };
 
 class pucch_processor_hip : public pucch_processor
@@ -152,14 +419,24 @@ public:
     }
     srs_amd_pucch_f0_pdu p = convert(config);
     unsigned             nof_ports = 0, nsubc = 0;
-    const uint32_t*      g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
-    auto*                r = static_cast<srs_amd_pucch_f0_result*>(h_res);
-    if (g == nullptr || !run([&] {
-          p.d_grid = g;
-          return srs_amd_pucch_f0_detect_slot(st->proc, &p, 1, nullptr, 0, 0, nof_ports, nsubc,
-                                              static_cast<srs_amd_pucch_f0_result*>(d_res), stream);
-        }, sizeof(srs_amd_pucch_f0_result))) {
-      return result;
+    const srs_amd_pucch_f0_result* r = static_cast<srs_amd_pucch_f0_result*>(h_res);
+    pucch_call                     call;
+    if (hip_resource_grid* hg = hip_grid_of(grid)) {
+      call.kind = pucch_call::F0;
+      call.f0   = p;
+      if (!rendezvous(call, *hg)) {
+        return result;
+      }
+      r = &call.r0;
+    } else {
+      const uint32_t* g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
+      if (g == nullptr || !run([&] {
+            p.d_grid = g;
+            return srs_amd_pucch_f0_detect_slot(st->proc, &p, 1, nullptr, 0, 0, nof_ports, nsubc,
+                                                static_cast<srs_amd_pucch_f0_result*>(d_res), stream);
+          }, sizeof(srs_amd_pucch_f0_result))) {
+        return result;
+      }
     }
     result.message = pucch_uci_message({.nof_sr = r->nof_sr, .nof_harq_ack = r->nof_harq_ack, .nof_csi_part1 = 0,
                                         .nof_csi_part2 = 0});
@@ -217,16 +494,27 @@ public:
       log_error("batch not processed", "too many entries");
       return out;
     }
-    unsigned        nof_ports = 0, nsubc = 0;
-    const uint32_t* g = grid_for(grid, b.ports, b.nof_ports, b.start_symbol_index, b.nof_symbols, nof_ports, nsubc);
-    if (g == nullptr || !run([&] {
-          b.d_grid = g;
-          return srs_amd_pucch_f1_detect_slot(st->proc, &b, 1, nullptr, 0, 0, nof_ports, nsubc,
-                                              static_cast<srs_amd_pucch_result*>(d_res), stream);
-        }, entries.size() * sizeof(srs_amd_pucch_result))) {
-      return out;
+    unsigned                    nof_ports = 0, nsubc = 0;
+    const srs_amd_pucch_result* r = static_cast<const srs_amd_pucch_result*>(h_res);
+    pucch_call                  call;
+    if (hip_resource_grid* hg = hip_grid_of(grid)) {
+      call.kind    = pucch_call::F1;
+      call.f1      = b;
+      call.entries = entries;
+      if (!rendezvous(call, *hg)) {
+        return out;
+      }
+      r = call.r1.data();
+    } else {
+      const uint32_t* g = grid_for(grid, b.ports, b.nof_ports, b.start_symbol_index, b.nof_symbols, nof_ports, nsubc);
+      if (g == nullptr || !run([&] {
+            b.d_grid = g;
+            return srs_amd_pucch_f1_detect_slot(st->proc, &b, 1, nullptr, 0, 0, nof_ports, nsubc,
+                                                static_cast<srs_amd_pucch_result*>(d_res), stream);
+          }, entries.size() * sizeof(srs_amd_pucch_result))) {
+        return out;
+      }
     }
-    const auto* r = static_cast<const srs_amd_pucch_result*>(h_res);
     for (unsigned k = 0; k != entries.size(); ++k) {
       pucch_processor_result& res = out.get(entries[k].initial_cyclic_shift, entries[k].time_domain_occ);
       for (unsigned i = 0; i != r[k].nof_harq_ack && i != 2; ++i) {
@@ -255,17 +543,31 @@ public:
     }
     srs_amd_pucch_f2_pdu p = convert(config);
     const unsigned       K = config.nof_sr + config.nof_harq_ack + config.nof_csi_part1 + config.nof_csi_part2;
-    unsigned             nof_ports = 0, nsubc = 0;
-    const uint32_t*      g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
-    auto*                d_pay = static_cast<uint8_t*>(d_res) + PAYLOAD_OFF;
-    if (g == nullptr || K > 1706 || !run([&] {
+    if (K > 1706) {
+      return result;
+    }
+    if (hip_resource_grid* hg = hip_grid_of(grid)) {
+      pucch_call call;
+      call.kind = pucch_call::F2;
+      call.f2   = p;
+      call.K    = K;
+      if (rendezvous(call, *hg)) {
+        fill_uci(result, K, call.ruci, call.payload.data());
+      }
+      return result;
+    }
+    unsigned        nof_ports = 0, nsubc = 0;
+    const uint32_t* g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
+    auto*           d_pay = static_cast<uint8_t*>(d_res) + PAYLOAD_OFF;
+    if (g == nullptr || !run([&] {
           p.d_grid = g;
           return srs_amd_pucch_f2_process_slot(st->proc, &p, 1, nullptr, 0, 0, nof_ports, nsubc,
                                                static_cast<srs_amd_pucch_uci_result*>(d_res), d_pay, 1706, stream);
         }, PAYLOAD_OFF + K)) {
       return result;
     }
-    fill_uci(result, K);
+    fill_uci(result, K, *static_cast<const srs_amd_pucch_uci_result*>(h_res),
+             static_cast<const uint8_t*>(h_res) + PAYLOAD_OFF);
     return result;
   }
 
@@ -309,25 +611,55 @@ private:
     if (!normal_cp(cp)) {
       return result;
     }
-    const unsigned  K         = sr + harq + csi1 + csi2;
+    const unsigned K = sr + harq + csi1 + csi2;
+    if (K > 1706) {
+      return result;
+    }
+    if (hip_resource_grid* hg = hip_grid_of(grid)) {
+      pucch_call call;
+      call.kind = pucch_call::F34;
+      call.f34  = p;
+      call.K    = K;
+      if (rendezvous(call, *hg)) {
+        fill_uci(result, K, call.ruci, call.payload.data());
+      }
+      return result;
+    }
     unsigned        nof_ports = 0, nsubc = 0;
     const uint32_t* g = grid_for(grid, p.ports, p.nof_ports, p.start_symbol_index, p.nof_symbols, nof_ports, nsubc);
     auto*           d_pay = static_cast<uint8_t*>(d_res) + PAYLOAD_OFF;
-    if (g == nullptr || K > 1706 || !run([&] {
+    if (g == nullptr || !run([&] {
           p.d_grid = g;
           return srs_amd_pucch_f34_process_slot(st->proc, &p, 1, nullptr, 0, 0, nof_ports, nsubc,
                                                 static_cast<srs_amd_pucch_uci_result*>(d_res), d_pay, 1706, stream);
         }, PAYLOAD_OFF + K)) {
       return result;
     }
-    fill_uci(result, K);
+    fill_uci(result, K, *static_cast<const srs_amd_pucch_uci_result*>(h_res),
+             static_cast<const uint8_t*>(h_res) + PAYLOAD_OFF);
     return result;
   }
 
-  void fill_uci(pucch_processor_result& result, unsigned K) const
+  // a device-resident grid: the call joins the factory's rendezvous (one launch for every call that waits with it)
+  bool rendezvous(pucch_call& call, hip_resource_grid& hg)
   {
-    const auto* r = static_cast<const srs_amd_pucch_uci_result*>(h_res);
-    std::memcpy(result.message.get_full_payload().data(), static_cast<const uint8_t*>(h_res) + PAYLOAD_OFF, K);
+    ++st->nof_device;
+    call.grid      = &hg;
+    call.nof_ports = hg.nof_ports();
+    call.nsubc     = hg.nof_subc();
+    st->rdv->submit(call);
+    if (!call.ok) {
+      ++st->nof_errors;
+      log_error("PDU not processed", "rendezvous batch failed");
+    }
+    return call.ok;
+  }
+
+  static void fill_uci(pucch_processor_result& result, unsigned K, const srs_amd_pucch_uci_result& res,
+                       const uint8_t* payload)
+  {
+    const auto* r = &res;
+    std::memcpy(result.message.get_full_payload().data(), payload, K);
     result.message.set_status(static_cast<uci_status>(r->status));
     result.csi = channel_state_information();
     result.csi.set_epre(r->epre_dB);
@@ -597,6 +929,9 @@ public:
     s.nof_pdus         = st->nof_pdus;
     s.nof_errors       = st->nof_errors;
     s.nof_device_grids = st->nof_device;
+    s.nof_batches      = st->rdv->nof_batches;
+    s.batch_host_us    = st->rdv->host_ns / 1000;
+    s.batch_wait_us    = st->rdv->wait_ns / 1000;
     return s;
   }
 
@@ -619,6 +954,12 @@ srsran::hip::create_pucch_processor_factory_hip(const pucch_processor_hip_config
   st->device = dev;
   if (srs_amd_pucch_processor_create(&st->proc, dev) != SRS_AMD_OK) {
     log_error("create", srs_amd_last_error());
+    return nullptr;
+  }
+  try {
+    st->rdv = std::make_unique<pucch_rendezvous>(st->proc, dev, cfg.rendezvous_window_us);
+  } catch (const std::exception& e) {
+    log_error("create", e.what());
     return nullptr;
   }
   return std::make_shared<pucch_processor_factory_hip_impl>(std::move(st));

@@ -51,6 +51,7 @@
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 using namespace srsran;
@@ -1296,13 +1297,98 @@ int srs_ref_phy_pucch_f2_validate(void* h, const srs_amd_pucch_f2_pdu* p, char* 
   return 0;
 }
 
-/* [0] PDUs, [1] errors, [2] device-resident grids. */
+/* [0] PDUs, [1] errors, [2] device-resident grids, [3] rendezvous batches, [4] / [5] the batches' host / wait us. */
 void srs_ref_phy_pucch_stats(void* h, uint64_t* out)
 {
   const auto s = static_cast<pucch_ctx*>(h)->factory->get_statistics();
   out[0]       = s.nof_pdus;
   out[1]       = s.nof_errors;
   out[2]       = s.nof_device_grids;
+  out[3]       = s.nof_batches;
+  out[4]       = s.batch_host_us;
+  out[5]       = s.batch_wait_us;
+}
+
+/* The PUCCHs of `ncells` cells through the plug-in as the reference's uplink processor drives them: every PDU of a
+ * cell's slot (the same lists for every cell, grid g[c]) one synchronous pucch_processor::process call each, spread
+ * over `threads` PUCCH-executor threads (each with its own processor of the factory: uplink_processor_impl posts one
+ * task per PDU), `reps` times.  Returns the wall seconds.  Outputs of the first rep (optional, per cell in list
+ * order): r0[ncells][n0], r1[ncells][sum of entries], r2 / r34 [ncells][n] with payloads p2 / p34 [..][64]. */
+double srs_ref_phy_pucch_mt_bench(void* h, void* const* grids, unsigned ncells, const srs_amd_pucch_f0_pdu* f0,
+                                  unsigned n0, const srs_amd_pucch_f1_batch* f1, unsigned n1,
+                                  const srs_amd_pucch_f2_pdu* f2, unsigned n2, const srs_amd_pucch_f34_pdu* f34,
+                                  unsigned n34, unsigned threads, unsigned reps, unsigned grid_prb,
+                                  srs_amd_pucch_result* r0, srs_amd_pucch_result* r1, srs_amd_pucch_uci_result* r2,
+                                  uint8_t* p2, srs_amd_pucch_uci_result* r34, uint8_t* p34)
+{
+  auto* base = static_cast<pucch_ctx*>(h);
+  std::vector<std::unique_ptr<pucch_ctx>> ctxs;
+  for (unsigned t = 0; t != threads; ++t) {
+    auto c     = std::make_unique<pucch_ctx>();
+    c->factory = base->factory;
+    c->proc    = base->factory->create();
+    if (!c->proc) {
+      return -1;
+    }
+    ctxs.push_back(std::move(c));
+  }
+  unsigned ne = 0;
+  std::vector<unsigned> e0(n1);
+  for (unsigned i = 0; i != n1; ++i) {
+    e0[i] = ne;
+    ne += f1[i].nof_entries;
+  }
+  const unsigned per_cell = n0 + n1 + n2 + n34;
+  const unsigned items    = per_cell * ncells;
+  std::atomic<unsigned> arrived{0};
+  auto worker = [&](unsigned t) {
+    srs_amd_pucch_result              x0;
+    std::vector<srs_amd_pucch_result> x1(std::max(ne, 1u));
+    srs_amd_pucch_uci_result xu;
+    uint8_t                  pay[1706];
+    arrived.fetch_add(1);
+    while (arrived.load() != threads + 1) {
+    }
+    for (unsigned r = 0; r != reps; ++r) {
+      for (unsigned it = t; it < items; it += threads) {
+        const unsigned c = it / per_cell, k = it % per_cell;
+        void*          g = grids[c];
+        const bool     keep = r == 0;
+        if (k < n0) {
+          srs_ref_phy_pucch_f0(ctxs[t].get(), g, &f0[k], grid_prb, keep && r0 ? &r0[c * n0 + k] : &x0);
+        } else if (k < n0 + n1) {
+          const unsigned b = k - n0;
+          srs_ref_phy_pucch_f1(ctxs[t].get(), g, &f1[b], grid_prb, keep && r1 ? &r1[c * ne + e0[b]] : x1.data());
+        } else if (k < n0 + n1 + n2) {
+          const unsigned i = k - n0 - n1;
+          std::memset(pay, 0, 64); // (bits past the PDU's payload are not written)
+          srs_ref_phy_pucch_f2(ctxs[t].get(), g, &f2[i], keep && r2 ? &r2[c * n2 + i] : &xu, pay);
+          if (keep && p2) {
+            std::memcpy(p2 + (static_cast<size_t>(c) * n2 + i) * 64, pay, 64);
+          }
+        } else {
+          const unsigned i = k - n0 - n1 - n2;
+          std::memset(pay, 0, 64);
+          srs_ref_phy_pucch_f34(ctxs[t].get(), g, &f34[i], keep && r34 ? &r34[c * n34 + i] : &xu, pay);
+          if (keep && p34) {
+            std::memcpy(p34 + (static_cast<size_t>(c) * n34 + i) * 64, pay, 64);
+          }
+        }
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (unsigned t = 0; t != threads; ++t) {
+    pool.emplace_back(worker, t);
+  }
+  while (arrived.load() != threads) {
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  arrived.fetch_add(1);
+  for (auto& th : pool) {
+    th.join();
+  }
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 } // extern "C"
@@ -1310,7 +1396,6 @@ void srs_ref_phy_pucch_stats(void* h, uint64_t* out)
 /* ---- OFDM: the demodulator plug-ins writing a device-resident grid, as the lower PHY drives them ---- */
 
 #include "../integration/ofdm_modulator_hip.h"
-#include <thread>
 
 namespace {
 

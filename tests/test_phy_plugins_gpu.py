@@ -13,6 +13,7 @@ identical, on_uci called exactly when the PDU carries UCI.
 PDSCH: the plug-in (pdsch_processor::process per PDU on one resource_grid_writer) against the reference's
 pdsch_processor_impl on the same PDUs and initial grid: the grids bit-identical.
 """
+import ctypes
 import os
 import time
 
@@ -714,7 +715,9 @@ def test_pucch_plugin_vs_reference(phy):
                 assert abs(getattr(got, k) - getattr(want, k)) <= 0.02, (i, k)
             n += 1
         nd += 1
-    assert plug.stats() == dict(pdus=n, errors=0, device_grids=nd), plug.stats()
+    # (one caller at a time: every device-grid call is a rendezvous batch of its own)
+    s = plug.stats()
+    assert (s["pdus"], s["errors"], s["device_grids"], s["batches"]) == (n, 0, nd, nd), s
     import srsran_project_amd as amd
 
     assert plug.validate_f2(amd.pucch.make_f2_pdu(nof_prb=2, nof_harq_ack=4, nof_csi_part2=3)) is not None
@@ -744,6 +747,76 @@ def test_pucch_plugin_latency(phy):
     with open(os.path.join(ROOT, "gpurun_out", "pucch_plugin_latency.json"), "w") as f:
         json.dump(out, f)
     assert out["device_grid"]["f0_us"] < 1000 and out["host_grid"]["f2_us"] < 2000, out
+
+
+def test_pucch_plugin_rendezvous_64_cells(phy):
+    """the synchronous PUCCH calls of 64 cells (bench_pucch.cell_pdus: 8 F0 + 2 F1 batches of 12 + 4 F2
+    + 2 F3 + 1 F4 per cell, 273 PRB, 4 ports, device-resident grids) from many PUCCH-executor threads, one
+    pucch_processor::process per PDU as uplink_processor_impl posts them: the calls that wait together share one
+    slot-form launch per format (the plug-in's rendezvous).  Bars: the results of 64 threads identical to those of one
+    thread (every result back to its own caller), far fewer launches than calls; the message rate at 16 / 64 / 256
+    threads beside 16 threads of the reference's pucch_processor_impl (one cell's PDUs per thread, concurrently).
+    Written to gpurun_out/pucch_rendezvous.json."""
+    import json
+    import threading
+
+    import oracle
+    import srsran_project_amd as amd
+    from bench_pucch import NPRB, PORTS, cell_pdus
+
+    ophy, _ = phy
+    ncell = 64
+    rng = np.random.default_rng(31)
+    grids = [rng.integers(0, 1 << 32, (PORTS, 14, 12 * NPRB), dtype=np.uint64).astype(np.uint32) for _ in range(ncell)]
+    dgs = [ophy.DeviceGrid(g, device=True) for g in grids]
+    f0, f1, f2, f34 = cell_pdus(amd, 0)
+    msgs = len(f0) + sum(b.nof_entries for b in f1) + len(f2) + len(f34)
+    plug = ophy.PucchProcessorPlugin(device=0)
+    _, serial = plug.mt_bench(dgs, f0, f1, f2, f34, 1, 1, NPRB)
+    s0 = plug.stats()
+    _, many = plug.mt_bench(dgs, f0, f1, f2, f34, 64, 1, NPRB)
+    s1 = plug.stats()
+    for a, b, name in zip(serial, many, ("f0", "f1", "f2", "p2", "f34", "p34")):
+        assert np.array_equal(a, b), name
+    calls = ncell * (len(f0) + len(f1) + len(f2) + len(f34))
+    assert s1["errors"] == 0 and s1["batches"] - s0["batches"] < calls // 4, (s0, s1)
+    out = {"cells": ncell, "messages_per_cell": msgs}
+    for threads in (16, 64, 256):
+        plug.mt_bench(dgs, f0, f1, f2, f34, threads, 1, NPRB)  # warm-up
+        b0 = plug.stats()
+        dt, _ = plug.mt_bench(dgs, f0, f1, f2, f34, threads, 5, NPRB)
+        b1 = plug.stats()
+        nb = max(b1["batches"] - b0["batches"], 1)
+        out["plugin_%d_threads" % threads] = dict(
+            messages_per_s=5 * ncell * msgs / dt, calls_per_batch=5 * calls / nb,
+            batch_host_us=(b1["batch_host_us"] - b0["batch_host_us"]) / nb,
+            batch_wait_us=(b1["batch_wait_us"] - b0["batch_wait_us"]) / nb)
+    # the reference: 16 threads, each one pucch_processor_impl over one cell's PDUs (srs_ref_pucch_time)
+    from srsran_project_amd.pucch import PucchF0Pdu, PucchF1Batch, PucchF2Pdu, PucchF34Pdu
+
+    f = oracle.REF.srs_ref_pucch_time
+    f.restype = ctypes.c_double
+    P = ctypes.c_void_p
+    f.argtypes = [P, ctypes.c_uint, ctypes.c_uint, P, ctypes.c_uint, P, ctypes.c_uint, P, ctypes.c_uint, P,
+                  ctypes.c_uint, ctypes.c_uint]
+    a0, a1 = (PucchF0Pdu * len(f0))(*f0), (PucchF1Batch * len(f1))(*f1)
+    a2, a34 = (PucchF2Pdu * len(f2))(*f2), (PucchF34Pdu * len(f34))(*f34)
+    reps = max(1, int(1.0 / max(f(grids[0].ctypes.data, PORTS, 12 * NPRB, a0, len(f0), a1, len(f1), a2, len(f2), a34,
+                                  len(f34), 1), 1e-6)))
+    threads = [threading.Thread(target=f, args=(grids[t].ctypes.data, PORTS, 12 * NPRB, a0, len(f0), a1, len(f1), a2,
+                                                len(f2), a34, len(f34), reps)) for t in range(16)]
+    t0 = time.perf_counter()
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    out["reference_16_threads"] = dict(messages_per_s=16 * reps * msgs / (time.perf_counter() - t0))
+    out["plugin_256_vs_reference_16"] = out["plugin_256_threads"]["messages_per_s"] / \
+        out["reference_16_threads"]["messages_per_s"]
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "pucch_rendezvous.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(out)
 
 
 # ---- the OFDM demodulator plug-in feeding the PUSCH plug-in on the device (VERDICT r5 #2) ----
