@@ -44,12 +44,69 @@ hip_resource_grid::hip_resource_grid(std::unique_ptr<resource_grid> host_, int d
   const size_t n = static_cast<size_t>(ports) * symbols * subc;
   check(hipMalloc(&d, sizeof(uint32_t) * n), "hipMalloc");
   check(hipStreamCreateWithFlags(&own, hipStreamNonBlocking), "stream");
-  check(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");
-  check(hipEventCreateWithFlags(&joiner, hipEventDisableTiming), "event");
   // the host mirror starts as the reference grid does (all zero): so do the device copy and the agreed state
   base.assign(n, 0u);
   check(hipMemsetAsync(d, 0, sizeof(uint32_t) * n, own), "hipMemsetAsync");
-  check(hipEventRecord(ready, own), "hipEventRecord");
+  add_producer(own);
+}
+
+hipEvent_t hip_resource_grid::take_event() const
+{
+  if (!spare.empty()) {
+    hipEvent_t e = spare.back();
+    spare.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+  return e;
+}
+
+void hip_resource_grid::add_producer(hipStream_t s) const
+{
+  hipEvent_t e = take_event();
+  check(hipEventRecord(e, s), "hipEventRecord");
+  producers.push_back(e);
+  if (producers.size() > 16) {
+    prune();
+  }
+}
+
+void hip_resource_grid::prune() const
+{
+  // completed producers need no waiting any more: their events go back to the pool
+  for (auto* list : {&producers, &retired}) {
+    for (size_t i = 0; i < list->size();) {
+      const hipError_t q = hipEventQuery((*list)[i]);
+      if (q == hipErrorNotReady) {
+        ++i;
+        continue;
+      }
+      if (q != hipSuccess) {
+        (void)hipGetLastError();
+      }
+      spare.push_back((*list)[i]);
+      (*list)[i] = list->back();
+      list->pop_back();
+    }
+  }
+}
+
+void hip_resource_grid::wait_producers(hipStream_t s) const
+{
+  prune();
+  for (hipEvent_t e : producers) {
+    check(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
+  }
+}
+
+void hip_resource_grid::sync_producers() const
+{
+  for (hipEvent_t e : producers) {
+    check(hipEventSynchronize(e), "hipEventSynchronize");
+  }
+  spare.insert(spare.end(), producers.begin(), producers.end());
+  producers.clear();
 }
 
 hip_resource_grid::~hip_resource_grid()
@@ -65,12 +122,11 @@ hip_resource_grid::~hip_resource_grid()
   if (own != nullptr) {
     (void)hipStreamSynchronize(own);
   }
-  if (ready != nullptr) {
-    (void)hipEventSynchronize(ready);
-    (void)hipEventDestroy(ready);
-  }
-  if (joiner != nullptr) {
-    (void)hipEventDestroy(joiner);
+  for (auto* list : {&producers, &retired, &spare}) {
+    for (hipEvent_t e : *list) {
+      (void)hipEventSynchronize(e);
+      (void)hipEventDestroy(e);
+    }
   }
   if (own != nullptr) {
     (void)hipStreamDestroy(own);
@@ -89,9 +145,12 @@ void hip_resource_grid::set_all_zero()
   host->set_all_zero();
   std::fill(base.begin(), base.end(), 0u);
   check(hipSetDevice(dev), "hipSetDevice");
-  check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
+  // the zeroing follows every earlier producer and supersedes them: the next accesses wait for it alone
+  wait_producers(own);
   check(hipMemsetAsync(d, 0, sizeof(uint32_t) * ports * symbols * subc, own), "hipMemsetAsync");
-  check(hipEventRecord(ready, own), "hipEventRecord");
+  retired.insert(retired.end(), producers.begin(), producers.end());
+  producers.clear();
+  add_producer(own);
   host_dirty   = false;
   view_open    = false; // the slot boundary: writes through earlier views are over
   device_dirty = false;
@@ -106,7 +165,7 @@ void hip_resource_grid::host_access(std::unique_lock<std::mutex>& lock, bool wri
     // the device's changes since the last agreement: host ^= device ^ base, base = device
     auto* self = const_cast<hip_resource_grid*>(this);
     check(hipSetDevice(dev), "hipSetDevice");
-    check(hipEventSynchronize(ready), "hipEventSynchronize");
+    sync_producers();
     std::vector<uint32_t> now(base.size());
     check(hipMemcpy(now.data(), d, sizeof(uint32_t) * now.size(), hipMemcpyDeviceToHost), "download");
     resource_grid_writer& w = self->host->get_writer();
@@ -174,13 +233,13 @@ void hip_resource_grid::device_access(std::unique_lock<std::mutex>& lock, hipStr
         check(hipMalloc(&d_delta, sizeof(uint32_t) * rows * subc), "hipMalloc");
         check(hipMalloc(&d_rows, sizeof(uint32_t) * rows), "hipMalloc");
       }
-      check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
+      wait_producers(own);
       check(hipMemcpyAsync(d_delta, delta.data(), sizeof(uint32_t) * delta.size(), hipMemcpyHostToDevice, own), "upload");
       check(hipMemcpyAsync(d_rows, ids.data(), sizeof(uint32_t) * ids.size(), hipMemcpyHostToDevice, own), "upload");
       if (srs_amd_grid_merge_rows(d, d_delta, d_rows, static_cast<uint32_t>(ids.size()), subc, own) != SRS_AMD_OK) {
         throw std::runtime_error(std::string("hip_resource_grid: merge: ") + srs_amd_last_error());
       }
-      check(hipEventRecord(ready, own), "hipEventRecord");
+      add_producer(own);
       check(hipStreamSynchronize(own), "upload"); // pageable host memory: the copies are done when this returns
       ++uploads;
     }
@@ -191,7 +250,8 @@ void hip_resource_grid::device_access(std::unique_lock<std::mutex>& lock, hipStr
     }
     host_dirty = view_open;
   }
-  check(hipStreamWaitEvent(stream, ready, 0), "hipStreamWaitEvent");
+  // every producer still running (a completed one needs no stream wait packet)
+  wait_producers(stream);
   if (write) {
     device_dirty = true;
     ++ver;
@@ -219,13 +279,9 @@ void hip_resource_grid::run_deferred(hip_grid_deferred_writer* only) const
     it                = deferred.erase(it);
     hipStream_t     s = w->stream();
     check(hipSetDevice(dev), "hipSetDevice");
-    check(hipStreamWaitEvent(s, ready, 0), "hipStreamWaitEvent");
+    wait_producers(s);
     w->issue(*const_cast<hip_resource_grid*>(this), d);
-    // ready := (every earlier producer) and (this writer), as device_written
-    check(hipEventRecord(joiner, s), "hipEventRecord");
-    check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
-    check(hipStreamWaitEvent(own, joiner, 0), "hipStreamWaitEvent");
-    check(hipEventRecord(ready, own), "hipEventRecord");
+    add_producer(s);
     device_dirty = true;
   }
 }
@@ -265,11 +321,8 @@ void hip_resource_grid::device_written(hipStream_t stream)
   {
     std::lock_guard<std::mutex> lock(mtx);
     check(hipSetDevice(dev), "hipSetDevice");
-    // ready := (every earlier producer) and (this writer): own waits for both, then records ready
-    check(hipEventRecord(joiner, stream), "hipEventRecord");
-    check(hipStreamWaitEvent(own, ready, 0), "hipStreamWaitEvent");
-    check(hipStreamWaitEvent(own, joiner, 0), "hipStreamWaitEvent");
-    check(hipEventRecord(ready, own), "hipEventRecord");
+    // one more producer: later readers wait for its event (and each other producer's still running)
+    add_producer(stream);
     device_dirty = true;
     pending      = pending > 0 ? pending - 1 : 0;
     ++ver;

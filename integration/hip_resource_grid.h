@@ -26,8 +26,9 @@
 // boundary (set_all_zero) or until a device reader finds no host change left (readers consume the finished slot):
 // writes through it after an upload are merged by the next device access.  Every device
 // writer is tracked: device_write / device_written bracket it (a pending count host accesses and device readers wait
-// for), and each device_written joins its stream into the `ready` event (the own stream waits for the old `ready` and
-// the writer's event, then records `ready` again), so readers wait for every producer, not only the last.  Calls are
+// for), and each device_written records an event of its own on the writer's stream; readers wait for every producer
+// event still running (r06: no join through a grid-owned stream, whose packets could sit in a hardware queue ahead of
+// unrelated work), so they wait for every producer, not only the last.  Calls are
 // serialised per grid by a mutex.  An RE written on both sides between two merges keeps neither value exactly (XOR):
 // the reference's processors never write the same RE twice in a slot.
 #pragma once
@@ -161,15 +162,22 @@ private:
   void mark_view_open() const { view_open = true; }
   // issues the registered deferred writers' staged writes (only: that one writer), lock held
   void run_deferred(hip_grid_deferred_writer* only) const;
+  // producer events, lock held
+  hipEvent_t take_event() const;
+  void       add_producer(hipStream_t s) const;
+  void       prune() const;
+  void       wait_producers(hipStream_t s) const;
+  void       sync_producers() const;
 
   std::unique_ptr<resource_grid> host;
   unsigned                       ports = 0, symbols = 0, subc = 0;
   int                            dev   = 0;
   uint64_t                       uid   = 0;
   uint32_t*                      d     = nullptr;
-  hipEvent_t                     ready  = nullptr; // every device producer's completion (joined on `own`)
-  hipEvent_t                     joiner = nullptr; // a writer's completion, joined into `ready`
-  hipStream_t                    own    = nullptr; // transfers, merges, joins
+  hipStream_t                    own    = nullptr; // zeroing, merges
+  // one event per device producer since the copies last agreed (writers, staged writes, zeroing, merges): readers
+  // wait for those still running; completed ones go back to `spare`, superseded ones wait in `retired`
+  mutable std::vector<hipEvent_t> producers, retired, spare;
   mutable std::mutex              mtx;
   mutable std::condition_variable cv;              // pending reaches 0
   mutable std::vector<uint32_t>   base;            // the state host and device copies last agreed on

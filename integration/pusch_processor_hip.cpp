@@ -171,7 +171,8 @@ std::string convert(const pusch_processor::pdu_t& pdu, size_t tb_bytes, srs_amd_
 class slot_engine
 {
 public:
-  explicit slot_engine(const pusch_processor_hip_config& c) : cfg(c), nsubc(12 * c.nof_prb), pool(c.nof_copy_threads)
+  explicit slot_engine(const pusch_processor_hip_config& c) :
+    cfg(c), nsubc(12 * c.nof_prb), pool(c.nof_copy_threads), npool(c.nof_notify_threads)
   {
     device = cfg.device;
     if (device < 0 && hipGetDevice(&device) != hipSuccess) {
@@ -256,6 +257,13 @@ public:
     s.nof_harq_soft_downloads = stats_soft_downloads;
     s.nof_retransmissions = stats_retx;
     s.nof_device_grids    = stats_device_grids;
+    s.stage_us            = t_stage / 1000;
+    s.set_wait_us         = t_set_wait / 1000;
+    s.wait_us             = t_wait / 1000;
+    s.notify_us           = t_notify / 1000;
+    s.stage_reads_us      = t_reads / 1000;
+    s.stage_call_us       = t_call / 1000;
+    s.stage_download_us   = t_download / 1000;
     return s;
   }
 
@@ -381,6 +389,15 @@ private:
   // Collector thread: stages and dispatches one batch; returns the number of PDUs reported as failed here.
   unsigned process(std::vector<pending_pdu>& batch)
   {
+    const auto t_begin = std::chrono::steady_clock::now();
+    struct stage_timer {
+      std::atomic<uint64_t>&                t;
+      std::chrono::steady_clock::time_point t0;
+      ~stage_timer()
+      {
+        t += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+      }
+    } timer{t_stage, t_begin};
     const unsigned n      = static_cast<unsigned>(batch.size());
     unsigned       errors = 0;
     if (hipSetDevice(device) != hipSuccess) {
@@ -419,12 +436,15 @@ private:
     if (m == 0) {
       return errors;
     }
-    buffer_set* bs = acquire_set();
-    j->bs          = bs;
+    const auto  t_acq = std::chrono::steady_clock::now();
+    buffer_set* bs    = acquire_set();
+    t_set_wait += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_acq).count();
+    j->bs = bs;
     // receive grids: a hip_resource_grid's device copy as it is (receive ports 0 .. P - 1); otherwise one staged
     // device grid per (reader, port list), a PDU whose ports are a prefix of another PDU's list on the same reader
     // sharing that grid
     std::vector<const uint32_t*> dev_grid(m, nullptr);
+    const auto                   t_r0 = std::chrono::steady_clock::now();
     for (size_t k = 0; k != m; ++k) {
       const pending_pdu& p  = j->pdus[k];
       hip_resource_grid* hg = hip_grid_of(*p.grid);
@@ -438,6 +458,7 @@ private:
         ++stats_device_grids;
       }
     }
+    t_reads += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_r0).count();
     std::unordered_map<const resource_grid_reader*, std::vector<uint8_t>> longest;
     for (size_t k = 0; k != m; ++k) {
       if (dev_grid[k] != nullptr) {
@@ -565,9 +586,13 @@ private:
                            hipMemcpyHostToDevice, stream);
       }
     }
-    int rc = e == hipSuccess ? run_slot(*j, j->sp, stream) : SRS_AMD_EHIP;
-    e      = rc == SRS_AMD_OK ? download(*j, stream) : hipErrorUnknown;
-    e      = e == hipSuccess ? hipEventRecord(bs->done, stream) : e;
+    const auto t_c0 = std::chrono::steady_clock::now();
+    int        rc   = e == hipSuccess ? run_slot(*j, j->sp, stream) : SRS_AMD_EHIP;
+    const auto t_c1 = std::chrono::steady_clock::now();
+    e               = rc == SRS_AMD_OK ? download(*j, stream) : hipErrorUnknown;
+    e               = e == hipSuccess ? hipEventRecord(bs->done, stream) : e;
+    t_call += std::chrono::duration_cast<std::chrono::nanoseconds>(t_c1 - t_c0).count();
+    t_download += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_c1).count();
     if (rc != SRS_AMD_OK || e != hipSuccess) {
       log_error("slot call", rc != SRS_AMD_OK ? std::string(srs_amd_last_error()) : hipGetErrorString(e));
       (void)hipStreamSynchronize(stream);
@@ -615,6 +640,7 @@ private:
   {
     buffer_set* bs = j.bs;
     const size_t m = j.pdus.size();
+    const auto   t_begin = std::chrono::steady_clock::now();
     if (!j.failed) {
       // poll the batch's event: an interrupt-driven wait could oversleep (device_buffer.h event_wait_spin)
       hipError_t e;
@@ -626,6 +652,16 @@ private:
         j.failed = true;
       }
     }
+    const auto t_ready = std::chrono::steady_clock::now();
+    t_wait += std::chrono::duration_cast<std::chrono::nanoseconds>(t_ready - t_begin).count();
+    struct notify_timer {
+      std::atomic<uint64_t>&                t;
+      std::chrono::steady_clock::time_point t0;
+      ~notify_timer()
+      {
+        t += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+      }
+    } timer{t_notify, t_ready};
     if (j.failed) {
       stats_late_errors += m;
       for (auto& p : j.pdus) {
@@ -664,8 +700,10 @@ private:
         }
       }
     }
-    // results, HARQ state back into the rx_buffers, notifications
-    for (size_t k = 0; k != m; ++k) {
+    // results, HARQ state back into the rx_buffers, notifications: the batch's PDUs in parallel on the notification
+    // pool (the transport-block copies out of pinned memory dominate: ~140 KB per 273-PRB 4-layer PDU), as the
+    // reference's PUSCH executor threads notify their PDUs concurrently
+    npool.run(m, [&](size_t k) {
       pending_pdu& p = j.pdus[k];
       if (keep[k]) {
         store_harq(p, j.pl[k], bs->soft.h + j.soft_off[k]);
@@ -673,7 +711,7 @@ private:
       notify(p, j.pl[k], res[k], reinterpret_cast<const int32_t*>(bs->cbi.h) + j.cb_off[k], j.prev_ok[k],
              bs->tbs.h + j.tb_off[k], bs->uci.h + j.uci_off[k],
              reinterpret_cast<const srs_amd_chest_port_stats*>(bs->pstats.h) + k * MAX_PORTS_HIP);
-    }
+    });
   }
 
   // srs_amd_pusch_process_slot_ex on the batch's device buffers; ids: the index of each PDU in the outputs (the
@@ -862,6 +900,8 @@ private:
 
 public:
   std::atomic<uint64_t> stats_retx{0}, stats_soft_downloads{0}, stats_late_errors{0}, stats_device_grids{0};
+  std::atomic<uint64_t> t_stage{0}, t_set_wait{0}, t_wait{0}, t_notify{0}; // ns
+  std::atomic<uint64_t> t_reads{0}, t_call{0}, t_download{0};                // ns, parts of t_stage
 
 private:
   pusch_processor_hip_config cfg;
@@ -874,6 +914,7 @@ private:
   std::unordered_map<std::string, plan_entry> plans;
   std::list<std::string>                      lru;
   row_pool                                    pool;
+  row_pool                                    npool; // completion thread: notifications
   // dispatched batches (collector -> completion thread) and the buffer sets they use
   buffer_set                        sets[2];
   std::mutex                        jmtx;

@@ -77,6 +77,9 @@ struct pusch_processor_hip_config {
   /// Worker threads copying the rows of host resource grids into the batch's pinned staging buffer (0: the
   /// collector thread alone).  Grids of a hip_resource_grid factory are used in HBM as they are.
   unsigned nof_copy_threads = 8;
+  /// Worker threads (beside the completion thread) writing the batch's results -- transport blocks, HARQ state --
+  /// and calling the notifiers, PDUs in parallel (0: the completion thread alone).
+  unsigned nof_notify_threads = 4;
 };
 
 /// pusch_processor_factory whose processors share one slot collector and one MI355X PUSCH processor.
@@ -95,6 +98,12 @@ public:
     uint64_t nof_harq_soft_downloads = 0;
     /// PDUs whose received grid was a hip_resource_grid read in place (no host staging, no PCIe copy).
     uint64_t nof_device_grids = 0;
+    /// Host time (microseconds, all batches): the collector thread staging and issuing batches (stage_us, of which
+    /// waiting for a free buffer set: set_wait_us), the completion thread waiting for batches' results (wait_us) and
+    /// writing HARQ state / calling the notifiers (notify_us).
+    uint64_t stage_us = 0, set_wait_us = 0, wait_us = 0, notify_us = 0;
+    /// Parts of stage_us: device-grid reads, the slot call (descriptors + launches), the result downloads.
+    uint64_t stage_reads_us = 0, stage_call_us = 0, stage_download_us = 0;
   };
   virtual statistics get_statistics() const = 0;
 };

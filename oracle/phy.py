@@ -33,7 +33,7 @@ def lib():
         L.srs_ref_phy_pusch_result.argtypes = [P, i, P, P, P, P, P, P]
         L.srs_ref_phy_pusch_stats.argtypes = [P, P]
         L.srs_ref_phy_pusch_bench.restype = d
-        L.srs_ref_phy_pusch_bench.argtypes = [P, P, u, P, u, u, P, u, P]
+        L.srs_ref_phy_pusch_bench.argtypes = [P, P, u, u, P, u, u, P, u, P]
         L.srs_ref_phy_hgrid_create.restype = P
         L.srs_ref_phy_hgrid_create.argtypes = [P, u, u, i]
         L.srs_ref_phy_hgrid_set_device.restype = i
@@ -239,19 +239,23 @@ class PuschProcessorPlugin:
         return t, tb[:fpdu.tb_bytes]
 
     def stats(self):
-        s = np.zeros(7, np.uint64)
+        s = np.zeros(14, np.uint64)
         lib().srs_ref_phy_pusch_stats(self.h, s.ctypes.data)
         return dict(zip(("pdus", "batches", "errors", "harq_redecodes", "retransmissions", "device_grids",
-                         "harq_soft_downloads"), (int(v) for v in s)))
+                         "harq_soft_downloads", "stage_us", "set_wait_us", "wait_us", "notify_us", "stage_reads_us",
+                         "stage_call_us", "stage_download_us"),
+                        (int(v) for v in s)))
 
-    def bench(self, grids, pdu, tb_bytes, warmup, steps):
-        """Seconds per step with one PDU per cell grid (process per PDU, flush, wait) and the TB CRC-OK count."""
+    def bench(self, grids, pdu, tb_bytes, warmup, steps, depth=1):
+        """Seconds per step with one PDU per cell grid (process per PDU, flush; depth 1: wait for every notification
+        each step; depth d: d slots in flight, grids = d sets of the cells' grids) and the TB CRC-OK count."""
+        cells = len(grids) // depth
         arr = (ctypes.c_void_p * len(grids))(*[g.h for g in grids])
-        tbs = np.zeros(len(grids) * tb_bytes, np.uint8)
+        tbs = np.zeros(cells * tb_bytes, np.uint8)
         ok = ctypes.c_uint()
-        dt = lib().srs_ref_phy_pusch_bench(self.h, arr, len(grids), ctypes.byref(pdu), warmup, steps,
+        dt = lib().srs_ref_phy_pusch_bench(self.h, arr, cells, depth, ctypes.byref(pdu), warmup, steps,
                                            tbs.ctypes.data, tb_bytes, ctypes.byref(ok))
-        return dt, ok.value, tbs.reshape(len(grids), tb_bytes)
+        return dt, ok.value, tbs.reshape(cells, tb_bytes)
 
 
 # ---- OFDM demodulator plug-ins on a device-resident grid ----
@@ -386,7 +390,7 @@ def _declare_pdsch(L):
     L.srs_ref_phy_pdsch_done.argtypes = [P, i]
     L.srs_ref_phy_pdsch_stats.argtypes = [P, P]
     L.srs_ref_phy_pdsch_bench.restype = d
-    L.srs_ref_phy_pdsch_bench.argtypes = [P, P, u, P, P, u, u, u]
+    L.srs_ref_phy_pdsch_bench.argtypes = [P, P, u, u, P, P, u, u, u]
 
 
 _pdsch_declared = False
@@ -464,11 +468,12 @@ class PdschProcessorPlugin:
         _L().srs_ref_phy_pdsch_stats(self.h, s.ctypes.data)
         return dict(zip(("pdus", "batches", "errors", "device_grids"), (int(v) for v in s)))
 
-    def bench(self, grids, pdu, tb, warmup, steps):
+    def bench(self, grids, pdu, tb, warmup, steps, depth=1):
+        """Seconds per step (depth: slots in flight, grids = depth sets of the cells' grids, as PuschProcessorPlugin)."""
         arr = (ctypes.c_void_p * len(grids))(*[g.h for g in grids])
         tb = np.ascontiguousarray(tb, np.uint8)
-        return _L().srs_ref_phy_pdsch_bench(self.h, arr, len(grids), ctypes.byref(pdu), tb.ctypes.data, tb.size,
-                                            warmup, steps)
+        return _L().srs_ref_phy_pdsch_bench(self.h, arr, len(grids) // depth, depth, ctypes.byref(pdu),
+                                            tb.ctypes.data, tb.size, warmup, steps)
 
 
 class PdcchProcessorPlugin:

@@ -682,7 +682,8 @@ int srs_ref_pusch_process_fapi(void* grid, void* fapi_pdu, unsigned nof_prb, uns
   return 0;
 }
 
-/* Plug-in statistics: PDUs, batches, errors, HARQ re-decodes, retransmissions, device grids, soft-buffer downloads. */
+/* Plug-in statistics: PDUs, batches, errors, HARQ re-decodes, retransmissions, device grids, soft-buffer downloads,
+ * host us: staging, buffer-set wait, result wait, notification. */
 void srs_ref_phy_pusch_stats(void* h, uint64_t* out)
 {
   const auto s = static_cast<pusch_ctx*>(h)->factory->get_statistics();
@@ -693,42 +694,75 @@ void srs_ref_phy_pusch_stats(void* h, uint64_t* out)
   out[4]       = s.nof_retransmissions;
   out[5]       = s.nof_device_grids;
   out[6]       = s.nof_harq_soft_downloads;
+  out[7]       = s.stage_us;
+  out[8]       = s.set_wait_us;
+  out[9]       = s.wait_us;
+  out[10]      = s.notify_us;
+  out[11]      = s.stage_reads_us;
+  out[12]      = s.stage_call_us;
+  out[13]      = s.stage_download_us;
 }
 
 /* Throughput through the plug-in as the upper PHY drives it: every step, one PDU per cell grid (nof_cells grids,
- * each with its own processor of the factory, i.e. one cell each), process() per PDU, flush() at the slot boundary,
- * wait for every notification.  tbs:
- * nof_cells rows of tb_bytes.  Returns seconds per step over `steps` timed steps after `warmup`; ok_out: TBs with
- * CRC OK in the timed steps. */
-double srs_ref_phy_pusch_bench(void* h, void* const* grids, unsigned nof_cells, const srs_amd_pusch_pdu* c,
-                               unsigned warmup, unsigned steps, uint8_t* tbs, unsigned tb_bytes, unsigned* ok_out)
+ * each with its own processor of the factory, i.e. one cell each), process() per PDU, flush() at the slot boundary.
+ * depth 1: every notification awaited before the next step; depth d > 1: d slots in flight, as the uplink processor
+ * keeps them (a slot's PUSCH is processed while the next slots' symbols arrive): step s waits only for the
+ * notifications of step s - d, and uses grids[(s % d) * nof_cells + i] (d sets of grids).  tbs: nof_cells rows of
+ * tb_bytes.  Returns seconds per step over `steps` timed steps after `warmup`; ok_out: TBs with CRC OK in the timed
+ * steps. */
+double srs_ref_phy_pusch_bench(void* h, void* const* grids, unsigned nof_cells, unsigned depth,
+                               const srs_amd_pusch_pdu* c, unsigned warmup, unsigned steps, uint8_t* tbs,
+                               unsigned tb_bytes, unsigned* ok_out)
 {
   auto*                                         ctx = static_cast<pusch_ctx*>(h);
   std::vector<std::unique_ptr<pusch_processor>> procs;
   for (unsigned i = 0; i != nof_cells; ++i) {
     procs.push_back(ctx->factory->create());
   }
-  std::vector<ticket>    tickets(nof_cells);
+  depth = std::max(depth, 1u);
+  std::vector<ticket>     tickets(static_cast<size_t>(nof_cells) * depth);
+  std::vector<char>       timed(depth, 0);
   const srs_amd_pusch_pdu pc = *c; // the grids hold one slot's DM-RS: every step is that slot again
   unsigned                ok = 0;
-  auto                   t0    = std::chrono::steady_clock::now();
-  for (unsigned s = 0; s != warmup + steps; ++s) {
-    if (s == warmup) {
-      t0 = std::chrono::steady_clock::now();
+  auto                    collect = [&](unsigned b) {
+    for (unsigned i = 0; i != nof_cells; ++i) {
+      ticket& t = tickets[static_cast<size_t>(b) * nof_cells + i];
+      while (!t.done.load(std::memory_order_acquire)) {
+        std::this_thread::sleep_for(std::chrono::microseconds(20)); // (a sleeping poll: no spinning host thread)
+      }
+      ok += timed[b] && t.sch.data.tb_crc_ok ? 1 : 0;
     }
+  };
+  auto t0 = std::chrono::steady_clock::now();
+  for (unsigned s = 0; s != warmup + steps; ++s) {
+    const unsigned b = s % depth;
+    if (s == warmup) {
+      // the warm-up steps drained: the timed region starts empty (and ends drained)
+      ctx->factory->wait_idle();
+      for (unsigned q = s >= depth ? s - depth : 0; q != s; ++q) {
+        collect(q % depth);
+      }
+      t0 = std::chrono::steady_clock::now();
+    } else if (s >= depth) {
+      collect(b); // the notifications of step s - depth
+    }
+    timed[b]                         = s >= warmup;
     const pusch_processor::pdu_t pdu = to_pdu(pc);
     for (unsigned i = 0; i != nof_cells; ++i) {
-      tickets[i].done.store(false);
-      procs[i]->process(span<uint8_t>(tbs + static_cast<size_t>(i) * tb_bytes, tb_bytes), unique_rx_buffer(),
-                        tickets[i], static_cast<any_grid*>(grids[i])->rd(), pdu);
+      ticket& t = tickets[static_cast<size_t>(b) * nof_cells + i];
+      t.done.store(false);
+      procs[i]->process(span<uint8_t>(tbs + static_cast<size_t>(i) * tb_bytes, tb_bytes), unique_rx_buffer(), t,
+                        static_cast<any_grid*>(grids[static_cast<size_t>(b) * nof_cells + i])->rd(), pdu);
     }
     ctx->factory->flush();
-    ctx->factory->wait_idle();
-    if (s >= warmup) {
-      for (unsigned i = 0; i != nof_cells; ++i) {
-        ok += tickets[i].sch.data.tb_crc_ok ? 1 : 0;
-      }
+    if (depth == 1) {
+      ctx->factory->wait_idle();
     }
+  }
+  ctx->factory->wait_idle();
+  const unsigned end = warmup + steps;
+  for (unsigned q = std::max(warmup, end >= depth ? end - depth : 0u); q < end; ++q) {
+    collect(q % depth);
   }
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   *ok_out         = ok;
@@ -897,29 +931,48 @@ void srs_ref_phy_pdsch_stats(void* h, uint64_t* out)
 
 /* Throughput through the PDSCH plug-in: every step one PDU per cell grid (a processor per cell), process() per PDU,
  * flush(), wait.  Returns seconds per step. */
-double srs_ref_phy_pdsch_bench(void* h, void* const* grids, unsigned nof_cells, const srs_ref_pdsch_pdu* c,
-                               const uint8_t* tb, unsigned tb_bytes, unsigned warmup, unsigned steps)
+double srs_ref_phy_pdsch_bench(void* h, void* const* grids, unsigned nof_cells, unsigned depth,
+                               const srs_ref_pdsch_pdu* c, const uint8_t* tb, unsigned tb_bytes, unsigned warmup,
+                               unsigned steps)
 {
   auto*                                         ctx = static_cast<pdsch_ctx*>(h);
   std::vector<std::unique_ptr<pdsch_processor>> procs;
   for (unsigned i = 0; i != nof_cells; ++i) {
     procs.push_back(ctx->factory->create());
   }
-  std::vector<pdsch_ticket>    tickets(nof_cells);
-  const pdsch_processor::pdu_t pdu = to_pdsch_pdu(*c);
-  auto                         t0  = std::chrono::steady_clock::now();
+  depth = std::max(depth, 1u);
+  std::vector<pdsch_ticket>    tickets(static_cast<size_t>(nof_cells) * depth);
+  const pdsch_processor::pdu_t pdu     = to_pdsch_pdu(*c);
+  auto                         collect = [&](unsigned b) {
+    for (unsigned i = 0; i != nof_cells; ++i) {
+      while (!tickets[static_cast<size_t>(b) * nof_cells + i].done.load(std::memory_order_acquire)) {
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+    }
+  };
+  auto t0 = std::chrono::steady_clock::now();
   for (unsigned s = 0; s != warmup + steps; ++s) {
+    const unsigned b = s % depth;
     if (s == warmup) {
+      ctx->factory->wait_idle(); // (the timed region starts empty and ends drained, as the PUSCH bench)
       t0 = std::chrono::steady_clock::now();
+    } else if (s >= depth) {
+      collect(b); // step s - depth's grids are written: the set is free again
     }
     for (unsigned i = 0; i != nof_cells; ++i) {
       static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
       data.emplace_back(span<const uint8_t>(tb, tb_bytes));
-      procs[i]->process(static_cast<any_grid*>(grids[i])->wr(), tickets[i], std::move(data), pdu);
+      pdsch_ticket& t = tickets[static_cast<size_t>(b) * nof_cells + i];
+      t.done.store(false);
+      procs[i]->process(static_cast<any_grid*>(grids[static_cast<size_t>(b) * nof_cells + i])->wr(), t,
+                        std::move(data), pdu);
     }
     ctx->factory->flush();
-    ctx->factory->wait_idle();
+    if (depth == 1) {
+      ctx->factory->wait_idle();
+    }
   }
+  ctx->factory->wait_idle();
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return steps ? dt / steps : 0.0;
 }

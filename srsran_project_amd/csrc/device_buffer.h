@@ -312,62 +312,77 @@ struct call_scope {
 
 // Host-built launch descriptors (per-item argument blocks of a slot call) staged in pinned memory and
 // uploaded on the call's stream: the buffer is rewritten only once its previous upload has completed.
+// Pinned host staging for per-call descriptor uploads: a ring of RING buffers, each rewritten only once its previous
+// upload has completed, so a call can stage its descriptors while up to RING - 1 earlier calls' uploads still wait
+// behind their stream's work (r06: the slot forms of consecutive batches no longer wait for each other on the host).
 struct pinned_stage {
-  void*      h    = nullptr;
-  size_t     size = 0;
-  hipEvent_t done = nullptr;
-  bool       used = false;
+  static constexpr int RING = 3;
+  struct slot {
+    void*      h    = nullptr;
+    size_t     size = 0;
+    hipEvent_t done = nullptr;
+    bool       used = false;
+  };
+  slot ring[RING];
+  int  cur = 0;
   pinned_stage()                               = default;
   pinned_stage(const pinned_stage&)            = delete;
   pinned_stage& operator=(const pinned_stage&) = delete;
   ~pinned_stage()
   {
-    if (done) {
-      (void)hipEventSynchronize(done);
-      (void)hipEventDestroy(done);
+    for (slot& b : ring) {
+      if (b.done) {
+        (void)hipEventSynchronize(b.done);
+        (void)hipEventDestroy(b.done);
+      }
+      (void)hipHostFree(b.h);
     }
-    (void)hipHostFree(h);
   }
-  // Waits for the previous upload and grows the buffer to n bytes; the host pointer is then writable.
+  // Moves to the next buffer of the ring, waits for its previous upload and grows it to n bytes; the host pointer is
+  // then writable.
   hipError_t acquire(size_t n)
   {
-    hipError_t e = used ? event_wait_spin(done) : hipSuccess;
-    used         = false;
-    if (e == hipSuccess && done == nullptr) {
-      e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    cur          = (cur + 1) % RING;
+    slot&      b = ring[cur];
+    hipError_t e = b.used ? event_wait_spin(b.done) : hipSuccess;
+    b.used       = false;
+    if (e == hipSuccess && b.done == nullptr) {
+      e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
     }
-    if (e == hipSuccess && size < n) {
-      (void)hipHostFree(h);
-      h    = nullptr;
-      size = 0;
-      e    = hipHostMalloc(&h, n, hipHostMallocDefault);
-      size = e == hipSuccess ? n : 0;
+    if (e == hipSuccess && b.size < n) {
+      (void)hipHostFree(b.h);
+      b.h    = nullptr;
+      b.size = 0;
+      e      = hipHostMalloc(&b.h, n, hipHostMallocDefault);
+      b.size = e == hipSuccess ? n : 0;
     }
     return e;
   }
   template <typename T>
   T* at(size_t offset) const
   {
-    return reinterpret_cast<T*>(static_cast<unsigned char*>(h) + offset);
+    return reinterpret_cast<T*>(static_cast<unsigned char*>(ring[cur].h) + offset);
   }
   // Copies the first n bytes to device memory d on stream s.
   hipError_t upload(void* d, size_t n, hipStream_t s)
   {
-    hipError_t e = upload_pinned(d, h, n, s);
+    slot&      b = ring[cur];
+    hipError_t e = upload_pinned(d, b.h, n, s);
     if (e == hipSuccess) {
-      e = hipEventRecord(done, s);
+      e = hipEventRecord(b.done, s);
     }
-    used = e == hipSuccess;
+    b.used = e == hipSuccess;
     return e;
   }
   // Copies rows of `width` bytes (consecutive in the stage) to device rows dpitch bytes apart.
   hipError_t upload_rows(void* d, size_t dpitch, size_t width, size_t rows, hipStream_t s)
   {
-    hipError_t e = hipMemcpy2DAsync(d, dpitch, h, width, width, rows, hipMemcpyHostToDevice, s);
+    slot&      b = ring[cur];
+    hipError_t e = hipMemcpy2DAsync(d, dpitch, b.h, width, width, rows, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
-      e = hipEventRecord(done, s);
+      e = hipEventRecord(b.done, s);
     }
-    used = e == hipSuccess;
+    b.used = e == hipSuccess;
     return e;
   }
 };

@@ -50,10 +50,7 @@ struct srs_amd_pdsch_encoder {
   stream_fan                 fan;   // srs_amd_pdsch_encode_slot: concurrent LDPC encoder bucket launches
   std::mutex                 mtx;
   // srs_amd_pdsch_encode_slot: descriptors staged in pinned memory, reused once their upload completed
-  void*                      h_stage      = nullptr;
-  size_t                     h_stage_size = 0;
-  hipEvent_t                 stage_done   = nullptr;
-  bool                       stage_used   = false;
+  pinned_stage hstage; // descriptors staged in pinned memory (a ring: each reused once its upload completed)
   ~srs_amd_pdsch_encoder()
   {
     (void)hipSetDevice(device);
@@ -61,11 +58,6 @@ struct srs_amd_pdsch_encoder {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
     }
-    if (stage_done) {
-      (void)hipEventSynchronize(stage_done);
-      (void)hipEventDestroy(stage_done);
-    }
-    (void)hipHostFree(h_stage);
     srs_amd_crc_calculator_destroy(crc16);
     srs_amd_crc_calculator_destroy(crc24a);
     srs_amd_crc_calculator_destroy(crc24b);
@@ -179,24 +171,10 @@ int fused_launch_locked(srs_amd_pdsch_encoder* e,
   call_scope scope(e->order, &e->fan, stream);
   he = e->order.begin(stream);
   if (he == hipSuccess && upload) {
-    // the pinned staging buffer is rewritten only once its previous upload completed
-    if (e->stage_used) {
-      he = event_wait_spin(e->stage_done);
-    }
-    if (he == hipSuccess && e->stage_done == nullptr) {
-      he = hipEventCreateWithFlags(&e->stage_done, hipEventDisableTiming);
-    }
-    if (he == hipSuccess && e->h_stage_size < L.total) {
-      (void)hipHostFree(e->h_stage);
-      e->h_stage      = nullptr;
-      e->h_stage_size = 0;
-      he              = hipHostMalloc(&e->h_stage, L.total, hipHostMallocDefault);
-      if (he == hipSuccess) {
-        e->h_stage_size = L.total;
-      }
-    }
+    // the next pinned staging buffer of the ring, free once its previous upload completed
+    he = e->hstage.acquire(L.total);
     if (he == hipSuccess) {
-      auto* h = static_cast<uint8_t*>(e->h_stage);
+      auto* h = e->hstage.at<uint8_t>(0);
       std::memcpy(h + L.o_E, f.row_E.data(), sizeof(uint32_t) * R);
       std::memcpy(h + L.o_out, f.row_out.data(), sizeof(uint32_t) * R);
       std::memcpy(h + L.o_geo, f.row_geo.data(), sizeof(uint32_t) * R);
@@ -208,11 +186,7 @@ int fused_launch_locked(srs_amd_pdsch_encoder* e,
       for (uint32_t t = 0; t < U; ++t) {
         lr[t] = f.tds[t].row0 + f.tds[t].nof_segments - 1;
       }
-      he = upload_pinned(dd, h, L.total, stream);
-    }
-    if (he == hipSuccess) {
-      he = hipEventRecord(e->stage_done, stream);
-      e->stage_used = he == hipSuccess;
+      he = e->hstage.upload(dd, L.total, stream);
     }
   }
   if (he != hipSuccess) {
@@ -592,21 +566,9 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   const size_t total = o_ER + enc_rows.size();
 
   hipError_t he = hipSetDevice(e->device);
-  // the pinned staging buffer is rewritten only once its previous upload completed
-  if (he == hipSuccess && e->stage_used) {
-    he = event_wait_spin(e->stage_done);
-  }
-  if (he == hipSuccess && e->stage_done == nullptr) {
-    he = hipEventCreateWithFlags(&e->stage_done, hipEventDisableTiming);
-  }
-  if (he == hipSuccess && e->h_stage_size < total) {
-    (void)hipHostFree(e->h_stage);
-    e->h_stage      = nullptr;
-    e->h_stage_size = 0;
-    he              = hipHostMalloc(&e->h_stage, total, hipHostMallocDefault);
-    if (he == hipSuccess) {
-      e->h_stage_size = total;
-    }
+  // the next pinned staging buffer of the ring, free once its previous upload completed
+  if (he == hipSuccess) {
+    he = e->hstage.acquire(total);
   }
   if (he == hipSuccess) {
     he = e->slot_desc.ensure(total);
@@ -623,7 +585,7 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   if (he != hipSuccess) {
     return hip_fail(he, "PDSCH slot encoder scratch");
   }
-  auto* h = static_cast<uint8_t*>(e->h_stage);
+  auto* h = e->hstage.at<uint8_t>(0);
   std::memcpy(h + o_E, row_E.data(), sizeof(uint32_t) * R);
   std::memcpy(h + o_out, row_out.data(), sizeof(uint32_t) * R);
   std::memcpy(h + o_geo, row_geo.data(), sizeof(uint32_t) * R);
@@ -635,15 +597,11 @@ int encode_slot_locked(srs_amd_pdsch_encoder*  e,
   call_scope scope(e->order, &e->fan, stream);
   he = e->order.begin(stream);
   if (he == hipSuccess) {
-    he = upload_pinned(dd, h, total, stream);
-  }
-  if (he == hipSuccess) {
-    he = hipEventRecord(e->stage_done, stream);
+    he = e->hstage.upload(dd, total, stream);
   }
   if (he != hipSuccess) {
     return hip_fail(he, "PDSCH slot descriptors upload");
   }
-  e->stage_used = true;
   // 1-3. TB CRCs, segmentation, codeblock CRCs.
   tx_slot_args ta{};
   ta.tbs           = d_tbs;

@@ -47,10 +47,7 @@ struct srs_amd_pusch_decoder {
   stream_fan                   fan;   // srs_amd_pusch_decode_slot: concurrent LDPC bucket launches
   std::mutex                   mtx;
   // srs_amd_pusch_decode_slot: descriptors staged in pinned memory, reused once their upload completed
-  void*                        h_stage      = nullptr;
-  size_t                       h_stage_size = 0;
-  hipEvent_t                   stage_done   = nullptr;
-  bool                         stage_used   = false;
+  pinned_stage hstage; // descriptors staged in pinned memory (a ring: each reused once its upload completed)
   ~srs_amd_pusch_decoder()
   {
     (void)hipSetDevice(device);
@@ -58,11 +55,6 @@ struct srs_amd_pusch_decoder {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
     }
-    if (stage_done) {
-      (void)hipEventSynchronize(stage_done);
-      (void)hipEventDestroy(stage_done);
-    }
-    (void)hipHostFree(h_stage);
     for (auto* c : crc) {
       srs_amd_crc_calculator_destroy(c);
     }
@@ -447,21 +439,9 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   }
 
   hipError_t he = hipSetDevice(d->device);
-  // the pinned staging buffer is rewritten only once its previous upload completed
-  if (he == hipSuccess && d->stage_used) {
-    he = event_wait_spin(d->stage_done);
-  }
-  if (he == hipSuccess && d->stage_done == nullptr) {
-    he = hipEventCreateWithFlags(&d->stage_done, hipEventDisableTiming);
-  }
-  if (he == hipSuccess && d->h_stage_size < total) {
-    (void)hipHostFree(d->h_stage);
-    d->h_stage      = nullptr;
-    d->h_stage_size = 0;
-    he              = hipHostMalloc(&d->h_stage, total, hipHostMallocDefault);
-    if (he == hipSuccess) {
-      d->h_stage_size = total;
-    }
+  // the next pinned staging buffer of the ring, free once its previous upload completed
+  if (he == hipSuccess) {
+    he = d->hstage.acquire(total);
   }
   if (he == hipSuccess) {
     he = d->slot_desc.ensure(total);
@@ -487,7 +467,7 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH slot decoder scratch");
   }
-  auto* h = static_cast<uint8_t*>(d->h_stage);
+  auto* h = d->hstage.at<uint8_t>(0);
   std::memcpy(h + o_E, row_E.data(), sizeof(uint32_t) * R);
   std::memcpy(h + o_in, row_in.data(), sizeof(uint32_t) * R);
   std::memcpy(h + o_geo, row_geo.data(), sizeof(uint32_t) * R);
@@ -518,15 +498,11 @@ int decode_slot_locked(srs_amd_pusch_decoder*              d,
   call_scope scope(d->order, &d->fan, stream);
   he = d->order.begin(stream);
   if (he == hipSuccess) {
-    he = upload_pinned(dd, h, total, stream);
-  }
-  if (he == hipSuccess) {
-    he = hipEventRecord(d->stage_done, stream);
+    he = d->hstage.upload(dd, total, stream);
   }
   if (he != hipSuccess) {
     return hip_fail(he, "PUSCH slot descriptors upload");
   }
-  d->stage_used = true;
   // 0. UEs whose UL-SCH geometry was selected on the device (CSI part 2): their rows' lengths / offsets
   if (nof_patches != 0) {
     he = launch_slot_row_patch(reinterpret_cast<const slot_row_patch*>(dd + o_PT), nof_patches, stream);
