@@ -588,8 +588,12 @@ def run_pipeline(args, dist, world, rank, dev, timed, hbm_peak, traffic=None):
                     "+ 1,060 B of message and iteration count per codeblock, / the live in-step launch time, / 8 TB/s); "
                     "traffic = HBM bytes per launch of the same in-step kernel from separate FETCH_SIZE / WRITE_SIZE "
                     "passes over this command, each counter scaled by its calibration in the kernel's own access "
-                    "forms (profiles/r05_traffic.json, tools/traffic_calib.hip).  Its limiter is VALU issue "
-                    "(valu: r05 PMC of the same launch, profiles/r05_ldpc_valu_model.json).",
+                    "forms (profiles/r05_traffic.json, tools/traffic_calib.hip).  Its limiter is VALU issue, not latency "
+                    "(valu: r06 PMC of the same launch, profiles/r06_ldpc_valu_model.json: SQ_ACTIVE_INST_VALU busy "
+                    "0.76 over its wave-instructions = 1.71 ns each, inside the measured cost of the slow opcode class "
+                    "-- v_pk_*, 32-bit min/max, med3, perm, bfe: 1.72-1.85 ns per wave-instruction per SIMD against "
+                    "1.06-1.16 ns for 32-bit add / logic, tools/valu_rate_probe.hip; higher-occupancy variants ran "
+                    "slower, profiles/r06_ldpc_hr_ab.json).",
         },
         "cpu_baseline": cpu,
     }
@@ -606,7 +610,9 @@ def valu_bound(cbs, its_mean, kernel_ms):
     import os
 
     prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
-    path = os.path.join(prof, "r05_ldpc_valu_model.json")
+    path = os.path.join(prof, "r06_ldpc_valu_model.json")
+    if not os.path.exists(path):
+        path = os.path.join(prof, "r05_ldpc_valu_model.json")
     if os.path.exists(path):
         m = json.load(open(path))
         insts = cbs * m["valu_insts_per_cb"] * (its_mean / m["iterations_mean"]) if m.get("scale_by_iterations") \
@@ -615,7 +621,10 @@ def valu_bound(cbs, its_mean, kernel_ms):
         issue_s = cycles / (1024 * 2.4e9)
         return {"achieved_frac_of_peak_issue": issue_s * 1e3 / kernel_ms, "issue_bound_ms": issue_s * 1e3,
                 "kernel_ms": kernel_ms, "valu_insts": insts, "cycles_per_valu_insn": m.get("cycles_per_valu_insn", 2.0),
-                "valu_busy_pmc": m.get("valu_busy"), "basis": "SQ_INSTS_VALU of the in-step launch (r05 PMC)",
+                "valu_busy_pmc": m.get("valu_busy"),
+                "basis": ("SQ_INSTS_VALU of the in-step launch at the mean issue cost of its opcode mix (r06 PMC + "
+                          "per-opcode microbenchmark)" if "r06" in os.path.basename(path)
+                          else "SQ_INSTS_VALU of the in-step launch (r05 PMC)"),
                 "model": os.path.basename(path), "iterations_mean": its_mean}
     path = os.path.join(prof, "ldpc_valu_model.json")
     if not os.path.exists(path):
