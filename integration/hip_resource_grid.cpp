@@ -291,6 +291,7 @@ void hip_resource_grid::defer(hip_grid_deferred_writer& w)
   std::lock_guard<std::mutex> lock(mtx);
   if (std::find(deferred.begin(), deferred.end(), &w) == deferred.end()) {
     deferred.push_back(&w);
+    w.attached(*this);
   }
   device_dirty = true;
   ++ver;

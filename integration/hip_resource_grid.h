@@ -63,6 +63,8 @@ public:
   virtual hipStream_t stream() const = 0;
   /// The grid is being destroyed: forget it, dropping what is staged for it.  Called with the grid locked.
   virtual void detach(hip_resource_grid& grid) = 0;
+  /// The grid registered this writer (defer); issue() or detach() unregister it.  Called with the grid locked.
+  virtual void attached(hip_resource_grid& grid) { (void)grid; }
 };
 
 /// Reader of a hip_resource_grid: the reference interface over the host mirror (downloaded on demand).

@@ -395,22 +395,17 @@ public:
     }
   }
 
-  // issues what is staged (into its grid) and waits for every launch of the stager to complete
+  // issues what is staged (every grid the stager is registered with: the list mirrors the grids' own, see
+  // attached / issue / detach) and waits for every launch of the stager to complete
   void flush()
   {
-    hip::hip_resource_grid* g;
+    std::vector<hip::hip_resource_grid*> grids;
     {
       std::lock_guard<std::mutex> lock(mtx);
-      g = cur;
+      grids = registered;
     }
-    if (g != nullptr) {
+    for (hip::hip_resource_grid* g : grids) {
       g->issue_deferred(*this);
-    }
-    {
-      std::lock_guard<std::mutex> lock(mtx);
-      if (cur == g) {
-        cur = nullptr;
-      }
     }
     stream_.drain();
   }
@@ -425,7 +420,7 @@ public:
     hip::hip_resource_grid* prev;
     {
       std::lock_guard<std::mutex> lock(mtx);
-      prev = cur;
+      prev = cur; // (non-null: symbols are staged for it, so it is registered and alive)
     }
     if (prev != nullptr && prev != &g) {
       prev->issue_deferred(*this); // another grid (the next slot's): what is staged for the previous one goes now
@@ -451,9 +446,11 @@ public:
     return true;
   }
 
+  // (called by g with g locked, g having just removed this writer from its list)
   void issue(hip::hip_resource_grid& g, uint32_t* d) override
   {
     std::lock_guard<std::mutex> lock(mtx);
+    unregister(g);
     batch& b = ring[next];
     if (cur != &g || b.count == 0) {
       return;
@@ -488,9 +485,16 @@ public:
 
   hipStream_t stream() const override { return stream_.s; }
 
+  void attached(hip::hip_resource_grid& g) override
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    registered.push_back(&g);
+  }
+
   void detach(hip::hip_resource_grid& g) override
   {
     std::lock_guard<std::mutex> lock(mtx);
+    unregister(g);
     if (cur == &g) {
       cur               = nullptr;
       ring[next].count = 0;
@@ -508,6 +512,11 @@ private:
     bool          in_flight = false;
     unsigned      count     = 0;
   };
+
+  void unregister(hip::hip_resource_grid& g)
+  {
+    registered.erase(std::remove(registered.begin(), registered.end(), &g), registered.end());
+  }
 
   // the batch allocated and free for the host (its last launch has completed); lock held
   bool ready(batch& b)
@@ -542,6 +551,7 @@ private:
   unsigned                  stride = 0; // samples per staged symbol (the longest symbol)
   std::mutex                mtx;
   hip::hip_resource_grid*   cur  = nullptr; // the grid the staged symbols belong to (nullptr: nothing staged)
+  std::vector<hip::hip_resource_grid*> registered; // the grids whose deferred list holds this writer
   std::array<batch, RING>   ring;
   unsigned                  next = 0;       // the batch being filled
 };
