@@ -1244,6 +1244,55 @@ __device__ __forceinline__ void fr_layer(lds_i8* lds, ST& st, uint32_t t, std::i
   }
 }
 
+// Barrier groups of BG1 layers (r06): consecutive layers that share no variable node read and write disjoint soft
+// bits, so no workgroup barrier is needed between them -- the result is the sequential one, bit for bit.  A layer
+// starts a new group when one of its columns is a column of a layer of the current group.  BG1 (the lower part is
+// built of orthogonal row pairs): 32 groups for 46 layers, layers 16-17, 20-21, 22-23, ..., 44-45 paired.
+#ifndef FR_GROUPS
+#define FR_GROUPS 1
+#endif
+template <int BG>
+struct bg_groups_t {
+  int first[bg_traits<BG>::M] = {}; // first layer of the group of layer l
+  int count                   = 0;
+  constexpr bg_groups_t()
+  {
+    int rs[bg_traits<BG>::M + 1] = {};
+    for (int l = 0; l < bg_traits<BG>::M; ++l) {
+      rs[l + 1] = rs[l] + bg_traits<BG>::deg(l);
+    }
+    auto col = [](int e) { return BG == 1 ? tables::SRS_BG1_EDGES[e][1] : tables::SRS_BG2_EDGES[e][1]; };
+    int  gs  = 0;
+    for (int l = 0; l < bg_traits<BG>::M; ++l) {
+      bool share = l == 0;
+      for (int a = gs; a < l && !share; ++a) {
+        for (int i = rs[a]; i < rs[a + 1] && !share; ++i) {
+          for (int j = rs[l]; j < rs[l + 1] && !share; ++j) {
+            share = col(i) == col(j);
+          }
+        }
+      }
+      if (share) {
+        gs = l;
+        ++count;
+      }
+      first[l] = gs;
+    }
+  }
+};
+template <int BG>
+inline constexpr bg_groups_t<BG> BG_GROUPS{};
+template <int BG>
+constexpr int bg_group_start(int l)
+{
+  return BG_GROUPS<BG>.first[l];
+}
+constexpr int bg1_group_start(int l)
+{
+  return bg_group_start<1>(l);
+}
+static_assert(BG_GROUPS<1>.count == 32 && BG_GROUPS<2>.count == 28, "BG1 / BG2 barrier groups of the decoders");
+
 template <int L, int ARITH, int MAXL, typename ST>
 __device__ __forceinline__ void fr_layers(lds_i8* lds, ST& st, uint32_t t, int nof_layers)
 {
@@ -1254,7 +1303,13 @@ __device__ __forceinline__ void fr_layers(lds_i8* lds, ST& st, uint32_t t, int n
     if (L < 4 || L < nof_layers) { // uniform; nof_layers >= 4
       asm volatile("" : "+v"(t));
       fr_layer<L, ARITH>(lds, st, t, std::make_integer_sequence<int, bg_traits<1>::deg(L)>{});
-      __syncthreads();
+      // a barrier before the next layer unless it continues this one's group (and runs); always one after the last
+      constexpr bool next_joins = FR_GROUPS && L + 1 < MAXL && bg1_group_start(L + 1) != L + 1;
+      if (!next_joins || !(L + 1 < 4 || L + 1 < nof_layers)) {
+        __syncthreads();
+      } else {
+        asm volatile("" ::: "memory"); // (program order of this lane's LDS accesses; the layers touch disjoint bytes)
+      }
     }
     fr_layers<L + 1, ARITH, MAXL>(lds, st, t, nof_layers);
   }
@@ -1890,8 +1945,15 @@ __device__ __forceinline__ void pk_layers(lds_i8* lds, pk_state<BG>& st, uint32_
       if (own) {
         pk_layer<BG, L, ARITH, 128 * W>(lds, st, t, g, std::make_integer_sequence<int, bg_traits<BG>::deg(L)>{});
       }
+      // no barrier before a next layer of the same group (disjoint columns, see bg_groups_t); always one after
+      // the last layer that runs
+      constexpr bool next_joins = FR_GROUPS && L + 1 < bg_traits<BG>::M && bg_group_start<BG>(L + 1) != L + 1;
       if constexpr (W > 1) {
-        __syncthreads();
+        if (!next_joins || !(L + 1 < 4 || L + 1 < nof_layers)) {
+          __syncthreads();
+        } else {
+          asm volatile("" ::: "memory");
+        }
       } else {
         asm volatile("" ::: "memory"); // one wave: LDS accesses execute in issue order
       }
