@@ -22,22 +22,40 @@ __device__ __forceinline__ float safe_rcp(float nv)
   return nv > 0.0f ? 1.0f / nv : 0.0f;
 }
 
-// quantize_ps (avx2_helpers.h:121): scale, clip to +-120, round half to even.
-__device__ __forceinline__ int q_simd(float v, float range)
-{
-#pragma clang fp contract(off)
-  const float x = v * (120.0f / range);
-  // clip as one v_med3_f32 (equal to the two compares for every non-NaN x; a NaN x gives 0 below)
-  const float c = __builtin_rintf(__builtin_amdgcn_fmed3f(x, -120.0f, 120.0f));
-  return x != x ? 0 : static_cast<int>(c);
-}
-
 // median(x, lo, hi) as one v_med3_i32 (lo <= hi)
 __device__ __forceinline__ int med3_int(int x, int lo, int hi)
 {
   int r;
   asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
   return r;
+}
+
+// v_cvt_i32_f32: round toward zero, out-of-range values saturate, NaN converts to 0 (the instruction's defined
+// behaviour, which a C++ conversion does not promise)
+__device__ __forceinline__ int cvt_i32(float x)
+{
+  int r;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+#ifndef DEMAP_Q_CVT
+#define DEMAP_Q_CVT 1
+#endif
+// quantize_ps (avx2_helpers.h:121): scale, clip to +-120, round half to even.
+__device__ __forceinline__ int q_simd(float v, float range)
+{
+#pragma clang fp contract(off)
+  const float x = v * (120.0f / range);
+#if DEMAP_Q_CVT
+  // round, convert (NaN -> 0, infinities saturate), then clip as one v_med3_i32: the same integer as clipping the
+  // float first for every x (the bounds are integers), without a per-value NaN compare and select (r06)
+  return med3_int(cvt_i32(__builtin_rintf(x)), -120, 120);
+#else
+  // clip as one v_med3_f32 (equal to the two compares for every non-NaN x; a NaN x gives 0 below)
+  const float c = __builtin_rintf(__builtin_amdgcn_fmed3f(x, -120.0f, 120.0f));
+  return x != x ? 0 : static_cast<int>(c);
+#endif
 }
 
 // log_likelihood_ratio::quantize: clip to the range, round half away from zero.
@@ -121,6 +139,11 @@ __device__ __forceinline__ void demap_symbol(const demodulate_args& a, const flo
   const int   m   = a.qm / 2;
   const float rcp = safe_rcp(nv);
   if (simd) {
+#if DEMAP_Q_CVT
+    // |x| <= NEAR_ZERO gives LLR 0: a zero reciprocal for that component (the quantizer maps the 0 * (finite) and
+    // 0 * inf = NaN products alike to 0), one select per component instead of one per LLR
+    const float rc[2] = {fabsf(xs[0]) <= NEAR_ZERO ? 0.0f : rcp, fabsf(xs[1]) <= NEAR_ZERO ? 0.0f : rcp};
+#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k) { // compile-time k: the table fields are scalar loads
       if (k >= m) {
@@ -131,10 +154,14 @@ __device__ __forceinline__ void demap_symbol(const demodulate_args& a, const flo
       for (int c = 0; c < 2; ++c) {
         const float x   = xs[c];
         const int   idx = med3_int(static_cast<int>(floorf(x * t.inv_width)) + t.n / 2, 0, t.n - 1);
-        float l         = (lt[(2 * k) * 16 + idx] * x + lt[(2 * k + 1) * 16 + idx]) * rcp;
+#if DEMAP_Q_CVT
+        const float l = (lt[(2 * k) * 16 + idx] * x + lt[(2 * k + 1) * 16 + idx]) * rc[c];
+#else
+        float l = (lt[(2 * k) * 16 + idx] * x + lt[(2 * k + 1) * 16 + idx]) * rcp;
         if (fabsf(x) <= NEAR_ZERO) {
           l = 0.0f;
         }
+#endif
         o[2 * k + c] = static_cast<int8_t>(q_simd(l, 20.0f));
       }
     }
