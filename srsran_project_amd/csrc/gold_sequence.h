@@ -29,6 +29,27 @@ constexpr int PRBS_NIB_OFF = PRBS_RADIX_OFF + 2 * PRBS_RADIX_DIGITS * 16 * 31;
 // [2][PRBS_RADIX_DIGITS][16][31] A^(d 16^k) (d = 0 unused) and the nibble tables [2][PRBS_NIB_NK][8][16].
 std::vector<uint32_t> gold_jump_tables();
 
+// Word basis of the sequence from its start: c is linear in c_init, so word w (bits c(32 w .. 32 w + 31)) of any c_init
+// is row 31 (the x1 part) XOR the rows j < 31 of the set bits j of c_init (x2 from c_init = 2^j), table
+// [32][GOLD_BASIS_WORDS].  A word then costs 32 independent loads instead of a chain of dependent jump-ahead products.
+constexpr uint32_t GOLD_BASIS_WORDS = 224; // bits 0 .. 7,167 (a DM-RS symbol's last pilot bit: 12 x 274 + 2 x 1,650)
+std::vector<uint32_t> gold_word_basis();
+
+__device__ __forceinline__ uint32_t gold_basis_word(const uint32_t* basis, uint32_t c_init, uint32_t w)
+{
+  uint32_t t[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    t[j] = basis[j * GOLD_BASIS_WORDS + w]; // every load issued before the first use
+  }
+  uint32_t r = t[31];
+#pragma unroll
+  for (int j = 0; j < 31; ++j) {
+    r ^= t[j] & (0u - ((c_init >> j) & 1u));
+  }
+  return r;
+}
+
 // state' = M * state over GF(2), M given by its 31 columns.
 __device__ __forceinline__ uint32_t gf2_apply(const uint32_t* cols, uint32_t state)
 {

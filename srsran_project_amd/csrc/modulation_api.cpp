@@ -161,6 +161,27 @@ std::vector<uint32_t> srs_amd::gold_jump_tables()
   return t;
 }
 
+std::vector<uint32_t> srs_amd::gold_word_basis()
+{
+  std::vector<uint32_t> t(32 * GOLD_BASIS_WORDS, 0u);
+  for (int row = 0; row < 32; ++row) {
+    // rows 0..30: x2 from c_init = 2^row; row 31: x1 (initial state 1)
+    const bool x2 = row < 31;
+    uint32_t   st = x2 ? (1u << row) : 1u;
+    for (int n = 0; n < 1600; ++n) {
+      st = lfsr_step(st, x2);
+    }
+    for (uint32_t w = 0; w < GOLD_BASIS_WORDS; ++w) {
+      uint32_t word = 0;
+      for (uint32_t b = 0; b < 32; ++b) {
+        word |= (st & 1u) << b;
+        st = lfsr_step(st, x2);
+      }
+      t[static_cast<size_t>(row) * GOLD_BASIS_WORDS + w] = word;
+    }
+  }
+  return t;
+}
 
 struct srs_amd_modulator {
   int                  device = 0;

@@ -36,6 +36,28 @@
 namespace srs_amd {
 namespace {
 
+// Phase probe (tools/chest_probe.py; never in the product build): -DSRS_AMD_CHEST_PROBE records per-workgroup
+// s_memtime stamps of the pilot and statistics kernels' phases, read back by srs_amd_chest_probe_read.
+#ifdef SRS_AMD_CHEST_PROBE
+constexpr uint32_t CHEST_PROBE_WG = 4096;
+__device__ uint64_t g_chest_probe[2][CHEST_PROBE_WG][16];
+#define CHEST_STAMP(k, i)                                                                                            \
+  do {                                                                                                               \
+    if (threadIdx.x == 0) {                                                                                          \
+      const uint32_t wg_ = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;                           \
+      if (wg_ < CHEST_PROBE_WG) {                                                                                    \
+        g_chest_probe[k][wg_][i] = (i) == 0 || (i) == 15 ? __builtin_amdgcn_s_memrealtime()                          \
+                                                         : __builtin_amdgcn_s_memtime();                             \
+      }                                                                                                              \
+    }                                                                                                                \
+  } while (0)
+#else
+#define CHEST_STAMP(k, i)                                                                                            \
+  do {                                                                                                               \
+  } while (0)
+#endif
+
+
 using chdev::bf16_bits;
 using chdev::cmul;
 using chdev::from_cbf16;
@@ -127,32 +149,22 @@ __device__ __forceinline__ uint32_t dmrs_nof_words(const chest_args& a, uint32_t
   return (bit_first + 2 * a.npil + 31) / 32 - w_first;
 }
 
-// The DM-RS words of the item into LDS, one wave per DM-RS symbol: the wave jumps to the allocation's first word
-// once (uniform c_init and position), each lane then to its own words w = lane and lane + 64 (gold_state_lanes;
-// nwords <= 106).  Workgroup (0, 0) of the item also keeps them in a.dmrs_seq for the
-// statistics kernel.  Returns the bit offset of the first allocated pilot in word 0.
+// The DM-RS words of the item into LDS, one thread per word (nds x nwords <= 4 x 106) from the word basis
+// (gold_basis_word: 32 independent loads per word, no dependent jump-ahead chain).  Workgroup (0, 0) of the item
+// also keeps them in a.dmrs_seq for the statistics kernel.  Returns the bit offset of the first allocated pilot in
+// word 0.
 __device__ __forceinline__ uint32_t dmrs_words_gen(const chest_args& a, uint32_t (*seq)[CH_SEQWORDS])
 {
   uint32_t       w_first;
   const uint32_t nwords = dmrs_nof_words(a, w_first);
-  const uint32_t lane   = threadIdx.x % 64;
   const bool     keep   = blockIdx.x == 0 && blockIdx.y == 0;
-  for (uint32_t d = threadIdx.x / 64; d < a.nds; d += blockDim.x / 64) {
-    uint32_t x1, x2;
-    gold_state_lanes(a.jump, a.c_init[d], 32 * w_first, lane, x1, x2);
-#pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {
-      const uint32_t w = lane + 64 * h;
-      if (w < nwords) {
-        const uint32_t word = gold_emit32(x1, x2);
-        seq[d][w]           = word;
-        if (keep) {
-          a.dmrs_seq[d * CH_SEQWORDS + w] = word;
-        }
-      }
-      if (h == 0) {
-        gold_advance_pow2(a.jump, 11, x1, x2); // + 64 words
-      }
+#pragma unroll 1
+  for (uint32_t i = threadIdx.x; i < a.nds * nwords; i += blockDim.x) {
+    const uint32_t d    = i / nwords, w = i % nwords;
+    const uint32_t word = gold_basis_word(a.gold_basis, a.c_init[d], w_first + w);
+    seq[d][w]           = word;
+    if (keep) {
+      a.dmrs_seq[d * CH_SEQWORDS + w] = word;
     }
   }
   return 12u * a.prb_lo - 32 * w_first;
@@ -259,6 +271,8 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
   const int      v     = static_cast<int>(slice / a.nof_lse);
   const int      s     = static_cast<int>(slice % a.nof_lse);
   const int      g     = v / 2;
+  CHEST_STAMP(0, 0);
+  CHEST_STAMP(0, 1);
 
   const uint32_t* gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc +
                           12 * a.prb_lo;
@@ -291,6 +305,7 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
   };
   const uint32_t bit0 = dmrs_words_gen(a, seq);
   __syncthreads(); // seq ready
+  CHEST_STAMP(0, 2);
 
   // The port's CFO: sum over the layers v of (rx_1 conj(p_1,v)) conj(rx_0 conj(p_0,v)).  The two layers of a CDM
   // group differ in their pilots by w_f = -1 on odd indices in both symbols, which cancels in the product: the
@@ -323,18 +338,17 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
       }
     }
     acc = block_sum4(acc, red);
-    if (tid == 0) {
+    // thread d < nds: the rotation of DM-RS symbol d (every such thread computes the same cfo)
+    if (tid < static_cast<uint32_t>(nds)) {
       const float de  = a.epoch[a.dmrs_sym[1]] - a.epoch[a.dmrs_sym[0]];
       float       cfo = atan2f(acc.y, acc.x) / TWOPI_F / de;
       if (a.ncdm > 1) {
         cfo += atan2f(acc.w, acc.z) / TWOPI_F / de;
       }
       cfo /= static_cast<float>(a.ncdm);
-      for (int d = 0; d < nds; ++d) {
-        s_rot[d] = a.compensate_cfo ? polar1(-TWOPI_F * a.epoch[a.dmrs_sym[d]] * cfo) : make_float2(1, 0);
-      }
+      s_rot[tid] = a.compensate_cfo ? polar1(-TWOPI_F * a.epoch[a.dmrs_sym[tid]] * cfo) : make_float2(1, 0);
       s_has_cfo = 1;
-      if (slice == 0) {
+      if (slice == 0 && tid == 0) {
         float* out = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
         out[3]     = 1.0f;
         out[4]     = cfo;
@@ -350,6 +364,7 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
     }
   }
   __syncthreads(); // rotations ready
+  CHEST_STAMP(0, 3);
   const bool  has_cfo  = s_has_cfo != 0;
   const bool  rotate   = has_cfo && a.compensate_cfo;
   const float total    = a.td == SRS_AMD_CHEST_TD_AVERAGE ? (1.0f / a.beta) / static_cast<float>(nds) : 1.0f / a.beta;
@@ -393,8 +408,10 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
     }
     x[k] = cscale(y, total);
   }
+  CHEST_STAMP(0, 4);
 
   // FD smoothing (apply_fd_smoothing, port_channel_estimator_helpers.cpp:213-260).
+  bool staged = false; // smoothed pilots already in enl_out
   if (a.fd == SRS_AMD_CHEST_FD_MEAN) {
     float4 sm = make_float4(0, 0, 0, 0);
 #pragma unroll
@@ -412,10 +429,10 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
     }
   } else if (a.fd == SRS_AMD_CHEST_FD_FILTER) {
     const int nv = a.nof_v;
-    for (uint32_t i = tid; i < npil + 2 * CH_MAXV; i += CS_THREADS) {
-      enl_in[i] = make_float2(0, 0);
+    // the pilots between zero pads of CH_MAXV (the virtual pilots overwrite nv of each pad)
+    if (tid < 2 * CH_MAXV) {
+      enl_in[tid < CH_MAXV ? tid : npil + tid] = make_float2(0, 0);
     }
-    __syncthreads();
 #pragma unroll
     for (int k = 0; k < CS_PPT; ++k) {
       const uint32_t m = tid + k * CS_THREADS;
@@ -424,6 +441,7 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
       }
     }
     __syncthreads();
+    CHEST_STAMP(0, 10);
     if (T == 64) { // one wave: both ends in turn
       virtual_pilots_wave(enl_in + CH_MAXV - nv, enl_in + CH_MAXV, nv, true);
       virtual_pilots_wave(enl_in + CH_MAXV + npil, enl_in + CH_MAXV + npil - nv, nv, false);
@@ -433,30 +451,60 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
       virtual_pilots_wave(enl_in + CH_MAXV + npil, enl_in + CH_MAXV + npil - nv, nv, false);
     }
     __syncthreads();
-    const int half = a.nof_taps / 2;
+    CHEST_STAMP(0, 11);
+    // Blocked FIR: thread t filters pilots FB t .. FB t + FB - 1 from one window of FB + 15 LDS values (23 reads
+    // instead of one per tap and pilot).  Inputs outside [-nv, npil + nv) read the zero pads: the reference skips
+    // them, and adding a +-0 product leaves every partial sum unchanged, so the per-tap order and values are the
+    // reference's (r06: 12.2 -> see DESIGN.md).
+    constexpr int FB   = CS_PPT;
+    constexpr int NWIN = FB + CH_MAXV + 3;
+    const int     half = a.nof_taps / 2;
+    const int     m0   = static_cast<int>(tid) * FB;
+    float2        y[FB];
+    if (m0 < static_cast<int>(npil)) {
+      float2 win[NWIN];
 #pragma unroll
-    for (int k = 0; k < CS_PPT; ++k) {
-      const int m = static_cast<int>(tid + k * CS_THREADS);
-      if (m < static_cast<int>(npil)) {
+      for (int q = 0; q < NWIN; ++q) {
+        win[q] = enl_in[CH_MAXV + m0 - half + q];
+      }
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
         float2 acc = make_float2(0, 0);
-        // compile-time tap bound: the LDS reads of every tap are issued together (same summation order)
 #pragma unroll
         for (int j = 0; j < CH_MAXV + 4; ++j) {
-          const int i = m + j - half; // convolution input index (pilot domain)
-          if (j < a.nof_taps && i >= -nv && i < static_cast<int>(npil) + nv) {
-            const float2 in = enl_in[CH_MAXV + i];
-            const float  c  = a.rc[a.nof_taps - 1 - j];
-            acc.x           = acc.x + in.x * c; // srsran_simd_f_mul then _add
-            acc.y           = acc.y + in.y * c;
+          if (j < a.nof_taps) {
+            const float c = a.rc[a.nof_taps - 1 - j];
+            acc.x         = acc.x + win[i + j].x * c; // srsran_simd_f_mul then _add
+            acc.y         = acc.y + win[i + j].y * c;
           }
         }
-        x[k] = acc;
+        y[i] = acc;
       }
     }
+    __syncthreads(); // every FIR read of enl_in is done before the smoothed pilots overwrite it
+    CHEST_STAMP(0, 12);
+    if (m0 < static_cast<int>(npil)) {
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
+        if (m0 + i < static_cast<int>(npil)) {
+          enl_out[m0 + i] = y[i];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CS_PPT; ++k) {
+      const uint32_t m = tid + k * CS_THREADS;
+      x[k]             = m < npil ? enl_out[m] : make_float2(0, 0);
+    }
+    staged = true;
   }
 
-  // RSRP share, store the smoothed pilots, stage them for the interpolation.
-  __syncthreads(); // every FIR read of enl_in is done before the smoothed pilots overwrite it
+  // RSRP share, store the smoothed pilots, stage them for the interpolation (the blocked FIR staged them already).
+  if (!staged) {
+    __syncthreads(); // every read of enl_in is done before the smoothed pilots overwrite it
+  }
+  CHEST_STAMP(0, 5);
   float   rsrp = 0;
   float2* filt = a.filt + (static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice) * npil;
 #pragma unroll
@@ -465,10 +513,15 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
     if (m < npil) {
       rsrp    = __builtin_fmaf(x[k].x * x[k].x + x[k].y * x[k].y, rsrp_nrm, rsrp);
       filt[m] = x[k];
-      enl_out[m] = x[k];
+      if (!staged) {
+        enl_out[m] = x[k];
+      }
     }
   }
-  __syncthreads();
+  if (!staged) {
+    __syncthreads();
+  }
+  CHEST_STAMP(0, 6);
   // Linear interpolation (interpolator_linear_impl.cpp): pilots at offset g + 2i.
   float2* fr = a.freq + (static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice) * a.nof_re;
   constexpr uint32_t IU = 4; // outputs per thread and round: their LDS reads issued together
@@ -497,6 +550,7 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
     }
   }
   // the slice's time-alignment correlation row (every thread takes part in the engine's barriers)
+  CHEST_STAMP(0, 7);
   float*   corr = a.corr + (static_cast<uint64_t>(gp) * a.L * a.nof_lse + slice) * a.ta_n;
   auto*    work = reinterpret_cast<dft::cf*>(enl_in);
   switch (a.ta_n) {
@@ -515,9 +569,12 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
       break;
   }
   const float4 tot = block_sum4(make_float4(rsrp, 0, 0, 0), red);
+  CHEST_STAMP(0, 8);
   if (tid == 0) {
     a.acc[static_cast<uint64_t>(gp) * CH_ACC + CH_ACC_RSRP + slice] = tot.x;
   }
+  CHEST_STAMP(0, 9);
+  CHEST_STAMP(0, 15);
 }
 
 // Per-port measurements, one workgroup per (grid, port): EPRE over every received DM-RS RE, the noise energy per
@@ -545,6 +602,8 @@ __global__ __launch_bounds__(ST) void chest_stats_kernel(chest_args a_in, chest_
   const int           nds  = static_cast<int>(a.nds);
   const int           L    = static_cast<int>(a.L);
   const uint32_t      N    = a.ta_n;
+  CHEST_STAMP(1, 0);
+  CHEST_STAMP(1, 1);
   const float*        acc  = a.acc + static_cast<uint64_t>(gp) * CH_ACC;
   const uint32_t      bit0 = dmrs_words(a, seq);
   const uint32_t      nsl  = a.L * a.nof_lse;
@@ -566,6 +625,7 @@ __global__ __launch_bounds__(ST) void chest_stats_kernel(chest_args a_in, chest_
     corr[k] = c;
   }
   __syncthreads(); // seq, corr ready
+  CHEST_STAMP(1, 2);
 
   const bool rotate = acc[3] != 0.0f && a.compensate_cfo;
   float2     rot_fwd[CH_MAXDMRS]; // the noise predictor's phase
@@ -573,13 +633,22 @@ __global__ __launch_bounds__(ST) void chest_stats_kernel(chest_args a_in, chest_
   for (int d = 0; d < CH_MAXDMRS; ++d) {
     rot_fwd[d] = d < nds ? polar1(TWOPI_F * a.epoch[a.dmrs_sym[d]] * acc[4]) : make_float2(1, 0);
   }
+  CHEST_STAMP(1, 10);
   const uint32_t* gridp = a.grids + grid * a.grid_stride + static_cast<uint64_t>(port) * CH_NSYMB * a.nsubc +
                           12 * a.prb_lo;
   const float2*   filt  = a.filt + static_cast<uint64_t>(gp) * a.L * a.nof_lse * npil;
   float           noise0 = 0, noise1 = 0, epre = 0;
   const float     sf     = a.beta / static_cast<float>(a.nof_lse);
   const int nlse = static_cast<int>(a.nof_lse);
-  for (uint32_t m = tid; m < npil; m += ST_THREADS) {
+  // at most two pilots per thread (npil <= 1,650 with 1,024 threads, <= 412 with 256): both unrolled, so the second
+  // pilot's loads are issued with the first's
+  static_assert(2 * ST_THREADS >= (ST_THREADS == 256 ? static_cast<int>(CH_SMALL_NPIL) : 6 * 275), "pilots per thread");
+#pragma unroll
+  for (uint32_t it = 0; it < 2; ++it) {
+    const uint32_t m = tid + it * ST_THREADS;
+    if (m >= npil) {
+      continue;
+    }
     // compile-time bounds on CDM groups, layers, LSE symbols and DM-RS symbols: every load of an iteration is
     // issued before the first is used (the runtime-bounded loops waited one memory latency per load)
 #pragma unroll
@@ -638,6 +707,7 @@ __global__ __launch_bounds__(ST) void chest_stats_kernel(chest_args a_in, chest_
     }
   }
   const float4 tot = block_sum4(make_float4(noise0, noise1, epre, 0), red);
+  CHEST_STAMP(1, 3);
 
   // Peak search of estimate_ta_correlation (time_alignment_estimator_dft_impl.cpp:248-310) over wave 0 instead
   // of a serial scan by one thread: the first maximum (strict >) of corr[0, max_taps) and of
@@ -745,6 +815,8 @@ __global__ __launch_bounds__(ST) void chest_stats_kernel(chest_args a_in, chest_
     st.cfo_hz           = acc[3] != 0.0f ? acc[4] * a.scs_hz : __builtin_nanf("");
     a.stats[gp]         = st;
   }
+  CHEST_STAMP(1, 4);
+  CHEST_STAMP(1, 15);
 }
 
 // Channel estimates: one thread per (grid, port, layer, symbol, subcarrier). Inside the
@@ -806,6 +878,25 @@ __global__ __launch_bounds__(256) void chest_expand_kernel(chest_args a_in, ches
 }
 
 } // namespace
+
+#ifdef SRS_AMD_CHEST_PROBE
+extern "C" int srs_amd_chest_probe_read(void* host, uint64_t bytes, int clear)
+{
+  if (bytes > sizeof(g_chest_probe)) {
+    bytes = sizeof(g_chest_probe);
+  }
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chest_probe), bytes) != hipSuccess) {
+    return -2;
+  }
+  if (clear) {
+    static const uint64_t zero[2 * CHEST_PROBE_WG * 16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_chest_probe), zero, sizeof(zero)) != hipSuccess) {
+      return -2;
+    }
+  }
+  return 0;
+}
+#endif
 
 hipError_t launch_chest(const chest_args& a, uint32_t nof_grids, hipStream_t stream, bool expand)
 {

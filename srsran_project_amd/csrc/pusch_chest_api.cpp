@@ -65,6 +65,7 @@ struct srs_amd_pusch_chest {
   int           device = 0;
   hipStream_t   stream = nullptr;
   uint32_t*     d_jump = nullptr;
+  uint32_t*     d_gold_basis = nullptr;
   float*        d_tw   = nullptr; // twiddle tables of N = 128 .. 4096, back to back
   device_buffer scratch;
   device_buffer host_io;
@@ -81,6 +82,7 @@ struct srs_amd_pusch_chest {
       (void)hipStreamDestroy(stream);
     }
     (void)hipFree(d_jump);
+    (void)hipFree(d_gold_basis);
     (void)hipFree(d_tw);
     for (auto& t : lp_tables) {
       (void)hipFree(t.second);
@@ -325,6 +327,13 @@ int srs_amd_pusch_chest_create(srs_amd_pusch_chest** chest, int device)
   if (e == hipSuccess) {
     e = hipMemcpy(c->d_jump, j.data(), j.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   }
+  const std::vector<uint32_t> gb = gold_word_basis();
+  if (e == hipSuccess) {
+    e = hipMalloc(&c->d_gold_basis, gb.size() * sizeof(uint32_t));
+  }
+  if (e == hipSuccess) {
+    e = hipMemcpy(c->d_gold_basis, gb.data(), gb.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) {
     e = hipMalloc(&c->d_tw, tw.size() * sizeof(float));
   }
@@ -408,6 +417,7 @@ static int estimate_batch_impl(srs_amd_pusch_chest*              chest,
   a.est_stride  = est_stride;
   a.stats       = d_stats;
   a.jump        = chest->d_jump;
+  a.gold_basis  = chest->d_gold_basis;
   a.ta_tw       = chest->tw(a.ta_n);
   a.lp_seq      = nullptr;
   if (cfg->low_papr) {
@@ -507,6 +517,7 @@ int srs_amd::chest_estimate_slot_unexpanded(::srs_amd_pusch_chest* chest,
     a.est_stride  = 0;
     a.stats       = items[i].d_stats;
     a.jump        = chest->d_jump;
+    a.gold_basis  = chest->d_gold_basis;
     a.ta_tw       = chest->tw(a.ta_n);
     a.lp_seq      = nullptr;
     if (items[i].cfg->low_papr) {

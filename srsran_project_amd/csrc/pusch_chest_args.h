@@ -40,6 +40,7 @@ struct chest_args {
   const float2* lp_seq; // transform precoding: the low-PAPR pilot sequence [npil] (nullptr: Gold sequence)
   // constants
   const uint32_t* jump;    // Gold-sequence jump matrices
+  const uint32_t* gold_basis; // Gold-sequence word basis [32][GOLD_BASIS_WORDS] (gold_sequence.h)
   const float2*   ta_tw;   // W_N^m table of the time-alignment IDFT size
   uint32_t nof_ports;
   uint32_t nsubc;
