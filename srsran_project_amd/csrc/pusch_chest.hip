@@ -452,11 +452,13 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
     }
     __syncthreads();
     CHEST_STAMP(0, 11);
-    // Blocked FIR: thread t filters pilots FB t .. FB t + FB - 1 from one window of FB + 15 LDS values (23 reads
+    // Blocked FIR: thread t filters pilots FB t .. FB t + FB - 1 from one window of FB + 15 LDS values (22 reads
     // instead of one per tap and pilot).  Inputs outside [-nv, npil + nv) read the zero pads: the reference skips
     // them, and adding a +-0 product leaves every partial sum unchanged, so the per-tap order and values are the
-    // reference's (r06: 12.2 -> see DESIGN.md).
-    constexpr int FB   = CS_PPT;
+    // reference's.  FB = 7: an odd stride of 14 dwords between lanes spreads a wave's window reads over every LDS
+    // bank (FB = 8, a 16-dword stride, measured 7.4 us per launch in 16-way bank conflicts).
+    constexpr int FB   = 7;
+    static_assert(FB * 64 >= static_cast<int>(CH_SMALL_NPIL) && FB * 256 >= 6 * 275, "FIR outputs per thread");
     constexpr int NWIN = FB + CH_MAXV + 3;
     const int     half = a.nof_taps / 2;
     const int     m0   = static_cast<int>(tid) * FB;
@@ -467,18 +469,26 @@ chest_pilot_kernel(chest_args a_in, chest_items items)
       for (int q = 0; q < NWIN; ++q) {
         win[q] = enl_in[CH_MAXV + m0 - half + q];
       }
+      // the coefficients once, all loads issued together (a runtime-indexed a.rc read per tap and output was one
+      // dependent scalar load each: 6.2 us of the launch)
+      float rcv[CH_MAXV + 4];
+#pragma unroll
+      for (int j = 0; j < CH_MAXV + 4; ++j) {
+        rcv[j] = a.rc[max(a.nof_taps - 1 - j, 0)];
+      }
 #pragma unroll
       for (int i = 0; i < FB; ++i) {
-        float2 acc = make_float2(0, 0);
+        y[i] = make_float2(0, 0);
+      }
 #pragma unroll
-        for (int j = 0; j < CH_MAXV + 4; ++j) {
-          if (j < a.nof_taps) {
-            const float c = a.rc[a.nof_taps - 1 - j];
-            acc.x         = acc.x + win[i + j].x * c; // srsran_simd_f_mul then _add
-            acc.y         = acc.y + win[i + j].y * c;
+      for (int j = 0; j < CH_MAXV + 4; ++j) {
+        if (j < a.nof_taps) { // per output, taps in ascending order as before
+#pragma unroll
+          for (int i = 0; i < FB; ++i) {
+            y[i].x = y[i].x + win[i + j].x * rcv[j]; // srsran_simd_f_mul then _add
+            y[i].y = y[i].y + win[i + j].y * rcv[j];
           }
         }
-        y[i] = acc;
       }
     }
     __syncthreads(); // every FIR read of enl_in is done before the smoothed pilots overwrite it
@@ -640,9 +650,30 @@ __global__ __launch_bounds__(ST) void chest_stats_kernel(chest_args a_in, chest_
   float           noise0 = 0, noise1 = 0, epre = 0;
   const float     sf     = a.beta / static_cast<float>(a.nof_lse);
   const int nlse = static_cast<int>(a.nof_lse);
-  // at most two pilots per thread (npil <= 1,650 with 1,024 threads, <= 412 with 256): both unrolled, so the second
-  // pilot's loads are issued with the first's
+  // At most two pilots per thread (npil <= 1,650 with 1,024 threads, <= 412 with 256).  Every load of both is issued
+  // before the first is used: the smoothed pilots and received DM-RS REs go into registers from clamped (always
+  // valid) addresses, the arithmetic then masks what does not exist -- loads under the runtime guards waited one
+  // memory latency per guard.  One LSE slice per layer (average TD strategy) takes this path.
   static_assert(2 * ST_THREADS >= (ST_THREADS == 256 ? static_cast<int>(CH_SMALL_NPIL) : 6 * 275), "pilots per thread");
+  float2   F[2][CH_MAXL];       // [pilot][layer]: smoothed pilots (one LSE slice)
+  uint32_t R[2][2][CH_MAXDMRS]; // [pilot][CDM group][DM-RS symbol]: received DM-RS REs
+  if (nlse == 1) {
+#pragma unroll
+    for (uint32_t it = 0; it < 2; ++it) {
+      const uint32_t mc = min(tid + it * ST_THREADS, npil - 1);
+#pragma unroll
+      for (int v = 0; v < CH_MAXL; ++v) {
+        F[it][v] = filt[static_cast<uint64_t>(min(v, L - 1)) * npil + mc];
+      }
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+#pragma unroll
+        for (int d = 0; d < CH_MAXDMRS; ++d) {
+          R[it][g][d] = gridp[a.dmrs_sym[min(d, nds - 1)] * a.nsubc + 2 * mc + min(g, static_cast<int>(a.ncdm) - 1)];
+        }
+      }
+    }
+  }
 #pragma unroll
   for (uint32_t it = 0; it < 2; ++it) {
     const uint32_t m = tid + it * ST_THREADS;
@@ -664,12 +695,17 @@ __global__ __launch_bounds__(ST) void chest_stats_kernel(chest_args a_in, chest_
         if (v >= v1) {
           continue;
         }
-        const float2* fv = filt + static_cast<uint64_t>(v) * a.nof_lse * npil + m;
-        float2        t  = cscale(fv[0], sf);
+        float2 t;
+        if (nlse == 1) {
+          t = cscale(F[it][v], sf);
+        } else {
+          const float2* fv = filt + static_cast<uint64_t>(v) * a.nof_lse * npil + m;
+          t                = cscale(fv[0], sf);
 #pragma unroll
-        for (int s = 1; s < CH_MAXDMRS; ++s) {
-          if (s < nlse) {
-            t = cadd(cscale(fv[static_cast<uint64_t>(s) * npil], sf), t);
+          for (int s = 1; s < CH_MAXDMRS; ++s) {
+            if (s < nlse) {
+              t = cadd(cscale(fv[static_cast<uint64_t>(s) * npil], sf), t);
+            }
           }
         }
         if (vi == 0) {
@@ -694,7 +730,7 @@ __global__ __launch_bounds__(ST) void chest_stats_kernel(chest_args a_in, chest_
           }
           pred = cadd(pred, po);
         }
-        const float2 rx = from_cbf16(gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + g]);
+        const float2 rx = from_cbf16(nlse == 1 ? R[it][g][d] : gridp[a.dmrs_sym[d] * a.nsubc + 2 * m + g]);
         epre            = __builtin_fmaf(rx.x, rx.x, __builtin_fmaf(rx.y, rx.y, epre));
         const float2 n  = csub(rx, pred);
         const float  e  = __builtin_fmaf(n.x, n.x, n.y * n.y);
