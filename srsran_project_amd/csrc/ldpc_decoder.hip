@@ -1057,13 +1057,163 @@ __device__ __forceinline__ void hr_layer(lds_i8* lds, MSGS& c2v, uint32_t t, std
       ...);
 }
 
+// hr_layer with the edges taken two at a time (HR_PAIRS=1, an r06 A/B kept for the record, not the default): each
+// packed operation of an edge pair is two independent v_pk_* instructions on a four-element vector (edge a's row
+// pair, edge b's row pair), so consecutive VOP3P instructions of one wave no longer depend on each other and the
+// hazard s_nop between dependent packed instructions goes (878 -> 224 in the headline decoder's code).  The even
+// edges feed the low half's reduction chain and the odd edges the high half's, exactly the two chains of hr_layer,
+// so outputs and iteration counts are identical (decoder and golden tests pass).  Measured slower: 388 vs 345 us
+// per in-step launch (profiles/r06_ldpc_pairs_ab.md) -- the pairs cost 80 extra v_perm_b32 and ~32 VGPRs of
+// scratch spills, and with eight waves per SIMD the nops of one wave were already covered by the others' issue.
+#ifndef HR_PAIRS
+#define HR_PAIRS 0
+#endif
+#ifndef HR_PCHUNK
+#define HR_PCHUNK 3
+#endif
+typedef short pk4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ pk4 pk_cat(pk16 a, pk16 b)
+{
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3);
+}
+__device__ __forceinline__ pk16 pk_lo(pk4 v)
+{
+  return __builtin_shufflevector(v, v, 0, 1);
+}
+__device__ __forceinline__ pk16 pk_hi(pk4 v)
+{
+  return __builtin_shufflevector(v, v, 2, 3);
+}
+__device__ __forceinline__ pk4 pk4_splat(int v)
+{
+  const short x = static_cast<short>(v);
+  return pk4{x, x, x, x};
+}
+__device__ __forceinline__ pk4 pk4_clamp(pk4 x, int lim)
+{
+  return __builtin_elementwise_min(__builtin_elementwise_max(x, pk4_splat(-lim)), pk4_splat(lim));
+}
+
+template <int L, int ARITH, int NP, typename MSGS, int... P>
+__device__ __forceinline__ void hr_layer_pairs(lds_i8* lds, MSGS& c2v, uint32_t t, std::integer_sequence<int, P...>)
+{
+  static_assert(!HR_KEYS, "the paired layer keeps |v2c| minima");
+  constexpr int E0  = row_start<1>(L);
+  constexpr int DEG = bg_traits<1>::deg(L);
+  constexpr int T   = HR_HALF / NP;
+  pk16          v[DEG][NP];
+  pk4           mn1[NP], mn2[NP], sg[NP]; // low half: the even edges' chain, high half: the odd edges'
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    mn1[k] = mn2[k] = pk4_splat(LLR_MAX);
+    sg[k]           = pk4_splat(0);
+  }
+  // pass 1 (ldpc_decoder_impl.cpp:235 / :290): v2c and the check-node statistics
+  (
+      [&] {
+        constexpr int Ea = 2 * P, Eb = 2 * P + 1;
+        if constexpr (P % HR_PCHUNK == 0 && P > 0) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        static_for<NP>([&](auto kc) {
+          constexpr int k  = decltype(kc)::value;
+          const pk16    sa = pk16{static_cast<short>(lds[hr_addr<E0 + Ea, 0, k * T>(t)]),
+                               static_cast<short>(lds[hr_addr<E0 + Ea, HR_HALF, k * T>(t)])};
+          if constexpr (Eb < DEG) {
+            const pk16 sb  = pk16{static_cast<short>(lds[hr_addr<E0 + Eb, 0, k * T>(t)]),
+                                 static_cast<short>(lds[hr_addr<E0 + Eb, HR_HALF, k * T>(t)])};
+            const pk4  s   = pk_cat(sa, sb);
+            const pk4  c   = pk_cat(c2v.template get<(E0 + Ea) * NP + k>(), c2v.template get<(E0 + Eb) * NP + k>());
+            const pk4  sat = pk4_clamp(s, LLR_MAX);
+            // infinite soft bits (+-SOFT_INF) push |v2c| beyond 220 (see edge_pass1)
+            const pk4 x  = (s - sat) * pk4_splat(INF_BOOST) + pk4_clamp(s - c, LLR_MAX);
+            const pk4 ax = __builtin_elementwise_abs(x);
+            mn2[k]       = __builtin_elementwise_max(mn1[k], __builtin_elementwise_min(ax, mn2[k]));
+            mn1[k]       = __builtin_elementwise_min(mn1[k], ax);
+            sg[k] ^= x;
+            v[Ea][k] = pk_lo(x);
+            v[Eb][k] = pk_hi(x);
+          } else { // the last edge of an odd degree: the even chain
+            const pk16 sat = pk_clamp(sa, LLR_MAX);
+            const pk16 x = (sa - sat) * pk_splat(INF_BOOST) + pk_clamp(sa - c2v.template get<(E0 + Ea) * NP + k>(), LLR_MAX);
+            const pk16 ax = __builtin_elementwise_abs(x);
+            pk16       a1 = pk_lo(mn1[k]), a2 = pk_lo(mn2[k]);
+            a2            = pk_max(a1, pk_min(ax, a2));
+            a1            = pk_min(a1, ax);
+            mn1[k]        = pk_cat(a1, pk_hi(mn1[k]));
+            mn2[k]        = pk_cat(a2, pk_hi(mn2[k]));
+            sg[k]         = pk_cat(pk_lo(sg[k]) ^ x, pk_hi(sg[k]));
+            v[Ea][k]      = x;
+          }
+        });
+      }(),
+      ...);
+  __builtin_amdgcn_sched_barrier(0);
+  pk4 m1q[NP], s2q[NP], d12q[NP], sgq[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    // merge the two chains: min1 = min(a1, b1), min2 = min(max(a1, b1), min(a2, b2))
+    const pk16 a1 = pk_lo(mn1[k]), b1 = pk_hi(mn1[k]);
+    const pk16 m1  = pk_min(a1, b1);
+    const pk16 mn2v = pk_min(pk_max(a1, b1), pk_min(pk_lo(mn2[k]), pk_hi(mn2[k])));
+    const pk16 s1  = pk_scale<ARITH>(m1);
+    const pk16 s2  = pk_scale<ARITH>(mn2v);
+    const pk16 sgn = pk_lo(sg[k]) ^ pk_hi(sg[k]);
+    m1q[k]         = pk_cat(m1, m1);
+    s2q[k]         = pk_cat(s2, s2);
+    d12q[k]        = pk_cat(s1 - s2, s1 - s2);
+    sgq[k]         = pk_cat(sgn, sgn);
+  }
+  // pass 2 (ldpc_decoder_impl.cpp:310, :270): new message and promotion sum
+  (
+      [&] {
+        constexpr int Ea = 2 * P, Eb = 2 * P + 1;
+        if constexpr (P % HR_PCHUNK == 0 && P > 0) {
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        static_for<NP>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          if constexpr (Eb < DEG) {
+            const pk4 x   = pk_cat(v[Ea][k], v[Eb][k]);
+            const pk4 f   = __builtin_elementwise_min(__builtin_elementwise_abs(x) - m1q[k], pk4_splat(1));
+            const pk4 mag = f * d12q[k] + s2q[k];
+            const pk4 neg = (sgq[k] ^ x) >> 15;
+            const pk4 c   = (mag ^ neg) - neg;
+            // promotion sum: |c + x| > LLR_MAX is +-SOFT_INF (see edge_pass2)
+            const pk4 out = pk4_clamp(c + x, SOFT_INF);
+            c2v.template set<(E0 + Ea) * NP + k>(pk_lo(c));
+            c2v.template set<(E0 + Eb) * NP + k>(pk_hi(c));
+            lds[hr_addr<E0 + Ea, 0, k * T>(t)]       = static_cast<int8_t>(out.x);
+            lds[hr_addr<E0 + Ea, HR_HALF, k * T>(t)] = static_cast<int8_t>(out.y);
+            lds[hr_addr<E0 + Eb, 0, k * T>(t)]       = static_cast<int8_t>(out.z);
+            lds[hr_addr<E0 + Eb, HR_HALF, k * T>(t)] = static_cast<int8_t>(out.w);
+          } else {
+            const pk16 x   = v[Ea][k];
+            const pk16 f   = pk_min(__builtin_elementwise_abs(x) - pk_lo(m1q[k]), pk_splat(1));
+            const pk16 mag = f * pk_lo(d12q[k]) + pk_lo(s2q[k]);
+            const pk16 neg = (pk_lo(sgq[k]) ^ x) >> 15;
+            const pk16 c   = (mag ^ neg) - neg;
+            const pk16 out = pk_clamp(c + x, SOFT_INF);
+            c2v.template set<(E0 + Ea) * NP + k>(c);
+            lds[hr_addr<E0 + Ea, 0, k * T>(t)]       = static_cast<int8_t>(out.x);
+            lds[hr_addr<E0 + Ea, HR_HALF, k * T>(t)] = static_cast<int8_t>(out.y);
+          }
+        });
+      }(),
+      ...);
+}
+
 template <int L, int MAXL, int ARITH, int NP, typename MSGS>
 __device__ __forceinline__ void hr_layers(lds_i8* lds, MSGS& c2v, uint32_t t, int nof_layers)
 {
   if constexpr (L < MAXL) {
     if (L < 4 || L < nof_layers) {
       asm volatile("" : "+v"(t));
-      hr_layer<L, ARITH, NP>(lds, c2v, t, std::make_integer_sequence<int, bg_traits<1>::deg(L)>{});
+      if constexpr (HR_PAIRS && !HR_KEYS) {
+        hr_layer_pairs<L, ARITH, NP>(lds, c2v, t, std::make_integer_sequence<int, (bg_traits<1>::deg(L) + 1) / 2>{});
+      } else {
+        hr_layer<L, ARITH, NP>(lds, c2v, t, std::make_integer_sequence<int, bg_traits<1>::deg(L)>{});
+      }
       if constexpr (NP == 1) {
         __syncthreads();
       } else {
