@@ -45,6 +45,19 @@ __device__ __forceinline__ float2 polar1(float theta)
   return make_float2(c, s);
 }
 
+// cmul as one packed multiply and one packed FMA (v_pk_mul_f32, v_pk_fma_f32): per component the same two roundings
+// as cmul -- the product a.y b.y (or a.y b.x) rounded, then one fused multiply-add -- so the bits are cmul's.
+__device__ __forceinline__ float2 cmul_pk(float2 a, float2 b)
+{
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 av = {a.x, a.y}, bv = {b.x, b.y};
+  f2       t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(av), "v"(bv)); // (a.y b.y, a.y b.x)
+  // (a.x b.x - t.x, a.x b.y + t.y)
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(av), "v"(bv), "v"(t));
+  return make_float2(r.x, r.y);
+}
+
 // CFO phase of OFDM symbol l for a port whose estimator accumulators are acc[0..7]
 // (port_channel_estimator_average_impl.cpp:184-193).
 __device__ __forceinline__ float2 cfo_phase(const chest_args& a, const float* acc, uint32_t l)
@@ -70,7 +83,7 @@ __device__ __forceinline__ uint32_t expand_pair(const chest_args& a, float2 x0, 
   }
   uint32_t out = to_cbf16(e);
   if (rot) {
-    out = to_cbf16(cmul(from_cbf16(out), ph));
+    out = to_cbf16(cmul_pk(from_cbf16(out), ph));
   }
   return out;
 }

@@ -168,6 +168,54 @@ __device__ __forceinline__ void mimo_init(mimo_system<L>& s)
   }
 }
 
+// acc += a conj(b) as two packed-FP32 FMAs (v_pk_fma_f32: both components of the complex accumulator per
+// instruction, op_sel / op_sel_hi broadcasting and swapping the halves, neg_hi the one subtracted product):
+//   (acc.x, acc.y) += (a.x, a.y) (b.x, b.x);   (acc.x, acc.y) += (a.y, -a.x) (b.y, b.y)
+// against mul_conj's two multiplies, two FMAs and two adds.  Only the L-layer solves use it (parity unpinned: fp64
+// tolerance); the reference-pinned 1 x N / 2 x N paths keep their scalar arithmetic.
+#ifndef EQ_PK_GRAM
+#define EQ_PK_GRAM 1
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void pk_cmac_conj(cplx& acc, cplx a, cplx b)
+{
+  f2v       c  = {acc.x, acc.y};
+  const f2v av = {a.x, a.y}, bv = {b.x, b.y};
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(c) : "v"(av), "v"(bv));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]" : "+v"(c) : "v"(av), "v"(bv));
+  acc = {c.x, c.y};
+}
+
+// acc -= a b and acc -= a conj(b), two packed FMAs each (the L-layer solve's complex multiply-accumulates).
+__device__ __forceinline__ void pk_cmsc(cplx& acc, cplx a, cplx b)
+{
+  f2v       c  = {acc.x, acc.y};
+  const f2v av = {a.x, a.y}, bv = {b.x, b.y};
+  // (acc.x, acc.y) -= (a.x, a.x) (b.x, b.y);  (acc.x, acc.y) += (a.y, -a.y) (b.y, b.x)
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "+v"(c) : "v"(av), "v"(bv));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]" : "+v"(c) : "v"(av), "v"(bv));
+  acc = {c.x, c.y};
+}
+__device__ __forceinline__ void pk_cmsc_conj(cplx& acc, cplx a, cplx b)
+{
+  f2v       c  = {acc.x, acc.y};
+  const f2v av = {a.x, a.y}, bv = {b.x, b.y};
+  // (acc.x, acc.y) -= (a.x, a.y) (b.x, b.x);  (acc.x, acc.y) += (-a.y, a.x) (b.y, b.y)
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "+v"(c) : "v"(av), "v"(bv));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "+v"(c) : "v"(av), "v"(bv));
+  acc = {c.x, c.y};
+}
+// acc += a b
+__device__ __forceinline__ void pk_cmac(cplx& acc, cplx a, cplx b)
+{
+  f2v       c  = {acc.x, acc.y};
+  const f2v av = {a.x, a.y}, bv = {b.x, b.y};
+  // (acc.x, acc.y) += (a.x, a.x) (b.x, b.y);  (acc.x, acc.y) += (-a.y, a.y) (b.y, b.x)
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(c) : "v"(av), "v"(bv));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]" : "+v"(c) : "v"(av), "v"(bv));
+  acc = {c.x, c.y};
+}
+
 // Port p's terms: hp[L] its channel coefficients, yp its received sample.
 template <int L>
 __device__ __forceinline__ void mimo_add_port(mimo_system<L>& s, const cplx* hp, cplx yp)
@@ -176,13 +224,23 @@ __device__ __forceinline__ void mimo_add_port(mimo_system<L>& s, const cplx* hp,
   for (int i = 0; i < L; ++i) {
 #pragma unroll
     for (int k = 0; k <= i; ++k) {
-      const cplx t = mul_conj(hp[k], hp[i]); // (H^H H)_{i,k} = sum_p conj(H_pi) H_pk
+      // (H^H H)_{i,k} = sum_p conj(H_pi) H_pk
+#if EQ_PK_GRAM
+      pk_cmac_conj(s.a[i][k], hp[k], hp[i]);
+#else
+      const cplx t = mul_conj(hp[k], hp[i]);
       s.a[i][k].x += t.x;
       s.a[i][k].y += t.y;
+#endif
     }
-    const cplx t = mul_conj(yp, hp[i]); // conj(h_i) y
+    // conj(h_i) y
+#if EQ_PK_GRAM
+    pk_cmac_conj(s.b[i], yp, hp[i]);
+#else
+    const cplx t = mul_conj(yp, hp[i]);
     s.b[i].x += t.x;
     s.b[i].y += t.y;
+#endif
   }
 }
 
@@ -232,9 +290,13 @@ __device__ __forceinline__ void mimo_solve(mimo_system<L>& sys,
       cplx s = a[i][k];
 #pragma unroll
       for (int j = 0; j < k; ++j) {
+#if EQ_PK_GRAM
+        pk_cmsc_conj(s, a[i][j], a[k][j]); // C_ij conj(C_kj)
+#else
         const cplx t = mul_conj(a[i][j], a[k][j]); // C_ij conj(C_kj)
         s.x -= t.x;
         s.y -= t.y;
+#endif
       }
       a[i][k] = {s.x * r[k], s.y * r[k]};
     }
@@ -246,9 +308,13 @@ __device__ __forceinline__ void mimo_solve(mimo_system<L>& sys,
     cplx s = b[k];
 #pragma unroll
     for (int j = 0; j < k; ++j) {
+#if EQ_PK_GRAM
+      pk_cmsc(s, a[k][j], z[j]);
+#else
       const cplx t = cmul(a[k][j], z[j]);
       s.x -= t.x;
       s.y -= t.y;
+#endif
     }
     z[k] = {s.x * r[k], s.y * r[k]};
   }
@@ -258,9 +324,13 @@ __device__ __forceinline__ void mimo_solve(mimo_system<L>& sys,
     cplx s = z[k];
 #pragma unroll
     for (int j = k + 1; j < L; ++j) {
+#if EQ_PK_GRAM
+      pk_cmsc_conj(s, x[j], a[j][k]); // conj(C_jk) x_j
+#else
       const cplx t = mul_conj(x[j], a[j][k]); // conj(C_jk) x_j
       s.x -= t.x;
       s.y -= t.y;
+#endif
     }
     x[k] = {s.x * r[k], s.y * r[k]};
   }
@@ -276,9 +346,13 @@ __device__ __forceinline__ void mimo_solve(mimo_system<L>& sys,
       cplx s = {0.0f, 0.0f};
 #pragma unroll
       for (int j = k; j < i; ++j) {
+#if EQ_PK_GRAM
+        pk_cmac(s, a[i][j], w[j]);
+#else
         const cplx t = cmul(a[i][j], w[j]);
         s.x += t.x;
         s.y += t.y;
+#endif
       }
       w[i] = {-s.x * r[i], -s.y * r[i]};
       acc += norm(w[i]);
